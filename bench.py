@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Drain-planner benchmark (BASELINE.json metric: drain-plan latency (ms) +
+pod x node feasibility checks/s at 5k nodes / 150k pods).
+
+One step = one housekeeping tick's planning segment on device-resident inputs:
+K0 tables -> K1 dense feasibility (every candidate pod x every spot node) ->
+K2 first-fit placement of every candidate -> [RCCL allreduce(min) for N>1] ->
+K3 winner mapping -> result download.  ms_per_step is therefore the drain-plan
+latency with inputs in HBM; `value` is dense (pod, spot node) checks per second
+over all ranks.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
+
+N > 1 runs one process per GPU (torch.distributed.run); candidates are the
+on-demand nodes of a cluster with N x 1,500 on-demand nodes and the same
+3,500-node spot pool, sharded c % N == rank (weak scaling: every GPU holds one
+C3-sized candidate set).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "k8s-spot-rescheduler_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+from spotplanner import capi  # noqa: E402
+from spotplanner.planner import PredicateChecker  # noqa: E402
+from spotplanner.synth import SynthCluster, build_candidates, new_node_map, shard  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+DEFAULT_OD = {1: 10, 2: 300, 3: 1500, 4: 15000, 5: 300}
+WORKLOAD = {1: "C1 rescheduler_test-style 20 nodes / 200 pods",
+            2: "C2 1k nodes (300 od / 700 spot) / 30k pods, resource fit + PreferNoSchedule",
+            3: "C3 5k nodes (1500 od / 3500 spot) / 150k pods, nodeSelector + node affinity + tolerations",
+            4: "C4 50k nodes (15000 od / 35000 spot) / 1.5M pods, all candidates per tick",
+            5: "C5 1k nodes host-port + DaemonSet heavy"}
+
+
+def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, seconds):
+    """The oracle (C restatement of the reference planner) on this host, rank 0 only."""
+    from oracle_lib import OracleSnapshot, oracle_plan
+    snap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
+    times, res = [], None
+    t_end = time.perf_counter() + seconds
+    while len(times) < 3 or (time.perf_counter() < t_end and len(times) < 500):
+        t0 = time.perf_counter()
+        res = oracle_plan(snap, sc.ptr, cand_off, cand_pods, mode=1, threads=1)
+        times.append(time.perf_counter() - t0)
+    ms_all = 1e3 * float(np.median(times))
+    t0 = time.perf_counter()
+    early = oracle_plan(snap, sc.ptr, cand_off, cand_pods, mode=0, threads=1)
+    ms_early = 1e3 * (time.perf_counter() - t0)
+    threads = min(16, os.cpu_count() or 1)
+    mt = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        oracle_plan(snap, sc.ptr, cand_off, cand_pods, mode=1, threads=threads)
+        mt.append(time.perf_counter() - t0)
+    ms_mt = 1e3 * float(np.median(mt))
+    dense = float(len(cand_pods)) * n_spot
+    parity = bool(np.array_equal(res["status"], gpu_status))
+    return {"value": dense / (ms_all / 1e3), "unit": "checks/s", "cores": 1, "kind": "port",
+            "sample": "full tick: all %d candidates / %d pods x %d spot nodes, median of %d runs (%.1f s)"
+                      % (len(cand_off) - 1, len(cand_pods), n_spot, len(times), sum(times)),
+            "ms_per_tick_all_candidates_1core": round(ms_all, 3),
+            "ms_per_tick_reference_faithful_1core": round(ms_early, 3),
+            "reference_faithful_first_ok": int(early["first_ok"]),
+            "ms_per_tick_all_candidates_%dcores" % threads: round(ms_mt, 3),
+            "issued_checks_per_tick": int(res["checks"]),
+            "plans_identical_to_gpu": parity}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+
+    lib = capi.load_planner()
+    sc = SynthCluster(args.config, n_on_demand=DEFAULT_OD[args.config] * world)
+    nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+    loff, lpods, gidx = shard(cand_off, cand_pods, rank, world)
+
+    snap = ctypes.c_void_p()
+    st = lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot),
+                                capi.ptr(nm.node_pod_off, capi.P32), capi.ptr(nm.node_pod_idx, capi.P32),
+                                ctypes.byref(snap))
+    assert st == capi.SR_OK
+    checker = PredicateChecker(local)
+    if world > 1:
+        uid = (ctypes.c_uint8 * capi.SR_UNIQUE_ID_BYTES)()
+        if rank == 0:
+            assert lib.sr_comm_unique_id(uid) == capi.SR_OK
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0)
+        uid = (ctypes.c_uint8 * capi.SR_UNIQUE_ID_BYTES).from_buffer_copy(box[0])
+        st = lib.sr_comm_init(checker.handle, uid, world, rank)
+        assert st == capi.SR_OK, checker.last_error()
+
+    cands = capi.sr_candidates(len(loff) - 1, capi.ptr(loff, capi.P32), capi.ptr(lpods, capi.P32),
+                               capi.ptr(gidx, capi.P32))
+    t0 = time.perf_counter()
+    st = lib.sr_plan_prepare(checker.handle, snap, sc.ptr, ctypes.byref(cands))
+    assert st == capi.SR_OK, checker.last_error()
+    pack_ms = 1e3 * (time.perf_counter() - t0)
+
+    maxp = int(np.max(np.diff(loff))) if len(loff) > 1 else 1
+    wmap = np.zeros(max(1, maxp), np.int32)
+    out = capi.sr_plan_out()
+    out.winner_map = capi.ptr(wmap, capi.P32)
+    for _ in range(args.warmup):
+        assert lib.sr_plan_run(checker.handle, ctypes.byref(out)) == capi.SR_OK, checker.last_error()
+
+    checker.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        lib.sr_plan_run(checker.handle, ctypes.byref(out))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tm = checker.timing()
+    local_checks = float(out.checks)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([local_checks], dtype=torch.float64)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        total_checks = float(c.item())
+    else:
+        total_checks = local_checks
+    ms_step = 1e3 * elapsed / args.steps
+
+    # full per-candidate outputs once (outside the timed region) for the parity check
+    status = np.zeros(max(1, len(loff) - 1), np.int32)
+    nodes_out = np.zeros(max(1, len(lpods)), np.int32)
+    full = capi.sr_plan_out()
+    full.status = capi.ptr(status, capi.P32)
+    full.node_of_pod = capi.ptr(nodes_out, capi.P32)
+    full.winner_map = capi.ptr(wmap, capi.P32)
+    assert lib.sr_plan_run(checker.handle, ctypes.byref(full)) == capi.SR_OK
+
+    if rank == 0:
+        n = max(1, tm.n_runs)
+        k = {"k0_tables": tm.ms_tables / n, "k1_feasibility": tm.ms_feasibility / n,
+             "k2_placement": tm.ms_placement / n, "k3_winner_and_download": tm.ms_winner / n}
+        dom = max(("k1_feasibility", "k2_placement", "k0_tables"), key=lambda x: k[x])
+        alg = {"k1_feasibility": tm.bytes_feasibility, "k2_placement": tm.bytes_placement,
+               "k0_tables": (tm.n_rows_a + tm.n_rows_b) * tm.n_words * 8 + 64 * tm.n_spot}[dom]
+        achieved = alg / (k[dom] * 1e-3) / 1e9 if k[dom] > 0 else 0.0
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "pmc_traffic_c%d.json" % args.config)
+        if os.path.exists(pmc) and world == 1:
+            with open(pmc) as f:
+                traffic = json.load(f).get(dom)
+        line = {
+            "metric": "pod x spot-node feasibility checks/s (drain-plan latency = ms_per_step)",
+            "value": total_checks / elapsed * args.steps if elapsed > 0 else 0.0,
+            "unit": "checks/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_step, "latency_ms": ms_step,
+            "plans_per_s": (len(cand_off) - 1) / (elapsed / args.steps),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic",
+            "config": {"workload": WORKLOAD[args.config], "nodes": sc.n_nodes, "pods": sc.n_pods,
+                       "spot_nodes": int(len(nm.spot)), "candidates": int(len(cand_off) - 1),
+                       "candidate_pods": int(len(cand_pods)), "parallelism": "candidates c%%%d" % world},
+            "first_ok": int(out.first_ok), "winner": int(out.winner),
+            "kernels_ms": {kk: round(v, 5) for kk, v in k.items()},
+            "host_pack_ms": round(pack_ms, 3),
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "algorithmic_bytes": int(alg)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(sc, nm, cand_off, cand_pods, int(len(nm.spot)), status[:len(loff) - 1],
+                                                args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    lib.sr_snapshot_destroy(snap)
+    checker.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

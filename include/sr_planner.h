@@ -1,0 +1,296 @@
+/*
+ * sr_planner.h — C-ABI of the MI355X drain planner (k8s-spot-rescheduler hot path).
+ *
+ * The reference (Go, github.com/pusher/k8s-spot-rescheduler) has no FFI: the hot
+ * path sits behind unexported Go functions plus cluster-autoscaler interfaces.
+ * Every entry point below names the reference interface it replaces (file:line
+ * into the reference tree).  A cgo binding for these entry points is shown in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain C types only; no torch / HIP types cross this boundary.
+ *  - Strings never cross.  The caller (the Go shim) interns every string it
+ *    needs (label keys/values, taint keys/values, node names, host IPs) into
+ *    int32 ids; the planner only compares ids.  `sr_cluster.id_empty`,
+ *    `id_metadata_name` and `id_unschedulable_key` tell the planner which ids
+ *    stand for "", "metadata.name" and "node.kubernetes.io/unschedulable".
+ *  - Quantities arrive already converted the way the reference converts them:
+ *    CPU via Quantity.MilliValue(), memory / ephemeral storage / pods via
+ *    Quantity.Value().
+ *  - Input buffers are owned by the caller for the duration of a call only;
+ *    nothing is retained after return (handles copy what they keep).
+ *  - Output buffers are caller-allocated.
+ *  - Handles are not thread-safe: one owner at a time.
+ */
+#ifndef SR_PLANNER_H
+#define SR_PLANNER_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SR_ABI_VERSION 1
+
+/* ------------------------------------------------------------------ status */
+typedef int32_t sr_status;
+#define SR_OK                 0
+#define SR_ERR_INVALID_ARG    1  /* malformed input (bad CSR, index out of range) */
+#define SR_ERR_HIP            2  /* HIP runtime error (message in sr_last_error) */
+#define SR_ERR_CAPACITY       3  /* a planner limit was exceeded */
+#define SR_ERR_NIL_PRIORITY   4  /* nodes/nodes.go:139 dereferences *Spec.Priority: the reference panics */
+#define SR_ERR_RCCL           5  /* RCCL error */
+#define SR_ERR_NO_DEVICE      6  /* no HIP device: the planner never falls back to the CPU */
+#define SR_ERR_STATE          7  /* call sequence error (e.g. Revert without Fork) */
+
+/* -------------------------------------------------------------- enumerations */
+/* Taint / toleration effects (k8s.io/api/core/v1 TaintEffect). */
+#define SR_EFFECT_EMPTY               0  /* toleration only: "" = every effect */
+#define SR_EFFECT_NO_SCHEDULE         1
+#define SR_EFFECT_PREFER_NO_SCHEDULE  2
+#define SR_EFFECT_NO_EXECUTE          3
+#define SR_EFFECT_OTHER               4  /* any other string */
+
+/* Toleration operators. */
+#define SR_TOL_EQUAL   0  /* "" or "Equal" */
+#define SR_TOL_EXISTS  1
+#define SR_TOL_OTHER   2  /* unknown operator: never tolerates */
+
+/* Node selector requirement operators (v1.NodeSelectorOperator). */
+#define SR_OP_IN              0
+#define SR_OP_NOT_IN          1
+#define SR_OP_EXISTS          2
+#define SR_OP_DOES_NOT_EXIST  3
+#define SR_OP_GT              4
+#define SR_OP_LT              5
+#define SR_OP_OTHER           6  /* unknown operator: the term fails to build */
+
+/* Host-port protocols ("" is sanitised to TCP by the shim, as HostPortInfo does). */
+#define SR_PROTO_TCP   0
+#define SR_PROTO_UDP   1
+#define SR_PROTO_SCTP  2
+
+/* Pod flags (sr_pods.flags). */
+#define SR_POD_DAEMONSET_CONTROLLER (1u << 0)  /* an owner ref with *Controller && Kind=="DaemonSet" (rescheduler.go:243-248) */
+#define SR_POD_MIRROR               (1u << 1)  /* mirror pod (config.mirror annotation) */
+#define SR_POD_HAS_REQ_ANTI_AFFINITY (1u << 2) /* carries required pod anti-affinity terms (matters when it sits on a spot node) */
+/* Fallback reasons set by the shim: features the encoded predicate set does not cover. */
+#define SR_POD_FB_SCALAR_RESOURCES  (1u << 8)  /* extended / hugepages / attachable-volume requests */
+#define SR_POD_FB_VOLUMES           (1u << 9)  /* PVCs or volumes inspected by volume filters */
+#define SR_POD_FB_TOPOLOGY_SPREAD   (1u << 10) /* DoNotSchedule topology spread constraints */
+#define SR_POD_FB_POD_AFFINITY      (1u << 11) /* required pod affinity or anti-affinity */
+#define SR_POD_FB_OTHER             (1u << 12) /* anything else the shim cannot encode */
+#define SR_POD_FB_MASK              (0xff00u)
+
+/* Candidate status codes (sr_plan_out.status).  >= 0: index of the first pod
+ * that fits on no spot node ("pod %s can't be rescheduled on any existing spot
+ * node", rescheduler.go:363). */
+#define SR_CAND_OK        (-1)
+#define SR_CAND_FALLBACK  (-2)  /* outside the encoded predicate set: evaluate with the reference path */
+#define SR_CAND_EMPTY     (-3)  /* no pods to move: run() skips it (rescheduler.go:260-264) */
+
+/* ------------------------------------------------------------- cluster model */
+/* Nodes (k8s.io/api/core/v1 Node), in the order the node lister returned them
+ * (rescheduler.go:186).  CSR arrays: x_off has n+1 entries. */
+typedef struct {
+  int32_t        n;
+  const int32_t *name;             /* interned ObjectMeta.Name (matchFields metadata.name) */
+  const int64_t *alloc_milli_cpu;  /* Status.Allocatable.Cpu().MilliValue() */
+  const int64_t *alloc_memory;     /* Status.Allocatable.Memory().Value() */
+  const int64_t *alloc_ephemeral;  /* Status.Allocatable.StorageEphemeral().Value() */
+  const int64_t *alloc_pods;       /* Status.Allocatable.Pods().Value() */
+  const uint8_t *unschedulable;    /* Spec.Unschedulable */
+  const int32_t *label_off;        /* ObjectMeta.Labels (keys unique per node) */
+  const int32_t *label_key;
+  const int32_t *label_val;
+  const int32_t *taint_off;        /* Spec.Taints */
+  const int32_t *taint_key;
+  const int32_t *taint_val;
+  const int32_t *taint_effect;     /* SR_EFFECT_* */
+} sr_nodes;
+
+/* Pods (k8s.io/api/core/v1 Pod).  Pods bound to one node appear in the order
+ * the per-node LIST returned them (nodes/nodes.go:130). */
+typedef struct {
+  int32_t        n;
+  const int32_t *node;             /* index into sr_nodes of Spec.NodeName, -1 if unbound */
+  const int64_t *cpu_sort_milli;   /* Σ regular containers Requests.Cpu().MilliValue() (nodes/nodes.go:159-165) */
+  const int64_t *req_milli_cpu;    /* scheduler request: max(Σ containers, each init container) + Overhead */
+  const int64_t *req_memory;       /*   (k8s v1.19 noderesources computePodResourceRequest) */
+  const int64_t *req_ephemeral;
+  const int32_t *priority;         /* *Spec.Priority */
+  const uint8_t *has_priority;     /* Spec.Priority != nil */
+  const uint32_t *flags;           /* SR_POD_* */
+  /* Spec.NodeSelector (key, value) pairs */
+  const int32_t *sel_off, *sel_key, *sel_val;
+  /* Spec.Affinity.NodeAffinity.RequiredDuringSchedulingIgnoredDuringExecution:
+   * aff_required[i] != 0 iff that pointer is non-nil.  Terms are ORed; a term
+   * ANDs its matchExpressions and its matchFields. */
+  const uint8_t *aff_required;
+  const int32_t *term_off;         /* [n+1]       pods  -> terms */
+  const int32_t *term_expr_off;    /* [terms+1]   terms -> matchExpressions */
+  const int32_t *term_field_off;   /* [terms+1]   terms -> matchFields */
+  const int32_t *expr_key, *expr_op, *expr_val_off, *expr_vals;     /* expr_val_off [exprs+1] */
+  const int32_t *field_key, *field_op, *field_val_off, *field_vals; /* field_val_off [fields+1] */
+  /* Spec.Tolerations */
+  const int32_t *tol_off, *tol_key, *tol_op, *tol_val, *tol_effect;  /* "" key/value = id_empty */
+  /* container host ports with HostPort > 0 (regular containers only) */
+  const int32_t *port_off, *port_proto, *port_num, *port_ip /* -1 = "" or "0.0.0.0" */;
+} sr_pods;
+
+typedef struct {
+  sr_nodes nodes;
+  sr_pods  pods;
+  int32_t  id_empty;          /* interned id of "" (-1 if never interned) */
+  int32_t  id_metadata_name;  /* interned id of "metadata.name" (-1 if never interned) */
+  int32_t  id_unschedulable_key; /* interned id of "node.kubernetes.io/unschedulable" (-1 if never interned) */
+} sr_cluster;
+
+/* ------------------------------------------------------------- NewNodeMap */
+/* A node-label flag: "key" (has_value = 0) or "key=value" (has_value = 1). */
+typedef struct {
+  int32_t key;
+  int32_t value;
+  int32_t has_value;
+} sr_node_label;
+
+typedef struct {
+  sr_node_label on_demand;     /* nodes.OnDemandNodeLabel  (nodes/nodes.go:33) */
+  sr_node_label spot;          /* nodes.SpotNodeLabel      (nodes/nodes.go:35) */
+  int32_t priority_threshold;  /* nodes.PriorityThreshold  (nodes/nodes.go:41) */
+} sr_node_map_params;
+
+/* Output of NewNodeMap; every array is caller-allocated. */
+typedef struct {
+  int32_t *spot;           /* [nodes.n] out: nodeMap[Spot], RequestedCPU desc (nodes/nodes.go:95-97) */
+  int32_t *n_spot;         /* [1] */
+  int32_t *on_demand;      /* [nodes.n] out: nodeMap[OnDemand], RequestedCPU asc (nodes/nodes.go:99-101) */
+  int32_t *n_on_demand;    /* [1] */
+  int32_t *node_pod_off;   /* [nodes.n+1] NodeInfo.Pods per node index (every node, mapped or not) */
+  int32_t *node_pod_idx;   /* [pods.n]    pod indices, CPU-desc sort order (nodes/nodes.go:76-80) */
+  int64_t *requested_cpu;  /* [nodes.n] NodeInfo.RequestedCPU */
+  int64_t *free_cpu;       /* [nodes.n] NodeInfo.FreeCPU */
+} sr_node_map;
+
+/* Replaces nodes.NewNodeMap (nodes/nodes.go:63-104) with the pod LIST already
+ * done by the caller (pods carry their node index).  Sorting reproduces Go
+ * 1.16 sort.Slice exactly, ties included.  Host-only: needs no GPU. */
+sr_status sr_new_node_map(const sr_cluster *cluster, const sr_node_map_params *params,
+                          sr_node_map *out);
+
+/* Replaces isSpotNode / isOnDemandNode (nodes/nodes.go:168-209).  Host-only. */
+int32_t sr_node_has_label(const sr_cluster *cluster, int32_t node, const sr_node_label *label);
+
+/* ------------------------------------------------------------ cluster snapshot */
+typedef struct sr_snapshot sr_snapshot;
+
+/* Replaces NodeInfoArray.GetClusterSnapshot (nodes/nodes.go:226-232):
+ * AddNodeWithPods(node, pods) per spot node, in NodeInfoArray order.
+ * node_pod_off/node_pod_idx: CSR indexed by node index (sr_node_map layout). */
+sr_status sr_snapshot_create(const sr_cluster *cluster, const int32_t *spot_nodes, int32_t n_spot,
+                             const int32_t *node_pod_off, const int32_t *node_pod_idx,
+                             sr_snapshot **out);
+void      sr_snapshot_destroy(sr_snapshot *snap);
+/* ClusterSnapshot.AddPod(pod, nodeName) (rescheduler.go:366); spot_pos = position in the NodeInfoArray. */
+sr_status sr_snapshot_add_pod(sr_snapshot *snap, const sr_cluster *cluster, int32_t pod, int32_t spot_pos);
+/* ClusterSnapshot.Fork / Revert (rescheduler.go:269,273): one level deep. */
+sr_status sr_snapshot_fork(sr_snapshot *snap);
+sr_status sr_snapshot_revert(sr_snapshot *snap);
+/* Introspection (tests, metrics): requested cpu/mem/eph, pod count of a spot node. */
+sr_status sr_snapshot_node_state(const sr_snapshot *snap, int32_t spot_pos, int64_t out_requested[3],
+                                 int32_t *out_num_pods);
+int32_t   sr_snapshot_num_nodes(const sr_snapshot *snap);
+
+/* ---------------------------------------------------------------- planner */
+typedef struct sr_ctx sr_ctx;
+
+/* Created once per process like the predicate checker (rescheduler.go:149).
+ * device: HIP device ordinal.  Returns SR_ERR_NO_DEVICE without a GPU. */
+sr_status   sr_create(int32_t device, sr_ctx **out);
+void        sr_destroy(sr_ctx *ctx);
+const char *sr_last_error(const sr_ctx *ctx);
+const char *sr_build_info(void);
+
+/* Batched findSpotNodeForPod (rescheduler.go:338-353): for each pod, the first
+ * spot node (NodeInfoArray order) whose predicates pass against the snapshot
+ * as it is; the snapshot is not modified.  out_spot_pos[i] = -1 is "".
+ * out_fallback[i] = 1: pod outside the encoded predicate set (not evaluated). */
+sr_status sr_find_spot_nodes(sr_ctx *ctx, const sr_snapshot *snap, const sr_cluster *cluster,
+                             const int32_t *pods, int32_t n, int32_t *out_spot_pos,
+                             uint8_t *out_fallback);
+
+/* canDrainNode (rescheduler.go:357-370): sequential first fit of `pods` in
+ * order; each placed pod is added to the snapshot (also on failure, for the
+ * pods placed before the failing one — exactly like the reference).
+ * *out_fail_pod = -1 (nil error) or the index of the first unplaceable pod.
+ * *out_fallback = 1: outside the encoded set; nothing evaluated or modified. */
+sr_status sr_can_drain_node(sr_ctx *ctx, sr_snapshot *snap, const sr_cluster *cluster,
+                            const int32_t *pods, int32_t n, int32_t *out_node_of_pod,
+                            int32_t *out_fail_pod, uint8_t *out_fallback);
+
+/* A batch of on-demand candidates in NodeInfoArray order (rescheduler.go:228),
+ * each with its podsForDeletion list (rescheduler.go:231-256). */
+typedef struct {
+  int32_t        n_cand;
+  const int32_t *cand_pod_off;  /* [n_cand+1] */
+  const int32_t *cand_pods;     /* pod indices, podsForDeletion order */
+  const int32_t *cand_global;   /* optional: global candidate index (sharded runs); NULL = 0..n-1 */
+} sr_candidates;
+
+typedef struct {
+  /* All indices are global candidate indices. */
+  int32_t  winner;          /* the node run() drains: first OK candidate with no unresolved
+                               fallback candidate before it; -1 = none (or unresolved) */
+  int32_t  first_ok;        /* first candidate whose plan succeeds on the GPU; -1 none */
+  int32_t  first_fallback;  /* first candidate flagged SR_CAND_FALLBACK; -1 none */
+  int32_t  winner_npods;    /* pods in winner_map (0 if the winner is not local) */
+  uint64_t checks;          /* (pod, spot node) pairs evaluated by the feasibility kernel */
+  uint64_t fallback_pods;   /* pods of fallback candidates */
+  /* optional outputs (NULL = not wanted) */
+  int32_t *status;          /* [n_cand] SR_CAND_* or failing pod index */
+  int32_t *node_of_pod;     /* [cand_pod_off[n_cand]] spot position, -1 not placed */
+  int32_t *winner_map;      /* [max pods of a candidate] spot position per pod of first_ok */
+} sr_plan_out;
+
+/* One housekeeping tick's planning segment (rescheduler.go:228-287): every
+ * candidate is evaluated from the same base snapshot (Fork / canDrainNode /
+ * Revert), all in parallel on the GPU.  The snapshot is not modified. */
+sr_status sr_plan(sr_ctx *ctx, const sr_snapshot *snap, const sr_cluster *cluster,
+                  const sr_candidates *cands, sr_plan_out *out);
+
+/* Split form of sr_plan for a resident workload (bench): prepare = host
+ * encoding + upload; run = device-only tick over the resident buffers
+ * (kernels + result download). */
+sr_status sr_plan_prepare(sr_ctx *ctx, const sr_snapshot *snap, const sr_cluster *cluster,
+                          const sr_candidates *cands);
+sr_status sr_plan_run(sr_ctx *ctx, sr_plan_out *out);
+
+/* Kernel timing (HIP events on the planner's stream). */
+typedef struct {
+  int32_t  n_runs;          /* timed runs accumulated */
+  double   ms_tables;       /* K0: class/threshold row tables */
+  double   ms_feasibility;  /* K1: dense pod x spot-node feasibility bitmask */
+  double   ms_placement;    /* K2: per-candidate first-fit placement */
+  double   ms_winner;       /* K3 + collective + download */
+  double   ms_pack_host;    /* last sr_plan_prepare host encoding */
+  double   ms_upload;       /* last sr_plan_prepare upload */
+  uint64_t bytes_feasibility; /* algorithmic bytes per K1 launch */
+  uint64_t bytes_placement;   /* algorithmic bytes per K2 launch */
+  int32_t  n_pods, n_spot, n_cand, n_words;
+  int32_t  n_rows_a, n_rows_b, n_classes;
+} sr_timing;
+sr_status sr_set_timing(sr_ctx *ctx, int32_t enable);
+sr_status sr_get_timing(const sr_ctx *ctx, sr_timing *out);
+
+/* Multi-GPU: one process per GPU; candidates sharded by the caller (use
+ * cand_global).  With a communicator attached, sr_plan_run reduces first_ok /
+ * first_fallback with one RCCL allreduce(min) over xGMI. */
+#define SR_UNIQUE_ID_BYTES 128
+sr_status sr_comm_unique_id(uint8_t out[SR_UNIQUE_ID_BYTES]);
+sr_status sr_comm_init(sr_ctx *ctx, const uint8_t id[SR_UNIQUE_ID_BYTES], int32_t nranks, int32_t rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SR_PLANNER_H */

@@ -1,0 +1,159 @@
+// gosort.hpp — Go 1.16 sort.Slice, reproduced exactly (tie order included).
+//
+// The reference sorts with sort.Slice, which is NOT stable: pods with equal
+// CPU requests (nodes/nodes.go:76-80) and nodes with equal RequestedCPU
+// (nodes/nodes.go:95-101) come out in the order Go's pattern of comparisons
+// and swaps leaves them.  That order decides first-fit placements, so it is
+// part of the answer.  Go <= 1.18 implements sort.Slice as quickSort_func
+// (go/src/sort/zfuncversion.go, generated from sort.go): introsort with an
+// insertion-sort cutoff at 12 elements, a gap-6 shell pass, Tukey's ninther
+// for spans > 40, a duplicate-protection pass, and heapsort at depth
+// 2*ceil(lg(n+1)).  go.mod:3 pins Go 1.15 and Dockerfile:3 builds with 1.16.
+#pragma once
+
+#include <cstdint>
+#include <utility>
+
+namespace sr {
+
+// Sorts data[0..n) of element ids; less(x, y) compares two element ids.
+template <class T, class Less>
+class GoSlice {
+ public:
+  GoSlice(T* data, Less less) : d_(data), less_(less) {}
+
+  void sort(int n) { quick(0, n, max_depth(n)); }
+
+ private:
+  T* d_;
+  Less less_;
+
+  bool lt(int i, int j) const { return less_(d_[i], d_[j]); }
+  void sw(int i, int j) { std::swap(d_[i], d_[j]); }
+
+  static int max_depth(int n) {
+    int depth = 0;
+    for (int i = n; i > 0; i >>= 1) ++depth;
+    return depth * 2;
+  }
+
+  void insertion(int a, int b) {
+    for (int i = a + 1; i < b; ++i)
+      for (int j = i; j > a && lt(j, j - 1); --j) sw(j, j - 1);
+  }
+
+  void sift_down(int lo, int hi, int first) {
+    int root = lo;
+    while (true) {
+      int child = 2 * root + 1;
+      if (child >= hi) return;
+      if (child + 1 < hi && lt(first + child, first + child + 1)) ++child;
+      if (!lt(first + root, first + child)) return;
+      sw(first + root, first + child);
+      root = child;
+    }
+  }
+
+  void heap(int a, int b) {
+    const int first = a, hi = b - a;
+    for (int i = (hi - 1) / 2; i >= 0; --i) sift_down(i, hi, first);
+    for (int i = hi - 1; i >= 0; --i) {
+      sw(first, first + i);
+      sift_down(0, i, first);
+    }
+  }
+
+  // Leaves the median of {m0, m1, m2} at m1 (Go's argument order: m1, m0, m2).
+  void median3(int m1, int m0, int m2) {
+    if (lt(m1, m0)) sw(m1, m0);
+    if (lt(m2, m1)) {
+      sw(m2, m1);
+      if (lt(m1, m0)) sw(m1, m0);
+    }
+  }
+
+  std::pair<int, int> pivot(int lo, int hi) {
+    const int m = static_cast<int>((static_cast<unsigned>(lo) + static_cast<unsigned>(hi)) >> 1);
+    if (hi - lo > 40) {
+      const int s = (hi - lo) / 8;
+      median3(lo, lo + s, lo + 2 * s);
+      median3(m, m - s, m + s);
+      median3(hi - 1, hi - 1 - s, hi - 1 - 2 * s);
+    }
+    median3(lo, m, hi - 1);
+
+    const int p = lo;
+    int a = lo + 1, c = hi - 1;
+    while (a < c && lt(a, p)) ++a;
+    int b = a;
+    while (true) {
+      while (b < c && !lt(p, b)) ++b;
+      while (b < c && lt(p, c - 1)) --c;
+      if (b >= c) break;
+      sw(b, c - 1);
+      ++b;
+      --c;
+    }
+    bool protect = hi - c < 5;
+    if (!protect && hi - c < (hi - lo) / 4) {
+      int dups = 0;
+      if (!lt(p, hi - 1)) {
+        sw(c, hi - 1);
+        ++c;
+        ++dups;
+      }
+      if (!lt(b - 1, p)) {
+        --b;
+        ++dups;
+      }
+      if (!lt(m, p)) {
+        sw(m, b - 1);
+        --b;
+        ++dups;
+      }
+      protect = dups > 1;
+    }
+    if (protect) {
+      while (true) {
+        while (a < b && !lt(b - 1, p)) --b;
+        while (a < b && lt(a, p)) ++a;
+        if (a >= b) break;
+        sw(a, b - 1);
+        ++a;
+        --b;
+      }
+    }
+    sw(p, b - 1);
+    return {b - 1, c};
+  }
+
+  void quick(int a, int b, int depth) {
+    while (b - a > 12) {
+      if (depth == 0) {
+        heap(a, b);
+        return;
+      }
+      --depth;
+      auto [mlo, mhi] = pivot(a, b);
+      if (mlo - a < b - mhi) {
+        quick(a, mlo, depth);
+        a = mhi;
+      } else {
+        quick(mhi, b, depth);
+        b = mlo;
+      }
+    }
+    if (b - a > 1) {
+      for (int i = a + 6; i < b; ++i)
+        if (lt(i, i - 6)) sw(i, i - 6);
+      insertion(a, b);
+    }
+  }
+};
+
+template <class T, class Less>
+inline void go_sort_slice(T* data, int n, Less less) {
+  GoSlice<T, Less>(data, less).sort(n);
+}
+
+}  // namespace sr

@@ -1,0 +1,130 @@
+// host.hpp — host-side model of the drain planner (C++).
+//
+// Mirrors the reference's cluster model (nodes/nodes.go NodeInfo /
+// NodeInfoArray) and the cluster-autoscaler ClusterSnapshot the predicate
+// checker reads [upstream CA simulator @03f60a4c3818], and declares the
+// encoder that turns a snapshot + candidate pod lists into the SoA workload
+// the gfx950 kernels consume (layout: DESIGN.md §HBM layout).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/sr_planner.h"
+
+namespace sr {
+
+struct Port {
+  int32_t ip;  // -1 = 0.0.0.0 / ""
+  int32_t proto;
+  int32_t port;
+};
+
+struct TaintRec {
+  int32_t key, val, effect;
+};
+
+// Static part of one spot node, copied out of the caller's cluster when the
+// snapshot is created (AddNodeWithPods, nodes/nodes.go:229).
+struct SpotNode {
+  int32_t name = -1;
+  int64_t alloc[3] = {0, 0, 0};  // milli-cpu, memory, ephemeral
+  int64_t alloc_pods = 0;
+  uint8_t unschedulable = 0;
+  std::vector<std::pair<int32_t, int32_t>> labels;  // (key, value)
+  std::vector<TaintRec> taints;
+};
+
+// Mutable part: scheduler NodeInfo.Requested, len(Pods), UsedPorts, and the
+// number of pods carrying required anti-affinity.
+struct NodeState {
+  int64_t requested[3] = {0, 0, 0};
+  int64_t npods = 0;
+  int32_t anti = 0;
+  std::vector<Port> ports;
+};
+
+}  // namespace sr
+
+// The opaque handle of the C-ABI.
+struct sr_snapshot {
+  int32_t id_empty = -1, id_metadata_name = -1, id_unschedulable_key = -1;
+  std::vector<sr::SpotNode> nodes;
+  std::vector<sr::NodeState> state;
+  std::vector<sr::NodeState> saved;
+  bool forked = false;
+  int64_t anti_total = 0;
+  uint64_t version = 0;  // bumped on every mutation
+};
+
+namespace sr {
+
+// Pod accessors over the caller's arrays.
+inline bool add_overflows(int64_t a, int64_t b) {
+  int64_t r;
+  return __builtin_add_overflow(a, b, &r);
+}
+
+void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t pos);
+
+// Class descriptor flags.
+enum : int32_t { CLS_AFF_REQUIRED = 1, CLS_IMPOSSIBLE = 2 };
+
+// The encoded workload of one planning call (host copy; uploaded as one arena).
+struct Workload {
+  // ---- dimensions
+  int32_t n_spot = 0;   // spot nodes
+  int32_t n_pad = 0;    // node arrays padded to Wp*64 entries
+  int32_t Wp = 0;       // 64-bit words per bitmask row (even)
+  int32_t WR = 0;       // words per requirement bitset
+  int32_t WT = 0;       // words per taint bitset
+  // ---- spot nodes (SoA, n_pad entries)
+  std::vector<int64_t> free_cpu, free_mem, free_eph;
+  std::vector<int32_t> pods_left;
+  std::vector<uint64_t> port_bits;
+  std::vector<uint64_t> req_bits;    // [WR][n_pad]
+  std::vector<uint64_t> taint_bits;  // [WT][n_pad]
+  // ---- static pod classes
+  int32_t n_classes = 0;
+  std::vector<uint64_t> cls_sel;    // [n_classes][WR]
+  std::vector<uint64_t> cls_tol;    // [n_classes][WT]
+  std::vector<uint64_t> cls_port;   // [n_classes]
+  std::vector<int32_t> cls_flags;   // CLS_*
+  std::vector<int32_t> cls_term_off;  // [n_classes+1]
+  std::vector<uint64_t> term_mask;    // [terms][WR]
+  // ---- A rows: (class, zero-request, cpu threshold, ephemeral threshold)
+  std::vector<int32_t> a_class, a_zero;
+  std::vector<int64_t> a_cpu, a_eph;
+  // ---- B rows: memory threshold (row 0 = "all nodes", used by zero-request pods)
+  std::vector<int64_t> b_mem;
+  std::vector<int32_t> b_all;
+  // ---- active pods, grouped by candidate, in podsForDeletion order
+  std::vector<int32_t> pod_a, pod_b, pod_zero;
+  std::vector<int64_t> pod_cpu, pod_mem, pod_eph;
+  std::vector<uint64_t> pod_ports;
+  std::vector<int32_t> pod_src;  // index into the caller's cand_pods array
+  // ---- active candidates
+  std::vector<int32_t> cand_off;     // [n_active+1] into active pods
+  std::vector<int32_t> cand_global;  // global candidate index
+  std::vector<int32_t> cand_src;     // index in the caller's candidate list
+  std::vector<int32_t> list_small, list_large;  // active candidates per K2 slot variant
+  int32_t max_cand_pods = 0;
+  // ---- host-decided outcomes for every input candidate
+  std::vector<int32_t> status_host;  // SR_CAND_EMPTY / SR_CAND_FALLBACK / PENDING
+  int32_t first_fallback = -1;       // global index
+  uint64_t fallback_pods = 0;
+  int32_t n_input_cand = 0;
+  int32_t n_input_pods = 0;
+};
+
+constexpr int32_t STATUS_PENDING = -100;
+constexpr int32_t SLOTS_SMALL = 128;   // touched spot nodes per candidate, small variant
+constexpr int32_t SLOTS_LARGE = 512;   // large variant
+constexpr int32_t MAX_WORDS = 64 * 32; // spot nodes <= 131072
+
+// Builds the workload; returns SR_OK or an error with *err filled.
+sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
+                          Workload* w, std::string* err);
+
+}  // namespace sr

@@ -1,0 +1,211 @@
+// nodemap.cpp — nodes.NewNodeMap and the cluster snapshot (host side).
+//
+// NewNodeMap (nodes/nodes.go:63-104) with the per-node pod LIST
+// (nodes/nodes.go:129-145) already resolved by the caller: pods carry their
+// node index and arrive in LIST order.  Sorting uses the Go-exact sort.Slice of
+// gosort.hpp.  GetClusterSnapshot (nodes/nodes.go:226-232) and the
+// ClusterSnapshot operations the planner needs (AddPod / Fork / Revert,
+// rescheduler.go:269,273,366) live here too.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "gosort.hpp"
+#include "host.hpp"
+
+namespace sr {
+
+// isSpotNode / isOnDemandNode (nodes/nodes.go:168-209).
+static bool node_has_label(const sr_cluster* c, int32_t node, const sr_node_label* l) {
+  const sr_nodes& N = c->nodes;
+  int32_t val = c->id_empty;
+  bool found = false;
+  for (int32_t i = N.label_off[node]; i < N.label_off[node + 1]; ++i) {
+    if (N.label_key[i] == l->key) {
+      found = true;
+      val = N.label_val[i];
+      break;
+    }
+  }
+  if (!l->has_value) return found;   // old label schema: key presence
+  return val == l->value;            // labels[k] == v, missing key reads as ""
+}
+
+static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, sr_node_map* out) {
+  const sr_nodes& N = c->nodes;
+  const sr_pods& P = c->pods;
+  const int32_t nn = N.n, np = P.n;
+  // Per-node LIST results: counting sort by node index keeps list order.
+  std::vector<int32_t> start(static_cast<size_t>(nn) + 1, 0);
+  for (int32_t i = 0; i < np; ++i) {
+    if (P.node[i] < -1 || P.node[i] >= nn) return SR_ERR_INVALID_ARG;
+    if (P.node[i] >= 0) ++start[P.node[i] + 1];
+  }
+  for (int32_t i = 0; i < nn; ++i) start[i + 1] += start[i];
+  std::vector<int32_t> listed(np > 0 ? np : 1), cursor(start.begin(), start.end() - 1);
+  for (int32_t i = 0; i < np; ++i)
+    if (P.node[i] >= 0) listed[cursor[P.node[i]]++] = i;
+
+  const int64_t* cpu = P.cpu_sort_milli;
+  auto by_cpu_desc = [cpu](int32_t x, int32_t y) { return cpu[x] > cpu[y]; };
+  int32_t kept = 0, ns = 0, nod = 0;
+  for (int32_t node = 0; node < nn; ++node) {
+    const bool spot = node_has_label(c, node, &p->spot);
+    out->node_pod_off[node] = kept;
+    const int32_t first = kept;
+    int64_t requested = 0;
+    for (int32_t j = start[node]; j < start[node + 1]; ++j) {
+      const int32_t pod = listed[j];
+      // int(*Spec.Priority) < PriorityThreshold && isSpotNode(node)  (:139);
+      // the dereference comes first, so a nil priority panics on any node.
+      if (!P.has_priority[pod]) return SR_ERR_NIL_PRIORITY;
+      if (P.priority[pod] < p->priority_threshold && spot) continue;
+      out->node_pod_idx[kept++] = pod;
+      requested += cpu[pod];
+    }
+    out->requested_cpu[node] = requested;
+    out->free_cpu[node] = N.alloc_milli_cpu[node] - requested;
+    go_sort_slice(out->node_pod_idx + first, kept - first, by_cpu_desc);
+    if (spot)
+      out->spot[ns++] = node;
+    else if (node_has_label(c, node, &p->on_demand))
+      out->on_demand[nod++] = node;
+  }
+  out->node_pod_off[nn] = kept;
+  const int64_t* req = out->requested_cpu;
+  go_sort_slice(out->spot, ns, [req](int32_t x, int32_t y) { return req[x] > req[y]; });
+  go_sort_slice(out->on_demand, nod, [req](int32_t x, int32_t y) { return req[x] < req[y]; });
+  *out->n_spot = ns;
+  *out->n_on_demand = nod;
+  return SR_OK;
+}
+
+// scheduler NodeInfo.AddPod [upstream k8s v1.19 framework/types.go]: Requested +=
+// the pod's request, Pods += pod, UsedPorts += container host ports.
+static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod) {
+  const sr_pods& P = c->pods;
+  // int64 addition wraps in Go; do the same without signed-overflow UB.
+  auto wrap_add = [](int64_t a, int64_t b) {
+    return static_cast<int64_t>(static_cast<uint64_t>(a) + static_cast<uint64_t>(b));
+  };
+  st.requested[0] = wrap_add(st.requested[0], P.req_milli_cpu[pod]);
+  st.requested[1] = wrap_add(st.requested[1], P.req_memory[pod]);
+  st.requested[2] = wrap_add(st.requested[2], P.req_ephemeral[pod]);
+  st.npods += 1;
+  if (P.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) st.anti += 1;
+  for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i)
+    if (P.port_num[i] > 0) st.ports.push_back(Port{P.port_ip[i], P.port_proto[i], P.port_num[i]});
+}
+
+void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t pos) {
+  const int32_t before = s->state[pos].anti;
+  state_add_pod(s->state[pos], c, pod);
+  s->anti_total += s->state[pos].anti - before;
+  s->version++;
+}
+
+static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32_t n_spot,
+                                 const int32_t* off, const int32_t* idx, sr_snapshot** out) {
+  if (n_spot < 0 || (n_spot > 0 && (!spot || !off || !idx))) return SR_ERR_INVALID_ARG;
+  auto* s = new sr_snapshot();
+  s->id_empty = c->id_empty;
+  s->id_metadata_name = c->id_metadata_name;
+  s->id_unschedulable_key = c->id_unschedulable_key;
+  s->nodes.resize(n_spot);
+  s->state.resize(n_spot);
+  const sr_nodes& N = c->nodes;
+  for (int32_t i = 0; i < n_spot; ++i) {
+    const int32_t node = spot[i];
+    if (node < 0 || node >= N.n) {
+      delete s;
+      return SR_ERR_INVALID_ARG;
+    }
+    SpotNode& sn = s->nodes[i];
+    sn.name = N.name[node];
+    sn.alloc[0] = N.alloc_milli_cpu[node];
+    sn.alloc[1] = N.alloc_memory[node];
+    sn.alloc[2] = N.alloc_ephemeral[node];
+    sn.alloc_pods = N.alloc_pods[node];
+    sn.unschedulable = N.unschedulable[node];
+    for (int32_t j = N.label_off[node]; j < N.label_off[node + 1]; ++j)
+      sn.labels.emplace_back(N.label_key[j], N.label_val[j]);
+    for (int32_t j = N.taint_off[node]; j < N.taint_off[node + 1]; ++j)
+      sn.taints.push_back(TaintRec{N.taint_key[j], N.taint_val[j], N.taint_effect[j]});
+    for (int32_t j = off[node]; j < off[node + 1]; ++j) {
+      const int32_t pod = idx[j];
+      if (pod < 0 || pod >= c->pods.n) {
+        delete s;
+        return SR_ERR_INVALID_ARG;
+      }
+      state_add_pod(s->state[i], c, pod);
+    }
+    s->anti_total += s->state[i].anti;
+  }
+  *out = s;
+  return SR_OK;
+}
+
+}  // namespace sr
+
+extern "C" {
+
+sr_status sr_new_node_map(const sr_cluster* cluster, const sr_node_map_params* params, sr_node_map* out) {
+  if (!cluster || !params || !out) return SR_ERR_INVALID_ARG;
+  return sr::new_node_map(cluster, params, out);
+}
+
+int32_t sr_node_has_label(const sr_cluster* cluster, int32_t node, const sr_node_label* label) {
+  if (!cluster || !label || node < 0 || node >= cluster->nodes.n) return 0;
+  return sr::node_has_label(cluster, node, label) ? 1 : 0;
+}
+
+sr_status sr_snapshot_create(const sr_cluster* cluster, const int32_t* spot_nodes, int32_t n_spot,
+                             const int32_t* node_pod_off, const int32_t* node_pod_idx, sr_snapshot** out) {
+  if (!cluster || !out) return SR_ERR_INVALID_ARG;
+  return sr::snapshot_create(cluster, spot_nodes, n_spot, node_pod_off, node_pod_idx, out);
+}
+
+void sr_snapshot_destroy(sr_snapshot* snap) { delete snap; }
+
+sr_status sr_snapshot_add_pod(sr_snapshot* snap, const sr_cluster* cluster, int32_t pod, int32_t spot_pos) {
+  if (!snap || !cluster || pod < 0 || pod >= cluster->pods.n || spot_pos < 0 ||
+      spot_pos >= static_cast<int32_t>(snap->nodes.size()))
+    return SR_ERR_INVALID_ARG;
+  sr::snapshot_add_pod(snap, cluster, pod, spot_pos);
+  return SR_OK;
+}
+
+sr_status sr_snapshot_fork(sr_snapshot* snap) {
+  if (!snap) return SR_ERR_INVALID_ARG;
+  if (snap->forked) return SR_ERR_STATE;  // DeltaClusterSnapshot forks one level deep
+  snap->saved = snap->state;
+  snap->forked = true;
+  return SR_OK;
+}
+
+sr_status sr_snapshot_revert(sr_snapshot* snap) {
+  if (!snap) return SR_ERR_INVALID_ARG;
+  if (!snap->forked) return SR_OK;  // Revert with nothing forked leaves the snapshot as is
+  snap->state.swap(snap->saved);
+  snap->saved.clear();
+  snap->forked = false;
+  snap->anti_total = 0;
+  for (const auto& st : snap->state) snap->anti_total += st.anti;
+  snap->version++;
+  return SR_OK;
+}
+
+sr_status sr_snapshot_node_state(const sr_snapshot* snap, int32_t spot_pos, int64_t out_requested[3],
+                                 int32_t* out_num_pods) {
+  if (!snap || spot_pos < 0 || spot_pos >= static_cast<int32_t>(snap->nodes.size())) return SR_ERR_INVALID_ARG;
+  const auto& st = snap->state[spot_pos];
+  if (out_requested) std::memcpy(out_requested, st.requested, sizeof(st.requested));
+  if (out_num_pods) *out_num_pods = static_cast<int32_t>(st.npods);
+  return SR_OK;
+}
+
+int32_t sr_snapshot_num_nodes(const sr_snapshot* snap) {
+  return snap ? static_cast<int32_t>(snap->nodes.size()) : 0;
+}
+
+}  // extern "C"

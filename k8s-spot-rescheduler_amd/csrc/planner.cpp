@@ -1,0 +1,463 @@
+// planner.cpp — device context, resident buffers and the planning tick.
+//
+// sr_ctx plays the role of the reference's predicate checker (created once,
+// rescheduler.go:149).  One tick (sr_plan_run) is four kernels and one small
+// download on a single HIP stream:
+//   K0 tables -> K1 feasibility -> K2 placement -> [RCCL allreduce(min)] -> K3 winner -> D2H
+// There is no CPU path: without a HIP device sr_create fails.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "host.hpp"
+#include "kernels.hpp"
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+}  // namespace
+
+struct sr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  DevBuf arena, tables, F, out_node, out_status, dmin, result;
+  HostBuf h_arena, h_result, h_status, h_node;
+  sr::Workload wl;
+  sr::DevWorkload dw{};
+  bool prepared = false;
+  bool timing = false;
+  hipEvent_t ev[5] = {};
+  sr_timing t{};
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace {
+
+sr_status hip_fail(sr_ctx* ctx, hipError_t e, const char* what) {
+  ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+  return SR_ERR_HIP;
+}
+
+#define HIP_TRY(ctx, expr)                                  \
+  do {                                                      \
+    hipError_t _e = (expr);                                 \
+    if (_e != hipSuccess) return hip_fail((ctx), _e, #expr); \
+  } while (0)
+
+hipError_t dev_reserve(DevBuf& b, size_t bytes) {
+  if (bytes <= b.cap) return hipSuccess;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t cap = std::max<size_t>(bytes + bytes / 4, 4096);
+  hipError_t e = hipMalloc(&b.p, cap);
+  if (e == hipSuccess) b.cap = cap;
+  return e;
+}
+
+hipError_t host_reserve(HostBuf& b, size_t bytes) {
+  if (bytes <= b.cap) return hipSuccess;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t cap = std::max<size_t>(bytes + bytes / 4, 4096);
+  hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
+  if (e == hipSuccess) b.cap = cap;
+  return e;
+}
+
+// Packs host vectors into one contiguous staging buffer (256-B aligned
+// sections) so the whole workload goes up in a single copy.
+class Packer {
+ public:
+  template <class T>
+  size_t add(const std::vector<T>& v) {
+    size_t off = (size_ + 255) & ~size_t(255);
+    items_.push_back({off, v.data(), v.size() * sizeof(T)});
+    size_ = off + v.size() * sizeof(T);
+    return off;
+  }
+  size_t size() const { return (size_ + 255) & ~size_t(255); }
+  void copy_to(char* dst) const {
+    for (const auto& it : items_)
+      if (it.bytes) std::memcpy(dst + it.off, it.src, it.bytes);
+  }
+
+ private:
+  struct Item {
+    size_t off;
+    const void* src;
+    size_t bytes;
+  };
+  std::vector<Item> items_;
+  size_t size_ = 0;
+};
+
+sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands) {
+  auto t0 = std::chrono::steady_clock::now();
+  ctx->prepared = false;
+  sr::Workload& w = ctx->wl;
+  std::string err;
+  sr_status st = sr::encode_workload(snap, c, cands, &w, &err);
+  if (st != SR_OK) {
+    ctx->err = err;
+    return st;
+  }
+  const int32_t na = static_cast<int32_t>(w.pod_a.size());
+  const int32_t ncand = static_cast<int32_t>(w.cand_global.size());
+  if (static_cast<uint64_t>(na) * static_cast<uint64_t>(w.Wp / 2) >= (1ull << 31)) {
+    ctx->err = "pod x node bitmask exceeds 2^31 16-byte items";
+    return SR_ERR_CAPACITY;
+  }
+  Packer pk;
+  const size_t o_fc = pk.add(w.free_cpu), o_fm = pk.add(w.free_mem), o_fe = pk.add(w.free_eph);
+  const size_t o_pl = pk.add(w.pods_left), o_pb = pk.add(w.port_bits);
+  const size_t o_rb = pk.add(w.req_bits), o_tb = pk.add(w.taint_bits);
+  const size_t o_cs = pk.add(w.cls_sel), o_ct = pk.add(w.cls_tol), o_cp = pk.add(w.cls_port);
+  const size_t o_cf = pk.add(w.cls_flags), o_cto = pk.add(w.cls_term_off), o_tm = pk.add(w.term_mask);
+  const size_t o_ac = pk.add(w.a_class), o_az = pk.add(w.a_zero), o_acp = pk.add(w.a_cpu), o_ae = pk.add(w.a_eph);
+  const size_t o_bm = pk.add(w.b_mem), o_ba = pk.add(w.b_all);
+  const size_t o_pa = pk.add(w.pod_a), o_pbb = pk.add(w.pod_b), o_pz = pk.add(w.pod_zero);
+  const size_t o_pc = pk.add(w.pod_cpu), o_pm = pk.add(w.pod_mem), o_pe = pk.add(w.pod_eph);
+  const size_t o_pp = pk.add(w.pod_ports);
+  const size_t o_co = pk.add(w.cand_off), o_cg = pk.add(w.cand_global);
+  const size_t o_ls = pk.add(w.list_small), o_ll = pk.add(w.list_large);
+  const size_t bytes = pk.size();
+
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, host_reserve(ctx->h_arena, bytes));
+  HIP_TRY(ctx, dev_reserve(ctx->arena, bytes));
+  const size_t n_rows = static_cast<size_t>(w.a_class.size() + w.b_mem.size());
+  const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
+  HIP_TRY(ctx, dev_reserve(ctx->tables, n_rows * row_bytes));
+  HIP_TRY(ctx, dev_reserve(ctx->F, std::max<size_t>(1, static_cast<size_t>(na)) * row_bytes));
+  HIP_TRY(ctx, dev_reserve(ctx->out_node, sizeof(int32_t) * std::max(1, na)));
+  HIP_TRY(ctx, dev_reserve(ctx->out_status, sizeof(int32_t) * std::max(1, ncand)));
+  HIP_TRY(ctx, dev_reserve(ctx->dmin, 64));
+  const size_t res_bytes = sizeof(int32_t) * (4 + static_cast<size_t>(std::max(1, w.max_cand_pods)));
+  HIP_TRY(ctx, dev_reserve(ctx->result, res_bytes));
+  HIP_TRY(ctx, host_reserve(ctx->h_result, res_bytes));
+  auto t1 = std::chrono::steady_clock::now();
+  pk.copy_to(static_cast<char*>(ctx->h_arena.p));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->arena.p, ctx->h_arena.p, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  auto t2 = std::chrono::steady_clock::now();
+
+  char* base = static_cast<char*>(ctx->arena.p);
+  auto at = [base](size_t off) { return static_cast<void*>(base + off); };
+  sr::DevWorkload& d = ctx->dw;
+  d = sr::DevWorkload{};
+  d.n_spot = w.n_spot;
+  d.n_pad = w.n_pad;
+  d.Wp = w.Wp;
+  d.WR = w.WR;
+  d.WT = w.WT;
+  d.free_cpu = static_cast<const int64_t*>(at(o_fc));
+  d.free_mem = static_cast<const int64_t*>(at(o_fm));
+  d.free_eph = static_cast<const int64_t*>(at(o_fe));
+  d.pods_left = static_cast<const int32_t*>(at(o_pl));
+  d.port_bits = static_cast<const uint64_t*>(at(o_pb));
+  d.req_bits = static_cast<const uint64_t*>(at(o_rb));
+  d.taint_bits = static_cast<const uint64_t*>(at(o_tb));
+  d.cls_sel = static_cast<const uint64_t*>(at(o_cs));
+  d.cls_tol = static_cast<const uint64_t*>(at(o_ct));
+  d.cls_port = static_cast<const uint64_t*>(at(o_cp));
+  d.cls_flags = static_cast<const int32_t*>(at(o_cf));
+  d.cls_term_off = static_cast<const int32_t*>(at(o_cto));
+  d.term_mask = static_cast<const uint64_t*>(at(o_tm));
+  d.n_a = static_cast<int32_t>(w.a_class.size());
+  d.n_b = static_cast<int32_t>(w.b_mem.size());
+  d.a_class = static_cast<const int32_t*>(at(o_ac));
+  d.a_zero = static_cast<const int32_t*>(at(o_az));
+  d.a_cpu = static_cast<const int64_t*>(at(o_acp));
+  d.a_eph = static_cast<const int64_t*>(at(o_ae));
+  d.b_mem = static_cast<const int64_t*>(at(o_bm));
+  d.b_all = static_cast<const int32_t*>(at(o_ba));
+  d.n_pods = na;
+  d.pod_a = static_cast<const int32_t*>(at(o_pa));
+  d.pod_b = static_cast<const int32_t*>(at(o_pbb));
+  d.pod_zero = static_cast<const int32_t*>(at(o_pz));
+  d.pod_cpu = static_cast<const int64_t*>(at(o_pc));
+  d.pod_mem = static_cast<const int64_t*>(at(o_pm));
+  d.pod_eph = static_cast<const int64_t*>(at(o_pe));
+  d.pod_ports = static_cast<const uint64_t*>(at(o_pp));
+  d.n_cand = ncand;
+  d.cand_off = static_cast<const int32_t*>(at(o_co));
+  d.cand_global = static_cast<const int32_t*>(at(o_cg));
+  d.list_small = static_cast<const int32_t*>(at(o_ls));
+  d.list_large = static_cast<const int32_t*>(at(o_ll));
+  d.n_small = static_cast<int32_t>(w.list_small.size());
+  d.n_large = static_cast<int32_t>(w.list_large.size());
+  d.A = static_cast<uint64_t*>(ctx->tables.p);
+  d.B = d.A + w.a_class.size() * static_cast<size_t>(w.Wp);
+  d.F = static_cast<uint64_t*>(ctx->F.p);
+  d.out_node = static_cast<int32_t*>(ctx->out_node.p);
+  d.out_status = static_cast<int32_t*>(ctx->out_status.p);
+  d.d_min = static_cast<int32_t*>(ctx->dmin.p);
+  d.result = static_cast<int32_t*>(ctx->result.p);
+
+  const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
+  ctx->t.bytes_feasibility = static_cast<uint64_t>(na) * row + n_rows * row + 8ull * na;
+  uint64_t k2 = 0;
+  for (int32_t q = 0; q < na; ++q) k2 += 8ull * std::min(w.Wp, 64) + 48;
+  ctx->t.bytes_placement = k2 + 16ull * ncand;
+  ctx->t.ms_pack_host = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  ctx->t.ms_upload = std::chrono::duration<double, std::milli>(t2 - t1).count();
+  ctx->t.n_pods = na;
+  ctx->t.n_spot = w.n_spot;
+  ctx->t.n_cand = ncand;
+  ctx->t.n_words = w.Wp;
+  ctx->t.n_rows_a = d.n_a;
+  ctx->t.n_rows_b = d.n_b;
+  ctx->t.n_classes = w.n_classes;
+  ctx->prepared = true;
+  return SR_OK;
+}
+
+sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
+  if (!ctx->prepared) {
+    ctx->err = "sr_plan_run before sr_plan_prepare";
+    return SR_ERR_STATE;
+  }
+  const sr::Workload& w = ctx->wl;
+  const sr::DevWorkload& d = ctx->dw;
+  hipStream_t s = ctx->stream;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[0], s));
+  HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s));
+  if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[1], s));
+  HIP_TRY(ctx, sr::launch_feasibility(d, s));
+  if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[2], s));
+  HIP_TRY(ctx, sr::launch_placement(d, s));
+  if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[3], s));
+  if (ctx->comm && use_comm) {
+    ncclResult_t r = ncclAllReduce(d.d_min, d.d_min, 2, ncclInt32, ncclMin, ctx->comm, s);
+    if (r != ncclSuccess) {
+      ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+      return SR_ERR_RCCL;
+    }
+  }
+  HIP_TRY(ctx, sr::launch_winner(d, s));
+  const size_t res_bytes = sizeof(int32_t) * (4 + static_cast<size_t>(std::max(1, w.max_cand_pods)));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->h_result.p, d.result, res_bytes, hipMemcpyDeviceToHost, s));
+  const int32_t na = d.n_pods, ncand = d.n_cand;
+  if (full) {
+    HIP_TRY(ctx, host_reserve(ctx->h_status, sizeof(int32_t) * std::max(1, ncand)));
+    HIP_TRY(ctx, host_reserve(ctx->h_node, sizeof(int32_t) * std::max(1, na)));
+    if (ncand)
+      HIP_TRY(ctx, hipMemcpyAsync(ctx->h_status.p, d.out_status, sizeof(int32_t) * ncand, hipMemcpyDeviceToHost, s));
+    if (na) HIP_TRY(ctx, hipMemcpyAsync(ctx->h_node.p, d.out_node, sizeof(int32_t) * na, hipMemcpyDeviceToHost, s));
+  }
+  if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[4], s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  if (ctx->timing) {
+    float ms[4];
+    for (int i = 0; i < 4; ++i) HIP_TRY(ctx, hipEventElapsedTime(&ms[i], ctx->ev[i], ctx->ev[i + 1]));
+    ctx->t.ms_tables += ms[0];
+    ctx->t.ms_feasibility += ms[1];
+    ctx->t.ms_placement += ms[2];
+    ctx->t.ms_winner += ms[3];
+    ctx->t.n_runs += 1;
+  }
+
+  const int32_t* r = static_cast<const int32_t*>(ctx->h_result.p);
+  out->first_ok = r[0];
+  out->first_fallback = r[3];
+  out->winner = (r[0] >= 0 && (r[3] < 0 || r[3] > r[0])) ? r[0] : -1;
+  out->winner_npods = r[1] ? r[2] : 0;
+  if (out->winner_map && r[1]) std::memcpy(out->winner_map, r + 4, sizeof(int32_t) * r[2]);
+  out->checks = static_cast<uint64_t>(na) * static_cast<uint64_t>(w.n_spot);
+  out->fallback_pods = w.fallback_pods;
+  if (full) {
+    const int32_t* hs = static_cast<const int32_t*>(ctx->h_status.p);
+    const int32_t* hn = static_cast<const int32_t*>(ctx->h_node.p);
+    if (out->status) {
+      for (int32_t i = 0; i < w.n_input_cand; ++i) out->status[i] = w.status_host[i];
+      for (int32_t k = 0; k < ncand; ++k) out->status[w.cand_src[k]] = hs[k];
+    }
+    if (out->node_of_pod) {
+      for (int32_t i = 0; i < w.n_input_pods; ++i) out->node_of_pod[i] = -1;
+      for (int32_t q = 0; q < na; ++q) out->node_of_pod[w.pod_src[q]] = hn[q];
+    }
+  }
+  return SR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sr_build_info(void) {
+  return "srplanner abi=1 target=gfx950 kernels=K0-tables,K1-feasibility,K2-placement,K3-winner";
+}
+
+sr_status sr_create(int32_t device, sr_ctx** out) {
+  if (!out) return SR_ERR_INVALID_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SR_ERR_NO_DEVICE;
+  if (device < 0 || device >= count) return SR_ERR_INVALID_ARG;
+  auto* ctx = new sr_ctx();
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return SR_ERR_HIP;
+  }
+  for (auto& e : ctx->ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete ctx;
+      return SR_ERR_HIP;
+    }
+  *out = ctx;
+  return SR_OK;
+}
+
+void sr_destroy(sr_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  for (DevBuf* b : {&ctx->arena, &ctx->tables, &ctx->F, &ctx->out_node, &ctx->out_status, &ctx->dmin, &ctx->result})
+    if (b->p) (void)hipFree(b->p);
+  for (HostBuf* b : {&ctx->h_arena, &ctx->h_result, &ctx->h_status, &ctx->h_node})
+    if (b->p) (void)hipHostFree(b->p);
+  for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* sr_last_error(const sr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+sr_status sr_plan_prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* cluster, const sr_candidates* cands) {
+  if (!ctx || !snap || !cluster || !cands || cands->n_cand < 0) return SR_ERR_INVALID_ARG;
+  return prepare(ctx, snap, cluster, cands);
+}
+
+sr_status sr_plan_run(sr_ctx* ctx, sr_plan_out* out) {
+  if (!ctx || !out) return SR_ERR_INVALID_ARG;
+  return run(ctx, out, out->status != nullptr || out->node_of_pod != nullptr, true);
+}
+
+sr_status sr_plan(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* cluster, const sr_candidates* cands,
+                  sr_plan_out* out) {
+  if (!ctx || !snap || !cluster || !cands || !out || cands->n_cand < 0) return SR_ERR_INVALID_ARG;
+  sr_status st = prepare(ctx, snap, cluster, cands);
+  if (st != SR_OK) return st;
+  return run(ctx, out, out->status != nullptr || out->node_of_pod != nullptr, true);
+}
+
+// Single-process helpers (no collective): findSpotNodeForPod / canDrainNode.
+static sr_status plan_local(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* cluster,
+                            const sr_candidates* cands, sr_plan_out* out) {
+  sr_status st = prepare(ctx, snap, cluster, cands);
+  if (st != SR_OK) return st;
+  return run(ctx, out, true, false);
+}
+
+sr_status sr_find_spot_nodes(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* cluster, const int32_t* pods,
+                             int32_t n, int32_t* out_spot_pos, uint8_t* out_fallback) {
+  if (!ctx || !snap || !cluster || n < 0 || (n > 0 && (!pods || !out_spot_pos))) return SR_ERR_INVALID_ARG;
+  if (n == 0) return SR_OK;
+  std::vector<int32_t> off(static_cast<size_t>(n) + 1), status(n);
+  for (int32_t i = 0; i <= n; ++i) off[i] = i;
+  sr_candidates c{n, off.data(), pods, nullptr};
+  sr_plan_out o{};
+  o.status = status.data();
+  o.node_of_pod = out_spot_pos;
+  sr_status st = plan_local(ctx, snap, cluster, &c, &o);
+  if (st != SR_OK) return st;
+  if (out_fallback)
+    for (int32_t i = 0; i < n; ++i) out_fallback[i] = status[i] == SR_CAND_FALLBACK ? 1 : 0;
+  return SR_OK;
+}
+
+sr_status sr_can_drain_node(sr_ctx* ctx, sr_snapshot* snap, const sr_cluster* cluster, const int32_t* pods,
+                            int32_t n, int32_t* out_node_of_pod, int32_t* out_fail_pod, uint8_t* out_fallback) {
+  if (!ctx || !snap || !cluster || n < 0 || (n > 0 && !pods) || !out_fail_pod) return SR_ERR_INVALID_ARG;
+  std::vector<int32_t> map(static_cast<size_t>(std::max(1, n)), -1);
+  int32_t off[2] = {0, n}, status = SR_CAND_EMPTY;
+  if (out_fallback) *out_fallback = 0;
+  *out_fail_pod = -1;
+  if (n > 0) {
+    sr_candidates c{1, off, pods, nullptr};
+    sr_plan_out o{};
+    o.status = &status;
+    o.node_of_pod = map.data();
+    sr_status st = plan_local(ctx, snap, cluster, &c, &o);
+    if (st != SR_OK) return st;
+    if (status == SR_CAND_FALLBACK) {
+      if (out_fallback) *out_fallback = 1;
+      if (out_node_of_pod)
+        for (int32_t i = 0; i < n; ++i) out_node_of_pod[i] = -1;
+      return SR_OK;
+    }
+    *out_fail_pod = status >= 0 ? status : -1;
+    // Side effect of the reference: every placed pod is added to the snapshot
+    // (rescheduler.go:366), also those before a failing pod.
+    for (int32_t i = 0; i < n; ++i)
+      if (map[i] >= 0) sr::snapshot_add_pod(snap, cluster, pods[i], map[i]);
+  }
+  if (out_node_of_pod)
+    for (int32_t i = 0; i < n; ++i) out_node_of_pod[i] = map[i];
+  return SR_OK;
+}
+
+sr_status sr_set_timing(sr_ctx* ctx, int32_t enable) {
+  if (!ctx) return SR_ERR_INVALID_ARG;
+  ctx->timing = enable != 0;
+  ctx->t.n_runs = 0;
+  ctx->t.ms_tables = ctx->t.ms_feasibility = ctx->t.ms_placement = ctx->t.ms_winner = 0;
+  return SR_OK;
+}
+
+sr_status sr_get_timing(const sr_ctx* ctx, sr_timing* out) {
+  if (!ctx || !out) return SR_ERR_INVALID_ARG;
+  *out = ctx->t;
+  return SR_OK;
+}
+
+sr_status sr_comm_unique_id(uint8_t out[SR_UNIQUE_ID_BYTES]) {
+  if (!out) return SR_ERR_INVALID_ARG;
+  ncclUniqueId id;
+  static_assert(sizeof(id) == SR_UNIQUE_ID_BYTES, "ncclUniqueId size");
+  if (ncclGetUniqueId(&id) != ncclSuccess) return SR_ERR_RCCL;
+  std::memcpy(out, &id, sizeof(id));
+  return SR_OK;
+}
+
+sr_status sr_comm_init(sr_ctx* ctx, const uint8_t id[SR_UNIQUE_ID_BYTES], int32_t nranks, int32_t rank) {
+  if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return SR_ERR_INVALID_ARG;
+  if (hipSetDevice(ctx->device) != hipSuccess) return SR_ERR_HIP;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    ctx->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+    ctx->comm = nullptr;
+    return SR_ERR_RCCL;
+  }
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return SR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,40 @@
+/*
+ * sr_synth.h — deterministic synthetic clusters for the BASELINE.json configs
+ * (bench / test infrastructure; the generator spec is in DESIGN.md §Workloads).
+ * Output is a cluster in the sr_cluster layout of include/sr_planner.h, with
+ * nodes and pods in a fixed "API list" order.
+ */
+#ifndef SR_SYNTH_H
+#define SR_SYNTH_H
+
+#include <stdint.h>
+
+#include "../../../include/sr_planner.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  int32_t config;          /* 1..5 = BASELINE.json configs[0..4] */
+  uint64_t seed;           /* 0 = 0x5EED0000 + config */
+  int32_t n_on_demand;     /* 0 = config default */
+  int32_t n_spot;          /* 0 = config default */
+  double pinned_fraction;  /* < 0 = default; share of on-demand pods pinned to on-demand nodes */
+} sr_synth_params;
+
+typedef struct sr_synth sr_synth;
+
+sr_synth *sr_synth_generate(const sr_synth_params *params);
+void sr_synth_destroy(sr_synth *s);
+/* Pointers stay valid until sr_synth_destroy. */
+void sr_synth_view(const sr_synth *s, sr_cluster *out);
+/* The --on-demand-node-label / --spot-node-label flags of the cluster (defaults of rescheduler.go:98-105). */
+void sr_synth_labels(const sr_synth *s, sr_node_label *on_demand, sr_node_label *spot);
+const char *sr_synth_string(const sr_synth *s, int32_t id);
+int32_t sr_synth_num_strings(const sr_synth *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

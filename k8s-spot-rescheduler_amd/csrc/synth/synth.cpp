@@ -1,0 +1,387 @@
+// synth.cpp — deterministic synthetic clusters (bench / test infrastructure).
+//
+// Spec (after SURVEY.md §8d): splitmix64 seeded with
+// 0x5EED0000 + config; nodes in a shuffled on-demand/spot "API list" order;
+// every node gets one DaemonSet pod first, then ReplicaSet pods until a
+// per-node CPU fill target; pod CPU drawn from {50,100,100,250,500,1000,2000}m
+// (tie-heavy on purpose: Go's unstable sort order matters), memory
+// log-uniform 64Mi..8Gi.  Config-specific mixes: PreferNoSchedule taints (C2),
+// zones / instance types / teams, nodeSelector, required node affinity,
+// NoSchedule dedicated taints and tolerations, pods pinned to on-demand nodes
+// (C3/C4), host ports + specific host IPs (C5).
+#include "sr_synth.h"
+
+#include <cmath>
+#include <cstdio>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+struct sr_synth {
+  std::vector<std::string> strings;
+  std::unordered_map<std::string, int32_t> ids;
+  // nodes
+  std::vector<int32_t> name;
+  std::vector<int64_t> alloc_cpu, alloc_mem, alloc_eph, alloc_pods;
+  std::vector<uint8_t> unsched;
+  std::vector<int32_t> label_off{0}, label_key, label_val;
+  std::vector<int32_t> taint_off{0}, taint_key, taint_val, taint_eff;
+  // pods
+  std::vector<int32_t> pod_node;
+  std::vector<int64_t> cpu_sort, req_cpu, req_mem, req_eph;
+  std::vector<int32_t> priority;
+  std::vector<uint8_t> has_priority;
+  std::vector<uint32_t> flags;
+  std::vector<int32_t> sel_off{0}, sel_key, sel_val;
+  std::vector<uint8_t> aff;
+  std::vector<int32_t> term_off{0}, term_expr_off{0}, term_field_off{0};
+  std::vector<int32_t> expr_key, expr_op, expr_val_off{0}, expr_vals;
+  std::vector<int32_t> field_key, field_op, field_val_off{0}, field_vals;
+  std::vector<int32_t> tol_off{0}, tol_key, tol_op, tol_val, tol_eff;
+  std::vector<int32_t> port_off{0}, port_proto, port_num, port_ip;
+  sr_node_label od{}, spot{};
+
+  int32_t id(const std::string& s) {
+    auto it = ids.find(s);
+    if (it != ids.end()) return it->second;
+    int32_t i = static_cast<int32_t>(strings.size());
+    ids.emplace(s, i);
+    strings.push_back(s);
+    return i;
+  }
+};
+
+namespace {
+
+struct Rng {
+  uint64_t s;
+  uint64_t next() {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  double uni() { return static_cast<double>(next() >> 11) * (1.0 / 9007199254740992.0); }
+  int below(int n) { return static_cast<int>(next() % static_cast<uint64_t>(n)); }
+  bool chance(double p) { return uni() < p; }
+};
+
+constexpr int64_t kMi = 1024ll * 1024;
+constexpr int64_t kGi = 1024ll * kMi;
+
+struct Cfg {
+  int n_od, n_spot, pods_min, pods_max;
+  double od_fill_lo, od_fill_hi, spot_fill_lo, spot_fill_hi;
+  bool prefer_taints, topology, constraints, ports;
+  double pinned;
+};
+
+Cfg config_defaults(int c) {
+  switch (c) {
+    case 1: return {10, 10, 9, 9, 0.3, 0.6, 0.4, 0.9, false, false, false, false, 0.0};
+    case 2: return {300, 700, 0, 0, 0.55, 0.98, 0.55, 0.98, true, true, false, false, 0.0};
+    case 3: return {1500, 3500, 0, 0, 0.5, 0.98, 0.5, 0.98, false, true, true, false, 0.15};
+    case 4: return {15000, 35000, 0, 0, 0.5, 0.98, 0.5, 0.98, false, true, true, false, 0.15};
+    default: return {300, 700, 0, 0, 0.55, 0.98, 0.55, 0.98, false, true, false, true, 0.0};
+  }
+}
+
+struct PodSpec {
+  int64_t cpu = 0, mem = 0, eph = 0;
+  int32_t prio = 0;
+  uint32_t flags = 0;
+  std::vector<std::pair<int32_t, int32_t>> sel;
+  bool aff = false;
+  struct Expr {
+    int32_t key, op;
+    std::vector<int32_t> vals;
+  };
+  std::vector<std::vector<Expr>> terms;
+  struct Tol {
+    int32_t key, op, val, eff;
+  };
+  std::vector<Tol> tols;
+  struct P {
+    int32_t proto, port, ip;
+  };
+  std::vector<P> ports;
+};
+
+void push_pod(sr_synth* s, int32_t node, const PodSpec& p) {
+  s->pod_node.push_back(node);
+  s->cpu_sort.push_back(p.cpu);
+  s->req_cpu.push_back(p.cpu);
+  s->req_mem.push_back(p.mem);
+  s->req_eph.push_back(p.eph);
+  s->priority.push_back(p.prio);
+  s->has_priority.push_back(1);
+  s->flags.push_back(p.flags);
+  for (auto& kv : p.sel) {
+    s->sel_key.push_back(kv.first);
+    s->sel_val.push_back(kv.second);
+  }
+  s->sel_off.push_back(static_cast<int32_t>(s->sel_key.size()));
+  s->aff.push_back(p.aff ? 1 : 0);
+  for (auto& t : p.terms) {
+    for (auto& e : t) {
+      s->expr_key.push_back(e.key);
+      s->expr_op.push_back(e.op);
+      s->expr_vals.insert(s->expr_vals.end(), e.vals.begin(), e.vals.end());
+      s->expr_val_off.push_back(static_cast<int32_t>(s->expr_vals.size()));
+    }
+    s->term_expr_off.push_back(static_cast<int32_t>(s->expr_key.size()));
+    s->term_field_off.push_back(static_cast<int32_t>(s->field_key.size()));
+  }
+  s->term_off.push_back(static_cast<int32_t>(s->term_expr_off.size() - 1));
+  for (auto& t : p.tols) {
+    s->tol_key.push_back(t.key);
+    s->tol_op.push_back(t.op);
+    s->tol_val.push_back(t.val);
+    s->tol_eff.push_back(t.eff);
+  }
+  s->tol_off.push_back(static_cast<int32_t>(s->tol_key.size()));
+  for (auto& q : p.ports) {
+    s->port_proto.push_back(q.proto);
+    s->port_num.push_back(q.port);
+    s->port_ip.push_back(q.ip);
+  }
+  s->port_off.push_back(static_cast<int32_t>(s->port_proto.size()));
+}
+
+}  // namespace
+
+extern "C" {
+
+sr_synth* sr_synth_generate(const sr_synth_params* prm) {
+  const int config = prm && prm->config >= 1 && prm->config <= 5 ? prm->config : 1;
+  Cfg cfg = config_defaults(config);
+  if (prm && prm->n_on_demand > 0) cfg.n_od = prm->n_on_demand;
+  if (prm && prm->n_spot > 0) cfg.n_spot = prm->n_spot;
+  if (prm && prm->pinned_fraction >= 0) cfg.pinned = prm->pinned_fraction;
+  Rng rng{prm && prm->seed ? prm->seed : 0x5EED0000ull + static_cast<uint64_t>(config)};
+  auto* s = new sr_synth();
+  // fixed ids first
+  const int32_t E = s->id(""), MN = s->id("metadata.name"), UK = s->id("node.kubernetes.io/unschedulable");
+  (void)E;
+  (void)MN;
+  (void)UK;
+  const int32_t ROLE = s->id("kubernetes.io/role"), WORKER = s->id("worker"), SPOTW = s->id("spot-worker");
+  const int32_t HOST = s->id("kubernetes.io/hostname");
+  const int32_t ZONE = s->id("topology.kubernetes.io/zone");
+  const int32_t ITYPE = s->id("node.kubernetes.io/instance-type");
+  const int32_t TEAM = s->id("team"), DEDICATED = s->id("dedicated"), GPU = s->id("gpu");
+  const int32_t ODT = s->id("on-demand"), SPT = s->id("spot"), TRUE_ = s->id("true");
+  int32_t zones[3], teams[4], types[8];
+  for (int i = 0; i < 3; ++i) zones[i] = s->id(std::string("zone-") + static_cast<char>('a' + i));
+  for (int i = 0; i < 4; ++i) teams[i] = s->id(std::string("team-") + static_cast<char>('a' + i));
+  const int type_cores[8] = {4, 8, 16, 32, 64, 8, 16, 32};
+  const int type_gib[8] = {16, 32, 64, 128, 256, 16, 32, 256};
+  for (int i = 0; i < 8; ++i) types[i] = s->id("type-" + std::to_string(i));
+  const int n_types = cfg.topology && cfg.constraints ? 8 : 5;
+  s->od = sr_node_label{ROLE, WORKER, 1};
+  s->spot = sr_node_label{ROLE, SPOTW, 1};
+
+  const int n_nodes = cfg.n_od + cfg.n_spot;
+  std::vector<uint8_t> is_spot(n_nodes, 0);
+  for (int i = 0; i < cfg.n_spot; ++i) is_spot[i] = 1;
+  for (int i = n_nodes - 1; i > 0; --i) std::swap(is_spot[i], is_spot[rng.below(i + 1)]);  // list order
+
+  const int64_t cpu_choices[7] = {50, 100, 100, 250, 500, 1000, 2000};
+  char buf[64];
+  for (int node = 0; node < n_nodes; ++node) {
+    const bool spot = is_spot[node];
+    std::snprintf(buf, sizeof(buf), "node-%06d", node);
+    const int32_t nm = s->id(buf);
+    const int t = rng.below(n_types);
+    s->name.push_back(nm);
+    s->alloc_cpu.push_back(1000ll * type_cores[t]);
+    s->alloc_mem.push_back(type_gib[t] * kGi);
+    s->alloc_eph.push_back(100 * kGi);
+    s->alloc_pods.push_back(110);
+    const bool unsched = cfg.constraints && spot && rng.chance(0.01);
+    s->unsched.push_back(unsched ? 1 : 0);
+    // labels
+    s->label_key.push_back(ROLE);
+    s->label_val.push_back(spot ? SPOTW : WORKER);
+    s->label_key.push_back(HOST);
+    s->label_val.push_back(nm);
+    int32_t team = -1;
+    if (cfg.topology) {
+      s->label_key.push_back(ZONE);
+      s->label_val.push_back(zones[rng.below(3)]);
+      s->label_key.push_back(ITYPE);
+      s->label_val.push_back(types[t]);
+    }
+    if (cfg.constraints && rng.chance(0.5)) {
+      team = teams[rng.below(4)];
+      s->label_key.push_back(TEAM);
+      s->label_val.push_back(team);
+    }
+    s->label_off.push_back(static_cast<int32_t>(s->label_key.size()));
+    // taints
+    if (cfg.prefer_taints && (!spot || rng.chance(0.10))) {
+      s->taint_key.push_back(spot ? SPT : ODT);
+      s->taint_val.push_back(TRUE_);
+      s->taint_eff.push_back(SR_EFFECT_PREFER_NO_SCHEDULE);
+    }
+    if (cfg.constraints && spot && rng.chance(0.15)) {
+      s->taint_key.push_back(DEDICATED);
+      s->taint_val.push_back(team >= 0 ? team : teams[rng.below(4)]);
+      s->taint_eff.push_back(SR_EFFECT_NO_SCHEDULE);
+    }
+    if (unsched) {
+      s->taint_key.push_back(UK);
+      s->taint_val.push_back(E);
+      s->taint_eff.push_back(SR_EFFECT_NO_SCHEDULE);
+    }
+    s->taint_off.push_back(static_cast<int32_t>(s->taint_key.size()));
+
+    // DaemonSet pod first in the node's list
+    PodSpec ds;
+    ds.cpu = 100;
+    ds.mem = 128 * kMi;
+    ds.flags = SR_POD_DAEMONSET_CONTROLLER;
+    if (cfg.ports) ds.ports.push_back({SR_PROTO_TCP, 9100, -1});
+    push_pod(s, node, ds);
+    // ReplicaSet pods up to a CPU fill target
+    const double lo = spot ? cfg.spot_fill_lo : cfg.od_fill_lo, hi = spot ? cfg.spot_fill_hi : cfg.od_fill_hi;
+    const int64_t target = static_cast<int64_t>((lo + (hi - lo) * rng.uni()) * 1000.0 * type_cores[t]);
+    // C1 has a fixed pod count (rescheduler_test-sized); the others fill each
+    // node to its CPU target (at most 109 pods: allocatable pods is 110).
+    const int want = config == 1 ? cfg.pods_min : 108;
+    int64_t used = ds.cpu;
+    for (int k = 0; k < want; ++k) {
+      PodSpec p;
+      p.cpu = cpu_choices[rng.below(7)];
+      if (config != 1 && used + p.cpu > target) break;
+      used += p.cpu;
+      p.mem = static_cast<int64_t>(std::exp(std::log(64.0) + (std::log(8192.0) - std::log(64.0)) * rng.uni())) * kMi;
+      if (cfg.constraints && rng.chance(0.10)) p.eph = (1 + rng.below(10)) * kGi;
+      if (spot && rng.chance(0.10)) p.prio = -1;
+      if (!spot && cfg.constraints) {
+        if (rng.chance(cfg.pinned)) {
+          p.sel.push_back({ROLE, WORKER});  // pinned to on-demand nodes: never movable to spot
+        } else if (rng.chance(0.20)) {
+          const int kind = rng.below(4);
+          if (kind < 2) p.sel.push_back({ZONE, zones[rng.below(3)]});
+          else if (kind == 2) p.sel.push_back({ITYPE, types[rng.below(n_types)]});
+          else p.sel.push_back({TEAM, teams[rng.below(4)]});
+        }
+        if (rng.chance(0.10)) {
+          p.aff = true;
+          const int nt = 1 + rng.below(3);
+          for (int ti = 0; ti < nt; ++ti) {
+            std::vector<PodSpec::Expr> term;
+            const int ne = 1 + rng.below(2);
+            for (int ei = 0; ei < ne; ++ei) {
+              switch (rng.below(4)) {
+                case 0:
+                  term.push_back({ZONE, SR_OP_IN, {zones[rng.below(3)], zones[rng.below(3)]}});
+                  break;
+                case 1:
+                  term.push_back({ITYPE, SR_OP_NOT_IN, {types[rng.below(n_types)]}});
+                  break;
+                case 2:
+                  term.push_back({TEAM, SR_OP_EXISTS, {}});
+                  break;
+                default:
+                  term.push_back({GPU, SR_OP_DOES_NOT_EXIST, {}});
+                  break;
+              }
+            }
+            p.terms.push_back(std::move(term));
+          }
+        }
+        if (rng.chance(0.20)) {
+          if (rng.chance(0.5))
+            p.tols.push_back({DEDICATED, SR_TOL_EQUAL, teams[rng.below(4)], SR_EFFECT_NO_SCHEDULE});
+          else
+            p.tols.push_back({DEDICATED, SR_TOL_EXISTS, E, SR_EFFECT_EMPTY});
+        }
+      }
+      if (cfg.ports && rng.chance(0.30)) {
+        static const int32_t kPorts[3] = {80, 443, 8080};
+        const int32_t port = kPorts[rng.below(3)];
+        int32_t ip = -1;
+        if (rng.chance(0.02)) {
+          std::snprintf(buf, sizeof(buf), "10.0.%d.%d", rng.below(4), rng.below(250));
+          ip = s->id(buf);
+        }
+        p.ports.push_back({SR_PROTO_TCP, port, ip});
+      }
+      push_pod(s, node, p);
+    }
+  }
+  return s;
+}
+
+void sr_synth_destroy(sr_synth* s) { delete s; }
+
+void sr_synth_view(const sr_synth* s, sr_cluster* c) {
+  sr_nodes& n = c->nodes;
+  n.n = static_cast<int32_t>(s->name.size());
+  n.name = s->name.data();
+  n.alloc_milli_cpu = s->alloc_cpu.data();
+  n.alloc_memory = s->alloc_mem.data();
+  n.alloc_ephemeral = s->alloc_eph.data();
+  n.alloc_pods = s->alloc_pods.data();
+  n.unschedulable = s->unsched.data();
+  n.label_off = s->label_off.data();
+  n.label_key = s->label_key.data();
+  n.label_val = s->label_val.data();
+  n.taint_off = s->taint_off.data();
+  n.taint_key = s->taint_key.data();
+  n.taint_val = s->taint_val.data();
+  n.taint_effect = s->taint_eff.data();
+  sr_pods& p = c->pods;
+  p.n = static_cast<int32_t>(s->pod_node.size());
+  p.node = s->pod_node.data();
+  p.cpu_sort_milli = s->cpu_sort.data();
+  p.req_milli_cpu = s->req_cpu.data();
+  p.req_memory = s->req_mem.data();
+  p.req_ephemeral = s->req_eph.data();
+  p.priority = s->priority.data();
+  p.has_priority = s->has_priority.data();
+  p.flags = s->flags.data();
+  p.sel_off = s->sel_off.data();
+  p.sel_key = s->sel_key.data();
+  p.sel_val = s->sel_val.data();
+  p.aff_required = s->aff.data();
+  p.term_off = s->term_off.data();
+  p.term_expr_off = s->term_expr_off.data();
+  p.term_field_off = s->term_field_off.data();
+  p.expr_key = s->expr_key.data();
+  p.expr_op = s->expr_op.data();
+  p.expr_val_off = s->expr_val_off.data();
+  p.expr_vals = s->expr_vals.data();
+  p.field_key = s->field_key.data();
+  p.field_op = s->field_op.data();
+  p.field_val_off = s->field_val_off.data();
+  p.field_vals = s->field_vals.data();
+  p.tol_off = s->tol_off.data();
+  p.tol_key = s->tol_key.data();
+  p.tol_op = s->tol_op.data();
+  p.tol_val = s->tol_val.data();
+  p.tol_effect = s->tol_eff.data();
+  p.port_off = s->port_off.data();
+  p.port_proto = s->port_proto.data();
+  p.port_num = s->port_num.data();
+  p.port_ip = s->port_ip.data();
+  c->id_empty = 0;
+  c->id_metadata_name = 1;
+  c->id_unschedulable_key = 2;
+}
+
+void sr_synth_labels(const sr_synth* s, sr_node_label* on_demand, sr_node_label* spot) {
+  if (on_demand) *on_demand = s->od;
+  if (spot) *spot = s->spot;
+}
+
+const char* sr_synth_string(const sr_synth* s, int32_t id) {
+  if (id < 0 || id >= static_cast<int32_t>(s->strings.size())) return "";
+  return s->strings[id].c_str();
+}
+
+int32_t sr_synth_num_strings(const sr_synth* s) { return static_cast<int32_t>(s->strings.size()); }
+
+}  // extern "C"

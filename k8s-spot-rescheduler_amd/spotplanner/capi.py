@@ -1,0 +1,226 @@
+"""ctypes view of include/sr_planner.h (constants, structs) and library loading.
+
+The constants are parsed from the header itself so the Python side cannot drift
+from the C-ABI.  `load_planner()` loads the in-tree libsrplanner.so and fails
+loudly if it is missing: there is no CPU fallback for the planner.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_PKG)                       # k8s-spot-rescheduler_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+HEADER = os.path.join(REPO_ROOT, "include", "sr_planner.h")
+LIB_DIR = os.path.join(PKG_ROOT, "lib")
+PLANNER_LIB = os.path.join(LIB_DIR, "libsrplanner.so")
+SYNTH_LIB = os.path.join(LIB_DIR, "libsrsynth.so")
+
+
+def _parse_defines(path):
+    out = {}
+    with open(path) as f:
+        for line in f:
+            m = re.match(r"#define\s+(SR_\w+)\s+\(?\s*(-?\d+)u?\s*(?:<<\s*(\d+))?\s*\)?", line)
+            if m:
+                v = int(m.group(2))
+                if m.group(3):
+                    v <<= int(m.group(3))
+                out[m.group(1)] = v
+            m = re.match(r"#define\s+(SR_\w+)\s+\((0x[0-9a-fA-F]+)u\)", line)
+            if m:
+                out[m.group(1)] = int(m.group(2), 16)
+    return out
+
+
+_DEF = _parse_defines(HEADER)
+globals().update(_DEF)
+
+P32 = ctypes.POINTER(ctypes.c_int32)
+P64 = ctypes.POINTER(ctypes.c_int64)
+PU8 = ctypes.POINTER(ctypes.c_uint8)
+PU32 = ctypes.POINTER(ctypes.c_uint32)
+
+
+class sr_nodes(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("name", P32), ("alloc_milli_cpu", P64), ("alloc_memory", P64),
+                ("alloc_ephemeral", P64), ("alloc_pods", P64), ("unschedulable", PU8),
+                ("label_off", P32), ("label_key", P32), ("label_val", P32),
+                ("taint_off", P32), ("taint_key", P32), ("taint_val", P32), ("taint_effect", P32)]
+
+
+class sr_pods(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("node", P32), ("cpu_sort_milli", P64), ("req_milli_cpu", P64),
+                ("req_memory", P64), ("req_ephemeral", P64), ("priority", P32), ("has_priority", PU8),
+                ("flags", PU32), ("sel_off", P32), ("sel_key", P32), ("sel_val", P32),
+                ("aff_required", PU8), ("term_off", P32), ("term_expr_off", P32), ("term_field_off", P32),
+                ("expr_key", P32), ("expr_op", P32), ("expr_val_off", P32), ("expr_vals", P32),
+                ("field_key", P32), ("field_op", P32), ("field_val_off", P32), ("field_vals", P32),
+                ("tol_off", P32), ("tol_key", P32), ("tol_op", P32), ("tol_val", P32), ("tol_effect", P32),
+                ("port_off", P32), ("port_proto", P32), ("port_num", P32), ("port_ip", P32)]
+
+
+class sr_cluster(ctypes.Structure):
+    _fields_ = [("nodes", sr_nodes), ("pods", sr_pods), ("id_empty", ctypes.c_int32),
+                ("id_metadata_name", ctypes.c_int32), ("id_unschedulable_key", ctypes.c_int32)]
+
+
+class sr_node_label(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_int32), ("value", ctypes.c_int32), ("has_value", ctypes.c_int32)]
+
+
+class sr_node_map_params(ctypes.Structure):
+    _fields_ = [("on_demand", sr_node_label), ("spot", sr_node_label), ("priority_threshold", ctypes.c_int32)]
+
+
+class sr_node_map(ctypes.Structure):
+    _fields_ = [("spot", P32), ("n_spot", P32), ("on_demand", P32), ("n_on_demand", P32),
+                ("node_pod_off", P32), ("node_pod_idx", P32), ("requested_cpu", P64), ("free_cpu", P64)]
+
+
+class sr_candidates(ctypes.Structure):
+    _fields_ = [("n_cand", ctypes.c_int32), ("cand_pod_off", P32), ("cand_pods", P32), ("cand_global", P32)]
+
+
+class sr_plan_out(ctypes.Structure):
+    _fields_ = [("winner", ctypes.c_int32), ("first_ok", ctypes.c_int32), ("first_fallback", ctypes.c_int32),
+                ("winner_npods", ctypes.c_int32), ("checks", ctypes.c_uint64), ("fallback_pods", ctypes.c_uint64),
+                ("status", P32), ("node_of_pod", P32), ("winner_map", P32)]
+
+
+class sr_timing(ctypes.Structure):
+    _fields_ = [("n_runs", ctypes.c_int32), ("ms_tables", ctypes.c_double), ("ms_feasibility", ctypes.c_double),
+                ("ms_placement", ctypes.c_double), ("ms_winner", ctypes.c_double),
+                ("ms_pack_host", ctypes.c_double), ("ms_upload", ctypes.c_double),
+                ("bytes_feasibility", ctypes.c_uint64), ("bytes_placement", ctypes.c_uint64),
+                ("n_pods", ctypes.c_int32), ("n_spot", ctypes.c_int32), ("n_cand", ctypes.c_int32),
+                ("n_words", ctypes.c_int32), ("n_rows_a", ctypes.c_int32), ("n_rows_b", ctypes.c_int32),
+                ("n_classes", ctypes.c_int32)]
+
+
+def ptr(arr, typ):
+    """Pointer to a contiguous numpy array (None for an empty array is fine)."""
+    if arr is None:
+        return ctypes.cast(None, typ)
+    return arr.ctypes.data_as(typ)
+
+
+def make_cluster_struct(A) -> sr_cluster:
+    c = sr_cluster()
+    n = c.nodes
+    n.n = A["n_nodes"]
+    n.name = ptr(A["node_name"], P32)
+    n.alloc_milli_cpu = ptr(A["alloc_cpu"], P64)
+    n.alloc_memory = ptr(A["alloc_mem"], P64)
+    n.alloc_ephemeral = ptr(A["alloc_eph"], P64)
+    n.alloc_pods = ptr(A["alloc_pods"], P64)
+    n.unschedulable = ptr(A["unsched"], PU8)
+    n.label_off = ptr(A["label_off"], P32)
+    n.label_key = ptr(A["label_key"], P32)
+    n.label_val = ptr(A["label_val"], P32)
+    n.taint_off = ptr(A["taint_off"], P32)
+    n.taint_key = ptr(A["taint_key"], P32)
+    n.taint_val = ptr(A["taint_val"], P32)
+    n.taint_effect = ptr(A["taint_eff"], P32)
+    p = c.pods
+    p.n = A["n_pods"]
+    p.node = ptr(A["pod_node"], P32)
+    p.cpu_sort_milli = ptr(A["cpu_sort"], P64)
+    p.req_milli_cpu = ptr(A["req_cpu"], P64)
+    p.req_memory = ptr(A["req_mem"], P64)
+    p.req_ephemeral = ptr(A["req_eph"], P64)
+    p.priority = ptr(A["priority"], P32)
+    p.has_priority = ptr(A["has_priority"], PU8)
+    p.flags = ptr(A["flags"], PU32)
+    for f in ("sel_off", "sel_key", "sel_val", "term_off", "term_expr_off", "term_field_off", "expr_key",
+              "expr_op", "expr_val_off", "expr_vals", "field_key", "field_op", "field_val_off", "field_vals",
+              "tol_off", "tol_key", "tol_op", "tol_val", "port_off", "port_proto", "port_num", "port_ip"):
+        setattr(p, f, ptr(A[f], P32))
+    p.tol_effect = ptr(A["tol_eff"], P32)
+    p.aff_required = ptr(A["aff_required"], PU8)
+    c.id_empty = A["id_empty"]
+    c.id_metadata_name = A["id_metadata_name"]
+    c.id_unschedulable_key = A["id_unschedulable_key"]
+    return c
+
+
+_planner = None
+
+
+class PlannerLibraryMissing(RuntimeError):
+    pass
+
+
+def load_planner():
+    """Load the in-tree HIP planner library; never substitutes anything for it."""
+    global _planner
+    if _planner is not None:
+        return _planner
+    if not os.path.exists(PLANNER_LIB):
+        raise PlannerLibraryMissing(
+            "%s is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the planner has no CPU fallback)" % PLANNER_LIB)
+    lib = ctypes.CDLL(PLANNER_LIB)
+    _declare_planner(lib)
+    _planner = lib
+    return lib
+
+
+def _declare_planner(lib):
+    S = ctypes.c_int32
+    VP = ctypes.c_void_p
+    PC = ctypes.POINTER(sr_cluster)
+    lib.sr_new_node_map.argtypes = [PC, ctypes.POINTER(sr_node_map_params), ctypes.POINTER(sr_node_map)]
+    lib.sr_new_node_map.restype = S
+    lib.sr_node_has_label.argtypes = [PC, ctypes.c_int32, ctypes.POINTER(sr_node_label)]
+    lib.sr_node_has_label.restype = ctypes.c_int32
+    lib.sr_snapshot_create.argtypes = [PC, P32, ctypes.c_int32, P32, P32, ctypes.POINTER(VP)]
+    lib.sr_snapshot_create.restype = S
+    lib.sr_snapshot_destroy.argtypes = [VP]
+    lib.sr_snapshot_destroy.restype = None
+    lib.sr_snapshot_add_pod.argtypes = [VP, PC, ctypes.c_int32, ctypes.c_int32]
+    lib.sr_snapshot_add_pod.restype = S
+    lib.sr_snapshot_fork.argtypes = [VP]
+    lib.sr_snapshot_fork.restype = S
+    lib.sr_snapshot_revert.argtypes = [VP]
+    lib.sr_snapshot_revert.restype = S
+    lib.sr_snapshot_node_state.argtypes = [VP, ctypes.c_int32, P64, P32]
+    lib.sr_snapshot_node_state.restype = S
+    lib.sr_snapshot_num_nodes.argtypes = [VP]
+    lib.sr_snapshot_num_nodes.restype = ctypes.c_int32
+    lib.sr_create.argtypes = [ctypes.c_int32, ctypes.POINTER(VP)]
+    lib.sr_create.restype = S
+    lib.sr_destroy.argtypes = [VP]
+    lib.sr_destroy.restype = None
+    lib.sr_last_error.argtypes = [VP]
+    lib.sr_last_error.restype = ctypes.c_char_p
+    lib.sr_build_info.argtypes = []
+    lib.sr_build_info.restype = ctypes.c_char_p
+    lib.sr_find_spot_nodes.argtypes = [VP, VP, PC, P32, ctypes.c_int32, P32, PU8]
+    lib.sr_find_spot_nodes.restype = S
+    lib.sr_can_drain_node.argtypes = [VP, VP, PC, P32, ctypes.c_int32, P32, P32, PU8]
+    lib.sr_can_drain_node.restype = S
+    lib.sr_plan.argtypes = [VP, VP, PC, ctypes.POINTER(sr_candidates), ctypes.POINTER(sr_plan_out)]
+    lib.sr_plan.restype = S
+    lib.sr_plan_prepare.argtypes = [VP, VP, PC, ctypes.POINTER(sr_candidates)]
+    lib.sr_plan_prepare.restype = S
+    lib.sr_plan_run.argtypes = [VP, ctypes.POINTER(sr_plan_out)]
+    lib.sr_plan_run.restype = S
+    lib.sr_set_timing.argtypes = [VP, ctypes.c_int32]
+    lib.sr_set_timing.restype = S
+    lib.sr_get_timing.argtypes = [VP, ctypes.POINTER(sr_timing)]
+    lib.sr_get_timing.restype = S
+    lib.sr_comm_unique_id.argtypes = [ctypes.POINTER(ctypes.c_uint8)]
+    lib.sr_comm_unique_id.restype = S
+    lib.sr_comm_init.argtypes = [VP, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32, ctypes.c_int32]
+    lib.sr_comm_init.restype = S
+
+
+# Every symbol include/sr_planner.h declares (checked by tests on CPU).
+EXPORTED = ["sr_new_node_map", "sr_node_has_label", "sr_snapshot_create", "sr_snapshot_destroy",
+            "sr_snapshot_add_pod", "sr_snapshot_fork", "sr_snapshot_revert", "sr_snapshot_node_state",
+            "sr_snapshot_num_nodes", "sr_create", "sr_destroy", "sr_last_error", "sr_build_info",
+            "sr_find_spot_nodes", "sr_can_drain_node", "sr_plan", "sr_plan_prepare", "sr_plan_run",
+            "sr_set_timing", "sr_get_timing", "sr_comm_unique_id", "sr_comm_init"]

@@ -1,0 +1,328 @@
+"""Kubernetes object model + the shim's encoding into the C-ABI cluster arrays.
+
+The dataclasses mirror the fields of k8s.io/api/core/v1 Pod / Node that the
+reference's hot path reads (rescheduler.go:338-370, nodes/nodes.go:63-165 and
+the k8s v1.19.2 scheduler filters behind CheckPredicates).  `encode_cluster`
+is what the Go shim of INTEGRATION.md does before crossing the C-ABI: intern
+strings into ids, convert quantities, compute the scheduler request of each
+pod and set fallback flags for features the encoded predicate set lacks.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import capi
+
+GiB = 1024 * 1024 * 1024
+MiB = 1024 * 1024
+
+EFFECTS = {"": capi.SR_EFFECT_EMPTY, "NoSchedule": capi.SR_EFFECT_NO_SCHEDULE,
+           "PreferNoSchedule": capi.SR_EFFECT_PREFER_NO_SCHEDULE, "NoExecute": capi.SR_EFFECT_NO_EXECUTE}
+TOL_OPS = {"": capi.SR_TOL_EQUAL, "Equal": capi.SR_TOL_EQUAL, "Exists": capi.SR_TOL_EXISTS}
+SEL_OPS = {"In": capi.SR_OP_IN, "NotIn": capi.SR_OP_NOT_IN, "Exists": capi.SR_OP_EXISTS,
+           "DoesNotExist": capi.SR_OP_DOES_NOT_EXIST, "Gt": capi.SR_OP_GT, "Lt": capi.SR_OP_LT}
+PROTOS = {"": capi.SR_PROTO_TCP, "TCP": capi.SR_PROTO_TCP, "UDP": capi.SR_PROTO_UDP,
+          "SCTP": capi.SR_PROTO_SCTP}
+MIRROR_ANNOTATION = "kubernetes.io/config.mirror"
+UNSCHEDULABLE_TAINT_KEY = "node.kubernetes.io/unschedulable"
+
+
+@dataclass
+class ContainerPort:
+    host_port: int
+    container_port: int = 0
+    protocol: str = "TCP"
+    host_ip: str = ""
+
+
+@dataclass
+class Container:
+    cpu_milli: int = 0          # Requests.Cpu().MilliValue()
+    memory: int = 0             # Requests.Memory().Value()
+    ephemeral: int = 0          # Requests.StorageEphemeral().Value()
+    scalar: Dict[str, int] = field(default_factory=dict)   # extended / hugepages requests
+    ports: List[ContainerPort] = field(default_factory=list)
+
+
+@dataclass
+class Toleration:
+    key: str = ""
+    operator: str = ""
+    value: str = ""
+    effect: str = ""
+
+
+@dataclass
+class Taint:
+    key: str
+    value: str = ""
+    effect: str = "NoSchedule"
+
+
+@dataclass
+class NodeSelectorRequirement:
+    key: str
+    operator: str
+    values: List[str] = field(default_factory=list)
+
+
+@dataclass
+class NodeSelectorTerm:
+    match_expressions: List[NodeSelectorRequirement] = field(default_factory=list)
+    match_fields: List[NodeSelectorRequirement] = field(default_factory=list)
+
+
+@dataclass
+class OwnerReference:
+    kind: str
+    name: str = ""
+    controller: Optional[bool] = True
+
+
+@dataclass
+class Pod:
+    name: str
+    namespace: str = "kube-system"
+    node_name: str = ""
+    containers: List[Container] = field(default_factory=list)
+    init_containers: List[Container] = field(default_factory=list)
+    overhead: Optional[Container] = None
+    priority: Optional[int] = 0
+    labels: Dict[str, str] = field(default_factory=dict)
+    annotations: Dict[str, str] = field(default_factory=dict)
+    node_selector: Dict[str, str] = field(default_factory=dict)
+    # Affinity.NodeAffinity.RequiredDuringSchedulingIgnoredDuringExecution.NodeSelectorTerms;
+    # None = the pointer is nil (no requirement).
+    required_node_affinity: Optional[List[NodeSelectorTerm]] = None
+    tolerations: List[Toleration] = field(default_factory=list)
+    owner_references: List[OwnerReference] = field(default_factory=list)
+    # features outside the encoded predicate set
+    has_pvc: bool = False
+    required_pod_affinity: bool = False
+    required_pod_anti_affinity: bool = False
+    hard_topology_spread: bool = False
+
+    def cpu_sort_milli(self) -> int:
+        """getPodCPURequests (nodes/nodes.go:159-165): Σ regular containers' CPU."""
+        return sum(c.cpu_milli for c in self.containers)
+
+    def scheduler_request(self):
+        """computePodResourceRequest (k8s v1.19 noderesources/fit.go):
+        max(Σ containers, each init container) + Overhead, per resource."""
+        cpu = sum(c.cpu_milli for c in self.containers)
+        mem = sum(c.memory for c in self.containers)
+        eph = sum(c.ephemeral for c in self.containers)
+        for ic in self.init_containers:
+            cpu, mem, eph = max(cpu, ic.cpu_milli), max(mem, ic.memory), max(eph, ic.ephemeral)
+        if self.overhead is not None:
+            cpu += self.overhead.cpu_milli
+            mem += self.overhead.memory
+            eph += self.overhead.ephemeral
+        return cpu, mem, eph
+
+    def host_ports(self):
+        return [p for c in self.containers for p in c.ports if p.host_port > 0]
+
+
+@dataclass
+class Node:
+    name: str
+    cpu_milli: int
+    memory: int = 2 * GiB
+    pods: int = 100
+    ephemeral: int = 0
+    labels: Dict[str, str] = field(default_factory=dict)
+    taints: List[Taint] = field(default_factory=list)
+    unschedulable: bool = False
+
+
+def pod_id(pod: Pod) -> str:
+    """podID (rescheduler.go:402-404)."""
+    return "%s/%s" % (pod.namespace, pod.name)
+
+
+class Interner:
+    """String -> int32 id, shared by every encoding that talks to one snapshot."""
+
+    def __init__(self):
+        self.ids: Dict[str, int] = {}
+        self.strings: List[str] = []
+
+    def id(self, s: str) -> int:
+        i = self.ids.get(s)
+        if i is None:
+            i = len(self.strings)
+            self.ids[s] = i
+            self.strings.append(s)
+        return i
+
+    def peek(self, s: str) -> int:
+        return self.ids.get(s, -1)
+
+
+def _i32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int32).reshape(-1))
+
+
+def _i64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int64).reshape(-1))
+
+
+def _u8(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint8).reshape(-1))
+
+
+def _u32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint32).reshape(-1))
+
+
+class NilControllerPanic(RuntimeError):
+    """rescheduler.go:244 dereferences *owner.Controller: the reference panics on nil."""
+
+
+def pod_flags(pod: Pod) -> int:
+    f = 0
+    for o in pod.owner_references:
+        if o.controller is None:
+            raise NilControllerPanic("nil OwnerReference.Controller on %s" % pod_id(pod))
+        if o.controller and o.kind == "DaemonSet":
+            f |= capi.SR_POD_DAEMONSET_CONTROLLER
+    if MIRROR_ANNOTATION in pod.annotations:
+        f |= capi.SR_POD_MIRROR
+    if pod.required_pod_anti_affinity:
+        f |= capi.SR_POD_HAS_REQ_ANTI_AFFINITY
+    conts = list(pod.containers) + list(pod.init_containers) + ([pod.overhead] if pod.overhead else [])
+    if any(c.scalar for c in conts):
+        f |= capi.SR_POD_FB_SCALAR_RESOURCES
+    if pod.has_pvc:
+        f |= capi.SR_POD_FB_VOLUMES
+    if pod.hard_topology_spread:
+        f |= capi.SR_POD_FB_TOPOLOGY_SPREAD
+    if pod.required_pod_affinity or pod.required_pod_anti_affinity:
+        f |= capi.SR_POD_FB_POD_AFFINITY
+    return f
+
+
+class EncodedCluster:
+    """numpy arrays in the sr_cluster layout + the ctypes struct pointing at them."""
+
+    def __init__(self, arrays: dict, interner: Interner):
+        self.a = arrays
+        self.interner = interner
+        self.struct = capi.make_cluster_struct(arrays)
+
+    @property
+    def ptr(self):
+        return ctypes.byref(self.struct)
+
+
+def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Interner] = None,
+                   pod_node: Optional[List[int]] = None) -> EncodedCluster:
+    """Encode nodes and pods.  pod_node[i] is the node index of pods[i] (default:
+    looked up by pod.node_name; -1 when unbound).  Pods of one node keep their
+    relative order (= the per-node LIST order)."""
+    it = interner or Interner()
+    e = it.id("")
+    mn = it.id("metadata.name")
+    uk = it.id(UNSCHEDULABLE_TAINT_KEY)
+    name_idx = {n.name: i for i, n in enumerate(nodes)}
+    A = {}
+    A["node_name"] = _i32([it.id(n.name) for n in nodes])
+    A["alloc_cpu"] = _i64([n.cpu_milli for n in nodes])
+    A["alloc_mem"] = _i64([n.memory for n in nodes])
+    A["alloc_eph"] = _i64([n.ephemeral for n in nodes])
+    A["alloc_pods"] = _i64([n.pods for n in nodes])
+    A["unsched"] = _u8([1 if n.unschedulable else 0 for n in nodes])
+    lo, lk, lv = [0], [], []
+    to, tk, tv, te = [0], [], [], []
+    for n in nodes:
+        for k, v in n.labels.items():
+            lk.append(it.id(k))
+            lv.append(it.id(v))
+        lo.append(len(lk))
+        for t in n.taints:
+            tk.append(it.id(t.key))
+            tv.append(it.id(t.value))
+            te.append(EFFECTS.get(t.effect, capi.SR_EFFECT_OTHER))
+        to.append(len(tk))
+    A.update(label_off=_i32(lo), label_key=_i32(lk), label_val=_i32(lv),
+             taint_off=_i32(to), taint_key=_i32(tk), taint_val=_i32(tv), taint_eff=_i32(te))
+
+    pn, sortc, rc, rm, re, pr, hp, fl = [], [], [], [], [], [], [], []
+    so, sk, sv = [0], [], []
+    aff, term_off = [], [0]
+    texpr, tfield = [0], [0]
+    ek, eo, evo, ev = [], [], [0], []
+    fk, fo, fvo, fv = [], [], [0], []
+    tolo, tolk, tolop, tolv, tole = [0], [], [], [], []
+    po, pp, pnum, pip = [0], [], [], []
+    for i, p in enumerate(pods):
+        if pod_node is not None:
+            pn.append(pod_node[i])
+        else:
+            pn.append(name_idx.get(p.node_name, -1))
+        sortc.append(p.cpu_sort_milli())
+        c, m, eph = p.scheduler_request()
+        rc.append(c)
+        rm.append(m)
+        re.append(eph)
+        hp.append(0 if p.priority is None else 1)
+        pr.append(0 if p.priority is None else p.priority)
+        fl.append(pod_flags(p))
+        for k, v in p.node_selector.items():
+            sk.append(it.id(k))
+            sv.append(it.id(v))
+        so.append(len(sk))
+        aff.append(0 if p.required_node_affinity is None else 1)
+        for term in (p.required_node_affinity or []):
+            for r in term.match_expressions:
+                ek.append(it.id(r.key))
+                eo.append(SEL_OPS.get(r.operator, capi.SR_OP_OTHER))
+                ev.extend(it.id(v) for v in r.values)
+                evo.append(len(ev))
+            texpr.append(len(ek))
+            for r in term.match_fields:
+                fk.append(it.id(r.key))
+                fo.append(SEL_OPS.get(r.operator, capi.SR_OP_OTHER))
+                fv.extend(it.id(v) for v in r.values)
+                fvo.append(len(fv))
+            tfield.append(len(fk))
+        term_off.append(len(texpr) - 1)
+        for t in p.tolerations:
+            tolk.append(it.id(t.key))
+            tolop.append(TOL_OPS.get(t.operator, capi.SR_TOL_OTHER))
+            tolv.append(it.id(t.value))
+            tole.append(EFFECTS.get(t.effect, capi.SR_EFFECT_OTHER))
+        tolo.append(len(tolk))
+        for hpz in p.host_ports():
+            pp.append(PROTOS.get(hpz.protocol, capi.SR_PROTO_TCP))
+            pnum.append(hpz.host_port)
+            pip.append(-1 if hpz.host_ip in ("", "0.0.0.0") else it.id(hpz.host_ip))
+        po.append(len(pp))
+    A.update(pod_node=_i32(pn), cpu_sort=_i64(sortc), req_cpu=_i64(rc), req_mem=_i64(rm),
+             req_eph=_i64(re), priority=_i32(pr), has_priority=_u8(hp), flags=_u32(fl),
+             sel_off=_i32(so), sel_key=_i32(sk), sel_val=_i32(sv), aff_required=_u8(aff),
+             term_off=_i32(term_off), term_expr_off=_i32(texpr), term_field_off=_i32(tfield),
+             expr_key=_i32(ek), expr_op=_i32(eo), expr_val_off=_i32(evo), expr_vals=_i32(ev),
+             field_key=_i32(fk), field_op=_i32(fo), field_val_off=_i32(fvo), field_vals=_i32(fv),
+             tol_off=_i32(tolo), tol_key=_i32(tolk), tol_op=_i32(tolop), tol_val=_i32(tolv),
+             tol_eff=_i32(tole), port_off=_i32(po), port_proto=_i32(pp), port_num=_i32(pnum),
+             port_ip=_i32(pip))
+    A["n_nodes"] = len(nodes)
+    A["n_pods"] = len(pods)
+    A["id_empty"] = e
+    A["id_metadata_name"] = mn
+    A["id_unschedulable_key"] = uk
+    return EncodedCluster(A, it)
+
+
+def label_flag(flag: str, interner: Interner) -> capi.sr_node_label:
+    """Parse a node-label flag the way isSpotNode does (strings.SplitN(label, "=", 2))."""
+    parts = flag.split("=", 1)
+    if len(parts) == 1:
+        return capi.sr_node_label(interner.id(parts[0]), -1, 0)
+    return capi.sr_node_label(interner.id(parts[0]), interner.id(parts[1]), 1)

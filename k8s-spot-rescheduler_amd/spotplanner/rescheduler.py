@@ -1,0 +1,130 @@
+"""Mirror of the reference's planning functions (rescheduler.go, package main).
+
+findSpotNodeForPod (rescheduler.go:338-353), canDrainNode (:357-370),
+validateArgs (:407-417), podID (:402-404), and plan_tick: the planning segment
+of run() (:228-287) evaluated for every candidate at once on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import capi
+from .model import Pod, pod_id
+from .planner import ClusterSnapshot, FallbackRequired, PlannerError, PredicateChecker
+
+podID = pod_id
+
+
+class GoError(Exception):
+    """A Go `error` value: str(err) is its Error() text."""
+
+
+def validateArgs(OnDemandNodeLabel: str, SpotNodeLabel: str) -> Optional[GoError]:
+    """rescheduler.go:407-417."""
+    if len(OnDemandNodeLabel.split("=")) > 2:
+        return GoError("the on demand node label is not correctly formatted: expected '<label_name>' or "
+                       "'<label_name>=<label_value>', but got %s" % OnDemandNodeLabel)
+    if len(SpotNodeLabel.split("=")) > 2:
+        return GoError("the spot node label is not correctly formatted: expected '<label_name>' or "
+                       "'<label_name>=<label_value>', but got %s" % SpotNodeLabel)
+    return None
+
+
+def _node_names(nodes) -> List[str]:
+    return [ni.Node.name for ni in nodes]
+
+
+def _check_order(snapshot: ClusterSnapshot, nodes):
+    snapshot.materialize()
+    if _node_names(nodes) != snapshot.node_names():
+        raise PlannerError("NodeInfoArray order must be the snapshot's node order")
+
+
+def findSpotNodeForPod(predicateChecker: PredicateChecker, spotSnapshot: ClusterSnapshot, nodes,
+                       pod: Pod) -> str:
+    """First spot node in NodeInfoArray order whose predicates pass, else ""."""
+    if len(nodes) == 0:
+        return ""
+    pod.node_name = ""  # :341 — pretend the pod is not scheduled
+    _check_order(spotSnapshot, nodes)
+    enc = spotSnapshot.encode_pods([pod])
+    idx = np.zeros(1, np.int32)
+    out = np.full(1, -1, np.int32)
+    fb = np.zeros(1, np.uint8)
+    lib = predicateChecker.lib
+    st = lib.sr_find_spot_nodes(predicateChecker.handle, spotSnapshot.handle, enc.ptr, capi.ptr(idx, capi.P32), 1,
+                                capi.ptr(out, capi.P32), capi.ptr(fb, capi.PU8))
+    if st != capi.SR_OK:
+        raise PlannerError("sr_find_spot_nodes: %d %s" % (st, predicateChecker.last_error()))
+    if fb[0]:
+        raise FallbackRequired(pod_id(pod))
+    return nodes[int(out[0])].Node.name if out[0] >= 0 else ""
+
+
+def canDrainNode(predicateChecker: PredicateChecker, spotSnapshot: ClusterSnapshot, nodes,
+                 pods: Sequence[Pod]) -> Optional[GoError]:
+    """Places pods one by one (first fit) and adds each to the snapshot; returns
+    the reference's error for the first pod that fits nowhere, else None."""
+    if len(pods) == 0:
+        return None
+    _check_order(spotSnapshot, nodes)
+    enc = spotSnapshot.encode_pods(list(pods))
+    idx = np.arange(len(pods), dtype=np.int32)
+    mapping = np.full(len(pods), -1, np.int32)
+    fail = ctypes.c_int32(-1)
+    fb = ctypes.c_uint8(0)
+    lib = predicateChecker.lib
+    st = lib.sr_can_drain_node(predicateChecker.handle, spotSnapshot.handle, enc.ptr, capi.ptr(idx, capi.P32),
+                               len(pods), capi.ptr(mapping, capi.P32), ctypes.byref(fail), ctypes.byref(fb))
+    if st != capi.SR_OK:
+        raise PlannerError("sr_can_drain_node: %d %s" % (st, predicateChecker.last_error()))
+    if fb.value:
+        raise FallbackRequired(", ".join(pod_id(p) for p in pods))
+    if len(nodes) > 0:
+        for p in pods:
+            p.node_name = ""  # :341 side effect on every evaluated pod
+    canDrainNode.last_mapping = [nodes[int(k)].Node.name if k >= 0 else "" for k in mapping]
+    if fail.value >= 0:
+        return GoError("pod %s can't be rescheduled on any existing spot node" % pod_id(pods[fail.value]))
+    return None
+
+
+canDrainNode.last_mapping = []
+
+
+@dataclass
+class PlanResult:
+    winner: int            # index of the candidate run() drains, -1 none / unresolved
+    first_ok: int
+    first_fallback: int
+    status: np.ndarray     # per candidate: SR_CAND_* or failing pod index
+    node_of_pod: np.ndarray  # flat, spot position per candidate pod (-1 not placed)
+    winner_map: np.ndarray
+    checks: int
+    fallback_pods: int
+
+
+def plan_arrays(predicateChecker: PredicateChecker, snapshot_handle, cluster_ptr, cand_off: np.ndarray,
+                cand_pods: np.ndarray, cand_global: Optional[np.ndarray] = None, full: bool = True) -> PlanResult:
+    """sr_plan over caller-built arrays (the batched drop-in of rescheduler.go:228-287)."""
+    lib = predicateChecker.lib
+    n = len(cand_off) - 1
+    c = capi.sr_candidates(n, capi.ptr(cand_off, capi.P32), capi.ptr(cand_pods, capi.P32),
+                           capi.ptr(cand_global, capi.P32) if cand_global is not None else None)
+    maxp = int(np.max(np.diff(cand_off))) if n > 0 else 0
+    status = np.zeros(max(n, 1), np.int32)
+    nodes = np.zeros(max(int(cand_off[-1]) if n > 0 else 0, 1), np.int32)
+    wmap = np.full(max(maxp, 1), -1, np.int32)
+    o = capi.sr_plan_out()
+    o.status = capi.ptr(status, capi.P32) if full else None
+    o.node_of_pod = capi.ptr(nodes, capi.P32) if full else None
+    o.winner_map = capi.ptr(wmap, capi.P32)
+    st = lib.sr_plan(predicateChecker.handle, snapshot_handle, cluster_ptr, ctypes.byref(c), ctypes.byref(o))
+    if st != capi.SR_OK:
+        raise PlannerError("sr_plan: %d %s" % (st, predicateChecker.last_error()))
+    return PlanResult(o.winner, o.first_ok, o.first_fallback, status[:n], nodes[: int(cand_off[-1]) if n else 0],
+                      wmap[: o.winner_npods], int(o.checks), int(o.fallback_pods))

@@ -1,0 +1,156 @@
+"""Binding of libsrsynth.so (synthetic clusters for bench and tests) and the
+tick builder used by bench.py and the parity tests: NewNodeMap ->
+GetClusterSnapshot -> podsForDeletion per on-demand node."""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import capi
+
+
+class sr_synth_params(ctypes.Structure):
+    _fields_ = [("config", ctypes.c_int32), ("seed", ctypes.c_uint64), ("n_on_demand", ctypes.c_int32),
+                ("n_spot", ctypes.c_int32), ("pinned_fraction", ctypes.c_double)]
+
+
+_synth = None
+
+
+def load_synth():
+    global _synth
+    if _synth is None:
+        if not os.path.exists(capi.SYNTH_LIB):
+            raise FileNotFoundError(capi.SYNTH_LIB + " missing: run __graft_entry__.build()")
+        lib = ctypes.CDLL(capi.SYNTH_LIB)
+        lib.sr_synth_generate.argtypes = [ctypes.POINTER(sr_synth_params)]
+        lib.sr_synth_generate.restype = ctypes.c_void_p
+        lib.sr_synth_destroy.argtypes = [ctypes.c_void_p]
+        lib.sr_synth_view.argtypes = [ctypes.c_void_p, ctypes.POINTER(capi.sr_cluster)]
+        lib.sr_synth_labels.argtypes = [ctypes.c_void_p, ctypes.POINTER(capi.sr_node_label),
+                                        ctypes.POINTER(capi.sr_node_label)]
+        lib.sr_synth_string.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        lib.sr_synth_string.restype = ctypes.c_char_p
+        lib.sr_synth_num_strings.argtypes = [ctypes.c_void_p]
+        lib.sr_synth_num_strings.restype = ctypes.c_int32
+        _synth = lib
+    return _synth
+
+
+class SynthCluster:
+    def __init__(self, config: int, seed: int = 0, n_on_demand: int = 0, n_spot: int = 0,
+                 pinned_fraction: float = -1.0):
+        self.lib = load_synth()
+        p = sr_synth_params(config, seed, n_on_demand, n_spot, pinned_fraction)
+        self.handle = self.lib.sr_synth_generate(ctypes.byref(p))
+        self.cluster = capi.sr_cluster()
+        self.lib.sr_synth_view(self.handle, ctypes.byref(self.cluster))
+        self.od_label = capi.sr_node_label()
+        self.spot_label = capi.sr_node_label()
+        self.lib.sr_synth_labels(self.handle, ctypes.byref(self.od_label), ctypes.byref(self.spot_label))
+        self.config = config
+
+    @property
+    def ptr(self):
+        return ctypes.byref(self.cluster)
+
+    @property
+    def n_nodes(self):
+        return self.cluster.nodes.n
+
+    @property
+    def n_pods(self):
+        return self.cluster.pods.n
+
+    def pod_flags(self) -> np.ndarray:
+        return np.ctypeslib.as_array(self.cluster.pods.flags, shape=(self.n_pods,))
+
+    def close(self):
+        if self.handle:
+            self.lib.sr_synth_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class NodeMapArrays:
+    spot: np.ndarray
+    on_demand: np.ndarray
+    node_pod_off: np.ndarray
+    node_pod_idx: np.ndarray
+    requested_cpu: np.ndarray
+    free_cpu: np.ndarray
+
+    def struct(self):
+        ns = np.array([len(self.spot)], np.int32)
+        nod = np.array([len(self.on_demand)], np.int32)
+        self._keep = (ns, nod)
+        return capi.sr_node_map(capi.ptr(self.spot, capi.P32), capi.ptr(ns, capi.P32),
+                                capi.ptr(self.on_demand, capi.P32), capi.ptr(nod, capi.P32),
+                                capi.ptr(self.node_pod_off, capi.P32), capi.ptr(self.node_pod_idx, capi.P32),
+                                capi.ptr(self.requested_cpu, capi.P64), capi.ptr(self.free_cpu, capi.P64))
+
+
+def new_node_map(fn, cluster_ptr, n_nodes: int, n_pods: int, od_label, spot_label, priority_threshold=0):
+    """Calls sr_new_node_map-shaped `fn` (the product's, or the oracle's in tests)."""
+    spot = np.zeros(max(n_nodes, 1), np.int32)
+    od = np.zeros(max(n_nodes, 1), np.int32)
+    ns, nod = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    off = np.zeros(n_nodes + 1, np.int32)
+    idx = np.zeros(max(n_pods, 1), np.int32)
+    req = np.zeros(max(n_nodes, 1), np.int64)
+    free = np.zeros(max(n_nodes, 1), np.int64)
+    m = capi.sr_node_map(capi.ptr(spot, capi.P32), capi.ptr(ns, capi.P32), capi.ptr(od, capi.P32),
+                         capi.ptr(nod, capi.P32), capi.ptr(off, capi.P32), capi.ptr(idx, capi.P32),
+                         capi.ptr(req, capi.P64), capi.ptr(free, capi.P64))
+    params = capi.sr_node_map_params(od_label, spot_label, priority_threshold)
+    st = fn(cluster_ptr, ctypes.byref(params), ctypes.byref(m))
+    if st != capi.SR_OK:
+        raise RuntimeError("new_node_map status %d" % st)
+    return NodeMapArrays(spot[: ns[0]].copy(), od[: nod[0]].copy(), off, idx[: int(off[-1])].copy(), req, free)
+
+
+def build_candidates(nm: NodeMapArrays, flags: np.ndarray):
+    """podsForDeletion per on-demand node in NodeInfoArray order: NodeInfo.Pods
+    minus mirror and DaemonSet-controlled pods (rescheduler.go:231-256)."""
+    off = [0]
+    pods = []
+    drop = capi.SR_POD_MIRROR | capi.SR_POD_DAEMONSET_CONTROLLER
+    for node in nm.on_demand:
+        ps = nm.node_pod_idx[nm.node_pod_off[node]:nm.node_pod_off[node + 1]]
+        keep = ps[(flags[ps] & drop) == 0]
+        pods.append(keep)
+        off.append(off[-1] + len(keep))
+    cand_pods = np.concatenate(pods).astype(np.int32) if pods else np.zeros(0, np.int32)
+    return np.asarray(off, np.int32), np.ascontiguousarray(cand_pods)
+
+
+@dataclass
+class Tick:
+    synth: SynthCluster
+    node_map: NodeMapArrays
+    snapshot: object           # sr_snapshot* handle (product)
+    cand_off: np.ndarray
+    cand_pods: np.ndarray
+
+
+def shard(cand_off: np.ndarray, cand_pods: np.ndarray, rank: int, world: int):
+    """Candidates c with c % world == rank (interleaved, so every rank holds early candidates)."""
+    idx = np.arange(rank, len(cand_off) - 1, world, dtype=np.int32)
+    off = [0]
+    pods = []
+    for c in idx:
+        seg = cand_pods[cand_off[c]:cand_off[c + 1]]
+        pods.append(seg)
+        off.append(off[-1] + len(seg))
+    return (np.asarray(off, np.int32), np.ascontiguousarray(np.concatenate(pods).astype(np.int32))
+            if pods else np.zeros(0, np.int32), idx)

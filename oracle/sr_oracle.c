@@ -1,0 +1,755 @@
+/*
+ * sr_oracle.c — CPU ORACLE (test infrastructure only; see sr_oracle.h).
+ *
+ * Deliberately written as a direct, unoptimised restatement: objects are
+ * walked one (pod, node) pair at a time exactly as the reference's predicate
+ * loop does, with no bitmask encoding, no interning tables and no code shared
+ * with the product.
+ */
+#include "sr_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ===================================================================== */
+/* Go 1.16 sort.Slice -> quickSort_func  [upstream: go/src/sort/zfuncversion.go,
+ * sort/sort.go]; Go 1.15/1.16 per go.mod:3 and Dockerfile:3. */
+typedef struct {
+  int32_t *a;
+  oracle_less_fn less;
+  const void *ctx;
+} o_ls;
+
+static int o_less(const o_ls *d, int i, int j) { return d->less(d->ctx, d->a[i], d->a[j]); }
+static void o_swap(o_ls *d, int i, int j) {
+  int32_t t = d->a[i];
+  d->a[i] = d->a[j];
+  d->a[j] = t;
+}
+
+static void o_insertion_sort(o_ls *d, int a, int b) {
+  for (int i = a + 1; i < b; i++)
+    for (int j = i; j > a && o_less(d, j, j - 1); j--) o_swap(d, j, j - 1);
+}
+
+static void o_sift_down(o_ls *d, int lo, int hi, int first) {
+  int root = lo;
+  for (;;) {
+    int child = 2 * root + 1;
+    if (child >= hi) break;
+    if (child + 1 < hi && o_less(d, first + child, first + child + 1)) child++;
+    if (!o_less(d, first + root, first + child)) return;
+    o_swap(d, first + root, first + child);
+    root = child;
+  }
+}
+
+static void o_heap_sort(o_ls *d, int a, int b) {
+  int first = a, lo = 0, hi = b - a;
+  for (int i = (hi - 1) / 2; i >= 0; i--) o_sift_down(d, i, hi, first);
+  for (int i = hi - 1; i >= 0; i--) {
+    o_swap(d, first, first + i);
+    o_sift_down(d, lo, i, first);
+  }
+}
+
+/* medianOfThree moves the median of data[m0], data[m1], data[m2] into data[m1]. */
+static void o_median_of_three(o_ls *d, int m1, int m0, int m2) {
+  if (o_less(d, m1, m0)) o_swap(d, m1, m0);
+  if (o_less(d, m2, m1)) {
+    o_swap(d, m2, m1);
+    if (o_less(d, m1, m0)) o_swap(d, m1, m0);
+  }
+}
+
+static void o_do_pivot(o_ls *d, int lo, int hi, int *midlo, int *midhi) {
+  int m = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+  if (hi - lo > 40) {
+    int s = (hi - lo) / 8;
+    o_median_of_three(d, lo, lo + s, lo + 2 * s);
+    o_median_of_three(d, m, m - s, m + s);
+    o_median_of_three(d, hi - 1, hi - 1 - s, hi - 1 - 2 * s);
+  }
+  o_median_of_three(d, lo, m, hi - 1);
+
+  int pivot = lo;
+  int a = lo + 1, c = hi - 1;
+  for (; a < c && o_less(d, a, pivot); a++) {
+  }
+  int b = a;
+  for (;;) {
+    for (; b < c && !o_less(d, pivot, b); b++) {
+    }
+    for (; b < c && o_less(d, pivot, c - 1); c--) {
+    }
+    if (b >= c) break;
+    o_swap(d, b, c - 1);
+    b++;
+    c--;
+  }
+  int protect = hi - c < 5;
+  if (!protect && hi - c < (hi - lo) / 4) {
+    int dups = 0;
+    if (!o_less(d, pivot, hi - 1)) {
+      o_swap(d, c, hi - 1);
+      c++;
+      dups++;
+    }
+    if (!o_less(d, b - 1, pivot)) {
+      b--;
+      dups++;
+    }
+    if (!o_less(d, m, pivot)) {
+      o_swap(d, m, b - 1);
+      b--;
+      dups++;
+    }
+    protect = dups > 1;
+  }
+  if (protect) {
+    for (;;) {
+      for (; a < b && !o_less(d, b - 1, pivot); b--) {
+      }
+      for (; a < b && o_less(d, a, pivot); a++) {
+      }
+      if (a >= b) break;
+      o_swap(d, a, b - 1);
+      a++;
+      b--;
+    }
+  }
+  o_swap(d, pivot, b - 1);
+  *midlo = b - 1;
+  *midhi = c;
+}
+
+static void o_quick_sort(o_ls *d, int a, int b, int max_depth) {
+  while (b - a > 12) {
+    if (max_depth == 0) {
+      o_heap_sort(d, a, b);
+      return;
+    }
+    max_depth--;
+    int mlo, mhi;
+    o_do_pivot(d, a, b, &mlo, &mhi);
+    if (mlo - a < b - mhi) {
+      o_quick_sort(d, a, mlo, max_depth);
+      a = mhi;
+    } else {
+      o_quick_sort(d, mhi, b, max_depth);
+      b = mlo;
+    }
+  }
+  if (b - a > 1) {
+    for (int i = a + 6; i < b; i++)
+      if (o_less(d, i, i - 6)) o_swap(d, i, i - 6);
+    o_insertion_sort(d, a, b);
+  }
+}
+
+static int o_max_depth(int n) {
+  int depth = 0;
+  for (int i = n; i > 0; i >>= 1) depth++;
+  return depth * 2;
+}
+
+void oracle_go_sort_slice(int32_t *a, int32_t n, oracle_less_fn less, const void *ctx) {
+  o_ls d = {a, less, ctx};
+  o_quick_sort(&d, 0, n, o_max_depth(n));
+}
+
+typedef struct {
+  const int64_t *key;
+} o_keyctx;
+static int o_less_desc(const void *ctx, int32_t x, int32_t y) {
+  const int64_t *k = ((const o_keyctx *)ctx)->key;
+  return k[x] > k[y];
+}
+static int o_less_asc(const void *ctx, int32_t x, int32_t y) {
+  const int64_t *k = ((const o_keyctx *)ctx)->key;
+  return k[x] < k[y];
+}
+void oracle_go_sort_by_key(int32_t *a, int32_t n, const int64_t *key, int32_t desc) {
+  o_keyctx k = {key};
+  oracle_go_sort_slice(a, n, desc ? o_less_desc : o_less_asc, &k);
+}
+
+/* ===================================================================== */
+/* Labels */
+
+/* labels[key] lookup; returns 1 and *val when present. */
+static int o_node_label(const sr_cluster *c, int32_t node, int32_t key, int32_t *val) {
+  const sr_nodes *N = &c->nodes;
+  for (int32_t i = N->label_off[node]; i < N->label_off[node + 1]; i++)
+    if (N->label_key[i] == key) {
+      *val = N->label_val[i];
+      return 1;
+    }
+  return 0;
+}
+
+/* isSpotNode / isOnDemandNode (nodes/nodes.go:168-209): "k" tests presence;
+ * "k=v" tests labels[k] == v where a missing key reads as "". */
+int32_t oracle_node_has_label(const sr_cluster *c, int32_t node, const sr_node_label *l) {
+  int32_t v;
+  int found = o_node_label(c, node, l->key, &v);
+  if (!l->has_value) return found;
+  if (!found) v = c->id_empty;
+  return v == l->value;
+}
+
+/* validateArgs (rescheduler.go:407-417): more than one '=' is an error. */
+int32_t oracle_validate_label_flag(int32_t n_equals_parts) { return n_equals_parts > 2 ? 0 : 1; }
+
+/* ===================================================================== */
+/* NewNodeMap (nodes/nodes.go:63-104) */
+
+int32_t oracle_new_node_map(const sr_cluster *c, const sr_node_map_params *p, sr_node_map *out) {
+  const sr_nodes *N = &c->nodes;
+  const sr_pods *P = &c->pods;
+  int32_t nn = N->n, np = P->n;
+  /* group pods per node in LIST order */
+  int32_t *cnt = (int32_t *)calloc((size_t)nn + 1, sizeof(int32_t));
+  for (int32_t i = 0; i < np; i++)
+    if (P->node[i] >= 0) cnt[P->node[i] + 1]++;
+  for (int32_t i = 0; i < nn; i++) cnt[i + 1] += cnt[i];
+  int32_t *listed = (int32_t *)malloc(sizeof(int32_t) * (size_t)(np ? np : 1));
+  int32_t *fill = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nn ? nn : 1));
+  for (int32_t i = 0; i < nn; i++) fill[i] = cnt[i];
+  for (int32_t i = 0; i < np; i++)
+    if (P->node[i] >= 0) listed[fill[P->node[i]]++] = i;
+
+  int32_t kept = 0, ns = 0, nod = 0;
+  int32_t rc = SR_OK;
+  for (int32_t node = 0; node < nn; node++) {
+    int spot = oracle_node_has_label(c, node, &p->spot);
+    out->node_pod_off[node] = kept;
+    int64_t requested = 0;
+    int32_t start = kept;
+    /* getPodsOnNode (nodes/nodes.go:129-145) */
+    for (int32_t j = cnt[node]; j < cnt[node + 1]; j++) {
+      int32_t pod = listed[j];
+      if (!P->has_priority[pod]) { /* int(*Spec.Priority) panics on nil */
+        rc = SR_ERR_NIL_PRIORITY;
+        goto done;
+      }
+      if (P->priority[pod] < p->priority_threshold && spot) continue;
+      out->node_pod_idx[kept++] = pod;
+      requested += P->cpu_sort_milli[pod]; /* calculateRequestedCPU (:149-156) */
+    }
+    out->requested_cpu[node] = requested;
+    out->free_cpu[node] = N->alloc_milli_cpu[node] - requested; /* newNodeInfo (:117) */
+    /* sort.Slice(pods, cpu(i) > cpu(j)) (:76-80) */
+    oracle_go_sort_by_key(out->node_pod_idx + start, kept - start, P->cpu_sort_milli, 1);
+    /* switch: spot first, then on-demand, else dropped (:82-91) */
+    if (spot)
+      out->spot[ns++] = node;
+    else if (oracle_node_has_label(c, node, &p->on_demand))
+      out->on_demand[nod++] = node;
+  }
+  out->node_pod_off[nn] = kept;
+  oracle_go_sort_by_key(out->spot, ns, out->requested_cpu, 1);      /* :95-97 */
+  oracle_go_sort_by_key(out->on_demand, nod, out->requested_cpu, 0); /* :99-101 */
+  *out->n_spot = ns;
+  *out->n_on_demand = nod;
+done:
+  free(cnt);
+  free(listed);
+  free(fill);
+  return rc;
+}
+
+void oracle_build_candidates(const sr_cluster *c, const sr_node_map *m, int32_t *cand_off,
+                             int32_t *cand_pods) {
+  int32_t k = 0;
+  for (int32_t i = 0; i < *m->n_on_demand; i++) {
+    int32_t node = m->on_demand[i];
+    cand_off[i] = k;
+    for (int32_t j = m->node_pod_off[node]; j < m->node_pod_off[node + 1]; j++) {
+      int32_t pod = m->node_pod_idx[j];
+      uint32_t f = c->pods.flags[pod];
+      if (f & (SR_POD_MIRROR | SR_POD_DAEMONSET_CONTROLLER)) continue;
+      cand_pods[k++] = pod;
+    }
+  }
+  cand_off[*m->n_on_demand] = k;
+}
+
+/* ===================================================================== */
+/* Cluster snapshot [upstream CA simulator BasicClusterSnapshot/DeltaClusterSnapshot
+ * over scheduler NodeInfo]: per node Requested (cpu, mem, eph), len(Pods),
+ * UsedPorts, and whether any pod carries required anti-affinity. */
+typedef struct {
+  int32_t ip, proto, port;
+} o_port;
+
+typedef struct {
+  int64_t req[3];
+  int32_t npods;
+  int32_t anti;
+  int32_t nports, cap;
+  o_port *ports;
+} o_state;
+
+struct oracle_snapshot {
+  int32_t n;
+  int32_t *node; /* cluster node index per position */
+  o_state *st;
+  o_state *saved;
+  int32_t forked;
+  int32_t anti_total;
+};
+
+static int64_t o_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+
+static void o_state_add_pod(o_state *st, const sr_cluster *c, int32_t pod) {
+  const sr_pods *P = &c->pods;
+  st->req[0] = o_add(st->req[0], P->req_milli_cpu[pod]);
+  st->req[1] = o_add(st->req[1], P->req_memory[pod]);
+  st->req[2] = o_add(st->req[2], P->req_ephemeral[pod]);
+  st->npods++;
+  if (P->flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) st->anti++;
+  for (int32_t i = P->port_off[pod]; i < P->port_off[pod + 1]; i++) {
+    if (P->port_num[i] <= 0) continue; /* HostPortInfo.Add ignores port <= 0 */
+    if (st->nports == st->cap) {
+      st->cap = st->cap ? st->cap * 2 : 4;
+      st->ports = (o_port *)realloc(st->ports, sizeof(o_port) * (size_t)st->cap);
+    }
+    st->ports[st->nports].ip = P->port_ip[i];
+    st->ports[st->nports].proto = P->port_proto[i];
+    st->ports[st->nports].port = P->port_num[i];
+    st->nports++;
+  }
+}
+
+oracle_snapshot *oracle_snapshot_create(const sr_cluster *c, const int32_t *spot, int32_t n_spot,
+                                        const int32_t *node_pod_off, const int32_t *node_pod_idx) {
+  oracle_snapshot *s = (oracle_snapshot *)calloc(1, sizeof(*s));
+  s->n = n_spot;
+  s->node = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n_spot ? n_spot : 1));
+  s->st = (o_state *)calloc((size_t)(n_spot ? n_spot : 1), sizeof(o_state));
+  for (int32_t i = 0; i < n_spot; i++) {
+    int32_t node = spot[i];
+    s->node[i] = node;
+    /* AddNodeWithPods(node.Node, node.Pods) (nodes/nodes.go:229) */
+    for (int32_t j = node_pod_off[node]; j < node_pod_off[node + 1]; j++)
+      o_state_add_pod(&s->st[i], c, node_pod_idx[j]);
+    s->anti_total += s->st[i].anti;
+  }
+  return s;
+}
+
+static void o_free_states(o_state *st, int32_t n) {
+  if (!st) return;
+  for (int32_t i = 0; i < n; i++) free(st[i].ports);
+  free(st);
+}
+
+static o_state *o_copy_states(const o_state *src, int32_t n) {
+  o_state *dst = (o_state *)calloc((size_t)(n ? n : 1), sizeof(o_state));
+  for (int32_t i = 0; i < n; i++) {
+    dst[i] = src[i];
+    dst[i].ports = NULL;
+    if (src[i].nports) {
+      dst[i].ports = (o_port *)malloc(sizeof(o_port) * (size_t)src[i].cap);
+      memcpy(dst[i].ports, src[i].ports, sizeof(o_port) * (size_t)src[i].nports);
+    }
+  }
+  return dst;
+}
+
+void oracle_snapshot_destroy(oracle_snapshot *s) {
+  if (!s) return;
+  o_free_states(s->st, s->n);
+  o_free_states(s->saved, s->n);
+  free(s->node);
+  free(s);
+}
+
+void oracle_snapshot_add_pod(oracle_snapshot *s, const sr_cluster *c, int32_t pod, int32_t pos) {
+  int32_t before = s->st[pos].anti;
+  o_state_add_pod(&s->st[pos], c, pod);
+  s->anti_total += s->st[pos].anti - before;
+}
+
+int32_t oracle_snapshot_fork(oracle_snapshot *s) {
+  if (s->forked) return SR_ERR_STATE; /* DeltaClusterSnapshot: one level */
+  s->saved = o_copy_states(s->st, s->n);
+  s->forked = 1;
+  return SR_OK;
+}
+
+int32_t oracle_snapshot_revert(oracle_snapshot *s) {
+  if (!s->forked) return SR_OK; /* Revert without Fork is a no-op in the CA snapshot */
+  o_free_states(s->st, s->n);
+  s->st = s->saved;
+  s->saved = NULL;
+  s->forked = 0;
+  s->anti_total = 0;
+  for (int32_t i = 0; i < s->n; i++) s->anti_total += s->st[i].anti;
+  return SR_OK;
+}
+
+void oracle_snapshot_node_state(const oracle_snapshot *s, int32_t pos, int64_t req[3], int32_t *npods) {
+  req[0] = s->st[pos].req[0];
+  req[1] = s->st[pos].req[1];
+  req[2] = s->st[pos].req[2];
+  *npods = s->st[pos].npods;
+}
+
+/* ===================================================================== */
+/* Predicates: k8s v1.19.2 filter plugins [upstream], one (pod, node) pair. */
+
+/* v1.Toleration.ToleratesTaint [upstream k8s.io/api/core/v1/toleration.go] */
+static int o_tolerates(const sr_cluster *c, int32_t pod, int32_t key, int32_t val, int32_t effect) {
+  const sr_pods *P = &c->pods;
+  for (int32_t t = P->tol_off[pod]; t < P->tol_off[pod + 1]; t++) {
+    int32_t te = P->tol_effect[t];
+    if (te != SR_EFFECT_EMPTY && (te != effect || te == SR_EFFECT_OTHER)) continue;
+    int32_t tk = P->tol_key[t];
+    if (tk != c->id_empty && tk != key) continue; /* len(t.Key) > 0 && t.Key != taint.Key */
+    switch (P->tol_op[t]) {
+      case SR_TOL_EQUAL:
+        if (P->tol_val[t] == val) return 1;
+        break;
+      case SR_TOL_EXISTS:
+        return 1;
+      default:
+        break;
+    }
+  }
+  return 0;
+}
+
+/* NodeUnschedulable.Filter [upstream plugins/nodeunschedulable] */
+static int o_unschedulable_ok(const sr_cluster *c, int32_t pod, int32_t node) {
+  if (!c->nodes.unschedulable[node]) return 1;
+  return o_tolerates(c, pod, c->id_unschedulable_key, c->id_empty, SR_EFFECT_NO_SCHEDULE);
+}
+
+/* TaintToleration.Filter: FindMatchingUntoleratedTaint over NoSchedule/NoExecute taints. */
+static int o_taints_ok(const sr_cluster *c, int32_t pod, int32_t node) {
+  const sr_nodes *N = &c->nodes;
+  for (int32_t t = N->taint_off[node]; t < N->taint_off[node + 1]; t++) {
+    int32_t e = N->taint_effect[t];
+    if (e != SR_EFFECT_NO_SCHEDULE && e != SR_EFFECT_NO_EXECUTE) continue;
+    if (!o_tolerates(c, pod, N->taint_key[t], N->taint_val[t], e)) return 0;
+  }
+  return 1;
+}
+
+static int o_in_values(const int32_t *vals, int32_t lo, int32_t hi, int32_t v) {
+  for (int32_t i = lo; i < hi; i++)
+    if (vals[i] == v) return 1;
+  return 0;
+}
+
+/* labels.NewRequirement validation + Requirement.Matches [upstream apimachinery labels]. */
+static int o_expr_valid(const sr_cluster *c, int32_t e) {
+  const sr_pods *P = &c->pods;
+  int32_t nv = P->expr_val_off[e + 1] - P->expr_val_off[e];
+  if (P->expr_key[e] == c->id_empty && c->id_empty != -1) return 0; /* empty key fails validateLabelKey */
+  switch (P->expr_op[e]) {
+    case SR_OP_IN:
+    case SR_OP_NOT_IN:
+      return nv > 0;
+    case SR_OP_EXISTS:
+    case SR_OP_DOES_NOT_EXIST:
+      return nv == 0;
+    default:
+      return 0; /* Gt/Lt are routed to fallback before we get here; others invalid */
+  }
+}
+
+static int o_expr_match(const sr_cluster *c, int32_t e, int32_t node) {
+  const sr_pods *P = &c->pods;
+  int32_t v;
+  int has = o_node_label(c, node, P->expr_key[e], &v);
+  int32_t lo = P->expr_val_off[e], hi = P->expr_val_off[e + 1];
+  switch (P->expr_op[e]) {
+    case SR_OP_IN:
+      return has && o_in_values(P->expr_vals, lo, hi, v);
+    case SR_OP_NOT_IN:
+      return !has || !o_in_values(P->expr_vals, lo, hi, v);
+    case SR_OP_EXISTS:
+      return has;
+    case SR_OP_DOES_NOT_EXIST:
+      return !has;
+    default:
+      return 0;
+  }
+}
+
+/* NodeSelectorRequirementsAsFieldSelector: In/NotIn with exactly one value
+ * against fields.Set{"metadata.name": node.Name}. */
+static int o_field_valid(const sr_cluster *c, int32_t f) {
+  const sr_pods *P = &c->pods;
+  int32_t nv = P->field_val_off[f + 1] - P->field_val_off[f];
+  int32_t op = P->field_op[f];
+  return (op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 1;
+}
+
+static int o_field_match(const sr_cluster *c, int32_t f, int32_t node) {
+  const sr_pods *P = &c->pods;
+  int32_t fv = (P->field_key[f] == c->id_metadata_name && c->id_metadata_name != -1)
+                   ? c->nodes.name[node]
+                   : c->id_empty;
+  int32_t want = P->field_vals[P->field_val_off[f]];
+  int eq = (fv == want) && fv != -1;
+  return P->field_op[f] == SR_OP_IN ? eq : !eq;
+}
+
+/* NodeAffinity.Filter = PodMatchesNodeSelectorAndAffinityTerms [upstream
+ * pkg/scheduler/framework/plugins/helper/node_affinity.go]. */
+static int o_affinity_ok(const sr_cluster *c, int32_t pod, int32_t node) {
+  const sr_pods *P = &c->pods;
+  for (int32_t i = P->sel_off[pod]; i < P->sel_off[pod + 1]; i++) {
+    int32_t v;
+    if (!o_node_label(c, node, P->sel_key[i], &v) || v != P->sel_val[i]) return 0;
+  }
+  if (!P->aff_required[pod]) return 1;
+  for (int32_t t = P->term_off[pod]; t < P->term_off[pod + 1]; t++) {
+    int32_t e0 = P->term_expr_off[t], e1 = P->term_expr_off[t + 1];
+    int32_t f0 = P->term_field_off[t], f1 = P->term_field_off[t + 1];
+    if (e0 == e1 && f0 == f1) continue; /* nil or empty term selects no objects */
+    int ok = 1;
+    if (e1 > e0) {
+      for (int32_t e = e0; e < e1 && ok; e++)
+        if (!o_expr_valid(c, e)) ok = 0;
+      for (int32_t e = e0; e < e1 && ok; e++)
+        if (!o_expr_match(c, e, node)) ok = 0;
+    }
+    if (ok && f1 > f0) {
+      for (int32_t f = f0; f < f1 && ok; f++)
+        if (!o_field_valid(c, f)) ok = 0;
+      for (int32_t f = f0; f < f1 && ok; f++)
+        if (!o_field_match(c, f, node)) ok = 0;
+    }
+    if (ok) return 1;
+  }
+  return 0;
+}
+
+/* NodePorts.Filter: HostPortInfo.CheckConflict [upstream framework/types.go]. */
+static int o_ports_ok(const o_state *st, const sr_cluster *c, int32_t pod) {
+  const sr_pods *P = &c->pods;
+  for (int32_t i = P->port_off[pod]; i < P->port_off[pod + 1]; i++) {
+    int32_t ip = P->port_ip[i], proto = P->port_proto[i], port = P->port_num[i];
+    if (port <= 0) continue;
+    for (int32_t j = 0; j < st->nports; j++) {
+      const o_port *u = &st->ports[j];
+      if (u->proto != proto || u->port != port) continue;
+      if (ip == -1) return 0;                    /* 0.0.0.0 conflicts with any IP */
+      if (u->ip == -1 || u->ip == ip) return 0;  /* else 0.0.0.0 or the same IP */
+    }
+  }
+  return 1;
+}
+
+/* NodeResourcesFit.Filter: fitsRequest [upstream plugins/noderesources/fit.go]. */
+static int o_resources_ok(const o_state *st, const sr_cluster *c, int32_t pod, int32_t node) {
+  const sr_pods *P = &c->pods;
+  const sr_nodes *N = &c->nodes;
+  if ((int64_t)st->npods + 1 > N->alloc_pods[node]) return 0;
+  int64_t rc = P->req_milli_cpu[pod], rm = P->req_memory[pod], re = P->req_ephemeral[pod];
+  if (rc == 0 && rm == 0 && re == 0) return 1;
+  if (N->alloc_milli_cpu[node] < o_add(rc, st->req[0])) return 0;
+  if (N->alloc_memory[node] < o_add(rm, st->req[1])) return 0;
+  if (N->alloc_ephemeral[node] < o_add(re, st->req[2])) return 0;
+  return 1;
+}
+
+int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c, int32_t pod) {
+  const sr_pods *P = &c->pods;
+  if (P->flags[pod] & SR_POD_FB_MASK) return 1;
+  /* an existing pod's required anti-affinity may select the incoming pod (InterPodAffinity) */
+  if (s->anti_total > 0) return 1;
+  if (P->aff_required[pod])
+    for (int32_t t = P->term_off[pod]; t < P->term_off[pod + 1]; t++)
+      for (int32_t e = P->term_expr_off[t]; e < P->term_expr_off[t + 1]; e++)
+        if (P->expr_op[e] == SR_OP_GT || P->expr_op[e] == SR_OP_LT) return 1;
+  return 0;
+}
+
+static int o_check(const o_state *st, const sr_cluster *c, int32_t pod, int32_t node) {
+  /* Filter order of the default provider; the result is their conjunction. */
+  if (!o_unschedulable_ok(c, pod, node)) return 0;
+  if (!o_resources_ok(st, c, pod, node)) return 0;
+  /* NodeName: passes, findSpotNodeForPod clears Spec.NodeName (rescheduler.go:341) */
+  if (!o_ports_ok(st, c, pod)) return 0;
+  if (!o_affinity_ok(c, pod, node)) return 0;
+  if (!o_taints_ok(c, pod, node)) return 0;
+  return 1;
+}
+
+int32_t oracle_check_predicates(const oracle_snapshot *s, const sr_cluster *c, int32_t pod, int32_t pos) {
+  if (oracle_pod_needs_fallback(s, c, pod)) return -1;
+  return o_check(&s->st[pos], c, pod, s->node[pos]);
+}
+
+/* findSpotNodeForPod (rescheduler.go:338-353) */
+static int32_t o_find(const o_state *st, const int32_t *node, int32_t n, const sr_cluster *c,
+                      int32_t pod, uint64_t *checks) {
+  for (int32_t pos = 0; pos < n; pos++) {
+    if (checks) (*checks)++;
+    if (o_check(&st[pos], c, pod, node[pos])) return pos;
+  }
+  return -1;
+}
+
+int32_t oracle_find_spot_node_for_pod(const oracle_snapshot *s, const sr_cluster *c, int32_t pod) {
+  if (oracle_pod_needs_fallback(s, c, pod)) return -2;
+  return o_find(s->st, s->node, s->n, c, pod, NULL);
+}
+
+/* canDrainNode (rescheduler.go:357-370) */
+int32_t oracle_can_drain_node(oracle_snapshot *s, const sr_cluster *c, const int32_t *pods, int32_t n,
+                              int32_t *node_of_pod) {
+  for (int32_t i = 0; i < n; i++)
+    if (oracle_pod_needs_fallback(s, c, pods[i])) return -2;
+  for (int32_t i = 0; i < n; i++) node_of_pod[i] = -1;
+  for (int32_t i = 0; i < n; i++) {
+    int32_t pos = o_find(s->st, s->node, s->n, c, pods[i], NULL);
+    if (pos < 0) return i;
+    node_of_pod[i] = pos;
+    oracle_snapshot_add_pod(s, c, pods[i], pos);
+  }
+  return -1;
+}
+
+/* ===================================================================== */
+/* The planning loop of run() (rescheduler.go:228-287). */
+
+typedef struct {
+  int32_t pos;
+  int64_t req[3];
+  int32_t npods, nports, anti;
+} o_undo;
+
+/* Evaluate one candidate from the base state `st` (Fork), then restore it (Revert). */
+static int32_t o_eval_candidate(o_state *st, const int32_t *node, int32_t n, const sr_cluster *c,
+                                const int32_t *pods, int32_t np, int32_t *map, o_undo *undo,
+                                uint64_t *checks) {
+  int32_t nu = 0, status = SR_CAND_OK;
+  for (int32_t i = 0; i < np; i++) map[i] = -1;
+  for (int32_t i = 0; i < np; i++) {
+    int32_t pos = o_find(st, node, n, c, pods[i], checks);
+    if (pos < 0) {
+      status = i;
+      break;
+    }
+    map[i] = pos;
+    o_undo *u = &undo[nu++];
+    u->pos = pos;
+    memcpy(u->req, st[pos].req, sizeof(u->req));
+    u->npods = st[pos].npods;
+    u->nports = st[pos].nports;
+    u->anti = st[pos].anti;
+    o_state_add_pod(&st[pos], c, pods[i]);
+  }
+  while (nu > 0) { /* Revert, newest first */
+    o_undo *u = &undo[--nu];
+    memcpy(st[u->pos].req, u->req, sizeof(u->req));
+    st[u->pos].npods = u->npods;
+    st[u->pos].nports = u->nports;
+    st[u->pos].anti = u->anti;
+  }
+  return status;
+}
+
+static int o_cand_fallback(const oracle_snapshot *s, const sr_cluster *c, const int32_t *pods, int32_t np) {
+  for (int32_t i = 0; i < np; i++)
+    if (oracle_pod_needs_fallback(s, c, pods[i])) return 1;
+  return 0;
+}
+
+int32_t oracle_plan(const oracle_snapshot *s, const sr_cluster *c, const sr_candidates *cands,
+                    int32_t mode, int32_t threads, sr_plan_out *out) {
+  int32_t nc = cands->n_cand;
+  const int32_t *off = cands->cand_pod_off;
+  int32_t maxp = 0;
+  for (int32_t i = 0; i < nc; i++)
+    if (off[i + 1] - off[i] > maxp) maxp = off[i + 1] - off[i];
+  int32_t *status = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nc ? nc : 1));
+  int32_t total = off[nc];
+  int32_t *map = (int32_t *)malloc(sizeof(int32_t) * (size_t)(total ? total : 1));
+  for (int32_t i = 0; i < nc; i++) status[i] = ORACLE_NOT_EVALUATED;
+  for (int32_t i = 0; i < total; i++) map[i] = -1;
+  uint64_t checks = 0, fb_pods = 0;
+
+  if (mode == 0 || threads <= 1) {
+    o_state *st = o_copy_states(s->st, s->n);
+    o_undo *undo = (o_undo *)malloc(sizeof(o_undo) * (size_t)(maxp ? maxp : 1));
+    for (int32_t i = 0; i < nc; i++) {
+      const int32_t *pods = cands->cand_pods + off[i];
+      int32_t np = off[i + 1] - off[i];
+      if (np < 1) {
+        status[i] = SR_CAND_EMPTY;
+        continue;
+      }
+      if (o_cand_fallback(s, c, pods, np)) {
+        status[i] = SR_CAND_FALLBACK;
+        fb_pods += (uint64_t)np;
+        continue;
+      }
+      status[i] = o_eval_candidate(st, s->node, s->n, c, pods, np, map + off[i], undo, &checks);
+      if (mode == 0 && status[i] == SR_CAND_OK) break; /* drain + break (rescheduler.go:286) */
+    }
+    free(undo);
+    o_free_states(st, s->n);
+  } else {
+#ifdef _OPENMP
+    omp_set_num_threads(threads);
+#endif
+#pragma omp parallel reduction(+ : checks, fb_pods)
+    {
+      o_state *st = o_copy_states(s->st, s->n);
+      o_undo *undo = (o_undo *)malloc(sizeof(o_undo) * (size_t)(maxp ? maxp : 1));
+#pragma omp for schedule(dynamic, 4)
+      for (int32_t i = 0; i < nc; i++) {
+        const int32_t *pods = cands->cand_pods + off[i];
+        int32_t np = off[i + 1] - off[i];
+        if (np < 1) {
+          status[i] = SR_CAND_EMPTY;
+          continue;
+        }
+        if (o_cand_fallback(s, c, pods, np)) {
+          status[i] = SR_CAND_FALLBACK;
+          fb_pods += (uint64_t)np;
+          continue;
+        }
+        status[i] = o_eval_candidate(st, s->node, s->n, c, pods, np, map + off[i], undo, &checks);
+      }
+      free(undo);
+      o_free_states(st, s->n);
+    }
+  }
+
+  int32_t first_ok = -1, first_fb = -1;
+  for (int32_t i = 0; i < nc; i++) {
+    int32_t g = cands->cand_global ? cands->cand_global[i] : i;
+    if (status[i] == SR_CAND_OK && (first_ok < 0 || g < first_ok)) first_ok = g;
+    if (status[i] == SR_CAND_FALLBACK && (first_fb < 0 || g < first_fb)) first_fb = g;
+  }
+  out->first_ok = first_ok;
+  out->first_fallback = first_fb;
+  out->winner = (first_ok >= 0 && (first_fb < 0 || first_fb > first_ok)) ? first_ok : -1;
+  out->checks = checks;
+  out->fallback_pods = fb_pods;
+  out->winner_npods = 0;
+  for (int32_t i = 0; i < nc; i++) {
+    int32_t g = cands->cand_global ? cands->cand_global[i] : i;
+    if (g == first_ok) {
+      out->winner_npods = off[i + 1] - off[i];
+      if (out->winner_map) memcpy(out->winner_map, map + off[i], sizeof(int32_t) * (size_t)out->winner_npods);
+    }
+  }
+  if (out->status) memcpy(out->status, status, sizeof(int32_t) * (size_t)nc);
+  if (out->node_of_pod) memcpy(out->node_of_pod, map, sizeof(int32_t) * (size_t)total);
+  free(status);
+  free(map);
+  return SR_OK;
+}

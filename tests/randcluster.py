@@ -1,0 +1,101 @@
+"""Random small clusters exercising every encoded predicate and its edge cases
+(zero requests, overcommitted nodes, pod-count limits, every taint effect,
+every toleration shape, selectors, node affinity incl. invalid / empty terms
+and matchFields, host ports incl. intra-candidate conflicts, fallback features).
+Seeded; sized so the oracle finishes in milliseconds."""
+from __future__ import annotations
+
+import random
+
+from spotplanner.model import (Container, ContainerPort, GiB, MiB, Node, NodeSelectorRequirement,
+                               NodeSelectorTerm, OwnerReference, Pod, Taint, Toleration)
+
+KEYS = ["zone", "type", "team", "disk", "gpu"]
+VALS = ["a", "b", "c", ""]
+EFFECTS = ["NoSchedule", "NoExecute", "PreferNoSchedule"]
+
+
+def rand_node(r: random.Random, name: str, features: bool) -> Node:
+    labels = {"kubernetes.io/hostname": name}
+    if features:
+        for k in KEYS:
+            if r.random() < 0.5:
+                labels[k] = r.choice(VALS)
+    taints = []
+    if features and r.random() < 0.3:
+        for _ in range(r.randint(1, 2)):
+            taints.append(Taint(r.choice(["dedicated", "team", "x"]), r.choice(VALS), r.choice(EFFECTS)))
+    return Node(name=name, cpu_milli=r.choice([500, 1000, 2000, 4000]), memory=r.choice([1, 2, 4]) * GiB,
+                pods=r.choice([3, 5, 110]), ephemeral=r.choice([0, 10 * GiB]), labels=labels, taints=taints,
+                unschedulable=features and r.random() < 0.1)
+
+
+def rand_pod(r: random.Random, name: str, features: bool, fallback: bool = False) -> Pod:
+    cpu = r.choice([0, 0, 50, 100, 250, 500, 1000])
+    mem = r.choice([0, 64 * MiB, 256 * MiB, 1 * GiB])
+    eph = r.choice([0, 0, 0, 1 * GiB])
+    conts = [Container(cpu_milli=cpu, memory=mem, ephemeral=eph)]
+    if r.random() < 0.2:
+        conts.append(Container(cpu_milli=r.choice([0, 100]), memory=r.choice([0, 128 * MiB])))
+    init = [Container(cpu_milli=r.choice([0, 800]), memory=r.choice([0, 2 * GiB]))] if r.random() < 0.15 else []
+    overhead = Container(cpu_milli=50, memory=32 * MiB) if r.random() < 0.1 else None
+    p = Pod(name=name, containers=conts, init_containers=init, overhead=overhead,
+            owner_references=[OwnerReference("ReplicaSet")])
+    if features:
+        if r.random() < 0.3:
+            p.node_selector = {r.choice(KEYS): r.choice(VALS)}
+        if r.random() < 0.25:
+            terms = []
+            for _ in range(r.randint(0, 3)):
+                exprs = []
+                for _ in range(r.randint(0, 2)):
+                    op = r.choice(["In", "NotIn", "Exists", "DoesNotExist", "Bogus"])
+                    vals = [] if op in ("Exists", "DoesNotExist") else r.sample(VALS, r.randint(1, 2))
+                    if r.random() < 0.05:  # invalid arity
+                        vals = [] if vals else ["a"]
+                    exprs.append(NodeSelectorRequirement(r.choice(KEYS), op, vals))
+                fields = []
+                if r.random() < 0.2:
+                    fields.append(NodeSelectorRequirement(r.choice(["metadata.name", "metadata.uid"]),
+                                                          r.choice(["In", "NotIn"]),
+                                                          ["n%d" % r.randint(0, 5)]))
+                terms.append(NodeSelectorTerm(exprs, fields))
+            p.required_node_affinity = terms
+        if r.random() < 0.35:
+            for _ in range(r.randint(1, 2)):
+                p.tolerations.append(Toleration(r.choice(["", "dedicated", "team", "x",
+                                                          "node.kubernetes.io/unschedulable"]),
+                                                r.choice(["", "Equal", "Exists", "Weird"]), r.choice(VALS),
+                                                r.choice(["", "NoSchedule", "NoExecute", "PreferNoSchedule"])))
+        if r.random() < 0.2:
+            p.containers[0].ports.append(ContainerPort(host_port=r.choice([80, 443, 9100]),
+                                                       protocol=r.choice(["TCP", "UDP", ""])))
+    if fallback and r.random() < 0.1:
+        kind = r.randint(0, 4)
+        if kind == 0:
+            p.has_pvc = True
+        elif kind == 1:
+            p.containers[0].scalar = {"nvidia.com/gpu": 1}
+        elif kind == 2:
+            p.required_pod_affinity = True
+        elif kind == 3:
+            p.containers[0].ports.append(ContainerPort(host_port=8080, host_ip="10.0.0.1"))
+        else:
+            p.required_node_affinity = [NodeSelectorTerm([NodeSelectorRequirement("zone", "Gt", ["1"])])]
+    return p
+
+
+def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 8, features: bool = True,
+                  fallback: bool = False):
+    """Returns (spot_nodes, spot_pods, candidates) with candidates a list of pod lists."""
+    r = random.Random(seed)
+    nodes = [rand_node(r, "n%d" % i, features) for i in range(n_spot)]
+    spot_pods = []
+    for i, n in enumerate(nodes):
+        ps = [rand_pod(r, "s%d_%d" % (i, k), features) for k in range(r.randint(0, 4))]
+        if r.random() < 0.15:  # overcommitted node
+            ps.append(Pod(name="big%d" % i, containers=[Container(cpu_milli=n.cpu_milli + 100)]))
+        spot_pods.append(ps)
+    cands = [[rand_pod(r, "c%d_%d" % (c, k), features, fallback) for k in range(r.randint(0, max_pods))]
+             for c in range(n_cand)]
+    return nodes, spot_pods, cands

@@ -1,0 +1,243 @@
+"""Parity of the HIP path (through the C-ABI) with the CPU oracle: bit-exact
+drain plans (per-candidate status and the full pod -> spot node mapping),
+findSpotNodeForPod answers and canDrainNode side effects, on seeded random
+clusters, on the BASELINE.json synthetic configs and on edge cases."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from helpers import Scenario
+from oracle_lib import OracleSnapshot, load_oracle, oracle_new_node_map, oracle_plan
+from randcluster import rand_scenario
+from spotplanner import capi
+from spotplanner.model import Container, ContainerPort, GiB, Node, Pod
+from spotplanner.rescheduler import plan_arrays
+from spotplanner.synth import SynthCluster, build_candidates, new_node_map
+
+pytestmark = pytest.mark.gpu
+
+OK, FB, EMPTY = capi.SR_CAND_OK, capi.SR_CAND_FALLBACK, capi.SR_CAND_EMPTY
+
+
+def product_only_fallback(pods):
+    """Candidates the product routes to the reference path although the oracle
+    can evaluate them: host ports bound to a specific hostIP."""
+    return any(pp.host_ip not in ("", "0.0.0.0") for p in pods for pp in p.host_ports())
+
+
+def compare_plans(o, p, cand_off, extra_fallback=None):
+    n = len(cand_off) - 1
+    exp_ok, exp_fb = -1, -1
+    for c in range(n):
+        os_, ps = int(o["status"][c]), int(p.status[c])
+        if os_ == FB:
+            assert ps == FB, (c, os_, ps)
+        elif ps == FB:
+            assert extra_fallback is not None and extra_fallback(c), (c, os_, ps)
+        else:
+            assert ps == os_, (c, os_, ps)
+            seg = slice(cand_off[c], cand_off[c + 1])
+            assert np.array_equal(p.node_of_pod[seg], o["node_of_pod"][seg]), c
+            if ps == OK and exp_ok < 0:
+                exp_ok = c
+        if ps == FB and exp_fb < 0:
+            exp_fb = c
+    assert p.first_ok == exp_ok
+    assert p.first_fallback == exp_fb
+    want_winner = exp_ok if exp_ok >= 0 and (exp_fb < 0 or exp_fb > exp_ok) else -1
+    assert p.winner == want_winner
+    if exp_ok >= 0:
+        assert np.array_equal(p.winner_map, o["node_of_pod"][cand_off[exp_ok]:cand_off[exp_ok + 1]])
+
+
+def run_scenario(checker, nodes, spot_pods, cands):
+    flat = [p for c in cands for p in c]
+    sc = Scenario(nodes, spot_pods, flat)
+    cand_off = np.cumsum([0] + [len(c) for c in cands]).astype(np.int32)
+    cand_pods = np.arange(sc.q0, sc.q0 + len(flat), dtype=np.int32)
+    o = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=1)
+    h = sc.product_snapshot()
+    try:
+        p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+    finally:
+        capi.load_planner().sr_snapshot_destroy(h)
+    compare_plans(o, p, cand_off, lambda c: product_only_fallback(cands[c]))
+    return sc, o, p
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_plans_match_oracle(checker, seed):
+    nodes, spot_pods, cands = rand_scenario(seed, n_spot=6 + seed % 40, n_cand=10, max_pods=6 + seed % 10)
+    run_scenario(checker, nodes, spot_pods, cands)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_plans_with_fallback_features(checker, seed):
+    nodes, spot_pods, cands = rand_scenario(1000 + seed, n_spot=20, n_cand=12, max_pods=8, fallback=True)
+    run_scenario(checker, nodes, spot_pods, cands)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_plans_resources_only(checker, seed):
+    nodes, spot_pods, cands = rand_scenario(2000 + seed, n_spot=30, n_cand=16, max_pods=12, features=False)
+    run_scenario(checker, nodes, spot_pods, cands)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_find_spot_nodes_match_oracle(checker, seed):
+    nodes, spot_pods, cands = rand_scenario(3000 + seed, n_spot=25, n_cand=6, max_pods=10)
+    flat = [p for c in cands for p in c]
+    sc = Scenario(nodes, spot_pods, flat)
+    osnap = sc.oracle_snapshot()
+    olib = load_oracle()
+    want = [olib.oracle_find_spot_node_for_pod(osnap.h, sc.ptr, sc.qidx(i)) for i in range(len(flat))]
+    h = sc.product_snapshot()
+    lib = capi.load_planner()
+    idx = np.arange(sc.q0, sc.q0 + len(flat), dtype=np.int32)
+    out = np.full(max(1, len(flat)), -7, np.int32)
+    fb = np.zeros(max(1, len(flat)), np.uint8)
+    assert lib.sr_find_spot_nodes(checker.handle, h, sc.ptr, capi.ptr(idx, capi.P32), len(flat),
+                                  capi.ptr(out, capi.P32), capi.ptr(fb, capi.PU8)) == capi.SR_OK
+    for i, w in enumerate(want):
+        if w == -2:
+            assert fb[i] == 1
+        elif fb[i] == 0:
+            assert out[i] == w, (i, w, out[i])
+        else:
+            assert product_only_fallback([flat[i]])
+    lib.sr_snapshot_destroy(h)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_can_drain_node_sequence_mutates_like_oracle(checker, seed):
+    """Several canDrainNode calls on ONE snapshot, without Fork/Revert
+    (rescheduler_test.go:140-150): results and snapshot state stay equal."""
+    nodes, spot_pods, cands = rand_scenario(4000 + seed, n_spot=10, n_cand=6, max_pods=6)
+    flat = [p for c in cands for p in c]
+    sc = Scenario(nodes, spot_pods, flat)
+    osnap = sc.oracle_snapshot()
+    olib = load_oracle()
+    h = sc.product_snapshot()
+    lib = capi.load_planner()
+    base = sc.q0
+    for c in cands:
+        n = len(c)
+        pods = np.arange(base, base + n, dtype=np.int32)
+        base += n
+        omap = np.full(max(n, 1), -1, np.int32)
+        r = olib.oracle_can_drain_node(osnap.h, sc.ptr, capi.ptr(pods, capi.P32), n, capi.ptr(omap, capi.P32))
+        pmap = np.full(max(n, 1), -1, np.int32)
+        fail = ctypes.c_int32()
+        fb = ctypes.c_uint8()
+        assert lib.sr_can_drain_node(checker.handle, h, sc.ptr, capi.ptr(pods, capi.P32), n,
+                                     capi.ptr(pmap, capi.P32), ctypes.byref(fail), ctypes.byref(fb)) == capi.SR_OK
+        if r == -2:
+            assert fb.value == 1
+            continue
+        if fb.value:
+            assert product_only_fallback(c)
+            break  # the oracle mutated, the product (correctly) did not: stop comparing states
+        assert fail.value == r
+        assert np.array_equal(pmap[:n], omap[:n])
+        for pos in range(len(nodes)):
+            req = np.zeros(3, np.int64)
+            k = ctypes.c_int32()
+            lib.sr_snapshot_node_state(h, pos, capi.ptr(req, capi.P64), ctypes.byref(k))
+            assert (tuple(req), k.value) == osnap.node_state(pos)
+    lib.sr_snapshot_destroy(h)
+
+
+# ------------------------------------------------------------------ edge cases
+def test_no_spot_nodes(checker):
+    cands = [[Pod("a", containers=[Container(100)])], [], [Pod("z", containers=[Container(0)])]]
+    _, o, p = run_scenario(checker, [], [], cands)
+    assert list(p.status) == [0, EMPTY, 0]
+
+
+def test_no_candidates(checker):
+    node = Node("n0", 1000)
+    _, o, p = run_scenario(checker, [node], [[]], [])
+    assert p.winner == -1 and p.first_ok == -1
+
+
+def test_zero_request_pods_skip_resource_checks(checker):
+    # overcommitted node: a zero-request pod still fits (only the pod count is checked)
+    node = Node("n0", 1000, pods=3)
+    spot = [[Pod("big", containers=[Container(5000)])]]
+    cands = [[Pod("z1", containers=[Container(0)]), Pod("z2", containers=[Container(0)]),
+              Pod("z3", containers=[Container(0)])], [Pod("c", containers=[Container(1)])]]
+    _, o, p = run_scenario(checker, [node], spot, cands)
+    assert list(p.status) == [2, 0]  # third zero pod exceeds allocatable pods (3)
+
+
+def test_intra_candidate_host_port_conflict(checker):
+    nodes = [Node("n0", 4000), Node("n1", 4000)]
+    mk = lambda name: Pod(name, containers=[Container(100, ports=[ContainerPort(80)])])
+    cands = [[mk("a"), mk("b"), mk("c")]]
+    _, o, p = run_scenario(checker, nodes, [[], []], cands)
+    assert list(p.status) == [2]
+    assert list(p.node_of_pod) == [0, 1, -1]
+
+
+def test_more_than_128_touched_nodes(checker):
+    # every spot node has room for exactly one more pod: 200 pods touch 200 nodes
+    nodes = [Node("n%d" % i, 1000, pods=1) for i in range(260)]
+    cands = [[Pod("p%d" % k, containers=[Container(10)]) for k in range(200)],
+             [Pod("q%d" % k, containers=[Container(10)]) for k in range(300)]]
+    _, o, p = run_scenario(checker, nodes, [[] for _ in nodes], cands)
+    assert p.status[0] == OK and p.status[1] == 260
+    assert list(p.node_of_pod[:200]) == list(range(200))
+
+
+def test_many_chunks_of_spot_nodes(checker):
+    # > 4096 spot nodes: bitmask rows span several 64-word chunks
+    nodes = [Node("n%d" % i, 100) for i in range(9000)] + [Node("big", 10000)]
+    cands = [[Pod("a", containers=[Container(500)]), Pod("b", containers=[Container(50)])]]
+    _, o, p = run_scenario(checker, nodes, [[] for _ in nodes], cands)
+    assert list(p.node_of_pod) == [9000, 0]
+
+
+# ------------------------------------------------------------ synthetic configs
+def tick_parity(checker, sc: SynthCluster, max_cands=None):
+    lib = capi.load_planner()
+    nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+    if max_cands is not None:
+        cand_off = cand_off[: max_cands + 1]
+        cand_pods = cand_pods[: cand_off[-1]]
+    h = ctypes.c_void_p()
+    assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot),
+                                  capi.ptr(nm.node_pod_off, capi.P32), capi.ptr(nm.node_pod_idx, capi.P32),
+                                  ctypes.byref(h)) == capi.SR_OK
+    p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+    lib.sr_snapshot_destroy(h)
+    osnap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
+    o = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
+    ip = np.ctypeslib.as_array(sc.cluster.pods.port_ip, shape=(max(1, sc.cluster.pods.port_off[sc.n_pods]),))
+    po = np.ctypeslib.as_array(sc.cluster.pods.port_off, shape=(sc.n_pods + 1,))
+
+    def specific_ip(c):
+        for q in cand_pods[cand_off[c]:cand_off[c + 1]]:
+            if np.any(ip[po[q]:po[q + 1]] != -1):
+                return True
+        return False
+
+    compare_plans(o, p, cand_off, specific_ip)
+    return o, p
+
+
+@pytest.mark.parametrize("config", [1, 2, 3, 5])
+def test_synthetic_config_plans_match_oracle(checker, config):
+    o, p = tick_parity(checker, SynthCluster(config))
+    assert p.checks > 0
+
+
+def test_synthetic_config3_other_seeds(checker):
+    for seed in (11, 12):
+        tick_parity(checker, SynthCluster(3, seed=seed, n_on_demand=500, n_spot=1200, pinned_fraction=0.05))
+
+
+def test_synthetic_config4_spot_pool_sampled_candidates(checker):
+    # full C4 spot pool (35k nodes: 9 chunks per row) with the first 1500 candidates
+    tick_parity(checker, SynthCluster(4, n_on_demand=1500), max_cands=1500)
