@@ -278,9 +278,15 @@ typedef struct {
   uint64_t bytes_feasibility; /* algorithmic bytes per K1 launch */
   uint64_t bytes_placement;   /* algorithmic bytes per K2 launch */
   int32_t  n_pods, n_spot, n_cand, n_words;
-  int32_t  n_rows_a, n_rows_b, n_classes;
+  int32_t  n_rows_static, n_rows_threshold, n_classes;
 } sr_timing;
-sr_status sr_set_timing(sr_ctx *ctx, int32_t enable);
+/* mask: which kernels sr_plan_run brackets with HIP events (resets the sums):
+ * 1 = K0, 2 = K1, 4 = K2, 8 = K3 + collective + download; 0 = no events. */
+#define SR_TIME_TABLES      1
+#define SR_TIME_FEASIBILITY 2
+#define SR_TIME_PLACEMENT   4
+#define SR_TIME_WINNER      8
+sr_status sr_set_timing(sr_ctx *ctx, int32_t mask);
 sr_status sr_get_timing(const sr_ctx *ctx, sr_timing *out);
 
 /* Multi-GPU: one process per GPU; candidates sharded by the caller (use

@@ -6,14 +6,14 @@
 // factors into a conjunction of terms that each depend on a low-cardinality
 // projection of the pod:
 //
-//   fits(p, n) = A[class(p), cpu(p), eph(p), zero(p)](n)  AND  B[mem(p)](n)
+//   fits(p, n) = S[class(p)](n) & T[cpu(p)](n) & T[mem(p)](n) & T[eph(p)](n)
 //
-//   A = static(class, n)            selector / affinity / taints / base ports
+//   S = static(class, n)            selector / affinity / taints / base ports
 //       AND len(pods)+1 <= allowed  (pod-count part of NodeResourcesFit)
-//       AND (zero-request OR (cpu <= free_cpu AND eph <= free_eph))
-//   B = zero-request OR mem <= free_mem
+//   T = free_dim(n) >= threshold    (zero-request pods use row 0 = all nodes:
+//                                    fitsRequest skips the resource checks)
 //
-// where "class" interns everything static about a pod.  Both tables are bitmask
+// where "class" interns everything static about a pod.  S and T are bitmask
 // rows over spot nodes in NodeInfoArray order, built on the GPU (K0); the dense
 // pod x node bitmask is their AND (K1).  Everything that changes while a
 // candidate's pods are placed (capacity, pod count, host ports) is rechecked
@@ -77,22 +77,6 @@ bool tolerates(const sr_pods& P, int32_t pod, int32_t id_empty, const TaintRec& 
   }
   return false;
 }
-
-struct TupleKey {
-  int32_t cls, zero;
-  int64_t cpu, eph;
-  bool operator==(const TupleKey& o) const {
-    return cls == o.cls && zero == o.zero && cpu == o.cpu && eph == o.eph;
-  }
-};
-struct TupleHash {
-  size_t operator()(const TupleKey& k) const {
-    uint64_t h = static_cast<uint64_t>(k.cls) * 0x9E3779B97F4A7C15ull;
-    h ^= static_cast<uint64_t>(k.cpu) + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
-    h ^= static_cast<uint64_t>(k.eph) + 0x8CB92BA72F3D8DD7ull + (h << 6) + (h >> 2);
-    return static_cast<size_t>(h ^ static_cast<uint64_t>(k.zero));
-  }
-};
 
 }  // namespace
 
@@ -215,15 +199,15 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     if (sn.unschedulable)
       node_taints[n].push_back(taint_id(TaintRec{snap->id_unschedulable_key, snap->id_empty, SR_EFFECT_NO_SCHEDULE}));
   }
-  w->WT = std::max<int32_t>(1, (static_cast<int32_t>(taints.size()) + 63) / 64);
+  const int32_t n_taints = static_cast<int32_t>(taints.size());
 
-  // ---- classes of active pods
+  // ---- static part of every active pod
   RequirementDict rdict;
   struct PodStatic {
     std::vector<int32_t> sel;                 // requirement ids
     std::vector<std::vector<int32_t>> terms;  // valid terms only
     int32_t flags = 0;
-    std::vector<uint64_t> tol;
+    const std::vector<int32_t>* untol = nullptr;  // taint ids the pod does not tolerate
     uint64_t ports = 0;
   };
   // Active pods in candidate order.
@@ -243,6 +227,11 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   }
   w->cand_off.push_back(static_cast<int32_t>(active_pod.size()));
   const int32_t na = static_cast<int32_t>(active_pod.size());
+
+  // Untolerated-taint sets, memoised by the pod's toleration list.
+  std::unordered_map<std::string, std::vector<int32_t>> untol_memo;
+  std::vector<int32_t> all_taints(static_cast<size_t>(n_taints));
+  for (int32_t t = 0; t < n_taints; ++t) all_taints[t] = t;
 
   std::vector<PodStatic> pstat(static_cast<size_t>(na));
   for (int32_t q = 0; q < na; ++q) {
@@ -291,61 +280,87 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       }
       if (ps.terms.empty()) ps.flags |= CLS_IMPOSSIBLE;
     }
-    ps.tol.assign(static_cast<size_t>(w->WT), 0);
-    if (P.tol_off[pod + 1] > P.tol_off[pod])
-      for (size_t t = 0; t < taints.size(); ++t)
-        if (tolerates(P, pod, c->id_empty, taints[t])) ps.tol[t >> 6] |= 1ull << (t & 63);
+    // Spec.Tolerations against the spot pool's taints.
+    const int32_t t0 = P.tol_off[pod], t1 = P.tol_off[pod + 1];
+    if (t0 == t1) {
+      ps.untol = &all_taints;
+    } else {
+      std::string key;
+      for (int32_t i = t0; i < t1; ++i) {
+        const int32_t rec[4] = {P.tol_key[i], P.tol_op[i], P.tol_val[i], P.tol_effect[i]};
+        key += bytes_of(rec, 4);
+      }
+      auto it = untol_memo.find(key);
+      if (it == untol_memo.end()) {
+        std::vector<int32_t> u;
+        for (int32_t t = 0; t < n_taints; ++t)
+          if (!tolerates(P, pod, c->id_empty, taints[t])) u.push_back(t);
+        it = untol_memo.emplace(std::move(key), std::move(u)).first;
+      }
+      ps.untol = &it->second;
+    }
     ps.ports = pod_port_mask(pod);
   }
   const std::vector<Requirement>& reqs = rdict.all();
-  w->WR = std::max<int32_t>(1, (static_cast<int32_t>(reqs.size()) + 63) / 64);
-  const int32_t WR = w->WR, WT = w->WT;
+  const int32_t n_reqs = static_cast<int32_t>(reqs.size());
+  const int32_t n_ports = static_cast<int32_t>(port_dict.size());
+  const int32_t A_REQ = 1, A_TAINT = 1 + n_reqs, A_PORT = 1 + n_reqs + n_taints;
+  w->n_atoms = A_PORT + n_ports;
 
-  // intern classes
+  // ---- intern classes (atom programs)
   std::unordered_map<std::string, int32_t> class_index;
   std::vector<int32_t> pod_class(static_cast<size_t>(na));
+  w->cls_and_off.push_back(0);
+  w->cls_not_off.push_back(0);
   w->cls_term_off.push_back(0);
-  std::vector<uint64_t> sig;
+  w->term_atom_off.push_back(0);
+  std::vector<int32_t> sig;
   for (int32_t q = 0; q < na; ++q) {
     const PodStatic& ps = pstat[q];
-    sig.assign(static_cast<size_t>(WR), 0);
-    for (int32_t r : ps.sel) sig[r >> 6] |= 1ull << (r & 63);
-    sig.push_back(static_cast<uint64_t>(ps.flags));
-    sig.push_back(ps.terms.size());
+    sig.clear();
+    sig.push_back(ps.flags);
+    sig.push_back(static_cast<int32_t>(ps.sel.size()));
+    sig.insert(sig.end(), ps.sel.begin(), ps.sel.end());
+    sig.push_back(static_cast<int32_t>(ps.terms.size()));
     for (const auto& t : ps.terms) {
-      const size_t base = sig.size();
-      sig.resize(base + WR, 0);
-      for (int32_t r : t) sig[base + (r >> 6)] |= 1ull << (r & 63);
+      sig.push_back(static_cast<int32_t>(t.size()));
+      sig.insert(sig.end(), t.begin(), t.end());
     }
-    sig.insert(sig.end(), ps.tol.begin(), ps.tol.end());
-    sig.push_back(ps.ports);
-    std::string key(reinterpret_cast<const char*>(sig.data()), sig.size() * sizeof(uint64_t));
-    auto ins = class_index.emplace(std::move(key), w->n_classes);
+    sig.push_back(static_cast<int32_t>(ps.untol->size()));
+    sig.insert(sig.end(), ps.untol->begin(), ps.untol->end());
+    sig.push_back(static_cast<int32_t>(ps.ports & 0xffffffffu));
+    sig.push_back(static_cast<int32_t>(ps.ports >> 32));
+    auto ins = class_index.emplace(bytes_of(sig.data(), sig.size()), w->n_classes);
     if (ins.second) {
-      w->cls_sel.insert(w->cls_sel.end(), sig.begin(), sig.begin() + WR);
-      w->cls_flags.push_back(ps.flags);
+      w->cls_and.push_back(0);  // len(pods)+1 <= allowed pods
+      for (int32_t r : ps.sel) w->cls_and.push_back(A_REQ + r);
+      w->cls_and_off.push_back(static_cast<int32_t>(w->cls_and.size()));
+      for (int32_t t : *ps.untol) w->cls_not.push_back(A_TAINT + t);
+      for (int32_t b = 0; b < 64; ++b)
+        if (ps.ports >> b & 1) w->cls_not.push_back(A_PORT + b);
+      w->cls_not_off.push_back(static_cast<int32_t>(w->cls_not.size()));
       for (const auto& t : ps.terms) {
-        const size_t base = w->term_mask.size();
-        w->term_mask.resize(base + WR, 0);
-        for (int32_t r : t) w->term_mask[base + (r >> 6)] |= 1ull << (r & 63);
+        for (int32_t r : t) w->term_atoms.push_back(A_REQ + r);
+        w->term_atom_off.push_back(static_cast<int32_t>(w->term_atoms.size()));
       }
-      w->cls_term_off.push_back(static_cast<int32_t>(w->term_mask.size() / WR));
-      w->cls_tol.insert(w->cls_tol.end(), ps.tol.begin(), ps.tol.end());
-      w->cls_port.push_back(ps.ports);
+      w->cls_term_off.push_back(static_cast<int32_t>(w->term_atom_off.size()) - 1);
+      w->cls_flags.push_back(ps.flags);
       w->n_classes++;
     }
     pod_class[q] = ins.first->second;
   }
 
-  // ---- spot nodes: dynamic base state, requirement / taint / port bitsets
-  const int32_t NP = w->n_pad;
+  // ---- spot nodes: base capacity state and the atom rows
+  const int32_t NP = w->n_pad, Wp = w->Wp;
   w->free_cpu.assign(NP, 0);
   w->free_mem.assign(NP, 0);
   w->free_eph.assign(NP, 0);
   w->pods_left.assign(NP, 0);
   w->port_bits.assign(NP, 0);
-  w->req_bits.assign(static_cast<size_t>(WR) * NP, 0);
-  w->taint_bits.assign(static_cast<size_t>(WT) * NP, 0);
+  w->atoms.assign(static_cast<size_t>(w->n_atoms) * Wp, 0);
+  auto set_atom = [&](int32_t atom, int32_t n) {
+    w->atoms[static_cast<size_t>(atom) * Wp + (n >> 6)] |= 1ull << (n & 63);
+  };
   for (int32_t n = 0; n < n_spot; ++n) {
     const SpotNode& sn = snap->nodes[n];
     const NodeState& st = snap->state[n];
@@ -360,15 +375,27 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     w->free_eph[n] = sn.alloc[2] - st.requested[2];
     const int64_t left = sn.alloc_pods - st.npods;
     w->pods_left[n] = static_cast<int32_t>(std::max<int64_t>(-(1 << 30), std::min<int64_t>(left, 1 << 30)));
+    if (left >= 1) set_atom(0, n);
     uint64_t pb = 0;
     for (const Port& u : st.ports) {
       auto it = port_dict.find(port_key(u.proto, u.port));
       if (it != port_dict.end()) pb |= 1ull << it->second;  // incoming pods bind 0.0.0.0
     }
     w->port_bits[n] = pb;
-    for (int32_t t : node_taints[n]) w->taint_bits[static_cast<size_t>(t >> 6) * NP + n] |= 1ull << (t & 63);
+    for (int32_t b = 0; b < 64; ++b)
+      if (pb >> b & 1) set_atom(A_PORT + b, n);
+    for (int32_t t : node_taints[n]) set_atom(A_TAINT + t, n);
   }
-  // requirement bits: one label-value column per distinct key
+  w->node_rec.assign(static_cast<size_t>(NP) * 8, 0);
+  for (int32_t n = 0; n < n_spot; ++n) {
+    uint64_t* r = &w->node_rec[static_cast<size_t>(n) * 8];
+    r[0] = static_cast<uint64_t>(w->free_cpu[n]);
+    r[1] = static_cast<uint64_t>(w->free_mem[n]);
+    r[2] = static_cast<uint64_t>(w->free_eph[n]);
+    r[3] = w->port_bits[n];
+    r[4] = static_cast<uint64_t>(static_cast<int64_t>(w->pods_left[n]));
+  }
+  // requirement atoms: one label-value column per distinct key
   std::unordered_map<int32_t, std::vector<int32_t>> col;  // key -> value per node (INT32_MIN absent)
   for (const Requirement& r : reqs)
     if (r.type != REQ_FIELD && !col.count(r.key)) col.emplace(r.key, std::vector<int32_t>(n_spot, INT32_MIN));
@@ -377,17 +404,16 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       auto it = col.find(kv.first);
       if (it != col.end()) it->second[n] = kv.second;
     }
-  for (size_t ri = 0; ri < reqs.size(); ++ri) {
+  for (int32_t ri = 0; ri < n_reqs; ++ri) {
     const Requirement& r = reqs[ri];
-    uint64_t* dst = w->req_bits.data() + (ri >> 6) * NP;
-    const uint64_t bit = 1ull << (ri & 63);
+    const int32_t atom = A_REQ + ri;
     if (r.type == REQ_FIELD) {
       // fields.Set{"metadata.name": node.Name}; any other key reads as "".
       const bool is_name = r.key == c->id_metadata_name && c->id_metadata_name != -1;
       for (int32_t n = 0; n < n_spot; ++n) {
         const int32_t fv = is_name ? snap->nodes[n].name : c->id_empty;
         const bool eq = fv == r.vals[0];
-        if (r.op == SR_OP_IN ? eq : !eq) dst[n] |= bit;
+        if (r.op == SR_OP_IN ? eq : !eq) set_atom(atom, n);
       }
       continue;
     }
@@ -409,17 +435,37 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
           m = !has;
           break;
       }
-      if (m) dst[n] |= bit;
+      if (m) set_atom(atom, n);
     }
   }
 
-  // ---- A / B row descriptors and per-pod arrays
-  std::unordered_map<TupleKey, int32_t, TupleHash> a_index;
-  std::unordered_map<int64_t, int32_t> b_index;
-  w->b_mem.push_back(0);
-  w->b_all.push_back(1);  // row 0: every node (zero-request pods skip the memory check)
-  w->pod_a.resize(na);
-  w->pod_b.resize(na);
+  // ---- T row descriptors.  A pod asking r in one dimension uses the row of the
+  // smallest node free value v >= r: it selects exactly the nodes with
+  // free >= r (no node value lies in [r, v)), and there are at most
+  // min(distinct requests, distinct node values) such rows.  A request above
+  // every node's free capacity maps to the empty row.
+  w->t_dim.push_back(3);
+  w->t_thr.push_back(0);  // row 0: every node
+  const int64_t kNever = INT64_MAX;  // free >= INT64_MAX never holds (free < 2^62)
+  std::vector<int64_t> node_vals[3];
+  const std::vector<int64_t>* frees[3] = {&w->free_cpu, &w->free_mem, &w->free_eph};
+  for (int d = 0; d < 3; ++d) {
+    node_vals[d].assign(frees[d]->begin(), frees[d]->begin() + n_spot);
+    std::sort(node_vals[d].begin(), node_vals[d].end());
+    node_vals[d].erase(std::unique(node_vals[d].begin(), node_vals[d].end()), node_vals[d].end());
+  }
+  std::unordered_map<int64_t, int32_t> t_index[3];
+  auto t_row = [&](int dim, int64_t req) {
+    auto lb = std::lower_bound(node_vals[dim].begin(), node_vals[dim].end(), req);
+    const int64_t thr = lb == node_vals[dim].end() ? kNever : *lb;
+    auto it = t_index[dim].emplace(thr, static_cast<int32_t>(w->t_dim.size()));
+    if (it.second) {
+      w->t_dim.push_back(dim);
+      w->t_thr.push_back(thr);
+    }
+    return it.first->second;
+  };
+  w->pod_rows.resize(static_cast<size_t>(na) * 4);
   w->pod_zero.resize(na);
   w->pod_cpu.resize(na);
   w->pod_mem.resize(na);
@@ -430,30 +476,24 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     const int32_t pod = active_pod[q];
     const int64_t rc = P.req_milli_cpu[pod], rm = P.req_memory[pod], re = P.req_ephemeral[pod];
     const int32_t zero = (rc == 0 && rm == 0 && re == 0) ? 1 : 0;
-    TupleKey k{pod_class[q], zero, zero ? 0 : rc, zero ? 0 : re};
-    auto ia = a_index.emplace(k, static_cast<int32_t>(w->a_class.size()));
-    if (ia.second) {
-      w->a_class.push_back(k.cls);
-      w->a_zero.push_back(k.zero);
-      w->a_cpu.push_back(k.cpu);
-      w->a_eph.push_back(k.eph);
-    }
-    int32_t b = 0;
-    if (!zero) {
-      auto ib = b_index.emplace(rm, static_cast<int32_t>(w->b_mem.size()));
-      if (ib.second) {
-        w->b_mem.push_back(rm);
-        w->b_all.push_back(0);
-      }
-      b = ib.first->second;
-    }
-    w->pod_a[q] = ia.first->second;
-    w->pod_b[q] = b;
+    int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
+    r[0] = pod_class[q];
+    r[1] = zero ? 0 : t_row(0, rc);
+    r[2] = zero ? 0 : t_row(1, rm);
+    r[3] = zero ? 0 : t_row(2, re);
     w->pod_zero[q] = zero;
     w->pod_cpu[q] = rc;
     w->pod_mem[q] = rm;
     w->pod_eph[q] = re;
     w->pod_ports[q] = pstat[q].ports;
+  }
+  w->pod_rec.resize(static_cast<size_t>(na) * 4);
+  for (int32_t q = 0; q < na; ++q) {
+    uint64_t* r = &w->pod_rec[static_cast<size_t>(q) * 4];
+    r[0] = static_cast<uint64_t>(w->pod_cpu[q]);
+    r[1] = static_cast<uint64_t>(w->pod_mem[q]);
+    r[2] = static_cast<uint64_t>(w->pod_eph[q]);
+    r[3] = w->pod_ports[q];
   }
 
   // ---- K2 variants by pod count (touched-node slots per wave)

@@ -77,32 +77,36 @@ struct Workload {
   int32_t n_spot = 0;   // spot nodes
   int32_t n_pad = 0;    // node arrays padded to Wp*64 entries
   int32_t Wp = 0;       // 64-bit words per bitmask row (even)
-  int32_t WR = 0;       // words per requirement bitset
-  int32_t WT = 0;       // words per taint bitset
-  // ---- spot nodes (SoA, n_pad entries)
+  // ---- spot nodes (SoA, n_pad entries): base capacity state read by K0 / K2
   std::vector<int64_t> free_cpu, free_mem, free_eph;
   std::vector<int32_t> pods_left;
-  std::vector<uint64_t> port_bits;
-  std::vector<uint64_t> req_bits;    // [WR][n_pad]
-  std::vector<uint64_t> taint_bits;  // [WT][n_pad]
-  // ---- static pod classes
+  std::vector<uint64_t> port_bits;   // base UsedPorts over the port dictionary
+  std::vector<uint64_t> node_rec;    // [n_pad][8] AoS record of the above for K2's new slots
+  // ---- atom rows [n_atoms][Wp]: node bitsets every static predicate is built from
+  //   atom 0                 len(pods)+1 <= allowed pods
+  //   atoms 1 .. R           node matches requirement r (nodeSelector pair, matchExpression, matchField)
+  //   atoms R+1 .. R+T       node carries NoSchedule/NoExecute taint t (incl. the unschedulable pseudo-taint)
+  //   atoms R+T+1 .. +Q      node's base UsedPorts holds (protocol, port) q
+  int32_t n_atoms = 0;
+  std::vector<uint64_t> atoms;
+  // ---- static pod classes as atom programs:
+  //   S[c] = AND(and atoms) & AND(~not atoms) & [OR over terms of AND(term atoms)]
   int32_t n_classes = 0;
-  std::vector<uint64_t> cls_sel;    // [n_classes][WR]
-  std::vector<uint64_t> cls_tol;    // [n_classes][WT]
-  std::vector<uint64_t> cls_port;   // [n_classes]
-  std::vector<int32_t> cls_flags;   // CLS_*
-  std::vector<int32_t> cls_term_off;  // [n_classes+1]
-  std::vector<uint64_t> term_mask;    // [terms][WR]
-  // ---- A rows: (class, zero-request, cpu threshold, ephemeral threshold)
-  std::vector<int32_t> a_class, a_zero;
-  std::vector<int64_t> a_cpu, a_eph;
-  // ---- B rows: memory threshold (row 0 = "all nodes", used by zero-request pods)
-  std::vector<int64_t> b_mem;
-  std::vector<int32_t> b_all;
+  std::vector<int32_t> cls_and_off, cls_and;    // CSR
+  std::vector<int32_t> cls_not_off, cls_not;    // CSR
+  std::vector<int32_t> cls_term_off;            // CSR classes -> terms
+  std::vector<int32_t> term_atom_off, term_atoms;  // CSR terms -> atoms
+  std::vector<int32_t> cls_flags;               // CLS_*
+  // ---- T rows: capacity thresholds.  Row 0 = every node (zero-request pods
+  // skip the resource checks); other rows: free_<dim>[n] >= thr.
+  std::vector<int32_t> t_dim;   // 0 cpu, 1 memory, 2 ephemeral, 3 all
+  std::vector<int64_t> t_thr;
   // ---- active pods, grouped by candidate, in podsForDeletion order
-  std::vector<int32_t> pod_a, pod_b, pod_zero;
+  std::vector<int32_t> pod_rows;  // [n][4]: S row (class), T rows for cpu, memory, ephemeral
+  std::vector<int32_t> pod_zero;
   std::vector<int64_t> pod_cpu, pod_mem, pod_eph;
   std::vector<uint64_t> pod_ports;
+  std::vector<uint64_t> pod_rec;  // [n][4] AoS {cpu, memory, ephemeral, ports} for K2
   std::vector<int32_t> pod_src;  // index into the caller's cand_pods array
   // ---- active candidates
   std::vector<int32_t> cand_off;     // [n_active+1] into active pods

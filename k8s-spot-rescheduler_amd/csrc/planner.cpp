@@ -37,13 +37,13 @@ struct sr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  DevBuf arena, tables, F, out_node, out_status, dmin, result;
+  DevBuf arena, tables, F, out_node, out_status, dmin;
   HostBuf h_arena, h_result, h_status, h_node;
   sr::Workload wl;
   sr::DevWorkload dw{};
   bool prepared = false;
-  bool timing = false;
-  hipEvent_t ev[5] = {};
+  int32_t timing = 0;
+  hipEvent_t ev[8] = {};
   sr_timing t{};
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -79,7 +79,7 @@ hipError_t host_reserve(HostBuf& b, size_t bytes) {
   b.p = nullptr;
   b.cap = 0;
   size_t cap = std::max<size_t>(bytes + bytes / 4, 4096);
-  hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
+  hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) b.cap = cap;
   return e;
 }
@@ -121,7 +121,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
     ctx->err = err;
     return st;
   }
-  const int32_t na = static_cast<int32_t>(w.pod_a.size());
+  const int32_t na = static_cast<int32_t>(w.pod_zero.size());
   const int32_t ncand = static_cast<int32_t>(w.cand_global.size());
   if (static_cast<uint64_t>(na) * static_cast<uint64_t>(w.Wp / 2) >= (1ull << 31)) {
     ctx->err = "pod x node bitmask exceeds 2^31 16-byte items";
@@ -129,15 +129,16 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   }
   Packer pk;
   const size_t o_fc = pk.add(w.free_cpu), o_fm = pk.add(w.free_mem), o_fe = pk.add(w.free_eph);
-  const size_t o_pl = pk.add(w.pods_left), o_pb = pk.add(w.port_bits);
-  const size_t o_rb = pk.add(w.req_bits), o_tb = pk.add(w.taint_bits);
-  const size_t o_cs = pk.add(w.cls_sel), o_ct = pk.add(w.cls_tol), o_cp = pk.add(w.cls_port);
-  const size_t o_cf = pk.add(w.cls_flags), o_cto = pk.add(w.cls_term_off), o_tm = pk.add(w.term_mask);
-  const size_t o_ac = pk.add(w.a_class), o_az = pk.add(w.a_zero), o_acp = pk.add(w.a_cpu), o_ae = pk.add(w.a_eph);
-  const size_t o_bm = pk.add(w.b_mem), o_ba = pk.add(w.b_all);
-  const size_t o_pa = pk.add(w.pod_a), o_pbb = pk.add(w.pod_b), o_pz = pk.add(w.pod_zero);
+  const size_t o_pl = pk.add(w.pods_left), o_pb = pk.add(w.port_bits), o_nr = pk.add(w.node_rec);
+  const size_t o_at = pk.add(w.atoms);
+  const size_t o_cao = pk.add(w.cls_and_off), o_ca = pk.add(w.cls_and);
+  const size_t o_cno = pk.add(w.cls_not_off), o_cn = pk.add(w.cls_not);
+  const size_t o_cto = pk.add(w.cls_term_off), o_tao = pk.add(w.term_atom_off), o_ta = pk.add(w.term_atoms);
+  const size_t o_cf = pk.add(w.cls_flags);
+  const size_t o_td = pk.add(w.t_dim), o_tt = pk.add(w.t_thr);
+  const size_t o_pr = pk.add(w.pod_rows), o_pz = pk.add(w.pod_zero);
   const size_t o_pc = pk.add(w.pod_cpu), o_pm = pk.add(w.pod_mem), o_pe = pk.add(w.pod_eph);
-  const size_t o_pp = pk.add(w.pod_ports);
+  const size_t o_pp = pk.add(w.pod_ports), o_prec = pk.add(w.pod_rec);
   const size_t o_co = pk.add(w.cand_off), o_cg = pk.add(w.cand_global);
   const size_t o_ls = pk.add(w.list_small), o_ll = pk.add(w.list_large);
   const size_t bytes = pk.size();
@@ -145,7 +146,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, host_reserve(ctx->h_arena, bytes));
   HIP_TRY(ctx, dev_reserve(ctx->arena, bytes));
-  const size_t n_rows = static_cast<size_t>(w.a_class.size() + w.b_mem.size());
+  const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
   HIP_TRY(ctx, dev_reserve(ctx->tables, n_rows * row_bytes));
   HIP_TRY(ctx, dev_reserve(ctx->F, std::max<size_t>(1, static_cast<size_t>(na)) * row_bytes));
@@ -153,8 +154,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, dev_reserve(ctx->out_status, sizeof(int32_t) * std::max(1, ncand)));
   HIP_TRY(ctx, dev_reserve(ctx->dmin, 64));
   const size_t res_bytes = sizeof(int32_t) * (4 + static_cast<size_t>(std::max(1, w.max_cand_pods)));
-  HIP_TRY(ctx, dev_reserve(ctx->result, res_bytes));
-  HIP_TRY(ctx, host_reserve(ctx->h_result, res_bytes));
+  HIP_TRY(ctx, host_reserve(ctx->h_result, res_bytes));  // mapped: K3 writes the result straight to the host
   auto t1 = std::chrono::steady_clock::now();
   pk.copy_to(static_cast<char*>(ctx->h_arena.p));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->arena.p, ctx->h_arena.p, bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -168,37 +168,34 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.n_spot = w.n_spot;
   d.n_pad = w.n_pad;
   d.Wp = w.Wp;
-  d.WR = w.WR;
-  d.WT = w.WT;
   d.free_cpu = static_cast<const int64_t*>(at(o_fc));
   d.free_mem = static_cast<const int64_t*>(at(o_fm));
   d.free_eph = static_cast<const int64_t*>(at(o_fe));
   d.pods_left = static_cast<const int32_t*>(at(o_pl));
   d.port_bits = static_cast<const uint64_t*>(at(o_pb));
-  d.req_bits = static_cast<const uint64_t*>(at(o_rb));
-  d.taint_bits = static_cast<const uint64_t*>(at(o_tb));
-  d.cls_sel = static_cast<const uint64_t*>(at(o_cs));
-  d.cls_tol = static_cast<const uint64_t*>(at(o_ct));
-  d.cls_port = static_cast<const uint64_t*>(at(o_cp));
-  d.cls_flags = static_cast<const int32_t*>(at(o_cf));
+  d.node_rec = static_cast<const uint64_t*>(at(o_nr));
+  d.n_atoms = w.n_atoms;
+  d.atoms = static_cast<const uint64_t*>(at(o_at));
+  d.cls_and_off = static_cast<const int32_t*>(at(o_cao));
+  d.cls_and = static_cast<const int32_t*>(at(o_ca));
+  d.cls_not_off = static_cast<const int32_t*>(at(o_cno));
+  d.cls_not = static_cast<const int32_t*>(at(o_cn));
   d.cls_term_off = static_cast<const int32_t*>(at(o_cto));
-  d.term_mask = static_cast<const uint64_t*>(at(o_tm));
-  d.n_a = static_cast<int32_t>(w.a_class.size());
-  d.n_b = static_cast<int32_t>(w.b_mem.size());
-  d.a_class = static_cast<const int32_t*>(at(o_ac));
-  d.a_zero = static_cast<const int32_t*>(at(o_az));
-  d.a_cpu = static_cast<const int64_t*>(at(o_acp));
-  d.a_eph = static_cast<const int64_t*>(at(o_ae));
-  d.b_mem = static_cast<const int64_t*>(at(o_bm));
-  d.b_all = static_cast<const int32_t*>(at(o_ba));
+  d.term_atom_off = static_cast<const int32_t*>(at(o_tao));
+  d.term_atoms = static_cast<const int32_t*>(at(o_ta));
+  d.cls_flags = static_cast<const int32_t*>(at(o_cf));
+  d.n_classes = w.n_classes;
+  d.n_t = static_cast<int32_t>(w.t_dim.size());
+  d.t_dim = static_cast<const int32_t*>(at(o_td));
+  d.t_thr = static_cast<const int64_t*>(at(o_tt));
   d.n_pods = na;
-  d.pod_a = static_cast<const int32_t*>(at(o_pa));
-  d.pod_b = static_cast<const int32_t*>(at(o_pbb));
+  d.pod_rows = static_cast<const int4*>(at(o_pr));
   d.pod_zero = static_cast<const int32_t*>(at(o_pz));
   d.pod_cpu = static_cast<const int64_t*>(at(o_pc));
   d.pod_mem = static_cast<const int64_t*>(at(o_pm));
   d.pod_eph = static_cast<const int64_t*>(at(o_pe));
   d.pod_ports = static_cast<const uint64_t*>(at(o_pp));
+  d.pod_rec = static_cast<const uint64_t*>(at(o_prec));
   d.n_cand = ncand;
   d.cand_off = static_cast<const int32_t*>(at(o_co));
   d.cand_global = static_cast<const int32_t*>(at(o_cg));
@@ -206,16 +203,20 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.list_large = static_cast<const int32_t*>(at(o_ll));
   d.n_small = static_cast<int32_t>(w.list_small.size());
   d.n_large = static_cast<int32_t>(w.list_large.size());
-  d.A = static_cast<uint64_t*>(ctx->tables.p);
-  d.B = d.A + w.a_class.size() * static_cast<size_t>(w.Wp);
+  d.S = static_cast<uint64_t*>(ctx->tables.p);
+  d.T = d.S + static_cast<size_t>(w.n_classes) * w.Wp;
   d.F = static_cast<uint64_t*>(ctx->F.p);
   d.out_node = static_cast<int32_t*>(ctx->out_node.p);
   d.out_status = static_cast<int32_t*>(ctx->out_status.p);
   d.d_min = static_cast<int32_t*>(ctx->dmin.p);
-  d.result = static_cast<int32_t*>(ctx->result.p);
+  void* dres = nullptr;
+  HIP_TRY(ctx, hipHostGetDevicePointer(&dres, ctx->h_result.p, 0));
+  d.result = static_cast<int32_t*>(dres);
 
   const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
-  ctx->t.bytes_feasibility = static_cast<uint64_t>(na) * row + n_rows * row + 8ull * na;
+  // K1 algorithmic bytes: the dense bitmask written once, every table row and
+  // every pod's four row indices read once.
+  ctx->t.bytes_feasibility = static_cast<uint64_t>(na) * row + n_rows * row + 16ull * na;
   uint64_t k2 = 0;
   for (int32_t q = 0; q < na; ++q) k2 += 8ull * std::min(w.Wp, 64) + 48;
   ctx->t.bytes_placement = k2 + 16ull * ncand;
@@ -225,8 +226,8 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   ctx->t.n_spot = w.n_spot;
   ctx->t.n_cand = ncand;
   ctx->t.n_words = w.Wp;
-  ctx->t.n_rows_a = d.n_a;
-  ctx->t.n_rows_b = d.n_b;
+  ctx->t.n_rows_static = d.n_classes;
+  ctx->t.n_rows_threshold = d.n_t;
   ctx->t.n_classes = w.n_classes;
   ctx->prepared = true;
   return SR_OK;
@@ -241,23 +242,27 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   const sr::DevWorkload& d = ctx->dw;
   hipStream_t s = ctx->stream;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[0], s));
+  auto mark = [&](int k, int end) -> hipError_t {
+    return (ctx->timing >> k & 1) ? hipEventRecord(ctx->ev[2 * k + end], s) : hipSuccess;
+  };
+  HIP_TRY(ctx, mark(0, 0));
   HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s));
-  if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[1], s));
+  HIP_TRY(ctx, mark(0, 1));
+  HIP_TRY(ctx, mark(1, 0));
   HIP_TRY(ctx, sr::launch_feasibility(d, s));
-  if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[2], s));
+  HIP_TRY(ctx, mark(1, 1));
+  HIP_TRY(ctx, mark(2, 0));
   HIP_TRY(ctx, sr::launch_placement(d, s));
-  if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[3], s));
+  HIP_TRY(ctx, mark(2, 1));
+  HIP_TRY(ctx, mark(3, 0));
   if (ctx->comm && use_comm) {
-    ncclResult_t r = ncclAllReduce(d.d_min, d.d_min, 2, ncclInt32, ncclMin, ctx->comm, s);
+    ncclResult_t r = ncclAllReduce(d.d_min, d.d_min, 2, ncclUint64, ncclMin, ctx->comm, s);
     if (r != ncclSuccess) {
       ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
       return SR_ERR_RCCL;
     }
   }
   HIP_TRY(ctx, sr::launch_winner(d, s));
-  const size_t res_bytes = sizeof(int32_t) * (4 + static_cast<size_t>(std::max(1, w.max_cand_pods)));
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->h_result.p, d.result, res_bytes, hipMemcpyDeviceToHost, s));
   const int32_t na = d.n_pods, ncand = d.n_cand;
   if (full) {
     HIP_TRY(ctx, host_reserve(ctx->h_status, sizeof(int32_t) * std::max(1, ncand)));
@@ -266,15 +271,16 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
       HIP_TRY(ctx, hipMemcpyAsync(ctx->h_status.p, d.out_status, sizeof(int32_t) * ncand, hipMemcpyDeviceToHost, s));
     if (na) HIP_TRY(ctx, hipMemcpyAsync(ctx->h_node.p, d.out_node, sizeof(int32_t) * na, hipMemcpyDeviceToHost, s));
   }
-  if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[4], s));
+  HIP_TRY(ctx, mark(3, 1));
   HIP_TRY(ctx, hipStreamSynchronize(s));
   if (ctx->timing) {
-    float ms[4];
-    for (int i = 0; i < 4; ++i) HIP_TRY(ctx, hipEventElapsedTime(&ms[i], ctx->ev[i], ctx->ev[i + 1]));
-    ctx->t.ms_tables += ms[0];
-    ctx->t.ms_feasibility += ms[1];
-    ctx->t.ms_placement += ms[2];
-    ctx->t.ms_winner += ms[3];
+    double* sums[4] = {&ctx->t.ms_tables, &ctx->t.ms_feasibility, &ctx->t.ms_placement, &ctx->t.ms_winner};
+    for (int k = 0; k < 4; ++k) {
+      if (!(ctx->timing >> k & 1)) continue;
+      float ms = 0;
+      HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev[2 * k], ctx->ev[2 * k + 1]));
+      *sums[k] += ms;
+    }
     ctx->t.n_runs += 1;
   }
 
@@ -335,7 +341,7 @@ void sr_destroy(sr_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
-  for (DevBuf* b : {&ctx->arena, &ctx->tables, &ctx->F, &ctx->out_node, &ctx->out_status, &ctx->dmin, &ctx->result})
+  for (DevBuf* b : {&ctx->arena, &ctx->tables, &ctx->F, &ctx->out_node, &ctx->out_status, &ctx->dmin})
     if (b->p) (void)hipFree(b->p);
   for (HostBuf* b : {&ctx->h_arena, &ctx->h_result, &ctx->h_status, &ctx->h_node})
     if (b->p) (void)hipHostFree(b->p);
@@ -421,9 +427,9 @@ sr_status sr_can_drain_node(sr_ctx* ctx, sr_snapshot* snap, const sr_cluster* cl
   return SR_OK;
 }
 
-sr_status sr_set_timing(sr_ctx* ctx, int32_t enable) {
+sr_status sr_set_timing(sr_ctx* ctx, int32_t mask) {
   if (!ctx) return SR_ERR_INVALID_ARG;
-  ctx->timing = enable != 0;
+  ctx->timing = mask & 15;
   ctx->t.n_runs = 0;
   ctx->t.ms_tables = ctx->t.ms_feasibility = ctx->t.ms_placement = ctx->t.ms_winner = 0;
   return SR_OK;

@@ -96,7 +96,7 @@ class sr_timing(ctypes.Structure):
                 ("ms_pack_host", ctypes.c_double), ("ms_upload", ctypes.c_double),
                 ("bytes_feasibility", ctypes.c_uint64), ("bytes_placement", ctypes.c_uint64),
                 ("n_pods", ctypes.c_int32), ("n_spot", ctypes.c_int32), ("n_cand", ctypes.c_int32),
-                ("n_words", ctypes.c_int32), ("n_rows_a", ctypes.c_int32), ("n_rows_b", ctypes.c_int32),
+                ("n_words", ctypes.c_int32), ("n_rows_static", ctypes.c_int32), ("n_rows_threshold", ctypes.c_int32),
                 ("n_classes", ctypes.c_int32)]
 
 

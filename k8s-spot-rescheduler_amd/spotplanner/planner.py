@@ -59,8 +59,9 @@ class PredicateChecker:
     def last_error(self) -> str:
         return self.lib.sr_last_error(self.handle).decode(errors="replace")
 
-    def set_timing(self, enable: bool):
-        self.lib.sr_set_timing(self.handle, 1 if enable else 0)
+    def set_timing(self, mask: int):
+        """Bracket kernels with HIP events: 1 K0, 2 K1, 4 K2, 8 K3 (+collective, download)."""
+        self.lib.sr_set_timing(self.handle, int(mask))
 
     def timing(self) -> capi.sr_timing:
         t = capi.sr_timing()

@@ -214,8 +214,9 @@ def tick_parity(checker, sc: SynthCluster, max_cands=None):
     lib.sr_snapshot_destroy(h)
     osnap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
     o = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
-    ip = np.ctypeslib.as_array(sc.cluster.pods.port_ip, shape=(max(1, sc.cluster.pods.port_off[sc.n_pods]),))
     po = np.ctypeslib.as_array(sc.cluster.pods.port_off, shape=(sc.n_pods + 1,))
+    n_ports = int(po[-1])
+    ip = np.ctypeslib.as_array(sc.cluster.pods.port_ip, shape=(n_ports,)) if n_ports else np.zeros(0, np.int32)
 
     def specific_ip(c):
         for q in cand_pods[cand_off[c]:cand_off[c + 1]]:
