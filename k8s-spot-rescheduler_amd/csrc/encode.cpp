@@ -20,14 +20,19 @@
 // exactly on the nodes the candidate touched (K2).  Features outside this set
 // route the whole candidate to the reference path (SR_CAND_FALLBACK).
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
 #include "host.hpp"
+#include "pool.hpp"
 
 namespace sr {
+
+double encode_phase_ms[9];  // host-side profile of the last encode (tools/encode_stats)
+
 namespace {
 
 constexpr int64_t kQuantityLimit = int64_t(1) << 62;
@@ -78,12 +83,164 @@ bool tolerates(const sr_pods& P, int32_t pod, int32_t id_empty, const TaintRec& 
   return false;
 }
 
+// lower_bound over a sorted array of distinct values, with a bucket index on
+// top: bucket b = (x - lo) >> shift holds the lower bound of its first value,
+// so a lookup is one table read plus a short scan (binary searches over
+// distinct memory requests mispredict on every level).
+class LowerBound {
+ public:
+  void build(const std::vector<int64_t>& v) {
+    v_ = &v;
+    table_.clear();
+    if (v.empty()) return;
+    lo_ = v.front();
+    const uint64_t span = static_cast<uint64_t>(v.back() - lo_) + 1;
+    shift_ = 0;
+    while ((span >> shift_) > (1u << 16)) ++shift_;
+    const size_t nb = static_cast<size_t>(span >> shift_) + 2;
+    table_.resize(nb);
+    size_t pos = 0;
+    for (size_t b = 0; b < nb; ++b) {
+      const int64_t start = lo_ + static_cast<int64_t>(static_cast<uint64_t>(b) << shift_);
+      while (pos < v.size() && v[pos] < start) ++pos;
+      table_[b] = static_cast<uint32_t>(pos);
+    }
+  }
+  size_t operator()(int64_t x) const {
+    const std::vector<int64_t>& v = *v_;
+    if (v.empty() || x <= lo_) return 0;
+    if (x > v.back()) return v.size();
+    size_t pos = table_[static_cast<size_t>(static_cast<uint64_t>(x - lo_) >> shift_)];
+    while (v[pos] < x) ++pos;  // stays inside x's bucket: v.back() >= x
+    return pos;
+  }
+
+ private:
+  const std::vector<int64_t>* v_ = nullptr;
+  std::vector<uint32_t> table_;
+  int64_t lo_ = 0;
+  int shift_ = 0;
+};
+
+// The raw static spec of a pod: nodeSelector, required node affinity,
+// tolerations, host ports.  Hash 0 is reserved for "no static constraints".
+template <class F>
+void for_each_spec_word(const sr_pods& P, int32_t pod, F&& f) {
+  const int32_t s0 = P.sel_off[pod], s1 = P.sel_off[pod + 1];
+  f(s1 - s0);
+  for (int32_t i = s0; i < s1; ++i) {
+    f(P.sel_key[i]);
+    f(P.sel_val[i]);
+  }
+  const bool aff = P.aff_required[pod] != 0;
+  f(aff ? P.term_off[pod + 1] - P.term_off[pod] : -1);
+  if (aff)
+    for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t) {
+      f(P.term_expr_off[t + 1] - P.term_expr_off[t]);
+      for (int32_t e = P.term_expr_off[t]; e < P.term_expr_off[t + 1]; ++e) {
+        f(P.expr_key[e]);
+        f(P.expr_op[e]);
+        f(P.expr_val_off[e + 1] - P.expr_val_off[e]);
+        for (int32_t v = P.expr_val_off[e]; v < P.expr_val_off[e + 1]; ++v) f(P.expr_vals[v]);
+      }
+      f(P.term_field_off[t + 1] - P.term_field_off[t]);
+      for (int32_t g = P.term_field_off[t]; g < P.term_field_off[t + 1]; ++g) {
+        f(P.field_key[g]);
+        f(P.field_op[g]);
+        f(P.field_val_off[g + 1] - P.field_val_off[g]);
+        for (int32_t v = P.field_val_off[g]; v < P.field_val_off[g + 1]; ++v) f(P.field_vals[v]);
+      }
+    }
+  const int32_t t0 = P.tol_off[pod], t1 = P.tol_off[pod + 1];
+  f(t1 - t0);
+  for (int32_t i = t0; i < t1; ++i) {
+    f(P.tol_key[i]);
+    f(P.tol_op[i]);
+    f(P.tol_val[i]);
+    f(P.tol_effect[i]);
+  }
+  for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i) {
+    f(P.port_proto[i]);
+    f(P.port_num[i]);
+  }
+}
+
+bool has_static_spec(const sr_pods& P, int32_t pod) {
+  return P.sel_off[pod] != P.sel_off[pod + 1] || P.tol_off[pod] != P.tol_off[pod + 1] ||
+         P.port_off[pod] != P.port_off[pod + 1] || P.aff_required[pod] != 0;
+}
+
+uint64_t raw_spec_hash(const sr_pods& P, int32_t pod) {
+  if (!has_static_spec(P, pod)) return 0;
+  uint64_t h = 1469598103934665603ull;
+  for_each_spec_word(P, pod, [&](int32_t x) { h = (h ^ static_cast<uint32_t>(x)) * 1099511628211ull; });
+  h ^= h >> 29;
+  return h ? h : 1;
+}
+
+bool same_spec(const sr_pods& P, int32_t a, int32_t b) {
+  static thread_local std::vector<int32_t> wa;
+  wa.clear();
+  for_each_spec_word(P, a, [&](int32_t x) { wa.push_back(x); });
+  size_t i = 0;
+  bool eq = true;
+  for_each_spec_word(P, b, [&](int32_t x) {
+    eq = eq && i < wa.size() && wa[i] == x;
+    ++i;
+  });
+  return eq && i == wa.size();
+}
+
+// hash -> spec id (open addressing), collisions resolved by comparing specs.
+class SpecTable {
+ public:
+  int32_t find_or_insert(const sr_pods& P, uint64_t h, int32_t pod, std::vector<int32_t>& spec_rep) {
+    if (slots_.empty() || (count_ + 1) * 2 > slots_.size()) grow();
+    size_t i = h & (slots_.size() - 1);
+    while (slots_[i].id >= 0) {
+      const Slot& s = slots_[i];
+      if (s.hash == h && same_spec(P, spec_rep[s.id], pod)) return s.id;
+      i = (i + 1) & (slots_.size() - 1);
+    }
+    const int32_t id = static_cast<int32_t>(spec_rep.size());
+    spec_rep.push_back(pod);
+    slots_[i] = Slot{h, id};
+    ++count_;
+    return id;
+  }
+
+ private:
+  struct Slot {
+    uint64_t hash;
+    int32_t id = -1;
+  };
+  void grow() {
+    std::vector<Slot> old;
+    old.swap(slots_);
+    slots_.assign(old.empty() ? 1024 : old.size() * 2, Slot{0, -1});
+    for (const Slot& s : old)
+      if (s.id >= 0) {
+        size_t i = s.hash & (slots_.size() - 1);
+        while (slots_[i].id >= 0) i = (i + 1) & (slots_.size() - 1);
+        slots_[i] = s;
+      }
+  }
+  std::vector<Slot> slots_;
+  size_t count_ = 0;
+};
+
 }  // namespace
 
 sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
                           Workload* w, std::string* err) {
   const sr_pods& P = c->pods;
   const int32_t nc = cands->n_cand;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](int i) {
+    auto now = std::chrono::steady_clock::now();
+    encode_phase_ms[i] = std::chrono::duration<double, std::milli>(now - t_last).count();
+    t_last = now;
+  };
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
   *w = Workload();
   w->n_input_cand = nc;
@@ -105,6 +262,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   }
   w->n_pad = w->Wp * 64;
 
+  phase(0);
   // ---- pass 1: candidate-level fallback (host-decided)
   w->status_host.assign(static_cast<size_t>(nc), STATUS_PENDING);
   auto pod_fallback = [&](int32_t pod) {
@@ -201,6 +359,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   }
   const int32_t n_taints = static_cast<int32_t>(taints.size());
 
+  phase(1);
   // ---- static part of every active pod
   RequirementDict rdict;
   struct PodStatic {
@@ -233,17 +392,39 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   std::vector<int32_t> all_taints(static_cast<size_t>(n_taints));
   for (int32_t t = 0; t < n_taints; ++t) all_taints[t] = t;
 
-  std::vector<PodStatic> pstat(static_cast<size_t>(na));
+  // Pods with byte-identical static specs (selector, affinity, tolerations,
+  // host ports) share one PodStatic: the raw spec is hashed once per pod and
+  // only first occurrences are interned.  Pods with no static constraints at
+  // all share spec 0.
+  std::vector<PodStatic> pstat(1);  // spec 0: unconstrained
+  pstat[0].untol = &all_taints;
+  std::vector<int32_t> pod_spec(static_cast<size_t>(na), 0);
+  std::vector<int32_t> spec_rep{-1};  // first pod of each spec
+  std::vector<uint64_t> spec_hash(static_cast<size_t>(na), 0);
+  parallel_for(static_cast<size_t>(na), 2048, [&](size_t lo, size_t hi) {
+    for (size_t q = lo; q < hi; ++q) spec_hash[q] = raw_spec_hash(P, active_pod[q]);
+  });
+  SpecTable table;
   for (int32_t q = 0; q < na; ++q) {
-    const int32_t pod = active_pod[q];
-    PodStatic& ps = pstat[q];
+    if (spec_hash[q] == 0) continue;  // no static constraints: spec 0
+    const int32_t id = table.find_or_insert(P, spec_hash[q], active_pod[q], spec_rep);
+    pod_spec[q] = id;
+  }
+  phase(7);
+  pstat.resize(spec_rep.size());
+  for (size_t sp = 1; sp < spec_rep.size(); ++sp) {
+    const int32_t pod = spec_rep[sp];
+    const int32_t s0 = P.sel_off[pod], s1 = P.sel_off[pod + 1];
+    const int32_t t0 = P.tol_off[pod], t1 = P.tol_off[pod + 1];
+    const bool aff = P.aff_required[pod] != 0;
+    PodStatic& ps = pstat[sp];
     // Spec.NodeSelector: labels.SelectorFromSet -> Equals requirements.
-    for (int32_t i = P.sel_off[pod]; i < P.sel_off[pod + 1]; ++i)
+    for (int32_t i = s0; i < s1; ++i)
       ps.sel.push_back(rdict.intern(Requirement{REQ_LABEL_EQ, P.sel_key[i], SR_OP_IN, {P.sel_val[i]}}));
     std::sort(ps.sel.begin(), ps.sel.end());
     ps.sel.erase(std::unique(ps.sel.begin(), ps.sel.end()), ps.sel.end());
     // Required node affinity: MatchNodeSelectorTerms.
-    if (P.aff_required[pod]) {
+    if (aff) {
       ps.flags |= CLS_AFF_REQUIRED;
       for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t) {
         const int32_t e0 = P.term_expr_off[t], e1 = P.term_expr_off[t + 1];
@@ -281,21 +462,20 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       if (ps.terms.empty()) ps.flags |= CLS_IMPOSSIBLE;
     }
     // Spec.Tolerations against the spot pool's taints.
-    const int32_t t0 = P.tol_off[pod], t1 = P.tol_off[pod + 1];
     if (t0 == t1) {
       ps.untol = &all_taints;
     } else {
-      std::string key;
+      std::string tkey;
       for (int32_t i = t0; i < t1; ++i) {
         const int32_t rec[4] = {P.tol_key[i], P.tol_op[i], P.tol_val[i], P.tol_effect[i]};
-        key += bytes_of(rec, 4);
+        tkey += bytes_of(rec, 4);
       }
-      auto it = untol_memo.find(key);
+      auto it = untol_memo.find(tkey);
       if (it == untol_memo.end()) {
         std::vector<int32_t> u;
         for (int32_t t = 0; t < n_taints; ++t)
           if (!tolerates(P, pod, c->id_empty, taints[t])) u.push_back(t);
-        it = untol_memo.emplace(std::move(key), std::move(u)).first;
+        it = untol_memo.emplace(std::move(tkey), std::move(u)).first;
       }
       ps.untol = &it->second;
     }
@@ -307,16 +487,17 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   const int32_t A_REQ = 1, A_TAINT = 1 + n_reqs, A_PORT = 1 + n_reqs + n_taints;
   w->n_atoms = A_PORT + n_ports;
 
-  // ---- intern classes (atom programs)
+  phase(2);
+  // ---- intern classes (atom programs), once per distinct spec
   std::unordered_map<std::string, int32_t> class_index;
-  std::vector<int32_t> pod_class(static_cast<size_t>(na));
+  std::vector<int32_t> spec_class(pstat.size());
   w->cls_and_off.push_back(0);
   w->cls_not_off.push_back(0);
   w->cls_term_off.push_back(0);
   w->term_atom_off.push_back(0);
   std::vector<int32_t> sig;
-  for (int32_t q = 0; q < na; ++q) {
-    const PodStatic& ps = pstat[q];
+  for (size_t sp = 0; sp < pstat.size(); ++sp) {
+    const PodStatic& ps = pstat[sp];
     sig.clear();
     sig.push_back(ps.flags);
     sig.push_back(static_cast<int32_t>(ps.sel.size()));
@@ -347,9 +528,10 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       w->cls_flags.push_back(ps.flags);
       w->n_classes++;
     }
-    pod_class[q] = ins.first->second;
+    spec_class[sp] = ins.first->second;
   }
 
+  phase(3);
   // ---- spot nodes: base capacity state and the atom rows
   const int32_t NP = w->n_pad, Wp = w->Wp;
   w->free_cpu.assign(NP, 0);
@@ -439,6 +621,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     }
   }
 
+  phase(4);
   // ---- T row descriptors.  A pod asking r in one dimension uses the row of the
   // smallest node free value v >= r: it selects exactly the nodes with
   // free >= r (no node value lies in [r, v)), and there are at most
@@ -454,53 +637,71 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     std::sort(node_vals[d].begin(), node_vals[d].end());
     node_vals[d].erase(std::unique(node_vals[d].begin(), node_vals[d].end()), node_vals[d].end());
   }
-  std::unordered_map<int64_t, int32_t> t_index[3];
-  auto t_row = [&](int dim, int64_t req) {
-    auto lb = std::lower_bound(node_vals[dim].begin(), node_vals[dim].end(), req);
-    const int64_t thr = lb == node_vals[dim].end() ? kNever : *lb;
-    auto it = t_index[dim].emplace(thr, static_cast<int32_t>(w->t_dim.size()));
-    if (it.second) {
-      w->t_dim.push_back(dim);
-      w->t_thr.push_back(thr);
-    }
-    return it.first->second;
-  };
+  std::vector<int32_t> t_index[3];  // lower-bound position -> T row (-1 none yet)
+  LowerBound lb[3];
+  for (int d = 0; d < 3; ++d) {
+    t_index[d].assign(node_vals[d].size() + 1, -1);
+    lb[d].build(node_vals[d]);
+  }
   w->pod_rows.resize(static_cast<size_t>(na) * 4);
   w->pod_zero.resize(na);
   w->pod_cpu.resize(na);
   w->pod_mem.resize(na);
   w->pod_eph.resize(na);
   w->pod_ports.resize(na);
-  w->pod_src = active_src;
-  for (int32_t q = 0; q < na; ++q) {
-    const int32_t pod = active_pod[q];
-    const int64_t rc = P.req_milli_cpu[pod], rm = P.req_memory[pod], re = P.req_ephemeral[pod];
-    const int32_t zero = (rc == 0 && rm == 0 && re == 0) ? 1 : 0;
-    int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
-    r[0] = pod_class[q];
-    r[1] = zero ? 0 : t_row(0, rc);
-    r[2] = zero ? 0 : t_row(1, rm);
-    r[3] = zero ? 0 : t_row(2, re);
-    w->pod_zero[q] = zero;
-    w->pod_cpu[q] = rc;
-    w->pod_mem[q] = rm;
-    w->pod_eph[q] = re;
-    w->pod_ports[q] = pstat[q].ports;
-  }
   w->pod_rec.resize(static_cast<size_t>(na) * 4);
+  w->pod_src = active_src;
+  // per pod (parallel): requests, records and the lower-bound position of each
+  // request among the node values (stored in pod_rows[1..3] for now)
+  parallel_for(static_cast<size_t>(na), 2048, [&](size_t lo, size_t hi) {
+    for (size_t q = lo; q < hi; ++q) {
+      const int32_t pod = active_pod[q];
+      const int64_t rc = P.req_milli_cpu[pod], rm = P.req_memory[pod], re = P.req_ephemeral[pod];
+      const int32_t zero = (rc == 0 && rm == 0 && re == 0) ? 1 : 0;
+      int32_t* r = &w->pod_rows[q * 4];
+      r[0] = spec_class[pod_spec[q]];
+      r[1] = zero ? -1 : static_cast<int32_t>(lb[0](rc));
+      r[2] = zero ? -1 : static_cast<int32_t>(lb[1](rm));
+      r[3] = zero ? -1 : static_cast<int32_t>(lb[2](re));
+      const uint64_t ports = pstat[pod_spec[q]].ports;
+      w->pod_zero[q] = zero;
+      w->pod_cpu[q] = rc;
+      w->pod_mem[q] = rm;
+      w->pod_eph[q] = re;
+      w->pod_ports[q] = ports;
+      uint64_t* rec = &w->pod_rec[q * 4];
+      rec[0] = static_cast<uint64_t>(rc);
+      rec[1] = static_cast<uint64_t>(rm);
+      rec[2] = static_cast<uint64_t>(re);
+      rec[3] = ports;
+    }
+  });
+  // positions -> T rows, numbered in first-use order (serial, deterministic)
   for (int32_t q = 0; q < na; ++q) {
-    uint64_t* r = &w->pod_rec[static_cast<size_t>(q) * 4];
-    r[0] = static_cast<uint64_t>(w->pod_cpu[q]);
-    r[1] = static_cast<uint64_t>(w->pod_mem[q]);
-    r[2] = static_cast<uint64_t>(w->pod_eph[q]);
-    r[3] = w->pod_ports[q];
+    int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
+    for (int d = 0; d < 3; ++d) {
+      if (r[1 + d] < 0) {
+        r[1 + d] = 0;  // zero-request pod: row 0 (every node)
+        continue;
+      }
+      const size_t pos = static_cast<size_t>(r[1 + d]);
+      int32_t& row = t_index[d][pos];
+      if (row < 0) {
+        row = static_cast<int32_t>(w->t_dim.size());
+        w->t_dim.push_back(d);
+        w->t_thr.push_back(pos == node_vals[d].size() ? kNever : node_vals[d][pos]);
+      }
+      r[1 + d] = row;
+    }
   }
 
+  phase(5);
   // ---- K2 variants by pod count (touched-node slots per wave)
   for (size_t i = 0; i + 1 < w->cand_off.size(); ++i) {
     const int32_t np = w->cand_off[i + 1] - w->cand_off[i];
     (np <= SLOTS_SMALL ? w->list_small : w->list_large).push_back(static_cast<int32_t>(i));
   }
+  phase(6);
   return SR_OK;
 }
 

@@ -1,0 +1,102 @@
+// pool.hpp — a small persistent worker pool for the host encoder's per-pod
+// passes.  parallel_for(n, grain, fn) runs fn(begin, end) over chunks of
+// [0, n) on up to SR_HOST_THREADS (default min(16, hardware)) threads and
+// returns when every chunk is done.  Results must not depend on the thread
+// count: callers write disjoint slots and merge serially.
+#pragma once
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace sr {
+
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool pool;
+    return pool;
+  }
+
+  void parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn) {
+    if (n == 0) return;
+    if (workers_.empty() || n <= grain) {
+      fn(0, n);
+      return;
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    job_ = &fn;
+    n_ = n;
+    grain_ = grain;
+    next_.store(0);
+    pending_ = workers_.size();
+    ++gen_;
+    cv_.notify_all();
+    lk.unlock();
+    run_chunks();
+    lk.lock();
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+
+ private:
+  Pool() {
+    unsigned hw = std::thread::hardware_concurrency();
+    unsigned want = std::min(16u, hw ? hw : 1u);
+    if (const char* e = std::getenv("SR_HOST_THREADS")) want = static_cast<unsigned>(std::max(1, std::atoi(e)));
+    for (unsigned i = 1; i < want; ++i) workers_.emplace_back([this] { loop(); });
+  }
+
+  void run_chunks() {
+    for (;;) {
+      const size_t b = next_.fetch_add(grain_);
+      if (b >= n_) return;
+      (*job_)(b, std::min(n_, b + grain_));
+    }
+  }
+
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (stop_) return;
+      lk.unlock();
+      run_chunks();
+      lk.lock();
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t, size_t)>* job_ = nullptr;
+  size_t n_ = 0, grain_ = 1;
+  std::atomic<size_t> next_{0};
+  size_t pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+inline void parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn) {
+  Pool::get().parallel_for(n, grain, fn);
+}
+
+}  // namespace sr

@@ -9,6 +9,8 @@
 #include "../k8s-spot-rescheduler_amd/csrc/host.hpp"
 #include "../k8s-spot-rescheduler_amd/csrc/synth/sr_synth.h"
 
+namespace sr { extern double encode_phase_ms[9]; }
+
 int main(int argc, char** argv) {
   sr_synth_params p{};
   p.config = argc > 1 ? atoi(argv[1]) : 3;
@@ -47,6 +49,9 @@ int main(int argc, char** argv) {
   auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   printf("config %d: nodes %d pods %d spot %d od %d cand_pods %zu\n", p.config, nn, np, ns, nod, cp.size());
   printf("new_node_map %.2f ms, snapshot %.2f ms, encode %.2f ms\n", ms(t0, t1), ms(t1, t2), ms(t3, t4) / reps);
+  printf("phases(ms): dims %.2f fallback+ports+taints %.2f pod-static %.2f classes %.2f nodes+atoms %.2f t-rows+pods %.2f lists %.2f (pod-static: keys %.2f; t-setup %.2f)\n",
+         sr::encode_phase_ms[0], sr::encode_phase_ms[1], sr::encode_phase_ms[2], sr::encode_phase_ms[3],
+         sr::encode_phase_ms[4], sr::encode_phase_ms[5], sr::encode_phase_ms[6], sr::encode_phase_ms[7], sr::encode_phase_ms[8]);
   printf("Wp %d atoms %d classes %d cls_and %zu cls_not %zu terms %zu term_atoms %zu t_rows %zu\n", w.Wp, w.n_atoms,
          w.n_classes, w.cls_and.size(), w.cls_not.size(), w.term_atom_off.size() - 1, w.term_atoms.size(), w.t_dim.size());
   int tc[4] = {0, 0, 0, 0};
