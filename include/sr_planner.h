@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SR_ABI_VERSION 1
+#define SR_ABI_VERSION 2
 
 /* ------------------------------------------------------------------ status */
 typedef int32_t sr_status;
@@ -269,23 +269,22 @@ sr_status sr_plan_run(sr_ctx *ctx, sr_plan_out *out);
 /* Kernel timing (HIP events on the planner's stream). */
 typedef struct {
   int32_t  n_runs;          /* timed runs accumulated */
-  double   ms_tables;       /* K0: class/threshold row tables */
-  double   ms_feasibility;  /* K1: dense pod x spot-node feasibility bitmask */
-  double   ms_placement;    /* K2: per-candidate first-fit placement */
-  double   ms_winner;       /* K3 + collective + download */
+  double   ms_tables;       /* K0: class / threshold row tables */
+  double   ms_placement;    /* K2: feasibility rows + per-candidate first-fit placement */
+  double   ms_winner;       /* K3 + collective (mapped-memory result) */
   double   ms_pack_host;    /* last sr_plan_prepare host encoding */
   double   ms_upload;       /* last sr_plan_prepare upload */
-  uint64_t bytes_feasibility; /* algorithmic bytes per K1 launch */
-  uint64_t bytes_placement;   /* algorithmic bytes per K2 launch */
+  uint64_t bytes_tables;    /* algorithmic bytes per K0 launch */
+  uint64_t bytes_placement; /* algorithmic bytes per K2 launch: exact after a run with status or
+                               node_of_pod outputs, an upper bound (every pod processed) before */
   int32_t  n_pods, n_spot, n_cand, n_words;
   int32_t  n_rows_static, n_rows_threshold, n_classes;
 } sr_timing;
 /* mask: which kernels sr_plan_run brackets with HIP events (resets the sums):
- * 1 = K0, 2 = K1, 4 = K2, 8 = K3 + collective + download; 0 = no events. */
+ * 1 = K0, 2 = K2, 4 = K3 + collective; 0 = no events. */
 #define SR_TIME_TABLES      1
-#define SR_TIME_FEASIBILITY 2
-#define SR_TIME_PLACEMENT   4
-#define SR_TIME_WINNER      8
+#define SR_TIME_PLACEMENT   2
+#define SR_TIME_WINNER      4
 sr_status sr_set_timing(sr_ctx *ctx, int32_t mask);
 sr_status sr_get_timing(const sr_ctx *ctx, sr_timing *out);
 

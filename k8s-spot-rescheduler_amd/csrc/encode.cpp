@@ -15,7 +15,7 @@
 //
 // where "class" interns everything static about a pod.  S and T are bitmask
 // rows over spot nodes in NodeInfoArray order, built on the GPU (K0); the dense
-// pod x node bitmask is their AND (K1).  Everything that changes while a
+// pod's feasibility row is their AND, formed inside K2.  Everything that changes while a
 // candidate's pods are placed (capacity, pod count, host ports) is rechecked
 // exactly on the nodes the candidate touched (K2).  Features outside this set
 // route the whole candidate to the reference path (SR_CAND_FALLBACK).
@@ -287,7 +287,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       w->status_host[i] = SR_CAND_EMPTY;
       continue;
     }
-    bool fb = snap->anti_total > 0 || (e - b) > SLOTS_LARGE;
+    bool fb = snap->anti_total > 0 || (e - b) > MAX_CAND_PODS;
     for (int32_t j = b; j < e && !fb; ++j) {
       const int32_t pod = cands->cand_pods[j];
       if (pod < 0 || pod >= P.n) {
@@ -644,12 +644,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     lb[d].build(node_vals[d]);
   }
   w->pod_rows.resize(static_cast<size_t>(na) * 4);
-  w->pod_zero.resize(na);
-  w->pod_cpu.resize(na);
-  w->pod_mem.resize(na);
-  w->pod_eph.resize(na);
-  w->pod_ports.resize(na);
-  w->pod_rec.resize(static_cast<size_t>(na) * 4);
+  w->pod_rec.assign(static_cast<size_t>(na + 128) * 6, 0);  // padded: K2 stages 64-pod halves
   w->pod_src = active_src;
   // per pod (parallel): requests, records and the lower-bound position of each
   // request among the node values (stored in pod_rows[1..3] for now)
@@ -657,23 +652,17 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     for (size_t q = lo; q < hi; ++q) {
       const int32_t pod = active_pod[q];
       const int64_t rc = P.req_milli_cpu[pod], rm = P.req_memory[pod], re = P.req_ephemeral[pod];
-      const int32_t zero = (rc == 0 && rm == 0 && re == 0) ? 1 : 0;
+      const bool zero = rc == 0 && rm == 0 && re == 0;
       int32_t* r = &w->pod_rows[q * 4];
       r[0] = spec_class[pod_spec[q]];
       r[1] = zero ? -1 : static_cast<int32_t>(lb[0](rc));
       r[2] = zero ? -1 : static_cast<int32_t>(lb[1](rm));
       r[3] = zero ? -1 : static_cast<int32_t>(lb[2](re));
-      const uint64_t ports = pstat[pod_spec[q]].ports;
-      w->pod_zero[q] = zero;
-      w->pod_cpu[q] = rc;
-      w->pod_mem[q] = rm;
-      w->pod_eph[q] = re;
-      w->pod_ports[q] = ports;
-      uint64_t* rec = &w->pod_rec[q * 4];
+      uint64_t* rec = &w->pod_rec[q * 6];
       rec[0] = static_cast<uint64_t>(rc);
       rec[1] = static_cast<uint64_t>(rm);
       rec[2] = static_cast<uint64_t>(re);
-      rec[3] = ports;
+      rec[3] = pstat[pod_spec[q]].ports;
     }
   });
   // positions -> T rows, numbered in first-use order (serial, deterministic)
@@ -693,13 +682,36 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       }
       r[1 + d] = row;
     }
+    uint64_t* rec = &w->pod_rec[static_cast<size_t>(q) * 6];
+    auto off = [&](int32_t table_row) { return static_cast<uint64_t>(table_row) * static_cast<uint64_t>(w->Wp); };
+    rec[4] = off(r[0]) | off(w->n_classes + r[1]) << 32;
+    rec[5] = off(w->n_classes + r[2]) | off(w->n_classes + r[3]) << 32;
+  }
+  if ((static_cast<uint64_t>(w->n_classes) + w->t_dim.size()) * static_cast<uint64_t>(w->Wp) >= (1ull << 32)) {
+    *err = "bitmask tables exceed 2^32 words";
+    return SR_ERR_CAPACITY;
   }
 
   phase(5);
-  // ---- K2 variants by pod count (touched-node slots per wave)
-  for (size_t i = 0; i + 1 < w->cand_off.size(); ++i) {
-    const int32_t np = w->cand_off[i + 1] - w->cand_off[i];
-    (np <= SLOTS_SMALL ? w->list_small : w->list_large).push_back(static_cast<int32_t>(i));
+  // ---- K2 work list: longest candidates first (counting sort, stable)
+  {
+    const size_t nc = w->cand_off.size() - 1;
+    std::vector<int32_t> cnt(MAX_CAND_PODS + 2, 0);
+    for (size_t i = 0; i < nc; ++i) ++cnt[MAX_CAND_PODS - (w->cand_off[i + 1] - w->cand_off[i])];
+    for (int32_t v = 0, acc = 0; v <= MAX_CAND_PODS + 1; ++v) {
+      const int32_t c = cnt[v];
+      cnt[v] = acc;
+      acc += c;
+    }
+    w->list.assign(nc * 4, 0);
+    for (size_t i = 0; i < nc; ++i) {
+      const int32_t b = w->cand_off[i], e = w->cand_off[i + 1];
+      int32_t* l = &w->list[static_cast<size_t>(cnt[MAX_CAND_PODS - (e - b)]++) * 4];
+      l[0] = static_cast<int32_t>(i);
+      l[1] = b;
+      l[2] = e;
+      l[3] = w->cand_global[i];
+    }
   }
   phase(6);
   return SR_OK;

@@ -103,16 +103,13 @@ struct Workload {
   std::vector<int64_t> t_thr;
   // ---- active pods, grouped by candidate, in podsForDeletion order
   std::vector<int32_t> pod_rows;  // [n][4]: S row (class), T rows for cpu, memory, ephemeral
-  std::vector<int32_t> pod_zero;
-  std::vector<int64_t> pod_cpu, pod_mem, pod_eph;
-  std::vector<uint64_t> pod_ports;
-  std::vector<uint64_t> pod_rec;  // [n][4] AoS {cpu, memory, ephemeral, ports} for K2
+  std::vector<uint64_t> pod_rec;  // [n + 128][6] AoS {cpu, memory, ephemeral, ports, rows} for K2
   std::vector<int32_t> pod_src;  // index into the caller's cand_pods array
   // ---- active candidates
   std::vector<int32_t> cand_off;     // [n_active+1] into active pods
   std::vector<int32_t> cand_global;  // global candidate index
   std::vector<int32_t> cand_src;     // index in the caller's candidate list
-  std::vector<int32_t> list_small, list_large;  // active candidates per K2 slot variant
+  std::vector<int32_t> list;  // [n][4] K2 work list {candidate, first pod, end pod, global}, longest first
   int32_t max_cand_pods = 0;
   // ---- host-decided outcomes for every input candidate
   std::vector<int32_t> status_host;  // SR_CAND_EMPTY / SR_CAND_FALLBACK / PENDING
@@ -123,8 +120,7 @@ struct Workload {
 };
 
 constexpr int32_t STATUS_PENDING = -100;
-constexpr int32_t SLOTS_SMALL = 128;   // touched spot nodes per candidate, small variant
-constexpr int32_t SLOTS_LARGE = 512;   // large variant
+constexpr int32_t MAX_CAND_PODS = 512;  // pods per candidate on the device (K2 kMaxPods)
 constexpr int32_t MAX_WORDS = 64 * 32; // spot nodes <= 131072
 
 // Builds the workload; returns SR_OK or an error with *err filled.

@@ -3,14 +3,12 @@
 //  K0 tables      S (static class) and T (capacity threshold) bitmask rows over
 //                 spot nodes: one lane per node, one 64-bit ballot per word
 //                 (predicate factorisation: encode.cpp).
-//  K1 feasibility dense pod x spot-node bitmask F = S & T & T & T per pod: the
-//                 (pod, node) predicate of every pair against the base snapshot,
-//                 16 B per lane, HBM-write bound.
 //  K2 placement   canDrainNode for every candidate at once (rescheduler.go:357-370):
-//                 one wave per candidate, pods in order, first fit in
-//                 NodeInfoArray order = lowest set bit of F[p] among untouched
-//                 nodes (ballot + ctz), touched nodes rechecked against the
-//                 candidate's private capacity copy held in registers.
+//                 one wave per candidate, pods in order; the pod's feasibility
+//                 row F = S & T & T & T is formed 64 words at a time from the
+//                 tables and first fit in NodeInfoArray order = lowest set bit
+//                 among untouched nodes (ballot + ctz), touched nodes rechecked
+//                 against the candidate's private capacity copy in registers.
 //  K3 winner      first drainable candidate's pod -> node mapping.
 //
 // No MFMA: there is no dense contraction anywhere on this path.
@@ -21,8 +19,6 @@
 
 namespace sr {
 namespace {
-
-constexpr int kWave = 64;
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v & 0xffffffffu), lane));
@@ -110,112 +106,93 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
   if (lane < nr) w.T[static_cast<size_t>(r0 + lane) * w.Wp + word] = acc;
 }
 
-// K1: F[p] = S[s] & T[cpu] & T[mem] & T[eph]; one item = 16 B of one row, four
-// independent items in flight per thread.
-__device__ __forceinline__ ulonglong2 and4(ulonglong2 a, ulonglong2 b, ulonglong2 c, ulonglong2 d) {
-  ulonglong2 f;
-  f.x = a.x & b.x & c.x & d.x;
-  f.y = a.y & b.y & c.y & d.y;
-  return f;
-}
-
-__global__ __launch_bounds__(256) void k1_feasibility(const ulonglong2* __restrict__ S, const ulonglong2* __restrict__ T,
-                                                      const int4* __restrict__ rows, ulonglong2* __restrict__ F,
-                                                      uint32_t n_pods, uint32_t half) {
-  const uint32_t total = n_pods * half;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  constexpr int U = 4;
-  for (; i + (U - 1) * stride < total; i += U * stride) {
-    ulonglong2 a[U], b[U], c[U], d[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t k = i + u * stride;
-      const uint32_t p = k / half;
-      const uint32_t j = k - p * half;
-      const int4 r = rows[p];
-      a[u] = S[static_cast<size_t>(r.x) * half + j];
-      b[u] = T[static_cast<size_t>(r.y) * half + j];
-      c[u] = T[static_cast<size_t>(r.z) * half + j];
-      d[u] = T[static_cast<size_t>(r.w) * half + j];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) F[i + u * stride] = and4(a[u], b[u], c[u], d[u]);
-  }
-  for (; i < total; i += stride) {
-    const uint32_t p = i / half;
-    const uint32_t j = i - p * half;
-    const int4 r = rows[p];
-    F[i] = and4(S[static_cast<size_t>(r.x) * half + j], T[static_cast<size_t>(r.y) * half + j],
-                T[static_cast<size_t>(r.z) * half + j], T[static_cast<size_t>(r.w) * half + j]);
-  }
-}
-
-// K2: one wave per candidate.  SPL touched-node slots per lane (64*SPL per
-// candidate), CH*64 bitmask words per row held as a register-resident
-// touched mask (lane l owns words ch*64 + l).
+// K2: one wave per candidate.  Touched-node slots live in registers, one per
+// lane (64; a candidate touching more distinct nodes is rerun with 512), and
+// CH*64 bitmask words per row are held as a register-resident touched mask
+// (lane l owns words ch*64 + l).
+//
+// The feasibility of pod p against the base snapshot is evaluated here, 64
+// words (4096 spot nodes) at a time: F = S[class] & T[cpu] & T[mem] & T[eph]
+// (encode.cpp).  The table rows are small and L2-resident, so no dense P x N
+// bitmask is ever written: a pod's chunk costs four 512-B row reads.
 //
 // It is one dependent chain per candidate, so it is built for latency: every
 // load inside the pod loop is an LDS-DMA (global_load_lds) whose completion
 // is waited for by hand with counted `s_waitcnt vmcnt(N)`:
-//   - chunk 0 of rows p+1..p+3 is always in flight (4-slot LDS ring);
+//   - chunk 0 of the four rows of pods p+1..p+3 is always in flight (4-slot
+//     LDS ring, 2 DMAs per pod);
 //   - the base record of the next pod's first untouched feasible node is
-//     fetched one pod ahead (speculative; used when the pod opens a new slot);
-//   - the candidate's pod records are staged once before the loop.
-// DMA issue order per step k (fixed): ... spec(k+1), row(k+4).  At the end of
-// step k-1, row k has >= 3 younger DMAs (spec(k-1)?, row(k+1), spec(k), row(k+2)
-// for k >= 2; row(k+1), spec(k)... for k = 1) -> vmcnt(3); spec(k) has exactly
-// one younger (row(k+3)) when step k consumes it -> vmcnt(1).  Extra DMAs
-// (rare paths) are always followed by vmcnt(0), which never weakens a count.
+//     fetched one pod ahead (speculative; used when the pod opens a new slot
+//     on a node >= kNodeCache; nodes below that come from an LDS cache);
+//   - the candidate's pod records are staged before the loop (128-pod window,
+//     restaged per 64 pods for larger candidates).
+// DMA issue order per step k (fixed): ... spec(k+1), rows(k+4) x2.  At the end
+// of step k, rows(k+1) has at most 6 younger DMAs (5 at k = 0) and every wait
+// below is for "all but the N youngest" -> vmcnt(5) is safe for every k;
+// spec(k) has exactly the two rows(k+3) DMAs younger when step k consumes it
+// -> vmcnt(2).  Rare-path DMAs are always followed by vmcnt(0), which never
+// weakens a later count.
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef __attribute__((address_space(1))) void* gbl_vp;
 #define SR_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
+constexpr int kPodWin = 128;    // pod records staged per wave: two 64-pod halves
+constexpr int kRecU64 = 6;      // {cpu, memory, ephemeral, ports, S | T cpu row offset, T mem | T eph row offset}
+constexpr int kNodeCache = 16;  // base records of spot nodes [0, 16) kept in LDS
+constexpr int kMaxPods = 512;   // pods per candidate on the device (encode.cpp: more -> fallback)
+
 struct K2Lds {
-  uint64_t row[4][64];  // row ring: chunk 0 of rows p..p+3
-  uint64_t chunk[64];   // rare: chunks > 0
-  uint64_t spec[8];     // speculative node record
-  uint64_t rec[8];      // rare: reloaded node record
+  uint64_t ring[4][256];            // chunk 0 of {S, T cpu, T mem, T eph} rows of pods k..k+3
+  uint64_t chunk[256];              // rare: chunk > 0 of the current pod's rows
+  uint64_t pods[kPodWin][kRecU64];  // pod record window
+  uint64_t cache[kNodeCache][8];    // base node records
+  uint64_t spec[8];                 // speculative node record
+  uint64_t rec[8];                  // rare: reloaded node record
+  int32_t omap[kMaxPods];           // spot position chosen for each pod
 };
 
-template <int SPL, int CH>
-__global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int32_t* __restrict__ list, int n_list) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
+struct K2Stats {
+  uint32_t n_spec_miss = 0, n_min = 0, n_far = 0;
+  uint64_t cyc_a = 0, cyc_b = 0, cyc_c = 0, cyc_d = 0;
+};
+
+// One candidate's canDrainNode with 64 * SPL touched-node slots.  Returns the
+// number of pods placed (np = all; status = failing pod or -1), or -1 when the
+// candidate touches more distinct nodes than it has slots (the caller reruns
+// it with more).
+template <int SPL, int CH, bool PROF>
+__device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int p0, const int np, int& status,
+                                      K2Stats& st) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wave);
-  if (li >= n_list) return;
-  const int ci = __builtin_amdgcn_readfirstlane(list[li]);
-  const int p0 = __builtin_amdgcn_readfirstlane(w.cand_off[ci]);
-  const int p1 = __builtin_amdgcn_readfirstlane(w.cand_off[ci + 1]);
-  const int np = p1 - p0;
   const int Wp = w.Wp;
-  // per-wave LDS: pod records [64*SPL][4] then the K2Lds block
-  uint64_t* pods = k2_lds + static_cast<size_t>(wave) * (64 * SPL * 4 + sizeof(K2Lds) / 8);
-  K2Lds& L = *reinterpret_cast<K2Lds*>(pods + 64 * SPL * 4);
+  const uint64_t* __restrict__ tab = w.S;  // S rows then T rows: pod records hold word offsets
 
   // DMA helpers: 16 B per lane, LDS destination = base + 16 * lane
-  auto dma_row = [&](uint64_t* dst, int p, int base) {  // 64 words of row p from word `base`
-    if (lane < 32) {
-      const int wi = min(base + 2 * lane, Wp - 2);
-      const uint64_t* src = w.F + static_cast<size_t>(min(p, p1 - 1)) * Wp + wi;
-      __builtin_amdgcn_global_load_lds((gbl_vp)src, (lds_vp)dst, 16, 0, 0);
-    }
+  auto dma = [&](const uint64_t* src, uint64_t* dst) {
+    __builtin_amdgcn_global_load_lds((gbl_vp)src, (lds_vp)dst, 16, 0, 0);
+  };
+  // 64 words from word `base` of the four rows at offsets {r01.lo, r01.hi, r23.lo, r23.hi} -> dst[4][64]
+  auto dma_rows = [&](uint64_t* dst, uint64_t r01, uint64_t r23, int base) {
+    const uint32_t wi = static_cast<uint32_t>(min(base + 2 * (lane & 31), Wp - 2));
+    const uint32_t ra = lane < 32 ? static_cast<uint32_t>(r01) : static_cast<uint32_t>(r01 >> 32);
+    const uint32_t rb = lane < 32 ? static_cast<uint32_t>(r23) : static_cast<uint32_t>(r23 >> 32);
+    dma(tab + (static_cast<uint64_t>(ra) + wi), dst);
+    dma(tab + (static_cast<uint64_t>(rb) + wi), dst + 128);
+  };
+  auto dma_rows_of = [&](uint64_t* dst, int q, int base) {
+    const uint64_t* pr = L.pods[q & (kPodWin - 1)];
+    dma_rows(dst, pr[4], pr[5], base);
   };
   auto dma_rec = [&](uint64_t* dst, int node) {
-    if (lane < 4) {
-      const uint64_t* src = w.node_rec + static_cast<size_t>(node == INT_MAX ? 0 : node) * 8 + 2 * lane;
-      __builtin_amdgcn_global_load_lds((gbl_vp)src, (lds_vp)dst, 16, 0, 0);
-    }
+    if (lane < 4) dma(w.node_rec + static_cast<size_t>(node == INT_MAX ? 0 : node) * 8 + 2 * lane, dst);
   };
-
-  // pod records (AoS, 32 B per pod): 2 KB per 64 pods = 2 DMAs of 1 KB
+  // records of pods [64 m, 64 m + 64) into window half m & 1 (pod_rec is padded)
+  auto dma_pods = [&](int m) {
+    const uint64_t* src = w.pod_rec + static_cast<size_t>(p0 + 64 * m) * kRecU64 + 2 * lane;
+    uint64_t* dst = L.pods[64 * (m & 1)];
 #pragma unroll
-  for (int b = 0; b < 2 * SPL; ++b)
-    if (b * 32 < np) {
-      const uint64_t* src = w.pod_rec + static_cast<size_t>(p0) * 4 + static_cast<size_t>(b) * 128 + 2 * lane;
-      __builtin_amdgcn_global_load_lds((gbl_vp)src, (lds_vp)(pods + b * 128), 16, 0, 0);
-    }
+    for (int j = 0; j < 3; ++j) dma(src + 128 * j, dst + 128 * j);
+  };
 
   uint64_t touched[CH];
 #pragma unroll
@@ -224,92 +201,133 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int32_t* __
   int64_t scpu[SPL], smem[SPL], seph[SPL];
   int sleft[SPL];
   uint64_t sport[SPL];
-  int bnode[SPL];
 #pragma unroll
   for (int s = 0; s < SPL; ++s) {
     snode[s] = INT_MAX;
     scpu[s] = smem[s] = seph[s] = 0;
     sleft[s] = 0;
     sport[s] = 0;
-    bnode[s] = -1;
   }
   int nslots = 0;
-  int status = -1;
+  uint64_t cyc_t = 0;
+  auto cyc = [&]() -> uint64_t { return PROF ? __builtin_amdgcn_s_memtime() : 0ull; };
   const uint64_t lane_mask = lane < Wp ? ~0ull : 0ull;
 
-  auto first_clean0 = [&](uint64_t word) -> int {
-    const uint64_t clean0 = word & ~touched[0];
+  // State of the next pod, gathered in one batch of LDS reads once its rows
+  // have landed: its chunk-0 feasibility word, first untouched feasible node,
+  // request, and the S-row bit of every touched node.
+  uint64_t word_next = 0;
+  int cnode0 = INT_MAX;
+  int64_t nrc = 0, nrm = 0, nre = 0;
+  uint64_t npm = 0;
+  bool sbit[SPL];
+  auto gather_next = [&](int kn) {
+    const uint64_t* img = L.ring[kn & 3];
+    const uint64_t* pr = L.pods[kn & (kPodWin - 1)];
+    uint64_t sw[SPL];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) sw[s] = img[snode[s] < 4096 ? snode[s] >> 6 : 0];
+    const uint64_t a = img[lane] & img[64 + lane] & img[128 + lane] & img[192 + lane];
+    nrc = static_cast<int64_t>(pr[0]);
+    nrm = static_cast<int64_t>(pr[1]);
+    nre = static_cast<int64_t>(pr[2]);
+    npm = pr[3];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) sbit[s] = (sw[s] >> (snode[s] & 63)) & 1ull;
+    word_next = a & lane_mask;
+    const uint64_t clean0 = word_next & ~touched[0];
     const uint64_t mc0 = __ballot(clean0 != 0);
-    if (!mc0) return INT_MAX;
-    const int L0 = __builtin_ctzll(mc0);
-    return L0 * 64 + __builtin_ctzll(readlane64(clean0, L0));
+    cnode0 = INT_MAX;
+    if (mc0) {
+      const int L0 = __builtin_ctzll(mc0);
+      cnode0 = L0 * 64 + __builtin_ctzll(readlane64(clean0, L0));
+    }
   };
 
-  // prologue: rows 0..2, then (row 0 landed) spec(0), row 3
-  dma_row(L.row[0], p0, 0);
-  dma_row(L.row[1], p0 + 1, 0);
-  dma_row(L.row[2], p0 + 2, 0);
-  SR_WAIT_VM(2);
-  uint64_t word_next = L.row[0][lane] & lane_mask;
-  int cnode0 = first_clean0(word_next);
+  // prologue: node cache + pod window, then rows 0..2, (row 0 landed) spec(0), row 3
+  dma(w.node_rec + 2 * lane, L.cache[0]);
+  dma_pods(0);
+  if (np > 64) dma_pods(1);
+  SR_WAIT_VM(0);
+  dma_rows_of(L.ring[0], 0, 0);
+  dma_rows_of(L.ring[1], min(1, np - 1), 0);
+  dma_rows_of(L.ring[2], min(2, np - 1), 0);
+  SR_WAIT_VM(4);
+  gather_next(0);
   dma_rec(L.spec, cnode0);
-  dma_row(L.row[3], p0 + 3, 0);
+  dma_rows_of(L.ring[3], min(3, np - 1), 0);
 
-  for (int k = 0; k < np; ++k) {
-    const int p = p0 + k;
-    const uint64_t word0 = word_next;
-    const uint64_t* prec = pods + static_cast<size_t>(k) * 4;
-    const int64_t rc = static_cast<int64_t>(prec[0]), rm = static_cast<int64_t>(prec[1]),
-                  re = static_cast<int64_t>(prec[2]);
-    const uint64_t pm = prec[3];
+  status = -1;
+  int k = 0;
+  for (; k < np; ++k) {
+    if (PROF) cyc_t = cyc();
+    const int64_t rc = nrc, rm = nrm, re = nre;
+    const uint64_t pm = npm;
     const bool zero = (rc | rm | re) == 0;  // fitsRequest skips the resource checks
-
-    int ans = INT_MAX;
+    // Chunk 0 (spot nodes [0, 4096)): touched nodes below the first untouched
+    // feasible one, rechecked branch-free: class bit from the S row, capacity /
+    // pod count / host ports from the candidate's own state (which implies the
+    // base T rows, base pod count and base ports).
+    int ans;
+    {
+      const int hi = min(cnode0, 4096);
+      int best = INT_MAX;
 #pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
+      for (int s = 0; s < SPL; ++s) {
+        const int nd = snode[s];
+        const bool fit = zero | ((rc <= scpu[s]) & (rm <= smem[s]) & (re <= seph[s]));  // NodeResourcesFit
+        const bool ok = (nd < hi) & sbit[s] & (sleft[s] >= 1) & ((sport[s] & pm) == 0) & fit;
+        best = ok ? min(best, nd) : best;
+      }
+      const uint64_t hb = __ballot(best != INT_MAX);
+      int dnode = INT_MAX;
+      if (hb) {
+        dnode = (hb & (hb - 1)) ? wave_min(best) : __builtin_amdgcn_readlane(best, __builtin_ctzll(hb));
+        if (PROF && (hb & (hb - 1))) ++st.n_min;
+      }
+      ans = min(cnode0, dnode);
+    }
+    // rare: the pod's first 4096 spot nodes hold no answer
+#pragma unroll
+    for (int ch = 1; ch < CH; ++ch) {
       const int base = ch * 64;
       if (ans != INT_MAX || base >= Wp) continue;  // wave-uniform; keeps the loop unrollable
-      uint64_t word = word0;
-      int cnode = cnode0;
-      if (ch > 0) {  // rare: the pod's first 4096 spot nodes hold no answer
-        dma_row(L.chunk, p, base);
-        SR_WAIT_VM(0);
-        word = (base + lane < Wp) ? L.chunk[lane] : 0;
-        const uint64_t clean = word & ~touched[ch];
-        const uint64_t mc = __ballot(clean != 0);
-        cnode = INT_MAX;
-        if (mc) {
-          const int L0 = __builtin_ctzll(mc);
-          cnode = (base + L0) * 64 + __builtin_ctzll(readlane64(clean, L0));
-        }
+      if (PROF) ++st.n_far;
+      dma_rows_of(L.chunk, k, base);
+      SR_WAIT_VM(0);
+      const uint64_t* img = L.chunk;
+      const uint64_t clean = (img[lane] & img[64 + lane] & img[128 + lane] & img[192 + lane]) &
+                             ((base + lane < Wp) ? ~touched[ch] : 0ull);
+      const uint64_t mc = __ballot(clean != 0);
+      int cnode = INT_MAX;
+      if (mc) {
+        const int L0 = __builtin_ctzll(mc);
+        cnode = (base + L0) * 64 + __builtin_ctzll(readlane64(clean, L0));
       }
-      // touched base-feasible nodes below it: recheck with the candidate's own state
-      int dnode = INT_MAX;
-      if (__ballot((word & touched[ch]) != 0)) {
-        const int lo = base * 64;
-        const int hi = min(cnode, lo + 64 * 64);
-        int best = INT_MAX;
+      const int lo = base * 64;
+      const int hi = min(cnode, lo + 64 * 64);
+      int best = INT_MAX;
 #pragma unroll
-        for (int s = 0; s < SPL; ++s) {
-          const int nd = snode[s];
-          const bool in = nd >= lo && nd < hi;
-          const uint64_t ws = __shfl(word, in ? (nd >> 6) - base : lane, kWave);
-          bool ok = in && ((ws >> (nd & 63)) & 1ull);
-          ok = ok && sleft[s] >= 1 && (sport[s] & pm) == 0;                 // pod count, host ports
-          ok = ok && (zero || (rc <= scpu[s] && rm <= smem[s] && re <= seph[s]));  // NodeResourcesFit
-          if (ok) best = min(best, nd);
-        }
-        dnode = wave_min(best);
+      for (int s = 0; s < SPL; ++s) {
+        const int nd = snode[s];
+        const bool in = (nd >= lo) & (nd < hi);
+        const uint64_t sw = img[in ? (nd >> 6) - base : 0];
+        const bool fit = zero | ((rc <= scpu[s]) & (rm <= smem[s]) & (re <= seph[s]));
+        const bool ok = in & (((sw >> (nd & 63)) & 1ull) != 0) & (sleft[s] >= 1) & ((sport[s] & pm) == 0) & fit;
+        best = ok ? min(best, nd) : best;
       }
-      ans = min(cnode, dnode);
+      ans = min(cnode, wave_min(best));
+    }
+    if (PROF) {
+      const uint64_t t = cyc();
+      st.cyc_a += t - cyc_t;
+      cyc_t = t;
     }
     if (ans == INT_MAX) {  // "pod %s can't be rescheduled on any existing spot node"
       status = k;
       break;
     }
-#pragma unroll
-    for (int b = 0; b < SPL; ++b)
-      if (b == (k >> 6) && lane == (k & 63)) bnode[b] = ans;
+    if (lane == 0) L.omap[k] = ans;
 
     // ClusterSnapshot.AddPod(pod, node) on the candidate's private copy
     bool hit = false;
@@ -326,9 +344,18 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int32_t* __
     }
     if (!__any(hit)) {
       const int ns = nslots++;
-      const uint64_t* rec = L.spec;
-      SR_WAIT_VM(1);  // spec(k): only row(k+3) is younger
-      if (ans != cnode0) {  // rare: not the speculated node
+      if (ns >= 64 * SPL) {  // slots exhausted: rerun with more
+        SR_WAIT_VM(0);
+        return -1;
+      }
+      const uint64_t* rec;
+      if (ans < kNodeCache) {
+        rec = L.cache[ans];
+      } else if (ans == cnode0) {
+        SR_WAIT_VM(2);  // spec(k): only rows(k+3) are younger
+        rec = L.spec;
+      } else {  // rare: not the speculated node
+        if (PROF) ++st.n_spec_miss;
         dma_rec(L.rec, ans);
         SR_WAIT_VM(0);
         rec = L.rec;
@@ -337,17 +364,15 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int32_t* __
                     fe = static_cast<int64_t>(rec[2]);
       const uint64_t pb = rec[3];
       const int pl = static_cast<int>(static_cast<int64_t>(rec[4]));
-      if (lane == (ns & 63)) {
 #pragma unroll
-        for (int s = 0; s < SPL; ++s) {
-          if (s == (ns >> 6)) {
-            snode[s] = ans;
-            scpu[s] = fc - rc;
-            smem[s] = fm - rm;
-            seph[s] = fe - re;
-            sleft[s] = pl - 1;
-            sport[s] = pb | pm;
-          }
+      for (int s = 0; s < SPL; ++s) {
+        if ((s == (ns >> 6)) & (lane == (ns & 63))) {
+          snode[s] = ans;
+          scpu[s] = fc - rc;
+          smem[s] = fm - rm;
+          seph[s] = fe - re;
+          sleft[s] = pl - 1;
+          sport[s] = pb | pm;
         }
       }
       const int tw = ans >> 6;
@@ -355,28 +380,82 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int32_t* __
       for (int ch = 0; ch < CH; ++ch)
         if (tw == ch * 64 + lane) touched[ch] |= 1ull << (ans & 63);
     }
-    // next pod: its row (>= 3 younger DMAs), its speculative record, row k + 4
+    if (PROF) {
+      const uint64_t t = cyc();
+      st.cyc_b += t - cyc_t;
+      cyc_t = t;
+    }
+    // next pod: its rows (<= 6 younger DMAs), its state, its speculative
+    // record, rows of pod k + 4
     if (k + 1 < np) {
-      SR_WAIT_VM(3);
-      word_next = L.row[(k + 1) & 3][lane] & lane_mask;
-      cnode0 = first_clean0(word_next);
+      const int q = min(k + 4, np - 1);
+      const bool restage = q == k + 4 && (q & 63) == 0 && q >= kPodWin;
+      if (restage) dma_pods(q >> 6);  // window: records [q, q + 64) replace [q - 128, q - 64)
+      SR_WAIT_VM(5);
+      if (restage) SR_WAIT_VM(0);
+      if (PROF) {
+        const uint64_t t = cyc();
+        st.cyc_c += t - cyc_t;
+        cyc_t = t;
+      }
+      const uint64_t* pq = L.pods[q & (kPodWin - 1)];
+      const uint64_t r01 = pq[4], r23 = pq[5];
+      gather_next(k + 1);
       dma_rec(L.spec, cnode0);  // L.spec's last reads (this step) have returned
-      dma_row(L.row[k & 3], p + 4, 0);
+      dma_rows(L.ring[k & 3], r01, r23, 0);
+      if (PROF) st.cyc_d += cyc() - cyc_t;
     }
   }
-
   SR_WAIT_VM(0);  // no LDS-DMA may outlive the wave's LDS allocation
-#pragma unroll
-  for (int b = 0; b < SPL; ++b) {
-    const int q = p0 + 64 * b + lane;
-    if (q < p1) w.out_node[q] = bnode[b];
-  }
+  return status >= 0 ? status : np;
+}
+
+// K2: one wave per candidate (list entries {candidate, first pod, end pod,
+// global index}, longest candidates first).
+template <int CH, bool PROF>
+__global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __restrict__ list, int n_list) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wave);
+  if (li >= n_list) return;
+  const uint64_t t_start = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
+  const uint64_t c_start = PROF ? __builtin_amdgcn_s_memtime() : 0;
+  const int4 e = list[li];
+  const int ci = __builtin_amdgcn_readfirstlane(e.x);
+  const int p0 = __builtin_amdgcn_readfirstlane(e.y);
+  const int np = __builtin_amdgcn_readfirstlane(e.z) - p0;  // >= 1: empty candidates never reach the device
+  const int g = __builtin_amdgcn_readfirstlane(e.w);
+  K2Lds& L = *reinterpret_cast<K2Lds*>(k2_lds + static_cast<size_t>(wave) * (sizeof(K2Lds) / 8));
+
+  K2Stats st;
+  int status = -1;
+  int placed = k2_run<1, CH, PROF>(w, L, p0, np, status, st);
+  const int wide = placed < 0 ? 1 : 0;
+  if (placed < 0) placed = k2_run<8, CH, PROF>(w, L, p0, np, status, st);  // > 64 distinct nodes
+
+  for (int i = lane; i < np; i += 64) w.out_node[p0 + i] = i < placed ? L.omap[i] : -1;
   if (lane == 0) {
     w.out_status[ci] = status;
     // packed (global candidate << 32 | local candidate): min = first drainable
     if (status < 0)
       atomicMin(reinterpret_cast<unsigned long long*>(w.d_min),
-                (static_cast<unsigned long long>(w.cand_global[ci]) << 32) | static_cast<unsigned>(ci));
+                (static_cast<unsigned long long>(g) << 32) | static_cast<unsigned>(ci));
+    if (PROF) {
+      uint64_t* pr = w.prof + static_cast<size_t>(ci) * 16;
+      pr[0] = t_start;
+      pr[1] = t_start;
+      pr[2] = __builtin_amdgcn_s_memrealtime();
+      pr[3] = __builtin_amdgcn_s_memtime() - c_start;
+      pr[4] = static_cast<uint64_t>(status >= 0 ? status + 1 : np);
+      pr[5] = static_cast<uint64_t>(wide);
+      pr[6] = st.n_spec_miss;
+      pr[7] = static_cast<uint64_t>(st.n_min) | (static_cast<uint64_t>(st.n_far) << 32);
+      pr[8] = st.cyc_a;
+      pr[9] = st.cyc_b;
+      pr[10] = st.cyc_c;
+      pr[11] = st.cyc_d;
+    }
   }
 }
 
@@ -402,18 +481,19 @@ __global__ __launch_bounds__(64) void k3_winner(DevWorkload w) {
   }
 }
 
-template <int SPL>
-hipError_t launch_k2_variant(const DevWorkload& w, const int32_t* list, int n, hipStream_t s) {
+template <bool PROF>
+hipError_t launch_k2(const DevWorkload& w, hipStream_t s) {
+  const int n = w.n_list;
   if (n <= 0) return hipSuccess;
   const dim3 grid((n + 3) / 4), block(256);
-  const size_t lds = 4 * (64 * SPL * 4 * sizeof(uint64_t) + sizeof(K2Lds));
+  const size_t lds = 4 * sizeof(K2Lds);
   const int chunks = (w.Wp + 63) / 64;
-  if (chunks <= 1) hipLaunchKernelGGL((k2_place<SPL, 1>), grid, block, lds, s, w, list, n);
-  else if (chunks <= 2) hipLaunchKernelGGL((k2_place<SPL, 2>), grid, block, lds, s, w, list, n);
-  else if (chunks <= 4) hipLaunchKernelGGL((k2_place<SPL, 4>), grid, block, lds, s, w, list, n);
-  else if (chunks <= 8) hipLaunchKernelGGL((k2_place<SPL, 8>), grid, block, lds, s, w, list, n);
-  else if (chunks <= 16) hipLaunchKernelGGL((k2_place<SPL, 16>), grid, block, lds, s, w, list, n);
-  else hipLaunchKernelGGL((k2_place<SPL, 32>), grid, block, lds, s, w, list, n);
+  if (chunks <= 1) hipLaunchKernelGGL((k2_place<1, PROF>), grid, block, lds, s, w, w.list, n);
+  else if (chunks <= 2) hipLaunchKernelGGL((k2_place<2, PROF>), grid, block, lds, s, w, w.list, n);
+  else if (chunks <= 4) hipLaunchKernelGGL((k2_place<4, PROF>), grid, block, lds, s, w, w.list, n);
+  else if (chunks <= 8) hipLaunchKernelGGL((k2_place<8, PROF>), grid, block, lds, s, w, w.list, n);
+  else if (chunks <= 16) hipLaunchKernelGGL((k2_place<16, PROF>), grid, block, lds, s, w, w.list, n);
+  else hipLaunchKernelGGL((k2_place<32, PROF>), grid, block, lds, s, w, w.list, n);
   return hipGetLastError();
 }
 
@@ -428,22 +508,8 @@ hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hip
   return hipGetLastError();
 }
 
-hipError_t launch_feasibility(const DevWorkload& w, hipStream_t s) {
-  if (w.n_pods <= 0) return hipSuccess;
-  const uint32_t half = static_cast<uint32_t>(w.Wp / 2);
-  const uint64_t total = static_cast<uint64_t>(w.n_pods) * half;
-  // ~4 items per thread, at least one wave of work per SIMD
-  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((total + 1023) / 1024, 256 * 16));
-  hipLaunchKernelGGL(k1_feasibility, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
-                     reinterpret_cast<const ulonglong2*>(w.S), reinterpret_cast<const ulonglong2*>(w.T), w.pod_rows,
-                     reinterpret_cast<ulonglong2*>(w.F), static_cast<uint32_t>(w.n_pods), half);
-  return hipGetLastError();
-}
-
 hipError_t launch_placement(const DevWorkload& w, hipStream_t s) {
-  hipError_t e = launch_k2_variant<2>(w, w.list_small, w.n_small, s);
-  if (e != hipSuccess) return e;
-  return launch_k2_variant<8>(w, w.list_large, w.n_large, s);
+  return w.prof ? launch_k2<true>(w, s) : launch_k2<false>(w, s);
 }
 
 hipError_t launch_winner(const DevWorkload& w, hipStream_t s) {

@@ -13,8 +13,6 @@ struct DevWorkload {
   const int64_t* free_cpu;
   const int64_t* free_mem;
   const int64_t* free_eph;
-  const int32_t* pods_left;
-  const uint64_t* port_bits;
   const uint64_t* node_rec;    // [n_pad][8] AoS {free cpu, mem, eph, ports, pods_left, 0, 0, 0} for K2
   int32_t n_atoms;
   const uint64_t* atoms;       // [n_atoms][Wp] node bitsets (encode.cpp)
@@ -31,34 +29,26 @@ struct DevWorkload {
   const int32_t* t_dim;     // 0 cpu, 1 memory, 2 ephemeral, 3 all
   const int64_t* t_thr;
   int32_t n_pods;
-  const int4* pod_rows;     // {S row, T cpu row, T memory row, T ephemeral row}
-  const int32_t* pod_zero;
-  const int64_t* pod_cpu;
-  const int64_t* pod_mem;
-  const int64_t* pod_eph;
-  const uint64_t* pod_ports;
-  const uint64_t* pod_rec;     // [n_pods][4] AoS {cpu, memory, ephemeral, ports} for K2 (32 B aligned)
+  const uint64_t* pod_rec;  // [n_pods + 128][6] AoS {cpu, memory, ephemeral, ports, S | T cpu row word
+                            //  offset, T mem | T eph row word offset} (48 B, padded for K2's window reads)
   int32_t n_cand;
   const int32_t* cand_off;
   const int32_t* cand_global;
-  const int32_t* list_small;
-  const int32_t* list_large;
-  int32_t n_small, n_large;
+  const int4* list;         // [n_list] {candidate, first pod, end pod, global index}, longest first
+  int32_t n_list;
   // outputs / scratch
-  uint64_t* S;         // [n_classes][Wp] static-class rows
-  uint64_t* T;         // [n_t][Wp] capacity threshold rows
-  uint64_t* F;         // [n_pods][Wp] dense feasibility bitmask vs the base snapshot
+  uint64_t* S;         // [n_classes][Wp] static-class rows, followed by
+  uint64_t* T;         // [n_t][Wp] capacity threshold rows (one table)
   int32_t* out_node;   // [n_pods] spot position or -1
   int32_t* out_status; // [n_cand]
   int32_t* d_min;      // 2 x u64 packed {global << 32 | local}: first ok, first fallback (~0 = none)
   int32_t* result;     // mapped host memory [4 + max pods] {winner, local, npods, first_fallback, mapping...}
+  uint64_t* prof;      // optional [n_cand][16] K2 per-wave profile (SR_K2_PROFILE), else null
 };
 
 // K0: S and T rows (also resets d_min: d_min[1] = local first fallback).
 hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hipStream_t s);
-// K1: F = S[s] & T[cpu] & T[mem] & T[eph] per pod.
-hipError_t launch_feasibility(const DevWorkload& w, hipStream_t s);
-// K2: per-candidate first-fit placement; atomicMin of first_ok into d_min[0].
+// K2: per-candidate feasibility rows + first-fit placement; atomicMin of first_ok into d_min[0].
 hipError_t launch_placement(const DevWorkload& w, hipStream_t s);
 // K3: winner mapping into `result`.
 hipError_t launch_winner(const DevWorkload& w, hipStream_t s);

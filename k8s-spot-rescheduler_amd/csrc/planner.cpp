@@ -1,9 +1,9 @@
 // planner.cpp — device context, resident buffers and the planning tick.
 //
 // sr_ctx plays the role of the reference's predicate checker (created once,
-// rescheduler.go:149).  One tick (sr_plan_run) is four kernels and one small
-// download on a single HIP stream:
-//   K0 tables -> K1 feasibility -> K2 placement -> [RCCL allreduce(min)] -> K3 winner -> D2H
+// rescheduler.go:149).  One tick (sr_plan_run) is three kernels on a single
+// HIP stream; K3 writes the result straight into mapped host memory:
+//   K0 tables -> K2 placement -> [RCCL allreduce(min)] -> K3 winner
 // There is no CPU path: without a HIP device sr_create fails.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -12,6 +12,7 @@
 #include <chrono>
 #include <climits>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -37,7 +38,7 @@ struct sr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  DevBuf arena, tables, F, out_node, out_status, dmin;
+  DevBuf arena, tables, out_node, out_status, dmin, prof;
   HostBuf h_arena, h_result, h_status, h_node;
   sr::Workload wl;
   sr::DevWorkload dw{};
@@ -47,6 +48,7 @@ struct sr_ctx {
   sr_timing t{};
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  FILE* prof_file = nullptr;  // SR_K2_PROFILE: per-wave K2 records appended per run
 };
 
 namespace {
@@ -121,26 +123,20 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
     ctx->err = err;
     return st;
   }
-  const int32_t na = static_cast<int32_t>(w.pod_zero.size());
+  const int32_t na = static_cast<int32_t>(w.pod_src.size());
   const int32_t ncand = static_cast<int32_t>(w.cand_global.size());
-  if (static_cast<uint64_t>(na) * static_cast<uint64_t>(w.Wp / 2) >= (1ull << 31)) {
-    ctx->err = "pod x node bitmask exceeds 2^31 16-byte items";
-    return SR_ERR_CAPACITY;
-  }
   Packer pk;
   const size_t o_fc = pk.add(w.free_cpu), o_fm = pk.add(w.free_mem), o_fe = pk.add(w.free_eph);
-  const size_t o_pl = pk.add(w.pods_left), o_pb = pk.add(w.port_bits), o_nr = pk.add(w.node_rec);
+  const size_t o_nr = pk.add(w.node_rec);
   const size_t o_at = pk.add(w.atoms);
   const size_t o_cao = pk.add(w.cls_and_off), o_ca = pk.add(w.cls_and);
   const size_t o_cno = pk.add(w.cls_not_off), o_cn = pk.add(w.cls_not);
   const size_t o_cto = pk.add(w.cls_term_off), o_tao = pk.add(w.term_atom_off), o_ta = pk.add(w.term_atoms);
   const size_t o_cf = pk.add(w.cls_flags);
   const size_t o_td = pk.add(w.t_dim), o_tt = pk.add(w.t_thr);
-  const size_t o_pr = pk.add(w.pod_rows), o_pz = pk.add(w.pod_zero);
-  const size_t o_pc = pk.add(w.pod_cpu), o_pm = pk.add(w.pod_mem), o_pe = pk.add(w.pod_eph);
-  const size_t o_pp = pk.add(w.pod_ports), o_prec = pk.add(w.pod_rec);
+  const size_t o_prec = pk.add(w.pod_rec);
   const size_t o_co = pk.add(w.cand_off), o_cg = pk.add(w.cand_global);
-  const size_t o_ls = pk.add(w.list_small), o_ll = pk.add(w.list_large);
+  const size_t o_ls = pk.add(w.list);
   const size_t bytes = pk.size();
 
   HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -149,7 +145,6 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
   HIP_TRY(ctx, dev_reserve(ctx->tables, n_rows * row_bytes));
-  HIP_TRY(ctx, dev_reserve(ctx->F, std::max<size_t>(1, static_cast<size_t>(na)) * row_bytes));
   HIP_TRY(ctx, dev_reserve(ctx->out_node, sizeof(int32_t) * std::max(1, na)));
   HIP_TRY(ctx, dev_reserve(ctx->out_status, sizeof(int32_t) * std::max(1, ncand)));
   HIP_TRY(ctx, dev_reserve(ctx->dmin, 64));
@@ -171,8 +166,6 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.free_cpu = static_cast<const int64_t*>(at(o_fc));
   d.free_mem = static_cast<const int64_t*>(at(o_fm));
   d.free_eph = static_cast<const int64_t*>(at(o_fe));
-  d.pods_left = static_cast<const int32_t*>(at(o_pl));
-  d.port_bits = static_cast<const uint64_t*>(at(o_pb));
   d.node_rec = static_cast<const uint64_t*>(at(o_nr));
   d.n_atoms = w.n_atoms;
   d.atoms = static_cast<const uint64_t*>(at(o_at));
@@ -189,37 +182,35 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.t_dim = static_cast<const int32_t*>(at(o_td));
   d.t_thr = static_cast<const int64_t*>(at(o_tt));
   d.n_pods = na;
-  d.pod_rows = static_cast<const int4*>(at(o_pr));
-  d.pod_zero = static_cast<const int32_t*>(at(o_pz));
-  d.pod_cpu = static_cast<const int64_t*>(at(o_pc));
-  d.pod_mem = static_cast<const int64_t*>(at(o_pm));
-  d.pod_eph = static_cast<const int64_t*>(at(o_pe));
-  d.pod_ports = static_cast<const uint64_t*>(at(o_pp));
   d.pod_rec = static_cast<const uint64_t*>(at(o_prec));
   d.n_cand = ncand;
   d.cand_off = static_cast<const int32_t*>(at(o_co));
   d.cand_global = static_cast<const int32_t*>(at(o_cg));
-  d.list_small = static_cast<const int32_t*>(at(o_ls));
-  d.list_large = static_cast<const int32_t*>(at(o_ll));
-  d.n_small = static_cast<int32_t>(w.list_small.size());
-  d.n_large = static_cast<int32_t>(w.list_large.size());
+  d.list = static_cast<const int4*>(at(o_ls));
+  d.n_list = static_cast<int32_t>(w.list.size() / 4);
   d.S = static_cast<uint64_t*>(ctx->tables.p);
   d.T = d.S + static_cast<size_t>(w.n_classes) * w.Wp;
-  d.F = static_cast<uint64_t*>(ctx->F.p);
   d.out_node = static_cast<int32_t*>(ctx->out_node.p);
   d.out_status = static_cast<int32_t*>(ctx->out_status.p);
   d.d_min = static_cast<int32_t*>(ctx->dmin.p);
+  d.prof = nullptr;
+  if (ctx->prof_file) {
+    HIP_TRY(ctx, dev_reserve(ctx->prof, sizeof(uint64_t) * 16 * std::max(1, ncand)));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->prof.p, 0, sizeof(uint64_t) * 16 * std::max(1, ncand), ctx->stream));
+    d.prof = static_cast<uint64_t*>(ctx->prof.p);
+  }
   void* dres = nullptr;
   HIP_TRY(ctx, hipHostGetDevicePointer(&dres, ctx->h_result.p, 0));
   d.result = static_cast<int32_t*>(dres);
 
   const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
-  // K1 algorithmic bytes: the dense bitmask written once, every table row and
-  // every pod's four row indices read once.
-  ctx->t.bytes_feasibility = static_cast<uint64_t>(na) * row + n_rows * row + 16ull * na;
-  uint64_t k2 = 0;
-  for (int32_t q = 0; q < na; ++q) k2 += 8ull * std::min(w.Wp, 64) + 48;
-  ctx->t.bytes_placement = k2 + 16ull * ncand;
+  // K0 algorithmic bytes: every table row written once; every atom row a class
+  // program names, the nodes' free capacities and the thresholds read once.
+  uint64_t atom_reads = w.cls_and.size() + w.cls_not.size() + w.term_atoms.size();
+  ctx->t.bytes_tables = n_rows * row + atom_reads * row + 3ull * 8 * w.n_pad + 12ull * w.t_dim.size();
+  // K2 (upper bound until a full run refines it, see run()): per pod its
+  // four row chunks and its record, per candidate its mapping and status.
+  ctx->t.bytes_placement = static_cast<uint64_t>(na) * (32ull * std::min(w.Wp, 64) + 48 + 4) + 4ull * ncand;
   ctx->t.ms_pack_host = std::chrono::duration<double, std::milli>(t1 - t0).count();
   ctx->t.ms_upload = std::chrono::duration<double, std::milli>(t2 - t1).count();
   ctx->t.n_pods = na;
@@ -249,12 +240,9 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s));
   HIP_TRY(ctx, mark(0, 1));
   HIP_TRY(ctx, mark(1, 0));
-  HIP_TRY(ctx, sr::launch_feasibility(d, s));
+  HIP_TRY(ctx, sr::launch_placement(d, s));
   HIP_TRY(ctx, mark(1, 1));
   HIP_TRY(ctx, mark(2, 0));
-  HIP_TRY(ctx, sr::launch_placement(d, s));
-  HIP_TRY(ctx, mark(2, 1));
-  HIP_TRY(ctx, mark(3, 0));
   if (ctx->comm && use_comm) {
     ncclResult_t r = ncclAllReduce(d.d_min, d.d_min, 2, ncclUint64, ncclMin, ctx->comm, s);
     if (r != ncclSuccess) {
@@ -271,11 +259,11 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
       HIP_TRY(ctx, hipMemcpyAsync(ctx->h_status.p, d.out_status, sizeof(int32_t) * ncand, hipMemcpyDeviceToHost, s));
     if (na) HIP_TRY(ctx, hipMemcpyAsync(ctx->h_node.p, d.out_node, sizeof(int32_t) * na, hipMemcpyDeviceToHost, s));
   }
-  HIP_TRY(ctx, mark(3, 1));
+  HIP_TRY(ctx, mark(2, 1));
   HIP_TRY(ctx, hipStreamSynchronize(s));
   if (ctx->timing) {
-    double* sums[4] = {&ctx->t.ms_tables, &ctx->t.ms_feasibility, &ctx->t.ms_placement, &ctx->t.ms_winner};
-    for (int k = 0; k < 4; ++k) {
+    double* sums[3] = {&ctx->t.ms_tables, &ctx->t.ms_placement, &ctx->t.ms_winner};
+    for (int k = 0; k < 3; ++k) {
       if (!(ctx->timing >> k & 1)) continue;
       float ms = 0;
       HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev[2 * k], ctx->ev[2 * k + 1]));
@@ -284,6 +272,14 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     ctx->t.n_runs += 1;
   }
 
+  if (ctx->prof_file && ncand > 0) {  // diagnostics only (tools/k2_profile.py)
+    std::vector<uint64_t> pr(static_cast<size_t>(ncand) * 16);
+    HIP_TRY(ctx, hipMemcpy(pr.data(), d.prof, pr.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    const int64_t hdr[2] = {ncand, d.Wp};
+    std::fwrite(hdr, sizeof(hdr), 1, ctx->prof_file);
+    std::fwrite(pr.data(), sizeof(uint64_t), pr.size(), ctx->prof_file);
+    std::fflush(ctx->prof_file);
+  }
   const int32_t* r = static_cast<const int32_t*>(ctx->h_result.p);
   out->first_ok = r[0];
   out->first_fallback = r[3];
@@ -299,6 +295,15 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
       for (int32_t i = 0; i < w.n_input_cand; ++i) out->status[i] = w.status_host[i];
       for (int32_t k = 0; k < ncand; ++k) out->status[w.cand_src[k]] = hs[k];
     }
+    // exact K2 algorithmic bytes: pods up to and including the failing one
+    uint64_t k2 = 4ull * ncand;
+    const uint64_t per_pod = 32ull * std::min(w.Wp, 64) + 48;
+    for (int32_t k = 0; k < ncand; ++k) {
+      const int32_t np = w.cand_off[k + 1] - w.cand_off[k];
+      const int32_t done = hs[k] >= 0 ? std::min(np, hs[k] + 1) : np;
+      k2 += per_pod * done + 4ull * np;
+    }
+    ctx->t.bytes_placement = k2;
     if (out->node_of_pod) {
       for (int32_t i = 0; i < w.n_input_pods; ++i) out->node_of_pod[i] = -1;
       for (int32_t q = 0; q < na; ++q) out->node_of_pod[w.pod_src[q]] = hn[q];
@@ -312,7 +317,7 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
 extern "C" {
 
 const char* sr_build_info(void) {
-  return "srplanner abi=1 target=gfx950 kernels=K0-tables,K1-feasibility,K2-placement,K3-winner";
+  return "srplanner abi=2 target=gfx950 kernels=K0-tables,K2-placement(fused feasibility),K3-winner";
 }
 
 sr_status sr_create(int32_t device, sr_ctx** out) {
@@ -332,6 +337,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
       delete ctx;
       return SR_ERR_HIP;
     }
+  if (const char* path = std::getenv("SR_K2_PROFILE")) ctx->prof_file = std::fopen(path, "ab");
   *out = ctx;
   return SR_OK;
 }
@@ -341,13 +347,14 @@ void sr_destroy(sr_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
-  for (DevBuf* b : {&ctx->arena, &ctx->tables, &ctx->F, &ctx->out_node, &ctx->out_status, &ctx->dmin})
+  for (DevBuf* b : {&ctx->arena, &ctx->tables, &ctx->out_node, &ctx->out_status, &ctx->dmin, &ctx->prof})
     if (b->p) (void)hipFree(b->p);
   for (HostBuf* b : {&ctx->h_arena, &ctx->h_result, &ctx->h_status, &ctx->h_node})
     if (b->p) (void)hipHostFree(b->p);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->prof_file) std::fclose(ctx->prof_file);
   delete ctx;
 }
 
@@ -431,7 +438,7 @@ sr_status sr_set_timing(sr_ctx* ctx, int32_t mask) {
   if (!ctx) return SR_ERR_INVALID_ARG;
   ctx->timing = mask & 15;
   ctx->t.n_runs = 0;
-  ctx->t.ms_tables = ctx->t.ms_feasibility = ctx->t.ms_placement = ctx->t.ms_winner = 0;
+  ctx->t.ms_tables = ctx->t.ms_placement = ctx->t.ms_winner = 0;
   return SR_OK;
 }
 

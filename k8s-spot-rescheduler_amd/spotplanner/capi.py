@@ -91,10 +91,10 @@ class sr_plan_out(ctypes.Structure):
 
 
 class sr_timing(ctypes.Structure):
-    _fields_ = [("n_runs", ctypes.c_int32), ("ms_tables", ctypes.c_double), ("ms_feasibility", ctypes.c_double),
+    _fields_ = [("n_runs", ctypes.c_int32), ("ms_tables", ctypes.c_double),
                 ("ms_placement", ctypes.c_double), ("ms_winner", ctypes.c_double),
                 ("ms_pack_host", ctypes.c_double), ("ms_upload", ctypes.c_double),
-                ("bytes_feasibility", ctypes.c_uint64), ("bytes_placement", ctypes.c_uint64),
+                ("bytes_tables", ctypes.c_uint64), ("bytes_placement", ctypes.c_uint64),
                 ("n_pods", ctypes.c_int32), ("n_spot", ctypes.c_int32), ("n_cand", ctypes.c_int32),
                 ("n_words", ctypes.c_int32), ("n_rows_static", ctypes.c_int32), ("n_rows_threshold", ctypes.c_int32),
                 ("n_classes", ctypes.c_int32)]

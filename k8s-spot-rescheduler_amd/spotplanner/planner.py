@@ -60,7 +60,7 @@ class PredicateChecker:
         return self.lib.sr_last_error(self.handle).decode(errors="replace")
 
     def set_timing(self, mask: int):
-        """Bracket kernels with HIP events: 1 K0, 2 K1, 4 K2, 8 K3 (+collective, download)."""
+        """Bracket kernels with HIP events: 1 K0, 2 K2, 4 K3 (+collective)."""
         self.lib.sr_set_timing(self.handle, int(mask))
 
     def timing(self) -> capi.sr_timing:

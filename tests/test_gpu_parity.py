@@ -190,6 +190,18 @@ def test_more_than_128_touched_nodes(checker):
     assert list(p.node_of_pod[:200]) == list(range(200))
 
 
+@pytest.mark.parametrize("n_touch", [63, 64, 65, 129])
+def test_touched_slot_boundaries(checker, n_touch):
+    # K2 keeps 64 touched-node slots in registers and reruns a candidate that
+    # needs more with 512: both sides of the boundary, plus pods that keep
+    # landing on already-touched nodes afterwards
+    nodes = [Node("n%d" % i, 1000, pods=1) for i in range(n_touch)] + [Node("big", 100000)]
+    pods = [Pod("p%d" % k, containers=[Container(10)]) for k in range(n_touch + 20)]
+    _, o, p = run_scenario(checker, nodes, [[] for _ in nodes], [pods, pods[:5]])
+    assert p.status[0] == OK and p.status[1] == OK
+    assert list(p.node_of_pod[:n_touch + 20]) == list(range(n_touch)) + [n_touch] * 20
+
+
 def test_many_chunks_of_spot_nodes(checker):
     # > 4096 spot nodes: bitmask rows span several 64-word chunks
     nodes = [Node("n%d" % i, 100) for i in range(9000)] + [Node("big", 10000)]

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Summarise K2 per-wave profiles written with SR_K2_PROFILE=<file>.
+
+Each sr_plan_run appends {int64 n_cand, int64 Wp} + n_cand x 16 u64:
+  [0] s_memrealtime at wave start (100 MHz)   [1] = [0]
+  [2] at the end                               [3] s_memtime cycles start->end
+  [4] pod steps executed                       [5] 1 if rerun with 512 slots
+  [6] speculative-record misses                [7] wave_min count | far-chunk count << 32
+  [8..11] cycles per step section: a = start -> answer, b = answer -> slot
+          update, c = wait for the next rows, d = next pod's first clean node
+          + DMA issue;  [12] cycles waiting for speculative records
+Only the last run in the file is summarised (earlier ones are warmup)."""
+import sys
+
+import numpy as np
+
+
+def load(path):
+    raw = np.fromfile(path, dtype=np.uint64)
+    runs, i = [], 0
+    while i + 2 <= len(raw):
+        n = int(raw[i]); i += 2
+        runs.append(raw[i:i + 16 * n].reshape(n, 16)); i += 16 * n
+    return runs
+
+
+def main():
+    runs = load(sys.argv[1])
+    r = runs[-1].astype(np.int64)
+    t0 = r[:, 0].min()
+    start = (r[:, 0] - t0) / 100.0          # us
+    pro = (r[:, 1] - r[:, 0]) / 100.0
+    end = (r[:, 2] - t0) / 100.0
+    dur = (r[:, 2] - r[:, 0]) / 100.0
+    steps = r[:, 4]
+    loop_us = (r[:, 2] - r[:, 1]) / 100.0
+    pct = lambda a: " ".join("%.2f" % x for x in np.percentile(a, [50, 90, 99, 100]))
+    print("runs %d  waves %d" % (len(runs), len(r)))
+    print("start skew us  p50/p90/p99/max:", pct(start))
+    print("prologue us    p50/p90/p99/max:", pct(pro))
+    print("wave dur us    p50/p90/p99/max:", pct(dur))
+    print("end us         p50/p90/p99/max:", pct(end))
+    print("steps          p50/p90/p99/max:", pct(steps))
+    ok = steps > 0
+    per = loop_us[ok] / steps[ok]
+    print("loop us/step   p50/p90/p99/max:", pct(per))
+    cyc = r[:, 3] / np.maximum(1, dur)     # cycles per us -> clock
+    print("clock MHz (memtime/realtime) p50:", "%.0f" % np.median(cyc[dur > 0]))
+    print("reruns with 512 slots:", int(r[:, 5].sum()))
+    print("spec misses total %d, wave_min total %d, far chunks total %d" %
+          (r[:, 6].sum(), (r[:, 7] & 0xffffffff).sum(), (r[:, 7] >> 32).sum()))
+    tot = r[:, 8:13].sum(axis=0)
+    st = max(1, steps.sum())
+    print("cycles/step by section a,b,c,d,spec-wait:", " ".join("%.0f" % (x / st) for x in tot))
+    last = np.argsort(-end)[:8]
+    print("latest-ending waves: cand start prologue loop steps slots")
+    for c in last:
+        print("  %5d %7.2f %7.2f %7.2f %4d %3d" % (c, start[c], pro[c], loop_us[c], steps[c], r[c, 5]))
+
+
+if __name__ == "__main__":
+    main()
