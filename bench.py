@@ -134,7 +134,7 @@ def main():
 
     # Calibration (untimed): every kernel bracketed with events -> per-kernel
     # breakdown and the dominant kernel.
-    names = ["k0_tables", "k2_placement", "k3_winner"]
+    names = ["k0_tables", "k2_placement", "k3_winner_and_collective"]
     checker.set_timing(7)
     for _ in range(max(5, min(args.steps, 20))):
         lib.sr_plan_run(checker.handle, ctypes.byref(out))

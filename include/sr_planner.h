@@ -271,7 +271,7 @@ typedef struct {
   int32_t  n_runs;          /* timed runs accumulated */
   double   ms_tables;       /* K0: class / threshold row tables */
   double   ms_placement;    /* K2: feasibility rows + per-candidate first-fit placement */
-  double   ms_winner;       /* K3 + collective (mapped-memory result) */
+  double   ms_winner;       /* collective (multi-GPU) + K3, which writes the result to mapped host memory */
   double   ms_pack_host;    /* last sr_plan_prepare host encoding */
   double   ms_upload;       /* last sr_plan_prepare upload */
   uint64_t bytes_tables;    /* algorithmic bytes per K0 launch */
@@ -281,12 +281,13 @@ typedef struct {
   int32_t  n_rows_static, n_rows_threshold, n_classes;
 } sr_timing;
 /* mask: which kernels sr_plan_run brackets with HIP events (resets the sums):
- * 1 = K0, 2 = K2, 4 = K3 + collective; 0 = no events. */
+ * 1 = K0, 2 = K2, 4 = collective (multi-GPU) + K3; 0 = no events.  Events are read back lazily, by
+ * sr_get_timing / sr_set_timing, so timed runs do not synchronise. */
 #define SR_TIME_TABLES      1
 #define SR_TIME_PLACEMENT   2
 #define SR_TIME_WINNER      4
 sr_status sr_set_timing(sr_ctx *ctx, int32_t mask);
-sr_status sr_get_timing(const sr_ctx *ctx, sr_timing *out);
+sr_status sr_get_timing(sr_ctx *ctx, sr_timing *out);
 
 /* Multi-GPU: one process per GPU; candidates sharded by the caller (use
  * cand_global).  With a communicator attached, sr_plan_run reduces first_ok /

@@ -491,10 +491,8 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   // ---- intern classes (atom programs), once per distinct spec
   std::unordered_map<std::string, int32_t> class_index;
   std::vector<int32_t> spec_class(pstat.size());
-  w->cls_and_off.push_back(0);
-  w->cls_not_off.push_back(0);
-  w->cls_term_off.push_back(0);
-  w->term_atom_off.push_back(0);
+  w->cls_prog_off.push_back(0);
+  auto emit = [&](int32_t atom, int32_t kind) { w->cls_prog.push_back(atom << 2 | kind); };
   std::vector<int32_t> sig;
   for (size_t sp = 0; sp < pstat.size(); ++sp) {
     const PodStatic& ps = pstat[sp];
@@ -513,19 +511,21 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     sig.push_back(static_cast<int32_t>(ps.ports >> 32));
     auto ins = class_index.emplace(bytes_of(sig.data(), sig.size()), w->n_classes);
     if (ins.second) {
-      w->cls_and.push_back(0);  // len(pods)+1 <= allowed pods
-      for (int32_t r : ps.sel) w->cls_and.push_back(A_REQ + r);
-      w->cls_and_off.push_back(static_cast<int32_t>(w->cls_and.size()));
-      for (int32_t t : *ps.untol) w->cls_not.push_back(A_TAINT + t);
+      // program: AND atoms, AND-NOT atoms, then the ORed terms (TERM_START
+      // opens a term, TERM_AND extends it); an impossible class ANDs atom 0
+      // with its complement
+      emit(0, PROG_AND);  // len(pods)+1 <= allowed pods
+      for (int32_t r : ps.sel) emit(A_REQ + r, PROG_AND);
+      for (int32_t t : *ps.untol) emit(A_TAINT + t, PROG_ANDNOT);
       for (int32_t b = 0; b < 64; ++b)
-        if (ps.ports >> b & 1) w->cls_not.push_back(A_PORT + b);
-      w->cls_not_off.push_back(static_cast<int32_t>(w->cls_not.size()));
-      for (const auto& t : ps.terms) {
-        for (int32_t r : t) w->term_atoms.push_back(A_REQ + r);
-        w->term_atom_off.push_back(static_cast<int32_t>(w->term_atoms.size()));
+        if (ps.ports >> b & 1) emit(A_PORT + b, PROG_ANDNOT);
+      if (ps.flags & CLS_IMPOSSIBLE) {
+        emit(0, PROG_ANDNOT);
+      } else {
+        for (const auto& t : ps.terms)
+          for (size_t i = 0; i < t.size(); ++i) emit(A_REQ + t[i], i == 0 ? PROG_TERM_START : PROG_TERM_AND);
       }
-      w->cls_term_off.push_back(static_cast<int32_t>(w->term_atom_off.size()) - 1);
-      w->cls_flags.push_back(ps.flags);
+      w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
       w->n_classes++;
     }
     spec_class[sp] = ins.first->second;
@@ -637,7 +637,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     std::sort(node_vals[d].begin(), node_vals[d].end());
     node_vals[d].erase(std::unique(node_vals[d].begin(), node_vals[d].end()), node_vals[d].end());
   }
-  std::vector<int32_t> t_index[3];  // lower-bound position -> T row (-1 none yet)
+  std::vector<int32_t> t_index[3];  // lower-bound position -> T row
   LowerBound lb[3];
   for (int d = 0; d < 3; ++d) {
     t_index[d].assign(node_vals[d].size() + 1, -1);
@@ -665,23 +665,30 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       rec[3] = pstat[pod_spec[q]].ports;
     }
   });
-  // positions -> T rows, numbered in first-use order (serial, deterministic)
+  // positions -> T rows: row 0 = every node, then the used positions of each
+  // dimension in increasing threshold order (rows grouped by dimension, so
+  // K0 compares one dimension per wave)
+  std::vector<uint8_t> used[3];
+  for (int d = 0; d < 3; ++d) used[d].assign(node_vals[d].size() + 1, 0);
+  for (int32_t q = 0; q < na; ++q) {
+    const int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
+    for (int d = 0; d < 3; ++d)
+      if (r[1 + d] >= 0) used[d][static_cast<size_t>(r[1 + d])] = 1;
+  }
+  w->t_off[0] = 0;
+  w->t_off[1] = 1;
+  for (int d = 0; d < 3; ++d) {
+    for (size_t pos = 0; pos < used[d].size(); ++pos) {
+      if (!used[d][pos]) continue;
+      t_index[d][pos] = static_cast<int32_t>(w->t_dim.size());
+      w->t_dim.push_back(d);
+      w->t_thr.push_back(pos == node_vals[d].size() ? kNever : node_vals[d][pos]);
+    }
+    w->t_off[d + 2] = static_cast<int32_t>(w->t_dim.size());
+  }
   for (int32_t q = 0; q < na; ++q) {
     int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
-    for (int d = 0; d < 3; ++d) {
-      if (r[1 + d] < 0) {
-        r[1 + d] = 0;  // zero-request pod: row 0 (every node)
-        continue;
-      }
-      const size_t pos = static_cast<size_t>(r[1 + d]);
-      int32_t& row = t_index[d][pos];
-      if (row < 0) {
-        row = static_cast<int32_t>(w->t_dim.size());
-        w->t_dim.push_back(d);
-        w->t_thr.push_back(pos == node_vals[d].size() ? kNever : node_vals[d][pos]);
-      }
-      r[1 + d] = row;
-    }
+    for (int d = 0; d < 3; ++d) r[1 + d] = r[1 + d] < 0 ? 0 : t_index[d][static_cast<size_t>(r[1 + d])];
     uint64_t* rec = &w->pod_rec[static_cast<size_t>(q) * 6];
     auto off = [&](int32_t table_row) { return static_cast<uint64_t>(table_row) * static_cast<uint64_t>(w->Wp); };
     rec[4] = off(r[0]) | off(w->n_classes + r[1]) << 32;

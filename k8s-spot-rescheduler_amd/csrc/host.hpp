@@ -70,6 +70,8 @@ void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t 
 
 // Class descriptor flags.
 enum : int32_t { CLS_AFF_REQUIRED = 1, CLS_IMPOSSIBLE = 2 };
+// class program ops (K0): acc &= atom | acc &= ~atom | open an ORed term | AND into the open term
+enum : int32_t { PROG_AND = 0, PROG_ANDNOT = 1, PROG_TERM_START = 2, PROG_TERM_AND = 3 };
 
 // The encoded workload of one planning call (host copy; uploaded as one arena).
 struct Workload {
@@ -92,15 +94,12 @@ struct Workload {
   // ---- static pod classes as atom programs:
   //   S[c] = AND(and atoms) & AND(~not atoms) & [OR over terms of AND(term atoms)]
   int32_t n_classes = 0;
-  std::vector<int32_t> cls_and_off, cls_and;    // CSR
-  std::vector<int32_t> cls_not_off, cls_not;    // CSR
-  std::vector<int32_t> cls_term_off;            // CSR classes -> terms
-  std::vector<int32_t> term_atom_off, term_atoms;  // CSR terms -> atoms
-  std::vector<int32_t> cls_flags;               // CLS_*
+  std::vector<int32_t> cls_prog_off, cls_prog;  // CSR class -> ops (atom << 2 | PROG_*)
   // ---- T rows: capacity thresholds.  Row 0 = every node (zero-request pods
   // skip the resource checks); other rows: free_<dim>[n] >= thr.
   std::vector<int32_t> t_dim;   // 0 cpu, 1 memory, 2 ephemeral, 3 all
   std::vector<int64_t> t_thr;
+  int32_t t_off[5] = {0, 0, 0, 0, 0};  // rows [t_off[i], t_off[i+1]): all, cpu, memory, ephemeral
   // ---- active pods, grouped by candidate, in podsForDeletion order
   std::vector<int32_t> pod_rows;  // [n][4]: S row (class), T rows for cpu, memory, ephemeral
   std::vector<uint64_t> pod_rec;  // [n + 128][6] AoS {cpu, memory, ephemeral, ports, rows} for K2

@@ -20,10 +20,34 @@
 namespace sr {
 namespace {
 
+// Lane mask of `p` (the compare feeds the mask directly, no 0/1 round trip).
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v & 0xffffffffu), lane));
   const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v >> 32), lane));
   return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// v[L] = x (x wave-uniform, L a constant: GFX9's constant bus takes one SGPR)
+template <int L>
+__device__ __forceinline__ void writelane(uint32_t& v, uint32_t x) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(L));
+}
+
+// K0 T rows: row r0 + t of a group = ballot(free >= thr[t]), kept in lane t.
+// Lane t holds thr[t]; a constant-lane readlane makes it scalar.
+template <int T>
+__device__ __forceinline__ void t_rows(uint32_t& lo, uint32_t& hi, int nr, bool valid, bool all, int64_t v,
+                                       int64_t my_thr) {
+  if constexpr (T < 64) {
+    if (T >= nr) return;
+    const int64_t thr = static_cast<int64_t>(readlane64(static_cast<uint64_t>(my_thr), T));
+    const uint64_t m = ballot(valid && (all || v >= thr));
+    writelane<T>(lo, static_cast<uint32_t>(m));
+    writelane<T>(hi, static_cast<uint32_t>(m >> 32));
+    t_rows<T + 1>(lo, hi, nr, valid, all, v, my_thr);
+  }
 }
 
 // Minimum over the 64 lanes with DPP row shifts / broadcasts (no LDS round trips).
@@ -41,109 +65,178 @@ __device__ __forceinline__ int wave_min(int v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
-// S row of one class for word w: its atom program evaluated 64 nodes at a time.
-//   NodeAffinity (nodeSelector pairs; required terms ORed, requirements ANDed),
-//   TaintToleration + NodeUnschedulable (untolerated taint atoms negated),
-//   NodePorts (the class's ports against base UsedPorts), pod count (atom 0).
-__device__ __forceinline__ uint64_t class_word(const DevWorkload& w, int cls, int word) {
-  const size_t Wp = static_cast<size_t>(w.Wp);
-  const uint64_t* __restrict__ at = w.atoms + word;
-  uint64_t acc = ~0ull;
-  for (int i = w.cls_and_off[cls]; i < w.cls_and_off[cls + 1]; ++i) acc &= at[w.cls_and[i] * Wp];
-  for (int i = w.cls_not_off[cls]; i < w.cls_not_off[cls + 1]; ++i) acc &= ~at[w.cls_not[i] * Wp];
-  const int flags = w.cls_flags[cls];
-  if (flags & 1) {
-    uint64_t any = 0;
-    for (int t = w.cls_term_off[cls]; t < w.cls_term_off[cls + 1]; ++t) {
-      uint64_t all = ~0ull;
-      for (int i = w.term_atom_off[t]; i < w.term_atom_off[t + 1]; ++i) all &= at[w.term_atoms[i] * Wp];
-      any |= all;
-    }
-    acc &= any;
-  }
-  return (flags & 2) ? 0 : acc;
-}
-
 // K0: bitmask rows.  Blocks [0, s_blocks): one wave per class, lanes = words
 // (S rows, word-parallel atom programs).  Blocks after: T rows, grid over
 // (row groups of 64) x (Wp / 4): each wave owns one 64-node word, loads its
 // nodes' free capacity once and evaluates 64 thresholds (one ballot each),
 // lane t keeping row r0 + t.
-__global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, int wblocks, int local_first_fallback) {
+__global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, int local_first_fallback) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  // diagnostics: per-wave {start, end} (s_memrealtime) after K2's records
+  const size_t pw = static_cast<size_t>(blockIdx.x) * 4 + wave;
+  uint64_t* const prof = w.prof && pw < kK0ProfWaves ? w.prof + static_cast<size_t>(w.n_cand) * 16 + 2 * pw : nullptr;
+  if (prof && lane == 0) prof[0] = __builtin_amdgcn_s_memrealtime();
+  struct Stamp {
+    uint64_t* p;
+    int lane;
+    __device__ ~Stamp() {
+      if (p && lane == 0) p[1] = __builtin_amdgcn_s_memrealtime();
+    }
+  } stamp{prof, lane};
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     unsigned long long* dm = reinterpret_cast<unsigned long long*>(w.d_min);
     dm[0] = ~0ull;
     dm[1] = local_first_fallback < 0 ? ~0ull : static_cast<unsigned long long>(local_first_fallback) << 32;
   }
   if (static_cast<int>(blockIdx.x) < s_blocks) {
+    // S row of one class: its atom program, 64 words (lanes) at a time.
+    //   NodeAffinity (nodeSelector pairs; required terms ORed, requirements
+    //   ANDed), TaintToleration + NodeUnschedulable (untolerated taint atoms
+    //   negated), NodePorts (the class's ports against base UsedPorts), pod
+    //   count (atom 0).  The program is loaded lane-parallel and its atom
+    //   words are fetched 8 at a time, so a class costs ~3 memory latencies.
     const int cls = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wave);
     if (cls >= w.n_classes) return;
-    for (int word = lane; word < w.Wp; word += 64)
-      w.S[static_cast<size_t>(cls) * w.Wp + word] = class_word(w, cls, word);
+    const int o0 = w.cls_prog_off[cls], n = w.cls_prog_off[cls + 1] - o0;
+    const size_t Wp = static_cast<size_t>(w.Wp);
+    for (int wb = 0; wb < w.Wp; wb += 64) {
+      const int word = wb + lane;
+      const bool wv = word < w.Wp;
+      const uint64_t* __restrict__ at = w.atoms + (wv ? word : 0);
+      uint64_t acc = ~0ull, any = 0, cur = 0;
+      bool has = false;
+      for (int base = 0; base < n; base += 64) {
+        const int m = min(64, n - base);
+        const int my = lane < m ? w.cls_prog[o0 + base + lane] : 0;
+        for (int j0 = 0; j0 < m; j0 += 8) {
+          uint64_t v[8];
+          int op[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            op[u] = __builtin_amdgcn_readlane(my, j0 + u);
+            v[u] = j0 + u < m ? at[static_cast<size_t>(op[u] >> 2) * Wp] : 0;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            if (j0 + u >= m) break;
+            switch (op[u] & 3) {
+              case 0: acc &= v[u]; break;
+              case 1: acc &= ~v[u]; break;
+              case 2:
+                any |= has ? cur : 0;
+                cur = v[u];
+                has = true;
+                break;
+              default: cur &= v[u]; break;
+            }
+          }
+        }
+      }
+      if (has) acc &= any | cur;
+      if (wv) w.S[static_cast<size_t>(cls) * Wp + word] = acc;
+    }
     return;
   }
-  const int b = static_cast<int>(blockIdx.x) - s_blocks;
-  const int g = b / wblocks;
-  const int word = (b - g * wblocks) * 4 + wave;
-  if (word >= w.Wp) return;  // wave-uniform
+  // T rows: one wave per (dimension, group of 64 rows, 64-node word), lanes =
+  // nodes; row r of the group = ballot(free >= thr[r]) written into lane r.
+  int tw = (static_cast<int>(blockIdx.x) - s_blocks) * 4 + wave;
+  int d = 0;
+  for (; d < 4; ++d) {
+    const int waves_d = (w.t_off[d + 1] - w.t_off[d] + 63) / 64 * w.Wp;
+    if (tw < waves_d) break;
+    tw -= waves_d;
+  }
+  if (d == 4) return;  // wave-uniform
+  const int g = tw / w.Wp;
+  const int word = tw - g * w.Wp;
   const int n = word * 64 + lane;  // < n_pad: node arrays are padded
   const bool valid = n < w.n_spot;
-  const int r0 = g * 64;
-  const int nr = min(64, w.n_t - r0);
-  const int64_t fc = w.free_cpu[n], fm = w.free_mem[n], fe = w.free_eph[n];
-  const int my_dim = lane < nr ? w.t_dim[r0 + lane] : 3;
+  const int r0 = w.t_off[d] + 64 * g;
+  const int nr = min(64, w.t_off[d + 1] - r0);
+  const int64_t v = d == 1 ? w.free_cpu[n] : (d == 2 ? w.free_mem[n] : (d == 3 ? w.free_eph[n] : 0));
+  uint32_t lo = 0, hi = 0;
   const int64_t my_thr = lane < nr ? w.t_thr[r0 + lane] : 0;
-  uint64_t acc = 0;
-  for (int t = 0; t < nr; ++t) {
-    const int dim = __builtin_amdgcn_readlane(my_dim, t);
-    const int64_t thr = static_cast<int64_t>(readlane64(static_cast<uint64_t>(my_thr), t));
-    const int64_t v = dim == 0 ? fc : (dim == 1 ? fm : fe);
-    const uint64_t m = __ballot(valid && (dim == 3 || v >= thr));
-    if (lane == t) acc = m;
-  }
-  if (lane < nr) w.T[static_cast<size_t>(r0 + lane) * w.Wp + word] = acc;
+  t_rows<0>(lo, hi, nr, valid, d == 0, v, my_thr);
+  if (lane < nr) w.T[static_cast<size_t>(r0 + lane) * w.Wp + word] = static_cast<uint64_t>(hi) << 32 | lo;
 }
+
 
 // K2: one wave per candidate.  Touched-node slots live in registers, one per
 // lane (64; a candidate touching more distinct nodes is rerun with 512), and
 // CH*64 bitmask words per row are held as a register-resident touched mask
 // (lane l owns words ch*64 + l).
 //
-// The feasibility of pod p against the base snapshot is evaluated here, 64
-// words (4096 spot nodes) at a time: F = S[class] & T[cpu] & T[mem] & T[eph]
-// (encode.cpp).  The table rows are small and L2-resident, so no dense P x N
-// bitmask is ever written: a pod's chunk costs four 512-B row reads.
+// The feasibility of pod p against the base snapshot is evaluated here: F =
+// S[class] & T[cpu] & T[mem] & T[eph] (encode.cpp), whose rows are small and
+// L2-resident, so no dense P x N bitmask is ever written.  First fit almost
+// always lands on the first few spot nodes, so only the head of a pod's rows
+// (32 words = 2048 nodes, 1 KB for all four rows) is prefetched; a pod with no
+// answer in the head scans whole 64-word chunks synchronously (rare, and
+// once per failing candidate).
 //
 // It is one dependent chain per candidate, so it is built for latency: every
 // load inside the pod loop is an LDS-DMA (global_load_lds) whose completion
 // is waited for by hand with counted `s_waitcnt vmcnt(N)`:
-//   - chunk 0 of the four rows of pods p+1..p+3 is always in flight (4-slot
-//     LDS ring, 2 DMAs per pod);
+//   - the heads of pods k+1..k+7 are in flight (8-slot LDS ring, one DMA per
+//     pod);
 //   - the base record of the next pod's first untouched feasible node is
 //     fetched one pod ahead (speculative; used when the pod opens a new slot
 //     on a node >= kNodeCache; nodes below that come from an LDS cache);
 //   - the candidate's pod records are staged before the loop (128-pod window,
 //     restaged per 64 pods for larger candidates).
-// DMA issue order per step k (fixed): ... spec(k+1), rows(k+4) x2.  At the end
-// of step k, rows(k+1) has at most 6 younger DMAs (5 at k = 0) and every wait
-// below is for "all but the N youngest" -> vmcnt(5) is safe for every k;
-// spec(k) has exactly the two rows(k+3) DMAs younger when step k consumes it
-// -> vmcnt(2).  Rare-path DMAs are always followed by vmcnt(0), which never
-// weakens a later count.
+// DMA issue order: prologue heads 0..6, spec(0), head 7; then per step k:
+// spec(k+1), head(k+8).  vmcnt(N) waits for all but the N youngest, so the
+// head of pod k+1 at the end of step k needs N <= min(k + 7, 12) and spec(k)
+// in step k needs N <= 1.  Rare-path DMAs are always followed by vmcnt(0),
+// which never weakens a later count.
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef __attribute__((address_space(1))) void* gbl_vp;
 #define SR_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
+// Winner: d_min[0] = packed first drainable candidate (possibly reduced over
+// ranks), d_min[1] = packed first fallback; the winner's mapping is copied
+// only by the rank that owns it.  `result` lives in mapped host memory: the
+// data first, then (after a system-scope fence) the run's sequence number,
+// which the host polls.
+__device__ __forceinline__ void write_winner(const DevWorkload& w) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long* dm = reinterpret_cast<const unsigned long long*>(w.d_min);
+  const unsigned long long ok = __hip_atomic_load(dm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long fb = __hip_atomic_load(dm + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int* r = w.result;
+  const bool any = ok != ~0ull;
+  const int g = any ? static_cast<int>(ok >> 32) : -1;
+  const int li = any ? static_cast<int>(ok & 0xffffffffu) : -1;
+  const bool local = any && li < w.n_cand && w.cand_global[li] == g;
+  const int off = local ? w.cand_off[li] : 0;
+  const int np = local ? w.cand_off[li + 1] - off : 0;
+  auto put = [&](int i, int v) { __hip_atomic_store(r + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+  for (int q = lane; q < np; q += 64)
+    put(kResultHeader + q, __hip_atomic_load(w.out_node + off + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (lane == 0) {
+    put(0, g);
+    put(1, local ? 1 : 0);
+    put(2, np);
+    put(3, fb == ~0ull ? -1 : static_cast<int>(fb >> 32));
+  }
+  SR_WAIT_VM(0);  // the data is acknowledged before the sequence number goes out
+  if (lane == 0) put(4, w.seq);
+}
+
+// K3: one wave (after the collective on multi-GPU runs).
+__global__ __launch_bounds__(64) void k3_winner(DevWorkload w) { write_winner(w); }
+
+constexpr int kHead = 32;       // head of a pod's rows prefetched per step: words [0, 32) = nodes [0, 2048)
+constexpr int kRing = 8;        // head ring: pods k..k+7 (rows of pod k+8 issued at the end of step k)
 constexpr int kPodWin = 128;    // pod records staged per wave: two 64-pod halves
 constexpr int kRecU64 = 6;      // {cpu, memory, ephemeral, ports, S | T cpu row offset, T mem | T eph row offset}
 constexpr int kNodeCache = 16;  // base records of spot nodes [0, 16) kept in LDS
 constexpr int kMaxPods = 512;   // pods per candidate on the device (encode.cpp: more -> fallback)
 
 struct K2Lds {
-  uint64_t ring[4][256];            // chunk 0 of {S, T cpu, T mem, T eph} rows of pods k..k+3
-  uint64_t chunk[256];              // rare: chunk > 0 of the current pod's rows
+  uint64_t ring[kRing][4 * kHead];  // head of the {S, T cpu, T mem, T eph} rows of pods k..k+7
+  uint64_t chunk[256];              // rare: a full 64-word chunk of the current pod's rows
   uint64_t pods[kPodWin][kRecU64];  // pod record window
   uint64_t cache[kNodeCache][8];    // base node records
   uint64_t spec[8];                 // speculative node record
@@ -183,6 +276,18 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
     const uint64_t* pr = L.pods[q & (kPodWin - 1)];
     dma_rows(dst, pr[4], pr[5], base);
   };
+  // head (kHead words) of the four rows: 16 lanes per row, one DMA -> dst[4][kHead]
+  auto dma_head = [&](uint64_t* dst, uint64_t r01, uint64_t r23) {
+    const int r = lane >> 4;
+    const uint32_t wi = static_cast<uint32_t>(min(2 * (lane & 15), Wp - 2));
+    const uint64_t rr = r < 2 ? r01 : r23;
+    const uint32_t off = (r & 1) ? static_cast<uint32_t>(rr >> 32) : static_cast<uint32_t>(rr);
+    dma(tab + (static_cast<uint64_t>(off) + wi), dst);
+  };
+  auto dma_head_of = [&](uint64_t* dst, int q) {
+    const uint64_t* pr = L.pods[q & (kPodWin - 1)];
+    dma_head(dst, pr[4], pr[5]);
+  };
   auto dma_rec = [&](uint64_t* dst, int node) {
     if (lane < 4) dma(w.node_rec + static_cast<size_t>(node == INT_MAX ? 0 : node) * 8 + 2 * lane, dst);
   };
@@ -211,23 +316,24 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
   int nslots = 0;
   uint64_t cyc_t = 0;
   auto cyc = [&]() -> uint64_t { return PROF ? __builtin_amdgcn_s_memtime() : 0ull; };
-  const uint64_t lane_mask = lane < Wp ? ~0ull : 0ull;
+  const uint64_t lane_mask = lane < min(Wp, kHead) ? ~0ull : 0ull;
 
-  // State of the next pod, gathered in one batch of LDS reads once its rows
-  // have landed: its chunk-0 feasibility word, first untouched feasible node,
-  // request, and the S-row bit of every touched node.
+  // State of the next pod, gathered in one batch of LDS reads once its head
+  // has landed: its head feasibility word, first untouched feasible node in
+  // the head, request, and the S-row bit of every touched node in the head.
   uint64_t word_next = 0;
   int cnode0 = INT_MAX;
   int64_t nrc = 0, nrm = 0, nre = 0;
   uint64_t npm = 0;
   bool sbit[SPL];
   auto gather_next = [&](int kn) {
-    const uint64_t* img = L.ring[kn & 3];
+    const uint64_t* img = L.ring[kn & (kRing - 1)];
     const uint64_t* pr = L.pods[kn & (kPodWin - 1)];
     uint64_t sw[SPL];
 #pragma unroll
-    for (int s = 0; s < SPL; ++s) sw[s] = img[snode[s] < 4096 ? snode[s] >> 6 : 0];
-    const uint64_t a = img[lane] & img[64 + lane] & img[128 + lane] & img[192 + lane];
+    for (int s = 0; s < SPL; ++s) sw[s] = img[snode[s] < 64 * kHead ? snode[s] >> 6 : 0];
+    const int hl = lane & (kHead - 1);
+    const uint64_t a = img[hl] & img[kHead + hl] & img[2 * kHead + hl] & img[3 * kHead + hl];
     nrc = static_cast<int64_t>(pr[0]);
     nrm = static_cast<int64_t>(pr[1]);
     nre = static_cast<int64_t>(pr[2]);
@@ -236,7 +342,7 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
     for (int s = 0; s < SPL; ++s) sbit[s] = (sw[s] >> (snode[s] & 63)) & 1ull;
     word_next = a & lane_mask;
     const uint64_t clean0 = word_next & ~touched[0];
-    const uint64_t mc0 = __ballot(clean0 != 0);
+    const uint64_t mc0 = ballot(clean0 != 0);
     cnode0 = INT_MAX;
     if (mc0) {
       const int L0 = __builtin_ctzll(mc0);
@@ -244,18 +350,19 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
     }
   };
 
-  // prologue: node cache + pod window, then rows 0..2, (row 0 landed) spec(0), row 3
+  // prologue: node cache + pod window, then heads 0..6, (head 0 landed)
+  // spec(0), head 7.  DMA order per step k afterwards: spec(k+1), head(k+8).
+  static_assert(kRing == 8, "the vmcnt immediates below assume an 8-deep ring");
   dma(w.node_rec + 2 * lane, L.cache[0]);
   dma_pods(0);
   if (np > 64) dma_pods(1);
   SR_WAIT_VM(0);
-  dma_rows_of(L.ring[0], 0, 0);
-  dma_rows_of(L.ring[1], min(1, np - 1), 0);
-  dma_rows_of(L.ring[2], min(2, np - 1), 0);
-  SR_WAIT_VM(4);
+#pragma unroll
+  for (int j = 0; j < kRing - 1; ++j) dma_head_of(L.ring[j], min(j, np - 1));
+  SR_WAIT_VM(6);  // head 0: heads 1..6 are younger
   gather_next(0);
   dma_rec(L.spec, cnode0);
-  dma_rows_of(L.ring[3], min(3, np - 1), 0);
+  dma_head_of(L.ring[kRing - 1], min(kRing - 1, np - 1));
 
   status = -1;
   int k = 0;
@@ -264,13 +371,13 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
     const int64_t rc = nrc, rm = nrm, re = nre;
     const uint64_t pm = npm;
     const bool zero = (rc | rm | re) == 0;  // fitsRequest skips the resource checks
-    // Chunk 0 (spot nodes [0, 4096)): touched nodes below the first untouched
+    // Head (spot nodes [0, 2048)): touched nodes below the first untouched
     // feasible one, rechecked branch-free: class bit from the S row, capacity /
     // pod count / host ports from the candidate's own state (which implies the
     // base T rows, base pod count and base ports).
     int ans;
     {
-      const int hi = min(cnode0, 4096);
+      const int hi = min(cnode0, 64 * kHead);
       int best = INT_MAX;
 #pragma unroll
       for (int s = 0; s < SPL; ++s) {
@@ -279,7 +386,7 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
         const bool ok = (nd < hi) & sbit[s] & (sleft[s] >= 1) & ((sport[s] & pm) == 0) & fit;
         best = ok ? min(best, nd) : best;
       }
-      const uint64_t hb = __ballot(best != INT_MAX);
+      const uint64_t hb = ballot(best != INT_MAX);
       int dnode = INT_MAX;
       if (hb) {
         dnode = (hb & (hb - 1)) ? wave_min(best) : __builtin_amdgcn_readlane(best, __builtin_ctzll(hb));
@@ -287,36 +394,40 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
       }
       ans = min(cnode0, dnode);
     }
-    // rare: the pod's first 4096 spot nodes hold no answer
+    // rare: nothing in the head; scan whole 64-word chunks (the head again
+    // included, which cannot change the outcome)
+    if (ans == INT_MAX && Wp > kHead) {
 #pragma unroll
-    for (int ch = 1; ch < CH; ++ch) {
-      const int base = ch * 64;
-      if (ans != INT_MAX || base >= Wp) continue;  // wave-uniform; keeps the loop unrollable
-      if (PROF) ++st.n_far;
-      dma_rows_of(L.chunk, k, base);
-      SR_WAIT_VM(0);
-      const uint64_t* img = L.chunk;
-      const uint64_t clean = (img[lane] & img[64 + lane] & img[128 + lane] & img[192 + lane]) &
-                             ((base + lane < Wp) ? ~touched[ch] : 0ull);
-      const uint64_t mc = __ballot(clean != 0);
-      int cnode = INT_MAX;
-      if (mc) {
-        const int L0 = __builtin_ctzll(mc);
-        cnode = (base + L0) * 64 + __builtin_ctzll(readlane64(clean, L0));
-      }
-      const int lo = base * 64;
-      const int hi = min(cnode, lo + 64 * 64);
-      int best = INT_MAX;
+      for (int ch = 0; ch < CH; ++ch) {
+        const int base = ch * 64;
+        if (ans != INT_MAX || base >= Wp) continue;  // wave-uniform; keeps the loop unrollable
+        if (PROF) ++st.n_far;
+        dma_rows_of(L.chunk, k, base);
+        SR_WAIT_VM(0);
+        const uint64_t* img = L.chunk;
+        const uint64_t clean = (img[lane] & img[64 + lane] & img[128 + lane] & img[192 + lane]) &
+                               ((base + lane < Wp) ? ~touched[ch] : 0ull);
+        const uint64_t mc = ballot(clean != 0);
+        int cnode = INT_MAX;
+        if (mc) {
+          const int L0 = __builtin_ctzll(mc);
+          cnode = (base + L0) * 64 + __builtin_ctzll(readlane64(clean, L0));
+        }
+        const int lo = base * 64;
+        const int hi = min(cnode, lo + 64 * 64);
+        int best = INT_MAX;
 #pragma unroll
-      for (int s = 0; s < SPL; ++s) {
-        const int nd = snode[s];
-        const bool in = (nd >= lo) & (nd < hi);
-        const uint64_t sw = img[in ? (nd >> 6) - base : 0];
-        const bool fit = zero | ((rc <= scpu[s]) & (rm <= smem[s]) & (re <= seph[s]));
-        const bool ok = in & (((sw >> (nd & 63)) & 1ull) != 0) & (sleft[s] >= 1) & ((sport[s] & pm) == 0) & fit;
-        best = ok ? min(best, nd) : best;
+        for (int s = 0; s < SPL; ++s) {
+          const int nd = snode[s];
+          const bool in = (nd >= lo) & (nd < hi);
+          const uint64_t sw = img[in ? (nd >> 6) - base : 0];
+          const bool fit = zero | ((rc <= scpu[s]) & (rm <= smem[s]) & (re <= seph[s]));
+          const bool ok =
+              in & (((sw >> (nd & 63)) & 1ull) != 0) & (sleft[s] >= 1) & ((sport[s] & pm) == 0) & fit;
+          best = ok ? min(best, nd) : best;
+        }
+        ans = min(cnode, wave_min(best));
       }
-      ans = min(cnode, wave_min(best));
     }
     if (PROF) {
       const uint64_t t = cyc();
@@ -342,7 +453,7 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
         hit = true;
       }
     }
-    if (!__any(hit)) {
+    if (!(ballot(hit) != 0)) {
       const int ns = nslots++;
       if (ns >= 64 * SPL) {  // slots exhausted: rerun with more
         SR_WAIT_VM(0);
@@ -352,7 +463,7 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
       if (ans < kNodeCache) {
         rec = L.cache[ans];
       } else if (ans == cnode0) {
-        SR_WAIT_VM(2);  // spec(k): only rows(k+3) are younger
+        SR_WAIT_VM(1);  // spec(k): only head(k+7) is younger
         rec = L.spec;
       } else {  // rare: not the speculated node
         if (PROF) ++st.n_spec_miss;
@@ -385,14 +496,19 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
       st.cyc_b += t - cyc_t;
       cyc_t = t;
     }
-    // next pod: its rows (<= 6 younger DMAs), its state, its speculative
-    // record, rows of pod k + 4
+    // next pod: its head (issued at the end of step k - 6: min(k + 7, 12)
+    // younger DMAs), its state, its speculative record, head of pod k + 8
     if (k + 1 < np) {
-      const int q = min(k + 4, np - 1);
-      const bool restage = q == k + 4 && (q & 63) == 0 && q >= kPodWin;
-      if (restage) dma_pods(q >> 6);  // window: records [q, q + 64) replace [q - 128, q - 64)
-      SR_WAIT_VM(5);
-      if (restage) SR_WAIT_VM(0);
+      const int q = min(k + kRing, np - 1);
+      const bool restage = q == k + kRing && (q & 63) == 0 && q >= kPodWin;
+      if (restage) {  // window: records [q, q + 64) replace [q - 128, q - 64)
+        dma_pods(q >> 6);
+        SR_WAIT_VM(0);
+      } else if (k >= 5) {
+        SR_WAIT_VM(12);
+      } else {
+        SR_WAIT_VM(7);
+      }
       if (PROF) {
         const uint64_t t = cyc();
         st.cyc_c += t - cyc_t;
@@ -402,7 +518,7 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
       const uint64_t r01 = pq[4], r23 = pq[5];
       gather_next(k + 1);
       dma_rec(L.spec, cnode0);  // L.spec's last reads (this step) have returned
-      dma_rows(L.ring[k & 3], r01, r23, 0);
+      dma_head(L.ring[k & (kRing - 1)], r01, r23);
       if (PROF) st.cyc_d += cyc() - cyc_t;
     }
   }
@@ -459,28 +575,6 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   }
 }
 
-// K3: one wave.  d_min[0] = packed first drainable candidate (possibly reduced
-// over ranks), d_min[1] = packed first fallback; the winner's mapping is
-// copied only by the rank that owns it.  `result` lives in mapped host memory.
-__global__ __launch_bounds__(64) void k3_winner(DevWorkload w) {
-  const unsigned long long* dm = reinterpret_cast<const unsigned long long*>(w.d_min);
-  const unsigned long long ok = dm[0], fb = dm[1];
-  int* r = w.result;
-  const bool any = ok != ~0ull;
-  const int g = any ? static_cast<int>(ok >> 32) : -1;
-  const int li = any ? static_cast<int>(ok & 0xffffffffu) : -1;
-  const bool local = any && li < w.n_cand && w.cand_global[li] == g;
-  const int off = local ? w.cand_off[li] : 0;
-  const int np = local ? w.cand_off[li + 1] - off : 0;
-  for (int q = threadIdx.x; q < np; q += 64) r[4 + q] = w.out_node[off + q];
-  if (threadIdx.x == 0) {
-    r[0] = g;
-    r[1] = local ? 1 : 0;
-    r[2] = np;
-    r[3] = fb == ~0ull ? -1 : static_cast<int>(fb >> 32);
-  }
-}
-
 template <bool PROF>
 hipError_t launch_k2(const DevWorkload& w, hipStream_t s) {
   const int n = w.n_list;
@@ -501,10 +595,10 @@ hipError_t launch_k2(const DevWorkload& w, hipStream_t s) {
 
 hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hipStream_t s) {
   const int s_blocks = (w.n_classes + 3) / 4;
-  const int t_groups = (w.n_t + 63) / 64;
-  const int wblocks = (w.Wp + 3) / 4;
-  const unsigned blocks = static_cast<unsigned>(std::max(1, s_blocks + t_groups * wblocks));
-  hipLaunchKernelGGL(k0_tables, dim3(blocks), dim3(256), 0, s, w, s_blocks, wblocks, local_first_fallback);
+  int t_waves = 0;
+  for (int d = 0; d < 4; ++d) t_waves += (w.t_off[d + 1] - w.t_off[d] + 63) / 64 * w.Wp;
+  const unsigned blocks = static_cast<unsigned>(std::max(1, s_blocks + (t_waves + 3) / 4));
+  hipLaunchKernelGGL(k0_tables, dim3(blocks), dim3(256), 0, s, w, s_blocks, local_first_fallback);
   return hipGetLastError();
 }
 

@@ -7,6 +7,9 @@
 
 namespace sr {
 
+constexpr int kResultHeader = 8;
+constexpr size_t kK0ProfWaves = 32768;  // K0 waves profiled after K2's [n_cand][16] records  // int32 words before the winner's mapping in `result`
+
 // Pointers into the device arena (layout: DESIGN.md §HBM layout).
 struct DevWorkload {
   int32_t n_spot, n_pad, Wp;
@@ -16,17 +19,11 @@ struct DevWorkload {
   const uint64_t* node_rec;    // [n_pad][8] AoS {free cpu, mem, eph, ports, pods_left, 0, 0, 0} for K2
   int32_t n_atoms;
   const uint64_t* atoms;       // [n_atoms][Wp] node bitsets (encode.cpp)
-  const int32_t* cls_and_off;  // class atom programs (CSR)
-  const int32_t* cls_and;
-  const int32_t* cls_not_off;
-  const int32_t* cls_not;
-  const int32_t* cls_term_off;
-  const int32_t* term_atom_off;
-  const int32_t* term_atoms;
-  const int32_t* cls_flags;
+  const int32_t* cls_prog_off; // class atom programs (CSR): ops atom << 2 | {AND, AND NOT,
+  const int32_t* cls_prog;     //   open an ORed term, AND into the open term}
   int32_t n_classes;
-  int32_t n_t;              // threshold rows (row 0 = every node)
-  const int32_t* t_dim;     // 0 cpu, 1 memory, 2 ephemeral, 3 all
+  int32_t n_t;              // threshold rows: row 0 = every node, then cpu, memory,
+  int32_t t_off[5];         //   ephemeral rows [t_off[d + 1], t_off[d + 2]) in threshold order
   const int64_t* t_thr;
   int32_t n_pods;
   const uint64_t* pod_rec;  // [n_pods + 128][6] AoS {cpu, memory, ephemeral, ports, S | T cpu row word
@@ -42,15 +39,18 @@ struct DevWorkload {
   int32_t* out_node;   // [n_pods] spot position or -1
   int32_t* out_status; // [n_cand]
   int32_t* d_min;      // 2 x u64 packed {global << 32 | local}: first ok, first fallback (~0 = none)
-  int32_t* result;     // mapped host memory [4 + max pods] {winner, local, npods, first_fallback, mapping...}
-  uint64_t* prof;      // optional [n_cand][16] K2 per-wave profile (SR_K2_PROFILE), else null
+  int32_t* result;     // mapped host memory [kResultHeader + max pods]
+                       //   {winner, local, npods, first_fallback, seq, mapping...}
+  int32_t seq;         // run sequence number written last into result[4]
+  uint64_t* prof;      // optional [n_cand][16] K2 + [kK0ProfWaves][2] K0 per-wave profile
+                       // (SR_K2_PROFILE), else null
 };
 
 // K0: S and T rows (also resets d_min: d_min[1] = local first fallback).
 hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hipStream_t s);
 // K2: per-candidate feasibility rows + first-fit placement; atomicMin of first_ok into d_min[0].
 hipError_t launch_placement(const DevWorkload& w, hipStream_t s);
-// K3: winner mapping into `result`.
+// K3: winner mapping into `result` (after the collective when ranks > 1), then the run's seq.
 hipError_t launch_winner(const DevWorkload& w, hipStream_t s);
 
 }  // namespace sr

@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <cstdio>
@@ -44,7 +45,12 @@ struct sr_ctx {
   sr::DevWorkload dw{};
   bool prepared = false;
   int32_t timing = 0;
-  hipEvent_t ev[8] = {};
+  // HIP event pairs bracketing timed kernels, read back lazily (flush_timing)
+  // so a timed run does not have to synchronise the stream.
+  std::vector<hipEvent_t> ev_start, ev_end;
+  std::vector<int8_t> ev_kernel;
+  size_t ev_used = 0;
+  int32_t seq = 0;
   sr_timing t{};
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -129,11 +135,8 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t o_fc = pk.add(w.free_cpu), o_fm = pk.add(w.free_mem), o_fe = pk.add(w.free_eph);
   const size_t o_nr = pk.add(w.node_rec);
   const size_t o_at = pk.add(w.atoms);
-  const size_t o_cao = pk.add(w.cls_and_off), o_ca = pk.add(w.cls_and);
-  const size_t o_cno = pk.add(w.cls_not_off), o_cn = pk.add(w.cls_not);
-  const size_t o_cto = pk.add(w.cls_term_off), o_tao = pk.add(w.term_atom_off), o_ta = pk.add(w.term_atoms);
-  const size_t o_cf = pk.add(w.cls_flags);
-  const size_t o_td = pk.add(w.t_dim), o_tt = pk.add(w.t_thr);
+  const size_t o_cpo = pk.add(w.cls_prog_off), o_cp = pk.add(w.cls_prog);
+  const size_t o_tt = pk.add(w.t_thr);
   const size_t o_prec = pk.add(w.pod_rec);
   const size_t o_co = pk.add(w.cand_off), o_cg = pk.add(w.cand_global);
   const size_t o_ls = pk.add(w.list);
@@ -148,7 +151,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, dev_reserve(ctx->out_node, sizeof(int32_t) * std::max(1, na)));
   HIP_TRY(ctx, dev_reserve(ctx->out_status, sizeof(int32_t) * std::max(1, ncand)));
   HIP_TRY(ctx, dev_reserve(ctx->dmin, 64));
-  const size_t res_bytes = sizeof(int32_t) * (4 + static_cast<size_t>(std::max(1, w.max_cand_pods)));
+  const size_t res_bytes = sizeof(int32_t) * (sr::kResultHeader + static_cast<size_t>(std::max(1, w.max_cand_pods)));
   HIP_TRY(ctx, host_reserve(ctx->h_result, res_bytes));  // mapped: K3 writes the result straight to the host
   auto t1 = std::chrono::steady_clock::now();
   pk.copy_to(static_cast<char*>(ctx->h_arena.p));
@@ -169,17 +172,11 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.node_rec = static_cast<const uint64_t*>(at(o_nr));
   d.n_atoms = w.n_atoms;
   d.atoms = static_cast<const uint64_t*>(at(o_at));
-  d.cls_and_off = static_cast<const int32_t*>(at(o_cao));
-  d.cls_and = static_cast<const int32_t*>(at(o_ca));
-  d.cls_not_off = static_cast<const int32_t*>(at(o_cno));
-  d.cls_not = static_cast<const int32_t*>(at(o_cn));
-  d.cls_term_off = static_cast<const int32_t*>(at(o_cto));
-  d.term_atom_off = static_cast<const int32_t*>(at(o_tao));
-  d.term_atoms = static_cast<const int32_t*>(at(o_ta));
-  d.cls_flags = static_cast<const int32_t*>(at(o_cf));
+  d.cls_prog_off = static_cast<const int32_t*>(at(o_cpo));
+  d.cls_prog = static_cast<const int32_t*>(at(o_cp));
   d.n_classes = w.n_classes;
   d.n_t = static_cast<int32_t>(w.t_dim.size());
-  d.t_dim = static_cast<const int32_t*>(at(o_td));
+  for (int i = 0; i < 5; ++i) d.t_off[i] = w.t_off[i];
   d.t_thr = static_cast<const int64_t*>(at(o_tt));
   d.n_pods = na;
   d.pod_rec = static_cast<const uint64_t*>(at(o_prec));
@@ -195,8 +192,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.d_min = static_cast<int32_t*>(ctx->dmin.p);
   d.prof = nullptr;
   if (ctx->prof_file) {
-    HIP_TRY(ctx, dev_reserve(ctx->prof, sizeof(uint64_t) * 16 * std::max(1, ncand)));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->prof.p, 0, sizeof(uint64_t) * 16 * std::max(1, ncand), ctx->stream));
+    const size_t pbytes = sizeof(uint64_t) * (16 * static_cast<size_t>(std::max(1, ncand)) + 2 * sr::kK0ProfWaves);
+    HIP_TRY(ctx, dev_reserve(ctx->prof, pbytes));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->prof.p, 0, pbytes, ctx->stream));
     d.prof = static_cast<uint64_t*>(ctx->prof.p);
   }
   void* dres = nullptr;
@@ -206,11 +204,11 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
   // K0 algorithmic bytes: every table row written once; every atom row a class
   // program names, the nodes' free capacities and the thresholds read once.
-  uint64_t atom_reads = w.cls_and.size() + w.cls_not.size() + w.term_atoms.size();
-  ctx->t.bytes_tables = n_rows * row + atom_reads * row + 3ull * 8 * w.n_pad + 12ull * w.t_dim.size();
+  uint64_t atom_reads = w.cls_prog.size();
+  ctx->t.bytes_tables = n_rows * row + atom_reads * row + 3ull * 8 * w.n_pad + 8ull * w.t_dim.size();
   // K2 (upper bound until a full run refines it, see run()): per pod its
   // four row chunks and its record, per candidate its mapping and status.
-  ctx->t.bytes_placement = static_cast<uint64_t>(na) * (32ull * std::min(w.Wp, 64) + 48 + 4) + 4ull * ncand;
+  ctx->t.bytes_placement = static_cast<uint64_t>(na) * (32ull * std::min(w.Wp, 32) + 48 + 4) + 4ull * ncand;
   ctx->t.ms_pack_host = std::chrono::duration<double, std::milli>(t1 - t0).count();
   ctx->t.ms_upload = std::chrono::duration<double, std::milli>(t2 - t1).count();
   ctx->t.n_pods = na;
@@ -224,26 +222,70 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   return SR_OK;
 }
 
+sr_status flush_timing(sr_ctx* ctx) {
+  if (ctx->ev_used == 0) return SR_OK;
+  HIP_TRY(ctx, hipEventSynchronize(ctx->ev_end[ctx->ev_used - 1]));
+  double* sums[3] = {&ctx->t.ms_tables, &ctx->t.ms_placement, &ctx->t.ms_winner};
+  for (size_t i = 0; i < ctx->ev_used; ++i) {
+    float ms = 0;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev_start[i], ctx->ev_end[i]));
+    *sums[ctx->ev_kernel[i]] += ms;
+  }
+  ctx->ev_used = 0;
+  return SR_OK;
+}
+
 sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   if (!ctx->prepared) {
     ctx->err = "sr_plan_run before sr_plan_prepare";
     return SR_ERR_STATE;
   }
   const sr::Workload& w = ctx->wl;
-  const sr::DevWorkload& d = ctx->dw;
+  sr::DevWorkload& d = ctx->dw;
   hipStream_t s = ctx->stream;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  auto mark = [&](int k, int end) -> hipError_t {
-    return (ctx->timing >> k & 1) ? hipEventRecord(ctx->ev[2 * k + end], s) : hipSuccess;
+  const bool collective = ctx->comm && use_comm;
+  d.seq = ++ctx->seq;
+  volatile int32_t* res = static_cast<volatile int32_t*>(ctx->h_result.p);
+  res[4] = 0;
+  size_t pair[3] = {0, 0, 0};
+  auto mark = [&](int k, int end) -> sr_status {
+    if (!(ctx->timing >> k & 1)) return SR_OK;
+    if (!end) {
+      if (ctx->ev_used == ctx->ev_start.size()) {
+        if (ctx->ev_used >= 3072) {  // bounded pool: read back what is pending
+          sr_status st = flush_timing(ctx);
+          if (st != SR_OK) return st;
+        } else {
+          hipEvent_t a, b;
+          HIP_TRY(ctx, hipEventCreate(&a));
+          HIP_TRY(ctx, hipEventCreate(&b));
+          ctx->ev_start.push_back(a);
+          ctx->ev_end.push_back(b);
+          ctx->ev_kernel.push_back(0);
+        }
+      }
+      pair[k] = ctx->ev_used++;
+      ctx->ev_kernel[pair[k]] = static_cast<int8_t>(k);
+      HIP_TRY(ctx, hipEventRecord(ctx->ev_start[pair[k]], s));
+    } else {
+      HIP_TRY(ctx, hipEventRecord(ctx->ev_end[pair[k]], s));
+    }
+    return SR_OK;
   };
-  HIP_TRY(ctx, mark(0, 0));
+#define MARK(k, e)                      \
+  do {                                  \
+    sr_status _st = mark((k), (e));     \
+    if (_st != SR_OK) return _st;       \
+  } while (0)
+  MARK(0, 0);
   HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s));
-  HIP_TRY(ctx, mark(0, 1));
-  HIP_TRY(ctx, mark(1, 0));
+  MARK(0, 1);
+  MARK(1, 0);
   HIP_TRY(ctx, sr::launch_placement(d, s));
-  HIP_TRY(ctx, mark(1, 1));
-  HIP_TRY(ctx, mark(2, 0));
-  if (ctx->comm && use_comm) {
+  MARK(1, 1);
+  MARK(2, 0);
+  if (collective) {
     ncclResult_t r = ncclAllReduce(d.d_min, d.d_min, 2, ncclUint64, ncclMin, ctx->comm, s);
     if (r != ncclSuccess) {
       ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
@@ -251,41 +293,49 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     }
   }
   HIP_TRY(ctx, sr::launch_winner(d, s));
+  MARK(2, 1);
+#undef MARK
+  if (ctx->timing) ctx->t.n_runs += 1;
   const int32_t na = d.n_pods, ncand = d.n_cand;
-  if (full) {
-    HIP_TRY(ctx, host_reserve(ctx->h_status, sizeof(int32_t) * std::max(1, ncand)));
-    HIP_TRY(ctx, host_reserve(ctx->h_node, sizeof(int32_t) * std::max(1, na)));
-    if (ncand)
-      HIP_TRY(ctx, hipMemcpyAsync(ctx->h_status.p, d.out_status, sizeof(int32_t) * ncand, hipMemcpyDeviceToHost, s));
-    if (na) HIP_TRY(ctx, hipMemcpyAsync(ctx->h_node.p, d.out_node, sizeof(int32_t) * na, hipMemcpyDeviceToHost, s));
-  }
-  HIP_TRY(ctx, mark(2, 1));
-  HIP_TRY(ctx, hipStreamSynchronize(s));
-  if (ctx->timing) {
-    double* sums[3] = {&ctx->t.ms_tables, &ctx->t.ms_placement, &ctx->t.ms_winner};
-    for (int k = 0; k < 3; ++k) {
-      if (!(ctx->timing >> k & 1)) continue;
-      float ms = 0;
-      HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev[2 * k], ctx->ev[2 * k + 1]));
-      *sums[k] += ms;
+  if (full || ctx->prof_file) {
+    if (full) {
+      HIP_TRY(ctx, host_reserve(ctx->h_status, sizeof(int32_t) * std::max(1, ncand)));
+      HIP_TRY(ctx, host_reserve(ctx->h_node, sizeof(int32_t) * std::max(1, na)));
+      if (ncand)
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_status.p, d.out_status, sizeof(int32_t) * ncand, hipMemcpyDeviceToHost, s));
+      if (na) HIP_TRY(ctx, hipMemcpyAsync(ctx->h_node.p, d.out_node, sizeof(int32_t) * na, hipMemcpyDeviceToHost, s));
     }
-    ctx->t.n_runs += 1;
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+  } else {
+    // The result's last word is this run's sequence number, written after a
+    // system-scope fence: poll it instead of waking up on stream completion.
+    // A run that has not finished after 100 ms falls back to the stream
+    // (which also surfaces a kernel fault as an error).
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t spins = 0;
+    while (res[4] != d.seq) {
+      if ((++spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100)) {
+        HIP_TRY(ctx, hipStreamSynchronize(s));
+        break;
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
   }
 
   if (ctx->prof_file && ncand > 0) {  // diagnostics only (tools/k2_profile.py)
-    std::vector<uint64_t> pr(static_cast<size_t>(ncand) * 16);
+    std::vector<uint64_t> pr(static_cast<size_t>(ncand) * 16 + 2 * sr::kK0ProfWaves);
     HIP_TRY(ctx, hipMemcpy(pr.data(), d.prof, pr.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    const int64_t hdr[2] = {ncand, d.Wp};
+    const int64_t hdr[2] = {ncand, static_cast<int64_t>(sr::kK0ProfWaves)};
     std::fwrite(hdr, sizeof(hdr), 1, ctx->prof_file);
     std::fwrite(pr.data(), sizeof(uint64_t), pr.size(), ctx->prof_file);
     std::fflush(ctx->prof_file);
   }
-  const int32_t* r = static_cast<const int32_t*>(ctx->h_result.p);
+  const int32_t* r = const_cast<const int32_t*>(res);
   out->first_ok = r[0];
   out->first_fallback = r[3];
   out->winner = (r[0] >= 0 && (r[3] < 0 || r[3] > r[0])) ? r[0] : -1;
   out->winner_npods = r[1] ? r[2] : 0;
-  if (out->winner_map && r[1]) std::memcpy(out->winner_map, r + 4, sizeof(int32_t) * r[2]);
+  if (out->winner_map && r[1]) std::memcpy(out->winner_map, r + sr::kResultHeader, sizeof(int32_t) * r[2]);
   out->checks = static_cast<uint64_t>(na) * static_cast<uint64_t>(w.n_spot);
   out->fallback_pods = w.fallback_pods;
   if (full) {
@@ -297,7 +347,7 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     }
     // exact K2 algorithmic bytes: pods up to and including the failing one
     uint64_t k2 = 4ull * ncand;
-    const uint64_t per_pod = 32ull * std::min(w.Wp, 64) + 48;
+    const uint64_t per_pod = 32ull * std::min(w.Wp, 32) + 48;
     for (int32_t k = 0; k < ncand; ++k) {
       const int32_t np = w.cand_off[k + 1] - w.cand_off[k];
       const int32_t done = hs[k] >= 0 ? std::min(np, hs[k] + 1) : np;
@@ -332,11 +382,6 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
     delete ctx;
     return SR_ERR_HIP;
   }
-  for (auto& e : ctx->ev)
-    if (hipEventCreate(&e) != hipSuccess) {
-      delete ctx;
-      return SR_ERR_HIP;
-    }
   if (const char* path = std::getenv("SR_K2_PROFILE")) ctx->prof_file = std::fopen(path, "ab");
   *out = ctx;
   return SR_OK;
@@ -351,8 +396,8 @@ void sr_destroy(sr_ctx* ctx) {
     if (b->p) (void)hipFree(b->p);
   for (HostBuf* b : {&ctx->h_arena, &ctx->h_result, &ctx->h_status, &ctx->h_node})
     if (b->p) (void)hipHostFree(b->p);
-  for (auto& e : ctx->ev)
-    if (e) (void)hipEventDestroy(e);
+  for (auto* v : {&ctx->ev_start, &ctx->ev_end})
+    for (hipEvent_t e : *v) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->prof_file) std::fclose(ctx->prof_file);
   delete ctx;
@@ -436,14 +481,18 @@ sr_status sr_can_drain_node(sr_ctx* ctx, sr_snapshot* snap, const sr_cluster* cl
 
 sr_status sr_set_timing(sr_ctx* ctx, int32_t mask) {
   if (!ctx) return SR_ERR_INVALID_ARG;
-  ctx->timing = mask & 15;
+  sr_status st = flush_timing(ctx);
+  if (st != SR_OK) return st;
+  ctx->timing = mask & 7;
   ctx->t.n_runs = 0;
   ctx->t.ms_tables = ctx->t.ms_placement = ctx->t.ms_winner = 0;
   return SR_OK;
 }
 
-sr_status sr_get_timing(const sr_ctx* ctx, sr_timing* out) {
+sr_status sr_get_timing(sr_ctx* ctx, sr_timing* out) {
   if (!ctx || !out) return SR_ERR_INVALID_ARG;
+  sr_status st = flush_timing(ctx);
+  if (st != SR_OK) return st;
   *out = ctx->t;
   return SR_OK;
 }

@@ -52,8 +52,8 @@ int main(int argc, char** argv) {
   printf("phases(ms): dims %.2f fallback+ports+taints %.2f pod-static %.2f classes %.2f nodes+atoms %.2f t-rows+pods %.2f lists %.2f (pod-static: keys %.2f; t-setup %.2f)\n",
          sr::encode_phase_ms[0], sr::encode_phase_ms[1], sr::encode_phase_ms[2], sr::encode_phase_ms[3],
          sr::encode_phase_ms[4], sr::encode_phase_ms[5], sr::encode_phase_ms[6], sr::encode_phase_ms[7], sr::encode_phase_ms[8]);
-  printf("Wp %d atoms %d classes %d cls_and %zu cls_not %zu terms %zu term_atoms %zu t_rows %zu\n", w.Wp, w.n_atoms,
-         w.n_classes, w.cls_and.size(), w.cls_not.size(), w.term_atom_off.size() - 1, w.term_atoms.size(), w.t_dim.size());
+  printf("Wp %d atoms %d classes %d program ops %zu t_rows %zu\n", w.Wp, w.n_atoms, w.n_classes, w.cls_prog.size(),
+         w.t_dim.size());
   int tc[4] = {0, 0, 0, 0};
   for (int d : w.t_dim) tc[d]++;
   printf("t rows: cpu %d mem %d eph %d all %d; max cand pods %d\n", tc[0], tc[1], tc[2], tc[3], w.max_cand_pods);

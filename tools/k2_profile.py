@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Summarise K2 per-wave profiles written with SR_K2_PROFILE=<file>.
 
-Each sr_plan_run appends {int64 n_cand, int64 Wp} + n_cand x 16 u64:
+Each sr_plan_run appends {int64 n_cand, int64 n_k0} + n_cand x 16 u64 (K2)
++ n_k0 x 2 u64 (K0 waves: start, end; zero = not launched):
   [0] s_memrealtime at wave start (100 MHz)   [1] = [0]
   [2] at the end                               [3] s_memtime cycles start->end
   [4] pod steps executed                       [5] 1 if rerun with 512 slots
@@ -17,17 +18,26 @@ import numpy as np
 
 def load(path):
     raw = np.fromfile(path, dtype=np.uint64)
-    runs, i = [], 0
+    runs, k0s, i = [], [], 0
     while i + 2 <= len(raw):
-        n = int(raw[i]); i += 2
+        n, m = int(raw[i]), int(raw[i + 1]); i += 2
         runs.append(raw[i:i + 16 * n].reshape(n, 16)); i += 16 * n
-    return runs
+        k0s.append(raw[i:i + 2 * m].reshape(m, 2)); i += 2 * m
+    return runs, k0s
 
 
 def main():
-    runs = load(sys.argv[1])
+    runs, k0s = load(sys.argv[1])
     r = runs[-1].astype(np.int64)
+    k0 = k0s[-1].astype(np.int64)
+    k0 = k0[k0[:, 0] > 0]
     t0 = r[:, 0].min()
+    if len(k0):
+        z = k0[:, 0].min()
+        print("K0 waves %d: start p50/p90/max %s us; duration p50/p90/max %s us; last end %.2f us; K2 first start %.2f us"
+              % (len(k0), " ".join("%.2f" % x for x in np.percentile((k0[:, 0] - z) / 100.0, [50, 90, 100])),
+                 " ".join("%.2f" % x for x in np.percentile((k0[:, 1] - k0[:, 0]) / 100.0, [50, 90, 100])),
+                 (k0[:, 1].max() - z) / 100.0, (t0 - z) / 100.0))
     start = (r[:, 0] - t0) / 100.0          # us
     pro = (r[:, 1] - r[:, 0]) / 100.0
     end = (r[:, 2] - t0) / 100.0
