@@ -526,6 +526,219 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
   return status >= 0 ? status : np;
 }
 
+// ------------------------------------------------------------ K2, node order
+// First fit in pod order (canDrainNode) equals first fit in NODE order: visit
+// the spot nodes in NodeInfoArray order and, at node n, consider the
+// candidate's unplaced pods in pod order, placing each one that fits n's
+// running state.  Every encoded predicate is node-local (a node's answer for
+// pod k depends only on the candidate's pods already placed on that node), so
+// by induction over k both orders place pod k on the same node: pods below k
+// have the same placements, hence every node presents the same state to k.
+// Each node is therefore visited at most once, at its base state, and only
+// base-feasible nodes (F = S & T & T & T) are worth visiting; a pod whose F
+// row has no bit left can never be placed: it is the failing pod once every
+// lower pod is placed, and pods above it are irrelevant (canDrainNode stops).
+//
+// One wave per candidate with <= 64 * G pods (G <= 4) on <= 64-word rows;
+// lane l holds pods l, 64 + l, ... (group g = pod / 64):
+//   prologue  F rows of the candidate's pods, 16 pods per batch (lanes =
+//             words, the four table rows ANDed in registers), stopping after
+//             the batch holding the first pod with an empty row; the row head
+//             (32 / G words) goes to LDS, the pod's lane keeps its mask of
+//             non-zero words;
+//   visits    n = min pointer over unplaced pods (DPP wave-min); node n's base
+//             record from a 64-node register window; greedy placement in pod
+//             order (group by group) with the running state in SGPRs; pods
+//             that did not fit move their pointer to the next set bit of their
+//             F row (LDS head, else the tables).
+// The chain is one step per visited node instead of one per pod, and a step
+// touches no global memory unless the window moves or a pointer leaves the
+// head.
+constexpr int kFBatch = 16;  // F rows loaded per batch (4 x 16 loads in flight per lane)
+
+// Word `wd` of the lane's own F row, straight from the tables (beyond the LDS head).
+__device__ __forceinline__ uint64_t f_word_far(const uint64_t* __restrict__ tab, uint64_t r01, uint64_t r23, int wd) {
+  return tab[static_cast<uint32_t>(r01) + wd] & tab[static_cast<uint32_t>(r01 >> 32) + wd] &
+         tab[static_cast<uint32_t>(r23) + wd] & tab[static_cast<uint32_t>(r23 >> 32) + wd];
+}
+
+template <int G, bool PROF>
+__device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __restrict__ F, const int p0,
+                                              const int np, int& status, K2Stats& st) {
+  constexpr int HW = kHead / G;  // row-head words per pod in LDS
+  constexpr int FS = HW + 1;     // LDS stride per pod (odd: spreads banks)
+  static_assert(64 * G * FS * 8 <= sizeof(K2Lds), "node-order LDS exceeds the wave's K2 region");
+  const int lane = threadIdx.x & 63;
+  const int Wp = w.Wp;  // <= 64
+  const uint64_t* __restrict__ tab = w.S;
+  int64_t rc[G], rm[G], re[G];
+  uint64_t pm[G], r01[G], r23[G], wmask[G], act[G];
+  bool zero[G];
+  int ptr[G], node[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint64_t* pr = w.pod_rec + static_cast<size_t>(p0 + min(64 * g + lane, np - 1)) * kRecU64;
+    rc[g] = static_cast<int64_t>(pr[0]);
+    rm[g] = static_cast<int64_t>(pr[1]);
+    re[g] = static_cast<int64_t>(pr[2]);
+    pm[g] = pr[3];
+    r01[g] = pr[4];
+    r23[g] = pr[5];
+    zero[g] = (rc[g] | rm[g] | re[g]) == 0;  // fitsRequest skips the resource checks
+    wmask[g] = 0;
+    ptr[g] = INT_MAX;
+    node[g] = -1;
+  }
+  uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
+
+  // F rows, 16 pods per batch; stop after the batch holding the first empty row
+  const bool wv = lane < Wp;
+  const uint32_t wi = wv ? static_cast<uint32_t>(lane) : 0u;
+  int dead = np;  // first pod with no feasible spot node left
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    for (int b0 = 64 * g; b0 < min(dead, 64 * g + 64); b0 += kFBatch) {
+      uint64_t x0[kFBatch], x1[kFBatch], x2[kFBatch], x3[kFBatch];
+#pragma unroll
+      for (int u = 0; u < kFBatch; ++u) {
+        const int k = min(b0 + u, np - 1) - 64 * g;  // lane of the pod within group g
+        const uint64_t a01 = readlane64(r01[g], k), a23 = readlane64(r23[g], k);
+        x0[u] = tab[static_cast<uint32_t>(a01) + wi];
+        x1[u] = tab[static_cast<uint32_t>(a01 >> 32) + wi];
+        x2[u] = tab[static_cast<uint32_t>(a23) + wi];
+        x3[u] = tab[static_cast<uint32_t>(a23 >> 32) + wi];
+      }
+#pragma unroll
+      for (int u = 0; u < kFBatch; ++u) {
+        const int k = b0 + u;
+        if (k < np) {  // wave-uniform
+          const uint64_t f = wv ? (x0[u] & x1[u] & x2[u] & x3[u]) : 0ull;
+          if (lane < HW) F[k * FS + lane] = f;
+          const uint64_t m = ballot(f != 0);
+          if (lane == k - 64 * g) wmask[g] = m;
+          if (m == 0) dead = min(dead, k);
+        }
+      }
+    }
+  }
+  if (PROF) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    st.cyc_a += t - cyc_t;
+    cyc_t = t;
+  }
+
+  // pointers: first feasible node of every pod below the first dead one
+  uint64_t any = 0;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int k = 64 * g + lane;
+    act[g] = ballot(k < dead);  // pods still to place
+    any |= act[g];
+    if (k < dead) {
+      const int w0 = __builtin_ctzll(wmask[g]);  // != 0: the pod has a feasible node
+      const uint64_t f0 = w0 < HW ? F[k * FS + w0] : f_word_far(tab, r01[g], r23[g], w0);
+      ptr[g] = w0 * 64 + __builtin_ctzll(f0);
+    }
+  }
+
+  int wcur = -1;  // register window: lane i holds the base record of node 64 * wcur + i
+  int64_t ncpu = 0, nmem = 0, neph = 0;
+  uint64_t nport = 0;
+  int nleft = 0;
+  int visits = 0, placements = 0, windows = 0;
+  while (any != 0) {
+    int mine = INT_MAX;
+#pragma unroll
+    for (int g = 0; g < G; ++g) mine = ((act[g] >> lane) & 1) ? min(mine, ptr[g]) : mine;
+    const int n = wave_min(mine);
+    if (n == INT_MAX) break;  // unreachable: every pod still to place has a pointer
+    ++visits;
+    const int W = n >> 6, b = n & 63;
+    if (W != wcur) {  // wave-uniform
+      const uint64_t* nr = w.node_rec + static_cast<size_t>(W * 64 + lane) * 8;
+      ncpu = static_cast<int64_t>(nr[0]);
+      nmem = static_cast<int64_t>(nr[1]);
+      neph = static_cast<int64_t>(nr[2]);
+      nport = nr[3];
+      nleft = static_cast<int>(static_cast<int64_t>(nr[4]));
+      wcur = W;
+      ++windows;
+    }
+    // node n's running state (ClusterSnapshot.AddPod on the candidate's copy)
+    int64_t cpu = static_cast<int64_t>(readlane64(static_cast<uint64_t>(ncpu), b));
+    int64_t mem = static_cast<int64_t>(readlane64(static_cast<uint64_t>(nmem), b));
+    int64_t eph = static_cast<int64_t>(readlane64(static_cast<uint64_t>(neph), b));
+    uint64_t ports = readlane64(nport, b);
+    int left = __builtin_amdgcn_readlane(nleft, b);
+    uint64_t failed[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {  // groups in pod order: the state flows from one to the next
+      const uint64_t cand = ballot(((act[g] >> lane) & 1) && ptr[g] == n);
+      uint64_t rest = cand, placed = 0;
+      while (rest != 0 && left >= 1) {  // NodeResourcesFit + NodePorts, pods in order
+        const bool fit = zero[g] | ((rc[g] <= cpu) & (rm[g] <= mem) & (re[g] <= eph));
+        const uint64_t fm = ballot((((rest >> lane) & 1) != 0) & fit & ((pm[g] & ports) == 0));
+        if (fm == 0) break;
+        const int j = __builtin_ctzll(fm);
+        placed |= 1ull << j;
+        rest &= ~((2ull << j) - 1);  // pods below j that did not fit failed at n
+        cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc[g]), j));
+        mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm[g]), j));
+        eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(re[g]), j));
+        ports |= readlane64(pm[g], j);
+        left -= 1;
+        ++placements;
+      }
+      if ((placed >> lane) & 1) node[g] = n;
+      act[g] &= ~placed;
+      failed[g] = cand & ~placed;
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (failed[g] == 0) continue;  // wave-uniform
+      // pods that did not fit n: next set bit of their F row after n
+      const int k = 64 * g + lane;
+      if ((failed[g] >> lane) & 1) {
+        uint64_t f = W < HW ? F[k * FS + W] : f_word_far(tab, r01[g], r23[g], W);
+        f = b == 63 ? 0ull : f & (~0ull << (b + 1));
+        int nx = INT_MAX;
+        if (f != 0) {
+          nx = W * 64 + __builtin_ctzll(f);
+        } else {
+          const uint64_t rem = W == 63 ? 0ull : wmask[g] & (~0ull << (W + 1));
+          if (rem != 0) {
+            const int w2 = __builtin_ctzll(rem);
+            const uint64_t h = w2 < HW ? F[k * FS + w2] : f_word_far(tab, r01[g], r23[g], w2);
+            nx = w2 * 64 + __builtin_ctzll(h);
+          }
+        }
+        ptr[g] = nx;
+      }
+      // a pod with no node left fails the candidate; pods above it are irrelevant
+      const uint64_t gone = ballot((((failed[g] >> lane) & 1) != 0) & (ptr[g] == INT_MAX));
+      if (gone != 0) dead = min(dead, 64 * g + __builtin_ctzll(gone));
+    }
+    any = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      act[g] &= ballot(64 * g + lane < dead);
+      any |= act[g];
+    }
+  }
+  if (PROF) {
+    st.cyc_b += __builtin_amdgcn_s_memtime() - cyc_t;
+    st.n_min = static_cast<uint32_t>(visits);
+    st.n_far = static_cast<uint32_t>(windows);
+    st.n_spec_miss = static_cast<uint32_t>(placements);
+  }
+  status = dead < np ? dead : -1;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int k = 64 * g + lane;
+    if (k < np) w.out_node[p0 + k] = k < dead ? node[g] : -1;
+  }
+}
+
 // K2: one wave per candidate (list entries {candidate, first pod, end pod,
 // global index}, longest candidates first).
 template <int CH, bool PROF>
@@ -546,11 +759,21 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
 
   K2Stats st;
   int status = -1;
-  int placed = k2_run<1, CH, PROF>(w, L, p0, np, status, st);
-  const int wide = placed < 0 ? 1 : 0;
-  if (placed < 0) placed = k2_run<8, CH, PROF>(w, L, p0, np, status, st);  // > 64 distinct nodes
-
-  for (int i = lane; i < np; i += 64) w.out_node[p0 + i] = i < placed ? L.omap[i] : -1;
+  int wide = 0;
+  bool node_order = false;
+  if constexpr (CH == 1) node_order = np <= 4 * 64 && w.k2_mode == 0;  // rows of <= 64 words
+  if (node_order) {  // writes out_node itself
+    uint64_t* F = reinterpret_cast<uint64_t*>(&L);
+    wide = 2;
+    if (np <= 64) k2_node_order<1, PROF>(w, F, p0, np, status, st);
+    else if (np <= 128) k2_node_order<2, PROF>(w, F, p0, np, status, st);
+    else k2_node_order<4, PROF>(w, F, p0, np, status, st);
+  } else {
+    int placed = k2_run<1, CH, PROF>(w, L, p0, np, status, st);
+    wide = placed < 0 ? 1 : 0;
+    if (placed < 0) placed = k2_run<8, CH, PROF>(w, L, p0, np, status, st);  // > 64 distinct nodes
+    for (int i = lane; i < np; i += 64) w.out_node[p0 + i] = i < placed ? L.omap[i] : -1;
+  }
   if (lane == 0) {
     w.out_status[ci] = status;
     // packed (global candidate << 32 | local candidate): min = first drainable

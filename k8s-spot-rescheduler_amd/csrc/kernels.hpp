@@ -42,6 +42,8 @@ struct DevWorkload {
   int32_t* result;     // mapped host memory [kResultHeader + max pods]
                        //   {winner, local, npods, first_fallback, seq, mapping...}
   int32_t seq;         // run sequence number written last into result[4]
+  int32_t k2_mode;     // 0: node-order first fit where it applies (<= 64 pods, <= 64-word rows);
+                       // 1: pod order everywhere (SR_K2_MODE=1, A/B measurement)
   uint64_t* prof;      // optional [n_cand][16] K2 + [kK0ProfWaves][2] K0 per-wave profile
                        // (SR_K2_PROFILE), else null
 };

@@ -55,6 +55,7 @@ struct sr_ctx {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   FILE* prof_file = nullptr;  // SR_K2_PROFILE: per-wave K2 records appended per run
+  int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
 };
 
 namespace {
@@ -118,6 +119,14 @@ class Packer {
   std::vector<Item> items_;
   size_t size_ = 0;
 };
+
+// K2 algorithmic bytes per pod processed: its 48-B record plus the rows it
+// reads -- the whole F row (4 rows x Wp words) in node order (<= 256 pods,
+// <= 64-word rows), the 32-word heads of the 4 rows in pod order.
+uint64_t k2_pod_bytes(int32_t Wp, int32_t np, int32_t k2_mode) {
+  const bool node_order = k2_mode == 0 && Wp <= 64 && np <= 256;
+  return 48ull + 32ull * static_cast<uint64_t>(node_order ? Wp : std::min(Wp, 32));
+}
 
 sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands) {
   auto t0 = std::chrono::steady_clock::now();
@@ -190,6 +199,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.out_node = static_cast<int32_t*>(ctx->out_node.p);
   d.out_status = static_cast<int32_t*>(ctx->out_status.p);
   d.d_min = static_cast<int32_t*>(ctx->dmin.p);
+  d.k2_mode = ctx->k2_mode;
   d.prof = nullptr;
   if (ctx->prof_file) {
     const size_t pbytes = sizeof(uint64_t) * (16 * static_cast<size_t>(std::max(1, ncand)) + 2 * sr::kK0ProfWaves);
@@ -208,7 +218,11 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   ctx->t.bytes_tables = n_rows * row + atom_reads * row + 3ull * 8 * w.n_pad + 8ull * w.t_dim.size();
   // K2 (upper bound until a full run refines it, see run()): per pod its
   // four row chunks and its record, per candidate its mapping and status.
-  ctx->t.bytes_placement = static_cast<uint64_t>(na) * (32ull * std::min(w.Wp, 32) + 48 + 4) + 4ull * ncand;
+  ctx->t.bytes_placement = 4ull * ncand;
+  for (int32_t k = 0; k < ncand; ++k) {
+    const int32_t np = w.cand_off[k + 1] - w.cand_off[k];
+    ctx->t.bytes_placement += (k2_pod_bytes(w.Wp, np, ctx->k2_mode) + 4) * static_cast<uint64_t>(np);
+  }
   ctx->t.ms_pack_host = std::chrono::duration<double, std::milli>(t1 - t0).count();
   ctx->t.ms_upload = std::chrono::duration<double, std::milli>(t2 - t1).count();
   ctx->t.n_pods = na;
@@ -346,12 +360,12 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
       for (int32_t k = 0; k < ncand; ++k) out->status[w.cand_src[k]] = hs[k];
     }
     // exact K2 algorithmic bytes: pods up to and including the failing one
+    // (node order: the pod's whole F row; pod order: the 32-word row heads)
     uint64_t k2 = 4ull * ncand;
-    const uint64_t per_pod = 32ull * std::min(w.Wp, 32) + 48;
     for (int32_t k = 0; k < ncand; ++k) {
       const int32_t np = w.cand_off[k + 1] - w.cand_off[k];
       const int32_t done = hs[k] >= 0 ? std::min(np, hs[k] + 1) : np;
-      k2 += per_pod * done + 4ull * np;
+      k2 += k2_pod_bytes(w.Wp, np, ctx->k2_mode) * done + 4ull * np;
     }
     ctx->t.bytes_placement = k2;
     if (out->node_of_pod) {
@@ -383,6 +397,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
     return SR_ERR_HIP;
   }
   if (const char* path = std::getenv("SR_K2_PROFILE")) ctx->prof_file = std::fopen(path, "ab");
+  if (const char* m = std::getenv("SR_K2_MODE")) ctx->k2_mode = std::atoi(m) == 1 ? 1 : 0;
   *out = ctx;
   return SR_OK;
 }

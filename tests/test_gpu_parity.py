@@ -148,6 +148,33 @@ def test_can_drain_node_sequence_mutates_like_oracle(checker, seed):
     lib.sr_snapshot_destroy(h)
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_random_large_candidates(checker, seed):
+    # 65..300 pods per candidate: K2's node-order path with 2 and 4 pod groups
+    # (a failing pod in any group) and, above 256 pods, the pod-order path
+    nodes, spot_pods, cands = rand_scenario(5000 + seed, n_spot=20 + 5 * seed, n_cand=4, max_pods=70 + 33 * seed,
+                                            features=seed % 2 == 0)
+    run_scenario(checker, nodes, spot_pods, cands)
+
+
+def test_pod_order_mode_matches_oracle():
+    # SR_K2_MODE=1 forces K2's pod-order path everywhere (the A/B arm of the bench)
+    import os
+    from spotplanner.planner import PredicateChecker
+    os.environ["SR_K2_MODE"] = "1"
+    try:
+        c = PredicateChecker(0)
+    finally:
+        del os.environ["SR_K2_MODE"]
+    try:
+        for seed in range(6):
+            nodes, spot_pods, cands = rand_scenario(6000 + seed, n_spot=8 + 7 * seed, n_cand=8, max_pods=12)
+            run_scenario(c, nodes, spot_pods, cands)
+        tick_parity(c, SynthCluster(3, seed=13, n_on_demand=300, n_spot=900))
+    finally:
+        c.close()
+
+
 # ------------------------------------------------------------------ edge cases
 def test_no_spot_nodes(checker):
     cands = [[Pod("a", containers=[Container(100)])], [], [Pod("z", containers=[Container(0)])]]

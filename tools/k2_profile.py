@@ -10,6 +10,8 @@ Each sr_plan_run appends {int64 n_cand, int64 n_k0} + n_cand x 16 u64 (K2)
   [8..11] cycles per step section: a = start -> answer, b = answer -> slot
           update, c = wait for the next rows, d = next pod's first clean node
           + DMA issue;  [12] cycles waiting for speculative records
+Node-order waves ([5] == 2) reuse the fields: [6] placements, [7] visits |
+windows << 32, [8] prologue (F rows) cycles, [9] visit-loop cycles.
 Only the last run in the file is summarised (earlier ones are warmup)."""
 import sys
 
@@ -56,16 +58,32 @@ def main():
     print("loop us/step   p50/p90/p99/max:", pct(per))
     cyc = r[:, 3] / np.maximum(1, dur)     # cycles per us -> clock
     print("clock MHz (memtime/realtime) p50:", "%.0f" % np.median(cyc[dur > 0]))
-    print("reruns with 512 slots:", int(r[:, 5].sum()))
+    mode = r[:, 5]
+    nodeo = mode == 2
+    print("waves: node order %d, pod order %d (of which rerun with 512 slots %d)"
+          % (int(nodeo.sum()), int((~nodeo).sum()), int((mode == 1).sum())))
+    if nodeo.any():
+        q = r[nodeo]
+        vis = (q[:, 7] & 0xffffffff).astype(np.int64)
+        print("node order: visits p50/p90/max %s; placements/visit %.2f; windows/wave %.2f"
+              % (" ".join("%d" % x for x in np.percentile(vis, [50, 90, 100])),
+                 q[:, 6].sum() / max(1, vis.sum()), (q[:, 7] >> 32).sum() / len(q)))
+        print("node order: prologue cycles p50/p90/max %s; loop cycles/visit p50/p90 %s"
+              % (" ".join("%.0f" % x for x in np.percentile(q[:, 8], [50, 90, 100])),
+                 " ".join("%.0f" % x for x in np.percentile(q[:, 9] / np.maximum(1, vis), [50, 90]))))
+        print("node order: wave dur us p50/p90/max %s" % pct(dur[nodeo]))
+    if (~nodeo).any():
+        print("pod order:  wave dur us p50/p90/max %s" % pct(dur[~nodeo]))
+    r = r[~nodeo] if (~nodeo).any() else r
     print("spec misses total %d, wave_min total %d, far chunks total %d" %
           (r[:, 6].sum(), (r[:, 7] & 0xffffffff).sum(), (r[:, 7] >> 32).sum()))
     tot = r[:, 8:13].sum(axis=0)
-    st = max(1, steps.sum())
+    st = max(1, (steps[~nodeo] if (~nodeo).any() else steps).sum())
     print("cycles/step by section a,b,c,d,spec-wait:", " ".join("%.0f" % (x / st) for x in tot))
     last = np.argsort(-end)[:8]
-    print("latest-ending waves: cand start prologue loop steps slots")
+    print("latest-ending waves: wave start loop_us steps mode(2=node order)")
     for c in last:
-        print("  %5d %7.2f %7.2f %7.2f %4d %3d" % (c, start[c], pro[c], loop_us[c], steps[c], r[c, 5]))
+        print("  %5d %7.2f %7.2f %4d %3d" % (c, start[c], loop_us[c], steps[c], mode[c]))
 
 
 if __name__ == "__main__":
