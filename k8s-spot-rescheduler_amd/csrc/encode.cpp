@@ -665,6 +665,58 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       rec[3] = pstat[pod_spec[q]].ports;
     }
   });
+  // Pods whose F row is certainly empty point at one all-zero class (atom 0
+  // AND NOT atom 0), so K2 knows them without reading their rows: a class
+  // that ANDs an empty atom, ANDs the complement of a full one, or whose
+  // terms each hold an empty atom; or a request above every node's free
+  // value in some dimension (the never-row).  Sound, not complete: the rest
+  // is found exactly on the device.
+  {
+    std::vector<uint8_t> atom_empty(static_cast<size_t>(w->n_atoms)), atom_full(static_cast<size_t>(w->n_atoms));
+    for (int32_t a = 0; a < w->n_atoms; ++a) {
+      const uint64_t* row = &w->atoms[static_cast<size_t>(a) * Wp];
+      int64_t pop = 0;
+      for (int32_t i = 0; i < Wp; ++i) pop += __builtin_popcountll(row[i]);
+      atom_empty[a] = pop == 0;
+      atom_full[a] = pop == n_spot;
+    }
+    std::vector<uint8_t> cls_empty(static_cast<size_t>(w->n_classes), 0);
+    for (int32_t c = 0; c < w->n_classes; ++c) {
+      bool empty = false, has_terms = false, all_terms_empty = true, term_empty = false;
+      for (int32_t o = w->cls_prog_off[c]; o < w->cls_prog_off[c + 1]; ++o) {
+        const int32_t atom = w->cls_prog[o] >> 2, kind = w->cls_prog[o] & 3;
+        if (kind == PROG_AND) {
+          empty = empty || atom_empty[atom];
+        } else if (kind == PROG_ANDNOT) {
+          empty = empty || atom_full[atom];
+        } else {
+          if (kind == PROG_TERM_START) {
+            if (has_terms) all_terms_empty = all_terms_empty && term_empty;
+            has_terms = true;
+            term_empty = false;
+          }
+          term_empty = term_empty || atom_empty[atom];
+        }
+      }
+      if (has_terms) all_terms_empty = all_terms_empty && term_empty;
+      cls_empty[c] = empty || (has_terms && all_terms_empty);
+    }
+    std::vector<int32_t> dead_pods;
+    for (int32_t q = 0; q < na; ++q) {
+      const int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
+      bool dead = cls_empty[r[0]] != 0;
+      for (int d = 0; d < 3; ++d)
+        dead = dead || (r[1 + d] >= 0 && static_cast<size_t>(r[1 + d]) == node_vals[d].size());
+      if (dead) dead_pods.push_back(q);
+    }
+    if (!dead_pods.empty()) {
+      emit(0, PROG_AND);
+      emit(0, PROG_ANDNOT);
+      w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
+      w->empty_class = w->n_classes++;
+      for (int32_t q : dead_pods) w->pod_rows[static_cast<size_t>(q) * 4] = w->empty_class;
+    }
+  }
   // positions -> T rows: row 0 = every node, then the used positions of each
   // dimension in increasing threshold order (rows grouped by dimension, so
   // K0 compares one dimension per wave)

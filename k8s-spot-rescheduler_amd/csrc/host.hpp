@@ -94,6 +94,7 @@ struct Workload {
   // ---- static pod classes as atom programs:
   //   S[c] = AND(and atoms) & AND(~not atoms) & [OR over terms of AND(term atoms)]
   int32_t n_classes = 0;
+  int32_t empty_class = -1;  // all-zero S row for pods whose F row is certainly empty (-1: none)
   std::vector<int32_t> cls_prog_off, cls_prog;  // CSR class -> ops (atom << 2 | PROG_*)
   // ---- T rows: capacity thresholds.  Row 0 = every node (zero-request pods
   // skip the resource checks); other rows: free_<dim>[n] >= thr.

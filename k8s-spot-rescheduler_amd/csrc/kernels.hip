@@ -541,40 +541,50 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
 //
 // One wave per candidate with <= 64 * G pods (G <= 4) on <= 64-word rows;
 // lane l holds pods l, 64 + l, ... (group g = pod / 64):
-//   prologue  F rows of the candidate's pods, 16 pods per batch (lanes =
-//             words, the four table rows ANDed in registers), stopping after
-//             the batch holding the first pod with an empty row; the row head
-//             (32 / G words) goes to LDS, the pod's lane keeps its mask of
-//             non-zero words;
+//   prologue  pods whose S row is certainly empty (the encoder points them at
+//             the all-zero class) bound the pods that matter; the F row head
+//             (kNH words = 512 nodes) of each of those, 8 pods per load
+//             instruction (lanes = pod x word), goes to LDS, the pod's lane
+//             keeps its 8-bit mask of non-zero head words;
 //   visits    n = min pointer over unplaced pods (DPP wave-min); node n's base
 //             record from a 64-node register window; greedy placement in pod
 //             order (group by group) with the running state in SGPRs; pods
 //             that did not fit move their pointer to the next set bit of their
-//             F row (LDS head, else the tables).
+//             F row.  A pod whose head holds no further bit points at kFar;
+//             when the minimum reaches kFar every such pod is resolved with one
+//             full-row scan (lanes = words), which also leaves its mask of
+//             non-zero words for later moves beyond the head.
 // The chain is one step per visited node instead of one per pod, and a step
-// touches no global memory unless the window moves or a pointer leaves the
-// head.
-constexpr int kFBatch = 16;  // F rows loaded per batch (4 x 16 loads in flight per lane)
+// touches no global memory unless the window moves or a pointer moves beyond
+// the head.
+constexpr int kNH = 8;             // F head words per pod kept in LDS (nodes [0, 512))
+constexpr int kNHS = kNH + 1;      // LDS stride per pod (odd number of words: conflict-free b64 reads)
+constexpr int kFar = 64 * kNH;     // pointer sentinel: next feasible node lies at or beyond the head, unresolved
 
-// Word `wd` of the lane's own F row, straight from the tables (beyond the LDS head).
+// Word `wd` of the lane's own F row, straight from the tables.
 __device__ __forceinline__ uint64_t f_word_far(const uint64_t* __restrict__ tab, uint64_t r01, uint64_t r23, int wd) {
   return tab[static_cast<uint32_t>(r01) + wd] & tab[static_cast<uint32_t>(r01 >> 32) + wd] &
          tab[static_cast<uint32_t>(r23) + wd] & tab[static_cast<uint32_t>(r23 >> 32) + wd];
 }
 
+// 32-bit value of lane `src` (per-lane source index), through the LDS crossbar.
+__device__ __forceinline__ uint32_t from_lane(uint32_t v, int src) {
+  return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(v)));
+}
+
 template <int G, bool PROF>
 __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __restrict__ F, const int p0,
                                               const int np, int& status, K2Stats& st) {
-  constexpr int HW = kHead / G;  // row-head words per pod in LDS
-  constexpr int FS = HW + 1;     // LDS stride per pod (odd: spreads banks)
-  static_assert(64 * G * FS * 8 <= sizeof(K2Lds), "node-order LDS exceeds the wave's K2 region");
+  static_assert(64 * G * kNHS * 8 <= sizeof(K2Lds), "node-order LDS exceeds the wave's K2 region");
   const int lane = threadIdx.x & 63;
   const int Wp = w.Wp;  // <= 64
   const uint64_t* __restrict__ tab = w.S;
   int64_t rc[G], rm[G], re[G];
-  uint64_t pm[G], r01[G], r23[G], wmask[G], act[G];
+  uint64_t pm[G], r01[G], r23[G], fmask[G], act[G];
+  uint32_t hmask[G];
   bool zero[G];
   int ptr[G], node[G];
+  int dead = np;  // first pod with no feasible spot node left
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const uint64_t* pr = w.pod_rec + static_cast<size_t>(p0 + min(64 * g + lane, np - 1)) * kRecU64;
@@ -585,60 +595,76 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     r01[g] = pr[4];
     r23[g] = pr[5];
     zero[g] = (rc[g] | rm[g] | re[g]) == 0;  // fitsRequest skips the resource checks
-    wmask[g] = 0;
+    fmask[g] = 0;
+    hmask[g] = 0;
     ptr[g] = INT_MAX;
     node[g] = -1;
+    const uint64_t e = ballot(64 * g + lane < np && static_cast<uint32_t>(r01[g]) == w.s_empty_off);
+    if (e != 0) dead = min(dead, 64 * g + __builtin_ctzll(e));
   }
   uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
 
-  // F rows, 16 pods per batch; stop after the batch holding the first empty row
-  const bool wv = lane < Wp;
-  const uint32_t wi = wv ? static_cast<uint32_t>(lane) : 0u;
-  int dead = np;  // first pod with no feasible spot node left
+  // F heads of pods [0, dead): lanes = 8 pods x 8 words, two such batches per step
+  {
+    const int sub = lane >> 3, wd = lane & 7;
+    const bool wv = wd < Wp;
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    for (int b0 = 64 * g; b0 < min(dead, 64 * g + 64); b0 += kFBatch) {
-      uint64_t x0[kFBatch], x1[kFBatch], x2[kFBatch], x3[kFBatch];
+    for (int g = 0; g < G; ++g) {
+      for (int b0 = 64 * g; b0 < min(dead, 64 * g + 64); b0 += 16) {
+        uint64_t x[2][4];
+        int kk[2];
 #pragma unroll
-      for (int u = 0; u < kFBatch; ++u) {
-        const int k = min(b0 + u, np - 1) - 64 * g;  // lane of the pod within group g
-        const uint64_t a01 = readlane64(r01[g], k), a23 = readlane64(r23[g], k);
-        x0[u] = tab[static_cast<uint32_t>(a01) + wi];
-        x1[u] = tab[static_cast<uint32_t>(a01 >> 32) + wi];
-        x2[u] = tab[static_cast<uint32_t>(a23) + wi];
-        x3[u] = tab[static_cast<uint32_t>(a23 >> 32) + wi];
-      }
+        for (int h = 0; h < 2; ++h) {
+          kk[h] = b0 + 8 * h + sub;
+          const int src = min(kk[h], np - 1) - 64 * g;  // lane of that pod in group g
+          const uint32_t o0 = from_lane(static_cast<uint32_t>(r01[g]), src);
+          const uint32_t o1 = from_lane(static_cast<uint32_t>(r01[g] >> 32), src);
+          const uint32_t o2 = from_lane(static_cast<uint32_t>(r23[g]), src);
+          const uint32_t o3 = from_lane(static_cast<uint32_t>(r23[g] >> 32), src);
+          const uint32_t wi = wv ? wd : 0u;
+          x[h][0] = tab[o0 + wi];
+          x[h][1] = tab[o1 + wi];
+          x[h][2] = tab[o2 + wi];
+          x[h][3] = tab[o3 + wi];
+        }
 #pragma unroll
-      for (int u = 0; u < kFBatch; ++u) {
-        const int k = b0 + u;
-        if (k < np) {  // wave-uniform
-          const uint64_t f = wv ? (x0[u] & x1[u] & x2[u] & x3[u]) : 0ull;
-          if (lane < HW) F[k * FS + lane] = f;
-          const uint64_t m = ballot(f != 0);
-          if (lane == k - 64 * g) wmask[g] = m;
-          if (m == 0) dead = min(dead, k);
+        for (int h = 0; h < 2; ++h) {
+          const uint64_t f = (wv && kk[h] < np) ? (x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
+          if (kk[h] < np) F[kk[h] * kNHS + wd] = f;
+          const uint64_t m = ballot(f != 0);  // 8 bits per pod: bit 8 * i + word
+          const int rel = 64 * g + lane - (b0 + 8 * h);
+          if (rel >= 0 && rel < 8) hmask[g] = static_cast<uint32_t>(m >> (8 * rel)) & 0xffu;
         }
       }
     }
+  }
+
+  // pointers: first feasible head node of every pod below `dead`, else kFar
+  // (beyond the head; resolved lazily) or none
+  uint64_t any = 0;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int k = 64 * g + lane;
+    if (k < dead) {
+      if (hmask[g] != 0) {
+        const int w0 = __builtin_ctz(hmask[g]);
+        ptr[g] = w0 * 64 + __builtin_ctzll(F[k * kNHS + w0]);
+      } else {
+        ptr[g] = Wp > kNH ? kFar : INT_MAX;
+      }
+    }
+    const uint64_t gone = ballot(k < dead && ptr[g] == INT_MAX);
+    if (gone != 0) dead = min(dead, 64 * g + __builtin_ctzll(gone));
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    act[g] = ballot(64 * g + lane < dead);  // pods still to place
+    any |= act[g];
   }
   if (PROF) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
     st.cyc_a += t - cyc_t;
     cyc_t = t;
-  }
-
-  // pointers: first feasible node of every pod below the first dead one
-  uint64_t any = 0;
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const int k = 64 * g + lane;
-    act[g] = ballot(k < dead);  // pods still to place
-    any |= act[g];
-    if (k < dead) {
-      const int w0 = __builtin_ctzll(wmask[g]);  // != 0: the pod has a feasible node
-      const uint64_t f0 = w0 < HW ? F[k * FS + w0] : f_word_far(tab, r01[g], r23[g], w0);
-      ptr[g] = w0 * 64 + __builtin_ctzll(f0);
-    }
   }
 
   int wcur = -1;  // register window: lane i holds the base record of node 64 * wcur + i
@@ -652,6 +678,54 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     for (int g = 0; g < G; ++g) mine = ((act[g] >> lane) & 1) ? min(mine, ptr[g]) : mine;
     const int n = wave_min(mine);
     if (n == INT_MAX) break;  // unreachable: every pod still to place has a pointer
+    if (n == kFar) {
+      // every node of the head is done: resolve the pods pointing beyond it,
+      // one full-row scan each (lanes = words)
+      const bool wv = lane >= kNH && lane < Wp;
+      const uint32_t wi = wv ? static_cast<uint32_t>(lane) : 0u;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        uint64_t pend = ballot(((act[g] >> lane) & 1) && ptr[g] == kFar);
+        while (pend != 0) {  // 4 pods per round: their 16 loads in flight together
+          int js[4];
+          uint64_t x[4][4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            js[q] = pend != 0 ? __builtin_ctzll(pend) : -1;
+            pend &= pend - 1;
+            const int j = js[q] < 0 ? 0 : js[q];
+            const uint64_t a01 = readlane64(r01[g], j), a23 = readlane64(r23[g], j);
+            x[q][0] = tab[static_cast<uint32_t>(a01) + wi];
+            x[q][1] = tab[static_cast<uint32_t>(a01 >> 32) + wi];
+            x[q][2] = tab[static_cast<uint32_t>(a23) + wi];
+            x[q][3] = tab[static_cast<uint32_t>(a23 >> 32) + wi];
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (js[q] < 0) continue;  // wave-uniform
+            const uint64_t f = wv ? (x[q][0] & x[q][1] & x[q][2] & x[q][3]) : 0ull;
+            const uint64_t m = ballot(f != 0);
+            int nx = INT_MAX;
+            if (m != 0) {
+              const int w2 = __builtin_ctzll(m);
+              nx = w2 * 64 + __builtin_ctzll(readlane64(f, w2));
+            }
+            if (lane == js[q]) {
+              fmask[g] = m;
+              ptr[g] = nx;
+            }
+            if (nx == INT_MAX) dead = min(dead, 64 * g + js[q]);
+          }
+        }
+      }
+      any = 0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        act[g] &= ballot(64 * g + lane < dead);
+        any |= act[g];
+      }
+      continue;
+    }
     ++visits;
     const int W = n >> 6, b = n & 63;
     if (W != wcur) {  // wave-uniform
@@ -670,6 +744,11 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     int64_t eph = static_cast<int64_t>(readlane64(static_cast<uint64_t>(neph), b));
     uint64_t ports = readlane64(nport, b);
     int left = __builtin_amdgcn_readlane(nleft, b);
+    if (PROF) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      st.cyc_b += t - cyc_t;
+      cyc_t = t;
+    }
     uint64_t failed[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {  // groups in pod order: the state flows from one to the next
@@ -693,23 +772,35 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       act[g] &= ~placed;
       failed[g] = cand & ~placed;
     }
+    if (PROF) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      st.cyc_c += t - cyc_t;
+      cyc_t = t;
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       if (failed[g] == 0) continue;  // wave-uniform
       // pods that did not fit n: next set bit of their F row after n
       const int k = 64 * g + lane;
       if ((failed[g] >> lane) & 1) {
-        uint64_t f = W < HW ? F[k * FS + W] : f_word_far(tab, r01[g], r23[g], W);
+        uint64_t f = W < kNH ? F[k * kNHS + W] : f_word_far(tab, r01[g], r23[g], W);
         f = b == 63 ? 0ull : f & (~0ull << (b + 1));
         int nx = INT_MAX;
         if (f != 0) {
           nx = W * 64 + __builtin_ctzll(f);
+        } else if (W < kNH) {
+          const uint32_t rem = hmask[g] & (0xffu << (W + 1)) & 0xffu;
+          if (rem != 0) {
+            const int w2 = __builtin_ctz(rem);
+            nx = w2 * 64 + __builtin_ctzll(F[k * kNHS + w2]);
+          } else if (Wp > kNH) {
+            nx = kFar;
+          }
         } else {
-          const uint64_t rem = W == 63 ? 0ull : wmask[g] & (~0ull << (W + 1));
+          const uint64_t rem = W == 63 ? 0ull : fmask[g] & (~0ull << (W + 1));
           if (rem != 0) {
             const int w2 = __builtin_ctzll(rem);
-            const uint64_t h = w2 < HW ? F[k * FS + w2] : f_word_far(tab, r01[g], r23[g], w2);
-            nx = w2 * 64 + __builtin_ctzll(h);
+            nx = w2 * 64 + __builtin_ctzll(f_word_far(tab, r01[g], r23[g], w2));
           }
         }
         ptr[g] = nx;
@@ -724,9 +815,13 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       act[g] &= ballot(64 * g + lane < dead);
       any |= act[g];
     }
+    if (PROF) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      st.cyc_d += t - cyc_t;
+      cyc_t = t;
+    }
   }
   if (PROF) {
-    st.cyc_b += __builtin_amdgcn_s_memtime() - cyc_t;
     st.n_min = static_cast<uint32_t>(visits);
     st.n_far = static_cast<uint32_t>(windows);
     st.n_spec_miss = static_cast<uint32_t>(placements);

@@ -22,6 +22,8 @@ struct DevWorkload {
   const int32_t* cls_prog_off; // class atom programs (CSR): ops atom << 2 | {AND, AND NOT,
   const int32_t* cls_prog;     //   open an ORed term, AND into the open term}
   int32_t n_classes;
+  uint32_t s_empty_off;     // word offset of the all-zero S row pods with a certainly empty F row point
+                            // at (encode.cpp), 0xffffffff if there is none
   int32_t n_t;              // threshold rows: row 0 = every node, then cpu, memory,
   int32_t t_off[5];         //   ephemeral rows [t_off[d + 1], t_off[d + 2]) in threshold order
   const int64_t* t_thr;

@@ -184,6 +184,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.cls_prog_off = static_cast<const int32_t*>(at(o_cpo));
   d.cls_prog = static_cast<const int32_t*>(at(o_cp));
   d.n_classes = w.n_classes;
+  d.s_empty_off = w.empty_class >= 0 ? static_cast<uint32_t>(w.empty_class) * static_cast<uint32_t>(w.Wp) : 0xffffffffu;
   d.n_t = static_cast<int32_t>(w.t_dim.size());
   for (int i = 0; i < 5; ++i) d.t_off[i] = w.t_off[i];
   d.t_thr = static_cast<const int64_t*>(at(o_tt));

@@ -11,7 +11,8 @@ Each sr_plan_run appends {int64 n_cand, int64 n_k0} + n_cand x 16 u64 (K2)
           update, c = wait for the next rows, d = next pod's first clean node
           + DMA issue;  [12] cycles waiting for speculative records
 Node-order waves ([5] == 2) reuse the fields: [6] placements, [7] visits |
-windows << 32, [8] prologue (F rows) cycles, [9] visit-loop cycles.
+windows << 32, [8] prologue (F heads) cycles, [9] min + window + node
+state, [10] placement, [11] pointer moves (+ far resolution).
 Only the last run in the file is summarised (earlier ones are warmup)."""
 import sys
 
@@ -68,9 +69,11 @@ def main():
         print("node order: visits p50/p90/max %s; placements/visit %.2f; windows/wave %.2f"
               % (" ".join("%d" % x for x in np.percentile(vis, [50, 90, 100])),
                  q[:, 6].sum() / max(1, vis.sum()), (q[:, 7] >> 32).sum() / len(q)))
-        print("node order: prologue cycles p50/p90/max %s; loop cycles/visit p50/p90 %s"
-              % (" ".join("%.0f" % x for x in np.percentile(q[:, 8], [50, 90, 100])),
-                 " ".join("%.0f" % x for x in np.percentile(q[:, 9] / np.maximum(1, vis), [50, 90]))))
+        print("node order: prologue cycles p50/p90/max %s" % " ".join(
+            "%.0f" % x for x in np.percentile(q[:, 8], [50, 90, 100])))
+        sv = max(1, vis.sum())
+        print("node order: cycles/visit min+window+state %.0f, placement %.0f, pointer moves %.0f"
+              % (q[:, 9].sum() / sv, q[:, 10].sum() / sv, q[:, 11].sum() / sv))
         print("node order: wave dur us p50/p90/max %s" % pct(dur[nodeo]))
     if (~nodeo).any():
         print("pod order:  wave dur us p50/p90/max %s" % pct(dur[~nodeo]))
