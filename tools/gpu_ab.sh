@@ -1,0 +1,19 @@
+#!/bin/bash
+# A/B of planner variants in ONE GPU session (same box, same clocks):
+#   tools/gpu_ab.sh tag "ENV=val ..." "ENV=val ..." ...   (each arm run twice, interleaved)
+tag=$1; shift
+R="$GRAFT_REPO_ROOT"; cd "$R" || exit 2
+out="$R/gpurun_out/$tag"; mkdir -p "$out"
+for rep in 1 2; do
+  i=0
+  for arm in "$@"; do
+    i=$((i+1))
+    env $arm timeout -k 10 200 python bench.py --config 3 --steps 300 --warmup 20 --no-cpu-baseline > "$out/arm${i}_rep${rep}.log" 2>&1 || exit $?
+    python - "$out/arm${i}_rep${rep}.log" "$arm" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print("%-40s ms/step %.4f  K0 %.4f  K2 %.4f  K3 %.4f" % (sys.argv[2], d["ms_per_step"], d["kernels_ms"]["k0_tables"],
+      d["kernels_ms"]["k2_placement"], d["kernels_ms"]["k3_winner_and_collective"]))
+PY
+  done
+done
