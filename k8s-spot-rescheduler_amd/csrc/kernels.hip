@@ -656,10 +656,14 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     const uint64_t gone = ballot(k < dead && ptr[g] == INT_MAX);
     if (gone != 0) dead = min(dead, 64 * g + __builtin_ctzll(gone));
   }
+  uint64_t zm[G];        // pods with an all-zero request (fitsRequest skips the resource checks)
+  uint64_t pm_any = 0;   // any pod with host ports: NodePorts checks are needed at all
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     act[g] = ballot(64 * g + lane < dead);  // pods still to place
     any |= act[g];
+    zm[g] = ballot(zero[g]);
+    pm_any |= ballot(pm[g] != 0);
   }
   if (PROF) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -755,8 +759,9 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       const uint64_t cand = ballot(((act[g] >> lane) & 1) && ptr[g] == n);
       uint64_t rest = cand, placed = 0;
       while (rest != 0 && left >= 1) {  // NodeResourcesFit + NodePorts, pods in order
-        const bool fit = zero[g] | ((rc[g] <= cpu) & (rm[g] <= mem) & (re[g] <= eph));
-        const uint64_t fm = ballot((((rest >> lane) & 1) != 0) & fit & ((pm[g] & ports) == 0));
+        // lane masks straight from the compares (no bool round trip through VGPRs)
+        uint64_t fm = rest & (zm[g] | (ballot(rc[g] <= cpu) & ballot(rm[g] <= mem) & ballot(re[g] <= eph)));
+        if (pm_any != 0 && ports != 0) fm &= ballot((pm[g] & ports) == 0);
         if (fm == 0) break;
         const int j = __builtin_ctzll(fm);
         placed |= 1ull << j;
@@ -764,7 +769,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc[g]), j));
         mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm[g]), j));
         eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(re[g]), j));
-        ports |= readlane64(pm[g], j);
+        if (pm_any != 0) ports |= readlane64(pm[g], j);
         left -= 1;
         ++placements;
       }

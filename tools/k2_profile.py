@@ -84,9 +84,14 @@ def main():
     st = max(1, (steps[~nodeo] if (~nodeo).any() else steps).sum())
     print("cycles/step by section a,b,c,d,spec-wait:", " ".join("%.0f" % (x / st) for x in tot))
     last = np.argsort(-end)[:8]
-    print("latest-ending waves: wave start loop_us steps mode(2=node order)")
+    full = runs[-1].astype(np.int64)
+    print("latest-ending waves: wave start_us dur_us steps mode | visits placements windows | "
+          "cycles: prologue min+state placement moves")
     for c in last:
-        print("  %5d %7.2f %7.2f %4d %3d" % (c, start[c], loop_us[c], steps[c], mode[c]))
+        f = full[c]
+        print("  %5d %6.2f %6.2f %4d %2d | %3d %3d %3d | %6d %6d %6d %6d"
+              % (c, start[c], dur[c], steps[c], mode[c], f[7] & 0xffffffff, f[6], f[7] >> 32,
+                 f[8], f[9], f[10], f[11]))
 
 
 if __name__ == "__main__":
