@@ -85,6 +85,10 @@ def main():
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true",
+                    help="A/B only: no HIP events in the timed region (roofline from the calibration pass)")
+    ap.add_argument("--event-every", type=int, default=16,
+                    help="HIP events on every n-th step of the timed region (timestamped dispatches lengthen a tick)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -137,7 +141,8 @@ def main():
     names = ["k0_tables", "k2_placement", "k3_winner_and_collective"]
     checker.set_timing(7)
     for _ in range(max(5, min(args.steps, 20))):
-        lib.sr_plan_run(checker.handle, ctypes.byref(out))
+        st = lib.sr_plan_run(checker.handle, ctypes.byref(out))
+        assert st == capi.SR_OK, (st, checker.last_error())
     tm = checker.timing()
     breakdown = dict(zip(names, [x / max(1, tm.n_runs) for x in
                                  (tm.ms_tables, tm.ms_placement, tm.ms_winner)]))
@@ -145,7 +150,7 @@ def main():
     dom_bit = 1 << names.index(dom)
 
     # Timed region: K steps, only the dominant kernel bracketed with events.
-    checker.set_timing(dom_bit)
+    checker.set_timing(0 if args.no_events else dom_bit | (max(1, args.event_every) << 8))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -157,7 +162,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     tm = checker.timing()
-    dom_ms = [tm.ms_tables, tm.ms_placement][names.index(dom)] / max(1, tm.n_runs)
+    dom_ms = ([tm.ms_tables, tm.ms_placement][names.index(dom)] / max(1, tm.n_runs) if not args.no_events
+              else breakdown[dom])
     checker.set_timing(0)
     local_checks = float(out.checks)
     if world > 1:
@@ -178,7 +184,8 @@ def main():
     full.status = capi.ptr(status, capi.P32)
     full.node_of_pod = capi.ptr(nodes_out, capi.P32)
     full.winner_map = capi.ptr(wmap, capi.P32)
-    assert lib.sr_plan_run(checker.handle, ctypes.byref(full)) == capi.SR_OK
+    st = lib.sr_plan_run(checker.handle, ctypes.byref(full))
+    assert st == capi.SR_OK, (st, checker.last_error())
     tm = checker.timing()  # bytes_placement is exact after a run with per-candidate outputs
 
     if rank == 0:

@@ -282,10 +282,12 @@ typedef struct {
 } sr_timing;
 /* mask: which kernels sr_plan_run brackets with HIP events (resets the sums):
  * 1 = K0, 2 = K2, 4 = collective (multi-GPU) + K3; 0 = no events.  Events are read back lazily, by
- * sr_get_timing / sr_set_timing, so timed runs do not synchronise. */
+ * sr_get_timing / sr_set_timing, so timed runs do not synchronise.  Timestamped dispatches
+ * lengthen a tick, so SR_TIME_EVERY(n) samples every n-th run only (n_runs counts sampled runs). */
 #define SR_TIME_TABLES      1
 #define SR_TIME_PLACEMENT   2
 #define SR_TIME_WINNER      4
+#define SR_TIME_EVERY(n)    ((n) << 8)
 sr_status sr_set_timing(sr_ctx *ctx, int32_t mask);
 sr_status sr_get_timing(sr_ctx *ctx, sr_timing *out);
 

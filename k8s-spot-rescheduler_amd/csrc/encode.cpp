@@ -485,7 +485,19 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   const int32_t n_reqs = static_cast<int32_t>(reqs.size());
   const int32_t n_ports = static_cast<int32_t>(port_dict.size());
   const int32_t A_REQ = 1, A_TAINT = 1 + n_reqs, A_PORT = 1 + n_reqs + n_taints;
-  w->n_atoms = A_PORT + n_ports;
+  // Composite atoms, one per distinct untolerated-taint set U of the pods:
+  // atom 0 AND NOT (OR of U's taint atoms) -- the pod-count check and
+  // TaintToleration / NodeUnschedulable in one row, so a class program opens
+  // with a single AND instead of 1 + |U| operations.
+  const int32_t A_COMP = A_PORT + n_ports;
+  std::unordered_map<const std::vector<int32_t>*, int32_t> comp_index;
+  std::vector<const std::vector<int32_t>*> comp_sets;
+  auto comp_atom = [&](const std::vector<int32_t>* u) {
+    if (u->empty()) return 0;  // tolerates every taint: the pod-count atom alone
+    auto ins = comp_index.emplace(u, static_cast<int32_t>(comp_sets.size()));
+    if (ins.second) comp_sets.push_back(u);
+    return A_COMP + ins.first->second;
+  };
 
   phase(2);
   // ---- intern classes (atom programs), once per distinct spec
@@ -514,9 +526,8 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       // program: AND atoms, AND-NOT atoms, then the ORed terms (TERM_START
       // opens a term, TERM_AND extends it); an impossible class ANDs atom 0
       // with its complement
-      emit(0, PROG_AND);  // len(pods)+1 <= allowed pods
+      emit(comp_atom(ps.untol), PROG_AND);  // len(pods)+1 <= allowed pods, untolerated taints
       for (int32_t r : ps.sel) emit(A_REQ + r, PROG_AND);
-      for (int32_t t : *ps.untol) emit(A_TAINT + t, PROG_ANDNOT);
       for (int32_t b = 0; b < 64; ++b)
         if (ps.ports >> b & 1) emit(A_PORT + b, PROG_ANDNOT);
       if (ps.flags & CLS_IMPOSSIBLE) {
@@ -531,6 +542,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     spec_class[sp] = ins.first->second;
   }
 
+  w->n_atoms = A_COMP + static_cast<int32_t>(comp_sets.size());
   phase(3);
   // ---- spot nodes: base capacity state and the atom rows
   const int32_t NP = w->n_pad, Wp = w->Wp;
@@ -576,6 +588,15 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     r[2] = static_cast<uint64_t>(w->free_eph[n]);
     r[3] = w->port_bits[n];
     r[4] = static_cast<uint64_t>(static_cast<int64_t>(w->pods_left[n]));
+  }
+  // composite atoms: atom 0 AND NOT (any taint of the set)
+  for (size_t k = 0; k < comp_sets.size(); ++k) {
+    uint64_t* row = &w->atoms[static_cast<size_t>(A_COMP + static_cast<int32_t>(k)) * Wp];
+    for (int32_t i = 0; i < Wp; ++i) {
+      uint64_t any = 0;
+      for (int32_t t : *comp_sets[k]) any |= w->atoms[static_cast<size_t>(A_TAINT + t) * Wp + i];
+      row[i] = w->atoms[i] & ~any;
+    }
   }
   // requirement atoms: one label-value column per distinct key
   std::unordered_map<int32_t, std::vector<int32_t>> col;  // key -> value per node (INT32_MIN absent)
@@ -738,6 +759,17 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     }
     w->t_off[d + 2] = static_cast<int32_t>(w->t_dim.size());
   }
+  // Node ranks: the dimension-d rows are in threshold order, so the rows a
+  // node belongs to (threshold <= its free value) are a prefix of them; K0
+  // sets bit n of the dimension's row r exactly when r < rank(n).
+  w->node_rank.assign(static_cast<size_t>(3) * NP, 0);
+  for (int d = 0; d < 3; ++d) {
+    std::vector<int32_t> below(used[d].size() + 1, 0);  // used positions in [0, pos)
+    for (size_t pos = 0; pos < used[d].size(); ++pos) below[pos + 1] = below[pos] + used[d][pos];
+    const std::vector<int64_t>& fr = *frees[d];
+    int32_t* rk = &w->node_rank[static_cast<size_t>(d) * NP];
+    for (int32_t n = 0; n < n_spot; ++n) rk[n] = below[lb[d](fr[n]) + 1];  // fr[n] is node_vals[d][pos]
+  }
   for (int32_t q = 0; q < na; ++q) {
     int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
     for (int d = 0; d < 3; ++d) r[1 + d] = r[1 + d] < 0 ? 0 : t_index[d][static_cast<size_t>(r[1 + d])];
@@ -749,6 +781,20 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   if ((static_cast<uint64_t>(w->n_classes) + w->t_dim.size()) * static_cast<uint64_t>(w->Wp) >= (1ull << 32)) {
     *err = "bitmask tables exceed 2^32 words";
     return SR_ERR_CAPACITY;
+  }
+
+  // ---- class programs of <= 8 operations in fixed 8-slot records (K0 reads
+  // one record with one scalar load); -1 pads, -2 in slot 0 marks a longer
+  // program (read through cls_prog_off)
+  w->cls_prog8.assign(static_cast<size_t>(w->n_classes) * 8, -1);
+  for (int32_t c = 0; c < w->n_classes; ++c) {
+    const int32_t o = w->cls_prog_off[c], len = w->cls_prog_off[c + 1] - o;
+    int32_t* slot = &w->cls_prog8[static_cast<size_t>(c) * 8];
+    if (len > 8) {
+      slot[0] = -2;
+      continue;
+    }
+    for (int32_t i = 0; i < len; ++i) slot[i] = w->cls_prog[o + i];
   }
 
   phase(5);

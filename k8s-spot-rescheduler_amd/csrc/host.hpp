@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/sr_planner.h"
+#include "progops.hpp"
 
 namespace sr {
 
@@ -70,8 +71,6 @@ void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t 
 
 // Class descriptor flags.
 enum : int32_t { CLS_AFF_REQUIRED = 1, CLS_IMPOSSIBLE = 2 };
-// class program ops (K0): acc &= atom | acc &= ~atom | open an ORed term | AND into the open term
-enum : int32_t { PROG_AND = 0, PROG_ANDNOT = 1, PROG_TERM_START = 2, PROG_TERM_AND = 3 };
 
 // The encoded workload of one planning call (host copy; uploaded as one arena).
 struct Workload {
@@ -96,10 +95,12 @@ struct Workload {
   int32_t n_classes = 0;
   int32_t empty_class = -1;  // all-zero S row for pods whose F row is certainly empty (-1: none)
   std::vector<int32_t> cls_prog_off, cls_prog;  // CSR class -> ops (atom << 2 | PROG_*)
+  std::vector<int32_t> cls_prog8;               // [n_classes][8] the same ops, -1 padded; -2: longer program
   // ---- T rows: capacity thresholds.  Row 0 = every node (zero-request pods
   // skip the resource checks); other rows: free_<dim>[n] >= thr.
   std::vector<int32_t> t_dim;   // 0 cpu, 1 memory, 2 ephemeral, 3 all
   std::vector<int64_t> t_thr;
+  std::vector<int32_t> node_rank;  // [3][n_pad] rows of the dimension a node belongs to (a prefix)
   int32_t t_off[5] = {0, 0, 0, 0, 0};  // rows [t_off[i], t_off[i+1]): all, cpu, memory, ephemeral
   // ---- active pods, grouped by candidate, in podsForDeletion order
   std::vector<int32_t> pod_rows;  // [n][4]: S row (class), T rows for cpu, memory, ephemeral

@@ -17,6 +17,8 @@
 
 #include "kernels.hpp"
 
+#include <hip/hip_ext.h>
+
 namespace sr {
 namespace {
 
@@ -35,21 +37,6 @@ __device__ __forceinline__ void writelane(uint32_t& v, uint32_t x) {
   asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(L));
 }
 
-// K0 T rows: row r0 + t of a group = ballot(free >= thr[t]), kept in lane t.
-// Lane t holds thr[t]; a constant-lane readlane makes it scalar.
-template <int T>
-__device__ __forceinline__ void t_rows(uint32_t& lo, uint32_t& hi, int nr, bool valid, bool all, int64_t v,
-                                       int64_t my_thr) {
-  if constexpr (T < 64) {
-    if (T >= nr) return;
-    const int64_t thr = static_cast<int64_t>(readlane64(static_cast<uint64_t>(my_thr), T));
-    const uint64_t m = ballot(valid && (all || v >= thr));
-    writelane<T>(lo, static_cast<uint32_t>(m));
-    writelane<T>(hi, static_cast<uint32_t>(m >> 32));
-    t_rows<T + 1>(lo, hi, nr, valid, all, v, my_thr);
-  }
-}
-
 // Minimum over the 64 lanes with DPP row shifts / broadcasts (no LDS round trips).
 template <int CTRL, int ROW_MASK = 0xf>
 __device__ __forceinline__ int dpp_min(int v) {
@@ -65,11 +52,55 @@ __device__ __forceinline__ int wave_min(int v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
-// K0: bitmask rows.  Blocks [0, s_blocks): one wave per class, lanes = words
-// (S rows, word-parallel atom programs).  Blocks after: T rows, grid over
-// (row groups of 64) x (Wp / 4): each wave owns one 64-node word, loads its
-// nodes' free capacity once and evaluates 64 thresholds (one ballot each),
-// lane t keeping row r0 + t.
+// K0: bitmask rows.  Blocks [0, s_blocks): S rows, kSClasses classes per
+// wave, lanes = words; blocks after: T rows, lanes = rows.
+constexpr int kSClasses = 2;  // S rows per wave: their atom loads are in flight together
+constexpr int kTWords = 2;    // T row words per wave
+
+// One S row by the class's atom program read through cls_prog_off (any length):
+// 64 words (lanes) at a time, the program loaded lane-parallel, its atom words
+// fetched 8 at a time.
+__device__ void s_row_general(const DevWorkload& w, int cls, int lane) {
+  const int o0 = w.cls_prog_off[cls], n = w.cls_prog_off[cls + 1] - o0;
+  const size_t Wp = static_cast<size_t>(w.Wp);
+  for (int wb = 0; wb < w.Wp; wb += 64) {
+    const int word = wb + lane;
+    const bool wv = word < w.Wp;
+    const uint64_t* __restrict__ at = w.atoms + (wv ? word : 0);
+    uint64_t acc = ~0ull, any = 0, cur = 0;
+    bool has = false;
+    for (int base = 0; base < n; base += 64) {
+      const int m = min(64, n - base);
+      const int my = lane < m ? w.cls_prog[o0 + base + lane] : 0;
+      for (int j0 = 0; j0 < m; j0 += 8) {
+        uint64_t v[8];
+        int op[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          op[u] = __builtin_amdgcn_readlane(my, j0 + u);
+          v[u] = j0 + u < m ? at[static_cast<size_t>(op[u] >> 2) * Wp] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (j0 + u >= m) break;
+          switch (op[u] & 3) {
+            case PROG_AND: acc &= v[u]; break;
+            case PROG_ANDNOT: acc &= ~v[u]; break;
+            case PROG_TERM_START:
+              any |= has ? cur : 0;
+              cur = v[u];
+              has = true;
+              break;
+            default: cur &= v[u]; break;
+          }
+        }
+      }
+    }
+    if (has) acc &= any | cur;
+    if (wv) w.S[static_cast<size_t>(cls) * Wp + word] = acc;
+  }
+}
+
 __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, int local_first_fallback) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -89,76 +120,104 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
     dm[0] = ~0ull;
     dm[1] = local_first_fallback < 0 ? ~0ull : static_cast<unsigned long long>(local_first_fallback) << 32;
   }
+  const size_t Wp = static_cast<size_t>(w.Wp);
   if (static_cast<int>(blockIdx.x) < s_blocks) {
-    // S row of one class: its atom program, 64 words (lanes) at a time.
-    //   NodeAffinity (nodeSelector pairs; required terms ORed, requirements
-    //   ANDed), TaintToleration + NodeUnschedulable (untolerated taint atoms
-    //   negated), NodePorts (the class's ports against base UsedPorts), pod
-    //   count (atom 0).  The program is loaded lane-parallel and its atom
-    //   words are fetched 8 at a time, so a class costs ~3 memory latencies.
-    const int cls = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wave);
-    if (cls >= w.n_classes) return;
-    const int o0 = w.cls_prog_off[cls], n = w.cls_prog_off[cls + 1] - o0;
-    const size_t Wp = static_cast<size_t>(w.Wp);
+    // S rows (NodeAffinity: nodeSelector pairs, required terms ORed with
+    // their requirements ANDed; TaintToleration + NodeUnschedulable + pod
+    // count: the composite atom; NodePorts: the class's ports against the
+    // base UsedPorts).  A program of <= 8 operations is one scalar load; the
+    // atom words of both classes are loaded before either is evaluated.
+    const int c0 = __builtin_amdgcn_readfirstlane((static_cast<int>(blockIdx.x) * 4 + wave) * kSClasses);
+    int op[kSClasses][8];
+#pragma unroll
+    for (int q = 0; q < kSClasses; ++q) {
+      const int cls = c0 + q;
+      if (cls < w.n_classes) {
+        const int4* p8 = reinterpret_cast<const int4*>(w.cls_prog8 + static_cast<size_t>(cls) * 8);
+        const int4 a = p8[0], b = p8[1];
+        op[q][0] = a.x; op[q][1] = a.y; op[q][2] = a.z; op[q][3] = a.w;
+        op[q][4] = b.x; op[q][5] = b.y; op[q][6] = b.z; op[q][7] = b.w;
+      } else {
+        op[q][0] = -3;  // no class
+#pragma unroll
+        for (int u = 1; u < 8; ++u) op[q][u] = -1;
+      }
+    }
     for (int wb = 0; wb < w.Wp; wb += 64) {
       const int word = wb + lane;
       const bool wv = word < w.Wp;
-      const uint64_t* __restrict__ at = w.atoms + (wv ? word : 0);
-      uint64_t acc = ~0ull, any = 0, cur = 0;
-      bool has = false;
-      for (int base = 0; base < n; base += 64) {
-        const int m = min(64, n - base);
-        const int my = lane < m ? w.cls_prog[o0 + base + lane] : 0;
-        for (int j0 = 0; j0 < m; j0 += 8) {
-          uint64_t v[8];
-          int op[8];
+      const size_t wi = wv ? static_cast<size_t>(word) : 0;
+      uint64_t v[kSClasses][8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            op[u] = __builtin_amdgcn_readlane(my, j0 + u);
-            v[u] = j0 + u < m ? at[static_cast<size_t>(op[u] >> 2) * Wp] : 0;
-          }
+      for (int q = 0; q < kSClasses; ++q)
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            if (j0 + u >= m) break;
-            switch (op[u] & 3) {
-              case 0: acc &= v[u]; break;
-              case 1: acc &= ~v[u]; break;
-              case 2:
-                any |= has ? cur : 0;
-                cur = v[u];
-                has = true;
-                break;
-              default: cur &= v[u]; break;
-            }
+        for (int u = 0; u < 8; ++u) v[q][u] = op[q][u] >= 0 ? w.atoms[static_cast<size_t>(op[q][u] >> 2) * Wp + wi] : 0;
+#pragma unroll
+      for (int q = 0; q < kSClasses; ++q) {
+        if (op[q][0] < 0 && op[q][0] != -1) continue;  // no class, or a long program (below)
+        uint64_t acc = ~0ull, any = 0, cur = 0;
+        bool has = false;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (op[q][u] < 0) break;  // wave-uniform
+          switch (op[q][u] & 3) {
+            case PROG_AND: acc &= v[q][u]; break;
+            case PROG_ANDNOT: acc &= ~v[q][u]; break;
+            case PROG_TERM_START:
+              any |= has ? cur : 0;
+              cur = v[q][u];
+              has = true;
+              break;
+            default: cur &= v[q][u]; break;
           }
         }
+        if (has) acc &= any | cur;
+        if (wv) w.S[static_cast<size_t>(c0 + q) * Wp + word] = acc;
       }
-      if (has) acc &= any | cur;
-      if (wv) w.S[static_cast<size_t>(cls) * Wp + word] = acc;
     }
+#pragma unroll
+    for (int q = 0; q < kSClasses; ++q)
+      if (op[q][0] == -2) s_row_general(w, c0 + q, lane);
     return;
   }
-  // T rows: one wave per (dimension, group of 64 rows, 64-node word), lanes =
-  // nodes; row r of the group = ballot(free >= thr[r]) written into lane r.
+  // T rows: one wave per (dimension, group of 64 rows, kTWords words), lanes
+  // = rows.  A node lies in its dimension's rows [0, rank) (the encoder's
+  // node ranks), so bit i of lane r's word W is r < rank[64 W + i]: the
+  // word's 64 ranks are one coalesced load, each broadcast by a readlane, and
+  // a node costs a compare and a shift-or -- no cross-lane ballots.
   int tw = (static_cast<int>(blockIdx.x) - s_blocks) * 4 + wave;
+  const int wgroups = (w.Wp + kTWords - 1) / kTWords;
   int d = 0;
   for (; d < 4; ++d) {
-    const int waves_d = (w.t_off[d + 1] - w.t_off[d] + 63) / 64 * w.Wp;
+    const int waves_d = (w.t_off[d + 1] - w.t_off[d] + 63) / 64 * wgroups;
     if (tw < waves_d) break;
     tw -= waves_d;
   }
   if (d == 4) return;  // wave-uniform
-  const int g = tw / w.Wp;
-  const int word = tw - g * w.Wp;
-  const int n = word * 64 + lane;  // < n_pad: node arrays are padded
-  const bool valid = n < w.n_spot;
+  const int g = tw / wgroups;
+  const int W0 = (tw - g * wgroups) * kTWords;
   const int r0 = w.t_off[d] + 64 * g;
   const int nr = min(64, w.t_off[d + 1] - r0);
-  const int64_t v = d == 1 ? w.free_cpu[n] : (d == 2 ? w.free_mem[n] : (d == 3 ? w.free_eph[n] : 0));
-  uint32_t lo = 0, hi = 0;
-  const int64_t my_thr = lane < nr ? w.t_thr[r0 + lane] : 0;
-  t_rows<0>(lo, hi, nr, valid, d == 0, v, my_thr);
-  if (lane < nr) w.T[static_cast<size_t>(r0 + lane) * w.Wp + word] = static_cast<uint64_t>(hi) << 32 | lo;
+  const int rr = 64 * g + lane;  // this lane's row within the dimension
+#pragma unroll
+  for (int ww = 0; ww < kTWords; ++ww) {
+    const int W = W0 + ww;
+    if (W >= w.Wp) break;  // wave-uniform
+    uint64_t word;
+    if (d == 0) {  // row 0: every node
+      const int nvalid = max(0, min(64, w.n_spot - 64 * W));
+      word = nvalid >= 64 ? ~0ull : (1ull << nvalid) - 1;
+    } else {
+      const int rk = w.node_rank[static_cast<size_t>(d - 1) * w.n_pad + 64 * W + lane];  // pad nodes: 0
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) lo |= static_cast<uint32_t>(rr < __builtin_amdgcn_readlane(rk, i)) << i;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) hi |= static_cast<uint32_t>(rr < __builtin_amdgcn_readlane(rk, 32 + i)) << i;
+      word = static_cast<uint64_t>(hi) << 32 | lo;
+    }
+    if (lane < nr) w.T[static_cast<size_t>(r0 + lane) * Wp + W] = word;
+  }
 }
 
 
@@ -898,39 +957,49 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   }
 }
 
+// Launch with optional HIP events recorded by the dispatch itself
+// (hipExtLaunchKernelGGL: no event packets or host calls around the kernel).
+template <typename K, typename... A>
+void launch(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, A... args) {
+  if (ev0) hipExtLaunchKernelGGL(kernel, grid, block, static_cast<uint32_t>(lds), s, ev0, ev1, 0, args...);
+  else hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+}
+
 template <bool PROF>
-hipError_t launch_k2(const DevWorkload& w, hipStream_t s) {
+hipError_t launch_k2(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
   if (n <= 0) return hipSuccess;
   const dim3 grid((n + 3) / 4), block(256);
   const size_t lds = 4 * sizeof(K2Lds);
   const int chunks = (w.Wp + 63) / 64;
-  if (chunks <= 1) hipLaunchKernelGGL((k2_place<1, PROF>), grid, block, lds, s, w, w.list, n);
-  else if (chunks <= 2) hipLaunchKernelGGL((k2_place<2, PROF>), grid, block, lds, s, w, w.list, n);
-  else if (chunks <= 4) hipLaunchKernelGGL((k2_place<4, PROF>), grid, block, lds, s, w, w.list, n);
-  else if (chunks <= 8) hipLaunchKernelGGL((k2_place<8, PROF>), grid, block, lds, s, w, w.list, n);
-  else if (chunks <= 16) hipLaunchKernelGGL((k2_place<16, PROF>), grid, block, lds, s, w, w.list, n);
-  else hipLaunchKernelGGL((k2_place<32, PROF>), grid, block, lds, s, w, w.list, n);
+  if (chunks <= 1) launch(k2_place<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (chunks <= 2) launch(k2_place<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (chunks <= 4) launch(k2_place<4, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (chunks <= 8) launch(k2_place<8, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (chunks <= 16) launch(k2_place<16, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else launch(k2_place<32, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hipStream_t s) {
-  const int s_blocks = (w.n_classes + 3) / 4;
+hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hipStream_t s, hipEvent_t ev0,
+                         hipEvent_t ev1) {
+  const int s_blocks = (w.n_classes + 4 * kSClasses - 1) / (4 * kSClasses);
+  const int wgroups = (w.Wp + kTWords - 1) / kTWords;
   int t_waves = 0;
-  for (int d = 0; d < 4; ++d) t_waves += (w.t_off[d + 1] - w.t_off[d] + 63) / 64 * w.Wp;
+  for (int d = 0; d < 4; ++d) t_waves += (w.t_off[d + 1] - w.t_off[d] + 63) / 64 * wgroups;
   const unsigned blocks = static_cast<unsigned>(std::max(1, s_blocks + (t_waves + 3) / 4));
-  hipLaunchKernelGGL(k0_tables, dim3(blocks), dim3(256), 0, s, w, s_blocks, local_first_fallback);
+  launch(k0_tables, dim3(blocks), dim3(256), 0, s, ev0, ev1, w, s_blocks, local_first_fallback);
   return hipGetLastError();
 }
 
-hipError_t launch_placement(const DevWorkload& w, hipStream_t s) {
-  return w.prof ? launch_k2<true>(w, s) : launch_k2<false>(w, s);
+hipError_t launch_placement(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  return w.prof ? launch_k2<true>(w, s, ev0, ev1) : launch_k2<false>(w, s, ev0, ev1);
 }
 
-hipError_t launch_winner(const DevWorkload& w, hipStream_t s) {
-  hipLaunchKernelGGL(k3_winner, dim3(1), dim3(64), 0, s, w);
+hipError_t launch_winner(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  launch(k3_winner, dim3(1), dim3(64), 0, s, ev0, ev1, w);
   return hipGetLastError();
 }
 

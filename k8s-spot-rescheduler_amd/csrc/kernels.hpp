@@ -5,6 +5,8 @@
 
 #include <cstdint>
 
+#include "progops.hpp"
+
 namespace sr {
 
 constexpr int kResultHeader = 8;
@@ -13,14 +15,13 @@ constexpr size_t kK0ProfWaves = 32768;  // K0 waves profiled after K2's [n_cand]
 // Pointers into the device arena (layout: DESIGN.md §HBM layout).
 struct DevWorkload {
   int32_t n_spot, n_pad, Wp;
-  const int64_t* free_cpu;
-  const int64_t* free_mem;
-  const int64_t* free_eph;
+  const int32_t* node_rank;    // [3][n_pad] per dimension: the node is in that dimension's T rows [0, rank)
   const uint64_t* node_rec;    // [n_pad][8] AoS {free cpu, mem, eph, ports, pods_left, 0, 0, 0} for K2
   int32_t n_atoms;
   const uint64_t* atoms;       // [n_atoms][Wp] node bitsets (encode.cpp)
   const int32_t* cls_prog_off; // class atom programs (CSR): ops atom << 2 | {AND, AND NOT,
   const int32_t* cls_prog;     //   open an ORed term, AND into the open term}
+  const int32_t* cls_prog8;    // [n_classes][8] programs of <= 8 ops (-1 pad, -2: use cls_prog)
   int32_t n_classes;
   uint32_t s_empty_off;     // word offset of the all-zero S row pods with a certainly empty F row point
                             // at (encode.cpp), 0xffffffff if there is none
@@ -51,10 +52,12 @@ struct DevWorkload {
 };
 
 // K0: S and T rows (also resets d_min: d_min[1] = local first fallback).
-hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hipStream_t s);
+// ev0 / ev1 (optional): HIP events the dispatch records around the kernel.
+hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hipStream_t s,
+                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // K2: per-candidate feasibility rows + first-fit placement; atomicMin of first_ok into d_min[0].
-hipError_t launch_placement(const DevWorkload& w, hipStream_t s);
+hipError_t launch_placement(const DevWorkload& w, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // K3: winner mapping into `result` (after the collective when ranks > 1), then the run's seq.
-hipError_t launch_winner(const DevWorkload& w, hipStream_t s);
+hipError_t launch_winner(const DevWorkload& w, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 }  // namespace sr

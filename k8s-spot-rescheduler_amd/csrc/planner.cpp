@@ -44,7 +44,9 @@ struct sr_ctx {
   sr::Workload wl;
   sr::DevWorkload dw{};
   bool prepared = false;
-  int32_t timing = 0;
+  int32_t timing = 0;        // SR_TIME_* kernel bits of the current setting
+  int32_t timing_every = 1;  // sample every n-th run
+  int64_t timing_runs = 0;   // runs since sr_set_timing
   // HIP event pairs bracketing timed kernels, read back lazily (flush_timing)
   // so a timed run does not have to synchronise the stream.
   std::vector<hipEvent_t> ev_start, ev_end;
@@ -141,10 +143,10 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const int32_t na = static_cast<int32_t>(w.pod_src.size());
   const int32_t ncand = static_cast<int32_t>(w.cand_global.size());
   Packer pk;
-  const size_t o_fc = pk.add(w.free_cpu), o_fm = pk.add(w.free_mem), o_fe = pk.add(w.free_eph);
+  const size_t o_rk = pk.add(w.node_rank);
   const size_t o_nr = pk.add(w.node_rec);
   const size_t o_at = pk.add(w.atoms);
-  const size_t o_cpo = pk.add(w.cls_prog_off), o_cp = pk.add(w.cls_prog);
+  const size_t o_cpo = pk.add(w.cls_prog_off), o_cp = pk.add(w.cls_prog), o_cp8 = pk.add(w.cls_prog8);
   const size_t o_tt = pk.add(w.t_thr);
   const size_t o_prec = pk.add(w.pod_rec);
   const size_t o_co = pk.add(w.cand_off), o_cg = pk.add(w.cand_global);
@@ -175,14 +177,13 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.n_spot = w.n_spot;
   d.n_pad = w.n_pad;
   d.Wp = w.Wp;
-  d.free_cpu = static_cast<const int64_t*>(at(o_fc));
-  d.free_mem = static_cast<const int64_t*>(at(o_fm));
-  d.free_eph = static_cast<const int64_t*>(at(o_fe));
+  d.node_rank = static_cast<const int32_t*>(at(o_rk));
   d.node_rec = static_cast<const uint64_t*>(at(o_nr));
   d.n_atoms = w.n_atoms;
   d.atoms = static_cast<const uint64_t*>(at(o_at));
   d.cls_prog_off = static_cast<const int32_t*>(at(o_cpo));
   d.cls_prog = static_cast<const int32_t*>(at(o_cp));
+  d.cls_prog8 = static_cast<const int32_t*>(at(o_cp8));
   d.n_classes = w.n_classes;
   d.s_empty_off = w.empty_class >= 0 ? static_cast<uint32_t>(w.empty_class) * static_cast<uint32_t>(w.Wp) : 0xffffffffu;
   d.n_t = static_cast<int32_t>(w.t_dim.size());
@@ -216,7 +217,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   // K0 algorithmic bytes: every table row written once; every atom row a class
   // program names, the nodes' free capacities and the thresholds read once.
   uint64_t atom_reads = w.cls_prog.size();
-  ctx->t.bytes_tables = n_rows * row + atom_reads * row + 3ull * 8 * w.n_pad + 8ull * w.t_dim.size();
+  ctx->t.bytes_tables = n_rows * row + atom_reads * row + 3ull * 4 * w.n_pad + 32ull * w.n_classes;
   // K2 (upper bound until a full run refines it, see run()): per pod its
   // four row chunks and its record, per candidate its mapping and status.
   ctx->t.bytes_placement = 4ull * ncand;
@@ -260,57 +261,60 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   hipStream_t s = ctx->stream;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   const bool collective = ctx->comm && use_comm;
+  const int32_t timing = (ctx->timing_runs++ % ctx->timing_every) == 0 ? ctx->timing : 0;
   d.seq = ++ctx->seq;
   volatile int32_t* res = static_cast<volatile int32_t*>(ctx->h_result.p);
   res[4] = 0;
-  size_t pair[3] = {0, 0, 0};
-  auto mark = [&](int k, int end) -> sr_status {
-    if (!(ctx->timing >> k & 1)) return SR_OK;
-    if (!end) {
-      if (ctx->ev_used == ctx->ev_start.size()) {
-        if (ctx->ev_used >= 3072) {  // bounded pool: read back what is pending
-          sr_status st = flush_timing(ctx);
-          if (st != SR_OK) return st;
-        } else {
-          hipEvent_t a, b;
-          HIP_TRY(ctx, hipEventCreate(&a));
-          HIP_TRY(ctx, hipEventCreate(&b));
-          ctx->ev_start.push_back(a);
-          ctx->ev_end.push_back(b);
-          ctx->ev_kernel.push_back(0);
-        }
+  // Timed kernels get an event pair from the pool, recorded by their own
+  // dispatch (hipExtLaunchKernelGGL); the collective is bracketed with
+  // plain records.  Events are read back lazily (flush_timing).
+  auto pair_for = [&](int k, hipEvent_t* a, hipEvent_t* b) -> sr_status {
+    *a = *b = nullptr;
+    if (!(timing >> k & 1)) return SR_OK;
+    if (ctx->ev_used == ctx->ev_start.size()) {
+      if (ctx->ev_used >= 3072) {  // bounded pool: read back what is pending
+        sr_status st = flush_timing(ctx);
+        if (st != SR_OK) return st;
+      } else {
+        hipEvent_t e0, e1;
+        HIP_TRY(ctx, hipEventCreate(&e0));
+        HIP_TRY(ctx, hipEventCreate(&e1));
+        ctx->ev_start.push_back(e0);
+        ctx->ev_end.push_back(e1);
+        ctx->ev_kernel.push_back(0);
       }
-      pair[k] = ctx->ev_used++;
-      ctx->ev_kernel[pair[k]] = static_cast<int8_t>(k);
-      HIP_TRY(ctx, hipEventRecord(ctx->ev_start[pair[k]], s));
-    } else {
-      HIP_TRY(ctx, hipEventRecord(ctx->ev_end[pair[k]], s));
     }
+    const size_t i = ctx->ev_used++;
+    ctx->ev_kernel[i] = static_cast<int8_t>(k);
+    *a = ctx->ev_start[i];
+    *b = ctx->ev_end[i];
     return SR_OK;
   };
-#define MARK(k, e)                      \
-  do {                                  \
-    sr_status _st = mark((k), (e));     \
-    if (_st != SR_OK) return _st;       \
+#define PAIR(k, a, b)                         \
+  hipEvent_t a, b;                            \
+  do {                                        \
+    sr_status _st = pair_for((k), &a, &b);    \
+    if (_st != SR_OK) return _st;             \
   } while (0)
-  MARK(0, 0);
-  HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s));
-  MARK(0, 1);
-  MARK(1, 0);
-  HIP_TRY(ctx, sr::launch_placement(d, s));
-  MARK(1, 1);
-  MARK(2, 0);
+  PAIR(0, e0a, e0b);
+  HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
+  PAIR(1, e1a, e1b);
+  HIP_TRY(ctx, sr::launch_placement(d, s, e1a, e1b));
+  PAIR(2, e2a, e2b);
   if (collective) {
+    if (e2a) HIP_TRY(ctx, hipEventRecord(e2a, s));
     ncclResult_t r = ncclAllReduce(d.d_min, d.d_min, 2, ncclUint64, ncclMin, ctx->comm, s);
     if (r != ncclSuccess) {
       ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
       return SR_ERR_RCCL;
     }
+    HIP_TRY(ctx, sr::launch_winner(d, s));
+    if (e2b) HIP_TRY(ctx, hipEventRecord(e2b, s));
+  } else {
+    HIP_TRY(ctx, sr::launch_winner(d, s, e2a, e2b));
   }
-  HIP_TRY(ctx, sr::launch_winner(d, s));
-  MARK(2, 1);
-#undef MARK
-  if (ctx->timing) ctx->t.n_runs += 1;
+#undef PAIR
+  if (timing) ctx->t.n_runs += 1;
   const int32_t na = d.n_pods, ncand = d.n_cand;
   if (full || ctx->prof_file) {
     if (full) {
@@ -500,6 +504,8 @@ sr_status sr_set_timing(sr_ctx* ctx, int32_t mask) {
   sr_status st = flush_timing(ctx);
   if (st != SR_OK) return st;
   ctx->timing = mask & 7;
+  ctx->timing_every = std::max(1, (mask >> 8) & 0xffff);
+  ctx->timing_runs = 0;
   ctx->t.n_runs = 0;
   ctx->t.ms_tables = ctx->t.ms_placement = ctx->t.ms_winner = 0;
   return SR_OK;
