@@ -640,6 +640,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   const uint64_t* __restrict__ tab = w.S;
   int64_t rc[G], rm[G], re[G];
   uint64_t pm[G], r01[G], r23[G], fmask[G], act[G];
+  uint64_t cur[G];  // F word holding the pod's pointer: moves inside a word need no LDS read
   uint32_t hmask[G];
   bool zero[G];
   int ptr[G], node[G];
@@ -656,6 +657,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     zero[g] = (rc[g] | rm[g] | re[g]) == 0;  // fitsRequest skips the resource checks
     fmask[g] = 0;
     hmask[g] = 0;
+    cur[g] = 0;
     ptr[g] = INT_MAX;
     node[g] = -1;
     const uint64_t e = ballot(64 * g + lane < np && static_cast<uint32_t>(r01[g]) == w.s_empty_off);
@@ -707,7 +709,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     if (k < dead) {
       if (hmask[g] != 0) {
         const int w0 = __builtin_ctz(hmask[g]);
-        ptr[g] = w0 * 64 + __builtin_ctzll(F[k * kNHS + w0]);
+        cur[g] = F[k * kNHS + w0];
+        ptr[g] = w0 * 64 + __builtin_ctzll(cur[g]);
       } else {
         ptr[g] = Wp > kNH ? kFar : INT_MAX;
       }
@@ -773,9 +776,11 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
               const int w2 = __builtin_ctzll(m);
               nx = w2 * 64 + __builtin_ctzll(readlane64(f, w2));
             }
+            const uint64_t fw = nx == INT_MAX ? 0ull : readlane64(f, nx >> 6);
             if (lane == js[q]) {
               fmask[g] = m;
               ptr[g] = nx;
+              cur[g] = fw;
             }
             if (nx == INT_MAX) dead = min(dead, 64 * g + js[q]);
           }
@@ -847,16 +852,16 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       // pods that did not fit n: next set bit of their F row after n
       const int k = 64 * g + lane;
       if ((failed[g] >> lane) & 1) {
-        uint64_t f = W < kNH ? F[k * kNHS + W] : f_word_far(tab, r01[g], r23[g], W);
-        f = b == 63 ? 0ull : f & (~0ull << (b + 1));
+        const uint64_t f = b == 63 ? 0ull : cur[g] & (~0ull << (b + 1));
         int nx = INT_MAX;
-        if (f != 0) {
+        if (f != 0) {  // the common case: the next feasible node is in the same word
           nx = W * 64 + __builtin_ctzll(f);
         } else if (W < kNH) {
           const uint32_t rem = hmask[g] & (0xffu << (W + 1)) & 0xffu;
           if (rem != 0) {
             const int w2 = __builtin_ctz(rem);
-            nx = w2 * 64 + __builtin_ctzll(F[k * kNHS + w2]);
+            cur[g] = F[k * kNHS + w2];
+            nx = w2 * 64 + __builtin_ctzll(cur[g]);
           } else if (Wp > kNH) {
             nx = kFar;
           }
@@ -864,7 +869,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
           const uint64_t rem = W == 63 ? 0ull : fmask[g] & (~0ull << (W + 1));
           if (rem != 0) {
             const int w2 = __builtin_ctzll(rem);
-            nx = w2 * 64 + __builtin_ctzll(f_word_far(tab, r01[g], r23[g], w2));
+            cur[g] = f_word_far(tab, r01[g], r23[g], w2);
+            nx = w2 * 64 + __builtin_ctzll(cur[g]);
           }
         }
         ptr[g] = nx;
