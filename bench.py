@@ -32,7 +32,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 from spotplanner import capi  # noqa: E402
 from spotplanner.planner import PredicateChecker  # noqa: E402
-from spotplanner.synth import SynthCluster, build_candidates, new_node_map, shard  # noqa: E402
+from spotplanner.synth import SynthCluster, new_node_map, pods_for_deletion, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 DEFAULT_OD = {1: 10, 2: 300, 3: 1500, 4: 15000, 5: 300}
@@ -103,7 +103,13 @@ def main():
     lib = capi.load_planner()
     sc = SynthCluster(args.config, n_on_demand=DEFAULT_OD[args.config] * world)
     nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
-    cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+    # run()'s candidate lists (rescheduler.go:228-264): GetPodsForDeletionOnNodeDrain + the
+    # DaemonSet-owner filter, on the host (sr_pods_for_deletion)
+    t0 = time.perf_counter()
+    cand_off, cand_pods, _, _, st = pods_for_deletion(lib.sr_pods_for_deletion, sc.ptr, ctypes.byref(sc.drain),
+                                                      nm.on_demand, nm.node_pod_off, nm.node_pod_idx)
+    pfd_ms = 1e3 * (time.perf_counter() - t0)
+    assert st == capi.SR_OK, st
     loff, lpods, gidx = shard(cand_off, cand_pods, rank, world)
 
     snap = ctypes.c_void_p()
@@ -213,6 +219,7 @@ def main():
             "workload_rows": {"static_classes": tm.n_rows_static, "threshold_rows": tm.n_rows_threshold,
                               "words_per_row": tm.n_words},
             "host_pack_ms": round(pack_ms, 3),
+            "host_pods_for_deletion_ms": round(pfd_ms, 3),
             "roofline": {"bound": "hbm", "kernel": dom, "kernel_ms": round(dom_ms, 5),
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

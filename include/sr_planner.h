@@ -43,6 +43,7 @@ typedef int32_t sr_status;
 #define SR_ERR_RCCL           5  /* RCCL error */
 #define SR_ERR_NO_DEVICE      6  /* no HIP device: the planner never falls back to the CPU */
 #define SR_ERR_STATE          7  /* call sequence error (e.g. Revert without Fork) */
+#define SR_ERR_NIL_CONTROLLER 8  /* rescheduler.go:244 dereferences a nil OwnerReference.Controller: the reference panics */
 
 /* -------------------------------------------------------------- enumerations */
 /* Taint / toleration effects (k8s.io/api/core/v1 TaintEffect). */
@@ -181,6 +182,74 @@ sr_status sr_new_node_map(const sr_cluster *cluster, const sr_node_map_params *p
 
 /* Replaces isSpotNode / isOnDemandNode (nodes/nodes.go:168-209).  Host-only. */
 int32_t sr_node_has_label(const sr_cluster *cluster, int32_t node, const sr_node_label *label);
+
+/* --------------------------------------------------- pods to move per candidate */
+/* Drain attributes of a pod for cluster-autoscaler utils/drain
+ * GetPodsForDeletionOnNodeDrain (@03f60a4c3818 [upstream, not in the reference
+ * tree]; call rescheduler.go:231), derived by the shim from the Pod object. */
+#define SR_DRAIN_CTRL_MASK          0x7u   /* kind of the ControllerRef (first owner ref with Controller == true): */
+#define SR_DRAIN_CTRL_NONE          0u
+#define SR_DRAIN_CTRL_REPLICATION_CONTROLLER 1u
+#define SR_DRAIN_CTRL_DAEMONSET     2u
+#define SR_DRAIN_CTRL_JOB           3u
+#define SR_DRAIN_CTRL_REPLICASET    4u
+#define SR_DRAIN_CTRL_STATEFULSET   5u
+#define SR_DRAIN_CTRL_OTHER         6u
+#define SR_DRAIN_DAEMONSET_ANNOTATION (1u << 3)  /* annotation cluster-autoscaler.kubernetes.io/daemonset-pod == "true" */
+#define SR_DRAIN_SAFE_TO_EVICT      (1u << 4)  /* annotation cluster-autoscaler.kubernetes.io/safe-to-evict == "true" */
+#define SR_DRAIN_NOT_SAFE_TO_EVICT  (1u << 5)  /*   ... == "false" */
+#define SR_DRAIN_DELETING           (1u << 6)  /* DeletionTimestamp != nil */
+#define SR_DRAIN_KUBE_SYSTEM        (1u << 7)  /* Namespace == "kube-system" */
+#define SR_DRAIN_KUBE_SYSTEM_PDB    (1u << 8)  /* checkKubeSystemPDBs(pod, kube-system PDBs in list order) == true */
+#define SR_DRAIN_PDB_ERROR          (1u << 9)  /* checkKubeSystemPDBs returns an error (a selector failing to
+                                                  convert before the first matching PDB) */
+#define SR_DRAIN_LOCAL_STORAGE      (1u << 10) /* an EmptyDir or HostPath volume */
+#define SR_DRAIN_NIL_CONTROLLER     (1u << 11) /* rescheduler.go:243-248 run on this pod dereferences a nil Controller */
+
+/* Pod phases (Status.Phase) and restart policies (Spec.RestartPolicy). */
+#define SR_PHASE_PENDING    0
+#define SR_PHASE_RUNNING    1
+#define SR_PHASE_SUCCEEDED  2
+#define SR_PHASE_FAILED     3
+#define SR_PHASE_UNKNOWN    4
+#define SR_RESTART_ALWAYS     0
+#define SR_RESTART_ON_FAILURE 1
+#define SR_RESTART_NEVER      2
+
+typedef struct {
+  int32_t         n;               /* = sr_pods.n */
+  const uint32_t *flags;           /* SR_DRAIN_* */
+  const uint8_t  *phase;           /* SR_PHASE_* */
+  const uint8_t  *restart_policy;  /* SR_RESTART_* */
+  const int64_t  *deletion_age_ns; /* now - DeletionTimestamp (read with SR_DRAIN_DELETING) */
+  const int64_t  *grace_seconds;   /* *Spec.TerminationGracePeriodSeconds, -1 = nil (30 s default) */
+} sr_pod_drain;
+
+typedef struct {
+  int32_t skip_nodes_with_system_pods;   /* argument 3 at rescheduler.go:231: *deleteNonReplicatedPods */
+  int32_t skip_nodes_with_local_storage; /* argument 4 at rescheduler.go:231: false */
+} sr_drain_params;
+
+/* drain.BlockingPodReason */
+#define SR_BLOCK_NONE                 0
+#define SR_BLOCK_NOT_REPLICATED       1
+#define SR_BLOCK_UNMOVABLE_KUBE_SYSTEM 2
+#define SR_BLOCK_LOCAL_STORAGE        3
+#define SR_BLOCK_NOT_SAFE_TO_EVICT    4
+#define SR_BLOCK_UNEXPECTED_ERROR     5
+
+/* The candidate lists of run() (rescheduler.go:228-264): for each node of
+ * `nodes` (on-demand NodeInfoArray order), GetPodsForDeletionOnNodeDrain over
+ * NodeInfo.Pods (node_pod_off / node_pod_idx, sr_node_map layout) with the
+ * reference's arguments, then the DaemonSet-owner filter (:240-256).
+ * out_cand_off [n_nodes + 1], out_cand_pods [<= all pods of the nodes]: the
+ * podsForDeletion of each node, in order.  A node with a blocking pod gets an
+ * empty list, its pod in out_block_pod (else -1) and the reason in
+ * out_block_reason (run() logs and `continue`s, :232-238).  Host-only. */
+sr_status sr_pods_for_deletion(const sr_cluster *cluster, const sr_pod_drain *drain, const sr_drain_params *params,
+                               const int32_t *nodes, int32_t n_nodes, const int32_t *node_pod_off,
+                               const int32_t *node_pod_idx, int32_t *out_cand_off, int32_t *out_cand_pods,
+                               int32_t *out_block_pod, int32_t *out_block_reason);
 
 /* ------------------------------------------------------------ cluster snapshot */
 typedef struct sr_snapshot sr_snapshot;

@@ -31,6 +31,8 @@ void sr_synth_destroy(sr_synth *s);
 void sr_synth_view(const sr_synth *s, sr_cluster *out);
 /* The --on-demand-node-label / --spot-node-label flags of the cluster (defaults of rescheduler.go:98-105). */
 void sr_synth_labels(const sr_synth *s, sr_node_label *on_demand, sr_node_label *spot);
+/* Drain attributes: ReplicaSet-controlled running pods, DaemonSet pods DaemonSet-controlled. */
+void sr_synth_drain(const sr_synth *s, sr_pod_drain *out);
 const char *sr_synth_string(const sr_synth *s, int32_t id);
 int32_t sr_synth_num_strings(const sr_synth *s);
 

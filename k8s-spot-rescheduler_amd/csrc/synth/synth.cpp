@@ -39,6 +39,10 @@ struct sr_synth {
   std::vector<int32_t> field_key, field_op, field_val_off{0}, field_vals;
   std::vector<int32_t> tol_off{0}, tol_key, tol_op, tol_val, tol_eff;
   std::vector<int32_t> port_off{0}, port_proto, port_num, port_ip;
+  // drain attributes (sr_pod_drain): ReplicaSet or DaemonSet controllers, running
+  std::vector<uint32_t> drain_flags;
+  std::vector<uint8_t> phase, restart;
+  std::vector<int64_t> deletion_age, grace;
   sr_node_label od{}, spot{};
 
   int32_t id(const std::string& s) {
@@ -146,6 +150,11 @@ void push_pod(sr_synth* s, int32_t node, const PodSpec& p) {
     s->port_ip.push_back(q.ip);
   }
   s->port_off.push_back(static_cast<int32_t>(s->port_proto.size()));
+  s->drain_flags.push_back((p.flags & SR_POD_DAEMONSET_CONTROLLER) ? SR_DRAIN_CTRL_DAEMONSET : SR_DRAIN_CTRL_REPLICASET);
+  s->phase.push_back(SR_PHASE_RUNNING);
+  s->restart.push_back(SR_RESTART_ALWAYS);
+  s->deletion_age.push_back(0);
+  s->grace.push_back(-1);
 }
 
 }  // namespace
@@ -370,6 +379,15 @@ void sr_synth_view(const sr_synth* s, sr_cluster* c) {
   c->id_empty = 0;
   c->id_metadata_name = 1;
   c->id_unschedulable_key = 2;
+}
+
+void sr_synth_drain(const sr_synth* s, sr_pod_drain* d) {
+  d->n = static_cast<int32_t>(s->drain_flags.size());
+  d->flags = s->drain_flags.data();
+  d->phase = s->phase.data();
+  d->restart_policy = s->restart.data();
+  d->deletion_age_ns = s->deletion_age.data();
+  d->grace_seconds = s->grace.data();
 }
 
 void sr_synth_labels(const sr_synth* s, sr_node_label* on_demand, sr_node_label* spot) {

@@ -20,18 +20,17 @@ SYNTH_LIB = os.path.join(LIB_DIR, "libsrsynth.so")
 
 
 def _parse_defines(path):
+    """Integer #defines: decimal or hex literals, optionally `(x << n)` and a `u` suffix."""
     out = {}
     with open(path) as f:
         for line in f:
-            m = re.match(r"#define\s+(SR_\w+)\s+\(?\s*(-?\d+)u?\s*(?:<<\s*(\d+))?\s*\)?", line)
+            m = re.match(r"#define\s+(SR_\w+)\s+\(?\s*(-?0x[0-9a-fA-F]+|-?\d+)u?\s*(?:<<\s*(\d+))?\s*\)?(\s|$)",
+                         line)
             if m:
-                v = int(m.group(2))
+                v = int(m.group(2), 0)
                 if m.group(3):
                     v <<= int(m.group(3))
                 out[m.group(1)] = v
-            m = re.match(r"#define\s+(SR_\w+)\s+\((0x[0-9a-fA-F]+)u\)", line)
-            if m:
-                out[m.group(1)] = int(m.group(2), 16)
     return out
 
 
@@ -78,6 +77,15 @@ class sr_node_map_params(ctypes.Structure):
 class sr_node_map(ctypes.Structure):
     _fields_ = [("spot", P32), ("n_spot", P32), ("on_demand", P32), ("n_on_demand", P32),
                 ("node_pod_off", P32), ("node_pod_idx", P32), ("requested_cpu", P64), ("free_cpu", P64)]
+
+
+class sr_pod_drain(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("flags", PU32), ("phase", PU8), ("restart_policy", PU8),
+                ("deletion_age_ns", P64), ("grace_seconds", P64)]
+
+
+class sr_drain_params(ctypes.Structure):
+    _fields_ = [("skip_nodes_with_system_pods", ctypes.c_int32), ("skip_nodes_with_local_storage", ctypes.c_int32)]
 
 
 class sr_candidates(ctypes.Structure):
@@ -176,6 +184,9 @@ def _declare_planner(lib):
     lib.sr_new_node_map.restype = S
     lib.sr_node_has_label.argtypes = [PC, ctypes.c_int32, ctypes.POINTER(sr_node_label)]
     lib.sr_node_has_label.restype = ctypes.c_int32
+    lib.sr_pods_for_deletion.argtypes = [PC, ctypes.POINTER(sr_pod_drain), ctypes.POINTER(sr_drain_params), P32,
+                                         ctypes.c_int32, P32, P32, P32, P32, P32, P32]
+    lib.sr_pods_for_deletion.restype = S
     lib.sr_snapshot_create.argtypes = [PC, P32, ctypes.c_int32, P32, P32, ctypes.POINTER(VP)]
     lib.sr_snapshot_create.restype = S
     lib.sr_snapshot_destroy.argtypes = [VP]
@@ -219,7 +230,7 @@ def _declare_planner(lib):
 
 
 # Every symbol include/sr_planner.h declares (checked by tests on CPU).
-EXPORTED = ["sr_new_node_map", "sr_node_has_label", "sr_snapshot_create", "sr_snapshot_destroy",
+EXPORTED = ["sr_new_node_map", "sr_node_has_label", "sr_pods_for_deletion", "sr_snapshot_create", "sr_snapshot_destroy",
             "sr_snapshot_add_pod", "sr_snapshot_fork", "sr_snapshot_revert", "sr_snapshot_node_state",
             "sr_snapshot_num_nodes", "sr_create", "sr_destroy", "sr_last_error", "sr_build_info",
             "sr_find_spot_nodes", "sr_can_drain_node", "sr_plan", "sr_plan_prepare", "sr_plan_run",

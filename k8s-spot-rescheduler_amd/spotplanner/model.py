@@ -105,6 +105,12 @@ class Pod:
     required_pod_affinity: bool = False
     required_pod_anti_affinity: bool = False
     hard_topology_spread: bool = False
+    # drain attributes (cluster-autoscaler utils/drain)
+    phase: str = "Running"                    # Status.Phase
+    restart_policy: str = "Always"            # Spec.RestartPolicy
+    deletion_age_s: Optional[float] = None    # now - DeletionTimestamp; None = not being deleted
+    grace_seconds: Optional[int] = None       # Spec.TerminationGracePeriodSeconds (None = nil)
+    local_storage: bool = False               # an EmptyDir or HostPath volume
 
     def cpu_sort_milli(self) -> int:
         """getPodCPURequests (nodes/nodes.go:159-165): Σ regular containers' CPU."""
@@ -184,13 +190,20 @@ class NilControllerPanic(RuntimeError):
     """rescheduler.go:244 dereferences *owner.Controller: the reference panics on nil."""
 
 
-def pod_flags(pod: Pod) -> int:
-    f = 0
+def _daemonset_owner_walk(pod: Pod):
+    """The owner loop of rescheduler.go:243-248: (controlledByDaemonSet, derefs a nil Controller)."""
     for o in pod.owner_references:
         if o.controller is None:
-            raise NilControllerPanic("nil OwnerReference.Controller on %s" % pod_id(pod))
+            return False, True
         if o.controller and o.kind == "DaemonSet":
-            f |= capi.SR_POD_DAEMONSET_CONTROLLER
+            return True, False
+    return False, False
+
+
+def pod_flags(pod: Pod) -> int:
+    f = 0
+    if _daemonset_owner_walk(pod)[0]:
+        f |= capi.SR_POD_DAEMONSET_CONTROLLER
     if MIRROR_ANNOTATION in pod.annotations:
         f |= capi.SR_POD_MIRROR
     if pod.required_pod_anti_affinity:
@@ -326,3 +339,75 @@ def label_flag(flag: str, interner: Interner) -> capi.sr_node_label:
     if len(parts) == 1:
         return capi.sr_node_label(interner.id(parts[0]), -1, 0)
     return capi.sr_node_label(interner.id(parts[0]), interner.id(parts[1]), 1)
+
+
+# ------------------------------------------------------------ drain attributes
+SAFE_TO_EVICT_ANNOTATION = "cluster-autoscaler.kubernetes.io/safe-to-evict"
+DAEMONSET_POD_ANNOTATION = "cluster-autoscaler.kubernetes.io/daemonset-pod"
+CONTROLLER_KINDS = {"ReplicationController": capi.SR_DRAIN_CTRL_REPLICATION_CONTROLLER,
+                    "DaemonSet": capi.SR_DRAIN_CTRL_DAEMONSET, "Job": capi.SR_DRAIN_CTRL_JOB,
+                    "ReplicaSet": capi.SR_DRAIN_CTRL_REPLICASET, "StatefulSet": capi.SR_DRAIN_CTRL_STATEFULSET}
+PHASES = {"Pending": capi.SR_PHASE_PENDING, "Running": capi.SR_PHASE_RUNNING, "Succeeded": capi.SR_PHASE_SUCCEEDED,
+          "Failed": capi.SR_PHASE_FAILED}
+RESTART = {"Always": capi.SR_RESTART_ALWAYS, "OnFailure": capi.SR_RESTART_ON_FAILURE, "Never": capi.SR_RESTART_NEVER}
+
+
+@dataclass
+class PodDisruptionBudget:
+    namespace: str = "kube-system"
+    match_labels: Optional[Dict[str, str]] = field(default_factory=dict)  # None = nil selector (selects nothing)
+    invalid: bool = False  # LabelSelectorAsSelector fails
+
+
+def _kube_system_pdb(pod: Pod, pdbs: List[PodDisruptionBudget]):
+    """checkKubeSystemPDBs over the kube-system PDBs in list order: (matched, error)."""
+    for pdb in pdbs:
+        if pdb.namespace != "kube-system":
+            continue
+        if pdb.invalid:
+            return False, True
+        if pdb.match_labels is not None and all(pod.labels.get(k) == v for k, v in pdb.match_labels.items()):
+            return True, False
+    return False, False
+
+
+class EncodedDrain:
+    """numpy arrays in the sr_pod_drain layout + the ctypes struct pointing at them."""
+
+    def __init__(self, pods: List[Pod], pdbs: List[PodDisruptionBudget]):
+        fl, ph, rp, age, gr = [], [], [], [], []
+        for p in pods:
+            f = 0
+            ctrl = next((o for o in p.owner_references if o.controller), None)  # metav1.GetControllerOf
+            if ctrl is not None:
+                f |= CONTROLLER_KINDS.get(ctrl.kind, capi.SR_DRAIN_CTRL_OTHER)
+            if p.annotations.get(DAEMONSET_POD_ANNOTATION) == "true":
+                f |= capi.SR_DRAIN_DAEMONSET_ANNOTATION
+            ste = p.annotations.get(SAFE_TO_EVICT_ANNOTATION)
+            if ste == "true":
+                f |= capi.SR_DRAIN_SAFE_TO_EVICT
+            elif ste == "false":
+                f |= capi.SR_DRAIN_NOT_SAFE_TO_EVICT
+            if p.deletion_age_s is not None:
+                f |= capi.SR_DRAIN_DELETING
+            if p.namespace == "kube-system":
+                f |= capi.SR_DRAIN_KUBE_SYSTEM
+                matched, err = _kube_system_pdb(p, pdbs)
+                f |= (capi.SR_DRAIN_KUBE_SYSTEM_PDB if matched else 0) | (capi.SR_DRAIN_PDB_ERROR if err else 0)
+            if p.local_storage:
+                f |= capi.SR_DRAIN_LOCAL_STORAGE
+            if _daemonset_owner_walk(p)[1]:
+                f |= capi.SR_DRAIN_NIL_CONTROLLER
+            fl.append(f)
+            ph.append(PHASES.get(p.phase, capi.SR_PHASE_UNKNOWN))
+            rp.append(RESTART.get(p.restart_policy, capi.SR_RESTART_ALWAYS))
+            age.append(0 if p.deletion_age_s is None else int(round(p.deletion_age_s * 1e9)))
+            gr.append(-1 if p.grace_seconds is None else p.grace_seconds)
+        self.a = dict(flags=_u32(fl), phase=_u8(ph), restart=_u8(rp), age=_i64(age), grace=_i64(gr))
+        self.struct = capi.sr_pod_drain(len(pods), capi.ptr(self.a["flags"], capi.PU32),
+                                        capi.ptr(self.a["phase"], capi.PU8), capi.ptr(self.a["restart"], capi.PU8),
+                                        capi.ptr(self.a["age"], capi.P64), capi.ptr(self.a["grace"], capi.P64))
+
+    @property
+    def ptr(self):
+        return ctypes.byref(self.struct)

@@ -13,8 +13,9 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from . import capi
-from .model import Pod, pod_id
+from .model import EncodedDrain, NilControllerPanic, Node, Pod, PodDisruptionBudget, encode_cluster, pod_id
 from .planner import ClusterSnapshot, FallbackRequired, PlannerError, PredicateChecker
+from .synth import pods_for_deletion
 
 podID = pod_id
 
@@ -32,6 +33,50 @@ def validateArgs(OnDemandNodeLabel: str, SpotNodeLabel: str) -> Optional[GoError
         return GoError("the spot node label is not correctly formatted: expected '<label_name>' or "
                        "'<label_name>=<label_value>', but got %s" % SpotNodeLabel)
     return None
+
+
+@dataclass
+class BlockingPod:
+    """drain.BlockingPod: the pod that stops a node from being drained and why (capi.SR_BLOCK_*)."""
+    Pod: Pod
+    Reason: int
+
+
+def _block_error(pod: Pod, reason: int) -> GoError:
+    """The error texts of drain.GetPodsForDeletionOnNodeDrain [upstream CA @03f60a4c3818]."""
+    if reason == capi.SR_BLOCK_NOT_REPLICATED:
+        return GoError("%s/%s is not replicated" % (pod.namespace, pod.name))
+    if reason == capi.SR_BLOCK_UNMOVABLE_KUBE_SYSTEM:
+        return GoError("non-daemonset, non-mirrored, non-pdb-assigned kube-system pod present: %s" % pod.name)
+    if reason == capi.SR_BLOCK_LOCAL_STORAGE:
+        return GoError("pod with local storage present: %s" % pod.name)
+    if reason == capi.SR_BLOCK_NOT_SAFE_TO_EVICT:
+        return GoError("pod annotated as not safe to evict present: %s" % pod.name)
+    return GoError("error matching pods to pdbs")
+
+
+def podsForDeletion(podList: Sequence[Pod], pdbs: Sequence[PodDisruptionBudget], deleteNonReplicatedPods: bool = False):
+    """The pods run() moves off one on-demand node (rescheduler.go:231-256):
+    GetPodsForDeletionOnNodeDrain(nodeInfo.Pods, pdbs, *deleteNonReplicatedPods,
+    false, false, nil, 0, now), then the DaemonSet-owner filter.  Returns
+    (podsForDeletion, blockingPod, err); evaluated by the planner library
+    (sr_pods_for_deletion).  A nil OwnerReference.Controller reached by the
+    filter raises NilControllerPanic, as the reference panics."""
+    pods = list(podList)
+    enc = encode_cluster([Node("node", 0)], pods, pod_node=[0] * len(pods))
+    drain = EncodedDrain(pods, list(pdbs))
+    lib = capi.load_planner()
+    off, idx, bp, br, st = pods_for_deletion(lib.sr_pods_for_deletion, enc.ptr, drain.ptr, np.zeros(1, np.int32),
+                                             np.array([0, len(pods)], np.int32), np.arange(len(pods), dtype=np.int32),
+                                             deleteNonReplicatedPods)
+    if st == capi.SR_ERR_NIL_CONTROLLER:
+        raise NilControllerPanic("nil OwnerReference.Controller (rescheduler.go:244)")
+    if st != capi.SR_OK:
+        raise PlannerError("sr_pods_for_deletion: status %d" % st)
+    if bp[0] >= 0:
+        blocking = pods[int(bp[0])]
+        return [], BlockingPod(blocking, int(br[0])), _block_error(blocking, int(br[0]))
+    return [pods[int(i)] for i in idx], None, None
 
 
 def _node_names(nodes) -> List[str]:

@@ -33,6 +33,7 @@ def load_synth():
         lib.sr_synth_view.argtypes = [ctypes.c_void_p, ctypes.POINTER(capi.sr_cluster)]
         lib.sr_synth_labels.argtypes = [ctypes.c_void_p, ctypes.POINTER(capi.sr_node_label),
                                         ctypes.POINTER(capi.sr_node_label)]
+        lib.sr_synth_drain.argtypes = [ctypes.c_void_p, ctypes.POINTER(capi.sr_pod_drain)]
         lib.sr_synth_string.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         lib.sr_synth_string.restype = ctypes.c_char_p
         lib.sr_synth_num_strings.argtypes = [ctypes.c_void_p]
@@ -52,6 +53,8 @@ class SynthCluster:
         self.od_label = capi.sr_node_label()
         self.spot_label = capi.sr_node_label()
         self.lib.sr_synth_labels(self.handle, ctypes.byref(self.od_label), ctypes.byref(self.spot_label))
+        self.drain = capi.sr_pod_drain()
+        self.lib.sr_synth_drain(self.handle, ctypes.byref(self.drain))
         self.config = config
 
     @property
@@ -117,6 +120,26 @@ def new_node_map(fn, cluster_ptr, n_nodes: int, n_pods: int, od_label, spot_labe
     if st != capi.SR_OK:
         raise RuntimeError("new_node_map status %d" % st)
     return NodeMapArrays(spot[: ns[0]].copy(), od[: nod[0]].copy(), off, idx[: int(off[-1])].copy(), req, free)
+
+
+def pods_for_deletion(fn, cluster_ptr, drain_ptr, nodes: np.ndarray, node_pod_off: np.ndarray,
+                      node_pod_idx: np.ndarray, delete_non_replicated: bool = False):
+    """sr_pods_for_deletion-shaped `fn` (the product's, or the oracle's in tests)
+    over `nodes`: (cand_off, cand_pods, block_pod, block_reason, status)."""
+    nodes = np.ascontiguousarray(nodes, np.int32)
+    n = len(nodes)
+    off = np.zeros(n + 1, np.int32)
+    npo = np.asarray(node_pod_off)
+    total = int(np.sum(npo[nodes + 1] - npo[nodes])) if n else 0
+    pods = np.zeros(max(1, total), np.int32)
+    bp = np.full(max(1, n), -1, np.int32)
+    br = np.zeros(max(1, n), np.int32)
+    prm = capi.sr_drain_params(1 if delete_non_replicated else 0, 0)  # rescheduler.go:231 arguments 3, 4
+    st = fn(cluster_ptr, drain_ptr, ctypes.byref(prm), capi.ptr(nodes, capi.P32), n,
+            capi.ptr(np.ascontiguousarray(node_pod_off, np.int32), capi.P32),
+            capi.ptr(np.ascontiguousarray(node_pod_idx, np.int32), capi.P32), capi.ptr(off, capi.P32),
+            capi.ptr(pods, capi.P32), capi.ptr(bp, capi.P32), capi.ptr(br, capi.P32))
+    return off, pods[: int(off[-1])].copy(), bp[:n], br[:n], st
 
 
 def build_candidates(nm: NodeMapArrays, flags: np.ndarray):

@@ -279,6 +279,113 @@ void oracle_build_candidates(const sr_cluster *c, const sr_node_map *m, int32_t 
 }
 
 /* ===================================================================== */
+/* GetPodsForDeletionOnNodeDrain [upstream CA utils/drain/drain.go @03f60a4c3818]
+ * as called at rescheduler.go:231 (checkReferences = false, no listers,
+ * minReplica 0), and the loop of rescheduler.go:240-256. */
+
+/* pod_util.IsDaemonSetPod: a DaemonSet ControllerRef, or the annotation */
+static int o_is_daemonset_pod(uint32_t f) {
+  return (f & SR_DRAIN_CTRL_MASK) == SR_DRAIN_CTRL_DAEMONSET || (f & SR_DRAIN_DAEMONSET_ANNOTATION) != 0;
+}
+
+/* drain.IsPodLongTerminating: deletionTimestamp + grace (default 30 s) + 30 s before now */
+static int o_long_terminating(const sr_pod_drain *d, int32_t pod) {
+  if (!(d->flags[pod] & SR_DRAIN_DELETING)) return 0;
+  long double grace = d->grace_seconds[pod] < 0 ? 30.0L : (long double)d->grace_seconds[pod];
+  return (long double)d->deletion_age_ns[pod] > (grace + 30.0L) * 1e9L;
+}
+
+/* drain.isPodTerminal */
+static int o_terminal(const sr_pod_drain *d, int32_t pod) {
+  int ph = d->phase[pod], rp = d->restart_policy[pod];
+  if (rp == SR_RESTART_NEVER && (ph == SR_PHASE_SUCCEEDED || ph == SR_PHASE_FAILED)) return 1;
+  if (rp == SR_RESTART_ON_FAILURE && ph == SR_PHASE_SUCCEEDED) return 1;
+  return ph == SR_PHASE_FAILED;
+}
+
+/* GetPodsForDeletionOnNodeDrain over one node's pods: returns the blocking pod
+ * (its reason in *reason) or -1 with the pods appended to out[*n]. */
+static int32_t o_get_pods_for_deletion(const sr_cluster *c, const sr_pod_drain *d, const sr_drain_params *prm,
+                                       const int32_t *pods, int32_t np, int32_t *out, int32_t *n, int32_t *reason) {
+  *n = 0;
+  *reason = SR_BLOCK_NONE;
+  for (int32_t i = 0; i < np; i++) {
+    int32_t pod = pods[i];
+    uint32_t f = d->flags[pod];
+    if (c->pods.flags[pod] & SR_POD_MIRROR) continue;
+    if (o_long_terminating(d, pod)) continue;
+    int replicated = 0, is_ds = 0;
+    uint32_t kind = f & SR_DRAIN_CTRL_MASK;
+    if (kind == SR_DRAIN_CTRL_REPLICATION_CONTROLLER) {
+      replicated = 1;
+    } else if (o_is_daemonset_pod(f)) {
+      is_ds = 1;
+    } else if (kind == SR_DRAIN_CTRL_JOB) {
+      replicated = 1;
+    } else if (kind == SR_DRAIN_CTRL_REPLICASET) {
+      replicated = 1;
+    } else if (kind == SR_DRAIN_CTRL_STATEFULSET) {
+      replicated = 1;
+    }
+    if (is_ds) continue;
+    if (!(f & SR_DRAIN_SAFE_TO_EVICT) && !o_terminal(d, pod)) {
+      if (!replicated) {
+        *reason = SR_BLOCK_NOT_REPLICATED;
+        return pod;
+      }
+      if ((f & SR_DRAIN_KUBE_SYSTEM) && prm->skip_nodes_with_system_pods) {
+        if (f & SR_DRAIN_PDB_ERROR) {
+          *reason = SR_BLOCK_UNEXPECTED_ERROR;
+          return pod;
+        }
+        if (!(f & SR_DRAIN_KUBE_SYSTEM_PDB)) {
+          *reason = SR_BLOCK_UNMOVABLE_KUBE_SYSTEM;
+          return pod;
+        }
+      }
+      if ((f & SR_DRAIN_LOCAL_STORAGE) && prm->skip_nodes_with_local_storage) {
+        *reason = SR_BLOCK_LOCAL_STORAGE;
+        return pod;
+      }
+      if (f & SR_DRAIN_NOT_SAFE_TO_EVICT) {
+        *reason = SR_BLOCK_NOT_SAFE_TO_EVICT;
+        return pod;
+      }
+    }
+    out[(*n)++] = pod;
+  }
+  return -1;
+}
+
+int32_t oracle_pods_for_deletion(const sr_cluster *c, const sr_pod_drain *d, const sr_drain_params *prm,
+                                 const int32_t *nodes, int32_t n_nodes, const int32_t *node_pod_off,
+                                 const int32_t *node_pod_idx, int32_t *cand_off, int32_t *cand_pods,
+                                 int32_t *block_pod, int32_t *block_reason) {
+  if (d->n != c->pods.n) return SR_ERR_INVALID_ARG;
+  int32_t k = 0;
+  int32_t *tmp = (int32_t *)malloc(sizeof(int32_t) * (size_t)(c->pods.n > 0 ? c->pods.n : 1));
+  for (int32_t i = 0; i < n_nodes; i++) {
+    int32_t node = nodes[i], n = 0;
+    cand_off[i] = k;
+    block_pod[i] = o_get_pods_for_deletion(c, d, prm, node_pod_idx + node_pod_off[node],
+                                           node_pod_off[node + 1] - node_pod_off[node], tmp, &n, &block_reason[i]);
+    if (block_pod[i] >= 0) continue; /* glog + continue (rescheduler.go:232-238) */
+    for (int32_t q = 0; q < n; q++) {
+      int32_t pod = tmp[q];
+      if (d->flags[pod] & SR_DRAIN_NIL_CONTROLLER) { /* *owner.Controller with Controller == nil */
+        free(tmp);
+        return SR_ERR_NIL_CONTROLLER;
+      }
+      if (c->pods.flags[pod] & SR_POD_DAEMONSET_CONTROLLER) continue; /* controlledByDaemonSet */
+      cand_pods[k++] = pod;
+    }
+  }
+  cand_off[n_nodes] = k;
+  free(tmp);
+  return SR_OK;
+}
+
+/* ===================================================================== */
 /* Cluster snapshot [upstream CA simulator BasicClusterSnapshot/DeltaClusterSnapshot
  * over scheduler NodeInfo]: per node Requested (cpu, mem, eph), len(Pods),
  * UsedPorts, and whether any pod carries required anti-affinity. */

@@ -58,6 +58,16 @@ int32_t oracle_new_node_map(const sr_cluster *c, const sr_node_map_params *p, sr
 void oracle_build_candidates(const sr_cluster *c, const sr_node_map *m, int32_t *cand_off,
                              int32_t *cand_pods);
 
+/* Candidate lists of run() (rescheduler.go:228-264) with the CA drain rules:
+ * GetPodsForDeletionOnNodeDrain (cluster-autoscaler utils/drain @03f60a4c3818,
+ * un-vendored: restated, parity unpinned) then the DaemonSet-owner filter.
+ * Same contract as sr_pods_for_deletion; returns SR_OK, SR_ERR_NIL_CONTROLLER
+ * or SR_ERR_INVALID_ARG. */
+int32_t oracle_pods_for_deletion(const sr_cluster *c, const sr_pod_drain *d, const sr_drain_params *prm,
+                                 const int32_t *nodes, int32_t n_nodes, const int32_t *node_pod_off,
+                                 const int32_t *node_pod_idx, int32_t *cand_off, int32_t *cand_pods,
+                                 int32_t *block_pod, int32_t *block_reason);
+
 typedef struct oracle_snapshot oracle_snapshot;
 oracle_snapshot *oracle_snapshot_create(const sr_cluster *c, const int32_t *spot, int32_t n_spot,
                                         const int32_t *node_pod_off, const int32_t *node_pod_idx);

@@ -38,6 +38,9 @@ def load_oracle():
     lib.oracle_validate_label_flag.restype = ctypes.c_int32
     lib.oracle_new_node_map.argtypes = [PC, ctypes.POINTER(capi.sr_node_map_params), ctypes.POINTER(capi.sr_node_map)]
     lib.oracle_new_node_map.restype = ctypes.c_int32
+    lib.oracle_pods_for_deletion.argtypes = [PC, ctypes.POINTER(capi.sr_pod_drain), ctypes.POINTER(capi.sr_drain_params),
+                                             P32, ctypes.c_int32, P32, P32, P32, P32, P32, P32]
+    lib.oracle_pods_for_deletion.restype = ctypes.c_int32
     lib.oracle_snapshot_create.argtypes = [PC, P32, ctypes.c_int32, P32, P32]
     lib.oracle_snapshot_create.restype = VP
     lib.oracle_snapshot_destroy.argtypes = [VP]
