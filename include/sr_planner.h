@@ -226,8 +226,10 @@ typedef struct {
 } sr_pod_drain;
 
 typedef struct {
-  int32_t skip_nodes_with_system_pods;   /* argument 3 at rescheduler.go:231: *deleteNonReplicatedPods */
-  int32_t skip_nodes_with_local_storage; /* argument 4 at rescheduler.go:231: false */
+  int32_t skip_nodes_with_system_pods;   /* argument 3 at rescheduler.go:231 / :391: *deleteNonReplicatedPods */
+  int32_t skip_nodes_with_local_storage; /* argument 4 at rescheduler.go:231 / :391: false */
+  int32_t owner_filter;                  /* 1: then the DaemonSet-owner filter of run() (:240-256);
+                                            0: GetPodsForDeletionOnNodeDrain alone, as updateSpotNodeMetrics (:388-399) */
 } sr_drain_params;
 
 /* drain.BlockingPodReason */
@@ -241,7 +243,9 @@ typedef struct {
 /* The candidate lists of run() (rescheduler.go:228-264): for each node of
  * `nodes` (on-demand NodeInfoArray order), GetPodsForDeletionOnNodeDrain over
  * NodeInfo.Pods (node_pod_off / node_pod_idx, sr_node_map layout) with the
- * reference's arguments, then the DaemonSet-owner filter (:240-256).
+ * reference's arguments, then (owner_filter) the DaemonSet-owner filter
+ * (:240-256).  With owner_filter = 0 over the spot nodes, the list lengths are
+ * updateSpotNodeMetrics' pod counts (:388-399; blocked nodes are skipped).
  * out_cand_off [n_nodes + 1], out_cand_pods [<= all pods of the nodes]: the
  * podsForDeletion of each node, in order.  A node with a blocking pod gets an
  * empty list, its pod in out_block_pod (else -1) and the reason in

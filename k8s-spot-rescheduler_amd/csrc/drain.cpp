@@ -88,7 +88,7 @@ extern "C" sr_status sr_pods_for_deletion(const sr_cluster* c, const sr_pod_drai
       }
       out_cand_pods[k++] = pod;
     }
-    if (out_block_pod[i] >= 0) continue;
+    if (out_block_pod[i] >= 0 || !prm->owner_filter) continue;
     // rescheduler.go:240-256: drop DaemonSet-controlled pods; *owner.Controller
     // is dereferenced for every owner reference it reaches
     int32_t kept = k0;

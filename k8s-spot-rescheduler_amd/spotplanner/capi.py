@@ -85,7 +85,8 @@ class sr_pod_drain(ctypes.Structure):
 
 
 class sr_drain_params(ctypes.Structure):
-    _fields_ = [("skip_nodes_with_system_pods", ctypes.c_int32), ("skip_nodes_with_local_storage", ctypes.c_int32)]
+    _fields_ = [("skip_nodes_with_system_pods", ctypes.c_int32), ("skip_nodes_with_local_storage", ctypes.c_int32),
+                ("owner_filter", ctypes.c_int32)]
 
 
 class sr_candidates(ctypes.Structure):

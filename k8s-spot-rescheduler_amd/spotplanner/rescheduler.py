@@ -79,6 +79,30 @@ def podsForDeletion(podList: Sequence[Pod], pdbs: Sequence[PodDisruptionBudget],
     return [pods[int(i)] for i in idx], None, None
 
 
+def updateSpotNodeMetrics(spotNodeInfos, pdbs: Sequence[PodDisruptionBudget], deleteNonReplicatedPods: bool = False):
+    """updateSpotNodeMetrics (rescheduler.go:388-399): per spot node, the number of
+    pods GetPodsForDeletionOnNodeDrain returns (the pods the rescheduler
+    understands), {node name: count}; nodes whose call errors are skipped, as the
+    reference logs and continues.  The Prometheus gauge itself stays in the Go
+    shim (metrics.UpdateNodePodsCount(SpotNodeLabel, name, count))."""
+    infos = list(spotNodeInfos)
+    pods, pod_node = [], []
+    for i, ni in enumerate(infos):
+        pods.extend(ni.Pods)
+        pod_node.extend([i] * len(ni.Pods))
+    enc = encode_cluster([ni.Node for ni in infos], pods, pod_node=pod_node)
+    drain = EncodedDrain(pods, list(pdbs))
+    off = np.zeros(len(infos) + 1, np.int32)
+    off[1:] = np.cumsum([len(ni.Pods) for ni in infos])
+    out_off, _, bp, _, st = pods_for_deletion(capi.load_planner().sr_pods_for_deletion, enc.ptr, drain.ptr,
+                                              np.arange(len(infos), dtype=np.int32), off,
+                                              np.arange(len(pods), dtype=np.int32), deleteNonReplicatedPods,
+                                              owner_filter=False)
+    if st != capi.SR_OK:
+        raise PlannerError("sr_pods_for_deletion: status %d" % st)
+    return {ni.Node.name: int(out_off[i + 1] - out_off[i]) for i, ni in enumerate(infos) if bp[i] < 0}
+
+
 def _node_names(nodes) -> List[str]:
     return [ni.Node.name for ni in nodes]
 

@@ -123,7 +123,7 @@ def new_node_map(fn, cluster_ptr, n_nodes: int, n_pods: int, od_label, spot_labe
 
 
 def pods_for_deletion(fn, cluster_ptr, drain_ptr, nodes: np.ndarray, node_pod_off: np.ndarray,
-                      node_pod_idx: np.ndarray, delete_non_replicated: bool = False):
+                      node_pod_idx: np.ndarray, delete_non_replicated: bool = False, owner_filter: bool = True):
     """sr_pods_for_deletion-shaped `fn` (the product's, or the oracle's in tests)
     over `nodes`: (cand_off, cand_pods, block_pod, block_reason, status)."""
     nodes = np.ascontiguousarray(nodes, np.int32)
@@ -134,7 +134,8 @@ def pods_for_deletion(fn, cluster_ptr, drain_ptr, nodes: np.ndarray, node_pod_of
     pods = np.zeros(max(1, total), np.int32)
     bp = np.full(max(1, n), -1, np.int32)
     br = np.zeros(max(1, n), np.int32)
-    prm = capi.sr_drain_params(1 if delete_non_replicated else 0, 0)  # rescheduler.go:231 arguments 3, 4
+    prm = capi.sr_drain_params(1 if delete_non_replicated else 0, 0,  # rescheduler.go:231 arguments 3, 4
+                               1 if owner_filter else 0)
     st = fn(cluster_ptr, drain_ptr, ctypes.byref(prm), capi.ptr(nodes, capi.P32), n,
             capi.ptr(np.ascontiguousarray(node_pod_off, np.int32), capi.P32),
             capi.ptr(np.ascontiguousarray(node_pod_idx, np.int32), capi.P32), capi.ptr(off, capi.P32),

@@ -370,6 +370,10 @@ int32_t oracle_pods_for_deletion(const sr_cluster *c, const sr_pod_drain *d, con
     block_pod[i] = o_get_pods_for_deletion(c, d, prm, node_pod_idx + node_pod_off[node],
                                            node_pod_off[node + 1] - node_pod_off[node], tmp, &n, &block_reason[i]);
     if (block_pod[i] >= 0) continue; /* glog + continue (rescheduler.go:232-238) */
+    if (!prm->owner_filter) { /* updateSpotNodeMetrics counts the CA's list as is (rescheduler.go:391-396) */
+      for (int32_t q = 0; q < n; q++) cand_pods[k++] = tmp[q];
+      continue;
+    }
     for (int32_t q = 0; q < n; q++) {
       int32_t pod = tmp[q];
       if (d->flags[pod] & SR_DRAIN_NIL_CONTROLLER) { /* *owner.Controller with Controller == nil */

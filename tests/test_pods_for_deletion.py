@@ -18,7 +18,7 @@ from oracle_lib import load_oracle
 from spotplanner import capi
 from spotplanner.model import (Container, EncodedDrain, NilControllerPanic, Node, OwnerReference, Pod,
                                PodDisruptionBudget, encode_cluster)
-from spotplanner.rescheduler import podsForDeletion
+from spotplanner.rescheduler import podsForDeletion, updateSpotNodeMetrics
 from spotplanner.synth import SynthCluster, build_candidates, new_node_map, pods_for_deletion
 
 B = capi
@@ -193,9 +193,11 @@ def test_product_matches_oracle_on_random_pods(seed):
     off = np.cumsum(off).astype(np.int32)
     idx = np.argsort(np.asarray(pod_node, np.int32), kind="stable").astype(np.int32)
     order = np.array(r.sample(range(n_nodes), n_nodes), np.int32)
-    for dnr in (False, True):
-        got = pods_for_deletion(capi.load_planner().sr_pods_for_deletion, enc.ptr, drain.ptr, order, off, idx, dnr)
-        want = pods_for_deletion(load_oracle().oracle_pods_for_deletion, enc.ptr, drain.ptr, order, off, idx, dnr)
+    for dnr, owner_filter in ((False, True), (True, True), (False, False), (True, False)):
+        got = pods_for_deletion(capi.load_planner().sr_pods_for_deletion, enc.ptr, drain.ptr, order, off, idx, dnr,
+                                owner_filter)
+        want = pods_for_deletion(load_oracle().oracle_pods_for_deletion, enc.ptr, drain.ptr, order, off, idx, dnr,
+                                 owner_filter)
         assert got[4] == want[4]
         if got[4] == capi.SR_OK:
             for a, b in zip(got[:4], want[:4]):
@@ -218,3 +220,16 @@ def test_synthetic_candidates(config):
     assert np.array_equal(got[0], off) and np.array_equal(got[1], pods)
     assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
     assert np.all(got[2] == -1)
+
+
+def test_update_spot_node_metrics_counts():
+    # rescheduler.go:388-399: counts of GetPodsForDeletionOnNodeDrain per spot
+    # node; no DaemonSet-owner filter and no panic on nil controllers there;
+    # a node whose call errors is skipped
+    from spotplanner.nodes import NodeInfo
+    n1 = NodeInfo(Node("s1", 4000), [mk("a"), mk("ds", owner_references=[OwnerReference("DaemonSet")]),
+                                     mk("q", owner_references=[OwnerReference("ReplicaSet"),
+                                                               OwnerReference("Foo", controller=None)])], 0, 0)
+    n2 = NodeInfo(Node("s2", 4000), [mk("b"), mk("lonely", owner_references=[])], 0, 0)
+    n3 = NodeInfo(Node("s3", 4000), [], 0, 0)
+    assert updateSpotNodeMetrics([n1, n2, n3], []) == {"s1": 2, "s3": 0}
