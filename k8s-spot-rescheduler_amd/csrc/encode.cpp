@@ -31,7 +31,7 @@
 
 namespace sr {
 
-double encode_phase_ms[9];  // host-side profile of the last encode (tools/encode_stats)
+double encode_phase_ms[16];  // host-side profile of the last encode (tools/encode_stats)
 
 namespace {
 
@@ -242,7 +242,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     t_last = now;
   };
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
-  *w = Workload();
+  w->reset();
   w->n_input_cand = nc;
   w->n_input_pods = nc > 0 ? cands->cand_pod_off[nc] : 0;
   if (!snap->nodes.empty() &&
@@ -278,27 +278,30 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     return false;
   };
   for (int32_t i = 0; i < nc; ++i) {
-    const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
-    if (e < b) {
+    if (cands->cand_pod_off[i + 1] < cands->cand_pod_off[i]) {
       *err = "cand_pod_off not monotone";
       return SR_ERR_INVALID_ARG;
     }
-    if (e == b) {
-      w->status_host[i] = SR_CAND_EMPTY;
-      continue;
-    }
-    bool fb = snap->anti_total > 0 || (e - b) > MAX_CAND_PODS;
-    for (int32_t j = b; j < e && !fb; ++j) {
-      const int32_t pod = cands->cand_pods[j];
-      if (pod < 0 || pod >= P.n) {
+    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j)
+      if (cands->cand_pods[j] < 0 || cands->cand_pods[j] >= P.n) {
         *err = "candidate pod index out of range";
         return SR_ERR_INVALID_ARG;
       }
-      fb = pod_fallback(pod);
-    }
-    if (fb) w->status_host[i] = SR_CAND_FALLBACK;
   }
+  parallel_for(static_cast<size_t>(nc), 64, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
+      if (e == b) {
+        w->status_host[i] = SR_CAND_EMPTY;
+        continue;
+      }
+      bool fb = snap->anti_total > 0 || (e - b) > MAX_CAND_PODS;
+      for (int32_t j = b; j < e && !fb; ++j) fb = pod_fallback(cands->cand_pods[j]);
+      if (fb) w->status_host[i] = SR_CAND_FALLBACK;
+    }
+  });
 
+  phase(8);
   // ---- host-port dictionary: (protocol, port) pairs of active pods, <= 64
   std::unordered_map<int64_t, int32_t> port_dict;
   auto port_key = [](int32_t proto, int32_t port) { return (static_cast<int64_t>(proto) << 32) | uint32_t(port); };
@@ -598,6 +601,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       row[i] = w->atoms[i] & ~any;
     }
   }
+  phase(9);
   // requirement atoms: one label-value column per distinct key
   std::unordered_map<int32_t, std::vector<int32_t>> col;  // key -> value per node (INT32_MIN absent)
   for (const Requirement& r : reqs)
@@ -607,9 +611,10 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       auto it = col.find(kv.first);
       if (it != col.end()) it->second[n] = kv.second;
     }
-  for (int32_t ri = 0; ri < n_reqs; ++ri) {
+  parallel_for(static_cast<size_t>(n_reqs), 1, [&](size_t rlo, size_t rhi) {
+  for (size_t ri = rlo; ri < rhi; ++ri) {  // one atom row per requirement: disjoint writes
     const Requirement& r = reqs[ri];
-    const int32_t atom = A_REQ + ri;
+    const int32_t atom = A_REQ + static_cast<int32_t>(ri);
     if (r.type == REQ_FIELD) {
       // fields.Set{"metadata.name": node.Name}; any other key reads as "".
       const bool is_name = r.key == c->id_metadata_name && c->id_metadata_name != -1;
@@ -620,7 +625,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       }
       continue;
     }
-    const std::vector<int32_t>& v = col[r.key];
+    const std::vector<int32_t>& v = col.at(r.key);
     for (int32_t n = 0; n < n_spot; ++n) {
       const bool has = v[n] != INT32_MIN;
       bool m;
@@ -641,6 +646,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       if (m) set_atom(atom, n);
     }
   }
+  });
 
   phase(4);
   // ---- T row descriptors.  A pod asking r in one dimension uses the row of the
@@ -686,6 +692,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       rec[3] = pstat[pod_spec[q]].ports;
     }
   });
+  phase(10);
   // Pods whose F row is certainly empty point at one all-zero class (atom 0
   // AND NOT atom 0), so K2 knows them without reading their rows: a class
   // that ANDs an empty atom, ANDs the complement of a full one, or whose
@@ -738,6 +745,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       for (int32_t q : dead_pods) w->pod_rows[static_cast<size_t>(q) * 4] = w->empty_class;
     }
   }
+  phase(11);
   // positions -> T rows: row 0 = every node, then the used positions of each
   // dimension in increasing threshold order (rows grouped by dimension, so
   // K0 compares one dimension per wave)
@@ -759,6 +767,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     }
     w->t_off[d + 2] = static_cast<int32_t>(w->t_dim.size());
   }
+  phase(12);
   // Node ranks: the dimension-d rows are in threshold order, so the rows a
   // node belongs to (threshold <= its free value) are a prefix of them; K0
   // sets bit n of the dimension's row r exactly when r < rank(n).
@@ -770,6 +779,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     int32_t* rk = &w->node_rank[static_cast<size_t>(d) * NP];
     for (int32_t n = 0; n < n_spot; ++n) rk[n] = below[lb[d](fr[n]) + 1];  // fr[n] is node_vals[d][pos]
   }
+  phase(13);
   for (int32_t q = 0; q < na; ++q) {
     int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
     for (int d = 0; d < 3; ++d) r[1 + d] = r[1 + d] < 0 ? 0 : t_index[d][static_cast<size_t>(r[1 + d])];

@@ -118,6 +118,23 @@ struct Workload {
   uint64_t fallback_pods = 0;
   int32_t n_input_cand = 0;
   int32_t n_input_pods = 0;
+
+  // Back to the default state, keeping every buffer's capacity: a planner
+  // encodes one tick after another, and fresh multi-MB buffers page-fault.
+  void reset() {
+    for (auto* v : {&free_cpu, &free_mem, &free_eph, &t_thr}) v->clear();
+    for (auto* v : {&pods_left, &cls_prog_off, &cls_prog, &cls_prog8, &t_dim, &node_rank, &pod_rows, &pod_src,
+                    &cand_off, &cand_global, &cand_src, &list, &status_host})
+      v->clear();
+    for (auto* v : {&port_bits, &node_rec, &atoms, &pod_rec}) v->clear();
+    n_spot = n_pad = Wp = n_atoms = n_classes = 0;
+    empty_class = -1;
+    for (int32_t& t : t_off) t = 0;
+    max_cand_pods = 0;
+    first_fallback = -1;
+    fallback_pods = 0;
+    n_input_cand = n_input_pods = 0;
+  }
 };
 
 constexpr int32_t STATUS_PENDING = -100;

@@ -9,7 +9,7 @@
 #include "../k8s-spot-rescheduler_amd/csrc/host.hpp"
 #include "../k8s-spot-rescheduler_amd/csrc/synth/sr_synth.h"
 
-namespace sr { extern double encode_phase_ms[9]; }
+namespace sr { extern double encode_phase_ms[16]; }
 
 int main(int argc, char** argv) {
   sr_synth_params p{};
@@ -52,6 +52,9 @@ int main(int argc, char** argv) {
   printf("phases(ms): dims %.2f fallback+ports+taints %.2f pod-static %.2f classes %.2f nodes+atoms %.2f t-rows+pods %.2f lists %.2f (pod-static: keys %.2f; t-setup %.2f)\n",
          sr::encode_phase_ms[0], sr::encode_phase_ms[1], sr::encode_phase_ms[2], sr::encode_phase_ms[3],
          sr::encode_phase_ms[4], sr::encode_phase_ms[5], sr::encode_phase_ms[6], sr::encode_phase_ms[7], sr::encode_phase_ms[8]);
+  printf("fine(ms): pass1 %.2f ports+taints %.2f | atoms-nodes %.2f atoms-reqs %.2f | lb+recs %.2f empty %.2f trows %.2f ranks %.2f recoffs %.2f\n",
+         sr::encode_phase_ms[8], sr::encode_phase_ms[1], sr::encode_phase_ms[9], sr::encode_phase_ms[4],
+         sr::encode_phase_ms[10], sr::encode_phase_ms[11], sr::encode_phase_ms[12], sr::encode_phase_ms[13], sr::encode_phase_ms[5]);
   printf("Wp %d atoms %d classes %d program ops %zu t_rows %zu\n", w.Wp, w.n_atoms, w.n_classes, w.cls_prog.size(),
          w.t_dim.size());
   int tc[4] = {0, 0, 0, 0};
