@@ -255,32 +255,32 @@ typedef __attribute__((address_space(1))) void* gbl_vp;
 
 // Winner: d_min[0] = packed first drainable candidate (possibly reduced over
 // ranks), d_min[1] = packed first fallback; the winner's mapping is copied
-// only by the rank that owns it.  `result` lives in mapped host memory: the
-// data first, then (after a system-scope fence) the run's sequence number,
-// which the host polls.
+// only by the rank that owns it.  `result` lives in mapped host memory, one
+// 64-bit word per value tagged with the run's sequence number.
 __device__ __forceinline__ void write_winner(const DevWorkload& w) {
   const int lane = threadIdx.x & 63;
   const unsigned long long* dm = reinterpret_cast<const unsigned long long*>(w.d_min);
   const unsigned long long ok = __hip_atomic_load(dm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long fb = __hip_atomic_load(dm + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  int* r = w.result;
+  uint64_t* r = w.result;
   const bool any = ok != ~0ull;
   const int g = any ? static_cast<int>(ok >> 32) : -1;
   const int li = any ? static_cast<int>(ok & 0xffffffffu) : -1;
   const bool local = any && li < w.n_cand && w.cand_global[li] == g;
   const int off = local ? w.cand_off[li] : 0;
   const int np = local ? w.cand_off[li + 1] - off : 0;
-  auto put = [&](int i, int v) { __hip_atomic_store(r + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+  // every word carries the run's sequence number in its upper half: the host
+  // accepts each word on its own tag, so no store has to wait for another
+  const uint64_t tag = static_cast<uint64_t>(static_cast<uint32_t>(w.seq)) << 32;
+  auto put = [&](int i, int v) {
+    __hip_atomic_store(r + i, tag | static_cast<uint32_t>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  };
   for (int q = lane; q < np; q += 64)
     put(kResultHeader + q, __hip_atomic_load(w.out_node + off + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  if (lane == 0) {
-    put(0, g);
-    put(1, local ? 1 : 0);
-    put(2, np);
-    put(3, fb == ~0ull ? -1 : static_cast<int>(fb >> 32));
-  }
-  SR_WAIT_VM(0);  // the data is acknowledged before the sequence number goes out
-  if (lane == 0) put(4, w.seq);
+  if (lane == 0) put(0, g);
+  if (lane == 1) put(1, local ? 1 : 0);
+  if (lane == 2) put(2, np);
+  if (lane == 3) put(3, fb == ~0ull ? -1 : static_cast<int>(fb >> 32));
 }
 
 // K3: one wave (after the collective on multi-GPU runs).

@@ -9,8 +9,8 @@
 
 namespace sr {
 
-constexpr int kResultHeader = 8;
-constexpr size_t kK0ProfWaves = 32768;  // K0 waves profiled after K2's [n_cand][16] records  // int32 words before the winner's mapping in `result`
+constexpr int kResultHeader = 8;           // words before the winner's mapping in `result`
+constexpr size_t kK0ProfWaves = 32768;  // K0 waves profiled after K2's [n_cand][16] records
 
 // Pointers into the device arena (layout: DESIGN.md §HBM layout).
 struct DevWorkload {
@@ -42,9 +42,9 @@ struct DevWorkload {
   int32_t* out_node;   // [n_pods] spot position or -1
   int32_t* out_status; // [n_cand]
   int32_t* d_min;      // 2 x u64 packed {global << 32 | local}: first ok, first fallback (~0 = none)
-  int32_t* result;     // mapped host memory [kResultHeader + max pods]
-                       //   {winner, local, npods, first_fallback, seq, mapping...}
-  int32_t seq;         // run sequence number written last into result[4]
+  uint64_t* result;    // mapped host memory [kResultHeader + max pods] words seq << 32 | value:
+                       //   {winner, local, npods, first_fallback, -, -, -, -, mapping...}
+  int32_t seq;         // run sequence number: the tag of every result word
   int32_t k2_mode;     // 0: node-order first fit where it applies (<= 64 pods, <= 64-word rows);
                        // 1: pod order everywhere (SR_K2_MODE=1, A/B measurement)
   uint64_t* prof;      // optional [n_cand][16] K2 + [kK0ProfWaves][2] K0 per-wave profile

@@ -162,7 +162,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, dev_reserve(ctx->out_node, sizeof(int32_t) * std::max(1, na)));
   HIP_TRY(ctx, dev_reserve(ctx->out_status, sizeof(int32_t) * std::max(1, ncand)));
   HIP_TRY(ctx, dev_reserve(ctx->dmin, 64));
-  const size_t res_bytes = sizeof(int32_t) * (sr::kResultHeader + static_cast<size_t>(std::max(1, w.max_cand_pods)));
+  const size_t res_bytes = sizeof(uint64_t) * (sr::kResultHeader + static_cast<size_t>(std::max(1, w.max_cand_pods)));
   HIP_TRY(ctx, host_reserve(ctx->h_result, res_bytes));  // mapped: K3 writes the result straight to the host
   auto t1 = std::chrono::steady_clock::now();
   pk.copy_to(static_cast<char*>(ctx->h_arena.p));
@@ -211,7 +211,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   }
   void* dres = nullptr;
   HIP_TRY(ctx, hipHostGetDevicePointer(&dres, ctx->h_result.p, 0));
-  d.result = static_cast<int32_t*>(dres);
+  d.result = static_cast<uint64_t*>(dres);
 
   const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
   // K0 algorithmic bytes: every table row written once; every atom row a class
@@ -263,8 +263,7 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   const bool collective = ctx->comm && use_comm;
   const int32_t timing = (ctx->timing_runs++ % ctx->timing_every) == 0 ? ctx->timing : 0;
   d.seq = ++ctx->seq;
-  volatile int32_t* res = static_cast<volatile int32_t*>(ctx->h_result.p);
-  res[4] = 0;
+  volatile uint64_t* res = static_cast<volatile uint64_t*>(ctx->h_result.p);
   // Timed kernels get an event pair from the pool, recorded by their own
   // dispatch (hipExtLaunchKernelGGL); the collective is bracketed with
   // plain records.  Events are read back lazily (flush_timing).
@@ -326,13 +325,24 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     }
     HIP_TRY(ctx, hipStreamSynchronize(s));
   } else {
-    // The result's last word is this run's sequence number, written after a
-    // system-scope fence: poll it instead of waking up on stream completion.
-    // A run that has not finished after 100 ms falls back to the stream
-    // (which also surfaces a kernel fault as an error).
+    // Every result word carries this run's sequence number in its upper
+    // half (K3 stores them without ordering): poll the header, then the
+    // winner's mapping, instead of waking up on stream completion.  A run
+    // that has not finished after 100 ms falls back to the stream (which
+    // also surfaces a kernel fault as an error).
+    const uint32_t tag = static_cast<uint32_t>(d.seq);
+    auto ready = [&](size_t i) { return static_cast<uint32_t>(res[i] >> 32) == tag; };
+    auto header_ready = [&] { return ready(0) && ready(1) && ready(2) && ready(3); };
+    auto map_ready = [&] {
+      if (!static_cast<uint32_t>(res[1])) return true;
+      const size_t np = static_cast<uint32_t>(res[2]);
+      for (size_t q = 0; q < np; ++q)
+        if (!ready(sr::kResultHeader + q)) return false;
+      return true;
+    };
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t spins = 0;
-    while (res[4] != d.seq) {
+    while (!(header_ready() && map_ready())) {
       if ((++spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100)) {
         HIP_TRY(ctx, hipStreamSynchronize(s));
         break;
@@ -349,12 +359,19 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     std::fwrite(pr.data(), sizeof(uint64_t), pr.size(), ctx->prof_file);
     std::fflush(ctx->prof_file);
   }
-  const int32_t* r = const_cast<const int32_t*>(res);
-  out->first_ok = r[0];
-  out->first_fallback = r[3];
-  out->winner = (r[0] >= 0 && (r[3] < 0 || r[3] > r[0])) ? r[0] : -1;
-  out->winner_npods = r[1] ? r[2] : 0;
-  if (out->winner_map && r[1]) std::memcpy(out->winner_map, r + sr::kResultHeader, sizeof(int32_t) * r[2]);
+  auto val = [&](size_t i) { return static_cast<int32_t>(static_cast<uint32_t>(res[i])); };
+  const uint32_t tag = static_cast<uint32_t>(d.seq);
+  for (size_t i = 0; i < 4; ++i)
+    if (static_cast<uint32_t>(res[i] >> 32) != tag) {
+      ctx->err = "result header not written by this run";
+      return SR_ERR_HIP;
+    }
+  out->first_ok = val(0);
+  out->first_fallback = val(3);
+  out->winner = (val(0) >= 0 && (val(3) < 0 || val(3) > val(0))) ? val(0) : -1;
+  out->winner_npods = val(1) ? val(2) : 0;
+  if (out->winner_map && val(1))
+    for (int32_t q = 0; q < val(2); ++q) out->winner_map[q] = val(sr::kResultHeader + q);
   out->checks = static_cast<uint64_t>(na) * static_cast<uint64_t>(w.n_spot);
   out->fallback_pods = w.fallback_pods;
   if (full) {
