@@ -43,6 +43,12 @@ WORKLOAD = {1: "C1 rescheduler_test-style 20 nodes / 200 pods",
             5: "C5 1k nodes host-port + DaemonSet heavy"}
 
 
+def host_threads():
+    """The encoder pool's thread count (csrc/pool.hpp: SR_HOST_THREADS, else min(16, cores))."""
+    env = os.environ.get("SR_HOST_THREADS")
+    return max(1, int(env)) if env else min(16, os.cpu_count() or 1)
+
+
 def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, seconds):
     """The oracle (C restatement of the reference planner) on this host, rank 0 only."""
     from oracle_lib import OracleSnapshot, oracle_plan
@@ -84,6 +90,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--e2e-reps", type=int, default=20, help="steady-state end-to-end ticks timed after the steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true",
                     help="A/B only: no HIP events in the timed region (roofline from the calibration pass)")
@@ -194,6 +201,28 @@ def main():
     assert st == capi.SR_OK, (st, checker.last_error())
     tm = checker.timing()  # bytes_placement is exact after a run with per-candidate outputs
 
+    # End-to-end tick in the steady state (untimed by the contract's K steps):
+    # candidate lists and snapshot on the host -> encode + H2D (sr_plan_prepare)
+    # -> kernels -> winner and mapping on the host (sr_plan_run).  The
+    # planner's buffers are already grown, as in every tick after the first.
+    e2e, enc, upl = [], [], []
+    for _ in range(args.e2e_reps):
+        t1 = time.perf_counter()
+        st = lib.sr_plan_prepare(checker.handle, snap, sc.ptr, ctypes.byref(cands))
+        assert st == capi.SR_OK, checker.last_error()
+        st = lib.sr_plan_run(checker.handle, ctypes.byref(out))
+        assert st == capi.SR_OK, checker.last_error()
+        e2e.append(1e3 * (time.perf_counter() - t1))
+        tq = checker.timing()
+        enc.append(tq.ms_pack_host)
+        upl.append(tq.ms_upload)
+    end_to_end = None
+    if e2e:
+        end_to_end = {"median_ms": round(float(np.median(e2e)), 3), "min_ms": round(float(np.min(e2e)), 3),
+                      "encode_ms": round(float(np.median(enc)), 3), "upload_ms": round(float(np.median(upl)), 3),
+                      "pods_for_deletion_ms": round(pfd_ms, 3), "reps": len(e2e), "host_threads": host_threads(),
+                      "span": "sr_plan_prepare (encode + H2D) + sr_plan_run, snapshot and candidate lists on host"}
+
     if rank == 0:
         alg = {"k2_placement": tm.bytes_placement, "k0_tables": tm.bytes_tables}[dom]
         achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
@@ -219,6 +248,7 @@ def main():
             "workload_rows": {"static_classes": tm.n_rows_static, "threshold_rows": tm.n_rows_threshold,
                               "words_per_row": tm.n_words},
             "host_pack_ms": round(pack_ms, 3),
+            "end_to_end_tick": end_to_end,
             "host_pods_for_deletion_ms": round(pfd_ms, 3),
             "roofline": {"bound": "hbm", "kernel": dom, "kernel_ms": round(dom_ms, 5),
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

@@ -20,6 +20,7 @@
 // exactly on the nodes the candidate touched (K2).  Features outside this set
 // route the whole candidate to the reference path (SR_CAND_FALLBACK).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <string>
@@ -28,6 +29,7 @@
 
 #include "host.hpp"
 #include "pool.hpp"
+#include "worddict.hpp"
 
 namespace sr {
 
@@ -45,28 +47,6 @@ enum : int32_t { REQ_LABEL_EQ = 0, REQ_LABEL_EXPR = 1, REQ_FIELD = 2 };
 struct Requirement {
   int32_t type, key, op;
   std::vector<int32_t> vals;  // sorted, unique
-};
-
-std::string bytes_of(const int32_t* p, size_t n) {
-  return std::string(reinterpret_cast<const char*>(p), n * sizeof(int32_t));
-}
-
-class RequirementDict {
- public:
-  int32_t intern(Requirement r) {
-    std::sort(r.vals.begin(), r.vals.end());
-    r.vals.erase(std::unique(r.vals.begin(), r.vals.end()), r.vals.end());
-    std::vector<int32_t> k = {r.type, r.key, r.op};
-    k.insert(k.end(), r.vals.begin(), r.vals.end());
-    auto ins = index_.emplace(bytes_of(k.data(), k.size()), static_cast<int32_t>(reqs_.size()));
-    if (ins.second) reqs_.push_back(std::move(r));
-    return ins.first->second;
-  }
-  const std::vector<Requirement>& all() const { return reqs_; }
-
- private:
-  std::unordered_map<std::string, int32_t> index_;
-  std::vector<Requirement> reqs_;
 };
 
 // v1.Toleration.ToleratesTaint [upstream k8s.io/api/core/v1/toleration.go].
@@ -170,64 +150,6 @@ bool has_static_spec(const sr_pods& P, int32_t pod) {
          P.port_off[pod] != P.port_off[pod + 1] || P.aff_required[pod] != 0;
 }
 
-uint64_t raw_spec_hash(const sr_pods& P, int32_t pod) {
-  if (!has_static_spec(P, pod)) return 0;
-  uint64_t h = 1469598103934665603ull;
-  for_each_spec_word(P, pod, [&](int32_t x) { h = (h ^ static_cast<uint32_t>(x)) * 1099511628211ull; });
-  h ^= h >> 29;
-  return h ? h : 1;
-}
-
-bool same_spec(const sr_pods& P, int32_t a, int32_t b) {
-  static thread_local std::vector<int32_t> wa;
-  wa.clear();
-  for_each_spec_word(P, a, [&](int32_t x) { wa.push_back(x); });
-  size_t i = 0;
-  bool eq = true;
-  for_each_spec_word(P, b, [&](int32_t x) {
-    eq = eq && i < wa.size() && wa[i] == x;
-    ++i;
-  });
-  return eq && i == wa.size();
-}
-
-// hash -> spec id (open addressing), collisions resolved by comparing specs.
-class SpecTable {
- public:
-  int32_t find_or_insert(const sr_pods& P, uint64_t h, int32_t pod, std::vector<int32_t>& spec_rep) {
-    if (slots_.empty() || (count_ + 1) * 2 > slots_.size()) grow();
-    size_t i = h & (slots_.size() - 1);
-    while (slots_[i].id >= 0) {
-      const Slot& s = slots_[i];
-      if (s.hash == h && same_spec(P, spec_rep[s.id], pod)) return s.id;
-      i = (i + 1) & (slots_.size() - 1);
-    }
-    const int32_t id = static_cast<int32_t>(spec_rep.size());
-    spec_rep.push_back(pod);
-    slots_[i] = Slot{h, id};
-    ++count_;
-    return id;
-  }
-
- private:
-  struct Slot {
-    uint64_t hash;
-    int32_t id = -1;
-  };
-  void grow() {
-    std::vector<Slot> old;
-    old.swap(slots_);
-    slots_.assign(old.empty() ? 1024 : old.size() * 2, Slot{0, -1});
-    for (const Slot& s : old)
-      if (s.id >= 0) {
-        size_t i = s.hash & (slots_.size() - 1);
-        while (slots_[i].id >= 0) i = (i + 1) & (slots_.size() - 1);
-        slots_[i] = s;
-      }
-  }
-  std::vector<Slot> slots_;
-  size_t count_ = 0;
-};
 
 }  // namespace
 
@@ -344,34 +266,26 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   // ---- taint dictionary over spot nodes (NoSchedule / NoExecute only; the
   // unschedulable flag is the pseudo-taint node.kubernetes.io/unschedulable:NoSchedule)
   std::vector<TaintRec> taints;
-  std::unordered_map<std::string, int32_t> taint_index;
+  WordDict taint_dict;
   auto taint_id = [&](const TaintRec& t) {
     const int32_t k[3] = {t.key, t.val, t.effect};
-    auto ins = taint_index.emplace(bytes_of(k, 3), static_cast<int32_t>(taints.size()));
-    if (ins.second) taints.push_back(t);
-    return ins.first->second;
+    bool ins = false;
+    const int32_t id = taint_dict.intern(k, 3, &ins);
+    if (ins) taints.push_back(t);
+    return id;
   };
-  std::vector<std::vector<int32_t>> node_taints(static_cast<size_t>(n_spot));
+  std::vector<int32_t> node_taint_off(static_cast<size_t>(n_spot) + 1, 0), node_taint_ids;
   for (int32_t n = 0; n < n_spot; ++n) {
     const SpotNode& sn = snap->nodes[n];
     for (const TaintRec& t : sn.taints)
-      if (t.effect == SR_EFFECT_NO_SCHEDULE || t.effect == SR_EFFECT_NO_EXECUTE)
-        node_taints[n].push_back(taint_id(t));
+      if (t.effect == SR_EFFECT_NO_SCHEDULE || t.effect == SR_EFFECT_NO_EXECUTE) node_taint_ids.push_back(taint_id(t));
     if (sn.unschedulable)
-      node_taints[n].push_back(taint_id(TaintRec{snap->id_unschedulable_key, snap->id_empty, SR_EFFECT_NO_SCHEDULE}));
+      node_taint_ids.push_back(taint_id(TaintRec{snap->id_unschedulable_key, snap->id_empty, SR_EFFECT_NO_SCHEDULE}));
+    node_taint_off[n + 1] = static_cast<int32_t>(node_taint_ids.size());
   }
   const int32_t n_taints = static_cast<int32_t>(taints.size());
 
   phase(1);
-  // ---- static part of every active pod
-  RequirementDict rdict;
-  struct PodStatic {
-    std::vector<int32_t> sel;                 // requirement ids
-    std::vector<std::vector<int32_t>> terms;  // valid terms only
-    int32_t flags = 0;
-    const std::vector<int32_t>* untol = nullptr;  // taint ids the pod does not tolerate
-    uint64_t ports = 0;
-  };
   // Active pods in candidate order.
   std::vector<int32_t> active_pod;   // cluster pod index
   std::vector<int32_t> active_src;   // flat index into cand_pods
@@ -390,102 +304,204 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   w->cand_off.push_back(static_cast<int32_t>(active_pod.size()));
   const int32_t na = static_cast<int32_t>(active_pod.size());
 
-  // Untolerated-taint sets, memoised by the pod's toleration list.
-  std::unordered_map<std::string, std::vector<int32_t>> untol_memo;
-  std::vector<int32_t> all_taints(static_cast<size_t>(n_taints));
-  for (int32_t t = 0; t < n_taints; ++t) all_taints[t] = t;
-
-  // Pods with byte-identical static specs (selector, affinity, tolerations,
-  // host ports) share one PodStatic: the raw spec is hashed once per pod and
-  // only first occurrences are interned.  Pods with no static constraints at
-  // all share spec 0.
-  std::vector<PodStatic> pstat(1);  // spec 0: unconstrained
-  pstat[0].untol = &all_taints;
+  // ---- distinct static specs.  Pods with word-identical static specs
+  // (selector, affinity, tolerations, host ports) share one spec; pods with no
+  // static constraints at all share spec 0.  The raw spec is hashed once per
+  // pod; the dictionaries are sharded by hash over the pool, and spec ids are
+  // assigned in first-occurrence order afterwards, so they do not depend on
+  // the thread count.
   std::vector<int32_t> pod_spec(static_cast<size_t>(na), 0);
-  std::vector<int32_t> spec_rep{-1};  // first pod of each spec
   std::vector<uint64_t> spec_hash(static_cast<size_t>(na), 0);
-  parallel_for(static_cast<size_t>(na), 2048, [&](size_t lo, size_t hi) {
-    for (size_t q = lo; q < hi; ++q) spec_hash[q] = raw_spec_hash(P, active_pod[q]);
+  std::vector<uint8_t> spec_shard(static_cast<size_t>(na), 0);
+  // The spec words are gathered once per pod (the pod arrays are read at
+  // scattered indices) into one buffer per 2048-pod chunk.
+  constexpr size_t kChunk = 2048;
+  std::vector<std::vector<int32_t>> spec_words((static_cast<size_t>(na) + kChunk - 1) / kChunk);
+  std::vector<uint32_t> spec_woff(static_cast<size_t>(na), 0);  // offset in its chunk's buffer
+  const size_t n_shards = std::min<size_t>(pool_threads(), 255);
+  auto shard_of = [n_shards](uint64_t h) { return static_cast<size_t>(((h >> 32) * n_shards) >> 32); };
+  parallel_for(spec_words.size(), 1, [&](size_t lo, size_t hi) {
+    for (size_t ch = lo; ch < hi; ++ch) {
+      std::vector<int32_t>& buf = spec_words[ch];
+      const size_t q1 = std::min(static_cast<size_t>(na), (ch + 1) * kChunk);
+      for (size_t q = ch * kChunk; q < q1; ++q) {
+        const size_t b0 = buf.size();
+        spec_woff[q] = static_cast<uint32_t>(b0);
+        const int32_t pod = active_pod[q];
+        if (!has_static_spec(P, pod)) {
+          spec_shard[q] = 255;  // spec 0
+          continue;
+        }
+        for_each_spec_word(P, pod, [&](int32_t x) { buf.push_back(x); });
+        const uint64_t h = hash_words(buf.data() + b0, buf.size() - b0);
+        spec_hash[q] = h;
+        spec_shard[q] = static_cast<uint8_t>(shard_of(h));
+      }
+    }
   });
-  SpecTable table;
-  for (int32_t q = 0; q < na; ++q) {
-    if (spec_hash[q] == 0) continue;  // no static constraints: spec 0
-    const int32_t id = table.find_or_insert(P, spec_hash[q], active_pod[q], spec_rep);
-    pod_spec[q] = id;
+  auto words_of = [&](size_t q, size_t* n) {
+    const std::vector<int32_t>& buf = spec_words[q / kChunk];
+    const size_t e = (q + 1) % kChunk == 0 || q + 1 == static_cast<size_t>(na) ? buf.size() : spec_woff[q + 1];
+    *n = e - spec_woff[q];
+    return buf.data() + spec_woff[q];
+  };
+  phase(14);
+  struct Shard {
+    WordDict dict;
+    std::vector<int32_t> rep_q;  // local id -> first active pod
+  };
+  std::vector<Shard> shards(n_shards);
+  parallel_for(n_shards, 1, [&](size_t lo, size_t hi) {
+    for (size_t sh = lo; sh < hi; ++sh) {
+      Shard& S = shards[sh];
+      S.dict.clear();
+      for (int32_t q = 0; q < na; ++q) {
+        if (spec_shard[q] != sh) continue;
+        size_t n = 0;
+        const int32_t* p = words_of(static_cast<size_t>(q), &n);
+        bool ins = false;
+        pod_spec[q] = S.dict.intern(p, n, spec_hash[q], &ins);
+        if (ins) S.rep_q.push_back(q);
+      }
+    }
+  });
+  phase(15);
+  std::vector<int32_t> spec_rep{-1};  // first pod of each spec
+  {
+    struct Rep {
+      int32_t q, shard, local;
+    };
+    std::vector<Rep> reps;
+    std::vector<std::vector<int32_t>> global(n_shards);
+    for (size_t sh = 0; sh < n_shards; ++sh) {
+      global[sh].resize(shards[sh].rep_q.size());
+      for (size_t l = 0; l < shards[sh].rep_q.size(); ++l)
+        reps.push_back(Rep{shards[sh].rep_q[l], static_cast<int32_t>(sh), static_cast<int32_t>(l)});
+    }
+    std::sort(reps.begin(), reps.end(), [](const Rep& x, const Rep& y) { return x.q < y.q; });
+    for (const Rep& r : reps) {
+      global[r.shard][r.local] = static_cast<int32_t>(spec_rep.size());
+      spec_rep.push_back(active_pod[r.q]);
+    }
+    parallel_for(static_cast<size_t>(na), 4096, [&](size_t lo, size_t hi) {
+      for (size_t q = lo; q < hi; ++q)
+        if (spec_shard[q] != 255) pod_spec[q] = global[spec_shard[q]][pod_spec[q]];
+    });
   }
+  const size_t n_specs = spec_rep.size();
   phase(7);
-  pstat.resize(spec_rep.size());
-  for (size_t sp = 1; sp < spec_rep.size(); ++sp) {
-    const int32_t pod = spec_rep[sp];
-    const int32_t s0 = P.sel_off[pod], s1 = P.sel_off[pod + 1];
-    const int32_t t0 = P.tol_off[pod], t1 = P.tol_off[pod + 1];
-    const bool aff = P.aff_required[pod] != 0;
-    PodStatic& ps = pstat[sp];
-    // Spec.NodeSelector: labels.SelectorFromSet -> Equals requirements.
-    for (int32_t i = s0; i < s1; ++i)
-      ps.sel.push_back(rdict.intern(Requirement{REQ_LABEL_EQ, P.sel_key[i], SR_OP_IN, {P.sel_val[i]}}));
-    std::sort(ps.sel.begin(), ps.sel.end());
-    ps.sel.erase(std::unique(ps.sel.begin(), ps.sel.end()), ps.sel.end());
-    // Required node affinity: MatchNodeSelectorTerms.
-    if (aff) {
-      ps.flags |= CLS_AFF_REQUIRED;
-      for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t) {
-        const int32_t e0 = P.term_expr_off[t], e1 = P.term_expr_off[t + 1];
-        const int32_t f0 = P.term_field_off[t], f1 = P.term_field_off[t + 1];
-        if (e0 == e1 && f0 == f1) continue;  // an empty term selects nothing
-        bool valid = true;
-        std::vector<int32_t> term;
-        for (int32_t e = e0; e < e1 && valid; ++e) {
-          const int32_t nv = P.expr_val_off[e + 1] - P.expr_val_off[e];
-          const int32_t op = P.expr_op[e];
-          if (P.expr_key[e] == c->id_empty) valid = false;  // validateLabelKey("") fails
-          else if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) valid = false;
-          else if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) valid = false;
-          else if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST)
-            valid = false;
-          if (!valid) break;
-          Requirement r{REQ_LABEL_EXPR, P.expr_key[e], op,
-                        std::vector<int32_t>(P.expr_vals + P.expr_val_off[e], P.expr_vals + P.expr_val_off[e + 1])};
-          term.push_back(rdict.intern(std::move(r)));
-        }
-        for (int32_t f = f0; f < f1 && valid; ++f) {
-          const int32_t nv = P.field_val_off[f + 1] - P.field_val_off[f];
-          const int32_t op = P.field_op[f];
-          if (!((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 1)) {
-            valid = false;
-            break;
+
+  // ---- per spec (parallel): canonical requirements, untolerated taints, ports.
+  // A requirement is the word group {len, type, key, op, sorted unique vals}.
+  struct SpecCanon {
+    int32_t flags = 0;
+    std::vector<int32_t> sel;    // nodeSelector requirement groups
+    std::vector<int32_t> terms;  // per valid term: {n_req, groups...}
+    int32_t n_terms = 0;
+    std::vector<int32_t> untol;  // taint ids the spec does not tolerate
+    uint64_t ports = 0;
+  };
+  std::vector<SpecCanon> canon(n_specs);
+  auto put_req = [](std::vector<int32_t>& out, int32_t type, int32_t key, int32_t op, const int32_t* v, int32_t nv) {
+    const size_t at = out.size();
+    out.push_back(0);
+    out.push_back(type);
+    out.push_back(key);
+    out.push_back(op);
+    const size_t vb = out.size();
+    out.insert(out.end(), v, v + nv);
+    std::sort(out.begin() + vb, out.end());
+    out.erase(std::unique(out.begin() + vb, out.end()), out.end());
+    out[at] = static_cast<int32_t>(out.size() - at - 1);
+  };
+  parallel_for(n_specs, 64, [&](size_t lo, size_t hi) {
+    std::vector<int32_t> term;
+    for (size_t sp = lo; sp < hi; ++sp) {
+      SpecCanon& sc = canon[sp];
+      if (sp == 0) {  // unconstrained: tolerates nothing
+        for (int32_t t = 0; t < n_taints; ++t) sc.untol.push_back(t);
+        continue;
+      }
+      const int32_t pod = spec_rep[sp];
+      // Spec.NodeSelector: labels.SelectorFromSet -> Equals requirements.
+      for (int32_t i = P.sel_off[pod]; i < P.sel_off[pod + 1]; ++i)
+        put_req(sc.sel, REQ_LABEL_EQ, P.sel_key[i], SR_OP_IN, &P.sel_val[i], 1);
+      // Required node affinity: MatchNodeSelectorTerms.
+      if (P.aff_required[pod]) {
+        sc.flags |= CLS_AFF_REQUIRED;
+        for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t) {
+          const int32_t e0 = P.term_expr_off[t], e1 = P.term_expr_off[t + 1];
+          const int32_t f0 = P.term_field_off[t], f1 = P.term_field_off[t + 1];
+          if (e0 == e1 && f0 == f1) continue;  // an empty term selects nothing
+          bool valid = true;
+          term.clear();
+          for (int32_t e = e0; e < e1 && valid; ++e) {
+            const int32_t nv = P.expr_val_off[e + 1] - P.expr_val_off[e];
+            const int32_t op = P.expr_op[e];
+            if (P.expr_key[e] == c->id_empty) valid = false;  // validateLabelKey("") fails
+            else if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) valid = false;
+            else if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) valid = false;
+            else if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST)
+              valid = false;
+            if (valid) put_req(term, REQ_LABEL_EXPR, P.expr_key[e], op, P.expr_vals + P.expr_val_off[e], nv);
           }
-          term.push_back(rdict.intern(Requirement{REQ_FIELD, P.field_key[f], op, {P.field_vals[P.field_val_off[f]]}}));
+          for (int32_t f = f0; f < f1 && valid; ++f) {
+            const int32_t nv = P.field_val_off[f + 1] - P.field_val_off[f];
+            const int32_t op = P.field_op[f];
+            valid = (op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 1;
+            if (valid) put_req(term, REQ_FIELD, P.field_key[f], op, &P.field_vals[P.field_val_off[f]], 1);
+          }
+          if (!valid) continue;  // a term that fails to build matches nothing
+          sc.terms.push_back(static_cast<int32_t>(f1 - f0 + e1 - e0));
+          sc.terms.insert(sc.terms.end(), term.begin(), term.end());
+          ++sc.n_terms;
         }
-        if (!valid) continue;  // a term that fails to build matches nothing
-        std::sort(term.begin(), term.end());
-        term.erase(std::unique(term.begin(), term.end()), term.end());
-        ps.terms.push_back(std::move(term));
+        if (sc.n_terms == 0) sc.flags |= CLS_IMPOSSIBLE;
       }
-      if (ps.terms.empty()) ps.flags |= CLS_IMPOSSIBLE;
+      // Spec.Tolerations against the spot pool's taints.
+      for (int32_t t = 0; t < n_taints; ++t)
+        if (!tolerates(P, pod, c->id_empty, taints[t])) sc.untol.push_back(t);
+      sc.ports = pod_port_mask(pod);
     }
-    // Spec.Tolerations against the spot pool's taints.
-    if (t0 == t1) {
-      ps.untol = &all_taints;
-    } else {
-      std::string tkey;
-      for (int32_t i = t0; i < t1; ++i) {
-        const int32_t rec[4] = {P.tol_key[i], P.tol_op[i], P.tol_val[i], P.tol_effect[i]};
-        tkey += bytes_of(rec, 4);
+  });
+
+  // ---- requirement ids and class signatures (serial: ids in spec order).
+  // Signature: {flags, n_sel, sel ids (sorted), n_terms, per term {n, ids (sorted)},
+  // untolerated-set id, ports lo, ports hi}.
+  WordDict rdict;      // requirement words {type, key, op, vals...}
+  WordDict untol_dict;  // untolerated taint sets
+  std::vector<int32_t> sig_words, sig_off{0}, ids;
+  for (size_t sp = 0; sp < n_specs; ++sp) {
+    const SpecCanon& sc = canon[sp];
+    auto intern_groups = [&](const int32_t* g, int32_t n_groups, size_t* used) {
+      ids.clear();
+      size_t i = 0;
+      for (int32_t k = 0; k < n_groups; ++k) {
+        ids.push_back(rdict.intern(g + i + 1, static_cast<size_t>(g[i])));
+        i += 1 + static_cast<size_t>(g[i]);
       }
-      auto it = untol_memo.find(tkey);
-      if (it == untol_memo.end()) {
-        std::vector<int32_t> u;
-        for (int32_t t = 0; t < n_taints; ++t)
-          if (!tolerates(P, pod, c->id_empty, taints[t])) u.push_back(t);
-        it = untol_memo.emplace(std::move(tkey), std::move(u)).first;
-      }
-      ps.untol = &it->second;
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      sig_words.push_back(static_cast<int32_t>(ids.size()));
+      sig_words.insert(sig_words.end(), ids.begin(), ids.end());
+      if (used) *used = i;
+    };
+    sig_words.push_back(sc.flags);
+    int32_t n_sel = 0;
+    for (size_t i = 0; i < sc.sel.size(); i += 1 + static_cast<size_t>(sc.sel[i])) ++n_sel;
+    intern_groups(sc.sel.data(), n_sel, nullptr);
+    sig_words.push_back(sc.n_terms);
+    for (size_t i = 0, k = 0; k < static_cast<size_t>(sc.n_terms); ++k) {
+      size_t used = 0;
+      intern_groups(sc.terms.data() + i + 1, sc.terms[i], &used);
+      i += 1 + used;
     }
-    ps.ports = pod_port_mask(pod);
+    sig_words.push_back(untol_dict.intern(sc.untol));
+    sig_words.push_back(static_cast<int32_t>(sc.ports & 0xffffffffu));
+    sig_words.push_back(static_cast<int32_t>(sc.ports >> 32));
+    sig_off.push_back(static_cast<int32_t>(sig_words.size()));
   }
-  const std::vector<Requirement>& reqs = rdict.all();
-  const int32_t n_reqs = static_cast<int32_t>(reqs.size());
+  const int32_t n_reqs = static_cast<int32_t>(rdict.size());
   const int32_t n_ports = static_cast<int32_t>(port_dict.size());
   const int32_t A_REQ = 1, A_TAINT = 1 + n_reqs, A_PORT = 1 + n_reqs + n_taints;
   // Composite atoms, one per distinct untolerated-taint set U of the pods:
@@ -493,58 +509,54 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   // TaintToleration / NodeUnschedulable in one row, so a class program opens
   // with a single AND instead of 1 + |U| operations.
   const int32_t A_COMP = A_PORT + n_ports;
-  std::unordered_map<const std::vector<int32_t>*, int32_t> comp_index;
-  std::vector<const std::vector<int32_t>*> comp_sets;
-  auto comp_atom = [&](const std::vector<int32_t>* u) {
-    if (u->empty()) return 0;  // tolerates every taint: the pod-count atom alone
-    auto ins = comp_index.emplace(u, static_cast<int32_t>(comp_sets.size()));
-    if (ins.second) comp_sets.push_back(u);
-    return A_COMP + ins.first->second;
+  std::vector<int32_t> comp_of(untol_dict.size(), -1), comp_sets;  // untolerated-set ids
+  auto comp_atom = [&](int32_t u) {
+    if (untol_dict.len(u) == 0) return 0;  // tolerates every taint: the pod-count atom alone
+    if (comp_of[u] < 0) {
+      comp_of[u] = static_cast<int32_t>(comp_sets.size());
+      comp_sets.push_back(u);
+    }
+    return A_COMP + comp_of[u];
   };
 
   phase(2);
-  // ---- intern classes (atom programs), once per distinct spec
-  std::unordered_map<std::string, int32_t> class_index;
-  std::vector<int32_t> spec_class(pstat.size());
+  // ---- intern classes (atom programs), once per distinct signature
+  WordDict class_dict;
+  std::vector<int32_t> spec_class(n_specs);
   w->cls_prog_off.push_back(0);
   auto emit = [&](int32_t atom, int32_t kind) { w->cls_prog.push_back(atom << 2 | kind); };
-  std::vector<int32_t> sig;
-  for (size_t sp = 0; sp < pstat.size(); ++sp) {
-    const PodStatic& ps = pstat[sp];
-    sig.clear();
-    sig.push_back(ps.flags);
-    sig.push_back(static_cast<int32_t>(ps.sel.size()));
-    sig.insert(sig.end(), ps.sel.begin(), ps.sel.end());
-    sig.push_back(static_cast<int32_t>(ps.terms.size()));
-    for (const auto& t : ps.terms) {
-      sig.push_back(static_cast<int32_t>(t.size()));
-      sig.insert(sig.end(), t.begin(), t.end());
-    }
-    sig.push_back(static_cast<int32_t>(ps.untol->size()));
-    sig.insert(sig.end(), ps.untol->begin(), ps.untol->end());
-    sig.push_back(static_cast<int32_t>(ps.ports & 0xffffffffu));
-    sig.push_back(static_cast<int32_t>(ps.ports >> 32));
-    auto ins = class_index.emplace(bytes_of(sig.data(), sig.size()), w->n_classes);
-    if (ins.second) {
-      // program: AND atoms, AND-NOT atoms, then the ORed terms (TERM_START
-      // opens a term, TERM_AND extends it); an impossible class ANDs atom 0
-      // with its complement
-      emit(comp_atom(ps.untol), PROG_AND);  // len(pods)+1 <= allowed pods, untolerated taints
-      for (int32_t r : ps.sel) emit(A_REQ + r, PROG_AND);
-      for (int32_t b = 0; b < 64; ++b)
-        if (ps.ports >> b & 1) emit(A_PORT + b, PROG_ANDNOT);
-      if (ps.flags & CLS_IMPOSSIBLE) {
-        emit(0, PROG_ANDNOT);
-      } else {
-        for (const auto& t : ps.terms)
-          for (size_t i = 0; i < t.size(); ++i) emit(A_REQ + t[i], i == 0 ? PROG_TERM_START : PROG_TERM_AND);
+  for (size_t sp = 0; sp < n_specs; ++sp) {
+    const int32_t* g = sig_words.data() + sig_off[sp];
+    bool ins = false;
+    spec_class[sp] = class_dict.intern(g, static_cast<size_t>(sig_off[sp + 1] - sig_off[sp]), &ins);
+    if (!ins) continue;
+    // program: AND atoms, AND-NOT atoms, then the ORed terms (TERM_START
+    // opens a term, TERM_AND extends it); an impossible class ANDs atom 0
+    // with its complement
+    const int32_t flags = g[0], n_sel = g[1];
+    const int32_t* sel = g + 2;
+    const int32_t* tp = sel + n_sel;
+    const int32_t n_terms = *tp++;
+    const int32_t* term_words = tp;
+    for (int32_t k = 0; k < n_terms; ++k) tp += 1 + *tp;
+    const int32_t untol = tp[0];
+    const uint64_t ports = static_cast<uint32_t>(tp[1]) | static_cast<uint64_t>(static_cast<uint32_t>(tp[2])) << 32;
+    emit(comp_atom(untol), PROG_AND);  // len(pods)+1 <= allowed pods, untolerated taints
+    for (int32_t k = 0; k < n_sel; ++k) emit(A_REQ + sel[k], PROG_AND);
+    for (int32_t b = 0; b < 64; ++b)
+      if (ports >> b & 1) emit(A_PORT + b, PROG_ANDNOT);
+    if (flags & CLS_IMPOSSIBLE) {
+      emit(0, PROG_ANDNOT);
+    } else {
+      for (int32_t k = 0; k < n_terms; ++k) {
+        const int32_t n = *term_words++;
+        for (int32_t i = 0; i < n; ++i) emit(A_REQ + term_words[i], i == 0 ? PROG_TERM_START : PROG_TERM_AND);
+        term_words += n;
       }
-      w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
-      w->n_classes++;
     }
-    spec_class[sp] = ins.first->second;
+    w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
+    w->n_classes++;
   }
-
   w->n_atoms = A_COMP + static_cast<int32_t>(comp_sets.size());
   phase(3);
   // ---- spot nodes: base capacity state and the atom rows
@@ -581,7 +593,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     w->port_bits[n] = pb;
     for (int32_t b = 0; b < 64; ++b)
       if (pb >> b & 1) set_atom(A_PORT + b, n);
-    for (int32_t t : node_taints[n]) set_atom(A_TAINT + t, n);
+    for (int32_t k = node_taint_off[n]; k < node_taint_off[n + 1]; ++k) set_atom(A_TAINT + node_taint_ids[k], n);
   }
   w->node_rec.assign(static_cast<size_t>(NP) * 8, 0);
   for (int32_t n = 0; n < n_spot; ++n) {
@@ -597,15 +609,18 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     uint64_t* row = &w->atoms[static_cast<size_t>(A_COMP + static_cast<int32_t>(k)) * Wp];
     for (int32_t i = 0; i < Wp; ++i) {
       uint64_t any = 0;
-      for (int32_t t : *comp_sets[k]) any |= w->atoms[static_cast<size_t>(A_TAINT + t) * Wp + i];
+      const int32_t* u = untol_dict.data(comp_sets[k]);
+      for (size_t j = 0; j < untol_dict.len(comp_sets[k]); ++j) any |= w->atoms[static_cast<size_t>(A_TAINT + u[j]) * Wp + i];
       row[i] = w->atoms[i] & ~any;
     }
   }
   phase(9);
   // requirement atoms: one label-value column per distinct key
   std::unordered_map<int32_t, std::vector<int32_t>> col;  // key -> value per node (INT32_MIN absent)
-  for (const Requirement& r : reqs)
-    if (r.type != REQ_FIELD && !col.count(r.key)) col.emplace(r.key, std::vector<int32_t>(n_spot, INT32_MIN));
+  for (int32_t ri = 0; ri < n_reqs; ++ri) {
+    const int32_t* r = rdict.data(ri);  // {type, key, op, vals...}
+    if (r[0] != REQ_FIELD && !col.count(r[1])) col.emplace(r[1], std::vector<int32_t>(n_spot, INT32_MIN));
+  }
   for (int32_t n = 0; n < n_spot; ++n)
     for (const auto& kv : snap->nodes[n].labels) {
       auto it = col.find(kv.first);
@@ -613,7 +628,8 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     }
   parallel_for(static_cast<size_t>(n_reqs), 1, [&](size_t rlo, size_t rhi) {
   for (size_t ri = rlo; ri < rhi; ++ri) {  // one atom row per requirement: disjoint writes
-    const Requirement& r = reqs[ri];
+    const int32_t* rw = rdict.data(static_cast<int32_t>(ri));
+    const Requirement r{rw[0], rw[1], rw[2], std::vector<int32_t>(rw + 3, rw + rdict.len(static_cast<int32_t>(ri)))};
     const int32_t atom = A_REQ + static_cast<int32_t>(ri);
     if (r.type == REQ_FIELD) {
       // fields.Set{"metadata.name": node.Name}; any other key reads as "".
@@ -659,46 +675,31 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   const int64_t kNever = INT64_MAX;  // free >= INT64_MAX never holds (free < 2^62)
   std::vector<int64_t> node_vals[3];
   const std::vector<int64_t>* frees[3] = {&w->free_cpu, &w->free_mem, &w->free_eph};
-  for (int d = 0; d < 3; ++d) {
-    node_vals[d].assign(frees[d]->begin(), frees[d]->begin() + n_spot);
-    std::sort(node_vals[d].begin(), node_vals[d].end());
-    node_vals[d].erase(std::unique(node_vals[d].begin(), node_vals[d].end()), node_vals[d].end());
-  }
   std::vector<int32_t> t_index[3];  // lower-bound position -> T row
   LowerBound lb[3];
-  for (int d = 0; d < 3; ++d) {
-    t_index[d].assign(node_vals[d].size() + 1, -1);
-    lb[d].build(node_vals[d]);
-  }
-  w->pod_rows.resize(static_cast<size_t>(na) * 4);
-  w->pod_rec.assign(static_cast<size_t>(na + 128) * 6, 0);  // padded: K2 stages 64-pod halves
-  w->pod_src = active_src;
-  // per pod (parallel): requests, records and the lower-bound position of each
-  // request among the node values (stored in pod_rows[1..3] for now)
-  parallel_for(static_cast<size_t>(na), 2048, [&](size_t lo, size_t hi) {
-    for (size_t q = lo; q < hi; ++q) {
-      const int32_t pod = active_pod[q];
-      const int64_t rc = P.req_milli_cpu[pod], rm = P.req_memory[pod], re = P.req_ephemeral[pod];
-      const bool zero = rc == 0 && rm == 0 && re == 0;
-      int32_t* r = &w->pod_rows[q * 4];
-      r[0] = spec_class[pod_spec[q]];
-      r[1] = zero ? -1 : static_cast<int32_t>(lb[0](rc));
-      r[2] = zero ? -1 : static_cast<int32_t>(lb[1](rm));
-      r[3] = zero ? -1 : static_cast<int32_t>(lb[2](re));
-      uint64_t* rec = &w->pod_rec[q * 6];
-      rec[0] = static_cast<uint64_t>(rc);
-      rec[1] = static_cast<uint64_t>(rm);
-      rec[2] = static_cast<uint64_t>(re);
-      rec[3] = pstat[pod_spec[q]].ports;
+  parallel_for(3, 1, [&](size_t lo, size_t hi) {
+    for (size_t d = lo; d < hi; ++d) {
+      node_vals[d].assign(frees[d]->begin(), frees[d]->begin() + n_spot);
+      std::sort(node_vals[d].begin(), node_vals[d].end());
+      node_vals[d].erase(std::unique(node_vals[d].begin(), node_vals[d].end()), node_vals[d].end());
+      t_index[d].assign(node_vals[d].size() + 1, -1);
+      lb[d].build(node_vals[d]);
     }
   });
-  phase(10);
+  // every field of pod_rows / pod_rec is written below (only the padding is
+  // cleared here): the vectors keep their size across encodes, so this is
+  // no zero fill in the steady state
+  w->pod_rows.resize(static_cast<size_t>(na) * 4);
+  w->pod_rec.resize(static_cast<size_t>(na + 128) * 6);  // padded: K2 stages 64-pod halves
+  std::fill(w->pod_rec.begin() + static_cast<size_t>(na) * 6, w->pod_rec.end(), 0);
+  w->pod_src = active_src;
   // Pods whose F row is certainly empty point at one all-zero class (atom 0
   // AND NOT atom 0), so K2 knows them without reading their rows: a class
   // that ANDs an empty atom, ANDs the complement of a full one, or whose
   // terms each hold an empty atom; or a request above every node's free
   // value in some dimension (the never-row).  Sound, not complete: the rest
   // is found exactly on the device.
+  std::vector<uint8_t> cls_empty(static_cast<size_t>(w->n_classes), 0);
   {
     std::vector<uint8_t> atom_empty(static_cast<size_t>(w->n_atoms)), atom_full(static_cast<size_t>(w->n_atoms));
     for (int32_t a = 0; a < w->n_atoms; ++a) {
@@ -708,7 +709,6 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       atom_empty[a] = pop == 0;
       atom_full[a] = pop == n_spot;
     }
-    std::vector<uint8_t> cls_empty(static_cast<size_t>(w->n_classes), 0);
     for (int32_t c = 0; c < w->n_classes; ++c) {
       bool empty = false, has_terms = false, all_terms_empty = true, term_empty = false;
       for (int32_t o = w->cls_prog_off[c]; o < w->cls_prog_off[c + 1]; ++o) {
@@ -729,21 +729,39 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       if (has_terms) all_terms_empty = all_terms_empty && term_empty;
       cls_empty[c] = empty || (has_terms && all_terms_empty);
     }
-    std::vector<int32_t> dead_pods;
-    for (int32_t q = 0; q < na; ++q) {
-      const int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
+  }
+  std::atomic<bool> any_dead{false};
+  // per pod (parallel): requests, records and the lower-bound position of each
+  // request among the node values (stored in pod_rows[1..3] for now)
+  parallel_for(static_cast<size_t>(na), 2048, [&](size_t lo, size_t hi) {
+    for (size_t q = lo; q < hi; ++q) {
+      const int32_t pod = active_pod[q];
+      const int64_t rc = P.req_milli_cpu[pod], rm = P.req_memory[pod], re = P.req_ephemeral[pod];
+      const bool zero = rc == 0 && rm == 0 && re == 0;
+      int32_t* r = &w->pod_rows[q * 4];
+      r[0] = spec_class[pod_spec[q]];
+      r[1] = zero ? -1 : static_cast<int32_t>(lb[0](rc));
+      r[2] = zero ? -1 : static_cast<int32_t>(lb[1](rm));
+      r[3] = zero ? -1 : static_cast<int32_t>(lb[2](re));
+      uint64_t* rec = &w->pod_rec[q * 6];
+      rec[0] = static_cast<uint64_t>(rc);
+      rec[1] = static_cast<uint64_t>(rm);
+      rec[2] = static_cast<uint64_t>(re);
+      rec[3] = canon[pod_spec[q]].ports;
       bool dead = cls_empty[r[0]] != 0;
-      for (int d = 0; d < 3; ++d)
-        dead = dead || (r[1 + d] >= 0 && static_cast<size_t>(r[1 + d]) == node_vals[d].size());
-      if (dead) dead_pods.push_back(q);
+      for (int d = 0; d < 3; ++d) dead = dead || (r[1 + d] >= 0 && static_cast<size_t>(r[1 + d]) == node_vals[d].size());
+      if (dead) {
+        r[0] = -1;  // the empty class, appended below
+        any_dead.store(true, std::memory_order_relaxed);
+      }
     }
-    if (!dead_pods.empty()) {
-      emit(0, PROG_AND);
-      emit(0, PROG_ANDNOT);
-      w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
-      w->empty_class = w->n_classes++;
-      for (int32_t q : dead_pods) w->pod_rows[static_cast<size_t>(q) * 4] = w->empty_class;
-    }
+  });
+  phase(10);
+  if (any_dead.load(std::memory_order_relaxed)) {
+    emit(0, PROG_AND);
+    emit(0, PROG_ANDNOT);
+    w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
+    w->empty_class = w->n_classes++;
   }
   phase(11);
   // positions -> T rows: row 0 = every node, then the used positions of each
@@ -780,14 +798,17 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     for (int32_t n = 0; n < n_spot; ++n) rk[n] = below[lb[d](fr[n]) + 1];  // fr[n] is node_vals[d][pos]
   }
   phase(13);
-  for (int32_t q = 0; q < na; ++q) {
-    int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
-    for (int d = 0; d < 3; ++d) r[1 + d] = r[1 + d] < 0 ? 0 : t_index[d][static_cast<size_t>(r[1 + d])];
-    uint64_t* rec = &w->pod_rec[static_cast<size_t>(q) * 6];
+  parallel_for(static_cast<size_t>(na), 4096, [&](size_t lo, size_t hi) {
     auto off = [&](int32_t table_row) { return static_cast<uint64_t>(table_row) * static_cast<uint64_t>(w->Wp); };
-    rec[4] = off(r[0]) | off(w->n_classes + r[1]) << 32;
-    rec[5] = off(w->n_classes + r[2]) | off(w->n_classes + r[3]) << 32;
-  }
+    for (size_t q = lo; q < hi; ++q) {
+      int32_t* r = &w->pod_rows[q * 4];
+      if (r[0] < 0) r[0] = w->empty_class;
+      for (int d = 0; d < 3; ++d) r[1 + d] = r[1 + d] < 0 ? 0 : t_index[d][static_cast<size_t>(r[1 + d])];
+      uint64_t* rec = &w->pod_rec[q * 6];
+      rec[4] = off(r[0]) | off(w->n_classes + r[1]) << 32;
+      rec[5] = off(w->n_classes + r[2]) | off(w->n_classes + r[3]) << 32;
+    }
+  });
   if ((static_cast<uint64_t>(w->n_classes) + w->t_dim.size()) * static_cast<uint64_t>(w->Wp) >= (1ull << 32)) {
     *err = "bitmask tables exceed 2^32 words";
     return SR_ERR_CAPACITY;

@@ -123,10 +123,12 @@ struct Workload {
   // encodes one tick after another, and fresh multi-MB buffers page-fault.
   void reset() {
     for (auto* v : {&free_cpu, &free_mem, &free_eph, &t_thr}) v->clear();
-    for (auto* v : {&pods_left, &cls_prog_off, &cls_prog, &cls_prog8, &t_dim, &node_rank, &pod_rows, &pod_src,
-                    &cand_off, &cand_global, &cand_src, &list, &status_host})
+    for (auto* v : {&pods_left, &cls_prog_off, &cls_prog, &cls_prog8, &t_dim, &node_rank, &pod_src, &cand_off,
+                    &cand_global, &cand_src, &list, &status_host})
       v->clear();
-    for (auto* v : {&port_bits, &node_rec, &atoms, &pod_rec}) v->clear();
+    for (auto* v : {&port_bits, &node_rec, &atoms}) v->clear();
+    // pod_rows / pod_rec keep their size: the encoder resizes them and writes
+    // every field, so a steady-state encode does not zero-fill them first
     n_spot = n_pad = Wp = n_atoms = n_classes = 0;
     empty_class = -1;
     for (int32_t& t : t_off) t = 0;

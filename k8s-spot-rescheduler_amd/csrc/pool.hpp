@@ -23,6 +23,8 @@ class Pool {
     return pool;
   }
 
+  size_t threads() const { return workers_.size() + 1; }
+
   void parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn) {
     if (n == 0) return;
     if (workers_.empty() || n <= grain) {
@@ -94,6 +96,8 @@ class Pool {
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
+
+inline size_t pool_threads() { return Pool::get().threads(); }
 
 inline void parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn) {
   Pool::get().parallel_for(n, grain, fn);

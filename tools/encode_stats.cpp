@@ -3,6 +3,7 @@
 //   make -C k8s-spot-rescheduler_amd tools && k8s-spot-rescheduler_amd/build/encode_stats 3
 #include <chrono>
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -43,12 +44,17 @@ int main(int argc, char** argv) {
   sr::Workload w;
   std::string err;
   auto t3 = std::chrono::steady_clock::now();
-  int reps = 5;
-  for (int r = 0; r < reps; ++r) sr::encode_workload(snap, &c, &cands, &w, &err);
+  int reps = 20;
+  double best = 1e30;
+  for (int r = 0; r < reps; ++r) {
+    auto a = std::chrono::steady_clock::now();
+    sr::encode_workload(snap, &c, &cands, &w, &err);
+    best = std::min(best, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count());
+  }
   auto t4 = std::chrono::steady_clock::now();
   auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   printf("config %d: nodes %d pods %d spot %d od %d cand_pods %zu\n", p.config, nn, np, ns, nod, cp.size());
-  printf("new_node_map %.2f ms, snapshot %.2f ms, encode %.2f ms\n", ms(t0, t1), ms(t1, t2), ms(t3, t4) / reps);
+  printf("new_node_map %.2f ms, snapshot %.2f ms, encode %.2f ms (best %.2f)\n", ms(t0, t1), ms(t1, t2), ms(t3, t4) / reps, best);
   printf("phases(ms): dims %.2f fallback+ports+taints %.2f pod-static %.2f classes %.2f nodes+atoms %.2f t-rows+pods %.2f lists %.2f (pod-static: keys %.2f; t-setup %.2f)\n",
          sr::encode_phase_ms[0], sr::encode_phase_ms[1], sr::encode_phase_ms[2], sr::encode_phase_ms[3],
          sr::encode_phase_ms[4], sr::encode_phase_ms[5], sr::encode_phase_ms[6], sr::encode_phase_ms[7], sr::encode_phase_ms[8]);
