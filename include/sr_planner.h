@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SR_ABI_VERSION 2
+#define SR_ABI_VERSION 3
 
 /* ------------------------------------------------------------------ status */
 typedef int32_t sr_status;
@@ -75,12 +75,15 @@ typedef int32_t sr_status;
 /* Pod flags (sr_pods.flags). */
 #define SR_POD_DAEMONSET_CONTROLLER (1u << 0)  /* an owner ref with *Controller && Kind=="DaemonSet" (rescheduler.go:243-248) */
 #define SR_POD_MIRROR               (1u << 1)  /* mirror pod (config.mirror annotation) */
-#define SR_POD_HAS_REQ_ANTI_AFFINITY (1u << 2) /* carries required pod anti-affinity terms (matters when it sits on a spot node) */
+#define SR_POD_HAS_REQ_ANTI_AFFINITY (1u << 2) /* carries required pod anti-affinity terms (matters when it sits on a spot node);
+                                                  without sr_cluster.pod_affinity, or with the flag but no terms
+                                                  there, the terms are opaque and every candidate falls back */
 /* Fallback reasons set by the shim: features the encoded predicate set does not cover. */
 #define SR_POD_FB_SCALAR_RESOURCES  (1u << 8)  /* extended / hugepages / attachable-volume requests */
 #define SR_POD_FB_VOLUMES           (1u << 9)  /* PVCs or volumes inspected by volume filters */
 #define SR_POD_FB_TOPOLOGY_SPREAD   (1u << 10) /* DoNotSchedule topology spread constraints */
-#define SR_POD_FB_POD_AFFINITY      (1u << 11) /* required pod affinity or anti-affinity */
+#define SR_POD_FB_POD_AFFINITY      (1u << 11) /* required pod affinity (and anti-affinity when the shim does not
+                                                  pass sr_cluster.pod_affinity) */
 #define SR_POD_FB_OTHER             (1u << 12) /* anything else the shim cannot encode */
 #define SR_POD_FB_MASK              (0xff00u)
 
@@ -140,12 +143,35 @@ typedef struct {
   const int32_t *port_off, *port_proto, *port_num, *port_ip /* -1 = "" or "0.0.0.0" */;
 } sr_pods;
 
+/* Required inter-pod anti-affinity: the InterPodAffinity filter of k8s
+ * v1.19.2 [upstream plugins/interpodaffinity] for
+ * Spec.Affinity.PodAntiAffinity.RequiredDuringSchedulingIgnoredDuringExecution,
+ * and the pod namespaces and labels its terms select on.  CSR arrays over
+ * sr_pods; terms are numbered across all pods.  A term's Namespaces list is
+ * empty when the API object's is (the term then selects in its own pod's
+ * namespace).  Selector operators: SR_OP_IN / NOT_IN / EXISTS / DOES_NOT_EXIST;
+ * anything else (or In/NotIn without values, Exists/DoesNotExist with values,
+ * an empty key) fails LabelSelectorAsSelector, and a pod carrying such a term
+ * is routed to the fallback path (on a spot node: every candidate). */
+typedef struct {
+  const int32_t *ns;                                /* [pods.n] interned ObjectMeta.Namespace */
+  const int32_t *label_off, *label_key, *label_val; /* [pods.n+1] ObjectMeta.Labels (keys unique per pod) */
+  const int32_t *anti_off;                          /* [pods.n+1] pods -> required anti-affinity terms */
+  const int32_t *topology_key;                      /* [terms] interned TopologyKey */
+  const int32_t *ns_off, *ns_ids;                   /* [terms+1] Namespaces */
+  const uint8_t *selector_nil;                      /* [terms] LabelSelector == nil: selects nothing */
+  const int32_t *ml_off, *ml_key, *ml_val;          /* [terms+1] MatchLabels */
+  const int32_t *me_off, *me_key, *me_op;           /* [terms+1] MatchExpressions */
+  const int32_t *me_val_off, *me_vals;              /* [exprs+1] their values */
+} sr_pod_affinity;
+
 typedef struct {
   sr_nodes nodes;
   sr_pods  pods;
   int32_t  id_empty;          /* interned id of "" (-1 if never interned) */
   int32_t  id_metadata_name;  /* interned id of "metadata.name" (-1 if never interned) */
   int32_t  id_unschedulable_key; /* interned id of "node.kubernetes.io/unschedulable" (-1 if never interned) */
+  const sr_pod_affinity *pod_affinity; /* NULL: required anti-affinity stays on the fallback path */
 } sr_cluster;
 
 /* ------------------------------------------------------------- NewNodeMap */

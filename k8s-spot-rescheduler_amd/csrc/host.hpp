@@ -37,13 +37,16 @@ struct SpotNode {
   std::vector<TaintRec> taints;
 };
 
-// Mutable part: scheduler NodeInfo.Requested, len(Pods), UsedPorts, and the
-// number of pods carrying required anti-affinity.
+// Mutable part: scheduler NodeInfo.Requested, len(Pods), UsedPorts, the pods
+// themselves (InterPodAffinity matches against them), the number carrying
+// required anti-affinity and, of those, the opaque ones (anti_opaque()).
 struct NodeState {
   int64_t requested[3] = {0, 0, 0};
   int64_t npods = 0;
   int32_t anti = 0;
+  int32_t opaque = 0;
   std::vector<Port> ports;
+  std::vector<int32_t> pods;
 };
 
 }  // namespace sr
@@ -56,6 +59,7 @@ struct sr_snapshot {
   std::vector<sr::NodeState> saved;
   bool forked = false;
   int64_t anti_total = 0;
+  int64_t opaque_total = 0;  // pods whose anti-affinity the encoder cannot read: every candidate falls back
   uint64_t version = 0;  // bumped on every mutation
 };
 
@@ -68,6 +72,15 @@ inline bool add_overflows(int64_t a, int64_t b) {
 }
 
 void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t pos);
+
+// The pod carries required anti-affinity terms.
+inline bool has_anti_terms(const sr_cluster* c, int32_t pod) {
+  return (c->pods.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) ||
+         (c->pod_affinity && c->pod_affinity->anti_off[pod + 1] > c->pod_affinity->anti_off[pod]);
+}
+// Its required anti-affinity is outside the encoded set: no sr_pod_affinity,
+// the flag without terms, or a selector LabelSelectorAsSelector rejects.
+bool anti_opaque(const sr_cluster* c, int32_t pod);
 
 // Class descriptor flags.
 enum : int32_t { CLS_AFF_REQUIRED = 1, CLS_IMPOSSIBLE = 2 };

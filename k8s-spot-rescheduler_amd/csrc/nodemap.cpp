@@ -92,15 +92,44 @@ static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod) {
   st.requested[1] = wrap_add(st.requested[1], P.req_memory[pod]);
   st.requested[2] = wrap_add(st.requested[2], P.req_ephemeral[pod]);
   st.npods += 1;
-  if (P.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) st.anti += 1;
+  if (has_anti_terms(c, pod)) {
+    st.anti += 1;
+    if (anti_opaque(c, pod)) st.opaque += 1;
+  }
+  st.pods.push_back(pod);
   for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i)
     if (P.port_num[i] > 0) st.ports.push_back(Port{P.port_ip[i], P.port_proto[i], P.port_num[i]});
 }
 
+bool anti_opaque(const sr_cluster* c, int32_t pod) {
+  if (!has_anti_terms(c, pod)) return false;
+  const sr_pod_affinity* A = c->pod_affinity;
+  if (!A || A->anti_off[pod] == A->anti_off[pod + 1]) return true;
+  const int32_t e_id = c->id_empty;
+  for (int32_t t = A->anti_off[pod]; t < A->anti_off[pod + 1]; ++t) {
+    if (A->selector_nil[t]) continue;
+    for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; ++i)
+      if (A->ml_key[i] == e_id && e_id != -1) return true;
+    for (int32_t e = A->me_off[t]; e < A->me_off[t + 1]; ++e) {
+      const int32_t nv = A->me_val_off[e + 1] - A->me_val_off[e], op = A->me_op[e];
+      if (A->me_key[e] == e_id && e_id != -1) return true;
+      if (op == SR_OP_IN || op == SR_OP_NOT_IN) {
+        if (nv == 0) return true;
+      } else if (op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) {
+        if (nv != 0) return true;
+      } else {
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
 void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t pos) {
-  const int32_t before = s->state[pos].anti;
+  const int32_t before = s->state[pos].anti, obefore = s->state[pos].opaque;
   state_add_pod(s->state[pos], c, pod);
   s->anti_total += s->state[pos].anti - before;
+  s->opaque_total += s->state[pos].opaque - obefore;
   s->version++;
 }
 
@@ -140,6 +169,7 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
       state_add_pod(s->state[i], c, pod);
     }
     s->anti_total += s->state[i].anti;
+    s->opaque_total += s->state[i].opaque;
   }
   *out = s;
   return SR_OK;
@@ -189,8 +219,11 @@ sr_status sr_snapshot_revert(sr_snapshot* snap) {
   snap->state.swap(snap->saved);
   snap->saved.clear();
   snap->forked = false;
-  snap->anti_total = 0;
-  for (const auto& st : snap->state) snap->anti_total += st.anti;
+  snap->anti_total = snap->opaque_total = 0;
+  for (const auto& st : snap->state) {
+    snap->anti_total += st.anti;
+    snap->opaque_total += st.opaque;
+  }
   snap->version++;
   return SR_OK;
 }

@@ -379,6 +379,7 @@ void sr_synth_view(const sr_synth* s, sr_cluster* c) {
   c->id_empty = 0;
   c->id_metadata_name = 1;
   c->id_unschedulable_key = 2;
+  c->pod_affinity = nullptr;  // the BASELINE configs carry no pod (anti-)affinity
 }
 
 void sr_synth_drain(const sr_synth* s, sr_pod_drain* d) {

@@ -61,9 +61,17 @@ class sr_pods(ctypes.Structure):
                 ("port_off", P32), ("port_proto", P32), ("port_num", P32), ("port_ip", P32)]
 
 
+class sr_pod_affinity(ctypes.Structure):
+    _fields_ = [("ns", P32), ("label_off", P32), ("label_key", P32), ("label_val", P32), ("anti_off", P32),
+                ("topology_key", P32), ("ns_off", P32), ("ns_ids", P32), ("selector_nil", PU8),
+                ("ml_off", P32), ("ml_key", P32), ("ml_val", P32), ("me_off", P32), ("me_key", P32),
+                ("me_op", P32), ("me_val_off", P32), ("me_vals", P32)]
+
+
 class sr_cluster(ctypes.Structure):
     _fields_ = [("nodes", sr_nodes), ("pods", sr_pods), ("id_empty", ctypes.c_int32),
-                ("id_metadata_name", ctypes.c_int32), ("id_unschedulable_key", ctypes.c_int32)]
+                ("id_metadata_name", ctypes.c_int32), ("id_unschedulable_key", ctypes.c_int32),
+                ("pod_affinity", ctypes.POINTER(sr_pod_affinity))]
 
 
 class sr_node_label(ctypes.Structure):
@@ -152,6 +160,14 @@ def make_cluster_struct(A) -> sr_cluster:
     c.id_empty = A["id_empty"]
     c.id_metadata_name = A["id_metadata_name"]
     c.id_unschedulable_key = A["id_unschedulable_key"]
+    if A.get("pa_ns") is not None:
+        pa = sr_pod_affinity()
+        for f in ("ns", "label_off", "label_key", "label_val", "anti_off", "topology_key", "ns_off", "ns_ids",
+                  "ml_off", "ml_key", "ml_val", "me_off", "me_key", "me_op", "me_val_off", "me_vals"):
+            setattr(pa, f, ptr(A["pa_" + f], P32))
+        pa.selector_nil = ptr(A["pa_selector_nil"], PU8)
+        c._pod_affinity = pa  # keeps the struct alive as long as the cluster struct
+        c.pod_affinity = ctypes.pointer(pa)
     return c
 
 

@@ -77,6 +77,26 @@ class NodeSelectorTerm:
 
 
 @dataclass
+class LabelSelectorRequirement:
+    key: str
+    operator: str
+    values: List[str] = field(default_factory=list)
+
+
+@dataclass
+class LabelSelector:
+    match_labels: Dict[str, str] = field(default_factory=dict)
+    match_expressions: List[LabelSelectorRequirement] = field(default_factory=list)
+
+
+@dataclass
+class PodAffinityTerm:
+    topology_key: str
+    label_selector: Optional[LabelSelector] = None   # None = nil: selects nothing
+    namespaces: List[str] = field(default_factory=list)  # [] = the term's own pod's namespace
+
+
+@dataclass
 class OwnerReference:
     kind: str
     name: str = ""
@@ -103,7 +123,9 @@ class Pod:
     # features outside the encoded predicate set
     has_pvc: bool = False
     required_pod_affinity: bool = False
-    required_pod_anti_affinity: bool = False
+    required_pod_anti_affinity: bool = False  # opaque anti-affinity (no terms given): fallback
+    # Affinity.PodAntiAffinity.RequiredDuringSchedulingIgnoredDuringExecution (encoded)
+    pod_anti_affinity: Optional[List[PodAffinityTerm]] = None
     hard_topology_spread: bool = False
     # drain attributes (cluster-autoscaler utils/drain)
     phase: str = "Running"                    # Status.Phase
@@ -206,7 +228,7 @@ def pod_flags(pod: Pod) -> int:
         f |= capi.SR_POD_DAEMONSET_CONTROLLER
     if MIRROR_ANNOTATION in pod.annotations:
         f |= capi.SR_POD_MIRROR
-    if pod.required_pod_anti_affinity:
+    if pod.required_pod_anti_affinity or pod.pod_anti_affinity:
         f |= capi.SR_POD_HAS_REQ_ANTI_AFFINITY
     conts = list(pod.containers) + list(pod.init_containers) + ([pod.overhead] if pod.overhead else [])
     if any(c.scalar for c in conts):
@@ -215,7 +237,7 @@ def pod_flags(pod: Pod) -> int:
         f |= capi.SR_POD_FB_VOLUMES
     if pod.hard_topology_spread:
         f |= capi.SR_POD_FB_TOPOLOGY_SPREAD
-    if pod.required_pod_affinity or pod.required_pod_anti_affinity:
+    if pod.required_pod_affinity or (pod.required_pod_anti_affinity and not pod.pod_anti_affinity):
         f |= capi.SR_POD_FB_POD_AFFINITY
     return f
 
@@ -231,6 +253,41 @@ class EncodedCluster:
     @property
     def ptr(self):
         return ctypes.byref(self.struct)
+
+
+def _encode_pod_affinity(pods: List[Pod], it: Interner) -> dict:
+    """sr_pod_affinity arrays: namespaces, labels and required anti-affinity terms."""
+    ns, lo, lk, lv, ao = [], [0], [], [], [0]
+    tk, nso, nsi, nil, mlo, mlk, mlv, meo, mek, mep, mevo, mev = [], [0], [], [], [0], [], [], [0], [], [], [0], []
+    for p in pods:
+        ns.append(it.id(p.namespace))
+        for k, v in p.labels.items():
+            lk.append(it.id(k))
+            lv.append(it.id(v))
+        lo.append(len(lk))
+        for t in (p.pod_anti_affinity or []):
+            tk.append(it.id(t.topology_key))
+            nsi.extend(it.id(x) for x in t.namespaces)
+            nso.append(len(nsi))
+            sel = t.label_selector
+            nil.append(1 if sel is None else 0)
+            for k, v in (sel.match_labels.items() if sel else []):
+                mlk.append(it.id(k))
+                mlv.append(it.id(v))
+            mlo.append(len(mlk))
+            for r in (sel.match_expressions if sel else []):
+                mek.append(it.id(r.key))
+                mep.append(SEL_OPS.get(r.operator, capi.SR_OP_OTHER) if r.operator not in ("Gt", "Lt")
+                           else capi.SR_OP_OTHER)
+                mev.extend(it.id(v) for v in r.values)
+                mevo.append(len(mev))
+            meo.append(len(mek))
+        ao.append(len(tk))
+    return dict(pa_ns=_i32(ns), pa_label_off=_i32(lo), pa_label_key=_i32(lk), pa_label_val=_i32(lv),
+                pa_anti_off=_i32(ao), pa_topology_key=_i32(tk), pa_ns_off=_i32(nso), pa_ns_ids=_i32(nsi),
+                pa_selector_nil=_u8(nil), pa_ml_off=_i32(mlo), pa_ml_key=_i32(mlk), pa_ml_val=_i32(mlv),
+                pa_me_off=_i32(meo), pa_me_key=_i32(mek), pa_me_op=_i32(mep), pa_me_val_off=_i32(mevo),
+                pa_me_vals=_i32(mev))
 
 
 def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Interner] = None,
@@ -325,6 +382,7 @@ def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Intern
              tol_off=_i32(tolo), tol_key=_i32(tolk), tol_op=_i32(tolop), tol_val=_i32(tolv),
              tol_eff=_i32(tole), port_off=_i32(po), port_proto=_i32(pp), port_num=_i32(pnum),
              port_ip=_i32(pip))
+    A.update(_encode_pod_affinity(pods, it))
     A["n_nodes"] = len(nodes)
     A["n_pods"] = len(pods)
     A["id_empty"] = e

@@ -400,9 +400,12 @@ typedef struct {
 typedef struct {
   int64_t req[3];
   int32_t npods;
-  int32_t anti;
+  int32_t anti;  /* pods with SR_POD_HAS_REQ_ANTI_AFFINITY */
+  int32_t opaque; /* of those, pods whose terms the planner cannot read (o_anti_opaque) */
   int32_t nports, cap;
   o_port *ports;
+  int32_t nlist, lcap; /* NodeInfo.Pods (InterPodAffinity matches against them) */
+  int32_t *list;
 } o_state;
 
 struct oracle_snapshot {
@@ -412,7 +415,32 @@ struct oracle_snapshot {
   o_state *saved;
   int32_t forked;
   int32_t anti_total;
+  int32_t opaque_total;
 };
+
+/* A pod whose required anti-affinity the encoded set cannot evaluate: no
+ * sr_pod_affinity at all, the flag without terms, or a term whose label
+ * selector fails LabelSelectorAsSelector [upstream apimachinery
+ * metav1.LabelSelectorAsSelector: In/NotIn need values, Exists/DoesNotExist
+ * take none, other operators and empty keys are errors]. */
+static int o_anti_opaque(const sr_cluster *c, int32_t pod) {
+  if (!(c->pods.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY)) return 0;
+  const sr_pod_affinity *A = c->pod_affinity;
+  if (!A || A->anti_off[pod] == A->anti_off[pod + 1]) return 1;
+  for (int32_t t = A->anti_off[pod]; t < A->anti_off[pod + 1]; t++) {
+    if (A->selector_nil[t]) continue;
+    for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; i++)
+      if (A->ml_key[i] == c->id_empty && c->id_empty != -1) return 1;
+    for (int32_t e = A->me_off[t]; e < A->me_off[t + 1]; e++) {
+      int32_t nv = A->me_val_off[e + 1] - A->me_val_off[e], op = A->me_op[e];
+      if (A->me_key[e] == c->id_empty && c->id_empty != -1) return 1;
+      if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) return 1;
+      if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) return 1;
+      if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST) return 1;
+    }
+  }
+  return 0;
+}
 
 static int64_t o_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 
@@ -422,7 +450,15 @@ static void o_state_add_pod(o_state *st, const sr_cluster *c, int32_t pod) {
   st->req[1] = o_add(st->req[1], P->req_memory[pod]);
   st->req[2] = o_add(st->req[2], P->req_ephemeral[pod]);
   st->npods++;
-  if (P->flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) st->anti++;
+  if ((P->flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) ||
+      (c->pod_affinity && c->pod_affinity->anti_off[pod + 1] > c->pod_affinity->anti_off[pod]))
+    st->anti++;
+  if (o_anti_opaque(c, pod)) st->opaque++;
+  if (st->nlist == st->lcap) {
+    st->lcap = st->lcap ? st->lcap * 2 : 8;
+    st->list = (int32_t *)realloc(st->list, sizeof(int32_t) * (size_t)st->lcap);
+  }
+  st->list[st->nlist++] = pod;
   for (int32_t i = P->port_off[pod]; i < P->port_off[pod + 1]; i++) {
     if (P->port_num[i] <= 0) continue; /* HostPortInfo.Add ignores port <= 0 */
     if (st->nports == st->cap) {
@@ -449,13 +485,17 @@ oracle_snapshot *oracle_snapshot_create(const sr_cluster *c, const int32_t *spot
     for (int32_t j = node_pod_off[node]; j < node_pod_off[node + 1]; j++)
       o_state_add_pod(&s->st[i], c, node_pod_idx[j]);
     s->anti_total += s->st[i].anti;
+    s->opaque_total += s->st[i].opaque;
   }
   return s;
 }
 
 static void o_free_states(o_state *st, int32_t n) {
   if (!st) return;
-  for (int32_t i = 0; i < n; i++) free(st[i].ports);
+  for (int32_t i = 0; i < n; i++) {
+    free(st[i].ports);
+    free(st[i].list);
+  }
   free(st);
 }
 
@@ -467,6 +507,11 @@ static o_state *o_copy_states(const o_state *src, int32_t n) {
     if (src[i].nports) {
       dst[i].ports = (o_port *)malloc(sizeof(o_port) * (size_t)src[i].cap);
       memcpy(dst[i].ports, src[i].ports, sizeof(o_port) * (size_t)src[i].nports);
+    }
+    dst[i].list = NULL;
+    if (src[i].nlist) {
+      dst[i].list = (int32_t *)malloc(sizeof(int32_t) * (size_t)src[i].lcap);
+      memcpy(dst[i].list, src[i].list, sizeof(int32_t) * (size_t)src[i].nlist);
     }
   }
   return dst;
@@ -481,9 +526,10 @@ void oracle_snapshot_destroy(oracle_snapshot *s) {
 }
 
 void oracle_snapshot_add_pod(oracle_snapshot *s, const sr_cluster *c, int32_t pod, int32_t pos) {
-  int32_t before = s->st[pos].anti;
+  int32_t before = s->st[pos].anti, obefore = s->st[pos].opaque;
   o_state_add_pod(&s->st[pos], c, pod);
   s->anti_total += s->st[pos].anti - before;
+  s->opaque_total += s->st[pos].opaque - obefore;
 }
 
 int32_t oracle_snapshot_fork(oracle_snapshot *s) {
@@ -499,8 +545,11 @@ int32_t oracle_snapshot_revert(oracle_snapshot *s) {
   s->st = s->saved;
   s->saved = NULL;
   s->forked = 0;
-  s->anti_total = 0;
-  for (int32_t i = 0; i < s->n; i++) s->anti_total += s->st[i].anti;
+  s->anti_total = s->opaque_total = 0;
+  for (int32_t i = 0; i < s->n; i++) {
+    s->anti_total += s->st[i].anti;
+    s->opaque_total += s->st[i].opaque;
+  }
   return SR_OK;
 }
 
@@ -673,11 +722,100 @@ static int o_resources_ok(const o_state *st, const sr_cluster *c, int32_t pod, i
   return 1;
 }
 
+/* labels.Selector.Matches over a pod's labels for term t (MatchLabels are
+ * Equals requirements; MatchExpressions In / NotIn / Exists / DoesNotExist;
+ * a nil selector selects nothing, an empty one everything). */
+static int o_pod_label(const sr_cluster *c, int32_t pod, int32_t key, int32_t *val) {
+  const sr_pod_affinity *A = c->pod_affinity;
+  for (int32_t i = A->label_off[pod]; i < A->label_off[pod + 1]; i++)
+    if (A->label_key[i] == key) {
+      *val = A->label_val[i];
+      return 1;
+    }
+  return 0;
+}
+
+static int o_selector_matches(const sr_cluster *c, int32_t t, int32_t pod) {
+  const sr_pod_affinity *A = c->pod_affinity;
+  if (A->selector_nil[t]) return 0;
+  for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; i++) {
+    int32_t v;
+    if (!o_pod_label(c, pod, A->ml_key[i], &v) || v != A->ml_val[i]) return 0;
+  }
+  for (int32_t e = A->me_off[t]; e < A->me_off[t + 1]; e++) {
+    int32_t v;
+    int has = o_pod_label(c, pod, A->me_key[e], &v);
+    int32_t lo = A->me_val_off[e], hi = A->me_val_off[e + 1];
+    int ok;
+    switch (A->me_op[e]) {
+      case SR_OP_IN: ok = has && o_in_values(A->me_vals, lo, hi, v); break;
+      case SR_OP_NOT_IN: ok = !has || !o_in_values(A->me_vals, lo, hi, v); break;
+      case SR_OP_EXISTS: ok = has; break;
+      case SR_OP_DOES_NOT_EXIST: ok = !has; break;
+      default: ok = 0; break;
+    }
+    if (!ok) return 0;
+  }
+  return 1;
+}
+
+/* schedutil.PodMatchesTermsNamespaceAndSelector for the term t of `owner`
+ * against `target`: namespace in the term's Namespaces (none: the owner's
+ * namespace, getNamespacesFromPodAffinityTerm) and the selector matches. */
+static int o_term_matches(const sr_cluster *c, int32_t owner, int32_t t, int32_t target) {
+  const sr_pod_affinity *A = c->pod_affinity;
+  int32_t tns = A->ns[target];
+  if (A->ns_off[t] == A->ns_off[t + 1]) {
+    if (tns != A->ns[owner]) return 0;
+  } else if (!o_in_values(A->ns_ids, A->ns_off[t], A->ns_off[t + 1], tns)) {
+    return 0;
+  }
+  return o_selector_matches(c, t, target);
+}
+
+/* InterPodAffinity.Filter, required anti-affinity part [upstream k8s v1.19.2
+ * plugins/interpodaffinity/filtering.go]: PreFilter counts topology pairs
+ * (key, value of the existing pod's node) for (1) every existing pod's
+ * anti-affinity term that matches the incoming pod and (2) every anti-affinity
+ * term of the incoming pod that matches an existing pod; Filter rejects a node
+ * whose value for such a pair's key equals the pair's value.  Existing pods =
+ * NodeInfo.Pods of every snapshot node.  (Required pod *affinity* stays on the
+ * fallback path.) */
+static int o_interpod_ok(const o_state *st, const int32_t *node, int32_t n, const sr_cluster *c, int32_t pod,
+                         int32_t nnode) {
+  const sr_pod_affinity *A = c->pod_affinity;
+  if (!A || A->anti_off[c->pods.n] == 0) return 1; /* no term anywhere */
+  for (int32_t m = 0; m < n; m++) {
+    if (st[m].anti == 0) continue;
+    for (int32_t j = 0; j < st[m].nlist; j++) {
+      int32_t e = st[m].list[j];
+      for (int32_t t = A->anti_off[e]; t < A->anti_off[e + 1]; t++) {
+        int32_t vm, vn;
+        if (!o_node_label(c, node[m], A->topology_key[t], &vm)) continue;
+        if (!o_node_label(c, nnode, A->topology_key[t], &vn) || vn != vm) continue;
+        if (o_term_matches(c, e, t, pod)) return 0;
+      }
+    }
+  }
+  for (int32_t t = A->anti_off[pod]; t < A->anti_off[pod + 1]; t++) {
+    int32_t vn;
+    if (!o_node_label(c, nnode, A->topology_key[t], &vn)) continue;
+    for (int32_t m = 0; m < n; m++) {
+      int32_t vm;
+      if (!o_node_label(c, node[m], A->topology_key[t], &vm) || vm != vn) continue;
+      for (int32_t j = 0; j < st[m].nlist; j++)
+        if (o_term_matches(c, pod, t, st[m].list[j])) return 0;
+    }
+  }
+  return 1;
+}
+
 int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c, int32_t pod) {
   const sr_pods *P = &c->pods;
   if (P->flags[pod] & SR_POD_FB_MASK) return 1;
-  /* an existing pod's required anti-affinity may select the incoming pod (InterPodAffinity) */
-  if (s->anti_total > 0) return 1;
+  /* an existing pod's required anti-affinity may select the incoming pod:
+   * opaque terms (o_anti_opaque) keep every pod on the fallback path */
+  if (s->opaque_total > 0 || o_anti_opaque(c, pod)) return 1;
   if (P->aff_required[pod])
     for (int32_t t = P->term_off[pod]; t < P->term_off[pod + 1]; t++)
       for (int32_t e = P->term_expr_off[t]; e < P->term_expr_off[t + 1]; e++)
@@ -685,20 +823,24 @@ int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c,
   return 0;
 }
 
-static int o_check(const o_state *st, const sr_cluster *c, int32_t pod, int32_t node) {
+static int o_check(const o_state *st, const int32_t *node, int32_t n, const sr_cluster *c, int32_t pod,
+                   int32_t pos) {
   /* Filter order of the default provider; the result is their conjunction. */
-  if (!o_unschedulable_ok(c, pod, node)) return 0;
-  if (!o_resources_ok(st, c, pod, node)) return 0;
+  const o_state *sp = &st[pos];
+  int32_t nd = node[pos];
+  if (!o_unschedulable_ok(c, pod, nd)) return 0;
+  if (!o_resources_ok(sp, c, pod, nd)) return 0;
   /* NodeName: passes, findSpotNodeForPod clears Spec.NodeName (rescheduler.go:341) */
-  if (!o_ports_ok(st, c, pod)) return 0;
-  if (!o_affinity_ok(c, pod, node)) return 0;
-  if (!o_taints_ok(c, pod, node)) return 0;
+  if (!o_ports_ok(sp, c, pod)) return 0;
+  if (!o_affinity_ok(c, pod, nd)) return 0;
+  if (!o_taints_ok(c, pod, nd)) return 0;
+  if (!o_interpod_ok(st, node, n, c, pod, nd)) return 0;
   return 1;
 }
 
 int32_t oracle_check_predicates(const oracle_snapshot *s, const sr_cluster *c, int32_t pod, int32_t pos) {
   if (oracle_pod_needs_fallback(s, c, pod)) return -1;
-  return o_check(&s->st[pos], c, pod, s->node[pos]);
+  return o_check(s->st, s->node, s->n, c, pod, pos);
 }
 
 /* findSpotNodeForPod (rescheduler.go:338-353) */
@@ -706,7 +848,7 @@ static int32_t o_find(const o_state *st, const int32_t *node, int32_t n, const s
                       int32_t pod, uint64_t *checks) {
   for (int32_t pos = 0; pos < n; pos++) {
     if (checks) (*checks)++;
-    if (o_check(&st[pos], c, pod, node[pos])) return pos;
+    if (o_check(st, node, n, c, pod, pos)) return pos;
   }
   return -1;
 }
@@ -737,7 +879,7 @@ int32_t oracle_can_drain_node(oracle_snapshot *s, const sr_cluster *c, const int
 typedef struct {
   int32_t pos;
   int64_t req[3];
-  int32_t npods, nports, anti;
+  int32_t npods, nports, anti, opaque, nlist;
 } o_undo;
 
 /* Evaluate one candidate from the base state `st` (Fork), then restore it (Revert). */
@@ -759,6 +901,8 @@ static int32_t o_eval_candidate(o_state *st, const int32_t *node, int32_t n, con
     u->npods = st[pos].npods;
     u->nports = st[pos].nports;
     u->anti = st[pos].anti;
+    u->opaque = st[pos].opaque;
+    u->nlist = st[pos].nlist;
     o_state_add_pod(&st[pos], c, pods[i]);
   }
   while (nu > 0) { /* Revert, newest first */
@@ -767,6 +911,8 @@ static int32_t o_eval_candidate(o_state *st, const int32_t *node, int32_t n, con
     st[u->pos].npods = u->npods;
     st[u->pos].nports = u->nports;
     st[u->pos].anti = u->anti;
+    st[u->pos].opaque = u->opaque;
+    st[u->pos].nlist = u->nlist;
   }
   return status;
 }
