@@ -1,0 +1,327 @@
+// antiaff.cpp — required inter-pod anti-affinity for the encoder.
+//
+// InterPodAffinity.Filter of k8s v1.19.2 [upstream
+// plugins/interpodaffinity/filtering.go], anti-affinity part: a pod P is
+// refused on node n when (1) an existing pod E on a node m carries a term t
+// that selects P (E's term namespaces, selector on P's labels) and m, n carry
+// the same value of t's topology key, or (2) P carries a term t that selects
+// an existing pod E on such a node m.  "Existing" = NodeInfo.Pods of every
+// snapshot node, which during canDrainNode includes the candidate's pods
+// already placed (rescheduler.go:366).
+//
+// Encoding:
+//  - static part, against the base snapshot: per distinct term t two node
+//    sets, DA(t) = nodes sharing a t-domain with a base pod that has t, and
+//    DB(t) = nodes sharing a t-domain with a base pod that t selects; a pod
+//    ANDs NOT DA(t) for every t it matches and NOT DB(t) for every t it has
+//    (atoms of its class program, so they land in its S row);
+//  - dynamic part, between the pods of one candidate: a term through which
+//    two of its pods interact must have a node-local topology key (every spot
+//    node carries it, values pairwise distinct, e.g. kubernetes.io/hostname);
+//    it then gets a pair of state bits (A: a pod having t is here, B: a pod
+//    t selects is here).  A pod sets A for its terms and B for the terms
+//    selecting it; it conflicts with a node whose state holds B for its
+//    terms or A for the terms selecting it -- the pair-swapped image of what
+//    it sets.  K2 keeps these bits with the host-port bits.  Interaction
+//    through any other key routes the candidate to the fallback path.
+#include <algorithm>
+#include <climits>
+#include <cstring>
+
+#include "host.hpp"
+#include "pool.hpp"
+#include "worddict.hpp"
+
+namespace sr {
+
+namespace {
+
+struct Expr {
+  int32_t key, op;
+  std::vector<int32_t> vals;  // sorted
+};
+
+// One distinct term, resolved against its owner (namespaces defaulted).
+struct Term {
+  int32_t tk = -1;
+  std::vector<int32_t> ns;  // sorted
+  bool nil = false;
+  std::vector<std::pair<int32_t, int32_t>> ml;  // sorted by key
+  std::vector<Expr> me;
+};
+
+void term_words(const sr_cluster* c, int32_t owner, int32_t t, std::vector<int32_t>& out) {
+  const sr_pod_affinity& A = *c->pod_affinity;
+  out.clear();
+  out.push_back(A.topology_key[t]);
+  const size_t ns_at = out.size();
+  out.push_back(0);
+  if (A.ns_off[t] == A.ns_off[t + 1]) {
+    out.push_back(A.ns[owner]);  // getNamespacesFromPodAffinityTerm: the owner's namespace
+  } else {
+    out.insert(out.end(), A.ns_ids + A.ns_off[t], A.ns_ids + A.ns_off[t + 1]);
+    std::sort(out.begin() + ns_at + 1, out.end());
+    out.erase(std::unique(out.begin() + ns_at + 1, out.end()), out.end());
+  }
+  out[ns_at] = static_cast<int32_t>(out.size() - ns_at - 1);
+  out.push_back(A.selector_nil[t] ? 1 : 0);
+  if (A.selector_nil[t]) return;
+  std::vector<std::pair<int32_t, int32_t>> ml;
+  for (int32_t i = A.ml_off[t]; i < A.ml_off[t + 1]; ++i) ml.emplace_back(A.ml_key[i], A.ml_val[i]);
+  std::sort(ml.begin(), ml.end());
+  out.push_back(static_cast<int32_t>(ml.size()));
+  for (const auto& kv : ml) {
+    out.push_back(kv.first);
+    out.push_back(kv.second);
+  }
+  out.push_back(A.me_off[t + 1] - A.me_off[t]);
+  for (int32_t e = A.me_off[t]; e < A.me_off[t + 1]; ++e) {
+    out.push_back(A.me_key[e]);
+    out.push_back(A.me_op[e]);
+    const size_t at = out.size();
+    out.push_back(0);
+    out.insert(out.end(), A.me_vals + A.me_val_off[e], A.me_vals + A.me_val_off[e + 1]);
+    std::sort(out.begin() + at + 1, out.end());
+    out.erase(std::unique(out.begin() + at + 1, out.end()), out.end());
+    out[at] = static_cast<int32_t>(out.size() - at - 1);
+  }
+}
+
+Term parse_term(const int32_t* w) {
+  Term t;
+  size_t i = 0;
+  t.tk = w[i++];
+  const int32_t nns = w[i++];
+  t.ns.assign(w + i, w + i + nns);
+  i += nns;
+  t.nil = w[i++] != 0;
+  if (t.nil) return t;
+  const int32_t nml = w[i++];
+  for (int32_t k = 0; k < nml; ++k, i += 2) t.ml.emplace_back(w[i], w[i + 1]);
+  const int32_t nme = w[i++];
+  for (int32_t k = 0; k < nme; ++k) {
+    Expr e;
+    e.key = w[i++];
+    e.op = w[i++];
+    const int32_t nv = w[i++];
+    e.vals.assign(w + i, w + i + nv);
+    i += nv;
+    t.me.push_back(std::move(e));
+  }
+  return t;
+}
+
+bool pod_label(const sr_pod_affinity& A, int32_t pod, int32_t key, int32_t* val) {
+  for (int32_t i = A.label_off[pod]; i < A.label_off[pod + 1]; ++i)
+    if (A.label_key[i] == key) {
+      *val = A.label_val[i];
+      return true;
+    }
+  return false;
+}
+
+// schedutil.PodMatchesTermsNamespaceAndSelector: namespace, then
+// labels.Selector.Matches (MatchLabels = Equals; In / NotIn / Exists /
+// DoesNotExist; nil selects nothing, empty everything).
+bool term_selects(const Term& t, const sr_pod_affinity& A, int32_t pod) {
+  if (!std::binary_search(t.ns.begin(), t.ns.end(), A.ns[pod])) return false;
+  if (t.nil) return false;
+  int32_t v;
+  for (const auto& kv : t.ml)
+    if (!pod_label(A, pod, kv.first, &v) || v != kv.second) return false;
+  for (const Expr& e : t.me) {
+    const bool has = pod_label(A, pod, e.key, &v);
+    bool ok;
+    switch (e.op) {
+      case SR_OP_IN: ok = has && std::binary_search(e.vals.begin(), e.vals.end(), v); break;
+      case SR_OP_NOT_IN: ok = !has || !std::binary_search(e.vals.begin(), e.vals.end(), v); break;
+      case SR_OP_EXISTS: ok = has; break;
+      default: ok = !has; break;  // DoesNotExist (anything else is opaque: never encoded)
+    }
+    if (!ok) return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
+                  std::vector<int32_t>& status, AntiTerms* out) {
+  AntiTerms& at = *out;
+  at = AntiTerms{};
+  const sr_pod_affinity* PA = c->pod_affinity;
+  const int32_t nc = cands->n_cand;
+  const int32_t n_flat = nc > 0 ? cands->cand_pod_off[nc] : 0;
+  at.pod_off.assign(static_cast<size_t>(n_flat) + 1, 0);
+  if (!PA || PA->anti_off[c->pods.n] == 0) return;  // no term anywhere in the cluster
+  const sr_pod_affinity& A = *PA;
+  const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
+
+  // ---- distinct terms: base pods (every snapshot node) and pending candidates
+  WordDict dict;
+  std::vector<int32_t> words;
+  std::vector<std::pair<int32_t, int32_t>> base_has;  // (node, term)
+  for (int32_t n = 0; n < n_spot; ++n)
+    for (int32_t e : snap->state[n].pods)
+      for (int32_t t = A.anti_off[e]; t < A.anti_off[e + 1]; ++t) {
+        term_words(c, e, t, words);
+        base_has.emplace_back(n, dict.intern(words));
+      }
+  std::vector<std::vector<int32_t>> has(static_cast<size_t>(n_flat));  // term ids per flat candidate pod
+  for (int32_t i = 0; i < nc; ++i) {
+    if (status[i] != STATUS_PENDING) continue;
+    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+      const int32_t pod = cands->cand_pods[j];
+      for (int32_t t = A.anti_off[pod]; t < A.anti_off[pod + 1]; ++t) {
+        term_words(c, pod, t, words);
+        has[j].push_back(dict.intern(words));
+      }
+      std::sort(has[j].begin(), has[j].end());
+      has[j].erase(std::unique(has[j].begin(), has[j].end()), has[j].end());
+    }
+  }
+  const int32_t T = static_cast<int32_t>(dict.size());
+  if (T == 0) return;
+  at.active = true;
+  at.n_terms = T;
+  std::vector<Term> terms(static_cast<size_t>(T));
+  for (int32_t t = 0; t < T; ++t) terms[t] = parse_term(dict.data(t));
+
+  // ---- topology values of every spot node per term; node-local keys
+  std::vector<int32_t> tval(static_cast<size_t>(T) * n_spot, INT_MIN);
+  at.node_local.assign(static_cast<size_t>(T), 0);
+  parallel_for(static_cast<size_t>(T), 1, [&](size_t lo, size_t hi) {
+    std::vector<int32_t> seen;
+    for (size_t t = lo; t < hi; ++t) {
+      bool all = true;
+      seen.clear();
+      for (int32_t n = 0; n < n_spot; ++n) {
+        for (const auto& kv : snap->nodes[n].labels)
+          if (kv.first == terms[t].tk) {
+            tval[t * n_spot + n] = kv.second;
+            break;
+          }
+        if (tval[t * n_spot + n] == INT_MIN) all = false;
+        else seen.push_back(tval[t * n_spot + n]);
+      }
+      std::sort(seen.begin(), seen.end());
+      at.node_local[t] = all && std::adjacent_find(seen.begin(), seen.end()) == seen.end();
+    }
+  });
+
+  // ---- domains of the base pods: SA(t) values hosting a pod that has t,
+  // SB(t) values hosting a pod t selects
+  std::vector<std::vector<int32_t>> sa(static_cast<size_t>(T)), sb(static_cast<size_t>(T));
+  for (const auto& nt : base_has) {
+    const int32_t v = tval[static_cast<size_t>(nt.second) * n_spot + nt.first];
+    if (v != INT_MIN) sa[nt.second].push_back(v);
+  }
+  parallel_for(static_cast<size_t>(T), 1, [&](size_t lo, size_t hi) {
+    for (size_t t = lo; t < hi; ++t)
+      for (int32_t n = 0; n < n_spot; ++n) {
+        const int32_t v = tval[t * n_spot + n];
+        if (v == INT_MIN) continue;
+        for (int32_t e : snap->state[n].pods)
+          if (term_selects(terms[t], A, e)) {
+            sb[t].push_back(v);
+            break;
+          }
+      }
+  });
+  at.da.assign(static_cast<size_t>(T) * Wp, 0);
+  at.db.assign(static_cast<size_t>(T) * Wp, 0);
+  at.da_any.assign(static_cast<size_t>(T), 0);
+  at.db_any.assign(static_cast<size_t>(T), 0);
+  for (int32_t t = 0; t < T; ++t) {
+    for (auto* s : {&sa[t], &sb[t]}) {
+      std::sort(s->begin(), s->end());
+      s->erase(std::unique(s->begin(), s->end()), s->end());
+    }
+    for (int32_t n = 0; n < n_spot; ++n) {
+      const int32_t v = tval[static_cast<size_t>(t) * n_spot + n];
+      if (v == INT_MIN) continue;
+      if (std::binary_search(sa[t].begin(), sa[t].end(), v)) {
+        at.da[static_cast<size_t>(t) * Wp + (n >> 6)] |= 1ull << (n & 63);
+        at.da_any[t] = 1;
+      }
+      if (std::binary_search(sb[t].begin(), sb[t].end(), v)) {
+        at.db[static_cast<size_t>(t) * Wp + (n >> 6)] |= 1ull << (n & 63);
+        at.db_any[t] = 1;
+      }
+    }
+  }
+
+  // ---- per pending candidate pod: ids t << 1 (t selects it) | t << 1 | 1 (it has t)
+  std::vector<std::vector<int32_t>> ids(static_cast<size_t>(n_flat));
+  parallel_for(static_cast<size_t>(nc), 16, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      if (status[i] != STATUS_PENDING) continue;
+      for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+        const int32_t pod = cands->cand_pods[j];
+        std::vector<int32_t>& v = ids[j];
+        for (int32_t t = 0; t < T; ++t)
+          if (term_selects(terms[t], A, pod)) v.push_back(t << 1);
+        for (int32_t t : has[j]) v.push_back(t << 1 | 1);
+        std::sort(v.begin(), v.end());
+      }
+    }
+  });
+
+  // ---- interactions inside each candidate: terms one pod has and another
+  // pod matches.  Node-local ones get a bit pair (first come, at most 32);
+  // any other interaction routes the candidate to the fallback path.
+  at.pair_of.assign(static_cast<size_t>(T), -1);
+  std::vector<int32_t> nh(static_cast<size_t>(T)), nm(static_cast<size_t>(T)), nb(static_cast<size_t>(T));
+  std::vector<int32_t> touched;
+  for (int32_t i = 0; i < nc; ++i) {
+    if (status[i] != STATUS_PENDING) continue;
+    touched.clear();
+    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+      const std::vector<int32_t>& v = ids[j];
+      for (size_t k = 0; k < v.size(); ++k) {
+        const int32_t t = v[k] >> 1;
+        if (nh[t] == 0 && nm[t] == 0) touched.push_back(t);
+        if (v[k] & 1) {
+          ++nh[t];
+          if (k > 0 && v[k - 1] == (t << 1)) ++nb[t];  // sorted: "selects" precedes "has"
+        } else {
+          ++nm[t];
+        }
+      }
+    }
+    bool fb = false;
+    std::vector<int32_t> need;
+    for (int32_t t : touched) {
+      const bool interacts = nh[t] >= 1 && nm[t] >= 1 && !(nh[t] == 1 && nm[t] == 1 && nb[t] == 1);
+      if (interacts) {
+        if (!at.node_local[t]) fb = true;
+        else if (at.pair_of[t] < 0) need.push_back(t);
+      }
+      nh[t] = nm[t] = nb[t] = 0;
+    }
+    if (!fb && at.n_pairs + static_cast<int32_t>(need.size()) > 32) fb = true;
+    if (fb) {
+      status[i] = SR_CAND_FALLBACK;
+      continue;
+    }
+    for (int32_t t : need) at.pair_of[t] = at.n_pairs++;
+  }
+
+  // ---- CSR of the ids; base pair bits per node
+  for (int32_t j = 0; j < n_flat; ++j) at.pod_off[j + 1] = at.pod_off[j] + static_cast<int32_t>(ids[j].size());
+  at.pod_ids.reserve(static_cast<size_t>(at.pod_off[n_flat]));
+  for (int32_t j = 0; j < n_flat; ++j) at.pod_ids.insert(at.pod_ids.end(), ids[j].begin(), ids[j].end());
+  at.base_bits.assign(static_cast<size_t>(n_spot), 0);
+  for (int32_t t = 0; t < T; ++t) {
+    const int32_t p = at.pair_of[t];
+    if (p < 0) continue;
+    for (int32_t n = 0; n < n_spot; ++n) {
+      const size_t wi = static_cast<size_t>(t) * Wp + (n >> 6);
+      const uint64_t bit = 1ull << (n & 63);
+      if (at.da[wi] & bit) at.base_bits[n] |= 1ull << (2 * p);
+      if (at.db[wi] & bit) at.base_bits[n] |= 1ull << (2 * p + 1);
+    }
+  }
+}
+
+}  // namespace sr

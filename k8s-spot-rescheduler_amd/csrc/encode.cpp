@@ -197,7 +197,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
           if (P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT) return true;
     for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i)
       if (P.port_ip[i] != -1 && P.port_num[i] > 0) return true;  // specific hostIP
-    return false;
+    return anti_opaque(c, pod);  // required anti-affinity the encoded set cannot read
   };
   for (int32_t i = 0; i < nc; ++i) {
     if (cands->cand_pod_off[i + 1] < cands->cand_pod_off[i]) {
@@ -217,14 +217,22 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
         w->status_host[i] = SR_CAND_EMPTY;
         continue;
       }
-      bool fb = snap->anti_total > 0 || (e - b) > MAX_CAND_PODS;
+      // an existing pod's opaque anti-affinity may select any incoming pod
+      bool fb = (c->pod_affinity ? snap->opaque_total : snap->anti_total) > 0 || (e - b) > MAX_CAND_PODS;
       for (int32_t j = b; j < e && !fb; ++j) fb = pod_fallback(cands->cand_pods[j]);
       if (fb) w->status_host[i] = SR_CAND_FALLBACK;
     }
   });
 
   phase(8);
-  // ---- host-port dictionary: (protocol, port) pairs of active pods, <= 64
+  // ---- required pod anti-affinity: static node sets, state-bit pairs and
+  // the candidates it sends to the fallback path (antiaff.cpp)
+  AntiTerms anti;
+  analyse_anti(snap, c, cands, w->Wp, w->status_host, &anti);
+  const int32_t bit_shift = 2 * anti.n_pairs;  // host-port bits sit above the pairs
+  w->swap_mask = bit_shift >= 64 ? ~0ull : (1ull << bit_shift) - 1;
+
+  // ---- host-port dictionary: (protocol, port) pairs of active pods, <= 64 - 2 * pairs
   std::unordered_map<int64_t, int32_t> port_dict;
   auto port_key = [](int32_t proto, int32_t port) { return (static_cast<int64_t>(proto) << 32) | uint32_t(port); };
   for (int32_t i = 0; i < nc; ++i) {
@@ -236,7 +244,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
         if (P.port_num[k] <= 0) continue;
         const int64_t key = port_key(P.port_proto[k], P.port_num[k]);
         if (port_dict.count(key)) continue;
-        if (port_dict.size() >= 64) {
+        if (static_cast<int32_t>(port_dict.size()) >= 64 - bit_shift) {
           overflow = true;
           continue;
         }
@@ -328,11 +336,23 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
         const size_t b0 = buf.size();
         spec_woff[q] = static_cast<uint32_t>(b0);
         const int32_t pod = active_pod[q];
-        if (!has_static_spec(P, pod)) {
+        // anti-affinity ids (term << 1 | has) of the pod, a suffix of its spec
+        const int32_t* aid = nullptr;
+        size_t nai = 0;
+        if (anti.active) {
+          const int32_t j = active_src[q];
+          aid = anti.pod_ids.data() + anti.pod_off[j];
+          nai = static_cast<size_t>(anti.pod_off[j + 1] - anti.pod_off[j]);
+        }
+        if (!has_static_spec(P, pod) && nai == 0) {
           spec_shard[q] = 255;  // spec 0
           continue;
         }
         for_each_spec_word(P, pod, [&](int32_t x) { buf.push_back(x); });
+        if (nai) {
+          buf.push_back(static_cast<int32_t>(nai));
+          buf.insert(buf.end(), aid, aid + nai);
+        }
         const uint64_t h = hash_words(buf.data() + b0, buf.size() - b0);
         spec_hash[q] = h;
         spec_shard[q] = static_cast<uint8_t>(shard_of(h));
@@ -366,7 +386,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     }
   });
   phase(15);
-  std::vector<int32_t> spec_rep{-1};  // first pod of each spec
+  std::vector<int32_t> spec_rep{-1}, spec_rep_q{-1};  // first pod of each spec (cluster / active index)
   {
     struct Rep {
       int32_t q, shard, local;
@@ -382,6 +402,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     for (const Rep& r : reps) {
       global[r.shard][r.local] = static_cast<int32_t>(spec_rep.size());
       spec_rep.push_back(active_pod[r.q]);
+      spec_rep_q.push_back(r.q);
     }
     parallel_for(static_cast<size_t>(na), 4096, [&](size_t lo, size_t hi) {
       for (size_t q = lo; q < hi; ++q)
@@ -399,7 +420,9 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     std::vector<int32_t> terms;  // per valid term: {n_req, groups...}
     int32_t n_terms = 0;
     std::vector<int32_t> untol;  // taint ids the spec does not tolerate
-    uint64_t ports = 0;
+    uint64_t ports = 0;          // host ports (dictionary bits)
+    std::vector<int32_t> anti_da, anti_db;  // anti-affinity terms: ANDNOT DA(t) / DB(t)
+    uint64_t anti_bits = 0;      // state-bit pairs the pod sets (A for terms it has, B for terms selecting it)
   };
   std::vector<SpecCanon> canon(n_specs);
   auto put_req = [](std::vector<int32_t>& out, int32_t type, int32_t key, int32_t op, const int32_t* v, int32_t nv) {
@@ -462,6 +485,19 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       for (int32_t t = 0; t < n_taints; ++t)
         if (!tolerates(P, pod, c->id_empty, taints[t])) sc.untol.push_back(t);
       sc.ports = pod_port_mask(pod);
+      if (anti.active) {
+        const int32_t j = active_src[spec_rep_q[sp]];
+        for (int32_t k = anti.pod_off[j]; k < anti.pod_off[j + 1]; ++k) {
+          const int32_t t = anti.pod_ids[k] >> 1, p = anti.pair_of[t];
+          if (anti.pod_ids[k] & 1) {  // it has t: refuses domains hosting pods t selects
+            if (anti.db_any[t]) sc.anti_db.push_back(t);
+            if (p >= 0) sc.anti_bits |= 1ull << (2 * p);
+          } else {  // t selects it: refused by domains hosting pods that have t
+            if (anti.da_any[t]) sc.anti_da.push_back(t);
+            if (p >= 0) sc.anti_bits |= 1ull << (2 * p + 1);
+          }
+        }
+      }
     }
   });
 
@@ -499,6 +535,10 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     sig_words.push_back(untol_dict.intern(sc.untol));
     sig_words.push_back(static_cast<int32_t>(sc.ports & 0xffffffffu));
     sig_words.push_back(static_cast<int32_t>(sc.ports >> 32));
+    sig_words.push_back(static_cast<int32_t>(sc.anti_da.size()));
+    sig_words.insert(sig_words.end(), sc.anti_da.begin(), sc.anti_da.end());
+    sig_words.push_back(static_cast<int32_t>(sc.anti_db.size()));
+    sig_words.insert(sig_words.end(), sc.anti_db.begin(), sc.anti_db.end());
     sig_off.push_back(static_cast<int32_t>(sig_words.size()));
   }
   const int32_t n_reqs = static_cast<int32_t>(rdict.size());
@@ -508,7 +548,8 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   // atom 0 AND NOT (OR of U's taint atoms) -- the pod-count check and
   // TaintToleration / NodeUnschedulable in one row, so a class program opens
   // with a single AND instead of 1 + |U| operations.
-  const int32_t A_COMP = A_PORT + n_ports;
+  const int32_t A_ANTI = A_PORT + n_ports;  // DA(t) at A_ANTI + 2t, DB(t) at A_ANTI + 2t + 1
+  const int32_t A_COMP = A_ANTI + 2 * anti.n_terms;
   std::vector<int32_t> comp_of(untol_dict.size(), -1), comp_sets;  // untolerated-set ids
   auto comp_atom = [&](int32_t u) {
     if (untol_dict.len(u) == 0) return 0;  // tolerates every taint: the pod-count atom alone
@@ -545,6 +586,13 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     for (int32_t k = 0; k < n_sel; ++k) emit(A_REQ + sel[k], PROG_AND);
     for (int32_t b = 0; b < 64; ++b)
       if (ports >> b & 1) emit(A_PORT + b, PROG_ANDNOT);
+    {  // anti-affinity base conflicts
+      const int32_t* ad = tp + 3;
+      const int32_t nda = ad[0];
+      for (int32_t k = 0; k < nda; ++k) emit(A_ANTI + 2 * ad[1 + k], PROG_ANDNOT);
+      const int32_t* bd = ad + 1 + nda;
+      for (int32_t k = 0; k < bd[0]; ++k) emit(A_ANTI + 2 * bd[1 + k] + 1, PROG_ANDNOT);
+    }
     if (flags & CLS_IMPOSSIBLE) {
       emit(0, PROG_ANDNOT);
     } else {
@@ -590,7 +638,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       auto it = port_dict.find(port_key(u.proto, u.port));
       if (it != port_dict.end()) pb |= 1ull << it->second;  // incoming pods bind 0.0.0.0
     }
-    w->port_bits[n] = pb;
+    w->port_bits[n] = (bit_shift < 64 ? pb << bit_shift : 0) | (anti.active ? anti.base_bits[n] : 0);
     for (int32_t b = 0; b < 64; ++b)
       if (pb >> b & 1) set_atom(A_PORT + b, n);
     for (int32_t k = node_taint_off[n]; k < node_taint_off[n + 1]; ++k) set_atom(A_TAINT + node_taint_ids[k], n);
@@ -603,6 +651,11 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     r[2] = static_cast<uint64_t>(w->free_eph[n]);
     r[3] = w->port_bits[n];
     r[4] = static_cast<uint64_t>(static_cast<int64_t>(w->pods_left[n]));
+  }
+  // anti-affinity base conflicts: DA(t), DB(t)
+  for (int32_t t = 0; t < anti.n_terms; ++t) {
+    std::copy_n(&anti.da[static_cast<size_t>(t) * Wp], Wp, &w->atoms[static_cast<size_t>(A_ANTI + 2 * t) * Wp]);
+    std::copy_n(&anti.db[static_cast<size_t>(t) * Wp], Wp, &w->atoms[static_cast<size_t>(A_ANTI + 2 * t + 1) * Wp]);
   }
   // composite atoms: atom 0 AND NOT (any taint of the set)
   for (size_t k = 0; k < comp_sets.size(); ++k) {
@@ -747,7 +800,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       rec[0] = static_cast<uint64_t>(rc);
       rec[1] = static_cast<uint64_t>(rm);
       rec[2] = static_cast<uint64_t>(re);
-      rec[3] = canon[pod_spec[q]].ports;
+      rec[3] = (bit_shift < 64 ? canon[pod_spec[q]].ports << bit_shift : 0) | canon[pod_spec[q]].anti_bits;
       bool dead = cls_empty[r[0]] != 0;
       for (int d = 0; d < 3; ++d) dead = dead || (r[1 + d] >= 0 && static_cast<size_t>(r[1 + d]) == node_vals[d].size());
       if (dead) {

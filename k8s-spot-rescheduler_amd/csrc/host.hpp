@@ -117,7 +117,11 @@ struct Workload {
   int32_t t_off[5] = {0, 0, 0, 0, 0};  // rows [t_off[i], t_off[i+1]): all, cpu, memory, ephemeral
   // ---- active pods, grouped by candidate, in podsForDeletion order
   std::vector<int32_t> pod_rows;  // [n][4]: S row (class), T rows for cpu, memory, ephemeral
-  std::vector<uint64_t> pod_rec;  // [n + 128][6] AoS {cpu, memory, ephemeral, ports, rows} for K2
+  std::vector<uint64_t> pod_rec;  // [n + 128][6] AoS {cpu, memory, ephemeral, state bits, rows} for K2
+  // state bits of a node / the bits a pod sets: anti-affinity pairs in
+  // [0, 2 * n_pairs) (pair-swapped to get the bits a pod conflicts with),
+  // host ports above them
+  uint64_t swap_mask = 0;
   std::vector<int32_t> pod_src;  // index into the caller's cand_pods array
   // ---- active candidates
   std::vector<int32_t> cand_off;     // [n_active+1] into active pods
@@ -144,6 +148,7 @@ struct Workload {
     // every field, so a steady-state encode does not zero-fill them first
     n_spot = n_pad = Wp = n_atoms = n_classes = 0;
     empty_class = -1;
+    swap_mask = 0;
     for (int32_t& t : t_off) t = 0;
     max_cand_pods = 0;
     first_fallback = -1;
@@ -155,6 +160,25 @@ struct Workload {
 constexpr int32_t STATUS_PENDING = -100;
 constexpr int32_t MAX_CAND_PODS = 512;  // pods per candidate on the device (K2 kMaxPods)
 constexpr int32_t MAX_WORDS = 64 * 32; // spot nodes <= 131072
+
+// Required pod anti-affinity of one encode (antiaff.cpp).
+struct AntiTerms {
+  bool active = false;
+  int32_t n_terms = 0;
+  std::vector<uint8_t> node_local;       // [term] every spot node has the key, values pairwise distinct
+  std::vector<uint64_t> da, db;          // [term][Wp] base conflicts: pods having / selected by the term
+  std::vector<uint8_t> da_any, db_any;   // [term] the set is not empty
+  std::vector<int32_t> pod_off, pod_ids; // [flat candidate pod + 1] -> ids: term << 1 (selects it) | 1 (it has)
+  std::vector<int32_t> pair_of;          // [term] state-bit pair (A = 2p, B = 2p + 1) or -1
+  int32_t n_pairs = 0;
+  std::vector<uint64_t> base_bits;       // [spot node] pair bits of the base snapshot
+};
+
+// Collects the terms of the snapshot's pods and of the pending candidates,
+// builds the static node sets and decides which candidates fall back
+// (status -> SR_CAND_FALLBACK) or need state bits.
+void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
+                  std::vector<int32_t>& status, AntiTerms* out);
 
 // Builds the workload; returns SR_OK or an error with *err filled.
 sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,

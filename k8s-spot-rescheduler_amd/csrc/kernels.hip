@@ -286,6 +286,14 @@ __device__ __forceinline__ void write_winner(const DevWorkload& w) {
 // K3: one wave (after the collective on multi-GPU runs).
 __global__ __launch_bounds__(64) void k3_winner(DevWorkload w) { write_winner(w); }
 
+// The bits a pod conflicts with, from the state bits it sets: anti-affinity
+// pairs (A: has the term, B: selected by it) swapped, host-port bits as they
+// are (encode.cpp / antiaff.cpp).  An involution.
+__device__ __forceinline__ uint64_t swap_pairs(uint64_t x, uint64_t m) {
+  const uint64_t y = x & m, e = 0x5555555555555555ull;
+  return (x & ~m) | ((y & e) << 1) | ((y >> 1) & e);
+}
+
 constexpr int kHead = 32;       // head of a pod's rows prefetched per step: words [0, 32) = nodes [0, 2048)
 constexpr int kRing = 8;        // head ring: pods k..k+7 (rows of pod k+8 issued at the end of step k)
 constexpr int kPodWin = 128;    // pod records staged per wave: two 64-pod halves
@@ -428,7 +436,8 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
   for (; k < np; ++k) {
     if (PROF) cyc_t = cyc();
     const int64_t rc = nrc, rm = nrm, re = nre;
-    const uint64_t pm = npm;
+    const uint64_t pm = npm;                          // state bits the pod sets
+    const uint64_t pin = swap_pairs(pm, w.swap_mask);  // ... and those it conflicts with
     const bool zero = (rc | rm | re) == 0;  // fitsRequest skips the resource checks
     // Head (spot nodes [0, 2048)): touched nodes below the first untouched
     // feasible one, rechecked branch-free: class bit from the S row, capacity /
@@ -442,7 +451,7 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
       for (int s = 0; s < SPL; ++s) {
         const int nd = snode[s];
         const bool fit = zero | ((rc <= scpu[s]) & (rm <= smem[s]) & (re <= seph[s]));  // NodeResourcesFit
-        const bool ok = (nd < hi) & sbit[s] & (sleft[s] >= 1) & ((sport[s] & pm) == 0) & fit;
+        const bool ok = (nd < hi) & sbit[s] & (sleft[s] >= 1) & ((sport[s] & pin) == 0) & fit;
         best = ok ? min(best, nd) : best;
       }
       const uint64_t hb = ballot(best != INT_MAX);
@@ -482,7 +491,7 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
           const uint64_t sw = img[in ? (nd >> 6) - base : 0];
           const bool fit = zero | ((rc <= scpu[s]) & (rm <= smem[s]) & (re <= seph[s]));
           const bool ok =
-              in & (((sw >> (nd & 63)) & 1ull) != 0) & (sleft[s] >= 1) & ((sport[s] & pm) == 0) & fit;
+              in & (((sw >> (nd & 63)) & 1ull) != 0) & (sleft[s] >= 1) & ((sport[s] & pin) == 0) & fit;
           best = ok ? min(best, nd) : best;
         }
         ans = min(cnode, wave_min(best));
@@ -651,7 +660,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     rc[g] = static_cast<int64_t>(pr[0]);
     rm[g] = static_cast<int64_t>(pr[1]);
     re[g] = static_cast<int64_t>(pr[2]);
-    pm[g] = pr[3];
+    pm[g] = swap_pairs(pr[3], w.swap_mask);  // the state bits the pod conflicts with
     r01[g] = pr[4];
     r23[g] = pr[5];
     zero[g] = (rc[g] | rm[g] | re[g]) == 0;  // fitsRequest skips the resource checks
@@ -833,7 +842,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc[g]), j));
         mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm[g]), j));
         eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(re[g]), j));
-        if (pm_any != 0) ports |= readlane64(pm[g], j);
+        if (pm_any != 0) ports |= swap_pairs(readlane64(pm[g], j), w.swap_mask);  // the bits it sets
         left -= 1;
         ++placements;
       }

@@ -16,7 +16,7 @@ constexpr size_t kK0ProfWaves = 32768;  // K0 waves profiled after K2's [n_cand]
 struct DevWorkload {
   int32_t n_spot, n_pad, Wp;
   const int32_t* node_rank;    // [3][n_pad] per dimension: the node is in that dimension's T rows [0, rank)
-  const uint64_t* node_rec;    // [n_pad][8] AoS {free cpu, mem, eph, ports, pods_left, 0, 0, 0} for K2
+  const uint64_t* node_rec;    // [n_pad][8] AoS {free cpu, mem, eph, state bits, pods_left, 0, 0, 0} for K2
   int32_t n_atoms;
   const uint64_t* atoms;       // [n_atoms][Wp] node bitsets (encode.cpp)
   const int32_t* cls_prog_off; // class atom programs (CSR): ops atom << 2 | {AND, AND NOT,
@@ -29,7 +29,9 @@ struct DevWorkload {
   int32_t t_off[5];         //   ephemeral rows [t_off[d + 1], t_off[d + 2]) in threshold order
   const int64_t* t_thr;
   int32_t n_pods;
-  const uint64_t* pod_rec;  // [n_pods + 128][6] AoS {cpu, memory, ephemeral, ports, S | T cpu row word
+  uint64_t swap_mask;       // state bits [0, 2 * pairs): anti-affinity pairs; a pod conflicts with the
+                            // pair-swapped image of the bits it sets (swap_pairs), host ports above
+  const uint64_t* pod_rec;  // [n_pods + 128][6] AoS {cpu, memory, ephemeral, state bits, S | T cpu row word
                             //  offset, T mem | T eph row word offset} (48 B, padded for K2's window reads)
   int32_t n_cand;
   const int32_t* cand_off;

@@ -202,6 +202,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.out_status = static_cast<int32_t*>(ctx->out_status.p);
   d.d_min = static_cast<int32_t*>(ctx->dmin.p);
   d.k2_mode = ctx->k2_mode;
+  d.swap_mask = w.swap_mask;
   d.prof = nullptr;
   if (ctx->prof_file) {
     const size_t pbytes = sizeof(uint64_t) * (16 * static_cast<size_t>(std::max(1, ncand)) + 2 * sr::kK0ProfWaves);

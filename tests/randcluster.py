@@ -7,8 +7,9 @@ from __future__ import annotations
 
 import random
 
-from spotplanner.model import (Container, ContainerPort, GiB, MiB, Node, NodeSelectorRequirement,
-                               NodeSelectorTerm, OwnerReference, Pod, Taint, Toleration)
+from spotplanner.model import (Container, ContainerPort, GiB, LabelSelector, LabelSelectorRequirement, MiB, Node,
+                               NodeSelectorRequirement, NodeSelectorTerm, OwnerReference, Pod, PodAffinityTerm,
+                               Taint, Toleration)
 
 KEYS = ["zone", "type", "team", "disk", "gpu"]
 VALS = ["a", "b", "c", ""]
@@ -85,9 +86,47 @@ def rand_pod(r: random.Random, name: str, features: bool, fallback: bool = False
     return p
 
 
+HOST = "kubernetes.io/hostname"
+APPS = ["web", "db", "cache"]
+NAMESPACES = ["default", "default", "other"]
+
+
+def rand_selector(r: random.Random):
+    k = r.random()
+    if k < 0.55:
+        return LabelSelector({"app": r.choice(APPS)})
+    if k < 0.75:
+        op = r.choice(["In", "NotIn", "Exists", "DoesNotExist"])
+        vals = [] if op in ("Exists", "DoesNotExist") else r.sample(["fe", "be"], r.randint(1, 2))
+        return LabelSelector({"app": r.choice(APPS)} if r.random() < 0.5 else {},
+                             [LabelSelectorRequirement("tier", op, vals)])
+    if k < 0.85:
+        return LabelSelector()  # selects every pod of the namespaces
+    if k < 0.95:
+        return None  # nil: selects nothing
+    return LabelSelector({}, [LabelSelectorRequirement("tier", "In", [])])  # invalid: fallback
+
+
+def rand_anti(r: random.Random, p: Pod, rate: float):
+    """Labels and namespace for every pod; required anti-affinity for some.
+    Topology keys: the hostname (node-local) mostly, zone / team (shared or
+    missing on some nodes) otherwise."""
+    p.namespace = r.choice(NAMESPACES)
+    p.labels = {"app": r.choice(APPS)}
+    if r.random() < 0.5:
+        p.labels["tier"] = r.choice(["fe", "be"])
+    if r.random() < rate:
+        p.pod_anti_affinity = []
+        for _ in range(r.randint(1, 2)):
+            tk = HOST if r.random() < 0.7 else r.choice(["zone", "team"])
+            ns = [] if r.random() < 0.7 else r.sample(["default", "other"], r.randint(1, 2))
+            p.pod_anti_affinity.append(PodAffinityTerm(tk, rand_selector(r), ns))
+
+
 def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 8, features: bool = True,
-                  fallback: bool = False):
-    """Returns (spot_nodes, spot_pods, candidates) with candidates a list of pod lists."""
+                  fallback: bool = False, anti: float = 0.0):
+    """Returns (spot_nodes, spot_pods, candidates) with candidates a list of pod lists.
+    anti > 0: pods carry namespaces / labels and that share required pod anti-affinity."""
     r = random.Random(seed)
     nodes = [rand_node(r, "n%d" % i, features) for i in range(n_spot)]
     spot_pods = []
@@ -98,4 +137,43 @@ def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 
         spot_pods.append(ps)
     cands = [[rand_pod(r, "c%d_%d" % (c, k), features, fallback) for k in range(r.randint(0, max_pods))]
              for c in range(n_cand)]
+    if anti > 0:
+        for ps in spot_pods + cands:
+            for p in ps:
+                rand_anti(r, p, anti)
     return nodes, spot_pods, cands
+
+
+def term_selects(owner: Pod, t: PodAffinityTerm, target: Pod) -> bool:
+    """Namespace + label selector of an anti-affinity term (test-side restatement)."""
+    if target.namespace not in (t.namespaces or [owner.namespace]):
+        return False
+    sel = t.label_selector
+    if sel is None:
+        return False
+    if any(target.labels.get(k) != v for k, v in sel.match_labels.items()):
+        return False
+    for e in sel.match_expressions:
+        v = target.labels.get(e.key)
+        ok = {"In": v is not None and v in e.values, "NotIn": v is None or v not in e.values,
+              "Exists": v is not None, "DoesNotExist": v is None}[e.operator]
+        if not ok:
+            return False
+    return True
+
+
+def anti_interacts_off_node(nodes, pods) -> bool:
+    """Two pods of one candidate interact through an anti-affinity term whose
+    topology key is not node-local on the spot pool (some node lacks it or two
+    nodes share a value): the product routes such a candidate to the fallback
+    path (antiaff.cpp), the oracle evaluates it."""
+    def node_local(tk):
+        vals = [n.labels.get(tk) for n in nodes]
+        return all(v is not None for v in vals) and len(set(vals)) == len(vals)
+    for i, a in enumerate(pods):
+        for t in a.pod_anti_affinity or []:
+            if node_local(t.topology_key):
+                continue
+            if any(j != i and term_selects(a, t, b) for j, b in enumerate(pods)):
+                return True
+    return False

@@ -9,7 +9,7 @@ import pytest
 
 from helpers import Scenario
 from oracle_lib import OracleSnapshot, load_oracle, oracle_new_node_map, oracle_plan
-from randcluster import rand_scenario
+from randcluster import anti_interacts_off_node, rand_scenario
 from spotplanner import capi
 from spotplanner.model import Container, ContainerPort, GiB, Node, Pod
 from spotplanner.rescheduler import plan_arrays
@@ -51,7 +51,7 @@ def compare_plans(o, p, cand_off, extra_fallback=None):
         assert np.array_equal(p.winner_map, o["node_of_pod"][cand_off[exp_ok]:cand_off[exp_ok + 1]])
 
 
-def run_scenario(checker, nodes, spot_pods, cands):
+def run_scenario(checker, nodes, spot_pods, cands, extra_fallback=None):
     flat = [p for c in cands for p in c]
     sc = Scenario(nodes, spot_pods, flat)
     cand_off = np.cumsum([0] + [len(c) for c in cands]).astype(np.int32)
@@ -62,7 +62,8 @@ def run_scenario(checker, nodes, spot_pods, cands):
         p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
     finally:
         capi.load_planner().sr_snapshot_destroy(h)
-    compare_plans(o, p, cand_off, lambda c: product_only_fallback(cands[c]))
+    compare_plans(o, p, cand_off,
+                  lambda c: product_only_fallback(cands[c]) or (extra_fallback is not None and extra_fallback(c)))
     return sc, o, p
 
 
@@ -145,6 +146,102 @@ def test_can_drain_node_sequence_mutates_like_oracle(checker, seed):
             k = ctypes.c_int32()
             lib.sr_snapshot_node_state(h, pos, capi.ptr(req, capi.P64), ctypes.byref(k))
             assert (tuple(req), k.value) == osnap.node_state(pos)
+    lib.sr_snapshot_destroy(h)
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_random_plans_with_pod_anti_affinity(checker, seed):
+    """Required pod anti-affinity (static base conflicts + state-bit pairs
+    between the pods of a candidate); the product may route a candidate to
+    the fallback path only for an interaction through a non-node-local key."""
+    nodes, spot_pods, cands = rand_scenario(6000 + seed, n_spot=8 + seed % 12, n_cand=10, max_pods=4 + seed % 8,
+                                            features=seed % 3 != 0, anti=0.3 + 0.02 * seed)
+    run_scenario(checker, nodes, spot_pods, cands, extra_fallback=lambda c: anti_interacts_off_node(nodes, cands[c]))
+
+
+def test_pod_anti_affinity_exercises_the_state_bits(checker):
+    """Some seeds above must plan candidates whose pods interact through the
+    hostname (the state-bit path), not only static conflicts or fallbacks."""
+    from randcluster import HOST, term_selects
+    hits = 0
+    for seed in range(30):
+        nodes, spot_pods, cands = rand_scenario(6000 + seed, n_spot=8 + seed % 12, n_cand=10,
+                                                max_pods=4 + seed % 8, features=seed % 3 != 0,
+                                                anti=0.3 + 0.02 * seed)
+        for c in cands:
+            hits += any(t.topology_key == HOST and any(j != i and term_selects(a, t, b) for j, b in enumerate(c))
+                        for i, a in enumerate(c) for t in a.pod_anti_affinity or [])
+    assert hits >= 20
+
+
+def test_replicas_spread_by_hostname_anti_affinity(checker):
+    from spotplanner.model import LabelSelector, PodAffinityTerm
+    HOST = "kubernetes.io/hostname"
+    nodes = [Node(name="n%d" % i, cpu_milli=4000, memory=8 * GiB, pods=110, labels={HOST: "n%d" % i})
+             for i in range(3)]
+    t = [PodAffinityTerm(HOST, LabelSelector({"app": "web"}))]
+    reps = [Pod(name="r%d" % i, namespace="default", containers=[Container(cpu_milli=100)],
+                labels={"app": "web"}, pod_anti_affinity=t) for i in range(4)]
+    other = Pod(name="x", namespace="default", containers=[Container(cpu_milli=100)], labels={"app": "db"})
+    _, o, p = run_scenario(checker, nodes, [[], [], []], [reps[:3] + [other], reps])
+    assert list(p.status) == [OK, 3]
+    assert list(p.node_of_pod[:4]) == [0, 1, 2, 0]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_find_spot_nodes_with_pod_anti_affinity(checker, seed):
+    nodes, spot_pods, cands = rand_scenario(7000 + seed, n_spot=15, n_cand=6, max_pods=10, anti=0.5)
+    flat = [p for c in cands for p in c]
+    sc = Scenario(nodes, spot_pods, flat)
+    osnap = sc.oracle_snapshot()
+    olib = load_oracle()
+    want = [olib.oracle_find_spot_node_for_pod(osnap.h, sc.ptr, sc.qidx(i)) for i in range(len(flat))]
+    h = sc.product_snapshot()
+    lib = capi.load_planner()
+    idx = np.arange(sc.q0, sc.q0 + len(flat), dtype=np.int32)
+    out = np.full(max(1, len(flat)), -7, np.int32)
+    fb = np.zeros(max(1, len(flat)), np.uint8)
+    assert lib.sr_find_spot_nodes(checker.handle, h, sc.ptr, capi.ptr(idx, capi.P32), len(flat),
+                                  capi.ptr(out, capi.P32), capi.ptr(fb, capi.PU8)) == capi.SR_OK
+    for i, w in enumerate(want):
+        if w == -2:
+            assert fb[i] == 1, i
+        else:
+            assert fb[i] == 0 and out[i] == w, (i, w, out[i], fb[i])  # one pod: nothing interacts
+    lib.sr_snapshot_destroy(h)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_can_drain_node_sequence_with_pod_anti_affinity(checker, seed):
+    """canDrainNode calls on ONE snapshot: the pods placed by earlier calls
+    (and their terms) are base pods of the later ones."""
+    nodes, spot_pods, cands = rand_scenario(8000 + seed, n_spot=10, n_cand=6, max_pods=6, anti=0.5)
+    flat = [p for c in cands for p in c]
+    sc = Scenario(nodes, spot_pods, flat)
+    osnap = sc.oracle_snapshot()
+    olib = load_oracle()
+    h = sc.product_snapshot()
+    lib = capi.load_planner()
+    base = sc.q0
+    for c in cands:
+        n = len(c)
+        pods = np.arange(base, base + n, dtype=np.int32)
+        base += n
+        omap = np.full(max(n, 1), -1, np.int32)
+        r = olib.oracle_can_drain_node(osnap.h, sc.ptr, capi.ptr(pods, capi.P32), n, capi.ptr(omap, capi.P32))
+        pmap = np.full(max(n, 1), -1, np.int32)
+        fail = ctypes.c_int32()
+        fb = ctypes.c_uint8()
+        assert lib.sr_can_drain_node(checker.handle, h, sc.ptr, capi.ptr(pods, capi.P32), n,
+                                     capi.ptr(pmap, capi.P32), ctypes.byref(fail), ctypes.byref(fb)) == capi.SR_OK
+        if r == -2:
+            assert fb.value == 1
+            continue
+        if fb.value:
+            assert product_only_fallback(c) or anti_interacts_off_node(nodes, c)
+            break  # the oracle mutated, the product did not: stop comparing states
+        assert fail.value == r
+        assert np.array_equal(pmap[:n], omap[:n])
     lib.sr_snapshot_destroy(h)
 
 
