@@ -727,14 +727,12 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     const uint64_t gone = ballot(k < dead && ptr[g] == INT_MAX);
     if (gone != 0) dead = min(dead, 64 * g + __builtin_ctzll(gone));
   }
-  uint64_t zm[G];        // pods with an all-zero request (fitsRequest skips the resource checks)
-  uint64_t pm_any = 0;   // any pod with host ports: NodePorts checks are needed at all
+  uint64_t zm[G];  // pods with an all-zero request (fitsRequest skips the resource checks)
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     act[g] = ballot(64 * g + lane < dead);  // pods still to place
     any |= act[g];
     zm[g] = ballot(zero[g]);
-    pm_any |= ballot(pm[g] != 0);
   }
   if (PROF) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -830,21 +828,28 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
 #pragma unroll
     for (int g = 0; g < G; ++g) {  // groups in pod order: the state flows from one to the next
       const uint64_t cand = ballot(((act[g] >> lane) & 1) && ptr[g] == n);
-      uint64_t rest = cand, placed = 0;
-      while (rest != 0 && left >= 1) {  // NodeResourcesFit + NodePorts, pods in order
-        // lane masks straight from the compares (no bool round trip through VGPRs)
-        uint64_t fm = rest & (zm[g] | (ballot(rc[g] <= cpu) & ballot(rm[g] <= mem) & ballot(re[g] <= eph)));
-        if (pm_any != 0 && ports != 0) fm &= ballot((pm[g] & ports) == 0);
-        if (fm == 0) break;
-        const int j = __builtin_ctzll(fm);
-        placed |= 1ull << j;
-        rest &= ~((2ull << j) - 1);  // pods below j that did not fit failed at n
-        cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc[g]), j));
-        mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm[g]), j));
-        eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(re[g]), j));
-        if (pm_any != 0) ports |= swap_pairs(readlane64(pm[g], j), w.swap_mask);  // the bits it sets
-        left -= 1;
-        ++placements;
+      uint64_t placed = 0;
+      if (cand != 0) {  // wave-uniform
+        // NodeResourcesFit + NodePorts / anti-affinity state, pods in order.
+        // One exit branch per placement: the checks are unconditional (lane
+        // masks straight from the compares) and the pod-count limit clears
+        // `rest` by a select.
+        uint64_t rest = left >= 1 ? cand : 0ull;
+        for (;;) {
+          uint64_t fm = rest & (zm[g] | (ballot(rc[g] <= cpu) & ballot(rm[g] <= mem) & ballot(re[g] <= eph)));
+          fm &= ballot((pm[g] & ports) == 0);
+          if (fm == 0) break;
+          const int j = __builtin_ctzll(fm);
+          placed |= 1ull << j;
+          rest &= ~((2ull << j) - 1);  // pods below j that did not fit failed at n
+          cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc[g]), j));
+          mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm[g]), j));
+          eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(re[g]), j));
+          ports |= swap_pairs(readlane64(pm[g], j), w.swap_mask);  // the bits it sets
+          left -= 1;
+          rest = left >= 1 ? rest : 0ull;
+          ++placements;
+        }
       }
       if ((placed >> lane) & 1) node[g] = n;
       act[g] &= ~placed;
