@@ -378,3 +378,42 @@ def test_synthetic_config3_other_seeds(checker):
 def test_synthetic_config4_spot_pool_sampled_candidates(checker):
     # full C4 spot pool (35k nodes: 9 chunks per row) with the first 1500 candidates
     tick_parity(checker, SynthCluster(4, n_on_demand=1500), max_cands=1500)
+
+
+def test_rccl_single_rank_collective_path_matches(checker):
+    """The multi-GPU tick (K0 + K2, ncclAllReduce(min) of d_min over RCCL, K3
+    on the owning rank) run with a one-rank communicator: same plan as the
+    single-GPU path.  The sharding itself is covered with gloo at world sizes
+    2 and 3 (test_distributed.py)."""
+    from spotplanner.planner import PredicateChecker
+    nodes, spot_pods, cands = rand_scenario(9100, n_spot=30, n_cand=20, max_pods=10)
+    flat = [p for c in cands for p in c]
+    sc = Scenario(nodes, spot_pods, flat)
+    cand_off = np.cumsum([0] + [len(c) for c in cands]).astype(np.int32)
+    cand_pods = np.arange(sc.q0, sc.q0 + len(flat), dtype=np.int32)
+    lib = capi.load_planner()
+    h = sc.product_snapshot()
+    comm_checker = PredicateChecker(0)
+    try:
+        uid = (ctypes.c_uint8 * capi.SR_UNIQUE_ID_BYTES)()
+        assert lib.sr_comm_unique_id(uid) == capi.SR_OK
+        assert lib.sr_comm_init(comm_checker.handle, uid, 1, 0) == capi.SR_OK, comm_checker.last_error()
+        want = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+        got = plan_arrays(comm_checker, h, sc.ptr, cand_off, cand_pods)
+        assert (got.winner, got.first_ok, got.first_fallback) == (want.winner, want.first_ok, want.first_fallback)
+        assert np.array_equal(got.status, want.status)
+        assert np.array_equal(got.node_of_pod, want.node_of_pod)
+        assert np.array_equal(got.winner_map, want.winner_map)
+        # the split prepare / run form the bench times goes through the collective too
+        c = capi.sr_candidates(len(cand_off) - 1, capi.ptr(cand_off, capi.P32), capi.ptr(cand_pods, capi.P32), None)
+        assert lib.sr_plan_prepare(comm_checker.handle, h, sc.ptr, ctypes.byref(c)) == capi.SR_OK
+        wmap = np.full(max(1, int(np.max(np.diff(cand_off)))), -1, np.int32)
+        out = capi.sr_plan_out()
+        out.winner_map = capi.ptr(wmap, capi.P32)
+        for _ in range(3):
+            assert lib.sr_plan_run(comm_checker.handle, ctypes.byref(out)) == capi.SR_OK, comm_checker.last_error()
+            assert out.winner == want.winner
+            assert np.array_equal(wmap[:out.winner_npods], want.winner_map)
+    finally:
+        comm_checker.close()
+        lib.sr_snapshot_destroy(h)
