@@ -7,11 +7,13 @@
 // ClusterSnapshot operations the planner needs (AddPod / Fork / Revert,
 // rescheduler.go:269,273,366) live here too.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <vector>
 
 #include "gosort.hpp"
 #include "host.hpp"
+#include "pool.hpp"
 
 namespace sr {
 
@@ -48,30 +50,54 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
 
   const int64_t* cpu = P.cpu_sort_milli;
   auto by_cpu_desc = [cpu](int32_t x, int32_t y) { return cpu[x] > cpu[y]; };
-  int32_t kept = 0, ns = 0, nod = 0;
-  for (int32_t node = 0; node < nn; ++node) {
-    const bool spot = node_has_label(c, node, &p->spot);
-    out->node_pod_off[node] = kept;
-    const int32_t first = kept;
-    int64_t requested = 0;
-    for (int32_t j = start[node]; j < start[node + 1]; ++j) {
-      const int32_t pod = listed[j];
-      // int(*Spec.Priority) < PriorityThreshold && isSpotNode(node)  (:139);
-      // the dereference comes first, so a nil priority panics on any node.
-      if (!P.has_priority[pod]) return SR_ERR_NIL_PRIORITY;
-      if (P.priority[pod] < p->priority_threshold && spot) continue;
-      out->node_pod_idx[kept++] = pod;
-      requested += cpu[pod];
+  // Per node (independent, on the pool): the spot / on-demand test, the
+  // priority filter of getPodsOnNode, RequestedCPU and the pod sort.  Pass 1
+  // counts the kept pods, pass 2 writes them at their prefix offsets.
+  std::vector<int8_t> kind(static_cast<size_t>(nn), 0);  // 1 spot, 2 on-demand
+  std::vector<int32_t> nkept(static_cast<size_t>(nn) + 1, 0);
+  std::atomic<bool> nil_priority{false};
+  parallel_for(static_cast<size_t>(nn), 64, [&](size_t lo, size_t hi) {
+    for (size_t node = lo; node < hi; ++node) {
+      const bool spot = node_has_label(c, static_cast<int32_t>(node), &p->spot);
+      kind[node] = spot ? 1 : node_has_label(c, static_cast<int32_t>(node), &p->on_demand) ? 2 : 0;
+      int32_t k = 0;
+      for (int32_t j = start[node]; j < start[node + 1]; ++j) {
+        const int32_t pod = listed[j];
+        // int(*Spec.Priority) < PriorityThreshold && isSpotNode(node)  (:139);
+        // the dereference comes first, so a nil priority panics on any node.
+        if (!P.has_priority[pod]) nil_priority.store(true, std::memory_order_relaxed);
+        else if (!(P.priority[pod] < p->priority_threshold && spot)) ++k;
+      }
+      nkept[node + 1] = k;
     }
-    out->requested_cpu[node] = requested;
-    out->free_cpu[node] = N.alloc_milli_cpu[node] - requested;
-    go_sort_slice(out->node_pod_idx + first, kept - first, by_cpu_desc);
-    if (spot)
+  });
+  if (nil_priority.load()) return SR_ERR_NIL_PRIORITY;
+  for (int32_t node = 0; node < nn; ++node) nkept[node + 1] += nkept[node];
+  parallel_for(static_cast<size_t>(nn), 64, [&](size_t lo, size_t hi) {
+    for (size_t node = lo; node < hi; ++node) {
+      const bool spot = kind[node] == 1;
+      int32_t kept = nkept[node];
+      out->node_pod_off[node] = kept;
+      int64_t requested = 0;
+      for (int32_t j = start[node]; j < start[node + 1]; ++j) {
+        const int32_t pod = listed[j];
+        if (P.priority[pod] < p->priority_threshold && spot) continue;
+        out->node_pod_idx[kept++] = pod;
+        requested += cpu[pod];
+      }
+      out->requested_cpu[node] = requested;
+      out->free_cpu[node] = N.alloc_milli_cpu[node] - requested;
+      go_sort_slice(out->node_pod_idx + nkept[node], kept - nkept[node], by_cpu_desc);
+    }
+  });
+  int32_t ns = 0, nod = 0;
+  for (int32_t node = 0; node < nn; ++node) {
+    if (kind[node] == 1)
       out->spot[ns++] = node;
-    else if (node_has_label(c, node, &p->on_demand))
+    else if (kind[node] == 2)
       out->on_demand[nod++] = node;
   }
-  out->node_pod_off[nn] = kept;
+  out->node_pod_off[nn] = nkept[nn];
   const int64_t* req = out->requested_cpu;
   go_sort_slice(out->spot, ns, [req](int32_t x, int32_t y) { return req[x] > req[y]; });
   go_sort_slice(out->on_demand, nod, [req](int32_t x, int32_t y) { return req[x] < req[y]; });
@@ -143,32 +169,39 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
   s->nodes.resize(n_spot);
   s->state.resize(n_spot);
   const sr_nodes& N = c->nodes;
-  for (int32_t i = 0; i < n_spot; ++i) {
+  for (int32_t i = 0; i < n_spot; ++i) {  // validate first: the build below cannot fail
     const int32_t node = spot[i];
     if (node < 0 || node >= N.n) {
       delete s;
       return SR_ERR_INVALID_ARG;
     }
-    SpotNode& sn = s->nodes[i];
-    sn.name = N.name[node];
-    sn.alloc[0] = N.alloc_milli_cpu[node];
-    sn.alloc[1] = N.alloc_memory[node];
-    sn.alloc[2] = N.alloc_ephemeral[node];
-    sn.alloc_pods = N.alloc_pods[node];
-    sn.unschedulable = N.unschedulable[node];
-    for (int32_t j = N.label_off[node]; j < N.label_off[node + 1]; ++j)
-      sn.labels.emplace_back(N.label_key[j], N.label_val[j]);
-    for (int32_t j = N.taint_off[node]; j < N.taint_off[node + 1]; ++j)
-      sn.taints.push_back(TaintRec{N.taint_key[j], N.taint_val[j], N.taint_effect[j]});
-    s->state[i].pods.reserve(static_cast<size_t>(off[node + 1] - off[node]));
-    for (int32_t j = off[node]; j < off[node + 1]; ++j) {
-      const int32_t pod = idx[j];
-      if (pod < 0 || pod >= c->pods.n) {
+    for (int32_t j = off[node]; j < off[node + 1]; ++j)
+      if (idx[j] < 0 || idx[j] >= c->pods.n) {
         delete s;
         return SR_ERR_INVALID_ARG;
       }
-      state_add_pod(s->state[i], c, pod);
+  }
+  // AddNodeWithPods per spot node: independent nodes, on the pool
+  parallel_for(static_cast<size_t>(n_spot), 32, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      const int32_t node = spot[i];
+      SpotNode& sn = s->nodes[i];
+      sn.name = N.name[node];
+      sn.alloc[0] = N.alloc_milli_cpu[node];
+      sn.alloc[1] = N.alloc_memory[node];
+      sn.alloc[2] = N.alloc_ephemeral[node];
+      sn.alloc_pods = N.alloc_pods[node];
+      sn.unschedulable = N.unschedulable[node];
+      sn.labels.reserve(static_cast<size_t>(N.label_off[node + 1] - N.label_off[node]));
+      for (int32_t j = N.label_off[node]; j < N.label_off[node + 1]; ++j)
+        sn.labels.emplace_back(N.label_key[j], N.label_val[j]);
+      for (int32_t j = N.taint_off[node]; j < N.taint_off[node + 1]; ++j)
+        sn.taints.push_back(TaintRec{N.taint_key[j], N.taint_val[j], N.taint_effect[j]});
+      s->state[i].pods.reserve(static_cast<size_t>(off[node + 1] - off[node]));
+      for (int32_t j = off[node]; j < off[node + 1]; ++j) state_add_pod(s->state[i], c, idx[j]);
     }
+  });
+  for (int32_t i = 0; i < n_spot; ++i) {
     s->anti_total += s->state[i].anti;
     s->opaque_total += s->state[i].opaque;
   }
