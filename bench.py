@@ -205,6 +205,7 @@ def main():
     # candidate lists and snapshot on the host -> encode + H2D (sr_plan_prepare)
     # -> kernels -> winner and mapping on the host (sr_plan_run).  The
     # planner's buffers are already grown, as in every tick after the first.
+    first_ok_ref = out.first_ok
     e2e, enc, upl = [], [], []
     for _ in range(args.e2e_reps):
         t1 = time.perf_counter()
@@ -216,12 +217,40 @@ def main():
         tq = checker.timing()
         enc.append(tq.ms_pack_host)
         upl.append(tq.ms_upload)
+    # The whole housekeeping tick from the cluster arrays: NewNodeMap (A1-A5),
+    # the candidate lists (GetPodsForDeletionOnNodeDrain + owner filter),
+    # GetClusterSnapshot (A6), then prepare + run as above.
+    full_tick = []
+    for _ in range(args.e2e_reps):
+        t1 = time.perf_counter()
+        nm2 = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+        co2, cp2, _, _, st = pods_for_deletion(lib.sr_pods_for_deletion, sc.ptr, ctypes.byref(sc.drain),
+                                               nm2.on_demand, nm2.node_pod_off, nm2.node_pod_idx)
+        assert st == capi.SR_OK, st
+        lo2, lp2, gi2 = shard(co2, cp2, rank, world)
+        snap2 = ctypes.c_void_p()
+        st = lib.sr_snapshot_create(sc.ptr, capi.ptr(nm2.spot, capi.P32), len(nm2.spot),
+                                    capi.ptr(nm2.node_pod_off, capi.P32), capi.ptr(nm2.node_pod_idx, capi.P32),
+                                    ctypes.byref(snap2))
+        assert st == capi.SR_OK
+        c2 = capi.sr_candidates(len(lo2) - 1, capi.ptr(lo2, capi.P32), capi.ptr(lp2, capi.P32),
+                                capi.ptr(gi2, capi.P32))
+        st = lib.sr_plan_prepare(checker.handle, snap2, sc.ptr, ctypes.byref(c2))
+        assert st == capi.SR_OK, checker.last_error()
+        st = lib.sr_plan_run(checker.handle, ctypes.byref(out))
+        assert st == capi.SR_OK, checker.last_error()
+        full_tick.append(1e3 * (time.perf_counter() - t1))
+        assert out.first_ok == first_ok_ref
+        lib.sr_snapshot_destroy(snap2)
     end_to_end = None
     if e2e:
         end_to_end = {"median_ms": round(float(np.median(e2e)), 3), "min_ms": round(float(np.min(e2e)), 3),
                       "encode_ms": round(float(np.median(enc)), 3), "upload_ms": round(float(np.median(upl)), 3),
                       "pods_for_deletion_ms": round(pfd_ms, 3), "reps": len(e2e), "host_threads": host_threads(),
-                      "span": "sr_plan_prepare (encode + H2D) + sr_plan_run, snapshot and candidate lists on host"}
+                      "span": "sr_plan_prepare (encode + H2D) + sr_plan_run, snapshot and candidate lists on host",
+                      "full_tick_median_ms": round(float(np.median(full_tick)), 3) if full_tick else None,
+                      "full_tick_span": "cluster arrays -> sr_new_node_map -> sr_pods_for_deletion -> "
+                                        "sr_snapshot_create -> sr_plan_prepare -> sr_plan_run"}
 
     if rank == 0:
         alg = {"k2_placement": tm.bytes_placement, "k0_tables": tm.bytes_tables}[dom]
