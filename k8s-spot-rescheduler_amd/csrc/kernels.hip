@@ -674,18 +674,27 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   }
   uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
 
-  // F heads of pods [0, dead): lanes = 8 pods x 8 words, two such batches per step
+  // F heads of pods [0, dead): lanes = 8 pods x 8 words, kPB such batches per
+  // step with all their loads in flight together (one memory round trip per
+  // 8 * kPB pods)
   {
+#ifndef SR_K2_PROLOGUE_BATCHES
+#define SR_K2_PROLOGUE_BATCHES 4
+#endif
+    constexpr int kPB = SR_K2_PROLOGUE_BATCHES;
     const int sub = lane >> 3, wd = lane & 7;
     const bool wv = wd < Wp;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      for (int b0 = 64 * g; b0 < min(dead, 64 * g + 64); b0 += 16) {
-        uint64_t x[2][4];
-        int kk[2];
+      const int lim = min(dead, 64 * g + 64);
+      for (int b0 = 64 * g; b0 < lim; b0 += 8 * kPB) {
+        uint64_t x[kPB][4];
+        int kk[kPB];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < kPB; ++h) {
           kk[h] = b0 + 8 * h + sub;
+          x[h][0] = x[h][1] = x[h][2] = x[h][3] = 0;
+          if (b0 + 8 * h >= lim) continue;  // wave-uniform
           const int src = min(kk[h], np - 1) - 64 * g;  // lane of that pod in group g
           const uint32_t o0 = from_lane(static_cast<uint32_t>(r01[g]), src);
           const uint32_t o1 = from_lane(static_cast<uint32_t>(r01[g] >> 32), src);
@@ -698,7 +707,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
           x[h][3] = tab[o3 + wi];
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < kPB; ++h) {
+          if (b0 + 8 * h >= lim) continue;  // wave-uniform
           const uint64_t f = (wv && kk[h] < np) ? (x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
           if (kk[h] < np) F[kk[h] * kNHS + wd] = f;
           const uint64_t m = ballot(f != 0);  // 8 bits per pod: bit 8 * i + word

@@ -183,11 +183,15 @@ def load_planner():
     global _planner
     if _planner is not None:
         return _planner
-    if not os.path.exists(PLANNER_LIB):
+    path = PLANNER_LIB
+    alt = os.environ.get("SR_PLANNER_LIB")  # same-box A/B of two builds (tools/gpu_ab.sh): an in-tree variant
+    if alt:
+        path = os.path.join(os.path.dirname(PLANNER_LIB), os.path.basename(alt))
+    if not os.path.exists(path):
         raise PlannerLibraryMissing(
             "%s is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
-            "(the planner has no CPU fallback)" % PLANNER_LIB)
-    lib = ctypes.CDLL(PLANNER_LIB)
+            "(the planner has no CPU fallback)" % path)
+    lib = ctypes.CDLL(path)
     _declare_planner(lib)
     _planner = lib
     return lib
