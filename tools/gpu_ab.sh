@@ -1,6 +1,8 @@
 #!/bin/bash
 # A/B of planner variants in ONE GPU session (same box, same clocks):
 #   tools/gpu_ab.sh tag "ENV=val ..." "ENV=val ..." ...   (each arm run twice, interleaved)
+# Two builds: `make -C k8s-spot-rescheduler_amd ab AB_FLAGS=-DNAME=value` builds
+# lib/libsrplanner_ab.so; the arm SR_PLANNER_LIB=libsrplanner_ab.so loads it.
 tag=$1; shift
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 2
 out="$R/gpurun_out/$tag"; mkdir -p "$out"
