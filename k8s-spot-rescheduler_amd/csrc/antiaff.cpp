@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstring>
+#include <unordered_map>
 
 #include "host.hpp"
 #include "pool.hpp"
@@ -187,69 +188,113 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
   std::vector<Term> terms(static_cast<size_t>(T));
   for (int32_t t = 0; t < T; ++t) terms[t] = parse_term(dict.data(t));
 
-  // ---- topology values of every spot node per term; node-local keys
-  std::vector<int32_t> tval(static_cast<size_t>(T) * n_spot, INT_MIN);
-  at.node_local.assign(static_cast<size_t>(T), 0);
-  parallel_for(static_cast<size_t>(T), 1, [&](size_t lo, size_t hi) {
-    std::vector<int32_t> seen;
-    for (size_t t = lo; t < hi; ++t) {
-      bool all = true;
-      seen.clear();
+  // ---- topology keys (few distinct: hostname, zone, ...): each spot node's
+  // value, the nodes of every value, node-local keys (every node carries the
+  // key, values pairwise distinct)
+  struct Key {
+    int32_t key;
+    std::vector<int32_t> val;                                 // [n_spot], INT_MIN: absent
+    std::unordered_map<int32_t, std::vector<int32_t>> nodes;  // value -> spot nodes
+    bool node_local = true;
+  };
+  std::vector<Key> keys;
+  std::vector<int32_t> kidx(static_cast<size_t>(T));
+  {
+    std::unordered_map<int32_t, int32_t> key_of;
+    for (int32_t t = 0; t < T; ++t) {
+      auto ins = key_of.emplace(terms[t].tk, static_cast<int32_t>(keys.size()));
+      if (ins.second) keys.push_back(Key{terms[t].tk, {}, {}, true});
+      kidx[t] = ins.first->second;
+    }
+  }
+  parallel_for(keys.size(), 1, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      Key& K = keys[k];
+      K.val.assign(static_cast<size_t>(n_spot), INT_MIN);
       for (int32_t n = 0; n < n_spot; ++n) {
         for (const auto& kv : snap->nodes[n].labels)
-          if (kv.first == terms[t].tk) {
-            tval[t * n_spot + n] = kv.second;
+          if (kv.first == K.key) {
+            K.val[n] = kv.second;
             break;
           }
-        if (tval[t * n_spot + n] == INT_MIN) all = false;
-        else seen.push_back(tval[t * n_spot + n]);
+        if (K.val[n] == INT_MIN) {
+          K.node_local = false;
+          continue;
+        }
+        std::vector<int32_t>& ns = K.nodes[K.val[n]];
+        ns.push_back(n);
+        if (ns.size() > 1) K.node_local = false;
       }
-      std::sort(seen.begin(), seen.end());
-      at.node_local[t] = all && std::adjacent_find(seen.begin(), seen.end()) == seen.end();
     }
   });
+  at.node_local.assign(static_cast<size_t>(T), 0);
+  for (int32_t t = 0; t < T; ++t) at.node_local[t] = keys[kidx[t]].node_local;
+
+  // ---- which terms select a pod: an index on each term's first MatchLabels
+  // pair (a pod can only be selected through one of its own labels); terms
+  // without MatchLabels are tried on every pod, nil selectors never
+  std::unordered_map<uint64_t, std::vector<int32_t>> by_label;
+  std::vector<int32_t> unindexed;
+  auto label_key = [](int32_t k, int32_t v) { return static_cast<uint64_t>(static_cast<uint32_t>(k)) << 32 | static_cast<uint32_t>(v); };
+  for (int32_t t = 0; t < T; ++t) {
+    if (terms[t].nil) continue;
+    if (terms[t].ml.empty()) unindexed.push_back(t);
+    else by_label[label_key(terms[t].ml[0].first, terms[t].ml[0].second)].push_back(t);
+  }
+  auto for_each_selecting = [&](int32_t pod, auto&& f) {
+    for (int32_t t : unindexed)
+      if (term_selects(terms[t], A, pod)) f(t);
+    for (int32_t i = A.label_off[pod]; i < A.label_off[pod + 1]; ++i) {
+      auto it = by_label.find(label_key(A.label_key[i], A.label_val[i]));
+      if (it == by_label.end()) continue;
+      for (int32_t t : it->second)
+        if (term_selects(terms[t], A, pod)) f(t);
+    }
+  };
 
   // ---- domains of the base pods: SA(t) values hosting a pod that has t,
   // SB(t) values hosting a pod t selects
   std::vector<std::vector<int32_t>> sa(static_cast<size_t>(T)), sb(static_cast<size_t>(T));
   for (const auto& nt : base_has) {
-    const int32_t v = tval[static_cast<size_t>(nt.second) * n_spot + nt.first];
+    const int32_t v = keys[kidx[nt.second]].val[nt.first];
     if (v != INT_MIN) sa[nt.second].push_back(v);
   }
-  parallel_for(static_cast<size_t>(T), 1, [&](size_t lo, size_t hi) {
-    for (size_t t = lo; t < hi; ++t)
-      for (int32_t n = 0; n < n_spot; ++n) {
-        const int32_t v = tval[t * n_spot + n];
-        if (v == INT_MIN) continue;
-        for (int32_t e : snap->state[n].pods)
-          if (term_selects(terms[t], A, e)) {
-            sb[t].push_back(v);
-            break;
-          }
-      }
-  });
+  {
+    constexpr size_t kNodes = 64;
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> part((static_cast<size_t>(n_spot) + kNodes - 1) / kNodes);
+    parallel_for(part.size(), 1, [&](size_t lo, size_t hi) {
+      for (size_t ch = lo; ch < hi; ++ch)
+        for (int32_t n = static_cast<int32_t>(ch * kNodes); n < std::min<int32_t>(n_spot, (ch + 1) * kNodes); ++n)
+          for (int32_t e : snap->state[n].pods)
+            for_each_selecting(e, [&](int32_t t) {
+              const int32_t v = keys[kidx[t]].val[n];
+              if (v != INT_MIN) part[ch].emplace_back(t, v);
+            });
+    });
+    for (const auto& pc : part)
+      for (const auto& tv : pc) sb[tv.first].push_back(tv.second);
+  }
   at.da.assign(static_cast<size_t>(T) * Wp, 0);
   at.db.assign(static_cast<size_t>(T) * Wp, 0);
   at.da_any.assign(static_cast<size_t>(T), 0);
   at.db_any.assign(static_cast<size_t>(T), 0);
-  for (int32_t t = 0; t < T; ++t) {
-    for (auto* s : {&sa[t], &sb[t]}) {
-      std::sort(s->begin(), s->end());
-      s->erase(std::unique(s->begin(), s->end()), s->end());
-    }
-    for (int32_t n = 0; n < n_spot; ++n) {
-      const int32_t v = tval[static_cast<size_t>(t) * n_spot + n];
-      if (v == INT_MIN) continue;
-      if (std::binary_search(sa[t].begin(), sa[t].end(), v)) {
-        at.da[static_cast<size_t>(t) * Wp + (n >> 6)] |= 1ull << (n & 63);
-        at.da_any[t] = 1;
+  parallel_for(static_cast<size_t>(T), 8, [&](size_t lo, size_t hi) {
+    for (size_t t = lo; t < hi; ++t) {
+      const Key& K = keys[kidx[t]];
+      for (int side = 0; side < 2; ++side) {
+        std::vector<int32_t>& s = side ? sb[t] : sa[t];
+        std::sort(s.begin(), s.end());
+        s.erase(std::unique(s.begin(), s.end()), s.end());
+        uint64_t* row = (side ? at.db.data() : at.da.data()) + t * Wp;
+        for (int32_t v : s) {
+          auto it = K.nodes.find(v);
+          if (it == K.nodes.end()) continue;
+          for (int32_t n : it->second) row[n >> 6] |= 1ull << (n & 63);
+        }
+        (side ? at.db_any : at.da_any)[t] = !s.empty();
       }
-      if (std::binary_search(sb[t].begin(), sb[t].end(), v)) {
-        at.db[static_cast<size_t>(t) * Wp + (n >> 6)] |= 1ull << (n & 63);
-        at.db_any[t] = 1;
-      }
     }
-  }
+  });
 
   // ---- per pending candidate pod: ids t << 1 (t selects it) | t << 1 | 1 (it has t)
   std::vector<std::vector<int32_t>> ids(static_cast<size_t>(n_flat));
@@ -259,8 +304,7 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
         const int32_t pod = cands->cand_pods[j];
         std::vector<int32_t>& v = ids[j];
-        for (int32_t t = 0; t < T; ++t)
-          if (term_selects(terms[t], A, pod)) v.push_back(t << 1);
+        for_each_selecting(pod, [&](int32_t t) { v.push_back(t << 1); });
         for (int32_t t : has[j]) v.push_back(t << 1 | 1);
         std::sort(v.begin(), v.end());
       }

@@ -417,3 +417,40 @@ def test_rccl_single_rank_collective_path_matches(checker):
     finally:
         comm_checker.close()
         lib.sr_snapshot_destroy(h)
+
+
+def test_many_deployments_with_hostname_anti_affinity(checker):
+    """A cluster shaped like production anti-affinity use: 120 Deployments,
+    each spreading its replicas one per host (required anti-affinity on
+    kubernetes.io/hostname selecting its own app label), on spot and
+    on-demand nodes alike; some Deployments also keep away from a database.
+    Exercises the term index, the static DA/DB sets and the state-bit pairs
+    with many distinct terms (more than the 32 pairs: candidates needing more
+    fall back, the rest must match the oracle)."""
+    import random
+    from spotplanner.model import LabelSelector, PodAffinityTerm
+    HOST = "kubernetes.io/hostname"
+    r = random.Random(77)
+    nodes = [Node(name="n%d" % i, cpu_milli=r.choice([2000, 4000, 8000]), memory=64 * GiB, pods=110,
+                  labels={HOST: "n%d" % i}) for i in range(150)]
+
+    def replica(app, i):
+        anti = [PodAffinityTerm(HOST, LabelSelector({"app": app}))]
+        if r.random() < 0.2:
+            anti.append(PodAffinityTerm(HOST, LabelSelector({"app": "db"})))
+        return Pod(name="%s-%d" % (app, i), namespace="default", labels={"app": app},
+                   containers=[Container(cpu_milli=r.choice([100, 250, 500]), memory=r.choice([1, 2]) * GiB)],
+                   pod_anti_affinity=anti if r.random() < 0.9 else None)
+
+    apps = ["app%d" % k for k in range(120)] + ["db"]
+    hot = apps[:10]  # the Deployments being drained also crowd the first spot nodes
+    spot_pods = [[] for _ in nodes]
+    for n in range(len(nodes)):
+        for k in range(r.randint(4, 12)):
+            spot_pods[n].append(replica(r.choice(hot if r.random() < 0.6 else apps), 100 * n + k))
+    cands = []
+    for c in range(60):  # 1-3 Deployments per on-demand node, 2-5 replicas each
+        cands.append([replica(a, 100000 + 100 * c + 10 * j + k) for j, a in enumerate(r.sample(hot, r.randint(1, 3)))
+                      for k in range(r.randint(2, 5))])
+    _, o, p = run_scenario(checker, nodes, spot_pods, cands)
+    assert len(set(int(x) for x in p.node_of_pod if x >= 0)) > 8  # conflicts push replicas past the first nodes
