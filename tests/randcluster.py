@@ -91,8 +91,8 @@ APPS = ["web", "db", "cache"]
 NAMESPACES = ["default", "default", "other"]
 
 
-def rand_selector(r: random.Random):
-    k = r.random()
+def rand_selector(r: random.Random, valid_only: bool = False):
+    k = r.random() * (0.95 if valid_only else 1.0)
     if k < 0.55:
         return LabelSelector({"app": r.choice(APPS)})
     if k < 0.75:
@@ -107,7 +107,7 @@ def rand_selector(r: random.Random):
     return LabelSelector({}, [LabelSelectorRequirement("tier", "In", [])])  # invalid: fallback
 
 
-def rand_anti(r: random.Random, p: Pod, rate: float):
+def rand_anti(r: random.Random, p: Pod, rate: float, hostname_only: bool = False):
     """Labels and namespace for every pod; required anti-affinity for some.
     Topology keys: the hostname (node-local) mostly, zone / team (shared or
     missing on some nodes) otherwise."""
@@ -118,15 +118,16 @@ def rand_anti(r: random.Random, p: Pod, rate: float):
     if r.random() < rate:
         p.pod_anti_affinity = []
         for _ in range(r.randint(1, 2)):
-            tk = HOST if r.random() < 0.7 else r.choice(["zone", "team"])
+            tk = HOST if hostname_only or r.random() < 0.7 else r.choice(["zone", "team"])
             ns = [] if r.random() < 0.7 else r.sample(["default", "other"], r.randint(1, 2))
-            p.pod_anti_affinity.append(PodAffinityTerm(tk, rand_selector(r), ns))
+            p.pod_anti_affinity.append(PodAffinityTerm(tk, rand_selector(r, hostname_only), ns))
 
 
 def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 8, features: bool = True,
-                  fallback: bool = False, anti: float = 0.0):
+                  fallback: bool = False, anti: float = 0.0, hostname_only: bool = False):
     """Returns (spot_nodes, spot_pods, candidates) with candidates a list of pod lists.
-    anti > 0: pods carry namespaces / labels and that share required pod anti-affinity."""
+    anti > 0: pods carry namespaces / labels and that share required pod anti-affinity
+    (hostname_only: every term on kubernetes.io/hostname with a valid selector)."""
     r = random.Random(seed)
     nodes = [rand_node(r, "n%d" % i, features) for i in range(n_spot)]
     spot_pods = []
@@ -140,7 +141,7 @@ def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 
     if anti > 0:
         for ps in spot_pods + cands:
             for p in ps:
-                rand_anti(r, p, anti)
+                rand_anti(r, p, anti, hostname_only)
     return nodes, spot_pods, cands
 
 

@@ -254,6 +254,14 @@ def test_random_large_candidates(checker, seed):
     run_scenario(checker, nodes, spot_pods, cands)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_random_large_candidates_with_pod_anti_affinity(checker, seed):
+    # the state-bit pairs through 2 and 4 pod groups and the pod-order path
+    nodes, spot_pods, cands = rand_scenario(5100 + seed, n_spot=40 + 10 * seed, n_cand=4, max_pods=70 + 66 * seed,
+                                            features=False, anti=0.15, hostname_only=True)
+    run_scenario(checker, nodes, spot_pods, cands, extra_fallback=lambda c: anti_interacts_off_node(nodes, cands[c]))
+
+
 def test_pod_order_mode_matches_oracle():
     # SR_K2_MODE=1 forces K2's pod-order path everywhere (the A/B arm of the bench)
     import os
@@ -267,6 +275,11 @@ def test_pod_order_mode_matches_oracle():
         for seed in range(6):
             nodes, spot_pods, cands = rand_scenario(6000 + seed, n_spot=8 + 7 * seed, n_cand=8, max_pods=12)
             run_scenario(c, nodes, spot_pods, cands)
+        for seed in range(10):  # anti-affinity state bits through the pod-order placement
+            nodes, spot_pods, cands = rand_scenario(6100 + seed, n_spot=8 + 3 * seed, n_cand=10, max_pods=10,
+                                                    anti=0.5)
+            run_scenario(c, nodes, spot_pods, cands,
+                         extra_fallback=lambda k: anti_interacts_off_node(nodes, cands[k]))
         tick_parity(c, SynthCluster(3, seed=13, n_on_demand=300, n_spot=900))
     finally:
         c.close()
