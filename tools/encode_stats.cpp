@@ -61,6 +61,7 @@ int main(int argc, char** argv) {
   printf("fine(ms): pass1 %.2f ports+taints %.2f | atoms-nodes %.2f atoms-reqs %.2f | lb+recs %.2f empty %.2f trows %.2f ranks %.2f recoffs %.2f\n",
          sr::encode_phase_ms[8], sr::encode_phase_ms[1], sr::encode_phase_ms[9], sr::encode_phase_ms[4],
          sr::encode_phase_ms[10], sr::encode_phase_ms[11], sr::encode_phase_ms[12], sr::encode_phase_ms[13], sr::encode_phase_ms[5]);
+  printf("keys split: gather+hash %.3f shards %.3f merge %.3f\n", sr::encode_phase_ms[14], sr::encode_phase_ms[15], sr::encode_phase_ms[7]);
   printf("Wp %d atoms %d classes %d program ops %zu t_rows %zu\n", w.Wp, w.n_atoms, w.n_classes, w.cls_prog.size(),
          w.t_dim.size());
   int tc[4] = {0, 0, 0, 0};
