@@ -18,12 +18,14 @@
 //  - dynamic part, between the pods of one candidate: a term through which
 //    two of its pods interact must have a node-local topology key (every spot
 //    node carries it, values pairwise distinct, e.g. kubernetes.io/hostname);
-//    it then gets a pair of state bits (A: a pod having t is here, B: a pod
-//    t selects is here).  A pod sets A for its terms and B for the terms
-//    selecting it; it conflicts with a node whose state holds B for its
-//    terms or A for the terms selecting it -- the pair-swapped image of what
-//    it sets.  K2 keeps these bits with the host-port bits.  Interaction
-//    through any other key routes the candidate to the fallback path.
+//    it then gets a pair of state bits of that candidate's own numbering (A:
+//    a pod having t is here, B: a pod t selects is here).  A pod sets A for
+//    its terms and B for the terms selecting it; it conflicts with a node
+//    whose state holds B for its terms or A for the terms selecting it -- the
+//    pair-swapped image of what it sets.  K2 keeps these bits with the
+//    host-port bits; the base snapshot needs none (its conflicts are the
+//    static part).  Interaction through any other key routes the candidate
+//    to the fallback path.
 #include <algorithm>
 #include <climits>
 #include <cstring>
@@ -312,60 +314,64 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
   });
 
   // ---- interactions inside each candidate: terms one pod has and another
-  // pod matches.  Node-local ones get a bit pair (first come, at most 32);
-  // any other interaction routes the candidate to the fallback path.
-  at.pair_of.assign(static_cast<size_t>(T), -1);
-  std::vector<int32_t> nh(static_cast<size_t>(T)), nm(static_cast<size_t>(T)), nb(static_cast<size_t>(T));
-  std::vector<int32_t> touched;
-  for (int32_t i = 0; i < nc; ++i) {
-    if (status[i] != STATUS_PENDING) continue;
-    touched.clear();
-    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
-      const std::vector<int32_t>& v = ids[j];
-      for (size_t k = 0; k < v.size(); ++k) {
-        const int32_t t = v[k] >> 1;
-        if (nh[t] == 0 && nm[t] == 0) touched.push_back(t);
-        if (v[k] & 1) {
-          ++nh[t];
-          if (k > 0 && v[k - 1] == (t << 1)) ++nb[t];  // sorted: "selects" precedes "has"
-        } else {
-          ++nm[t];
+  // pod matches.  Node-local ones get a bit pair of the candidate's own (the
+  // state is per candidate; base conflicts are in the F rows already), at most
+  // 32; any other interaction routes the candidate to the fallback path.
+  at.pod_bits.assign(static_cast<size_t>(n_flat), 0);
+  std::vector<int32_t> pairs(static_cast<size_t>(nc), 0);
+  parallel_for(static_cast<size_t>(nc), 16, [&](size_t lo, size_t hi) {
+    std::vector<int32_t> nh(static_cast<size_t>(T)), nm(static_cast<size_t>(T)), nb(static_cast<size_t>(T));
+    std::vector<int32_t> pair(static_cast<size_t>(T), -1), touched, need;
+    for (size_t i = lo; i < hi; ++i) {
+      if (status[i] != STATUS_PENDING) continue;
+      touched.clear();
+      need.clear();
+      for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+        const std::vector<int32_t>& v = ids[j];
+        for (size_t k = 0; k < v.size(); ++k) {
+          const int32_t t = v[k] >> 1;
+          if (nh[t] == 0 && nm[t] == 0) touched.push_back(t);
+          if (v[k] & 1) {
+            ++nh[t];
+            if (k > 0 && v[k - 1] == (t << 1)) ++nb[t];  // sorted: "selects" precedes "has"
+          } else {
+            ++nm[t];
+          }
         }
       }
-    }
-    bool fb = false;
-    std::vector<int32_t> need;
-    for (int32_t t : touched) {
-      const bool interacts = nh[t] >= 1 && nm[t] >= 1 && !(nh[t] == 1 && nm[t] == 1 && nb[t] == 1);
-      if (interacts) {
-        if (!at.node_local[t]) fb = true;
-        else if (at.pair_of[t] < 0) need.push_back(t);
+      bool fb = false;
+      std::sort(touched.begin(), touched.end());
+      for (int32_t t : touched) {
+        const bool interacts = nh[t] >= 1 && nm[t] >= 1 && !(nh[t] == 1 && nm[t] == 1 && nb[t] == 1);
+        if (interacts) {
+          if (!at.node_local[t]) fb = true;
+          else need.push_back(t);
+        }
+        nh[t] = nm[t] = nb[t] = 0;
       }
-      nh[t] = nm[t] = nb[t] = 0;
+      if (fb || need.size() > 32) {
+        status[i] = SR_CAND_FALLBACK;
+        continue;
+      }
+      for (size_t p = 0; p < need.size(); ++p) pair[need[p]] = static_cast<int32_t>(p);
+      for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+        uint64_t bits = 0;
+        for (int32_t id : ids[j]) {
+          const int32_t p = pair[id >> 1];
+          if (p >= 0) bits |= 1ull << (2 * p + ((id & 1) ? 0 : 1));  // A: it has t, B: t selects it
+        }
+        at.pod_bits[j] = bits;
+      }
+      for (int32_t t : need) pair[t] = -1;
+      pairs[i] = static_cast<int32_t>(need.size());
     }
-    if (!fb && at.n_pairs + static_cast<int32_t>(need.size()) > 32) fb = true;
-    if (fb) {
-      status[i] = SR_CAND_FALLBACK;
-      continue;
-    }
-    for (int32_t t : need) at.pair_of[t] = at.n_pairs++;
-  }
+  });
+  for (int32_t i = 0; i < nc; ++i) at.n_pairs = std::max(at.n_pairs, pairs[i]);
 
-  // ---- CSR of the ids; base pair bits per node
+  // ---- CSR of the ids
   for (int32_t j = 0; j < n_flat; ++j) at.pod_off[j + 1] = at.pod_off[j] + static_cast<int32_t>(ids[j].size());
   at.pod_ids.reserve(static_cast<size_t>(at.pod_off[n_flat]));
   for (int32_t j = 0; j < n_flat; ++j) at.pod_ids.insert(at.pod_ids.end(), ids[j].begin(), ids[j].end());
-  at.base_bits.assign(static_cast<size_t>(n_spot), 0);
-  for (int32_t t = 0; t < T; ++t) {
-    const int32_t p = at.pair_of[t];
-    if (p < 0) continue;
-    for (int32_t n = 0; n < n_spot; ++n) {
-      const size_t wi = static_cast<size_t>(t) * Wp + (n >> 6);
-      const uint64_t bit = 1ull << (n & 63);
-      if (at.da[wi] & bit) at.base_bits[n] |= 1ull << (2 * p);
-      if (at.db[wi] & bit) at.base_bits[n] |= 1ull << (2 * p + 1);
-    }
-  }
 }
 
 }  // namespace sr

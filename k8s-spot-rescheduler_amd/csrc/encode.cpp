@@ -422,7 +422,6 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     std::vector<int32_t> untol;  // taint ids the spec does not tolerate
     uint64_t ports = 0;          // host ports (dictionary bits)
     std::vector<int32_t> anti_da, anti_db;  // anti-affinity terms: ANDNOT DA(t) / DB(t)
-    uint64_t anti_bits = 0;      // state-bit pairs the pod sets (A for terms it has, B for terms selecting it)
   };
   std::vector<SpecCanon> canon(n_specs);
   auto put_req = [](std::vector<int32_t>& out, int32_t type, int32_t key, int32_t op, const int32_t* v, int32_t nv) {
@@ -488,13 +487,11 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       if (anti.active) {
         const int32_t j = active_src[spec_rep_q[sp]];
         for (int32_t k = anti.pod_off[j]; k < anti.pod_off[j + 1]; ++k) {
-          const int32_t t = anti.pod_ids[k] >> 1, p = anti.pair_of[t];
+          const int32_t t = anti.pod_ids[k] >> 1;
           if (anti.pod_ids[k] & 1) {  // it has t: refuses domains hosting pods t selects
             if (anti.db_any[t]) sc.anti_db.push_back(t);
-            if (p >= 0) sc.anti_bits |= 1ull << (2 * p);
           } else {  // t selects it: refused by domains hosting pods that have t
             if (anti.da_any[t]) sc.anti_da.push_back(t);
-            if (p >= 0) sc.anti_bits |= 1ull << (2 * p + 1);
           }
         }
       }
@@ -638,7 +635,8 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       auto it = port_dict.find(port_key(u.proto, u.port));
       if (it != port_dict.end()) pb |= 1ull << it->second;  // incoming pods bind 0.0.0.0
     }
-    w->port_bits[n] = (bit_shift < 64 ? pb << bit_shift : 0) | (anti.active ? anti.base_bits[n] : 0);
+    // base state: host ports only (base anti-affinity conflicts are static, in the F rows)
+    w->port_bits[n] = bit_shift < 64 ? pb << bit_shift : 0;
     for (int32_t b = 0; b < 64; ++b)
       if (pb >> b & 1) set_atom(A_PORT + b, n);
     for (int32_t k = node_taint_off[n]; k < node_taint_off[n + 1]; ++k) set_atom(A_TAINT + node_taint_ids[k], n);
@@ -800,7 +798,8 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       rec[0] = static_cast<uint64_t>(rc);
       rec[1] = static_cast<uint64_t>(rm);
       rec[2] = static_cast<uint64_t>(re);
-      rec[3] = (bit_shift < 64 ? canon[pod_spec[q]].ports << bit_shift : 0) | canon[pod_spec[q]].anti_bits;
+      rec[3] = (bit_shift < 64 ? canon[pod_spec[q]].ports << bit_shift : 0) |
+               (anti.active ? anti.pod_bits[active_src[q]] : 0);
       bool dead = cls_empty[r[0]] != 0;
       for (int d = 0; d < 3; ++d) dead = dead || (r[1 + d] >= 0 && static_cast<size_t>(r[1 + d]) == node_vals[d].size());
       if (dead) {

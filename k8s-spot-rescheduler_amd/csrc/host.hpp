@@ -169,9 +169,9 @@ struct AntiTerms {
   std::vector<uint64_t> da, db;          // [term][Wp] base conflicts: pods having / selected by the term
   std::vector<uint8_t> da_any, db_any;   // [term] the set is not empty
   std::vector<int32_t> pod_off, pod_ids; // [flat candidate pod + 1] -> ids: term << 1 (selects it) | 1 (it has)
-  std::vector<int32_t> pair_of;          // [term] state-bit pair (A = 2p, B = 2p + 1) or -1
-  int32_t n_pairs = 0;
-  std::vector<uint64_t> base_bits;       // [spot node] pair bits of the base snapshot
+  std::vector<uint64_t> pod_bits;         // [flat candidate pod] state-bit pairs it sets, numbered per
+                                         // candidate (A = 2p: it has term p, B = 2p + 1: term p selects it)
+  int32_t n_pairs = 0;                   // most pairs any candidate uses (<= 32)
 };
 
 // Collects the terms of the snapshot's pods and of the pending candidates,
