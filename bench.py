@@ -49,7 +49,24 @@ def host_threads():
     return max(1, int(env)) if env else min(16, os.cpu_count() or 1)
 
 
-def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, seconds):
+def plan_parity(o, gpu_status, gpu_nodes, cand_off):
+    """Same rule as tests/test_gpu_parity.compare_plans: every candidate the
+    device evaluates has the oracle's status and, pod by pod, the oracle's
+    spot node; a candidate the device flags SR_CAND_FALLBACK goes to the
+    reference path (rescheduler.go:357-370 on the host), so its oracle result
+    is the tick's result.  Returns (identical, n_fallback, fallback pods)."""
+    fb = gpu_status == capi.SR_CAND_FALLBACK
+    ok = bool(np.all(fb | (gpu_status == o["status"])))
+    for c in np.flatnonzero(~fb):
+        seg = slice(int(cand_off[c]), int(cand_off[c + 1]))
+        if not np.array_equal(gpu_nodes[seg], o["node_of_pod"][seg]):
+            ok = False
+            break
+    n_fb_pods = int(np.sum(np.diff(cand_off)[fb])) if fb.any() else 0
+    return ok, int(fb.sum()), n_fb_pods
+
+
+def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, seconds):
     """The oracle (C restatement of the reference planner) on this host, rank 0 only."""
     from oracle_lib import OracleSnapshot, oracle_plan
     snap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
@@ -71,7 +88,7 @@ def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, seconds):
         mt.append(time.perf_counter() - t0)
     ms_mt = 1e3 * float(np.median(mt))
     dense = float(len(cand_pods)) * n_spot
-    parity = bool(np.array_equal(res["status"], gpu_status))
+    parity, n_fb, n_fb_pods = plan_parity(res, gpu_status, gpu_nodes, cand_off)
     return {"value": dense / (ms_all / 1e3), "unit": "checks/s", "cores": 1, "kind": "port",
             "sample": "full tick: all %d candidates / %d pods x %d spot nodes, median of %d runs (%.1f s)"
                       % (len(cand_off) - 1, len(cand_pods), n_spot, len(times), sum(times)),
@@ -80,7 +97,11 @@ def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, seconds):
             "reference_faithful_first_ok": int(early["first_ok"]),
             "ms_per_tick_all_candidates_%dcores" % threads: round(ms_mt, 3),
             "issued_checks_per_tick": int(res["checks"]),
-            "plans_identical_to_gpu": parity}
+            "plans_identical_to_gpu": parity,
+            "parity_rule": "device-evaluated candidates: status + every pod's node equal to the oracle; "
+                           "fallback candidates take the reference path",
+            "fallback_candidates": n_fb, "fallback_candidate_pods": n_fb_pods,
+            "fallback_ratio": round(n_fb / max(1, len(cand_off) - 1), 4)}
 
 
 def main():
@@ -273,6 +294,7 @@ def main():
                        "spot_nodes": int(len(nm.spot)), "candidates": int(len(cand_off) - 1),
                        "candidate_pods": int(len(cand_pods)), "parallelism": "candidates c%%%d" % world},
             "first_ok": int(out.first_ok), "winner": int(out.winner),
+            "fallback_candidates": int(np.sum(status[:len(loff) - 1] == capi.SR_CAND_FALLBACK)),
             "kernels_ms": {kk: round(v, 5) for kk, v in breakdown.items()},
             "workload_rows": {"static_classes": tm.n_rows_static, "threshold_rows": tm.n_rows_threshold,
                               "words_per_row": tm.n_words},
@@ -286,7 +308,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(sc, nm, cand_off, cand_pods, int(len(nm.spot)), status[:len(loff) - 1],
-                                                args.cpu_seconds)
+                                                nodes_out[:len(lpods)], args.cpu_seconds)
         print(json.dumps(line), flush=True)
     lib.sr_snapshot_destroy(snap)
     checker.close()

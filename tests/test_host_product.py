@@ -309,3 +309,25 @@ def test_snapshot_fork_revert_host():
     assert req[0] == 300 and n.value == 1
     assert lib.sr_snapshot_revert(h) == capi.SR_OK
     lib.sr_snapshot_destroy(h)
+
+
+def test_bench_plan_parity_rule():
+    # bench.py's cpu_baseline parity: fallback candidates are the reference path's,
+    # every device-evaluated candidate must match the oracle pod by pod.
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    FB, OK = capi.SR_CAND_FALLBACK, capi.SR_CAND_OK
+    cand_off = np.array([0, 2, 3, 5], np.int32)
+    o = {"status": np.array([OK, 0, OK], np.int32), "node_of_pod": np.array([1, 2, -1, 0, 0], np.int32)}
+    gpu_nodes = np.array([1, 2, -1, 0, 0], np.int32)
+    assert bench.plan_parity(o, np.array([OK, 0, OK], np.int32), gpu_nodes, cand_off) == (True, 0, 0)
+    assert bench.plan_parity(o, np.array([OK, FB, OK], np.int32), gpu_nodes, cand_off) == (True, 1, 1)
+    assert not bench.plan_parity(o, np.array([OK, 0, FB + 10], np.int32), gpu_nodes, cand_off)[0]
+    bad = gpu_nodes.copy()
+    bad[4] = 1
+    assert not bench.plan_parity(o, np.array([OK, 0, OK], np.int32), bad, cand_off)[0]
+    assert bench.plan_parity(o, np.array([OK, 0, FB], np.int32), bad, cand_off) == (True, 1, 2)
