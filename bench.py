@@ -6,9 +6,11 @@ One step = one housekeeping tick's planning segment on device-resident inputs:
 K0 tables -> K2 feasibility rows + first-fit placement of every candidate ->
 [RCCL allreduce(min) for N>1] -> K3 winner mapping into mapped host memory.
 ms_per_step is therefore the drain-plan latency with inputs in HBM; `value` is
-dense-equivalent (pod, spot node) checks per second over all ranks: every
-candidate pod x every spot node, the work the reference's loop would do to
-plan every candidate of the tick.
+reference-equivalent (pod, spot node) predicate checks per second over all
+ranks: the CheckPredicates calls (rescheduler.go:344) the reference's loop
+makes to reach the same plan of every candidate (findSpotNodeForPod stops at
+the first fit).  The dense-equivalent rate (every candidate pod x every spot
+node) is reported beside it, labelled as such.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
 
@@ -66,7 +68,7 @@ def plan_parity(o, gpu_status, gpu_nodes, cand_off):
     return ok, int(fb.sum()), n_fb_pods
 
 
-def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, seconds):
+def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, gpu_checks, seconds):
     """The oracle (C restatement of the reference planner) on this host, rank 0 only."""
     from oracle_lib import OracleSnapshot, oracle_plan
     snap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
@@ -89,7 +91,10 @@ def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, sec
     ms_mt = 1e3 * float(np.median(mt))
     dense = float(len(cand_pods)) * n_spot
     parity, n_fb, n_fb_pods = plan_parity(res, gpu_status, gpu_nodes, cand_off)
-    return {"value": dense / (ms_all / 1e3), "unit": "checks/s", "cores": 1, "kind": "port",
+    return {"value": float(res["checks"]) / (ms_all / 1e3), "unit": "checks/s", "cores": 1, "kind": "port",
+            "host_cpus": os.cpu_count(), "host_cpus_available": len(os.sched_getaffinity(0)),
+            "value_definition": "reference-equivalent checks (issued CheckPredicates calls) / 1-core all-candidates tick",
+            "dense_equivalent_per_s": dense / (ms_all / 1e3),
             "sample": "full tick: all %d candidates / %d pods x %d spot nodes, median of %d runs (%.1f s)"
                       % (len(cand_off) - 1, len(cand_pods), n_spot, len(times), sum(times)),
             "ms_per_tick_all_candidates_1core": round(ms_all, 3),
@@ -98,6 +103,7 @@ def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, sec
             "ms_per_tick_all_candidates_%dcores" % threads: round(ms_mt, 3),
             "issued_checks_per_tick": int(res["checks"]),
             "plans_identical_to_gpu": parity,
+            "reference_equivalent_checks_match_gpu": int(res["checks"]) == int(gpu_checks),
             "parity_rule": "device-evaluated candidates: status + every pod's node equal to the oracle; "
                            "fallback candidates take the reference path",
             "fallback_candidates": n_fb, "fallback_candidate_pods": n_fb_pods,
@@ -167,6 +173,17 @@ def main():
     wmap = np.zeros(max(1, maxp), np.int32)
     out = capi.sr_plan_out()
     out.winner_map = capi.ptr(wmap, capi.P32)
+    # one run with per-candidate outputs first: K2's byte counts and the
+    # reference-equivalent check count of this workload's plan
+    status = np.zeros(max(1, len(loff) - 1), np.int32)
+    nodes_out = np.zeros(max(1, len(lpods)), np.int32)
+    full = capi.sr_plan_out()
+    full.status = capi.ptr(status, capi.P32)
+    full.node_of_pod = capi.ptr(nodes_out, capi.P32)
+    full.winner_map = capi.ptr(wmap, capi.P32)
+    st = lib.sr_plan_run(checker.handle, ctypes.byref(full))
+    assert st == capi.SR_OK, (st, checker.last_error())
+    issued_local, dense_local = float(full.checks), float(full.checks_dense)
     for _ in range(args.warmup):
         assert lib.sr_plan_run(checker.handle, ctypes.byref(out)) == capi.SR_OK, checker.last_error()
 
@@ -188,39 +205,35 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    bad = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        lib.sr_plan_run(checker.handle, ctypes.byref(out))
+        bad |= lib.sr_plan_run(checker.handle, ctypes.byref(out))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    assert bad == capi.SR_OK, (bad, checker.last_error())  # a failing run must not be timed as a fast step
     tm = checker.timing()
     dom_ms = ([tm.ms_tables, tm.ms_placement][names.index(dom)] / max(1, tm.n_runs) if not args.no_events
               else breakdown[dom])
     checker.set_timing(0)
-    local_checks = float(out.checks)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor([local_checks], dtype=torch.float64)
+        c = torch.tensor([issued_local, dense_local], dtype=torch.float64)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        total_checks = float(c.item())
+        total_issued, total_dense = float(c[0].item()), float(c[1].item())
     else:
-        total_checks = local_checks
+        total_issued, total_dense = issued_local, dense_local
     ms_step = 1e3 * elapsed / args.steps
 
-    # full per-candidate outputs once (outside the timed region) for the parity check
-    status = np.zeros(max(1, len(loff) - 1), np.int32)
-    nodes_out = np.zeros(max(1, len(lpods)), np.int32)
-    full = capi.sr_plan_out()
-    full.status = capi.ptr(status, capi.P32)
-    full.node_of_pod = capi.ptr(nodes_out, capi.P32)
-    full.winner_map = capi.ptr(wmap, capi.P32)
+    # per-candidate outputs once more (outside the timed region): the parity
+    # check and K2's byte counts of the same plan
     st = lib.sr_plan_run(checker.handle, ctypes.byref(full))
     assert st == capi.SR_OK, (st, checker.last_error())
-    tm = checker.timing()  # bytes_placement is exact after a run with per-candidate outputs
+    tm = checker.timing()
 
     # End-to-end tick in the steady state (untimed by the contract's K steps):
     # candidate lists and snapshot on the host -> encode + H2D (sr_plan_prepare)
@@ -282,9 +295,14 @@ def main():
             with open(pmc) as f:
                 traffic = json.load(f).get(dom)
         line = {
-            "metric": "pod x spot-node feasibility checks/s (drain-plan latency = ms_per_step)",
-            "value": total_checks / elapsed * args.steps if elapsed > 0 else 0.0,
+            "metric": "reference-equivalent pod x spot-node feasibility checks/s (drain-plan latency = ms_per_step)",
+            "value": total_issued / elapsed * args.steps if elapsed > 0 else 0.0,
             "unit": "checks/s",
+            "checks_per_tick": {"reference_equivalent": int(total_issued), "dense_equivalent": int(total_dense),
+                                "dense_equivalent_per_s": total_dense / elapsed * args.steps if elapsed > 0 else 0.0,
+                                "note": "reference_equivalent = CheckPredicates calls the reference loop makes for "
+                                        "the same plan of every candidate (value); dense_equivalent = candidate "
+                                        "pods x spot nodes (notional, not work done)"},
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_step, "latency_ms": ms_step,
             "plans_per_s": (len(cand_off) - 1) / (elapsed / args.steps),
@@ -304,11 +322,16 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "kernel_ms": round(dom_ms, 5),
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes": int(alg)},
+                         "algorithmic_bytes": int(alg),
+                         "bytes_definition": "bytes the kernel moves, counted by K2 per candidate (pod records, "
+                                             "F-row heads and full-row scans, 64-node record windows, outputs; "
+                                             "SURVEY 8(d) K2 formula over what is actually read)",
+                         "limiter": "latency: one dependent placement chain per candidate (one wave each); the "
+                                    "longest chain sets the kernel time, not bytes (DESIGN.md 4)"},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(sc, nm, cand_off, cand_pods, int(len(nm.spot)), status[:len(loff) - 1],
-                                                nodes_out[:len(lpods)], args.cpu_seconds)
+                                                nodes_out[:len(lpods)], issued_local, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     lib.sr_snapshot_destroy(snap)
     checker.close()

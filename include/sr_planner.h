@@ -344,12 +344,18 @@ typedef struct {
   int32_t  first_ok;        /* first candidate whose plan succeeds on the GPU; -1 none */
   int32_t  first_fallback;  /* first candidate flagged SR_CAND_FALLBACK; -1 none */
   int32_t  winner_npods;    /* pods in winner_map (0 if the winner is not local) */
-  uint64_t checks;          /* (pod, spot node) pairs evaluated by the feasibility kernel */
+  uint64_t checks;          /* CheckPredicates calls (rescheduler.go:344) the reference's loop makes to reach
+                               the same plan of the evaluated candidates: per pod its spot position + 1
+                               (findSpotNodeForPod returns at the first fit), the spot-node count for a pod
+                               that fits nowhere (canDrainNode returns there).  The device does not evaluate
+                               pairs one by one; this is the reference-equivalent work.  Known after a run
+                               with status or node_of_pod outputs since the last prepare (0 before). */
   uint64_t fallback_pods;   /* pods of fallback candidates */
   /* optional outputs (NULL = not wanted) */
   int32_t *status;          /* [n_cand] SR_CAND_* or failing pod index */
   int32_t *node_of_pod;     /* [cand_pod_off[n_cand]] spot position, -1 not placed */
   int32_t *winner_map;      /* [max pods of a candidate] spot position per pod of first_ok */
+  uint64_t checks_dense;    /* candidate pods x spot nodes of the evaluated candidates (dense-equivalent pairs) */
 } sr_plan_out;
 
 /* One housekeeping tick's planning segment (rescheduler.go:228-287): every
@@ -374,8 +380,9 @@ typedef struct {
   double   ms_pack_host;    /* last sr_plan_prepare host encoding */
   double   ms_upload;       /* last sr_plan_prepare upload */
   uint64_t bytes_tables;    /* algorithmic bytes per K0 launch */
-  uint64_t bytes_placement; /* algorithmic bytes per K2 launch: exact after a run with status or
-                               node_of_pod outputs, an upper bound (every pod processed) before */
+  uint64_t bytes_placement; /* bytes K2 moved in its last launch, counted by the kernel per candidate (records,
+                               row heads and scans, node-record windows, outputs); read back by a run with
+                               status or node_of_pod outputs (0 before) */
   int32_t  n_pods, n_spot, n_cand, n_words;
   int32_t  n_rows_static, n_rows_threshold, n_classes;
 } sr_timing;

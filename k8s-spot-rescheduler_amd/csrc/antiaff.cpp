@@ -53,7 +53,9 @@ struct Term {
   std::vector<Expr> me;
 };
 
-void term_words(const sr_cluster* c, int32_t owner, int32_t t, std::vector<int32_t>& out) {
+}  // namespace
+
+void anti_term_words(const sr_cluster* c, int32_t owner, int32_t t, std::vector<int32_t>& out) {
   const sr_pod_affinity& A = *c->pod_affinity;
   out.clear();
   out.push_back(A.topology_key[t]);
@@ -90,6 +92,8 @@ void term_words(const sr_cluster* c, int32_t owner, int32_t t, std::vector<int32
   }
 }
 
+namespace {
+
 Term parse_term(const int32_t* w) {
   Term t;
   size_t i = 0;
@@ -114,10 +118,26 @@ Term parse_term(const int32_t* w) {
   return t;
 }
 
-bool pod_label(const sr_pod_affinity& A, int32_t pod, int32_t key, int32_t* val) {
-  for (int32_t i = A.label_off[pod]; i < A.label_off[pod + 1]; ++i)
-    if (A.label_key[i] == key) {
-      *val = A.label_val[i];
+// A pod's namespace and labels, from the caller's cluster or the snapshot's copy.
+struct PodMeta {
+  int32_t ns;
+  const int32_t *key, *val;
+  int32_t n;
+};
+
+PodMeta meta_of(const sr_pod_affinity& A, int32_t pod) {
+  return PodMeta{A.ns[pod], A.label_key + A.label_off[pod], A.label_val + A.label_off[pod],
+                 A.label_off[pod + 1] - A.label_off[pod]};
+}
+
+PodMeta meta_of(const SnapPod& p) {
+  return PodMeta{p.ns, p.lkey.data(), p.lval.data(), static_cast<int32_t>(p.lkey.size())};
+}
+
+bool pod_label(const PodMeta& m, int32_t key, int32_t* val) {
+  for (int32_t i = 0; i < m.n; ++i)
+    if (m.key[i] == key) {
+      *val = m.val[i];
       return true;
     }
   return false;
@@ -126,14 +146,14 @@ bool pod_label(const sr_pod_affinity& A, int32_t pod, int32_t key, int32_t* val)
 // schedutil.PodMatchesTermsNamespaceAndSelector: namespace, then
 // labels.Selector.Matches (MatchLabels = Equals; In / NotIn / Exists /
 // DoesNotExist; nil selects nothing, empty everything).
-bool term_selects(const Term& t, const sr_pod_affinity& A, int32_t pod) {
-  if (!std::binary_search(t.ns.begin(), t.ns.end(), A.ns[pod])) return false;
+bool term_selects(const Term& t, const PodMeta& m) {
+  if (!std::binary_search(t.ns.begin(), t.ns.end(), m.ns)) return false;
   if (t.nil) return false;
   int32_t v;
   for (const auto& kv : t.ml)
-    if (!pod_label(A, pod, kv.first, &v) || v != kv.second) return false;
+    if (!pod_label(m, kv.first, &v) || v != kv.second) return false;
   for (const Expr& e : t.me) {
-    const bool has = pod_label(A, pod, e.key, &v);
+    const bool has = pod_label(m, e.key, &v);
     bool ok;
     switch (e.op) {
       case SR_OP_IN: ok = has && std::binary_search(e.vals.begin(), e.vals.end(), v); break;
@@ -156,32 +176,42 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
   const int32_t nc = cands->n_cand;
   const int32_t n_flat = nc > 0 ? cands->cand_pod_off[nc] : 0;
   at.pod_off.assign(static_cast<size_t>(n_flat) + 1, 0);
-  if (!PA || PA->anti_off[c->pods.n] == 0) return;  // no term anywhere in the cluster
+  // Without sr_pod_affinity a candidate pod's labels are unknown: if the
+  // snapshot holds anti-affinity, pass 1 already sent every candidate to the
+  // fallback path.
+  if (!PA) return;
+  if (PA->anti_off[c->pods.n] == 0 && snap->anti_total == 0) return;  // no term anywhere
   const sr_pod_affinity& A = *PA;
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
 
-  // ---- distinct terms: base pods (every snapshot node) and pending candidates
+  // ---- distinct terms: base pods (every snapshot node; the snapshot's own
+  // copies) and pending candidates (the call's cluster)
   WordDict dict;
   std::vector<int32_t> words;
   std::vector<std::pair<int32_t, int32_t>> base_has;  // (node, term)
   for (int32_t n = 0; n < n_spot; ++n)
-    for (int32_t e : snap->state[n].pods)
-      for (int32_t t = A.anti_off[e]; t < A.anti_off[e + 1]; ++t) {
-        term_words(c, e, t, words);
-        base_has.emplace_back(n, dict.intern(words));
-      }
+    for (int32_t e : snap->state[n].pods) {
+      const std::vector<int32_t>& tw = snap->pods[e].terms;
+      for (size_t i = 0; i < tw.size(); i += 1 + static_cast<size_t>(tw[i]))
+        base_has.emplace_back(n, dict.intern(tw.data() + i + 1, static_cast<size_t>(tw[i])));
+    }
   std::vector<std::vector<int32_t>> has(static_cast<size_t>(n_flat));  // term ids per flat candidate pod
   for (int32_t i = 0; i < nc; ++i) {
     if (status[i] != STATUS_PENDING) continue;
+    bool own_terms = false;
     for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
       const int32_t pod = cands->cand_pods[j];
       for (int32_t t = A.anti_off[pod]; t < A.anti_off[pod + 1]; ++t) {
-        term_words(c, pod, t, words);
+        anti_term_words(c, pod, t, words);
         has[j].push_back(dict.intern(words));
+        own_terms = true;
       }
       std::sort(has[j].begin(), has[j].end());
       has[j].erase(std::unique(has[j].begin(), has[j].end()), has[j].end());
     }
+    // its terms would have to be matched against snapshot pods whose labels
+    // are unknown (added from a cluster without sr_pod_affinity)
+    if (own_terms && snap->unknown_total > 0) status[i] = SR_CAND_FALLBACK;
   }
   const int32_t T = static_cast<int32_t>(dict.size());
   if (T == 0) return;
@@ -243,14 +273,14 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
     if (terms[t].ml.empty()) unindexed.push_back(t);
     else by_label[label_key(terms[t].ml[0].first, terms[t].ml[0].second)].push_back(t);
   }
-  auto for_each_selecting = [&](int32_t pod, auto&& f) {
+  auto for_each_selecting = [&](const PodMeta& m, auto&& f) {
     for (int32_t t : unindexed)
-      if (term_selects(terms[t], A, pod)) f(t);
-    for (int32_t i = A.label_off[pod]; i < A.label_off[pod + 1]; ++i) {
-      auto it = by_label.find(label_key(A.label_key[i], A.label_val[i]));
+      if (term_selects(terms[t], m)) f(t);
+    for (int32_t i = 0; i < m.n; ++i) {
+      auto it = by_label.find(label_key(m.key[i], m.val[i]));
       if (it == by_label.end()) continue;
       for (int32_t t : it->second)
-        if (term_selects(terms[t], A, pod)) f(t);
+        if (term_selects(terms[t], m)) f(t);
     }
   };
 
@@ -268,7 +298,7 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       for (size_t ch = lo; ch < hi; ++ch)
         for (int32_t n = static_cast<int32_t>(ch * kNodes); n < std::min<int32_t>(n_spot, (ch + 1) * kNodes); ++n)
           for (int32_t e : snap->state[n].pods)
-            for_each_selecting(e, [&](int32_t t) {
+            for_each_selecting(meta_of(snap->pods[e]), [&](int32_t t) {
               const int32_t v = keys[kidx[t]].val[n];
               if (v != INT_MIN) part[ch].emplace_back(t, v);
             });
@@ -306,7 +336,7 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
         const int32_t pod = cands->cand_pods[j];
         std::vector<int32_t>& v = ids[j];
-        for_each_selecting(pod, [&](int32_t t) { v.push_back(t << 1); });
+        for_each_selecting(meta_of(A, pod), [&](int32_t t) { v.push_back(t << 1); });
         for (int32_t t : has[j]) v.push_back(t << 1 | 1);
         std::sort(v.begin(), v.end());
       }

@@ -142,6 +142,7 @@ void for_each_spec_word(const sr_pods& P, int32_t pod, F&& f) {
   for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i) {
     f(P.port_proto[i]);
     f(P.port_num[i]);
+    f(P.port_ip[i]);
   }
 }
 
@@ -195,8 +196,6 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t)
         for (int32_t e = P.term_expr_off[t]; e < P.term_expr_off[t + 1]; ++e)
           if (P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT) return true;
-    for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i)
-      if (P.port_ip[i] != -1 && P.port_num[i] > 0) return true;  // specific hostIP
     return anti_opaque(c, pod);  // required anti-affinity the encoded set cannot read
   };
   for (int32_t i = 0; i < nc; ++i) {
@@ -230,35 +229,106 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   AntiTerms anti;
   analyse_anti(snap, c, cands, w->Wp, w->status_host, &anti);
   const int32_t bit_shift = 2 * anti.n_pairs;  // host-port bits sit above the pairs
-  w->swap_mask = bit_shift >= 64 ? ~0ull : (1ull << bit_shift) - 1;
 
-  // ---- host-port dictionary: (protocol, port) pairs of active pods, <= 64 - 2 * pairs
-  std::unordered_map<int64_t, int32_t> port_dict;
+  // ---- host ports: HostPortInfo.CheckConflict [upstream k8s v1.19
+  // framework/types.go] as state bits.  A (protocol, port) group whose active
+  // pods all bind 0.0.0.0 ("" is 0.0.0.0) is one bit a pod sets and conflicts
+  // with.  A group with specific host IPs gets a swapped pair (W, S) plus one
+  // bit I(ip) per IP: a 0.0.0.0 pod sets W and S, a pod on ip sets S and
+  // I(ip); the conflict bits are the pair-swapped image of the set bits (W <->
+  // S, I(ip) fixed), so 0.0.0.0 conflicts with every IP of the group and an
+  // IP with 0.0.0.0 and itself only.  Layout: anti-affinity pairs, port pairs
+  // (the swapped region), then the single bits.  Pass A classifies the groups,
+  // pass B numbers the bits in candidate order; a candidate that would take
+  // the state word past 64 bits falls back.
   auto port_key = [](int32_t proto, int32_t port) { return (static_cast<int64_t>(proto) << 32) | uint32_t(port); };
+  std::unordered_map<int64_t, uint8_t> group_specific;  // (proto, port) -> has a specific IP
   for (int32_t i = 0; i < nc; ++i) {
     if (w->status_host[i] != STATUS_PENDING) continue;
-    bool overflow = false;
+    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+      const int32_t pod = cands->cand_pods[j];
+      for (int32_t k = P.port_off[pod]; k < P.port_off[pod + 1]; ++k)
+        if (P.port_num[k] > 0) group_specific[port_key(P.port_proto[k], P.port_num[k])] |= P.port_ip[k] != -1;
+    }
+  }
+  struct PortGroup {
+    int32_t pair = -1;                            // pair index (specific IPs), else
+    int32_t single = -1;                          // single-bit index (0.0.0.0 only)
+    std::unordered_map<int32_t, int32_t> ip_bit;  // specific IP -> single-bit index
+  };
+  std::unordered_map<int64_t, PortGroup> groups;
+  int32_t n_port_pairs = 0, n_port_single = 0;
+  for (int32_t i = 0; i < nc; ++i) {
+    if (w->status_host[i] != STATUS_PENDING) continue;
+    const int32_t pairs0 = n_port_pairs, single0 = n_port_single;
+    std::vector<std::pair<int64_t, int32_t>> added_ips;  // undone if the candidate overflows
+    std::vector<int64_t> added_groups;
     for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
       const int32_t pod = cands->cand_pods[j];
       for (int32_t k = P.port_off[pod]; k < P.port_off[pod + 1]; ++k) {
         if (P.port_num[k] <= 0) continue;
         const int64_t key = port_key(P.port_proto[k], P.port_num[k]);
-        if (port_dict.count(key)) continue;
-        if (static_cast<int32_t>(port_dict.size()) >= 64 - bit_shift) {
-          overflow = true;
-          continue;
+        auto ins = groups.emplace(key, PortGroup{});
+        PortGroup& g = ins.first->second;
+        if (ins.second) {
+          added_groups.push_back(key);
+          if (group_specific[key]) g.pair = n_port_pairs++;
+          else g.single = n_port_single++;
         }
-        port_dict.emplace(key, static_cast<int32_t>(port_dict.size()));
+        if (P.port_ip[k] != -1 && g.ip_bit.emplace(P.port_ip[k], n_port_single).second) {
+          ++n_port_single;
+          added_ips.emplace_back(key, P.port_ip[k]);
+        }
       }
     }
-    if (overflow) w->status_host[i] = SR_CAND_FALLBACK;
+    if (bit_shift + 2 * n_port_pairs + n_port_single > 64) {  // overflow: undo, fall back
+      for (const auto& ki : added_ips) groups[ki.first].ip_bit.erase(ki.second);
+      for (int64_t key : added_groups) groups.erase(key);
+      n_port_pairs = pairs0;
+      n_port_single = single0;
+      w->status_host[i] = SR_CAND_FALLBACK;
+    }
   }
+  const int32_t single_base = bit_shift + 2 * n_port_pairs;
+  w->swap_mask = single_base >= 64 ? ~0ull : (1ull << single_base) - 1;
+  // Static conflicts with the base snapshot's UsedPorts: one atom per
+  // (protocol, port, ip) a pod can ask for, addressed by the bit that stands
+  // for the query (single bits: 0.0.0.0 of a single group or I(ip); the W bit
+  // of a pair: 0.0.0.0 of that group).
+  struct PortQuery {
+    int32_t proto, port, ip;
+  };
+  std::vector<PortQuery> port_query;
+  int32_t bit_query[64];
+  for (int32_t& b : bit_query) b = -1;
+  for (const auto& kv : groups) {
+    const int32_t proto = static_cast<int32_t>(kv.first >> 32), port = static_cast<int32_t>(kv.first & 0xffffffff);
+    const PortGroup& g = kv.second;
+    const int32_t wbit = g.pair >= 0 ? bit_shift + 2 * g.pair : single_base + g.single;
+    bit_query[wbit] = static_cast<int32_t>(port_query.size());
+    port_query.push_back(PortQuery{proto, port, -1});
+    for (const auto& ib : g.ip_bit) {
+      bit_query[single_base + ib.second] = static_cast<int32_t>(port_query.size());
+      port_query.push_back(PortQuery{proto, port, ib.first});
+    }
+  }
+  // The state bits a pod sets (absolute positions).
   auto pod_port_mask = [&](int32_t pod) {
     uint64_t m = 0;
     for (int32_t k = P.port_off[pod]; k < P.port_off[pod + 1]; ++k) {
       if (P.port_num[k] <= 0) continue;
-      auto it = port_dict.find(port_key(P.port_proto[k], P.port_num[k]));
-      if (it != port_dict.end()) m |= 1ull << it->second;
+      auto it = groups.find(port_key(P.port_proto[k], P.port_num[k]));
+      if (it == groups.end()) continue;  // a fallback candidate's pod
+      const PortGroup& g = it->second;
+      if (g.pair < 0) {
+        m |= 1ull << (single_base + g.single);
+      } else if (P.port_ip[k] == -1) {
+        m |= 3ull << (bit_shift + 2 * g.pair);  // W and S
+      } else {
+        auto ib = g.ip_bit.find(P.port_ip[k]);
+        if (ib == g.ip_bit.end()) continue;
+        m |= (2ull << (bit_shift + 2 * g.pair)) | (1ull << (single_base + ib->second));  // S and I(ip)
+      }
     }
     return m;
   };
@@ -420,7 +490,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     std::vector<int32_t> terms;  // per valid term: {n_req, groups...}
     int32_t n_terms = 0;
     std::vector<int32_t> untol;  // taint ids the spec does not tolerate
-    uint64_t ports = 0;          // host ports (dictionary bits)
+    uint64_t ports = 0;          // host-port state bits it sets (pod_port_mask)
     std::vector<int32_t> anti_da, anti_db;  // anti-affinity terms: ANDNOT DA(t) / DB(t)
   };
   std::vector<SpecCanon> canon(n_specs);
@@ -539,7 +609,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     sig_off.push_back(static_cast<int32_t>(sig_words.size()));
   }
   const int32_t n_reqs = static_cast<int32_t>(rdict.size());
-  const int32_t n_ports = static_cast<int32_t>(port_dict.size());
+  const int32_t n_ports = static_cast<int32_t>(port_query.size());
   const int32_t A_REQ = 1, A_TAINT = 1 + n_reqs, A_PORT = 1 + n_reqs + n_taints;
   // Composite atoms, one per distinct untolerated-taint set U of the pods:
   // atom 0 AND NOT (OR of U's taint atoms) -- the pod-count check and
@@ -581,8 +651,8 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     const uint64_t ports = static_cast<uint32_t>(tp[1]) | static_cast<uint64_t>(static_cast<uint32_t>(tp[2])) << 32;
     emit(comp_atom(untol), PROG_AND);  // len(pods)+1 <= allowed pods, untolerated taints
     for (int32_t k = 0; k < n_sel; ++k) emit(A_REQ + sel[k], PROG_AND);
-    for (int32_t b = 0; b < 64; ++b)
-      if (ports >> b & 1) emit(A_PORT + b, PROG_ANDNOT);
+    for (int32_t b = 0; b < 64; ++b)  // the base UsedPorts conflicting with each host port it asks for
+      if ((ports >> b & 1) && bit_query[b] >= 0) emit(A_PORT + bit_query[b], PROG_ANDNOT);
     {  // anti-affinity base conflicts
       const int32_t* ad = tp + 3;
       const int32_t nda = ad[0];
@@ -630,15 +700,15 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     const int64_t left = sn.alloc_pods - st.npods;
     w->pods_left[n] = static_cast<int32_t>(std::max<int64_t>(-(1 << 30), std::min<int64_t>(left, 1 << 30)));
     if (left >= 1) set_atom(0, n);
-    uint64_t pb = 0;
-    for (const Port& u : st.ports) {
-      auto it = port_dict.find(port_key(u.proto, u.port));
-      if (it != port_dict.end()) pb |= 1ull << it->second;  // incoming pods bind 0.0.0.0
-    }
-    // base state: host ports only (base anti-affinity conflicts are static, in the F rows)
-    w->port_bits[n] = bit_shift < 64 ? pb << bit_shift : 0;
-    for (int32_t b = 0; b < 64; ++b)
-      if (pb >> b & 1) set_atom(A_PORT + b, n);
+    // base UsedPorts: static conflicts (atoms A_PORT + q, in the F rows); the
+    // state word starts empty (it only carries the candidate's own pods)
+    w->port_bits[n] = 0;
+    for (const Port& u : st.ports)
+      for (int32_t q = 0; q < n_ports; ++q) {
+        const PortQuery& pq = port_query[q];
+        if (pq.proto == u.proto && pq.port == u.port && (pq.ip == -1 || u.ip == -1 || u.ip == pq.ip))
+          set_atom(A_PORT + q, n);
+      }
     for (int32_t k = node_taint_off[n]; k < node_taint_off[n + 1]; ++k) set_atom(A_TAINT + node_taint_ids[k], n);
   }
   w->node_rec.assign(static_cast<size_t>(NP) * 8, 0);
@@ -798,7 +868,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       rec[0] = static_cast<uint64_t>(rc);
       rec[1] = static_cast<uint64_t>(rm);
       rec[2] = static_cast<uint64_t>(re);
-      rec[3] = (bit_shift < 64 ? canon[pod_spec[q]].ports << bit_shift : 0) |
+      rec[3] = canon[pod_spec[q]].ports |
                (anti.active ? anti.pod_bits[active_src[q]] : 0);
       bool dead = cls_empty[r[0]] != 0;
       for (int d = 0; d < 3; ++d) dead = dead || (r[1 + d] >= 0 && static_cast<size_t>(r[1 + d]) == node_vals[d].size());

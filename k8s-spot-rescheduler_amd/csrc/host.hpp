@@ -37,14 +37,30 @@ struct SpotNode {
   std::vector<TaintRec> taints;
 };
 
+// The snapshot's own copy of what InterPodAffinity reads from a pod it holds
+// (scheduler NodeInfo.Pods): namespace, labels and required anti-affinity
+// terms (resolved words, anti_term_words).  Copied when the pod enters the
+// snapshot, so later calls may pass any cluster encoded with the same string
+// interner: pod indices of the creating cluster are never kept.
+struct SnapPod {
+  int32_t ns = -1;
+  uint8_t meta = 0;    // ns / labels / terms known (the cluster passed sr_pod_affinity)
+  uint8_t anti = 0;    // carries required anti-affinity
+  uint8_t opaque = 0;  // ... that the encoder cannot read (anti_opaque)
+  std::vector<int32_t> lkey, lval;  // labels
+  std::vector<int32_t> terms;       // anti-affinity terms: {n words, words...} per term
+};
+
 // Mutable part: scheduler NodeInfo.Requested, len(Pods), UsedPorts, the pods
-// themselves (InterPodAffinity matches against them), the number carrying
-// required anti-affinity and, of those, the opaque ones (anti_opaque()).
+// themselves (indices into sr_snapshot::pods; InterPodAffinity matches against
+// them), the number carrying required anti-affinity, of those the opaque ones,
+// and the pods whose metadata is unknown.
 struct NodeState {
   int64_t requested[3] = {0, 0, 0};
   int64_t npods = 0;
   int32_t anti = 0;
   int32_t opaque = 0;
+  int32_t unknown = 0;
   std::vector<Port> ports;
   std::vector<int32_t> pods;
 };
@@ -57,9 +73,12 @@ struct sr_snapshot {
   std::vector<sr::SpotNode> nodes;
   std::vector<sr::NodeState> state;
   std::vector<sr::NodeState> saved;
+  std::vector<sr::SnapPod> pods;  // every pod ever added (NodeState::pods index it)
+  size_t fork_pods = 0;           // pods.size() at Fork: Revert drops the rest
   bool forked = false;
   int64_t anti_total = 0;
-  int64_t opaque_total = 0;  // pods whose anti-affinity the encoder cannot read: every candidate falls back
+  int64_t opaque_total = 0;   // pods whose anti-affinity the encoder cannot read: every candidate falls back
+  int64_t unknown_total = 0;  // pods without metadata: candidates whose own terms need it fall back
   uint64_t version = 0;  // bumped on every mutation
 };
 
@@ -81,6 +100,11 @@ inline bool has_anti_terms(const sr_cluster* c, int32_t pod) {
 // Its required anti-affinity is outside the encoded set: no sr_pod_affinity,
 // the flag without terms, or a selector LabelSelectorAsSelector rejects.
 bool anti_opaque(const sr_cluster* c, int32_t pod);
+// The words of the pod's anti-affinity term t (antiaff.cpp): topology key,
+// namespaces (defaulted to the owner's), selector; equal words = equal terms.
+void anti_term_words(const sr_cluster* c, int32_t owner, int32_t t, std::vector<int32_t>& out);
+// The snapshot's copy of a pod of `c` (SnapPod).
+void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out);
 
 // Class descriptor flags.
 enum : int32_t { CLS_AFF_REQUIRED = 1, CLS_IMPOSSIBLE = 2 };

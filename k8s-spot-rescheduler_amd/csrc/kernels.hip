@@ -322,7 +322,7 @@ struct K2Stats {
 // it with more).
 template <int SPL, int CH, bool PROF>
 __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int p0, const int np, int& status,
-                                      K2Stats& st) {
+                                      K2Stats& st, uint32_t& nbytes) {
   const int lane = threadIdx.x & 63;
   const int Wp = w.Wp;
   const uint64_t* __restrict__ tab = w.S;  // S rows then T rows: pod records hold word offsets
@@ -423,6 +423,10 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
   dma(w.node_rec + 2 * lane, L.cache[0]);
   dma_pods(0);
   if (np > 64) dma_pods(1);
+  // bytes moved (algorithmic, wave-uniform): node cache, pod records, per
+  // step the head DMA (4 rows x kHead words) and the speculative record, rare
+  // chunk scans and record reloads, the mapping and status writes
+  nbytes += 64u * kNodeCache + (48u + 4u) * static_cast<uint32_t>(np) + 4u;
   SR_WAIT_VM(0);
 #pragma unroll
   for (int j = 0; j < kRing - 1; ++j) dma_head_of(L.ring[j], min(j, np - 1));
@@ -435,6 +439,7 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
   int k = 0;
   for (; k < np; ++k) {
     if (PROF) cyc_t = cyc();
+    nbytes += 4u * kHead * 8u + 64u;  // this pod's head and speculative record
     const int64_t rc = nrc, rm = nrm, re = nre;
     const uint64_t pm = npm;                          // state bits the pod sets
     const uint64_t pin = swap_pairs(pm, w.swap_mask);  // ... and those it conflicts with
@@ -470,6 +475,7 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
         const int base = ch * 64;
         if (ans != INT_MAX || base >= Wp) continue;  // wave-uniform; keeps the loop unrollable
         if (PROF) ++st.n_far;
+        nbytes += 4u * 64u * 8u;
         dma_rows_of(L.chunk, k, base);
         SR_WAIT_VM(0);
         const uint64_t* img = L.chunk;
@@ -535,6 +541,7 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
         rec = L.spec;
       } else {  // rare: not the speculated node
         if (PROF) ++st.n_spec_miss;
+        nbytes += 64u;
         dma_rec(L.rec, ans);
         SR_WAIT_VM(0);
         rec = L.rec;
@@ -642,7 +649,7 @@ __device__ __forceinline__ uint32_t from_lane(uint32_t v, int src) {
 
 template <int G, bool PROF>
 __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __restrict__ F, const int p0,
-                                              const int np, int& status, K2Stats& st) {
+                                              const int np, int& status, K2Stats& st, uint32_t& nbytes) {
   static_assert(64 * G * kNHS * 8 <= sizeof(K2Lds), "node-order LDS exceeds the wave's K2 region");
   const int lane = threadIdx.x & 63;
   const int Wp = w.Wp;  // <= 64
@@ -673,6 +680,10 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     if (e != 0) dead = min(dead, 64 * g + __builtin_ctzll(e));
   }
   uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
+  // bytes moved (algorithmic, wave-uniform): pod records, F heads of pods
+  // [0, dead) (4 rows x min(Wp, kNH) words), 64-node record windows (5 words
+  // each), full-row scans and far words, the mapping and status writes
+  nbytes += (48u + 4u) * static_cast<uint32_t>(np) + 4u + 32u * static_cast<uint32_t>(min(Wp, kNH)) * dead;
 
   // F heads of pods [0, dead): lanes = 8 pods x 8 words, kPB such batches per
   // step with all their loads in flight together (one memory round trip per
@@ -786,6 +797,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             if (js[q] < 0) continue;  // wave-uniform
+            nbytes += 32u * static_cast<uint32_t>(Wp - kNH);
             const uint64_t f = wv ? (x[q][0] & x[q][1] & x[q][2] & x[q][3]) : 0ull;
             const uint64_t m = ballot(f != 0);
             int nx = INT_MAX;
@@ -822,6 +834,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       nleft = static_cast<int>(static_cast<int64_t>(nr[4]));
       wcur = W;
       ++windows;
+      nbytes += 64u * 40u;
     }
     // node n's running state (ClusterSnapshot.AddPod on the candidate's copy)
     int64_t cpu = static_cast<int64_t>(readlane64(static_cast<uint64_t>(ncpu), b));
@@ -875,6 +888,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       if (failed[g] == 0) continue;  // wave-uniform
       // pods that did not fit n: next set bit of their F row after n
       const int k = 64 * g + lane;
+      bool far_word = false;
       if ((failed[g] >> lane) & 1) {
         const uint64_t f = b == 63 ? 0ull : cur[g] & (~0ull << (b + 1));
         int nx = INT_MAX;
@@ -895,10 +909,12 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
             const int w2 = __builtin_ctzll(rem);
             cur[g] = f_word_far(tab, r01[g], r23[g], w2);
             nx = w2 * 64 + __builtin_ctzll(cur[g]);
+            far_word = true;
           }
         }
         ptr[g] = nx;
       }
+      nbytes += 32u * static_cast<uint32_t>(__builtin_popcountll(ballot(far_word)));
       // a pod with no node left fails the candidate; pods above it are irrelevant
       const uint64_t gone = ballot((((failed[g] >> lane) & 1) != 0) & (ptr[g] == INT_MAX));
       if (gone != 0) dead = min(dead, 64 * g + __builtin_ctzll(gone));
@@ -949,22 +965,24 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   K2Stats st;
   int status = -1;
   int wide = 0;
+  uint32_t nbytes = 0;
   bool node_order = false;
   if constexpr (CH == 1) node_order = np <= 4 * 64 && w.k2_mode == 0;  // rows of <= 64 words
   if (node_order) {  // writes out_node itself
     uint64_t* F = reinterpret_cast<uint64_t*>(&L);
     wide = 2;
-    if (np <= 64) k2_node_order<1, PROF>(w, F, p0, np, status, st);
-    else if (np <= 128) k2_node_order<2, PROF>(w, F, p0, np, status, st);
-    else k2_node_order<4, PROF>(w, F, p0, np, status, st);
+    if (np <= 64) k2_node_order<1, PROF>(w, F, p0, np, status, st, nbytes);
+    else if (np <= 128) k2_node_order<2, PROF>(w, F, p0, np, status, st, nbytes);
+    else k2_node_order<4, PROF>(w, F, p0, np, status, st, nbytes);
   } else {
-    int placed = k2_run<1, CH, PROF>(w, L, p0, np, status, st);
+    int placed = k2_run<1, CH, PROF>(w, L, p0, np, status, st, nbytes);
     wide = placed < 0 ? 1 : 0;
-    if (placed < 0) placed = k2_run<8, CH, PROF>(w, L, p0, np, status, st);  // > 64 distinct nodes
+    if (placed < 0) placed = k2_run<8, CH, PROF>(w, L, p0, np, status, st, nbytes);  // > 64 distinct nodes
     for (int i = lane; i < np; i += 64) w.out_node[p0 + i] = i < placed ? L.omap[i] : -1;
   }
   if (lane == 0) {
     w.out_status[ci] = status;
+    w.out_bytes[ci] = nbytes;
     // packed (global candidate << 32 | local candidate): min = first drainable
     if (status < 0)
       atomicMin(reinterpret_cast<unsigned long long*>(w.d_min),

@@ -43,10 +43,11 @@ struct DevWorkload {
   uint64_t* T;         // [n_t][Wp] capacity threshold rows (one table)
   int32_t* out_node;   // [n_pods] spot position or -1
   int32_t* out_status; // [n_cand]
+  uint32_t* out_bytes; // [n_cand] bytes K2 moved for the candidate (the roofline's algorithmic bytes)
   int32_t* d_min;      // 2 x u64 packed {global << 32 | local}: first ok, first fallback (~0 = none)
   uint64_t* result;    // mapped host memory [kResultHeader + max pods] words seq << 32 | value:
                        //   {winner, local, npods, first_fallback, -, -, -, -, mapping...}
-  int32_t seq;         // run sequence number: the tag of every result word
+  uint32_t seq;        // run sequence number: the tag of every result word (wraps)
   int32_t k2_mode;     // 0: node-order first fit where it applies (<= 64 pods, <= 64-word rows);
                        // 1: pod order everywhere (SR_K2_MODE=1, A/B measurement)
   uint64_t* prof;      // optional [n_cand][16] K2 + [kK0ProfWaves][2] K0 per-wave profile

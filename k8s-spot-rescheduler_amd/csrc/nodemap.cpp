@@ -106,9 +106,29 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   return SR_OK;
 }
 
+void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out) {
+  *out = SnapPod{};
+  out->anti = has_anti_terms(c, pod) ? 1 : 0;
+  out->opaque = anti_opaque(c, pod) ? 1 : 0;
+  const sr_pod_affinity* A = c->pod_affinity;
+  if (!A) return;
+  out->meta = 1;
+  out->ns = A->ns[pod];
+  out->lkey.assign(A->label_key + A->label_off[pod], A->label_key + A->label_off[pod + 1]);
+  out->lval.assign(A->label_val + A->label_off[pod], A->label_val + A->label_off[pod + 1]);
+  if (out->opaque) return;  // never read: every candidate falls back while it is there
+  std::vector<int32_t> words;
+  for (int32_t t = A->anti_off[pod]; t < A->anti_off[pod + 1]; ++t) {
+    anti_term_words(c, pod, t, words);
+    out->terms.push_back(static_cast<int32_t>(words.size()));
+    out->terms.insert(out->terms.end(), words.begin(), words.end());
+  }
+}
+
 // scheduler NodeInfo.AddPod [upstream k8s v1.19 framework/types.go]: Requested +=
-// the pod's request, Pods += pod, UsedPorts += container host ports.
-static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod) {
+// the pod's request, Pods += pod, UsedPorts += container host ports.  `sp` is
+// the snapshot's copy of the pod (index `store` in sr_snapshot::pods).
+static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod, const SnapPod& sp, int32_t store) {
   const sr_pods& P = c->pods;
   // int64 addition wraps in Go; do the same without signed-overflow UB.
   auto wrap_add = [](int64_t a, int64_t b) {
@@ -118,11 +138,10 @@ static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod) {
   st.requested[1] = wrap_add(st.requested[1], P.req_memory[pod]);
   st.requested[2] = wrap_add(st.requested[2], P.req_ephemeral[pod]);
   st.npods += 1;
-  if (has_anti_terms(c, pod)) {
-    st.anti += 1;
-    if (anti_opaque(c, pod)) st.opaque += 1;
-  }
-  st.pods.push_back(pod);
+  st.anti += sp.anti;
+  st.opaque += sp.opaque;
+  st.unknown += sp.meta ? 0 : 1;
+  st.pods.push_back(store);
   for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i)
     if (P.port_num[i] > 0) st.ports.push_back(Port{P.port_ip[i], P.port_proto[i], P.port_num[i]});
 }
@@ -152,10 +171,14 @@ bool anti_opaque(const sr_cluster* c, int32_t pod) {
 }
 
 void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t pos) {
-  const int32_t before = s->state[pos].anti, obefore = s->state[pos].opaque;
-  state_add_pod(s->state[pos], c, pod);
-  s->anti_total += s->state[pos].anti - before;
-  s->opaque_total += s->state[pos].opaque - obefore;
+  const int32_t store = static_cast<int32_t>(s->pods.size());
+  s->pods.emplace_back();
+  snap_pod_from(c, pod, &s->pods.back());
+  const SnapPod& sp = s->pods.back();
+  state_add_pod(s->state[pos], c, pod, sp, store);
+  s->anti_total += sp.anti;
+  s->opaque_total += sp.opaque;
+  s->unknown_total += sp.meta ? 0 : 1;
   s->version++;
 }
 
@@ -181,6 +204,10 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
         return SR_ERR_INVALID_ARG;
       }
   }
+  // the snapshot's pod store: the pods of spot node i at [base[i], base[i + 1])
+  std::vector<int32_t> base(static_cast<size_t>(n_spot) + 1, 0);
+  for (int32_t i = 0; i < n_spot; ++i) base[i + 1] = base[i] + (off[spot[i] + 1] - off[spot[i]]);
+  s->pods.resize(static_cast<size_t>(base[n_spot]));
   // AddNodeWithPods per spot node: independent nodes, on the pool
   parallel_for(static_cast<size_t>(n_spot), 32, [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
@@ -198,12 +225,17 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
       for (int32_t j = N.taint_off[node]; j < N.taint_off[node + 1]; ++j)
         sn.taints.push_back(TaintRec{N.taint_key[j], N.taint_val[j], N.taint_effect[j]});
       s->state[i].pods.reserve(static_cast<size_t>(off[node + 1] - off[node]));
-      for (int32_t j = off[node]; j < off[node + 1]; ++j) state_add_pod(s->state[i], c, idx[j]);
+      for (int32_t j = off[node]; j < off[node + 1]; ++j) {
+        const int32_t store = base[i] + (j - off[node]);
+        snap_pod_from(c, idx[j], &s->pods[store]);
+        state_add_pod(s->state[i], c, idx[j], s->pods[store], store);
+      }
     }
   });
   for (int32_t i = 0; i < n_spot; ++i) {
     s->anti_total += s->state[i].anti;
     s->opaque_total += s->state[i].opaque;
+    s->unknown_total += s->state[i].unknown;
   }
   *out = s;
   return SR_OK;
@@ -243,6 +275,7 @@ sr_status sr_snapshot_fork(sr_snapshot* snap) {
   if (!snap) return SR_ERR_INVALID_ARG;
   if (snap->forked) return SR_ERR_STATE;  // DeltaClusterSnapshot forks one level deep
   snap->saved = snap->state;
+  snap->fork_pods = snap->pods.size();
   snap->forked = true;
   return SR_OK;
 }
@@ -252,11 +285,13 @@ sr_status sr_snapshot_revert(sr_snapshot* snap) {
   if (!snap->forked) return SR_OK;  // Revert with nothing forked leaves the snapshot as is
   snap->state.swap(snap->saved);
   snap->saved.clear();
+  snap->pods.resize(snap->fork_pods);  // pods added since Fork are referenced by no state any more
   snap->forked = false;
-  snap->anti_total = snap->opaque_total = 0;
+  snap->anti_total = snap->opaque_total = snap->unknown_total = 0;
   for (const auto& st : snap->state) {
     snap->anti_total += st.anti;
     snap->opaque_total += st.opaque;
+    snap->unknown_total += st.unknown;
   }
   snap->version++;
   return SR_OK;

@@ -39,8 +39,10 @@ struct sr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  DevBuf arena, tables, out_node, out_status, dmin, prof;
-  HostBuf h_arena, h_result, h_status, h_node;
+  DevBuf arena, tables, out_node, out_status, out_bytes, dmin, prof;
+  HostBuf h_arena, h_result, h_status, h_node, h_bytes;
+  uint64_t issued_checks = 0;  // checks of the prepared workload's plan (known after a full run)
+  bool issued_known = false;
   sr::Workload wl;
   sr::DevWorkload dw{};
   bool prepared = false;
@@ -52,7 +54,7 @@ struct sr_ctx {
   std::vector<hipEvent_t> ev_start, ev_end;
   std::vector<int8_t> ev_kernel;
   size_t ev_used = 0;
-  int32_t seq = 0;
+  uint32_t seq = 0;  // run sequence number (wraps: tags compare as uint32)
   sr_timing t{};
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -122,14 +124,6 @@ class Packer {
   size_t size_ = 0;
 };
 
-// K2 algorithmic bytes per pod processed: its 48-B record plus the rows it
-// reads -- the whole F row (4 rows x Wp words) in node order (<= 256 pods,
-// <= 64-word rows), the 32-word heads of the 4 rows in pod order.
-uint64_t k2_pod_bytes(int32_t Wp, int32_t np, int32_t k2_mode) {
-  const bool node_order = k2_mode == 0 && Wp <= 64 && np <= 256;
-  return 48ull + 32ull * static_cast<uint64_t>(node_order ? Wp : std::min(Wp, 32));
-}
-
 sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands) {
   auto t0 = std::chrono::steady_clock::now();
   ctx->prepared = false;
@@ -161,6 +155,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, dev_reserve(ctx->tables, n_rows * row_bytes));
   HIP_TRY(ctx, dev_reserve(ctx->out_node, sizeof(int32_t) * std::max(1, na)));
   HIP_TRY(ctx, dev_reserve(ctx->out_status, sizeof(int32_t) * std::max(1, ncand)));
+  HIP_TRY(ctx, dev_reserve(ctx->out_bytes, sizeof(uint32_t) * std::max(1, ncand)));
   HIP_TRY(ctx, dev_reserve(ctx->dmin, 64));
   const size_t res_bytes = sizeof(uint64_t) * (sr::kResultHeader + static_cast<size_t>(std::max(1, w.max_cand_pods)));
   HIP_TRY(ctx, host_reserve(ctx->h_result, res_bytes));  // mapped: K3 writes the result straight to the host
@@ -200,6 +195,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.T = d.S + static_cast<size_t>(w.n_classes) * w.Wp;
   d.out_node = static_cast<int32_t*>(ctx->out_node.p);
   d.out_status = static_cast<int32_t*>(ctx->out_status.p);
+  d.out_bytes = static_cast<uint32_t*>(ctx->out_bytes.p);
   d.d_min = static_cast<int32_t*>(ctx->dmin.p);
   d.k2_mode = ctx->k2_mode;
   d.swap_mask = w.swap_mask;
@@ -219,13 +215,11 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   // program names, the nodes' free capacities and the thresholds read once.
   uint64_t atom_reads = w.cls_prog.size();
   ctx->t.bytes_tables = n_rows * row + atom_reads * row + 3ull * 4 * w.n_pad + 32ull * w.n_classes;
-  // K2 (upper bound until a full run refines it, see run()): per pod its
-  // four row chunks and its record, per candidate its mapping and status.
-  ctx->t.bytes_placement = 4ull * ncand;
-  for (int32_t k = 0; k < ncand; ++k) {
-    const int32_t np = w.cand_off[k + 1] - w.cand_off[k];
-    ctx->t.bytes_placement += (k2_pod_bytes(w.Wp, np, ctx->k2_mode) + 4) * static_cast<uint64_t>(np);
-  }
+  // K2: counted by the kernel itself per candidate (out_bytes), read back by
+  // the next run with status or node_of_pod outputs
+  ctx->t.bytes_placement = 0;
+  ctx->issued_known = false;
+  ctx->issued_checks = 0;
   ctx->t.ms_pack_host = std::chrono::duration<double, std::milli>(t1 - t0).count();
   ctx->t.ms_upload = std::chrono::duration<double, std::milli>(t2 - t1).count();
   ctx->t.n_pods = na;
@@ -263,7 +257,8 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   const bool collective = ctx->comm && use_comm;
   const int32_t timing = (ctx->timing_runs++ % ctx->timing_every) == 0 ? ctx->timing : 0;
-  d.seq = ++ctx->seq;
+  if (++ctx->seq == 0) ctx->seq = 1;  // tag 0 is never used: fresh result memory may hold zeros
+  d.seq = ctx->seq;
   volatile uint64_t* res = static_cast<volatile uint64_t*>(ctx->h_result.p);
   // Timed kernels get an event pair from the pool, recorded by their own
   // dispatch (hipExtLaunchKernelGGL); the collective is bracketed with
@@ -320,8 +315,11 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     if (full) {
       HIP_TRY(ctx, host_reserve(ctx->h_status, sizeof(int32_t) * std::max(1, ncand)));
       HIP_TRY(ctx, host_reserve(ctx->h_node, sizeof(int32_t) * std::max(1, na)));
-      if (ncand)
+      HIP_TRY(ctx, host_reserve(ctx->h_bytes, sizeof(uint32_t) * std::max(1, ncand)));
+      if (ncand) {
         HIP_TRY(ctx, hipMemcpyAsync(ctx->h_status.p, d.out_status, sizeof(int32_t) * ncand, hipMemcpyDeviceToHost, s));
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_bytes.p, d.out_bytes, sizeof(uint32_t) * ncand, hipMemcpyDeviceToHost, s));
+      }
       if (na) HIP_TRY(ctx, hipMemcpyAsync(ctx->h_node.p, d.out_node, sizeof(int32_t) * na, hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(ctx, hipStreamSynchronize(s));
@@ -373,29 +371,36 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   out->winner_npods = val(1) ? val(2) : 0;
   if (out->winner_map && val(1))
     for (int32_t q = 0; q < val(2); ++q) out->winner_map[q] = val(sr::kResultHeader + q);
-  out->checks = static_cast<uint64_t>(na) * static_cast<uint64_t>(w.n_spot);
+  out->checks_dense = static_cast<uint64_t>(na) * static_cast<uint64_t>(w.n_spot);
   out->fallback_pods = w.fallback_pods;
   if (full) {
     const int32_t* hs = static_cast<const int32_t*>(ctx->h_status.p);
     const int32_t* hn = static_cast<const int32_t*>(ctx->h_node.p);
+    const uint32_t* hb = static_cast<const uint32_t*>(ctx->h_bytes.p);
     if (out->status) {
       for (int32_t i = 0; i < w.n_input_cand; ++i) out->status[i] = w.status_host[i];
       for (int32_t k = 0; k < ncand; ++k) out->status[w.cand_src[k]] = hs[k];
     }
-    // exact K2 algorithmic bytes: pods up to and including the failing one
-    // (node order: the pod's whole F row; pod order: the 32-word row heads)
-    uint64_t k2 = 4ull * ncand;
+    // K2's own byte counts; the reference's CheckPredicates calls for the same
+    // plan: findSpotNodeForPod stops at the first fit (position + 1 calls) and
+    // scans every spot node for a pod that fits nowhere, where canDrainNode stops
+    uint64_t bytes = 0, issued = 0;
     for (int32_t k = 0; k < ncand; ++k) {
-      const int32_t np = w.cand_off[k + 1] - w.cand_off[k];
-      const int32_t done = hs[k] >= 0 ? std::min(np, hs[k] + 1) : np;
-      k2 += k2_pod_bytes(w.Wp, np, ctx->k2_mode) * done + 4ull * np;
+      bytes += hb[k];
+      const int32_t o = w.cand_off[k], np = w.cand_off[k + 1] - o;
+      const int32_t done = hs[k] >= 0 ? std::min(np, hs[k]) : np;
+      for (int32_t q = 0; q < done; ++q) issued += static_cast<uint64_t>(hn[o + q]) + 1;
+      if (hs[k] >= 0) issued += static_cast<uint64_t>(w.n_spot);
     }
-    ctx->t.bytes_placement = k2;
+    ctx->t.bytes_placement = bytes;
+    ctx->issued_checks = issued;
+    ctx->issued_known = true;
     if (out->node_of_pod) {
       for (int32_t i = 0; i < w.n_input_pods; ++i) out->node_of_pod[i] = -1;
       for (int32_t q = 0; q < na; ++q) out->node_of_pod[w.pod_src[q]] = hn[q];
     }
   }
+  out->checks = ctx->issued_known ? ctx->issued_checks : 0;
   return SR_OK;
 }
 
@@ -430,9 +435,10 @@ void sr_destroy(sr_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
-  for (DevBuf* b : {&ctx->arena, &ctx->tables, &ctx->out_node, &ctx->out_status, &ctx->dmin, &ctx->prof})
+  for (DevBuf* b : {&ctx->arena, &ctx->tables, &ctx->out_node, &ctx->out_status, &ctx->out_bytes, &ctx->dmin,
+                    &ctx->prof})
     if (b->p) (void)hipFree(b->p);
-  for (HostBuf* b : {&ctx->h_arena, &ctx->h_result, &ctx->h_status, &ctx->h_node})
+  for (HostBuf* b : {&ctx->h_arena, &ctx->h_result, &ctx->h_status, &ctx->h_node, &ctx->h_bytes})
     if (b->p) (void)hipHostFree(b->p);
   for (auto* v : {&ctx->ev_start, &ctx->ev_end})
     for (hipEvent_t e : *v) (void)hipEventDestroy(e);

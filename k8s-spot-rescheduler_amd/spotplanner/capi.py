@@ -104,7 +104,7 @@ class sr_candidates(ctypes.Structure):
 class sr_plan_out(ctypes.Structure):
     _fields_ = [("winner", ctypes.c_int32), ("first_ok", ctypes.c_int32), ("first_fallback", ctypes.c_int32),
                 ("winner_npods", ctypes.c_int32), ("checks", ctypes.c_uint64), ("fallback_pods", ctypes.c_uint64),
-                ("status", P32), ("node_of_pod", P32), ("winner_map", P32)]
+                ("status", P32), ("node_of_pod", P32), ("winner_map", P32), ("checks_dense", ctypes.c_uint64)]
 
 
 class sr_timing(ctypes.Structure):

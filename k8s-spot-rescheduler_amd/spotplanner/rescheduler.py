@@ -1,8 +1,8 @@
 """Mirror of the reference's planning functions (rescheduler.go, package main).
 
 findSpotNodeForPod (rescheduler.go:338-353), canDrainNode (:357-370),
-validateArgs (:407-417), podID (:402-404), and plan_tick: the planning segment
-of run() (:228-287) evaluated for every candidate at once on the GPU.
+validateArgs (:407-417), podID (:402-404), and plan_arrays: the planning
+segment of run() (:228-287) evaluated for every candidate at once on the GPU.
 """
 from __future__ import annotations
 
@@ -154,8 +154,11 @@ def canDrainNode(predicateChecker: PredicateChecker, spotSnapshot: ClusterSnapsh
     if fb.value:
         raise FallbackRequired(", ".join(pod_id(p) for p in pods))
     if len(nodes) > 0:
-        for p in pods:
-            p.node_name = ""  # :341 side effect on every evaluated pod
+        # :341 runs for every pod findSpotNodeForPod evaluates: up to and
+        # including the first pod that fits nowhere (canDrainNode returns there)
+        evaluated = pods if fail.value < 0 else pods[:fail.value + 1]
+        for p in evaluated:
+            p.node_name = ""
     canDrainNode.last_mapping = [nodes[int(k)].Node.name if k >= 0 else "" for k in mapping]
     if fail.value >= 0:
         return GoError("pod %s can't be rescheduled on any existing spot node" % pod_id(pods[fail.value]))

@@ -996,6 +996,9 @@ int32_t oracle_plan(const oracle_snapshot *s, const sr_cluster *c, const sr_cand
   out->winner = (first_ok >= 0 && (first_fb < 0 || first_fb > first_ok)) ? first_ok : -1;
   out->checks = checks;
   out->fallback_pods = fb_pods;
+  out->checks_dense = 0;
+  for (int32_t i = 0; i < nc; i++)
+    if (status[i] >= SR_CAND_OK) out->checks_dense += (uint64_t)(off[i + 1] - off[i]) * (uint64_t)s->n;
   out->winner_npods = 0;
   for (int32_t i = 0; i < nc; i++) {
     int32_t g = cands->cand_global ? cands->cand_global[i] : i;

@@ -1,0 +1,208 @@
+"""Hand-derived known-answer cases for the scheduler filters behind
+CheckPredicates (call site rescheduler.go:344).  The reference's own tests pin
+only CPU fit (rescheduler_test.go:40-151); every other filter rule comes from
+the pinned upstream modules, which are not in the reference tree:
+
+  k8s.io/kubernetes v1.19.2  pkg/scheduler/framework/plugins/
+      noderesources/fit.go          fitsRequest, computePodResourceRequest
+      tainttoleration/taint_toleration.go  Filter (NoSchedule / NoExecute only)
+      nodeunschedulable/node_unschedulable.go  Filter
+      nodeaffinity/node_affinity.go -> helper/node_affinity.go
+                                    PodMatchesNodeSelectorAndAffinityTerms
+      nodeports/node_ports.go       fitsPorts -> framework/types.go
+                                    HostPortInfo.CheckConflict
+  k8s.io/api v0.19.2 core/v1/toleration.go  Toleration.ToleratesTaint
+  k8s.io/api v0.19.2 core/v1/helper MatchNodeSelectorTerms
+
+Each case gives one pod, spot nodes (with the pods already on them) and the
+answer of the filter chain for the pod on each node, derived by hand from the
+rule quoted in `rule`.  tests/test_known_answer.py checks every answer on the
+oracle (CPU) and, one node at a time through sr_find_spot_nodes, on the GPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List
+
+from spotplanner.model import (Container, ContainerPort, GiB, MiB, Node, NodeSelectorRequirement, NodeSelectorTerm,
+                               Pod, Taint, Toleration)
+
+
+@dataclass
+class Case:
+    name: str
+    rule: str
+    pod: Pod
+    nodes: List[Node]
+    base: List[List[Pod]]
+    fits: List[bool]
+    tags: List[str] = field(default_factory=list)
+
+
+def P(name="p", cpu=100, mem=0, eph=0, **kw) -> Pod:
+    return Pod(name, containers=[Container(cpu_milli=cpu, memory=mem, ephemeral=eph)], **kw)
+
+
+def N(name, cpu=4000, mem=8 * GiB, pods=110, eph=0, **kw) -> Node:
+    return Node(name, cpu_milli=cpu, memory=mem, pods=pods, ephemeral=eph, **kw)
+
+
+def used(cpu=0, mem=0, eph=0, name="used") -> Pod:
+    return P(name, cpu=cpu, mem=mem, eph=eph)
+
+
+def _resources():
+    fit = "fitsRequest: fail iff allocatable < podRequest + nodeInfo.Requested (per resource)"
+    yield Case("memory_exact_fit", fit, P(cpu=0, mem=512 * MiB),
+               [N("a", mem=2 * GiB), N("b", mem=2 * GiB)], [[used(mem=1536 * MiB)], [used(mem=1537 * MiB)]],
+               [True, False])
+    yield Case("ephemeral_exact_fit", fit, P(cpu=0, eph=1 * GiB),
+               [N("a", eph=10 * GiB), N("b", eph=10 * GiB), N("c", eph=0)],
+               [[used(eph=9 * GiB)], [used(eph=9 * GiB + 1)], []], [True, False, False])
+    yield Case("cpu_exact_fit", fit, P(cpu=700), [N("a", cpu=1000), N("b", cpu=1000)],
+               [[used(cpu=300)], [used(cpu=301)]], [True, False])
+    yield Case("pod_count", "fitsRequest: len(nodeInfo.Pods)+1 > allowedPodNumber fails, before the zero-request "
+               "shortcut", P(cpu=0), [N("a", pods=2), N("b", pods=2), N("c", pods=0)],
+               [[used(), used()], [used()], []], [False, True, False])
+    yield Case("zero_request_skips_resources", "fitsRequest: an all-zero request returns after the pod-count check",
+               P(cpu=0, mem=0, eph=0), [N("a", cpu=1000, mem=1 * GiB)], [[used(cpu=5000, mem=4 * GiB)]], [True])
+    yield Case("nonzero_request_on_overcommitted_node", fit + " (memory checked for a cpu-only pod too)",
+               P(cpu=1, mem=0), [N("a", cpu=1000, mem=1 * GiB), N("b", cpu=1000, mem=1 * GiB)],
+               [[used(mem=1 * GiB + 1)], [used(mem=1 * GiB)]], [False, True])
+    ic = Pod("p", containers=[Container(cpu_milli=100, memory=64 * MiB)],
+             init_containers=[Container(cpu_milli=800), Container(cpu_milli=50, memory=1 * GiB)])
+    yield Case("init_container_max", "computePodResourceRequest: max(sum(containers), each init container) per "
+               "resource: cpu 800, memory 1Gi", ic,
+               [N("a", cpu=1000, mem=8 * GiB), N("b", cpu=1000, mem=8 * GiB), N("c", cpu=1000, mem=2 * GiB)],
+               [[used(cpu=201)], [used(cpu=200)], [used(mem=1 * GiB + 1)]], [False, True, False])
+    oh = Pod("p", containers=[Container(cpu_milli=400), Container(cpu_milli=0, memory=0)],
+             overhead=Container(cpu_milli=200, memory=100 * MiB))
+    yield Case("pod_overhead", "computePodResourceRequest: + Spec.Overhead: cpu 600, memory 100Mi", oh,
+               [N("a", cpu=1000), N("b", cpu=1000), N("c", cpu=1000, mem=1 * GiB)],
+               [[used(cpu=401)], [used(cpu=400)], [used(mem=1 * GiB - 100 * MiB + 1)]], [False, True, False])
+    yield Case("sum_of_containers", "computePodResourceRequest: regular containers add up",
+               Pod("p", containers=[Container(cpu_milli=300), Container(cpu_milli=300)]),
+               [N("a", cpu=1000), N("b", cpu=1000)], [[used(cpu=401)], [used(cpu=400)]], [False, True])
+
+
+def _taints():
+    flt = "TaintToleration.Filter: FindMatchingUntoleratedTaint over NoSchedule / NoExecute taints"
+    tt = "Toleration.ToleratesTaint: effect empty or equal, key empty or equal, Exists or Equal with equal value"
+    yield Case("no_schedule_and_no_execute_filter", flt, P(),
+               [N("a", taints=[Taint("k", "v", "NoSchedule")]), N("b", taints=[Taint("k", "v", "NoExecute")]),
+                N("c")], [[], [], []], [False, False, True])
+    yield Case("prefer_no_schedule_never_filters", flt, P(),
+               [N("a", taints=[Taint("k", "v", "PreferNoSchedule")])], [[]], [True])
+    yield Case("empty_effect_tolerates_every_effect", tt, P(tolerations=[Toleration("k", "Equal", "v", "")]),
+               [N("a", taints=[Taint("k", "v", "NoSchedule")]), N("b", taints=[Taint("k", "v", "NoExecute")]),
+                N("c", taints=[Taint("k", "w", "NoSchedule")])], [[], [], []], [True, True, False])
+    yield Case("effect_must_match", tt, P(tolerations=[Toleration("k", "Exists", "", "NoSchedule")]),
+               [N("a", taints=[Taint("k", "v", "NoExecute")]), N("b", taints=[Taint("k", "v", "NoSchedule")])],
+               [[], []], [False, True])
+    yield Case("empty_key_exists_tolerates_everything", tt, P(tolerations=[Toleration("", "Exists")]),
+               [N("a", taints=[Taint("k", "v", "NoSchedule"), Taint("j", "", "NoExecute")])], [[]], [True])
+    yield Case("empty_key_equal_matches_empty_values_only", tt, P(tolerations=[Toleration("", "Equal", "")]),
+               [N("a", taints=[Taint("k", "", "NoSchedule")]), N("b", taints=[Taint("k", "v", "NoSchedule")])],
+               [[], []], [True, False])
+    yield Case("equal_with_empty_value", tt + " (operator \"\" is Equal)", P(tolerations=[Toleration("k", "", "")]),
+               [N("a", taints=[Taint("k", "", "NoSchedule")]), N("b", taints=[Taint("k", "v", "NoSchedule")])],
+               [[], []], [True, False])
+    yield Case("unknown_operator_tolerates_nothing", tt, P(tolerations=[Toleration("k", "Weird", "v")]),
+               [N("a", taints=[Taint("k", "v", "NoSchedule")])], [[]], [False])
+    yield Case("every_taint_must_be_tolerated", flt,
+               P(tolerations=[Toleration("k", "Exists", "", "NoSchedule")]),
+               [N("a", taints=[Taint("k", "v", "NoSchedule"), Taint("j", "v", "NoSchedule")]),
+                N("b", taints=[Taint("k", "v", "NoSchedule"), Taint("j", "v", "PreferNoSchedule")])],
+               [[], []], [False, True])
+
+
+def _unschedulable():
+    r = ("NodeUnschedulable.Filter: Spec.Unschedulable and the pod does not tolerate "
+         "node.kubernetes.io/unschedulable:NoSchedule")
+    k = "node.kubernetes.io/unschedulable"
+    yield Case("unschedulable_without_toleration", r, P(), [N("a", unschedulable=True), N("b")], [[], []],
+               [False, True])
+    yield Case("unschedulable_tolerated_exists", r, P(tolerations=[Toleration(k, "Exists", "", "NoSchedule")]),
+               [N("a", unschedulable=True)], [[]], [True])
+    yield Case("unschedulable_tolerated_equal_empty_value", r, P(tolerations=[Toleration(k, "Equal", "")]),
+               [N("a", unschedulable=True)], [[]], [True])
+    yield Case("unschedulable_tolerated_by_wildcard", r, P(tolerations=[Toleration("", "Exists")]),
+               [N("a", unschedulable=True)], [[]], [True])
+    yield Case("unschedulable_wrong_effect", r, P(tolerations=[Toleration(k, "Exists", "", "NoExecute")]),
+               [N("a", unschedulable=True)], [[]], [False])
+
+
+def _affinity():
+    sel = "PodMatchesNodeSelectorAndAffinityTerms: every nodeSelector pair must equal the node label"
+    mt = ("MatchNodeSelectorTerms: terms ORed; an empty term or a term that fails to build selects nothing; "
+          "requirements ANDed")
+    z = lambda v: {"zone": v}  # noqa: E731
+    nodes3 = [N("a", labels=z("a")), N("b", labels=z("b")), N("c", labels={})]
+
+    def aff(*terms):
+        return P(required_node_affinity=list(terms))
+
+    def T(*exprs, fields=()):
+        return NodeSelectorTerm([NodeSelectorRequirement(*e) for e in exprs],
+                                [NodeSelectorRequirement(*f) for f in fields])
+
+    yield Case("node_selector", sel, P(node_selector={"zone": "a"}), nodes3, [[], [], []], [True, False, False])
+    yield Case("in", mt, aff(T(("zone", "In", ["b", "x"]))), nodes3, [[], [], []], [False, True, False])
+    yield Case("not_in_missing_key", mt + "; NotIn holds when the key is absent", aff(T(("zone", "NotIn", ["a"]))),
+               nodes3, [[], [], []], [False, True, True])
+    yield Case("does_not_exist_missing_key", mt, aff(T(("zone", "DoesNotExist", []))), nodes3, [[], [], []],
+               [False, False, True])
+    yield Case("exists", mt, aff(T(("zone", "Exists", []))), nodes3, [[], [], []], [True, True, False])
+    yield Case("empty_term_list_matches_nothing", mt, aff(), nodes3, [[], [], []], [False, False, False])
+    yield Case("empty_term_matches_nothing", mt, aff(T()), nodes3, [[], [], []], [False, False, False])
+    yield Case("empty_term_or_valid_term", mt, aff(T(), T(("zone", "In", ["a"]))), nodes3, [[], [], []],
+               [True, False, False])
+    yield Case("terms_ored", mt, aff(T(("zone", "In", ["a"])), T(("zone", "DoesNotExist", []))), nodes3,
+               [[], [], []], [True, False, True])
+    yield Case("requirements_anded", mt,
+               aff(T(("zone", "Exists", []), ("disk", "In", ["ssd"]))),
+               [N("a", labels={"zone": "a", "disk": "ssd"}), N("b", labels={"zone": "b"}),
+                N("c", labels={"disk": "ssd"})], [[], [], []], [True, False, False])
+    yield Case("node_selector_and_terms", sel + "; then the required terms",
+               P(node_selector={"zone": "a"}, required_node_affinity=[T(("disk", "In", ["ssd"]))]),
+               [N("a", labels={"zone": "a"}), N("b", labels={"zone": "b", "disk": "ssd"}),
+                N("c", labels={"zone": "a", "disk": "ssd"})], [[], [], []], [False, False, True])
+    yield Case("invalid_requirement_fails_its_term", mt + "; In without values fails NewRequirement",
+               aff(T(("zone", "In", [])), T(("zone", "In", ["b"]))), nodes3, [[], [], []], [False, True, False])
+    yield Case("match_fields_name_in", mt + "; fields.Set{metadata.name: node.Name}",
+               aff(T(fields=[("metadata.name", "In", ["b"])])), nodes3, [[], [], []], [False, True, False])
+    yield Case("match_fields_name_not_in", mt, aff(T(fields=[("metadata.name", "NotIn", ["b"])])), nodes3,
+               [[], [], []], [True, False, True])
+    yield Case("match_fields_two_values_invalid", mt + "; In on a field needs exactly one value",
+               aff(T(fields=[("metadata.name", "In", ["a", "b"])])), nodes3, [[], [], []], [False, False, False])
+    yield Case("match_fields_and_expressions", mt,
+               aff(T(("zone", "Exists", []), fields=[("metadata.name", "NotIn", ["a"])])), nodes3, [[], [], []],
+               [False, True, False])
+
+
+def _ports():
+    r = ("HostPortInfo.CheckConflict: port <= 0 never conflicts; 0.0.0.0 (or \"\") conflicts with every IP of the "
+         "same (protocol, port); a specific IP with 0.0.0.0 and itself")
+
+    def hp(name, port, ip="", proto="TCP"):
+        return Pod(name, containers=[Container(cpu_milli=10, ports=[ContainerPort(port, protocol=proto,
+                                                                                   host_ip=ip)])])
+    nodes = [N("a"), N("b"), N("c"), N("d"), N("e")]
+    base = [[hp("x", 80, "10.0.0.1")], [hp("y", 80)], [hp("z", 80, "10.0.0.2")], [hp("u", 80, proto="UDP")],
+            [hp("v", 8080)]]
+    yield Case("wildcard_against_specific", r, hp("p", 80), nodes, base, [False, False, False, True, True])
+    yield Case("specific_against_wildcard_and_itself", r, hp("p", 80, "10.0.0.1"), nodes, base,
+               [False, False, True, True, True])
+    yield Case("explicit_0000_is_wildcard", r, hp("p", 80, "0.0.0.0"), nodes, base,
+               [False, False, False, True, True])
+    yield Case("protocol_separates", r, hp("p", 80, proto="UDP"), nodes, base, [True, True, True, False, True])
+    yield Case("zero_host_port_ignored", r, hp("p", 0), nodes, base, [True, True, True, True, True])
+
+
+def cases() -> List[Case]:
+    out = []
+    for gen in (_resources, _taints, _unschedulable, _affinity, _ports):
+        out.extend(gen())
+    names = [c.name for c in out]
+    assert len(names) == len(set(names))
+    return out

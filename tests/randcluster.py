@@ -70,7 +70,9 @@ def rand_pod(r: random.Random, name: str, features: bool, fallback: bool = False
                                                 r.choice(["", "NoSchedule", "NoExecute", "PreferNoSchedule"])))
         if r.random() < 0.2:
             p.containers[0].ports.append(ContainerPort(host_port=r.choice([80, 443, 9100]),
-                                                       protocol=r.choice(["TCP", "UDP", ""])))
+                                                       protocol=r.choice(["TCP", "UDP", ""]),
+                                                       host_ip=r.choice(["", "", "0.0.0.0", "10.0.0.1",
+                                                                         "10.0.0.2"])))
     if fallback and r.random() < 0.1:
         kind = r.randint(0, 4)
         if kind == 0:
