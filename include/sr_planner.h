@@ -93,6 +93,8 @@ typedef int32_t sr_status;
 #define SR_CAND_OK        (-1)
 #define SR_CAND_FALLBACK  (-2)  /* outside the encoded predicate set: evaluate with the reference path */
 #define SR_CAND_EMPTY     (-3)  /* no pods to move: run() skips it (rescheduler.go:260-264) */
+#define SR_CAND_SKIPPED   (-4)  /* sr_plan_first: after the first drainable candidate, never evaluated
+                                   (run() drains it and breaks, rescheduler.go:280-286) */
 
 /* ------------------------------------------------------------- cluster model */
 /* Nodes (k8s.io/api/core/v1 Node), in the order the node lister returned them
@@ -353,7 +355,7 @@ typedef struct {
   uint64_t fallback_pods;   /* pods of fallback candidates */
   /* optional outputs (NULL = not wanted) */
   int32_t *status;          /* [n_cand] SR_CAND_* or failing pod index */
-  int32_t *node_of_pod;     /* [cand_pod_off[n_cand]] spot position, -1 not placed */
+  int32_t *node_of_pod;     /* [cand_pod_off[n_cand] - cand_pod_off[0]] spot position, -1 not placed */
   int32_t *winner_map;      /* [max pods of a candidate] spot position per pod of first_ok */
   uint64_t checks_dense;    /* candidate pods x spot nodes of the evaluated candidates (dense-equivalent pairs) */
 } sr_plan_out;
@@ -364,9 +366,24 @@ typedef struct {
 sr_status sr_plan(sr_ctx *ctx, const sr_snapshot *snap, const sr_cluster *cluster,
                   const sr_candidates *cands, sr_plan_out *out);
 
+/* The planning segment as run() executes it (rescheduler.go:228-287): the
+ * candidates in order until the first whose plan succeeds (drain + break,
+ * :280-286).  The device plans prefix batches of 64, 128, 256, ... candidates
+ * (the environment variable SR_PREFIX_BATCH sets the first size) and stops
+ * after the batch holding the first drainable candidate; a batch's host
+ * encoding costs in proportion to its pods, so a tick whose winner comes early
+ * encodes little.  Outputs as sr_plan for the evaluated candidates and
+ * SR_CAND_SKIPPED for the rest; `checks` / `checks_dense` cover the evaluated
+ * ones.  With a communicator every rank passes its shard (cand_global) and the
+ * ranks stop after the same batch. */
+sr_status sr_plan_first(sr_ctx *ctx, const sr_snapshot *snap, const sr_cluster *cluster,
+                        const sr_candidates *cands, sr_plan_out *out);
+
 /* Split form of sr_plan for a resident workload (bench): prepare = host
  * encoding + upload; run = device-only tick over the resident buffers
- * (kernels + result download). */
+ * (kernels + result download).  The planner keeps what it derived from the
+ * spot pool and the pod specs across calls: a prepare encodes
+ * only what changed since the previous one. */
 sr_status sr_plan_prepare(sr_ctx *ctx, const sr_snapshot *snap, const sr_cluster *cluster,
                           const sr_candidates *cands);
 sr_status sr_plan_run(sr_ctx *ctx, sr_plan_out *out);
@@ -385,6 +402,11 @@ typedef struct {
                                status or node_of_pod outputs (0 before) */
   int32_t  n_pods, n_spot, n_cand, n_words;
   int32_t  n_rows_static, n_rows_threshold, n_classes;
+  uint64_t bytes_uploaded;     /* last prepare's H2D bytes (the spot nodes' records only when their state changed) */
+  int32_t  enc_new_specs;      /* pod specs the last prepare had never seen (canonicalised) */
+  int32_t  enc_static_rebuilt; /* 1: the last prepare rebuilt the spot pool's static view (order, labels, taints) */
+  int32_t  enc_state_nodes;    /* spot nodes whose capacity state the last prepare re-encoded */
+  int32_t  prefix_batches;     /* batches the last sr_plan_first ran */
 } sr_timing;
 /* mask: which kernels sr_plan_run brackets with HIP events (resets the sums):
  * 1 = K0, 2 = K2, 4 = collective (multi-GPU) + K3; 0 = no events.  Events are read back lazily, by

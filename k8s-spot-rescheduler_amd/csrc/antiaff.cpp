@@ -174,7 +174,9 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
   at = AntiTerms{};
   const sr_pod_affinity* PA = c->pod_affinity;
   const int32_t nc = cands->n_cand;
-  const int32_t n_flat = nc > 0 ? cands->cand_pod_off[nc] : 0;
+  const int32_t base = nc > 0 ? cands->cand_pod_off[0] : 0;  // per-pod arrays: flat index - base
+  const int32_t n_flat = nc > 0 ? cands->cand_pod_off[nc] - base : 0;
+  at.base = base;
   at.pod_off.assign(static_cast<size_t>(n_flat) + 1, 0);
   // Without sr_pod_affinity a candidate pod's labels are unknown: if the
   // snapshot holds anti-affinity, pass 1 already sent every candidate to the
@@ -203,11 +205,11 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       const int32_t pod = cands->cand_pods[j];
       for (int32_t t = A.anti_off[pod]; t < A.anti_off[pod + 1]; ++t) {
         anti_term_words(c, pod, t, words);
-        has[j].push_back(dict.intern(words));
+        has[j - base].push_back(dict.intern(words));
         own_terms = true;
       }
-      std::sort(has[j].begin(), has[j].end());
-      has[j].erase(std::unique(has[j].begin(), has[j].end()), has[j].end());
+      std::sort(has[j - base].begin(), has[j - base].end());
+      has[j - base].erase(std::unique(has[j - base].begin(), has[j - base].end()), has[j - base].end());
     }
     // its terms would have to be matched against snapshot pods whose labels
     // are unknown (added from a cluster without sr_pod_affinity)
@@ -335,9 +337,9 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       if (status[i] != STATUS_PENDING) continue;
       for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
         const int32_t pod = cands->cand_pods[j];
-        std::vector<int32_t>& v = ids[j];
+        std::vector<int32_t>& v = ids[j - base];
         for_each_selecting(meta_of(A, pod), [&](int32_t t) { v.push_back(t << 1); });
-        for (int32_t t : has[j]) v.push_back(t << 1 | 1);
+        for (int32_t t : has[j - base]) v.push_back(t << 1 | 1);
         std::sort(v.begin(), v.end());
       }
     }
@@ -357,7 +359,7 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       touched.clear();
       need.clear();
       for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
-        const std::vector<int32_t>& v = ids[j];
+        const std::vector<int32_t>& v = ids[j - base];
         for (size_t k = 0; k < v.size(); ++k) {
           const int32_t t = v[k] >> 1;
           if (nh[t] == 0 && nm[t] == 0) touched.push_back(t);
@@ -386,11 +388,11 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       for (size_t p = 0; p < need.size(); ++p) pair[need[p]] = static_cast<int32_t>(p);
       for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
         uint64_t bits = 0;
-        for (int32_t id : ids[j]) {
+        for (int32_t id : ids[j - base]) {
           const int32_t p = pair[id >> 1];
           if (p >= 0) bits |= 1ull << (2 * p + ((id & 1) ? 0 : 1));  // A: it has t, B: t selects it
         }
-        at.pod_bits[j] = bits;
+        at.pod_bits[j - base] = bits;
       }
       for (int32_t t : need) pair[t] = -1;
       pairs[i] = static_cast<int32_t>(need.size());

@@ -2,9 +2,9 @@
 //
 // The predicate of one (pod, spot node) pair against the *base* snapshot
 // (k8s v1.19.2 NodeUnschedulable, NodeResourcesFit, NodeName, NodePorts,
-// NodeAffinity, TaintToleration [upstream]; call site rescheduler.go:344)
-// factors into a conjunction of terms that each depend on a low-cardinality
-// projection of the pod:
+// NodeAffinity, TaintToleration, InterPodAffinity [upstream]; call site
+// rescheduler.go:344) factors into a conjunction of terms that each depend on
+// a low-cardinality projection of the pod:
 //
 //   fits(p, n) = S[class(p)](n) & T[cpu(p)](n) & T[mem(p)](n) & T[eph(p)](n)
 //
@@ -14,15 +14,26 @@
 //                                    fitsRequest skips the resource checks)
 //
 // where "class" interns everything static about a pod.  S and T are bitmask
-// rows over spot nodes in NodeInfoArray order, built on the GPU (K0); the dense
-// pod's feasibility row is their AND, formed inside K2.  Everything that changes while a
-// candidate's pods are placed (capacity, pod count, host ports) is rechecked
-// exactly on the nodes the candidate touched (K2).  Features outside this set
-// route the whole candidate to the reference path (SR_CAND_FALLBACK).
+// rows over spot nodes in NodeInfoArray order, built on the GPU (K0); the
+// pod's feasibility row is their AND, formed inside K2.  Everything that
+// changes while a candidate's pods are placed (capacity, pod count, host
+// ports, anti-affinity pairs) is state K2 carries per candidate.  Features
+// outside this set route the whole candidate to the reference path
+// (SR_CAND_FALLBACK).
+//
+// Persistence (EncoderCache, one per sr_ctx): a planner sees one snapshot
+// after another, mostly identical.  The spot pool is compared with the last
+// call's view by per-node fingerprints; label columns, requirement rows and
+// taint rows survive while the static view does, capacity records and sorted
+// free values while the state view does (a few changed nodes are patched in
+// place).  Pod specs and requirements are interned by content across calls,
+// so a call canonicalises only specs it has never seen.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <climits>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -38,35 +49,37 @@ double encode_phase_ms[16];  // host-side profile of the last encode (tools/enco
 namespace {
 
 constexpr int64_t kQuantityLimit = int64_t(1) << 62;
+constexpr size_t kSpecShards = 16;             // fixed: spec ids do not depend on the thread count
+constexpr size_t kMaxSpecs = size_t(1) << 21;  // content dictionaries are dropped beyond these
+constexpr size_t kMaxReqs = size_t(1) << 18;
+constexpr int32_t kSerialPods = 4096;          // below this, per-pod passes run on the calling thread
 
 bool in_range(int64_t v) { return v >= 0 && v < kQuantityLimit; }
 
 enum : int32_t { REQ_LABEL_EQ = 0, REQ_LABEL_EXPR = 1, REQ_FIELD = 2 };
 
-// A node-side requirement: nodeSelector pair, matchExpression or matchField.
-struct Requirement {
-  int32_t type, key, op;
-  std::vector<int32_t> vals;  // sorted, unique
-};
+inline uint64_t mix(uint64_t h, uint64_t x) {
+  h = (h ^ x) * 0xff51afd7ed558ccdull;
+  return h ^ (h >> 32);
+}
 
-// v1.Toleration.ToleratesTaint [upstream k8s.io/api/core/v1/toleration.go].
-bool tolerates(const sr_pods& P, int32_t pod, int32_t id_empty, const TaintRec& t) {
-  for (int32_t i = P.tol_off[pod]; i < P.tol_off[pod + 1]; ++i) {
-    const int32_t eff = P.tol_effect[i];
+// v1.Toleration.ToleratesTaint [upstream k8s.io/api/core/v1/toleration.go]
+// over a spec's toleration words {key, op, value, effect}.
+bool tolerates(const std::vector<int32_t>& tol, int32_t id_empty, const TaintRec& t) {
+  for (size_t i = 0; i + 4 <= tol.size(); i += 4) {
+    const int32_t key = tol[i], op = tol[i + 1], val = tol[i + 2], eff = tol[i + 3];
     if (eff != SR_EFFECT_EMPTY && (eff == SR_EFFECT_OTHER || eff != t.effect)) continue;
-    const int32_t key = P.tol_key[i];
     if (key != id_empty && key != t.key) continue;
-    const int32_t op = P.tol_op[i];
     if (op == SR_TOL_EXISTS) return true;
-    if (op == SR_TOL_EQUAL && P.tol_val[i] == t.val) return true;
+    if (op == SR_TOL_EQUAL && val == t.val) return true;
   }
   return false;
 }
 
-// lower_bound over a sorted array of distinct values, with a bucket index on
-// top: bucket b = (x - lo) >> shift holds the lower bound of its first value,
-// so a lookup is one table read plus a short scan (binary searches over
-// distinct memory requests mispredict on every level).
+// lower_bound over a sorted array of distinct values with a bucket index on
+// top (bucket b = (x - lo) >> shift holds the position of its first value):
+// one table read plus a binary search inside the bucket.  Lookups over
+// scattered requests mispredict on every level of a plain binary search.
 class LowerBound {
  public:
   void build(const std::vector<int64_t>& v) {
@@ -75,8 +88,9 @@ class LowerBound {
     if (v.empty()) return;
     lo_ = v.front();
     const uint64_t span = static_cast<uint64_t>(v.back() - lo_) + 1;
+    const uint64_t want = std::max<uint64_t>(64, 2 * v.size());
     shift_ = 0;
-    while ((span >> shift_) > (1u << 16)) ++shift_;
+    while ((span >> shift_) > want) ++shift_;
     const size_t nb = static_cast<size_t>(span >> shift_) + 2;
     table_.resize(nb);
     size_t pos = 0;
@@ -90,9 +104,8 @@ class LowerBound {
     const std::vector<int64_t>& v = *v_;
     if (v.empty() || x <= lo_) return 0;
     if (x > v.back()) return v.size();
-    size_t pos = table_[static_cast<size_t>(static_cast<uint64_t>(x - lo_) >> shift_)];
-    while (v[pos] < x) ++pos;  // stays inside x's bucket: v.back() >= x
-    return pos;
+    const size_t b = static_cast<size_t>(static_cast<uint64_t>(x - lo_) >> shift_);
+    return static_cast<size_t>(std::lower_bound(v.begin() + table_[b], v.begin() + table_[b + 1], x) - v.begin());
   }
 
  private:
@@ -103,7 +116,7 @@ class LowerBound {
 };
 
 // The raw static spec of a pod: nodeSelector, required node affinity,
-// tolerations, host ports.  Hash 0 is reserved for "no static constraints".
+// tolerations, host ports (with their host IP).
 template <class F>
 void for_each_spec_word(const sr_pods& P, int32_t pod, F&& f) {
   const int32_t s0 = P.sel_off[pod], s1 = P.sel_off[pod + 1];
@@ -151,11 +164,297 @@ bool has_static_spec(const sr_pods& P, int32_t pod) {
          P.port_off[pod] != P.port_off[pod + 1] || P.aff_required[pod] != 0;
 }
 
+// Requirement word group {len, type, key, op, sorted unique values}.
+void put_req(std::vector<int32_t>& out, int32_t type, int32_t key, int32_t op, const int32_t* v, int32_t nv) {
+  const size_t at = out.size();
+  out.push_back(0);
+  out.push_back(type);
+  out.push_back(key);
+  out.push_back(op);
+  const size_t vb = out.size();
+  out.insert(out.end(), v, v + nv);
+  std::sort(out.begin() + vb, out.end());
+  out.erase(std::unique(out.begin() + vb, out.end()), out.end());
+  out[at] = static_cast<int32_t>(out.size() - at - 1);
+}
+
+// A new spec's canonical form before its requirements are interned.
+struct SpecDraft {
+  int32_t flags = 0;
+  std::vector<int32_t> sel;    // nodeSelector requirement groups
+  std::vector<int32_t> terms;  // per buildable term: {n groups, groups...}
+  int32_t n_terms = 0;
+  std::vector<int32_t> tol, ports;
+};
+
+void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
+  const sr_pods& P = c->pods;
+  // Spec.NodeSelector: labels.SelectorFromSet -> Equals requirements.
+  for (int32_t i = P.sel_off[pod]; i < P.sel_off[pod + 1]; ++i)
+    put_req(d->sel, REQ_LABEL_EQ, P.sel_key[i], SR_OP_IN, &P.sel_val[i], 1);
+  // Required node affinity: MatchNodeSelectorTerms [upstream core/v1/helper].
+  if (P.aff_required[pod]) {
+    d->flags |= CLS_AFF_REQUIRED;
+    std::vector<int32_t> term;
+    for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t) {
+      const int32_t e0 = P.term_expr_off[t], e1 = P.term_expr_off[t + 1];
+      const int32_t f0 = P.term_field_off[t], f1 = P.term_field_off[t + 1];
+      if (e0 == e1 && f0 == f1) continue;  // an empty term selects nothing
+      bool valid = true;
+      term.clear();
+      int32_t n = 0;
+      for (int32_t e = e0; e < e1 && valid; ++e) {
+        const int32_t nv = P.expr_val_off[e + 1] - P.expr_val_off[e];
+        const int32_t op = P.expr_op[e];
+        if (P.expr_key[e] == c->id_empty) valid = false;  // validateLabelKey("") fails
+        else if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) valid = false;
+        else if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) valid = false;
+        else if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST)
+          valid = false;
+        if (valid) {
+          put_req(term, REQ_LABEL_EXPR, P.expr_key[e], op, P.expr_vals + P.expr_val_off[e], nv);
+          ++n;
+        }
+      }
+      for (int32_t f = f0; f < f1 && valid; ++f) {  // NodeSelectorRequirementsAsFieldSelector
+        const int32_t nv = P.field_val_off[f + 1] - P.field_val_off[f];
+        const int32_t op = P.field_op[f];
+        valid = (op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 1;
+        if (valid) {
+          put_req(term, REQ_FIELD, P.field_key[f], op, &P.field_vals[P.field_val_off[f]], 1);
+          ++n;
+        }
+      }
+      if (!valid) continue;  // a term that fails to build matches nothing
+      d->terms.push_back(n);
+      d->terms.insert(d->terms.end(), term.begin(), term.end());
+      ++d->n_terms;
+    }
+    if (d->n_terms == 0) d->flags |= CLS_IMPOSSIBLE;
+  }
+  for (int32_t i = P.tol_off[pod]; i < P.tol_off[pod + 1]; ++i) {
+    d->tol.push_back(P.tol_key[i]);
+    d->tol.push_back(P.tol_op[i]);
+    d->tol.push_back(P.tol_val[i]);
+    d->tol.push_back(P.tol_effect[i]);
+  }
+  for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i) {
+    if (P.port_num[i] <= 0) continue;  // HostPortInfo ignores port <= 0
+    d->ports.push_back(P.port_proto[i]);
+    d->ports.push_back(P.port_num[i]);
+    d->ports.push_back(P.port_ip[i]);
+  }
+}
+
+// Interns a draft's requirement groups; returns the sorted unique ids.
+void intern_groups(WordDict& dict, const int32_t* g, int32_t n_groups, std::vector<int32_t>& ids, size_t* used) {
+  ids.clear();
+  size_t i = 0;
+  for (int32_t k = 0; k < n_groups; ++k) {
+    ids.push_back(dict.intern(g + i + 1, static_cast<size_t>(g[i])));
+    i += 1 + static_cast<size_t>(g[i]);
+  }
+  std::sort(ids.begin(), ids.end());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  if (used) *used = i;
+}
+
+uint64_t node_state_fp(const SpotNode& sn, const NodeState& st) {
+  uint64_t h = 0x51ED270B7A1DE5ull;
+  for (int r = 0; r < 3; ++r) h = mix(mix(h, static_cast<uint64_t>(sn.alloc[r])), static_cast<uint64_t>(st.requested[r]));
+  h = mix(mix(h, static_cast<uint64_t>(sn.alloc_pods)), static_cast<uint64_t>(st.npods));
+  uint64_t ports = 0;  // order-independent
+  for (const Port& u : st.ports)
+    ports += mix(mix(mix(0x9E37ull, static_cast<uint32_t>(u.ip)), static_cast<uint32_t>(u.proto)),
+                 static_cast<uint32_t>(u.port));
+  return mix(h, ports);
+}
+
+// ---- static view: names, labels, taints of the spot pool in NodeInfoArray order
+void refresh_static(EncoderCache& C, const sr_snapshot* snap, int32_t Wp) {
+  const int32_t n = static_cast<int32_t>(snap->nodes.size());
+  bool same = C.n_spot == n && C.Wp == Wp;
+  for (int32_t i = 0; same && i < n; ++i)
+    same = C.names[i] == snap->nodes[i].name && C.static_fp[i] == snap->nodes[i].static_fp;
+  C.last_static_changed = same ? 0 : 1;
+  if (same) return;
+  ++C.static_gen;
+  C.n_spot = n;
+  C.Wp = Wp;
+  C.n_pad = Wp * 64;
+  C.names.resize(n);
+  C.static_fp.resize(n);
+  for (int32_t i = 0; i < n; ++i) {
+    C.names[i] = snap->nodes[i].name;
+    C.static_fp[i] = snap->nodes[i].static_fp;
+  }
+  C.label_col.clear();
+  // taints: NoSchedule / NoExecute only (TaintToleration.Filter); the
+  // unschedulable flag is the pseudo-taint node.kubernetes.io/unschedulable:NoSchedule
+  WordDict taint_dict;
+  C.taints.clear();
+  std::vector<std::pair<int32_t, int32_t>> hits;  // (taint, node)
+  auto add = [&](const TaintRec& t, int32_t node) {
+    const int32_t k[3] = {t.key, t.val, t.effect};
+    bool ins = false;
+    const int32_t id = taint_dict.intern(k, 3, &ins);
+    if (ins) C.taints.push_back(t);
+    hits.emplace_back(id, node);
+  };
+  for (int32_t i = 0; i < n; ++i) {
+    const SpotNode& sn = snap->nodes[i];
+    for (const TaintRec& t : sn.taints)
+      if (t.effect == SR_EFFECT_NO_SCHEDULE || t.effect == SR_EFFECT_NO_EXECUTE) add(t, i);
+    if (sn.unschedulable) add(TaintRec{snap->id_unschedulable_key, snap->id_empty, SR_EFFECT_NO_SCHEDULE}, i);
+  }
+  C.taint_rows.assign(C.taints.size() * static_cast<size_t>(Wp), 0);
+  for (const auto& h : hits)
+    C.taint_rows[static_cast<size_t>(h.first) * Wp + (h.second >> 6)] |= 1ull << (h.second & 63);
+  C.state_fp.clear();  // positions may have moved: the state view is rebuilt too
+}
+
+// ---- state view: capacity records, free values (sorted), pod-count atom
+sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* err) {
+  const int32_t n = C.n_spot, NP = C.n_pad, Wp = C.Wp;
+  std::vector<uint64_t> fp(static_cast<size_t>(n));
+  auto fill_fp = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) fp[i] = node_state_fp(snap->nodes[i], snap->state[i]);
+  };
+  if (n > kSerialPods) parallel_for(static_cast<size_t>(n), 1024, fill_fp);
+  else fill_fp(0, static_cast<size_t>(n));
+  std::vector<int32_t> changed;
+  const bool full = C.state_fp.size() != static_cast<size_t>(n);
+  if (!full)
+    for (int32_t i = 0; i < n; ++i)
+      if (fp[i] != C.state_fp[i]) changed.push_back(i);
+  C.last_state_changed = full ? n : static_cast<int32_t>(changed.size());
+  if (!full && changed.empty()) return SR_OK;
+  ++C.state_gen;
+  auto node_values = [&](int32_t i, int64_t out[3], int64_t* left) -> bool {
+    const SpotNode& sn = snap->nodes[i];
+    const NodeState& st = snap->state[i];
+    for (int r = 0; r < 3; ++r) {
+      if (!in_range(sn.alloc[r]) || !in_range(st.requested[r])) return false;
+      out[r] = sn.alloc[r] - st.requested[r];
+    }
+    *left = sn.alloc_pods - st.npods;
+    return true;
+  };
+  auto write_node = [&](int32_t i, const int64_t f[3], int64_t left) {
+    uint64_t* r = &C.node_rec[static_cast<size_t>(i) * 8];
+    for (int d = 0; d < 3; ++d) {
+      r[d] = static_cast<uint64_t>(f[d]);
+      C.node_free[static_cast<size_t>(d) * NP + i] = f[d];
+    }
+    r[3] = 0;  // state bits: the base UsedPorts are static conflicts (F rows)
+    const int32_t pl = static_cast<int32_t>(std::max<int64_t>(-(1 << 30), std::min<int64_t>(left, 1 << 30)));
+    r[4] = static_cast<uint64_t>(static_cast<int64_t>(pl));
+    uint64_t& word = C.podcount_row[static_cast<size_t>(i >> 6)];
+    const uint64_t bit = 1ull << (i & 63);
+    word = left >= 1 ? (word | bit) : (word & ~bit);
+  };
+  auto fail = [&]() {
+    C.state_fp.clear();
+    *err = "spot node quantity outside [0, 2^62)";
+    return SR_ERR_CAPACITY;
+  };
+  if (full || changed.size() * 8 > static_cast<size_t>(n)) {
+    C.node_rec.assign(static_cast<size_t>(NP) * 8, 0);
+    C.node_free.assign(static_cast<size_t>(3) * NP, INT64_MIN);  // pads never pass a threshold
+    C.podcount_row.assign(static_cast<size_t>(Wp), 0);
+    for (int d = 0; d < 3; ++d) C.sorted_free[d].resize(static_cast<size_t>(n));
+    for (int32_t i = 0; i < n; ++i) {
+      int64_t f[3], left;
+      if (!node_values(i, f, &left)) return fail();
+      write_node(i, f, left);
+      for (int d = 0; d < 3; ++d) C.sorted_free[d][i] = f[d];
+    }
+    for (int d = 0; d < 3; ++d) std::sort(C.sorted_free[d].begin(), C.sorted_free[d].end());
+  } else {  // a few nodes changed: patch their records and the sorted values
+    for (int32_t i : changed) {
+      int64_t f[3], left;
+      if (!node_values(i, f, &left)) return fail();
+      for (int d = 0; d < 3; ++d) {
+        std::vector<int64_t>& s = C.sorted_free[d];
+        const int64_t old = C.node_free[static_cast<size_t>(d) * NP + i];
+        s.erase(std::lower_bound(s.begin(), s.end(), old));
+        s.insert(std::upper_bound(s.begin(), s.end(), f[d]), f[d]);
+      }
+      write_node(i, f, left);
+    }
+  }
+  for (int d = 0; d < 3; ++d) {
+    C.node_vals[d].assign(C.sorted_free[d].begin(), C.sorted_free[d].end());
+    C.node_vals[d].erase(std::unique(C.node_vals[d].begin(), C.node_vals[d].end()), C.node_vals[d].end());
+  }
+  C.state_fp.swap(fp);
+  return SR_OK;
+}
+
+// Label value column of `key` over the static view (built on first use).
+const std::vector<int32_t>& label_column(EncoderCache& C, const sr_snapshot* snap, int32_t key) {
+  for (const auto& kc : C.label_col)
+    if (kc.first == key) return kc.second;
+  std::vector<int32_t> col(static_cast<size_t>(C.n_spot), INT32_MIN);
+  for (int32_t n = 0; n < C.n_spot; ++n)
+    for (const auto& kv : snap->nodes[n].labels)
+      if (kv.first == key) {
+        col[n] = kv.second;
+        break;
+      }
+  C.label_col.emplace_back(key, std::move(col));
+  return C.label_col.back().second;
+}
+
+// Node row of requirement `rw` = {type, key, op, vals...} over the static view:
+// Requirement.Matches on the node's labels, or the metadata.name field.
+void build_req_row(const EncoderCache& C, const sr_snapshot* snap, const int32_t* rw, size_t len,
+                   const std::vector<int32_t>* col, std::vector<uint64_t>& row) {
+  const int32_t type = rw[0], key = rw[1], op = rw[2];
+  const int32_t* vals = rw + 3;
+  const size_t nv = len - 3;
+  row.assign(static_cast<size_t>(C.Wp), 0);
+  auto set = [&](int32_t n) { row[static_cast<size_t>(n >> 6)] |= 1ull << (n & 63); };
+  if (type == REQ_FIELD) {
+    // fields.Set{"metadata.name": node.Name}; any other key reads as "".
+    const bool is_name = key == C.id_metadata_name && C.id_metadata_name != -1;
+    for (int32_t n = 0; n < C.n_spot; ++n) {
+      const int32_t fv = is_name ? snap->nodes[n].name : C.id_empty;
+      const bool eq = fv == vals[0];
+      if (op == SR_OP_IN ? eq : !eq) set(n);
+    }
+    return;
+  }
+  for (int32_t n = 0; n < C.n_spot; ++n) {
+    const int32_t v = (*col)[n];
+    const bool has = v != INT32_MIN;
+    bool m;
+    switch (op) {
+      case SR_OP_IN: m = has && std::binary_search(vals, vals + nv, v); break;
+      case SR_OP_NOT_IN: m = !has || !std::binary_search(vals, vals + nv, v); break;
+      case SR_OP_EXISTS: m = has; break;
+      default: m = !has; break;  // DoesNotExist
+    }
+    if (m) set(n);
+  }
+}
 
 }  // namespace
 
-sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
-                          Workload* w, std::string* err) {
+uint64_t node_static_fp(const SpotNode& n) {
+  uint64_t h = mix(mix(0xC0FFEEull, static_cast<uint32_t>(n.name)), n.unschedulable);
+  uint64_t labels = 0, taints = 0;  // order-independent sums (Go map iteration order varies)
+  for (const auto& kv : n.labels)
+    labels += mix(mix(0x1AB3ull, static_cast<uint32_t>(kv.first)), static_cast<uint32_t>(kv.second));
+  for (const TaintRec& t : n.taints)
+    taints += mix(mix(mix(0x7A1Eull, static_cast<uint32_t>(t.key)), static_cast<uint32_t>(t.val)),
+                  static_cast<uint32_t>(t.effect));
+  return mix(mix(h, labels), taints);
+}
+
+sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr_cluster* c,
+                          const sr_candidates* cands, Workload* w, std::string* err) {
+  EncoderCache& C = *cache;
   const sr_pods& P = c->pods;
   const int32_t nc = cands->n_cand;
   auto t_last = std::chrono::steady_clock::now();
@@ -167,25 +466,45 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
   w->reset();
   w->n_input_cand = nc;
-  w->n_input_pods = nc > 0 ? cands->cand_pod_off[nc] : 0;
+  w->pod_base = nc > 0 ? cands->cand_pod_off[0] : 0;
+  w->n_input_pods = nc > 0 ? cands->cand_pod_off[nc] - w->pod_base : 0;
   if (!snap->nodes.empty() &&
       (c->id_empty != snap->id_empty || c->id_metadata_name != snap->id_metadata_name ||
        c->id_unschedulable_key != snap->id_unschedulable_key)) {
     *err = "cluster string ids differ from the snapshot's (one interner per snapshot)";
     return SR_ERR_INVALID_ARG;
   }
+  // content dictionaries are a function of the interned ids of these strings
+  if (C.id_empty != c->id_empty || C.id_metadata_name != c->id_metadata_name ||
+      C.id_unschedulable_key != c->id_unschedulable_key || C.spec.size() > kMaxSpecs ||
+      C.req_dict.size() > kMaxReqs) {
+    C.clear_content();
+    C.id_empty = c->id_empty;
+    C.id_metadata_name = c->id_metadata_name;
+    C.id_unschedulable_key = c->id_unschedulable_key;
+    C.n_spot = -1;  // and the node views
+  }
+  if (C.spec.empty()) {  // spec 0: no static constraints
+    C.spec.emplace_back();
+    C.spec_shards.assign(kSpecShards, EncoderCache::SpecShard{});
+  }
 
-  // ---- spot node dimensions
+  // ---- spot node dimensions and the cached node views
   const int32_t W = (n_spot + 63) / 64;
-  w->n_spot = n_spot;
-  w->Wp = std::max(2, (W + 1) & ~1);
-  if (w->Wp > MAX_WORDS) {
+  const int32_t Wp = std::max(2, (W + 1) & ~1);
+  if (Wp > MAX_WORDS) {
     *err = "too many spot nodes for one device plan";
     return SR_ERR_CAPACITY;
   }
-  w->n_pad = w->Wp * 64;
-
+  w->n_spot = n_spot;
+  w->Wp = Wp;
+  w->n_pad = Wp * 64;
+  refresh_static(C, snap, Wp);
+  sr_status st = refresh_state(C, snap, err);
+  if (st != SR_OK) return st;
+  w->state_gen = C.state_gen;
   phase(0);
+
   // ---- pass 1: candidate-level fallback (host-decided)
   w->status_host.assign(static_cast<size_t>(nc), STATUS_PENDING);
   auto pod_fallback = [&](int32_t pod) {
@@ -209,7 +528,7 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
         return SR_ERR_INVALID_ARG;
       }
   }
-  parallel_for(static_cast<size_t>(nc), 64, [&](size_t lo, size_t hi) {
+  auto pass1 = [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
       const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
       if (e == b) {
@@ -221,13 +540,14 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       for (int32_t j = b; j < e && !fb; ++j) fb = pod_fallback(cands->cand_pods[j]);
       if (fb) w->status_host[i] = SR_CAND_FALLBACK;
     }
-  });
+  };
+  if (w->n_input_pods > kSerialPods) parallel_for(static_cast<size_t>(nc), 64, pass1);
+  else pass1(0, static_cast<size_t>(nc));
 
-  phase(8);
   // ---- required pod anti-affinity: static node sets, state-bit pairs and
   // the candidates it sends to the fallback path (antiaff.cpp)
   AntiTerms anti;
-  analyse_anti(snap, c, cands, w->Wp, w->status_host, &anti);
+  analyse_anti(snap, c, cands, Wp, w->status_host, &anti);
   const int32_t bit_shift = 2 * anti.n_pairs;  // host-port bits sit above the pairs
 
   // ---- host ports: HostPortInfo.CheckConflict [upstream k8s v1.19
@@ -258,37 +578,38 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   };
   std::unordered_map<int64_t, PortGroup> groups;
   int32_t n_port_pairs = 0, n_port_single = 0;
-  for (int32_t i = 0; i < nc; ++i) {
-    if (w->status_host[i] != STATUS_PENDING) continue;
-    const int32_t pairs0 = n_port_pairs, single0 = n_port_single;
-    std::vector<std::pair<int64_t, int32_t>> added_ips;  // undone if the candidate overflows
-    std::vector<int64_t> added_groups;
-    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
-      const int32_t pod = cands->cand_pods[j];
-      for (int32_t k = P.port_off[pod]; k < P.port_off[pod + 1]; ++k) {
-        if (P.port_num[k] <= 0) continue;
-        const int64_t key = port_key(P.port_proto[k], P.port_num[k]);
-        auto ins = groups.emplace(key, PortGroup{});
-        PortGroup& g = ins.first->second;
-        if (ins.second) {
-          added_groups.push_back(key);
-          if (group_specific[key]) g.pair = n_port_pairs++;
-          else g.single = n_port_single++;
-        }
-        if (P.port_ip[k] != -1 && g.ip_bit.emplace(P.port_ip[k], n_port_single).second) {
-          ++n_port_single;
-          added_ips.emplace_back(key, P.port_ip[k]);
+  if (!group_specific.empty())
+    for (int32_t i = 0; i < nc; ++i) {
+      if (w->status_host[i] != STATUS_PENDING) continue;
+      const int32_t pairs0 = n_port_pairs, single0 = n_port_single;
+      std::vector<std::pair<int64_t, int32_t>> added_ips;  // undone if the candidate overflows
+      std::vector<int64_t> added_groups;
+      for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+        const int32_t pod = cands->cand_pods[j];
+        for (int32_t k = P.port_off[pod]; k < P.port_off[pod + 1]; ++k) {
+          if (P.port_num[k] <= 0) continue;
+          const int64_t key = port_key(P.port_proto[k], P.port_num[k]);
+          auto ins = groups.emplace(key, PortGroup{});
+          PortGroup& g = ins.first->second;
+          if (ins.second) {
+            added_groups.push_back(key);
+            if (group_specific[key]) g.pair = n_port_pairs++;
+            else g.single = n_port_single++;
+          }
+          if (P.port_ip[k] != -1 && g.ip_bit.emplace(P.port_ip[k], n_port_single).second) {
+            ++n_port_single;
+            added_ips.emplace_back(key, P.port_ip[k]);
+          }
         }
       }
+      if (bit_shift + 2 * n_port_pairs + n_port_single > 64) {  // overflow: undo, fall back
+        for (const auto& ki : added_ips) groups[ki.first].ip_bit.erase(ki.second);
+        for (int64_t key : added_groups) groups.erase(key);
+        n_port_pairs = pairs0;
+        n_port_single = single0;
+        w->status_host[i] = SR_CAND_FALLBACK;
+      }
     }
-    if (bit_shift + 2 * n_port_pairs + n_port_single > 64) {  // overflow: undo, fall back
-      for (const auto& ki : added_ips) groups[ki.first].ip_bit.erase(ki.second);
-      for (int64_t key : added_groups) groups.erase(key);
-      n_port_pairs = pairs0;
-      n_port_single = single0;
-      w->status_host[i] = SR_CAND_FALLBACK;
-    }
-  }
   const int32_t single_base = bit_shift + 2 * n_port_pairs;
   w->swap_mask = single_base >= 64 ? ~0ull : (1ull << single_base) - 1;
   // Static conflicts with the base snapshot's UsedPorts: one atom per
@@ -312,20 +633,19 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       port_query.push_back(PortQuery{proto, port, ib.first});
     }
   }
-  // The state bits a pod sets (absolute positions).
-  auto pod_port_mask = [&](int32_t pod) {
+  // The state bits a spec's host ports {proto, port, ip}* set (absolute positions).
+  auto port_mask = [&](const std::vector<int32_t>& ports) {
     uint64_t m = 0;
-    for (int32_t k = P.port_off[pod]; k < P.port_off[pod + 1]; ++k) {
-      if (P.port_num[k] <= 0) continue;
-      auto it = groups.find(port_key(P.port_proto[k], P.port_num[k]));
+    for (size_t k = 0; k + 3 <= ports.size(); k += 3) {
+      auto it = groups.find(port_key(ports[k], ports[k + 1]));
       if (it == groups.end()) continue;  // a fallback candidate's pod
       const PortGroup& g = it->second;
       if (g.pair < 0) {
         m |= 1ull << (single_base + g.single);
-      } else if (P.port_ip[k] == -1) {
+      } else if (ports[k + 2] == -1) {
         m |= 3ull << (bit_shift + 2 * g.pair);  // W and S
       } else {
-        auto ib = g.ip_bit.find(P.port_ip[k]);
+        auto ib = g.ip_bit.find(ports[k + 2]);
         if (ib == g.ip_bit.end()) continue;
         m |= (2ull << (bit_shift + 2 * g.pair)) | (1ull << (single_base + ib->second));  // S and I(ip)
       }
@@ -340,30 +660,8 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     if (w->first_fallback < 0 || g < w->first_fallback) w->first_fallback = g;
     w->fallback_pods += static_cast<uint64_t>(cands->cand_pod_off[i + 1] - cands->cand_pod_off[i]);
   }
-
-  // ---- taint dictionary over spot nodes (NoSchedule / NoExecute only; the
-  // unschedulable flag is the pseudo-taint node.kubernetes.io/unschedulable:NoSchedule)
-  std::vector<TaintRec> taints;
-  WordDict taint_dict;
-  auto taint_id = [&](const TaintRec& t) {
-    const int32_t k[3] = {t.key, t.val, t.effect};
-    bool ins = false;
-    const int32_t id = taint_dict.intern(k, 3, &ins);
-    if (ins) taints.push_back(t);
-    return id;
-  };
-  std::vector<int32_t> node_taint_off(static_cast<size_t>(n_spot) + 1, 0), node_taint_ids;
-  for (int32_t n = 0; n < n_spot; ++n) {
-    const SpotNode& sn = snap->nodes[n];
-    for (const TaintRec& t : sn.taints)
-      if (t.effect == SR_EFFECT_NO_SCHEDULE || t.effect == SR_EFFECT_NO_EXECUTE) node_taint_ids.push_back(taint_id(t));
-    if (sn.unschedulable)
-      node_taint_ids.push_back(taint_id(TaintRec{snap->id_unschedulable_key, snap->id_empty, SR_EFFECT_NO_SCHEDULE}));
-    node_taint_off[n + 1] = static_cast<int32_t>(node_taint_ids.size());
-  }
-  const int32_t n_taints = static_cast<int32_t>(taints.size());
-
   phase(1);
+
   // Active pods in candidate order.
   std::vector<int32_t> active_pod;   // cluster pod index
   std::vector<int32_t> active_src;   // flat index into cand_pods
@@ -381,51 +679,38 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   }
   w->cand_off.push_back(static_cast<int32_t>(active_pod.size()));
   const int32_t na = static_cast<int32_t>(active_pod.size());
+  const bool big = na > kSerialPods;
+  auto pfor = [&](size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn) {
+    if (big) parallel_for(n, grain, fn);
+    else fn(0, n);
+  };
 
-  // ---- distinct static specs.  Pods with word-identical static specs
-  // (selector, affinity, tolerations, host ports) share one spec; pods with no
-  // static constraints at all share spec 0.  The raw spec is hashed once per
-  // pod; the dictionaries are sharded by hash over the pool, and spec ids are
-  // assigned in first-occurrence order afterwards, so they do not depend on
-  // the thread count.
+  // ---- static specs, interned by content across calls.  Each pod's raw spec
+  // words are gathered once into per-chunk buffers and hashed; the hash picks
+  // one of kSpecShards persistent dictionaries, each scanned by one thread;
+  // specs never seen before get their ids serially afterwards (in shard,
+  // first-occurrence order: independent of the thread count) and are
+  // canonicalised in parallel.
   std::vector<int32_t> pod_spec(static_cast<size_t>(na), 0);
   std::vector<uint64_t> spec_hash(static_cast<size_t>(na), 0);
-  std::vector<uint8_t> spec_shard(static_cast<size_t>(na), 0);
-  // The spec words are gathered once per pod (the pod arrays are read at
-  // scattered indices) into one buffer per 2048-pod chunk.
+  std::vector<uint8_t> spec_shard(static_cast<size_t>(na), 0xff);
   constexpr size_t kChunk = 2048;
   std::vector<std::vector<int32_t>> spec_words((static_cast<size_t>(na) + kChunk - 1) / kChunk);
-  std::vector<uint32_t> spec_woff(static_cast<size_t>(na), 0);  // offset in its chunk's buffer
-  const size_t n_shards = std::min<size_t>(pool_threads(), 255);
-  auto shard_of = [n_shards](uint64_t h) { return static_cast<size_t>(((h >> 32) * n_shards) >> 32); };
-  parallel_for(spec_words.size(), 1, [&](size_t lo, size_t hi) {
+  std::vector<uint32_t> spec_woff(static_cast<size_t>(na), 0);
+  pfor(spec_words.size(), 1, [&](size_t lo, size_t hi) {
     for (size_t ch = lo; ch < hi; ++ch) {
       std::vector<int32_t>& buf = spec_words[ch];
+      buf.clear();
       const size_t q1 = std::min(static_cast<size_t>(na), (ch + 1) * kChunk);
       for (size_t q = ch * kChunk; q < q1; ++q) {
         const size_t b0 = buf.size();
         spec_woff[q] = static_cast<uint32_t>(b0);
         const int32_t pod = active_pod[q];
-        // anti-affinity ids (term << 1 | has) of the pod, a suffix of its spec
-        const int32_t* aid = nullptr;
-        size_t nai = 0;
-        if (anti.active) {
-          const int32_t j = active_src[q];
-          aid = anti.pod_ids.data() + anti.pod_off[j];
-          nai = static_cast<size_t>(anti.pod_off[j + 1] - anti.pod_off[j]);
-        }
-        if (!has_static_spec(P, pod) && nai == 0) {
-          spec_shard[q] = 255;  // spec 0
-          continue;
-        }
+        if (!has_static_spec(P, pod)) continue;  // spec 0
         for_each_spec_word(P, pod, [&](int32_t x) { buf.push_back(x); });
-        if (nai) {
-          buf.push_back(static_cast<int32_t>(nai));
-          buf.insert(buf.end(), aid, aid + nai);
-        }
         const uint64_t h = hash_words(buf.data() + b0, buf.size() - b0);
         spec_hash[q] = h;
-        spec_shard[q] = static_cast<uint8_t>(shard_of(h));
+        spec_shard[q] = static_cast<uint8_t>(((h >> 32) * kSpecShards) >> 32);
       }
     }
   });
@@ -435,358 +720,279 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     *n = e - spec_woff[q];
     return buf.data() + spec_woff[q];
   };
-  phase(14);
-  struct Shard {
-    WordDict dict;
-    std::vector<int32_t> rep_q;  // local id -> first active pod
-  };
-  std::vector<Shard> shards(n_shards);
-  parallel_for(n_shards, 1, [&](size_t lo, size_t hi) {
+  std::vector<std::vector<int32_t>> shard_new(kSpecShards);  // first pod of each new local id
+  pfor(kSpecShards, 1, [&](size_t lo, size_t hi) {
     for (size_t sh = lo; sh < hi; ++sh) {
-      Shard& S = shards[sh];
-      S.dict.clear();
+      EncoderCache::SpecShard& S = C.spec_shards[sh];
+      shard_new[sh].clear();
       for (int32_t q = 0; q < na; ++q) {
         if (spec_shard[q] != sh) continue;
         size_t n = 0;
         const int32_t* p = words_of(static_cast<size_t>(q), &n);
         bool ins = false;
-        pod_spec[q] = S.dict.intern(p, n, spec_hash[q], &ins);
-        if (ins) S.rep_q.push_back(q);
+        const int32_t local = S.dict.intern(p, n, spec_hash[q], &ins);
+        if (ins) {
+          S.global.push_back(-1);
+          shard_new[sh].push_back(q);
+        }
+        pod_spec[q] = local;  // local for now
       }
     }
   });
-  phase(15);
-  std::vector<int32_t> spec_rep{-1}, spec_rep_q{-1};  // first pod of each spec (cluster / active index)
-  {
-    struct Rep {
-      int32_t q, shard, local;
+  phase(14);
+  std::vector<int32_t> new_spec_pod;  // representative pod of each new spec
+  const int32_t spec0 = static_cast<int32_t>(C.spec.size());
+  for (size_t sh = 0; sh < kSpecShards; ++sh)
+    for (int32_t q : shard_new[sh]) {
+      EncoderCache::SpecShard& S = C.spec_shards[sh];
+      S.global[pod_spec[q]] = spec0 + static_cast<int32_t>(new_spec_pod.size());
+      new_spec_pod.push_back(active_pod[q]);
+    }
+  C.last_new_specs = static_cast<int32_t>(new_spec_pod.size());
+  pfor(static_cast<size_t>(na), 4096, [&](size_t lo, size_t hi) {
+    for (size_t q = lo; q < hi; ++q)
+      pod_spec[q] = spec_shard[q] == 0xff ? 0 : C.spec_shards[spec_shard[q]].global[pod_spec[q]];
+  });
+  if (!new_spec_pod.empty()) {
+    std::vector<SpecDraft> drafts(new_spec_pod.size());
+    auto draft = [&](size_t lo, size_t hi) {
+      for (size_t k = lo; k < hi; ++k) draft_spec(c, new_spec_pod[k], &drafts[k]);
     };
-    std::vector<Rep> reps;
-    std::vector<std::vector<int32_t>> global(n_shards);
-    for (size_t sh = 0; sh < n_shards; ++sh) {
-      global[sh].resize(shards[sh].rep_q.size());
-      for (size_t l = 0; l < shards[sh].rep_q.size(); ++l)
-        reps.push_back(Rep{shards[sh].rep_q[l], static_cast<int32_t>(sh), static_cast<int32_t>(l)});
+    if (drafts.size() > 256) parallel_for(drafts.size(), 64, draft);
+    else draft(0, drafts.size());
+    C.spec.resize(static_cast<size_t>(spec0) + drafts.size());
+    std::vector<int32_t> ids;
+    for (size_t k = 0; k < drafts.size(); ++k) {  // requirement ids: serial
+      SpecDraft& d = drafts[k];
+      SpecInfo& sp = C.spec[static_cast<size_t>(spec0) + k];
+      sp.flags = d.flags;
+      int32_t n_sel = 0;
+      for (size_t i = 0; i < d.sel.size(); i += 1 + static_cast<size_t>(d.sel[i])) ++n_sel;
+      intern_groups(C.req_dict, d.sel.data(), n_sel, sp.sel, nullptr);
+      sp.n_terms = d.n_terms;
+      for (size_t i = 0, t = 0; t < static_cast<size_t>(d.n_terms); ++t) {
+        size_t used = 0;
+        intern_groups(C.req_dict, d.terms.data() + i + 1, d.terms[i], ids, &used);
+        sp.terms.push_back(static_cast<int32_t>(ids.size()));
+        sp.terms.insert(sp.terms.end(), ids.begin(), ids.end());
+        i += 1 + used;
+      }
+      sp.tol.swap(d.tol);
+      sp.ports.swap(d.ports);
     }
-    std::sort(reps.begin(), reps.end(), [](const Rep& x, const Rep& y) { return x.q < y.q; });
-    for (const Rep& r : reps) {
-      global[r.shard][r.local] = static_cast<int32_t>(spec_rep.size());
-      spec_rep.push_back(active_pod[r.q]);
-      spec_rep_q.push_back(r.q);
-    }
-    parallel_for(static_cast<size_t>(na), 4096, [&](size_t lo, size_t hi) {
-      for (size_t q = lo; q < hi; ++q)
-        if (spec_shard[q] != 255) pod_spec[q] = global[spec_shard[q]][pod_spec[q]];
-    });
   }
-  const size_t n_specs = spec_rep.size();
   phase(7);
 
-  // ---- per spec (parallel): canonical requirements, untolerated taints, ports.
-  // A requirement is the word group {len, type, key, op, sorted unique vals}.
-  struct SpecCanon {
-    int32_t flags = 0;
-    std::vector<int32_t> sel;    // nodeSelector requirement groups
-    std::vector<int32_t> terms;  // per valid term: {n_req, groups...}
-    int32_t n_terms = 0;
-    std::vector<int32_t> untol;  // taint ids the spec does not tolerate
-    uint64_t ports = 0;          // host-port state bits it sets (pod_port_mask)
-    std::vector<int32_t> anti_da, anti_db;  // anti-affinity terms: ANDNOT DA(t) / DB(t)
-  };
-  std::vector<SpecCanon> canon(n_specs);
-  auto put_req = [](std::vector<int32_t>& out, int32_t type, int32_t key, int32_t op, const int32_t* v, int32_t nv) {
-    const size_t at = out.size();
-    out.push_back(0);
-    out.push_back(type);
-    out.push_back(key);
-    out.push_back(op);
-    const size_t vb = out.size();
-    out.insert(out.end(), v, v + nv);
-    std::sort(out.begin() + vb, out.end());
-    out.erase(std::unique(out.begin() + vb, out.end()), out.end());
-    out[at] = static_cast<int32_t>(out.size() - at - 1);
-  };
-  parallel_for(n_specs, 64, [&](size_t lo, size_t hi) {
-    std::vector<int32_t> term;
-    for (size_t sp = lo; sp < hi; ++sp) {
-      SpecCanon& sc = canon[sp];
-      if (sp == 0) {  // unconstrained: tolerates nothing
-        for (int32_t t = 0; t < n_taints; ++t) sc.untol.push_back(t);
+  // ---- class keys: the static spec, plus (with anti-affinity) the pod's
+  // term ids of this call.  Pods without ids use their spec id as key.
+  const int32_t n_spec_ids = static_cast<int32_t>(C.spec.size());
+  std::vector<int32_t> pod_key(static_cast<size_t>(na));
+  std::vector<int32_t> key_spec;               // keys >= n_spec_ids: spec of the combined key
+  std::vector<std::vector<int32_t>> key_anti;  // ... and its term ids
+  {
+    WordDict combo;
+    std::vector<int32_t> kw;
+    for (int32_t q = 0; q < na; ++q) {
+      const int32_t j = active_src[q] - anti.base;
+      const int32_t n_ids = anti.active ? anti.pod_off[j + 1] - anti.pod_off[j] : 0;
+      if (n_ids == 0) {
+        pod_key[q] = pod_spec[q];
         continue;
       }
-      const int32_t pod = spec_rep[sp];
-      // Spec.NodeSelector: labels.SelectorFromSet -> Equals requirements.
-      for (int32_t i = P.sel_off[pod]; i < P.sel_off[pod + 1]; ++i)
-        put_req(sc.sel, REQ_LABEL_EQ, P.sel_key[i], SR_OP_IN, &P.sel_val[i], 1);
-      // Required node affinity: MatchNodeSelectorTerms.
-      if (P.aff_required[pod]) {
-        sc.flags |= CLS_AFF_REQUIRED;
-        for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t) {
-          const int32_t e0 = P.term_expr_off[t], e1 = P.term_expr_off[t + 1];
-          const int32_t f0 = P.term_field_off[t], f1 = P.term_field_off[t + 1];
-          if (e0 == e1 && f0 == f1) continue;  // an empty term selects nothing
-          bool valid = true;
-          term.clear();
-          for (int32_t e = e0; e < e1 && valid; ++e) {
-            const int32_t nv = P.expr_val_off[e + 1] - P.expr_val_off[e];
-            const int32_t op = P.expr_op[e];
-            if (P.expr_key[e] == c->id_empty) valid = false;  // validateLabelKey("") fails
-            else if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) valid = false;
-            else if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) valid = false;
-            else if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST)
-              valid = false;
-            if (valid) put_req(term, REQ_LABEL_EXPR, P.expr_key[e], op, P.expr_vals + P.expr_val_off[e], nv);
-          }
-          for (int32_t f = f0; f < f1 && valid; ++f) {
-            const int32_t nv = P.field_val_off[f + 1] - P.field_val_off[f];
-            const int32_t op = P.field_op[f];
-            valid = (op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 1;
-            if (valid) put_req(term, REQ_FIELD, P.field_key[f], op, &P.field_vals[P.field_val_off[f]], 1);
-          }
-          if (!valid) continue;  // a term that fails to build matches nothing
-          sc.terms.push_back(static_cast<int32_t>(f1 - f0 + e1 - e0));
-          sc.terms.insert(sc.terms.end(), term.begin(), term.end());
-          ++sc.n_terms;
-        }
-        if (sc.n_terms == 0) sc.flags |= CLS_IMPOSSIBLE;
+      kw.assign(1, pod_spec[q]);
+      kw.insert(kw.end(), anti.pod_ids.begin() + anti.pod_off[j], anti.pod_ids.begin() + anti.pod_off[j + 1]);
+      bool ins = false;
+      const int32_t id = combo.intern(kw, &ins);
+      if (ins) {
+        key_spec.push_back(pod_spec[q]);
+        key_anti.emplace_back(kw.begin() + 1, kw.end());
       }
-      // Spec.Tolerations against the spot pool's taints.
-      for (int32_t t = 0; t < n_taints; ++t)
-        if (!tolerates(P, pod, c->id_empty, taints[t])) sc.untol.push_back(t);
-      sc.ports = pod_port_mask(pod);
-      if (anti.active) {
-        const int32_t j = active_src[spec_rep_q[sp]];
-        for (int32_t k = anti.pod_off[j]; k < anti.pod_off[j + 1]; ++k) {
-          const int32_t t = anti.pod_ids[k] >> 1;
-          if (anti.pod_ids[k] & 1) {  // it has t: refuses domains hosting pods t selects
-            if (anti.db_any[t]) sc.anti_db.push_back(t);
-          } else {  // t selects it: refused by domains hosting pods that have t
-            if (anti.da_any[t]) sc.anti_da.push_back(t);
-          }
-        }
-      }
+      pod_key[q] = n_spec_ids + id;
     }
-  });
-
-  // ---- requirement ids and class signatures (serial: ids in spec order).
-  // Signature: {flags, n_sel, sel ids (sorted), n_terms, per term {n, ids (sorted)},
-  // untolerated-set id, ports lo, ports hi}.
-  WordDict rdict;      // requirement words {type, key, op, vals...}
-  WordDict untol_dict;  // untolerated taint sets
-  std::vector<int32_t> sig_words, sig_off{0}, ids;
-  for (size_t sp = 0; sp < n_specs; ++sp) {
-    const SpecCanon& sc = canon[sp];
-    auto intern_groups = [&](const int32_t* g, int32_t n_groups, size_t* used) {
-      ids.clear();
-      size_t i = 0;
-      for (int32_t k = 0; k < n_groups; ++k) {
-        ids.push_back(rdict.intern(g + i + 1, static_cast<size_t>(g[i])));
-        i += 1 + static_cast<size_t>(g[i]);
-      }
-      std::sort(ids.begin(), ids.end());
-      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-      sig_words.push_back(static_cast<int32_t>(ids.size()));
-      sig_words.insert(sig_words.end(), ids.begin(), ids.end());
-      if (used) *used = i;
-    };
-    sig_words.push_back(sc.flags);
-    int32_t n_sel = 0;
-    for (size_t i = 0; i < sc.sel.size(); i += 1 + static_cast<size_t>(sc.sel[i])) ++n_sel;
-    intern_groups(sc.sel.data(), n_sel, nullptr);
-    sig_words.push_back(sc.n_terms);
-    for (size_t i = 0, k = 0; k < static_cast<size_t>(sc.n_terms); ++k) {
-      size_t used = 0;
-      intern_groups(sc.terms.data() + i + 1, sc.terms[i], &used);
-      i += 1 + used;
-    }
-    sig_words.push_back(untol_dict.intern(sc.untol));
-    sig_words.push_back(static_cast<int32_t>(sc.ports & 0xffffffffu));
-    sig_words.push_back(static_cast<int32_t>(sc.ports >> 32));
-    sig_words.push_back(static_cast<int32_t>(sc.anti_da.size()));
-    sig_words.insert(sig_words.end(), sc.anti_da.begin(), sc.anti_da.end());
-    sig_words.push_back(static_cast<int32_t>(sc.anti_db.size()));
-    sig_words.insert(sig_words.end(), sc.anti_db.begin(), sc.anti_db.end());
-    sig_off.push_back(static_cast<int32_t>(sig_words.size()));
   }
-  const int32_t n_reqs = static_cast<int32_t>(rdict.size());
+  // distinct keys of this call, in first-occurrence order
+  std::vector<int32_t> key_slot(static_cast<size_t>(n_spec_ids) + key_spec.size(), -1);
+  std::vector<int32_t> keys;
+  for (int32_t q = 0; q < na; ++q)
+    if (key_slot[pod_key[q]] < 0) {
+      key_slot[pod_key[q]] = static_cast<int32_t>(keys.size());
+      keys.push_back(pod_key[q]);
+    }
+
+  // ---- per key: untolerated taints (cached per spec and static view), host
+  // ports of this call, anti-affinity atoms; the requirement atoms in use
+  if (C.untol_gen != C.static_gen) {
+    C.untol_dict.clear();
+    C.untol_gen = C.static_gen;
+  }
+  const int32_t n_taints = static_cast<int32_t>(C.taints.size());
+  std::vector<int32_t> untol_scratch;
+  auto untol_of = [&](int32_t spec_id) {
+    SpecInfo& sp = C.spec[spec_id];
+    if (sp.untol_gen != C.static_gen) {
+      untol_scratch.clear();
+      for (int32_t t = 0; t < n_taints; ++t)  // spec 0 (no tolerations) tolerates nothing
+        if (!tolerates(sp.tol, c->id_empty, C.taints[t])) untol_scratch.push_back(t);
+      sp.untol = C.untol_dict.intern(untol_scratch);
+      sp.untol_gen = C.static_gen;
+    }
+    return sp.untol;
+  };
+  std::vector<int32_t> req_atom(C.req_dict.size(), -1), used_reqs;
+  auto use_req = [&](int32_t r) {
+    if (req_atom[r] < 0) {
+      req_atom[r] = static_cast<int32_t>(used_reqs.size());
+      used_reqs.push_back(r);
+    }
+  };
+  for (int32_t k : keys) {
+    const SpecInfo& sp = C.spec[k < n_spec_ids ? k : key_spec[k - n_spec_ids]];
+    for (int32_t r : sp.sel) use_req(r);
+    for (size_t i = 0; i < sp.terms.size(); i += 1 + static_cast<size_t>(sp.terms[i]))
+      for (int32_t t = 0; t < sp.terms[i]; ++t) use_req(sp.terms[i + 1 + t]);
+  }
+  const int32_t n_reqs = static_cast<int32_t>(used_reqs.size());
   const int32_t n_ports = static_cast<int32_t>(port_query.size());
-  const int32_t A_REQ = 1, A_TAINT = 1 + n_reqs, A_PORT = 1 + n_reqs + n_taints;
+  const int32_t A_REQ = 1, A_TAINT = 1 + n_reqs, A_PORT = A_TAINT + n_taints;
+  const int32_t A_ANTI = A_PORT + n_ports;  // DA(t) at A_ANTI + 2t, DB(t) at A_ANTI + 2t + 1
+  const int32_t A_COMP = A_ANTI + 2 * anti.n_terms;
   // Composite atoms, one per distinct untolerated-taint set U of the pods:
   // atom 0 AND NOT (OR of U's taint atoms) -- the pod-count check and
   // TaintToleration / NodeUnschedulable in one row, so a class program opens
   // with a single AND instead of 1 + |U| operations.
-  const int32_t A_ANTI = A_PORT + n_ports;  // DA(t) at A_ANTI + 2t, DB(t) at A_ANTI + 2t + 1
-  const int32_t A_COMP = A_ANTI + 2 * anti.n_terms;
-  std::vector<int32_t> comp_of(untol_dict.size(), -1), comp_sets;  // untolerated-set ids
+  std::vector<int32_t> comp_of, comp_sets;
   auto comp_atom = [&](int32_t u) {
-    if (untol_dict.len(u) == 0) return 0;  // tolerates every taint: the pod-count atom alone
+    if (C.untol_dict.len(u) == 0) return 0;  // tolerates every taint: the pod-count atom alone
+    if (static_cast<size_t>(u) >= comp_of.size()) comp_of.resize(static_cast<size_t>(u) + 1, -1);
     if (comp_of[u] < 0) {
       comp_of[u] = static_cast<int32_t>(comp_sets.size());
       comp_sets.push_back(u);
     }
     return A_COMP + comp_of[u];
   };
-
   phase(2);
-  // ---- intern classes (atom programs), once per distinct signature
+
+  // ---- classes: one program per distinct signature {flags, selector ids,
+  // terms, untolerated set, host-port bits, anti-affinity atoms}
   WordDict class_dict;
-  std::vector<int32_t> spec_class(n_specs);
+  std::vector<int32_t> key_class(keys.size());
+  std::vector<uint64_t> key_ports(keys.size());
+  std::vector<int32_t> sig, da, db;
   w->cls_prog_off.push_back(0);
   auto emit = [&](int32_t atom, int32_t kind) { w->cls_prog.push_back(atom << 2 | kind); };
-  for (size_t sp = 0; sp < n_specs; ++sp) {
-    const int32_t* g = sig_words.data() + sig_off[sp];
+  for (size_t ki = 0; ki < keys.size(); ++ki) {
+    const int32_t k = keys[ki];
+    const int32_t spec_id = k < n_spec_ids ? k : key_spec[k - n_spec_ids];
+    const SpecInfo& sp = C.spec[spec_id];
+    const int32_t untol = untol_of(spec_id);
+    const uint64_t ports = port_mask(sp.ports);
+    key_ports[ki] = ports;
+    da.clear();
+    db.clear();
+    if (k >= n_spec_ids)
+      for (int32_t id : key_anti[k - n_spec_ids]) {
+        const int32_t t = id >> 1;
+        if (id & 1) {  // it has t: refuses domains hosting pods t selects
+          if (anti.db_any[t]) db.push_back(t);
+        } else {  // t selects it: refused by domains hosting pods that have t
+          if (anti.da_any[t]) da.push_back(t);
+        }
+      }
+    sig.clear();
+    sig.push_back(sp.flags);
+    sig.push_back(static_cast<int32_t>(sp.sel.size()));
+    sig.insert(sig.end(), sp.sel.begin(), sp.sel.end());
+    sig.push_back(sp.n_terms);
+    sig.insert(sig.end(), sp.terms.begin(), sp.terms.end());
+    sig.push_back(untol);
+    sig.push_back(static_cast<int32_t>(ports & 0xffffffffu));
+    sig.push_back(static_cast<int32_t>(ports >> 32));
+    sig.push_back(static_cast<int32_t>(da.size()));
+    sig.insert(sig.end(), da.begin(), da.end());
+    sig.push_back(static_cast<int32_t>(db.size()));
+    sig.insert(sig.end(), db.begin(), db.end());
     bool ins = false;
-    spec_class[sp] = class_dict.intern(g, static_cast<size_t>(sig_off[sp + 1] - sig_off[sp]), &ins);
+    key_class[ki] = class_dict.intern(sig, &ins);
     if (!ins) continue;
     // program: AND atoms, AND-NOT atoms, then the ORed terms (TERM_START
     // opens a term, TERM_AND extends it); an impossible class ANDs atom 0
     // with its complement
-    const int32_t flags = g[0], n_sel = g[1];
-    const int32_t* sel = g + 2;
-    const int32_t* tp = sel + n_sel;
-    const int32_t n_terms = *tp++;
-    const int32_t* term_words = tp;
-    for (int32_t k = 0; k < n_terms; ++k) tp += 1 + *tp;
-    const int32_t untol = tp[0];
-    const uint64_t ports = static_cast<uint32_t>(tp[1]) | static_cast<uint64_t>(static_cast<uint32_t>(tp[2])) << 32;
     emit(comp_atom(untol), PROG_AND);  // len(pods)+1 <= allowed pods, untolerated taints
-    for (int32_t k = 0; k < n_sel; ++k) emit(A_REQ + sel[k], PROG_AND);
+    for (int32_t r : sp.sel) emit(A_REQ + req_atom[r], PROG_AND);
     for (int32_t b = 0; b < 64; ++b)  // the base UsedPorts conflicting with each host port it asks for
       if ((ports >> b & 1) && bit_query[b] >= 0) emit(A_PORT + bit_query[b], PROG_ANDNOT);
-    {  // anti-affinity base conflicts
-      const int32_t* ad = tp + 3;
-      const int32_t nda = ad[0];
-      for (int32_t k = 0; k < nda; ++k) emit(A_ANTI + 2 * ad[1 + k], PROG_ANDNOT);
-      const int32_t* bd = ad + 1 + nda;
-      for (int32_t k = 0; k < bd[0]; ++k) emit(A_ANTI + 2 * bd[1 + k] + 1, PROG_ANDNOT);
-    }
-    if (flags & CLS_IMPOSSIBLE) {
+    for (int32_t t : da) emit(A_ANTI + 2 * t, PROG_ANDNOT);  // anti-affinity base conflicts
+    for (int32_t t : db) emit(A_ANTI + 2 * t + 1, PROG_ANDNOT);
+    if (sp.flags & CLS_IMPOSSIBLE) {
       emit(0, PROG_ANDNOT);
     } else {
-      for (int32_t k = 0; k < n_terms; ++k) {
-        const int32_t n = *term_words++;
-        for (int32_t i = 0; i < n; ++i) emit(A_REQ + term_words[i], i == 0 ? PROG_TERM_START : PROG_TERM_AND);
-        term_words += n;
-      }
+      for (size_t i = 0; i < sp.terms.size(); i += 1 + static_cast<size_t>(sp.terms[i]))
+        for (int32_t t = 0; t < sp.terms[i]; ++t)
+          emit(A_REQ + req_atom[sp.terms[i + 1 + t]], t == 0 ? PROG_TERM_START : PROG_TERM_AND);
     }
     w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
     w->n_classes++;
   }
   w->n_atoms = A_COMP + static_cast<int32_t>(comp_sets.size());
   phase(3);
-  // ---- spot nodes: base capacity state and the atom rows
-  const int32_t NP = w->n_pad, Wp = w->Wp;
-  w->free_cpu.assign(NP, 0);
-  w->free_mem.assign(NP, 0);
-  w->free_eph.assign(NP, 0);
-  w->pods_left.assign(NP, 0);
-  w->port_bits.assign(NP, 0);
+
+  // ---- atom rows: pod count (state), requirements and taints (static view,
+  // requirement rows cached), base port conflicts, anti-affinity, composites
   w->atoms.assign(static_cast<size_t>(w->n_atoms) * Wp, 0);
-  auto set_atom = [&](int32_t atom, int32_t n) {
-    w->atoms[static_cast<size_t>(atom) * Wp + (n >> 6)] |= 1ull << (n & 63);
-  };
-  for (int32_t n = 0; n < n_spot; ++n) {
-    const SpotNode& sn = snap->nodes[n];
-    const NodeState& st = snap->state[n];
-    for (int r = 0; r < 3; ++r) {
-      if (!in_range(sn.alloc[r]) || !in_range(st.requested[r])) {
-        *err = "spot node quantity outside [0, 2^62)";
-        return SR_ERR_CAPACITY;
-      }
+  uint64_t* A = w->atoms.data();
+  std::copy(C.podcount_row.begin(), C.podcount_row.end(), A);
+  {
+    if (C.req_rows.size() < C.req_dict.size()) {
+      C.req_rows.resize(C.req_dict.size());
+      C.req_row_gen.resize(C.req_dict.size(), ~0ull);
     }
-    w->free_cpu[n] = sn.alloc[0] - st.requested[0];
-    w->free_mem[n] = sn.alloc[1] - st.requested[1];
-    w->free_eph[n] = sn.alloc[2] - st.requested[2];
-    const int64_t left = sn.alloc_pods - st.npods;
-    w->pods_left[n] = static_cast<int32_t>(std::max<int64_t>(-(1 << 30), std::min<int64_t>(left, 1 << 30)));
-    if (left >= 1) set_atom(0, n);
-    // base UsedPorts: static conflicts (atoms A_PORT + q, in the F rows); the
-    // state word starts empty (it only carries the candidate's own pods)
-    w->port_bits[n] = 0;
-    for (const Port& u : st.ports)
-      for (int32_t q = 0; q < n_ports; ++q) {
-        const PortQuery& pq = port_query[q];
-        if (pq.proto == u.proto && pq.port == u.port && (pq.ip == -1 || u.ip == -1 || u.ip == pq.ip))
-          set_atom(A_PORT + q, n);
+    std::vector<int32_t> stale;
+    for (int32_t r : used_reqs)
+      if (C.req_row_gen[r] != C.static_gen) stale.push_back(r);
+    std::vector<const std::vector<int32_t>*> cols(stale.size(), nullptr);
+    for (size_t i = 0; i < stale.size(); ++i) {  // label columns: serial (the cache is not thread-safe)
+      const int32_t* rw = C.req_dict.data(stale[i]);
+      if (rw[0] != REQ_FIELD) cols[i] = &label_column(C, snap, rw[1]);
+    }
+    auto build = [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        const int32_t r = stale[i];
+        build_req_row(C, snap, C.req_dict.data(r), C.req_dict.len(r), cols[i], C.req_rows[r]);
+        C.req_row_gen[r] = C.static_gen;
       }
-    for (int32_t k = node_taint_off[n]; k < node_taint_off[n + 1]; ++k) set_atom(A_TAINT + node_taint_ids[k], n);
+    };
+    if (stale.size() > 8 && n_spot > 1024) parallel_for(stale.size(), 1, build);
+    else build(0, stale.size());
+    for (int32_t i = 0; i < n_reqs; ++i)
+      std::copy(C.req_rows[used_reqs[i]].begin(), C.req_rows[used_reqs[i]].end(),
+                A + static_cast<size_t>(A_REQ + i) * Wp);
   }
-  w->node_rec.assign(static_cast<size_t>(NP) * 8, 0);
-  for (int32_t n = 0; n < n_spot; ++n) {
-    uint64_t* r = &w->node_rec[static_cast<size_t>(n) * 8];
-    r[0] = static_cast<uint64_t>(w->free_cpu[n]);
-    r[1] = static_cast<uint64_t>(w->free_mem[n]);
-    r[2] = static_cast<uint64_t>(w->free_eph[n]);
-    r[3] = w->port_bits[n];
-    r[4] = static_cast<uint64_t>(static_cast<int64_t>(w->pods_left[n]));
-  }
-  // anti-affinity base conflicts: DA(t), DB(t)
+  std::copy(C.taint_rows.begin(), C.taint_rows.end(), A + static_cast<size_t>(A_TAINT) * Wp);
+  if (n_ports > 0)
+    for (int32_t n = 0; n < n_spot; ++n)
+      for (const Port& u : snap->state[n].ports)
+        for (int32_t q = 0; q < n_ports; ++q) {
+          const PortQuery& pq = port_query[q];
+          if (pq.proto == u.proto && pq.port == u.port && (pq.ip == -1 || u.ip == -1 || u.ip == pq.ip))
+            A[static_cast<size_t>(A_PORT + q) * Wp + (n >> 6)] |= 1ull << (n & 63);
+        }
   for (int32_t t = 0; t < anti.n_terms; ++t) {
-    std::copy_n(&anti.da[static_cast<size_t>(t) * Wp], Wp, &w->atoms[static_cast<size_t>(A_ANTI + 2 * t) * Wp]);
-    std::copy_n(&anti.db[static_cast<size_t>(t) * Wp], Wp, &w->atoms[static_cast<size_t>(A_ANTI + 2 * t + 1) * Wp]);
+    std::copy_n(&anti.da[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t) * Wp);
+    std::copy_n(&anti.db[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t + 1) * Wp);
   }
-  // composite atoms: atom 0 AND NOT (any taint of the set)
-  for (size_t k = 0; k < comp_sets.size(); ++k) {
-    uint64_t* row = &w->atoms[static_cast<size_t>(A_COMP + static_cast<int32_t>(k)) * Wp];
+  for (size_t k = 0; k < comp_sets.size(); ++k) {  // atom 0 AND NOT (any taint of the set)
+    uint64_t* row = A + static_cast<size_t>(A_COMP + static_cast<int32_t>(k)) * Wp;
+    const int32_t* u = C.untol_dict.data(comp_sets[k]);
+    const size_t nu = C.untol_dict.len(comp_sets[k]);
     for (int32_t i = 0; i < Wp; ++i) {
       uint64_t any = 0;
-      const int32_t* u = untol_dict.data(comp_sets[k]);
-      for (size_t j = 0; j < untol_dict.len(comp_sets[k]); ++j) any |= w->atoms[static_cast<size_t>(A_TAINT + u[j]) * Wp + i];
-      row[i] = w->atoms[i] & ~any;
+      for (size_t j = 0; j < nu; ++j) any |= C.taint_rows[static_cast<size_t>(u[j]) * Wp + i];
+      row[i] = A[i] & ~any;
     }
   }
-  phase(9);
-  // requirement atoms: one label-value column per distinct key
-  std::unordered_map<int32_t, std::vector<int32_t>> col;  // key -> value per node (INT32_MIN absent)
-  for (int32_t ri = 0; ri < n_reqs; ++ri) {
-    const int32_t* r = rdict.data(ri);  // {type, key, op, vals...}
-    if (r[0] != REQ_FIELD && !col.count(r[1])) col.emplace(r[1], std::vector<int32_t>(n_spot, INT32_MIN));
-  }
-  for (int32_t n = 0; n < n_spot; ++n)
-    for (const auto& kv : snap->nodes[n].labels) {
-      auto it = col.find(kv.first);
-      if (it != col.end()) it->second[n] = kv.second;
-    }
-  parallel_for(static_cast<size_t>(n_reqs), 1, [&](size_t rlo, size_t rhi) {
-  for (size_t ri = rlo; ri < rhi; ++ri) {  // one atom row per requirement: disjoint writes
-    const int32_t* rw = rdict.data(static_cast<int32_t>(ri));
-    const Requirement r{rw[0], rw[1], rw[2], std::vector<int32_t>(rw + 3, rw + rdict.len(static_cast<int32_t>(ri)))};
-    const int32_t atom = A_REQ + static_cast<int32_t>(ri);
-    if (r.type == REQ_FIELD) {
-      // fields.Set{"metadata.name": node.Name}; any other key reads as "".
-      const bool is_name = r.key == c->id_metadata_name && c->id_metadata_name != -1;
-      for (int32_t n = 0; n < n_spot; ++n) {
-        const int32_t fv = is_name ? snap->nodes[n].name : c->id_empty;
-        const bool eq = fv == r.vals[0];
-        if (r.op == SR_OP_IN ? eq : !eq) set_atom(atom, n);
-      }
-      continue;
-    }
-    const std::vector<int32_t>& v = col.at(r.key);
-    for (int32_t n = 0; n < n_spot; ++n) {
-      const bool has = v[n] != INT32_MIN;
-      bool m;
-      switch (r.op) {
-        case SR_OP_IN:
-          m = has && std::binary_search(r.vals.begin(), r.vals.end(), v[n]);
-          break;
-        case SR_OP_NOT_IN:
-          m = !has || !std::binary_search(r.vals.begin(), r.vals.end(), v[n]);
-          break;
-        case SR_OP_EXISTS:
-          m = has;
-          break;
-        default:  // DoesNotExist
-          m = !has;
-          break;
-      }
-      if (m) set_atom(atom, n);
-    }
-  }
-  });
-
   phase(4);
-  // ---- T row descriptors.  A pod asking r in one dimension uses the row of the
+
+  // ---- T rows.  A pod asking r in one dimension uses the row of the
   // smallest node free value v >= r: it selects exactly the nodes with
   // free >= r (no node value lies in [r, v)), and there are at most
   // min(distinct requests, distinct node values) such rows.  A request above
@@ -794,22 +1000,16 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   w->t_dim.push_back(3);
   w->t_thr.push_back(0);  // row 0: every node
   const int64_t kNever = INT64_MAX;  // free >= INT64_MAX never holds (free < 2^62)
-  std::vector<int64_t> node_vals[3];
-  const std::vector<int64_t>* frees[3] = {&w->free_cpu, &w->free_mem, &w->free_eph};
-  std::vector<int32_t> t_index[3];  // lower-bound position -> T row
   LowerBound lb[3];
-  parallel_for(3, 1, [&](size_t lo, size_t hi) {
-    for (size_t d = lo; d < hi; ++d) {
-      node_vals[d].assign(frees[d]->begin(), frees[d]->begin() + n_spot);
-      std::sort(node_vals[d].begin(), node_vals[d].end());
-      node_vals[d].erase(std::unique(node_vals[d].begin(), node_vals[d].end()), node_vals[d].end());
-      t_index[d].assign(node_vals[d].size() + 1, -1);
-      lb[d].build(node_vals[d]);
-    }
-  });
+  if (big)
+    for (int d = 0; d < 3; ++d) lb[d].build(C.node_vals[d]);
+  auto lower = [&](int d, int64_t x) -> size_t {
+    if (big) return lb[d](x);
+    const std::vector<int64_t>& v = C.node_vals[d];
+    return static_cast<size_t>(std::lower_bound(v.begin(), v.end(), x) - v.begin());
+  };
   // every field of pod_rows / pod_rec is written below (only the padding is
-  // cleared here): the vectors keep their size across encodes, so this is
-  // no zero fill in the steady state
+  // cleared here): the vectors keep their size across encodes
   w->pod_rows.resize(static_cast<size_t>(na) * 4);
   w->pod_rec.resize(static_cast<size_t>(na + 128) * 6);  // padded: K2 stages 64-pod halves
   std::fill(w->pod_rec.begin() + static_cast<size_t>(na) * 6, w->pod_rec.end(), 0);
@@ -824,15 +1024,15 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
   {
     std::vector<uint8_t> atom_empty(static_cast<size_t>(w->n_atoms)), atom_full(static_cast<size_t>(w->n_atoms));
     for (int32_t a = 0; a < w->n_atoms; ++a) {
-      const uint64_t* row = &w->atoms[static_cast<size_t>(a) * Wp];
+      const uint64_t* row = A + static_cast<size_t>(a) * Wp;
       int64_t pop = 0;
       for (int32_t i = 0; i < Wp; ++i) pop += __builtin_popcountll(row[i]);
       atom_empty[a] = pop == 0;
       atom_full[a] = pop == n_spot;
     }
-    for (int32_t c = 0; c < w->n_classes; ++c) {
+    for (int32_t k = 0; k < w->n_classes; ++k) {
       bool empty = false, has_terms = false, all_terms_empty = true, term_empty = false;
-      for (int32_t o = w->cls_prog_off[c]; o < w->cls_prog_off[c + 1]; ++o) {
+      for (int32_t o = w->cls_prog_off[k]; o < w->cls_prog_off[k + 1]; ++o) {
         const int32_t atom = w->cls_prog[o] >> 2, kind = w->cls_prog[o] & 3;
         if (kind == PROG_AND) {
           empty = empty || atom_empty[atom];
@@ -848,30 +1048,31 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
         }
       }
       if (has_terms) all_terms_empty = all_terms_empty && term_empty;
-      cls_empty[c] = empty || (has_terms && all_terms_empty);
+      cls_empty[k] = empty || (has_terms && all_terms_empty);
     }
   }
   std::atomic<bool> any_dead{false};
-  // per pod (parallel): requests, records and the lower-bound position of each
-  // request among the node values (stored in pod_rows[1..3] for now)
-  parallel_for(static_cast<size_t>(na), 2048, [&](size_t lo, size_t hi) {
+  // per pod: requests, records and the lower-bound position of each request
+  // among the node values (stored in pod_rows[1..3] for now)
+  pfor(static_cast<size_t>(na), 2048, [&](size_t lo, size_t hi) {
     for (size_t q = lo; q < hi; ++q) {
       const int32_t pod = active_pod[q];
       const int64_t rc = P.req_milli_cpu[pod], rm = P.req_memory[pod], re = P.req_ephemeral[pod];
       const bool zero = rc == 0 && rm == 0 && re == 0;
+      const int32_t ki = key_slot[pod_key[q]];
       int32_t* r = &w->pod_rows[q * 4];
-      r[0] = spec_class[pod_spec[q]];
-      r[1] = zero ? -1 : static_cast<int32_t>(lb[0](rc));
-      r[2] = zero ? -1 : static_cast<int32_t>(lb[1](rm));
-      r[3] = zero ? -1 : static_cast<int32_t>(lb[2](re));
+      r[0] = key_class[ki];
+      r[1] = zero ? -1 : static_cast<int32_t>(lower(0, rc));
+      r[2] = zero ? -1 : static_cast<int32_t>(lower(1, rm));
+      r[3] = zero ? -1 : static_cast<int32_t>(lower(2, re));
       uint64_t* rec = &w->pod_rec[q * 6];
       rec[0] = static_cast<uint64_t>(rc);
       rec[1] = static_cast<uint64_t>(rm);
       rec[2] = static_cast<uint64_t>(re);
-      rec[3] = canon[pod_spec[q]].ports |
-               (anti.active ? anti.pod_bits[active_src[q]] : 0);
+      rec[3] = key_ports[ki] | (anti.active ? anti.pod_bits[active_src[q] - anti.base] : 0);
       bool dead = cls_empty[r[0]] != 0;
-      for (int d = 0; d < 3; ++d) dead = dead || (r[1 + d] >= 0 && static_cast<size_t>(r[1 + d]) == node_vals[d].size());
+      for (int d = 0; d < 3; ++d)
+        dead = dead || (r[1 + d] >= 0 && static_cast<size_t>(r[1 + d]) == C.node_vals[d].size());
       if (dead) {
         r[0] = -1;  // the empty class, appended below
         any_dead.store(true, std::memory_order_relaxed);
@@ -885,43 +1086,34 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
     w->empty_class = w->n_classes++;
   }
-  phase(11);
   // positions -> T rows: row 0 = every node, then the used positions of each
   // dimension in increasing threshold order (rows grouped by dimension, so
   // K0 compares one dimension per wave)
-  std::vector<uint8_t> used[3];
-  for (int d = 0; d < 3; ++d) used[d].assign(node_vals[d].size() + 1, 0);
-  for (int32_t q = 0; q < na; ++q) {
-    const int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
-    for (int d = 0; d < 3; ++d)
-      if (r[1 + d] >= 0) used[d][static_cast<size_t>(r[1 + d])] = 1;
-  }
-  w->t_off[0] = 0;
-  w->t_off[1] = 1;
-  for (int d = 0; d < 3; ++d) {
-    for (size_t pos = 0; pos < used[d].size(); ++pos) {
-      if (!used[d][pos]) continue;
-      t_index[d][pos] = static_cast<int32_t>(w->t_dim.size());
-      w->t_dim.push_back(d);
-      w->t_thr.push_back(pos == node_vals[d].size() ? kNever : node_vals[d][pos]);
+  std::vector<int32_t> t_index[3];
+  {
+    std::vector<uint8_t> used[3];
+    for (int d = 0; d < 3; ++d) used[d].assign(C.node_vals[d].size() + 1, 0);
+    for (int32_t q = 0; q < na; ++q) {
+      const int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
+      for (int d = 0; d < 3; ++d)
+        if (r[1 + d] >= 0) used[d][static_cast<size_t>(r[1 + d])] = 1;
     }
-    w->t_off[d + 2] = static_cast<int32_t>(w->t_dim.size());
+    w->t_off[0] = 0;
+    w->t_off[1] = 1;
+    for (int d = 0; d < 3; ++d) {
+      t_index[d].assign(used[d].size(), -1);
+      for (size_t pos = 0; pos < used[d].size(); ++pos) {
+        if (!used[d][pos]) continue;
+        t_index[d][pos] = static_cast<int32_t>(w->t_dim.size());
+        w->t_dim.push_back(d);
+        w->t_thr.push_back(pos == C.node_vals[d].size() ? kNever : C.node_vals[d][pos]);
+      }
+      w->t_off[d + 2] = static_cast<int32_t>(w->t_dim.size());
+    }
   }
   phase(12);
-  // Node ranks: the dimension-d rows are in threshold order, so the rows a
-  // node belongs to (threshold <= its free value) are a prefix of them; K0
-  // sets bit n of the dimension's row r exactly when r < rank(n).
-  w->node_rank.assign(static_cast<size_t>(3) * NP, 0);
-  for (int d = 0; d < 3; ++d) {
-    std::vector<int32_t> below(used[d].size() + 1, 0);  // used positions in [0, pos)
-    for (size_t pos = 0; pos < used[d].size(); ++pos) below[pos + 1] = below[pos] + used[d][pos];
-    const std::vector<int64_t>& fr = *frees[d];
-    int32_t* rk = &w->node_rank[static_cast<size_t>(d) * NP];
-    for (int32_t n = 0; n < n_spot; ++n) rk[n] = below[lb[d](fr[n]) + 1];  // fr[n] is node_vals[d][pos]
-  }
-  phase(13);
-  parallel_for(static_cast<size_t>(na), 4096, [&](size_t lo, size_t hi) {
-    auto off = [&](int32_t table_row) { return static_cast<uint64_t>(table_row) * static_cast<uint64_t>(w->Wp); };
+  pfor(static_cast<size_t>(na), 4096, [&](size_t lo, size_t hi) {
+    auto off = [&](int32_t table_row) { return static_cast<uint64_t>(table_row) * static_cast<uint64_t>(Wp); };
     for (size_t q = lo; q < hi; ++q) {
       int32_t* r = &w->pod_rows[q * 4];
       if (r[0] < 0) r[0] = w->empty_class;
@@ -931,18 +1123,19 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
       rec[5] = off(w->n_classes + r[2]) | off(w->n_classes + r[3]) << 32;
     }
   });
-  if ((static_cast<uint64_t>(w->n_classes) + w->t_dim.size()) * static_cast<uint64_t>(w->Wp) >= (1ull << 32)) {
+  if ((static_cast<uint64_t>(w->n_classes) + w->t_dim.size()) * static_cast<uint64_t>(Wp) >= (1ull << 32)) {
     *err = "bitmask tables exceed 2^32 words";
     return SR_ERR_CAPACITY;
   }
+  phase(13);
 
   // ---- class programs of <= 8 operations in fixed 8-slot records (K0 reads
   // one record with one scalar load); -1 pads, -2 in slot 0 marks a longer
   // program (read through cls_prog_off)
   w->cls_prog8.assign(static_cast<size_t>(w->n_classes) * 8, -1);
-  for (int32_t c = 0; c < w->n_classes; ++c) {
-    const int32_t o = w->cls_prog_off[c], len = w->cls_prog_off[c + 1] - o;
-    int32_t* slot = &w->cls_prog8[static_cast<size_t>(c) * 8];
+  for (int32_t k = 0; k < w->n_classes; ++k) {
+    const int32_t o = w->cls_prog_off[k], len = w->cls_prog_off[k + 1] - o;
+    int32_t* slot = &w->cls_prog8[static_cast<size_t>(k) * 8];
     if (len > 8) {
       slot[0] = -2;
       continue;
@@ -950,19 +1143,18 @@ sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr
     for (int32_t i = 0; i < len; ++i) slot[i] = w->cls_prog[o + i];
   }
 
-  phase(5);
   // ---- K2 work list: longest candidates first (counting sort, stable)
   {
-    const size_t nc = w->cand_off.size() - 1;
+    const size_t n_act = w->cand_off.size() - 1;
     std::vector<int32_t> cnt(MAX_CAND_PODS + 2, 0);
-    for (size_t i = 0; i < nc; ++i) ++cnt[MAX_CAND_PODS - (w->cand_off[i + 1] - w->cand_off[i])];
+    for (size_t i = 0; i < n_act; ++i) ++cnt[MAX_CAND_PODS - (w->cand_off[i + 1] - w->cand_off[i])];
     for (int32_t v = 0, acc = 0; v <= MAX_CAND_PODS + 1; ++v) {
-      const int32_t c = cnt[v];
+      const int32_t k = cnt[v];
       cnt[v] = acc;
-      acc += c;
+      acc += k;
     }
-    w->list.assign(nc * 4, 0);
-    for (size_t i = 0; i < nc; ++i) {
+    w->list.assign(n_act * 4, 0);
+    for (size_t i = 0; i < n_act; ++i) {
       const int32_t b = w->cand_off[i], e = w->cand_off[i + 1];
       int32_t* l = &w->list[static_cast<size_t>(cnt[MAX_CAND_PODS - (e - b)]++) * 4];
       l[0] = static_cast<int32_t>(i);

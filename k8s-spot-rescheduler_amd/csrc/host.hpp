@@ -7,12 +7,15 @@
 // the gfx950 kernels consume (layout: DESIGN.md §HBM layout).
 #pragma once
 
+#include <climits>
+#include <deque>
 #include <cstdint>
 #include <string>
 #include <vector>
 
 #include "../../include/sr_planner.h"
 #include "progops.hpp"
+#include "worddict.hpp"
 
 namespace sr {
 
@@ -29,6 +32,7 @@ struct TaintRec {
 // Static part of one spot node, copied out of the caller's cluster when the
 // snapshot is created (AddNodeWithPods, nodes/nodes.go:229).
 struct SpotNode {
+  uint64_t static_fp = 0;  // node_static_fp
   int32_t name = -1;
   int64_t alloc[3] = {0, 0, 0};  // milli-cpu, memory, ephemeral
   int64_t alloc_pods = 0;
@@ -109,22 +113,21 @@ void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out);
 // Class descriptor flags.
 enum : int32_t { CLS_AFF_REQUIRED = 1, CLS_IMPOSSIBLE = 2 };
 
-// The encoded workload of one planning call (host copy; uploaded as one arena).
+// The encoded workload of one planning call (host copy; uploaded as one
+// arena).  The spot nodes' state (capacity records, free values) lives in the
+// EncoderCache and is uploaded only when it changes.
 struct Workload {
   // ---- dimensions
   int32_t n_spot = 0;   // spot nodes
   int32_t n_pad = 0;    // node arrays padded to Wp*64 entries
   int32_t Wp = 0;       // 64-bit words per bitmask row (even)
-  // ---- spot nodes (SoA, n_pad entries): base capacity state read by K0 / K2
-  std::vector<int64_t> free_cpu, free_mem, free_eph;
-  std::vector<int32_t> pods_left;
-  std::vector<uint64_t> port_bits;   // base UsedPorts over the port dictionary
-  std::vector<uint64_t> node_rec;    // [n_pad][8] AoS record of the above for K2's new slots
+  uint64_t state_gen = 0;  // EncoderCache state the workload refers to (node_rec / node_free)
   // ---- atom rows [n_atoms][Wp]: node bitsets every static predicate is built from
   //   atom 0                 len(pods)+1 <= allowed pods
   //   atoms 1 .. R           node matches requirement r (nodeSelector pair, matchExpression, matchField)
   //   atoms R+1 .. R+T       node carries NoSchedule/NoExecute taint t (incl. the unschedulable pseudo-taint)
-  //   atoms R+T+1 .. +Q      node's base UsedPorts holds (protocol, port) q
+  //   atoms R+T+1 .. +Q      node's base UsedPorts conflict with host port query q
+  //   then anti-affinity DA/DB pairs and composite (pod count AND NOT untolerated taints) atoms
   int32_t n_atoms = 0;
   std::vector<uint64_t> atoms;
   // ---- static pod classes as atom programs:
@@ -137,14 +140,13 @@ struct Workload {
   // skip the resource checks); other rows: free_<dim>[n] >= thr.
   std::vector<int32_t> t_dim;   // 0 cpu, 1 memory, 2 ephemeral, 3 all
   std::vector<int64_t> t_thr;
-  std::vector<int32_t> node_rank;  // [3][n_pad] rows of the dimension a node belongs to (a prefix)
   int32_t t_off[5] = {0, 0, 0, 0, 0};  // rows [t_off[i], t_off[i+1]): all, cpu, memory, ephemeral
   // ---- active pods, grouped by candidate, in podsForDeletion order
   std::vector<int32_t> pod_rows;  // [n][4]: S row (class), T rows for cpu, memory, ephemeral
   std::vector<uint64_t> pod_rec;  // [n + 128][6] AoS {cpu, memory, ephemeral, state bits, rows} for K2
-  // state bits of a node / the bits a pod sets: anti-affinity pairs in
-  // [0, 2 * n_pairs) (pair-swapped to get the bits a pod conflicts with),
-  // host ports above them
+  // state bits of a node / the bits a pod sets: anti-affinity pairs and host-port
+  // pairs in [0, swap region) (pair-swapped to get the bits a pod conflicts with),
+  // single host-port bits above them
   uint64_t swap_mask = 0;
   std::vector<int32_t> pod_src;  // index into the caller's cand_pods array
   // ---- active candidates
@@ -159,25 +161,95 @@ struct Workload {
   uint64_t fallback_pods = 0;
   int32_t n_input_cand = 0;
   int32_t n_input_pods = 0;
+  int32_t pod_base = 0;  // cand_pod_off[0] of the call: pod_src - pod_base indexes its pods
 
   // Back to the default state, keeping every buffer's capacity: a planner
   // encodes one tick after another, and fresh multi-MB buffers page-fault.
   void reset() {
-    for (auto* v : {&free_cpu, &free_mem, &free_eph, &t_thr}) v->clear();
-    for (auto* v : {&pods_left, &cls_prog_off, &cls_prog, &cls_prog8, &t_dim, &node_rank, &pod_src, &cand_off,
-                    &cand_global, &cand_src, &list, &status_host})
+    t_thr.clear();
+    for (auto* v : {&cls_prog_off, &cls_prog, &cls_prog8, &t_dim, &pod_src, &cand_off, &cand_global, &cand_src, &list,
+                    &status_host})
       v->clear();
-    for (auto* v : {&port_bits, &node_rec, &atoms}) v->clear();
+    atoms.clear();
     // pod_rows / pod_rec keep their size: the encoder resizes them and writes
     // every field, so a steady-state encode does not zero-fill them first
     n_spot = n_pad = Wp = n_atoms = n_classes = 0;
+    state_gen = 0;
     empty_class = -1;
     swap_mask = 0;
     for (int32_t& t : t_off) t = 0;
     max_cand_pods = 0;
     first_fallback = -1;
     fallback_pods = 0;
-    n_input_cand = n_input_pods = 0;
+    n_input_cand = n_input_pods = pod_base = 0;
+  }
+};
+
+// A distinct static pod spec (nodeSelector, required node affinity,
+// tolerations, host ports), canonical and independent of the nodes.
+struct SpecInfo {
+  int32_t flags = 0;           // CLS_AFF_REQUIRED, CLS_IMPOSSIBLE
+  std::vector<int32_t> sel;    // requirement ids of the nodeSelector pairs, sorted
+  std::vector<int32_t> terms;  // per buildable required term: {n, requirement ids sorted}
+  int32_t n_terms = 0;
+  std::vector<int32_t> tol;    // Spec.Tolerations {key, op, value, effect}*
+  std::vector<int32_t> ports;  // host ports {protocol, port, ip}* with port > 0
+  uint64_t untol_gen = ~0ull;  // static generation `untol` was computed for
+  int32_t untol = -1;          // set of spot-pool taints it does not tolerate (EncoderCache::untol_dict)
+};
+
+// What the encoder keeps across calls (one per sr_ctx).  The spot pool is
+// compared position by position against the last call's view through two
+// fingerprints per node: the static one (name, labels, taints, unschedulable)
+// and the state one (allocatable, requested, pod count, host ports).  Data
+// derived from an unchanged view is reused: label columns, requirement rows
+// and taint rows (static), capacity records, free values and their sorted
+// distinct values (state).  Specs, requirements and untolerated-taint sets are
+// interned by content; all of it is dropped when the interned ids of "",
+// "metadata.name" or the unschedulable key change, or when the dictionaries
+// grow past their bounds.
+struct EncoderCache {
+  int32_t id_empty = INT32_MIN, id_metadata_name = INT32_MIN, id_unschedulable_key = INT32_MIN;
+  // ---- static view
+  int32_t n_spot = -1, Wp = 0, n_pad = 0;
+  std::vector<int32_t> names;       // spot order (interned node names)
+  std::vector<uint64_t> static_fp;  // per position
+  uint64_t static_gen = 0;
+  std::deque<std::pair<int32_t, std::vector<int32_t>>> label_col;  // key -> value per position (INT32_MIN: absent);
+                                                                  // a deque: columns stay put while more are added
+  std::vector<TaintRec> taints;     // NoSchedule / NoExecute taints of the pool + the unschedulable pseudo-taint
+  std::vector<uint64_t> taint_rows; // [taint][Wp]
+  std::vector<uint64_t> req_row_gen;             // [req] static generation of its row (~0: none)
+  std::vector<std::vector<uint64_t>> req_rows;   // [req][Wp]
+  // ---- state view
+  std::vector<uint64_t> state_fp;
+  uint64_t state_gen = 0;
+  std::vector<uint64_t> node_rec;      // [n_pad][8] {free cpu, mem, eph, state bits (0), pods left, 0, 0, 0}
+  std::vector<int64_t> node_free;      // [3][n_pad] free cpu / memory / ephemeral (pads: INT64_MIN)
+  std::vector<uint64_t> podcount_row;  // [Wp] len(pods)+1 <= allowed pods
+  std::vector<int64_t> sorted_free[3]; // every node's free value, sorted
+  std::vector<int64_t> node_vals[3];   // distinct free values, sorted
+  // ---- content-interned, node independent
+  struct SpecShard {
+    WordDict dict;               // static spec words -> local id
+    std::vector<int32_t> global; // local id -> spec id
+  };
+  std::vector<SpecShard> spec_shards;  // by spec-word hash (a fixed count: ids do not depend on threads)
+  std::vector<SpecInfo> spec;          // [spec id]; spec 0 = no static constraints
+  WordDict req_dict;                   // requirement words {type, key, op, vals...} -> requirement id
+  WordDict untol_dict;                 // untolerated-taint sets (valid for untol_gen)
+  uint64_t untol_gen = ~0ull;
+  // ---- per-call counters (bench: what the last call had to rebuild)
+  int32_t last_new_specs = 0, last_static_changed = 0, last_state_changed = 0;
+
+  void clear_content() {  // drops every content-interned dictionary
+    spec_shards.clear();
+    spec.clear();
+    req_dict.clear();
+    req_rows.clear();
+    req_row_gen.clear();
+    untol_dict.clear();
+    untol_gen = ~0ull;
   }
 };
 
@@ -188,11 +260,12 @@ constexpr int32_t MAX_WORDS = 64 * 32; // spot nodes <= 131072
 // Required pod anti-affinity of one encode (antiaff.cpp).
 struct AntiTerms {
   bool active = false;
+  int32_t base = 0;                      // cand_pod_off[0]: per-pod arrays are indexed by flat index - base
   int32_t n_terms = 0;
   std::vector<uint8_t> node_local;       // [term] every spot node has the key, values pairwise distinct
   std::vector<uint64_t> da, db;          // [term][Wp] base conflicts: pods having / selected by the term
   std::vector<uint8_t> da_any, db_any;   // [term] the set is not empty
-  std::vector<int32_t> pod_off, pod_ids; // [flat candidate pod + 1] -> ids: term << 1 (selects it) | 1 (it has)
+  std::vector<int32_t> pod_off, pod_ids; // [flat candidate pod - base + 1] -> ids: term << 1 (selects it) | 1 (it has)
   std::vector<uint64_t> pod_bits;         // [flat candidate pod] state-bit pairs it sets, numbered per
                                          // candidate (A = 2p: it has term p, B = 2p + 1: term p selects it)
   int32_t n_pairs = 0;                   // most pairs any candidate uses (<= 32)
@@ -204,8 +277,13 @@ struct AntiTerms {
 void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
                   std::vector<int32_t>& status, AntiTerms* out);
 
-// Builds the workload; returns SR_OK or an error with *err filled.
-sr_status encode_workload(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
-                          Workload* w, std::string* err);
+// Builds the workload; returns SR_OK or an error with *err filled.  `cache`
+// carries what the previous calls derived (and is updated).
+sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr_cluster* c,
+                          const sr_candidates* cands, Workload* w, std::string* err);
+
+// Fingerprint of a spot node's static part (name, unschedulable, labels,
+// taints): computed when the snapshot is created.
+uint64_t node_static_fp(const SpotNode& n);
 
 }  // namespace sr

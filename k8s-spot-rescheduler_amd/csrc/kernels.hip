@@ -181,10 +181,10 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
     return;
   }
   // T rows: one wave per (dimension, group of 64 rows, kTWords words), lanes
-  // = rows.  A node lies in its dimension's rows [0, rank) (the encoder's
-  // node ranks), so bit i of lane r's word W is r < rank[64 W + i]: the
-  // word's 64 ranks are one coalesced load, each broadcast by a readlane, and
-  // a node costs a compare and a shift-or -- no cross-lane ballots.
+  // = rows.  Bit i of lane r's word W is free[64 W + i] >= threshold[r]: the
+  // word's 64 free values are one coalesced load, each broadcast by a
+  // readlane pair, and a node costs a 64-bit compare and a shift-or -- no
+  // cross-lane ballots.  Pad nodes hold INT64_MIN and never pass.
   int tw = (static_cast<int>(blockIdx.x) - s_blocks) * 4 + wave;
   const int wgroups = (w.Wp + kTWords - 1) / kTWords;
   int d = 0;
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
   const int W0 = (tw - g * wgroups) * kTWords;
   const int r0 = w.t_off[d] + 64 * g;
   const int nr = min(64, w.t_off[d + 1] - r0);
-  const int rr = 64 * g + lane;  // this lane's row within the dimension
+  const int64_t thr = lane < nr ? w.t_thr[r0 + lane] : INT64_MAX;
 #pragma unroll
   for (int ww = 0; ww < kTWords; ++ww) {
     const int W = W0 + ww;
@@ -208,12 +208,13 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
       const int nvalid = max(0, min(64, w.n_spot - 64 * W));
       word = nvalid >= 64 ? ~0ull : (1ull << nvalid) - 1;
     } else {
-      const int rk = w.node_rank[static_cast<size_t>(d - 1) * w.n_pad + 64 * W + lane];  // pad nodes: 0
+      const uint64_t fv = static_cast<uint64_t>(w.node_free[static_cast<size_t>(d - 1) * w.n_pad + 64 * W + lane]);
       uint32_t lo = 0, hi = 0;
 #pragma unroll
-      for (int i = 0; i < 32; ++i) lo |= static_cast<uint32_t>(rr < __builtin_amdgcn_readlane(rk, i)) << i;
+      for (int i = 0; i < 32; ++i) lo |= static_cast<uint32_t>(static_cast<int64_t>(readlane64(fv, i)) >= thr) << i;
 #pragma unroll
-      for (int i = 0; i < 32; ++i) hi |= static_cast<uint32_t>(rr < __builtin_amdgcn_readlane(rk, 32 + i)) << i;
+      for (int i = 0; i < 32; ++i)
+        hi |= static_cast<uint32_t>(static_cast<int64_t>(readlane64(fv, 32 + i)) >= thr) << i;
       word = static_cast<uint64_t>(hi) << 32 | lo;
     }
     if (lane < nr) w.T[static_cast<size_t>(r0 + lane) * Wp + W] = word;

@@ -15,7 +15,7 @@ constexpr size_t kK0ProfWaves = 32768;  // K0 waves profiled after K2's [n_cand]
 // Pointers into the device arena (layout: DESIGN.md §HBM layout).
 struct DevWorkload {
   int32_t n_spot, n_pad, Wp;
-  const int32_t* node_rank;    // [3][n_pad] per dimension: the node is in that dimension's T rows [0, rank)
+  const int64_t* node_free;    // [3][n_pad] free cpu / memory / ephemeral per spot node (pads: INT64_MIN)
   const uint64_t* node_rec;    // [n_pad][8] AoS {free cpu, mem, eph, state bits, pods_left, 0, 0, 0} for K2
   int32_t n_atoms;
   const uint64_t* atoms;       // [n_atoms][Wp] node bitsets (encode.cpp)

@@ -39,11 +39,15 @@ struct sr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  DevBuf arena, tables, out_node, out_status, out_bytes, dmin, prof;
+  DevBuf arena, tables, out_node, out_status, out_bytes, dmin, prof, scratch;
   HostBuf h_arena, h_result, h_status, h_node, h_bytes;
   uint64_t issued_checks = 0;  // checks of the prepared workload's plan (known after a full run)
   bool issued_known = false;
   sr::Workload wl;
+  sr::EncoderCache enc;      // what the encoder keeps across calls (encode.cpp)
+  uint64_t dev_state_gen = ~0ull;  // encoder state whose node records the device arena holds
+  hipEvent_t ev_upload = nullptr;  // the last upload (the staging buffer is reused after it)
+  int32_t prefix_batch = 64;       // first batch of sr_plan_first (SR_PREFIX_BATCH)
   sr::DevWorkload dw{};
   bool prepared = false;
   int32_t timing = 0;        // SR_TIME_* kernel bits of the current setting
@@ -109,9 +113,9 @@ class Packer {
     return off;
   }
   size_t size() const { return (size_ + 255) & ~size_t(255); }
-  void copy_to(char* dst) const {
+  void copy_to(char* dst, size_t from = 0) const {  // the sections at or after `from`
     for (const auto& it : items_)
-      if (it.bytes) std::memcpy(dst + it.off, it.src, it.bytes);
+      if (it.bytes && it.off >= from) std::memcpy(dst + it.off, it.src, it.bytes);
   }
 
  private:
@@ -129,16 +133,21 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   ctx->prepared = false;
   sr::Workload& w = ctx->wl;
   std::string err;
-  sr_status st = sr::encode_workload(snap, c, cands, &w, &err);
+  sr_status st = sr::encode_workload(&ctx->enc, snap, c, cands, &w, &err);
   if (st != SR_OK) {
     ctx->err = err;
+    ctx->dev_state_gen = ~0ull;  // the encoder may have moved on: upload the node records again
     return st;
   }
   const int32_t na = static_cast<int32_t>(w.pod_src.size());
   const int32_t ncand = static_cast<int32_t>(w.cand_global.size());
+  // Arena: the spot nodes' records and free values first (uploaded only when
+  // the encoder's state view changed), then this call's sections.
+  const sr::EncoderCache& E = ctx->enc;
   Packer pk;
-  const size_t o_rk = pk.add(w.node_rank);
-  const size_t o_nr = pk.add(w.node_rec);
+  const size_t o_nr = pk.add(E.node_rec);
+  const size_t o_nf = pk.add(E.node_free);
+  const size_t node_bytes = pk.size();
   const size_t o_at = pk.add(w.atoms);
   const size_t o_cpo = pk.add(w.cls_prog_off), o_cp = pk.add(w.cls_prog), o_cp8 = pk.add(w.cls_prog8);
   const size_t o_tt = pk.add(w.t_thr);
@@ -148,8 +157,11 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t bytes = pk.size();
 
   HIP_TRY(ctx, hipSetDevice(ctx->device));
+  if (ctx->ev_upload) HIP_TRY(ctx, hipEventSynchronize(ctx->ev_upload));  // staging buffer free again
   HIP_TRY(ctx, host_reserve(ctx->h_arena, bytes));
-  HIP_TRY(ctx, dev_reserve(ctx->arena, bytes));
+  const size_t arena_cap = ctx->arena.cap;
+  HIP_TRY(ctx, dev_reserve(ctx->arena, bytes));  // a new allocation holds no node records
+  const bool nodes_resident = ctx->arena.cap == arena_cap && ctx->dev_state_gen == w.state_gen;
   const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
   HIP_TRY(ctx, dev_reserve(ctx->tables, n_rows * row_bytes));
@@ -160,9 +172,13 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t res_bytes = sizeof(uint64_t) * (sr::kResultHeader + static_cast<size_t>(std::max(1, w.max_cand_pods)));
   HIP_TRY(ctx, host_reserve(ctx->h_result, res_bytes));  // mapped: K3 writes the result straight to the host
   auto t1 = std::chrono::steady_clock::now();
-  pk.copy_to(static_cast<char*>(ctx->h_arena.p));
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->arena.p, ctx->h_arena.p, bytes, hipMemcpyHostToDevice, ctx->stream));
-  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  const size_t from = nodes_resident ? node_bytes : 0;
+  pk.copy_to(static_cast<char*>(ctx->h_arena.p), from);
+  HIP_TRY(ctx, hipMemcpyAsync(static_cast<char*>(ctx->arena.p) + from, static_cast<char*>(ctx->h_arena.p) + from,
+                              bytes - from, hipMemcpyHostToDevice, ctx->stream));
+  if (!ctx->ev_upload) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_upload, hipEventDisableTiming));
+  HIP_TRY(ctx, hipEventRecord(ctx->ev_upload, ctx->stream));  // kernels queue behind the copy
+  ctx->dev_state_gen = w.state_gen;
   auto t2 = std::chrono::steady_clock::now();
 
   char* base = static_cast<char*>(ctx->arena.p);
@@ -172,8 +188,8 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.n_spot = w.n_spot;
   d.n_pad = w.n_pad;
   d.Wp = w.Wp;
-  d.node_rank = static_cast<const int32_t*>(at(o_rk));
   d.node_rec = static_cast<const uint64_t*>(at(o_nr));
+  d.node_free = static_cast<const int64_t*>(at(o_nf));
   d.n_atoms = w.n_atoms;
   d.atoms = static_cast<const uint64_t*>(at(o_at));
   d.cls_prog_off = static_cast<const int32_t*>(at(o_cpo));
@@ -209,12 +225,13 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   void* dres = nullptr;
   HIP_TRY(ctx, hipHostGetDevicePointer(&dres, ctx->h_result.p, 0));
   d.result = static_cast<uint64_t*>(dres);
+  ctx->t.bytes_uploaded = static_cast<uint64_t>(bytes - from);
 
   const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
   // K0 algorithmic bytes: every table row written once; every atom row a class
   // program names, the nodes' free capacities and the thresholds read once.
   uint64_t atom_reads = w.cls_prog.size();
-  ctx->t.bytes_tables = n_rows * row + atom_reads * row + 3ull * 4 * w.n_pad + 32ull * w.n_classes;
+  ctx->t.bytes_tables = n_rows * row + atom_reads * row + 3ull * 8 * w.n_pad + 32ull * w.n_classes;
   // K2: counted by the kernel itself per candidate (out_bytes), read back by
   // the next run with status or node_of_pod outputs
   ctx->t.bytes_placement = 0;
@@ -229,6 +246,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   ctx->t.n_rows_static = d.n_classes;
   ctx->t.n_rows_threshold = d.n_t;
   ctx->t.n_classes = w.n_classes;
+  ctx->t.enc_new_specs = ctx->enc.last_new_specs;
+  ctx->t.enc_static_rebuilt = ctx->enc.last_static_changed;
+  ctx->t.enc_state_nodes = ctx->enc.last_state_changed;
   ctx->prepared = true;
   return SR_OK;
 }
@@ -397,7 +417,7 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     ctx->issued_known = true;
     if (out->node_of_pod) {
       for (int32_t i = 0; i < w.n_input_pods; ++i) out->node_of_pod[i] = -1;
-      for (int32_t q = 0; q < na; ++q) out->node_of_pod[w.pod_src[q]] = hn[q];
+      for (int32_t q = 0; q < na; ++q) out->node_of_pod[w.pod_src[q] - w.pod_base] = hn[q];
     }
   }
   out->checks = ctx->issued_known ? ctx->issued_checks : 0;
@@ -405,6 +425,9 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
 }
 
 }  // namespace
+
+static sr_status plan_first(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
+                            sr_plan_out* out);
 
 extern "C" {
 
@@ -426,6 +449,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   }
   if (const char* path = std::getenv("SR_K2_PROFILE")) ctx->prof_file = std::fopen(path, "ab");
   if (const char* m = std::getenv("SR_K2_MODE")) ctx->k2_mode = std::atoi(m) == 1 ? 1 : 0;
+  if (const char* b = std::getenv("SR_PREFIX_BATCH")) ctx->prefix_batch = std::max(1, std::atoi(b));
   *out = ctx;
   return SR_OK;
 }
@@ -436,8 +460,9 @@ void sr_destroy(sr_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   for (DevBuf* b : {&ctx->arena, &ctx->tables, &ctx->out_node, &ctx->out_status, &ctx->out_bytes, &ctx->dmin,
-                    &ctx->prof})
+                    &ctx->prof, &ctx->scratch})
     if (b->p) (void)hipFree(b->p);
+  if (ctx->ev_upload) (void)hipEventDestroy(ctx->ev_upload);
   for (HostBuf* b : {&ctx->h_arena, &ctx->h_result, &ctx->h_status, &ctx->h_node, &ctx->h_bytes})
     if (b->p) (void)hipHostFree(b->p);
   for (auto* v : {&ctx->ev_start, &ctx->ev_end})
@@ -448,6 +473,12 @@ void sr_destroy(sr_ctx* ctx) {
 }
 
 const char* sr_last_error(const sr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+sr_status sr_plan_first(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* cluster, const sr_candidates* cands,
+                        sr_plan_out* out) {
+  if (!ctx || !snap || !cluster || !cands || !out || cands->n_cand < 0) return SR_ERR_INVALID_ARG;
+  return plan_first(ctx, snap, cluster, cands, out);
+}
 
 sr_status sr_plan_prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* cluster, const sr_candidates* cands) {
   if (!ctx || !snap || !cluster || !cands || cands->n_cand < 0) return SR_ERR_INVALID_ARG;
@@ -465,6 +496,90 @@ sr_status sr_plan(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* cluste
   sr_status st = prepare(ctx, snap, cluster, cands);
   if (st != SR_OK) return st;
   return run(ctx, out, out->status != nullptr || out->node_of_pod != nullptr, true);
+}
+
+// Largest value over the ranks (one RCCL allreduce; the value itself without a communicator).
+static sr_status comm_max(sr_ctx* ctx, int32_t v, int32_t* out) {
+  *out = v;
+  if (!ctx->comm) return SR_OK;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, dev_reserve(ctx->scratch, 64));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->scratch.p, &v, sizeof(v), hipMemcpyHostToDevice, ctx->stream));
+  ncclResult_t r = ncclAllReduce(ctx->scratch.p, ctx->scratch.p, 1, ncclInt32, ncclMax, ctx->comm, ctx->stream);
+  if (r != ncclSuccess) {
+    ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+    return SR_ERR_RCCL;
+  }
+  HIP_TRY(ctx, hipMemcpyAsync(out, ctx->scratch.p, sizeof(*out), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return SR_OK;
+}
+
+// run()'s loop with its break (rescheduler.go:228-287): prefix batches of
+// candidates, each encoded and planned on its own, until one holds a
+// drainable candidate.  Batch k covers local candidates [lo_k, hi_k) on every
+// rank, so every global index below the ranks' hi_k has been planned once it
+// ends: the first drainable one found is the first overall.
+static sr_status plan_first(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
+                            sr_plan_out* out) {
+  const int32_t n = cands->n_cand;
+  const int32_t* off = cands->cand_pod_off;
+  const bool full = out->status != nullptr || out->node_of_pod != nullptr;
+  if (out->status)
+    for (int32_t i = 0; i < n; ++i) out->status[i] = SR_CAND_SKIPPED;
+  if (out->node_of_pod && n > 0)
+    for (int32_t i = 0; i < off[n] - off[0]; ++i) out->node_of_pod[i] = -1;
+  std::vector<int32_t> glob;
+  if (!cands->cand_global) {
+    glob.resize(static_cast<size_t>(std::max(0, n)));
+    for (int32_t i = 0; i < n; ++i) glob[i] = i;
+  }
+  const int32_t* G = cands->cand_global ? cands->cand_global : glob.data();
+  int32_t n_all = n;
+  sr_status st = comm_max(ctx, n, &n_all);
+  if (st != SR_OK) return st;
+  out->winner = out->first_ok = out->first_fallback = -1;
+  out->winner_npods = 0;
+  out->checks = out->fallback_pods = out->checks_dense = 0;
+  std::vector<int32_t> bst, bnode;
+  int32_t batches = 0;
+  for (int32_t lo = 0, B = ctx->prefix_batch; lo < n_all || batches == 0; B = std::min(B * 2, 1 << 20)) {
+    const int32_t hi = std::min(n_all, lo + B);
+    const int32_t l0 = std::min(lo, n), l1 = std::min(hi, n);
+    sr_candidates sub{l1 - l0, off + l0, cands->cand_pods, G + l0};
+    sr_plan_out o{};
+    o.winner_map = out->winner_map;
+    if (full) {
+      bst.assign(static_cast<size_t>(std::max(1, l1 - l0)), 0);
+      bnode.assign(static_cast<size_t>(std::max(1, n > 0 ? off[l1] - off[l0] : 0)), -1);
+      o.status = bst.data();
+      o.node_of_pod = bnode.data();
+    }
+    st = prepare(ctx, snap, c, &sub);
+    if (st != SR_OK) return st;
+    st = run(ctx, &o, full, true);
+    if (st != SR_OK) return st;
+    ++batches;
+    if (full) {
+      if (out->status) std::copy(bst.begin(), bst.begin() + (l1 - l0), out->status + l0);
+      if (out->node_of_pod && n > 0) std::copy(bnode.begin(), bnode.begin() + (off[l1] - off[l0]), out->node_of_pod + (off[l0] - off[0]));
+    }
+    out->checks += o.checks;
+    out->checks_dense += o.checks_dense;
+    out->fallback_pods += o.fallback_pods;
+    if (o.first_fallback >= 0 && (out->first_fallback < 0 || o.first_fallback < out->first_fallback))
+      out->first_fallback = o.first_fallback;
+    if (o.first_ok >= 0) {
+      out->first_ok = o.first_ok;
+      out->winner_npods = o.winner_npods;
+      break;
+    }
+    lo = hi;
+  }
+  out->winner = (out->first_ok >= 0 && (out->first_fallback < 0 || out->first_fallback > out->first_ok))
+                    ? out->first_ok : -1;
+  ctx->t.prefix_batches = batches;
+  return SR_OK;
 }
 
 // Single-process helpers (no collective): findSpotNodeForPod / canDrainNode.

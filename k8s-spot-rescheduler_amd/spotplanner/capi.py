@@ -114,7 +114,9 @@ class sr_timing(ctypes.Structure):
                 ("bytes_tables", ctypes.c_uint64), ("bytes_placement", ctypes.c_uint64),
                 ("n_pods", ctypes.c_int32), ("n_spot", ctypes.c_int32), ("n_cand", ctypes.c_int32),
                 ("n_words", ctypes.c_int32), ("n_rows_static", ctypes.c_int32), ("n_rows_threshold", ctypes.c_int32),
-                ("n_classes", ctypes.c_int32)]
+                ("n_classes", ctypes.c_int32), ("bytes_uploaded", ctypes.c_uint64), ("enc_new_specs", ctypes.c_int32),
+                ("enc_static_rebuilt", ctypes.c_int32), ("enc_state_nodes", ctypes.c_int32),
+                ("prefix_batches", ctypes.c_int32)]
 
 
 def ptr(arr, typ):
@@ -236,6 +238,8 @@ def _declare_planner(lib):
     lib.sr_can_drain_node.restype = S
     lib.sr_plan.argtypes = [VP, VP, PC, ctypes.POINTER(sr_candidates), ctypes.POINTER(sr_plan_out)]
     lib.sr_plan.restype = S
+    lib.sr_plan_first.argtypes = [VP, VP, PC, ctypes.POINTER(sr_candidates), ctypes.POINTER(sr_plan_out)]
+    lib.sr_plan_first.restype = S
     lib.sr_plan_prepare.argtypes = [VP, VP, PC, ctypes.POINTER(sr_candidates)]
     lib.sr_plan_prepare.restype = S
     lib.sr_plan_run.argtypes = [VP, ctypes.POINTER(sr_plan_out)]
@@ -254,5 +258,5 @@ def _declare_planner(lib):
 EXPORTED = ["sr_new_node_map", "sr_node_has_label", "sr_pods_for_deletion", "sr_snapshot_create", "sr_snapshot_destroy",
             "sr_snapshot_add_pod", "sr_snapshot_fork", "sr_snapshot_revert", "sr_snapshot_node_state",
             "sr_snapshot_num_nodes", "sr_create", "sr_destroy", "sr_last_error", "sr_build_info",
-            "sr_find_spot_nodes", "sr_can_drain_node", "sr_plan", "sr_plan_prepare", "sr_plan_run",
+            "sr_find_spot_nodes", "sr_can_drain_node", "sr_plan", "sr_plan_first", "sr_plan_prepare", "sr_plan_run",
             "sr_set_timing", "sr_get_timing", "sr_comm_unique_id", "sr_comm_init"]

@@ -1,0 +1,228 @@
+"""Consecutive ticks through one planner (the persistent encoder)
+and the reference-faithful prefix-batched tick (sr_plan_first).
+
+run() rebuilds its model every housekeeping tick (rescheduler.go:195,215) and
+stops at the first drainable candidate (:280-286).  The planner keeps what it
+derived from the previous tick (spot-node views, specs, requirement rows) and
+re-encodes what changed; these tests change one thing at a time between ticks
+-- a pod added on one spot node, node labels and taints, a different cluster,
+a different string interner -- and check every tick against the oracle."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from helpers import Scenario
+from oracle_lib import OracleSnapshot, oracle_plan
+from randcluster import rand_scenario
+from spotplanner import capi
+from spotplanner.model import Interner, Taint
+from spotplanner.rescheduler import plan_arrays
+from spotplanner.synth import SynthCluster, build_candidates, new_node_map
+
+pytestmark = pytest.mark.gpu
+SKIPPED = capi.SR_CAND_SKIPPED
+
+
+def plan_first(checker, h, cluster_ptr, cand_off, cand_pods, full=True):
+    lib = capi.load_planner()
+    n = len(cand_off) - 1
+    c = capi.sr_candidates(n, capi.ptr(cand_off, capi.P32), capi.ptr(cand_pods, capi.P32), None)
+    status = np.full(max(1, n), -99, np.int32)
+    nodes = np.full(max(1, int(cand_off[-1]) if n else 1), -99, np.int32)
+    wmap = np.full(max(1, int(np.max(np.diff(cand_off))) if n else 1), -1, np.int32)
+    o = capi.sr_plan_out()
+    if full:
+        o.status = capi.ptr(status, capi.P32)
+        o.node_of_pod = capi.ptr(nodes, capi.P32)
+    o.winner_map = capi.ptr(wmap, capi.P32)
+    st = lib.sr_plan_first(checker.handle, h, cluster_ptr, ctypes.byref(c), ctypes.byref(o))
+    assert st == capi.SR_OK, checker.last_error()
+    return o, status[:n], nodes[: int(cand_off[-1]) if n else 0], wmap[: o.winner_npods]
+
+
+def check_first(o, status, nodes, wmap, ref_all, ref_early, cand_off, full=True):
+    """sr_plan_first against the oracle: the reference loop's winner and
+    mapping; every candidate it evaluated (up to its batch's end) equal to the
+    all-candidates oracle, SR_CAND_SKIPPED after."""
+    assert o.first_ok == ref_early["first_ok"] == ref_all["first_ok"]
+    assert o.winner == ref_early["winner"]
+    assert list(wmap) == list(ref_early["winner_map"])
+    if not full:
+        return
+    n = len(cand_off) - 1
+    seen_skip = False
+    for c in range(n):
+        if status[c] == SKIPPED:
+            seen_skip = True
+            assert o.first_ok >= 0 and c > o.first_ok, c
+            continue
+        assert not seen_skip, c  # evaluated candidates form a prefix
+        assert status[c] == ref_all["status"][c], c
+        seg = slice(int(cand_off[c]), int(cand_off[c + 1]))
+        assert list(nodes[seg]) == list(ref_all["node_of_pod"][seg]), c
+
+
+@pytest.fixture(scope="module")
+def small_batch_checker():
+    from spotplanner.planner import PredicateChecker
+    os.environ["SR_PREFIX_BATCH"] = "2"
+    try:
+        c = PredicateChecker(0)
+    finally:
+        del os.environ["SR_PREFIX_BATCH"]
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("which", ["default", "batch2"])
+def test_plan_first_matches_reference_loop(checker, small_batch_checker, seed, which):
+    ck = checker if which == "default" else small_batch_checker
+    nodes, spot_pods, cands = rand_scenario(9500 + seed, n_spot=6 + seed % 9, n_cand=14, max_pods=9,
+                                            anti=0.3 if seed % 3 == 0 else 0.0)
+    flat = [p for c in cands for p in c]
+    sc = Scenario(nodes, spot_pods, flat)
+    cand_off = np.cumsum([0] + [len(c) for c in cands]).astype(np.int32)
+    cand_pods = np.arange(sc.q0, sc.q0 + len(flat), dtype=np.int32)
+    ref_all = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=1)
+    ref_early = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=0)
+    if any(s == capi.SR_CAND_FALLBACK for s in ref_all["status"]):
+        pytest.skip("the oracle routes a candidate to the reference path")
+    h = sc.product_snapshot()
+    try:
+        for full in (True, False):
+            o, status, nodes_o, wmap = plan_first(ck, h, sc.ptr, cand_off, cand_pods, full)
+            if o.first_fallback >= 0:  # the product routed one more candidate (off-node anti-affinity)
+                continue
+            check_first(o, status, nodes_o, wmap, ref_all, ref_early, cand_off, full)
+    finally:
+        capi.load_planner().sr_snapshot_destroy(h)
+
+
+@pytest.mark.parametrize("config", [1, 2, 3, 5])
+def test_plan_first_synthetic_configs(checker, small_batch_checker, config):
+    sc = SynthCluster(config)
+    lib = capi.load_planner()
+    nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+    osnap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
+    ref_all = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
+    ref_early = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=0)
+    h = ctypes.c_void_p()
+    assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot),
+                                  capi.ptr(nm.node_pod_off, capi.P32), capi.ptr(nm.node_pod_idx, capi.P32),
+                                  ctypes.byref(h)) == capi.SR_OK
+    try:
+        for ck in (checker, small_batch_checker):
+            o, status, nodes_o, wmap = plan_first(ck, h, sc.ptr, cand_off, cand_pods)
+            check_first(o, status, nodes_o, wmap, ref_all, ref_early, cand_off)
+            assert o.checks > 0 and ck.timing().prefix_batches >= 1
+    finally:
+        lib.sr_snapshot_destroy(h)
+
+
+def _snapshot(lib, sc, nm):
+    h = ctypes.c_void_p()
+    assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot),
+                                  capi.ptr(nm.node_pod_off, capi.P32), capi.ptr(nm.node_pod_idx, capi.P32),
+                                  ctypes.byref(h)) == capi.SR_OK
+    return h
+
+
+def test_consecutive_ticks_one_node_changed(checker):
+    """Tick after tick on fresh snapshots of one cluster, each with one more
+    pod placed on some spot node (its state changes, the static view not):
+    every full plan equals the oracle on the same mutated snapshot."""
+    sc = SynthCluster(3, seed=21, n_on_demand=200, n_spot=450)
+    lib = capi.load_planner()
+    nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+    rng = np.random.default_rng(5)
+    extra = []
+    for tick in range(8):
+        h = _snapshot(lib, sc, nm)
+        osnap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
+        if tick:  # one more pod on one spot node (several ticks accumulate on different nodes)
+            extra.append((int(cand_pods[rng.integers(len(cand_pods))]), int(rng.integers(len(nm.spot)))))
+        for pod, pos in extra[-1:]:
+            assert lib.sr_snapshot_add_pod(h, sc.ptr, pod, pos) == capi.SR_OK
+            osnap.lib.oracle_snapshot_add_pod(osnap.h, sc.ptr, pod, pos)
+        p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+        t = checker.timing()
+        o = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
+        assert np.array_equal(p.status, o["status"]), tick
+        assert np.array_equal(p.node_of_pod, o["node_of_pod"]), tick
+        assert p.winner == o["winner"]
+        if tick >= 2:  # steady state: one node's state re-encoded, no spec is new
+            assert t.enc_static_rebuilt == 0 and t.enc_state_nodes <= 2 and t.enc_new_specs == 0, \
+                (t.enc_static_rebuilt, t.enc_state_nodes, t.enc_new_specs)
+        lib.sr_snapshot_destroy(h)
+
+
+def test_ticks_alternating_clusters_and_interners(checker):
+    """Static-view changes between ticks: two clusters in turn (different
+    spot pools and specs), and the same random scenario encoded through two
+    interners whose ids differ: no cached row, spec or taint set may leak
+    from one into the other."""
+    lib = capi.load_planner()
+    a = SynthCluster(3, seed=31, n_on_demand=120, n_spot=300)
+    b = SynthCluster(2, seed=32, n_on_demand=100, n_spot=250)
+    plans = {}
+    for sc in (a, b, a, b, a):
+        nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+        cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+        h = _snapshot(lib, sc, nm)
+        p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+        lib.sr_snapshot_destroy(h)
+        o = oracle_plan(OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx), sc.ptr, cand_off,
+                        cand_pods, mode=1, threads=8)
+        assert np.array_equal(p.status, o["status"]) and np.array_equal(p.node_of_pod, o["node_of_pod"])
+        plans.setdefault(id(sc), []).append(p.node_of_pod.copy())
+    for runs in plans.values():
+        assert all(np.array_equal(runs[0], r) for r in runs)
+    nodes, spot_pods, cands = rand_scenario(777, n_spot=20, n_cand=10, max_pods=8)
+    flat = [p for c in cands for p in c]
+    first = None
+    for warm in (Interner(), Interner()):
+        for s in ("zone", "team", "type", "dedicated", "x", "a", "b"):  # shifts every later id
+            warm.id("pad-" + s)
+        sc = Scenario(nodes, spot_pods, flat, interner=warm)
+        cand_off = np.cumsum([0] + [len(c) for c in cands]).astype(np.int32)
+        cand_pods = np.arange(sc.q0, sc.q0 + len(flat), dtype=np.int32)
+        h = sc.product_snapshot()
+        p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+        lib.sr_snapshot_destroy(h)
+        o = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=1)
+        assert np.array_equal(p.status, o["status"]) and np.array_equal(p.node_of_pod, o["node_of_pod"])
+        first = p if first is None else first
+        assert np.array_equal(p.node_of_pod, first.node_of_pod)
+
+
+def test_ticks_node_labels_and_taints_change(checker):
+    """The same spot pool with one node's labels, then its taints changed:
+    requirement rows and taint rows are rebuilt for the new static view."""
+    lib = capi.load_planner()
+    nodes, spot_pods, cands = rand_scenario(4242, n_spot=16, n_cand=10, max_pods=8)
+    flat = [p for c in cands for p in c]
+    cand_off = np.cumsum([0] + [len(c) for c in cands]).astype(np.int32)
+    variants = [list(nodes)]
+    import copy
+    n2 = copy.deepcopy(nodes)
+    n2[0].labels = dict(n2[0].labels, zone="b", team="a")
+    variants.append(n2)
+    n3 = copy.deepcopy(n2)
+    n3[1].taints = n3[1].taints + [Taint("dedicated", "a", "NoSchedule")]
+    n3[2].unschedulable = not n3[2].unschedulable
+    variants.append(n3)
+    variants.append(list(nodes))
+    interner = Interner()
+    for ns in variants:
+        sc = Scenario(ns, spot_pods, flat, interner=interner)
+        cand_pods = np.arange(sc.q0, sc.q0 + len(flat), dtype=np.int32)
+        h = sc.product_snapshot()
+        p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+        lib.sr_snapshot_destroy(h)
+        o = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=1)
+        assert np.array_equal(p.status, o["status"]) and np.array_equal(p.node_of_pod, o["node_of_pod"])

@@ -1,6 +1,9 @@
 // Host-only harness: NewNodeMap + snapshot + encode_workload on a synthetic
 // config, printing the workload's dimensions and host-side timings (no GPU).
-//   make -C k8s-spot-rescheduler_amd tools && k8s-spot-rescheduler_amd/build/encode_stats 3
+//   make -C k8s-spot-rescheduler_amd tools && k8s-spot-rescheduler_amd/build/encode_stats 3 [max candidates]
+// Encodes are timed cold (empty encoder cache), warm (the same snapshot
+// again) and after one spot node changed (a fresh snapshot with one more pod
+// on one node), the steady state of a planner between two ticks.
 #include <chrono>
 #include <cstdio>
 #include <algorithm>
@@ -11,6 +14,17 @@
 #include "../k8s-spot-rescheduler_amd/csrc/synth/sr_synth.h"
 
 namespace sr { extern double encode_phase_ms[16]; }
+
+static double ms_since(std::chrono::steady_clock::time_point a) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+}
+
+static void phases(const char* tag) {
+  const double* p = sr::encode_phase_ms;
+  printf("  %-6s phases(ms): views %.3f fallback+ports %.3f specs-hash %.3f specs-new %.3f keys %.3f classes %.3f "
+         "atoms %.3f pods %.3f trows %.3f recs %.3f lists %.3f\n",
+         tag, p[0], p[1], p[14], p[7], p[2], p[3], p[4], p[10], p[12], p[13], p[6]);
+}
 
 int main(int argc, char** argv) {
   sr_synth_params p{};
@@ -29,11 +43,14 @@ int main(int argc, char** argv) {
   sr_node_map_params prm{od, sp, 0};
   auto t0 = std::chrono::steady_clock::now();
   if (sr_new_node_map(&c, &prm, &m) != SR_OK) return 1;
-  auto t1 = std::chrono::steady_clock::now();
+  const double ms_map = ms_since(t0);
   sr_snapshot* snap = nullptr;
+  t0 = std::chrono::steady_clock::now();
   sr_snapshot_create(&c, spot.data(), ns, off.data(), idx.data(), &snap);
-  auto t2 = std::chrono::steady_clock::now();
+  const double ms_snap = ms_since(t0);
   std::vector<int32_t> coff{0}, cp;
+  const int max_cands = argc > 2 ? atoi(argv[2]) : nod;
+  if (max_cands < nod) nod = max_cands;
   for (int i = 0; i < nod; ++i) {
     int node = odn[i];
     for (int j = off[node]; j < off[node + 1]; ++j)
@@ -42,26 +59,43 @@ int main(int argc, char** argv) {
   }
   sr_candidates cands{nod, coff.data(), cp.data(), nullptr};
   sr::Workload w;
+  sr::EncoderCache cache;
   std::string err;
-  auto t3 = std::chrono::steady_clock::now();
-  int reps = 20;
-  double best = 1e30;
-  for (int r = 0; r < reps; ++r) {
-    auto a = std::chrono::steady_clock::now();
-    sr::encode_workload(snap, &c, &cands, &w, &err);
-    best = std::min(best, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count());
-  }
-  auto t4 = std::chrono::steady_clock::now();
-  auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   printf("config %d: nodes %d pods %d spot %d od %d cand_pods %zu\n", p.config, nn, np, ns, nod, cp.size());
-  printf("new_node_map %.2f ms, snapshot %.2f ms, encode %.2f ms (best %.2f)\n", ms(t0, t1), ms(t1, t2), ms(t3, t4) / reps, best);
-  printf("phases(ms): dims %.2f fallback+ports+taints %.2f pod-static %.2f classes %.2f nodes+atoms %.2f t-rows+pods %.2f lists %.2f (pod-static: keys %.2f; t-setup %.2f)\n",
-         sr::encode_phase_ms[0], sr::encode_phase_ms[1], sr::encode_phase_ms[2], sr::encode_phase_ms[3],
-         sr::encode_phase_ms[4], sr::encode_phase_ms[5], sr::encode_phase_ms[6], sr::encode_phase_ms[7], sr::encode_phase_ms[8]);
-  printf("fine(ms): pass1 %.2f ports+taints %.2f | atoms-nodes %.2f atoms-reqs %.2f | lb+recs %.2f empty %.2f trows %.2f ranks %.2f recoffs %.2f\n",
-         sr::encode_phase_ms[8], sr::encode_phase_ms[1], sr::encode_phase_ms[9], sr::encode_phase_ms[4],
-         sr::encode_phase_ms[10], sr::encode_phase_ms[11], sr::encode_phase_ms[12], sr::encode_phase_ms[13], sr::encode_phase_ms[5]);
-  printf("keys split: gather+hash %.3f shards %.3f merge %.3f\n", sr::encode_phase_ms[14], sr::encode_phase_ms[15], sr::encode_phase_ms[7]);
+  printf("new_node_map %.2f ms, snapshot %.2f ms\n", ms_map, ms_snap);
+  t0 = std::chrono::steady_clock::now();
+  if (sr::encode_workload(&cache, snap, &c, &cands, &w, &err) != SR_OK) {
+    printf("encode failed: %s\n", err.c_str());
+    return 1;
+  }
+  printf("cold encode %.3f ms (new specs %d)\n", ms_since(t0), cache.last_new_specs);
+  phases("cold");
+  double best = 1e30;
+  for (int r = 0; r < 20; ++r) {
+    t0 = std::chrono::steady_clock::now();
+    sr::encode_workload(&cache, snap, &c, &cands, &w, &err);
+    best = std::min(best, ms_since(t0));
+  }
+  printf("warm encode (same snapshot) best %.3f ms\n", best);
+  phases("warm");
+  // one spot node changed: a fresh snapshot (as every tick builds) with one
+  // more pod on spot position 7
+  best = 1e30;
+  int last_state = 0, last_static = 0;
+  for (int r = 0; r < 10; ++r) {
+    sr_snapshot* s2 = nullptr;
+    sr_snapshot_create(&c, spot.data(), ns, off.data(), idx.data(), &s2);
+    if (r & 1) sr_snapshot_add_pod(s2, &c, cp.empty() ? 0 : cp[0], std::min(7, ns - 1));
+    t0 = std::chrono::steady_clock::now();
+    sr::encode_workload(&cache, s2, &c, &cands, &w, &err);
+    best = std::min(best, ms_since(t0));
+    last_state = cache.last_state_changed;
+    last_static = cache.last_static_changed;
+    sr_snapshot_destroy(s2);
+  }
+  printf("one-node-changed encode (fresh snapshot) best %.3f ms (state nodes %d, static rebuilt %d)\n", best,
+         last_state, last_static);
+  phases("1node");
   printf("Wp %d atoms %d classes %d program ops %zu t_rows %zu\n", w.Wp, w.n_atoms, w.n_classes, w.cls_prog.size(),
          w.t_dim.size());
   int tc[4] = {0, 0, 0, 0};
