@@ -82,8 +82,8 @@ typedef int32_t sr_status;
 #define SR_POD_FB_SCALAR_RESOURCES  (1u << 8)  /* extended / hugepages / attachable-volume requests */
 #define SR_POD_FB_VOLUMES           (1u << 9)  /* PVCs or volumes inspected by volume filters */
 #define SR_POD_FB_TOPOLOGY_SPREAD   (1u << 10) /* DoNotSchedule topology spread constraints */
-#define SR_POD_FB_POD_AFFINITY      (1u << 11) /* required pod affinity (and anti-affinity when the shim does not
-                                                  pass sr_cluster.pod_affinity) */
+#define SR_POD_FB_POD_AFFINITY      (1u << 11) /* required pod (anti-)affinity the shim does not pass in
+                                                  sr_cluster.pod_affinity */
 #define SR_POD_FB_OTHER             (1u << 12) /* anything else the shim cannot encode */
 #define SR_POD_FB_MASK              (0xff00u)
 
@@ -145,10 +145,11 @@ typedef struct {
   const int32_t *port_off, *port_proto, *port_num, *port_ip /* -1 = "" or "0.0.0.0" */;
 } sr_pods;
 
-/* Required inter-pod anti-affinity: the InterPodAffinity filter of k8s
+/* Required inter-pod (anti-)affinity: the InterPodAffinity filter of k8s
  * v1.19.2 [upstream plugins/interpodaffinity] for
- * Spec.Affinity.PodAntiAffinity.RequiredDuringSchedulingIgnoredDuringExecution,
- * and the pod namespaces and labels its terms select on.  CSR arrays over
+ * Spec.Affinity.PodAntiAffinity.RequiredDuringSchedulingIgnoredDuringExecution
+ * and Spec.Affinity.PodAffinity.RequiredDuringSchedulingIgnoredDuringExecution,
+ * and the pod namespaces and labels their terms select on.  CSR arrays over
  * sr_pods; terms are numbered across all pods.  A term's Namespaces list is
  * empty when the API object's is (the term then selects in its own pod's
  * namespace).  Selector operators: SR_OP_IN / NOT_IN / EXISTS / DOES_NOT_EXIST;
@@ -165,6 +166,11 @@ typedef struct {
   const int32_t *ml_off, *ml_key, *ml_val;          /* [terms+1] MatchLabels */
   const int32_t *me_off, *me_key, *me_op;           /* [terms+1] MatchExpressions */
   const int32_t *me_val_off, *me_vals;              /* [exprs+1] their values */
+  /* Spec.Affinity.PodAffinity.RequiredDuringSchedulingIgnoredDuringExecution:
+   * [pods.n+1] pods -> required pod AFFINITY terms, in the same term tables
+   * (numbered after every anti-affinity term).  NULL: none given.  A pod whose
+   * affinity the shim cannot pass carries SR_POD_FB_POD_AFFINITY instead. */
+  const int32_t *aff_off;
 } sr_pod_affinity;
 
 typedef struct {

@@ -406,4 +406,153 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
   for (int32_t j = 0; j < n_flat; ++j) at.pod_ids.insert(at.pod_ids.end(), ids[j].begin(), ids[j].end());
 }
 
+// Required pod affinity (InterPodAffinity.Filter, satisfyPodAffinity [upstream
+// k8s v1.19.2 plugins/interpodaffinity/filtering.go]).  A pod's terms form a
+// set S (canonical words of its resolved terms); M(S) = the snapshot pods that
+// match every term of S (updateWithAffinityTerms counts only those).  Per set:
+// KEYS(S) = nodes carrying every term's topology key; SAT(S) = KEYS(S) and,
+// per term, a pod of M(S) in the node's domain of the term's key; map_empty =
+// no pod of M(S) runs on a node carrying any of the keys.  A pod passes a node
+// of SAT(S) -- or, with map_empty and the pod matching its own terms (the
+// first pod of a self-affine group), a node of KEYS(S).  A candidate in which
+// an earlier pod matches every term of a later pod's set changes that pod's
+// domains while it is planned: it takes the reference path.
+void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
+                      std::vector<int32_t>& status, AffTerms* out) {
+  AffTerms& af = *out;
+  af = AffTerms{};
+  const sr_pod_affinity* PA = c->pod_affinity;
+  const int32_t nc = cands->n_cand;
+  const int32_t base = nc > 0 ? cands->cand_pod_off[0] : 0;
+  const int32_t n_flat = nc > 0 ? cands->cand_pod_off[nc] - base : 0;
+  af.base = base;
+  af.pod_code.assign(static_cast<size_t>(n_flat), -1);
+  if (!PA || !PA->aff_off) return;
+  const sr_pod_affinity& A = *PA;
+  const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
+
+  // ---- distinct sets of the pending candidates' pods
+  WordDict set_dict;
+  std::vector<std::vector<Term>> sets;
+  std::vector<std::vector<int32_t>> tws;
+  std::vector<int32_t> words, setw;
+  for (int32_t i = 0; i < nc; ++i) {
+    if (status[i] != STATUS_PENDING) continue;
+    bool any = false;
+    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+      const int32_t pod = cands->cand_pods[j];
+      if (A.aff_off[pod] == A.aff_off[pod + 1]) continue;
+      any = true;
+      tws.clear();
+      for (int32_t t = A.aff_off[pod]; t < A.aff_off[pod + 1]; ++t) {
+        anti_term_words(c, pod, t, words);
+        tws.push_back(words);
+      }
+      std::sort(tws.begin(), tws.end());
+      tws.erase(std::unique(tws.begin(), tws.end()), tws.end());
+      setw.assign(1, static_cast<int32_t>(tws.size()));
+      for (const auto& tw : tws) {
+        setw.push_back(static_cast<int32_t>(tw.size()));
+        setw.insert(setw.end(), tw.begin(), tw.end());
+      }
+      bool ins = false;
+      const int32_t sid = set_dict.intern(setw, &ins);
+      if (ins) {
+        sets.emplace_back();
+        for (const auto& tw : tws) sets.back().push_back(parse_term(tw.data()));
+      }
+      bool self = true;  // podMatchesAllAffinityTerms(pod, its own terms)
+      for (const Term& t : sets[sid]) self = self && term_selects(t, meta_of(A, pod));
+      af.pod_code[j - base] = 2 * sid + (self ? 1 : 0);
+    }
+    // snapshot pods whose labels are unknown may match its terms
+    if (any && snap->unknown_total > 0) status[i] = SR_CAND_FALLBACK;
+  }
+  const int32_t S = static_cast<int32_t>(sets.size());
+  if (S == 0) return;
+  af.active = true;
+  af.n_sets = S;
+
+  // ---- topology key values of the spot nodes (few distinct keys)
+  std::vector<int32_t> key_ids;
+  std::vector<std::vector<int32_t>> key_val;  // [key][node], INT_MIN: absent
+  auto key_slot = [&](int32_t key) {
+    for (size_t k = 0; k < key_ids.size(); ++k)
+      if (key_ids[k] == key) return static_cast<int32_t>(k);
+    key_ids.push_back(key);
+    key_val.emplace_back(static_cast<size_t>(n_spot), INT_MIN);
+    std::vector<int32_t>& v = key_val.back();
+    for (int32_t n = 0; n < n_spot; ++n)
+      for (const auto& kv : snap->nodes[n].labels)
+        if (kv.first == key) {
+          v[n] = kv.second;
+          break;
+        }
+    return static_cast<int32_t>(key_ids.size() - 1);
+  };
+  std::vector<std::vector<int32_t>> set_keys(static_cast<size_t>(S));
+  for (int32_t s = 0; s < S; ++s)
+    for (const Term& t : sets[s]) set_keys[s].push_back(key_slot(t.tk));
+
+  // ---- M(S) over the snapshot pods: per set and term, the key values of
+  // the nodes hosting a matching pod; map_empty
+  std::vector<std::vector<std::vector<int32_t>>> vals(static_cast<size_t>(S));
+  for (int32_t s = 0; s < S; ++s) vals[s].resize(sets[s].size());
+  af.map_empty.assign(static_cast<size_t>(S), 1);
+  for (int32_t n = 0; n < n_spot; ++n)
+    for (int32_t e : snap->state[n].pods) {
+      const SnapPod& sp = snap->pods[e];
+      if (!sp.meta) continue;  // candidates with terms already fell back
+      const PodMeta m = meta_of(sp);
+      for (int32_t s = 0; s < S; ++s) {
+        bool all = true;
+        for (const Term& t : sets[s]) all = all && term_selects(t, m);
+        if (!all) continue;
+        for (size_t t = 0; t < sets[s].size(); ++t) {
+          const int32_t v = key_val[set_keys[s][t]][n];
+          if (v == INT_MIN) continue;
+          vals[s][t].push_back(v);
+          af.map_empty[s] = 0;
+        }
+      }
+    }
+  af.sat.assign(static_cast<size_t>(S) * Wp, 0);
+  af.keys.assign(static_cast<size_t>(S) * Wp, 0);
+  for (int32_t s = 0; s < S; ++s) {
+    for (auto& v : vals[s]) {
+      std::sort(v.begin(), v.end());
+      v.erase(std::unique(v.begin(), v.end()), v.end());
+    }
+    for (int32_t n = 0; n < n_spot; ++n) {
+      bool keys = true, sat = true;
+      for (size_t t = 0; t < sets[s].size(); ++t) {
+        const int32_t v = key_val[set_keys[s][t]][n];
+        keys = keys && v != INT_MIN;
+        sat = sat && v != INT_MIN && std::binary_search(vals[s][t].begin(), vals[s][t].end(), v);
+      }
+      if (keys) af.keys[static_cast<size_t>(s) * Wp + (n >> 6)] |= 1ull << (n & 63);
+      if (sat) af.sat[static_cast<size_t>(s) * Wp + (n >> 6)] |= 1ull << (n & 63);
+    }
+  }
+
+  // ---- interactions inside a candidate: an earlier pod matching every term
+  // of a later pod's set
+  for (int32_t i = 0; i < nc; ++i) {
+    if (status[i] != STATUS_PENDING) continue;
+    const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
+    bool fb = false;
+    for (int32_t k = b + 1; k < e && !fb; ++k) {
+      const int32_t code = af.pod_code[k - base];
+      if (code < 0) continue;
+      for (int32_t q = b; q < k && !fb; ++q) {
+        const PodMeta m = meta_of(A, cands->cand_pods[q]);
+        bool all = true;
+        for (const Term& t : sets[code >> 1]) all = all && term_selects(t, m);
+        fb = all;
+      }
+    }
+    if (fb) status[i] = SR_CAND_FALLBACK;
+  }
+}
+
 }  // namespace sr

@@ -515,7 +515,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t)
         for (int32_t e = P.term_expr_off[t]; e < P.term_expr_off[t + 1]; ++e)
           if (P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT) return true;
-    return anti_opaque(c, pod);  // required anti-affinity the encoded set cannot read
+    return anti_opaque(c, pod) || aff_opaque(c, pod);  // required (anti-)affinity the encoded set cannot read
   };
   for (int32_t i = 0; i < nc; ++i) {
     if (cands->cand_pod_off[i + 1] < cands->cand_pod_off[i]) {
@@ -549,6 +549,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   AntiTerms anti;
   analyse_anti(snap, c, cands, Wp, w->status_host, &anti);
   const int32_t bit_shift = 2 * anti.n_pairs;  // host-port bits sit above the pairs
+  // ---- required pod affinity: term sets, their node rows, and the
+  // candidates whose pods interact through them (antiaff.cpp)
+  AffTerms aff;
+  analyse_affinity(snap, c, cands, Wp, w->status_host, &aff);
 
   // ---- host ports: HostPortInfo.CheckConflict [upstream k8s v1.19
   // framework/types.go] as state bits.  A (protocol, port) group whose active
@@ -783,29 +787,34 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   }
   phase(7);
 
-  // ---- class keys: the static spec, plus (with anti-affinity) the pod's
-  // term ids of this call.  Pods without ids use their spec id as key.
+  // ---- class keys: the static spec, plus (with inter-pod affinity) the pod's
+  // anti-affinity term ids and affinity set of this call.  Pods without either
+  // use their spec id as key.
   const int32_t n_spec_ids = static_cast<int32_t>(C.spec.size());
   std::vector<int32_t> pod_key(static_cast<size_t>(na));
-  std::vector<int32_t> key_spec;               // keys >= n_spec_ids: spec of the combined key
-  std::vector<std::vector<int32_t>> key_anti;  // ... and its term ids
+  std::vector<int32_t> key_spec;               // keys >= n_spec_ids: spec of the combined key,
+  std::vector<std::vector<int32_t>> key_anti;  // ... its anti-affinity term ids
+  std::vector<int32_t> key_aff;                // ... and its affinity code (AffTerms::pod_code)
   {
     WordDict combo;
     std::vector<int32_t> kw;
     for (int32_t q = 0; q < na; ++q) {
       const int32_t j = active_src[q] - anti.base;
       const int32_t n_ids = anti.active ? anti.pod_off[j + 1] - anti.pod_off[j] : 0;
-      if (n_ids == 0) {
+      const int32_t code = aff.active ? aff.pod_code[active_src[q] - aff.base] : -1;
+      if (n_ids == 0 && code < 0) {
         pod_key[q] = pod_spec[q];
         continue;
       }
       kw.assign(1, pod_spec[q]);
-      kw.insert(kw.end(), anti.pod_ids.begin() + anti.pod_off[j], anti.pod_ids.begin() + anti.pod_off[j + 1]);
+      kw.push_back(code);
+      if (n_ids) kw.insert(kw.end(), anti.pod_ids.begin() + anti.pod_off[j], anti.pod_ids.begin() + anti.pod_off[j + 1]);
       bool ins = false;
       const int32_t id = combo.intern(kw, &ins);
       if (ins) {
         key_spec.push_back(pod_spec[q]);
-        key_anti.emplace_back(kw.begin() + 1, kw.end());
+        key_aff.push_back(code);
+        key_anti.emplace_back(kw.begin() + 2, kw.end());
       }
       pod_key[q] = n_spec_ids + id;
     }
@@ -855,7 +864,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   const int32_t n_ports = static_cast<int32_t>(port_query.size());
   const int32_t A_REQ = 1, A_TAINT = 1 + n_reqs, A_PORT = A_TAINT + n_taints;
   const int32_t A_ANTI = A_PORT + n_ports;  // DA(t) at A_ANTI + 2t, DB(t) at A_ANTI + 2t + 1
-  const int32_t A_COMP = A_ANTI + 2 * anti.n_terms;
+  const int32_t A_AFF = A_ANTI + 2 * anti.n_terms;  // SAT(S) at A_AFF + 2s, KEYS(S) at A_AFF + 2s + 1
+  const int32_t A_COMP = A_AFF + 2 * aff.n_sets;
   // Composite atoms, one per distinct untolerated-taint set U of the pods:
   // atom 0 AND NOT (OR of U's taint atoms) -- the pod-count check and
   // TaintToleration / NodeUnschedulable in one row, so a class program opens
@@ -889,6 +899,13 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     key_ports[ki] = ports;
     da.clear();
     db.clear();
+    // pod affinity: SAT(S); with an empty pair map KEYS(S) for a pod matching
+    // its own terms, nothing otherwise (-2)
+    int32_t aff_atom = -1;
+    if (k >= n_spec_ids && key_aff[k - n_spec_ids] >= 0) {
+      const int32_t code = key_aff[k - n_spec_ids], set = code >> 1;
+      aff_atom = !aff.map_empty[set] ? A_AFF + 2 * set : (code & 1) ? A_AFF + 2 * set + 1 : -2;
+    }
     if (k >= n_spec_ids)
       for (int32_t id : key_anti[k - n_spec_ids]) {
         const int32_t t = id >> 1;
@@ -911,6 +928,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     sig.insert(sig.end(), da.begin(), da.end());
     sig.push_back(static_cast<int32_t>(db.size()));
     sig.insert(sig.end(), db.begin(), db.end());
+    sig.push_back(aff_atom);
     bool ins = false;
     key_class[ki] = class_dict.intern(sig, &ins);
     if (!ins) continue;
@@ -923,7 +941,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       if ((ports >> b & 1) && bit_query[b] >= 0) emit(A_PORT + bit_query[b], PROG_ANDNOT);
     for (int32_t t : da) emit(A_ANTI + 2 * t, PROG_ANDNOT);  // anti-affinity base conflicts
     for (int32_t t : db) emit(A_ANTI + 2 * t + 1, PROG_ANDNOT);
-    if (sp.flags & CLS_IMPOSSIBLE) {
+    if (aff_atom >= 0) emit(aff_atom, PROG_AND);
+    if ((sp.flags & CLS_IMPOSSIBLE) || aff_atom == -2) {
       emit(0, PROG_ANDNOT);
     } else {
       for (size_t i = 0; i < sp.terms.size(); i += 1 + static_cast<size_t>(sp.terms[i]))
@@ -979,6 +998,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   for (int32_t t = 0; t < anti.n_terms; ++t) {
     std::copy_n(&anti.da[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t) * Wp);
     std::copy_n(&anti.db[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t + 1) * Wp);
+  }
+  for (int32_t t = 0; t < aff.n_sets; ++t) {
+    std::copy_n(&aff.sat[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_AFF + 2 * t) * Wp);
+    std::copy_n(&aff.keys[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_AFF + 2 * t + 1) * Wp);
   }
   for (size_t k = 0; k < comp_sets.size(); ++k) {  // atom 0 AND NOT (any taint of the set)
     uint64_t* row = A + static_cast<size_t>(A_COMP + static_cast<int32_t>(k)) * Wp;

@@ -104,6 +104,8 @@ inline bool has_anti_terms(const sr_cluster* c, int32_t pod) {
 // Its required anti-affinity is outside the encoded set: no sr_pod_affinity,
 // the flag without terms, or a selector LabelSelectorAsSelector rejects.
 bool anti_opaque(const sr_cluster* c, int32_t pod);
+// Its required pod affinity has a selector LabelSelectorAsSelector rejects.
+bool aff_opaque(const sr_cluster* c, int32_t pod);
 // The words of the pod's anti-affinity term t (antiaff.cpp): topology key,
 // namespaces (defaulted to the owner's), selector; equal words = equal terms.
 void anti_term_words(const sr_cluster* c, int32_t owner, int32_t t, std::vector<int32_t>& out);
@@ -276,6 +278,21 @@ struct AntiTerms {
 // (status -> SR_CAND_FALLBACK) or need state bits.
 void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
                   std::vector<int32_t>& status, AntiTerms* out);
+
+// Required pod affinity of one encode (antiaff.cpp).
+struct AffTerms {
+  bool active = false;
+  int32_t base = 0;                 // per-pod arrays: flat index - base
+  int32_t n_sets = 0;               // distinct term sets of the pending pods
+  std::vector<uint64_t> sat, keys;  // [set][Wp] SAT(S) (keys and a matching pod in every term's domain), KEYS(S)
+  std::vector<uint8_t> map_empty;   // [set] no matching pod on a node carrying any of the keys
+  std::vector<int32_t> pod_code;    // [flat - base] -1 none, else 2 * set + (the pod matches its own terms)
+};
+
+// The sets, their node rows, and the candidates whose pods interact through
+// them (status -> SR_CAND_FALLBACK).
+void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
+                      std::vector<int32_t>& status, AffTerms* out);
 
 // Builds the workload; returns SR_OK or an error with *err filled.  `cache`
 // carries what the previous calls derived (and is updated).

@@ -146,27 +146,43 @@ static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod, const
     if (P.port_num[i] > 0) st.ports.push_back(Port{P.port_ip[i], P.port_proto[i], P.port_num[i]});
 }
 
+// A term whose label selector metav1.LabelSelectorAsSelector rejects: an
+// empty key, In / NotIn without values, Exists / DoesNotExist with values,
+// any other operator [upstream apimachinery].
+static bool term_invalid(const sr_cluster* c, int32_t t) {
+  const sr_pod_affinity* A = c->pod_affinity;
+  const int32_t e_id = c->id_empty;
+  if (A->selector_nil[t]) return false;
+  for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; ++i)
+    if (A->ml_key[i] == e_id && e_id != -1) return true;
+  for (int32_t e = A->me_off[t]; e < A->me_off[t + 1]; ++e) {
+    const int32_t nv = A->me_val_off[e + 1] - A->me_val_off[e], op = A->me_op[e];
+    if (A->me_key[e] == e_id && e_id != -1) return true;
+    if (op == SR_OP_IN || op == SR_OP_NOT_IN) {
+      if (nv == 0) return true;
+    } else if (op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) {
+      if (nv != 0) return true;
+    } else {
+      return true;
+    }
+  }
+  return false;
+}
+
 bool anti_opaque(const sr_cluster* c, int32_t pod) {
   if (!has_anti_terms(c, pod)) return false;
   const sr_pod_affinity* A = c->pod_affinity;
   if (!A || A->anti_off[pod] == A->anti_off[pod + 1]) return true;
-  const int32_t e_id = c->id_empty;
-  for (int32_t t = A->anti_off[pod]; t < A->anti_off[pod + 1]; ++t) {
-    if (A->selector_nil[t]) continue;
-    for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; ++i)
-      if (A->ml_key[i] == e_id && e_id != -1) return true;
-    for (int32_t e = A->me_off[t]; e < A->me_off[t + 1]; ++e) {
-      const int32_t nv = A->me_val_off[e + 1] - A->me_val_off[e], op = A->me_op[e];
-      if (A->me_key[e] == e_id && e_id != -1) return true;
-      if (op == SR_OP_IN || op == SR_OP_NOT_IN) {
-        if (nv == 0) return true;
-      } else if (op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) {
-        if (nv != 0) return true;
-      } else {
-        return true;
-      }
-    }
-  }
+  for (int32_t t = A->anti_off[pod]; t < A->anti_off[pod + 1]; ++t)
+    if (term_invalid(c, t)) return true;
+  return false;
+}
+
+bool aff_opaque(const sr_cluster* c, int32_t pod) {
+  const sr_pod_affinity* A = c->pod_affinity;
+  if (!A || !A->aff_off) return false;
+  for (int32_t t = A->aff_off[pod]; t < A->aff_off[pod + 1]; ++t)
+    if (term_invalid(c, t)) return true;
   return false;
 }
 

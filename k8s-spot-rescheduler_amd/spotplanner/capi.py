@@ -65,7 +65,7 @@ class sr_pod_affinity(ctypes.Structure):
     _fields_ = [("ns", P32), ("label_off", P32), ("label_key", P32), ("label_val", P32), ("anti_off", P32),
                 ("topology_key", P32), ("ns_off", P32), ("ns_ids", P32), ("selector_nil", PU8),
                 ("ml_off", P32), ("ml_key", P32), ("ml_val", P32), ("me_off", P32), ("me_key", P32),
-                ("me_op", P32), ("me_val_off", P32), ("me_vals", P32)]
+                ("me_op", P32), ("me_val_off", P32), ("me_vals", P32), ("aff_off", P32)]
 
 
 class sr_cluster(ctypes.Structure):
@@ -165,7 +165,7 @@ def make_cluster_struct(A) -> sr_cluster:
     if A.get("pa_ns") is not None:
         pa = sr_pod_affinity()
         for f in ("ns", "label_off", "label_key", "label_val", "anti_off", "topology_key", "ns_off", "ns_ids",
-                  "ml_off", "ml_key", "ml_val", "me_off", "me_key", "me_op", "me_val_off", "me_vals"):
+                  "ml_off", "ml_key", "ml_val", "me_off", "me_key", "me_op", "me_val_off", "me_vals", "aff_off"):
             setattr(pa, f, ptr(A["pa_" + f], P32))
         pa.selector_nil = ptr(A["pa_selector_nil"], PU8)
         c._pod_affinity = pa  # keeps the struct alive as long as the cluster struct

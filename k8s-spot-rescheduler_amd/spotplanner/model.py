@@ -126,6 +126,8 @@ class Pod:
     required_pod_anti_affinity: bool = False  # opaque anti-affinity (no terms given): fallback
     # Affinity.PodAntiAffinity.RequiredDuringSchedulingIgnoredDuringExecution (encoded)
     pod_anti_affinity: Optional[List[PodAffinityTerm]] = None
+    # Affinity.PodAffinity.RequiredDuringSchedulingIgnoredDuringExecution (encoded)
+    pod_affinity: Optional[List[PodAffinityTerm]] = None
     hard_topology_spread: bool = False
     # drain attributes (cluster-autoscaler utils/drain)
     phase: str = "Running"                    # Status.Phase
@@ -256,9 +258,29 @@ class EncodedCluster:
 
 
 def _encode_pod_affinity(pods: List[Pod], it: Interner) -> dict:
-    """sr_pod_affinity arrays: namespaces, labels and required anti-affinity terms."""
+    """sr_pod_affinity arrays: namespaces, labels, required anti-affinity terms,
+    then required affinity terms (one term table, anti-affinity terms first)."""
     ns, lo, lk, lv, ao = [], [0], [], [], [0]
     tk, nso, nsi, nil, mlo, mlk, mlv, meo, mek, mep, mevo, mev = [], [0], [], [], [0], [], [], [0], [], [], [0], []
+
+    def add_term(t):
+        tk.append(it.id(t.topology_key))
+        nsi.extend(it.id(x) for x in t.namespaces)
+        nso.append(len(nsi))
+        sel = t.label_selector
+        nil.append(1 if sel is None else 0)
+        for k, v in (sel.match_labels.items() if sel else []):
+            mlk.append(it.id(k))
+            mlv.append(it.id(v))
+        mlo.append(len(mlk))
+        for r in (sel.match_expressions if sel else []):
+            mek.append(it.id(r.key))
+            mep.append(SEL_OPS.get(r.operator, capi.SR_OP_OTHER) if r.operator not in ("Gt", "Lt")
+                       else capi.SR_OP_OTHER)
+            mev.extend(it.id(v) for v in r.values)
+            mevo.append(len(mev))
+        meo.append(len(mek))
+
     for p in pods:
         ns.append(it.id(p.namespace))
         for k, v in p.labels.items():
@@ -266,28 +288,18 @@ def _encode_pod_affinity(pods: List[Pod], it: Interner) -> dict:
             lv.append(it.id(v))
         lo.append(len(lk))
         for t in (p.pod_anti_affinity or []):
-            tk.append(it.id(t.topology_key))
-            nsi.extend(it.id(x) for x in t.namespaces)
-            nso.append(len(nsi))
-            sel = t.label_selector
-            nil.append(1 if sel is None else 0)
-            for k, v in (sel.match_labels.items() if sel else []):
-                mlk.append(it.id(k))
-                mlv.append(it.id(v))
-            mlo.append(len(mlk))
-            for r in (sel.match_expressions if sel else []):
-                mek.append(it.id(r.key))
-                mep.append(SEL_OPS.get(r.operator, capi.SR_OP_OTHER) if r.operator not in ("Gt", "Lt")
-                           else capi.SR_OP_OTHER)
-                mev.extend(it.id(v) for v in r.values)
-                mevo.append(len(mev))
-            meo.append(len(mek))
+            add_term(t)
         ao.append(len(tk))
+    fo = [len(tk)]  # affinity terms are numbered after every anti-affinity term
+    for p in pods:
+        for t in (p.pod_affinity or []):
+            add_term(t)
+        fo.append(len(tk))
     return dict(pa_ns=_i32(ns), pa_label_off=_i32(lo), pa_label_key=_i32(lk), pa_label_val=_i32(lv),
                 pa_anti_off=_i32(ao), pa_topology_key=_i32(tk), pa_ns_off=_i32(nso), pa_ns_ids=_i32(nsi),
                 pa_selector_nil=_u8(nil), pa_ml_off=_i32(mlo), pa_ml_key=_i32(mlk), pa_ml_val=_i32(mlv),
                 pa_me_off=_i32(meo), pa_me_key=_i32(mek), pa_me_op=_i32(mep), pa_me_val_off=_i32(mevo),
-                pa_me_vals=_i32(mev))
+                pa_me_vals=_i32(mev), pa_aff_off=_i32(fo))
 
 
 def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Interner] = None,

@@ -442,6 +442,31 @@ static int o_anti_opaque(const sr_cluster *c, int32_t pod) {
   return 0;
 }
 
+/* A term whose label selector fails LabelSelectorAsSelector (same rules as above). */
+static int o_term_invalid(const sr_cluster *c, int32_t t) {
+  const sr_pod_affinity *A = c->pod_affinity;
+  if (A->selector_nil[t]) return 0;
+  for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; i++)
+    if (A->ml_key[i] == c->id_empty && c->id_empty != -1) return 1;
+  for (int32_t e = A->me_off[t]; e < A->me_off[t + 1]; e++) {
+    int32_t nv = A->me_val_off[e + 1] - A->me_val_off[e], op = A->me_op[e];
+    if (A->me_key[e] == c->id_empty && c->id_empty != -1) return 1;
+    if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) return 1;
+    if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) return 1;
+    if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST) return 1;
+  }
+  return 0;
+}
+
+/* Required pod affinity the planner cannot evaluate: a selector that fails to build. */
+static int o_aff_opaque(const sr_cluster *c, int32_t pod) {
+  const sr_pod_affinity *A = c->pod_affinity;
+  if (!A || !A->aff_off) return 0;
+  for (int32_t t = A->aff_off[pod]; t < A->aff_off[pod + 1]; t++)
+    if (o_term_invalid(c, t)) return 1;
+  return 0;
+}
+
 static int64_t o_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 
 static void o_state_add_pod(o_state *st, const sr_cluster *c, int32_t pod) {
@@ -810,12 +835,64 @@ static int o_interpod_ok(const o_state *st, const int32_t *node, int32_t n, cons
   return 1;
 }
 
+/* InterPodAffinity.Filter, required affinity part [upstream k8s v1.19.2
+ * plugins/interpodaffinity filtering.go satisfyPodAffinity]: PreFilter counts
+ * topology pairs (key, value of the existing pod's node) over every term of
+ * the incoming pod, for each existing pod that matches ALL of its terms
+ * (updateWithAffinityTerms / podMatchesAllAffinityTerms).  A node passes when
+ * it carries every term's topology key and each term's pair has a count; or,
+ * when no pair was counted at all and the pod matches its own terms (the
+ * first pod of a group with affinity to itself), when it carries every key. */
+static int o_pod_affinity_ok(const o_state *st, const int32_t *node, int32_t n, const sr_cluster *c, int32_t pod,
+                             int32_t nnode) {
+  const sr_pod_affinity *A = c->pod_affinity;
+  if (!A || !A->aff_off || A->aff_off[pod] == A->aff_off[pod + 1]) return 1;
+  int32_t t0 = A->aff_off[pod], t1 = A->aff_off[pod + 1];
+  int32_t vn[64];
+  if (t1 - t0 > 64) return 0; /* never reached: the shim's terms per pod are few */
+  for (int32_t t = t0; t < t1; t++)
+    if (!o_node_label(c, nnode, A->topology_key[t], &vn[t - t0])) return 0; /* all topology labels must exist */
+  int map_empty = 1, all_sat = 1;
+  for (int32_t t = t0; t < t1 && all_sat; t++) {
+    int sat = 0;
+    for (int32_t m = 0; m < n && !sat; m++) {
+      int32_t vm;
+      if (!o_node_label(c, node[m], A->topology_key[t], &vm) || vm != vn[t - t0]) continue;
+      for (int32_t j = 0; j < st[m].nlist && !sat; j++) {
+        int32_t e = st[m].list[j], all = 1;
+        for (int32_t u = t0; u < t1 && all; u++) all = o_term_matches(c, pod, u, e);
+        sat = all;
+      }
+    }
+    all_sat = sat;
+  }
+  if (all_sat) return 1;
+  /* podsExist is false: the self-affinity exception needs an empty pair map */
+  for (int32_t m = 0; m < n && map_empty; m++) {
+    int has_key = 0;
+    for (int32_t t = t0; t < t1 && !has_key; t++) {
+      int32_t v;
+      has_key = o_node_label(c, node[m], A->topology_key[t], &v);
+    }
+    if (!has_key) continue;
+    for (int32_t j = 0; j < st[m].nlist && map_empty; j++) {
+      int32_t e = st[m].list[j], all = 1;
+      for (int32_t u = t0; u < t1 && all; u++) all = o_term_matches(c, pod, u, e);
+      if (all) map_empty = 0;
+    }
+  }
+  if (!map_empty) return 0;
+  for (int32_t u = t0; u < t1; u++)
+    if (!o_term_matches(c, pod, u, pod)) return 0;
+  return 1;
+}
+
 int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c, int32_t pod) {
   const sr_pods *P = &c->pods;
   if (P->flags[pod] & SR_POD_FB_MASK) return 1;
   /* an existing pod's required anti-affinity may select the incoming pod:
    * opaque terms (o_anti_opaque) keep every pod on the fallback path */
-  if (s->opaque_total > 0 || o_anti_opaque(c, pod)) return 1;
+  if (s->opaque_total > 0 || o_anti_opaque(c, pod) || o_aff_opaque(c, pod)) return 1;
   if (P->aff_required[pod])
     for (int32_t t = P->term_off[pod]; t < P->term_off[pod + 1]; t++)
       for (int32_t e = P->term_expr_off[t]; e < P->term_expr_off[t + 1]; e++)
@@ -835,6 +912,7 @@ static int o_check(const o_state *st, const int32_t *node, int32_t n, const sr_c
   if (!o_affinity_ok(c, pod, nd)) return 0;
   if (!o_taints_ok(c, pod, nd)) return 0;
   if (!o_interpod_ok(st, node, n, c, pod, nd)) return 0;
+  if (!o_pod_affinity_ok(st, node, n, c, pod, nd)) return 0;
   return 1;
 }
 

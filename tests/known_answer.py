@@ -11,6 +11,8 @@ the pinned upstream modules, which are not in the reference tree:
                                     PodMatchesNodeSelectorAndAffinityTerms
       nodeports/node_ports.go       fitsPorts -> framework/types.go
                                     HostPortInfo.CheckConflict
+      interpodaffinity/filtering.go satisfyPodAffinity, satisfyPodAntiAffinity,
+                                    satisfyExistingPodsAntiAffinity
   k8s.io/api v0.19.2 core/v1/toleration.go  Toleration.ToleratesTaint
   k8s.io/api v0.19.2 core/v1/helper MatchNodeSelectorTerms
 
@@ -24,8 +26,8 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import List
 
-from spotplanner.model import (Container, ContainerPort, GiB, MiB, Node, NodeSelectorRequirement, NodeSelectorTerm,
-                               Pod, Taint, Toleration)
+from spotplanner.model import (Container, ContainerPort, GiB, LabelSelector, LabelSelectorRequirement, MiB, Node,
+                               NodeSelectorRequirement, NodeSelectorTerm, Pod, PodAffinityTerm, Taint, Toleration)
 
 
 @dataclass
@@ -199,9 +201,72 @@ def _ports():
     yield Case("zero_host_port_ignored", r, hp("p", 0), nodes, base, [True, True, True, True, True])
 
 
+def _interpod():
+    aff = ("satisfyPodAffinity: the node carries every term's topology key and, per term, an existing pod that "
+           "matches ALL the pod's terms runs in the node's domain; else, when no such pod runs on a node with any of "
+           "the keys and the pod matches its own terms, every node carrying the keys")
+    anti = ("satisfyPodAntiAffinity / satisfyExistingPodsAntiAffinity: no pod selected by the pod's term (or whose "
+            "term selects the pod) in the node's domain of the term's key; a node without the key passes")
+    Z, H = "zone", "kubernetes.io/hostname"
+
+    def nodes():
+        return [N("n1", labels={Z: "a", H: "n1"}), N("n2", labels={Z: "a", H: "n2"}),
+                N("n3", labels={Z: "b", H: "n3"}), N("n4", labels={H: "n4"})]
+
+    def pod(name, labels, ns="default", affinity=None, anti_affinity=None):
+        return Pod(name, namespace=ns, labels=dict(labels), containers=[Container(cpu_milli=10)],
+                   pod_affinity=affinity, pod_anti_affinity=anti_affinity)
+
+    def term(key, sel, namespaces=()):
+        return PodAffinityTerm(key, sel, list(namespaces))
+
+    cache = LabelSelector({"app": "cache"})
+    web = LabelSelector({"app": "web"})
+    yield Case("aff_zone_existing_pod", aff, pod("w", {"app": "web"}, affinity=[term(Z, cache)]), nodes(),
+               [[], [], [pod("c", {"app": "cache"})], []], [False, False, True, False])
+    yield Case("aff_zone_whole_domain", aff, pod("w", {"app": "web"}, affinity=[term(Z, cache)]), nodes(),
+               [[pod("c", {"app": "cache"})], [], [], []], [True, True, False, False])
+    yield Case("aff_hostname", aff, pod("w", {"app": "web"}, affinity=[term(H, cache)]), nodes(),
+               [[], [pod("c", {"app": "cache"})], [], []], [False, True, False, False])
+    yield Case("aff_first_pod_of_self_affine_group", aff, pod("w", {"app": "web"}, affinity=[term(Z, web)]),
+               nodes(), [[], [], [], []], [True, True, True, False])
+    yield Case("aff_nothing_matches", aff, pod("w", {"app": "web"}, affinity=[term(Z, cache)]), nodes(),
+               [[pod("x", {"app": "db"})], [], [], []], [False, False, False, False])
+    yield Case("aff_match_on_node_without_key_not_self", aff, pod("w", {"app": "web"}, affinity=[term(Z, cache)]),
+               nodes(), [[], [], [], [pod("c", {"app": "cache"})]], [False, False, False, False])
+    yield Case("aff_match_on_node_without_key_self", aff + " (the pair map stays empty)",
+               pod("w", {"app": "web"}, affinity=[term(Z, web)]), nodes(),
+               [[], [], [], [pod("w0", {"app": "web"})]], [True, True, True, False])
+    yield Case("aff_self_affine_group_already_placed", aff, pod("w", {"app": "web"}, affinity=[term(Z, web)]),
+               nodes(), [[], [], [pod("w0", {"app": "web"})], []], [False, False, True, False])
+    two = [term(Z, cache), term(H, LabelSelector({"tier": "be"}))]
+    yield Case("aff_existing_pod_must_match_all_terms", aff, pod("w", {"app": "web"}, affinity=two), nodes(),
+               [[pod("x", {"app": "cache", "tier": "be"})], [], [pod("y", {"app": "cache"})], []],
+               [True, False, False, False])
+    yield Case("aff_term_namespace_defaults_to_pod", aff, pod("w", {"app": "web"}, affinity=[term(Z, cache)]),
+               nodes(), [[], [], [pod("c", {"app": "cache"}, ns="other")], []], [False, False, False, False])
+    yield Case("aff_term_namespaces_listed", aff,
+               pod("w", {"app": "web"}, affinity=[term(Z, cache, ["other", "default"])]), nodes(),
+               [[], [], [pod("c", {"app": "cache"}, ns="other")], []], [False, False, True, False])
+    yield Case("aff_nil_selector_matches_nothing", aff, pod("w", {"app": "web"}, affinity=[term(Z, None)]),
+               nodes(), [[pod("c", {"app": "cache"})], [], [], []], [False, False, False, False])
+    yield Case("aff_match_expressions", aff,
+               pod("w", {"app": "web"}, affinity=[term(Z, LabelSelector({}, [LabelSelectorRequirement(
+                   "app", "In", ["cache", "db"])]))]), nodes(),
+               [[], [], [pod("d", {"app": "db"})], []], [False, False, True, False])
+    yield Case("anti_zone_existing_pod_refuses", anti, pod("w", {"app": "web"}), nodes(),
+               [[pod("d", {"app": "db"}, anti_affinity=[term(Z, web)])], [], [], []], [False, False, True, True])
+    yield Case("anti_zone_incoming_pod_refuses", anti,
+               pod("w", {"app": "web"}, anti_affinity=[term(Z, LabelSelector({"app": "db"}))]), nodes(),
+               [[], [], [pod("d", {"app": "db"})], []], [True, True, False, True])
+    yield Case("aff_and_anti_together", aff + "; " + anti,
+               pod("w", {"app": "web"}, affinity=[term(Z, cache)], anti_affinity=[term(H, cache)]), nodes(),
+               [[pod("c", {"app": "cache"})], [], [], []], [False, True, False, False])
+
+
 def cases() -> List[Case]:
     out = []
-    for gen in (_resources, _taints, _unschedulable, _affinity, _ports):
+    for gen in (_resources, _taints, _unschedulable, _affinity, _ports, _interpod):
         out.extend(gen())
     names = [c.name for c in out]
     assert len(names) == len(set(names))

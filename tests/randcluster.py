@@ -125,11 +125,23 @@ def rand_anti(r: random.Random, p: Pod, rate: float, hostname_only: bool = False
             p.pod_anti_affinity.append(PodAffinityTerm(tk, rand_selector(r, hostname_only), ns))
 
 
+def rand_aff(r: random.Random, p: Pod, rate: float):
+    """Required pod affinity for some pods: one or two terms on the hostname or
+    a shared key (zone / team), valid selectors mostly on the app label."""
+    if r.random() < rate:
+        p.pod_affinity = []
+        for _ in range(r.randint(1, 2)):
+            tk = r.choice([HOST, "zone", "zone", "team"])
+            ns = [] if r.random() < 0.8 else r.sample(["default", "other"], r.randint(1, 2))
+            p.pod_affinity.append(PodAffinityTerm(tk, rand_selector(r, True), ns))
+
+
 def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 8, features: bool = True,
-                  fallback: bool = False, anti: float = 0.0, hostname_only: bool = False):
+                  fallback: bool = False, anti: float = 0.0, hostname_only: bool = False, aff: float = 0.0):
     """Returns (spot_nodes, spot_pods, candidates) with candidates a list of pod lists.
     anti > 0: pods carry namespaces / labels and that share required pod anti-affinity
-    (hostname_only: every term on kubernetes.io/hostname with a valid selector)."""
+    (hostname_only: every term on kubernetes.io/hostname with a valid selector).
+    aff > 0: that share of the pods (spot and candidate) carries required pod affinity."""
     r = random.Random(seed)
     nodes = [rand_node(r, "n%d" % i, features) for i in range(n_spot)]
     spot_pods = []
@@ -140,10 +152,14 @@ def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 
         spot_pods.append(ps)
     cands = [[rand_pod(r, "c%d_%d" % (c, k), features, fallback) for k in range(r.randint(0, max_pods))]
              for c in range(n_cand)]
-    if anti > 0:
+    if anti > 0 or aff > 0:
         for ps in spot_pods + cands:
             for p in ps:
                 rand_anti(r, p, anti, hostname_only)
+    if aff > 0:
+        for ps in spot_pods + cands:
+            for p in ps:
+                rand_aff(r, p, aff)
     return nodes, spot_pods, cands
 
 
@@ -179,4 +195,15 @@ def anti_interacts_off_node(nodes, pods) -> bool:
                 continue
             if any(j != i and term_selects(a, t, b) for j, b in enumerate(pods)):
                 return True
+    return False
+
+
+def aff_interacts(pods) -> bool:
+    """An earlier pod of the candidate matches every required affinity term of a
+    later one: that pod's allowed domains change while the candidate is
+    planned; the product routes such a candidate to the reference path."""
+    for k, p in enumerate(pods):
+        terms = p.pod_affinity or []
+        if terms and any(all(term_selects(p, t, q) for t in terms) for q in pods[:k]):
+            return True
     return False

@@ -9,7 +9,7 @@ import pytest
 
 from helpers import Scenario
 from oracle_lib import OracleSnapshot, load_oracle, oracle_new_node_map, oracle_plan
-from randcluster import anti_interacts_off_node, rand_scenario
+from randcluster import aff_interacts, anti_interacts_off_node, rand_scenario
 from spotplanner import capi
 from spotplanner.model import Container, ContainerPort, GiB, Node, Pod
 from spotplanner.rescheduler import plan_arrays
@@ -148,6 +148,17 @@ def test_random_plans_with_pod_anti_affinity(checker, seed):
     nodes, spot_pods, cands = rand_scenario(6000 + seed, n_spot=8 + seed % 12, n_cand=10, max_pods=4 + seed % 8,
                                             features=seed % 3 != 0, anti=0.3 + 0.02 * seed)
     run_scenario(checker, nodes, spot_pods, cands, extra_fallback=lambda c: anti_interacts_off_node(nodes, cands[c]))
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_random_plans_with_pod_affinity(checker, seed):
+    """Required pod affinity (static SAT / KEYS rows per term set) together with
+    anti-affinity; a candidate whose pods interact through an affinity set, or
+    through an anti-affinity term on a shared key, takes the reference path."""
+    nodes, spot_pods, cands = rand_scenario(6600 + seed, n_spot=8 + seed % 14, n_cand=10, max_pods=3 + seed % 7,
+                                            features=seed % 2 == 0, anti=0.15, aff=0.25 + 0.02 * seed)
+    run_scenario(checker, nodes, spot_pods, cands,
+                 extra_fallback=lambda c: aff_interacts(cands[c]) or anti_interacts_off_node(nodes, cands[c]))
 
 
 def test_pod_anti_affinity_exercises_the_state_bits(checker):

@@ -1,6 +1,6 @@
 // Host-only harness: NewNodeMap + snapshot + encode_workload on a synthetic
 // config, printing the workload's dimensions and host-side timings (no GPU).
-//   make -C k8s-spot-rescheduler_amd tools && k8s-spot-rescheduler_amd/build/encode_stats 3 [max candidates]
+//   make -C k8s-spot-rescheduler_amd tools && k8s-spot-rescheduler_amd/bin/encode_stats 3 [max candidates]
 // Encodes are timed cold (empty encoder cache), warm (the same snapshot
 // again) and after one spot node changed (a fresh snapshot with one more pod
 // on one node), the steady state of a planner between two ticks.
