@@ -310,7 +310,7 @@ void refresh_static(EncoderCache& C, const sr_snapshot* snap, int32_t Wp) {
   C.taint_rows.assign(C.taints.size() * static_cast<size_t>(Wp), 0);
   for (const auto& h : hits)
     C.taint_rows[static_cast<size_t>(h.first) * Wp + (h.second >> 6)] |= 1ull << (h.second & 63);
-  C.state_fp.clear();  // positions may have moved: the state view is rebuilt too
+  C.state_valid = false;  // positions may have moved: the state view is rebuilt too
 }
 
 // ---- state view: capacity records, free values (sorted), pod-count atom
@@ -323,7 +323,7 @@ sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* e
   if (n > kSerialPods) parallel_for(static_cast<size_t>(n), 1024, fill_fp);
   else fill_fp(0, static_cast<size_t>(n));
   std::vector<int32_t> changed;
-  const bool full = C.state_fp.size() != static_cast<size_t>(n);
+  const bool full = !C.state_valid || C.state_fp.size() != static_cast<size_t>(n);
   if (!full)
     for (int32_t i = 0; i < n; ++i)
       if (fp[i] != C.state_fp[i]) changed.push_back(i);
@@ -354,7 +354,7 @@ sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* e
     word = left >= 1 ? (word | bit) : (word & ~bit);
   };
   auto fail = [&]() {
-    C.state_fp.clear();
+    C.state_valid = false;
     *err = "spot node quantity outside [0, 2^62)";
     return SR_ERR_CAPACITY;
   };
@@ -388,6 +388,7 @@ sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* e
     C.node_vals[d].erase(std::unique(C.node_vals[d].begin(), C.node_vals[d].end()), C.node_vals[d].end());
   }
   C.state_fp.swap(fp);
+  C.state_valid = true;
   return SR_OK;
 }
 
@@ -528,6 +529,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         return SR_ERR_INVALID_ARG;
       }
   }
+  std::vector<uint8_t>& cand_ports = C.scratch.cand_ports;  // the candidate's pods ask for host ports
+  cand_ports.assign(static_cast<size_t>(nc), 0);
   auto pass1 = [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
       const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
@@ -539,10 +542,13 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       bool fb = (c->pod_affinity ? snap->opaque_total : snap->anti_total) > 0 || (e - b) > MAX_CAND_PODS;
       for (int32_t j = b; j < e && !fb; ++j) fb = pod_fallback(cands->cand_pods[j]);
       if (fb) w->status_host[i] = SR_CAND_FALLBACK;
+      for (int32_t j = b; j < e && !fb && !cand_ports[i]; ++j)
+        cand_ports[i] = P.port_off[cands->cand_pods[j]] != P.port_off[cands->cand_pods[j] + 1];
     }
   };
   if (w->n_input_pods > kSerialPods) parallel_for(static_cast<size_t>(nc), 64, pass1);
   else pass1(0, static_cast<size_t>(nc));
+  phase(5);
 
   // ---- required pod anti-affinity: static node sets, state-bit pairs and
   // the candidates it sends to the fallback path (antiaff.cpp)
@@ -568,7 +574,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   auto port_key = [](int32_t proto, int32_t port) { return (static_cast<int64_t>(proto) << 32) | uint32_t(port); };
   std::unordered_map<int64_t, uint8_t> group_specific;  // (proto, port) -> has a specific IP
   for (int32_t i = 0; i < nc; ++i) {
-    if (w->status_host[i] != STATUS_PENDING) continue;
+    if (w->status_host[i] != STATUS_PENDING || !cand_ports[i]) continue;
     for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
       const int32_t pod = cands->cand_pods[j];
       for (int32_t k = P.port_off[pod]; k < P.port_off[pod + 1]; ++k)
@@ -584,7 +590,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   int32_t n_port_pairs = 0, n_port_single = 0;
   if (!group_specific.empty())
     for (int32_t i = 0; i < nc; ++i) {
-      if (w->status_host[i] != STATUS_PENDING) continue;
+      if (w->status_host[i] != STATUS_PENDING || !cand_ports[i]) continue;
       const int32_t pairs0 = n_port_pairs, single0 = n_port_single;
       std::vector<std::pair<int64_t, int32_t>> added_ips;  // undone if the candidate overflows
       std::vector<int64_t> added_groups;
@@ -666,28 +672,41 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   }
   phase(1);
 
-  // Active pods in candidate order.
-  std::vector<int32_t> active_pod;   // cluster pod index
-  std::vector<int32_t> active_src;   // flat index into cand_pods
-  for (int32_t i = 0; i < nc; ++i) {
+  // Active pods in candidate order: offsets per candidate, then a parallel fill.
+  std::vector<int32_t>& active_pod = C.scratch.active_pod;  // cluster pod index
+  std::vector<int32_t>& active_src = C.scratch.active_src;  // flat index into cand_pods
+  std::vector<int32_t>& act_of = C.scratch.act_of;          // input candidate -> active candidate (-1)
+  act_of.assign(static_cast<size_t>(nc), -1);
+  for (int32_t i = 0, acc = 0; i < nc; ++i) {
     if (w->status_host[i] != STATUS_PENDING) continue;
     const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
-    w->cand_off.push_back(static_cast<int32_t>(active_pod.size()));
+    act_of[i] = static_cast<int32_t>(w->cand_src.size());
+    w->cand_off.push_back(acc);
     w->cand_global.push_back(cands->cand_global ? cands->cand_global[i] : i);
     w->cand_src.push_back(i);
     w->max_cand_pods = std::max(w->max_cand_pods, e - b);
-    for (int32_t j = b; j < e; ++j) {
-      active_pod.push_back(cands->cand_pods[j]);
-      active_src.push_back(j);
-    }
+    acc += e - b;
   }
-  w->cand_off.push_back(static_cast<int32_t>(active_pod.size()));
-  const int32_t na = static_cast<int32_t>(active_pod.size());
+  const int32_t n_act = static_cast<int32_t>(w->cand_src.size());
+  const int32_t na = n_act > 0 ? w->cand_off.back() + (cands->cand_pod_off[w->cand_src.back() + 1] -
+                                                        cands->cand_pod_off[w->cand_src.back()]) : 0;
+  w->cand_off.push_back(na);
+  active_pod.resize(static_cast<size_t>(na));
+  active_src.resize(static_cast<size_t>(na));
   const bool big = na > kSerialPods;
   auto pfor = [&](size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn) {
     if (big) parallel_for(n, grain, fn);
     else fn(0, n);
   };
+  pfor(static_cast<size_t>(n_act), 256, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      const int32_t i = w->cand_src[k], b = cands->cand_pod_off[i];
+      for (int32_t q = w->cand_off[k]; q < w->cand_off[k + 1]; ++q) {
+        active_pod[q] = cands->cand_pods[b + (q - w->cand_off[k])];
+        active_src[q] = b + (q - w->cand_off[k]);
+      }
+    }
+  });
 
   // ---- static specs, interned by content across calls.  Each pod's raw spec
   // words are gathered once into per-chunk buffers and hashed; the hash picks
@@ -695,16 +714,28 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   // specs never seen before get their ids serially afterwards (in shard,
   // first-occurrence order: independent of the thread count) and are
   // canonicalised in parallel.
-  std::vector<int32_t> pod_spec(static_cast<size_t>(na), 0);
-  std::vector<uint64_t> spec_hash(static_cast<size_t>(na), 0);
-  std::vector<uint8_t> spec_shard(static_cast<size_t>(na), 0xff);
+  EncoderCache::Scratch& X = C.scratch;
+  std::vector<int32_t>& pod_spec = X.pod_spec;
+  std::vector<uint64_t>& spec_hash = X.spec_hash;
+  std::vector<uint8_t>& spec_shard = X.spec_shard;
+  pod_spec.assign(static_cast<size_t>(na), 0);
+  spec_hash.resize(static_cast<size_t>(na));
+  spec_shard.assign(static_cast<size_t>(na), 0xff);
   constexpr size_t kChunk = 2048;
-  std::vector<std::vector<int32_t>> spec_words((static_cast<size_t>(na) + kChunk - 1) / kChunk);
-  std::vector<uint32_t> spec_woff(static_cast<size_t>(na), 0);
-  pfor(spec_words.size(), 1, [&](size_t lo, size_t hi) {
+  const size_t n_chunks = (static_cast<size_t>(na) + kChunk - 1) / kChunk;
+  std::vector<std::vector<int32_t>>& spec_words = X.spec_words;
+  if (spec_words.size() < n_chunks) spec_words.resize(n_chunks);
+  std::vector<uint32_t>& spec_woff = X.spec_woff;
+  spec_woff.resize(static_cast<size_t>(na));
+  // per chunk and shard, the chunk's pods of the shard (in order): each shard
+  // then scans only its own pods
+  std::vector<std::vector<int32_t>>& chunk_shard = X.chunk_shard;  // [chunk * kSpecShards + shard]
+  if (chunk_shard.size() < n_chunks * kSpecShards) chunk_shard.resize(n_chunks * kSpecShards);
+  pfor(n_chunks, 1, [&](size_t lo, size_t hi) {
     for (size_t ch = lo; ch < hi; ++ch) {
       std::vector<int32_t>& buf = spec_words[ch];
       buf.clear();
+      for (size_t sh = 0; sh < kSpecShards; ++sh) chunk_shard[ch * kSpecShards + sh].clear();
       const size_t q1 = std::min(static_cast<size_t>(na), (ch + 1) * kChunk);
       for (size_t q = ch * kChunk; q < q1; ++q) {
         const size_t b0 = buf.size();
@@ -714,10 +745,13 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         for_each_spec_word(P, pod, [&](int32_t x) { buf.push_back(x); });
         const uint64_t h = hash_words(buf.data() + b0, buf.size() - b0);
         spec_hash[q] = h;
-        spec_shard[q] = static_cast<uint8_t>(((h >> 32) * kSpecShards) >> 32);
+        const size_t sh = static_cast<size_t>(((h >> 32) * kSpecShards) >> 32);
+        spec_shard[q] = static_cast<uint8_t>(sh);
+        chunk_shard[ch * kSpecShards + sh].push_back(static_cast<int32_t>(q));
       }
     }
   });
+  phase(9);
   auto words_of = [&](size_t q, size_t* n) {
     const std::vector<int32_t>& buf = spec_words[q / kChunk];
     const size_t e = (q + 1) % kChunk == 0 || q + 1 == static_cast<size_t>(na) ? buf.size() : spec_woff[q + 1];
@@ -729,18 +763,18 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     for (size_t sh = lo; sh < hi; ++sh) {
       EncoderCache::SpecShard& S = C.spec_shards[sh];
       shard_new[sh].clear();
-      for (int32_t q = 0; q < na; ++q) {
-        if (spec_shard[q] != sh) continue;
-        size_t n = 0;
-        const int32_t* p = words_of(static_cast<size_t>(q), &n);
-        bool ins = false;
-        const int32_t local = S.dict.intern(p, n, spec_hash[q], &ins);
-        if (ins) {
-          S.global.push_back(-1);
-          shard_new[sh].push_back(q);
+      for (size_t ch = 0; ch < n_chunks; ++ch)
+        for (int32_t q : chunk_shard[ch * kSpecShards + sh]) {
+          size_t n = 0;
+          const int32_t* p = words_of(static_cast<size_t>(q), &n);
+          bool ins = false;
+          const int32_t local = S.dict.intern(p, n, spec_hash[q], &ins);
+          if (ins) {
+            S.global.push_back(-1);
+            shard_new[sh].push_back(q);
+          }
+          pod_spec[q] = local;  // local for now
         }
-        pod_spec[q] = local;  // local for now
-      }
     }
   });
   phase(14);
@@ -791,11 +825,13 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   // anti-affinity term ids and affinity set of this call.  Pods without either
   // use their spec id as key.
   const int32_t n_spec_ids = static_cast<int32_t>(C.spec.size());
-  std::vector<int32_t> pod_key(static_cast<size_t>(na));
+  const bool combos = anti.active || aff.active;
+  std::vector<int32_t>& pod_key_buf = X.pod_key;
   std::vector<int32_t> key_spec;               // keys >= n_spec_ids: spec of the combined key,
   std::vector<std::vector<int32_t>> key_anti;  // ... its anti-affinity term ids
   std::vector<int32_t> key_aff;                // ... and its affinity code (AffTerms::pod_code)
-  {
+  if (combos) {
+    pod_key_buf.resize(static_cast<size_t>(na));
     WordDict combo;
     std::vector<int32_t> kw;
     for (int32_t q = 0; q < na; ++q) {
@@ -803,7 +839,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       const int32_t n_ids = anti.active ? anti.pod_off[j + 1] - anti.pod_off[j] : 0;
       const int32_t code = aff.active ? aff.pod_code[active_src[q] - aff.base] : -1;
       if (n_ids == 0 && code < 0) {
-        pod_key[q] = pod_spec[q];
+        pod_key_buf[q] = pod_spec[q];
         continue;
       }
       kw.assign(1, pod_spec[q]);
@@ -816,16 +852,27 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         key_aff.push_back(code);
         key_anti.emplace_back(kw.begin() + 2, kw.end());
       }
-      pod_key[q] = n_spec_ids + id;
+      pod_key_buf[q] = n_spec_ids + id;
     }
   }
-  // distinct keys of this call, in first-occurrence order
-  std::vector<int32_t> key_slot(static_cast<size_t>(n_spec_ids) + key_spec.size(), -1);
+  const std::vector<int32_t>& pod_key = combos ? pod_key_buf : pod_spec;
+  // distinct keys of this call, in key order: flags set in parallel, slots serially
+  const size_t n_key_ids = static_cast<size_t>(n_spec_ids) + key_spec.size();
+  std::vector<uint8_t>& key_seen = X.key_seen;
+  key_seen.assign(n_key_ids, 0);
+  pfor(static_cast<size_t>(na), 8192, [&](size_t lo, size_t hi) {
+    for (size_t q = lo; q < hi; ++q) {  // read first: a shared line written by every thread would bounce
+      uint8_t* f = &key_seen[pod_key[q]];
+      if (!__atomic_load_n(f, __ATOMIC_RELAXED)) __atomic_store_n(f, uint8_t(1), __ATOMIC_RELAXED);
+    }
+  });
+  std::vector<int32_t>& key_slot = X.key_slot;
+  key_slot.assign(n_key_ids, -1);
   std::vector<int32_t> keys;
-  for (int32_t q = 0; q < na; ++q)
-    if (key_slot[pod_key[q]] < 0) {
-      key_slot[pod_key[q]] = static_cast<int32_t>(keys.size());
-      keys.push_back(pod_key[q]);
+  for (size_t k = 0; k < n_key_ids; ++k)
+    if (key_seen[k]) {
+      key_slot[k] = static_cast<int32_t>(keys.size());
+      keys.push_back(static_cast<int32_t>(k));
     }
 
   // ---- per key: untolerated taints (cached per spec and static view), host
@@ -882,19 +929,84 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   };
   phase(2);
 
-  // ---- classes: one program per distinct signature {flags, selector ids,
-  // terms, untolerated set, host-port bits, anti-affinity atoms}
-  WordDict class_dict;
-  std::vector<int32_t> key_class(keys.size());
-  std::vector<uint64_t> key_ports(keys.size());
-  std::vector<int32_t> sig, da, db;
+  // ---- classes: one program per distinct signature.  A spec without host
+  // ports and without inter-pod terms has a signature that only depends on
+  // the spec and the static view {flags, selector ids, terms, untolerated
+  // set}: it is interned once per static view (SpecInfo::psig) and its class
+  // found by one table lookup per call.  Other keys add this call's host-port
+  // bits, anti-affinity atoms and affinity atom and are interned per call.
+  if (C.psig_gen != C.static_gen) {
+    C.psig_dict.clear();
+    C.psig_gen = C.static_gen;
+  }
+  std::vector<int32_t> sig, da, db, call_class;
+  auto static_sig = [&](const SpecInfo& sp, int32_t untol, std::vector<int32_t>& out) {
+    out.clear();
+    out.push_back(sp.flags);
+    out.push_back(static_cast<int32_t>(sp.sel.size()));
+    out.insert(out.end(), sp.sel.begin(), sp.sel.end());
+    out.push_back(sp.n_terms);
+    out.insert(out.end(), sp.terms.begin(), sp.terms.end());
+    out.push_back(untol);
+  };
   w->cls_prog_off.push_back(0);
   auto emit = [&](int32_t atom, int32_t kind) { w->cls_prog.push_back(atom << 2 | kind); };
+  // program: AND atoms, AND-NOT atoms, then the ORed terms (TERM_START opens a
+  // term, TERM_AND extends it); an impossible class ANDs atom 0 with its
+  // complement.  `sw` = static signature words.
+  auto emit_class = [&](const int32_t* sw, uint64_t ports, const std::vector<int32_t>* da_, const std::vector<int32_t>* db_,
+                        int32_t aff_atom) {
+    const int32_t flags = sw[0], n_sel = sw[1];
+    const int32_t* sel = sw + 2;
+    const int32_t* tp = sel + n_sel;
+    const int32_t n_terms = *tp++;
+    const int32_t* term_words = tp;
+    for (int32_t k = 0; k < n_terms; ++k) tp += 1 + *tp;
+    const int32_t untol = *tp;
+    emit(comp_atom(untol), PROG_AND);  // len(pods)+1 <= allowed pods, untolerated taints
+    for (int32_t k = 0; k < n_sel; ++k) emit(A_REQ + req_atom[sel[k]], PROG_AND);
+    for (int32_t b = 0; b < 64; ++b)  // the base UsedPorts conflicting with each host port it asks for
+      if ((ports >> b & 1) && bit_query[b] >= 0) emit(A_PORT + bit_query[b], PROG_ANDNOT);
+    if (da_)
+      for (int32_t t : *da_) emit(A_ANTI + 2 * t, PROG_ANDNOT);  // anti-affinity base conflicts
+    if (db_)
+      for (int32_t t : *db_) emit(A_ANTI + 2 * t + 1, PROG_ANDNOT);
+    if (aff_atom >= 0) emit(aff_atom, PROG_AND);
+    if ((flags & CLS_IMPOSSIBLE) || aff_atom == -2) {
+      emit(0, PROG_ANDNOT);
+    } else {
+      for (int32_t k = 0; k < n_terms; ++k) {
+        const int32_t n = *term_words++;
+        for (int32_t i = 0; i < n; ++i)
+          emit(A_REQ + req_atom[term_words[i]], i == 0 ? PROG_TERM_START : PROG_TERM_AND);
+        term_words += n;
+      }
+    }
+    w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
+    return w->n_classes++;
+  };
+  WordDict class_dict;
+  std::vector<int32_t> key_class(keys.size());
+  std::vector<uint64_t> key_ports(keys.size(), 0);
+  std::vector<int32_t>& psig_class = X.psig_class;  // static signature -> class of this call
+  psig_class.assign(C.psig_dict.size(), -1);
   for (size_t ki = 0; ki < keys.size(); ++ki) {
     const int32_t k = keys[ki];
     const int32_t spec_id = k < n_spec_ids ? k : key_spec[k - n_spec_ids];
-    const SpecInfo& sp = C.spec[spec_id];
+    SpecInfo& sp = C.spec[spec_id];
     const int32_t untol = untol_of(spec_id);
+    if (k < n_spec_ids && sp.ports.empty()) {
+      if (sp.psig_gen != C.static_gen) {
+        static_sig(sp, untol, sig);
+        sp.psig = C.psig_dict.intern(sig);
+        sp.psig_gen = C.static_gen;
+      }
+      if (static_cast<size_t>(sp.psig) >= psig_class.size()) psig_class.resize(C.psig_dict.size(), -1);
+      int32_t& cls = psig_class[sp.psig];
+      if (cls < 0) cls = emit_class(C.psig_dict.data(sp.psig), 0, nullptr, nullptr, -1);
+      key_class[ki] = cls;
+      continue;
+    }
     const uint64_t ports = port_mask(sp.ports);
     key_ports[ki] = ports;
     da.clear();
@@ -915,13 +1027,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
           if (anti.da_any[t]) da.push_back(t);
         }
       }
-    sig.clear();
-    sig.push_back(sp.flags);
-    sig.push_back(static_cast<int32_t>(sp.sel.size()));
-    sig.insert(sig.end(), sp.sel.begin(), sp.sel.end());
-    sig.push_back(sp.n_terms);
-    sig.insert(sig.end(), sp.terms.begin(), sp.terms.end());
-    sig.push_back(untol);
+    static_sig(sp, untol, sig);
+    const size_t n_static = sig.size();
     sig.push_back(static_cast<int32_t>(ports & 0xffffffffu));
     sig.push_back(static_cast<int32_t>(ports >> 32));
     sig.push_back(static_cast<int32_t>(da.size()));
@@ -930,27 +1037,12 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     sig.insert(sig.end(), db.begin(), db.end());
     sig.push_back(aff_atom);
     bool ins = false;
-    key_class[ki] = class_dict.intern(sig, &ins);
-    if (!ins) continue;
-    // program: AND atoms, AND-NOT atoms, then the ORed terms (TERM_START
-    // opens a term, TERM_AND extends it); an impossible class ANDs atom 0
-    // with its complement
-    emit(comp_atom(untol), PROG_AND);  // len(pods)+1 <= allowed pods, untolerated taints
-    for (int32_t r : sp.sel) emit(A_REQ + req_atom[r], PROG_AND);
-    for (int32_t b = 0; b < 64; ++b)  // the base UsedPorts conflicting with each host port it asks for
-      if ((ports >> b & 1) && bit_query[b] >= 0) emit(A_PORT + bit_query[b], PROG_ANDNOT);
-    for (int32_t t : da) emit(A_ANTI + 2 * t, PROG_ANDNOT);  // anti-affinity base conflicts
-    for (int32_t t : db) emit(A_ANTI + 2 * t + 1, PROG_ANDNOT);
-    if (aff_atom >= 0) emit(aff_atom, PROG_AND);
-    if ((sp.flags & CLS_IMPOSSIBLE) || aff_atom == -2) {
-      emit(0, PROG_ANDNOT);
-    } else {
-      for (size_t i = 0; i < sp.terms.size(); i += 1 + static_cast<size_t>(sp.terms[i]))
-        for (int32_t t = 0; t < sp.terms[i]; ++t)
-          emit(A_REQ + req_atom[sp.terms[i + 1 + t]], t == 0 ? PROG_TERM_START : PROG_TERM_AND);
+    const int32_t id = class_dict.intern(sig, &ins);
+    if (ins) {
+      sig.resize(n_static);
+      call_class.push_back(emit_class(sig.data(), ports, &da, &db, aff_atom));
     }
-    w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
-    w->n_classes++;
+    key_class[ki] = call_class[id];
   }
   w->n_atoms = A_COMP + static_cast<int32_t>(comp_sets.size());
   phase(3);
@@ -1074,6 +1166,9 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       cls_empty[k] = empty || (has_terms && all_terms_empty);
     }
   }
+  phase(8);
+  std::vector<uint8_t> used[3];  // lower-bound positions some pod asks for, per dimension
+  for (int d = 0; d < 3; ++d) used[d].assign(C.node_vals[d].size() + 1, 0);
   std::atomic<bool> any_dead{false};
   // per pod: requests, records and the lower-bound position of each request
   // among the node values (stored in pod_rows[1..3] for now)
@@ -1094,8 +1189,12 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       rec[2] = static_cast<uint64_t>(re);
       rec[3] = key_ports[ki] | (anti.active ? anti.pod_bits[active_src[q] - anti.base] : 0);
       bool dead = cls_empty[r[0]] != 0;
-      for (int d = 0; d < 3; ++d)
-        dead = dead || (r[1 + d] >= 0 && static_cast<size_t>(r[1 + d]) == C.node_vals[d].size());
+      for (int d = 0; d < 3; ++d) {
+        if (r[1 + d] < 0) continue;
+        uint8_t* u = &used[d][static_cast<size_t>(r[1 + d])];  // read first (see key_seen)
+        if (!__atomic_load_n(u, __ATOMIC_RELAXED)) __atomic_store_n(u, uint8_t(1), __ATOMIC_RELAXED);
+        dead = dead || static_cast<size_t>(r[1 + d]) == C.node_vals[d].size();
+      }
       if (dead) {
         r[0] = -1;  // the empty class, appended below
         any_dead.store(true, std::memory_order_relaxed);
@@ -1114,13 +1213,6 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   // K0 compares one dimension per wave)
   std::vector<int32_t> t_index[3];
   {
-    std::vector<uint8_t> used[3];
-    for (int d = 0; d < 3; ++d) used[d].assign(C.node_vals[d].size() + 1, 0);
-    for (int32_t q = 0; q < na; ++q) {
-      const int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
-      for (int d = 0; d < 3; ++d)
-        if (r[1 + d] >= 0) used[d][static_cast<size_t>(r[1 + d])] = 1;
-    }
     w->t_off[0] = 0;
     w->t_off[1] = 1;
     for (int d = 0; d < 3; ++d) {

@@ -198,6 +198,8 @@ struct SpecInfo {
   std::vector<int32_t> ports;  // host ports {protocol, port, ip}* with port > 0
   uint64_t untol_gen = ~0ull;  // static generation `untol` was computed for
   int32_t untol = -1;          // set of spot-pool taints it does not tolerate (EncoderCache::untol_dict)
+  uint64_t psig_gen = ~0ull;   // static generation `psig` was interned for
+  int32_t psig = -1;           // its class signature (EncoderCache::psig_dict) when it asks for no host port
 };
 
 // What the encoder keeps across calls (one per sr_ctx).  The spot pool is
@@ -225,6 +227,7 @@ struct EncoderCache {
   std::vector<std::vector<uint64_t>> req_rows;   // [req][Wp]
   // ---- state view
   std::vector<uint64_t> state_fp;
+  bool state_valid = false;  // the arrays below describe the current static view
   uint64_t state_gen = 0;
   std::vector<uint64_t> node_rec;      // [n_pad][8] {free cpu, mem, eph, state bits (0), pods left, 0, 0, 0}
   std::vector<int64_t> node_free;      // [3][n_pad] free cpu / memory / ephemeral (pads: INT64_MIN)
@@ -241,6 +244,16 @@ struct EncoderCache {
   WordDict req_dict;                   // requirement words {type, key, op, vals...} -> requirement id
   WordDict untol_dict;                 // untolerated-taint sets (valid for untol_gen)
   uint64_t untol_gen = ~0ull;
+  WordDict psig_dict;                  // class signatures of port-free specs (valid for psig_gen)
+  uint64_t psig_gen = ~0ull;
+  // ---- per-call scratch (kept: fresh multi-MB buffers page-fault on every call)
+  struct Scratch {
+    std::vector<uint8_t> cand_ports, spec_shard, key_seen;
+    std::vector<int32_t> active_pod, active_src, act_of, pod_spec, pod_key, key_slot, psig_class;
+    std::vector<uint64_t> spec_hash;
+    std::vector<uint32_t> spec_woff;
+    std::vector<std::vector<int32_t>> spec_words, chunk_shard;
+  } scratch;
   // ---- per-call counters (bench: what the last call had to rebuild)
   int32_t last_new_specs = 0, last_static_changed = 0, last_state_changed = 0;
 
@@ -252,6 +265,8 @@ struct EncoderCache {
     req_row_gen.clear();
     untol_dict.clear();
     untol_gen = ~0ull;
+    psig_dict.clear();
+    psig_gen = ~0ull;
   }
 };
 

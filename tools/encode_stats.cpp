@@ -21,9 +21,9 @@ static double ms_since(std::chrono::steady_clock::time_point a) {
 
 static void phases(const char* tag) {
   const double* p = sr::encode_phase_ms;
-  printf("  %-6s phases(ms): views %.3f fallback+ports %.3f specs-hash %.3f specs-new %.3f keys %.3f classes %.3f "
-         "atoms %.3f pods %.3f trows %.3f recs %.3f lists %.3f\n",
-         tag, p[0], p[1], p[14], p[7], p[2], p[3], p[4], p[10], p[12], p[13], p[6]);
+  printf("  %-6s phases(ms): views %.3f pass1 %.3f ports %.3f gather %.3f shards %.3f specs-new %.3f keys %.3f "
+         "classes %.3f atoms %.3f lb+empty %.3f pods %.3f trows %.3f recs %.3f lists %.3f\n",
+         tag, p[0], p[5], p[1], p[9], p[14], p[7], p[2], p[3], p[4], p[8], p[10], p[12], p[13], p[6]);
 }
 
 int main(int argc, char** argv) {
