@@ -2,6 +2,8 @@
 hand-derived answer on the oracle (CPU) and on the GPU path through the C-ABI:
 sr_find_spot_nodes one spot node at a time (the per-node answer) and sr_plan
 over all nodes of the case (first fit = the first node whose answer is yes)."""
+import dataclasses
+
 import numpy as np
 import pytest
 
@@ -9,6 +11,7 @@ from helpers import Scenario
 from known_answer import cases
 from oracle_lib import load_oracle
 from spotplanner import capi
+from spotplanner.model import Taint
 
 CASES = cases()
 IDS = [c.name for c in CASES]
@@ -54,9 +57,19 @@ def _gpu_first_fit(checker, sc, n_nodes):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES, ids=IDS)
 def test_gpu_known_answer(checker, case):
+    inter_pod = case.name.startswith(("aff_", "anti_"))
     for i, node in enumerate(case.nodes):  # the answer of every node on its own
-        sc = Scenario([node], [case.base[i]], [case.pod])
-        assert _gpu_first_fit(checker, sc, 1) == (0 if case.fits[i] else -1), (case.rule, node.name)
+        if inter_pod:
+            # the topology domain spans the other nodes' pods: keep every node,
+            # and keep the pod off the others with a taint it does not tolerate
+            others = [dataclasses.replace(n, taints=list(n.taints) + [Taint("ka-only-this-node")]) if j != i else n
+                      for j, n in enumerate(case.nodes)]
+            sc = Scenario(others, case.base, [case.pod])
+            want = i if case.fits[i] else -1
+        else:
+            sc = Scenario([node], [case.base[i]], [case.pod])
+            want = 0 if case.fits[i] else -1
+        assert _gpu_first_fit(checker, sc, len(sc.nodes)) == want, (case.rule, node.name)
     # first fit over all nodes, through the batched planner (one candidate)
     sc = Scenario(case.nodes, case.base, [case.pod])
     first = next((i for i, f in enumerate(case.fits) if f), -1)
