@@ -55,8 +55,6 @@ __device__ __forceinline__ int wave_min(int v) {
 // K0: bitmask rows.  Blocks [0, s_blocks): S rows, kSClasses classes per
 // wave, lanes = words; blocks after: T rows, lanes = rows.
 constexpr int kSClasses = 2;  // S rows per wave: their atom loads are in flight together
-constexpr int kSClassesL = 8; // S rows per wave when the atom table is staged in LDS
-constexpr int kAtomLdsWords = 6144;  // atom tables up to 48 KB are staged in LDS
 constexpr int kTWords = 2;    // T row words per wave
 
 // One S row by the class's atom program read through cls_prog_off (any length):
@@ -103,68 +101,6 @@ __device__ void s_row_general(const DevWorkload& w, int cls, int lane) {
   }
 }
 
-// S rows from the atom table staged in LDS: the block's one memory round trip
-// brings the atoms and each wave's 8 class programs together; every class is
-// then evaluated from LDS (lanes = words, conflict-free b64 reads).
-__device__ __forceinline__ void s_rows_lds(const DevWorkload& w, int c0, int lane) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t k0_atoms[];
-  const int Wp = w.Wp;
-  int op[kSClassesL][8];
-#pragma unroll
-  for (int q = 0; q < kSClassesL; ++q) {
-    const int cls = c0 + q;
-    if (cls < w.n_classes) {
-      const int4* p8 = reinterpret_cast<const int4*>(w.cls_prog8 + static_cast<size_t>(cls) * 8);
-      const int4 a = p8[0], b = p8[1];
-      op[q][0] = a.x; op[q][1] = a.y; op[q][2] = a.z; op[q][3] = a.w;
-      op[q][4] = b.x; op[q][5] = b.y; op[q][6] = b.z; op[q][7] = b.w;
-    } else {
-      op[q][0] = -3;  // no class
-#pragma unroll
-      for (int u = 1; u < 8; ++u) op[q][u] = -1;
-    }
-  }
-  const int nw = w.n_atoms * Wp;  // even: Wp is
-  for (int i = 2 * static_cast<int>(threadIdx.x); i < nw; i += 2 * static_cast<int>(blockDim.x)) {
-    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(w.atoms + i);
-    k0_atoms[i] = a.x;
-    k0_atoms[i + 1] = a.y;
-  }
-  __syncthreads();
-  for (int wb = 0; wb < Wp; wb += 64) {
-    const int word = wb + lane;
-    const bool wv = word < Wp;
-    const int wi = wv ? word : 0;
-#pragma unroll
-    for (int q = 0; q < kSClassesL; ++q) {
-      if (op[q][0] < 0 && op[q][0] != -1) continue;  // no class, or a long program (below)
-      uint64_t acc = ~0ull, any = 0, cur = 0;
-      bool has = false;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (op[q][u] < 0) break;  // wave-uniform
-        const uint64_t v = k0_atoms[(op[q][u] >> 2) * Wp + wi];
-        switch (op[q][u] & 3) {
-          case PROG_AND: acc &= v; break;
-          case PROG_ANDNOT: acc &= ~v; break;
-          case PROG_TERM_START:
-            any |= has ? cur : 0;
-            cur = v;
-            has = true;
-            break;
-          default: cur &= v; break;
-        }
-      }
-      if (has) acc &= any | cur;
-      if (wv) w.S[static_cast<size_t>(c0 + q) * Wp + word] = acc;
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < kSClassesL; ++q)
-    if (op[q][0] == -2) s_row_general(w, c0 + q, lane);
-}
-
-template <bool LA>
 __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, int local_first_fallback) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -185,10 +121,6 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
     dm[1] = local_first_fallback < 0 ? ~0ull : static_cast<unsigned long long>(local_first_fallback) << 32;
   }
   const size_t Wp = static_cast<size_t>(w.Wp);
-  if (LA && static_cast<int>(blockIdx.x) < s_blocks) {
-    s_rows_lds(w, __builtin_amdgcn_readfirstlane((static_cast<int>(blockIdx.x) * 4 + wave) * kSClassesL), lane);
-    return;
-  }
   if (static_cast<int>(blockIdx.x) < s_blocks) {
     // S rows (NodeAffinity: nodeSelector pairs, required terms ORed with
     // their requirements ANDed; TaintToleration + NodeUnschedulable + pod
@@ -1102,18 +1034,12 @@ hipError_t launch_k2(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEve
 
 hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hipStream_t s, hipEvent_t ev0,
                          hipEvent_t ev1) {
-  const bool lds = w.k0_lds && w.n_atoms * w.Wp <= kAtomLdsWords;
-  const int per_block = 4 * (lds ? kSClassesL : kSClasses);
-  const int s_blocks = (w.n_classes + per_block - 1) / per_block;
+  const int s_blocks = (w.n_classes + 4 * kSClasses - 1) / (4 * kSClasses);
   const int wgroups = (w.Wp + kTWords - 1) / kTWords;
   int t_waves = 0;
   for (int d = 0; d < 4; ++d) t_waves += (w.t_off[d + 1] - w.t_off[d] + 63) / 64 * wgroups;
   const unsigned blocks = static_cast<unsigned>(std::max(1, s_blocks + (t_waves + 3) / 4));
-  if (lds)
-    launch(k0_tables<true>, dim3(blocks), dim3(256), sizeof(uint64_t) * w.n_atoms * w.Wp, s, ev0, ev1, w, s_blocks,
-           local_first_fallback);
-  else
-    launch(k0_tables<false>, dim3(blocks), dim3(256), 0, s, ev0, ev1, w, s_blocks, local_first_fallback);
+  launch(k0_tables, dim3(blocks), dim3(256), 0, s, ev0, ev1, w, s_blocks, local_first_fallback);
   return hipGetLastError();
 }
 

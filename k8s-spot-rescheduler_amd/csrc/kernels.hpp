@@ -48,7 +48,6 @@ struct DevWorkload {
   uint64_t* result;    // mapped host memory [kResultHeader + max pods] words seq << 32 | value:
                        //   {winner, local, npods, first_fallback, -, -, -, -, mapping...}
   uint32_t seq;        // run sequence number: the tag of every result word (wraps)
-  int32_t k0_lds;      // 1: K0 stages the atom table in LDS when it fits (SR_K0_LDS=0 turns it off for A/B)
   int32_t k2_mode;     // 0: node-order first fit where it applies (<= 64 pods, <= 64-word rows);
                        // 1: pod order everywhere (SR_K2_MODE=1, A/B measurement)
   uint64_t* prof;      // optional [n_cand][16] K2 + [kK0ProfWaves][2] K0 per-wave profile
