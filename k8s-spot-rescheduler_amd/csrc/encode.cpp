@@ -518,20 +518,23 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
           if (P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT) return true;
     return anti_opaque(c, pod) || aff_opaque(c, pod);  // required (anti-)affinity the encoded set cannot read
   };
-  for (int32_t i = 0; i < nc; ++i) {
+  for (int32_t i = 0; i < nc; ++i)
     if (cands->cand_pod_off[i + 1] < cands->cand_pod_off[i]) {
       *err = "cand_pod_off not monotone";
       return SR_ERR_INVALID_ARG;
     }
-    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j)
-      if (cands->cand_pods[j] < 0 || cands->cand_pods[j] >= P.n) {
-        *err = "candidate pod index out of range";
-        return SR_ERR_INVALID_ARG;
-      }
-  }
   std::vector<uint8_t>& cand_ports = C.scratch.cand_ports;  // the candidate's pods ask for host ports
   cand_ports.assign(static_cast<size_t>(nc), 0);
+  std::atomic<bool> bad_index{false};
   auto pass1 = [&](size_t lo, size_t hi) {
+    bool bad = false;
+    for (size_t i = lo; i < hi; ++i)
+      for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j)
+        bad = bad || cands->cand_pods[j] < 0 || cands->cand_pods[j] >= P.n;
+    if (bad) {
+      bad_index.store(true, std::memory_order_relaxed);
+      return;
+    }
     for (size_t i = lo; i < hi; ++i) {
       const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
       if (e == b) {
@@ -548,6 +551,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   };
   if (w->n_input_pods > kSerialPods) parallel_for(static_cast<size_t>(nc), 64, pass1);
   else pass1(0, static_cast<size_t>(nc));
+  if (bad_index.load(std::memory_order_relaxed)) {
+    *err = "candidate pod index out of range";
+    return SR_ERR_INVALID_ARG;
+  }
   phase(5);
 
   // ---- required pod anti-affinity: static node sets, state-bit pairs and
@@ -733,9 +740,17 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   if (chunk_shard.size() < n_chunks * kSpecShards) chunk_shard.resize(n_chunks * kSpecShards);
   pfor(n_chunks, 1, [&](size_t lo, size_t hi) {
     for (size_t ch = lo; ch < hi; ++ch) {
-      std::vector<int32_t>& buf = spec_words[ch];
+      // fill stack-held vectors (swapped in and out): the vector headers in
+      // spec_words / chunk_shard share cache lines with the neighbouring
+      // chunks' headers, which other threads update
+      std::vector<int32_t> buf;
+      buf.swap(spec_words[ch]);
       buf.clear();
-      for (size_t sh = 0; sh < kSpecShards; ++sh) chunk_shard[ch * kSpecShards + sh].clear();
+      std::vector<int32_t> mine[kSpecShards];
+      for (size_t sh = 0; sh < kSpecShards; ++sh) {
+        mine[sh].swap(chunk_shard[ch * kSpecShards + sh]);
+        mine[sh].clear();
+      }
       const size_t q1 = std::min(static_cast<size_t>(na), (ch + 1) * kChunk);
       for (size_t q = ch * kChunk; q < q1; ++q) {
         const size_t b0 = buf.size();
@@ -747,8 +762,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         spec_hash[q] = h;
         const size_t sh = static_cast<size_t>(((h >> 32) * kSpecShards) >> 32);
         spec_shard[q] = static_cast<uint8_t>(sh);
-        chunk_shard[ch * kSpecShards + sh].push_back(static_cast<int32_t>(q));
+        mine[sh].push_back(static_cast<int32_t>(q));
       }
+      buf.swap(spec_words[ch]);
+      for (size_t sh = 0; sh < kSpecShards; ++sh) mine[sh].swap(chunk_shard[ch * kSpecShards + sh]);
     }
   });
   phase(9);
@@ -1173,6 +1190,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   // per pod: requests, records and the lower-bound position of each request
   // among the node values (stored in pod_rows[1..3] for now)
   pfor(static_cast<size_t>(na), 2048, [&](size_t lo, size_t hi) {
+    bool chunk_dead = false;  // one shared store per chunk, not per pod
     for (size_t q = lo; q < hi; ++q) {
       const int32_t pod = active_pod[q];
       const int64_t rc = P.req_milli_cpu[pod], rm = P.req_memory[pod], re = P.req_ephemeral[pod];
@@ -1197,9 +1215,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
       if (dead) {
         r[0] = -1;  // the empty class, appended below
-        any_dead.store(true, std::memory_order_relaxed);
+        chunk_dead = true;
       }
     }
+    if (chunk_dead) any_dead.store(true, std::memory_order_relaxed);
   });
   phase(10);
   if (any_dead.load(std::memory_order_relaxed)) {

@@ -52,6 +52,38 @@ __device__ __forceinline__ int wave_min(int v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
+// Inclusive prefix sum / OR over the 64 lanes: DPP row shifts within each row
+// of 16, then the row totals broadcast into the rows above (no LDS).
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint64_t dpp_shifted(uint64_t v) {
+  const uint32_t lo = static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(v)), CTRL, ROW_MASK, 0xf, true));
+  const uint32_t hi = static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(v >> 32)), CTRL, ROW_MASK, 0xf, true));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+__device__ __forceinline__ int64_t scan_add(int64_t x) {
+  uint64_t v = static_cast<uint64_t>(x);
+  v += dpp_shifted<0x111>(v);       // row_shr:1
+  v += dpp_shifted<0x112>(v);       // row_shr:2
+  v += dpp_shifted<0x114>(v);       // row_shr:4
+  v += dpp_shifted<0x118>(v);       // row_shr:8
+  v += dpp_shifted<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v += dpp_shifted<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  return static_cast<int64_t>(v);
+}
+// OR of the lanes below (exclusive): shift up one lane (wave_shr:1), then scan
+__device__ __forceinline__ uint64_t scan_or_excl(uint64_t v) {
+  v = dpp_shifted<0x138>(v);
+  v |= dpp_shifted<0x111>(v);
+  v |= dpp_shifted<0x112>(v);
+  v |= dpp_shifted<0x114>(v);
+  v |= dpp_shifted<0x118>(v);
+  v |= dpp_shifted<0x142, 0xa>(v);
+  v |= dpp_shifted<0x143, 0xc>(v);
+  return v;
+}
+
 // K0: bitmask rows.  Blocks [0, s_blocks): S rows, kSClasses classes per
 // wave, lanes = words; blocks after: T rows, lanes = rows.
 constexpr int kSClasses = 2;  // S rows per wave: their atom loads are in flight together
@@ -648,6 +680,59 @@ __device__ __forceinline__ uint32_t from_lane(uint32_t v, int src) {
   return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(v)));
 }
 
+// All pods `P` (lanes, pod order) that point at one node, placed in one pass:
+// with inclusive prefix sums of their requests, pod j fits iff every pod of P
+// below it fits and the node's free capacity covers the prefix through j, so
+// the first pod that fails ends a run of placements.  Its request leaves the
+// prefix of the pods above it and the pass repeats from there: one round per
+// failing pod instead of one per placement (NodeResourcesFit's per-resource
+// compare, the pod-count limit and the NodePorts / anti-affinity state bits,
+// pod by pod as ClusterSnapshot.AddPod would see them).
+__device__ __forceinline__ uint64_t place_run(uint64_t P, int lane, int64_t rc, int64_t rm, int64_t re, uint64_t pm,
+                                              uint64_t sb, uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
+                                              uint64_t& ports, int& left) {
+  if (left < 1) return 0;
+  const bool in = (P >> lane) & 1;
+  int64_t ic = scan_add(in ? rc : 0), im = scan_add(in ? rm : 0), ie = 0;
+  const bool need_e = ballot(in && re != 0) != 0;  // ephemeral requests are rare
+  if (need_e) ie = scan_add(in ? re : 0);
+  const bool need_or = ballot(in && sb != 0) != 0;  // so are ports and anti-affinity bits
+  uint64_t xo = need_or ? scan_or_excl(in ? sb : 0ull) : 0ull;
+  uint64_t Q = P;  // pods contributing to the prefixes: placed or still pending
+  uint64_t placed = 0;
+  for (;;) {
+    const int below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(Q >> 32),
+                                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(Q), 0));
+    const uint64_t room = ballot(below < left);
+    const uint64_t ok = room & (zm | (ballot(ic <= cpu) & ballot(im <= mem) & ballot(ie <= eph))) &
+                        ballot((pm & (ports | xo)) == 0);
+    const uint64_t bad = P & ~ok;
+    if (bad == 0) {
+      placed |= P;
+      break;
+    }
+    const int j = __builtin_ctzll(bad);
+    placed |= P & ((1ull << j) - 1);
+    P &= j == 63 ? 0ull : ~0ull << (j + 1);
+    Q &= ~(1ull << j);
+    if (P == 0 || ((room >> j) & 1) == 0) break;  // the node is full: every pod above fails too
+    const bool after = lane > j;
+    ic -= after ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), j)) : 0;
+    im -= after ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), j)) : 0;
+    if (need_e) ie -= after ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), j)) : 0;
+    if (need_or && readlane64(sb, j) != 0) xo = scan_or_excl(((Q >> lane) & 1) ? sb : 0ull);
+  }
+  if (placed != 0) {
+    const int last = 63 - __builtin_clzll(placed);
+    cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(ic), last));
+    mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(im), last));
+    if (need_e) eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(ie), last));
+    if (need_or) ports |= readlane64(xo, last) | readlane64(sb, last);
+    left -= __builtin_popcountll(placed);
+  }
+  return placed;
+}
+
 template <int G, bool PROF>
 __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __restrict__ F, const int p0,
                                               const int np, int& status, K2Stats& st, uint32_t& nbytes) {
@@ -853,7 +938,11 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     for (int g = 0; g < G; ++g) {  // groups in pod order: the state flows from one to the next
       const uint64_t cand = ballot(((act[g] >> lane) & 1) && ptr[g] == n);
       uint64_t placed = 0;
-      if (cand != 0) {  // wave-uniform
+      if (cand != 0 && __builtin_popcountll(cand) >= w.k2_scan_min) {  // wave-uniform
+        placed = place_run(cand, lane, rc[g], rm[g], re[g], pm[g], swap_pairs(pm[g], w.swap_mask), zm[g], cpu, mem,
+                           eph, ports, left);
+        placements += __builtin_popcountll(placed);
+      } else if (cand != 0) {  // wave-uniform
         // NodeResourcesFit + NodePorts / anti-affinity state, pods in order.
         // One exit branch per placement: the checks are unconditional (lane
         // masks straight from the compares) and the pod-count limit clears
