@@ -680,57 +680,92 @@ __device__ __forceinline__ uint32_t from_lane(uint32_t v, int src) {
   return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(v)));
 }
 
-// All pods `P` (lanes, pod order) that point at one node, placed in one pass:
-// with inclusive prefix sums of their requests, pod j fits iff every pod of P
-// below it fits and the node's free capacity covers the prefix through j, so
-// the first pod that fails ends a run of placements.  Its request leaves the
-// prefix of the pods above it and the pass repeats from there: one round per
-// failing pod instead of one per placement (NodeResourcesFit's per-resource
-// compare, the pod-count limit and the NodePorts / anti-affinity state bits,
-// pod by pod as ClusterSnapshot.AddPod would see them).
-__device__ __forceinline__ uint64_t place_run(uint64_t P, int lane, int64_t rc, int64_t rm, int64_t re, uint64_t pm,
-                                              uint64_t sb, uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
-                                              uint64_t& ports, int& left) {
-  if (left < 1) return 0;
-  const bool in = (P >> lane) & 1;
-  int64_t ic = scan_add(in ? rc : 0), im = scan_add(in ? rm : 0), ie = 0;
-  const bool need_e = ballot(in && re != 0) != 0;  // ephemeral requests are rare
-  if (need_e) ie = scan_add(in ? re : 0);
-  const bool need_or = ballot(in && sb != 0) != 0;  // so are ports and anti-affinity bits
-  uint64_t xo = need_or ? scan_or_excl(in ? sb : 0ull) : 0ull;
-  uint64_t Q = P;  // pods contributing to the prefixes: placed or still pending
+// Pods `P` (lanes, in pod order) whose pointer is node n, placed on n one by
+// one as ClusterSnapshot.AddPod would see them: NodeResourcesFit's compare per
+// resource, the pod-count limit, and the NodePorts / anti-affinity state bits.
+// E: some pod of P asks for ephemeral storage; O: some pod of P sets or
+// conflicts with state bits.  Without them those compares are uniform (a zero
+// request against the node's free value) and their state never changes.
+template <bool E, bool O>
+__device__ __forceinline__ uint64_t place_seq(uint64_t P, int lane, int64_t rc, int64_t rm, int64_t re, uint64_t pm,
+                                              uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
+                                              uint64_t& ports, int& left, uint64_t swap_mask) {
   uint64_t placed = 0;
+  uint64_t rest = left >= 1 ? P : 0ull;
+  // One exit branch per placement: the checks are unconditional (lane masks
+  // straight from the compares); pods below the one placed that did not fit
+  // failed at n.
   for (;;) {
-    const int below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(Q >> 32),
-                                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(Q), 0));
-    const uint64_t room = ballot(below < left);
-    const uint64_t ok = room & (zm | (ballot(ic <= cpu) & ballot(im <= mem) & ballot(ie <= eph))) &
-                        ballot((pm & (ports | xo)) == 0);
-    const uint64_t bad = P & ~ok;
-    if (bad == 0) {
-      placed |= P;
-      break;
-    }
-    const int j = __builtin_ctzll(bad);
-    placed |= P & ((1ull << j) - 1);
-    P &= j == 63 ? 0ull : ~0ull << (j + 1);
-    Q &= ~(1ull << j);
-    if (P == 0 || ((room >> j) & 1) == 0) break;  // the node is full: every pod above fails too
-    const bool after = lane > j;
-    ic -= after ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), j)) : 0;
-    im -= after ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), j)) : 0;
-    if (need_e) ie -= after ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), j)) : 0;
-    if (need_or && readlane64(sb, j) != 0) xo = scan_or_excl(((Q >> lane) & 1) ? sb : 0ull);
-  }
-  if (placed != 0) {
-    const int last = 63 - __builtin_clzll(placed);
-    cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(ic), last));
-    mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(im), last));
-    if (need_e) eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(ie), last));
-    if (need_or) ports |= readlane64(xo, last) | readlane64(sb, last);
-    left -= __builtin_popcountll(placed);
+    uint64_t res = ballot(rc <= cpu) & ballot(rm <= mem);
+    res &= E ? ballot(re <= eph) : (eph >= 0 ? ~0ull : 0ull);
+    uint64_t fm = rest & (zm | res);
+    if (O) fm &= ballot((pm & ports) == 0);
+    if (fm == 0) break;
+    const int j = __builtin_ctzll(fm);
+    placed |= 1ull << j;
+    rest &= j == 63 ? 0ull : ~0ull << (j + 1);
+    cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), j));
+    mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), j));
+    if (E) eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), j));
+    if (O) ports |= swap_pairs(readlane64(pm, j), swap_mask);  // the bits it sets
+    left -= 1;
+    rest = left >= 1 ? rest : 0ull;
   }
   return placed;
+}
+
+// The same placement by runs: with inclusive prefix sums of the requests of P,
+// every pod below the first one that fails fits (each against the node with
+// all pods before it placed), so that run is placed at once.  The first
+// failing pod then fails on its own, and so does every pod of P that does not
+// fit the node after the run: all of them are dropped before the next pass.
+// One pass per run of placements instead of one round per placement.
+template <bool E, bool O>
+__device__ __forceinline__ uint64_t place_runs(uint64_t P, int lane, int64_t rc, int64_t rm, int64_t re, uint64_t pm,
+                                               uint64_t sb, uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
+                                               uint64_t& ports, int& left) {
+  uint64_t placed = 0;
+  while (P != 0 && left >= 1) {
+    const bool in = (P >> lane) & 1;
+    const int64_t ic = scan_add(in ? rc : 0), im = scan_add(in ? rm : 0);
+    const int64_t ie = E ? scan_add(in ? re : 0) : 0;
+    const uint64_t xo = O ? scan_or_excl(in ? sb : 0ull) : 0ull;
+    const int below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(P >> 32),
+                                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(P), 0));
+    uint64_t res = ballot(ic <= cpu) & ballot(im <= mem);
+    res &= E ? ballot(ie <= eph) : (eph >= 0 ? ~0ull : 0ull);
+    uint64_t ok = ballot(below < left) & (zm | res);
+    if (O) ok &= ballot((pm & (ports | xo)) == 0);
+    const uint64_t bad = P & ~ok;
+    const uint64_t run = bad == 0 ? P : P & ((1ull << __builtin_ctzll(bad)) - 1);
+    if (run != 0) {
+      const int last = 63 - __builtin_clzll(run);
+      cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(ic), last));
+      mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(im), last));
+      if (E) eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(ie), last));
+      if (O) ports |= readlane64(xo, last) | readlane64(sb, last);
+      left -= __builtin_popcountll(run);
+      placed |= run;
+    }
+    if (bad == 0) break;
+    P &= ~run;
+    // pods that do not fit the node as it is now fail whatever comes after
+    uint64_t alone = ballot(rc <= cpu) & ballot(rm <= mem);
+    alone &= E ? ballot(re <= eph) : (eph >= 0 ? ~0ull : 0ull);
+    alone = zm | alone;
+    if (O) alone &= ballot((pm & ports) == 0);
+    P &= alone;
+  }
+  return placed;
+}
+
+template <bool E, bool O>
+__device__ __forceinline__ uint64_t place_at(const DevWorkload& w, uint64_t P, int lane, int64_t rc, int64_t rm,
+                                             int64_t re, uint64_t pm, uint64_t zm, int64_t& cpu, int64_t& mem,
+                                             int64_t& eph, uint64_t& ports, int& left) {
+  if (__builtin_popcountll(P) >= w.k2_scan_min)
+    return place_runs<E, O>(P, lane, rc, rm, re, pm, swap_pairs(pm, w.swap_mask), zm, cpu, mem, eph, ports, left);
+  return place_seq<E, O>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
 }
 
 template <int G, bool PROF>
@@ -938,31 +973,17 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     for (int g = 0; g < G; ++g) {  // groups in pod order: the state flows from one to the next
       const uint64_t cand = ballot(((act[g] >> lane) & 1) && ptr[g] == n);
       uint64_t placed = 0;
-      if (cand != 0 && __builtin_popcountll(cand) >= w.k2_scan_min) {  // wave-uniform
-        placed = place_run(cand, lane, rc[g], rm[g], re[g], pm[g], swap_pairs(pm[g], w.swap_mask), zm[g], cpu, mem,
-                           eph, ports, left);
+      if (cand != 0) {  // wave-uniform
+        const bool E = (ballot(re[g] != 0) & cand) != 0;
+        const bool O = (ballot(pm[g] != 0) & cand) != 0;
+#define SR_PLACE_AT(E_, O_) \
+  place_at<E_, O_>(w, cand, lane, rc[g], rm[g], re[g], pm[g], zm[g], cpu, mem, eph, ports, left)
+        if (E && O) placed = SR_PLACE_AT(true, true);
+        else if (E) placed = SR_PLACE_AT(true, false);
+        else if (O) placed = SR_PLACE_AT(false, true);
+        else placed = SR_PLACE_AT(false, false);
+#undef SR_PLACE_AT
         placements += __builtin_popcountll(placed);
-      } else if (cand != 0) {  // wave-uniform
-        // NodeResourcesFit + NodePorts / anti-affinity state, pods in order.
-        // One exit branch per placement: the checks are unconditional (lane
-        // masks straight from the compares) and the pod-count limit clears
-        // `rest` by a select.
-        uint64_t rest = left >= 1 ? cand : 0ull;
-        for (;;) {
-          uint64_t fm = rest & (zm[g] | (ballot(rc[g] <= cpu) & ballot(rm[g] <= mem) & ballot(re[g] <= eph)));
-          fm &= ballot((pm[g] & ports) == 0);
-          if (fm == 0) break;
-          const int j = __builtin_ctzll(fm);
-          placed |= 1ull << j;
-          rest &= ~((2ull << j) - 1);  // pods below j that did not fit failed at n
-          cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc[g]), j));
-          mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm[g]), j));
-          eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(re[g]), j));
-          ports |= swap_pairs(readlane64(pm[g], j), w.swap_mask);  // the bits it sets
-          left -= 1;
-          rest = left >= 1 ? rest : 0ull;
-          ++placements;
-        }
       }
       if ((placed >> lane) & 1) node[g] = n;
       act[g] &= ~placed;
