@@ -800,6 +800,25 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     const uint64_t e = ballot(64 * g + lane < np && static_cast<uint32_t>(r01[g]) == w.s_empty_off);
     if (e != 0) dead = min(dead, 64 * g + __builtin_ctzll(e));
   }
+  // node records of window 0 (spot nodes [0, 64)), where first fit usually
+  // lands: in flight together with the F heads below
+  int wcur = -1;  // register window: lane i holds the base record of node 64 * wcur + i
+  int64_t ncpu = 0, nmem = 0, neph = 0;
+  uint64_t nport = 0;
+  int nleft = 0;
+#ifndef SR_K2_PREFETCH_W0
+#define SR_K2_PREFETCH_W0 1
+#endif
+  if (SR_K2_PREFETCH_W0 && dead > 0) {
+    const uint64_t* nr = w.node_rec + static_cast<size_t>(lane) * 8;
+    ncpu = static_cast<int64_t>(nr[0]);
+    nmem = static_cast<int64_t>(nr[1]);
+    neph = static_cast<int64_t>(nr[2]);
+    nport = nr[3];
+    nleft = static_cast<int>(static_cast<int64_t>(nr[4]));
+    wcur = 0;
+    nbytes += 64u * 40u;
+  }
   uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
   // bytes moved (algorithmic, wave-uniform): pod records, F heads of pods
   // [0, dead) (4 rows x min(Wp, kNH) words), 64-node record windows (5 words
@@ -811,9 +830,10 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   // 8 * kPB pods)
   {
 #ifndef SR_K2_PROLOGUE_BATCHES
-#define SR_K2_PROLOGUE_BATCHES 4
+#define SR_K2_PROLOGUE_BATCHES 0
 #endif
-    constexpr int kPB = SR_K2_PROLOGUE_BATCHES;
+    // up to 64 pods in one round trip (G = 1), 32 per round beyond
+    constexpr int kPB = SR_K2_PROLOGUE_BATCHES > 0 ? SR_K2_PROLOGUE_BATCHES : (G == 1 ? 8 : 4);
     const int sub = lane >> 3, wd = lane & 7;
     const bool wv = wd < Wp;
 #pragma unroll
@@ -882,11 +902,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     cyc_t = t;
   }
 
-  int wcur = -1;  // register window: lane i holds the base record of node 64 * wcur + i
-  int64_t ncpu = 0, nmem = 0, neph = 0;
-  uint64_t nport = 0;
-  int nleft = 0;
-  int visits = 0, placements = 0, windows = 0;
+  int visits = 0, placements = 0, windows = wcur + 1;
   while (any != 0) {
     int mine = INT_MAX;
 #pragma unroll

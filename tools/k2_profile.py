@@ -13,7 +13,8 @@ Each sr_plan_run appends {int64 n_cand, int64 n_k0} + n_cand x 16 u64 (K2)
 Node-order waves ([5] == 2) reuse the fields: [6] placements, [7] visits |
 windows << 32, [8] prologue (F heads) cycles, [9] min + window + node
 state, [10] placement, [11] pointer moves (+ far resolution).
-Only the last run in the file is summarised (earlier ones are warmup)."""
+The last of the widest runs in the file is summarised (earlier ones are
+warmup; narrower ones are prefix batches of sr_plan_first)."""
 import sys
 
 import numpy as np
@@ -31,8 +32,9 @@ def load(path):
 
 def main():
     runs, k0s = load(sys.argv[1])
-    r = runs[-1].astype(np.int64)
-    k0 = k0s[-1].astype(np.int64)
+    last_run = max(range(len(runs)), key=lambda i: (len(runs[i]), i))
+    r = runs[last_run].astype(np.int64)
+    k0 = k0s[last_run].astype(np.int64)
     k0 = k0[k0[:, 0] > 0]
     t0 = r[:, 0].min()
     if len(k0):
@@ -84,7 +86,7 @@ def main():
     st = max(1, (steps[~nodeo] if (~nodeo).any() else steps).sum())
     print("cycles/step by section a,b,c,d,spec-wait:", " ".join("%.0f" % (x / st) for x in tot))
     last = np.argsort(-end)[:8]
-    full = runs[-1].astype(np.int64)
+    full = runs[last_run].astype(np.int64)
     print("latest-ending waves: wave start_us dur_us steps mode | visits placements windows | "
           "cycles: prologue min+state placement moves")
     for c in last:
