@@ -759,6 +759,9 @@ __device__ __forceinline__ uint64_t place_runs(uint64_t P, int lane, int64_t rc,
   return placed;
 }
 
+#ifndef SR_K2_LEAN
+#define SR_K2_LEAN 0
+#endif
 // The same placement with the pods' values read into scalar registers one
 // pod at a time: the capacity chain runs on the scalar unit (no vector compare
 // -> mask -> lane read round trip per pod).
@@ -794,7 +797,7 @@ __device__ __forceinline__ uint64_t place_at(const DevWorkload& w, uint64_t P, i
                                              int64_t& eph, uint64_t& ports, int& left) {
   if (__builtin_popcountll(P) >= w.k2_scan_min)
     return place_runs<E, O>(P, lane, rc, rm, re, pm, swap_pairs(pm, w.swap_mask), zm, cpu, mem, eph, ports, left);
-  if (w.k2_place_scalar) return place_scalar<E, O>(P, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
+  if (!SR_K2_LEAN && w.k2_place_scalar) return place_scalar<E, O>(P, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
   return place_seq<E, O>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
 }
 
@@ -1024,7 +1027,10 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         const bool O = (ballot(pm[g] != 0) & cand) != 0;
 #define SR_PLACE_AT(E_, O_) \
   place_at<E_, O_>(w, cand, lane, rc[g], rm[g], re[g], pm[g], zm[g], cpu, mem, eph, ports, left)
-        if (E && O) placed = SR_PLACE_AT(true, true);
+#ifndef SR_K2_LEAN
+#define SR_K2_LEAN 0
+#endif
+        if (SR_K2_LEAN || (E && O)) placed = SR_PLACE_AT(true, true);
         else if (E) placed = SR_PLACE_AT(true, false);
         else if (O) placed = SR_PLACE_AT(false, true);
         else placed = SR_PLACE_AT(false, false);
