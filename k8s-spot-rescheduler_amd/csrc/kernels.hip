@@ -1144,15 +1144,13 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
     if (placed < 0) placed = k2_run<8, CH, PROF>(w, L, p0, np, status, st, nbytes);  // > 64 distinct nodes
     for (int i = lane; i < np; i += 64) w.out_node[p0 + i] = i < placed ? L.omap[i] : -1;
   }
-  bool improved = false;  // this candidate became the first drainable one so far
   if (lane == 0) {
     w.out_status[ci] = status;
     w.out_bytes[ci] = nbytes;
     // packed (global candidate << 32 | local candidate): min = first drainable
-    if (status < 0) {
-      const unsigned long long mine = (static_cast<unsigned long long>(g) << 32) | static_cast<unsigned>(ci);
-      improved = atomicMin(reinterpret_cast<unsigned long long*>(w.d_min), mine) > mine;
-    }
+    if (status < 0)
+      atomicMin(reinterpret_cast<unsigned long long*>(w.d_min),
+                (static_cast<unsigned long long>(g) << 32) | static_cast<unsigned>(ci));
     if (PROF) {
       uint64_t* pr = w.prof + static_cast<size_t>(ci) * 16;
       pr[0] = t_start;
@@ -1170,12 +1168,11 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
     }
   }
   if (w.fuse_winner) {
-    // the last wave to finish writes the winner (K3's work, without a launch).
-    // Only a wave that lowered d_min can be the winner: it releases its
-    // mapping before counting itself done (a release per wave costs an L2
-    // write-back each), and the last wave acquires before reading it.
+    // the last wave to finish writes the winner (K3's work, without a launch):
+    // its own results are released before it counts itself done, and the
+    // last one acquires everyone's before reading them
     unsigned* done = reinterpret_cast<unsigned*>(w.d_min + 4);
-    if (__builtin_amdgcn_readfirstlane(improved ? 1 : 0)) __threadfence();
+    __threadfence();
     unsigned before = 0;
     if (lane == 0) before = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     before = __builtin_amdgcn_readfirstlane(before);
