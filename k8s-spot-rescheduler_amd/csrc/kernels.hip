@@ -151,7 +151,6 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
     unsigned long long* dm = reinterpret_cast<unsigned long long*>(w.d_min);
     dm[0] = ~0ull;
     dm[1] = local_first_fallback < 0 ? ~0ull : static_cast<unsigned long long>(local_first_fallback) << 32;
-    dm[2] = 0;  // K2's finished-wave count (fused winner)
   }
   const size_t Wp = static_cast<size_t>(w.Wp);
   if (static_cast<int>(blockIdx.x) < s_blocks) {
@@ -1165,21 +1164,6 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
       pr[9] = st.cyc_b;
       pr[10] = st.cyc_c;
       pr[11] = st.cyc_d;
-    }
-  }
-  if (w.fuse_winner) {
-    // the last wave to finish writes the winner (K3's work, without a launch):
-    // its own results are released before it counts itself done, and the
-    // last one acquires everyone's before reading them
-    unsigned* done = reinterpret_cast<unsigned*>(w.d_min + 4);
-    __threadfence();
-    unsigned before = 0;
-    if (lane == 0) before = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    before = __builtin_amdgcn_readfirstlane(before);
-    if (before == static_cast<unsigned>(n_list) - 1) {
-      __threadfence();
-      write_winner(w);
-      if (lane == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

@@ -44,13 +44,11 @@ struct DevWorkload {
   int32_t* out_node;   // [n_pods] spot position or -1
   int32_t* out_status; // [n_cand]
   uint32_t* out_bytes; // [n_cand] bytes K2 moved for the candidate (the roofline's algorithmic bytes)
-  int32_t* d_min;      // 2 x u64 packed {global << 32 | local}: first ok, first fallback (~0 = none);
-                       // then K2's finished-wave count (u32, reset by K0 and by the last wave)
+  int32_t* d_min;      // 2 x u64 packed {global << 32 | local}: first ok, first fallback (~0 = none)
   uint64_t* result;    // mapped host memory [kResultHeader + max pods] words seq << 32 | value:
                        //   {winner, local, npods, first_fallback, -, -, -, -, mapping...}
   uint32_t seq;        // run sequence number: the tag of every result word (wraps)
   int32_t k2_scan_min; // node visits with at least this many pods use the prefix-sum pass (place_run)
-  int32_t fuse_winner;  // 1: K2's last wave writes the winner (no K3 launch; single rank)
   int32_t k2_place_scalar;  // 1: smaller node visits placed pod by pod on the scalar unit, 0: by vector masks
   int32_t k2_mode;     // 0: node-order first fit where it applies (<= 64 pods, <= 64-word rows);
                        // 1: pod order everywhere (SR_K2_MODE=1, A/B measurement)

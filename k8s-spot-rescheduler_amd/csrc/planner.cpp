@@ -64,7 +64,6 @@ struct sr_ctx {
   int nranks = 1, rank = 0;
   FILE* prof_file = nullptr;  // SR_K2_PROFILE: per-wave K2 records appended per run
   int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
-  int32_t fuse_winner = 1;      // SR_FUSE_WINNER=0: K3 launched after K2 on one rank too (A/B)
   int32_t k2_place_scalar = 1;  // SR_K2_SCALAR=0: vector-mask placement for small node visits (A/B)
   int32_t k2_scan_min = 2;    // SR_K2_SCAN_MIN: smallest node visit placed by prefix sums (65: never)
 };
@@ -317,24 +316,21 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     if (_st != SR_OK) return _st;             \
   } while (0)
   PAIR(0, e0a, e0b);
-  d.fuse_winner = ctx->fuse_winner && !collective && d.n_list > 0 ? 1 : 0;
   HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
   PAIR(1, e1a, e1b);
   HIP_TRY(ctx, sr::launch_placement(d, s, e1a, e1b));
-  if (!d.fuse_winner) {  // else K2's last wave wrote the winner
-    PAIR(2, e2a, e2b);
-    if (collective) {
-      if (e2a) HIP_TRY(ctx, hipEventRecord(e2a, s));
-      ncclResult_t r = ncclAllReduce(d.d_min, d.d_min, 2, ncclUint64, ncclMin, ctx->comm, s);
-      if (r != ncclSuccess) {
-        ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
-        return SR_ERR_RCCL;
-      }
-      HIP_TRY(ctx, sr::launch_winner(d, s));
-      if (e2b) HIP_TRY(ctx, hipEventRecord(e2b, s));
-    } else {
-      HIP_TRY(ctx, sr::launch_winner(d, s, e2a, e2b));
+  PAIR(2, e2a, e2b);
+  if (collective) {
+    if (e2a) HIP_TRY(ctx, hipEventRecord(e2a, s));
+    ncclResult_t r = ncclAllReduce(d.d_min, d.d_min, 2, ncclUint64, ncclMin, ctx->comm, s);
+    if (r != ncclSuccess) {
+      ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+      return SR_ERR_RCCL;
     }
+    HIP_TRY(ctx, sr::launch_winner(d, s));
+    if (e2b) HIP_TRY(ctx, hipEventRecord(e2b, s));
+  } else {
+    HIP_TRY(ctx, sr::launch_winner(d, s, e2a, e2b));
   }
 #undef PAIR
   if (timing) ctx->t.n_runs += 1;
@@ -457,7 +453,6 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   }
   if (const char* path = std::getenv("SR_K2_PROFILE")) ctx->prof_file = std::fopen(path, "ab");
   if (const char* m = std::getenv("SR_K2_MODE")) ctx->k2_mode = std::atoi(m) == 1 ? 1 : 0;
-  if (const char* m = std::getenv("SR_FUSE_WINNER")) ctx->fuse_winner = std::atoi(m) != 0 ? 1 : 0;
   if (const char* m = std::getenv("SR_K2_SCALAR")) ctx->k2_place_scalar = std::atoi(m) != 0 ? 1 : 0;
   if (const char* m = std::getenv("SR_K2_SCAN_MIN")) ctx->k2_scan_min = std::max(1, std::atoi(m));
   if (const char* b = std::getenv("SR_PREFIX_BATCH")) ctx->prefix_batch = std::max(1, std::atoi(b));
