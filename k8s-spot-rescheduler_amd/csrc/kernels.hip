@@ -759,45 +759,12 @@ __device__ __forceinline__ uint64_t place_runs(uint64_t P, int lane, int64_t rc,
   return placed;
 }
 
-#ifndef SR_K2_LEAN
-#define SR_K2_LEAN 0
-#endif
-// The same placement with the pods' values read into scalar registers one
-// pod at a time: the capacity chain runs on the scalar unit (no vector compare
-// -> mask -> lane read round trip per pod).
-template <bool E, bool O>
-__device__ __forceinline__ uint64_t place_scalar(uint64_t P, int64_t rc, int64_t rm, int64_t re, uint64_t pm,
-                                                 uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
-                                                 uint64_t& ports, int& left, uint64_t swap_mask) {
-  uint64_t placed = 0;
-  uint64_t rest = P;
-  while (rest != 0 && left >= 1) {
-    const int j = __builtin_ctzll(rest);
-    rest &= rest - 1;
-    const int64_t c = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), j));
-    const int64_t m = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), j));
-    const int64_t e = E ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), j)) : 0;
-    const uint64_t q = O ? readlane64(pm, j) : 0ull;
-    const bool res = ((zm >> j) & 1) != 0 || (c <= cpu && m <= mem && (E ? e <= eph : eph >= 0));
-    if (res && (!O || (q & ports) == 0)) {
-      placed |= 1ull << j;
-      cpu -= c;
-      mem -= m;
-      if (E) eph -= e;
-      if (O) ports |= swap_pairs(q, swap_mask);
-      left -= 1;
-    }
-  }
-  return placed;
-}
-
 template <bool E, bool O>
 __device__ __forceinline__ uint64_t place_at(const DevWorkload& w, uint64_t P, int lane, int64_t rc, int64_t rm,
                                              int64_t re, uint64_t pm, uint64_t zm, int64_t& cpu, int64_t& mem,
                                              int64_t& eph, uint64_t& ports, int& left) {
   if (__builtin_popcountll(P) >= w.k2_scan_min)
     return place_runs<E, O>(P, lane, rc, rm, re, pm, swap_pairs(pm, w.swap_mask), zm, cpu, mem, eph, ports, left);
-  if (!SR_K2_LEAN && w.k2_place_scalar) return place_scalar<E, O>(P, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
   return place_seq<E, O>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
 }
 
@@ -1027,10 +994,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         const bool O = (ballot(pm[g] != 0) & cand) != 0;
 #define SR_PLACE_AT(E_, O_) \
   place_at<E_, O_>(w, cand, lane, rc[g], rm[g], re[g], pm[g], zm[g], cpu, mem, eph, ports, left)
-#ifndef SR_K2_LEAN
-#define SR_K2_LEAN 0
-#endif
-        if (SR_K2_LEAN || (E && O)) placed = SR_PLACE_AT(true, true);
+        if (E && O) placed = SR_PLACE_AT(true, true);
         else if (E) placed = SR_PLACE_AT(true, false);
         else if (O) placed = SR_PLACE_AT(false, true);
         else placed = SR_PLACE_AT(false, false);

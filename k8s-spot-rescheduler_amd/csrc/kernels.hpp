@@ -49,7 +49,6 @@ struct DevWorkload {
                        //   {winner, local, npods, first_fallback, -, -, -, -, mapping...}
   uint32_t seq;        // run sequence number: the tag of every result word (wraps)
   int32_t k2_scan_min; // node visits with at least this many pods use the prefix-sum pass (place_run)
-  int32_t k2_place_scalar;  // 1: smaller node visits placed pod by pod on the scalar unit, 0: by vector masks
   int32_t k2_mode;     // 0: node-order first fit where it applies (<= 64 pods, <= 64-word rows);
                        // 1: pod order everywhere (SR_K2_MODE=1, A/B measurement)
   uint64_t* prof;      // optional [n_cand][16] K2 + [kK0ProfWaves][2] K0 per-wave profile

@@ -64,7 +64,6 @@ struct sr_ctx {
   int nranks = 1, rank = 0;
   FILE* prof_file = nullptr;  // SR_K2_PROFILE: per-wave K2 records appended per run
   int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
-  int32_t k2_place_scalar = 1;  // SR_K2_SCALAR=0: vector-mask placement for small node visits (A/B)
   int32_t k2_scan_min = 2;    // SR_K2_SCAN_MIN: smallest node visit placed by prefix sums (65: never)
 };
 
@@ -217,7 +216,6 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.d_min = static_cast<int32_t*>(ctx->dmin.p);
   d.k2_mode = ctx->k2_mode;
   d.k2_scan_min = ctx->k2_scan_min;
-  d.k2_place_scalar = ctx->k2_place_scalar;
   d.swap_mask = w.swap_mask;
   d.prof = nullptr;
   if (ctx->prof_file) {
@@ -453,7 +451,6 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   }
   if (const char* path = std::getenv("SR_K2_PROFILE")) ctx->prof_file = std::fopen(path, "ab");
   if (const char* m = std::getenv("SR_K2_MODE")) ctx->k2_mode = std::atoi(m) == 1 ? 1 : 0;
-  if (const char* m = std::getenv("SR_K2_SCALAR")) ctx->k2_place_scalar = std::atoi(m) != 0 ? 1 : 0;
   if (const char* m = std::getenv("SR_K2_SCAN_MIN")) ctx->k2_scan_min = std::max(1, std::atoi(m));
   if (const char* b = std::getenv("SR_PREFIX_BATCH")) ctx->prefix_batch = std::max(1, std::atoi(b));
   *out = ctx;
