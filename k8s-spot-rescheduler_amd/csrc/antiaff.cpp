@@ -24,8 +24,12 @@
 //    whose state holds B for its terms or A for the terms selecting it -- the
 //    pair-swapped image of what it sets.  K2 keeps these bits with the
 //    host-port bits; the base snapshot needs none (its conflicts are the
-//    static part).  Interaction through any other key routes the candidate
-//    to the fallback path.
+//    static part).  Interaction through a key whose domains span several
+//    nodes (zone-style) puts the candidate on K2's domain path: each pod
+//    records, per key slot, the earlier pods of its candidate it interacts
+//    with, and the device refuses it the domains those pods were placed in
+//    (DomKeys: <= kDomKeys keys of <= kDomMax domains, <= kDynPods pods;
+//    beyond that the candidate takes the fallback path).
 #include <algorithm>
 #include <climits>
 #include <cstring>
@@ -90,6 +94,37 @@ void anti_term_words(const sr_cluster* c, int32_t owner, int32_t t, std::vector<
     out.erase(std::unique(out.begin() + at + 1, out.end()), out.end());
     out[at] = static_cast<int32_t>(out.size() - at - 1);
   }
+}
+
+int32_t DomKeys::slot(const sr_snapshot* snap, int32_t k) {
+  for (size_t i = 0; i < key.size(); ++i)
+    if (key[i] == k) return static_cast<int32_t>(i);
+  if (key.size() >= static_cast<size_t>(kDomKeys)) return -1;
+  const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
+  std::vector<int32_t> d(static_cast<size_t>(n_spot), -1);
+  std::unordered_map<int32_t, int32_t> id_of;
+  bool local = true;
+  for (int32_t n = 0; n < n_spot; ++n) {
+    const auto& lb = snap->nodes[n].labels;
+    auto it = std::find_if(lb.begin(), lb.end(), [k](const std::pair<int32_t, int32_t>& kv) { return kv.first == k; });
+    if (it == lb.end()) {
+      local = false;
+      continue;
+    }
+    auto ins = id_of.emplace(it->second, static_cast<int32_t>(id_of.size()));
+    if (!ins.second) local = false;
+    d[n] = ins.first->second;
+  }
+  if (local) {
+    for (int32_t n = 0; n < n_spot; ++n) d[n] = n;
+  } else if (id_of.size() > static_cast<size_t>(kDomMax)) {
+    return -1;
+  }
+  key.push_back(k);
+  node_local.push_back(local ? 1 : 0);
+  dom.push_back(std::move(d));
+  n_dom.push_back(local ? n_spot : static_cast<int32_t>(id_of.size()));
+  return static_cast<int32_t>(key.size() - 1);
 }
 
 namespace {
@@ -169,7 +204,7 @@ bool term_selects(const Term& t, const PodMeta& m) {
 }  // namespace
 
 void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
-                  std::vector<int32_t>& status, AntiTerms* out) {
+                  std::vector<int32_t>& status, DomKeys* dk, AntiTerms* out) {
   AntiTerms& at = *out;
   at = AntiTerms{};
   const sr_pod_affinity* PA = c->pod_affinity;
@@ -348,16 +383,18 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
   // ---- interactions inside each candidate: terms one pod has and another
   // pod matches.  Node-local ones get a bit pair of the candidate's own (the
   // state is per candidate; base conflicts are in the F rows already), at most
-  // 32; any other interaction routes the candidate to the fallback path.
+  // 32; the others ("far" terms) put the candidate on the domain path.
   at.pod_bits.assign(static_cast<size_t>(n_flat), 0);
   std::vector<int32_t> pairs(static_cast<size_t>(nc), 0);
+  std::vector<std::vector<int32_t>> far_of(static_cast<size_t>(nc));
   parallel_for(static_cast<size_t>(nc), 16, [&](size_t lo, size_t hi) {
     std::vector<int32_t> nh(static_cast<size_t>(T)), nm(static_cast<size_t>(T)), nb(static_cast<size_t>(T));
-    std::vector<int32_t> pair(static_cast<size_t>(T), -1), touched, need;
+    std::vector<int32_t> pair(static_cast<size_t>(T), -1), touched, need, far;
     for (size_t i = lo; i < hi; ++i) {
       if (status[i] != STATUS_PENDING) continue;
       touched.clear();
       need.clear();
+      far.clear();
       for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
         const std::vector<int32_t>& v = ids[j - base];
         for (size_t k = 0; k < v.size(); ++k) {
@@ -371,20 +408,20 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
           }
         }
       }
-      bool fb = false;
       std::sort(touched.begin(), touched.end());
       for (int32_t t : touched) {
         const bool interacts = nh[t] >= 1 && nm[t] >= 1 && !(nh[t] == 1 && nm[t] == 1 && nb[t] == 1);
         if (interacts) {
-          if (!at.node_local[t]) fb = true;
+          if (!at.node_local[t]) far.push_back(t);
           else need.push_back(t);
         }
         nh[t] = nm[t] = nb[t] = 0;
       }
-      if (fb || need.size() > 32) {
+      if (need.size() > 32 || (!far.empty() && cands->cand_pod_off[i + 1] - cands->cand_pod_off[i] > kDynPods)) {
         status[i] = SR_CAND_FALLBACK;
         continue;
       }
+      if (!far.empty()) far_of[i] = far;
       for (size_t p = 0; p < need.size(); ++p) pair[need[p]] = static_cast<int32_t>(p);
       for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
         uint64_t bits = 0;
@@ -399,6 +436,39 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
     }
   });
   for (int32_t i = 0; i < nc; ++i) at.n_pairs = std::max(at.n_pairs, pairs[i]);
+
+  // ---- domain path: per pod, the earlier pods of its candidate it interacts
+  // with through each far term's key (either has the term and the other one
+  // matches it): the device refuses it the domains they were placed in
+  std::vector<int32_t> fslot;
+  for (int32_t i = 0; i < nc; ++i) {
+    if (far_of[i].empty() || status[i] != STATUS_PENDING) continue;
+    fslot.clear();
+    bool ok = true;
+    for (int32_t t : far_of[i]) {
+      const int32_t sl = dk->slot(snap, terms[t].tk);
+      ok = ok && sl >= 0;
+      fslot.push_back(sl);
+    }
+    if (!ok) {
+      status[i] = SR_CAND_FALLBACK;
+      continue;
+    }
+    if (at.amask.empty()) {
+      at.amask.assign(static_cast<size_t>(n_flat) * kDomKeys, 0);
+      at.cand_dyn.assign(static_cast<size_t>(nc), 0);
+    }
+    at.cand_dyn[i] = 1;
+    const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
+    auto has = [&](int32_t j, int32_t id) { return std::binary_search(ids[j - base].begin(), ids[j - base].end(), id); };
+    for (int32_t q = b + 1; q < e; ++q)
+      for (int32_t p = b; p < q; ++p)
+        for (size_t f = 0; f < far_of[i].size(); ++f) {
+          const int32_t t = far_of[i][f];
+          if ((has(p, t << 1 | 1) && has(q, t << 1)) || (has(q, t << 1 | 1) && has(p, t << 1)))
+            at.amask[static_cast<size_t>(q - base) * kDomKeys + fslot[f]] |= 1ull << (p - b);
+        }
+  }
 
   // ---- CSR of the ids
   for (int32_t j = 0; j < n_flat; ++j) at.pod_off[j + 1] = at.pod_off[j] + static_cast<int32_t>(ids[j].size());
@@ -416,9 +486,12 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
 // of SAT(S) -- or, with map_empty and the pod matching its own terms (the
 // first pod of a self-affine group), a node of KEYS(S).  A candidate in which
 // an earlier pod matches every term of a later pod's set changes that pod's
-// domains while it is planned: it takes the reference path.
+// pair map while it is planned: it takes K2's domain path, where the later
+// pod's class carries KEYS(S) and the device adds, per term, the domains of
+// the earlier matching pods' nodes to the base row (and drops the map-empty
+// exception once one of them sits on a node with a key).
 void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
-                      std::vector<int32_t>& status, AffTerms* out) {
+                      std::vector<int32_t>& status, DomKeys* dk, AffTerms* out) {
   AffTerms& af = *out;
   af = AffTerms{};
   const sr_pod_affinity* PA = c->pod_affinity;
@@ -536,22 +609,65 @@ void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_can
   }
 
   // ---- interactions inside a candidate: an earlier pod matching every term
-  // of a later pod's set
+  // of a later pod's set adds its domains to that pod's pair map while the
+  // candidate is planned: the candidate takes K2's domain path (per pod, the
+  // mask of those earlier pods), or the fallback path beyond its limits
+  std::vector<uint64_t> masks;
   for (int32_t i = 0; i < nc; ++i) {
     if (status[i] != STATUS_PENDING) continue;
     const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
-    bool fb = false;
-    for (int32_t k = b + 1; k < e && !fb; ++k) {
+    masks.assign(static_cast<size_t>(e - b), 0);
+    bool any = false;
+    for (int32_t k = b + 1; k < e; ++k) {
       const int32_t code = af.pod_code[k - base];
       if (code < 0) continue;
-      for (int32_t q = b; q < k && !fb; ++q) {
+      for (int32_t q = b; q < k; ++q) {
         const PodMeta m = meta_of(A, cands->cand_pods[q]);
         bool all = true;
         for (const Term& t : sets[code >> 1]) all = all && term_selects(t, m);
-        fb = all;
+        if (all && q - b < 64) masks[k - b] |= 1ull << (q - b);
+        any = any || all;
       }
     }
-    if (fb) status[i] = SR_CAND_FALLBACK;
+    if (!any) continue;
+    bool ok = e - b <= kDynPods;
+    for (int32_t k = b; k < e && ok; ++k) {
+      if (masks[k - b] == 0) continue;
+      const int32_t set = af.pod_code[k - base] >> 1;
+      ok = sets[set].size() <= static_cast<size_t>(kDynTerms);
+      for (size_t t = 0; t < sets[set].size() && ok; ++t) ok = dk->slot(snap, sets[set][t].tk) >= 0;
+    }
+    if (!ok) {
+      status[i] = SR_CAND_FALLBACK;
+      continue;
+    }
+    if (af.mmask.empty()) {
+      af.mmask.assign(static_cast<size_t>(n_flat), 0);
+      af.cand_dyn.assign(static_cast<size_t>(nc), 0);
+      af.set_dyn.assign(static_cast<size_t>(S), 0);
+      af.set_slots.resize(static_cast<size_t>(S));
+      af.term_rows.resize(static_cast<size_t>(S));
+    }
+    af.cand_dyn[i] = 1;
+    for (int32_t k = b; k < e; ++k) {
+      af.mmask[k - base] = masks[k - b];
+      if (masks[k - b] != 0) af.set_dyn[af.pod_code[k - base] >> 1] = 1;
+    }
+  }
+  // per set planned there: each term's key slot, and its base row (nodes
+  // whose domain of the term's key hosts a snapshot pod of M(S))
+  for (int32_t s = 0; s < static_cast<int32_t>(af.set_dyn.size()); ++s) {
+    if (!af.set_dyn[s]) continue;
+    const size_t nt = sets[s].size();
+    af.set_slots[s].resize(nt);
+    af.term_rows[s].assign(nt * Wp, 0);
+    for (size_t t = 0; t < nt; ++t) {
+      af.set_slots[s][t] = dk->slot(snap, sets[s][t].tk);
+      const std::vector<int32_t>& kv = key_val[set_keys[s][t]];
+      for (int32_t n = 0; n < n_spot; ++n)
+        if (kv[n] != INT_MIN && std::binary_search(vals[s][t].begin(), vals[s][t].end(), kv[n]))
+          af.term_rows[s][t * Wp + (n >> 6)] |= 1ull << (n & 63);
+    }
   }
 }
 

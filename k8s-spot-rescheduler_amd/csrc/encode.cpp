@@ -559,13 +559,17 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
 
   // ---- required pod anti-affinity: static node sets, state-bit pairs and
   // the candidates it sends to the fallback path (antiaff.cpp)
+  DomKeys dk;  // topology keys of the domain path (K2 k2_domain)
   AntiTerms anti;
-  analyse_anti(snap, c, cands, Wp, w->status_host, &anti);
+  analyse_anti(snap, c, cands, Wp, w->status_host, &dk, &anti);
   const int32_t bit_shift = 2 * anti.n_pairs;  // host-port bits sit above the pairs
   // ---- required pod affinity: term sets, their node rows, and the
   // candidates whose pods interact through them (antiaff.cpp)
   AffTerms aff;
-  analyse_affinity(snap, c, cands, Wp, w->status_host, &aff);
+  analyse_affinity(snap, c, cands, Wp, w->status_host, &dk, &aff);
+  // affinity planned on the domain path: the pod's class carries KEYS(S), the
+  // device the rest (an earlier pod of its candidate matches all its terms)
+  auto aff_dyn = [&](int32_t flat) { return !aff.mmask.empty() && aff.mmask[flat - aff.base] != 0; };
 
   // ---- host ports: HostPortInfo.CheckConflict [upstream k8s v1.19
   // framework/types.go] as state bits.  A (protocol, port) group whose active
@@ -846,7 +850,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   std::vector<int32_t>& pod_key_buf = X.pod_key;
   std::vector<int32_t> key_spec;               // keys >= n_spec_ids: spec of the combined key,
   std::vector<std::vector<int32_t>> key_anti;  // ... its anti-affinity term ids
-  std::vector<int32_t> key_aff;                // ... and its affinity code (AffTerms::pod_code)
+  std::vector<int32_t> key_aff;                // ... and its affinity code (AffTerms::pod_code; 1 << 30: domain path)
   if (combos) {
     pod_key_buf.resize(static_cast<size_t>(na));
     WordDict combo;
@@ -859,14 +863,15 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         pod_key_buf[q] = pod_spec[q];
         continue;
       }
+      const int32_t kcode = code < 0 ? code : code | (aff_dyn(active_src[q]) ? 1 << 30 : 0);
       kw.assign(1, pod_spec[q]);
-      kw.push_back(code);
+      kw.push_back(kcode);
       if (n_ids) kw.insert(kw.end(), anti.pod_ids.begin() + anti.pod_off[j], anti.pod_ids.begin() + anti.pod_off[j + 1]);
       bool ins = false;
       const int32_t id = combo.intern(kw, &ins);
       if (ins) {
         key_spec.push_back(pod_spec[q]);
-        key_aff.push_back(code);
+        key_aff.push_back(kcode);
         key_anti.emplace_back(kw.begin() + 2, kw.end());
       }
       pod_key_buf[q] = n_spec_ids + id;
@@ -1032,8 +1037,9 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     // its own terms, nothing otherwise (-2)
     int32_t aff_atom = -1;
     if (k >= n_spec_ids && key_aff[k - n_spec_ids] >= 0) {
-      const int32_t code = key_aff[k - n_spec_ids], set = code >> 1;
-      aff_atom = !aff.map_empty[set] ? A_AFF + 2 * set : (code & 1) ? A_AFF + 2 * set + 1 : -2;
+      const int32_t code = key_aff[k - n_spec_ids] & ~(1 << 30), set = code >> 1;
+      if (key_aff[k - n_spec_ids] & (1 << 30)) aff_atom = A_AFF + 2 * set + 1;  // domain path: the device adds SAT
+      else aff_atom = !aff.map_empty[set] ? A_AFF + 2 * set : (code & 1) ? A_AFF + 2 * set + 1 : -2;
     }
     if (k >= n_spec_ids)
       for (int32_t id : key_anti[k - n_spec_ids]) {
@@ -1061,7 +1067,24 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     }
     key_class[ki] = call_class[id];
   }
-  w->n_atoms = A_COMP + static_cast<int32_t>(comp_sets.size());
+  // domain path rows, named by no class program: each domain of a table key
+  // slot, then each term's base row of the sets planned there
+  const int32_t A_DOM = A_COMP + static_cast<int32_t>(comp_sets.size());
+  int32_t n_dom_rows = 0;
+  for (size_t k = 0; k < dk.key.size(); ++k)
+    if (!dk.node_local[k]) {
+      w->dk_row[k] = A_DOM + n_dom_rows;
+      n_dom_rows += dk.n_dom[k];
+    }
+  const int32_t A_TERM = A_DOM + n_dom_rows;
+  std::vector<int32_t> term_atom(static_cast<size_t>(aff.n_sets), -1);
+  int32_t n_term_rows = 0;
+  for (int32_t s2 = 0; s2 < static_cast<int32_t>(aff.set_dyn.size()); ++s2)
+    if (aff.set_dyn[s2]) {
+      term_atom[s2] = A_TERM + n_term_rows;
+      n_term_rows += static_cast<int32_t>(aff.set_slots[s2].size());
+    }
+  w->n_atoms = A_TERM + n_term_rows;
   phase(3);
 
   // ---- atom rows: pod count (state), requirements and taints (static view,
@@ -1120,6 +1143,48 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       uint64_t any = 0;
       for (size_t j = 0; j < nu; ++j) any |= C.taint_rows[static_cast<size_t>(u[j]) * Wp + i];
       row[i] = A[i] & ~any;
+    }
+  }
+  for (size_t k = 0; k < dk.key.size(); ++k)
+    if (!dk.node_local[k])
+      for (int32_t n = 0; n < n_spot; ++n)
+        if (dk.dom[k][n] >= 0)
+          A[static_cast<size_t>(w->dk_row[k] + dk.dom[k][n]) * Wp + (n >> 6)] |= 1ull << (n & 63);
+  for (int32_t s2 = 0; s2 < static_cast<int32_t>(term_atom.size()); ++s2)
+    if (term_atom[s2] >= 0)
+      std::copy(aff.term_rows[s2].begin(), aff.term_rows[s2].end(), A + static_cast<size_t>(term_atom[s2]) * Wp);
+  // domain path: key slots, sets, and the candidates' pod records
+  const bool dyn_any = !anti.cand_dyn.empty() || !aff.cand_dyn.empty();
+  if (dyn_any) {
+    w->n_dk = static_cast<int32_t>(dk.key.size());
+    for (const auto& d : dk.dom) w->dk_dom.insert(w->dk_dom.end(), d.begin(), d.end());
+    constexpr int32_t kInfo = 2 + 2 * kDynTerms;
+    w->ds_info.assign(static_cast<size_t>(std::max(1, aff.n_sets)) * kInfo, 0);
+    for (int32_t s2 = 0; s2 < static_cast<int32_t>(term_atom.size()); ++s2) {
+      if (term_atom[s2] < 0) continue;
+      int32_t* info = &w->ds_info[static_cast<size_t>(s2) * kInfo];
+      info[0] = static_cast<int32_t>(aff.set_slots[s2].size());
+      info[1] = aff.map_empty[s2];
+      for (int32_t t = 0; t < info[0]; ++t) {
+        info[2 + 2 * t] = aff.set_slots[s2][t];
+        info[3 + 2 * t] = term_atom[s2] + t;
+      }
+    }
+    const int32_t n_act = static_cast<int32_t>(w->cand_src.size());
+    w->dyn_cand.assign(static_cast<size_t>(n_act), -1);
+    for (int32_t k = 0; k < n_act; ++k) {
+      const int32_t i = w->cand_src[k];
+      const bool dyn = (!anti.cand_dyn.empty() && anti.cand_dyn[i]) || (!aff.cand_dyn.empty() && aff.cand_dyn[i]);
+      if (!dyn) continue;
+      w->dyn_cand[k] = static_cast<int32_t>(w->dyn_pod.size() / kDynU64);
+      for (int32_t q = w->cand_off[k]; q < w->cand_off[k + 1]; ++q) {
+        const int32_t j = active_src[q];
+        for (int32_t sl = 0; sl < kDomKeys; ++sl)
+          w->dyn_pod.push_back(anti.amask.empty() ? 0 : anti.amask[static_cast<size_t>(j - anti.base) * kDomKeys + sl]);
+        const uint64_t mm = aff.mmask.empty() ? 0 : aff.mmask[j - aff.base];
+        w->dyn_pod.push_back(mm);
+        w->dyn_pod.push_back(mm != 0 ? static_cast<uint64_t>(aff.pod_code[j - aff.base]) : ~0ull);
+      }
     }
   }
   phase(4);

@@ -115,6 +115,13 @@ void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out);
 // Class descriptor flags.
 enum : int32_t { CLS_AFF_REQUIRED = 1, CLS_IMPOSSIBLE = 2 };
 
+// K2 domain path limits (antiaff.cpp, kernels.hip k2_domain)
+constexpr int kDomKeys = 4;   // key slots per encode
+constexpr int kDomMax = 64;   // domains of a table key (one bit each in a 64-bit mask)
+constexpr int kDynTerms = 4;  // terms of an affinity set planned on the domain path
+constexpr int kDynPods = 64;  // pods of a candidate planned on the domain path
+constexpr int kDynU64 = 6;    // words per pod record (kernels.hpp)
+
 // The encoded workload of one planning call (host copy; uploaded as one
 // arena).  The spot nodes' state (capacity records, free values) lives in the
 // EncoderCache and is uploaded only when it changes.
@@ -157,6 +164,17 @@ struct Workload {
   std::vector<int32_t> cand_src;     // index in the caller's candidate list
   std::vector<int32_t> list;  // [n][4] K2 work list {candidate, first pod, end pod, global}, longest first
   int32_t max_cand_pods = 0;
+  // ---- domain path: candidates whose pods interact through a topology key
+  // with shared domains (antiaff.cpp), planned by K2's k2_domain
+  std::vector<int32_t> dyn_cand;  // [n_active] first record in dyn_pod, -1: other paths (empty: none)
+  std::vector<uint64_t> dyn_pod;  // [pods of those candidates][kDynU64]: anti-affinity masks per
+                                  // key slot (earlier pods of the candidate it interacts with),
+                                  // affinity mask (earlier pods matching every term of its set),
+                                  // set << 1 | matches its own terms (~0: none)
+  int32_t n_dk = 0;               // key slots in use
+  std::vector<int32_t> dk_dom;    // [n_dk][n_spot] domain of each spot node (node-local key: the node), -1 absent
+  int32_t dk_row[kDomKeys] = {-1, -1, -1, -1};  // atom of domain 0 of each table key (-1: node-local key)
+  std::vector<int32_t> ds_info;   // [set][2 + 2 * kDynTerms] {terms, map_empty, (key slot, base atom) per term}
   // ---- host-decided outcomes for every input candidate
   std::vector<int32_t> status_host;  // SR_CAND_EMPTY / SR_CAND_FALLBACK / PENDING
   int32_t first_fallback = -1;       // global index
@@ -170,8 +188,11 @@ struct Workload {
   void reset() {
     t_thr.clear();
     for (auto* v : {&cls_prog_off, &cls_prog, &cls_prog8, &t_dim, &pod_src, &cand_off, &cand_global, &cand_src, &list,
-                    &status_host})
+                    &status_host, &dyn_cand, &dk_dom, &ds_info})
       v->clear();
+    dyn_pod.clear();
+    n_dk = 0;
+    for (int32_t& r : dk_row) r = -1;
     atoms.clear();
     // pod_rows / pod_rec keep their size: the encoder resizes them and writes
     // every field, so a steady-state encode does not zero-fill them first
@@ -275,6 +296,20 @@ constexpr int32_t MAX_CAND_PODS = 512;  // pods per candidate on the device (K2 
 constexpr int32_t MAX_WORDS = 64 * 32; // spot nodes <= 131072
 
 // Required pod anti-affinity of one encode (antiaff.cpp).
+// Topology keys through which the pods of one candidate interact with
+// shared domains (zone-style keys; node-local keys for affinity): K2's domain
+// path tracks, per candidate, the domains its placed pods occupy.
+
+struct DomKeys {
+  std::vector<int32_t> key;               // [slot] label key id
+  std::vector<uint8_t> node_local;        // [slot] every spot node carries it, values pairwise distinct
+  std::vector<std::vector<int32_t>> dom;  // [slot][n_spot] domain id (node-local: the node), -1 absent
+  std::vector<int32_t> n_dom;             // [slot] domains (node-local: n_spot)
+  // The slot of `key`, registered (its domains computed) on first use; -1
+  // when the slots are full or a shared-domain key has more than kDomMax values.
+  int32_t slot(const sr_snapshot* snap, int32_t key);
+};
+
 struct AntiTerms {
   bool active = false;
   int32_t base = 0;                      // cand_pod_off[0]: per-pod arrays are indexed by flat index - base
@@ -286,13 +321,18 @@ struct AntiTerms {
   std::vector<uint64_t> pod_bits;         // [flat candidate pod] state-bit pairs it sets, numbered per
                                          // candidate (A = 2p: it has term p, B = 2p + 1: term p selects it)
   int32_t n_pairs = 0;                   // most pairs any candidate uses (<= 32)
+  // domain path: candidates interacting through shared-domain keys, and per
+  // flat pod of those, the earlier pods of its candidate it interacts with
+  // through each key slot ([flat - base][kDomKeys]; empty: no such candidate)
+  std::vector<uint8_t> cand_dyn;         // [candidate]
+  std::vector<uint64_t> amask;
 };
 
 // Collects the terms of the snapshot's pods and of the pending candidates,
 // builds the static node sets and decides which candidates fall back
 // (status -> SR_CAND_FALLBACK) or need state bits.
 void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
-                  std::vector<int32_t>& status, AntiTerms* out);
+                  std::vector<int32_t>& status, DomKeys* dk, AntiTerms* out);
 
 // Required pod affinity of one encode (antiaff.cpp).
 struct AffTerms {
@@ -302,12 +342,20 @@ struct AffTerms {
   std::vector<uint64_t> sat, keys;  // [set][Wp] SAT(S) (keys and a matching pod in every term's domain), KEYS(S)
   std::vector<uint8_t> map_empty;   // [set] no matching pod on a node carrying any of the keys
   std::vector<int32_t> pod_code;    // [flat - base] -1 none, else 2 * set + (the pod matches its own terms)
+  // domain path: candidates in which an earlier pod matches every term of a
+  // later pod's set; per flat pod the mask of those earlier pods (0: static
+  // SAT(S) is exact); per set planned there, each term's key slot and base row
+  std::vector<uint8_t> cand_dyn;    // [candidate]
+  std::vector<uint64_t> mmask;      // [flat - base] (empty: no such candidate)
+  std::vector<uint8_t> set_dyn;     // [set]
+  std::vector<std::vector<int32_t>> set_slots;     // [set][term] key slot (sets planned dynamically)
+  std::vector<std::vector<uint64_t>> term_rows;    // [set][term * Wp] nodes whose domain hosts a base pod of M(S)
 };
 
 // The sets, their node rows, and the candidates whose pods interact through
 // them (status -> SR_CAND_FALLBACK).
 void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
-                      std::vector<int32_t>& status, AffTerms* out);
+                      std::vector<int32_t>& status, DomKeys* dk, AffTerms* out);
 
 // Builds the workload; returns SR_OK or an error with *err filled.  `cache`
 // carries what the previous calls derived (and is updated).

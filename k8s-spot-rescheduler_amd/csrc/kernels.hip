@@ -1071,6 +1071,204 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   }
 }
 
+// ------------------------------------------------------------ K2, domain path
+// Candidates whose pods interact through a topology key with shared domains
+// (InterPodAffinity across nodes: antiaff.cpp).  Placing a pod changes other
+// nodes' answers -- every node of its domain -- so neither the node-order
+// induction nor the static F rows hold.  Pods in order (canDrainNode), one
+// wave, lanes = row words 64 at a time: F = S & T & T & T & the pod's
+// dynamic row, where the dynamic row
+//  - refuses, per key slot, the domains of the earlier pods it interacts with
+//    through anti-affinity (satisfyExistingPodsAntiAffinity /
+//    satisfyPodAntiAffinity against the pods AddPod put on the snapshot);
+//  - with an affinity set whose terms an earlier pod matches, requires per
+//    term a node in the base row or in the domain of such a pod's node, unless
+//    the pair map is still empty and the pod matches its own terms
+//    (satisfyPodAffinity); its class carries KEYS(S).
+// Nodes the candidate already touched are rechecked against its own copy of
+// their state (capacity, pod count, state bits), as in the pod order path.
+// <= 64 pods: lane k keeps pod k's node and its domain per key slot, lane s
+// the s-th touched node's state.
+__device__ __forceinline__ uint64_t wave_or(uint64_t v) {
+  v |= dpp_shifted<0x111>(v);
+  v |= dpp_shifted<0x112>(v);
+  v |= dpp_shifted<0x114>(v);
+  v |= dpp_shifted<0x118>(v);
+  v |= dpp_shifted<0x142, 0xa>(v);
+  v |= dpp_shifted<0x143, 0xc>(v);
+  return readlane64(v, 63);
+}
+
+__device__ __forceinline__ int dk_row_of(const DevWorkload& w, int k) {
+  return k == 0 ? w.dk_row[0] : k == 1 ? w.dk_row[1] : k == 2 ? w.dk_row[2] : w.dk_row[3];
+}
+
+static_assert(64 * 32 * 8 <= sizeof(K2Lds), "domain path: touched bitmap of 2048 words in the wave's LDS");
+template <int CH>
+__device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __restrict__ tl, const int p0,
+                                          const int np, const int dbase, int& status, uint32_t& nbytes) {
+  static_assert(kDevDomKeys == 4 && kDevDynTerms == 4, "the selects below unroll 4 key slots / terms");
+  const int lane = threadIdx.x & 63;
+  const int Wp = w.Wp;
+  const uint64_t* __restrict__ tab = w.S;
+  const uint64_t* __restrict__ at = w.atoms;
+  // touched nodes: lane s holds the s-th one's running state
+  int snode = INT_MAX, sleft = 0, nslots = 0;
+  int64_t scpu = 0, smem = 0, seph = 0;
+  uint64_t sport = 0;
+  for (int i = lane; i < 64 * CH; i += 64) tl[i] = 0;  // touched nodes (bitmap in the wave's LDS)
+  // lane k: pod k's node and its domain in every key slot
+  int pnode = -1;
+  int pdom[kDevDomKeys] = {-1, -1, -1, -1};
+  nbytes += (48u + 48u + 4u) * static_cast<uint32_t>(np) + 4u;
+  status = -1;
+  int k = 0;
+  for (; k < np; ++k) {
+    const uint64_t* pr = w.pod_rec + static_cast<size_t>(p0 + k) * kRecU64;
+    const int64_t rc = static_cast<int64_t>(pr[0]), rm = static_cast<int64_t>(pr[1]), re = static_cast<int64_t>(pr[2]);
+    const uint64_t pm = pr[3], r01 = pr[4], r23 = pr[5];
+    const uint64_t pin = swap_pairs(pm, w.swap_mask);
+    const bool zero = (rc | rm | re) == 0;
+    const uint64_t* dr = w.dyn_pod + static_cast<size_t>(dbase + k) * kDevDynU64;
+    const bool mine = lane < k;  // pods placed before this one
+    // anti-affinity: domains refused per key slot
+    uint64_t fdom[kDevDomKeys];
+#pragma unroll
+    for (int kk = 0; kk < kDevDomKeys; ++kk) {
+      const uint64_t m = kk < w.n_dk ? dr[kk] : 0ull;
+      const bool in = mine && ((m >> lane) & 1) && pdom[kk] >= 0;
+      fdom[kk] = m != 0 ? wave_or(in ? 1ull << pdom[kk] : 0ull) : 0ull;
+    }
+    // affinity: per term its key slot, base row and the earlier matching pods'
+    // domains (table key) or nodes (node-local key)
+    const uint64_t mm = dr[4], meta = dr[5];
+    int nt = 0;
+    int tslot[kDevDynTerms] = {0, 0, 0, 0}, tbase[kDevDynTerms] = {0, 0, 0, 0};
+    uint64_t adom[kDevDynTerms] = {0, 0, 0, 0};
+    if (meta != ~0ull) {
+      const int set = static_cast<int>(meta >> 1);
+      const bool self = (meta & 1) != 0;
+      const int32_t* si = w.ds_info + set * (2 + 2 * kDevDynTerms);
+      nt = si[0];
+      bool map_has = si[1] == 0;
+#pragma unroll
+      for (int i = 0; i < kDevDynTerms; ++i) {
+        if (i >= nt) continue;
+        tslot[i] = si[2 + 2 * i];
+        tbase[i] = si[3 + 2 * i];
+        int d = -1;
+#pragma unroll
+        for (int kk = 0; kk < kDevDomKeys; ++kk) d = kk == tslot[i] ? pdom[kk] : d;
+        const bool in = mine && ((mm >> lane) & 1) && d >= 0;
+        const uint64_t b = ballot(in);
+        map_has = map_has || b != 0;
+        adom[i] = dk_row_of(w, tslot[i]) >= 0 ? wave_or(in ? 1ull << d : 0ull) : b;
+      }
+      if (!map_has && self) nt = 0;  // first pod of a self-affine group: KEYS(S) (in its class) only
+    }
+    int ans = INT_MAX;
+    for (int ch = 0; ch < CH && ans == INT_MAX && ch * 64 < Wp; ++ch) {
+      const int wd = ch * 64 + lane;
+      const bool wv = wd < Wp;
+      const uint32_t wi = wv ? static_cast<uint32_t>(wd) : 0u;
+      const uint64_t sv = tab[static_cast<uint32_t>(r01) + wi];
+      const uint64_t tv = tab[static_cast<uint32_t>(r01 >> 32) + wi] & tab[static_cast<uint32_t>(r23) + wi] &
+                          tab[static_cast<uint32_t>(r23 >> 32) + wi];
+      nbytes += 64u * 32u;
+      uint64_t dyn = ~0ull;
+#pragma unroll
+      for (int kk = 0; kk < kDevDomKeys; ++kk) {
+        uint64_t m = fdom[kk];
+        const int row0 = dk_row_of(w, kk);
+        while (m != 0) {
+          const int d = __builtin_ctzll(m);
+          m &= m - 1;
+          dyn &= ~at[static_cast<size_t>(row0 + d) * Wp + wi];
+          nbytes += 64u * 8u;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kDevDynTerms; ++i) {
+        if (i >= nt) continue;
+        uint64_t row = at[static_cast<size_t>(tbase[i]) * Wp + wi];
+        nbytes += 64u * 8u;
+        uint64_t m = adom[i];
+        const int row0 = dk_row_of(w, tslot[i]);
+        while (m != 0) {
+          const int x = __builtin_ctzll(m);
+          m &= m - 1;
+          if (row0 >= 0) {  // domain x of a table key
+            row |= at[static_cast<size_t>(row0 + x) * Wp + wi];
+            nbytes += 64u * 8u;
+          } else {  // pod x's node (node-local key)
+            const int y = __builtin_amdgcn_readlane(pnode, x);
+            if ((y >> 6) == wd) row |= 1ull << (y & 63);
+          }
+        }
+        dyn &= row;
+      }
+      const uint64_t sd = wv ? sv & dyn : 0ull;
+      const uint64_t clean = sd & tv & ~tl[wd];
+      const uint64_t mc = ballot(clean != 0);
+      int cn = INT_MAX;
+      if (mc != 0) {
+        const int L0 = __builtin_ctzll(mc);
+        cn = (ch * 64 + L0) * 64 + __builtin_ctzll(readlane64(clean, L0));
+      }
+      // touched nodes of this chunk below cn: S and dynamic bit from the word's
+      // lane, the rest from the candidate's copy of the node
+      const bool in = snode >= ch * 4096 && snode < min(cn, (ch + 1) * 4096);
+      const int src = in ? (snode >> 6) - ch * 64 : 0;
+      const uint64_t ws = (static_cast<uint64_t>(from_lane(static_cast<uint32_t>(sd >> 32), src)) << 32) |
+                          from_lane(static_cast<uint32_t>(sd), src);
+      const bool fit = zero | ((rc <= scpu) & (rm <= smem) & (re <= seph));
+      const bool ok = in & (((ws >> (snode & 63)) & 1ull) != 0) & (sleft >= 1) & ((sport & pin) == 0) & fit;
+      ans = min(cn, wave_min(ok ? snode : INT_MAX));
+    }
+    if (ans == INT_MAX) {  // "pod %s can't be rescheduled on any existing spot node"
+      status = k;
+      break;
+    }
+    // ClusterSnapshot.AddPod on the candidate's copy
+    if (ballot(snode == ans) != 0) {
+      if (snode == ans) {
+        scpu -= rc;
+        smem -= rm;
+        seph -= re;
+        sleft -= 1;
+        sport |= pm;
+      }
+    } else {
+      const uint64_t* rec = w.node_rec + static_cast<size_t>(ans) * 8;
+      const int64_t fc = static_cast<int64_t>(rec[0]), fm = static_cast<int64_t>(rec[1]),
+                    fe = static_cast<int64_t>(rec[2]);
+      const uint64_t pb = rec[3];
+      const int pl = static_cast<int>(static_cast<int64_t>(rec[4]));
+      nbytes += 40u;
+      if (lane == nslots) {
+        snode = ans;
+        scpu = fc - rc;
+        smem = fm - rm;
+        seph = fe - re;
+        sleft = pl - 1;
+        sport = pb | pm;
+      }
+      ++nslots;
+      if (lane == 0) tl[ans >> 6] |= 1ull << (ans & 63);
+    }
+    int dn[kDevDomKeys];
+#pragma unroll
+    for (int kk = 0; kk < kDevDomKeys; ++kk)
+      dn[kk] = kk < w.n_dk ? w.dk_dom[static_cast<size_t>(kk) * w.n_spot + ans] : -1;
+    if (lane == k) {
+      pnode = ans;
+#pragma unroll
+      for (int kk = 0; kk < kDevDomKeys; ++kk) pdom[kk] = dn[kk];
+    }
+  }
+  if (lane < np) w.out_node[p0 + lane] = (status < 0 || lane < status) ? pnode : -1;
+}
+
 // K2: one wave per candidate (list entries {candidate, first pod, end pod,
 // global index}, longest candidates first).
 template <int CH, bool PROF>
@@ -1095,7 +1293,11 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   uint32_t nbytes = 0;
   bool node_order = false;
   if constexpr (CH == 1) node_order = np <= 4 * 64 && w.k2_mode == 0;  // rows of <= 64 words
-  if (node_order) {  // writes out_node itself
+  const int dbase = w.dyn_cand ? __builtin_amdgcn_readfirstlane(w.dyn_cand[ci]) : -1;
+  if (dbase >= 0) {  // writes out_node itself
+    wide = 3;
+    k2_domain<CH>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes);
+  } else if (node_order) {  // writes out_node itself
     uint64_t* F = reinterpret_cast<uint64_t*>(&L);
     wide = 2;
     if (np <= 64) k2_node_order<1, PROF>(w, F, p0, np, status, st, nbytes);

@@ -11,6 +11,9 @@ namespace sr {
 
 constexpr int kResultHeader = 8;           // words before the winner's mapping in `result`
 constexpr size_t kK0ProfWaves = 32768;  // K0 waves profiled after K2's [n_cand][16] records
+constexpr int kDevDynU64 = 6;           // domain-path pod record words (host.hpp kDynU64)
+constexpr int kDevDomKeys = 4;          // key slots (host.hpp kDomKeys)
+constexpr int kDevDynTerms = 4;         // terms per domain-path affinity set (host.hpp kDynTerms)
 
 // Pointers into the device arena (layout: DESIGN.md §HBM layout).
 struct DevWorkload {
@@ -38,6 +41,15 @@ struct DevWorkload {
   const int32_t* cand_global;
   const int4* list;         // [n_list] {candidate, first pod, end pod, global index}, longest first
   int32_t n_list;
+  // domain path (k2_domain): candidates whose pods interact through shared-domain
+  // topology keys (antiaff.cpp); null when the call has none
+  const int32_t* dyn_cand;  // [n_cand] first record in dyn_pod, -1: node / pod order
+  const uint64_t* dyn_pod;  // [..][kDynU64] {anti-affinity mask per key slot x4, affinity mask,
+                            //  set << 1 | self or ~0}; masks over the candidate's earlier pods
+  int32_t n_dk;             // key slots
+  const int32_t* dk_dom;    // [n_dk][n_spot] domain of each spot node (node-local key: the node), -1 absent
+  int32_t dk_row[4];        // atom of domain 0 per table key slot, -1: node-local key
+  const int32_t* ds_info;   // [set][2 + 2 * 4] {terms, map_empty, (key slot, base-row atom) per term}
   // outputs / scratch
   uint64_t* S;         // [n_classes][Wp] static-class rows, followed by
   uint64_t* T;         // [n_t][Wp] capacity threshold rows (one table)

@@ -155,6 +155,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t o_prec = pk.add(w.pod_rec);
   const size_t o_co = pk.add(w.cand_off), o_cg = pk.add(w.cand_global);
   const size_t o_ls = pk.add(w.list);
+  const bool dyn = !w.dyn_cand.empty();
+  const size_t o_dc = dyn ? pk.add(w.dyn_cand) : 0, o_dp = dyn ? pk.add(w.dyn_pod) : 0;
+  const size_t o_dd = dyn ? pk.add(w.dk_dom) : 0, o_di = dyn ? pk.add(w.ds_info) : 0;
   const size_t bytes = pk.size();
 
   HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -208,6 +211,14 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.cand_global = static_cast<const int32_t*>(at(o_cg));
   d.list = static_cast<const int4*>(at(o_ls));
   d.n_list = static_cast<int32_t>(w.list.size() / 4);
+  d.dyn_cand = dyn ? static_cast<const int32_t*>(at(o_dc)) : nullptr;
+  d.dyn_pod = dyn ? static_cast<const uint64_t*>(at(o_dp)) : nullptr;
+  d.dk_dom = dyn ? static_cast<const int32_t*>(at(o_dd)) : nullptr;
+  d.ds_info = dyn ? static_cast<const int32_t*>(at(o_di)) : nullptr;
+  d.n_dk = w.n_dk;
+  static_assert(sr::kDevDynU64 == sr::kDynU64 && sr::kDevDomKeys == sr::kDomKeys && sr::kDevDynTerms == sr::kDynTerms,
+                "domain-path layout shared by encode.cpp and kernels.hip");
+  for (int k = 0; k < sr::kDomKeys; ++k) d.dk_row[k] = w.dk_row[k];
   d.S = static_cast<uint64_t*>(ctx->tables.p);
   d.T = d.S + static_cast<size_t>(w.n_classes) * w.Wp;
   d.out_node = static_cast<int32_t*>(ctx->out_node.p);

@@ -109,10 +109,10 @@ def rand_selector(r: random.Random, valid_only: bool = False):
     return LabelSelector({}, [LabelSelectorRequirement("tier", "In", [])])  # invalid: fallback
 
 
-def rand_anti(r: random.Random, p: Pod, rate: float, hostname_only: bool = False):
+def rand_anti(r: random.Random, p: Pod, rate: float, hostname_only: bool = False, shared_keys: bool = False):
     """Labels and namespace for every pod; required anti-affinity for some.
     Topology keys: the hostname (node-local) mostly, zone / team (shared or
-    missing on some nodes) otherwise."""
+    missing on some nodes) otherwise (always with shared_keys)."""
     p.namespace = r.choice(NAMESPACES)
     p.labels = {"app": r.choice(APPS)}
     if r.random() < 0.5:
@@ -120,28 +120,30 @@ def rand_anti(r: random.Random, p: Pod, rate: float, hostname_only: bool = False
     if r.random() < rate:
         p.pod_anti_affinity = []
         for _ in range(r.randint(1, 2)):
-            tk = HOST if hostname_only or r.random() < 0.7 else r.choice(["zone", "team"])
+            tk = HOST if hostname_only or (not shared_keys and r.random() < 0.7) else r.choice(["zone", "team"])
             ns = [] if r.random() < 0.7 else r.sample(["default", "other"], r.randint(1, 2))
             p.pod_anti_affinity.append(PodAffinityTerm(tk, rand_selector(r, hostname_only), ns))
 
 
-def rand_aff(r: random.Random, p: Pod, rate: float):
+def rand_aff(r: random.Random, p: Pod, rate: float, shared_keys: bool = False):
     """Required pod affinity for some pods: one or two terms on the hostname or
     a shared key (zone / team), valid selectors mostly on the app label."""
     if r.random() < rate:
         p.pod_affinity = []
         for _ in range(r.randint(1, 2)):
-            tk = r.choice([HOST, "zone", "zone", "team"])
+            tk = r.choice(["zone", "zone", "team"] if shared_keys else [HOST, "zone", "zone", "team"])
             ns = [] if r.random() < 0.8 else r.sample(["default", "other"], r.randint(1, 2))
             p.pod_affinity.append(PodAffinityTerm(tk, rand_selector(r, True), ns))
 
 
 def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 8, features: bool = True,
-                  fallback: bool = False, anti: float = 0.0, hostname_only: bool = False, aff: float = 0.0):
+                  fallback: bool = False, anti: float = 0.0, hostname_only: bool = False, aff: float = 0.0,
+                  shared_keys: bool = False):
     """Returns (spot_nodes, spot_pods, candidates) with candidates a list of pod lists.
     anti > 0: pods carry namespaces / labels and that share required pod anti-affinity
     (hostname_only: every term on kubernetes.io/hostname with a valid selector).
-    aff > 0: that share of the pods (spot and candidate) carries required pod affinity."""
+    aff > 0: that share of the pods (spot and candidate) carries required pod affinity.
+    shared_keys: every inter-pod term on zone / team (shared domains)."""
     r = random.Random(seed)
     nodes = [rand_node(r, "n%d" % i, features) for i in range(n_spot)]
     spot_pods = []
@@ -155,11 +157,11 @@ def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 
     if anti > 0 or aff > 0:
         for ps in spot_pods + cands:
             for p in ps:
-                rand_anti(r, p, anti, hostname_only)
+                rand_anti(r, p, anti, hostname_only, shared_keys)
     if aff > 0:
         for ps in spot_pods + cands:
             for p in ps:
-                rand_aff(r, p, aff)
+                rand_aff(r, p, aff, shared_keys)
     return nodes, spot_pods, cands
 
 
@@ -184,8 +186,8 @@ def term_selects(owner: Pod, t: PodAffinityTerm, target: Pod) -> bool:
 def anti_interacts_off_node(nodes, pods) -> bool:
     """Two pods of one candidate interact through an anti-affinity term whose
     topology key is not node-local on the spot pool (some node lacks it or two
-    nodes share a value): the product routes such a candidate to the fallback
-    path (antiaff.cpp), the oracle evaluates it."""
+    nodes share a value): the product plans such a candidate on K2's domain
+    path (antiaff.cpp, kernels.hip k2_domain)."""
     def node_local(tk):
         vals = [n.labels.get(tk) for n in nodes]
         return all(v is not None for v in vals) and len(set(vals)) == len(vals)
@@ -201,7 +203,7 @@ def anti_interacts_off_node(nodes, pods) -> bool:
 def aff_interacts(pods) -> bool:
     """An earlier pod of the candidate matches every required affinity term of a
     later one: that pod's allowed domains change while the candidate is
-    planned; the product routes such a candidate to the reference path."""
+    planned; the product plans such a candidate on K2's domain path."""
     for k, p in enumerate(pods):
         terms = p.pod_affinity or []
         if terms and any(all(term_selects(p, t, q) for t in terms) for q in pods[:k]):

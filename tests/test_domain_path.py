@@ -1,0 +1,82 @@
+"""K2's domain path (candidates whose pods interact through inter-pod
+(anti-)affinity across nodes): the hand-derived plans of domain_cases.py on the
+oracle (CPU) and on the GPU through the C-ABI, random clusters with shared-key
+terms planned without fallback, and the path's limits."""
+import numpy as np
+import pytest
+
+from domain_cases import cases, nodes
+from helpers import Scenario
+from oracle_lib import oracle_plan
+from randcluster import aff_interacts, anti_interacts_off_node, rand_scenario
+from spotplanner import capi
+from spotplanner.rescheduler import plan_arrays
+
+CASES = cases()
+IDS = [c.name for c in CASES]
+
+
+def _plan(sc, n, use_gpu, checker=None):
+    cand_off = np.array([0, n], np.int32)
+    cand_pods = np.arange(sc.q0, sc.q0 + n, dtype=np.int32)
+    if not use_gpu:
+        o = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=1)
+        return int(o["status"][0]), list(o["node_of_pod"])
+    h = sc.product_snapshot()
+    try:
+        p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+    finally:
+        capi.load_planner().sr_snapshot_destroy(h)
+    return int(p.status[0]), list(p.node_of_pod)
+
+
+def _expect(case):
+    return (capi.SR_CAND_OK if case.fail < 0 else case.fail), case.want
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+def test_oracle_domain_case(case):
+    sc = Scenario(nodes(), [[] for _ in range(4)], case.pods)
+    assert _plan(sc, len(case.pods), False) == _expect(case), case.why
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+def test_gpu_domain_case(checker, case):
+    sc = Scenario(nodes(), [[] for _ in range(4)], case.pods)
+    assert _plan(sc, len(case.pods), True, checker) == _expect(case), case.why
+
+
+def test_random_scenarios_reach_the_domain_path():
+    """The random parity seeds below plan candidates that interact across
+    nodes (not only static conflicts): both kinds must occur."""
+    anti = aff = 0
+    for seed in range(30):
+        nodes_, _, cands = rand_scenario(7000 + seed, n_spot=8 + seed % 10, n_cand=10, max_pods=3 + seed % 8,
+                                         features=seed % 2 == 0, anti=0.3, aff=0.3, shared_keys=True)
+        anti += sum(anti_interacts_off_node(nodes_, c) for c in cands)
+        aff += sum(aff_interacts(c) for c in cands)
+    assert anti >= 30 and aff >= 30, (anti, aff)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(30))
+def test_gpu_random_shared_key_plans(checker, seed):
+    """Anti-affinity and affinity on zone / team keys (shared, missing on some
+    nodes) between the pods of a candidate: planned on the device, bit-exact
+    with the oracle, no fallback."""
+    from test_gpu_parity import run_scenario
+    nodes_, spot_pods, cands = rand_scenario(7000 + seed, n_spot=8 + seed % 10, n_cand=10, max_pods=3 + seed % 8,
+                                             features=seed % 2 == 0, anti=0.3, aff=0.3, shared_keys=True)
+    run_scenario(checker, nodes_, spot_pods, cands)
+
+
+@pytest.mark.gpu
+def test_gpu_domain_path_limit_falls_back(checker):
+    """More than 64 pods interacting across nodes: the candidate takes the
+    fallback path (kDynPods); a 64-pod one is still planned."""
+    from domain_cases import pod, term
+    from test_gpu_parity import run_scenario
+    big = [[pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(64)] + [pod("d", "db")],
+           [pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(63)] + [pod("d", "db")]]
+    run_scenario(checker, nodes(), [[] for _ in range(4)], big, extra_fallback=lambda c: c == 0)
