@@ -759,13 +759,23 @@ __device__ __forceinline__ uint64_t place_runs(uint64_t P, int lane, int64_t rc,
   return placed;
 }
 
-template <bool E, bool O>
+// Placement at one node visit.  Visits whose pods set or meet state bits
+// (host ports, anti-affinity pairs) run pod by pod: the run pass would add an
+// OR scan and a rescan per failing pod, and measured slower there (C5).  The
+// others take the run pass from k2_scan_min pods on.  Few variants on purpose:
+// every extra copy of this code is instruction-cache footprint a wave jumps
+// between (measured on C5: specialising all four E / O combinations cost 5 %).
 __device__ __forceinline__ uint64_t place_at(const DevWorkload& w, uint64_t P, int lane, int64_t rc, int64_t rm,
                                              int64_t re, uint64_t pm, uint64_t zm, int64_t& cpu, int64_t& mem,
                                              int64_t& eph, uint64_t& ports, int& left) {
-  if (__builtin_popcountll(P) >= w.k2_scan_min)
-    return place_runs<E, O>(P, lane, rc, rm, re, pm, swap_pairs(pm, w.swap_mask), zm, cpu, mem, eph, ports, left);
-  return place_seq<E, O>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
+  const bool E = (ballot(re != 0) & P) != 0;  // some pod asks for ephemeral storage
+  const bool O = (ballot(pm != 0) & P) != 0;  // some pod sets / meets state bits
+  if (O) return place_seq<true, true>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
+  if (__builtin_popcountll(P) >= w.k2_scan_min) {
+    if (E) return place_runs<true, false>(P, lane, rc, rm, re, pm, 0ull, zm, cpu, mem, eph, ports, left);
+    return place_runs<false, false>(P, lane, rc, rm, re, pm, 0ull, zm, cpu, mem, eph, ports, left);
+  }
+  return place_seq<true, false>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
 }
 
 template <int G, bool PROF>
@@ -990,15 +1000,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       const uint64_t cand = ballot(((act[g] >> lane) & 1) && ptr[g] == n);
       uint64_t placed = 0;
       if (cand != 0) {  // wave-uniform
-        const bool E = (ballot(re[g] != 0) & cand) != 0;
-        const bool O = (ballot(pm[g] != 0) & cand) != 0;
-#define SR_PLACE_AT(E_, O_) \
-  place_at<E_, O_>(w, cand, lane, rc[g], rm[g], re[g], pm[g], zm[g], cpu, mem, eph, ports, left)
-        if (E && O) placed = SR_PLACE_AT(true, true);
-        else if (E) placed = SR_PLACE_AT(true, false);
-        else if (O) placed = SR_PLACE_AT(false, true);
-        else placed = SR_PLACE_AT(false, false);
-#undef SR_PLACE_AT
+        placed = place_at(w, cand, lane, rc[g], rm[g], re[g], pm[g], zm[g], cpu, mem, eph, ports, left);
         placements += __builtin_popcountll(placed);
       }
       if ((placed >> lane) & 1) node[g] = n;
