@@ -165,8 +165,8 @@ PodMeta meta_of(const sr_pod_affinity& A, int32_t pod) {
                  A.label_off[pod + 1] - A.label_off[pod]};
 }
 
-PodMeta meta_of(const SnapPod& p) {
-  return PodMeta{p.ns, p.lkey.data(), p.lval.data(), static_cast<int32_t>(p.lkey.size())};
+PodMeta meta_of(const sr_snapshot* s, const SnapPod& p) {
+  return PodMeta{p.ns, s->lkey.data() + p.lab, s->lval.data() + p.lab, static_cast<int32_t>(p.nlab)};
 }
 
 bool pod_label(const PodMeta& m, int32_t key, int32_t* val) {
@@ -228,9 +228,10 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
   std::vector<std::pair<int32_t, int32_t>> base_has;  // (node, term)
   for (int32_t n = 0; n < n_spot; ++n)
     for (int32_t e : snap->state[n].pods) {
-      const std::vector<int32_t>& tw = snap->pods[e].terms;
-      for (size_t i = 0; i < tw.size(); i += 1 + static_cast<size_t>(tw[i]))
-        base_has.emplace_back(n, dict.intern(tw.data() + i + 1, static_cast<size_t>(tw[i])));
+      const SnapPod& sp = snap->pods[e];
+      const int32_t* tw = snap->term_words.data() + sp.terms;
+      for (size_t i = 0; i < sp.nterms; i += 1 + static_cast<size_t>(tw[i]))
+        base_has.emplace_back(n, dict.intern(tw + i + 1, static_cast<size_t>(tw[i])));
     }
   std::vector<std::vector<int32_t>> has(static_cast<size_t>(n_flat));  // term ids per flat candidate pod
   for (int32_t i = 0; i < nc; ++i) {
@@ -335,7 +336,7 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       for (size_t ch = lo; ch < hi; ++ch)
         for (int32_t n = static_cast<int32_t>(ch * kNodes); n < std::min<int32_t>(n_spot, (ch + 1) * kNodes); ++n)
           for (int32_t e : snap->state[n].pods)
-            for_each_selecting(meta_of(snap->pods[e]), [&](int32_t t) {
+            for_each_selecting(meta_of(snap, snap->pods[e]), [&](int32_t t) {
               const int32_t v = keys[kidx[t]].val[n];
               if (v != INT_MIN) part[ch].emplace_back(t, v);
             });
@@ -576,7 +577,7 @@ void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_can
     for (int32_t e : snap->state[n].pods) {
       const SnapPod& sp = snap->pods[e];
       if (!sp.meta) continue;  // candidates with terms already fell back
-      const PodMeta m = meta_of(sp);
+      const PodMeta m = meta_of(snap, sp);
       for (int32_t s = 0; s < S; ++s) {
         bool all = true;
         for (const Term& t : sets[s]) all = all && term_selects(t, m);

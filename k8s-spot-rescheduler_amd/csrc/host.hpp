@@ -51,8 +51,9 @@ struct SnapPod {
   uint8_t meta = 0;    // ns / labels / terms known (the cluster passed sr_pod_affinity)
   uint8_t anti = 0;    // carries required anti-affinity
   uint8_t opaque = 0;  // ... that the encoder cannot read (anti_opaque)
-  std::vector<int32_t> lkey, lval;  // labels
-  std::vector<int32_t> terms;       // anti-affinity terms: {n words, words...} per term
+  uint32_t lab = 0, nlab = 0;       // labels: sr_snapshot::lkey / lval [lab, lab + nlab)
+  uint32_t terms = 0, nterms = 0;   // anti-affinity terms: sr_snapshot::term_words [terms, terms + nterms),
+                                    // {n words, words...} per term (rare)
 };
 
 // Mutable part: scheduler NodeInfo.Requested, len(Pods), UsedPorts, the pods
@@ -78,7 +79,11 @@ struct sr_snapshot {
   std::vector<sr::NodeState> state;
   std::vector<sr::NodeState> saved;
   std::vector<sr::SnapPod> pods;  // every pod ever added (NodeState::pods index it)
+  std::vector<int32_t> lkey, lval;  // the pods' labels (one arena: no allocation per pod)
+  std::vector<int32_t> term_words;  // the pods' anti-affinity terms (one arena)
   size_t fork_pods = 0;           // pods.size() at Fork: Revert drops the rest
+  size_t fork_labels = 0;         // lkey.size() at Fork
+  size_t fork_terms = 0;          // term_words.size() at Fork
   bool forked = false;
   int64_t anti_total = 0;
   int64_t opaque_total = 0;   // pods whose anti-affinity the encoder cannot read: every candidate falls back
@@ -110,7 +115,15 @@ bool aff_opaque(const sr_cluster* c, int32_t pod);
 // namespaces (defaulted to the owner's), selector; equal words = equal terms.
 void anti_term_words(const sr_cluster* c, int32_t owner, int32_t t, std::vector<int32_t>& out);
 // The snapshot's copy of a pod of `c` (SnapPod).
-void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out);
+// The snapshot's copy of a pod's metadata; its labels go to (*k, *v)
+// [lab, lab + their count), which the caller sized, its anti-affinity terms
+// (rare) to `terms` (appended; callers on several threads pass their own).
+void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out, int32_t* k, int32_t* v, uint32_t lab,
+                   std::vector<int32_t>* terms);
+inline uint32_t pod_label_count(const sr_cluster* c, int32_t pod) {
+  const sr_pod_affinity* A = c->pod_affinity;
+  return A ? static_cast<uint32_t>(A->label_off[pod + 1] - A->label_off[pod]) : 0u;
+}
 
 // Class descriptor flags.
 enum : int32_t { CLS_AFF_REQUIRED = 1, CLS_IMPOSSIBLE = 2 };

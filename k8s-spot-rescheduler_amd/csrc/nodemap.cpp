@@ -106,7 +106,8 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   return SR_OK;
 }
 
-void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out) {
+void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out, int32_t* k, int32_t* v, uint32_t lab,
+                   std::vector<int32_t>* terms) {
   *out = SnapPod{};
   out->anti = has_anti_terms(c, pod) ? 1 : 0;
   out->opaque = anti_opaque(c, pod) ? 1 : 0;
@@ -114,15 +115,19 @@ void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out) {
   if (!A) return;
   out->meta = 1;
   out->ns = A->ns[pod];
-  out->lkey.assign(A->label_key + A->label_off[pod], A->label_key + A->label_off[pod + 1]);
-  out->lval.assign(A->label_val + A->label_off[pod], A->label_val + A->label_off[pod + 1]);
-  if (out->opaque) return;  // never read: every candidate falls back while it is there
+  out->lab = lab;
+  out->nlab = pod_label_count(c, pod);
+  std::copy(A->label_key + A->label_off[pod], A->label_key + A->label_off[pod + 1], k + lab);
+  std::copy(A->label_val + A->label_off[pod], A->label_val + A->label_off[pod + 1], v + lab);
+  if (out->opaque || !out->anti) return;  // opaque: never read, every candidate falls back while it is there
   std::vector<int32_t> words;
+  out->terms = static_cast<uint32_t>(terms->size());
   for (int32_t t = A->anti_off[pod]; t < A->anti_off[pod + 1]; ++t) {
     anti_term_words(c, pod, t, words);
-    out->terms.push_back(static_cast<int32_t>(words.size()));
-    out->terms.insert(out->terms.end(), words.begin(), words.end());
+    terms->push_back(static_cast<int32_t>(words.size()));
+    terms->insert(terms->end(), words.begin(), words.end());
   }
+  out->nterms = static_cast<uint32_t>(terms->size()) - out->terms;
 }
 
 // scheduler NodeInfo.AddPod [upstream k8s v1.19 framework/types.go]: Requested +=
@@ -189,7 +194,10 @@ bool aff_opaque(const sr_cluster* c, int32_t pod) {
 void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t pos) {
   const int32_t store = static_cast<int32_t>(s->pods.size());
   s->pods.emplace_back();
-  snap_pod_from(c, pod, &s->pods.back());
+  const uint32_t lab = static_cast<uint32_t>(s->lkey.size());
+  s->lkey.resize(lab + pod_label_count(c, pod));
+  s->lval.resize(s->lkey.size());
+  snap_pod_from(c, pod, &s->pods.back(), s->lkey.data(), s->lval.data(), lab, &s->term_words);
   const SnapPod& sp = s->pods.back();
   state_add_pod(s->state[pos], c, pod, sp, store);
   s->anti_total += sp.anti;
@@ -224,9 +232,27 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
   std::vector<int32_t> base(static_cast<size_t>(n_spot) + 1, 0);
   for (int32_t i = 0; i < n_spot; ++i) base[i + 1] = base[i] + (off[spot[i] + 1] - off[spot[i]]);
   s->pods.resize(static_cast<size_t>(base[n_spot]));
-  // AddNodeWithPods per spot node: independent nodes, on the pool
-  parallel_for(static_cast<size_t>(n_spot), 32, [&](size_t lo, size_t hi) {
+  // their labels: node i's at [lbase[i], lbase[i + 1])
+  std::vector<uint32_t> lbase(static_cast<size_t>(n_spot) + 1, 0);
+  if (c->pod_affinity) {
+    parallel_for(static_cast<size_t>(n_spot), 256, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        uint32_t n = 0;
+        for (int32_t j = off[spot[i]]; j < off[spot[i] + 1]; ++j) n += pod_label_count(c, idx[j]);
+        lbase[i + 1] = n;
+      }
+    });
+    for (int32_t i = 0; i < n_spot; ++i) lbase[i + 1] += lbase[i];
+  }
+  s->lkey.resize(lbase[n_spot]);
+  s->lval.resize(lbase[n_spot]);
+  // AddNodeWithPods per spot node: independent nodes, on the pool; the rare
+  // anti-affinity terms go to per-chunk arenas, concatenated afterwards
+  constexpr size_t kNodeChunk = 32;
+  std::vector<std::vector<int32_t>> chunk_terms((static_cast<size_t>(n_spot) + kNodeChunk - 1) / kNodeChunk);
+  parallel_for(static_cast<size_t>(n_spot), kNodeChunk, [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
+      std::vector<int32_t>* terms = &chunk_terms[i / kNodeChunk];
       const int32_t node = spot[i];
       SpotNode& sn = s->nodes[i];
       sn.name = N.name[node];
@@ -242,13 +268,23 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
         sn.taints.push_back(TaintRec{N.taint_key[j], N.taint_val[j], N.taint_effect[j]});
       sn.static_fp = node_static_fp(sn);
       s->state[i].pods.reserve(static_cast<size_t>(off[node + 1] - off[node]));
+      uint32_t lab = lbase[i];
       for (int32_t j = off[node]; j < off[node + 1]; ++j) {
         const int32_t store = base[i] + (j - off[node]);
-        snap_pod_from(c, idx[j], &s->pods[store]);
+        snap_pod_from(c, idx[j], &s->pods[store], s->lkey.data(), s->lval.data(), lab, terms);
+        lab += s->pods[store].nlab;
         state_add_pod(s->state[i], c, idx[j], s->pods[store], store);
       }
     }
   });
+  for (size_t ch = 0; ch < chunk_terms.size(); ++ch) {
+    if (chunk_terms[ch].empty()) continue;
+    const uint32_t shift = static_cast<uint32_t>(s->term_words.size());
+    s->term_words.insert(s->term_words.end(), chunk_terms[ch].begin(), chunk_terms[ch].end());
+    const size_t i1 = std::min(static_cast<size_t>(n_spot), (ch + 1) * kNodeChunk);
+    for (int32_t q = base[ch * kNodeChunk]; q < base[i1]; ++q)
+      if (s->pods[q].nterms) s->pods[q].terms += shift;
+  }
   for (int32_t i = 0; i < n_spot; ++i) {
     s->anti_total += s->state[i].anti;
     s->opaque_total += s->state[i].opaque;
@@ -293,6 +329,8 @@ sr_status sr_snapshot_fork(sr_snapshot* snap) {
   if (snap->forked) return SR_ERR_STATE;  // DeltaClusterSnapshot forks one level deep
   snap->saved = snap->state;
   snap->fork_pods = snap->pods.size();
+  snap->fork_labels = snap->lkey.size();
+  snap->fork_terms = snap->term_words.size();
   snap->forked = true;
   return SR_OK;
 }
@@ -303,6 +341,9 @@ sr_status sr_snapshot_revert(sr_snapshot* snap) {
   snap->state.swap(snap->saved);
   snap->saved.clear();
   snap->pods.resize(snap->fork_pods);  // pods added since Fork are referenced by no state any more
+  snap->lkey.resize(snap->fork_labels);
+  snap->lval.resize(snap->fork_labels);
+  snap->term_words.resize(snap->fork_terms);
   snap->forked = false;
   snap->anti_total = snap->opaque_total = snap->unknown_total = 0;
   for (const auto& st : snap->state) {
