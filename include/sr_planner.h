@@ -294,7 +294,16 @@ typedef struct sr_snapshot sr_snapshot;
 
 /* Replaces NodeInfoArray.GetClusterSnapshot (nodes/nodes.go:226-232):
  * AddNodeWithPods(node, pods) per spot node, in NodeInfoArray order.
- * node_pod_off/node_pod_idx: CSR indexed by node index (sr_node_map layout). */
+ * node_pod_off/node_pod_idx: CSR indexed by node index (sr_node_map layout).
+ *
+ * Ownership: the snapshot COPIES what it needs of every pod it holds (requests,
+ * host ports, namespace, labels, anti-affinity terms) when the pod is added, by
+ * sr_snapshot_create or sr_snapshot_add_pod.  Later calls may pass any
+ * sr_cluster (e.g. one holding only the pods being queried): pod indices in a
+ * call always index that call's cluster, never the one the snapshot was built
+ * from.  A pod added from a cluster without sr_pod_affinity has unknown labels;
+ * a candidate whose own inter-pod terms would have to match it is routed to the
+ * fallback path. */
 sr_status sr_snapshot_create(const sr_cluster *cluster, const int32_t *spot_nodes, int32_t n_spot,
                              const int32_t *node_pod_off, const int32_t *node_pod_idx,
                              sr_snapshot **out);
