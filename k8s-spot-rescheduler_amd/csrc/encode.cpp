@@ -259,35 +259,20 @@ void intern_groups(WordDict& dict, const int32_t* g, int32_t n_groups, std::vect
   if (used) *used = i;
 }
 
-uint64_t node_state_fp(const SpotNode& sn, const NodeState& st) {
-  uint64_t h = 0x51ED270B7A1DE5ull;
-  for (int r = 0; r < 3; ++r) h = mix(mix(h, static_cast<uint64_t>(sn.alloc[r])), static_cast<uint64_t>(st.requested[r]));
-  h = mix(mix(h, static_cast<uint64_t>(sn.alloc_pods)), static_cast<uint64_t>(st.npods));
-  uint64_t ports = 0;  // order-independent
-  for (const Port& u : st.ports)
-    ports += mix(mix(mix(0x9E37ull, static_cast<uint32_t>(u.ip)), static_cast<uint32_t>(u.proto)),
-                 static_cast<uint32_t>(u.port));
-  return mix(h, ports);
-}
-
 // ---- static view: names, labels, taints of the spot pool in NodeInfoArray order
 void refresh_static(EncoderCache& C, const sr_snapshot* snap, int32_t Wp) {
   const int32_t n = static_cast<int32_t>(snap->nodes.size());
   bool same = C.n_spot == n && C.Wp == Wp;
-  for (int32_t i = 0; same && i < n; ++i)
-    same = C.names[i] == snap->nodes[i].name && C.static_fp[i] == snap->nodes[i].static_fp;
+  same = same && std::equal(C.names.begin(), C.names.end(), snap->node_names.begin()) &&
+         std::equal(C.static_fp.begin(), C.static_fp.end(), snap->node_sfp.begin());
   C.last_static_changed = same ? 0 : 1;
   if (same) return;
   ++C.static_gen;
   C.n_spot = n;
   C.Wp = Wp;
   C.n_pad = Wp * 64;
-  C.names.resize(n);
-  C.static_fp.resize(n);
-  for (int32_t i = 0; i < n; ++i) {
-    C.names[i] = snap->nodes[i].name;
-    C.static_fp[i] = snap->nodes[i].static_fp;
-  }
+  C.names = snap->node_names;
+  C.static_fp = snap->node_sfp;
   C.label_col.clear();
   // taints: NoSchedule / NoExecute only (TaintToleration.Filter); the
   // unschedulable flag is the pseudo-taint node.kubernetes.io/unschedulable:NoSchedule
@@ -316,12 +301,7 @@ void refresh_static(EncoderCache& C, const sr_snapshot* snap, int32_t Wp) {
 // ---- state view: capacity records, free values (sorted), pod-count atom
 sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* err) {
   const int32_t n = C.n_spot, NP = C.n_pad, Wp = C.Wp;
-  std::vector<uint64_t> fp(static_cast<size_t>(n));
-  auto fill_fp = [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) fp[i] = node_state_fp(snap->nodes[i], snap->state[i]);
-  };
-  if (n > kSerialPods) parallel_for(static_cast<size_t>(n), 1024, fill_fp);
-  else fill_fp(0, static_cast<size_t>(n));
+  const std::vector<uint64_t>& fp = snap->node_dfp;  // kept current by the snapshot
   std::vector<int32_t> changed;
   const bool full = !C.state_valid || C.state_fp.size() != static_cast<size_t>(n);
   if (!full)
@@ -329,6 +309,8 @@ sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* e
       if (fp[i] != C.state_fp[i]) changed.push_back(i);
   C.last_state_changed = full ? n : static_cast<int32_t>(changed.size());
   if (!full && changed.empty()) return SR_OK;
+  C.patched_from = ~0ull;
+  C.patched_nodes.clear();
   ++C.state_gen;
   auto node_values = [&](int32_t i, int64_t out[3], int64_t* left) -> bool {
     const SpotNode& sn = snap->nodes[i];
@@ -371,23 +353,29 @@ sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* e
     }
     for (int d = 0; d < 3; ++d) std::sort(C.sorted_free[d].begin(), C.sorted_free[d].end());
   } else {  // a few nodes changed: patch their records and the sorted values
+    C.patched_from = C.state_gen - 1;
+    C.patched_nodes = changed;
     for (int32_t i : changed) {
       int64_t f[3], left;
       if (!node_values(i, f, &left)) return fail();
-      for (int d = 0; d < 3; ++d) {
+      for (int d = 0; d < 3; ++d) {  // the sorted values with multiplicity, and the distinct ones
         std::vector<int64_t>& s = C.sorted_free[d];
+        std::vector<int64_t>& v = C.node_vals[d];
         const int64_t old = C.node_free[static_cast<size_t>(d) * NP + i];
         s.erase(std::lower_bound(s.begin(), s.end(), old));
+        if (!std::binary_search(s.begin(), s.end(), old)) v.erase(std::lower_bound(v.begin(), v.end(), old));
+        if (!std::binary_search(s.begin(), s.end(), f[d])) v.insert(std::lower_bound(v.begin(), v.end(), f[d]), f[d]);
         s.insert(std::upper_bound(s.begin(), s.end(), f[d]), f[d]);
       }
       write_node(i, f, left);
     }
   }
-  for (int d = 0; d < 3; ++d) {
-    C.node_vals[d].assign(C.sorted_free[d].begin(), C.sorted_free[d].end());
-    C.node_vals[d].erase(std::unique(C.node_vals[d].begin(), C.node_vals[d].end()), C.node_vals[d].end());
-  }
-  C.state_fp.swap(fp);
+  if (full || changed.size() * 8 > static_cast<size_t>(n))
+    for (int d = 0; d < 3; ++d) {
+      C.node_vals[d].assign(C.sorted_free[d].begin(), C.sorted_free[d].end());
+      C.node_vals[d].erase(std::unique(C.node_vals[d].begin(), C.node_vals[d].end()), C.node_vals[d].end());
+    }
+  C.state_fp = fp;
   C.state_valid = true;
   return SR_OK;
 }
@@ -451,6 +439,17 @@ uint64_t node_static_fp(const SpotNode& n) {
     taints += mix(mix(mix(0x7A1Eull, static_cast<uint32_t>(t.key)), static_cast<uint32_t>(t.val)),
                   static_cast<uint32_t>(t.effect));
   return mix(mix(h, labels), taints);
+}
+
+uint64_t node_state_fp(const SpotNode& sn, const NodeState& st) {
+  uint64_t h = 0x51ED270B7A1DE5ull;
+  for (int r = 0; r < 3; ++r) h = mix(mix(h, static_cast<uint64_t>(sn.alloc[r])), static_cast<uint64_t>(st.requested[r]));
+  h = mix(mix(h, static_cast<uint64_t>(sn.alloc_pods)), static_cast<uint64_t>(st.npods));
+  uint64_t ports = 0;  // order-independent
+  for (const Port& u : st.ports)
+    ports += mix(mix(mix(0x9E37ull, static_cast<uint32_t>(u.ip)), static_cast<uint32_t>(u.proto)),
+                 static_cast<uint32_t>(u.port));
+  return mix(h, ports);
 }
 
 sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr_cluster* c,
@@ -1251,6 +1250,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   phase(8);
   std::vector<uint8_t> used[3];  // lower-bound positions some pod asks for, per dimension
   for (int d = 0; d < 3; ++d) used[d].assign(C.node_vals[d].size() + 1, 0);
+  std::vector<int32_t> used_list[3];  // the same positions, listed (serial runs: no scan of `used`)
   std::atomic<bool> any_dead{false};
   // per pod: requests, records and the lower-bound position of each request
   // among the node values (stored in pod_rows[1..3] for now)
@@ -1275,7 +1275,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       for (int d = 0; d < 3; ++d) {
         if (r[1 + d] < 0) continue;
         uint8_t* u = &used[d][static_cast<size_t>(r[1 + d])];  // read first (see key_seen)
-        if (!__atomic_load_n(u, __ATOMIC_RELAXED)) __atomic_store_n(u, uint8_t(1), __ATOMIC_RELAXED);
+        if (!__atomic_load_n(u, __ATOMIC_RELAXED)) {
+          __atomic_store_n(u, uint8_t(1), __ATOMIC_RELAXED);
+          if (!big) used_list[d].push_back(r[1 + d]);
+        }
         dead = dead || static_cast<size_t>(r[1 + d]) == C.node_vals[d].size();
       }
       if (dead) {
@@ -1301,11 +1304,17 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     w->t_off[1] = 1;
     for (int d = 0; d < 3; ++d) {
       t_index[d].assign(used[d].size(), -1);
-      for (size_t pos = 0; pos < used[d].size(); ++pos) {
-        if (!used[d][pos]) continue;
+      auto add_row = [&](size_t pos) {
         t_index[d][pos] = static_cast<int32_t>(w->t_dim.size());
         w->t_dim.push_back(d);
         w->t_thr.push_back(pos == C.node_vals[d].size() ? kNever : C.node_vals[d][pos]);
+      };
+      if (big) {
+        for (size_t pos = 0; pos < used[d].size(); ++pos)
+          if (used[d][pos]) add_row(pos);
+      } else {
+        std::sort(used_list[d].begin(), used_list[d].end());
+        for (int32_t pos : used_list[d]) add_row(static_cast<size_t>(pos));
       }
       w->t_off[d + 2] = static_cast<int32_t>(w->t_dim.size());
     }

@@ -78,6 +78,11 @@ struct sr_snapshot {
   std::vector<sr::SpotNode> nodes;
   std::vector<sr::NodeState> state;
   std::vector<sr::NodeState> saved;
+  // per spot node, contiguous (the encoder compares them with its cached views
+  // every call): name, static fingerprint (node_static_fp), state
+  // fingerprint (node_state_fp, kept current by AddPod / Revert)
+  std::vector<int32_t> node_names;
+  std::vector<uint64_t> node_sfp, node_dfp, saved_dfp;
   std::vector<sr::SnapPod> pods;  // every pod ever added (NodeState::pods index it)
   std::vector<int32_t> lkey, lval;  // the pods' labels (one arena: no allocation per pod)
   std::vector<int32_t> term_words;  // the pods' anti-affinity terms (one arena)
@@ -290,6 +295,10 @@ struct EncoderCache {
   } scratch;
   // ---- per-call counters (bench: what the last call had to rebuild)
   int32_t last_new_specs = 0, last_static_changed = 0, last_state_changed = 0;
+  // the last state refresh patched these nodes' records on top of generation
+  // patched_from (~0: it rebuilt them all); the planner uploads only those
+  std::vector<int32_t> patched_nodes;
+  uint64_t patched_from = ~0ull;
 
   void clear_content() {  // drops every content-interned dictionary
     spec_shards.clear();
@@ -378,5 +387,6 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
 // Fingerprint of a spot node's static part (name, unschedulable, labels,
 // taints): computed when the snapshot is created.
 uint64_t node_static_fp(const SpotNode& n);
+uint64_t node_state_fp(const SpotNode& sn, const NodeState& st);
 
 }  // namespace sr

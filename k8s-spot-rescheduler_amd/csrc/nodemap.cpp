@@ -200,6 +200,7 @@ void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t 
   snap_pod_from(c, pod, &s->pods.back(), s->lkey.data(), s->lval.data(), lab, &s->term_words);
   const SnapPod& sp = s->pods.back();
   state_add_pod(s->state[pos], c, pod, sp, store);
+  s->node_dfp[pos] = node_state_fp(s->nodes[pos], s->state[pos]);
   s->anti_total += sp.anti;
   s->opaque_total += sp.opaque;
   s->unknown_total += sp.meta ? 0 : 1;
@@ -215,6 +216,9 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
   s->id_unschedulable_key = c->id_unschedulable_key;
   s->nodes.resize(n_spot);
   s->state.resize(n_spot);
+  s->node_names.resize(n_spot);
+  s->node_sfp.resize(n_spot);
+  s->node_dfp.resize(n_spot);
   const sr_nodes& N = c->nodes;
   for (int32_t i = 0; i < n_spot; ++i) {  // validate first: the build below cannot fail
     const int32_t node = spot[i];
@@ -275,6 +279,9 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
         lab += s->pods[store].nlab;
         state_add_pod(s->state[i], c, idx[j], s->pods[store], store);
       }
+      s->node_names[i] = sn.name;
+      s->node_sfp[i] = sn.static_fp;
+      s->node_dfp[i] = node_state_fp(sn, s->state[i]);
     }
   });
   for (size_t ch = 0; ch < chunk_terms.size(); ++ch) {
@@ -328,6 +335,7 @@ sr_status sr_snapshot_fork(sr_snapshot* snap) {
   if (!snap) return SR_ERR_INVALID_ARG;
   if (snap->forked) return SR_ERR_STATE;  // DeltaClusterSnapshot forks one level deep
   snap->saved = snap->state;
+  snap->saved_dfp = snap->node_dfp;
   snap->fork_pods = snap->pods.size();
   snap->fork_labels = snap->lkey.size();
   snap->fork_terms = snap->term_words.size();
@@ -340,6 +348,7 @@ sr_status sr_snapshot_revert(sr_snapshot* snap) {
   if (!snap->forked) return SR_OK;  // Revert with nothing forked leaves the snapshot as is
   snap->state.swap(snap->saved);
   snap->saved.clear();
+  snap->node_dfp.swap(snap->saved_dfp);
   snap->pods.resize(snap->fork_pods);  // pods added since Fork are referenced by no state any more
   snap->lkey.resize(snap->fork_labels);
   snap->lval.resize(snap->fork_labels);

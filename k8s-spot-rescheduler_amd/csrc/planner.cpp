@@ -64,6 +64,7 @@ struct sr_ctx {
   int nranks = 1, rank = 0;
   FILE* prof_file = nullptr;  // SR_K2_PROFILE: per-wave K2 records appended per run
   int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
+  size_t patch_min_bytes = 512u << 10;  // SR_PATCH_MIN_BYTES: node sections below go up whole
   int32_t k2_scan_min = 2;    // SR_K2_SCAN_MIN: smallest node visit placed by prefix sums (65: never)
 };
 
@@ -165,7 +166,14 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, host_reserve(ctx->h_arena, bytes));
   const size_t arena_cap = ctx->arena.cap;
   HIP_TRY(ctx, dev_reserve(ctx->arena, bytes));  // a new allocation holds no node records
-  const bool nodes_resident = ctx->arena.cap == arena_cap && ctx->dev_state_gen == w.state_gen;
+  const bool same_arena = ctx->arena.cap == arena_cap;
+  const bool nodes_resident = same_arena && ctx->dev_state_gen == w.state_gen;
+  // a few nodes changed since the generation on the device: upload just their
+  // records (4 small copies each) instead of the whole node section
+  constexpr size_t kPatchNodes = 8;
+  const bool nodes_patch = !nodes_resident && same_arena && ctx->dev_state_gen == E.patched_from &&
+                           E.state_gen == w.state_gen && !E.patched_nodes.empty() &&
+                           E.patched_nodes.size() <= kPatchNodes && node_bytes > ctx->patch_min_bytes;
   const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
   HIP_TRY(ctx, dev_reserve(ctx->tables, n_rows * row_bytes));
@@ -176,8 +184,24 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t res_bytes = sizeof(uint64_t) * (sr::kResultHeader + static_cast<size_t>(std::max(1, w.max_cand_pods)));
   HIP_TRY(ctx, host_reserve(ctx->h_result, res_bytes));  // mapped: K3 writes the result straight to the host
   auto t1 = std::chrono::steady_clock::now();
-  const size_t from = nodes_resident ? node_bytes : 0;
+  const size_t from = nodes_resident || nodes_patch ? node_bytes : 0;
   pk.copy_to(static_cast<char*>(ctx->h_arena.p), from);
+  size_t patch_bytes = 0;
+  if (nodes_patch) {
+    char* hs = static_cast<char*>(ctx->h_arena.p);
+    char* ds = static_cast<char*>(ctx->arena.p);
+    const size_t NP = static_cast<size_t>(w.n_pad);
+    auto put = [&](size_t off, const void* src, size_t n) -> hipError_t {
+      std::memcpy(hs + off, src, n);
+      patch_bytes += n;
+      return hipMemcpyAsync(ds + off, hs + off, n, hipMemcpyHostToDevice, ctx->stream);
+    };
+    for (int32_t i : E.patched_nodes) {
+      HIP_TRY(ctx, put(o_nr + static_cast<size_t>(i) * 64, &E.node_rec[static_cast<size_t>(i) * 8], 64));
+      for (size_t dm = 0; dm < 3; ++dm)
+        HIP_TRY(ctx, put(o_nf + (dm * NP + static_cast<size_t>(i)) * 8, &E.node_free[dm * NP + i], 8));
+    }
+  }
   HIP_TRY(ctx, hipMemcpyAsync(static_cast<char*>(ctx->arena.p) + from, static_cast<char*>(ctx->h_arena.p) + from,
                               bytes - from, hipMemcpyHostToDevice, ctx->stream));
   if (!ctx->ev_upload) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_upload, hipEventDisableTiming));
@@ -238,7 +262,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   void* dres = nullptr;
   HIP_TRY(ctx, hipHostGetDevicePointer(&dres, ctx->h_result.p, 0));
   d.result = static_cast<uint64_t*>(dres);
-  ctx->t.bytes_uploaded = static_cast<uint64_t>(bytes - from);
+  ctx->t.bytes_uploaded = static_cast<uint64_t>(bytes - from + patch_bytes);
 
   const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
   // K0 algorithmic bytes: every table row written once; every atom row a class
@@ -462,6 +486,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   }
   if (const char* path = std::getenv("SR_K2_PROFILE")) ctx->prof_file = std::fopen(path, "ab");
   if (const char* m = std::getenv("SR_K2_MODE")) ctx->k2_mode = std::atoi(m) == 1 ? 1 : 0;
+  if (const char* m = std::getenv("SR_PATCH_MIN_BYTES")) ctx->patch_min_bytes = std::strtoull(m, nullptr, 10);
   if (const char* m = std::getenv("SR_K2_SCAN_MIN")) ctx->k2_scan_min = std::max(1, std::atoi(m));
   if (const char* b = std::getenv("SR_PREFIX_BATCH")) ctx->prefix_batch = std::max(1, std::atoi(b));
   *out = ctx;

@@ -131,10 +131,28 @@ def _snapshot(lib, sc, nm):
     return h
 
 
-def test_consecutive_ticks_one_node_changed(checker):
+@pytest.fixture(scope="module")
+def patch_checker():
+    """A planner that uploads changed node records one by one at any pool size
+    (SR_PATCH_MIN_BYTES=0; by default only node sections above 512 KiB are patched)."""
+    from spotplanner.planner import PredicateChecker
+    os.environ["SR_PATCH_MIN_BYTES"] = "0"
+    try:
+        c = PredicateChecker(0)
+    finally:
+        del os.environ["SR_PATCH_MIN_BYTES"]
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("which", ["default", "patch"])
+def test_consecutive_ticks_one_node_changed(checker, patch_checker, which):
     """Tick after tick on fresh snapshots of one cluster, each with one more
     pod placed on some spot node (its state changes, the static view not):
-    every full plan equals the oracle on the same mutated snapshot."""
+    every full plan equals the oracle on the same mutated snapshot.  `patch`:
+    the changed nodes' records go to the device one by one."""
+    other = checker
+    checker = patch_checker if which == "patch" else checker
     sc = SynthCluster(3, seed=21, n_on_demand=200, n_spot=450)
     lib = capi.load_planner()
     nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
@@ -151,6 +169,9 @@ def test_consecutive_ticks_one_node_changed(checker):
             osnap.lib.oracle_snapshot_add_pod(osnap.h, sc.ptr, pod, pos)
         p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
         t = checker.timing()
+        if which == "patch":  # the same tick through the default planner: its upload for comparison
+            plan_arrays(other, h, sc.ptr, cand_off, cand_pods)
+            up_default = other.timing().bytes_uploaded
         o = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
         assert np.array_equal(p.status, o["status"]), tick
         assert np.array_equal(p.node_of_pod, o["node_of_pod"]), tick
@@ -158,6 +179,9 @@ def test_consecutive_ticks_one_node_changed(checker):
         if tick >= 2:  # steady state: one node's state re-encoded, no spec is new
             assert t.enc_static_rebuilt == 0 and t.enc_state_nodes <= 2 and t.enc_new_specs == 0, \
                 (t.enc_static_rebuilt, t.enc_state_nodes, t.enc_new_specs)
+            if which == "patch":  # <= 2 node records (64 B + 3 free values each) instead of the section
+                n_pad = (len(nm.spot) + 127) // 128 * 128
+                assert up_default - t.bytes_uploaded >= n_pad * 88 - 256 - 2 * 88, (up_default, t.bytes_uploaded)
         lib.sr_snapshot_destroy(h)
 
 
