@@ -180,6 +180,14 @@ typedef struct {
   int32_t  id_metadata_name;  /* interned id of "metadata.name" (-1 if never interned) */
   int32_t  id_unschedulable_key; /* interned id of "node.kubernetes.io/unschedulable" (-1 if never interned) */
   const sr_pod_affinity *pod_affinity; /* NULL: required anti-affinity stays on the fallback path */
+  /* Integer values of the interned strings, for node-affinity Gt / Lt
+   * (labels.Requirement.Matches: strconv.ParseInt(s, 10, 64) of the node's label
+   * value and of the requirement's single value).  str_int_ok[id] = 1 when string
+   * `id` parses, str_int[id] its value; ids >= n_strings never parse.  NULL: a pod
+   * with Gt / Lt is routed to the fallback path. */
+  int32_t        n_strings;
+  const int64_t *str_int;
+  const uint8_t *str_int_ok;
 } sr_cluster;
 
 /* ------------------------------------------------------------- NewNodeMap */

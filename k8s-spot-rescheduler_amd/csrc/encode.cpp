@@ -209,8 +209,12 @@ void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
         if (P.expr_key[e] == c->id_empty) valid = false;  // validateLabelKey("") fails
         else if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) valid = false;
         else if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) valid = false;
-        else if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST)
+        else if (op == SR_OP_GT || op == SR_OP_LT) {  // exactly one value, an integer (labels.NewRequirement)
+          int64_t x;
+          valid = nv == 1 && str_int(c, P.expr_vals[P.expr_val_off[e]], &x);
+        } else if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST) {
           valid = false;
+        }
         if (valid) {
           put_req(term, REQ_LABEL_EXPR, P.expr_key[e], op, P.expr_vals + P.expr_val_off[e], nv);
           ++n;
@@ -397,8 +401,8 @@ const std::vector<int32_t>& label_column(EncoderCache& C, const sr_snapshot* sna
 
 // Node row of requirement `rw` = {type, key, op, vals...} over the static view:
 // Requirement.Matches on the node's labels, or the metadata.name field.
-void build_req_row(const EncoderCache& C, const sr_snapshot* snap, const int32_t* rw, size_t len,
-                   const std::vector<int32_t>* col, std::vector<uint64_t>& row) {
+void build_req_row(const EncoderCache& C, const sr_snapshot* snap, const sr_cluster* c, const int32_t* rw,
+                   size_t len, const std::vector<int32_t>* col, std::vector<uint64_t>& row) {
   const int32_t type = rw[0], key = rw[1], op = rw[2];
   const int32_t* vals = rw + 3;
   const size_t nv = len - 3;
@@ -414,14 +418,19 @@ void build_req_row(const EncoderCache& C, const sr_snapshot* snap, const int32_t
     }
     return;
   }
+  int64_t bound = 0;  // Gt / Lt: the requirement's integer (validated when the spec was drafted)
+  if (op == SR_OP_GT || op == SR_OP_LT) str_int(c, vals[0], &bound);
   for (int32_t n = 0; n < C.n_spot; ++n) {
     const int32_t v = (*col)[n];
     const bool has = v != INT32_MIN;
     bool m;
+    int64_t x;
     switch (op) {
       case SR_OP_IN: m = has && std::binary_search(vals, vals + nv, v); break;
       case SR_OP_NOT_IN: m = !has || !std::binary_search(vals, vals + nv, v); break;
       case SR_OP_EXISTS: m = has; break;
+      case SR_OP_GT: m = has && str_int(c, v, &x) && x > bound; break;  // a label that does not parse: false
+      case SR_OP_LT: m = has && str_int(c, v, &x) && x < bound; break;
       default: m = !has; break;  // DoesNotExist
     }
     if (m) set(n);
@@ -514,7 +523,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     if (P.aff_required[pod])
       for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t)
         for (int32_t e = P.term_expr_off[t]; e < P.term_expr_off[t + 1]; ++e)
-          if (P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT) return true;
+          if ((P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT) && !c->str_int) return true;
     return anti_opaque(c, pod) || aff_opaque(c, pod);  // required (anti-)affinity the encoded set cannot read
   };
   for (int32_t i = 0; i < nc; ++i)
@@ -1107,7 +1116,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     auto build = [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         const int32_t r = stale[i];
-        build_req_row(C, snap, C.req_dict.data(r), C.req_dict.len(r), cols[i], C.req_rows[r]);
+        build_req_row(C, snap, c, C.req_dict.data(r), C.req_dict.len(r), cols[i], C.req_rows[r]);
         C.req_row_gen[r] = C.static_gen;
       }
     };

@@ -107,6 +107,12 @@ inline bool add_overflows(int64_t a, int64_t b) {
 void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t pos);
 
 // The pod carries required anti-affinity terms.
+// strconv.ParseInt(string `id`, 10, 64) through the shim's table (false: does not parse / no table).
+inline bool str_int(const sr_cluster* c, int32_t id, int64_t* v) {
+  if (!c->str_int || !c->str_int_ok || id < 0 || id >= c->n_strings || !c->str_int_ok[id]) return false;
+  *v = c->str_int[id];
+  return true;
+}
 inline bool has_anti_terms(const sr_cluster* c, int32_t pod) {
   return (c->pods.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) ||
          (c->pod_affinity && c->pod_affinity->anti_off[pod + 1] > c->pod_affinity->anti_off[pod]);

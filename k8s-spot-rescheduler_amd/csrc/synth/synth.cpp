@@ -380,6 +380,9 @@ void sr_synth_view(const sr_synth* s, sr_cluster* c) {
   c->id_metadata_name = 1;
   c->id_unschedulable_key = 2;
   c->pod_affinity = nullptr;  // the BASELINE configs carry no pod (anti-)affinity
+  c->n_strings = 0;           // ... nor node-affinity Gt / Lt
+  c->str_int = nullptr;
+  c->str_int_ok = nullptr;
 }
 
 void sr_synth_drain(const sr_synth* s, sr_pod_drain* d) {

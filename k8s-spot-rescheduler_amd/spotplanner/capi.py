@@ -71,7 +71,8 @@ class sr_pod_affinity(ctypes.Structure):
 class sr_cluster(ctypes.Structure):
     _fields_ = [("nodes", sr_nodes), ("pods", sr_pods), ("id_empty", ctypes.c_int32),
                 ("id_metadata_name", ctypes.c_int32), ("id_unschedulable_key", ctypes.c_int32),
-                ("pod_affinity", ctypes.POINTER(sr_pod_affinity))]
+                ("pod_affinity", ctypes.POINTER(sr_pod_affinity)), ("n_strings", ctypes.c_int32),
+                ("str_int", ctypes.POINTER(ctypes.c_int64)), ("str_int_ok", ctypes.POINTER(ctypes.c_uint8))]
 
 
 class sr_node_label(ctypes.Structure):
@@ -162,6 +163,10 @@ def make_cluster_struct(A) -> sr_cluster:
     c.id_empty = A["id_empty"]
     c.id_metadata_name = A["id_metadata_name"]
     c.id_unschedulable_key = A["id_unschedulable_key"]
+    if A.get("str_int") is not None:
+        c.n_strings = len(A["str_int"])
+        c.str_int = ptr(A["str_int"], P64)
+        c.str_int_ok = ptr(A["str_int_ok"], PU8)
     if A.get("pa_ns") is not None:
         pa = sr_pod_affinity()
         for f in ("ns", "label_off", "label_key", "label_val", "anti_off", "topology_key", "ns_off", "ns_ids",

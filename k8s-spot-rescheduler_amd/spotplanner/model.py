@@ -10,6 +10,7 @@ pod and set fallback flags for features the encoded predicate set lacks.
 from __future__ import annotations
 
 import ctypes
+import re
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -244,13 +245,32 @@ def pod_flags(pod: Pod) -> int:
     return f
 
 
+_INT64 = re.compile(r"[+-]?[0-9]+\Z")
+
+
+def parse_int64(s: str):
+    """strconv.ParseInt(s, 10, 64): optional sign, decimal digits, in range; None otherwise."""
+    if not _INT64.match(s):
+        return None
+    v = int(s)
+    return v if -(1 << 63) <= v < (1 << 63) else None
+
+
+def string_ints(interner: Interner):
+    """sr_cluster.str_int / str_int_ok over the interner's strings (node-affinity Gt / Lt)."""
+    vals = [parse_int64(s) for s in interner.strings]
+    return (np.ascontiguousarray([0 if v is None else v for v in vals], dtype=np.int64).reshape(-1),
+            np.ascontiguousarray([v is not None for v in vals], dtype=np.uint8).reshape(-1))
+
+
 class EncodedCluster:
     """numpy arrays in the sr_cluster layout + the ctypes struct pointing at them."""
 
     def __init__(self, arrays: dict, interner: Interner):
         self.a = arrays
         self.interner = interner
-        self.struct = capi.make_cluster_struct(arrays)
+        self.a["str_int"], self.a["str_int_ok"] = string_ints(interner)
+        self.struct = capi.make_cluster_struct(self.a)
 
     @property
     def ptr(self):

@@ -632,6 +632,14 @@ static int o_in_values(const int32_t *vals, int32_t lo, int32_t hi, int32_t v) {
   return 0;
 }
 
+/* strconv.ParseInt(string id, 10, 64), through the shim's table of the
+ * interned strings' integer values (sr_cluster.str_int). */
+static int o_str_int(const sr_cluster *c, int32_t id, int64_t *v) {
+  if (!c->str_int || !c->str_int_ok || id < 0 || id >= c->n_strings || !c->str_int_ok[id]) return 0;
+  *v = c->str_int[id];
+  return 1;
+}
+
 /* labels.NewRequirement validation + Requirement.Matches [upstream apimachinery labels]. */
 static int o_expr_valid(const sr_cluster *c, int32_t e) {
   const sr_pods *P = &c->pods;
@@ -644,8 +652,14 @@ static int o_expr_valid(const sr_cluster *c, int32_t e) {
     case SR_OP_EXISTS:
     case SR_OP_DOES_NOT_EXIST:
       return nv == 0;
+    case SR_OP_GT:
+    case SR_OP_LT: {
+      /* labels.NewRequirement: exactly one value, and it parses as an int64 */
+      int64_t x;
+      return nv == 1 && o_str_int(c, P->expr_vals[P->expr_val_off[e]], &x);
+    }
     default:
-      return 0; /* Gt/Lt are routed to fallback before we get here; others invalid */
+      return 0; /* unknown operator: the term fails to build */
   }
 }
 
@@ -654,7 +668,12 @@ static int o_expr_match(const sr_cluster *c, int32_t e, int32_t node) {
   int32_t v;
   int has = o_node_label(c, node, P->expr_key[e], &v);
   int32_t lo = P->expr_val_off[e], hi = P->expr_val_off[e + 1];
+  int64_t lv, rv;
   switch (P->expr_op[e]) {
+    case SR_OP_GT: /* labels.Requirement.Matches: the node's value must parse too */
+      return has && o_str_int(c, v, &lv) && o_str_int(c, P->expr_vals[lo], &rv) && lv > rv;
+    case SR_OP_LT:
+      return has && o_str_int(c, v, &lv) && o_str_int(c, P->expr_vals[lo], &rv) && lv < rv;
     case SR_OP_IN:
       return has && o_in_values(P->expr_vals, lo, hi, v);
     case SR_OP_NOT_IN:
@@ -896,7 +915,7 @@ int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c,
   if (P->aff_required[pod])
     for (int32_t t = P->term_off[pod]; t < P->term_off[pod + 1]; t++)
       for (int32_t e = P->term_expr_off[t]; e < P->term_expr_off[t + 1]; e++)
-        if (P->expr_op[e] == SR_OP_GT || P->expr_op[e] == SR_OP_LT) return 1;
+        if ((P->expr_op[e] == SR_OP_GT || P->expr_op[e] == SR_OP_LT) && !c->str_int) return 1;
   return 0;
 }
 

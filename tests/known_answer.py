@@ -180,6 +180,25 @@ def _affinity():
     yield Case("match_fields_and_expressions", mt,
                aff(T(("zone", "Exists", []), fields=[("metadata.name", "NotIn", ["a"])])), nodes3, [[], [], []],
                [False, True, False])
+    # Gt / Lt: Requirement.Matches parses the node's value with strconv.ParseInt(v, 10, 64) (a value that
+    # does not parse, or a missing key, fails); NewRequirement needs exactly one value that parses
+    gt = mt + "; Gt/Lt: ParseInt of the node's label value against the single integer value"
+    gen = [N("g1", labels={"gen": "7"}), N("g2", labels={"gen": "+12"}), N("g3", labels={"gen": "-3"}),
+           N("g4", labels={"gen": "x9"}), N("g5", labels={})]
+    none = [[] for _ in gen]
+    yield Case("gt_integer_labels", gt, aff(T(("gen", "Gt", ["6"]))), gen, none, [True, True, False, False, False])
+    yield Case("lt_integer_labels", gt, aff(T(("gen", "Lt", ["7"]))), gen, none, [False, False, True, False, False])
+    yield Case("gt_is_strict_and_signed", gt, aff(T(("gen", "Gt", ["-3"]))), gen, none,
+               [True, True, False, False, False])
+    yield Case("gt_value_with_leading_zero_and_sign", gt, aff(T(("gen", "Lt", ["+012"]))), gen, none,
+               [True, False, True, False, False])
+    yield Case("gt_non_integer_value_fails_its_term", gt + "; a value that does not parse fails NewRequirement",
+               aff(T(("gen", "Gt", ["six"])), T(("gen", "Lt", ["0"]))), gen, none,
+               [False, False, True, False, False])
+    yield Case("gt_two_values_fails_its_term", gt + "; exactly one value", aff(T(("gen", "Gt", ["1", "2"]))), gen,
+               none, [False, False, False, False, False])
+    yield Case("gt_anded_with_in", gt, aff(T(("gen", "Gt", ["0"]), ("gen", "NotIn", ["7"]))), gen, none,
+               [False, True, False, False, False])
 
 
 def _ports():

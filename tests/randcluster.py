@@ -12,6 +12,7 @@ from spotplanner.model import (Container, ContainerPort, GiB, LabelSelector, Lab
                                Taint, Toleration)
 
 KEYS = ["zone", "type", "team", "disk", "gpu"]
+GENS = ["1", "2", "10", "-3", "+4", "07", "x", ""]  # node label values (some do not parse as int64)
 VALS = ["a", "b", "c", ""]
 EFFECTS = ["NoSchedule", "NoExecute", "PreferNoSchedule"]
 
@@ -22,6 +23,8 @@ def rand_node(r: random.Random, name: str, features: bool) -> Node:
         for k in KEYS:
             if r.random() < 0.5:
                 labels[k] = r.choice(VALS)
+        if r.random() < 0.6:  # an integer-ish label for node-affinity Gt / Lt
+            labels["gen"] = r.choice(GENS)
     taints = []
     if features and r.random() < 0.3:
         for _ in range(r.randint(1, 2)):
@@ -50,11 +53,16 @@ def rand_pod(r: random.Random, name: str, features: bool, fallback: bool = False
             for _ in range(r.randint(0, 3)):
                 exprs = []
                 for _ in range(r.randint(0, 2)):
-                    op = r.choice(["In", "NotIn", "Exists", "DoesNotExist", "Bogus"])
-                    vals = [] if op in ("Exists", "DoesNotExist") else r.sample(VALS, r.randint(1, 2))
+                    op = r.choice(["In", "NotIn", "Exists", "DoesNotExist", "Bogus", "Gt", "Lt"])
+                    key = r.choice(KEYS)
+                    if op in ("Gt", "Lt"):  # integer compares on the "gen" label (some values invalid)
+                        key = "gen" if r.random() < 0.8 else key
+                        vals = [r.choice(["2", "-1", "07", "+3", "x"])]
+                    else:
+                        vals = [] if op in ("Exists", "DoesNotExist") else r.sample(VALS, r.randint(1, 2))
                     if r.random() < 0.05:  # invalid arity
                         vals = [] if vals else ["a"]
-                    exprs.append(NodeSelectorRequirement(r.choice(KEYS), op, vals))
+                    exprs.append(NodeSelectorRequirement(key, op, vals))
                 fields = []
                 if r.random() < 0.2:
                     fields.append(NodeSelectorRequirement(r.choice(["metadata.name", "metadata.uid"]),
