@@ -118,7 +118,7 @@ class LowerBound {
 // The raw static spec of a pod: nodeSelector, required node affinity,
 // tolerations, host ports (with their host IP).
 template <class F>
-void for_each_spec_word(const sr_pods& P, int32_t pod, F&& f) {
+void for_each_spec_word(const sr_cluster* c, const sr_pods& P, int32_t pod, F&& f) {
   const int32_t s0 = P.sel_off[pod], s1 = P.sel_off[pod + 1];
   f(s1 - s0);
   for (int32_t i = s0; i < s1; ++i) {
@@ -135,6 +135,13 @@ void for_each_spec_word(const sr_pods& P, int32_t pod, F&& f) {
         f(P.expr_op[e]);
         f(P.expr_val_off[e + 1] - P.expr_val_off[e]);
         for (int32_t v = P.expr_val_off[e]; v < P.expr_val_off[e + 1]; ++v) f(P.expr_vals[v]);
+        if (P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT)  // the values' integers, not only their ids
+          for (int32_t v = P.expr_val_off[e]; v < P.expr_val_off[e + 1]; ++v) {
+            int64_t x = 0;
+            f(str_int(c, P.expr_vals[v], &x) ? 1 : 0);
+            f(static_cast<int32_t>(static_cast<uint64_t>(x)));
+            f(static_cast<int32_t>(static_cast<uint64_t>(x) >> 32));
+          }
       }
       f(P.term_field_off[t + 1] - P.term_field_off[t]);
       for (int32_t g = P.term_field_off[t]; g < P.term_field_off[t + 1]; ++g) {
@@ -215,7 +222,14 @@ void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
         } else if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST) {
           valid = false;
         }
-        if (valid) {
+        if (valid && (op == SR_OP_GT || op == SR_OP_LT)) {  // {value id, its integer (lo, hi)}
+          int64_t x = 0;
+          str_int(c, P.expr_vals[P.expr_val_off[e]], &x);
+          const int32_t w[3] = {P.expr_vals[P.expr_val_off[e]], static_cast<int32_t>(static_cast<uint64_t>(x)),
+                                static_cast<int32_t>(static_cast<uint64_t>(x) >> 32)};
+          term.insert(term.end(), {6, REQ_LABEL_EXPR, P.expr_key[e], op, w[0], w[1], w[2]});
+          ++n;
+        } else if (valid) {
           put_req(term, REQ_LABEL_EXPR, P.expr_key[e], op, P.expr_vals + P.expr_val_off[e], nv);
           ++n;
         }
@@ -418,8 +432,11 @@ void build_req_row(const EncoderCache& C, const sr_snapshot* snap, const sr_clus
     }
     return;
   }
-  int64_t bound = 0;  // Gt / Lt: the requirement's integer (validated when the spec was drafted)
-  if (op == SR_OP_GT || op == SR_OP_LT) str_int(c, vals[0], &bound);
+  // Gt / Lt: {value id, its integer (lo, hi)}, validated when the spec was drafted
+  const int64_t bound = (op == SR_OP_GT || op == SR_OP_LT) && nv == 3
+                            ? static_cast<int64_t>(static_cast<uint64_t>(static_cast<uint32_t>(vals[1])) |
+                                                   static_cast<uint64_t>(static_cast<uint32_t>(vals[2])) << 32)
+                            : 0;
   for (int32_t n = 0; n < C.n_spot; ++n) {
     const int32_t v = (*col)[n];
     const bool has = v != INT32_MIN;
@@ -439,11 +456,14 @@ void build_req_row(const EncoderCache& C, const sr_snapshot* snap, const sr_clus
 
 }  // namespace
 
-uint64_t node_static_fp(const SpotNode& n) {
+uint64_t node_static_fp(const SpotNode& n, const sr_cluster* c) {
   uint64_t h = mix(mix(0xC0FFEEull, static_cast<uint32_t>(n.name)), n.unschedulable);
   uint64_t labels = 0, taints = 0;  // order-independent sums (Go map iteration order varies)
-  for (const auto& kv : n.labels)
-    labels += mix(mix(0x1AB3ull, static_cast<uint32_t>(kv.first)), static_cast<uint32_t>(kv.second));
+  for (const auto& kv : n.labels) {
+    int64_t x = 0;  // Gt / Lt read the value's integer: part of the node's static content
+    const uint64_t iv = str_int(c, kv.second, &x) ? mix(0x17ull, static_cast<uint64_t>(x)) : 0;
+    labels += mix(mix(mix(0x1AB3ull, static_cast<uint32_t>(kv.first)), static_cast<uint32_t>(kv.second)), iv);
+  }
   for (const TaintRec& t : n.taints)
     taints += mix(mix(mix(0x7A1Eull, static_cast<uint32_t>(t.key)), static_cast<uint32_t>(t.val)),
                   static_cast<uint32_t>(t.effect));
@@ -769,7 +789,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         spec_woff[q] = static_cast<uint32_t>(b0);
         const int32_t pod = active_pod[q];
         if (!has_static_spec(P, pod)) continue;  // spec 0
-        for_each_spec_word(P, pod, [&](int32_t x) { buf.push_back(x); });
+        for_each_spec_word(c, P, pod, [&](int32_t x) { buf.push_back(x); });
         const uint64_t h = hash_words(buf.data() + b0, buf.size() - b0);
         spec_hash[q] = h;
         const size_t sh = static_cast<size_t>(((h >> 32) * kSpecShards) >> 32);

@@ -392,7 +392,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
 
 // Fingerprint of a spot node's static part (name, unschedulable, labels,
 // taints): computed when the snapshot is created.
-uint64_t node_static_fp(const SpotNode& n);
+uint64_t node_static_fp(const SpotNode& n, const sr_cluster* c);
 uint64_t node_state_fp(const SpotNode& sn, const NodeState& st);
 
 }  // namespace sr

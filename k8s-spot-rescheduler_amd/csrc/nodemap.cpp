@@ -270,7 +270,7 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
         sn.labels.emplace_back(N.label_key[j], N.label_val[j]);
       for (int32_t j = N.taint_off[node]; j < N.taint_off[node + 1]; ++j)
         sn.taints.push_back(TaintRec{N.taint_key[j], N.taint_val[j], N.taint_effect[j]});
-      sn.static_fp = node_static_fp(sn);
+      sn.static_fp = node_static_fp(sn, c);
       s->state[i].pods.reserve(static_cast<size_t>(off[node + 1] - off[node]));
       uint32_t lab = lbase[i];
       for (int32_t j = off[node]; j < off[node + 1]; ++j) {
