@@ -347,6 +347,8 @@ struct K2Lds {
 struct K2Stats {
   uint32_t n_spec_miss = 0, n_min = 0, n_far = 0;
   uint64_t cyc_a = 0, cyc_b = 0, cyc_c = 0, cyc_d = 0;
+  // node order (profile builds): run-pass iterations / pod-by-pod rounds, and the visits taking each
+  uint32_t run_it = 0, seq_it = 0, run_visits = 0, seq_visits = 0;
 };
 
 // One candidate's canDrainNode with 64 * SPL touched-node slots.  Returns the
@@ -689,13 +691,14 @@ __device__ __forceinline__ uint32_t from_lane(uint32_t v, int src) {
 template <bool E, bool O>
 __device__ __forceinline__ uint64_t place_seq(uint64_t P, int lane, int64_t rc, int64_t rm, int64_t re, uint64_t pm,
                                               uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
-                                              uint64_t& ports, int& left, uint64_t swap_mask) {
+                                              uint64_t& ports, int& left, uint64_t swap_mask, uint32_t& it) {
   uint64_t placed = 0;
   uint64_t rest = left >= 1 ? P : 0ull;
   // One exit branch per placement: the checks are unconditional (lane masks
   // straight from the compares); pods below the one placed that did not fit
   // failed at n.
   for (;;) {
+    ++it;
     uint64_t res = ballot(rc <= cpu) & ballot(rm <= mem);
     res &= E ? ballot(re <= eph) : (eph >= 0 ? ~0ull : 0ull);
     uint64_t fm = rest & (zm | res);
@@ -723,9 +726,10 @@ __device__ __forceinline__ uint64_t place_seq(uint64_t P, int lane, int64_t rc, 
 template <bool E, bool O>
 __device__ __forceinline__ uint64_t place_runs(uint64_t P, int lane, int64_t rc, int64_t rm, int64_t re, uint64_t pm,
                                                uint64_t sb, uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
-                                               uint64_t& ports, int& left) {
+                                               uint64_t& ports, int& left, uint32_t& it) {
   uint64_t placed = 0;
   while (P != 0 && left >= 1) {
+    ++it;
     const bool in = (P >> lane) & 1;
     const int64_t ic = scan_add(in ? rc : 0), im = scan_add(in ? rm : 0);
     const int64_t ie = E ? scan_add(in ? re : 0) : 0;
@@ -767,15 +771,20 @@ __device__ __forceinline__ uint64_t place_runs(uint64_t P, int lane, int64_t rc,
 // between (measured on C5: specialising all four E / O combinations cost 5 %).
 __device__ __forceinline__ uint64_t place_at(const DevWorkload& w, uint64_t P, int lane, int64_t rc, int64_t rm,
                                              int64_t re, uint64_t pm, uint64_t zm, int64_t& cpu, int64_t& mem,
-                                             int64_t& eph, uint64_t& ports, int& left) {
+                                             int64_t& eph, uint64_t& ports, int& left, K2Stats& st) {
   const bool E = (ballot(re != 0) & P) != 0;  // some pod asks for ephemeral storage
   const bool O = (ballot(pm != 0) & P) != 0;  // some pod sets / meets state bits
-  if (O) return place_seq<true, true>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
-  if (__builtin_popcountll(P) >= w.k2_scan_min) {
-    if (E) return place_runs<true, false>(P, lane, rc, rm, re, pm, 0ull, zm, cpu, mem, eph, ports, left);
-    return place_runs<false, false>(P, lane, rc, rm, re, pm, 0ull, zm, cpu, mem, eph, ports, left);
+  if (O) {
+    ++st.seq_visits;
+    return place_seq<true, true>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask, st.seq_it);
   }
-  return place_seq<true, false>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask);
+  if (__builtin_popcountll(P) >= w.k2_scan_min) {
+    ++st.run_visits;
+    if (E) return place_runs<true, false>(P, lane, rc, rm, re, pm, 0ull, zm, cpu, mem, eph, ports, left, st.run_it);
+    return place_runs<false, false>(P, lane, rc, rm, re, pm, 0ull, zm, cpu, mem, eph, ports, left, st.run_it);
+  }
+  ++st.seq_visits;
+  return place_seq<true, false>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask, st.seq_it);
 }
 
 template <int G, bool PROF>
@@ -1000,7 +1009,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       const uint64_t cand = ballot(((act[g] >> lane) & 1) && ptr[g] == n);
       uint64_t placed = 0;
       if (cand != 0) {  // wave-uniform
-        placed = place_at(w, cand, lane, rc[g], rm[g], re[g], pm[g], zm[g], cpu, mem, eph, ports, left);
+        placed = place_at(w, cand, lane, rc[g], rm[g], re[g], pm[g], zm[g], cpu, mem, eph, ports, left, st);
         placements += __builtin_popcountll(placed);
       }
       if ((placed >> lane) & 1) node[g] = n;
@@ -1332,6 +1341,10 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
       pr[9] = st.cyc_b;
       pr[10] = st.cyc_c;
       pr[11] = st.cyc_d;
+      if (wide == 2) {  // node order: placement passes
+        pr[12] = static_cast<uint64_t>(st.run_it) | static_cast<uint64_t>(st.seq_it) << 32;
+        pr[13] = static_cast<uint64_t>(st.run_visits) | static_cast<uint64_t>(st.seq_visits) << 32;
+      }
     }
   }
 }

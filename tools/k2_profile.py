@@ -83,17 +83,25 @@ def main():
     print("spec misses total %d, wave_min total %d, far chunks total %d" %
           (r[:, 6].sum(), (r[:, 7] & 0xffffffff).sum(), (r[:, 7] >> 32).sum()))
     tot = r[:, 8:13].sum(axis=0)
+    if not (~nodeo).any():
+        tot[4] = 0  # node-order records hold placement counters there
     st = max(1, (steps[~nodeo] if (~nodeo).any() else steps).sum())
     print("cycles/step by section a,b,c,d,spec-wait:", " ".join("%.0f" % (x / st) for x in tot))
     last = np.argsort(-end)[:8]
     full = runs[last_run].astype(np.int64)
+    nodeo_rows = full[full[:, 5] == 2] if len(full) else full
+    if len(nodeo_rows):
+        ri, si = nodeo_rows[:, 12] & 0xffffffff, nodeo_rows[:, 12] >> 32
+        rv, sv = nodeo_rows[:, 13] & 0xffffffff, nodeo_rows[:, 13] >> 32
+        print("node order placement: run-pass visits %d (%.2f passes each), pod-by-pod visits %d (%.2f rounds each)"
+              % (rv.sum(), ri.sum() / max(1, rv.sum()), sv.sum(), si.sum() / max(1, sv.sum())))
     print("latest-ending waves: wave start_us dur_us steps mode | visits placements windows | "
-          "cycles: prologue min+state placement moves")
+          "cycles: prologue min+state placement moves | run visits/passes seq visits/rounds")
     for c in last:
         f = full[c]
-        print("  %5d %6.2f %6.2f %4d %2d | %3d %3d %3d | %6d %6d %6d %6d"
+        print("  %5d %6.2f %6.2f %4d %2d | %3d %3d %3d | %6d %6d %6d %6d | %3d/%3d %3d/%3d"
               % (c, start[c], dur[c], steps[c], mode[c], f[7] & 0xffffffff, f[6], f[7] >> 32,
-                 f[8], f[9], f[10], f[11]))
+                 f[8], f[9], f[10], f[11], f[13] & 0xffffffff, f[12] & 0xffffffff, f[13] >> 32, f[12] >> 32))
 
 
 if __name__ == "__main__":
