@@ -11,5 +11,5 @@ for cfg in 3 5; do
   SR_K2_PROFILE="gpurun_out/$T/k2prof_c$cfg.bin" timeout -k 10 300 python bench.py --config $cfg --steps 3 --warmup 3 \
     --no-cpu-baseline > gpurun_out/$T/bench_prof_c$cfg.log 2>&1 || exit $?
   python tools/k2_profile.py gpurun_out/$T/k2prof_c$cfg.bin > gpurun_out/$T/k2prof_c$cfg.txt 2>&1
-  echo "== C$cfg"; tail -13 gpurun_out/$T/k2prof_c$cfg.txt
+  echo "== C$cfg"; tail -13 gpurun_out/$T/k2prof_c$cfg.txt; rm -f gpurun_out/$T/k2prof_c$cfg.bin
 done
