@@ -117,7 +117,8 @@ def rand_selector(r: random.Random, valid_only: bool = False):
     return LabelSelector({}, [LabelSelectorRequirement("tier", "In", [])])  # invalid: fallback
 
 
-def rand_anti(r: random.Random, p: Pod, rate: float, hostname_only: bool = False, shared_keys: bool = False):
+def rand_anti(r: random.Random, p: Pod, rate: float, hostname_only: bool = False, shared_keys: bool = False,
+              valid_only: bool = False):
     """Labels and namespace for every pod; required anti-affinity for some.
     Topology keys: the hostname (node-local) mostly, zone / team (shared or
     missing on some nodes) otherwise (always with shared_keys)."""
@@ -130,7 +131,7 @@ def rand_anti(r: random.Random, p: Pod, rate: float, hostname_only: bool = False
         for _ in range(r.randint(1, 2)):
             tk = HOST if hostname_only or (not shared_keys and r.random() < 0.7) else r.choice(["zone", "team"])
             ns = [] if r.random() < 0.7 else r.sample(["default", "other"], r.randint(1, 2))
-            p.pod_anti_affinity.append(PodAffinityTerm(tk, rand_selector(r, hostname_only), ns))
+            p.pod_anti_affinity.append(PodAffinityTerm(tk, rand_selector(r, hostname_only or valid_only), ns))
 
 
 def rand_aff(r: random.Random, p: Pod, rate: float, shared_keys: bool = False):
@@ -146,12 +147,13 @@ def rand_aff(r: random.Random, p: Pod, rate: float, shared_keys: bool = False):
 
 def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 8, features: bool = True,
                   fallback: bool = False, anti: float = 0.0, hostname_only: bool = False, aff: float = 0.0,
-                  shared_keys: bool = False):
+                  shared_keys: bool = False, valid_selectors: bool = False):
     """Returns (spot_nodes, spot_pods, candidates) with candidates a list of pod lists.
     anti > 0: pods carry namespaces / labels and that share required pod anti-affinity
     (hostname_only: every term on kubernetes.io/hostname with a valid selector).
     aff > 0: that share of the pods (spot and candidate) carries required pod affinity.
-    shared_keys: every inter-pod term on zone / team (shared domains)."""
+    shared_keys: every inter-pod term on zone / team (shared domains).
+    valid_selectors: no selector that LabelSelectorAsSelector rejects (those send candidates to fallback)."""
     r = random.Random(seed)
     nodes = [rand_node(r, "n%d" % i, features) for i in range(n_spot)]
     spot_pods = []
@@ -165,7 +167,7 @@ def rand_scenario(seed: int, n_spot: int = 12, n_cand: int = 8, max_pods: int = 
     if anti > 0 or aff > 0:
         for ps in spot_pods + cands:
             for p in ps:
-                rand_anti(r, p, anti, hostname_only, shared_keys)
+                rand_anti(r, p, anti, hostname_only, shared_keys, valid_selectors)
     if aff > 0:
         for ps in spot_pods + cands:
             for p in ps:
