@@ -536,10 +536,17 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
 
   // ---- pass 1: candidate-level fallback (host-decided)
   w->status_host.assign(static_cast<size_t>(nc), STATUS_PENDING);
-  auto pod_fallback = [&](int32_t pod) {
+  // the candidate pods' requests, gathered once in input order (the per-pod
+  // pass later reads them sequentially instead of from the cluster arrays)
+  std::vector<int64_t>& req_flat = C.scratch.req_flat;
+  req_flat.resize(static_cast<size_t>(w->n_input_pods) * 3);
+  auto pod_fallback = [&](int32_t pod, int32_t j) {
     if (P.flags[pod] & SR_POD_FB_MASK) return true;
-    if (!in_range(P.req_milli_cpu[pod]) || !in_range(P.req_memory[pod]) || !in_range(P.req_ephemeral[pod]))
-      return true;
+    int64_t* rq = &req_flat[static_cast<size_t>(j - w->pod_base) * 3];
+    rq[0] = P.req_milli_cpu[pod];
+    rq[1] = P.req_memory[pod];
+    rq[2] = P.req_ephemeral[pod];
+    if (!in_range(rq[0]) || !in_range(rq[1]) || !in_range(rq[2])) return true;
     if (P.aff_required[pod])
       for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t)
         for (int32_t e = P.term_expr_off[t]; e < P.term_expr_off[t + 1]; ++e)
@@ -571,7 +578,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
       // an existing pod's opaque anti-affinity may select any incoming pod
       bool fb = (c->pod_affinity ? snap->opaque_total : snap->anti_total) > 0 || (e - b) > MAX_CAND_PODS;
-      for (int32_t j = b; j < e && !fb; ++j) fb = pod_fallback(cands->cand_pods[j]);
+      for (int32_t j = b; j < e && !fb; ++j) fb = pod_fallback(cands->cand_pods[j], j);
       if (fb) w->status_host[i] = SR_CAND_FALLBACK;
       for (int32_t j = b; j < e && !fb && !cand_ports[i]; ++j)
         cand_ports[i] = P.port_off[cands->cand_pods[j]] != P.port_off[cands->cand_pods[j] + 1];
@@ -1286,8 +1293,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   pfor(static_cast<size_t>(na), 2048, [&](size_t lo, size_t hi) {
     bool chunk_dead = false;  // one shared store per chunk, not per pod
     for (size_t q = lo; q < hi; ++q) {
-      const int32_t pod = active_pod[q];
-      const int64_t rc = P.req_milli_cpu[pod], rm = P.req_memory[pod], re = P.req_ephemeral[pod];
+      const int64_t* rq = &req_flat[static_cast<size_t>(active_src[q] - w->pod_base) * 3];
+      const int64_t rc = rq[0], rm = rq[1], re = rq[2];
       const bool zero = rc == 0 && rm == 0 && re == 0;
       const int32_t ki = key_slot[pod_key[q]];
       int32_t* r = &w->pod_rows[q * 4];

@@ -296,6 +296,7 @@ struct EncoderCache {
     std::vector<uint8_t> cand_ports, spec_shard, key_seen;
     std::vector<int32_t> active_pod, active_src, act_of, pod_spec, pod_key, key_slot, psig_class;
     std::vector<uint64_t> spec_hash;
+    std::vector<int64_t> req_flat;  // [input candidate pod][3] requests (cpu, memory, ephemeral)
     std::vector<uint32_t> spec_woff;
     std::vector<std::vector<int32_t>> spec_words, chunk_shard;
   } scratch;
