@@ -801,7 +801,11 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         spec_hash[q] = h;
         const size_t sh = static_cast<size_t>(((h >> 32) * kSpecShards) >> 32);
         spec_shard[q] = static_cast<uint8_t>(sh);
-        mine[sh].push_back(static_cast<int32_t>(q));
+        // known specs resolve here, read-only, while the words are hot; the
+        // shard pass below interns the rest
+        const int32_t local = C.spec_shards[sh].dict.find(buf.data() + b0, buf.size() - b0, h);
+        if (local >= 0) pod_spec[q] = local;
+        else mine[sh].push_back(static_cast<int32_t>(q));
       }
       buf.swap(spec_words[ch]);
       for (size_t sh = 0; sh < kSpecShards; ++sh) mine[sh].swap(chunk_shard[ch * kSpecShards + sh]);
@@ -843,9 +847,19 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       new_spec_pod.push_back(active_pod[q]);
     }
   C.last_new_specs = static_cast<int32_t>(new_spec_pod.size());
+  const int32_t n_spec_ids = spec0 + static_cast<int32_t>(new_spec_pod.size());
+  const bool combos = anti.active || aff.active;
+  // keys present in this call (pods without inter-pod terms: the spec id),
+  // flagged here with the global ids; read first: a shared line written by
+  // every thread would bounce
+  std::vector<uint8_t>& key_seen = X.key_seen;
+  key_seen.assign(static_cast<size_t>(n_spec_ids), 0);
   pfor(static_cast<size_t>(na), 4096, [&](size_t lo, size_t hi) {
-    for (size_t q = lo; q < hi; ++q)
-      pod_spec[q] = spec_shard[q] == 0xff ? 0 : C.spec_shards[spec_shard[q]].global[pod_spec[q]];
+    for (size_t q = lo; q < hi; ++q) {
+      const int32_t g = spec_shard[q] == 0xff ? 0 : C.spec_shards[spec_shard[q]].global[pod_spec[q]];
+      pod_spec[q] = g;
+      if (!combos && !__atomic_load_n(&key_seen[g], __ATOMIC_RELAXED)) __atomic_store_n(&key_seen[g], uint8_t(1), __ATOMIC_RELAXED);
+    }
   });
   if (!new_spec_pod.empty()) {
     std::vector<SpecDraft> drafts(new_spec_pod.size());
@@ -875,13 +889,18 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       sp.ports.swap(d.ports);
     }
   }
+  for (size_t id = C.spec_req_off.size() - 1; id < C.spec.size(); ++id) {
+    const SpecInfo& sp = C.spec[id];
+    C.spec_req.insert(C.spec_req.end(), sp.sel.begin(), sp.sel.end());
+    for (size_t i = 0; i < sp.terms.size(); i += 1 + static_cast<size_t>(sp.terms[i]))
+      C.spec_req.insert(C.spec_req.end(), sp.terms.begin() + i + 1, sp.terms.begin() + i + 1 + sp.terms[i]);
+    C.spec_req_off.push_back(static_cast<uint32_t>(C.spec_req.size()));
+  }
   phase(7);
 
   // ---- class keys: the static spec, plus (with inter-pod affinity) the pod's
   // anti-affinity term ids and affinity set of this call.  Pods without either
   // use their spec id as key.
-  const int32_t n_spec_ids = static_cast<int32_t>(C.spec.size());
-  const bool combos = anti.active || aff.active;
   std::vector<int32_t>& pod_key_buf = X.pod_key;
   std::vector<int32_t> key_spec;               // keys >= n_spec_ids: spec of the combined key,
   std::vector<std::vector<int32_t>> key_anti;  // ... its anti-affinity term ids
@@ -915,14 +934,15 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   const std::vector<int32_t>& pod_key = combos ? pod_key_buf : pod_spec;
   // distinct keys of this call, in key order: flags set in parallel, slots serially
   const size_t n_key_ids = static_cast<size_t>(n_spec_ids) + key_spec.size();
-  std::vector<uint8_t>& key_seen = X.key_seen;
-  key_seen.assign(n_key_ids, 0);
-  pfor(static_cast<size_t>(na), 8192, [&](size_t lo, size_t hi) {
-    for (size_t q = lo; q < hi; ++q) {  // read first: a shared line written by every thread would bounce
-      uint8_t* f = &key_seen[pod_key[q]];
-      if (!__atomic_load_n(f, __ATOMIC_RELAXED)) __atomic_store_n(f, uint8_t(1), __ATOMIC_RELAXED);
-    }
-  });
+  if (combos) {
+    key_seen.assign(n_key_ids, 0);
+    pfor(static_cast<size_t>(na), 8192, [&](size_t lo, size_t hi) {
+      for (size_t q = lo; q < hi; ++q) {
+        uint8_t* f = &key_seen[pod_key[q]];
+        if (!__atomic_load_n(f, __ATOMIC_RELAXED)) __atomic_store_n(f, uint8_t(1), __ATOMIC_RELAXED);
+      }
+    });
+  }
   std::vector<int32_t>& key_slot = X.key_slot;
   key_slot.assign(n_key_ids, -1);
   std::vector<int32_t> keys;
@@ -959,10 +979,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     }
   };
   for (int32_t k : keys) {
-    const SpecInfo& sp = C.spec[k < n_spec_ids ? k : key_spec[k - n_spec_ids]];
-    for (int32_t r : sp.sel) use_req(r);
-    for (size_t i = 0; i < sp.terms.size(); i += 1 + static_cast<size_t>(sp.terms[i]))
-      for (int32_t t = 0; t < sp.terms[i]; ++t) use_req(sp.terms[i + 1 + t]);
+    const int32_t id = k < n_spec_ids ? k : key_spec[k - n_spec_ids];
+    for (uint32_t i = C.spec_req_off[id]; i < C.spec_req_off[id + 1]; ++i) use_req(C.spec_req[i]);
   }
   const int32_t n_reqs = static_cast<int32_t>(used_reqs.size());
   const int32_t n_ports = static_cast<int32_t>(port_query.size());
@@ -1022,8 +1040,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     const int32_t untol = *tp;
     emit(comp_atom(untol), PROG_AND);  // len(pods)+1 <= allowed pods, untolerated taints
     for (int32_t k = 0; k < n_sel; ++k) emit(A_REQ + req_atom[sel[k]], PROG_AND);
-    for (int32_t b = 0; b < 64; ++b)  // the base UsedPorts conflicting with each host port it asks for
-      if ((ports >> b & 1) && bit_query[b] >= 0) emit(A_PORT + bit_query[b], PROG_ANDNOT);
+    for (uint64_t m = ports; m; m &= m - 1) {  // the base UsedPorts conflicting with each host port it asks for
+      const int32_t b = __builtin_ctzll(m);
+      if (bit_query[b] >= 0) emit(A_PORT + bit_query[b], PROG_ANDNOT);
+    }
     if (da_)
       for (int32_t t : *da_) emit(A_ANTI + 2 * t, PROG_ANDNOT);  // anti-affinity base conflicts
     if (db_)

@@ -286,6 +286,8 @@ struct EncoderCache {
   };
   std::vector<SpecShard> spec_shards;  // by spec-word hash (a fixed count: ids do not depend on threads)
   std::vector<SpecInfo> spec;          // [spec id]; spec 0 = no static constraints
+  std::vector<uint32_t> spec_req_off{0};  // [spec id + 1] the specs' requirement ids (selector, then
+  std::vector<int32_t> spec_req;          //   terms), flat: the per-call key pass reads them in key order
   WordDict req_dict;                   // requirement words {type, key, op, vals...} -> requirement id
   WordDict untol_dict;                 // untolerated-taint sets (valid for untol_gen)
   uint64_t untol_gen = ~0ull;
@@ -310,6 +312,8 @@ struct EncoderCache {
   void clear_content() {  // drops every content-interned dictionary
     spec_shards.clear();
     spec.clear();
+    spec_req_off.assign(1, 0);
+    spec_req.clear();
     req_dict.clear();
     req_rows.clear();
     req_row_gen.clear();

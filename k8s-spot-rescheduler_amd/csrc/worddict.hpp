@@ -2,6 +2,10 @@
 // intern() returns a dense id per distinct sequence, in first-insertion
 // order; the words live in one arena and the index is open addressing over
 // 64-bit hashes, so interning allocates nothing once the arena has grown.
+//
+// Arena layout: each entry is its length followed by its words, and a slot
+// holds the arena position of its entry's words, so a lookup touches one slot
+// and one arena run (the offsets table is only read through data()/len()).
 #pragma once
 
 #include <cstdint>
@@ -23,12 +27,12 @@ class WordDict {
  public:
   void clear() {
     words_.clear();
-    off_.assign(1, 0);
+    off_.clear();
     slots_.clear();
   }
-  size_t size() const { return off_.size() - 1; }
+  size_t size() const { return off_.size(); }
   const int32_t* data(int32_t id) const { return words_.data() + off_[id]; }
-  size_t len(int32_t id) const { return off_[id + 1] - off_[id]; }
+  size_t len(int32_t id) const { return static_cast<uint32_t>(words_[off_[id] - 1]); }
 
   int32_t intern(const int32_t* p, size_t n, bool* inserted = nullptr) {
     return intern(p, n, hash_words(p, n), inserted);
@@ -45,15 +49,34 @@ class WordDict {
       Slot& s = slots_[i];
       if (s.id < 0) {
         const int32_t id = static_cast<int32_t>(size());
+        words_.push_back(static_cast<int32_t>(n));
+        const size_t w0 = words_.size();
         words_.insert(words_.end(), p, p + n);
-        off_.push_back(words_.size());
-        s = Slot{h, id};
+        off_.push_back(w0);
+        s = Slot{h, id, w0};
         if (inserted) *inserted = true;
         return id;
       }
-      if (s.hash == h && len(s.id) == n && (n == 0 || std::memcmp(data(s.id), p, n * sizeof(int32_t)) == 0)) {
-        if (inserted) *inserted = false;
-        return s.id;
+      if (s.hash == h) {
+        const int32_t* e = words_.data() + s.off;
+        if (static_cast<uint32_t>(e[-1]) == n && (n == 0 || std::memcmp(e, p, n * sizeof(int32_t)) == 0)) {
+          if (inserted) *inserted = false;
+          return s.id;
+        }
+      }
+    }
+  }
+  // Lookup only (-1 if absent); safe to call from many threads while no
+  // thread interns.
+  int32_t find(const int32_t* p, size_t n, uint64_t h) const {
+    if (slots_.empty()) return -1;
+    const size_t mask = slots_.size() - 1;
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      const Slot& s = slots_[i];
+      if (s.id < 0) return -1;
+      if (s.hash == h) {
+        const int32_t* e = words_.data() + s.off;
+        if (static_cast<uint32_t>(e[-1]) == n && (n == 0 || std::memcmp(e, p, n * sizeof(int32_t)) == 0)) return s.id;
       }
     }
   }
@@ -62,11 +85,12 @@ class WordDict {
   struct Slot {
     uint64_t hash;
     int32_t id;
+    size_t off;  // arena position of the entry's words
   };
   void grow() {
     std::vector<Slot> old;
     old.swap(slots_);
-    slots_.assign(old.empty() ? 64 : old.size() * 2, Slot{0, -1});
+    slots_.assign(old.empty() ? 64 : old.size() * 2, Slot{0, -1, 0});
     const size_t mask = slots_.size() - 1;
     for (const Slot& s : old)
       if (s.id >= 0) {
@@ -76,7 +100,7 @@ class WordDict {
       }
   }
   std::vector<int32_t> words_;
-  std::vector<size_t> off_{0};
+  std::vector<size_t> off_;
   std::vector<Slot> slots_;
 };
 
