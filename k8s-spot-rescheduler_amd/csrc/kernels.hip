@@ -1320,13 +1320,15 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
     if (placed < 0) placed = k2_run<8, CH, PROF>(w, L, p0, np, status, st, nbytes);  // > 64 distinct nodes
     for (int i = lane; i < np; i += 64) w.out_node[p0 + i] = i < placed ? L.omap[i] : -1;
   }
+  int best = 0;  // lane 0: this candidate is the first drainable one so far
   if (lane == 0) {
     w.out_status[ci] = status;
     w.out_bytes[ci] = nbytes;
     // packed (global candidate << 32 | local candidate): min = first drainable
-    if (status < 0)
-      atomicMin(reinterpret_cast<unsigned long long*>(w.d_min),
-                (static_cast<unsigned long long>(g) << 32) | static_cast<unsigned>(ci));
+    if (status < 0) {
+      const unsigned long long key = (static_cast<unsigned long long>(g) << 32) | static_cast<unsigned>(ci);
+      best = key < atomicMin(reinterpret_cast<unsigned long long*>(w.d_min), key);
+    }
     if (PROF) {
       uint64_t* pr = w.prof + static_cast<size_t>(ci) * 16;
       pr[0] = t_start;
@@ -1346,6 +1348,25 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
         pr[13] = static_cast<uint64_t>(st.run_visits) | static_cast<uint64_t>(st.seq_visits) << 32;
       }
     }
+  }
+  if (w.res_stat) {
+    // Single rank: the host walks res_stat in candidate order and stops at the
+    // first drainable candidate, whose mapping is in res_map -- its wave was
+    // necessarily the first drainable one so far when it finished -- so the
+    // result is in host memory as soon as the candidates up to the winner are
+    // planned, not when the whole grid is.  Every word carries the run's tag
+    // and is accepted on its own: no store waits for another.
+    const uint64_t tag = static_cast<uint64_t>(w.seq) << 32;
+    if (__builtin_amdgcn_readfirstlane(best)) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's out_node stores, then read back
+      for (int q = lane; q < np; q += 64)
+        __hip_atomic_store(w.res_map + p0 + q,
+                           tag | static_cast<uint32_t>(__hip_atomic_load(w.out_node + p0 + q, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (lane == 0)
+      __hip_atomic_store(w.res_stat + ci, tag | (status < 0 ? 1u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

@@ -59,6 +59,11 @@ struct DevWorkload {
   int32_t* d_min;      // 2 x u64 packed {global << 32 | local}: first ok, first fallback (~0 = none)
   uint64_t* result;    // mapped host memory [kResultHeader + max pods] words seq << 32 | value:
                        //   {winner, local, npods, first_fallback, -, -, -, -, mapping...}
+  uint64_t* res_stat;  // single-rank runs: mapped host memory [n_cand] words seq << 32 | drainable, one
+                       // stored by K2 per finished candidate, and
+  uint64_t* res_map;   // [n_pods] words seq << 32 | spot position: a candidate's mapping, stored by K2
+                       // when the candidate was the first drainable one so far as it finished (no K3);
+                       // both null on runs that end with K3
   uint32_t seq;        // run sequence number: the tag of every result word (wraps)
   int32_t k2_scan_min; // node visits with at least this many pods use the prefix-sum pass (place_run)
   int32_t k2_mode;     // 0: node-order first fit where it applies (<= 64 pods, <= 64-word rows);
@@ -74,6 +79,7 @@ hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hip
 // K2: per-candidate feasibility rows + first-fit placement; atomicMin of first_ok into d_min[0].
 hipError_t launch_placement(const DevWorkload& w, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // K3: winner mapping into `result` (after the collective when ranks > 1), then the run's seq.
+// Not launched when K2 writes res_stat / res_map itself (single rank).
 hipError_t launch_winner(const DevWorkload& w, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 }  // namespace sr

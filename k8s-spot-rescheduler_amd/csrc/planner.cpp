@@ -41,6 +41,9 @@ struct sr_ctx {
   std::string err;
   DevBuf arena, tables, out_node, out_status, out_bytes, dmin, prof, scratch;
   HostBuf h_arena, h_result, h_status, h_node, h_bytes;
+  HostBuf h_early;           // mapped: K2's per-candidate result words (single-rank runs)
+  bool in_flight = false;    // a run returned with K2 still planning candidates past the winner
+  uint64_t* d_early = nullptr;  // device address of h_early
   uint64_t issued_checks = 0;  // checks of the prepared workload's plan (known after a full run)
   bool issued_known = false;
   sr::Workload wl;
@@ -53,6 +56,7 @@ struct sr_ctx {
   int32_t timing = 0;        // SR_TIME_* kernel bits of the current setting
   int32_t timing_every = 1;  // sample every n-th run
   int64_t timing_runs = 0;   // runs since sr_set_timing
+  int32_t timing_cur = 0;    // SR_TIME_* bits of the current run
   // HIP event pairs bracketing timed kernels, read back lazily (flush_timing)
   // so a timed run does not have to synchronise the stream.
   std::vector<hipEvent_t> ev_start, ev_end;
@@ -130,6 +134,16 @@ class Packer {
   size_t size_ = 0;
 };
 
+// A run may return while K2 still plans the candidates after the winner (the
+// stream keeps later work in order); host-side reallocation of its buffers
+// waits for it here.
+sr_status settle(sr_ctx* ctx) {
+  if (!ctx->in_flight) return SR_OK;
+  ctx->in_flight = false;
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return SR_OK;
+}
+
 sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands) {
   auto t0 = std::chrono::steady_clock::now();
   ctx->prepared = false;
@@ -162,6 +176,8 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t bytes = pk.size();
 
   HIP_TRY(ctx, hipSetDevice(ctx->device));
+  st = settle(ctx);
+  if (st != SR_OK) return st;
   if (ctx->ev_upload) HIP_TRY(ctx, hipEventSynchronize(ctx->ev_upload));  // staging buffer free again
   HIP_TRY(ctx, host_reserve(ctx->h_arena, bytes));
   const size_t arena_cap = ctx->arena.cap;
@@ -183,6 +199,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, dev_reserve(ctx->dmin, 64));
   const size_t res_bytes = sizeof(uint64_t) * (sr::kResultHeader + static_cast<size_t>(std::max(1, w.max_cand_pods)));
   HIP_TRY(ctx, host_reserve(ctx->h_result, res_bytes));  // mapped: K3 writes the result straight to the host
+  HIP_TRY(ctx, host_reserve(ctx->h_early, sizeof(uint64_t) * (static_cast<size_t>(ncand) + na + 1)));
   auto t1 = std::chrono::steady_clock::now();
   const size_t from = nodes_resident || nodes_patch ? node_bytes : 0;
   pk.copy_to(static_cast<char*>(ctx->h_arena.p), from);
@@ -262,6 +279,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   void* dres = nullptr;
   HIP_TRY(ctx, hipHostGetDevicePointer(&dres, ctx->h_result.p, 0));
   d.result = static_cast<uint64_t*>(dres);
+  HIP_TRY(ctx, hipHostGetDevicePointer(&dres, ctx->h_early.p, 0));
+  ctx->d_early = static_cast<uint64_t*>(dres);
+  d.res_stat = d.res_map = nullptr;  // set per run
   ctx->t.bytes_uploaded = static_cast<uint64_t>(bytes - from + patch_bytes);
 
   const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
@@ -303,6 +323,63 @@ sr_status flush_timing(sr_ctx* ctx) {
   return SR_OK;
 }
 
+// The end of a single-rank winner-only run: walk K2's per-candidate words in
+// candidate order up to the first drainable candidate, then read its mapping
+// (rescheduler.go:280-286 stops there too).  A run whose words have not all
+// arrived after 100 ms falls back to the stream, which also surfaces a kernel
+// fault as an error.
+sr_status finish_early(sr_ctx* ctx, sr_plan_out* out) {
+  const sr::Workload& w = ctx->wl;
+  const sr::DevWorkload& d = ctx->dw;
+  if (ctx->timing_cur) ctx->t.n_runs += 1;
+  volatile uint64_t* stat = static_cast<volatile uint64_t*>(ctx->h_early.p);
+  volatile uint64_t* map = stat + d.n_cand;
+  const uint32_t tag = d.seq;
+  auto ready = [&](volatile uint64_t* p) { return static_cast<uint32_t>(*p >> 32) == tag; };
+  const auto t0 = std::chrono::steady_clock::now();
+  uint32_t spins = 0;
+  bool synced = false;
+  auto wait = [&](volatile uint64_t* p) -> sr_status {
+    while (!ready(p)) {
+      if (!synced && (++spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100)) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        synced = true;
+      }
+      if (synced && !ready(p)) {
+        ctx->err = "K2 result word not written by this run";
+        return SR_ERR_HIP;
+      }
+    }
+    return SR_OK;
+  };
+  int32_t k = 0;
+  for (; k < d.n_cand; ++k) {
+    sr_status st = wait(stat + k);
+    if (st != SR_OK) return st;
+    if (static_cast<uint32_t>(stat[k]) == 1) break;
+  }
+  ctx->in_flight = !synced;
+  out->first_fallback = w.first_fallback;
+  out->first_ok = k < d.n_cand ? w.cand_global[k] : -1;
+  out->winner = (out->first_ok >= 0 && (w.first_fallback < 0 || w.first_fallback > out->first_ok)) ? out->first_ok : -1;
+  out->winner_npods = 0;
+  if (k < d.n_cand) {
+    const int32_t o = w.cand_off[k], np = w.cand_off[k + 1] - o;
+    for (int32_t q = 0; q < np; ++q) {
+      sr_status st = wait(map + o + q);
+      if (st != SR_OK) return st;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    out->winner_npods = np;
+    if (out->winner_map)
+      for (int32_t q = 0; q < np; ++q) out->winner_map[q] = static_cast<int32_t>(static_cast<uint32_t>(map[o + q]));
+  }
+  out->checks_dense = static_cast<uint64_t>(d.n_pods) * static_cast<uint64_t>(w.n_spot);
+  out->fallback_pods = w.fallback_pods;
+  out->checks = ctx->issued_known ? ctx->issued_checks : 0;
+  return SR_OK;
+}
+
 sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   if (!ctx->prepared) {
     ctx->err = "sr_plan_run before sr_plan_prepare";
@@ -313,7 +390,11 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   hipStream_t s = ctx->stream;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   const bool collective = ctx->comm && use_comm;
+  // Single rank, winner only: K2 writes each candidate's outcome to the host
+  // and the run returns once the candidates up to the winner are known (no K3)
+  const bool early = !collective && !full && !ctx->prof_file;
   const int32_t timing = (ctx->timing_runs++ % ctx->timing_every) == 0 ? ctx->timing : 0;
+  ctx->timing_cur = timing;
   if (++ctx->seq == 0) ctx->seq = 1;  // tag 0 is never used: fresh result memory may hold zeros
   d.seq = ctx->seq;
   volatile uint64_t* res = static_cast<volatile uint64_t*>(ctx->h_result.p);
@@ -351,7 +432,14 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   PAIR(0, e0a, e0b);
   HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
   PAIR(1, e1a, e1b);
+  if (early) {
+    d.res_stat = ctx->d_early;
+    d.res_map = ctx->d_early + d.n_cand;
+  } else {
+    d.res_stat = d.res_map = nullptr;
+  }
   HIP_TRY(ctx, sr::launch_placement(d, s, e1a, e1b));
+  if (early) return finish_early(ctx, out);
   PAIR(2, e2a, e2b);
   if (collective) {
     if (e2a) HIP_TRY(ctx, hipEventRecord(e2a, s));

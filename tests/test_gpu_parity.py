@@ -53,10 +53,15 @@ def run_scenario(checker, nodes, spot_pods, cands, extra_fallback=None):
     o = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=1)
     h = sc.product_snapshot()
     try:
+        # winner only first (single rank: K2 writes each candidate's outcome to
+        # the host and the run returns at the winner), then every output
+        q = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods, full=False)
         p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
     finally:
         capi.load_planner().sr_snapshot_destroy(h)
     compare_plans(o, p, cand_off, extra_fallback)
+    assert (q.first_ok, q.first_fallback, q.winner) == (p.first_ok, p.first_fallback, p.winner)
+    assert np.array_equal(q.winner_map, p.winner_map)
     if np.array_equal(p.status, o["status"]):  # same candidates evaluated: the same reference-equivalent work
         assert p.checks == o["checks"]
     return sc, o, p
@@ -373,8 +378,11 @@ def tick_parity(checker, sc: SynthCluster, max_cands=None, oracle_threads=8):
     assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot),
                                   capi.ptr(nm.node_pod_off, capi.P32), capi.ptr(nm.node_pod_idx, capi.P32),
                                   ctypes.byref(h)) == capi.SR_OK
+    q = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods, full=False)  # winner only (returns at the winner)
     p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
     lib.sr_snapshot_destroy(h)
+    assert (q.first_ok, q.first_fallback, q.winner) == (p.first_ok, p.first_fallback, p.winner)
+    assert np.array_equal(q.winner_map, p.winner_map)
     osnap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
     o = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=oracle_threads)
     compare_plans(o, p, cand_off)
