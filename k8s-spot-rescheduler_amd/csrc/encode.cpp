@@ -32,6 +32,7 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <string>
@@ -44,7 +45,19 @@
 
 namespace sr {
 
-double encode_phase_ms[16];  // host-side profile of the last encode (tools/encode_stats)
+double encode_phase_ms[16];
+
+namespace {
+// Candidates dispatched ahead of the longest-first rest (SR_LIST_HEAD, default
+// 1024: about one wave per SIMD).
+int32_t list_head() {
+  static const int32_t v = [] {
+    const char* e = std::getenv("SR_LIST_HEAD");
+    return e ? std::max(0, std::atoi(e)) : 1024;
+  }();
+  return v;
+}
+}  // namespace  // host-side profile of the last encode (tools/encode_stats)
 
 namespace {
 
@@ -1407,20 +1420,30 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     for (int32_t i = 0; i < len; ++i) slot[i] = w->cls_prog[o + i];
   }
 
-  // ---- K2 work list: longest candidates first (counting sort, stable)
+  // ---- K2 work list: the first kListHead candidates, then the rest, each part
+  // longest first (counting sort, stable).  Longest first shortens the grid's
+  // makespan; the head goes first because a winner-only tick returns once the
+  // candidates up to the winner are planned, and run() drains the first
+  // drainable one (rescheduler.go:280-286) -- on a grid larger than the chip
+  // holds at once, low indices must not wait for a later dispatch round.
   {
     const size_t n_act = w->cand_off.size() - 1;
-    std::vector<int32_t> cnt(MAX_CAND_PODS + 2, 0);
-    for (size_t i = 0; i < n_act; ++i) ++cnt[MAX_CAND_PODS - (w->cand_off[i + 1] - w->cand_off[i])];
-    for (int32_t v = 0, acc = 0; v <= MAX_CAND_PODS + 1; ++v) {
+    const int32_t kListHead = list_head();
+    auto bucket = [&](size_t i) {
+      const int32_t len = w->cand_off[i + 1] - w->cand_off[i];
+      return (static_cast<int32_t>(i) < kListHead ? 0 : MAX_CAND_PODS + 1) + MAX_CAND_PODS - len;
+    };
+    std::vector<int32_t> cnt(2 * (MAX_CAND_PODS + 1) + 1, 0);
+    for (size_t i = 0; i < n_act; ++i) ++cnt[bucket(i)];
+    for (size_t v = 0, acc = 0; v < cnt.size(); ++v) {
       const int32_t k = cnt[v];
-      cnt[v] = acc;
-      acc += k;
+      cnt[v] = static_cast<int32_t>(acc);
+      acc += static_cast<size_t>(k);
     }
     w->list.assign(n_act * 4, 0);
     for (size_t i = 0; i < n_act; ++i) {
       const int32_t b = w->cand_off[i], e = w->cand_off[i + 1];
-      int32_t* l = &w->list[static_cast<size_t>(cnt[MAX_CAND_PODS - (e - b)]++) * 4];
+      int32_t* l = &w->list[static_cast<size_t>(cnt[bucket(i)]++) * 4];
       l[0] = static_cast<int32_t>(i);
       l[1] = b;
       l[2] = e;

@@ -14,8 +14,9 @@ for rep in 1 2; do
     python - "$out/arm${i}_rep${rep}.log" "$arm" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print("%-40s ms/step %.4f  K0 %.4f  K2 %.4f  K3 %.4f" % (sys.argv[2], d["ms_per_step"], d["kernels_ms"]["k0_tables"],
-      d["kernels_ms"]["k2_placement"], d["kernels_ms"]["k3_winner_and_collective"]))
+print("%-40s ms/step %.4f  latency %.4f  K0 %.4f  K2 %.4f  K3 %.4f" % (sys.argv[2], d["ms_per_step"],
+      d.get("latency_ms", 0), d["kernels_ms"]["k0_tables"], d["kernels_ms"]["k2_placement"],
+      d["kernels_ms"]["k3_winner_and_collective"]))
 PY
   done
 done
