@@ -139,7 +139,8 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
   // diagnostics: per-wave {start, end} (s_memrealtime) after K2's records
   const size_t pw = static_cast<size_t>(blockIdx.x) * 4 + wave;
   uint64_t* const prof = w.prof && pw < kK0ProfWaves ? w.prof + static_cast<size_t>(w.n_cand) * 16 + 2 * pw : nullptr;
-  if (prof && lane == 0) prof[0] = __builtin_amdgcn_s_memrealtime();
+  if (prof && lane == 0)  // bit 63: an S-row wave
+    prof[0] = __builtin_amdgcn_s_memrealtime() | (static_cast<int>(blockIdx.x) < s_blocks ? 1ull << 63 : 0ull);
   struct Stamp {
     uint64_t* p;
     int lane;

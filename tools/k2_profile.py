@@ -35,10 +35,19 @@ def main():
     last_run = max(range(len(runs)), key=lambda i: (len(runs[i]), i))
     r = runs[last_run].astype(np.int64)
     k0 = k0s[last_run].astype(np.int64)
-    k0 = k0[k0[:, 0] > 0]
+    k0 = k0[k0[:, 0] != 0]
     t0 = r[:, 0].min()
     if len(k0):
+        is_s = k0[:, 0] < 0  # bit 63 of the start stamp: an S-row wave
+        k0[:, 0] &= (1 << 63) - 1
         z = k0[:, 0].min()
+        for name, m in (("S", is_s), ("T", ~is_s)):
+            if m.any():
+                print("K0 %s waves %d: start p50/p90/max %s us; duration p50/p90/max %s us; last end %.2f us"
+                      % (name, int(m.sum()),
+                         " ".join("%.2f" % x for x in np.percentile((k0[m, 0] - z) / 100.0, [50, 90, 100])),
+                         " ".join("%.2f" % x for x in np.percentile((k0[m, 1] - k0[m, 0]) / 100.0, [50, 90, 100])),
+                         (k0[m, 1].max() - z) / 100.0))
         print("K0 waves %d: start p50/p90/max %s us; duration p50/p90/max %s us; last end %.2f us; K2 first start %.2f us"
               % (len(k0), " ".join("%.2f" % x for x in np.percentile((k0[:, 0] - z) / 100.0, [50, 90, 100])),
                  " ".join("%.2f" % x for x in np.percentile((k0[:, 1] - k0[:, 0]) / 100.0, [50, 90, 100])),
