@@ -45,6 +45,9 @@ WORKLOAD = {1: "C1 rescheduler_test-style 20 nodes / 200 pods",
             5: "C5 1k nodes host-port + DaemonSet heavy"}
 
 
+E2E_IDLE = os.environ.get("SR_BENCH_E2E_IDLE", "1") != "0"
+
+
 def host_threads():
     """The encoder pool's thread count (csrc/pool.hpp: SR_HOST_THREADS, else min(16, cores))."""
     env = os.environ.get("SR_HOST_THREADS")
@@ -277,14 +280,18 @@ def main():
     def summary(xs):
         return {"median_ms": round(float(np.median(xs)), 4), "min_ms": round(float(np.min(xs)), 4)}
 
-    ref_t, ref_batches, ref_enc, ref_state, ref_up = [], [], [], [], []
+    ref_t, ref_batches, ref_enc, ref_state, ref_up, ref_upl = [], [], [], [], [], []
     all_t, all_enc, all_upl, all_state = [], [], [], []
     wmap2 = np.zeros_like(wmap)
     for r in range(args.e2e_reps + 2):  # two untimed ticks first: the planner's view of the pool settles
         h = fresh_snapshot(r)
-        # reference-faithful tick: candidates in order until the first drainable one (sr_plan_first)
+        # reference-faithful tick: candidates in order until the first drainable one (sr_plan_first),
+        # on an idle device as between two housekeeping ticks (the previous iteration's every-candidate
+        # run may still be planning candidates past its winner)
         fo = capi.sr_plan_out()
         fo.winner_map = capi.ptr(wmap2, capi.P32)
+        if E2E_IDLE:
+            torch.cuda.synchronize()
         t1 = time.perf_counter()
         st = lib.sr_plan_first(checker.handle, h, sc.ptr, ctypes.byref(cands), ctypes.byref(fo))
         dt = 1e3 * (time.perf_counter() - t1)
@@ -294,9 +301,12 @@ def main():
             ref_t.append(dt)
             ref_batches.append(tq.prefix_batches)
             ref_enc.append(tq.ms_pack_host)
+            ref_upl.append(tq.ms_upload)
             ref_state.append(tq.enc_state_nodes)
             ref_up.append(tq.bytes_uploaded)
         # all candidates planned: prepare + run
+        if E2E_IDLE:
+            torch.cuda.synchronize()
         t1 = time.perf_counter()
         st = lib.sr_plan_prepare(checker.handle, h, sc.ptr, ctypes.byref(cands))
         assert st == capi.SR_OK, checker.last_error()
@@ -343,6 +353,7 @@ def main():
                     "prefix-batched encode + H2D + kernels until the first drainable candidate, winner and "
                     "mapping on the host (run() stops there, rescheduler.go:286)",
             "prefix_batches": int(np.median(ref_batches)), "encode_ms_last_batch": round(float(np.median(ref_enc)), 4),
+            "upload_issue_ms_last_batch": round(float(np.median(ref_upl)), 4),
             "state_nodes_reencoded": int(np.median(ref_state)), "upload_bytes": int(np.median(ref_up)),
             "all_candidates": dict(summary(all_t), **{
                 "encode_ms": round(float(np.median(all_enc)), 3), "upload_ms": round(float(np.median(all_upl)), 3),

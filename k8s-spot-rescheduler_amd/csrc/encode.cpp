@@ -45,9 +45,10 @@
 
 namespace sr {
 
-double encode_phase_ms[16];
+double encode_phase_ms[16];  // host-side profile of the last encode (tools/encode_stats)
 
 namespace {
+
 // Candidates dispatched ahead of the longest-first rest (SR_LIST_HEAD, default
 // 1024: about one wave per SIMD).
 int32_t list_head() {
@@ -57,15 +58,19 @@ int32_t list_head() {
   }();
   return v;
 }
-}  // namespace  // host-side profile of the last encode (tools/encode_stats)
-
-namespace {
 
 constexpr int64_t kQuantityLimit = int64_t(1) << 62;
 constexpr size_t kSpecShards = 16;             // fixed: spec ids do not depend on the thread count
 constexpr size_t kMaxSpecs = size_t(1) << 21;  // content dictionaries are dropped beyond these
 constexpr size_t kMaxReqs = size_t(1) << 18;
-constexpr int32_t kSerialPods = 4096;          // below this, per-pod passes run on the calling thread
+// below this many pods, per-pod passes run on the calling thread (SR_SERIAL_PODS)
+int32_t serial_pods() {
+  static const int32_t v = [] {
+    const char* e = std::getenv("SR_SERIAL_PODS");
+    return e ? std::max(0, std::atoi(e)) : 4096;
+  }();
+  return v;
+}
 
 bool in_range(int64_t v) { return v >= 0 && v < kQuantityLimit; }
 
@@ -597,7 +602,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         cand_ports[i] = P.port_off[cands->cand_pods[j]] != P.port_off[cands->cand_pods[j] + 1];
     }
   };
-  if (w->n_input_pods > kSerialPods) parallel_for(static_cast<size_t>(nc), 64, pass1);
+  if (w->n_input_pods > serial_pods()) parallel_for(static_cast<size_t>(nc), 64, pass1);
   else pass1(0, static_cast<size_t>(nc));
   if (bad_index.load(std::memory_order_relaxed)) {
     *err = "candidate pod index out of range";
@@ -752,7 +757,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   w->cand_off.push_back(na);
   active_pod.resize(static_cast<size_t>(na));
   active_src.resize(static_cast<size_t>(na));
-  const bool big = na > kSerialPods;
+  const bool big = na > serial_pods();
   auto pfor = [&](size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn) {
     if (big) parallel_for(n, grain, fn);
     else fn(0, n);
