@@ -21,7 +21,38 @@
 #include "host.hpp"
 #include "kernels.hpp"
 
+#include <dlfcn.h>
+
 namespace {
+
+// RCCL is loaded on first use (sr_comm_unique_id / sr_comm_init): a
+// single-GPU planner never maps it.  The calls keep their rccl.h signatures.
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  bool ok = false;
+};
+
+const Rccl& rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return x;
+    x.get_unique_id = reinterpret_cast<decltype(x.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+    x.comm_init_rank = reinterpret_cast<decltype(x.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+    x.all_reduce = reinterpret_cast<decltype(x.all_reduce)>(dlsym(h, "ncclAllReduce"));
+    x.comm_destroy = reinterpret_cast<decltype(x.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(h, "ncclGetErrorString"));
+    x.ok = x.get_unique_id && x.comm_init_rank && x.all_reduce && x.comm_destroy && x.error_string;
+    return x;
+  }();
+  return r;
+}
 
 struct DevBuf {
   void* p = nullptr;
@@ -443,9 +474,9 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   PAIR(2, e2a, e2b);
   if (collective) {
     if (e2a) HIP_TRY(ctx, hipEventRecord(e2a, s));
-    ncclResult_t r = ncclAllReduce(d.d_min, d.d_min, 2, ncclUint64, ncclMin, ctx->comm, s);
+    ncclResult_t r = rccl().all_reduce(d.d_min, d.d_min, 2, ncclUint64, ncclMin, ctx->comm, s);
     if (r != ncclSuccess) {
-      ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+      ctx->err = std::string("ncclAllReduce: ") + rccl().error_string(r);
       return SR_ERR_RCCL;
     }
     HIP_TRY(ctx, sr::launch_winner(d, s));
@@ -585,7 +616,7 @@ void sr_destroy(sr_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  if (ctx->comm) (void)rccl().comm_destroy(ctx->comm);
   for (DevBuf* b : {&ctx->arena, &ctx->tables, &ctx->out_node, &ctx->out_status, &ctx->out_bytes, &ctx->dmin,
                     &ctx->prof, &ctx->scratch})
     if (b->p) (void)hipFree(b->p);
@@ -632,9 +663,9 @@ static sr_status comm_max(sr_ctx* ctx, int32_t v, int32_t* out) {
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, dev_reserve(ctx->scratch, 64));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->scratch.p, &v, sizeof(v), hipMemcpyHostToDevice, ctx->stream));
-  ncclResult_t r = ncclAllReduce(ctx->scratch.p, ctx->scratch.p, 1, ncclInt32, ncclMax, ctx->comm, ctx->stream);
+  ncclResult_t r = rccl().all_reduce(ctx->scratch.p, ctx->scratch.p, 1, ncclInt32, ncclMax, ctx->comm, ctx->stream);
   if (r != ncclSuccess) {
-    ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+    ctx->err = std::string("ncclAllReduce: ") + rccl().error_string(r);
     return SR_ERR_RCCL;
   }
   HIP_TRY(ctx, hipMemcpyAsync(out, ctx->scratch.p, sizeof(*out), hipMemcpyDeviceToHost, ctx->stream));
@@ -789,7 +820,7 @@ sr_status sr_comm_unique_id(uint8_t out[SR_UNIQUE_ID_BYTES]) {
   if (!out) return SR_ERR_INVALID_ARG;
   ncclUniqueId id;
   static_assert(sizeof(id) == SR_UNIQUE_ID_BYTES, "ncclUniqueId size");
-  if (ncclGetUniqueId(&id) != ncclSuccess) return SR_ERR_RCCL;
+  if (!rccl().ok || rccl().get_unique_id(&id) != ncclSuccess) return SR_ERR_RCCL;
   std::memcpy(out, &id, sizeof(id));
   return SR_OK;
 }
@@ -799,9 +830,13 @@ sr_status sr_comm_init(sr_ctx* ctx, const uint8_t id[SR_UNIQUE_ID_BYTES], int32_
   if (hipSetDevice(ctx->device) != hipSuccess) return SR_ERR_HIP;
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
-  ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, uid, rank);
+  if (!rccl().ok) {
+    ctx->err = "RCCL (librccl.so) could not be loaded";
+    return SR_ERR_RCCL;
+  }
+  ncclResult_t r = rccl().comm_init_rank(&ctx->comm, nranks, uid, rank);
   if (r != ncclSuccess) {
-    ctx->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+    ctx->err = std::string("ncclCommInitRank: ") + rccl().error_string(r);
     ctx->comm = nullptr;
     return SR_ERR_RCCL;
   }
