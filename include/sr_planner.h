@@ -391,7 +391,7 @@ sr_status sr_plan(sr_ctx *ctx, const sr_snapshot *snap, const sr_cluster *cluste
 
 /* The planning segment as run() executes it (rescheduler.go:228-287): the
  * candidates in order until the first whose plan succeeds (drain + break,
- * :280-286).  The device plans prefix batches of 64, 128, 256, ... candidates
+ * :280-286).  The device plans prefix batches of 16, 32, 64, ... candidates
  * (the environment variable SR_PREFIX_BATCH sets the first size) and stops
  * after the batch holding the first drainable candidate; a batch's host
  * encoding costs in proportion to its pods, so a tick whose winner comes early

@@ -81,7 +81,7 @@ struct sr_ctx {
   sr::EncoderCache enc;      // what the encoder keeps across calls (encode.cpp)
   uint64_t dev_state_gen = ~0ull;  // encoder state whose node records the device arena holds
   hipEvent_t ev_upload = nullptr;  // the last upload (the staging buffer is reused after it)
-  int32_t prefix_batch = 64;       // first batch of sr_plan_first (SR_PREFIX_BATCH)
+  int32_t prefix_batch = 16;       // first batch of sr_plan_first (SR_PREFIX_BATCH; tools/gpu_prefix.sh)
   sr::DevWorkload dw{};
   bool prepared = false;
   int32_t timing = 0;        // SR_TIME_* kernel bits of the current setting

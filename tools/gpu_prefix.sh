@@ -2,9 +2,9 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
 out=gpurun_out/${TAG:-prefix}
 mkdir -p $out
-for cfg in 3 4 2; do
+for cfg in ${CFGS:-3 4 2 5 1}; do
   for b in 64 32 16 8; do
-    steps=100; [ $cfg = 4 ] && steps=20
+    steps=50; [ $cfg = 4 ] && steps=20
     SR_PREFIX_BATCH=$b timeout -k 10 300 python bench.py --config $cfg --steps $steps --warmup 5 --no-cpu-baseline \
       > $out/c${cfg}_b$b.log 2>&1 || exit $?
     tail -1 $out/c${cfg}_b$b.log | python3 -c "

@@ -26,10 +26,12 @@ SR_K2_MODE=1 timeout -k 10 300 python bench.py --config "$cfg" --steps 200 --war
   > "$out/bench_podorder.log" 2>&1
 rc=$?; echo "bench(pod order) rc=$rc"; tail -1 "$out/bench_podorder.log" | cut -c1-400
 [ $rc -ne 0 ] && exit $rc
-rm -f "$out/k2prof.bin"
-SR_K2_PROFILE="$out/k2prof.bin" timeout -k 10 300 python bench.py --config "$cfg" --steps 3 --warmup 3 \
-  --no-cpu-baseline > "$out/bench_prof.log" 2>&1 || exit $?
-python tools/k2_profile.py "$out/k2prof.bin" > "$out/k2prof.txt" 2>&1; cat "$out/k2prof.txt"
+# the raw per-wave records (tens of MB) stay on the box: only the summary comes back
+rm -f /tmp/k2prof_$tag.bin
+SR_K2_PROFILE="/tmp/k2prof_$tag.bin" timeout -k 10 300 python bench.py --config "$cfg" --steps 3 --warmup 3 \
+  --e2e-reps 0 --no-cpu-baseline > "$out/bench_prof.log" 2>&1 || exit $?
+python tools/k2_profile.py "/tmp/k2prof_$tag.bin" > "$out/k2prof.txt" 2>&1; cat "$out/k2prof.txt"
+rm -f /tmp/k2prof_$tag.bin
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run --output-format csv -- \
   python3 "$R/bench.py" --config "$cfg" --steps 200 --warmup 10 --no-cpu-baseline > "$out/prof.log" 2>&1
