@@ -350,6 +350,7 @@ struct K2Stats {
   uint64_t cyc_a = 0, cyc_b = 0, cyc_c = 0, cyc_d = 0;
   // node order (profile builds): run-pass iterations / pod-by-pod rounds, and the visits taking each
   uint32_t run_it = 0, seq_it = 0, run_visits = 0, seq_visits = 0;
+  uint64_t cyc_rec = 0;  // node order: wave entry -> pod records in registers
 };
 
 // One candidate's canDrainNode with 64 * SPL touched-node slots.  Returns the
@@ -839,6 +840,10 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     wcur = 0;
     nbytes += 64u * 40u;
   }
+  if (PROF) {  // profile builds: wait for the pod records and window 0 here
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st.cyc_rec = __builtin_amdgcn_s_memtime();
+  }
   uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
   // bytes moved (algorithmic, wave-uniform): pod records, F heads of pods
   // [0, dead) (4 rows x min(Wp, kNH) words), 64-node record windows (5 words
@@ -1297,6 +1302,8 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   const int p0 = __builtin_amdgcn_readfirstlane(e.y);
   const int np = __builtin_amdgcn_readfirstlane(e.z) - p0;  // >= 1: empty candidates never reach the device
   const int g = __builtin_amdgcn_readfirstlane(e.w);
+  if (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the work-list entry has arrived
+  const uint64_t t_list = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
   K2Lds& L = *reinterpret_cast<K2Lds*>(k2_lds + static_cast<size_t>(wave) * (sizeof(K2Lds) / 8));
 
   K2Stats st;
@@ -1333,7 +1340,7 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
     if (PROF) {
       uint64_t* pr = w.prof + static_cast<size_t>(ci) * 16;
       pr[0] = t_start;
-      pr[1] = t_start;
+      pr[1] = t_list;  // the work-list entry has arrived
       pr[2] = __builtin_amdgcn_s_memrealtime();
       pr[3] = __builtin_amdgcn_s_memtime() - c_start;
       pr[4] = static_cast<uint64_t>(status >= 0 ? status + 1 : np);
@@ -1347,6 +1354,7 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
       if (wide == 2) {  // node order: placement passes
         pr[12] = static_cast<uint64_t>(st.run_it) | static_cast<uint64_t>(st.seq_it) << 32;
         pr[13] = static_cast<uint64_t>(st.run_visits) | static_cast<uint64_t>(st.seq_visits) << 32;
+        pr[14] = st.cyc_rec - c_start;
       }
     }
   }

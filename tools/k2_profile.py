@@ -3,7 +3,8 @@
 
 Each sr_plan_run appends {int64 n_cand, int64 n_k0} + n_cand x 16 u64 (K2)
 + n_k0 x 2 u64 (K0 waves: start, end; zero = not launched):
-  [0] s_memrealtime at wave start (100 MHz)   [1] = [0]
+  [0] s_memrealtime at wave start (100 MHz)
+ [1] at the arrival of the work-list entry
   [2] at the end                               [3] s_memtime cycles start->end
   [4] pod steps executed                       [5] 1 if rerun with 512 slots
   [6] speculative-record misses                [7] wave_min count | far-chunk count << 32
@@ -12,7 +13,8 @@ Each sr_plan_run appends {int64 n_cand, int64 n_k0} + n_cand x 16 u64 (K2)
           + DMA issue;  [12] cycles waiting for speculative records
 Node-order waves ([5] == 2) reuse the fields: [6] placements, [7] visits |
 windows << 32, [8] prologue (F heads) cycles, [9] min + window + node
-state, [10] placement, [11] pointer moves (+ far resolution).
+state, [10] placement, [11] pointer moves (+ far resolution), [14] cycles
+from wave start to the pod records and window 0 in registers.
 The last of the widest runs in the file is summarised (earlier ones are
 warmup; narrower ones are prefix batches of sr_plan_first)."""
 import sys
@@ -61,7 +63,7 @@ def main():
     pct = lambda a: " ".join("%.2f" % x for x in np.percentile(a, [50, 90, 99, 100]))
     print("runs %d  waves %d" % (len(runs), len(r)))
     print("start skew us  p50/p90/p99/max:", pct(start))
-    print("prologue us    p50/p90/p99/max:", pct(pro))
+    print("entry->list us p50/p90/p99/max:", pct(pro))
     print("wave dur us    p50/p90/p99/max:", pct(dur))
     print("end us         p50/p90/p99/max:", pct(end))
     print("steps          p50/p90/p99/max:", pct(steps))
@@ -80,8 +82,9 @@ def main():
         print("node order: visits p50/p90/max %s; placements/visit %.2f; windows/wave %.2f"
               % (" ".join("%d" % x for x in np.percentile(vis, [50, 90, 100])),
                  q[:, 6].sum() / max(1, vis.sum()), (q[:, 7] >> 32).sum() / len(q)))
-        print("node order: prologue cycles p50/p90/max %s" % " ".join(
-            "%.0f" % x for x in np.percentile(q[:, 8], [50, 90, 100])))
+        print("node order: entry->records cycles p50/p90/max %s; prologue (F heads) cycles p50/p90/max %s" % (
+            " ".join("%.0f" % x for x in np.percentile(q[:, 14], [50, 90, 100])),
+            " ".join("%.0f" % x for x in np.percentile(q[:, 8], [50, 90, 100]))))
         sv = max(1, vis.sum())
         print("node order: cycles/visit min+window+state %.0f, placement %.0f, pointer moves %.0f"
               % (q[:, 9].sum() / sv, q[:, 10].sum() / sv, q[:, 11].sum() / sv))
@@ -105,11 +108,11 @@ def main():
         print("node order placement: run-pass visits %d (%.2f passes each), pod-by-pod visits %d (%.2f rounds each)"
               % (rv.sum(), ri.sum() / max(1, rv.sum()), sv.sum(), si.sum() / max(1, sv.sum())))
     print("latest-ending waves: wave start_us dur_us steps mode | visits placements windows | "
-          "cycles: prologue min+state placement moves | run visits/passes seq visits/rounds")
+          "cycles: entry->records prologue min+state placement moves | run visits/passes seq visits/rounds")
     for c in last:
         f = full[c]
-        print("  %5d %6.2f %6.2f %4d %2d | %3d %3d %3d | %6d %6d %6d %6d | %3d/%3d %3d/%3d"
-              % (c, start[c], dur[c], steps[c], mode[c], f[7] & 0xffffffff, f[6], f[7] >> 32,
+        print("  %5d %6.2f %6.2f %4d %2d | %3d %3d %3d | %6d %6d %6d %6d %6d | %3d/%3d %3d/%3d"
+              % (c, start[c], dur[c], steps[c], mode[c], f[7] & 0xffffffff, f[6], f[7] >> 32, f[14],
                  f[8], f[9], f[10], f[11], f[13] & 0xffffffff, f[12] & 0xffffffff, f[13] >> 32, f[12] >> 32))
 
 
