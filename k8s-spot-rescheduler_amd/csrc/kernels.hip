@@ -72,6 +72,17 @@ __device__ __forceinline__ int64_t scan_add(int64_t x) {
   v += dpp_shifted<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
   return static_cast<int64_t>(v);
 }
+// The same inclusive prefix sum on 32-bit lanes: one DPP add per step.
+__device__ __forceinline__ uint32_t scan_add32(uint32_t v) {
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, true));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, true));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, true));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, true));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, true));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, true));
+  return v;
+}
+
 // OR of the lanes below (exclusive): shift up one lane (wave_shr:1), then scan
 __device__ __forceinline__ uint64_t scan_or_excl(uint64_t v) {
   v = dpp_shifted<0x138>(v);
@@ -351,6 +362,8 @@ struct K2Stats {
   // node order (profile builds): run-pass iterations / pod-by-pod rounds, and the visits taking each
   uint32_t run_it = 0, seq_it = 0, run_visits = 0, seq_visits = 0;
   uint64_t cyc_rec = 0;  // node order: wave entry -> pod records in registers
+  uint64_t cyc_run = 0;  // node order: cycles in run-pass visits
+  uint32_t narrow = 0;   // node order: the candidate's run passes are 32-bit scaled
 };
 
 // One candidate's canDrainNode with 64 * SPL touched-node slots.  Returns the
@@ -765,6 +778,57 @@ __device__ __forceinline__ uint64_t place_runs(uint64_t P, int lane, int64_t rc,
   return placed;
 }
 
+// Narrow requests of a candidate: in each dimension every request is a
+// multiple of 2^k (k = the smallest trailing-zero count among them) and
+// request >> k < 2^26, so 64 of them sum below 2^32.  A sum S of such requests
+// fits a free value f exactly when S >> k <= f >> k (f >= 0; S is a multiple
+// of 2^k), so the run pass can scan 32-bit scaled requests.
+struct Narrow {
+  int kc, km, ke;
+};
+__device__ __forceinline__ uint32_t cap32(int64_t f, int k) {  // f >> k clamped to [0, 2^32); f < 0: nothing fits
+  const int64_t q = f >> k;
+  return q < 0 ? 0u : (q > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(q));
+}
+
+template <bool E>
+__device__ __forceinline__ uint64_t place_runs_narrow(uint64_t P, int lane, int64_t rc, int64_t rm, int64_t re,
+                                                      uint32_t nc, uint32_t nm, uint32_t ne, const Narrow& k,
+                                                      uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
+                                                      int& left, uint32_t& it) {
+  uint64_t placed = 0;
+  while (P != 0 && left >= 1) {
+    ++it;
+    const bool in = (P >> lane) & 1;
+    const uint32_t ic = scan_add32(in ? nc : 0u), im = scan_add32(in ? nm : 0u);
+    const uint32_t ie = E ? scan_add32(in ? ne : 0u) : 0u;
+    const int below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(P >> 32),
+                                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(P), 0));
+    // a negative free value: no sum fits (zero sums included), as with the 64-bit compare
+    uint64_t res = (cpu >= 0 ? ballot(ic <= cap32(cpu, k.kc)) : 0ull) & (mem >= 0 ? ballot(im <= cap32(mem, k.km)) : 0ull);
+    res &= eph >= 0 ? (E ? ballot(ie <= cap32(eph, k.ke)) : ~0ull) : 0ull;
+    const uint64_t ok = ballot(below < left) & (zm | res);
+    const uint64_t bad = P & ~ok;
+    const uint64_t run = bad == 0 ? P : P & ((1ull << __builtin_ctzll(bad)) - 1);
+    if (run != 0) {
+      const int last = 63 - __builtin_clzll(run);
+      cpu -= static_cast<int64_t>(static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ic), last))) << k.kc);
+      mem -= static_cast<int64_t>(static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(im), last))) << k.km);
+      if (E)
+        eph -= static_cast<int64_t>(static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ie), last))) << k.ke);
+      left -= __builtin_popcountll(run);
+      placed |= run;
+    }
+    if (bad == 0) break;
+    P &= ~run;
+    // pods that do not fit the node as it is now fail whatever comes after
+    uint64_t alone = ballot(rc <= cpu) & ballot(rm <= mem);
+    alone &= E ? ballot(re <= eph) : (eph >= 0 ? ~0ull : 0ull);
+    P &= zm | alone;
+  }
+  return placed;
+}
+
 // Placement at one node visit.  Visits whose pods set or meet state bits
 // (host ports, anti-affinity pairs) run pod by pod: the run pass would add an
 // OR scan and a rescan per failing pod, and measured slower there (C5).  The
@@ -772,7 +836,8 @@ __device__ __forceinline__ uint64_t place_runs(uint64_t P, int lane, int64_t rc,
 // every extra copy of this code is instruction-cache footprint a wave jumps
 // between (measured on C5: specialising all four E / O combinations cost 5 %).
 __device__ __forceinline__ uint64_t place_at(const DevWorkload& w, uint64_t P, int lane, int64_t rc, int64_t rm,
-                                             int64_t re, uint64_t pm, uint64_t zm, int64_t& cpu, int64_t& mem,
+                                             int64_t re, uint64_t pm, uint64_t zm, uint32_t nc, uint32_t nm,
+                                             uint32_t ne, const Narrow& k, bool narrow, int64_t& cpu, int64_t& mem,
                                              int64_t& eph, uint64_t& ports, int& left, K2Stats& st) {
   const bool E = (ballot(re != 0) & P) != 0;  // some pod asks for ephemeral storage
   const bool O = (ballot(pm != 0) & P) != 0;  // some pod sets / meets state bits
@@ -782,6 +847,11 @@ __device__ __forceinline__ uint64_t place_at(const DevWorkload& w, uint64_t P, i
   }
   if (__builtin_popcountll(P) >= w.k2_scan_min) {
     ++st.run_visits;
+    st.narrow = narrow;
+    if (narrow) {
+      if (E) return place_runs_narrow<true>(P, lane, rc, rm, re, nc, nm, ne, k, zm, cpu, mem, eph, left, st.run_it);
+      return place_runs_narrow<false>(P, lane, rc, rm, re, nc, nm, ne, k, zm, cpu, mem, eph, left, st.run_it);
+    }
     if (E) return place_runs<true, false>(P, lane, rc, rm, re, pm, 0ull, zm, cpu, mem, eph, ports, left, st.run_it);
     return place_runs<false, false>(P, lane, rc, rm, re, pm, 0ull, zm, cpu, mem, eph, ports, left, st.run_it);
   }
@@ -820,6 +890,36 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     node[g] = -1;
     const uint64_t e = ballot(64 * g + lane < np && static_cast<uint32_t>(r01[g]) == w.s_empty_off);
     if (e != 0) dead = min(dead, 64 * g + __builtin_ctzll(e));
+  }
+  // Narrow (32-bit scaled) run passes when every request of the candidate
+  // allows them (place_runs_narrow): the smallest trailing-zero count per
+  // dimension, then every scaled request below 2^26.
+  Narrow nk;
+  bool narrow;
+  uint32_t nc[G], nm[G], ne[G];
+  {
+    auto tz = [](int64_t v) { return v == 0 ? 64 : __builtin_ctzll(static_cast<uint64_t>(v)); };
+    int mc = 64, mm = 64, me = 64;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      mc = min(mc, tz(rc[g]));
+      mm = min(mm, tz(rm[g]));
+      me = min(me, tz(re[g]));
+    }
+    nk.kc = min(wave_min(mc), 62);
+    nk.km = min(wave_min(mm), 62);
+    nk.ke = min(wave_min(me), 62);
+    bool ok = true;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint64_t a = static_cast<uint64_t>(rc[g]) >> nk.kc, b = static_cast<uint64_t>(rm[g]) >> nk.km,
+                     c = static_cast<uint64_t>(re[g]) >> nk.ke;
+      ok = ok && (a | b | c) < (1ull << 26);
+      nc[g] = static_cast<uint32_t>(a);
+      nm[g] = static_cast<uint32_t>(b);
+      ne[g] = static_cast<uint32_t>(c);
+    }
+    narrow = w.k2_narrow && ballot(!ok) == 0;
   }
   // node records of window 0 (spot nodes [0, 64)), where first fit usually
   // lands: in flight together with the F heads below
@@ -1015,7 +1115,11 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       const uint64_t cand = ballot(((act[g] >> lane) & 1) && ptr[g] == n);
       uint64_t placed = 0;
       if (cand != 0) {  // wave-uniform
-        placed = place_at(w, cand, lane, rc[g], rm[g], re[g], pm[g], zm[g], cpu, mem, eph, ports, left, st);
+        const uint32_t rv = st.run_visits;
+        const uint64_t t0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
+        placed = place_at(w, cand, lane, rc[g], rm[g], re[g], pm[g], zm[g], nc[g], nm[g], ne[g], nk, narrow, cpu,
+                          mem, eph, ports, left, st);
+        if (PROF && st.run_visits != rv) st.cyc_run += __builtin_amdgcn_s_memtime() - t0 + (placed & 0);
         placements += __builtin_popcountll(placed);
       }
       if ((placed >> lane) & 1) node[g] = n;
@@ -1355,6 +1459,7 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
         pr[12] = static_cast<uint64_t>(st.run_it) | static_cast<uint64_t>(st.seq_it) << 32;
         pr[13] = static_cast<uint64_t>(st.run_visits) | static_cast<uint64_t>(st.seq_visits) << 32;
         pr[14] = st.cyc_rec - c_start;
+        pr[15] = st.cyc_run << 1 | st.narrow;
       }
     }
   }

@@ -11,7 +11,7 @@ from helpers import Scenario
 from oracle_lib import OracleSnapshot, load_oracle, oracle_new_node_map, oracle_plan
 from randcluster import rand_scenario
 from spotplanner import capi
-from spotplanner.model import Container, ContainerPort, GiB, Node, Pod
+from spotplanner.model import Container, ContainerPort, GiB, Node, OwnerReference, Pod
 from spotplanner.rescheduler import plan_arrays
 from spotplanner.synth import SynthCluster, build_candidates, new_node_map
 
@@ -486,3 +486,72 @@ def test_many_deployments_with_hostname_anti_affinity(checker):
                       for k in range(r.randint(2, 5))])
     _, o, p = run_scenario(checker, nodes, spot_pods, cands)
     assert len(set(int(x) for x in p.node_of_pod if x >= 0)) > 8  # conflicts push replicas past the first nodes
+
+
+# ------------------------------------------- node order: 32-bit scaled run passes
+def _granular_scenario(seed: int):
+    """Many small pods onto few nodes (run passes of several pods), with request
+    granularities that do and do not allow the scaled 32-bit sums: MiB multiples,
+    odd byte counts, scaled values at the 2^26 limit, sums landing exactly on a
+    node's free value (not itself a multiple of the granularity), and
+    overcommitted nodes (negative free values)."""
+    import random
+    r = random.Random(seed)
+    mode = seed % 4
+    unit = {0: 1 << 20, 1: 1, 2: 1 << 20, 3: 3}[mode]
+    n_spot = 3 + seed % 5
+    nodes = []
+    for i in range(n_spot):
+        mem = r.choice([1, 2, 4]) * GiB + r.choice([0, 1, 12345])
+        if mode == 2:
+            mem = (1 << 46) + r.choice([0, 1, 1 << 20])  # scaled by 2^20: just around 2^26
+        nodes.append(Node(name="n%d" % i, cpu_milli=r.choice([1000, 2000, 4001]), memory=mem, pods=110,
+                          ephemeral=r.choice([0, 10 * GiB + 7]), labels={"kubernetes.io/hostname": "n%d" % i}))
+    spot_pods = []
+    for i, n in enumerate(nodes):
+        ps = []
+        if r.random() < 0.3:  # overcommitted: free values below zero
+            ps.append(Pod(name="big%d" % i, containers=[Container(cpu_milli=n.cpu_milli + 100,
+                                                                  memory=n.memory + unit)]))
+        spot_pods.append(ps)
+    cands = []
+    for c in range(10):
+        pods = []
+        for k in range(r.randint(2, 24)):
+            if mode == 2:
+                mem = r.choice([(1 << 45), (1 << 44) + (1 << 20), ((1 << 26) - 1) << 20, 1 << 20])
+            else:
+                mem = r.randint(1, 600) * unit * (1 if mode != 0 else r.choice([1, 1, 64]))
+            cpu = r.choice([0, 50, 100, 250, 333, 1000])
+            eph = r.choice([0, 0, unit * r.randint(1, 1 << 20)])
+            pods.append(Pod(name="c%d_%d" % (c, k), containers=[Container(cpu_milli=cpu, memory=mem, ephemeral=eph)],
+                            owner_references=[OwnerReference("ReplicaSet")]))
+        # a pod sized to the remaining free memory of node 0 exactly
+        if c % 3 == 0 and not spot_pods[0]:
+            pods.append(Pod(name="c%d_fill" % c, containers=[Container(memory=nodes[0].memory - sum(
+                p.containers[0].memory for p in pods) % nodes[0].memory)], owner_references=[OwnerReference("ReplicaSet")]))
+        cands.append(pods)
+    return nodes, spot_pods, cands
+
+
+@pytest.mark.parametrize("narrow", [0, 1])
+def test_scaled_run_pass_matches_oracle(narrow):
+    # SR_K2_NARROW=0 keeps every run pass on 64-bit sums; 1 (the default) scales
+    # a candidate's requests to 32 bits where that is exact
+    import os
+    from spotplanner.planner import PredicateChecker
+    os.environ["SR_K2_NARROW"] = str(narrow)
+    try:
+        c = PredicateChecker(0)
+    finally:
+        del os.environ["SR_K2_NARROW"]
+    try:
+        for seed in range(24):
+            nodes, spot_pods, cands = _granular_scenario(7000 + seed)
+            run_scenario(c, nodes, spot_pods, cands)
+        for seed in range(10):
+            nodes, spot_pods, cands = rand_scenario(7100 + seed, n_spot=4 + seed, n_cand=12, max_pods=30,
+                                                    features=False)
+            run_scenario(c, nodes, spot_pods, cands)
+    finally:
+        c.close()

@@ -14,7 +14,8 @@ Each sr_plan_run appends {int64 n_cand, int64 n_k0} + n_cand x 16 u64 (K2)
 Node-order waves ([5] == 2) reuse the fields: [6] placements, [7] visits |
 windows << 32, [8] prologue (F heads) cycles, [9] min + window + node
 state, [10] placement, [11] pointer moves (+ far resolution), [14] cycles
-from wave start to the pod records and window 0 in registers.
+from wave start to the pod records and window 0 in registers, [15] cycles
+in run-pass visits << 1 | 1 if the candidate's run passes are 32-bit scaled.
 The last of the widest runs in the file is summarised (earlier ones are
 warmup; narrower ones are prefix batches of sr_plan_first)."""
 import sys
@@ -89,6 +90,9 @@ def main():
         print("node order: cycles/visit min+window+state %.0f, placement %.0f, pointer moves %.0f"
               % (q[:, 9].sum() / sv, q[:, 10].sum() / sv, q[:, 11].sum() / sv))
         print("node order: wave dur us p50/p90/max %s" % pct(dur[nodeo]))
+        runv = (q[:, 13] & 0xffffffff).astype(np.int64)
+        print("node order: 32-bit scaled run passes in %d of %d waves; cycles per run-pass visit %.0f"
+              % (int((q[:, 15] & 1).sum()), len(q), (q[:, 15] >> 1).sum() / max(1, runv.sum())))
     if (~nodeo).any():
         print("pod order:  wave dur us p50/p90/max %s" % pct(dur[~nodeo]))
     r = r[~nodeo] if (~nodeo).any() else r
