@@ -1,5 +1,7 @@
 #!/bin/bash
 # One GPU session: parity tests, bench (default K2 + pod-order A/B), K2 per-wave
+# (rocprof and PMC passes run without the end-to-end ticks, whose prefix-batch
+# launches would pull the per-launch averages below the full tick's),
 # profile, rocprofv3 kernel trace and the two PMC traffic passes.
 #   tools/gpu_round.sh [tag] [config] [skip-tests]
 # Every GPU step has its own time limit; the script stops at the first step
@@ -34,14 +36,14 @@ python tools/k2_profile.py "/tmp/k2prof_$tag.bin" > "$out/k2prof.txt" 2>&1; cat 
 rm -f /tmp/k2prof_$tag.bin
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run --output-format csv -- \
-  python3 "$R/bench.py" --config "$cfg" --steps 200 --warmup 10 --no-cpu-baseline > "$out/prof.log" 2>&1
+  python3 "$R/bench.py" --config "$cfg" --steps 200 --warmup 10 --no-cpu-baseline --e2e-reps 0 > "$out/prof.log" 2>&1
 rc=$?; echo "rocprof trace rc=$rc"; tail -1 "$out/prof.log" | cut -c1-300
 [ $rc -ne 0 ] && exit $rc
 f=$(find "$out/prof" -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cut -c1-200 "$f"
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$out/pmc_fetch" -o run --output-format csv -- \
-  python3 "$R/bench.py" --config "$cfg" --steps 20 --warmup 2 --no-cpu-baseline > "$out/pmc_fetch.log" 2>&1
+  python3 "$R/bench.py" --config "$cfg" --steps 20 --warmup 2 --no-cpu-baseline --e2e-reps 0 > "$out/pmc_fetch.log" 2>&1
 rc=$?; echo "pmc FETCH_SIZE rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$out/pmc_write" -o run --output-format csv -- \
-  python3 "$R/bench.py" --config "$cfg" --steps 20 --warmup 2 --no-cpu-baseline > "$out/pmc_write.log" 2>&1
+  python3 "$R/bench.py" --config "$cfg" --steps 20 --warmup 2 --no-cpu-baseline --e2e-reps 0 > "$out/pmc_write.log" 2>&1
 rc=$?; echo "pmc WRITE_SIZE rc=$rc"; [ $rc -ne 0 ] && exit $rc
 cd "$R" && python tools/pmc_traffic.py "$out/pmc_fetch" "$out/pmc_write" "$out/pmc_traffic_c$cfg.json"
