@@ -553,5 +553,10 @@ def test_scaled_run_pass_matches_oracle(narrow):
             nodes, spot_pods, cands = rand_scenario(7100 + seed, n_spot=4 + seed, n_cand=12, max_pods=30,
                                                     features=False)
             run_scenario(c, nodes, spot_pods, cands)
+        for seed in range(16):  # host ports and hostname anti-affinity next to scaled runs
+            nodes, spot_pods, cands = rand_scenario(7200 + seed, n_spot=4 + seed % 8, n_cand=12, max_pods=24,
+                                                    anti=0.3, hostname_only=True)
+            run_scenario(c, nodes, spot_pods, cands)
+        tick_parity(c, SynthCluster(5, seed=21))
     finally:
         c.close()
