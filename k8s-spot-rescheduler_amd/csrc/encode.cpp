@@ -1192,14 +1192,76 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
                 A + static_cast<size_t>(A_REQ + i) * Wp);
   }
   std::copy(C.taint_rows.begin(), C.taint_rows.end(), A + static_cast<size_t>(A_TAINT) * Wp);
-  if (n_ports > 0)
-    for (int32_t n = 0; n < n_spot; ++n)
+  if (n_ports > 0) {
+    // HostPortInfo.CheckConflict of each query against every node's base
+    // UsedPorts.  Rows are kept across calls by query: a state refresh that
+    // patched a few nodes patches their bits, any other refresh drops them.
+    auto conflicts = [&](int32_t n, const PortQuery& pq) {
       for (const Port& u : snap->state[n].ports)
-        for (int32_t q = 0; q < n_ports; ++q) {
-          const PortQuery& pq = port_query[q];
-          if (pq.proto == u.proto && pq.port == u.port && (pq.ip == -1 || u.ip == -1 || u.ip == pq.ip))
-            A[static_cast<size_t>(A_PORT + q) * Wp + (n >> 6)] |= 1ull << (n & 63);
+        if (pq.proto == u.proto && pq.port == u.port && (pq.ip == -1 || u.ip == -1 || u.ip == pq.ip)) return true;
+      return false;
+    };
+    auto qkey = [](const PortQuery& pq) {
+      return mix(mix(mix(0x51ull, static_cast<uint32_t>(pq.proto)), static_cast<uint32_t>(pq.port)),
+                 static_cast<uint32_t>(pq.ip));
+    };
+    if (C.port_rows_gen != C.state_gen) {
+      const bool patch = C.port_rows_gen == C.patched_from && !C.patched_nodes.empty() && C.port_rows.size() < 4096;
+      if (patch) {
+        for (auto& kv : C.port_rows) {
+          // the key does not carry the query: rebuild it from the row's stored tail
+          const std::vector<uint64_t>& row = kv.second;
+          const PortQuery pq{static_cast<int32_t>(row[Wp]), static_cast<int32_t>(row[Wp + 1]),
+                             static_cast<int32_t>(row[Wp + 2])};
+          for (int32_t n : C.patched_nodes) {
+            uint64_t& wd = kv.second[static_cast<size_t>(n >> 6)];
+            const uint64_t bit = 1ull << (n & 63);
+            wd = conflicts(n, pq) ? (wd | bit) : (wd & ~bit);
+          }
         }
+      } else {
+        C.port_rows.clear();
+      }
+      C.port_rows_gen = C.state_gen;
+    }
+    std::vector<int32_t> missing;
+    std::vector<std::vector<uint64_t>*> rows(static_cast<size_t>(n_ports), nullptr);
+    for (int32_t q = 0; q < n_ports; ++q) {
+      const PortQuery& pq = port_query[q];
+      auto it = C.port_rows.find(qkey(pq));
+      if (it != C.port_rows.end() && static_cast<int32_t>(it->second[Wp]) == pq.proto &&
+          static_cast<int32_t>(it->second[Wp + 1]) == pq.port && static_cast<int32_t>(it->second[Wp + 2]) == pq.ip) {
+        rows[q] = &it->second;
+      } else {
+        missing.push_back(q);
+      }
+    }
+    if (!missing.empty()) {  // one pass over the nodes for every query not cached
+      std::vector<std::vector<uint64_t>> fresh(missing.size(), std::vector<uint64_t>(static_cast<size_t>(Wp) + 3, 0));
+      for (int32_t n = 0; n < n_spot; ++n)
+        for (const Port& u : snap->state[n].ports)
+          for (size_t m = 0; m < missing.size(); ++m) {
+            const PortQuery& pq = port_query[missing[m]];
+            if (pq.proto == u.proto && pq.port == u.port && (pq.ip == -1 || u.ip == -1 || u.ip == pq.ip))
+              fresh[m][static_cast<size_t>(n >> 6)] |= 1ull << (n & 63);
+          }
+      for (size_t m = 0; m < missing.size(); ++m) {
+        const PortQuery& pq = port_query[missing[m]];
+        fresh[m][Wp] = static_cast<uint64_t>(static_cast<uint32_t>(pq.proto));
+        fresh[m][Wp + 1] = static_cast<uint64_t>(static_cast<uint32_t>(pq.port));
+        fresh[m][Wp + 2] = static_cast<uint64_t>(static_cast<uint32_t>(pq.ip));
+        if (C.port_rows.size() < 4096 && C.port_rows.find(qkey(pq)) == C.port_rows.end()) {
+          auto& slot = C.port_rows[qkey(pq)];
+          slot = std::move(fresh[m]);
+          rows[missing[m]] = &slot;
+        } else {  // full, or another query under the same key: not cached
+          std::copy_n(fresh[m].begin(), Wp, A + static_cast<size_t>(A_PORT + missing[m]) * Wp);
+        }
+      }
+    }
+    for (int32_t q = 0; q < n_ports; ++q)
+      if (rows[q]) std::copy_n(rows[q]->begin(), Wp, A + static_cast<size_t>(A_PORT + q) * Wp);
+  }
   for (int32_t t = 0; t < anti.n_terms; ++t) {
     std::copy_n(&anti.da[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t) * Wp);
     std::copy_n(&anti.db[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t + 1) * Wp);

@@ -11,6 +11,7 @@
 #include <deque>
 #include <cstdint>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/sr_planner.h"
@@ -279,6 +280,10 @@ struct EncoderCache {
   std::vector<uint64_t> podcount_row;  // [Wp] len(pods)+1 <= allowed pods
   std::vector<int64_t> sorted_free[3]; // every node's free value, sorted
   std::vector<int64_t> node_vals[3];   // distinct free values, sorted
+  // base UsedPorts conflict rows by query (proto, port, ip), valid for state
+  // generation port_rows_gen (patched node by node when few nodes changed)
+  std::unordered_map<uint64_t, std::vector<uint64_t>> port_rows;
+  uint64_t port_rows_gen = ~0ull;
   // ---- content-interned, node independent
   struct SpecShard {
     WordDict dict;               // static spec words -> local id

@@ -145,15 +145,18 @@ def patch_checker():
     c.close()
 
 
+@pytest.mark.parametrize("config", [3, 5])
 @pytest.mark.parametrize("which", ["default", "patch"])
-def test_consecutive_ticks_one_node_changed(checker, patch_checker, which):
+def test_consecutive_ticks_one_node_changed(checker, patch_checker, which, config):
     """Tick after tick on fresh snapshots of one cluster, each with one more
     pod placed on some spot node (its state changes, the static view not):
     every full plan equals the oracle on the same mutated snapshot.  `patch`:
-    the changed nodes' records go to the device one by one."""
+    the changed nodes' records go to the device one by one.  Config 5: the
+    added pods carry host ports, so the cached base port-conflict rows are
+    patched node by node."""
     other = checker
     checker = patch_checker if which == "patch" else checker
-    sc = SynthCluster(3, seed=21, n_on_demand=200, n_spot=450)
+    sc = SynthCluster(config, seed=21, n_on_demand=200, n_spot=450)
     lib = capi.load_planner()
     nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
     cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
