@@ -80,6 +80,7 @@ struct sr_ctx {
   sr::Workload wl;
   sr::EncoderCache enc;      // what the encoder keeps across calls (encode.cpp)
   uint64_t dev_state_gen = ~0ull;  // encoder state whose node records the device arena holds
+  uint64_t host_state_gen = ~0ull; // ... and the pinned staging arena (kept between calls)
   hipEvent_t ev_upload = nullptr;  // the last upload (the staging buffer is reused after it)
   int32_t prefix_batch = 16;       // first batch of sr_plan_first (SR_PREFIX_BATCH; tools/gpu_prefix.sh)
   sr::DevWorkload dw{};
@@ -211,7 +212,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   st = settle(ctx);
   if (st != SR_OK) return st;
   if (ctx->ev_upload) HIP_TRY(ctx, hipEventSynchronize(ctx->ev_upload));  // staging buffer free again
+  const size_t h_cap = ctx->h_arena.cap;
   HIP_TRY(ctx, host_reserve(ctx->h_arena, bytes));
+  if (ctx->h_arena.cap != h_cap) ctx->host_state_gen = ~0ull;  // a new staging buffer holds no node records
   const size_t arena_cap = ctx->arena.cap;
   HIP_TRY(ctx, dev_reserve(ctx->arena, bytes));  // a new allocation holds no node records
   const bool same_arena = ctx->arena.cap == arena_cap;
@@ -234,14 +237,34 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, host_reserve(ctx->h_early, sizeof(uint64_t) * (static_cast<size_t>(ncand) + na + 1)));
   auto t1 = std::chrono::steady_clock::now();
   const size_t from = nodes_resident || nodes_patch ? node_bytes : 0;
-  pk.copy_to(static_cast<char*>(ctx->h_arena.p), from);
+  // The staging arena keeps the node section of the generation it last held:
+  // when that is the current one, or the one the encoder patched a few nodes
+  // on, only those nodes' records are rewritten (no copy of the whole section).
+  {
+    char* hs = static_cast<char*>(ctx->h_arena.p);
+    const size_t NP = static_cast<size_t>(w.n_pad);
+    if (ctx->host_state_gen == w.state_gen) {
+      // current
+    } else if (ctx->host_state_gen == E.patched_from && E.state_gen == w.state_gen && !E.patched_nodes.empty()) {
+      for (int32_t i : E.patched_nodes) {
+        std::memcpy(hs + o_nr + static_cast<size_t>(i) * 64, &E.node_rec[static_cast<size_t>(i) * 8], 64);
+        for (size_t dm = 0; dm < 3; ++dm)
+          std::memcpy(hs + o_nf + (dm * NP + static_cast<size_t>(i)) * 8, &E.node_free[dm * NP + i], 8);
+      }
+    } else {
+      std::memcpy(hs + o_nr, E.node_rec.data(), E.node_rec.size() * sizeof(uint64_t));
+      std::memcpy(hs + o_nf, E.node_free.data(), E.node_free.size() * sizeof(int64_t));
+    }
+    ctx->host_state_gen = w.state_gen;
+  }
+  pk.copy_to(static_cast<char*>(ctx->h_arena.p), node_bytes);
   size_t patch_bytes = 0;
   if (nodes_patch) {
     char* hs = static_cast<char*>(ctx->h_arena.p);
     char* ds = static_cast<char*>(ctx->arena.p);
     const size_t NP = static_cast<size_t>(w.n_pad);
-    auto put = [&](size_t off, const void* src, size_t n) -> hipError_t {
-      std::memcpy(hs + off, src, n);
+    auto put = [&](size_t off, const void* src, size_t n) -> hipError_t {  // the staging copy is current
+      (void)src;
       patch_bytes += n;
       return hipMemcpyAsync(ds + off, hs + off, n, hipMemcpyHostToDevice, ctx->stream);
     };
