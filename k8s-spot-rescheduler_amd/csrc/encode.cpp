@@ -1206,7 +1206,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
                  static_cast<uint32_t>(pq.ip));
     };
     if (C.port_rows_gen != C.state_gen) {
-      const bool patch = C.port_rows_gen == C.patched_from && !C.patched_nodes.empty() && C.port_rows.size() < 4096;
+      const bool patch = C.patched_from != ~0ull && C.port_rows_gen == C.patched_from && !C.patched_nodes.empty() &&
+                         C.port_rows.size() < 4096;
       if (patch) {
         for (auto& kv : C.port_rows) {
           // the key does not carry the query: rebuild it from the row's stored tail

@@ -245,7 +245,8 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
     const size_t NP = static_cast<size_t>(w.n_pad);
     if (ctx->host_state_gen == w.state_gen) {
       // current
-    } else if (ctx->host_state_gen == E.patched_from && E.state_gen == w.state_gen && !E.patched_nodes.empty()) {
+    } else if (E.patched_from != ~0ull && ctx->host_state_gen == E.patched_from && E.state_gen == w.state_gen &&
+               !E.patched_nodes.empty()) {
       for (int32_t i : E.patched_nodes) {
         std::memcpy(hs + o_nr + static_cast<size_t>(i) * 64, &E.node_rec[static_cast<size_t>(i) * 8], 64);
         for (size_t dm = 0; dm < 3; ++dm)
