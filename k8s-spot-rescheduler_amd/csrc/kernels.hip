@@ -864,10 +864,12 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
                                               const int np, int& status, K2Stats& st, uint32_t& nbytes) {
   static_assert(64 * G * kNHS * 8 <= sizeof(K2Lds), "node-order LDS exceeds the wave's K2 region");
   const int lane = threadIdx.x & 63;
-  const int Wp = w.Wp;  // <= 64
+  const int Wp = w.Wp;
   const uint64_t* __restrict__ tab = w.S;
   int64_t rc[G], rm[G], re[G];
   uint64_t pm[G], r01[G], r23[G], fmask[G], act[G];
+  int fbase[G];  // first word of the 64-word chunk fmask describes (rows wider than 64 words)
+  bool unres[G]; // the pointer is a chunk boundary not yet scanned (kFar: the end of the head)
   uint64_t cur[G];  // F word holding the pod's pointer: moves inside a word need no LDS read
   uint32_t hmask[G];
   bool zero[G];
@@ -884,6 +886,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     r23[g] = pr[5];
     zero[g] = (rc[g] | rm[g] | re[g]) == 0;  // fitsRequest skips the resource checks
     fmask[g] = 0;
+    fbase[g] = 0;
+    unres[g] = false;
     hmask[g] = 0;
     cur[g] = 0;
     ptr[g] = INT_MAX;
@@ -1009,6 +1013,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         ptr[g] = w0 * 64 + __builtin_ctzll(cur[g]);
       } else {
         ptr[g] = Wp > kNH ? kFar : INT_MAX;
+        unres[g] = Wp > kNH;
       }
     }
     const uint64_t gone = ballot(k < dead && ptr[g] == INT_MAX);
@@ -1034,46 +1039,73 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     for (int g = 0; g < G; ++g) mine = ((act[g] >> lane) & 1) ? min(mine, ptr[g]) : mine;
     const int n = wave_min(mine);
     if (n == INT_MAX) break;  // unreachable: every pod still to place has a pointer
-    if (n == kFar) {
-      // every node of the head is done: resolve the pods pointing beyond it,
-      // one full-row scan each (lanes = words)
-      const bool wv = lane >= kNH && lane < Wp;
-      const uint32_t wi = wv ? static_cast<uint32_t>(lane) : 0u;
+    // Unresolved pointers sit on chunk boundaries (kFar: the end of the head;
+    // beyond it, the end of a 64-word chunk whose mask ran out).  When the
+    // minimum reaches one, its pods scan their F rows from there, 64 words
+    // per round (lanes = words), before node n is visited: a pod may resolve
+    // to n itself.
+    uint64_t unres_n = 0;
+    if (n == kFar || (n & 4095) == 0) {  // wave-uniform
+#pragma unroll
+      for (int g = 0; g < G; ++g) unres_n |= ballot(((act[g] >> lane) & 1) && ptr[g] == n && unres[g]);
+    }
+    if (unres_n != 0) {
+      const int sw = n >> 6;  // first word to scan (every pending pod points at n)
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        uint64_t pend = ballot(((act[g] >> lane) & 1) && ptr[g] == kFar);
-        while (pend != 0) {  // 4 pods per round: their 16 loads in flight together
+        uint64_t pend = ballot(((act[g] >> lane) & 1) && ptr[g] == n && unres[g]);
+        while (pend != 0) {  // 4 pods per round: their 16 loads per chunk in flight together
           int js[4];
-          uint64_t x[4][4];
+          uint64_t a01[4], a23[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             js[q] = pend != 0 ? __builtin_ctzll(pend) : -1;
             pend &= pend - 1;
             const int j = js[q] < 0 ? 0 : js[q];
-            const uint64_t a01 = readlane64(r01[g], j), a23 = readlane64(r23[g], j);
-            x[q][0] = tab[static_cast<uint32_t>(a01) + wi];
-            x[q][1] = tab[static_cast<uint32_t>(a01 >> 32) + wi];
-            x[q][2] = tab[static_cast<uint32_t>(a23) + wi];
-            x[q][3] = tab[static_cast<uint32_t>(a23 >> 32) + wi];
+            a01[q] = readlane64(r01[g], j);
+            a23[q] = readlane64(r23[g], j);
           }
+          int todo = 0;  // bit q: pod js[q] not resolved yet
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (js[q] < 0) continue;  // wave-uniform
-            nbytes += 32u * static_cast<uint32_t>(Wp - kNH);
-            const uint64_t f = wv ? (x[q][0] & x[q][1] & x[q][2] & x[q][3]) : 0ull;
-            const uint64_t m = ballot(f != 0);
-            int nx = INT_MAX;
-            if (m != 0) {
-              const int w2 = __builtin_ctzll(m);
-              nx = w2 * 64 + __builtin_ctzll(readlane64(f, w2));
+          for (int q = 0; q < 4; ++q) todo |= js[q] >= 0 ? 1 << q : 0;
+          for (int cb = (sw >> 6) << 6; todo != 0 && cb < Wp; cb += 64) {  // wave-uniform, <= Wp / 64 rounds
+            const int word = cb + lane;
+            const bool wv = word >= sw && word < Wp;
+            const uint32_t wi = wv ? static_cast<uint32_t>(word) : 0u;
+            uint64_t x[4][4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (!((todo >> q) & 1)) continue;  // wave-uniform
+              x[q][0] = tab[static_cast<uint32_t>(a01[q]) + wi];
+              x[q][1] = tab[static_cast<uint32_t>(a01[q] >> 32) + wi];
+              x[q][2] = tab[static_cast<uint32_t>(a23[q]) + wi];
+              x[q][3] = tab[static_cast<uint32_t>(a23[q] >> 32) + wi];
             }
-            const uint64_t fw = nx == INT_MAX ? 0ull : readlane64(f, nx >> 6);
-            if (lane == js[q]) {
-              fmask[g] = m;
-              ptr[g] = nx;
-              cur[g] = fw;
+            const uint32_t nw = static_cast<uint32_t>(__builtin_popcountll(ballot(wv)));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (!((todo >> q) & 1)) continue;  // wave-uniform
+              nbytes += 32u * nw;
+              const uint64_t f = wv ? (x[q][0] & x[q][1] & x[q][2] & x[q][3]) : 0ull;
+              const uint64_t m = ballot(f != 0);
+              if (m == 0 && cb + 64 < Wp) continue;  // nothing in this chunk: the next one
+              todo &= ~(1 << q);
+              int nx = INT_MAX;
+              uint64_t fw = 0;
+              if (m != 0) {
+                const int w2 = __builtin_ctzll(m);
+                fw = readlane64(f, w2);
+                nx = (cb + w2) * 64 + __builtin_ctzll(fw);
+              }
+              if (lane == js[q]) {
+                fmask[g] = m;
+                fbase[g] = cb;
+                ptr[g] = nx;
+                cur[g] = fw;
+                unres[g] = false;
+              }
+              if (nx == INT_MAX) dead = min(dead, 64 * g + js[q]);
             }
-            if (nx == INT_MAX) dead = min(dead, 64 * g + js[q]);
           }
         }
       }
@@ -1150,14 +1182,19 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
             nx = w2 * 64 + __builtin_ctzll(cur[g]);
           } else if (Wp > kNH) {
             nx = kFar;
+            unres[g] = true;
           }
         } else {
-          const uint64_t rem = W == 63 ? 0ull : fmask[g] & (~0ull << (W + 1));
+          const int lw = W - fbase[g];  // the pointer's word within the chunk fmask describes
+          const uint64_t rem = lw >= 63 ? 0ull : fmask[g] & (~0ull << (lw + 1));
           if (rem != 0) {
-            const int w2 = __builtin_ctzll(rem);
+            const int w2 = fbase[g] + __builtin_ctzll(rem);
             cur[g] = f_word_far(tab, r01[g], r23[g], w2);
             nx = w2 * 64 + __builtin_ctzll(cur[g]);
             far_word = true;
+          } else if (fbase[g] + 64 < Wp) {
+            nx = (fbase[g] + 64) * 64;  // the next chunk, scanned when the minimum gets there
+            unres[g] = true;
           }
         }
         ptr[g] = nx;
@@ -1415,7 +1452,7 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   int wide = 0;
   uint32_t nbytes = 0;
   bool node_order = false;
-  if constexpr (CH == 1) node_order = np <= 4 * 64 && w.k2_mode == 0;  // rows of <= 64 words
+  node_order = np <= 4 * 64 && w.k2_mode == 0;
   const int dbase = w.dyn_cand ? __builtin_amdgcn_readfirstlane(w.dyn_cand[ci]) : -1;
   if (dbase >= 0) {  // writes out_node itself
     wide = 3;

@@ -366,6 +366,25 @@ def test_many_chunks_of_spot_nodes(checker):
     assert list(p.node_of_pod) == [9000, 0]
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_wide_pool_sparse_capacity(checker, seed):
+    # rows of 133 words (three 64-word chunks): capacity only on scattered nodes,
+    # some right at the chunk boundaries, so pods resolve beyond the head, run
+    # out of a chunk's mask and move on to the next chunk
+    import random
+    r = random.Random(seed)
+    n = 2 * 4096 + 300
+    big = set(r.sample(range(n), 40)) | {511, 512, 4095, 4096, 4097, 8191, 8192, n - 1}
+    if seed % 2:
+        big -= set(range(0, 512))  # nothing in the head: every pod starts unresolved
+    nodes = [Node("n%d" % i, r.choice([1000, 1500, 2500]) if i in big else 100) for i in range(n)]
+    cands = []
+    for c in range(8):
+        cands.append([Pod("c%d_%d" % (c, k), containers=[Container(r.choice([200, 400, 600, 900]))])
+                      for k in range(r.randint(3, 40))])
+    run_scenario(checker, nodes, [[] for _ in nodes], cands)
+
+
 # ------------------------------------------------------------ synthetic configs
 def tick_parity(checker, sc: SynthCluster, max_cands=None, oracle_threads=8):
     lib = capi.load_planner()
