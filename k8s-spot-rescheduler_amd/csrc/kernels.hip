@@ -187,36 +187,49 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
         for (int u = 1; u < 8; ++u) op[q][u] = -1;
       }
     }
-    for (int wb = 0; wb < w.Wp; wb += 64) {
-      const int word = wb + lane;
-      const bool wv = word < w.Wp;
-      const size_t wi = wv ? static_cast<size_t>(word) : 0;
-      uint64_t v[kSClasses][8];
+    // rows wider than 64 words (C4: 548): two 64-word chunks per round, all
+    // their atom loads in flight together
+    for (int wb = 0; wb < w.Wp; wb += 128) {
+      const bool two = wb + 64 < w.Wp;  // wave-uniform
+      uint64_t v[2][kSClasses][8];
 #pragma unroll
-      for (int q = 0; q < kSClasses; ++q)
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        const int word = wb + 64 * h + lane;
+        const size_t wi = word < w.Wp ? static_cast<size_t>(word) : 0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[q][u] = op[q][u] >= 0 ? w.atoms[static_cast<size_t>(op[q][u] >> 2) * Wp + wi] : 0;
+        for (int q = 0; q < kSClasses; ++q)
 #pragma unroll
-      for (int q = 0; q < kSClasses; ++q) {
-        if (op[q][0] < 0 && op[q][0] != -1) continue;  // no class, or a long program (below)
-        uint64_t acc = ~0ull, any = 0, cur = 0;
-        bool has = false;
+          for (int u = 0; u < 8; ++u)
+            v[h][q][u] = op[q][u] >= 0 ? w.atoms[static_cast<size_t>(op[q][u] >> 2) * Wp + wi] : 0;
+      }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (op[q][u] < 0) break;  // wave-uniform
-          switch (op[q][u] & 3) {
-            case PROG_AND: acc &= v[q][u]; break;
-            case PROG_ANDNOT: acc &= ~v[q][u]; break;
-            case PROG_TERM_START:
-              any |= has ? cur : 0;
-              cur = v[q][u];
-              has = true;
-              break;
-            default: cur &= v[q][u]; break;
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        const int word = wb + 64 * h + lane;
+        const bool wv = word < w.Wp;
+#pragma unroll
+        for (int q = 0; q < kSClasses; ++q) {
+          if (op[q][0] < 0 && op[q][0] != -1) continue;  // no class, or a long program (below)
+          uint64_t acc = ~0ull, any = 0, cur = 0;
+          bool has = false;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            if (op[q][u] < 0) break;  // wave-uniform
+            switch (op[q][u] & 3) {
+              case PROG_AND: acc &= v[h][q][u]; break;
+              case PROG_ANDNOT: acc &= ~v[h][q][u]; break;
+              case PROG_TERM_START:
+                any |= has ? cur : 0;
+                cur = v[h][q][u];
+                has = true;
+                break;
+              default: cur &= v[h][q][u]; break;
+            }
           }
+          if (has) acc &= any | cur;
+          if (wv) w.S[static_cast<size_t>(c0 + q) * Wp + word] = acc;
         }
-        if (has) acc &= any | cur;
-        if (wv) w.S[static_cast<size_t>(c0 + q) * Wp + word] = acc;
       }
     }
 #pragma unroll
@@ -1081,13 +1094,17 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
               x[q][2] = tab[static_cast<uint32_t>(a23[q]) + wi];
               x[q][3] = tab[static_cast<uint32_t>(a23[q] >> 32) + wi];
             }
-            const uint32_t nw = static_cast<uint32_t>(__builtin_popcountll(ballot(wv)));
+            const uint64_t vw = ballot(wv);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               if (!((todo >> q) & 1)) continue;  // wave-uniform
-              nbytes += 32u * nw;
               const uint64_t f = wv ? (x[q][0] & x[q][1] & x[q][2] & x[q][3]) : 0ull;
               const uint64_t m = ballot(f != 0);
+              // algorithmic bytes: the words a sequential scan reads, up to the
+              // first non-zero one (the rest of the chunk is speculative)
+              const int upto = m != 0 ? __builtin_ctzll(m) : 63;
+              const uint64_t need = upto == 63 ? vw : vw & ((2ull << upto) - 1);
+              nbytes += 32u * static_cast<uint32_t>(__builtin_popcountll(need));
               if (m == 0 && cb + 64 < Wp) continue;  // nothing in this chunk: the next one
               todo &= ~(1 << q);
               int nx = INT_MAX;
@@ -1429,61 +1446,48 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
 
 // K2: one wave per candidate (list entries {candidate, first pod, end pod,
 // global index}, longest candidates first).
-template <int CH, bool PROF>
-__global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __restrict__ list, int n_list) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wave);
-  if (li >= n_list) return;
-  const uint64_t t_start = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
-  const uint64_t c_start = PROF ? __builtin_amdgcn_s_memtime() : 0;
+// A K2 wave's work-list entry (and profile stamps).
+struct K2Entry {
+  int ci, p0, np, g;
+  uint64_t t_start, c_start, t_list;
+};
+template <bool PROF>
+__device__ __forceinline__ K2Entry k2_entry(const int4* __restrict__ list, int li) {
+  K2Entry x;
+  x.t_start = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
+  x.c_start = PROF ? __builtin_amdgcn_s_memtime() : 0;
   const int4 e = list[li];
-  const int ci = __builtin_amdgcn_readfirstlane(e.x);
-  const int p0 = __builtin_amdgcn_readfirstlane(e.y);
-  const int np = __builtin_amdgcn_readfirstlane(e.z) - p0;  // >= 1: empty candidates never reach the device
-  const int g = __builtin_amdgcn_readfirstlane(e.w);
+  x.ci = __builtin_amdgcn_readfirstlane(e.x);
+  x.p0 = __builtin_amdgcn_readfirstlane(e.y);
+  x.np = __builtin_amdgcn_readfirstlane(e.z) - x.p0;  // >= 1: empty candidates never reach the device
+  x.g = __builtin_amdgcn_readfirstlane(e.w);
   if (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the work-list entry has arrived
-  const uint64_t t_list = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
-  K2Lds& L = *reinterpret_cast<K2Lds*>(k2_lds + static_cast<size_t>(wave) * (sizeof(K2Lds) / 8));
+  x.t_list = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
+  return x;
+}
 
-  K2Stats st;
-  int status = -1;
-  int wide = 0;
-  uint32_t nbytes = 0;
-  bool node_order = false;
-  node_order = np <= 4 * 64 && w.k2_mode == 0;
-  const int dbase = w.dyn_cand ? __builtin_amdgcn_readfirstlane(w.dyn_cand[ci]) : -1;
-  if (dbase >= 0) {  // writes out_node itself
-    wide = 3;
-    k2_domain<CH>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes);
-  } else if (node_order) {  // writes out_node itself
-    uint64_t* F = reinterpret_cast<uint64_t*>(&L);
-    wide = 2;
-    if (np <= 64) k2_node_order<1, PROF>(w, F, p0, np, status, st, nbytes);
-    else if (np <= 128) k2_node_order<2, PROF>(w, F, p0, np, status, st, nbytes);
-    else k2_node_order<4, PROF>(w, F, p0, np, status, st, nbytes);
-  } else {
-    int placed = k2_run<1, CH, PROF>(w, L, p0, np, status, st, nbytes);
-    wide = placed < 0 ? 1 : 0;
-    if (placed < 0) placed = k2_run<8, CH, PROF>(w, L, p0, np, status, st, nbytes);  // > 64 distinct nodes
-    for (int i = lane; i < np; i += 64) w.out_node[p0 + i] = i < placed ? L.omap[i] : -1;
-  }
+// A K2 wave's outcome: status, bytes, the packed first-drainable minimum, the
+// profile record and (single rank) the tagged words the host polls.
+template <bool PROF>
+__device__ __forceinline__ void k2_finish(const DevWorkload& w, const K2Entry& x, int status, int wide,
+                                          uint32_t nbytes, const K2Stats& st) {
+  const int lane = threadIdx.x & 63;
+  const int ci = x.ci, p0 = x.p0, np = x.np;
   int best = 0;  // lane 0: this candidate is the first drainable one so far
   if (lane == 0) {
     w.out_status[ci] = status;
     w.out_bytes[ci] = nbytes;
     // packed (global candidate << 32 | local candidate): min = first drainable
     if (status < 0) {
-      const unsigned long long key = (static_cast<unsigned long long>(g) << 32) | static_cast<unsigned>(ci);
+      const unsigned long long key = (static_cast<unsigned long long>(x.g) << 32) | static_cast<unsigned>(ci);
       best = key < atomicMin(reinterpret_cast<unsigned long long*>(w.d_min), key);
     }
     if (PROF) {
       uint64_t* pr = w.prof + static_cast<size_t>(ci) * 16;
-      pr[0] = t_start;
-      pr[1] = t_list;  // the work-list entry has arrived
+      pr[0] = x.t_start;
+      pr[1] = x.t_list;  // the work-list entry has arrived
       pr[2] = __builtin_amdgcn_s_memrealtime();
-      pr[3] = __builtin_amdgcn_s_memtime() - c_start;
+      pr[3] = __builtin_amdgcn_s_memtime() - x.c_start;
       pr[4] = static_cast<uint64_t>(status >= 0 ? status + 1 : np);
       pr[5] = static_cast<uint64_t>(wide);
       pr[6] = st.n_spec_miss;
@@ -1495,7 +1499,7 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
       if (wide == 2) {  // node order: placement passes
         pr[12] = static_cast<uint64_t>(st.run_it) | static_cast<uint64_t>(st.seq_it) << 32;
         pr[13] = static_cast<uint64_t>(st.run_visits) | static_cast<uint64_t>(st.seq_visits) << 32;
-        pr[14] = st.cyc_rec - c_start;
+        pr[14] = st.cyc_rec - x.c_start;
         pr[15] = st.cyc_run << 1 | st.narrow;
       }
     }
@@ -1521,6 +1525,62 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   }
 }
 
+template <int CH, bool PROF>
+__global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __restrict__ list, int n_list) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wave);
+  if (li >= n_list) return;
+  const K2Entry x = k2_entry<PROF>(list, li);
+  const int ci = x.ci, p0 = x.p0, np = x.np;
+  K2Lds& L = *reinterpret_cast<K2Lds*>(k2_lds + static_cast<size_t>(wave) * (sizeof(K2Lds) / 8));
+
+  K2Stats st;
+  int status = -1;
+  int wide = 0;
+  uint32_t nbytes = 0;
+  const bool node_order = np <= 4 * 64 && w.k2_mode == 0;
+  const int dbase = w.dyn_cand ? __builtin_amdgcn_readfirstlane(w.dyn_cand[ci]) : -1;
+  if (dbase >= 0) {  // writes out_node itself
+    wide = 3;
+    k2_domain<CH>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes);
+  } else if (node_order) {  // writes out_node itself
+    uint64_t* F = reinterpret_cast<uint64_t*>(&L);
+    wide = 2;
+    if (np <= 64) k2_node_order<1, PROF>(w, F, p0, np, status, st, nbytes);
+    else if (np <= 128) k2_node_order<2, PROF>(w, F, p0, np, status, st, nbytes);
+    else k2_node_order<4, PROF>(w, F, p0, np, status, st, nbytes);
+  } else {
+    int placed = k2_run<1, CH, PROF>(w, L, p0, np, status, st, nbytes);
+    wide = placed < 0 ? 1 : 0;
+    if (placed < 0) placed = k2_run<8, CH, PROF>(w, L, p0, np, status, st, nbytes);  // > 64 distinct nodes
+    for (int i = lane; i < np; i += 64) w.out_node[p0 + i] = i < placed ? L.omap[i] : -1;
+  }
+  k2_finish<PROF>(w, x, status, wide, nbytes, st);
+}
+
+// K2 when every candidate of the launch takes node order (no domain-path
+// candidate, <= 64 * GMAX pods, default mode): only that path is compiled, so
+// the kernel holds far fewer registers than k2_place (more waves per SIMD on
+// the large configs), and a wave's LDS is just its F heads.
+template <int GMAX, bool PROF>
+__global__ __launch_bounds__(256) void k2_node(DevWorkload w, const int4* __restrict__ list, int n_list) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
+  const int wave = threadIdx.x >> 6;
+  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wave);
+  if (li >= n_list) return;
+  const K2Entry x = k2_entry<PROF>(list, li);
+  uint64_t* F = k2_lds + static_cast<size_t>(wave) * (64 * GMAX * kNHS);
+  K2Stats st;
+  int status = -1;
+  uint32_t nbytes = 0;
+  if (GMAX == 1 || x.np <= 64) k2_node_order<1, PROF>(w, F, x.p0, x.np, status, st, nbytes);
+  else if (GMAX == 2 || x.np <= 128) k2_node_order<(GMAX >= 2 ? 2 : 1), PROF>(w, F, x.p0, x.np, status, st, nbytes);
+  else k2_node_order<GMAX, PROF>(w, F, x.p0, x.np, status, st, nbytes);
+  k2_finish<PROF>(w, x, status, 2, nbytes, st);
+}
+
 // Launch with optional HIP events recorded by the dispatch itself
 // (hipExtLaunchKernelGGL: no event packets or host calls around the kernel).
 template <typename K, typename... A>
@@ -1534,6 +1594,14 @@ hipError_t launch_k2(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEve
   const int n = w.n_list;
   if (n <= 0) return hipSuccess;
   const dim3 grid((n + 3) / 4), block(256);
+  if (!w.dyn_cand && w.k2_mode == 0 && w.max_np >= 1 && w.max_np <= 4 * 64 && w.k2_node_kernel) {
+    const int G = w.max_np <= 64 ? 1 : (w.max_np <= 128 ? 2 : 4);
+    const size_t lds = 4 * static_cast<size_t>(64 * G * kNHS) * 8;
+    if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+    else if (G == 2) launch(k2_node<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+    else launch(k2_node<4, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+    return hipGetLastError();
+  }
   const size_t lds = 4 * sizeof(K2Lds);
   const int chunks = (w.Wp + 63) / 64;
   if (chunks <= 1) launch(k2_place<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);

@@ -101,7 +101,8 @@ struct sr_ctx {
   FILE* prof_file = nullptr;  // SR_K2_PROFILE: per-wave K2 records appended per run
   int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
   size_t patch_min_bytes = 512u << 10;  // SR_PATCH_MIN_BYTES: node sections below go up whole
-  int32_t k2_narrow = 1;      // SR_K2_NARROW: 32-bit scaled run passes in node order (0: 64-bit only)
+  int32_t k2_narrow = 1;
+  int32_t k2_node_kernel = 1; // SR_K2_NODE_KERNEL: node-order-only K2 kernel when every candidate takes that path      // SR_K2_NARROW: 32-bit scaled run passes in node order (0: 64-bit only)
   int32_t k2_scan_min = 2;    // SR_K2_SCAN_MIN: smallest node visit placed by prefix sums (65: never)
 };
 
@@ -308,6 +309,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.cand_global = static_cast<const int32_t*>(at(o_cg));
   d.list = static_cast<const int4*>(at(o_ls));
   d.n_list = static_cast<int32_t>(w.list.size() / 4);
+  d.max_np = w.max_cand_pods;
   d.dyn_cand = dyn ? static_cast<const int32_t*>(at(o_dc)) : nullptr;
   d.dyn_pod = dyn ? static_cast<const uint64_t*>(at(o_dp)) : nullptr;
   d.dk_dom = dyn ? static_cast<const int32_t*>(at(o_dd)) : nullptr;
@@ -325,6 +327,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.k2_mode = ctx->k2_mode;
   d.k2_scan_min = ctx->k2_scan_min;
   d.k2_narrow = ctx->k2_narrow;
+  d.k2_node_kernel = ctx->k2_node_kernel;
   d.swap_mask = w.swap_mask;
   d.prof = nullptr;
   if (ctx->prof_file) {
@@ -634,6 +637,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_PATCH_MIN_BYTES")) ctx->patch_min_bytes = std::strtoull(m, nullptr, 10);
   if (const char* m = std::getenv("SR_K2_SCAN_MIN")) ctx->k2_scan_min = std::max(1, std::atoi(m));
   if (const char* m = std::getenv("SR_K2_NARROW")) ctx->k2_narrow = std::atoi(m) != 0;
+  if (const char* m = std::getenv("SR_K2_NODE_KERNEL")) ctx->k2_node_kernel = std::atoi(m) != 0;
   if (const char* b = std::getenv("SR_PREFIX_BATCH")) ctx->prefix_batch = std::max(1, std::atoi(b));
   *out = ctx;
   return SR_OK;
