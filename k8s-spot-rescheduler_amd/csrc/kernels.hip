@@ -677,8 +677,8 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
 // row has no bit left can never be placed: it is the failing pod once every
 // lower pod is placed, and pods above it are irrelevant (canDrainNode stops).
 //
-// One wave per candidate with <= 64 * G pods (G <= 4) on <= 64-word rows;
-// lane l holds pods l, 64 + l, ... (group g = pod / 64):
+// One wave per candidate with <= 64 * G pods (G <= 4); lane l holds pods l,
+// 64 + l, ... (group g = pod / 64):
 //   prologue  pods whose S row is certainly empty (the encoder points them at
 //             the all-zero class) bound the pods that matter; the F row head
 //             (kNH words = 512 nodes) of each of those, 8 pods per load
@@ -688,10 +688,12 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
 //             record from a 64-node register window; greedy placement in pod
 //             order (group by group) with the running state in SGPRs; pods
 //             that did not fit move their pointer to the next set bit of their
-//             F row.  A pod whose head holds no further bit points at kFar;
-//             when the minimum reaches kFar every such pod is resolved with one
-//             full-row scan (lanes = words), which also leaves its mask of
-//             non-zero words for later moves beyond the head.
+//             F row.  A pod whose head holds no further bit points at kFar,
+//             the first chunk boundary: an unresolved pointer.  When the
+//             minimum reaches an unresolved pointer, its pods scan their rows
+//             from there, 64 words per round (lanes = words), which leaves a
+//             mask of the chunk's non-zero words for later moves; a mask that
+//             runs out makes the pointer the next chunk boundary, unresolved.
 // The chain is one step per visited node instead of one per pod, and a step
 // touches no global memory unless the window moves or a pointer moves beyond
 // the head.
