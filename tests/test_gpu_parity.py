@@ -385,6 +385,16 @@ def test_wide_pool_sparse_capacity(checker, seed):
     run_scenario(checker, nodes, [[] for _ in nodes], cands)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_wide_pool_random_features(checker, seed):
+    # every encoded feature (selectors, node affinity, taints, host ports,
+    # anti-affinity state bits) on pools of 4,100-9,000 nodes: sparse S rows
+    # beyond the head and across chunk boundaries
+    nodes, spot_pods, cands = rand_scenario(7300 + seed, n_spot=4100 + 1600 * seed, n_cand=10, max_pods=20,
+                                            anti=0.2, hostname_only=True)
+    run_scenario(checker, nodes, spot_pods, cands)
+
+
 # ------------------------------------------------------------ synthetic configs
 def tick_parity(checker, sc: SynthCluster, max_cands=None, oracle_threads=8):
     lib = capi.load_planner()
