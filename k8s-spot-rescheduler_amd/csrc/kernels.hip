@@ -95,6 +95,31 @@ __device__ __forceinline__ uint64_t scan_or_excl(uint64_t v) {
   return v;
 }
 
+// One word of an S row from its class's 8-slot program and the program's atom
+// words v[u] (AND, AND NOT, terms ORed with their atoms ANDed).
+__device__ __forceinline__ uint64_t eval_prog8(const int (&op)[8], const uint64_t (&v)[8]) {
+  uint64_t acc = ~0ull, any = 0, cur = 0;
+  bool has = false;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    if (op[u] < 0) break;  // wave-uniform in K0; per lane in K2
+    switch (op[u] & 3) {
+      case PROG_AND: acc &= v[u]; break;
+      case PROG_ANDNOT: acc &= ~v[u]; break;
+      case PROG_TERM_START:
+        any |= has ? cur : 0;
+        cur = v[u];
+        has = true;
+        break;
+      default: cur &= v[u]; break;
+    }
+  }
+  if (has) acc &= any | cur;
+  return acc;
+}
+
+constexpr int kSHead = 8;  // S-row words K0 writes when s_head_only (= K2's F head, kNH)
+
 // K0: bitmask rows.  Blocks [0, s_blocks): S rows, kSClasses classes per
 // wave, lanes = words; blocks after: T rows, lanes = rows.
 constexpr int kSClasses = 2;  // S rows per wave: their atom loads are in flight together
@@ -188,15 +213,16 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
       }
     }
     // rows wider than 64 words (C4: 548): two 64-word chunks per round, all
-    // their atom loads in flight together
-    for (int wb = 0; wb < w.Wp; wb += 128) {
-      const bool two = wb + 64 < w.Wp;  // wave-uniform
+    // their atom loads in flight together; with s_head_only just the head
+    const int s_words = w.s_head_only ? min(w.Wp, kSHead) : w.Wp;
+    for (int wb = 0; wb < s_words; wb += 128) {
+      const bool two = wb + 64 < s_words;  // wave-uniform
       uint64_t v[2][kSClasses][8];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         if (h == 1 && !two) break;
         const int word = wb + 64 * h + lane;
-        const size_t wi = word < w.Wp ? static_cast<size_t>(word) : 0;
+        const size_t wi = word < s_words ? static_cast<size_t>(word) : 0;
 #pragma unroll
         for (int q = 0; q < kSClasses; ++q)
 #pragma unroll
@@ -207,27 +233,11 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
       for (int h = 0; h < 2; ++h) {
         if (h == 1 && !two) break;
         const int word = wb + 64 * h + lane;
-        const bool wv = word < w.Wp;
+        const bool wv = word < s_words;
 #pragma unroll
         for (int q = 0; q < kSClasses; ++q) {
           if (op[q][0] < 0 && op[q][0] != -1) continue;  // no class, or a long program (below)
-          uint64_t acc = ~0ull, any = 0, cur = 0;
-          bool has = false;
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            if (op[q][u] < 0) break;  // wave-uniform
-            switch (op[q][u] & 3) {
-              case PROG_AND: acc &= v[h][q][u]; break;
-              case PROG_ANDNOT: acc &= ~v[h][q][u]; break;
-              case PROG_TERM_START:
-                any |= has ? cur : 0;
-                cur = v[h][q][u];
-                has = true;
-                break;
-              default: cur &= v[h][q][u]; break;
-            }
-          }
-          if (has) acc &= any | cur;
+          const uint64_t acc = eval_prog8(op[q], v[h][q]);
           if (wv) w.S[static_cast<size_t>(c0 + q) * Wp + word] = acc;
         }
       }
@@ -707,6 +717,20 @@ __device__ __forceinline__ uint64_t f_word_far(const uint64_t* __restrict__ tab,
          tab[static_cast<uint32_t>(r23) + wd] & tab[static_cast<uint32_t>(r23 >> 32) + wd];
 }
 
+// The same word with the S part evaluated from the lane's class program (in
+// LDS) when K0 wrote only the heads of the S rows (s_head_only).
+__device__ __forceinline__ uint64_t f_word_prog(const DevWorkload& w, const uint64_t* __restrict__ tab,
+                                                const int32_t* pg, uint64_t r01, uint64_t r23, int wd) {
+  int op[8];
+  uint64_t v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) op[u] = pg[u];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = op[u] >= 0 ? w.atoms[static_cast<size_t>(op[u] >> 2) * w.Wp + wd] : 0ull;
+  return eval_prog8(op, v) & tab[static_cast<uint32_t>(r01 >> 32) + wd] & tab[static_cast<uint32_t>(r23) + wd] &
+         tab[static_cast<uint32_t>(r23 >> 32) + wd];
+}
+
 // 32-bit value of lane `src` (per-lane source index), through the LDS crossbar.
 __device__ __forceinline__ uint32_t from_lane(uint32_t v, int src) {
   return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(v)));
@@ -963,6 +987,21 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     st.cyc_rec = __builtin_amdgcn_s_memtime();
   }
+  // s_head_only: each pod's class program (8 slots) in LDS after the F heads,
+  // for the S words beyond the head (k2_node sizes its LDS for it)
+  int32_t* PG = reinterpret_cast<int32_t*>(F + 64 * G * kNHS);
+  if (w.s_head_only) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint32_t cls = static_cast<uint32_t>(r01[g]) / static_cast<uint32_t>(Wp);
+      const int4* p8 = reinterpret_cast<const int4*>(w.cls_prog8 + static_cast<size_t>(cls) * 8);
+      const int4 a = p8[0], b = p8[1];
+      int4* dst = reinterpret_cast<int4*>(PG + (64 * g + lane) * 8);
+      dst[0] = a;
+      dst[1] = b;
+    }
+    nbytes += 32u * static_cast<uint32_t>(np);
+  }
   uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
   // bytes moved (algorithmic, wave-uniform): pod records, F heads of pods
   // [0, dead) (4 rows x min(Wp, kNH) words), 64-node record windows (5 words
@@ -1066,68 +1105,105 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     }
     if (unres_n != 0) {
       const int sw = n >> 6;  // first word to scan (every pending pod points at n)
+      // Q pods per round, all their loads for one chunk in flight together:
+      // 4 row words each, or (s_head_only) their programs' atom words and 3 T
+      // row words each
+      auto resolve = [&](auto qc, auto ho) {
+        constexpr int Q = decltype(qc)::value;
+        constexpr bool HO = decltype(ho)::value;
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        uint64_t pend = ballot(((act[g] >> lane) & 1) && ptr[g] == n && unres[g]);
-        while (pend != 0) {  // 4 pods per round: their 16 loads per chunk in flight together
-          int js[4];
-          uint64_t a01[4], a23[4];
+        for (int g = 0; g < G; ++g) {
+          uint64_t pend = ballot(((act[g] >> lane) & 1) && ptr[g] == n && unres[g]);
+          while (pend != 0) {
+            int js[Q];
+            uint64_t a01[Q], a23[Q];
+            int op[Q][8];
+            uint32_t nops[Q];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            js[q] = pend != 0 ? __builtin_ctzll(pend) : -1;
-            pend &= pend - 1;
-            const int j = js[q] < 0 ? 0 : js[q];
-            a01[q] = readlane64(r01[g], j);
-            a23[q] = readlane64(r23[g], j);
-          }
-          int todo = 0;  // bit q: pod js[q] not resolved yet
+            for (int q = 0; q < Q; ++q) {
+              js[q] = pend != 0 ? __builtin_ctzll(pend) : -1;
+              pend &= pend - 1;
+              const int j = js[q] < 0 ? 0 : js[q];
+              a01[q] = readlane64(r01[g], j);
+              a23[q] = readlane64(r23[g], j);
+              nops[q] = 0;
+              if constexpr (HO) {  // the pod's class program (LDS, broadcast)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) todo |= js[q] >= 0 ? 1 << q : 0;
-          for (int cb = (sw >> 6) << 6; todo != 0 && cb < Wp; cb += 64) {  // wave-uniform, <= Wp / 64 rounds
-            const int word = cb + lane;
-            const bool wv = word >= sw && word < Wp;
-            const uint32_t wi = wv ? static_cast<uint32_t>(word) : 0u;
-            uint64_t x[4][4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              if (!((todo >> q) & 1)) continue;  // wave-uniform
-              x[q][0] = tab[static_cast<uint32_t>(a01[q]) + wi];
-              x[q][1] = tab[static_cast<uint32_t>(a01[q] >> 32) + wi];
-              x[q][2] = tab[static_cast<uint32_t>(a23[q]) + wi];
-              x[q][3] = tab[static_cast<uint32_t>(a23[q] >> 32) + wi];
+                for (int u = 0; u < 8; ++u) {
+                  op[q][u] = __builtin_amdgcn_readfirstlane(PG[(64 * g + j) * 8 + u]);
+                  nops[q] += op[q][u] >= 0 ? 1u : 0u;
+                }
+              }
             }
-            const uint64_t vw = ballot(wv);
+            int todo = 0;  // bit q: pod js[q] not resolved yet
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              if (!((todo >> q) & 1)) continue;  // wave-uniform
-              const uint64_t f = wv ? (x[q][0] & x[q][1] & x[q][2] & x[q][3]) : 0ull;
-              const uint64_t m = ballot(f != 0);
-              // algorithmic bytes: the words a sequential scan reads, up to the
-              // first non-zero one (the rest of the chunk is speculative)
-              const int upto = m != 0 ? __builtin_ctzll(m) : 63;
-              const uint64_t need = upto == 63 ? vw : vw & ((2ull << upto) - 1);
-              nbytes += 32u * static_cast<uint32_t>(__builtin_popcountll(need));
-              if (m == 0 && cb + 64 < Wp) continue;  // nothing in this chunk: the next one
-              todo &= ~(1 << q);
-              int nx = INT_MAX;
-              uint64_t fw = 0;
-              if (m != 0) {
-                const int w2 = __builtin_ctzll(m);
-                fw = readlane64(f, w2);
-                nx = (cb + w2) * 64 + __builtin_ctzll(fw);
+            for (int q = 0; q < Q; ++q) todo |= js[q] >= 0 ? 1 << q : 0;
+            for (int cb = (sw >> 6) << 6; todo != 0 && cb < Wp; cb += 64) {  // wave-uniform, <= Wp / 64 rounds
+              const int word = cb + lane;
+              const bool wv = word >= sw && word < Wp;
+              const uint32_t wi = wv ? static_cast<uint32_t>(word) : 0u;
+              uint64_t x[Q][HO ? 11 : 4];
+#pragma unroll
+              for (int q = 0; q < Q; ++q) {
+                if (!((todo >> q) & 1)) continue;  // wave-uniform
+                if constexpr (HO) {
+#pragma unroll
+                  for (int u = 0; u < 8; ++u)
+                    x[q][u] = op[q][u] >= 0 ? w.atoms[static_cast<size_t>(op[q][u] >> 2) * Wp + wi] : 0ull;
+                  x[q][8] = tab[static_cast<uint32_t>(a01[q] >> 32) + wi];
+                  x[q][9] = tab[static_cast<uint32_t>(a23[q]) + wi];
+                  x[q][10] = tab[static_cast<uint32_t>(a23[q] >> 32) + wi];
+                } else {
+                  x[q][0] = tab[static_cast<uint32_t>(a01[q]) + wi];
+                  x[q][1] = tab[static_cast<uint32_t>(a01[q] >> 32) + wi];
+                  x[q][2] = tab[static_cast<uint32_t>(a23[q]) + wi];
+                  x[q][3] = tab[static_cast<uint32_t>(a23[q] >> 32) + wi];
+                }
               }
-              if (lane == js[q]) {
-                fmask[g] = m;
-                fbase[g] = cb;
-                ptr[g] = nx;
-                cur[g] = fw;
-                unres[g] = false;
+              const uint64_t vw = ballot(wv);
+#pragma unroll
+              for (int q = 0; q < Q; ++q) {
+                if (!((todo >> q) & 1)) continue;  // wave-uniform
+                uint64_t f;
+                if constexpr (HO) {
+                  uint64_t v8[8];
+#pragma unroll
+                  for (int u = 0; u < 8; ++u) v8[u] = x[q][u];
+                  f = eval_prog8(op[q], v8) & x[q][8] & x[q][9] & x[q][10];
+                } else {
+                  f = x[q][0] & x[q][1] & x[q][2] & x[q][3];
+                }
+                f = wv ? f : 0ull;
+                const uint64_t m = ballot(f != 0);
+                // algorithmic bytes: the words a sequential scan reads, up to the
+                // first non-zero one (the rest of the chunk is speculative)
+                const int upto = m != 0 ? __builtin_ctzll(m) : 63;
+                const uint64_t need = upto == 63 ? vw : vw & ((2ull << upto) - 1);
+                nbytes += (HO ? 8u * (nops[q] + 3u) : 32u) * static_cast<uint32_t>(__builtin_popcountll(need));
+                if (m == 0 && cb + 64 < Wp) continue;  // nothing in this chunk: the next one
+                todo &= ~(1 << q);
+                int nx = INT_MAX;
+                uint64_t fw = 0;
+                if (m != 0) {
+                  const int w2 = __builtin_ctzll(m);
+                  fw = readlane64(f, w2);
+                  nx = (cb + w2) * 64 + __builtin_ctzll(fw);
+                }
+                if (lane == js[q]) {
+                  fmask[g] = m;
+                  fbase[g] = cb;
+                  ptr[g] = nx;
+                  cur[g] = fw;
+                  unres[g] = false;
+                }
+                if (nx == INT_MAX) dead = min(dead, 64 * g + js[q]);
               }
-              if (nx == INT_MAX) dead = min(dead, 64 * g + js[q]);
             }
           }
         }
-      }
+      };
+      if (w.s_head_only) resolve(std::integral_constant<int, 2>{}, std::true_type{});
+      else resolve(std::integral_constant<int, 4>{}, std::false_type{});
       any = 0;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
@@ -1208,7 +1284,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
           const uint64_t rem = lw >= 63 ? 0ull : fmask[g] & (~0ull << (lw + 1));
           if (rem != 0) {
             const int w2 = fbase[g] + __builtin_ctzll(rem);
-            cur[g] = f_word_far(tab, r01[g], r23[g], w2);
+            cur[g] = w.s_head_only ? f_word_prog(w, tab, PG + (64 * g + lane) * 8, r01[g], r23[g], w2)
+                                   : f_word_far(tab, r01[g], r23[g], w2);
             nx = w2 * 64 + __builtin_ctzll(cur[g]);
             far_word = true;
           } else if (fbase[g] + 64 < Wp) {
@@ -1573,7 +1650,7 @@ __global__ __launch_bounds__(256) void k2_node(DevWorkload w, const int4* __rest
   const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wave);
   if (li >= n_list) return;
   const K2Entry x = k2_entry<PROF>(list, li);
-  uint64_t* F = k2_lds + static_cast<size_t>(wave) * (64 * GMAX * kNHS);
+  uint64_t* F = k2_lds + static_cast<size_t>(wave) * (64 * GMAX * kNHS + (w.s_head_only ? 64 * GMAX * 4 : 0));
   K2Stats st;
   int status = -1;
   uint32_t nbytes = 0;
@@ -1598,7 +1675,7 @@ hipError_t launch_k2(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEve
   const dim3 grid((n + 3) / 4), block(256);
   if (!w.dyn_cand && w.k2_mode == 0 && w.max_np >= 1 && w.max_np <= 4 * 64 && w.k2_node_kernel) {
     const int G = w.max_np <= 64 ? 1 : (w.max_np <= 128 ? 2 : 4);
-    const size_t lds = 4 * static_cast<size_t>(64 * G * kNHS) * 8;
+    const size_t lds = 4 * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
     if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
     else if (G == 2) launch(k2_node<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
     else launch(k2_node<4, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);

@@ -43,6 +43,8 @@ struct DevWorkload {
   int32_t n_list;
   int32_t max_np;       // most pods in one candidate of this call
   int32_t k2_node_kernel; // launch the node-order-only K2 when every candidate takes that path (SR_K2_NODE_KERNEL=0: never)
+  int32_t s_head_only;    // K0 writes only the head words of S rows; K2 evaluates S words beyond them from the
+                          // class programs (wide rows, node-order kernel, every program <= 8 operations)
   // domain path (k2_domain): candidates whose pods interact through shared-domain
   // topology keys (antiaff.cpp); null when the call has none
   const int32_t* dyn_cand;  // [n_cand] first record in dyn_pod, -1: node / pod order

@@ -102,7 +102,8 @@ struct sr_ctx {
   int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
   size_t patch_min_bytes = 512u << 10;  // SR_PATCH_MIN_BYTES: node sections below go up whole
   int32_t k2_narrow = 1;
-  int32_t k2_node_kernel = 1; // SR_K2_NODE_KERNEL: node-order-only K2 kernel when every candidate takes that path      // SR_K2_NARROW: 32-bit scaled run passes in node order (0: 64-bit only)
+  int32_t k2_node_kernel = 1; // SR_K2_NODE_KERNEL: node-order-only K2 kernel when every candidate takes that path
+  int32_t s_head_only = 1;    // SR_S_HEAD_ONLY: K0 writes S-row heads only on rows wider than 64 words (0: never)      // SR_K2_NARROW: 32-bit scaled run passes in node order (0: 64-bit only)
   int32_t k2_scan_min = 2;    // SR_K2_SCAN_MIN: smallest node visit placed by prefix sums (65: never)
 };
 
@@ -328,6 +329,17 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.k2_scan_min = ctx->k2_scan_min;
   d.k2_narrow = ctx->k2_narrow;
   d.k2_node_kernel = ctx->k2_node_kernel;
+  // Wide rows, every candidate on the node-order kernel (launch_k2's condition)
+  // and every class program in its 8-slot record: K0 writes only the S-row
+  // heads, K2 evaluates S words beyond them from the programs.
+  d.s_head_only = 0;
+  if (ctx->s_head_only && w.Wp > 64 && w.dyn_cand.empty() && ctx->k2_mode == 0 && ctx->k2_node_kernel &&
+      w.max_cand_pods >= 1 && w.max_cand_pods <= 256) {
+    bool short_programs = true;
+    for (int32_t k = 0; k < w.n_classes && short_programs; ++k)
+      short_programs = w.cls_prog8[static_cast<size_t>(k) * 8] != -2;
+    d.s_head_only = short_programs ? 1 : 0;
+  }
   d.swap_mask = w.swap_mask;
   d.prof = nullptr;
   if (ctx->prof_file) {
@@ -348,7 +360,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   // K0 algorithmic bytes: every table row written once; every atom row a class
   // program names, the nodes' free capacities and the thresholds read once.
   uint64_t atom_reads = w.cls_prog.size();
-  ctx->t.bytes_tables = n_rows * row + atom_reads * row + 3ull * 8 * w.n_pad + 32ull * w.n_classes;
+  const uint64_t s_row = d.s_head_only ? static_cast<uint64_t>(std::min(w.Wp, 8)) * 8 : row;  // S words K0 writes
+  ctx->t.bytes_tables = static_cast<uint64_t>(w.n_classes) * s_row + w.t_dim.size() * row + atom_reads * s_row +
+                        3ull * 8 * w.n_pad + 32ull * w.n_classes;
   // K2: counted by the kernel itself per candidate (out_bytes), read back by
   // the next run with status or node_of_pod outputs
   ctx->t.bytes_placement = 0;
@@ -638,6 +652,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_K2_SCAN_MIN")) ctx->k2_scan_min = std::max(1, std::atoi(m));
   if (const char* m = std::getenv("SR_K2_NARROW")) ctx->k2_narrow = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K2_NODE_KERNEL")) ctx->k2_node_kernel = std::atoi(m) != 0;
+  if (const char* m = std::getenv("SR_S_HEAD_ONLY")) ctx->s_head_only = std::atoi(m) != 0;
   if (const char* b = std::getenv("SR_PREFIX_BATCH")) ctx->prefix_batch = std::max(1, std::atoi(b));
   *out = ctx;
   return SR_OK;

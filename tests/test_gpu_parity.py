@@ -395,6 +395,26 @@ def test_wide_pool_random_features(checker, seed):
     run_scenario(checker, nodes, spot_pods, cands)
 
 
+@pytest.mark.parametrize("head_only", [0, 1])
+def test_wide_pool_head_only_s_rows(head_only):
+    # SR_S_HEAD_ONLY=1 (the default on rows wider than 64 words): K0 writes only
+    # the heads of the S rows and K2 evaluates the rest from the class programs
+    import os
+    from spotplanner.planner import PredicateChecker
+    os.environ["SR_S_HEAD_ONLY"] = str(head_only)
+    try:
+        c = PredicateChecker(0)
+    finally:
+        del os.environ["SR_S_HEAD_ONLY"]
+    try:
+        for seed in range(6):
+            nodes, spot_pods, cands = rand_scenario(7400 + seed, n_spot=4200 + 900 * seed, n_cand=10, max_pods=24)
+            run_scenario(c, nodes, spot_pods, cands)
+        tick_parity(c, SynthCluster(4, seed=5, n_on_demand=400, n_spot=6000))
+    finally:
+        c.close()
+
+
 # ------------------------------------------------------------ synthetic configs
 def tick_parity(checker, sc: SynthCluster, max_cands=None, oracle_threads=8):
     lib = capi.load_planner()
