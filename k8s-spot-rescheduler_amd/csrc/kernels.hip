@@ -31,12 +31,6 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-// v[L] = x (x wave-uniform, L a constant: GFX9's constant bus takes one SGPR)
-template <int L>
-__device__ __forceinline__ void writelane(uint32_t& v, uint32_t x) {
-  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(L));
-}
-
 // Minimum over the 64 lanes with DPP row shifts / broadcasts (no LDS round trips).
 template <int CTRL, int ROW_MASK = 0xf>
 __device__ __forceinline__ int dpp_min(int v) {
