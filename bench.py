@@ -3,9 +3,11 @@
 pod x node feasibility checks/s at 5k nodes / 150k pods).
 
 One step = one housekeeping tick's planning segment on device-resident inputs:
-K0 tables -> K2 feasibility rows + first-fit placement of every candidate ->
-[RCCL allreduce(min) for N>1] -> K3 winner mapping into mapped host memory.
-ms_per_step is therefore the drain-plan latency with inputs in HBM; `value` is
+K0 tables -> K2 feasibility rows + first-fit placement of every candidate (one
+GPU: each candidate's outcome and the first drainable mapping go straight to
+mapped host memory) -> for N>1: RCCL allreduce(min) -> K3 winner mapping.
+ms_per_step is the back-to-back tick with inputs in HBM (latency_ms: one tick
+on an idle device, launch to the winner on the host); `value` is
 reference-equivalent (pod, spot node) predicate checks per second over all
 ranks: the CheckPredicates calls (rescheduler.go:344) the reference's loop
 makes to reach the same plan of every candidate (findSpotNodeForPod stops at
