@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Tick stress (tools only): one planner encodes tick after tick of a synthetic
+cluster whose spot nodes gain random pods (1-3 per tick, host ports at C5), on
+fresh snapshots, alternating the reference-faithful sr_plan_first and the
+every-candidate plan, each against the oracle on the same mutated snapshot.
+Exercises the persistent encoder's caches (state patches, port-conflict rows,
+staging arena, node-record patch uploads).  GPU required.
+
+  python tools/tick_stress.py [--seconds 150]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "tests"), os.path.join(REPO, "k8s-spot-rescheduler_amd")]
+
+from oracle_lib import OracleSnapshot, oracle_plan  # noqa: E402
+from spotplanner import capi  # noqa: E402
+from spotplanner.planner import PredicateChecker  # noqa: E402
+from spotplanner.rescheduler import plan_arrays  # noqa: E402
+from spotplanner.synth import SynthCluster, build_candidates, new_node_map  # noqa: E402
+import test_gpu_ticks as T  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=150.0)
+    a = ap.parse_args()
+    lib = capi.load_planner()
+    os.environ["SR_PATCH_MIN_BYTES"] = "0"  # the second planner uploads changed records one by one
+    patcher = PredicateChecker(0)
+    del os.environ["SR_PATCH_MIN_BYTES"]
+    default = PredicateChecker(0)
+    t0, ticks = time.time(), 0
+    rng = np.random.default_rng(11)
+    clusters = [SynthCluster(5, seed=3, n_on_demand=120, n_spot=400), SynthCluster(3, seed=4, n_on_demand=150, n_spot=500)]
+    maps = []
+    for sc in clusters:
+        nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+        maps.append((nm, *build_candidates(nm, sc.pod_flags())))
+    extra = [[], []]
+    while time.time() - t0 < a.seconds:
+        ci = (ticks // 10) % 2  # ten ticks of one cluster, then ten of the other
+        sc, (nm, cand_off, cand_pods) = clusters[ci], maps[ci]
+        ck = patcher if ticks % 3 == 0 else default
+        if rng.random() < 0.3 and extra[ci]:
+            extra[ci].pop(int(rng.integers(len(extra[ci]))))  # a pod leaves again
+        for _ in range(int(rng.integers(1, 4))):
+            extra[ci].append((int(cand_pods[rng.integers(len(cand_pods))]), int(rng.integers(len(nm.spot)))))
+        extra[ci] = extra[ci][-6:]
+        h = T._snapshot(lib, sc, nm)
+        osnap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
+        for pod, pos in extra[ci]:
+            assert lib.sr_snapshot_add_pod(h, sc.ptr, pod, pos) == capi.SR_OK
+            osnap.lib.oracle_snapshot_add_pod(osnap.h, sc.ptr, pod, pos)
+        ref_all = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
+        if ticks % 2 == 0:
+            ref_early = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=0)
+            o, status, nodes, wmap = T.plan_first(ck, h, sc.ptr, cand_off, cand_pods)
+            T.check_first(o, status, nodes, wmap, ref_all, ref_early, cand_off)
+        else:
+            p = plan_arrays(ck, h, sc.ptr, cand_off, cand_pods)
+            assert np.array_equal(p.status, ref_all["status"]), ticks
+            assert np.array_equal(p.node_of_pod, ref_all["node_of_pod"]), ticks
+            assert p.winner == ref_all["winner"], ticks
+        lib.sr_snapshot_destroy(h)
+        ticks += 1
+        if ticks % 20 == 0:
+            print("  %d ticks, %.0f s" % (ticks, time.time() - t0), flush=True)
+    patcher.close()
+    default.close()
+    print("tick stress: %d ticks in %.0f s, every plan equal to the oracle" % (ticks, time.time() - t0))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
