@@ -1,15 +1,22 @@
 // kernels.hip — gfx950 (CDNA4, wave64) kernels of the drain planner.
 //
 //  K0 tables      S (static class) and T (capacity threshold) bitmask rows over
-//                 spot nodes: one lane per node, one 64-bit ballot per word
-//                 (predicate factorisation: encode.cpp).
-//  K2 placement   canDrainNode for every candidate at once (rescheduler.go:357-370):
-//                 one wave per candidate, pods in order; the pod's feasibility
-//                 row F = S & T & T & T is formed 64 words at a time from the
-//                 tables and first fit in NodeInfoArray order = lowest set bit
-//                 among untouched nodes (ballot + ctz), touched nodes rechecked
-//                 against the candidate's private capacity copy in registers.
-//  K3 winner      first drainable candidate's pod -> node mapping.
+//                 spot nodes (predicate factorisation: encode.cpp); S rows by
+//                 lanes = words from the class programs over the atom rows, T
+//                 rows by lanes = rows against the nodes' free values.
+//  K2 placement   canDrainNode for every candidate at once (rescheduler.go:357-370),
+//                 one wave per candidate, with feasibility F = S & T & T & T:
+//                  - node order (k2_node_order; the k2_node kernel when every
+//                    candidate takes it): spot nodes visited in NodeInfoArray
+//                    order, each at most once, the candidate's pods placed on
+//                    it in pod order -- the same first fit as pod by pod;
+//                  - pod order (k2_run): candidates of more than 256 pods;
+//                  - the domain path (k2_domain): pods interacting through
+//                    shared topology domains (inter-pod (anti-)affinity).
+//                 On one GPU each wave writes its outcome (and the first
+//                 drainable mapping) straight to mapped host memory.
+//  K3 winner      N GPUs: after the RCCL allreduce(min), the owning rank's
+//                 first drainable candidate's pod -> node mapping.
 //
 // No MFMA: there is no dense contraction anywhere on this path.
 #include <algorithm>
