@@ -50,6 +50,29 @@ WORKLOAD = {1: "C1 rescheduler_test-style 20 nodes / 200 pods",
 E2E_IDLE = os.environ.get("SR_BENCH_E2E_IDLE", "1") != "0"
 
 
+def k2_chain_summary(path):
+    """K2's chain costs from the committed per-wave profile of this config
+    (tools/k2_profile.py output, SR_K2_PROFILE run of the same build), or None."""
+    if not os.path.exists(path):
+        return None
+    out = {"source": os.path.relpath(path, REPO)}
+    lines = open(path).read().splitlines()
+    for i, line in enumerate(lines):
+        if line.startswith("latest-ending waves") and i + 1 < len(lines):
+            out["longest_wave"] = {"columns": line.split(":", 1)[1].strip(), "values": lines[i + 1].strip()}
+    for line in lines:
+        if line.startswith("node order: cycles/visit"):
+            nums = [float(x.strip(",")) for x in line.split() if x.strip(",").replace(".", "").isdigit()]
+            if len(nums) >= 3:
+                out.update({"cycles_per_visit_min_state": nums[0], "cycles_per_visit_placement": nums[1],
+                            "cycles_per_visit_pointer_moves": nums[2]})
+        elif line.startswith("node order: visits"):
+            out["visits_line"] = line.strip()
+        elif line.startswith("wave dur us"):
+            out["wave_us_p50_p90_p99_max"] = [float(x) for x in line.split(":")[1].split()]
+    return out
+
+
 def host_threads():
     """The encoder pool's thread count (csrc/pool.hpp: SR_HOST_THREADS, else min(16, cores))."""
     env = os.environ.get("SR_HOST_THREADS")
@@ -374,6 +397,7 @@ def main():
         if os.path.exists(pmc) and world == 1:
             with open(pmc) as f:
                 traffic = json.load(f).get(dom)
+        chain = k2_chain_summary(os.path.join(REPO, "profiles", "r02", "c%d_k2_wave_profile.txt" % args.config))
         line = {
             "metric": "reference-equivalent pod x spot-node feasibility checks/s (drain-plan latency = ms_per_step)",
             "value": total_issued / elapsed * args.steps if elapsed > 0 else 0.0,
@@ -409,7 +433,8 @@ def main():
                                              "F-row heads and full-row scans, 64-node record windows, outputs; "
                                              "SURVEY 8(d) K2 formula over what is actually read)",
                          "limiter": "latency: one dependent placement chain per candidate (one wave each); the "
-                                    "longest chain sets the kernel time, not bytes (DESIGN.md 4)"},
+                                    "longest chain sets the kernel time, not bytes (DESIGN.md 4)",
+                         "chain": chain},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(sc, nm, cand_off, cand_pods, int(len(nm.spot)), status[:len(loff) - 1],
