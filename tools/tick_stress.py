@@ -29,6 +29,7 @@ import test_gpu_ticks as T  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=150.0)
+    ap.add_argument("--wide", action="store_true", help="C4-shaped clusters (5,000-node pools: rows over 64 words)")
     a = ap.parse_args()
     lib = capi.load_planner()
     os.environ["SR_PATCH_MIN_BYTES"] = "0"  # the second planner uploads changed records one by one
@@ -37,7 +38,10 @@ def main():
     default = PredicateChecker(0)
     t0, ticks = time.time(), 0
     rng = np.random.default_rng(11)
-    clusters = [SynthCluster(5, seed=3, n_on_demand=120, n_spot=400), SynthCluster(3, seed=4, n_on_demand=150, n_spot=500)]
+    if a.wide:
+        clusters = [SynthCluster(4, seed=3, n_on_demand=150, n_spot=5000), SynthCluster(4, seed=4, n_on_demand=100, n_spot=4300)]
+    else:
+        clusters = [SynthCluster(5, seed=3, n_on_demand=120, n_spot=400), SynthCluster(3, seed=4, n_on_demand=150, n_spot=500)]
     maps = []
     for sc in clusters:
         nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
