@@ -16,15 +16,21 @@ node) is reported beside it, labelled as such.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
 
-N > 1 runs one process per GPU (torch.distributed.run); candidates are the
-on-demand nodes of a cluster with N x 1,500 on-demand nodes and the same
-3,500-node spot pool, sharded c % N == rank (weak scaling: every GPU holds one
-C3-sized candidate set).
+N > 1 runs one process per GPU: under torch.distributed.run (RANK /
+WORLD_SIZE / LOCAL_RANK / MASTER_* from the environment), or, when
+WORLD_SIZE is not set, as N child processes this one starts and waits for
+(it touches no GPU itself and exits non-zero if fewer than N devices are
+visible or any rank fails).  Candidates are the on-demand nodes of a cluster
+with N x 1,500 on-demand nodes and the same 3,500-node spot pool, sharded
+c % N == rank (weak scaling: every GPU holds one C3-sized candidate set);
+the ranks reduce each tick's outcome with one RCCL allreduce(min).
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -73,6 +79,16 @@ def k2_chain_summary(path):
     return out
 
 
+def cpu_share():
+    """Host threads the all-cores CPU baseline may use: the CPUs this process may
+    run on (sched_getaffinity), capped by the job's CPU share when the host
+    sets one (OMP_NUM_THREADS: 16 per GPU on the MI355X boxes, whose
+    sched_getaffinity lists all 256 host CPUs of 8 GPUs' jobs), or --cpu-threads."""
+    avail = len(os.sched_getaffinity(0))
+    env = os.environ.get("SR_BENCH_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(avail, int(env))) if env else avail
+
+
 def host_threads():
     """The encoder pool's thread count (csrc/pool.hpp: SR_HOST_THREADS, else min(16, cores))."""
     env = os.environ.get("SR_HOST_THREADS")
@@ -97,38 +113,46 @@ def plan_parity(o, gpu_status, gpu_nodes, cand_off):
 
 
 def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, gpu_checks, seconds):
-    """The oracle (C restatement of the reference planner) on this host, rank 0 only."""
+    """The oracle (C restatement of the reference planner) on this host, rank 0
+    only; BASELINE.md's three modes, each a median after 2 untimed warm-ups:
+    all candidates on 1 thread (bounded by `seconds`, >= 3 runs), the
+    reference-faithful early exit on 1 thread (>= 10 runs), all candidates on
+    the host's CPU share (>= 10 runs)."""
     from oracle_lib import OracleSnapshot, oracle_plan
     snap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
-    times, res = [], None
-    t_end = time.perf_counter() + seconds
-    while len(times) < 3 or (time.perf_counter() < t_end and len(times) < 500):
-        t0 = time.perf_counter()
-        res = oracle_plan(snap, sc.ptr, cand_off, cand_pods, mode=1, threads=1)
-        times.append(time.perf_counter() - t0)
-    ms_all = 1e3 * float(np.median(times))
-    t0 = time.perf_counter()
-    early = oracle_plan(snap, sc.ptr, cand_off, cand_pods, mode=0, threads=1)
-    ms_early = 1e3 * (time.perf_counter() - t0)
-    threads = min(16, os.cpu_count() or 1)
-    mt = []
-    for _ in range(5):
-        t0 = time.perf_counter()
-        oracle_plan(snap, sc.ptr, cand_off, cand_pods, mode=1, threads=threads)
-        mt.append(time.perf_counter() - t0)
-    ms_mt = 1e3 * float(np.median(mt))
+
+    def timed(mode, threads, min_runs, budget_s, max_runs=500):
+        for _ in range(2):  # warm-ups
+            oracle_plan(snap, sc.ptr, cand_off, cand_pods, mode=mode, threads=threads)
+        ts, r = [], None
+        t_end = time.perf_counter() + budget_s
+        while len(ts) < min_runs or (time.perf_counter() < t_end and len(ts) < max_runs):
+            t0 = time.perf_counter()
+            r = oracle_plan(snap, sc.ptr, cand_off, cand_pods, mode=mode, threads=threads)
+            ts.append(time.perf_counter() - t0)
+        return 1e3 * float(np.median(ts)), len(ts), sum(ts), r
+
+    ms_all, n_all, s_all, res = timed(1, 1, 3, seconds)
+    ms_early, n_early, _, early = timed(0, 1, 10, min(2.0, seconds / 4))
+    threads = cpu_share()
+    ms_mt, n_mt, _, _ = timed(1, threads, 10, min(3.0, seconds / 3))
     dense = float(len(cand_pods)) * n_spot
     parity, n_fb, n_fb_pods = plan_parity(res, gpu_status, gpu_nodes, cand_off)
     return {"value": float(res["checks"]) / (ms_all / 1e3), "unit": "checks/s", "cores": 1, "kind": "port",
-            "host_cpus": os.cpu_count(), "host_cpus_available": len(os.sched_getaffinity(0)),
+            "host_cpus": os.cpu_count(), "host_cpus_affinity": len(os.sched_getaffinity(0)),
+            "host_cpu_share_threads": threads,
             "value_definition": "reference-equivalent checks (issued CheckPredicates calls) / 1-core all-candidates tick",
             "dense_equivalent_per_s": dense / (ms_all / 1e3),
-            "sample": "full tick: all %d candidates / %d pods x %d spot nodes, median of %d runs (%.1f s)"
-                      % (len(cand_off) - 1, len(cand_pods), n_spot, len(times), sum(times)),
+            "sample": "full tick: all %d candidates / %d pods x %d spot nodes, median of %d runs (%.1f s) after 2 "
+                      "warm-ups" % (len(cand_off) - 1, len(cand_pods), n_spot, n_all, s_all),
             "ms_per_tick_all_candidates_1core": round(ms_all, 3),
-            "ms_per_tick_reference_faithful_1core": round(ms_early, 3),
+            "ms_per_tick_reference_faithful_1core": round(ms_early, 4),
+            "reference_faithful_runs": n_early,
             "reference_faithful_first_ok": int(early["first_ok"]),
-            "ms_per_tick_all_candidates_%dcores" % threads: round(ms_mt, 3),
+            "ms_per_tick_all_candidates_%dthreads" % threads: round(ms_mt, 3),
+            "all_candidates_threads_runs": n_mt,
+            "threads_note": "all-candidates mode on the job's CPU share: min(sched_getaffinity, OMP_NUM_THREADS or "
+                            "SR_BENCH_CPU_THREADS); each mode is a median after 2 warm-ups",
             "issued_checks_per_tick": int(res["checks"]),
             "plans_identical_to_gpu": parity,
             "reference_equivalent_checks_match_gpu": int(res["checks"]) == int(gpu_checks),
@@ -136,6 +160,55 @@ def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, gpu
                            "fallback candidates take the reference path",
             "fallback_candidates": n_fb, "fallback_candidate_pods": n_fb_pods,
             "fallback_ratio": round(n_fb / max(1, len(cand_off) - 1), 4)}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_devices():
+    """HIP devices this process would see, without initialising the GPU
+    (torch.cuda.device_count() does not initialise HIP on this image)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(n, argv, script=None, devices=None):
+    """One child process per GPU (ranks 0..n-1, LOCAL_RANK = rank) running this
+    script with the same arguments; rank 0 prints the JSON line.  This process
+    never touches the GPU and never execs: it waits for the children, stops the
+    others when one fails, and exits with the first failure's code.
+    (`script` / `devices`: tests only.)"""
+    have = visible_devices() if devices is None else devices
+    if have < n:
+        print("bench.py --gpus %d: only %d HIP device(s) visible; refusing to run %d ranks on fewer GPUs"
+              % (n, have, n), file=sys.stderr)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # the other ranks would wait in a collective forever
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def main():
@@ -153,9 +226,14 @@ def main():
                     help="HIP events on every n-th step of the timed region (timestamped dispatches lengthen a tick)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -180,6 +258,7 @@ def main():
                                 ctypes.byref(snap))
     assert st == capi.SR_OK
     checker = PredicateChecker(local)
+    rccl_ranks = 0
     if world > 1:
         uid = (ctypes.c_uint8 * capi.SR_UNIQUE_ID_BYTES)()
         if rank == 0:
@@ -189,6 +268,7 @@ def main():
         uid = (ctypes.c_uint8 * capi.SR_UNIQUE_ID_BYTES).from_buffer_copy(box[0])
         st = lib.sr_comm_init(checker.handle, uid, world, rank)
         assert st == capi.SR_OK, checker.last_error()
+        rccl_ranks = world
 
     cands = capi.sr_candidates(len(loff) - 1, capi.ptr(loff, capi.P32), capi.ptr(lpods, capi.P32),
                                capi.ptr(gidx, capi.P32))
@@ -392,11 +472,15 @@ def main():
     if rank == 0:
         alg = {"k2_placement": tm.bytes_placement, "k0_tables": tm.bytes_tables}[dom]
         achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-        traffic = None
+        traffic, traffic_src = None, None
         pmc = os.path.join(REPO, "profiles", "pmc_traffic_c%d.json" % args.config)
         if os.path.exists(pmc) and world == 1:
             with open(pmc) as f:
-                traffic = json.load(f).get(dom)
+                pj = json.load(f)
+            traffic = pj.get(dom)
+            traffic_src = {"file": os.path.relpath(pmc, REPO), "measured_at_head": pj.get("measured_at_head", "unknown"),
+                           "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench command "
+                                  "(tools/gpu_round.sh); not measured in this run"}
         chain = k2_chain_summary(os.path.join(REPO, "profiles", "r02", "c%d_k2_wave_profile.txt" % args.config))
         line = {
             "metric": "reference-equivalent pod x spot-node feasibility checks/s (drain-plan latency = ms_per_step)",
@@ -417,6 +501,8 @@ def main():
             "config": {"workload": WORKLOAD[args.config], "nodes": sc.n_nodes, "pods": sc.n_pods,
                        "spot_nodes": int(len(nm.spot)), "candidates": int(len(cand_off) - 1),
                        "candidate_pods": int(len(cand_pods)), "parallelism": "candidates c%%%d" % world},
+            "collective": {"backend": "rccl" if rccl_ranks else "none", "ranks": rccl_ranks,
+                           "per_tick": "one allreduce(min) of 3 x u64" if rccl_ranks else "none (one GPU)"},
             "first_ok": int(out.first_ok), "winner": int(out.winner),
             "fallback_candidates": int(np.sum(status[:len(loff) - 1] == capi.SR_CAND_FALLBACK)),
             "kernels_ms": {kk: round(v, 5) for kk, v in breakdown.items()},
@@ -428,6 +514,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "kernel_ms": round(dom_ms, 5),
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "algorithmic_bytes": int(alg),
                          "bytes_definition": "bytes the kernel moves, counted by K2 per candidate (pod records, "
                                              "F-row heads and full-row scans, 64-node record windows, outputs; "

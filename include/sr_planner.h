@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SR_ABI_VERSION 3
+#define SR_ABI_VERSION 4
 
 /* ------------------------------------------------------------------ status */
 typedef int32_t sr_status;
@@ -154,8 +154,9 @@ typedef struct {
  * empty when the API object's is (the term then selects in its own pod's
  * namespace).  Selector operators: SR_OP_IN / NOT_IN / EXISTS / DOES_NOT_EXIST;
  * anything else (or In/NotIn without values, Exists/DoesNotExist with values,
- * an empty key) fails LabelSelectorAsSelector, and a pod carrying such a term
- * is routed to the fallback path (on a spot node: every candidate). */
+ * a key that is not a qualified name, a value that is not a valid label value:
+ * sr_cluster.str_label) fails LabelSelectorAsSelector, and a pod carrying such
+ * a term is routed to the fallback path (on a spot node: every candidate). */
 typedef struct {
   const int32_t *ns;                                /* [pods.n] interned ObjectMeta.Namespace */
   const int32_t *label_off, *label_key, *label_val; /* [pods.n+1] ObjectMeta.Labels (keys unique per pod) */
@@ -188,7 +189,23 @@ typedef struct {
   int32_t        n_strings;
   const int64_t *str_int;
   const uint8_t *str_int_ok;
+  /* labels.NewRequirement's validation of the interned strings [upstream
+   * apimachinery v0.19.2 labels/selector.go: validateLabelKey =
+   * validation.IsQualifiedName, validateLabelValue = validation.IsValidLabelValue],
+   * which NodeSelectorRequirementsAsSelector (required node affinity) and
+   * metav1.LabelSelectorAsSelector (inter-pod terms) run on every key and value:
+   * str_label[id] & SR_STR_LABEL_VALUE when string `id` is a valid label value,
+   * & SR_STR_LABEL_KEY when it is a qualified name; ids >= n_strings are neither.
+   * The Go shim fills it with apimachinery's own functions.  A node-affinity term
+   * with an invalid key or value matches nothing; a pod (anti-)affinity term with
+   * one is opaque (fallback).  NULL: validity unknown -- a pod with node-affinity
+   * matchExpressions, or an inter-pod term with a label requirement, is routed to
+   * the fallback path.  (Spec.NodeSelector goes through labels.SelectorFromSet,
+   * which does not validate in v0.19.) */
+  const uint8_t *str_label;
 } sr_cluster;
+#define SR_STR_LABEL_VALUE 1u
+#define SR_STR_LABEL_KEY   2u
 
 /* ------------------------------------------------------------- NewNodeMap */
 /* A node-label flag: "key" (has_value = 0) or "key=value" (has_value = 1). */
@@ -397,8 +414,10 @@ sr_status sr_plan(sr_ctx *ctx, const sr_snapshot *snap, const sr_cluster *cluste
  * encoding costs in proportion to its pods, so a tick whose winner comes early
  * encodes little.  Outputs as sr_plan for the evaluated candidates and
  * SR_CAND_SKIPPED for the rest; `checks` / `checks_dense` cover the evaluated
- * ones.  With a communicator every rank passes its shard (cand_global) and the
- * ranks stop after the same batch. */
+ * ones.  With a communicator every rank passes its shard (cand_global, any
+ * partition) and plans the same number of batches: a batch's drainable
+ * candidate is the winner once every global index below it has been planned
+ * on some rank (the reduced smallest unplanned index lies above it). */
 sr_status sr_plan_first(sr_ctx *ctx, const sr_snapshot *snap, const sr_cluster *cluster,
                         const sr_candidates *cands, sr_plan_out *out);
 
@@ -443,11 +462,22 @@ sr_status sr_set_timing(sr_ctx *ctx, int32_t mask);
 sr_status sr_get_timing(sr_ctx *ctx, sr_timing *out);
 
 /* Multi-GPU: one process per GPU; candidates sharded by the caller (use
- * cand_global).  With a communicator attached, sr_plan_run reduces first_ok /
- * first_fallback with one RCCL allreduce(min) over xGMI. */
+ * cand_global: any partition of the global candidate indices; interleaved
+ * c % nranks keeps every rank busy on the early candidates sr_plan_first
+ * needs).  With a communicator attached, sr_plan_run reduces first_ok /
+ * first_fallback (and, for sr_plan_first, the smallest global index any rank
+ * has not planned yet) with one allreduce(min) of three 64-bit words: RCCL
+ * over xGMI, or the caller's own collective (sr_comm_init_host). */
 #define SR_UNIQUE_ID_BYTES 128
 sr_status sr_comm_unique_id(uint8_t out[SR_UNIQUE_ID_BYTES]);
 sr_status sr_comm_init(sr_ctx *ctx, const uint8_t id[SR_UNIQUE_ID_BYTES], int32_t nranks, int32_t rank);
+/* A caller-provided collective instead of RCCL (the orchestrator's own
+ * transport, ranks on several hosts, or tests): fn(user, words, n) replaces
+ * words[0..n) by their elementwise minimum over the ranks (every rank calls it
+ * with the same n, in the same order) and returns 0 (nonzero: the call fails
+ * with SR_ERR_RCCL).  It is called from the thread that called the planner. */
+typedef int32_t (*sr_allreduce_min_fn)(void *user, uint64_t *words, int32_t n);
+sr_status sr_comm_init_host(sr_ctx *ctx, int32_t nranks, int32_t rank, sr_allreduce_min_fn fn, void *user);
 
 #ifdef __cplusplus
 }

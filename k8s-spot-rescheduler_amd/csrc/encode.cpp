@@ -153,6 +153,8 @@ void for_each_spec_word(const sr_cluster* c, const sr_pods& P, int32_t pod, F&& 
         f(P.expr_op[e]);
         f(P.expr_val_off[e + 1] - P.expr_val_off[e]);
         for (int32_t v = P.expr_val_off[e]; v < P.expr_val_off[e + 1]; ++v) f(P.expr_vals[v]);
+        // the strings' validity (labels.NewRequirement), not only their ids
+        f(label_req_strings_ok(c, P.expr_key[e], P.expr_vals, P.expr_val_off[e], P.expr_val_off[e + 1]) ? 1 : 0);
         if (P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT)  // the values' integers, not only their ids
           for (int32_t v = P.expr_val_off[e]; v < P.expr_val_off[e + 1]; ++v) {
             int64_t x = 0;
@@ -232,6 +234,9 @@ void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
         const int32_t nv = P.expr_val_off[e + 1] - P.expr_val_off[e];
         const int32_t op = P.expr_op[e];
         if (P.expr_key[e] == c->id_empty) valid = false;  // validateLabelKey("") fails
+        // validateLabelKey / validateLabelValue on every value (every operator)
+        else if (!label_req_strings_ok(c, P.expr_key[e], P.expr_vals, P.expr_val_off[e], P.expr_val_off[e + 1]))
+          valid = false;
         else if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) valid = false;
         else if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) valid = false;
         else if (op == SR_OP_GT || op == SR_OP_LT) {  // exactly one value, an integer (labels.NewRequirement)
@@ -567,8 +572,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     if (!in_range(rq[0]) || !in_range(rq[1]) || !in_range(rq[2])) return true;
     if (P.aff_required[pod])
       for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t)
-        for (int32_t e = P.term_expr_off[t]; e < P.term_expr_off[t + 1]; ++e)
+        for (int32_t e = P.term_expr_off[t]; e < P.term_expr_off[t + 1]; ++e) {
           if ((P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT) && !c->str_int) return true;
+          if (!c->str_label) return true;  // NewRequirement's validation unknown
+        }
     return anti_opaque(c, pod) || aff_opaque(c, pod);  // required (anti-)affinity the encoded set cannot read
   };
   for (int32_t i = 0; i < nc; ++i)

@@ -114,6 +114,18 @@ inline bool str_int(const sr_cluster* c, int32_t id, int64_t* v) {
   *v = c->str_int[id];
   return true;
 }
+// labels.NewRequirement's key / value validation through the shim's table
+// (sr_cluster.str_label; false without a table: callers route to fallback first).
+inline bool label_str_ok(const sr_cluster* c, int32_t id, uint8_t what) {
+  return c->str_label && id >= 0 && id < c->n_strings && (c->str_label[id] & what) == what;
+}
+// Every key / value of requirement (key, vals[lo, hi)) passes NewRequirement's validation.
+inline bool label_req_strings_ok(const sr_cluster* c, int32_t key, const int32_t* vals, int32_t lo, int32_t hi) {
+  if (!label_str_ok(c, key, SR_STR_LABEL_KEY)) return false;
+  for (int32_t v = lo; v < hi; ++v)
+    if (!label_str_ok(c, vals[v], SR_STR_LABEL_VALUE)) return false;
+  return true;
+}
 inline bool has_anti_terms(const sr_cluster* c, int32_t pod) {
   return (c->pods.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) ||
          (c->pod_affinity && c->pod_affinity->anti_off[pod + 1] > c->pod_affinity->anti_off[pod]);

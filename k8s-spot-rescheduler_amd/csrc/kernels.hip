@@ -189,6 +189,7 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
     unsigned long long* dm = reinterpret_cast<unsigned long long*>(w.d_min);
     dm[0] = ~0ull;
     dm[1] = local_first_fallback < 0 ? ~0ull : static_cast<unsigned long long>(local_first_fallback) << 32;
+    dm[2] = w.rank_next;
   }
   const size_t Wp = static_cast<size_t>(w.Wp);
   if (static_cast<int>(blockIdx.x) < s_blocks) {
@@ -331,6 +332,7 @@ __device__ __forceinline__ void write_winner(const DevWorkload& w) {
   const unsigned long long* dm = reinterpret_cast<const unsigned long long*>(w.d_min);
   const unsigned long long ok = __hip_atomic_load(dm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long fb = __hip_atomic_load(dm + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long nx = __hip_atomic_load(dm + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint64_t* r = w.result;
   const bool any = ok != ~0ull;
   const int g = any ? static_cast<int>(ok >> 32) : -1;
@@ -350,6 +352,7 @@ __device__ __forceinline__ void write_winner(const DevWorkload& w) {
   if (lane == 1) put(1, local ? 1 : 0);
   if (lane == 2) put(2, np);
   if (lane == 3) put(3, fb == ~0ull ? -1 : static_cast<int>(fb >> 32));
+  if (lane == 4) put(4, nx == ~0ull ? -1 : static_cast<int>(nx));
 }
 
 // K3: one wave (after the collective on multi-GPU runs).

@@ -60,9 +60,13 @@ struct DevWorkload {
   int32_t* out_node;   // [n_pods] spot position or -1
   int32_t* out_status; // [n_cand]
   uint32_t* out_bytes; // [n_cand] bytes K2 moved for the candidate (the roofline's algorithmic bytes)
-  int32_t* d_min;      // 2 x u64 packed {global << 32 | local}: first ok, first fallback (~0 = none)
+  int32_t* d_min;      // 3 x u64, reduced (min) over the ranks: packed {global << 32 | local} first ok,
+                       // first fallback (~0 = none), and the smallest global candidate index a rank has
+                       // not planned yet (rank_next; ~0 = none)
+  uint64_t rank_next;  // this rank's d_min[2] (sr_plan_first's prefix batches; ~0 otherwise)
   uint64_t* result;    // mapped host memory [kResultHeader + max pods] words seq << 32 | value:
-                       //   {winner, local, npods, first_fallback, -, -, -, -, mapping...}
+                       //   {winner, local, npods, first_fallback, reduced rank_next (-1: none), -, -, -,
+                       //    mapping...}
   uint64_t* res_stat;  // single-rank runs: mapped host memory [n_cand] words seq << 32 | drainable, one
                        // stored by K2 per finished candidate, and
   uint64_t* res_map;   // [n_pods] words seq << 32 | spot position: a candidate's mapping, stored by K2

@@ -151,18 +151,25 @@ static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod, const
     if (P.port_num[i] > 0) st.ports.push_back(Port{P.port_ip[i], P.port_proto[i], P.port_num[i]});
 }
 
-// A term whose label selector metav1.LabelSelectorAsSelector rejects: an
-// empty key, In / NotIn without values, Exists / DoesNotExist with values,
-// any other operator [upstream apimachinery].
+// A term whose label selector metav1.LabelSelectorAsSelector rejects: a key
+// that is not a qualified name (the empty key included), a value that is not
+// a valid label value (labels.NewRequirement on every matchLabels pair and
+// matchExpression), In / NotIn without values, Exists / DoesNotExist with
+// values, any other operator [upstream apimachinery v0.19.2].  Without the
+// shim's validity table (sr_cluster.str_label) any label requirement counts
+// as rejected: the planner cannot tell.
 static bool term_invalid(const sr_cluster* c, int32_t t) {
   const sr_pod_affinity* A = c->pod_affinity;
   const int32_t e_id = c->id_empty;
   if (A->selector_nil[t]) return false;
-  for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; ++i)
+  for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; ++i) {
     if (A->ml_key[i] == e_id && e_id != -1) return true;
+    if (!label_req_strings_ok(c, A->ml_key[i], A->ml_val, i, i + 1)) return true;
+  }
   for (int32_t e = A->me_off[t]; e < A->me_off[t + 1]; ++e) {
     const int32_t nv = A->me_val_off[e + 1] - A->me_val_off[e], op = A->me_op[e];
     if (A->me_key[e] == e_id && e_id != -1) return true;
+    if (!label_req_strings_ok(c, A->me_key[e], A->me_vals, A->me_val_off[e], A->me_val_off[e + 1])) return true;
     if (op == SR_OP_IN || op == SR_OP_NOT_IN) {
       if (nv == 0) return true;
     } else if (op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) {

@@ -73,6 +73,7 @@ struct sr_ctx {
   DevBuf arena, tables, out_node, out_status, out_bytes, dmin, prof, scratch;
   HostBuf h_arena, h_result, h_status, h_node, h_bytes;
   HostBuf h_early;           // mapped: K2's per-candidate result words (single-rank runs)
+  HostBuf h_comm;            // pinned: the reduced words of a caller-provided collective
   bool in_flight = false;    // a run returned with K2 still planning candidates past the winner
   uint64_t* d_early = nullptr;  // device address of h_early
   uint64_t issued_checks = 0;  // checks of the prepared workload's plan (known after a full run)
@@ -97,13 +98,16 @@ struct sr_ctx {
   uint32_t seq = 0;  // run sequence number (wraps: tags compare as uint32)
   sr_timing t{};
   ncclComm_t comm = nullptr;
+  sr_allreduce_min_fn host_fn = nullptr;  // sr_comm_init_host: the caller's allreduce(min)
+  void* host_user = nullptr;
   int nranks = 1, rank = 0;
+  int64_t last_rank_next = -1;  // reduced smallest unplanned global index of the last collective run (-1: none)
   FILE* prof_file = nullptr;  // SR_K2_PROFILE: per-wave K2 records appended per run
   int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
   size_t patch_min_bytes = 512u << 10;  // SR_PATCH_MIN_BYTES: node sections below go up whole
-  int32_t k2_narrow = 1;
+  int32_t k2_narrow = 1;      // SR_K2_NARROW: 32-bit scaled run passes in node order (0: 64-bit only)
   int32_t k2_node_kernel = 1; // SR_K2_NODE_KERNEL: node-order-only K2 kernel when every candidate takes that path
-  int32_t s_head_only = 1;    // SR_S_HEAD_ONLY: K0 writes S-row heads only on rows wider than 64 words (0: never)      // SR_K2_NARROW: 32-bit scaled run passes in node order (0: 64-bit only)
+  int32_t s_head_only = 1;    // SR_S_HEAD_ONLY: K0 writes S-row heads only on rows wider than 64 words (0: never)
   int32_t k2_scan_min = 2;    // SR_K2_SCAN_MIN: smallest node visit placed by prefix sums (65: never)
 };
 
@@ -131,6 +135,9 @@ hipError_t dev_reserve(DevBuf& b, size_t bytes) {
   return e;
 }
 
+// Fresh pinned blocks are zeroed: the runtime may hand back memory an earlier
+// context freed, and the tagged result words (mapped memory) must never carry
+// a stale tag (run sequence numbers also come from one process-wide counter).
 hipError_t host_reserve(HostBuf& b, size_t bytes) {
   if (bytes <= b.cap) return hipSuccess;
   if (b.p) (void)hipHostFree(b.p);
@@ -138,9 +145,16 @@ hipError_t host_reserve(HostBuf& b, size_t bytes) {
   b.cap = 0;
   size_t cap = std::max<size_t>(bytes + bytes / 4, 4096);
   hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocMapped | hipHostMallocCoherent);
-  if (e == hipSuccess) b.cap = cap;
+  if (e == hipSuccess) {
+    b.cap = cap;
+    std::memset(b.p, 0, cap);
+  }
   return e;
 }
+
+// Run tags of every context of the process: a tag is never reused while the
+// process lives (2^32 runs), so words a freed context left behind cannot match.
+std::atomic<uint32_t> g_run_seq{0};
 
 // Packs host vectors into one contiguous staging buffer (256-B aligned
 // sections) so the whole workload goes up in a single copy.
@@ -176,6 +190,32 @@ sr_status settle(sr_ctx* ctx) {
   if (!ctx->in_flight) return SR_OK;
   ctx->in_flight = false;
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return SR_OK;
+}
+
+bool has_comm(const sr_ctx* ctx) { return ctx->comm != nullptr || ctx->host_fn != nullptr; }
+
+// allreduce(min) of n <= 8 uint64 words in device memory, stream-ordered:
+// RCCL in place, or the caller's collective on a pinned host copy.
+sr_status allreduce_min_dev(sr_ctx* ctx, void* words, int32_t n) {
+  if (ctx->comm) {
+    ncclResult_t r = rccl().all_reduce(words, words, static_cast<size_t>(n), ncclUint64, ncclMin, ctx->comm,
+                                       ctx->stream);
+    if (r != ncclSuccess) {
+      ctx->err = std::string("ncclAllReduce: ") + rccl().error_string(r);
+      return SR_ERR_RCCL;
+    }
+    return SR_OK;
+  }
+  HIP_TRY(ctx, host_reserve(ctx->h_comm, 64));
+  uint64_t* h = static_cast<uint64_t*>(ctx->h_comm.p);
+  HIP_TRY(ctx, hipMemcpyAsync(h, words, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->host_fn(ctx->host_user, h, n) != 0) {
+    ctx->err = "caller-provided allreduce(min) failed";
+    return SR_ERR_RCCL;
+  }
+  HIP_TRY(ctx, hipMemcpyAsync(words, h, sizeof(uint64_t) * n, hipMemcpyHostToDevice, ctx->stream));
   return SR_OK;
 }
 
@@ -341,6 +381,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
     d.s_head_only = short_programs ? 1 : 0;
   }
   d.swap_mask = w.swap_mask;
+  d.rank_next = ~0ull;  // sr_plan_first sets its batch's value
   d.prof = nullptr;
   if (ctx->prof_file) {
     const size_t pbytes = sizeof(uint64_t) * (16 * static_cast<size_t>(std::max(1, ncand)) + 2 * sr::kK0ProfWaves);
@@ -463,13 +504,14 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   sr::DevWorkload& d = ctx->dw;
   hipStream_t s = ctx->stream;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const bool collective = ctx->comm && use_comm;
+  const bool collective = has_comm(ctx) && use_comm;
   // Single rank, winner only: K2 writes each candidate's outcome to the host
   // and the run returns once the candidates up to the winner are known (no K3)
   const bool early = !collective && !full && !ctx->prof_file;
   const int32_t timing = (ctx->timing_runs++ % ctx->timing_every) == 0 ? ctx->timing : 0;
   ctx->timing_cur = timing;
-  if (++ctx->seq == 0) ctx->seq = 1;  // tag 0 is never used: fresh result memory may hold zeros
+  do ctx->seq = g_run_seq.fetch_add(1, std::memory_order_relaxed) + 1;
+  while (ctx->seq == 0);  // tag 0 is never used: fresh result memory holds zeros
   d.seq = ctx->seq;
   volatile uint64_t* res = static_cast<volatile uint64_t*>(ctx->h_result.p);
   // Timed kernels get an event pair from the pool, recorded by their own
@@ -517,11 +559,8 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   PAIR(2, e2a, e2b);
   if (collective) {
     if (e2a) HIP_TRY(ctx, hipEventRecord(e2a, s));
-    ncclResult_t r = rccl().all_reduce(d.d_min, d.d_min, 2, ncclUint64, ncclMin, ctx->comm, s);
-    if (r != ncclSuccess) {
-      ctx->err = std::string("ncclAllReduce: ") + rccl().error_string(r);
-      return SR_ERR_RCCL;
-    }
+    sr_status cst = allreduce_min_dev(ctx, d.d_min, 3);  // first ok, first fallback, rank_next
+    if (cst != SR_OK) return cst;
     HIP_TRY(ctx, sr::launch_winner(d, s));
     if (e2b) HIP_TRY(ctx, hipEventRecord(e2b, s));
   } else {
@@ -550,7 +589,7 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     // also surfaces a kernel fault as an error).
     const uint32_t tag = static_cast<uint32_t>(d.seq);
     auto ready = [&](size_t i) { return static_cast<uint32_t>(res[i] >> 32) == tag; };
-    auto header_ready = [&] { return ready(0) && ready(1) && ready(2) && ready(3); };
+    auto header_ready = [&] { return ready(0) && ready(1) && ready(2) && ready(3) && ready(4); };
     auto map_ready = [&] {
       if (!static_cast<uint32_t>(res[1])) return true;
       const size_t np = static_cast<uint32_t>(res[2]);
@@ -579,13 +618,14 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   }
   auto val = [&](size_t i) { return static_cast<int32_t>(static_cast<uint32_t>(res[i])); };
   const uint32_t tag = static_cast<uint32_t>(d.seq);
-  for (size_t i = 0; i < 4; ++i)
+  for (size_t i = 0; i < 5; ++i)
     if (static_cast<uint32_t>(res[i] >> 32) != tag) {
       ctx->err = "result header not written by this run";
       return SR_ERR_HIP;
     }
   out->first_ok = val(0);
   out->first_fallback = val(3);
+  ctx->last_rank_next = val(4);
   out->winner = (val(0) >= 0 && (val(3) < 0 || val(3) > val(0))) ? val(0) : -1;
   out->winner_npods = val(1) ? val(2) : 0;
   if (out->winner_map && val(1))
@@ -667,7 +707,8 @@ void sr_destroy(sr_ctx* ctx) {
                     &ctx->prof, &ctx->scratch})
     if (b->p) (void)hipFree(b->p);
   if (ctx->ev_upload) (void)hipEventDestroy(ctx->ev_upload);
-  for (HostBuf* b : {&ctx->h_arena, &ctx->h_result, &ctx->h_status, &ctx->h_node, &ctx->h_bytes})
+  for (HostBuf* b : {&ctx->h_arena, &ctx->h_result, &ctx->h_status, &ctx->h_node, &ctx->h_bytes, &ctx->h_early,
+                     &ctx->h_comm})
     if (b->p) (void)hipHostFree(b->p);
   for (auto* v : {&ctx->ev_start, &ctx->ev_end})
     for (hipEvent_t e : *v) (void)hipEventDestroy(e);
@@ -702,28 +743,15 @@ sr_status sr_plan(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* cluste
   return run(ctx, out, out->status != nullptr || out->node_of_pod != nullptr, true);
 }
 
-// Largest value over the ranks (one RCCL allreduce; the value itself without a communicator).
-static sr_status comm_max(sr_ctx* ctx, int32_t v, int32_t* out) {
-  *out = v;
-  if (!ctx->comm) return SR_OK;
-  HIP_TRY(ctx, hipSetDevice(ctx->device));
-  HIP_TRY(ctx, dev_reserve(ctx->scratch, 64));
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->scratch.p, &v, sizeof(v), hipMemcpyHostToDevice, ctx->stream));
-  ncclResult_t r = rccl().all_reduce(ctx->scratch.p, ctx->scratch.p, 1, ncclInt32, ncclMax, ctx->comm, ctx->stream);
-  if (r != ncclSuccess) {
-    ctx->err = std::string("ncclAllReduce: ") + rccl().error_string(r);
-    return SR_ERR_RCCL;
-  }
-  HIP_TRY(ctx, hipMemcpyAsync(out, ctx->scratch.p, sizeof(*out), hipMemcpyDeviceToHost, ctx->stream));
-  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-  return SR_OK;
-}
-
 // run()'s loop with its break (rescheduler.go:228-287): prefix batches of
-// candidates, each encoded and planned on its own, until one holds a
-// drainable candidate.  Batch k covers local candidates [lo_k, hi_k) on every
-// rank, so every global index below the ranks' hi_k has been planned once it
-// ends: the first drainable one found is the first overall.
+// candidates, each encoded and planned on its own, until the first drainable
+// candidate is known.  Batch k covers local candidates [lo_k, hi_k) on every
+// rank.  The run's collective also reduces the smallest global index some rank
+// has not planned yet (rank_next): a drainable candidate below it is the first
+// overall, whatever the partition of the global indices over the ranks (with
+// contiguous shards, rank 1's early batches hold late indices, and batching
+// goes on until rank 0 has planned everything below them).  Every rank sees the
+// same reduced values, so all stop after the same batch.
 static sr_status plan_first(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
                             sr_plan_out* out) {
   const int32_t n = cands->n_cand;
@@ -739,28 +767,38 @@ static sr_status plan_first(sr_ctx* ctx, const sr_snapshot* snap, const sr_clust
     for (int32_t i = 0; i < n; ++i) glob[i] = i;
   }
   const int32_t* G = cands->cand_global ? cands->cand_global : glob.data();
-  int32_t n_all = n;
-  sr_status st = comm_max(ctx, n, &n_all);
-  if (st != SR_OK) return st;
+  // suffix minima of the global indices: the smallest one not planned after a batch ending at l
+  std::vector<int32_t> next(static_cast<size_t>(std::max(0, n)) + 1, INT32_MAX);
+  int32_t maxp = 1;
+  for (int32_t i = n - 1; i >= 0; --i) {
+    if (G[i] < 0) {
+      ctx->err = "cand_global holds a negative index";
+      return SR_ERR_INVALID_ARG;
+    }
+    next[i] = std::min(next[i + 1], G[i]);
+    maxp = std::max(maxp, off[i + 1] - off[i]);
+  }
   out->winner = out->first_ok = out->first_fallback = -1;
   out->winner_npods = 0;
   out->checks = out->fallback_pods = out->checks_dense = 0;
-  std::vector<int32_t> bst, bnode;
+  std::vector<int32_t> bst, bnode, bmap(out->winner_map ? static_cast<size_t>(maxp) : 0);
+  const bool coll = has_comm(ctx);
   int32_t batches = 0;
-  for (int32_t lo = 0, B = ctx->prefix_batch; lo < n_all || batches == 0; B = std::min(B * 2, 1 << 20)) {
-    const int32_t hi = std::min(n_all, lo + B);
+  for (int32_t lo = 0, B = ctx->prefix_batch;; B = std::min(B * 2, 1 << 20)) {
+    const int32_t hi = static_cast<int32_t>(std::min<int64_t>(INT32_MAX, static_cast<int64_t>(lo) + B));
     const int32_t l0 = std::min(lo, n), l1 = std::min(hi, n);
     sr_candidates sub{l1 - l0, off + l0, cands->cand_pods, G + l0};
     sr_plan_out o{};
-    o.winner_map = out->winner_map;
+    o.winner_map = out->winner_map ? bmap.data() : nullptr;
     if (full) {
       bst.assign(static_cast<size_t>(std::max(1, l1 - l0)), 0);
       bnode.assign(static_cast<size_t>(std::max(1, n > 0 ? off[l1] - off[l0] : 0)), -1);
       o.status = bst.data();
       o.node_of_pod = bnode.data();
     }
-    st = prepare(ctx, snap, c, &sub);
+    sr_status st = prepare(ctx, snap, c, &sub);
     if (st != SR_OK) return st;
+    ctx->dw.rank_next = next[l1] == INT32_MAX ? ~0ull : static_cast<uint64_t>(next[l1]);
     st = run(ctx, &o, full, true);
     if (st != SR_OK) return st;
     ++batches;
@@ -773,11 +811,16 @@ static sr_status plan_first(sr_ctx* ctx, const sr_snapshot* snap, const sr_clust
     out->fallback_pods += o.fallback_pods;
     if (o.first_fallback >= 0 && (out->first_fallback < 0 || o.first_fallback < out->first_fallback))
       out->first_fallback = o.first_fallback;
-    if (o.first_ok >= 0) {
+    if (o.first_ok >= 0 && (out->first_ok < 0 || o.first_ok < out->first_ok)) {
       out->first_ok = o.first_ok;
-      out->winner_npods = o.winner_npods;
-      break;
+      out->winner_npods = o.winner_npods;  // 0 on the ranks that do not own it
+      if (out->winner_map)
+        std::copy(bmap.begin(), bmap.begin() + o.winner_npods, out->winner_map);
     }
+    // the smallest global index no rank has planned yet (reduced by the run's collective)
+    const int64_t bound = coll ? (ctx->last_rank_next < 0 ? INT64_MAX : ctx->last_rank_next)
+                               : (next[l1] == INT32_MAX ? INT64_MAX : next[l1]);
+    if (bound == INT64_MAX || (out->first_ok >= 0 && out->first_ok < bound)) break;
     lo = hi;
   }
   out->winner = (out->first_ok >= 0 && (out->first_fallback < 0 || out->first_fallback > out->first_ok))
@@ -871,8 +914,17 @@ sr_status sr_comm_unique_id(uint8_t out[SR_UNIQUE_ID_BYTES]) {
   return SR_OK;
 }
 
+sr_status sr_comm_init_host(sr_ctx* ctx, int32_t nranks, int32_t rank, sr_allreduce_min_fn fn, void* user) {
+  if (!ctx || !fn || nranks < 1 || rank < 0 || rank >= nranks || has_comm(ctx)) return SR_ERR_INVALID_ARG;
+  ctx->host_fn = fn;
+  ctx->host_user = user;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return SR_OK;
+}
+
 sr_status sr_comm_init(sr_ctx* ctx, const uint8_t id[SR_UNIQUE_ID_BYTES], int32_t nranks, int32_t rank) {
-  if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return SR_ERR_INVALID_ARG;
+  if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks || has_comm(ctx)) return SR_ERR_INVALID_ARG;
   if (hipSetDevice(ctx->device) != hipSuccess) return SR_ERR_HIP;
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));

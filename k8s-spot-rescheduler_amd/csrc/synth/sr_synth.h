@@ -35,6 +35,8 @@ void sr_synth_labels(const sr_synth *s, sr_node_label *on_demand, sr_node_label 
 void sr_synth_drain(const sr_synth *s, sr_pod_drain *out);
 const char *sr_synth_string(const sr_synth *s, int32_t id);
 int32_t sr_synth_num_strings(const sr_synth *s);
+/* The generator's sr_cluster.str_label entry for one string (SR_STR_LABEL_*). */
+uint8_t sr_synth_label_flags(const char *s);
 
 #ifdef __cplusplus
 }

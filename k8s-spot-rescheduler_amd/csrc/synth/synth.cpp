@@ -44,6 +44,7 @@ struct sr_synth {
   std::vector<uint8_t> phase, restart;
   std::vector<int64_t> deletion_age, grace;
   sr_node_label od{}, spot{};
+  std::vector<uint8_t> str_label;  // sr_cluster.str_label over `strings`
 
   int32_t id(const std::string& s) {
     auto it = ids.find(s);
@@ -69,6 +70,44 @@ struct Rng {
   int below(int n) { return static_cast<int>(next() % static_cast<uint64_t>(n)); }
   bool chance(double p) { return uni() < p; }
 };
+
+// apimachinery v0.19.2 util/validation [upstream], as the Go shim calls it:
+// ([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9] (qualifiedNameFmt)
+bool qname_part(const std::string& s) {
+  auto alnum = [](char ch) { return (ch >= 'a' && ch <= 'z') || (ch >= 'A' && ch <= 'Z') || (ch >= '0' && ch <= '9'); };
+  if (s.empty() || !alnum(s.front()) || !alnum(s.back())) return false;
+  for (char ch : s)
+    if (!alnum(ch) && ch != '-' && ch != '_' && ch != '.') return false;
+  return true;
+}
+bool dns1123_subdomain(const std::string& s) {
+  if (s.empty() || s.size() > 253) return false;
+  size_t a = 0;
+  while (a <= s.size()) {  // labels [a-z0-9]([-a-z0-9]*[a-z0-9])? separated by '.'
+    size_t b = s.find('.', a);
+    if (b == std::string::npos) b = s.size();
+    if (b == a) return false;
+    auto lc = [](char ch) { return (ch >= 'a' && ch <= 'z') || (ch >= '0' && ch <= '9'); };
+    if (!lc(s[a]) || !lc(s[b - 1])) return false;
+    for (size_t i = a; i < b; ++i)
+      if (!lc(s[i]) && s[i] != '-') return false;
+    a = b + 1;
+  }
+  return true;
+}
+uint8_t label_flags(const std::string& s) {
+  uint8_t f = 0;
+  if (s.empty() || (s.size() <= 63 && qname_part(s))) f |= SR_STR_LABEL_VALUE;  // IsValidLabelValue
+  const size_t slash = s.find('/');
+  std::string name = s;
+  bool ok = true;
+  if (slash != std::string::npos) {  // IsQualifiedName: [prefix "/"] name
+    ok = s.find('/', slash + 1) == std::string::npos && dns1123_subdomain(s.substr(0, slash));
+    name = s.substr(slash + 1);
+  }
+  if (ok && name.size() <= 63 && qname_part(name)) f |= SR_STR_LABEL_KEY;
+  return f;
+}
 
 constexpr int64_t kMi = 1024ll * 1024;
 constexpr int64_t kGi = 1024ll * kMi;
@@ -321,6 +360,7 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
       push_pod(s, node, p);
     }
   }
+  for (const std::string& str : s->strings) s->str_label.push_back(label_flags(str));
   return s;
 }
 
@@ -380,9 +420,10 @@ void sr_synth_view(const sr_synth* s, sr_cluster* c) {
   c->id_metadata_name = 1;
   c->id_unschedulable_key = 2;
   c->pod_affinity = nullptr;  // the BASELINE configs carry no pod (anti-)affinity
-  c->n_strings = 0;           // ... nor node-affinity Gt / Lt
-  c->str_int = nullptr;
+  c->n_strings = static_cast<int32_t>(s->str_label.size());
+  c->str_int = nullptr;       // ... nor node-affinity Gt / Lt
   c->str_int_ok = nullptr;
+  c->str_label = s->str_label.data();
 }
 
 void sr_synth_drain(const sr_synth* s, sr_pod_drain* d) {
@@ -405,5 +446,7 @@ const char* sr_synth_string(const sr_synth* s, int32_t id) {
 }
 
 int32_t sr_synth_num_strings(const sr_synth* s) { return static_cast<int32_t>(s->strings.size()); }
+
+uint8_t sr_synth_label_flags(const char* s) { return label_flags(s ? std::string(s) : std::string()); }
 
 }  // extern "C"

@@ -72,7 +72,8 @@ class sr_cluster(ctypes.Structure):
     _fields_ = [("nodes", sr_nodes), ("pods", sr_pods), ("id_empty", ctypes.c_int32),
                 ("id_metadata_name", ctypes.c_int32), ("id_unschedulable_key", ctypes.c_int32),
                 ("pod_affinity", ctypes.POINTER(sr_pod_affinity)), ("n_strings", ctypes.c_int32),
-                ("str_int", ctypes.POINTER(ctypes.c_int64)), ("str_int_ok", ctypes.POINTER(ctypes.c_uint8))]
+                ("str_int", ctypes.POINTER(ctypes.c_int64)), ("str_int_ok", ctypes.POINTER(ctypes.c_uint8)),
+                ("str_label", ctypes.POINTER(ctypes.c_uint8))]
 
 
 class sr_node_label(ctypes.Structure):
@@ -106,6 +107,10 @@ class sr_plan_out(ctypes.Structure):
     _fields_ = [("winner", ctypes.c_int32), ("first_ok", ctypes.c_int32), ("first_fallback", ctypes.c_int32),
                 ("winner_npods", ctypes.c_int32), ("checks", ctypes.c_uint64), ("fallback_pods", ctypes.c_uint64),
                 ("status", P32), ("node_of_pod", P32), ("winner_map", P32), ("checks_dense", ctypes.c_uint64)]
+
+
+# sr_allreduce_min_fn: int32 fn(void *user, uint64_t *words, int32_t n)
+ALLREDUCE_MIN_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32)
 
 
 class sr_timing(ctypes.Structure):
@@ -167,6 +172,9 @@ def make_cluster_struct(A) -> sr_cluster:
         c.n_strings = len(A["str_int"])
         c.str_int = ptr(A["str_int"], P64)
         c.str_int_ok = ptr(A["str_int_ok"], PU8)
+    if A.get("str_label") is not None:
+        c.n_strings = len(A["str_label"])
+        c.str_label = ptr(A["str_label"], PU8)
     if A.get("pa_ns") is not None:
         pa = sr_pod_affinity()
         for f in ("ns", "label_off", "label_key", "label_val", "anti_off", "topology_key", "ns_off", "ns_ids",
@@ -257,6 +265,8 @@ def _declare_planner(lib):
     lib.sr_comm_unique_id.restype = S
     lib.sr_comm_init.argtypes = [VP, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32, ctypes.c_int32]
     lib.sr_comm_init.restype = S
+    lib.sr_comm_init_host.argtypes = [VP, ctypes.c_int32, ctypes.c_int32, ALLREDUCE_MIN_FN, VP]
+    lib.sr_comm_init_host.restype = S
 
 
 # Every symbol include/sr_planner.h declares (checked by tests on CPU).
@@ -264,4 +274,4 @@ EXPORTED = ["sr_new_node_map", "sr_node_has_label", "sr_pods_for_deletion", "sr_
             "sr_snapshot_add_pod", "sr_snapshot_fork", "sr_snapshot_revert", "sr_snapshot_node_state",
             "sr_snapshot_num_nodes", "sr_create", "sr_destroy", "sr_last_error", "sr_build_info",
             "sr_find_spot_nodes", "sr_can_drain_node", "sr_plan", "sr_plan_first", "sr_plan_prepare", "sr_plan_run",
-            "sr_set_timing", "sr_get_timing", "sr_comm_unique_id", "sr_comm_init"]
+            "sr_set_timing", "sr_get_timing", "sr_comm_unique_id", "sr_comm_init", "sr_comm_init_host"]

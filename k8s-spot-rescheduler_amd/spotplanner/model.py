@@ -263,6 +263,41 @@ def string_ints(interner: Interner):
             np.ascontiguousarray([v is not None for v in vals], dtype=np.uint8).reshape(-1))
 
 
+# apimachinery v0.19.2 util/validation [upstream]: qualifiedNameFmt is
+# ([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]; a label value is empty or such a
+# name of at most 63 characters; a qualified name is [DNS-1123 subdomain "/"]
+# name, the name part non-empty and at most 63 characters, the prefix at most
+# 253 characters of [a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*.
+# Go's regexp `$` matches at the end of the text only: fullmatch.
+_QNAME = re.compile(r"([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]")
+_DNS1123_SUBDOMAIN = re.compile(r"[a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*")
+
+
+def is_valid_label_value(s: str) -> bool:
+    """validation.IsValidLabelValue: labels.NewRequirement's validateLabelValue."""
+    return len(s.encode()) <= 63 and (s == "" or _QNAME.fullmatch(s) is not None)
+
+
+def is_qualified_name(s: str) -> bool:
+    """validation.IsQualifiedName: labels.NewRequirement's validateLabelKey."""
+    parts = s.split("/")
+    if len(parts) > 2:
+        return False
+    if len(parts) == 2:
+        prefix = parts[0]
+        if not prefix or len(prefix.encode()) > 253 or _DNS1123_SUBDOMAIN.fullmatch(prefix) is None:
+            return False
+    name = parts[-1]
+    return 0 < len(name.encode()) <= 63 and _QNAME.fullmatch(name) is not None
+
+
+def string_label_flags(interner: Interner):
+    """sr_cluster.str_label over the interner's strings (labels.NewRequirement validation)."""
+    return np.ascontiguousarray([(capi.SR_STR_LABEL_VALUE if is_valid_label_value(s) else 0) |
+                                 (capi.SR_STR_LABEL_KEY if is_qualified_name(s) else 0)
+                                 for s in interner.strings], dtype=np.uint8).reshape(-1)
+
+
 class EncodedCluster:
     """numpy arrays in the sr_cluster layout + the ctypes struct pointing at them."""
 
@@ -270,6 +305,7 @@ class EncodedCluster:
         self.a = arrays
         self.interner = interner
         self.a["str_int"], self.a["str_int_ok"] = string_ints(interner)
+        self.a["str_label"] = string_label_flags(interner)
         self.struct = capi.make_cluster_struct(self.a)
 
     @property

@@ -68,6 +68,22 @@ class PredicateChecker:
         self.lib.sr_get_timing(self.handle, ctypes.byref(t))
         return t
 
+    def attach_collective(self, nranks: int, rank: int, allreduce_min):
+        """sr_comm_init_host: the planner's allreduce(min) over the ranks is
+        `allreduce_min(values: list[int]) -> list[int]` (e.g. torch.distributed
+        over gloo), instead of RCCL."""
+        def fn(_user, words, n):
+            try:
+                out = allreduce_min([int(words[i]) for i in range(n)])
+                for i in range(n):
+                    words[i] = int(out[i])
+                return 0
+            except Exception:  # noqa: BLE001 -- reported to the planner as a failed collective
+                return 1
+        self._collective = capi.ALLREDUCE_MIN_FN(fn)  # kept alive as long as the handle
+        _check(self.lib, self.lib.sr_comm_init_host(self.handle, nranks, rank, self._collective, None), self.handle,
+               "sr_comm_init_host")
+
 
 def NewTestPredicateChecker(device: int = 0):
     """simulator.NewTestPredicateChecker() -> (checker, err) (rescheduler_test.go:41)."""

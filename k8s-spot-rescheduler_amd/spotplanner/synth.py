@@ -38,8 +38,15 @@ def load_synth():
         lib.sr_synth_string.restype = ctypes.c_char_p
         lib.sr_synth_num_strings.argtypes = [ctypes.c_void_p]
         lib.sr_synth_num_strings.restype = ctypes.c_int32
+        lib.sr_synth_label_flags.argtypes = [ctypes.c_char_p]
+        lib.sr_synth_label_flags.restype = ctypes.c_uint8
         _synth = lib
     return _synth
+
+
+def synth_label_flags(s: str) -> int:
+    """The generator's sr_cluster.str_label entry for `s` (its C++ validity functions)."""
+    return int(load_synth().sr_synth_label_flags(s.encode()))
 
 
 class SynthCluster:

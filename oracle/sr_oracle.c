@@ -418,6 +418,45 @@ struct oracle_snapshot {
   int32_t opaque_total;
 };
 
+/* labels.NewRequirement's validateLabelKey (validation.IsQualifiedName) /
+ * validateLabelValue (validation.IsValidLabelValue) [upstream apimachinery
+ * v0.19.2 labels/selector.go], through the shim's table (sr_cluster.str_label).
+ * Without a table the strings' validity is unknown: callers treat the
+ * requirement as unverifiable (fallback). */
+static int o_label_ok(const sr_cluster *c, int32_t id, uint8_t what) {
+  return c->str_label && id >= 0 && id < c->n_strings && (c->str_label[id] & what) == what;
+}
+
+static int o_req_strings_ok(const sr_cluster *c, int32_t key, const int32_t *vals, int32_t lo, int32_t hi) {
+  if (!o_label_ok(c, key, SR_STR_LABEL_KEY)) return 0;
+  for (int32_t v = lo; v < hi; v++)
+    if (!o_label_ok(c, vals[v], SR_STR_LABEL_VALUE)) return 0;
+  return 1;
+}
+
+/* A term whose label selector fails metav1.LabelSelectorAsSelector [upstream
+ * apimachinery v0.19.2]: NewRequirement(key, op, values) on every matchLabels
+ * pair (Equals) and matchExpression -- the key a qualified name, every value a
+ * valid label value, In/NotIn with values, Exists/DoesNotExist without, no
+ * other operator. */
+static int o_term_invalid(const sr_cluster *c, int32_t t) {
+  const sr_pod_affinity *A = c->pod_affinity;
+  if (A->selector_nil[t]) return 0;
+  for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; i++) {
+    if (A->ml_key[i] == c->id_empty && c->id_empty != -1) return 1;
+    if (!o_req_strings_ok(c, A->ml_key[i], A->ml_val, i, i + 1)) return 1;
+  }
+  for (int32_t e = A->me_off[t]; e < A->me_off[t + 1]; e++) {
+    int32_t nv = A->me_val_off[e + 1] - A->me_val_off[e], op = A->me_op[e];
+    if (A->me_key[e] == c->id_empty && c->id_empty != -1) return 1;
+    if (!o_req_strings_ok(c, A->me_key[e], A->me_vals, A->me_val_off[e], A->me_val_off[e + 1])) return 1;
+    if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) return 1;
+    if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) return 1;
+    if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST) return 1;
+  }
+  return 0;
+}
+
 /* A pod whose required anti-affinity the encoded set cannot evaluate: no
  * sr_pod_affinity at all, the flag without terms, or a term whose label
  * selector fails LabelSelectorAsSelector [upstream apimachinery
@@ -427,34 +466,8 @@ static int o_anti_opaque(const sr_cluster *c, int32_t pod) {
   if (!(c->pods.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY)) return 0;
   const sr_pod_affinity *A = c->pod_affinity;
   if (!A || A->anti_off[pod] == A->anti_off[pod + 1]) return 1;
-  for (int32_t t = A->anti_off[pod]; t < A->anti_off[pod + 1]; t++) {
-    if (A->selector_nil[t]) continue;
-    for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; i++)
-      if (A->ml_key[i] == c->id_empty && c->id_empty != -1) return 1;
-    for (int32_t e = A->me_off[t]; e < A->me_off[t + 1]; e++) {
-      int32_t nv = A->me_val_off[e + 1] - A->me_val_off[e], op = A->me_op[e];
-      if (A->me_key[e] == c->id_empty && c->id_empty != -1) return 1;
-      if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) return 1;
-      if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) return 1;
-      if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST) return 1;
-    }
-  }
-  return 0;
-}
-
-/* A term whose label selector fails LabelSelectorAsSelector (same rules as above). */
-static int o_term_invalid(const sr_cluster *c, int32_t t) {
-  const sr_pod_affinity *A = c->pod_affinity;
-  if (A->selector_nil[t]) return 0;
-  for (int32_t i = A->ml_off[t]; i < A->ml_off[t + 1]; i++)
-    if (A->ml_key[i] == c->id_empty && c->id_empty != -1) return 1;
-  for (int32_t e = A->me_off[t]; e < A->me_off[t + 1]; e++) {
-    int32_t nv = A->me_val_off[e + 1] - A->me_val_off[e], op = A->me_op[e];
-    if (A->me_key[e] == c->id_empty && c->id_empty != -1) return 1;
-    if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) return 1;
-    if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) return 1;
-    if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST) return 1;
-  }
+  for (int32_t t = A->anti_off[pod]; t < A->anti_off[pod + 1]; t++)
+    if (o_term_invalid(c, t)) return 1;
   return 0;
 }
 
@@ -645,6 +658,9 @@ static int o_expr_valid(const sr_cluster *c, int32_t e) {
   const sr_pods *P = &c->pods;
   int32_t nv = P->expr_val_off[e + 1] - P->expr_val_off[e];
   if (P->expr_key[e] == c->id_empty && c->id_empty != -1) return 0; /* empty key fails validateLabelKey */
+  /* validateLabelKey(key), then (after the operator's arity / integer checks)
+   * validateLabelValue on every value: any failure fails the term */
+  if (!o_req_strings_ok(c, P->expr_key[e], P->expr_vals, P->expr_val_off[e], P->expr_val_off[e + 1])) return 0;
   switch (P->expr_op[e]) {
     case SR_OP_IN:
     case SR_OP_NOT_IN:
@@ -915,7 +931,7 @@ int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c,
   if (P->aff_required[pod])
     for (int32_t t = P->term_off[pod]; t < P->term_off[pod + 1]; t++)
       for (int32_t e = P->term_expr_off[t]; e < P->term_expr_off[t + 1]; e++)
-        if ((P->expr_op[e] == SR_OP_GT || P->expr_op[e] == SR_OP_LT) && !c->str_int) return 1;
+        if (((P->expr_op[e] == SR_OP_GT || P->expr_op[e] == SR_OP_LT) && !c->str_int) || !c->str_label) return 1;
   return 0;
 }
 

@@ -188,10 +188,41 @@ def _affinity():
     none = [[] for _ in gen]
     yield Case("gt_integer_labels", gt, aff(T(("gen", "Gt", ["6"]))), gen, none, [True, True, False, False, False])
     yield Case("lt_integer_labels", gt, aff(T(("gen", "Lt", ["7"]))), gen, none, [False, False, True, False, False])
-    yield Case("gt_is_strict_and_signed", gt, aff(T(("gen", "Gt", ["-3"]))), gen, none,
-               [True, True, False, False, False])
-    yield Case("gt_value_with_leading_zero_and_sign", gt, aff(T(("gen", "Lt", ["+012"]))), gen, none,
-               [True, False, True, False, False])
+    yield Case("gt_is_strict", gt, aff(T(("gen", "Gt", ["7"]))), gen, none, [False, True, False, False, False])
+    yield Case("lt_value_with_leading_zero", gt + "; ParseInt(\"012\") = 12", aff(T(("gen", "Lt", ["012"]))), gen,
+               none, [True, False, True, False, False])
+    # labels.NewRequirement runs validateLabelValue (validation.IsValidLabelValue: <= 63 characters of
+    # ([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9], or empty) on every value after the operator checks, and
+    # validateLabelKey (validation.IsQualifiedName) on the key: a requirement that fails makes
+    # NodeSelectorRequirementsAsSelector return an error, and MatchNodeSelectorTerms skips the term
+    lv = mt + "; NewRequirement: validateLabelKey / validateLabelValue on the key and every value"
+    yield Case("gt_signed_value_fails_label_validation", lv + " (\"-3\" starts with '-')",
+               aff(T(("gen", "Gt", ["-3"]))), gen, none, [False, False, False, False, False])
+    yield Case("lt_plus_sign_fails_label_validation", lv + " (\"+012\" starts with '+')",
+               aff(T(("gen", "Lt", ["+012"]))), gen, none, [False, False, False, False, False])
+    yield Case("not_in_invalid_value_fails_its_term", lv + "; NotIn [\"-x\"] would hold on every node",
+               aff(T(("zone", "NotIn", ["-x"]))), nodes3, [[], [], []], [False, False, False])
+    yield Case("not_in_invalid_value_other_term_holds", lv, aff(T(("zone", "NotIn", ["b", "a."])),
+                                                               T(("zone", "In", ["b"]))), nodes3, [[], [], []],
+               [False, True, False])
+    yield Case("in_64_character_value_fails_its_term", lv + " (63 characters at most)",
+               aff(T(("zone", "In", ["a", "v" * 64]))), nodes3 + [N("d", labels=z("v" * 64))], [[], [], [], []],
+               [False, False, False, False])
+    yield Case("in_63_character_value_is_valid", lv,
+               aff(T(("zone", "In", ["a", "v" * 63]))), nodes3 + [N("d", labels=z("v" * 63))], [[], [], [], []],
+               [True, False, False, True])
+    yield Case("exists_invalid_key_fails_its_term", lv + " (\"bad key\" is not a qualified name)",
+               aff(T(("bad key", "DoesNotExist", [])), T(("zone", "Exists", []))), nodes3, [[], [], []],
+               [True, True, False])
+    yield Case("prefixed_key_is_valid", lv + " (DNS-1123 subdomain prefix)",
+               aff(T(("example.com/zone", "DoesNotExist", []))), nodes3, [[], [], []], [True, True, True])
+    yield Case("uppercase_prefix_fails_key_validation", lv + " (the prefix is lower case)",
+               aff(T(("Example.com/zone", "DoesNotExist", []))), nodes3, [[], [], []], [False, False, False])
+    yield Case("empty_value_is_valid", lv + " (an empty label value is valid)", aff(T(("zone", "NotIn", [""]))),
+               nodes3, [[], [], []], [True, True, True])
+    yield Case("node_selector_values_not_validated", sel + "; labels.SelectorFromSet does not validate in v0.19",
+               P(node_selector={"zone": "-x"}), [N("a", labels=z("-x")), N("b", labels=z("a"))], [[], []],
+               [True, False])
     yield Case("gt_non_integer_value_fails_its_term", gt + "; a value that does not parse fails NewRequirement",
                aff(T(("gen", "Gt", ["six"])), T(("gen", "Lt", ["0"]))), gen, none,
                [False, False, True, False, False])

@@ -15,6 +15,7 @@ import pytest
 
 from helpers import Scenario
 from oracle_lib import OracleSnapshot, oracle_plan
+from plan_first_cases import check_plan_first, plan_first_scenario
 from randcluster import rand_scenario
 from spotplanner import capi
 from spotplanner.model import Interner, Taint
@@ -43,25 +44,8 @@ def plan_first(checker, h, cluster_ptr, cand_off, cand_pods, full=True):
 
 
 def check_first(o, status, nodes, wmap, ref_all, ref_early, cand_off, full=True):
-    """sr_plan_first against the oracle: the reference loop's winner and
-    mapping; every candidate it evaluated (up to its batch's end) equal to the
-    all-candidates oracle, SR_CAND_SKIPPED after."""
-    assert o.first_ok == ref_early["first_ok"] == ref_all["first_ok"]
-    assert o.winner == ref_early["winner"]
-    assert list(wmap) == list(ref_early["winner_map"])
-    if not full:
-        return
-    n = len(cand_off) - 1
-    seen_skip = False
-    for c in range(n):
-        if status[c] == SKIPPED:
-            seen_skip = True
-            assert o.first_ok >= 0 and c > o.first_ok, c
-            continue
-        assert not seen_skip, c  # evaluated candidates form a prefix
-        assert status[c] == ref_all["status"][c], c
-        seg = slice(int(cand_off[c]), int(cand_off[c + 1]))
-        assert list(nodes[seg]) == list(ref_all["node_of_pod"][seg]), c
+    segs = [nodes[int(cand_off[c]):int(cand_off[c + 1])] for c in range(len(cand_off) - 1)]
+    check_plan_first(o.first_ok, o.first_fallback, o.winner, wmap, status, segs, ref_all, ref_early, cand_off, full)
 
 
 @pytest.fixture(scope="module")
@@ -76,26 +60,28 @@ def small_batch_checker():
     c.close()
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(24))
 @pytest.mark.parametrize("which", ["default", "batch2"])
 def test_plan_first_matches_reference_loop(checker, small_batch_checker, seed, which):
+    """Fallback candidates before, right after, far after and instead of the
+    first drainable one, across prefix-batch boundaries, with hostname / zone
+    (anti-)affinity on three seeds in four: the winner, -1 when a fallback
+    candidate precedes it, the first fallback, every evaluated status and
+    mapping, equal to the oracle's loop."""
     ck = checker if which == "default" else small_batch_checker
-    nodes, spot_pods, cands = rand_scenario(9500 + seed, n_spot=6 + seed % 9, n_cand=14, max_pods=9,
-                                            anti=0.3 if seed % 3 == 0 else 0.0)
+    nodes, spot_pods, cands, pattern, win, fb = plan_first_scenario(seed)
     flat = [p for c in cands for p in c]
     sc = Scenario(nodes, spot_pods, flat)
     cand_off = np.cumsum([0] + [len(c) for c in cands]).astype(np.int32)
     cand_pods = np.arange(sc.q0, sc.q0 + len(flat), dtype=np.int32)
     ref_all = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=1)
     ref_early = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=0)
-    if any(s == capi.SR_CAND_FALLBACK for s in ref_all["status"]):
-        pytest.skip("the oracle routes a candidate to the reference path")
+    for c in fb:  # the injected candidates take the reference path on both sides
+        assert ref_all["status"][c] == capi.SR_CAND_FALLBACK
     h = sc.product_snapshot()
     try:
         for full in (True, False):
             o, status, nodes_o, wmap = plan_first(ck, h, sc.ptr, cand_off, cand_pods, full)
-            if o.first_fallback >= 0:  # the product routed one more candidate (off-node anti-affinity)
-                continue
             check_first(o, status, nodes_o, wmap, ref_all, ref_early, cand_off, full)
     finally:
         capi.load_planner().sr_snapshot_destroy(h)

@@ -60,7 +60,8 @@ def main():
     fetch_dir, write_dir, path = sys.argv[1:4]
     fetch = per_launch(fetch_dir, "FETCH_SIZE")
     write = per_launch(write_dir, "WRITE_SIZE")
-    res = {"_raw": {}}
+    res = {"_raw": {}, "measured_at_head": os.environ.get("SR_SOURCE_HEAD", "unknown"),
+           "command": os.environ.get("SR_PMC_COMMAND", "bench.py (see tools/gpu_round.sh)")}
     for key in sorted(set(fetch) | set(write)):
         f = fetch.get(key, [])
         w = write.get(key, [])
