@@ -203,6 +203,32 @@ typedef struct {
    * the fallback path.  (Spec.NodeSelector goes through labels.SelectorFromSet,
    * which does not validate in v0.19.) */
   const uint8_t *str_label;
+  /* Scalar resources (v1helper.IsScalarResourceName: extended resources,
+   * hugepages-*, attachable-volumes-*): the ScalarResources loop of
+   * NodeResourcesFit fitsRequest [upstream k8s v1.19.2 noderesources/fit.go]:
+   * a pod fits when alloc[s] >= req[s] + requested[s] for every name s it
+   * lists (a node without s allocates 0; a listed name, even with 0, disables
+   * the all-zero-request shortcut).  CSR per pod / per node, names interned;
+   * Value() quantities.  pod_scalar_req: computePodResourceRequest (max of the
+   * containers' sum and each init container, plus Overhead); pod_scalar_acc:
+   * what NodeInfo.AddPod adds to Requested for the same name.  NULL
+   * pod_scalar_off: no scalar tables (the shim flags such pods
+   * SR_POD_FB_SCALAR_RESOURCES). */
+  const int32_t *pod_scalar_off;   /* [pods.n+1] */
+  const int32_t *pod_scalar_name;
+  const int64_t *pod_scalar_req;
+  const int64_t *pod_scalar_acc;
+  const int32_t *node_scalar_off;  /* [nodes.n+1] Status.Allocatable scalar resources */
+  const int32_t *node_scalar_name;
+  const int64_t *node_scalar_alloc;
+  /* NodeInfo.AddPod's accounting of cpu / memory / ephemeral storage
+   * (calculateResource) for each pod; it can differ from the fit request
+   * req_* (init containers).  The snapshot's Requested sums these.  NULL: the
+   * same as req_*.  The Go shim fills both sides from the pinned scheduler
+   * (framework.NewNodeInfo(pod).Requested). */
+  const int64_t *acc_milli_cpu;
+  const int64_t *acc_memory;
+  const int64_t *acc_ephemeral;
 } sr_cluster;
 #define SR_STR_LABEL_VALUE 1u
 #define SR_STR_LABEL_KEY   2u

@@ -29,6 +29,7 @@
 // place).  Pod specs and requirements are interned by content across calls,
 // so a call canonicalises only specs it has never seen.
 #include <algorithm>
+#include <map>
 #include <atomic>
 #include <chrono>
 #include <climits>
@@ -184,11 +185,19 @@ void for_each_spec_word(const sr_cluster* c, const sr_pods& P, int32_t pod, F&& 
     f(P.port_num[i]);
     f(P.port_ip[i]);
   }
+  if (has_scalars(c, pod)) {  // scalar resources: (name, fit request)
+    f(-7);
+    for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; ++i) {
+      f(c->pod_scalar_name[i]);
+      f(static_cast<int32_t>(static_cast<uint64_t>(c->pod_scalar_req[i])));
+      f(static_cast<int32_t>(static_cast<uint64_t>(c->pod_scalar_req[i]) >> 32));
+    }
+  }
 }
 
-bool has_static_spec(const sr_pods& P, int32_t pod) {
+bool has_static_spec(const sr_cluster* c, const sr_pods& P, int32_t pod) {
   return P.sel_off[pod] != P.sel_off[pod + 1] || P.tol_off[pod] != P.tol_off[pod + 1] ||
-         P.port_off[pod] != P.port_off[pod + 1] || P.aff_required[pod] != 0;
+         P.port_off[pod] != P.port_off[pod + 1] || P.aff_required[pod] != 0 || has_scalars(c, pod);
 }
 
 // Requirement word group {len, type, key, op, sorted unique values}.
@@ -212,6 +221,7 @@ struct SpecDraft {
   std::vector<int32_t> terms;  // per buildable term: {n groups, groups...}
   int32_t n_terms = 0;
   std::vector<int32_t> tol, ports;
+  std::vector<int64_t> scalars;  // {name, fit request}*, sorted by name
 };
 
 void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
@@ -284,6 +294,16 @@ void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
     d->ports.push_back(P.port_proto[i]);
     d->ports.push_back(P.port_num[i]);
     d->ports.push_back(P.port_ip[i]);
+  }
+  if (has_scalars(c, pod)) {  // fitsRequest's ScalarResources loop: one (name, request) check each
+    std::vector<std::pair<int64_t, int64_t>> sc;
+    for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; ++i)
+      sc.emplace_back(c->pod_scalar_name[i], c->pod_scalar_req[i]);
+    std::sort(sc.begin(), sc.end());
+    for (const auto& x : sc) {
+      d->scalars.push_back(x.first);
+      d->scalars.push_back(x.second);
+    }
   }
 }
 
@@ -497,6 +517,10 @@ uint64_t node_state_fp(const SpotNode& sn, const NodeState& st) {
   uint64_t h = 0x51ED270B7A1DE5ull;
   for (int r = 0; r < 3; ++r) h = mix(mix(h, static_cast<uint64_t>(sn.alloc[r])), static_cast<uint64_t>(st.requested[r]));
   h = mix(mix(h, static_cast<uint64_t>(sn.alloc_pods)), static_cast<uint64_t>(st.npods));
+  for (const auto& a : sn.scalar_alloc)  // sorted by name: the order is canonical
+    h = mix(mix(mix(h, 0x5CA1ull), static_cast<uint32_t>(a.first)), static_cast<uint64_t>(a.second));
+  for (const auto& r : st.scalar_req)
+    h = mix(mix(mix(h, 0x5CA2ull), static_cast<uint32_t>(r.first)), static_cast<uint64_t>(r.second));
   uint64_t ports = 0;  // order-independent
   for (const Port& u : st.ports)
     ports += mix(mix(mix(0x9E37ull, static_cast<uint32_t>(u.ip)), static_cast<uint32_t>(u.proto)),
@@ -563,13 +587,26 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   // pass later reads them sequentially instead of from the cluster arrays)
   std::vector<int64_t>& req_flat = C.scratch.req_flat;
   req_flat.resize(static_cast<size_t>(w->n_input_pods) * 3);
-  auto pod_fallback = [&](int32_t pod, int32_t j) {
+  auto pod_fallback = [&](int32_t pod, int32_t j, bool last) {
     if (P.flags[pod] & SR_POD_FB_MASK) return true;
     int64_t* rq = &req_flat[static_cast<size_t>(j - w->pod_base) * 3];
     rq[0] = P.req_milli_cpu[pod];
     rq[1] = P.req_memory[pod];
     rq[2] = P.req_ephemeral[pod];
     if (!in_range(rq[0]) || !in_range(rq[1]) || !in_range(rq[2])) return true;
+    // NodeInfo.AddPod adds another amount than the fit request (init
+    // containers) and later pods of the candidate see it: the device's
+    // running state subtracts the request
+    for (int r = 0; r < 3 && !last; ++r)
+      if (pod_acc(c, pod, r) != rq[r]) return true;
+    if (has_scalars(c, pod)) {
+      // a listed scalar keeps an all-zero cpu / memory / ephemeral request
+      // from skipping the resource checks: not encoded
+      if (rq[0] == 0 && rq[1] == 0 && rq[2] == 0) return true;
+      if (snap->scalar_unknown_total > 0) return true;  // some node's scalar usage is unknown
+      for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; ++i)
+        if (!in_range(c->pod_scalar_req[i]) || !in_range(c->pod_scalar_acc[i])) return true;
+    }
     if (P.aff_required[pod])
       for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1]; ++t)
         for (int32_t e = P.term_expr_off[t]; e < P.term_expr_off[t + 1]; ++e) {
@@ -603,7 +640,22 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
       // an existing pod's opaque anti-affinity may select any incoming pod
       bool fb = (c->pod_affinity ? snap->opaque_total : snap->anti_total) > 0 || (e - b) > MAX_CAND_PODS;
-      for (int32_t j = b; j < e && !fb; ++j) fb = pod_fallback(cands->cand_pods[j], j);
+      for (int32_t j = b; j < e && !fb; ++j) fb = pod_fallback(cands->cand_pods[j], j, j + 1 == e);
+      if (!fb && c->pod_scalar_off) {
+        // two pods of the candidate listing one scalar resource: the later
+        // one sees the earlier one's AddPod on the node -- a running state
+        // the device does not keep for scalars (the check is a static atom)
+        int32_t names[64], nn = 0;
+        for (int32_t j = b; j < e && !fb; ++j) {
+          const int32_t pod = cands->cand_pods[j];
+          for (int32_t k = c->pod_scalar_off[pod]; k < c->pod_scalar_off[pod + 1] && !fb; ++k) {
+            const int32_t name = c->pod_scalar_name[k];
+            for (int32_t u = 0; u < nn && !fb; ++u) fb = names[u] == name;
+            if (nn == 64) fb = true;
+            else names[nn++] = name;
+          }
+        }
+      }
       if (fb) w->status_host[i] = SR_CAND_FALLBACK;
       for (int32_t j = b; j < e && !fb && !cand_ports[i]; ++j)
         cand_ports[i] = P.port_off[cands->cand_pods[j]] != P.port_off[cands->cand_pods[j] + 1];
@@ -820,7 +872,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         const size_t b0 = buf.size();
         spec_woff[q] = static_cast<uint32_t>(b0);
         const int32_t pod = active_pod[q];
-        if (!has_static_spec(P, pod)) continue;  // spec 0
+        if (!has_static_spec(c, P, pod)) continue;  // spec 0
         for_each_spec_word(c, P, pod, [&](int32_t x) { buf.push_back(x); });
         const uint64_t h = hash_words(buf.data() + b0, buf.size() - b0);
         spec_hash[q] = h;
@@ -912,6 +964,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
       sp.tol.swap(d.tol);
       sp.ports.swap(d.ports);
+      sp.scalars.swap(d.scalars);
     }
   }
   for (size_t id = C.spec_req_off.size() - 1; id < C.spec.size(); ++id) {
@@ -1003,14 +1056,26 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       used_reqs.push_back(r);
     }
   };
+  // scalar resource checks of this call: one atom per distinct (name, request)
+  std::vector<std::pair<int64_t, int64_t>> scalar_query;
+  std::map<std::pair<int64_t, int64_t>, int32_t> scalar_index;
+  auto scalar_atom_index = [&](int64_t name, int64_t req) {
+    auto ins = scalar_index.emplace(std::make_pair(name, req), static_cast<int32_t>(scalar_query.size()));
+    if (ins.second) scalar_query.emplace_back(name, req);
+    return ins.first->second;
+  };
   for (int32_t k : keys) {
     const int32_t id = k < n_spec_ids ? k : key_spec[k - n_spec_ids];
     for (uint32_t i = C.spec_req_off[id]; i < C.spec_req_off[id + 1]; ++i) use_req(C.spec_req[i]);
+    const std::vector<int64_t>& sc = C.spec[id].scalars;
+    for (size_t i = 0; i + 2 <= sc.size(); i += 2) scalar_atom_index(sc[i], sc[i + 1]);
   }
   const int32_t n_reqs = static_cast<int32_t>(used_reqs.size());
   const int32_t n_ports = static_cast<int32_t>(port_query.size());
+  const int32_t n_scalars = static_cast<int32_t>(scalar_query.size());
   const int32_t A_REQ = 1, A_TAINT = 1 + n_reqs, A_PORT = A_TAINT + n_taints;
-  const int32_t A_ANTI = A_PORT + n_ports;  // DA(t) at A_ANTI + 2t, DB(t) at A_ANTI + 2t + 1
+  const int32_t A_SCALAR = A_PORT + n_ports;
+  const int32_t A_ANTI = A_SCALAR + n_scalars;  // DA(t) at A_ANTI + 2t, DB(t) at A_ANTI + 2t + 1
   const int32_t A_AFF = A_ANTI + 2 * anti.n_terms;  // SAT(S) at A_AFF + 2s, KEYS(S) at A_AFF + 2s + 1
   const int32_t A_COMP = A_AFF + 2 * aff.n_sets;
   // Composite atoms, one per distinct untolerated-taint set U of the pods:
@@ -1039,7 +1104,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     C.psig_dict.clear();
     C.psig_gen = C.static_gen;
   }
-  std::vector<int32_t> sig, da, db, call_class;
+  std::vector<int32_t> sig, da, db, call_class, scq;
   auto static_sig = [&](const SpecInfo& sp, int32_t untol, std::vector<int32_t>& out) {
     out.clear();
     out.push_back(sp.flags);
@@ -1055,7 +1120,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   // term, TERM_AND extends it); an impossible class ANDs atom 0 with its
   // complement.  `sw` = static signature words.
   auto emit_class = [&](const int32_t* sw, uint64_t ports, const std::vector<int32_t>* da_, const std::vector<int32_t>* db_,
-                        int32_t aff_atom) {
+                        int32_t aff_atom, const std::vector<int32_t>* sc_ = nullptr) {
     const int32_t flags = sw[0], n_sel = sw[1];
     const int32_t* sel = sw + 2;
     const int32_t* tp = sel + n_sel;
@@ -1069,6 +1134,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       const int32_t b = __builtin_ctzll(m);
       if (bit_query[b] >= 0) emit(A_PORT + bit_query[b], PROG_ANDNOT);
     }
+    if (sc_)
+      for (int32_t q : *sc_) emit(A_SCALAR + q, PROG_AND);  // alloc[s] >= request + requested[s]
     if (da_)
       for (int32_t t : *da_) emit(A_ANTI + 2 * t, PROG_ANDNOT);  // anti-affinity base conflicts
     if (db_)
@@ -1097,7 +1164,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     const int32_t spec_id = k < n_spec_ids ? k : key_spec[k - n_spec_ids];
     SpecInfo& sp = C.spec[spec_id];
     const int32_t untol = untol_of(spec_id);
-    if (k < n_spec_ids && sp.ports.empty()) {
+    if (k < n_spec_ids && sp.ports.empty() && sp.scalars.empty()) {
       if (sp.psig_gen != C.static_gen) {
         static_sig(sp, untol, sig);
         sp.psig = C.psig_dict.intern(sig);
@@ -1130,8 +1197,12 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
           if (anti.da_any[t]) da.push_back(t);
         }
       }
+    scq.clear();
+    for (size_t i = 0; i + 2 <= sp.scalars.size(); i += 2) scq.push_back(scalar_atom_index(sp.scalars[i], sp.scalars[i + 1]));
     static_sig(sp, untol, sig);
     const size_t n_static = sig.size();
+    sig.push_back(static_cast<int32_t>(scq.size()));
+    sig.insert(sig.end(), scq.begin(), scq.end());
     sig.push_back(static_cast<int32_t>(ports & 0xffffffffu));
     sig.push_back(static_cast<int32_t>(ports >> 32));
     sig.push_back(static_cast<int32_t>(da.size()));
@@ -1143,7 +1214,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     const int32_t id = class_dict.intern(sig, &ins);
     if (ins) {
       sig.resize(n_static);
-      call_class.push_back(emit_class(sig.data(), ports, &da, &db, aff_atom));
+      call_class.push_back(emit_class(sig.data(), ports, &da, &db, aff_atom, &scq));
     }
     key_class[ki] = call_class[id];
   }
@@ -1269,6 +1340,25 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     }
     for (int32_t q = 0; q < n_ports; ++q)
       if (rows[q]) std::copy_n(rows[q]->begin(), Wp, A + static_cast<size_t>(A_PORT + q) * Wp);
+  }
+  // NodeResourcesFit's ScalarResources loop against the base snapshot:
+  // alloc[s] < request + requested[s] fails (a node without s allocates 0)
+  if (n_scalars > 0) {
+    auto value_of = [](const std::vector<std::pair<int32_t, int64_t>>& v, int64_t name) -> int64_t {
+      auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(static_cast<int32_t>(name), INT64_MIN));
+      return it != v.end() && it->first == name ? it->second : 0;
+    };
+    for (int32_t q = 0; q < n_scalars; ++q) {
+      uint64_t* row = A + static_cast<size_t>(A_SCALAR + q) * Wp;
+      const int64_t name = scalar_query[q].first, req = scalar_query[q].second;
+      for (int32_t n = 0; n < n_spot; ++n) {
+        const int64_t alloc = value_of(snap->nodes[n].scalar_alloc, name);
+        const int64_t used = value_of(snap->state[n].scalar_req, name);
+        // Go int64 arithmetic: request + requested wraps like the reference's
+        const int64_t need = static_cast<int64_t>(static_cast<uint64_t>(req) + static_cast<uint64_t>(used));
+        if (!(alloc < need)) row[n >> 6] |= 1ull << (n & 63);
+      }
+    }
   }
   for (int32_t t = 0; t < anti.n_terms; ++t) {
     std::copy_n(&anti.da[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t) * Wp);

@@ -40,6 +40,7 @@ struct SpotNode {
   uint8_t unschedulable = 0;
   std::vector<std::pair<int32_t, int32_t>> labels;  // (key, value)
   std::vector<TaintRec> taints;
+  std::vector<std::pair<int32_t, int64_t>> scalar_alloc;  // Allocatable scalar resources (name, value), by name
 };
 
 // The snapshot's own copy of what InterPodAffinity reads from a pod it holds
@@ -69,6 +70,8 @@ struct NodeState {
   int32_t unknown = 0;
   std::vector<Port> ports;
   std::vector<int32_t> pods;
+  std::vector<std::pair<int32_t, int64_t>> scalar_req;  // Requested scalar resources (name, value), by name
+  int32_t scalar_unknown = 0;  // pods added without scalar tables that carry scalar requests
 };
 
 }  // namespace sr
@@ -94,6 +97,7 @@ struct sr_snapshot {
   int64_t anti_total = 0;
   int64_t opaque_total = 0;   // pods whose anti-affinity the encoder cannot read: every candidate falls back
   int64_t unknown_total = 0;  // pods without metadata: candidates whose own terms need it fall back
+  int64_t scalar_unknown_total = 0;  // pods whose scalar requests are unknown: candidates asking for any fall back
   uint64_t version = 0;  // bumped on every mutation
 };
 
@@ -125,6 +129,19 @@ inline bool label_req_strings_ok(const sr_cluster* c, int32_t key, const int32_t
   for (int32_t v = lo; v < hi; ++v)
     if (!label_str_ok(c, vals[v], SR_STR_LABEL_VALUE)) return false;
   return true;
+}
+// The pod lists scalar resources (sr_cluster.pod_scalar_*).
+inline bool has_scalars(const sr_cluster* c, int32_t pod) {
+  return c->pod_scalar_off && c->pod_scalar_off[pod + 1] > c->pod_scalar_off[pod];
+}
+// NodeInfo.AddPod's accounting of resource r (0 cpu, 1 memory, 2 ephemeral) for the pod.
+inline int64_t pod_acc(const sr_cluster* c, int32_t pod, int r) {
+  const sr_pods& P = c->pods;
+  switch (r) {
+    case 0: return c->acc_milli_cpu ? c->acc_milli_cpu[pod] : P.req_milli_cpu[pod];
+    case 1: return c->acc_memory ? c->acc_memory[pod] : P.req_memory[pod];
+    default: return c->acc_ephemeral ? c->acc_ephemeral[pod] : P.req_ephemeral[pod];
+  }
 }
 inline bool has_anti_terms(const sr_cluster* c, int32_t pod) {
   return (c->pods.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) ||
@@ -254,6 +271,7 @@ struct SpecInfo {
   int32_t n_terms = 0;
   std::vector<int32_t> tol;    // Spec.Tolerations {key, op, value, effect}*
   std::vector<int32_t> ports;  // host ports {protocol, port, ip}* with port > 0
+  std::vector<int64_t> scalars;  // scalar resources {name, fit request}*, sorted by name
   uint64_t untol_gen = ~0ull;  // static generation `untol` was computed for
   int32_t untol = -1;          // set of spot-pool taints it does not tolerate (EncoderCache::untol_dict)
   uint64_t psig_gen = ~0ull;   // static generation `psig` was interned for

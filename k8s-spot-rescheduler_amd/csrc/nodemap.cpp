@@ -139,9 +139,17 @@ static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod, const
   auto wrap_add = [](int64_t a, int64_t b) {
     return static_cast<int64_t>(static_cast<uint64_t>(a) + static_cast<uint64_t>(b));
   };
-  st.requested[0] = wrap_add(st.requested[0], P.req_milli_cpu[pod]);
-  st.requested[1] = wrap_add(st.requested[1], P.req_memory[pod]);
-  st.requested[2] = wrap_add(st.requested[2], P.req_ephemeral[pod]);
+  for (int r = 0; r < 3; ++r) st.requested[r] = wrap_add(st.requested[r], pod_acc(c, pod, r));
+  if (has_scalars(c, pod)) {  // Requested.ScalarResources[name] += value (kept sorted by name)
+    for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; ++i) {
+      const int32_t name = c->pod_scalar_name[i];
+      auto it = std::lower_bound(st.scalar_req.begin(), st.scalar_req.end(), std::make_pair(name, INT64_MIN));
+      if (it == st.scalar_req.end() || it->first != name) it = st.scalar_req.insert(it, {name, 0});
+      it->second = wrap_add(it->second, c->pod_scalar_acc[i]);
+    }
+  } else if (!c->pod_scalar_off && (P.flags[pod] & SR_POD_FB_SCALAR_RESOURCES)) {
+    st.scalar_unknown += 1;  // its scalar requests are not in the call: unknown to the planner
+  }
   st.npods += 1;
   st.anti += sp.anti;
   st.opaque += sp.opaque;
@@ -211,6 +219,7 @@ void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t 
   s->anti_total += sp.anti;
   s->opaque_total += sp.opaque;
   s->unknown_total += sp.meta ? 0 : 1;
+  s->scalar_unknown_total += !c->pod_scalar_off && (c->pods.flags[pod] & SR_POD_FB_SCALAR_RESOURCES) ? 1 : 0;
   s->version++;
 }
 
@@ -277,6 +286,11 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
         sn.labels.emplace_back(N.label_key[j], N.label_val[j]);
       for (int32_t j = N.taint_off[node]; j < N.taint_off[node + 1]; ++j)
         sn.taints.push_back(TaintRec{N.taint_key[j], N.taint_val[j], N.taint_effect[j]});
+      if (c->node_scalar_off) {
+        for (int32_t j = c->node_scalar_off[node]; j < c->node_scalar_off[node + 1]; ++j)
+          sn.scalar_alloc.emplace_back(c->node_scalar_name[j], c->node_scalar_alloc[j]);
+        std::sort(sn.scalar_alloc.begin(), sn.scalar_alloc.end());
+      }
       sn.static_fp = node_static_fp(sn, c);
       s->state[i].pods.reserve(static_cast<size_t>(off[node + 1] - off[node]));
       uint32_t lab = lbase[i];
@@ -303,6 +317,7 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
     s->anti_total += s->state[i].anti;
     s->opaque_total += s->state[i].opaque;
     s->unknown_total += s->state[i].unknown;
+    s->scalar_unknown_total += s->state[i].scalar_unknown;
   }
   *out = s;
   return SR_OK;
@@ -361,11 +376,12 @@ sr_status sr_snapshot_revert(sr_snapshot* snap) {
   snap->lval.resize(snap->fork_labels);
   snap->term_words.resize(snap->fork_terms);
   snap->forked = false;
-  snap->anti_total = snap->opaque_total = snap->unknown_total = 0;
+  snap->anti_total = snap->opaque_total = snap->unknown_total = snap->scalar_unknown_total = 0;
   for (const auto& st : snap->state) {
     snap->anti_total += st.anti;
     snap->opaque_total += st.opaque;
     snap->unknown_total += st.unknown;
+    snap->scalar_unknown_total += st.scalar_unknown;
   }
   snap->version++;
   return SR_OK;

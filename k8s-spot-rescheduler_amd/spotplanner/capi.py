@@ -73,7 +73,10 @@ class sr_cluster(ctypes.Structure):
                 ("id_metadata_name", ctypes.c_int32), ("id_unschedulable_key", ctypes.c_int32),
                 ("pod_affinity", ctypes.POINTER(sr_pod_affinity)), ("n_strings", ctypes.c_int32),
                 ("str_int", ctypes.POINTER(ctypes.c_int64)), ("str_int_ok", ctypes.POINTER(ctypes.c_uint8)),
-                ("str_label", ctypes.POINTER(ctypes.c_uint8))]
+                ("str_label", ctypes.POINTER(ctypes.c_uint8)),
+                ("pod_scalar_off", P32), ("pod_scalar_name", P32), ("pod_scalar_req", P64), ("pod_scalar_acc", P64),
+                ("node_scalar_off", P32), ("node_scalar_name", P32), ("node_scalar_alloc", P64),
+                ("acc_milli_cpu", P64), ("acc_memory", P64), ("acc_ephemeral", P64)]
 
 
 class sr_node_label(ctypes.Structure):
@@ -175,6 +178,18 @@ def make_cluster_struct(A) -> sr_cluster:
     if A.get("str_label") is not None:
         c.n_strings = len(A["str_label"])
         c.str_label = ptr(A["str_label"], PU8)
+    if A.get("pod_scalar_off") is not None:
+        c.pod_scalar_off = ptr(A["pod_scalar_off"], P32)
+        c.pod_scalar_name = ptr(A["pod_scalar_name"], P32)
+        c.pod_scalar_req = ptr(A["pod_scalar_req"], P64)
+        c.pod_scalar_acc = ptr(A["pod_scalar_acc"], P64)
+        c.node_scalar_off = ptr(A["node_scalar_off"], P32)
+        c.node_scalar_name = ptr(A["node_scalar_name"], P32)
+        c.node_scalar_alloc = ptr(A["node_scalar_alloc"], P64)
+    if A.get("acc_cpu") is not None:
+        c.acc_milli_cpu = ptr(A["acc_cpu"], P64)
+        c.acc_memory = ptr(A["acc_mem"], P64)
+        c.acc_ephemeral = ptr(A["acc_eph"], P64)
     if A.get("pa_ns") is not None:
         pa = sr_pod_affinity()
         for f in ("ns", "label_off", "label_key", "label_val", "anti_off", "topology_key", "ns_off", "ns_ids",

@@ -155,6 +155,43 @@ class Pod:
             eph += self.overhead.ephemeral
         return cpu, mem, eph
 
+    def scalar_request(self) -> Dict[str, int]:
+        """computePodResourceRequest's ScalarResources: max(Σ containers, each
+        init container) + Overhead per name (every name listed anywhere)."""
+        out: Dict[str, int] = {}
+        for c in self.containers:
+            for k, v in c.scalar.items():
+                out[k] = out.get(k, 0) + v
+        for ic in self.init_containers:
+            for k, v in ic.scalar.items():
+                out[k] = max(out.get(k, 0), v)
+        if self.overhead is not None:
+            for k, v in self.overhead.scalar.items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def node_accounting(self):
+        """What NodeInfo.AddPod adds to the node's Requested in k8s v1.19.2
+        (framework/v1alpha1/types.go calculateResource): the regular containers'
+        sum plus Overhead -- init containers are not counted there, unlike in
+        the fit request (parity unpinned: the module is not in the reference
+        tree; the Go shim takes both from the pinned scheduler itself).
+        Returns (cpu, memory, ephemeral, {scalar name: amount})."""
+        cpu = sum(c.cpu_milli for c in self.containers)
+        mem = sum(c.memory for c in self.containers)
+        eph = sum(c.ephemeral for c in self.containers)
+        sc: Dict[str, int] = {}
+        for c in self.containers:
+            for k, v in c.scalar.items():
+                sc[k] = sc.get(k, 0) + v
+        if self.overhead is not None:
+            cpu += self.overhead.cpu_milli
+            mem += self.overhead.memory
+            eph += self.overhead.ephemeral
+            for k, v in self.overhead.scalar.items():
+                sc[k] = sc.get(k, 0) + v
+        return cpu, mem, eph, sc
+
     def host_ports(self):
         return [p for c in self.containers for p in c.ports if p.host_port > 0]
 
@@ -169,6 +206,7 @@ class Node:
     labels: Dict[str, str] = field(default_factory=dict)
     taints: List[Taint] = field(default_factory=list)
     unschedulable: bool = False
+    scalar: Dict[str, int] = field(default_factory=dict)  # Allocatable extended / hugepages resources
 
 
 def pod_id(pod: Pod) -> str:
@@ -225,7 +263,7 @@ def _daemonset_owner_walk(pod: Pod):
     return False, False
 
 
-def pod_flags(pod: Pod) -> int:
+def pod_flags(pod: Pod, scalar_tables: bool = True) -> int:
     f = 0
     if _daemonset_owner_walk(pod)[0]:
         f |= capi.SR_POD_DAEMONSET_CONTROLLER
@@ -234,7 +272,7 @@ def pod_flags(pod: Pod) -> int:
     if pod.required_pod_anti_affinity or pod.pod_anti_affinity:
         f |= capi.SR_POD_HAS_REQ_ANTI_AFFINITY
     conts = list(pod.containers) + list(pod.init_containers) + ([pod.overhead] if pod.overhead else [])
-    if any(c.scalar for c in conts):
+    if not scalar_tables and any(c.scalar for c in conts):  # the shim passes no scalar tables
         f |= capi.SR_POD_FB_SCALAR_RESOURCES
     if pod.has_pvc:
         f |= capi.SR_POD_FB_VOLUMES
@@ -359,10 +397,13 @@ def _encode_pod_affinity(pods: List[Pod], it: Interner) -> dict:
 
 
 def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Interner] = None,
-                   pod_node: Optional[List[int]] = None) -> EncodedCluster:
+                   pod_node: Optional[List[int]] = None, scalar_tables: bool = True,
+                   accounting: bool = True) -> EncodedCluster:
     """Encode nodes and pods.  pod_node[i] is the node index of pods[i] (default:
     looked up by pod.node_name; -1 when unbound).  Pods of one node keep their
-    relative order (= the per-node LIST order)."""
+    relative order (= the per-node LIST order).  scalar_tables=False: no scalar
+    resource tables (pods listing scalars are flagged for the fallback path);
+    accounting=False: no acc_* table (NodeInfo.AddPod adds the fit request)."""
     it = interner or Interner()
     e = it.id("")
     mn = it.id("metadata.name")
@@ -410,7 +451,7 @@ def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Intern
         re.append(eph)
         hp.append(0 if p.priority is None else 1)
         pr.append(0 if p.priority is None else p.priority)
-        fl.append(pod_flags(p))
+        fl.append(pod_flags(p, scalar_tables))
         for k, v in p.node_selector.items():
             sk.append(it.id(k))
             sv.append(it.id(v))
@@ -451,6 +492,29 @@ def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Intern
              tol_eff=_i32(tole), port_off=_i32(po), port_proto=_i32(pp), port_num=_i32(pnum),
              port_ip=_i32(pip))
     A.update(_encode_pod_affinity(pods, it))
+    if scalar_tables:
+        so_, sn_, sr_, sa_ = [0], [], [], []
+        for p in pods:
+            req = p.scalar_request()
+            acc = p.node_accounting()[3]
+            for name in sorted(req):
+                sn_.append(it.id(name))
+                sr_.append(req[name])
+                sa_.append(acc.get(name, 0))
+            so_.append(len(sn_))
+        no_, nn_, na_ = [0], [], []
+        for n in nodes:
+            for name in sorted(n.scalar):
+                nn_.append(it.id(name))
+                na_.append(n.scalar[name])
+            no_.append(len(nn_))
+        A.update(pod_scalar_off=_i32(so_), pod_scalar_name=_i32(sn_), pod_scalar_req=_i64(sr_),
+                 pod_scalar_acc=_i64(sa_), node_scalar_off=_i32(no_), node_scalar_name=_i32(nn_),
+                 node_scalar_alloc=_i64(na_))
+    if accounting:
+        accs = [p.node_accounting() for p in pods]
+        A.update(acc_cpu=_i64([a[0] for a in accs]), acc_mem=_i64([a[1] for a in accs]),
+                 acc_eph=_i64([a[2] for a in accs]))
     A["n_nodes"] = len(nodes)
     A["n_pods"] = len(pods)
     A["id_empty"] = e

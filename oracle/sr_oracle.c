@@ -406,6 +406,10 @@ typedef struct {
   o_port *ports;
   int32_t nlist, lcap; /* NodeInfo.Pods (InterPodAffinity matches against them) */
   int32_t *list;
+  int32_t nsc, sccap;  /* Requested.ScalarResources as (name, amount) entries, one per AddPod entry */
+  int32_t *sc_name;
+  int64_t *sc_val;
+  int32_t sc_unknown;  /* pods added without scalar tables that carry scalar requests */
 } o_state;
 
 struct oracle_snapshot {
@@ -416,6 +420,10 @@ struct oracle_snapshot {
   int32_t forked;
   int32_t anti_total;
   int32_t opaque_total;
+  int32_t sc_unknown_total;
+  /* Allocatable scalar resources per position, copied at AddNodeWithPods */
+  int32_t *alloc_off, *alloc_name;
+  int64_t *alloc_val;
 };
 
 /* labels.NewRequirement's validateLabelKey (validation.IsQualifiedName) /
@@ -482,11 +490,37 @@ static int o_aff_opaque(const sr_cluster *c, int32_t pod) {
 
 static int64_t o_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 
+/* What NodeInfo.AddPod adds to Requested (calculateResource [upstream k8s
+ * v1.19.2 framework/v1alpha1/types.go]); the shim's acc_* table, else the
+ * fit request. */
+static int64_t o_acc(const sr_cluster *c, int32_t pod, int r) {
+  const sr_pods *P = &c->pods;
+  if (r == 0) return c->acc_milli_cpu ? c->acc_milli_cpu[pod] : P->req_milli_cpu[pod];
+  if (r == 1) return c->acc_memory ? c->acc_memory[pod] : P->req_memory[pod];
+  return c->acc_ephemeral ? c->acc_ephemeral[pod] : P->req_ephemeral[pod];
+}
+
+static int o_has_scalars(const sr_cluster *c, int32_t pod) {
+  return c->pod_scalar_off && c->pod_scalar_off[pod + 1] > c->pod_scalar_off[pod];
+}
+
 static void o_state_add_pod(o_state *st, const sr_cluster *c, int32_t pod) {
   const sr_pods *P = &c->pods;
-  st->req[0] = o_add(st->req[0], P->req_milli_cpu[pod]);
-  st->req[1] = o_add(st->req[1], P->req_memory[pod]);
-  st->req[2] = o_add(st->req[2], P->req_ephemeral[pod]);
+  for (int r = 0; r < 3; r++) st->req[r] = o_add(st->req[r], o_acc(c, pod, r));
+  if (o_has_scalars(c, pod)) {
+    for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; i++) {
+      if (st->nsc == st->sccap) {
+        st->sccap = st->sccap ? st->sccap * 2 : 4;
+        st->sc_name = (int32_t *)realloc(st->sc_name, sizeof(int32_t) * (size_t)st->sccap);
+        st->sc_val = (int64_t *)realloc(st->sc_val, sizeof(int64_t) * (size_t)st->sccap);
+      }
+      st->sc_name[st->nsc] = c->pod_scalar_name[i];
+      st->sc_val[st->nsc] = c->pod_scalar_acc[i];
+      st->nsc++;
+    }
+  } else if (!c->pod_scalar_off && (P->flags[pod] & SR_POD_FB_SCALAR_RESOURCES)) {
+    st->sc_unknown++;
+  }
   st->npods++;
   if ((P->flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) ||
       (c->pod_affinity && c->pod_affinity->anti_off[pod + 1] > c->pod_affinity->anti_off[pod]))
@@ -524,7 +558,22 @@ oracle_snapshot *oracle_snapshot_create(const sr_cluster *c, const int32_t *spot
       o_state_add_pod(&s->st[i], c, node_pod_idx[j]);
     s->anti_total += s->st[i].anti;
     s->opaque_total += s->st[i].opaque;
+    s->sc_unknown_total += s->st[i].sc_unknown;
   }
+  s->alloc_off = (int32_t *)calloc((size_t)n_spot + 1, sizeof(int32_t));
+  int32_t total = 0;
+  for (int32_t i = 0; i < n_spot; i++) {
+    s->alloc_off[i] = total;
+    if (c->node_scalar_off) total += c->node_scalar_off[spot[i] + 1] - c->node_scalar_off[spot[i]];
+  }
+  s->alloc_off[n_spot] = total;
+  s->alloc_name = (int32_t *)malloc(sizeof(int32_t) * (size_t)(total ? total : 1));
+  s->alloc_val = (int64_t *)malloc(sizeof(int64_t) * (size_t)(total ? total : 1));
+  for (int32_t i = 0; i < n_spot && c->node_scalar_off; i++)
+    for (int32_t j = c->node_scalar_off[spot[i]], k = s->alloc_off[i]; j < c->node_scalar_off[spot[i] + 1]; j++, k++) {
+      s->alloc_name[k] = c->node_scalar_name[j];
+      s->alloc_val[k] = c->node_scalar_alloc[j];
+    }
   return s;
 }
 
@@ -533,6 +582,8 @@ static void o_free_states(o_state *st, int32_t n) {
   for (int32_t i = 0; i < n; i++) {
     free(st[i].ports);
     free(st[i].list);
+    free(st[i].sc_name);
+    free(st[i].sc_val);
   }
   free(st);
 }
@@ -551,6 +602,14 @@ static o_state *o_copy_states(const o_state *src, int32_t n) {
       dst[i].list = (int32_t *)malloc(sizeof(int32_t) * (size_t)src[i].lcap);
       memcpy(dst[i].list, src[i].list, sizeof(int32_t) * (size_t)src[i].nlist);
     }
+    dst[i].sc_name = NULL;
+    dst[i].sc_val = NULL;
+    if (src[i].nsc) {
+      dst[i].sc_name = (int32_t *)malloc(sizeof(int32_t) * (size_t)src[i].sccap);
+      dst[i].sc_val = (int64_t *)malloc(sizeof(int64_t) * (size_t)src[i].sccap);
+      memcpy(dst[i].sc_name, src[i].sc_name, sizeof(int32_t) * (size_t)src[i].nsc);
+      memcpy(dst[i].sc_val, src[i].sc_val, sizeof(int64_t) * (size_t)src[i].nsc);
+    }
   }
   return dst;
 }
@@ -560,14 +619,18 @@ void oracle_snapshot_destroy(oracle_snapshot *s) {
   o_free_states(s->st, s->n);
   o_free_states(s->saved, s->n);
   free(s->node);
+  free(s->alloc_off);
+  free(s->alloc_name);
+  free(s->alloc_val);
   free(s);
 }
 
 void oracle_snapshot_add_pod(oracle_snapshot *s, const sr_cluster *c, int32_t pod, int32_t pos) {
-  int32_t before = s->st[pos].anti, obefore = s->st[pos].opaque;
+  int32_t before = s->st[pos].anti, obefore = s->st[pos].opaque, ubefore = s->st[pos].sc_unknown;
   o_state_add_pod(&s->st[pos], c, pod);
   s->anti_total += s->st[pos].anti - before;
   s->opaque_total += s->st[pos].opaque - obefore;
+  s->sc_unknown_total += s->st[pos].sc_unknown - ubefore;
 }
 
 int32_t oracle_snapshot_fork(oracle_snapshot *s) {
@@ -583,10 +646,11 @@ int32_t oracle_snapshot_revert(oracle_snapshot *s) {
   s->st = s->saved;
   s->saved = NULL;
   s->forked = 0;
-  s->anti_total = s->opaque_total = 0;
+  s->anti_total = s->opaque_total = s->sc_unknown_total = 0;
   for (int32_t i = 0; i < s->n; i++) {
     s->anti_total += s->st[i].anti;
     s->opaque_total += s->st[i].opaque;
+    s->sc_unknown_total += s->st[i].sc_unknown;
   }
   return SR_OK;
 }
@@ -769,16 +833,32 @@ static int o_ports_ok(const o_state *st, const sr_cluster *c, int32_t pod) {
   return 1;
 }
 
-/* NodeResourcesFit.Filter: fitsRequest [upstream plugins/noderesources/fit.go]. */
-static int o_resources_ok(const o_state *st, const sr_cluster *c, int32_t pod, int32_t node) {
+/* NodeResourcesFit.Filter: fitsRequest [upstream k8s v1.19.2
+ * plugins/noderesources/fit.go]: the pod count, then -- unless cpu, memory,
+ * ephemeral storage are all zero and no scalar resource is listed -- every
+ * resource: Allocatable < request + Requested fails; for each listed scalar
+ * resource the node's Allocatable.ScalarResources (0 when absent) against
+ * the request plus Requested.ScalarResources. */
+static int o_resources_ok(const oracle_snapshot *s, const o_state *st, const sr_cluster *c, int32_t pod, int32_t pos,
+                          int32_t node) {
   const sr_pods *P = &c->pods;
   const sr_nodes *N = &c->nodes;
   if ((int64_t)st->npods + 1 > N->alloc_pods[node]) return 0;
   int64_t rc = P->req_milli_cpu[pod], rm = P->req_memory[pod], re = P->req_ephemeral[pod];
-  if (rc == 0 && rm == 0 && re == 0) return 1;
+  if (rc == 0 && rm == 0 && re == 0 && !o_has_scalars(c, pod)) return 1;
   if (N->alloc_milli_cpu[node] < o_add(rc, st->req[0])) return 0;
   if (N->alloc_memory[node] < o_add(rm, st->req[1])) return 0;
   if (N->alloc_ephemeral[node] < o_add(re, st->req[2])) return 0;
+  if (o_has_scalars(c, pod))
+    for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; i++) {
+      int32_t name = c->pod_scalar_name[i];
+      int64_t alloc = 0, used = 0;
+      for (int32_t k = s->alloc_off[pos]; k < s->alloc_off[pos + 1]; k++)
+        if (s->alloc_name[k] == name) alloc = s->alloc_val[k];
+      for (int32_t k = 0; k < st->nsc; k++)
+        if (st->sc_name[k] == name) used = o_add(used, st->sc_val[k]);
+      if (alloc < o_add(c->pod_scalar_req[i], used)) return 0;
+    }
   return 1;
 }
 
@@ -925,6 +1005,12 @@ static int o_pod_affinity_ok(const o_state *st, const int32_t *node, int32_t n, 
 int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c, int32_t pod) {
   const sr_pods *P = &c->pods;
   if (P->flags[pod] & SR_POD_FB_MASK) return 1;
+  /* outside the encoded set: scalar resources on an all-zero
+   * cpu / memory / ephemeral request, or while some snapshot pod's scalar
+   * usage is unknown */
+  if (o_has_scalars(c, pod) &&
+      ((P->req_milli_cpu[pod] == 0 && P->req_memory[pod] == 0 && P->req_ephemeral[pod] == 0) || s->sc_unknown_total > 0))
+    return 1;
   /* an existing pod's required anti-affinity may select the incoming pod:
    * opaque terms (o_anti_opaque) keep every pod on the fallback path */
   if (s->opaque_total > 0 || o_anti_opaque(c, pod) || o_aff_opaque(c, pod)) return 1;
@@ -935,13 +1021,13 @@ int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c,
   return 0;
 }
 
-static int o_check(const o_state *st, const int32_t *node, int32_t n, const sr_cluster *c, int32_t pod,
+static int o_check(const oracle_snapshot *s, const o_state *st, const int32_t *node, int32_t n, const sr_cluster *c, int32_t pod,
                    int32_t pos) {
   /* Filter order of the default provider; the result is their conjunction. */
   const o_state *sp = &st[pos];
   int32_t nd = node[pos];
   if (!o_unschedulable_ok(c, pod, nd)) return 0;
-  if (!o_resources_ok(sp, c, pod, nd)) return 0;
+  if (!o_resources_ok(s, sp, c, pod, pos, nd)) return 0;
   /* NodeName: passes, findSpotNodeForPod clears Spec.NodeName (rescheduler.go:341) */
   if (!o_ports_ok(sp, c, pod)) return 0;
   if (!o_affinity_ok(c, pod, nd)) return 0;
@@ -953,32 +1039,33 @@ static int o_check(const o_state *st, const int32_t *node, int32_t n, const sr_c
 
 int32_t oracle_check_predicates(const oracle_snapshot *s, const sr_cluster *c, int32_t pod, int32_t pos) {
   if (oracle_pod_needs_fallback(s, c, pod)) return -1;
-  return o_check(s->st, s->node, s->n, c, pod, pos);
+  return o_check(s, s->st, s->node, s->n, c, pod, pos);
 }
 
 /* findSpotNodeForPod (rescheduler.go:338-353) */
-static int32_t o_find(const o_state *st, const int32_t *node, int32_t n, const sr_cluster *c,
+static int32_t o_find(const oracle_snapshot *s, const o_state *st, const int32_t *node, int32_t n, const sr_cluster *c,
                       int32_t pod, uint64_t *checks) {
   for (int32_t pos = 0; pos < n; pos++) {
     if (checks) (*checks)++;
-    if (o_check(st, node, n, c, pod, pos)) return pos;
+    if (o_check(s, st, node, n, c, pod, pos)) return pos;
   }
   return -1;
 }
 
 int32_t oracle_find_spot_node_for_pod(const oracle_snapshot *s, const sr_cluster *c, int32_t pod) {
   if (oracle_pod_needs_fallback(s, c, pod)) return -2;
-  return o_find(s->st, s->node, s->n, c, pod, NULL);
+  return o_find(s, s->st, s->node, s->n, c, pod, NULL);
 }
+
+static int o_cand_fallback(const oracle_snapshot *s, const sr_cluster *c, const int32_t *pods, int32_t np);
 
 /* canDrainNode (rescheduler.go:357-370) */
 int32_t oracle_can_drain_node(oracle_snapshot *s, const sr_cluster *c, const int32_t *pods, int32_t n,
                               int32_t *node_of_pod) {
-  for (int32_t i = 0; i < n; i++)
-    if (oracle_pod_needs_fallback(s, c, pods[i])) return -2;
+  if (o_cand_fallback(s, c, pods, n)) return -2;
   for (int32_t i = 0; i < n; i++) node_of_pod[i] = -1;
   for (int32_t i = 0; i < n; i++) {
-    int32_t pos = o_find(s->st, s->node, s->n, c, pods[i], NULL);
+    int32_t pos = o_find(s, s->st, s->node, s->n, c, pods[i], NULL);
     if (pos < 0) return i;
     node_of_pod[i] = pos;
     oracle_snapshot_add_pod(s, c, pods[i], pos);
@@ -992,17 +1079,17 @@ int32_t oracle_can_drain_node(oracle_snapshot *s, const sr_cluster *c, const int
 typedef struct {
   int32_t pos;
   int64_t req[3];
-  int32_t npods, nports, anti, opaque, nlist;
+  int32_t npods, nports, anti, opaque, nlist, nsc;
 } o_undo;
 
 /* Evaluate one candidate from the base state `st` (Fork), then restore it (Revert). */
-static int32_t o_eval_candidate(o_state *st, const int32_t *node, int32_t n, const sr_cluster *c,
+static int32_t o_eval_candidate(const oracle_snapshot *s, o_state *st, const int32_t *node, int32_t n, const sr_cluster *c,
                                 const int32_t *pods, int32_t np, int32_t *map, o_undo *undo,
                                 uint64_t *checks) {
   int32_t nu = 0, status = SR_CAND_OK;
   for (int32_t i = 0; i < np; i++) map[i] = -1;
   for (int32_t i = 0; i < np; i++) {
-    int32_t pos = o_find(st, node, n, c, pods[i], checks);
+    int32_t pos = o_find(s, st, node, n, c, pods[i], checks);
     if (pos < 0) {
       status = i;
       break;
@@ -1016,6 +1103,7 @@ static int32_t o_eval_candidate(o_state *st, const int32_t *node, int32_t n, con
     u->anti = st[pos].anti;
     u->opaque = st[pos].opaque;
     u->nlist = st[pos].nlist;
+    u->nsc = st[pos].nsc;
     o_state_add_pod(&st[pos], c, pods[i]);
   }
   while (nu > 0) { /* Revert, newest first */
@@ -1026,13 +1114,34 @@ static int32_t o_eval_candidate(o_state *st, const int32_t *node, int32_t n, con
     st[u->pos].anti = u->anti;
     st[u->pos].opaque = u->opaque;
     st[u->pos].nlist = u->nlist;
+    st[u->pos].nsc = u->nsc;
   }
   return status;
 }
 
 static int o_cand_fallback(const oracle_snapshot *s, const sr_cluster *c, const int32_t *pods, int32_t np) {
+  const sr_pods *P = &c->pods;
   for (int32_t i = 0; i < np; i++)
     if (oracle_pod_needs_fallback(s, c, pods[i])) return 1;
+  /* a pod followed by more pods of the candidate whose AddPod accounting
+   * differs from its fit request (init containers): outside the encoded set */
+  for (int32_t i = 0; i + 1 < np; i++)
+    if (o_acc(c, pods[i], 0) != P->req_milli_cpu[pods[i]] || o_acc(c, pods[i], 1) != P->req_memory[pods[i]] ||
+        o_acc(c, pods[i], 2) != P->req_ephemeral[pods[i]])
+      return 1;
+  /* two pods of the candidate listing one scalar resource (the later one sees
+   * the earlier one's AddPod): outside the encoded set */
+  if (c->pod_scalar_off) {
+    int32_t entries = 0; /* the planner tracks up to 64 scalar entries per candidate */
+    for (int32_t i = 0; i < np; i++) entries += c->pod_scalar_off[pods[i] + 1] - c->pod_scalar_off[pods[i]];
+    if (entries > 64) return 1;
+  }
+  if (c->pod_scalar_off)
+    for (int32_t i = 0; i < np; i++)
+      for (int32_t a = c->pod_scalar_off[pods[i]]; a < c->pod_scalar_off[pods[i] + 1]; a++)
+        for (int32_t j = i + 1; j < np; j++)
+          for (int32_t b = c->pod_scalar_off[pods[j]]; b < c->pod_scalar_off[pods[j] + 1]; b++)
+            if (c->pod_scalar_name[a] == c->pod_scalar_name[b]) return 1;
   return 0;
 }
 
@@ -1065,7 +1174,7 @@ int32_t oracle_plan(const oracle_snapshot *s, const sr_cluster *c, const sr_cand
         fb_pods += (uint64_t)np;
         continue;
       }
-      status[i] = o_eval_candidate(st, s->node, s->n, c, pods, np, map + off[i], undo, &checks);
+      status[i] = o_eval_candidate(s, st, s->node, s->n, c, pods, np, map + off[i], undo, &checks);
       if (mode == 0 && status[i] == SR_CAND_OK) break; /* drain + break (rescheduler.go:286) */
     }
     free(undo);
@@ -1091,7 +1200,7 @@ int32_t oracle_plan(const oracle_snapshot *s, const sr_cluster *c, const sr_cand
           fb_pods += (uint64_t)np;
           continue;
         }
-        status[i] = o_eval_candidate(st, s->node, s->n, c, pods, np, map + off[i], undo, &checks);
+        status[i] = o_eval_candidate(s, st, s->node, s->n, c, pods, np, map + off[i], undo, &checks);
       }
       free(undo);
       o_free_states(st, s->n);

@@ -87,6 +87,42 @@ def _resources():
                [N("a", cpu=1000), N("b", cpu=1000)], [[used(cpu=401)], [used(cpu=400)]], [False, True])
 
 
+def _scalar():
+    sr = ("fitsRequest: for each scalar resource the pod lists, Allocatable.ScalarResources[name] (0 when the node "
+          "has none) < request + Requested.ScalarResources[name] fails")
+    G = "nvidia.com/gpu"
+
+    def gp(name="p", gpu=1, cpu=100, **kw):
+        return Pod(name, containers=[Container(cpu_milli=cpu, scalar={G: gpu} if gpu is not None else {})], **kw)
+    yield Case("scalar_request_needs_the_resource", sr, gp(gpu=1),
+               [N("a", scalar={G: 2}), N("b"), N("c", scalar={G: 1}), N("d", scalar={G: 2})],
+               [[], [], [gp("u", gpu=1)], [gp("u", gpu=1)]], [True, False, False, True])
+    yield Case("scalar_zero_request_listed", sr + " (0 < 0 + 0 is false: a listed zero fits anywhere)", gp(gpu=0),
+               [N("a"), N("b", scalar={G: 1})], [[], [gp("u", gpu=1)]], [True, True])
+    hp = "hugepages-2Mi"
+    yield Case("hugepages_exact_fit", sr,
+               Pod("p", containers=[Container(cpu_milli=10, scalar={hp: 2 * MiB})]),
+               [N("a", scalar={hp: 4 * MiB}), N("b", scalar={hp: 4 * MiB})],
+               [[Pod("u", containers=[Container(cpu_milli=10, scalar={hp: 2 * MiB})])],
+                [Pod("u", containers=[Container(cpu_milli=10, scalar={hp: 2 * MiB + 1})])]], [True, False])
+    ini = Pod("p", containers=[Container(cpu_milli=100, scalar={G: 1})],
+              init_containers=[Container(cpu_milli=0, scalar={G: 3})])
+    yield Case("scalar_init_container_max", sr + "; computePodResourceRequest: max(sum, each init container) = 3",
+               ini, [N("a", scalar={G: 2}), N("b", scalar={G: 3})], [[], []], [False, True])
+    oh = Pod("p", containers=[Container(cpu_milli=100, scalar={G: 1})], overhead=Container(scalar={G: 1}))
+    yield Case("scalar_overhead", sr + "; + Spec.Overhead", oh, [N("a", scalar={G: 1}), N("b", scalar={G: 2})],
+               [[], []], [False, True])
+    yield Case("scalar_and_cpu_both_checked", sr + "; cpu is checked as well", gp(gpu=1, cpu=900),
+               [N("a", cpu=1000, scalar={G: 1}), N("b", cpu=1000, scalar={G: 1})],
+               [[used(cpu=200)], [used(cpu=100)]], [False, True])
+    acc = ("NodeInfo.AddPod (calculateResource, k8s v1.19.2 framework/v1alpha1/types.go): Requested adds the "
+           "regular containers and Overhead, not init containers")
+    base_ini = Pod("u", containers=[Container(cpu_milli=100, scalar={G: 1})],
+                   init_containers=[Container(cpu_milli=800, scalar={G: 2})])
+    yield Case("node_accounting_skips_init_containers", acc + " (parity unpinned: the module is not vendored)",
+               gp(gpu=1, cpu=500), [N("a", cpu=1000, scalar={G: 2})], [[base_ini]], [True])
+
+
 def _taints():
     flt = "TaintToleration.Filter: FindMatchingUntoleratedTaint over NoSchedule / NoExecute taints"
     tt = "Toleration.ToleratesTaint: effect empty or equal, key empty or equal, Exists or Equal with equal value"
@@ -316,7 +352,7 @@ def _interpod():
 
 def cases() -> List[Case]:
     out = []
-    for gen in (_resources, _taints, _unschedulable, _affinity, _ports, _interpod):
+    for gen in (_resources, _scalar, _taints, _unschedulable, _affinity, _ports, _interpod):
         out.extend(gen())
     names = [c.name for c in out]
     assert len(names) == len(set(names))

@@ -35,6 +35,11 @@ def plan_first_scenario(seed: int, n_cand: int = 24):
     elif seed % 4 == 3:
         kw = dict(anti=0.15, aff=0.3, valid_selectors=True)
     nodes, spot_pods, cands = rand_scenario(9600 + seed, n_spot=8 + seed % 9, n_cand=n_cand, max_pods=6, **kw)
+    for c in cands:  # only the injected candidates leave the encoded set
+        for p in c:
+            p.init_containers = []
+            for ct in p.containers:
+                ct.scalar = {}
     pattern = PATTERNS[seed % len(PATTERNS)]
     win = 1 + (seed * 5) % (n_cand - 6)  # 1..18: before and after the boundaries 2, 6, 14, 16
     ns = cands[0][0].namespace if cands[0] else "default"

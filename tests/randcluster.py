@@ -29,9 +29,14 @@ def rand_node(r: random.Random, name: str, features: bool) -> Node:
     if features and r.random() < 0.3:
         for _ in range(r.randint(1, 2)):
             taints.append(Taint(r.choice(["dedicated", "team", "x"]), r.choice(VALS), r.choice(EFFECTS)))
+    scalar = {}
+    if features and r.random() < 0.3:  # extended resources / hugepages (NodeResourcesFit's scalar loop)
+        scalar["nvidia.com/gpu"] = r.choice([0, 1, 2, 4])
+        if r.random() < 0.3:
+            scalar["hugepages-2Mi"] = r.choice([0, 4 * MiB])
     return Node(name=name, cpu_milli=r.choice([500, 1000, 2000, 4000]), memory=r.choice([1, 2, 4]) * GiB,
                 pods=r.choice([3, 5, 110]), ephemeral=r.choice([0, 10 * GiB]), labels=labels, taints=taints,
-                unschedulable=features and r.random() < 0.1)
+                unschedulable=features and r.random() < 0.1, scalar=scalar)
 
 
 def rand_pod(r: random.Random, name: str, features: bool, fallback: bool = False) -> Pod:
@@ -46,6 +51,12 @@ def rand_pod(r: random.Random, name: str, features: bool, fallback: bool = False
     p = Pod(name=name, containers=conts, init_containers=init, overhead=overhead,
             owner_references=[OwnerReference("ReplicaSet")])
     if features:
+        if r.random() < 0.12:  # scalar resources (sometimes also on an init container)
+            p.containers[0].scalar = {"nvidia.com/gpu": r.choice([0, 1, 1, 2])}
+            if r.random() < 0.2:
+                p.containers[0].scalar["hugepages-2Mi"] = r.choice([2 * MiB, 4 * MiB])
+            if init and r.random() < 0.5:
+                init[0].scalar = {"nvidia.com/gpu": r.choice([1, 3])}
         if r.random() < 0.3:
             p.node_selector = {r.choice(KEYS): r.choice(VALS)}
         if r.random() < 0.25:

@@ -79,6 +79,8 @@ def test_node_order_first_fit_equals_pod_order(seed):
         want = olib.oracle_can_drain_node(snap.h, sc.ptr, capi.ptr(arr, capi.P32), len(pods),
                                           capi.ptr(want_map, capi.P32))
         olib.oracle_snapshot_revert(snap.h)
+        if want == -2:  # candidate-level fallback (an init-container pod before others)
+            continue
         assert got[0] == want, (seed, got, want)
         assert got[1] == [int(x) for x in want_map[:len(pods)]], (seed, got, want_map)
         compared += 1
