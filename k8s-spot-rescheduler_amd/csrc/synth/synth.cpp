@@ -424,6 +424,10 @@ void sr_synth_view(const sr_synth* s, sr_cluster* c) {
   c->str_int = nullptr;       // ... nor node-affinity Gt / Lt
   c->str_int_ok = nullptr;
   c->str_label = s->str_label.data();
+  c->pod_scalar_off = c->node_scalar_off = nullptr;  // no scalar resources in the BASELINE configs
+  c->pod_scalar_name = c->node_scalar_name = nullptr;
+  c->pod_scalar_req = c->pod_scalar_acc = c->node_scalar_alloc = nullptr;
+  c->acc_milli_cpu = c->acc_memory = c->acc_ephemeral = nullptr;  // AddPod adds the fit request
 }
 
 void sr_synth_drain(const sr_synth* s, sr_pod_drain* d) {
