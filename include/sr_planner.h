@@ -174,6 +174,29 @@ typedef struct {
   const int32_t *aff_off;
 } sr_pod_affinity;
 
+/* Spec.TopologySpreadConstraints with WhenUnsatisfiable = DoNotSchedule: the
+ * PodTopologySpread filter of k8s v1.19.2 [upstream
+ * plugins/podtopologyspread/filtering.go].  ScheduleAnyway constraints never
+ * filter and are not passed.  For each constraint: the nodes of the snapshot
+ * that pass the pod's nodeSelector / required node affinity and carry every
+ * constraint's topology key define the topology pairs; a pair counts the
+ * snapshot pods in the pod's own namespace, not terminating, matching the
+ * selector; a node passes when it carries every key and, per constraint,
+ * count(pair) + (the pod matches the selector) - min over the pairs <= maxSkew.
+ * Selector tables in the sr_pod_affinity term format; a selector that fails
+ * LabelSelectorAsSelector (or any pod with constraints when the cluster passes
+ * no sr_spread) goes to the fallback path. */
+typedef struct {
+  const int32_t *off;            /* [pods.n+1] pods -> DoNotSchedule constraints */
+  const int32_t *max_skew;       /* [constraints] */
+  const int32_t *topology_key;   /* [constraints] interned TopologyKey */
+  const uint8_t *selector_nil;   /* [constraints] LabelSelector == nil: matches nothing */
+  const int32_t *ml_off, *ml_key, *ml_val;  /* [constraints+1] MatchLabels */
+  const int32_t *me_off, *me_key, *me_op;   /* [constraints+1] MatchExpressions */
+  const int32_t *me_val_off, *me_vals;      /* [exprs+1] their values */
+  const uint8_t *terminating;    /* [pods.n] DeletionTimestamp != nil: never counted */
+} sr_spread;
+
 typedef struct {
   sr_nodes nodes;
   sr_pods  pods;
@@ -229,6 +252,10 @@ typedef struct {
   const int64_t *acc_milli_cpu;
   const int64_t *acc_memory;
   const int64_t *acc_ephemeral;
+  /* DoNotSchedule topology spread constraints (NULL: a pod that has them
+   * carries SR_POD_FB_TOPOLOGY_SPREAD).  Pod labels and namespaces come from
+   * pod_affinity, which must be given with it. */
+  const sr_spread *spread;
 } sr_cluster;
 #define SR_STR_LABEL_VALUE 1u
 #define SR_STR_LABEL_KEY   2u

@@ -456,7 +456,7 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       continue;
     }
     if (at.amask.empty()) {
-      at.amask.assign(static_cast<size_t>(n_flat) * kDomKeys, 0);
+      at.amask.assign(static_cast<size_t>(n_flat) * kDomKeys * kDynG, 0);
       at.cand_dyn.assign(static_cast<size_t>(nc), 0);
     }
     at.cand_dyn[i] = 1;
@@ -467,7 +467,8 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
         for (size_t f = 0; f < far_of[i].size(); ++f) {
           const int32_t t = far_of[i][f];
           if ((has(p, t << 1 | 1) && has(q, t << 1)) || (has(q, t << 1 | 1) && has(p, t << 1)))
-            at.amask[static_cast<size_t>(q - base) * kDomKeys + fslot[f]] |= 1ull << (p - b);
+            at.amask[(static_cast<size_t>(q - base) * kDomKeys + fslot[f]) * kDynG + (p - b) / 64] |=
+                1ull << ((p - b) % 64);
         }
   }
 
@@ -613,11 +614,11 @@ void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_can
   // of a later pod's set adds its domains to that pod's pair map while the
   // candidate is planned: the candidate takes K2's domain path (per pod, the
   // mask of those earlier pods), or the fallback path beyond its limits
-  std::vector<uint64_t> masks;
+  std::vector<uint64_t> masks;  // [pod of the candidate][kDynG]
   for (int32_t i = 0; i < nc; ++i) {
     if (status[i] != STATUS_PENDING) continue;
     const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
-    masks.assign(static_cast<size_t>(e - b), 0);
+    masks.assign(static_cast<size_t>(e - b) * kDynG, 0);
     bool any = false;
     for (int32_t k = b + 1; k < e; ++k) {
       const int32_t code = af.pod_code[k - base];
@@ -626,14 +627,19 @@ void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_can
         const PodMeta m = meta_of(A, cands->cand_pods[q]);
         bool all = true;
         for (const Term& t : sets[code >> 1]) all = all && term_selects(t, m);
-        if (all && q - b < 64) masks[k - b] |= 1ull << (q - b);
+        if (all && q - b < kDynPods) masks[static_cast<size_t>(k - b) * kDynG + (q - b) / 64] |= 1ull << ((q - b) % 64);
         any = any || all;
       }
     }
     if (!any) continue;
     bool ok = e - b <= kDynPods;
+    auto masked = [&](int32_t k) {
+      for (int g = 0; g < kDynG; ++g)
+        if (masks[static_cast<size_t>(k - b) * kDynG + g] != 0) return true;
+      return false;
+    };
     for (int32_t k = b; k < e && ok; ++k) {
-      if (masks[k - b] == 0) continue;
+      if (!masked(k)) continue;
       const int32_t set = af.pod_code[k - base] >> 1;
       ok = sets[set].size() <= static_cast<size_t>(kDynTerms);
       for (size_t t = 0; t < sets[set].size() && ok; ++t) ok = dk->slot(snap, sets[set][t].tk) >= 0;
@@ -643,7 +649,7 @@ void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_can
       continue;
     }
     if (af.mmask.empty()) {
-      af.mmask.assign(static_cast<size_t>(n_flat), 0);
+      af.mmask.assign(static_cast<size_t>(n_flat) * kDynG, 0);
       af.cand_dyn.assign(static_cast<size_t>(nc), 0);
       af.set_dyn.assign(static_cast<size_t>(S), 0);
       af.set_slots.resize(static_cast<size_t>(S));
@@ -651,8 +657,8 @@ void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_can
     }
     af.cand_dyn[i] = 1;
     for (int32_t k = b; k < e; ++k) {
-      af.mmask[k - base] = masks[k - b];
-      if (masks[k - b] != 0) af.set_dyn[af.pod_code[k - base] >> 1] = 1;
+      std::copy_n(&masks[static_cast<size_t>(k - b) * kDynG], kDynG, &af.mmask[static_cast<size_t>(k - base) * kDynG]);
+      if (masked(k)) af.set_dyn[af.pod_code[k - base] >> 1] = 1;
     }
   }
   // per set planned there: each term's key slot, and its base row (nodes

@@ -185,6 +185,12 @@ void for_each_spec_word(const sr_cluster* c, const sr_pods& P, int32_t pod, F&& 
     f(P.port_num[i]);
     f(P.port_ip[i]);
   }
+  if (has_spread(c, pod)) {  // topology spread constraints (with the pod's namespace and self-match)
+    f(-8);
+    std::vector<int32_t> w;
+    spread_words(c, pod, w);
+    for (int32_t x : w) f(x);
+  }
   if (has_scalars(c, pod)) {  // scalar resources: (name, fit request)
     f(-7);
     for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; ++i) {
@@ -197,7 +203,8 @@ void for_each_spec_word(const sr_cluster* c, const sr_pods& P, int32_t pod, F&& 
 
 bool has_static_spec(const sr_cluster* c, const sr_pods& P, int32_t pod) {
   return P.sel_off[pod] != P.sel_off[pod + 1] || P.tol_off[pod] != P.tol_off[pod + 1] ||
-         P.port_off[pod] != P.port_off[pod + 1] || P.aff_required[pod] != 0 || has_scalars(c, pod);
+         P.port_off[pod] != P.port_off[pod + 1] || P.aff_required[pod] != 0 || has_scalars(c, pod) ||
+         has_spread(c, pod);
 }
 
 // Requirement word group {len, type, key, op, sorted unique values}.
@@ -222,6 +229,7 @@ struct SpecDraft {
   int32_t n_terms = 0;
   std::vector<int32_t> tol, ports;
   std::vector<int64_t> scalars;  // {name, fit request}*, sorted by name
+  std::vector<int32_t> spread;   // spread_words
 };
 
 void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
@@ -295,6 +303,7 @@ void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
     d->ports.push_back(P.port_num[i]);
     d->ports.push_back(P.port_ip[i]);
   }
+  if (has_spread(c, pod)) spread_words(c, pod, d->spread);
   if (has_scalars(c, pod)) {  // fitsRequest's ScalarResources loop: one (name, request) check each
     std::vector<std::pair<int64_t, int64_t>> sc;
     for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; ++i)
@@ -613,6 +622,13 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
           if ((P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT) && !c->str_int) return true;
           if (!c->str_label) return true;  // NewRequirement's validation unknown
         }
+    if (has_spread(c, pod)) {
+      // the counts need every snapshot pod's namespace, labels and deletion
+      // state; a selector that fails to build errors PreFilter
+      if (!c->pod_affinity || !c->str_label || snap->unknown_total > 0 || snap->term_unknown_total > 0) return true;
+      for (int32_t k = c->spread->off[pod]; k < c->spread->off[pod + 1]; ++k)
+        if (spread_invalid(c, k)) return true;
+    }
     return anti_opaque(c, pod) || aff_opaque(c, pod);  // required (anti-)affinity the encoded set cannot read
   };
   for (int32_t i = 0; i < nc; ++i)
@@ -656,6 +672,20 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
           }
         }
       }
+      if (!fb && c->spread && c->pod_affinity) {
+        // a pod whose spread constraint counts an earlier pod of its candidate
+        // (same namespace, not terminating): its counts change while the
+        // candidate is planned, the row is against the base snapshot
+        const sr_spread* S = c->spread;
+        for (int32_t j = b + 1; j < e && !fb; ++j) {
+          const int32_t pod = cands->cand_pods[j];
+          for (int32_t k = S->off[pod]; k < S->off[pod + 1] && !fb; ++k)
+            for (int32_t u = b; u < j && !fb; ++u) {
+              const int32_t q = cands->cand_pods[u];
+              fb = !S->terminating[q] && c->pod_affinity->ns[q] == c->pod_affinity->ns[pod] && spread_selects(c, k, q);
+            }
+        }
+      }
       if (fb) w->status_host[i] = SR_CAND_FALLBACK;
       for (int32_t j = b; j < e && !fb && !cand_ports[i]; ++j)
         cand_ports[i] = P.port_off[cands->cand_pods[j]] != P.port_off[cands->cand_pods[j] + 1];
@@ -681,7 +711,12 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   analyse_affinity(snap, c, cands, Wp, w->status_host, &dk, &aff);
   // affinity planned on the domain path: the pod's class carries KEYS(S), the
   // device the rest (an earlier pod of its candidate matches all its terms)
-  auto aff_dyn = [&](int32_t flat) { return !aff.mmask.empty() && aff.mmask[flat - aff.base] != 0; };
+  auto aff_dyn = [&](int32_t flat) {
+    if (aff.mmask.empty()) return false;
+    for (int g = 0; g < kDynG; ++g)
+      if (aff.mmask[static_cast<size_t>(flat - aff.base) * kDynG + g] != 0) return true;
+    return false;
+  };
 
   // ---- host ports: HostPortInfo.CheckConflict [upstream k8s v1.19
   // framework/types.go] as state bits.  A (protocol, port) group whose active
@@ -965,6 +1000,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       sp.tol.swap(d.tol);
       sp.ports.swap(d.ports);
       sp.scalars.swap(d.scalars);
+      sp.spread.swap(d.spread);
     }
   }
   for (size_t id = C.spec_req_off.size() - 1; id < C.spec.size(); ++id) {
@@ -1064,18 +1100,29 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     if (ins.second) scalar_query.emplace_back(name, req);
     return ins.first->second;
   };
+  // topology spread of this call: one atom per spec carrying constraints
+  std::vector<int32_t> spread_query;
+  std::unordered_map<int32_t, int32_t> spread_index;
+  auto spread_atom_index = [&](int32_t spec_id) {
+    auto ins = spread_index.emplace(spec_id, static_cast<int32_t>(spread_query.size()));
+    if (ins.second) spread_query.push_back(spec_id);
+    return ins.first->second;
+  };
   for (int32_t k : keys) {
     const int32_t id = k < n_spec_ids ? k : key_spec[k - n_spec_ids];
     for (uint32_t i = C.spec_req_off[id]; i < C.spec_req_off[id + 1]; ++i) use_req(C.spec_req[i]);
     const std::vector<int64_t>& sc = C.spec[id].scalars;
     for (size_t i = 0; i + 2 <= sc.size(); i += 2) scalar_atom_index(sc[i], sc[i + 1]);
+    if (!C.spec[id].spread.empty()) spread_atom_index(id);
   }
   const int32_t n_reqs = static_cast<int32_t>(used_reqs.size());
   const int32_t n_ports = static_cast<int32_t>(port_query.size());
   const int32_t n_scalars = static_cast<int32_t>(scalar_query.size());
   const int32_t A_REQ = 1, A_TAINT = 1 + n_reqs, A_PORT = A_TAINT + n_taints;
+  const int32_t n_spreads = static_cast<int32_t>(spread_query.size());
   const int32_t A_SCALAR = A_PORT + n_ports;
-  const int32_t A_ANTI = A_SCALAR + n_scalars;  // DA(t) at A_ANTI + 2t, DB(t) at A_ANTI + 2t + 1
+  const int32_t A_SPREAD = A_SCALAR + n_scalars;  // scalar and spread atoms: the class's `sc_` list
+  const int32_t A_ANTI = A_SPREAD + n_spreads;  // DA(t) at A_ANTI + 2t, DB(t) at A_ANTI + 2t + 1
   const int32_t A_AFF = A_ANTI + 2 * anti.n_terms;  // SAT(S) at A_AFF + 2s, KEYS(S) at A_AFF + 2s + 1
   const int32_t A_COMP = A_AFF + 2 * aff.n_sets;
   // Composite atoms, one per distinct untolerated-taint set U of the pods:
@@ -1135,7 +1182,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       if (bit_query[b] >= 0) emit(A_PORT + bit_query[b], PROG_ANDNOT);
     }
     if (sc_)
-      for (int32_t q : *sc_) emit(A_SCALAR + q, PROG_AND);  // alloc[s] >= request + requested[s]
+      for (int32_t q : *sc_) emit(A_SCALAR + q, PROG_AND);  // alloc[s] >= request + requested[s]; spread rows
     if (da_)
       for (int32_t t : *da_) emit(A_ANTI + 2 * t, PROG_ANDNOT);  // anti-affinity base conflicts
     if (db_)
@@ -1164,7 +1211,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     const int32_t spec_id = k < n_spec_ids ? k : key_spec[k - n_spec_ids];
     SpecInfo& sp = C.spec[spec_id];
     const int32_t untol = untol_of(spec_id);
-    if (k < n_spec_ids && sp.ports.empty() && sp.scalars.empty()) {
+    if (k < n_spec_ids && sp.ports.empty() && sp.scalars.empty() && sp.spread.empty()) {
       if (sp.psig_gen != C.static_gen) {
         static_sig(sp, untol, sig);
         sp.psig = C.psig_dict.intern(sig);
@@ -1199,6 +1246,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
     scq.clear();
     for (size_t i = 0; i + 2 <= sp.scalars.size(); i += 2) scq.push_back(scalar_atom_index(sp.scalars[i], sp.scalars[i + 1]));
+    if (!sp.spread.empty()) scq.push_back(n_scalars + spread_atom_index(spec_id));
     static_sig(sp, untol, sig);
     const size_t n_static = sig.size();
     sig.push_back(static_cast<int32_t>(scq.size()));
@@ -1360,6 +1408,27 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
     }
   }
+  // PodTopologySpread against the base snapshot, over the spec's NodeAffinity
+  // row (nodeSelector AND, OR of the required terms) built from its requirement rows
+  for (int32_t q = 0; q < n_spreads; ++q) {
+    const SpecInfo& sp = C.spec[spread_query[q]];
+    std::vector<uint64_t> aff_row(static_cast<size_t>(Wp), (sp.flags & CLS_IMPOSSIBLE) ? 0ull : ~0ull);
+    for (int32_t r : sp.sel)
+      for (int32_t i = 0; i < Wp; ++i) aff_row[i] &= A[static_cast<size_t>(A_REQ + req_atom[r]) * Wp + i];
+    if ((sp.flags & CLS_AFF_REQUIRED) && !(sp.flags & CLS_IMPOSSIBLE)) {
+      std::vector<uint64_t> any(static_cast<size_t>(Wp), 0), t_row(static_cast<size_t>(Wp));
+      for (size_t i = 0; i < sp.terms.size(); i += 1 + static_cast<size_t>(sp.terms[i])) {
+        std::fill(t_row.begin(), t_row.end(), ~0ull);
+        for (int32_t j = 0; j < sp.terms[i]; ++j) {
+          const uint64_t* rr = A + static_cast<size_t>(A_REQ + req_atom[sp.terms[i + 1 + j]]) * Wp;
+          for (int32_t x = 0; x < Wp; ++x) t_row[x] &= rr[x];
+        }
+        for (int32_t x = 0; x < Wp; ++x) any[x] |= t_row[x];
+      }
+      for (int32_t x = 0; x < Wp; ++x) aff_row[x] &= any[x];
+    }
+    spread_row(snap, sp.spread.data(), aff_row.data(), A + static_cast<size_t>(A_SPREAD + q) * Wp);
+  }
   for (int32_t t = 0; t < anti.n_terms; ++t) {
     std::copy_n(&anti.da[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t) * Wp);
     std::copy_n(&anti.db[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t + 1) * Wp);
@@ -1413,10 +1482,17 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       for (int32_t q = w->cand_off[k]; q < w->cand_off[k + 1]; ++q) {
         const int32_t j = active_src[q];
         for (int32_t sl = 0; sl < kDomKeys; ++sl)
-          w->dyn_pod.push_back(anti.amask.empty() ? 0 : anti.amask[static_cast<size_t>(j - anti.base) * kDomKeys + sl]);
-        const uint64_t mm = aff.mmask.empty() ? 0 : aff.mmask[j - aff.base];
-        w->dyn_pod.push_back(mm);
-        w->dyn_pod.push_back(mm != 0 ? static_cast<uint64_t>(aff.pod_code[j - aff.base]) : ~0ull);
+          for (int g = 0; g < kDynG; ++g)
+            w->dyn_pod.push_back(anti.amask.empty()
+                                     ? 0
+                                     : anti.amask[(static_cast<size_t>(j - anti.base) * kDomKeys + sl) * kDynG + g]);
+        uint64_t any_mm = 0;
+        for (int g = 0; g < kDynG; ++g) {
+          const uint64_t mm = aff.mmask.empty() ? 0 : aff.mmask[static_cast<size_t>(j - aff.base) * kDynG + g];
+          any_mm |= mm;
+          w->dyn_pod.push_back(mm);
+        }
+        w->dyn_pod.push_back(any_mm != 0 ? static_cast<uint64_t>(aff.pod_code[j - aff.base]) : ~0ull);
       }
     }
   }

@@ -53,6 +53,7 @@ struct SnapPod {
   uint8_t meta = 0;    // ns / labels / terms known (the cluster passed sr_pod_affinity)
   uint8_t anti = 0;    // carries required anti-affinity
   uint8_t opaque = 0;  // ... that the encoder cannot read (anti_opaque)
+  uint8_t term = 0;    // DeletionTimestamp set (countPodsMatchSelector skips it); 2: unknown (no sr_spread)
   uint32_t lab = 0, nlab = 0;       // labels: sr_snapshot::lkey / lval [lab, lab + nlab)
   uint32_t terms = 0, nterms = 0;   // anti-affinity terms: sr_snapshot::term_words [terms, terms + nterms),
                                     // {n words, words...} per term (rare)
@@ -72,6 +73,7 @@ struct NodeState {
   std::vector<int32_t> pods;
   std::vector<std::pair<int32_t, int64_t>> scalar_req;  // Requested scalar resources (name, value), by name
   int32_t scalar_unknown = 0;  // pods added without scalar tables that carry scalar requests
+  int32_t term_unknown = 0;    // pods added without sr_spread (deletion state unknown)
 };
 
 }  // namespace sr
@@ -98,6 +100,7 @@ struct sr_snapshot {
   int64_t opaque_total = 0;   // pods whose anti-affinity the encoder cannot read: every candidate falls back
   int64_t unknown_total = 0;  // pods without metadata: candidates whose own terms need it fall back
   int64_t scalar_unknown_total = 0;  // pods whose scalar requests are unknown: candidates asking for any fall back
+  int64_t term_unknown_total = 0;    // pods whose deletion state is unknown: pods with spread constraints fall back
   uint64_t version = 0;  // bumped on every mutation
 };
 
@@ -143,6 +146,20 @@ inline int64_t pod_acc(const sr_cluster* c, int32_t pod, int r) {
     default: return c->acc_ephemeral ? c->acc_ephemeral[pod] : P.req_ephemeral[pod];
   }
 }
+// The pod carries DoNotSchedule topology spread constraints (sr_cluster.spread).
+inline bool has_spread(const sr_cluster* c, int32_t pod) {
+  return c->spread && c->spread->off[pod + 1] > c->spread->off[pod];
+}
+// PodTopologySpread (spread.cpp): constraint k's selector fails to build
+// (LabelSelectorAsSelector); the pod's constraints as canonical words
+// {namespace, n, per constraint {maxSkew, topologyKey, selects the pod itself,
+// nil, n matchLabels, (key, value)*, n matchExpressions, (key, op, n, values)*}};
+// the node row of such words against the base snapshot, given the pod's
+// NodeAffinity row (nodes passing its nodeSelector / required affinity).
+bool spread_invalid(const sr_cluster* c, int32_t k);
+bool spread_selects(const sr_cluster* c, int32_t k, int32_t pod);
+void spread_words(const sr_cluster* c, int32_t pod, std::vector<int32_t>& out);
+void spread_row(const sr_snapshot* snap, const int32_t* words, const uint64_t* aff_row, uint64_t* row);
 inline bool has_anti_terms(const sr_cluster* c, int32_t pod) {
   return (c->pods.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) ||
          (c->pod_affinity && c->pod_affinity->anti_off[pod + 1] > c->pod_affinity->anti_off[pod]);
@@ -173,8 +190,9 @@ enum : int32_t { CLS_AFF_REQUIRED = 1, CLS_IMPOSSIBLE = 2 };
 constexpr int kDomKeys = 4;   // key slots per encode
 constexpr int kDomMax = 64;   // domains of a table key (one bit each in a 64-bit mask)
 constexpr int kDynTerms = 4;  // terms of an affinity set planned on the domain path
-constexpr int kDynPods = 64;  // pods of a candidate planned on the domain path
-constexpr int kDynU64 = 6;    // words per pod record (kernels.hpp)
+constexpr int kDynG = 4;      // domain path: mask words per pod set (64 pods each)
+constexpr int kDynPods = 64 * kDynG;  // pods of a candidate planned on the domain path
+constexpr int kDynU64 = 5 * kDynG + 1;  // words per pod record (kernels.hpp)
 
 // The encoded workload of one planning call (host copy; uploaded as one
 // arena).  The spot nodes' state (capacity records, free values) lives in the
@@ -272,6 +290,7 @@ struct SpecInfo {
   std::vector<int32_t> tol;    // Spec.Tolerations {key, op, value, effect}*
   std::vector<int32_t> ports;  // host ports {protocol, port, ip}* with port > 0
   std::vector<int64_t> scalars;  // scalar resources {name, fit request}*, sorted by name
+  std::vector<int32_t> spread;   // DoNotSchedule topology spread constraints (spread_words), empty: none
   uint64_t untol_gen = ~0ull;  // static generation `untol` was computed for
   int32_t untol = -1;          // set of spot-pool taints it does not tolerate (EncoderCache::untol_dict)
   uint64_t psig_gen = ~0ull;   // static generation `psig` was interned for
@@ -393,7 +412,7 @@ struct AntiTerms {
   // flat pod of those, the earlier pods of its candidate it interacts with
   // through each key slot ([flat - base][kDomKeys]; empty: no such candidate)
   std::vector<uint8_t> cand_dyn;         // [candidate]
-  std::vector<uint64_t> amask;
+  std::vector<uint64_t> amask;          // [flat - base][kDomKeys][kDynG]
 };
 
 // Collects the terms of the snapshot's pods and of the pending candidates,
@@ -414,7 +433,7 @@ struct AffTerms {
   // later pod's set; per flat pod the mask of those earlier pods (0: static
   // SAT(S) is exact); per set planned there, each term's key slot and base row
   std::vector<uint8_t> cand_dyn;    // [candidate]
-  std::vector<uint64_t> mmask;      // [flat - base] (empty: no such candidate)
+  std::vector<uint64_t> mmask;      // [flat - base][kDynG] (empty: no such candidate)
   std::vector<uint8_t> set_dyn;     // [set]
   std::vector<std::vector<int32_t>> set_slots;     // [set][term] key slot (sets planned dynamically)
   std::vector<std::vector<uint64_t>> term_rows;    // [set][term * Wp] nodes whose domain hosts a base pod of M(S)

@@ -1362,23 +1362,39 @@ __device__ __forceinline__ int dk_row_of(const DevWorkload& w, int k) {
 }
 
 static_assert(64 * 32 * 8 <= sizeof(K2Lds), "domain path: touched bitmap of 2048 words in the wave's LDS");
-template <int CH>
+// G groups of 64 pods (G = 1: <= 64 pods, G = 4: <= 256): lane l of group g
+// keeps pod 64 g + l's node and domains, and the (64 g + l)-th touched node's
+// state.  A pod record holds, per key slot, G mask words over the earlier
+// pods, G affinity mask words and the set word (kDevDynU64 words, layout of
+// encode.cpp).
+template <int CH, int G>
 __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __restrict__ tl, const int p0,
                                           const int np, const int dbase, int& status, uint32_t& nbytes) {
   static_assert(kDevDomKeys == 4 && kDevDynTerms == 4, "the selects below unroll 4 key slots / terms");
+  static_assert(G >= 1 && G <= kDevDynG, "pod groups of the domain-path record");
   const int lane = threadIdx.x & 63;
   const int Wp = w.Wp;
   const uint64_t* __restrict__ tab = w.S;
   const uint64_t* __restrict__ at = w.atoms;
-  // touched nodes: lane s holds the s-th one's running state
-  int snode = INT_MAX, sleft = 0, nslots = 0;
-  int64_t scpu = 0, smem = 0, seph = 0;
-  uint64_t sport = 0;
+  // touched nodes: slot 64 g + lane holds the running state of the slot's node
+  int snode[G], sleft[G], nslots = 0;
+  int64_t scpu[G], smem[G], seph[G];
+  uint64_t sport[G];
+  // pod 64 g + lane: its node and its domain in every key slot
+  int pnode[G];
+  int pdom[G][kDevDomKeys];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    snode[g] = INT_MAX;
+    sleft[g] = 0;
+    scpu[g] = smem[g] = seph[g] = 0;
+    sport[g] = 0;
+    pnode[g] = -1;
+#pragma unroll
+    for (int kk = 0; kk < kDevDomKeys; ++kk) pdom[g][kk] = -1;
+  }
   for (int i = lane; i < 64 * CH; i += 64) tl[i] = 0;  // touched nodes (bitmap in the wave's LDS)
-  // lane k: pod k's node and its domain in every key slot
-  int pnode = -1;
-  int pdom[kDevDomKeys] = {-1, -1, -1, -1};
-  nbytes += (48u + 48u + 4u) * static_cast<uint32_t>(np) + 4u;
+  nbytes += (48u + 8u * kDevDynU64 + 4u) * static_cast<uint32_t>(np) + 4u;
   status = -1;
   int k = 0;
   for (; k < np; ++k) {
@@ -1388,21 +1404,30 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
     const uint64_t pin = swap_pairs(pm, w.swap_mask);
     const bool zero = (rc | rm | re) == 0;
     const uint64_t* dr = w.dyn_pod + static_cast<size_t>(dbase + k) * kDevDynU64;
-    const bool mine = lane < k;  // pods placed before this one
-    // anti-affinity: domains refused per key slot
+    // anti-affinity: domains refused per key slot (earlier pods it interacts with)
     uint64_t fdom[kDevDomKeys];
 #pragma unroll
     for (int kk = 0; kk < kDevDomKeys; ++kk) {
-      const uint64_t m = kk < w.n_dk ? dr[kk] : 0ull;
-      const bool in = mine && ((m >> lane) & 1) && pdom[kk] >= 0;
-      fdom[kk] = m != 0 ? wave_or(in ? 1ull << pdom[kk] : 0ull) : 0ull;
+      uint64_t any = 0, bits = 0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const uint64_t m = kk < w.n_dk ? dr[kk * kDevDynG + g] : 0ull;
+        any |= m;
+        const bool in = 64 * g + lane < k && ((m >> lane) & 1) && pdom[g][kk] >= 0;
+        bits |= in ? 1ull << pdom[g][kk] : 0ull;
+      }
+      fdom[kk] = any != 0 ? wave_or(bits) : 0ull;
     }
     // affinity: per term its key slot, base row and the earlier matching pods'
-    // domains (table key) or nodes (node-local key)
-    const uint64_t mm = dr[4], meta = dr[5];
+    // domains (table key) or pods (node-local key: adom holds their lanes per group)
+    const uint64_t meta = dr[5 * kDevDynG];
     int nt = 0;
     int tslot[kDevDynTerms] = {0, 0, 0, 0}, tbase[kDevDynTerms] = {0, 0, 0, 0};
-    uint64_t adom[kDevDynTerms] = {0, 0, 0, 0};
+    uint64_t adom[kDevDynTerms][G];
+#pragma unroll
+    for (int i = 0; i < kDevDynTerms; ++i)
+#pragma unroll
+      for (int g = 0; g < G; ++g) adom[i][g] = 0;
     if (meta != ~0ull) {
       const int set = static_cast<int>(meta >> 1);
       const bool self = (meta & 1) != 0;
@@ -1414,13 +1439,21 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
         if (i >= nt) continue;
         tslot[i] = si[2 + 2 * i];
         tbase[i] = si[3 + 2 * i];
-        int d = -1;
+        const bool table = dk_row_of(w, tslot[i]) >= 0;
+        uint64_t bits = 0;
 #pragma unroll
-        for (int kk = 0; kk < kDevDomKeys; ++kk) d = kk == tslot[i] ? pdom[kk] : d;
-        const bool in = mine && ((mm >> lane) & 1) && d >= 0;
-        const uint64_t b = ballot(in);
-        map_has = map_has || b != 0;
-        adom[i] = dk_row_of(w, tslot[i]) >= 0 ? wave_or(in ? 1ull << d : 0ull) : b;
+        for (int g = 0; g < G; ++g) {
+          const uint64_t mm = dr[4 * kDevDynG + g];
+          int d = -1;
+#pragma unroll
+          for (int kk = 0; kk < kDevDomKeys; ++kk) d = kk == tslot[i] ? pdom[g][kk] : d;
+          const bool in = 64 * g + lane < k && ((mm >> lane) & 1) && d >= 0;
+          const uint64_t b = ballot(in);
+          map_has = map_has || b != 0;
+          bits |= in ? 1ull << d : 0ull;
+          adom[i][g] = table ? 0ull : b;
+        }
+        if (table) adom[i][0] = wave_or(bits);
       }
       if (!map_has && self) nt = 0;  // first pod of a self-affine group: KEYS(S) (in its class) only
     }
@@ -1450,17 +1483,25 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
         if (i >= nt) continue;
         uint64_t row = at[static_cast<size_t>(tbase[i]) * Wp + wi];
         nbytes += 64u * 8u;
-        uint64_t m = adom[i];
         const int row0 = dk_row_of(w, tslot[i]);
-        while (m != 0) {
-          const int x = __builtin_ctzll(m);
-          m &= m - 1;
-          if (row0 >= 0) {  // domain x of a table key
+        if (row0 >= 0) {  // domains of a table key
+          uint64_t m = adom[i][0];
+          while (m != 0) {
+            const int x = __builtin_ctzll(m);
+            m &= m - 1;
             row |= at[static_cast<size_t>(row0 + x) * Wp + wi];
             nbytes += 64u * 8u;
-          } else {  // pod x's node (node-local key)
-            const int y = __builtin_amdgcn_readlane(pnode, x);
-            if ((y >> 6) == wd) row |= 1ull << (y & 63);
+          }
+        } else {  // the matching pods' nodes (node-local key)
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            uint64_t m = adom[i][g];
+            while (m != 0) {
+              const int x = __builtin_ctzll(m);
+              m &= m - 1;
+              const int y = __builtin_amdgcn_readlane(pnode[g], x);
+              if ((y >> 6) == wd) row |= 1ull << (y & 63);
+            }
           }
         }
         dyn &= row;
@@ -1475,42 +1516,55 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
       }
       // touched nodes of this chunk below cn: S and dynamic bit from the word's
       // lane, the rest from the candidate's copy of the node
-      const bool in = snode >= ch * 4096 && snode < min(cn, (ch + 1) * 4096);
-      const int src = in ? (snode >> 6) - ch * 64 : 0;
-      const uint64_t ws = (static_cast<uint64_t>(from_lane(static_cast<uint32_t>(sd >> 32), src)) << 32) |
-                          from_lane(static_cast<uint32_t>(sd), src);
-      const bool fit = zero | ((rc <= scpu) & (rm <= smem) & (re <= seph));
-      const bool ok = in & (((ws >> (snode & 63)) & 1ull) != 0) & (sleft >= 1) & ((sport & pin) == 0) & fit;
-      ans = min(cn, wave_min(ok ? snode : INT_MAX));
+      int best = INT_MAX;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const bool in = snode[g] >= ch * 4096 && snode[g] < min(cn, (ch + 1) * 4096);
+        const int src = in ? (snode[g] >> 6) - ch * 64 : 0;
+        const uint64_t ws = (static_cast<uint64_t>(from_lane(static_cast<uint32_t>(sd >> 32), src)) << 32) |
+                            from_lane(static_cast<uint32_t>(sd), src);
+        const bool fit = zero | ((rc <= scpu[g]) & (rm <= smem[g]) & (re <= seph[g]));
+        const bool ok = in & (((ws >> (snode[g] & 63)) & 1ull) != 0) & (sleft[g] >= 1) & ((sport[g] & pin) == 0) & fit;
+        best = ok ? min(best, snode[g]) : best;
+      }
+      ans = min(cn, wave_min(best));
     }
     if (ans == INT_MAX) {  // "pod %s can't be rescheduled on any existing spot node"
       status = k;
       break;
     }
     // ClusterSnapshot.AddPod on the candidate's copy
-    if (ballot(snode == ans) != 0) {
-      if (snode == ans) {
-        scpu -= rc;
-        smem -= rm;
-        seph -= re;
-        sleft -= 1;
-        sport |= pm;
+    bool hit = false;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (ballot(snode[g] == ans) != 0) {
+        hit = true;
+        if (snode[g] == ans) {
+          scpu[g] -= rc;
+          smem[g] -= rm;
+          seph[g] -= re;
+          sleft[g] -= 1;
+          sport[g] |= pm;
+        }
       }
-    } else {
+    }
+    if (!hit) {
       const uint64_t* rec = w.node_rec + static_cast<size_t>(ans) * 8;
       const int64_t fc = static_cast<int64_t>(rec[0]), fm = static_cast<int64_t>(rec[1]),
                     fe = static_cast<int64_t>(rec[2]);
       const uint64_t pb = rec[3];
       const int pl = static_cast<int>(static_cast<int64_t>(rec[4]));
       nbytes += 40u;
-      if (lane == nslots) {
-        snode = ans;
-        scpu = fc - rc;
-        smem = fm - rm;
-        seph = fe - re;
-        sleft = pl - 1;
-        sport = pb | pm;
-      }
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (lane + 64 * g == nslots) {
+          snode[g] = ans;
+          scpu[g] = fc - rc;
+          smem[g] = fm - rm;
+          seph[g] = fe - re;
+          sleft[g] = pl - 1;
+          sport[g] = pb | pm;
+        }
       ++nslots;
       if (lane == 0) tl[ans >> 6] |= 1ull << (ans & 63);
     }
@@ -1518,13 +1572,19 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
 #pragma unroll
     for (int kk = 0; kk < kDevDomKeys; ++kk)
       dn[kk] = kk < w.n_dk ? w.dk_dom[static_cast<size_t>(kk) * w.n_spot + ans] : -1;
-    if (lane == k) {
-      pnode = ans;
 #pragma unroll
-      for (int kk = 0; kk < kDevDomKeys; ++kk) pdom[kk] = dn[kk];
-    }
+    for (int g = 0; g < G; ++g)
+      if (lane + 64 * g == k) {
+        pnode[g] = ans;
+#pragma unroll
+        for (int kk = 0; kk < kDevDomKeys; ++kk) pdom[g][kk] = dn[kk];
+      }
   }
-  if (lane < np) w.out_node[p0 + lane] = (status < 0 || lane < status) ? pnode : -1;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int kq = 64 * g + lane;
+    if (kq < np) w.out_node[p0 + kq] = (status < 0 || kq < status) ? pnode[g] : -1;
+  }
 }
 
 // K2: one wave per candidate (list entries {candidate, first pod, end pod,
@@ -1627,7 +1687,8 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   const int dbase = w.dyn_cand ? __builtin_amdgcn_readfirstlane(w.dyn_cand[ci]) : -1;
   if (dbase >= 0) {  // writes out_node itself
     wide = 3;
-    k2_domain<CH>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes);
+    if (np <= 64) k2_domain<CH, 1>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes);
+    else k2_domain<CH, kDevDynG>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes);
   } else if (node_order) {  // writes out_node itself
     uint64_t* F = reinterpret_cast<uint64_t*>(&L);
     wide = 2;

@@ -11,7 +11,9 @@ namespace sr {
 
 constexpr int kResultHeader = 8;           // words before the winner's mapping in `result`
 constexpr size_t kK0ProfWaves = 32768;  // K0 waves profiled after K2's [n_cand][16] records
-constexpr int kDevDynU64 = 6;           // domain-path pod record words (host.hpp kDynU64)
+constexpr int kDevDynG = 4;             // domain path: groups of 64 pods (<= 256 pods per candidate)
+constexpr int kDevDynU64 = 5 * kDevDynG + 1;  // domain-path pod record words (host.hpp kDynU64): per key slot
+                                        // kDevDynG mask words, kDevDynG affinity mask words, the set word
 constexpr int kDevDomKeys = 4;          // key slots (host.hpp kDomKeys)
 constexpr int kDevDynTerms = 4;         // terms per domain-path affinity set (host.hpp kDynTerms)
 
@@ -48,8 +50,9 @@ struct DevWorkload {
   // domain path (k2_domain): candidates whose pods interact through shared-domain
   // topology keys (antiaff.cpp); null when the call has none
   const int32_t* dyn_cand;  // [n_cand] first record in dyn_pod, -1: node / pod order
-  const uint64_t* dyn_pod;  // [..][kDynU64] {anti-affinity mask per key slot x4, affinity mask,
-                            //  set << 1 | self or ~0}; masks over the candidate's earlier pods
+  const uint64_t* dyn_pod;  // [..][kDevDynU64] {anti-affinity masks per key slot (4 x kDevDynG words),
+                            //  affinity masks (kDevDynG words), set << 1 | self or ~0}; masks over the
+                            //  candidate's earlier pods, 64 per word
   int32_t n_dk;             // key slots
   const int32_t* dk_dom;    // [n_dk][n_spot] domain of each spot node (node-local key: the node), -1 absent
   int32_t dk_row[4];        // atom of domain 0 per table key slot, -1: node-local key

@@ -111,6 +111,7 @@ void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out, int32_t* k, i
   *out = SnapPod{};
   out->anti = has_anti_terms(c, pod) ? 1 : 0;
   out->opaque = anti_opaque(c, pod) ? 1 : 0;
+  out->term = c->spread ? (c->spread->terminating[pod] ? 1 : 0) : 2;
   const sr_pod_affinity* A = c->pod_affinity;
   if (!A) return;
   out->meta = 1;
@@ -154,6 +155,7 @@ static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod, const
   st.anti += sp.anti;
   st.opaque += sp.opaque;
   st.unknown += sp.meta ? 0 : 1;
+  st.term_unknown += sp.term == 2 ? 1 : 0;
   st.pods.push_back(store);
   for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i)
     if (P.port_num[i] > 0) st.ports.push_back(Port{P.port_ip[i], P.port_proto[i], P.port_num[i]});
@@ -220,6 +222,7 @@ void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t 
   s->opaque_total += sp.opaque;
   s->unknown_total += sp.meta ? 0 : 1;
   s->scalar_unknown_total += !c->pod_scalar_off && (c->pods.flags[pod] & SR_POD_FB_SCALAR_RESOURCES) ? 1 : 0;
+  s->term_unknown_total += sp.term == 2 ? 1 : 0;
   s->version++;
 }
 
@@ -318,6 +321,7 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
     s->opaque_total += s->state[i].opaque;
     s->unknown_total += s->state[i].unknown;
     s->scalar_unknown_total += s->state[i].scalar_unknown;
+    s->term_unknown_total += s->state[i].term_unknown;
   }
   *out = s;
   return SR_OK;
@@ -377,11 +381,13 @@ sr_status sr_snapshot_revert(sr_snapshot* snap) {
   snap->term_words.resize(snap->fork_terms);
   snap->forked = false;
   snap->anti_total = snap->opaque_total = snap->unknown_total = snap->scalar_unknown_total = 0;
+  snap->term_unknown_total = 0;
   for (const auto& st : snap->state) {
     snap->anti_total += st.anti;
     snap->opaque_total += st.opaque;
     snap->unknown_total += st.unknown;
     snap->scalar_unknown_total += st.scalar_unknown;
+    snap->term_unknown_total += st.term_unknown;
   }
   snap->version++;
   return SR_OK;

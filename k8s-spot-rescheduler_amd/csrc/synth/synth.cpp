@@ -428,6 +428,7 @@ void sr_synth_view(const sr_synth* s, sr_cluster* c) {
   c->pod_scalar_name = c->node_scalar_name = nullptr;
   c->pod_scalar_req = c->pod_scalar_acc = c->node_scalar_alloc = nullptr;
   c->acc_milli_cpu = c->acc_memory = c->acc_ephemeral = nullptr;  // AddPod adds the fit request
+  c->spread = nullptr;  // no topology spread constraints in the BASELINE configs
 }
 
 void sr_synth_drain(const sr_synth* s, sr_pod_drain* d) {

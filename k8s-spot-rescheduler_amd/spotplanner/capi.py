@@ -68,6 +68,12 @@ class sr_pod_affinity(ctypes.Structure):
                 ("me_op", P32), ("me_val_off", P32), ("me_vals", P32), ("aff_off", P32)]
 
 
+class sr_spread(ctypes.Structure):
+    _fields_ = [("off", P32), ("max_skew", P32), ("topology_key", P32), ("selector_nil", PU8),
+                ("ml_off", P32), ("ml_key", P32), ("ml_val", P32), ("me_off", P32), ("me_key", P32),
+                ("me_op", P32), ("me_val_off", P32), ("me_vals", P32), ("terminating", PU8)]
+
+
 class sr_cluster(ctypes.Structure):
     _fields_ = [("nodes", sr_nodes), ("pods", sr_pods), ("id_empty", ctypes.c_int32),
                 ("id_metadata_name", ctypes.c_int32), ("id_unschedulable_key", ctypes.c_int32),
@@ -76,7 +82,8 @@ class sr_cluster(ctypes.Structure):
                 ("str_label", ctypes.POINTER(ctypes.c_uint8)),
                 ("pod_scalar_off", P32), ("pod_scalar_name", P32), ("pod_scalar_req", P64), ("pod_scalar_acc", P64),
                 ("node_scalar_off", P32), ("node_scalar_name", P32), ("node_scalar_alloc", P64),
-                ("acc_milli_cpu", P64), ("acc_memory", P64), ("acc_ephemeral", P64)]
+                ("acc_milli_cpu", P64), ("acc_memory", P64), ("acc_ephemeral", P64),
+                ("spread", ctypes.POINTER(sr_spread))]
 
 
 class sr_node_label(ctypes.Structure):
@@ -190,6 +197,15 @@ def make_cluster_struct(A) -> sr_cluster:
         c.acc_milli_cpu = ptr(A["acc_cpu"], P64)
         c.acc_memory = ptr(A["acc_mem"], P64)
         c.acc_ephemeral = ptr(A["acc_eph"], P64)
+    if A.get("ts_off") is not None:
+        ts = sr_spread()
+        for f in ("off", "max_skew", "topology_key", "ml_off", "ml_key", "ml_val", "me_off", "me_key", "me_op",
+                  "me_val_off", "me_vals"):
+            setattr(ts, f, ptr(A["ts_" + f], P32))
+        ts.selector_nil = ptr(A["ts_selector_nil"], PU8)
+        ts.terminating = ptr(A["ts_terminating"], PU8)
+        c._spread = ts  # keeps the struct alive as long as the cluster struct
+        c.spread = ctypes.pointer(ts)
     if A.get("pa_ns") is not None:
         pa = sr_pod_affinity()
         for f in ("ns", "label_off", "label_key", "label_val", "anti_off", "topology_key", "ns_off", "ns_ids",

@@ -98,6 +98,14 @@ class PodAffinityTerm:
 
 
 @dataclass
+class TopologySpreadConstraint:
+    max_skew: int
+    topology_key: str
+    when_unsatisfiable: str = "DoNotSchedule"   # ScheduleAnyway never filters
+    label_selector: Optional[LabelSelector] = None  # None = nil: matches nothing
+
+
+@dataclass
 class OwnerReference:
     kind: str
     name: str = ""
@@ -129,7 +137,9 @@ class Pod:
     pod_anti_affinity: Optional[List[PodAffinityTerm]] = None
     # Affinity.PodAffinity.RequiredDuringSchedulingIgnoredDuringExecution (encoded)
     pod_affinity: Optional[List[PodAffinityTerm]] = None
-    hard_topology_spread: bool = False
+    hard_topology_spread: bool = False  # opaque DoNotSchedule spread (no constraints given): fallback
+    # Spec.TopologySpreadConstraints (encoded)
+    topology_spread: List[TopologySpreadConstraint] = field(default_factory=list)
     # drain attributes (cluster-autoscaler utils/drain)
     phase: str = "Running"                    # Status.Phase
     restart_policy: str = "Always"            # Spec.RestartPolicy
@@ -263,7 +273,7 @@ def _daemonset_owner_walk(pod: Pod):
     return False, False
 
 
-def pod_flags(pod: Pod, scalar_tables: bool = True) -> int:
+def pod_flags(pod: Pod, scalar_tables: bool = True, spread_tables: bool = True) -> int:
     f = 0
     if _daemonset_owner_walk(pod)[0]:
         f |= capi.SR_POD_DAEMONSET_CONTROLLER
@@ -276,7 +286,8 @@ def pod_flags(pod: Pod, scalar_tables: bool = True) -> int:
         f |= capi.SR_POD_FB_SCALAR_RESOURCES
     if pod.has_pvc:
         f |= capi.SR_POD_FB_VOLUMES
-    if pod.hard_topology_spread:
+    if pod.hard_topology_spread or (not spread_tables and any(c.when_unsatisfiable == "DoNotSchedule"
+                                                              for c in pod.topology_spread)):
         f |= capi.SR_POD_FB_TOPOLOGY_SPREAD
     if pod.required_pod_affinity or (pod.required_pod_anti_affinity and not pod.pod_anti_affinity):
         f |= capi.SR_POD_FB_POD_AFFINITY
@@ -396,9 +407,40 @@ def _encode_pod_affinity(pods: List[Pod], it: Interner) -> dict:
                 pa_me_vals=_i32(mev), pa_aff_off=_i32(fo))
 
 
+def _encode_spread(pods: List[Pod], it: Interner) -> dict:
+    """sr_spread arrays: the DoNotSchedule constraints of every pod."""
+    off, skew, tk, nil, mlo, mlk, mlv, meo, mek, mep, mevo, mev, term = \
+        [0], [], [], [], [0], [], [], [0], [], [], [0], [], []
+    for p in pods:
+        for c in p.topology_spread:
+            if c.when_unsatisfiable != "DoNotSchedule":
+                continue
+            skew.append(c.max_skew)
+            tk.append(it.id(c.topology_key))
+            sel = c.label_selector
+            nil.append(1 if sel is None else 0)
+            for k, v in (sel.match_labels.items() if sel else []):
+                mlk.append(it.id(k))
+                mlv.append(it.id(v))
+            mlo.append(len(mlk))
+            for r in (sel.match_expressions if sel else []):
+                mek.append(it.id(r.key))
+                mep.append(SEL_OPS.get(r.operator, capi.SR_OP_OTHER) if r.operator not in ("Gt", "Lt")
+                           else capi.SR_OP_OTHER)
+                mev.extend(it.id(v) for v in r.values)
+                mevo.append(len(mev))
+            meo.append(len(mek))
+        off.append(len(skew))
+        term.append(1 if p.deletion_age_s is not None else 0)
+    return dict(ts_off=_i32(off), ts_max_skew=_i32(skew), ts_topology_key=_i32(tk), ts_selector_nil=_u8(nil),
+                ts_ml_off=_i32(mlo), ts_ml_key=_i32(mlk), ts_ml_val=_i32(mlv), ts_me_off=_i32(meo),
+                ts_me_key=_i32(mek), ts_me_op=_i32(mep), ts_me_val_off=_i32(mevo), ts_me_vals=_i32(mev),
+                ts_terminating=_u8(term))
+
+
 def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Interner] = None,
                    pod_node: Optional[List[int]] = None, scalar_tables: bool = True,
-                   accounting: bool = True) -> EncodedCluster:
+                   accounting: bool = True, spread_tables: bool = True) -> EncodedCluster:
     """Encode nodes and pods.  pod_node[i] is the node index of pods[i] (default:
     looked up by pod.node_name; -1 when unbound).  Pods of one node keep their
     relative order (= the per-node LIST order).  scalar_tables=False: no scalar
@@ -451,7 +493,7 @@ def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Intern
         re.append(eph)
         hp.append(0 if p.priority is None else 1)
         pr.append(0 if p.priority is None else p.priority)
-        fl.append(pod_flags(p, scalar_tables))
+        fl.append(pod_flags(p, scalar_tables, spread_tables))
         for k, v in p.node_selector.items():
             sk.append(it.id(k))
             sv.append(it.id(v))
@@ -492,6 +534,8 @@ def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Intern
              tol_eff=_i32(tole), port_off=_i32(po), port_proto=_i32(pp), port_num=_i32(pnum),
              port_ip=_i32(pip))
     A.update(_encode_pod_affinity(pods, it))
+    if spread_tables:
+        A.update(_encode_spread(pods, it))
     if scalar_tables:
         so_, sn_, sr_, sa_ = [0], [], [], []
         for p in pods:

@@ -1002,6 +1002,132 @@ static int o_pod_affinity_ok(const o_state *st, const int32_t *node, int32_t n, 
   return 1;
 }
 
+/* ---- PodTopologySpread (DoNotSchedule) [upstream k8s v1.19.2
+ * plugins/podtopologyspread/filtering.go]. */
+
+/* labels.Selector.Matches of constraint k's selector over a pod's labels. */
+static int o_spread_sel(const sr_cluster *c, int32_t k, int32_t pod) {
+  const sr_spread *S = c->spread;
+  if (S->selector_nil[k]) return 0; /* LabelSelectorAsSelector(nil) = labels.Nothing() */
+  for (int32_t i = S->ml_off[k]; i < S->ml_off[k + 1]; i++) {
+    int32_t v;
+    if (!o_pod_label(c, pod, S->ml_key[i], &v) || v != S->ml_val[i]) return 0;
+  }
+  for (int32_t e = S->me_off[k]; e < S->me_off[k + 1]; e++) {
+    int32_t v;
+    int has = o_pod_label(c, pod, S->me_key[e], &v), ok;
+    int32_t lo = S->me_val_off[e], hi = S->me_val_off[e + 1];
+    switch (S->me_op[e]) {
+      case SR_OP_IN: ok = has && o_in_values(S->me_vals, lo, hi, v); break;
+      case SR_OP_NOT_IN: ok = !has || !o_in_values(S->me_vals, lo, hi, v); break;
+      case SR_OP_EXISTS: ok = has; break;
+      case SR_OP_DOES_NOT_EXIST: ok = !has; break;
+      default: ok = 0; break;
+    }
+    if (!ok) return 0;
+  }
+  return 1;
+}
+
+/* filterTopologySpreadConstraints -> metav1.LabelSelectorAsSelector: a
+ * constraint selector that fails to build (NewRequirement's rules). */
+static int o_spread_invalid(const sr_cluster *c, int32_t k) {
+  const sr_spread *S = c->spread;
+  if (S->selector_nil[k]) return 0;
+  for (int32_t i = S->ml_off[k]; i < S->ml_off[k + 1]; i++)
+    if (!o_req_strings_ok(c, S->ml_key[i], S->ml_val, i, i + 1)) return 1;
+  for (int32_t e = S->me_off[k]; e < S->me_off[k + 1]; e++) {
+    int32_t nv = S->me_val_off[e + 1] - S->me_val_off[e], op = S->me_op[e];
+    if (!o_req_strings_ok(c, S->me_key[e], S->me_vals, S->me_val_off[e], S->me_val_off[e + 1])) return 1;
+    if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) return 1;
+    if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) return 1;
+    if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST) return 1;
+  }
+  return 0;
+}
+
+static int o_affinity_ok(const sr_cluster *c, int32_t pod, int32_t node);
+
+/* node.Labels[key] with Go's zero value: "" when the key is absent. */
+static int32_t o_label_or_empty(const sr_cluster *c, int32_t node, int32_t key) {
+  int32_t v;
+  return o_node_label(c, node, key, &v) ? v : c->id_empty;
+}
+
+/* PreFilter (calPreFilterState) + Filter for `pod` on snapshot position `pos`:
+ * the pairs (topology key, value) of the nodes passing the pod's nodeSelector
+ * / required affinity and carrying every constraint's key; per pair the
+ * matching pods (the pod's namespace, not terminating, the constraint's
+ * selector) on every node whose value of that key is the pair's -- counted
+ * into the pair itself, so two constraints on one key share their pairs'
+ * counts, as TpPairToMatchNum does; min per key over its pairs. */
+static int o_spread_ok(const o_state *st, const int32_t *node, int32_t n, const sr_cluster *c, int32_t pod,
+                       int32_t pos) {
+  const sr_spread *S = c->spread;
+  if (!S || S->off[pod] == S->off[pod + 1]) return 1;
+  const sr_pod_affinity *A = c->pod_affinity;
+  int32_t k0 = S->off[pod], k1 = S->off[pod + 1], nk = k1 - k0;
+  if (nk > 16) return 0; /* never reached: the shim's constraints per pod are few */
+  /* pairs: up to one per distinct (key, value) over the map nodes */
+  int32_t cap = n * nk + 1, np_ = 0;
+  int32_t *pkey = (int32_t *)malloc(sizeof(int32_t) * (size_t)cap);
+  int32_t *pval = (int32_t *)malloc(sizeof(int32_t) * (size_t)cap);
+  int64_t *pcnt = (int64_t *)malloc(sizeof(int64_t) * (size_t)cap);
+  for (int32_t m = 0; m < n; m++) {
+    if (!o_affinity_ok(c, pod, node[m])) continue;
+    int all = 1;
+    for (int32_t k = k0; k < k1 && all; k++) {
+      int32_t v;
+      all = o_node_label(c, node[m], S->topology_key[k], &v);
+    }
+    if (!all) continue;
+    for (int32_t k = k0; k < k1; k++) {
+      int32_t key = S->topology_key[k], v = o_label_or_empty(c, node[m], key), found = 0;
+      for (int32_t q = 0; q < np_ && !found; q++) found = pkey[q] == key && pval[q] == v;
+      if (!found) {
+        pkey[np_] = key;
+        pval[np_] = v;
+        pcnt[np_] = 0;
+        np_++;
+      }
+    }
+  }
+  int ok = 1;
+  if (np_ > 0) {
+    /* processNode: every node, every constraint, the pair of the node's value */
+    for (int32_t m = 0; m < n; m++)
+      for (int32_t k = k0; k < k1; k++) {
+        int32_t key = S->topology_key[k], v = o_label_or_empty(c, node[m], key), q = 0;
+        while (q < np_ && !(pkey[q] == key && pval[q] == v)) q++;
+        if (q == np_) continue;
+        for (int32_t j = 0; j < st[m].nlist; j++) {
+          int32_t e = st[m].list[j];
+          if (S->terminating[e] || A->ns[e] != A->ns[pod]) continue;
+          if (o_spread_sel(c, k, e)) pcnt[q]++;
+        }
+      }
+    for (int32_t k = k0; k < k1 && ok; k++) {
+      int32_t key = S->topology_key[k], v;
+      if (!o_node_label(c, node[pos], key, &v)) {
+        ok = 0; /* the node lacks the key: UnschedulableAndUnresolvable */
+        break;
+      }
+      int64_t minc = INT64_MAX, match = 0;
+      for (int32_t q = 0; q < np_; q++)
+        if (pkey[q] == key) {
+          if (pcnt[q] < minc) minc = pcnt[q];
+          if (pval[q] == v) match = pcnt[q];
+        }
+      int64_t self = o_spread_sel(c, k, pod);
+      if (match + self - minc > S->max_skew[k]) ok = 0;
+    }
+  }
+  free(pkey);
+  free(pval);
+  free(pcnt);
+  return ok;
+}
+
 int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c, int32_t pod) {
   const sr_pods *P = &c->pods;
   if (P->flags[pod] & SR_POD_FB_MASK) return 1;
@@ -1011,6 +1137,13 @@ int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c,
   if (o_has_scalars(c, pod) &&
       ((P->req_milli_cpu[pod] == 0 && P->req_memory[pod] == 0 && P->req_ephemeral[pod] == 0) || s->sc_unknown_total > 0))
     return 1;
+  /* topology spread constraints the planner cannot read: no pod metadata or
+   * validation table, or a selector that fails to build (PreFilter errors) */
+  if (c->spread && c->spread->off[pod + 1] > c->spread->off[pod]) {
+    if (!c->pod_affinity || !c->str_label) return 1;
+    for (int32_t k = c->spread->off[pod]; k < c->spread->off[pod + 1]; k++)
+      if (o_spread_invalid(c, k)) return 1;
+  }
   /* an existing pod's required anti-affinity may select the incoming pod:
    * opaque terms (o_anti_opaque) keep every pod on the fallback path */
   if (s->opaque_total > 0 || o_anti_opaque(c, pod) || o_aff_opaque(c, pod)) return 1;
@@ -1032,6 +1165,7 @@ static int o_check(const oracle_snapshot *s, const o_state *st, const int32_t *n
   if (!o_ports_ok(sp, c, pod)) return 0;
   if (!o_affinity_ok(c, pod, nd)) return 0;
   if (!o_taints_ok(c, pod, nd)) return 0;
+  if (!o_spread_ok(st, node, n, c, pod, pos)) return 0;
   if (!o_interpod_ok(st, node, n, c, pod, nd)) return 0;
   if (!o_pod_affinity_ok(st, node, n, c, pod, nd)) return 0;
   return 1;
@@ -1129,6 +1263,16 @@ static int o_cand_fallback(const oracle_snapshot *s, const sr_cluster *c, const 
     if (o_acc(c, pods[i], 0) != P->req_milli_cpu[pods[i]] || o_acc(c, pods[i], 1) != P->req_memory[pods[i]] ||
         o_acc(c, pods[i], 2) != P->req_ephemeral[pods[i]])
       return 1;
+  /* a pod whose spread constraint selects an earlier pod of the candidate (same
+   * namespace, not terminating): its counts change while the candidate is
+   * planned -- outside the encoded set */
+  if (c->spread && c->pod_affinity)
+    for (int32_t i = 1; i < np; i++)
+      for (int32_t k = c->spread->off[pods[i]]; k < c->spread->off[pods[i] + 1]; k++)
+        for (int32_t j = 0; j < i; j++)
+          if (!c->spread->terminating[pods[j]] && c->pod_affinity->ns[pods[j]] == c->pod_affinity->ns[pods[i]] &&
+              o_spread_sel(c, k, pods[j]))
+            return 1;
   /* two pods of the candidate listing one scalar resource (the later one sees
    * the earlier one's AddPod): outside the encoded set */
   if (c->pod_scalar_off) {

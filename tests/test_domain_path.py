@@ -73,10 +73,44 @@ def test_gpu_random_shared_key_plans(checker, seed):
 
 @pytest.mark.gpu
 def test_gpu_domain_path_limit_falls_back(checker):
-    """More than 64 pods interacting across nodes: the candidate takes the
-    fallback path (kDynPods); a 64-pod one is still planned."""
+    """Up to 256 pods interacting across nodes are planned on the device
+    (4 groups of 64 lanes); a 257-pod candidate takes the fallback path
+    (kDynPods).  The oracle plans every one of them."""
     from domain_cases import pod, term
     from test_gpu_parity import run_scenario
-    big = [[pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(64)] + [pod("d", "db")],
+    big = [[pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(256)] + [pod("d", "db")],
+           [pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(255)] + [pod("d", "db")],
+           [pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(64)] + [pod("d", "db")],
            [pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(63)] + [pod("d", "db")]]
-    run_scenario(checker, nodes(), [[] for _ in range(4)], big, extra_fallback=lambda c: c == 0)
+    _, o, p = run_scenario(checker, nodes(), [[] for _ in range(4)], big, extra_fallback=lambda c: c == 0)
+    assert [int(x) for x in p.status[1:]] == [int(x) for x in o["status"][1:]]
+    assert int(p.status[0]) == capi.SR_CAND_FALLBACK
+
+
+def _strip_init(cands):
+    # init containers make AddPod's accounting differ from the fit request:
+    # such a pod followed by others sends its candidate to the fallback path
+    for c in cands:
+        for p in c:
+            p.init_containers = []
+            for ct in p.containers:
+                ct.scalar = {}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_large_shared_key_candidates(checker, seed):
+    """65-200 pods per candidate interacting through zone / team anti-affinity
+    (and affinity on half the seeds): the domain path with 2-4 pod groups,
+    bit-exact with the oracle and without fallback."""
+    from test_gpu_parity import run_scenario
+    nodes_, spot_pods, cands = rand_scenario(7400 + seed, n_spot=24 + 4 * seed, n_cand=3, max_pods=200,
+                                             features=False, anti=0.2, aff=0.15 if seed % 2 else 0.0,
+                                             shared_keys=True, valid_selectors=True)
+    _strip_init(cands)
+    for i, c in enumerate(cands):  # 65 .. 200 pods each
+        while len(c) < 65 + 45 * i:
+            c.extend(cands[(i + 1) % 3][:65 + 45 * i - len(c)] or [c[0]])
+    _, o, p = run_scenario(checker, nodes_, spot_pods, cands)
+    assert all(int(s) != capi.SR_CAND_FALLBACK for s in o["status"])
+    assert any(anti_interacts_off_node(nodes_, c) or aff_interacts(c) for c in cands)

@@ -30,7 +30,7 @@ def main():
     kinds = {}
     try:
         while time.time() - t0 < a.seconds:
-            k = seed % 7
+            k = seed % 9
             if k == 0:
                 args = dict(n_spot=5 + seed % 60, n_cand=12, max_pods=4 + seed % 30)
             elif k == 1:
@@ -45,9 +45,31 @@ def main():
                 args = dict(n_spot=10 + seed % 40, n_cand=6, max_pods=70 + seed % 200, features=seed % 2 == 0)
             elif k == 5:
                 args = dict(n_spot=4100 + seed % 3000, n_cand=6, max_pods=20)
-            else:
+            elif k == 6:
                 args = dict(n_spot=20, n_cand=12, max_pods=8, fallback=True)
+            elif k == 7:  # the domain path with 2-4 pod groups (65-230 interacting pods)
+                args = dict(n_spot=20 + seed % 30, n_cand=3, max_pods=65 + seed % 165, features=False, anti=0.2,
+                            aff=0.15 if seed % 2 else 0.0, shared_keys=True, valid_selectors=True)
+            else:  # scalar resources on most nodes and candidates
+                args = dict(n_spot=6 + seed % 20, n_cand=12, max_pods=4 + seed % 8)
             nodes, spot_pods, cands = rand_scenario(seed, **args)
+            if k == 7:
+                for c in cands:  # no init containers / scalars: nothing sends them to the fallback path
+                    for p in c:
+                        p.init_containers = []
+                        for ct in p.containers:
+                            ct.scalar = {}
+            if k == 8:
+                import random
+                r = random.Random(seed)
+                for nd in nodes:
+                    if r.random() < 0.7:
+                        nd.scalar = {"nvidia.com/gpu": r.choice([0, 1, 2, 4]), "hugepages-2Mi": r.choice([0, 4 << 20])}
+                for c in cands:
+                    if c and r.random() < 0.7:
+                        p = c[r.randrange(len(c))]
+                        p.containers[0].scalar = {"nvidia.com/gpu": r.choice([0, 1, 2])}
+                        p.containers[0].cpu_milli = max(p.containers[0].cpu_milli, 10)
             P.run_scenario(c, nodes, spot_pods, cands)
             kinds[k] = kinds.get(k, 0) + 1
             n += 1
@@ -55,7 +77,7 @@ def main():
             if n % 25 == 0:
                 print("  %d scenarios, %.0f s" % (n, time.time() - t0), flush=True)
     except Exception:
-        print("MISMATCH at seed %d kind %d" % (seed, seed % 7))
+        print("MISMATCH at seed %d kind %d" % (seed, seed % 9))
         traceback.print_exc()
         return 1
     finally:
