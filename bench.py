@@ -56,10 +56,22 @@ WORKLOAD = {1: "C1 rescheduler_test-style 20 nodes / 200 pods",
 E2E_IDLE = os.environ.get("SR_BENCH_E2E_IDLE", "1") != "0"
 
 
+def latest_profile(name):
+    """profiles/rNN/<name> of the newest round that has it, or None."""
+    base = os.path.join(REPO, "profiles")
+    rounds = sorted((d for d in os.listdir(base) if d.startswith("r") and d[1:].isdigit()), reverse=True) \
+        if os.path.isdir(base) else []
+    for d in rounds:
+        p = os.path.join(base, d, name)
+        if os.path.exists(p):
+            return p
+    return None
+
+
 def k2_chain_summary(path):
     """K2's chain costs from the committed per-wave profile of this config
     (tools/k2_profile.py output, SR_K2_PROFILE run of the same build), or None."""
-    if not os.path.exists(path):
+    if path is None or not os.path.exists(path):
         return None
     out = {"source": os.path.relpath(path, REPO)}
     lines = open(path).read().splitlines()
@@ -481,7 +493,7 @@ def main():
             traffic_src = {"file": os.path.relpath(pmc, REPO), "measured_at_head": pj.get("measured_at_head", "unknown"),
                            "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench command "
                                   "(tools/gpu_round.sh); not measured in this run"}
-        chain = k2_chain_summary(os.path.join(REPO, "profiles", "r02", "c%d_k2_wave_profile.txt" % args.config))
+        chain = k2_chain_summary(latest_profile("c%d_k2_wave_profile.txt" % args.config))
         line = {
             "metric": "reference-equivalent pod x spot-node feasibility checks/s (drain-plan latency = ms_per_step)",
             "value": total_issued / elapsed * args.steps if elapsed > 0 else 0.0,
