@@ -506,6 +506,196 @@ void build_req_row(const EncoderCache& C, const sr_snapshot* snap, const sr_clus
   }
 }
 
+// The NodeAffinity row of a pod (nodeSelector AND, OR of the required
+// terms), from its drafted spec's requirements over the static view.
+void pod_affinity_row(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* c, int32_t pod,
+                      std::vector<uint64_t>& out) {
+  SpecDraft d;
+  draft_spec(c, pod, &d);
+  const int32_t Wp = C.Wp, n_spot = C.n_spot;
+  out.assign(static_cast<size_t>(Wp), 0);
+  if (d.flags & CLS_IMPOSSIBLE) return;
+  for (int32_t n = 0; n < n_spot; ++n) out[n >> 6] |= 1ull << (n & 63);
+  std::vector<uint64_t> r;
+  auto group_row = [&](const int32_t* g) {  // {len, type, key, op, vals...}
+    const int32_t* rw = g + 1;
+    build_req_row(C, snap, c, rw, static_cast<size_t>(g[0]), rw[0] != REQ_FIELD ? &label_column(C, snap, rw[1]) : nullptr,
+                  r);
+  };
+  for (size_t i = 0; i < d.sel.size(); i += 1 + static_cast<size_t>(d.sel[i])) {
+    group_row(&d.sel[i]);
+    for (int32_t x = 0; x < Wp; ++x) out[x] &= r[x];
+  }
+  if (!(d.flags & CLS_AFF_REQUIRED)) return;
+  std::vector<uint64_t> any(static_cast<size_t>(Wp), 0), t(static_cast<size_t>(Wp));
+  for (size_t i = 0; i < d.terms.size();) {
+    const int32_t ng = d.terms[i++];
+    std::fill(t.begin(), t.end(), ~0ull);
+    for (int32_t q = 0; q < ng; ++q) {
+      group_row(&d.terms[i]);
+      for (int32_t x = 0; x < Wp; ++x) t[x] &= r[x];
+      i += 1 + static_cast<size_t>(d.terms[i]);
+    }
+    for (int32_t x = 0; x < Wp; ++x) any[x] |= t[x];
+  }
+  for (int32_t x = 0; x < Wp; ++x) out[x] &= any[x];
+}
+
+// Topology spread between the pods of one candidate (SpreadDyn, DESIGN.md
+// §2.9): a pod whose DoNotSchedule constraint counts earlier pods of its
+// candidate (its namespace, not terminating, selected) sends the candidate to
+// the domain path, or to the reference path beyond its limits -- more than
+// kDynPods pods, more than kSpreadSlots such constraints in a pod, another
+// constraint of the pod on the same key, a key without a domain slot, or a
+// node-local key whose minimum could move (no more nodes at the minimum than
+// the constraint counts pods of the candidate).
+void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
+                    std::vector<int32_t>& status, DomKeys* dk, SpreadDyn* out) {
+  SpreadDyn& sd = *out;
+  sd = SpreadDyn{};
+  const sr_spread* S = c->spread;
+  const sr_pod_affinity* A = c->pod_affinity;
+  const int32_t nc = cands->n_cand;
+  if (!S || !A || nc == 0) return;
+  const int32_t base = cands->cand_pod_off[0];
+  sd.base = base;
+  const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
+  auto counted = [&](int32_t k, int32_t pod, int32_t q) {  // earlier pod q counted by pod's constraint k
+    return !S->terminating[q] && A->ns[q] == A->ns[pod] && spread_selects(c, k, q);
+  };
+  std::vector<uint64_t> aff, words;
+  std::vector<int32_t> cnt;
+  for (int32_t i = 0; i < nc; ++i) {
+    if (status[i] != STATUS_PENDING) continue;
+    const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
+    bool any = false;
+    for (int32_t u = b + 1; u < e && !any; ++u) {
+      const int32_t pod = cands->cand_pods[u];
+      for (int32_t k = S->off[pod]; k < S->off[pod + 1] && !any; ++k)
+        for (int32_t t = b; t < u && !any; ++t) any = counted(k, pod, cands->cand_pods[t]);
+    }
+    if (!any) continue;
+    bool fb = e - b > kDynPods;
+    words.assign(static_cast<size_t>(e - b) * kSpreadU64, 0);
+    std::vector<uint8_t> dm(static_cast<size_t>(e - b), 0);
+    const size_t tab0 = sd.tab.size();
+    for (int32_t u = b; u < e && !fb; ++u) {
+      const int32_t pod = cands->cand_pods[u];
+      uint64_t* rec = &words[static_cast<size_t>(u - b) * kSpreadU64];
+      for (int s2 = 0; s2 < kSpreadSlots; ++s2) rec[s2 * (kDynG + 3) + kDynG] = ~0ull;  // slot unused
+      if (S->off[pod + 1] == S->off[pod]) continue;
+      // the pairs: nodes passing the pod's NodeAffinity and carrying every key
+      bool affd = false;
+      int32_t slots = 0;
+      for (int32_t k = S->off[pod]; k < S->off[pod + 1] && !fb; ++k) {
+        uint64_t mk[kDynG] = {0, 0, 0, 0};
+        int32_t n_counted = 0;
+        for (int32_t t = b; t < u; ++t)
+          if (counted(k, pod, cands->cand_pods[t])) {
+            mk[(t - b) >> 6] |= 1ull << ((t - b) & 63);
+            ++n_counted;
+          }
+        if (n_counted == 0) continue;
+        if (!affd) {
+          pod_affinity_row(C, snap, c, pod, aff);
+          for (int32_t k2 = S->off[pod]; k2 < S->off[pod + 1]; ++k2) {
+            const std::vector<int32_t>& col = label_column(C, snap, S->topology_key[k2]);
+            for (int32_t n = 0; n < n_spot; ++n)
+              if (col[n] == INT32_MIN) aff[n >> 6] &= ~(1ull << (n & 63));
+          }
+          affd = true;
+        }
+        bool pairs = false;
+        for (uint64_t x : aff) pairs = pairs || x != 0;
+        if (!pairs) break;  // no pair at all: the filter passes every node (the static row says so)
+        const int32_t key = S->topology_key[k];
+        for (int32_t k2 = S->off[pod]; k2 < S->off[pod + 1]; ++k2)
+          fb = fb || (k2 != k && S->topology_key[k2] == key);  // shared pair counts: not on the device
+        if (fb || slots == kSpreadSlots) {
+          fb = true;
+          break;
+        }
+        const int32_t slot = dk->slot(snap, key);
+        if (slot < 0) {
+          fb = true;
+          break;
+        }
+        const int32_t self = spread_selects(c, k, pod) ? 1 : 0, skew = S->max_skew[k];
+        spread_node_counts(snap, c, k, A->ns[pod], cnt);
+        const std::vector<int32_t>& dom = dk->dom[slot];
+        uint64_t* sw = rec + slots * (kDynG + 3);
+        for (int g = 0; g < kDynG; ++g) sw[g] = mk[g];
+        const uint32_t off = static_cast<uint32_t>(sd.tab.size());
+        if (dk->node_local[slot]) {
+          // the minimum over the pairs and how many nodes hold it
+          int64_t m0 = INT64_MAX, n0 = 0;
+          for (int32_t n = 0; n < n_spot; ++n) {
+            if (!((aff[n >> 6] >> (n & 63)) & 1)) continue;
+            if (cnt[n] < m0) {
+              m0 = cnt[n];
+              n0 = 0;
+            }
+            n0 += cnt[n] == m0 ? 1 : 0;
+          }
+          if (n0 <= n_counted) {
+            fb = true;
+            break;
+          }
+          for (int32_t n = 0; n < n_spot; ++n) {
+            const bool in = (aff[n >> 6] >> (n & 63)) & 1;
+            sd.tab.push_back(in ? static_cast<int32_t>(std::max<int64_t>(INT32_MIN, std::min<int64_t>(
+                                      INT32_MAX - 1, static_cast<int64_t>(skew) - self + m0 - cnt[n])))
+                                : INT32_MAX);
+          }
+          sw[kDynG] = static_cast<uint64_t>(slot) | 1ull << 2 | static_cast<uint64_t>(self) << 3 |
+                      static_cast<uint64_t>(static_cast<uint32_t>(skew)) << 32;
+          sw[kDynG + 1] = off;
+          sw[kDynG + 2] = 0;
+        } else {
+          // pairs by domain; a node lacking the key counts into the pair of ""
+          int32_t edom = -1;
+          for (int32_t n = 0; n < n_spot && edom < 0; ++n) {
+            int32_t v = INT32_MIN;
+            for (const auto& kv : snap->nodes[n].labels)
+              if (kv.first == key) v = kv.second;
+            if (v == snap->id_empty && v != INT32_MIN) edom = dom[n];
+          }
+          uint64_t pm = 0;
+          for (int32_t n = 0; n < n_spot; ++n)
+            if (((aff[n >> 6] >> (n & 63)) & 1) && dom[n] >= 0) pm |= 1ull << dom[n];
+          int64_t bc[kDomMax] = {0};
+          for (int32_t n = 0; n < n_spot; ++n) {
+            const int32_t d = dom[n] >= 0 ? dom[n] : edom;
+            if (d >= 0 && ((pm >> d) & 1)) bc[d] += cnt[n];
+          }
+          for (int32_t d = 0; d < kDomMax; ++d)
+            sd.tab.push_back(static_cast<int32_t>(std::min<int64_t>(bc[d], INT32_MAX / 4)));
+          sw[kDynG] = static_cast<uint64_t>(slot) | static_cast<uint64_t>(self) << 3 |
+                      static_cast<uint64_t>(static_cast<uint32_t>(skew)) << 32;
+          sw[kDynG + 1] = off | static_cast<uint64_t>(static_cast<uint32_t>(edom)) << 32;
+          sw[kDynG + 2] = pm;
+          dm[u - b] |= static_cast<uint8_t>(1u << (k - S->off[pod]));
+        }
+        ++slots;
+      }
+    }
+    if (fb) {
+      status[i] = SR_CAND_FALLBACK;
+      sd.tab.resize(tab0);
+      continue;
+    }
+    if (sd.cand_dyn.empty()) {
+      sd.cand_dyn.assign(static_cast<size_t>(nc), 0);
+      sd.rec.assign(static_cast<size_t>(cands->cand_pod_off[nc] - base) * kSpreadU64, 0);
+      sd.dmask.assign(static_cast<size_t>(cands->cand_pod_off[nc] - base), 0);
+    }
+    sd.cand_dyn[i] = 1;
+    sd.active = true;
+    std::copy(words.begin(), words.end(), sd.rec.begin() + static_cast<size_t>(b - base) * kSpreadU64);
+    std::copy(dm.begin(), dm.end(), sd.dmask.begin() + (b - base));
+  }
+}
+
 }  // namespace
 
 uint64_t node_static_fp(const SpotNode& n, const sr_cluster* c) {
@@ -672,20 +862,6 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
           }
         }
       }
-      if (!fb && c->spread && c->pod_affinity) {
-        // a pod whose spread constraint counts an earlier pod of its candidate
-        // (same namespace, not terminating): its counts change while the
-        // candidate is planned, the row is against the base snapshot
-        const sr_spread* S = c->spread;
-        for (int32_t j = b + 1; j < e && !fb; ++j) {
-          const int32_t pod = cands->cand_pods[j];
-          for (int32_t k = S->off[pod]; k < S->off[pod + 1] && !fb; ++k)
-            for (int32_t u = b; u < j && !fb; ++u) {
-              const int32_t q = cands->cand_pods[u];
-              fb = !S->terminating[q] && c->pod_affinity->ns[q] == c->pod_affinity->ns[pod] && spread_selects(c, k, q);
-            }
-        }
-      }
       if (fb) w->status_host[i] = SR_CAND_FALLBACK;
       for (int32_t j = b; j < e && !fb && !cand_ports[i]; ++j)
         cand_ports[i] = P.port_off[cands->cand_pods[j]] != P.port_off[cands->cand_pods[j] + 1];
@@ -709,6 +885,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   // candidates whose pods interact through them (antiaff.cpp)
   AffTerms aff;
   analyse_affinity(snap, c, cands, Wp, w->status_host, &dk, &aff);
+  // ---- topology spread between the pods of one candidate (domain path)
+  SpreadDyn sdyn;
+  analyse_spread(C, snap, c, cands, w->status_host, &dk, &sdyn);
+  auto spread_dm = [&](int32_t flat) -> int32_t { return sdyn.dmask.empty() ? 0 : sdyn.dmask[flat - sdyn.base]; };
   // affinity planned on the domain path: the pod's class carries KEYS(S), the
   // device the rest (an earlier pod of its candidate matches all its terms)
   auto aff_dyn = [&](int32_t flat) {
@@ -960,7 +1140,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     }
   C.last_new_specs = static_cast<int32_t>(new_spec_pod.size());
   const int32_t n_spec_ids = spec0 + static_cast<int32_t>(new_spec_pod.size());
-  const bool combos = anti.active || aff.active;
+  const bool combos = anti.active || aff.active || sdyn.active;
   // keys present in this call (pods without inter-pod terms: the spec id),
   // flagged here with the global ids; read first: a shared line written by
   // every thread would bounce
@@ -1019,6 +1199,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   std::vector<int32_t> key_spec;               // keys >= n_spec_ids: spec of the combined key,
   std::vector<std::vector<int32_t>> key_anti;  // ... its anti-affinity term ids
   std::vector<int32_t> key_aff;                // ... and its affinity code (AffTerms::pod_code; 1 << 30: domain path)
+  std::vector<int32_t> key_sdm;                // ... and its device-planned spread constraints (SpreadDyn::dmask)
   if (combos) {
     pod_key_buf.resize(static_cast<size_t>(na));
     WordDict combo;
@@ -1027,20 +1208,23 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       const int32_t j = active_src[q] - anti.base;
       const int32_t n_ids = anti.active ? anti.pod_off[j + 1] - anti.pod_off[j] : 0;
       const int32_t code = aff.active ? aff.pod_code[active_src[q] - aff.base] : -1;
-      if (n_ids == 0 && code < 0) {
+      const int32_t sdm = spread_dm(active_src[q]);
+      if (n_ids == 0 && code < 0 && sdm == 0) {
         pod_key_buf[q] = pod_spec[q];
         continue;
       }
       const int32_t kcode = code < 0 ? code : code | (aff_dyn(active_src[q]) ? 1 << 30 : 0);
       kw.assign(1, pod_spec[q]);
       kw.push_back(kcode);
+      kw.push_back(sdm);
       if (n_ids) kw.insert(kw.end(), anti.pod_ids.begin() + anti.pod_off[j], anti.pod_ids.begin() + anti.pod_off[j + 1]);
       bool ins = false;
       const int32_t id = combo.intern(kw, &ins);
       if (ins) {
         key_spec.push_back(pod_spec[q]);
         key_aff.push_back(kcode);
-        key_anti.emplace_back(kw.begin() + 2, kw.end());
+        key_sdm.push_back(sdm);
+        key_anti.emplace_back(kw.begin() + 3, kw.end());
       }
       pod_key_buf[q] = n_spec_ids + id;
     }
@@ -1100,20 +1284,23 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     if (ins.second) scalar_query.emplace_back(name, req);
     return ins.first->second;
   };
-  // topology spread of this call: one atom per spec carrying constraints
-  std::vector<int32_t> spread_query;
-  std::unordered_map<int32_t, int32_t> spread_index;
-  auto spread_atom_index = [&](int32_t spec_id) {
-    auto ins = spread_index.emplace(spec_id, static_cast<int32_t>(spread_query.size()));
-    if (ins.second) spread_query.push_back(spec_id);
+  // topology spread of this call: one atom per spec carrying constraints and
+  // set of device-planned constraints
+  std::vector<std::pair<int32_t, int32_t>> spread_query;
+  std::unordered_map<int64_t, int32_t> spread_index;
+  auto spread_atom_index = [&](int32_t spec_id, int32_t dm) {
+    auto ins = spread_index.emplace(static_cast<int64_t>(spec_id) << 32 | static_cast<uint32_t>(dm),
+                                    static_cast<int32_t>(spread_query.size()));
+    if (ins.second) spread_query.emplace_back(spec_id, dm);
     return ins.first->second;
   };
+  auto key_dm = [&](int32_t k) { return k < n_spec_ids ? 0 : key_sdm[k - n_spec_ids]; };
   for (int32_t k : keys) {
     const int32_t id = k < n_spec_ids ? k : key_spec[k - n_spec_ids];
     for (uint32_t i = C.spec_req_off[id]; i < C.spec_req_off[id + 1]; ++i) use_req(C.spec_req[i]);
     const std::vector<int64_t>& sc = C.spec[id].scalars;
     for (size_t i = 0; i + 2 <= sc.size(); i += 2) scalar_atom_index(sc[i], sc[i + 1]);
-    if (!C.spec[id].spread.empty()) spread_atom_index(id);
+    if (!C.spec[id].spread.empty()) spread_atom_index(id, key_dm(k));
   }
   const int32_t n_reqs = static_cast<int32_t>(used_reqs.size());
   const int32_t n_ports = static_cast<int32_t>(port_query.size());
@@ -1246,7 +1433,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
     scq.clear();
     for (size_t i = 0; i + 2 <= sp.scalars.size(); i += 2) scq.push_back(scalar_atom_index(sp.scalars[i], sp.scalars[i + 1]));
-    if (!sp.spread.empty()) scq.push_back(n_scalars + spread_atom_index(spec_id));
+    if (!sp.spread.empty()) scq.push_back(n_scalars + spread_atom_index(spec_id, key_dm(k)));
     static_sig(sp, untol, sig);
     const size_t n_static = sig.size();
     sig.push_back(static_cast<int32_t>(scq.size()));
@@ -1411,7 +1598,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   // PodTopologySpread against the base snapshot, over the spec's NodeAffinity
   // row (nodeSelector AND, OR of the required terms) built from its requirement rows
   for (int32_t q = 0; q < n_spreads; ++q) {
-    const SpecInfo& sp = C.spec[spread_query[q]];
+    const SpecInfo& sp = C.spec[spread_query[q].first];
     std::vector<uint64_t> aff_row(static_cast<size_t>(Wp), (sp.flags & CLS_IMPOSSIBLE) ? 0ull : ~0ull);
     for (int32_t r : sp.sel)
       for (int32_t i = 0; i < Wp; ++i) aff_row[i] &= A[static_cast<size_t>(A_REQ + req_atom[r]) * Wp + i];
@@ -1427,7 +1614,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
       for (int32_t x = 0; x < Wp; ++x) aff_row[x] &= any[x];
     }
-    spread_row(snap, sp.spread.data(), aff_row.data(), A + static_cast<size_t>(A_SPREAD + q) * Wp);
+    spread_row(snap, sp.spread.data(), aff_row.data(), static_cast<uint32_t>(spread_query[q].second),
+               A + static_cast<size_t>(A_SPREAD + q) * Wp);
   }
   for (int32_t t = 0; t < anti.n_terms; ++t) {
     std::copy_n(&anti.da[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t) * Wp);
@@ -1456,9 +1644,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     if (term_atom[s2] >= 0)
       std::copy(aff.term_rows[s2].begin(), aff.term_rows[s2].end(), A + static_cast<size_t>(term_atom[s2]) * Wp);
   // domain path: key slots, sets, and the candidates' pod records
-  const bool dyn_any = !anti.cand_dyn.empty() || !aff.cand_dyn.empty();
+  const bool dyn_any = !anti.cand_dyn.empty() || !aff.cand_dyn.empty() || !sdyn.cand_dyn.empty();
   if (dyn_any) {
     w->n_dk = static_cast<int32_t>(dk.key.size());
+    w->sp_tab = sdyn.tab;
     for (const auto& d : dk.dom) w->dk_dom.insert(w->dk_dom.end(), d.begin(), d.end());
     constexpr int32_t kInfo = 2 + 2 * kDynTerms;
     w->ds_info.assign(static_cast<size_t>(std::max(1, aff.n_sets)) * kInfo, 0);
@@ -1476,7 +1665,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     w->dyn_cand.assign(static_cast<size_t>(n_act), -1);
     for (int32_t k = 0; k < n_act; ++k) {
       const int32_t i = w->cand_src[k];
-      const bool dyn = (!anti.cand_dyn.empty() && anti.cand_dyn[i]) || (!aff.cand_dyn.empty() && aff.cand_dyn[i]);
+      const bool dyn = (!anti.cand_dyn.empty() && anti.cand_dyn[i]) || (!aff.cand_dyn.empty() && aff.cand_dyn[i]) ||
+                       (!sdyn.cand_dyn.empty() && sdyn.cand_dyn[i]);
       if (!dyn) continue;
       w->dyn_cand[k] = static_cast<int32_t>(w->dyn_pod.size() / kDynU64);
       for (int32_t q = w->cand_off[k]; q < w->cand_off[k + 1]; ++q) {
@@ -1493,6 +1683,15 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
           w->dyn_pod.push_back(mm);
         }
         w->dyn_pod.push_back(any_mm != 0 ? static_cast<uint64_t>(aff.pod_code[j - aff.base]) : ~0ull);
+        if (!sdyn.cand_dyn.empty() && sdyn.cand_dyn[i]) {
+          const uint64_t* sw = &sdyn.rec[static_cast<size_t>(j - sdyn.base) * kSpreadU64];
+          w->dyn_pod.insert(w->dyn_pod.end(), sw, sw + kSpreadU64);
+        } else {
+          for (int s2 = 0; s2 < kSpreadSlots; ++s2) {
+            for (int g = 0; g < kDynG; ++g) w->dyn_pod.push_back(0);
+            w->dyn_pod.insert(w->dyn_pod.end(), {~0ull, 0ull, 0ull});
+          }
+        }
       }
     }
   }

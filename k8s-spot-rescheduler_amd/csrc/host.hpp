@@ -159,7 +159,10 @@ inline bool has_spread(const sr_cluster* c, int32_t pod) {
 bool spread_invalid(const sr_cluster* c, int32_t k);
 bool spread_selects(const sr_cluster* c, int32_t k, int32_t pod);
 void spread_words(const sr_cluster* c, int32_t pod, std::vector<int32_t>& out);
-void spread_row(const sr_snapshot* snap, const int32_t* words, const uint64_t* aff_row, uint64_t* row);
+// Constraints in `dmask` (bit k: the k-th) keep only their key check (SpreadDyn).
+void spread_row(const sr_snapshot* snap, const int32_t* words, const uint64_t* aff_row, uint32_t dmask, uint64_t* row);
+// Per spot node, the snapshot pods constraint k counts (namespace `ns`, not terminating, selected).
+void spread_node_counts(const sr_snapshot* snap, const sr_cluster* c, int32_t k, int32_t ns, std::vector<int32_t>& out);
 inline bool has_anti_terms(const sr_cluster* c, int32_t pod) {
   return (c->pods.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) ||
          (c->pod_affinity && c->pod_affinity->anti_off[pod + 1] > c->pod_affinity->anti_off[pod]);
@@ -192,7 +195,9 @@ constexpr int kDomMax = 64;   // domains of a table key (one bit each in a 64-bi
 constexpr int kDynTerms = 4;  // terms of an affinity set planned on the domain path
 constexpr int kDynG = 4;      // domain path: mask words per pod set (64 pods each)
 constexpr int kDynPods = 64 * kDynG;  // pods of a candidate planned on the domain path
-constexpr int kDynU64 = 5 * kDynG + 1;  // words per pod record (kernels.hpp)
+constexpr int kSpreadSlots = 2;  // topology spread constraints per pod planned on the domain path
+constexpr int kSpreadU64 = kSpreadSlots * (kDynG + 3);  // their words in the pod record
+constexpr int kDynU64 = 5 * kDynG + 1 + kSpreadU64;  // words per pod record (kernels.hpp)
 
 // The encoded workload of one planning call (host copy; uploaded as one
 // arena).  The spot nodes' state (capacity records, free values) lives in the
@@ -242,7 +247,10 @@ struct Workload {
   std::vector<uint64_t> dyn_pod;  // [pods of those candidates][kDynU64]: anti-affinity masks per
                                   // key slot (earlier pods of the candidate it interacts with),
                                   // affinity mask (earlier pods matching every term of its set),
-                                  // set << 1 | matches its own terms (~0: none)
+                                  // set << 1 | matches its own terms (~0: none), then per spread
+                                  // slot the earlier pods its constraint counts and 3 info words
+                                  // (SpreadDyn)
+  std::vector<int32_t> sp_tab;    // spread base counts per domain / caps per node (SpreadDyn::tab)
   int32_t n_dk = 0;               // key slots in use
   std::vector<int32_t> dk_dom;    // [n_dk][n_spot] domain of each spot node (node-local key: the node), -1 absent
   int32_t dk_row[kDomKeys] = {-1, -1, -1, -1};  // atom of domain 0 of each table key (-1: node-local key)
@@ -260,7 +268,7 @@ struct Workload {
   void reset() {
     t_thr.clear();
     for (auto* v : {&cls_prog_off, &cls_prog, &cls_prog8, &t_dim, &pod_src, &cand_off, &cand_global, &cand_src, &list,
-                    &status_host, &dyn_cand, &dk_dom, &ds_info})
+                    &status_host, &dyn_cand, &dk_dom, &ds_info, &sp_tab})
       v->clear();
     dyn_pod.clear();
     n_dk = 0;
@@ -443,6 +451,31 @@ struct AffTerms {
 // them (status -> SR_CAND_FALLBACK).
 void analyse_affinity(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
                       std::vector<int32_t>& status, DomKeys* dk, AffTerms* out);
+
+// DoNotSchedule topology spread between the pods of one candidate (encode.cpp
+// analyse_spread): a pod whose constraint counts earlier pods
+// of its candidate is planned on the domain path.  Per such constraint (at
+// most kSpreadSlots per pod) the record holds the mask of those earlier pods
+// and three info words:
+//   w0 = key slot | node-local << 2 | selects itself << 3 | maxSkew << 32
+//   w1 = offset in `tab` | domain of the value "" << 32 (-1: none)  [table key]
+//   w2 = the pairs' domains (bit per domain id)                        [table key]
+// Table key: tab[offset + d] = the base count of domain d's pair; the device
+// adds the earlier pods' domains, takes the minimum over the pairs and refuses
+// the domains over maxSkew (the pod's atom keeps only the key check).
+// Node-local key: tab[offset + n] = maxSkew - self + minimum - base count of
+// node n (INT32_MAX off the pairs); the minimum cannot move (more nodes at it
+// than the constraint counts pods in the candidate), so the pod's atom keeps
+// the full base check and the device refuses the nodes whose count of earlier
+// pods exceeds that cap.
+struct SpreadDyn {
+  bool active = false;
+  int32_t base = 0;                // per-pod arrays: flat index - base
+  std::vector<uint8_t> cand_dyn;   // [candidate]
+  std::vector<uint64_t> rec;       // [flat - base][kSpreadU64] (empty: no such candidate)
+  std::vector<uint8_t> dmask;      // [flat - base] bit k: the pod's k-th constraint is a device-planned table key
+  std::vector<int32_t> tab;
+};
 
 // Builds the workload; returns SR_OK or an error with *err filled.  `cache`
 // carries what the previous calls derived (and is updated).

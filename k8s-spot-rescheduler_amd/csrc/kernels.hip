@@ -1418,6 +1418,94 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
       }
       fdom[kk] = any != 0 ? wave_or(bits) : 0ull;
     }
+    // topology spread planned here (SpreadDyn, encode.cpp): the pair counts
+    // with the earlier pods the constraint counts.  Table key: base count per
+    // domain in lane d, plus those pods domain by domain, the minimum over the
+    // pairs, the domains over maxSkew refused (into fdom).  Node-local key:
+    // the nodes where those pods exceed the node's cap (lanes in nlref).
+    uint64_t nlref[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) nlref[g] = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < kDevSpreadSlots; ++s2) {
+      const uint64_t* sw = dr + 5 * kDevDynG + 1 + s2 * (kDevDynG + 3);
+      const uint64_t i0 = sw[kDevDynG];
+      if (i0 == ~0ull) continue;  // wave-uniform
+      const int kk = static_cast<int>(i0 & 3);
+      const bool nl = ((i0 >> 2) & 1) != 0;
+      const int self = static_cast<int>((i0 >> 3) & 1);
+      const int64_t skew = static_cast<int32_t>(static_cast<uint32_t>(i0 >> 32));
+      const uint32_t off = static_cast<uint32_t>(sw[kDevDynG + 1]);
+      uint64_t rem[G];
+      int pd[G];  // the pod's domain of key slot kk
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        rem[g] = sw[g] & ballot(64 * g + lane < k);  // every earlier pod is placed
+        int d = -1;
+#pragma unroll
+        for (int k2 = 0; k2 < kDevDomKeys; ++k2) d = k2 == kk ? pdom[g][k2] : d;
+        pd[g] = d;
+      }
+      nbytes += 8u * (kDevDynG + 3) + 256u;
+      if (!nl) {
+        const int edom = static_cast<int32_t>(static_cast<uint32_t>(sw[kDevDynG + 1] >> 32));
+        const uint64_t pm = sw[kDevDynG + 2];
+#pragma unroll
+        for (int g = 0; g < G; ++g) pd[g] = pd[g] >= 0 ? pd[g] : edom;  // a keyless node: the pair of ""
+        int cv = w.sp_tab[off + lane];
+        for (;;) {  // wave-uniform: one round per distinct domain of the counted pods
+          int gs = -1;
+#pragma unroll
+          for (int g = G - 1; g >= 0; --g) gs = rem[g] != 0 ? g : gs;
+          if (gs < 0) break;
+          int d = 0;
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+            if (g == gs) d = __builtin_amdgcn_readlane(pd[g], __builtin_ctzll(rem[g]));
+          int n = 0;
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const uint64_t same = rem[g] & ballot(pd[g] == d);
+            rem[g] &= ~same;
+            n += __builtin_popcountll(same);
+          }
+          if (d >= 0 && lane == d) cv += n;
+        }
+        const bool inp = ((pm >> lane) & 1) != 0;
+        const int mn = wave_min(inp ? cv : INT_MAX);
+        fdom[kk] |= ballot(inp && static_cast<int64_t>(cv) + self - mn > skew);
+      } else {
+        int capv[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) capv[g] = ((rem[g] >> lane) & 1) ? w.sp_tab[off + static_cast<uint32_t>(pnode[g])] : INT_MAX;
+        for (;;) {  // wave-uniform: one round per distinct node of the counted pods
+          int gs = -1;
+#pragma unroll
+          for (int g = G - 1; g >= 0; --g) gs = rem[g] != 0 ? g : gs;
+          if (gs < 0) break;
+          int y = 0, cap = 0;
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+            if (g == gs) {
+              const int j = __builtin_ctzll(rem[g]);
+              y = __builtin_amdgcn_readlane(pnode[g], j);
+              cap = __builtin_amdgcn_readlane(capv[g], j);
+            }
+          uint64_t same[G];
+          int n = 0;
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            same[g] = rem[g] & ballot(pnode[g] == y);
+            rem[g] &= ~same[g];
+            n += __builtin_popcountll(same[g]);
+          }
+          if (n > cap) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) nlref[g] |= same[g];
+          }
+        }
+      }
+    }
     // affinity: per term its key slot, base row and the earlier matching pods'
     // domains (table key) or pods (node-local key: adom holds their lanes per group)
     const uint64_t meta = dr[5 * kDevDynG];
@@ -1505,6 +1593,16 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
           }
         }
         dyn &= row;
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {  // spread: nodes a node-local constraint refuses
+        uint64_t m = nlref[g];
+        while (m != 0) {
+          const int x = __builtin_ctzll(m);
+          m &= m - 1;
+          const int y = __builtin_amdgcn_readlane(pnode[g], x);
+          if ((y >> 6) == wd) dyn &= ~(1ull << (y & 63));
+        }
       }
       const uint64_t sd = wv ? sv & dyn : 0ull;
       const uint64_t clean = sd & tv & ~tl[wd];

@@ -12,8 +12,11 @@ namespace sr {
 constexpr int kResultHeader = 8;           // words before the winner's mapping in `result`
 constexpr size_t kK0ProfWaves = 32768;  // K0 waves profiled after K2's [n_cand][16] records
 constexpr int kDevDynG = 4;             // domain path: groups of 64 pods (<= 256 pods per candidate)
-constexpr int kDevDynU64 = 5 * kDevDynG + 1;  // domain-path pod record words (host.hpp kDynU64): per key slot
-                                        // kDevDynG mask words, kDevDynG affinity mask words, the set word
+constexpr int kDevSpreadSlots = 2;     // spread constraints per pod on the domain path (host.hpp kSpreadSlots)
+constexpr int kDevDynU64 = 5 * kDevDynG + 1 + kDevSpreadSlots * (kDevDynG + 3);
+                                        // domain-path pod record words (host.hpp kDynU64): per key slot
+                                        // kDevDynG mask words, kDevDynG affinity mask words, the set word,
+                                        // per spread slot kDevDynG mask words and 3 info words (SpreadDyn)
 constexpr int kDevDomKeys = 4;          // key slots (host.hpp kDomKeys)
 constexpr int kDevDynTerms = 4;         // terms per domain-path affinity set (host.hpp kDynTerms)
 
@@ -56,6 +59,7 @@ struct DevWorkload {
   int32_t n_dk;             // key slots
   const int32_t* dk_dom;    // [n_dk][n_spot] domain of each spot node (node-local key: the node), -1 absent
   int32_t dk_row[4];        // atom of domain 0 per table key slot, -1: node-local key
+  const int32_t* sp_tab;    // spread base counts per domain / caps per node (host.hpp SpreadDyn)
   const int32_t* ds_info;   // [set][2 + 2 * 4] {terms, map_empty, (key slot, base-row atom) per term}
   // outputs / scratch
   uint64_t* S;         // [n_classes][Wp] static-class rows, followed by

@@ -248,6 +248,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const bool dyn = !w.dyn_cand.empty();
   const size_t o_dc = dyn ? pk.add(w.dyn_cand) : 0, o_dp = dyn ? pk.add(w.dyn_pod) : 0;
   const size_t o_dd = dyn ? pk.add(w.dk_dom) : 0, o_di = dyn ? pk.add(w.ds_info) : 0;
+  const size_t o_st = dyn ? pk.add(w.sp_tab) : 0;
   const size_t bytes = pk.size();
 
   HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -355,8 +356,10 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.dyn_pod = dyn ? static_cast<const uint64_t*>(at(o_dp)) : nullptr;
   d.dk_dom = dyn ? static_cast<const int32_t*>(at(o_dd)) : nullptr;
   d.ds_info = dyn ? static_cast<const int32_t*>(at(o_di)) : nullptr;
+  d.sp_tab = dyn ? static_cast<const int32_t*>(at(o_st)) : nullptr;
   d.n_dk = w.n_dk;
-  static_assert(sr::kDevDynU64 == sr::kDynU64 && sr::kDevDomKeys == sr::kDomKeys && sr::kDevDynTerms == sr::kDynTerms,
+  static_assert(sr::kDevDynU64 == sr::kDynU64 && sr::kDevDomKeys == sr::kDomKeys && sr::kDevDynTerms == sr::kDynTerms &&
+                    sr::kDevSpreadSlots == sr::kSpreadSlots,
                 "domain-path layout shared by encode.cpp and kernels.hip");
   for (int k = 0; k < sr::kDomKeys; ++k) d.dk_row[k] = w.dk_row[k];
   d.S = static_cast<uint64_t*>(ctx->tables.p);

@@ -13,12 +13,16 @@
 //    constraint's key fails, and a node whose pair count + (the pod selects
 //    itself) - the key's minimum exceeds maxSkew fails.
 //
-// Encoding (DESIGN.md §2.8): with the counts taken over the base snapshot,
+// Encoding (DESIGN.md §2.9): with the counts taken over the base snapshot,
 // the result for a pod is one node row -- a static atom of its class, one per
 // spec carrying constraints.  That is exact while no earlier pod of the same
-// candidate is counted by the pod's constraints (the counts would change
-// while the candidate is planned): such candidates go to the reference path
-// (encode.cpp pass 1), as do pods whose selectors fail to build.
+// candidate is counted by the pod's constraints.  A candidate with such pods
+// is planned on K2's domain path (encode.cpp analyse_spread, kernels.hip
+// k2_domain): the device adds the earlier pods to the pair counts; the pod's
+// atom keeps only the key check of a device-planned table-key constraint
+// (`dmask`), and the full base check of a node-local one, whose minimum the
+// encoder proved cannot move.  Selectors that fail to build go to the
+// reference path.
 #include <algorithm>
 #include <climits>
 #include <unordered_map>
@@ -144,6 +148,44 @@ bool spread_selects(const sr_cluster* c, int32_t k, int32_t pod) {
   return true;
 }
 
+void spread_node_counts(const sr_snapshot* snap, const sr_cluster* c, int32_t k, int32_t ns, std::vector<int32_t>& out) {
+  const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
+  const sr_spread* S = c->spread;
+  out.assign(static_cast<size_t>(n_spot), 0);
+  if (S->selector_nil[k]) return;
+  for (int32_t n = 0; n < n_spot; ++n)
+    for (int32_t e : snap->state[n].pods) {
+      const SnapPod& sp = snap->pods[e];
+      if (sp.term || sp.ns != ns) continue;
+      const int32_t *lk = snap->lkey.data() + sp.lab, *lv = snap->lval.data() + sp.lab;
+      const int32_t nl = static_cast<int32_t>(sp.nlab);
+      auto label = [&](int32_t key, int32_t* v) {
+        for (int32_t i = 0; i < nl; ++i)
+          if (lk[i] == key) {
+            *v = lv[i];
+            return true;
+          }
+        return false;
+      };
+      bool ok = true;
+      int32_t v;
+      for (int32_t i = S->ml_off[k]; i < S->ml_off[k + 1] && ok; ++i) ok = label(S->ml_key[i], &v) && v == S->ml_val[i];
+      for (int32_t x = S->me_off[k]; x < S->me_off[k + 1] && ok; ++x) {
+        const bool has = label(S->me_key[x], &v);
+        const int32_t* vals = S->me_vals + S->me_val_off[x];
+        const int32_t nv = S->me_val_off[x + 1] - S->me_val_off[x];
+        const bool in = has && std::find(vals, vals + nv, v) != vals + nv;
+        switch (S->me_op[x]) {
+          case SR_OP_IN: ok = in; break;
+          case SR_OP_NOT_IN: ok = !in; break;
+          case SR_OP_EXISTS: ok = has; break;
+          default: ok = !has; break;  // DoesNotExist (anything else fails to build: never encoded)
+        }
+      }
+      if (ok) ++out[n];
+    }
+}
+
 void spread_words(const sr_cluster* c, int32_t pod, std::vector<int32_t>& out) {
   const sr_spread* S = c->spread;
   out.clear();
@@ -179,7 +221,7 @@ void spread_words(const sr_cluster* c, int32_t pod, std::vector<int32_t>& out) {
   }
 }
 
-void spread_row(const sr_snapshot* snap, const int32_t* w, const uint64_t* aff_row, uint64_t* row) {
+void spread_row(const sr_snapshot* snap, const int32_t* w, const uint64_t* aff_row, uint32_t dmask, uint64_t* row) {
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
   const int32_t ns = w[0], nk = w[1];
   std::vector<Constraint> cs(static_cast<size_t>(nk));
@@ -231,6 +273,7 @@ void spread_row(const sr_snapshot* snap, const int32_t* w, const uint64_t* aff_r
         ok = false;  // the node lacks the key: UnschedulableAndUnresolvable
         break;
       }
+      if ((dmask >> k) & 1) continue;  // planned on the device (domain path): the key check only
       auto it = count.find(pair_key(cs[k].key, value(k, n)));
       const int64_t match = it == count.end() ? 0 : it->second;
       ok = match + cs[k].self - min_of[cs[k].key] <= cs[k].max_skew;

@@ -1253,6 +1253,95 @@ static int32_t o_eval_candidate(const oracle_snapshot *s, o_state *st, const int
   return status;
 }
 
+/* Topology spread between the pods of one candidate beyond what the planner
+ * plans on its domain path: a pod whose constraint counts an
+ * earlier pod of the candidate (its namespace, not terminating, selected),
+ * when the pod has pairs at all, makes the candidate a fallback if it has
+ * more than 256 pods, if the pod has another constraint on that key or more
+ * than 2 such constraints, if the key is shared (not on every spot node with
+ * distinct values) and has more than 64 values, or if the key is node-local
+ * and no more of the pairs' nodes hold the minimum count than the constraint
+ * counts earlier pods. */
+static int o_spread_counted(const sr_cluster *c, int32_t k, int32_t pod, int32_t q) {
+  return !c->spread->terminating[q] && c->pod_affinity->ns[q] == c->pod_affinity->ns[pod] && o_spread_sel(c, k, q);
+}
+
+static int o_spread_dyn_fallback(const oracle_snapshot *s, const sr_cluster *c, const int32_t *pods, int32_t np) {
+  const sr_spread *S = c->spread;
+  if (!S || !c->pod_affinity) return 0;
+  int any = 0;
+  for (int32_t i = 1; i < np && !any; i++)
+    for (int32_t k = S->off[pods[i]]; k < S->off[pods[i] + 1] && !any; k++)
+      for (int32_t j = 0; j < i && !any; j++) any = o_spread_counted(c, k, pods[i], pods[j]);
+  if (!any) return 0;
+  if (np > 256) return 1;
+  const int32_t n = s->n;
+  uint8_t *pair = (uint8_t *)malloc((size_t)n + 1);
+  int fb = 0;
+  for (int32_t i = 1; i < np && !fb; i++) {
+    const int32_t pod = pods[i];
+    int npair = 0, slots = 0;
+    for (int32_t m = 0; m < n; m++) {
+      int all = o_affinity_ok(c, pod, s->node[m]);
+      for (int32_t k = S->off[pod]; k < S->off[pod + 1] && all; k++) {
+        int32_t v;
+        all = o_node_label(c, s->node[m], S->topology_key[k], &v);
+      }
+      pair[m] = (uint8_t)all;
+      npair += all;
+    }
+    for (int32_t k = S->off[pod]; k < S->off[pod + 1] && !fb; k++) {
+      int32_t counted = 0;
+      for (int32_t j = 0; j < i; j++) counted += o_spread_counted(c, k, pod, pods[j]);
+      if (counted == 0) continue;
+      if (npair == 0) break; /* no pair: the filter passes every node */
+      for (int32_t k2 = S->off[pod]; k2 < S->off[pod + 1]; k2++)
+        if (k2 != k && S->topology_key[k2] == S->topology_key[k]) fb = 1;
+      if (fb || ++slots > 2) {
+        fb = 1;
+        break;
+      }
+      /* node-local: every spot node carries the key, values pairwise distinct */
+      int32_t key = S->topology_key[k], nvals = 0, local = 1;
+      int32_t *vals = (int32_t *)malloc(sizeof(int32_t) * ((size_t)n + 1));
+      for (int32_t m = 0; m < n; m++) {
+        int32_t v;
+        if (!o_node_label(c, s->node[m], key, &v)) {
+          local = 0;
+          continue;
+        }
+        int32_t seen = 0;
+        for (int32_t q = 0; q < nvals && !seen; q++) seen = vals[q] == v;
+        if (seen) local = 0;
+        else vals[nvals++] = v;
+      }
+      free(vals);
+      if (!local) {
+        if (nvals > 64) fb = 1;
+        continue;
+      }
+      /* the pairs' minimum count and how many nodes hold it */
+      int64_t m0 = INT64_MAX, n0 = 0;
+      for (int32_t m = 0; m < n; m++) {
+        if (!pair[m]) continue;
+        int64_t cnt = 0;
+        for (int32_t j = 0; j < s->st[m].nlist; j++) {
+          int32_t e = s->st[m].list[j];
+          if (!S->terminating[e] && c->pod_affinity->ns[e] == c->pod_affinity->ns[pod] && o_spread_sel(c, k, e)) cnt++;
+        }
+        if (cnt < m0) {
+          m0 = cnt;
+          n0 = 0;
+        }
+        if (cnt == m0) n0++;
+      }
+      if (n0 <= counted) fb = 1;
+    }
+  }
+  free(pair);
+  return fb;
+}
+
 static int o_cand_fallback(const oracle_snapshot *s, const sr_cluster *c, const int32_t *pods, int32_t np) {
   const sr_pods *P = &c->pods;
   for (int32_t i = 0; i < np; i++)
@@ -1263,16 +1352,7 @@ static int o_cand_fallback(const oracle_snapshot *s, const sr_cluster *c, const 
     if (o_acc(c, pods[i], 0) != P->req_milli_cpu[pods[i]] || o_acc(c, pods[i], 1) != P->req_memory[pods[i]] ||
         o_acc(c, pods[i], 2) != P->req_ephemeral[pods[i]])
       return 1;
-  /* a pod whose spread constraint selects an earlier pod of the candidate (same
-   * namespace, not terminating): its counts change while the candidate is
-   * planned -- outside the encoded set */
-  if (c->spread && c->pod_affinity)
-    for (int32_t i = 1; i < np; i++)
-      for (int32_t k = c->spread->off[pods[i]]; k < c->spread->off[pods[i] + 1]; k++)
-        for (int32_t j = 0; j < i; j++)
-          if (!c->spread->terminating[pods[j]] && c->pod_affinity->ns[pods[j]] == c->pod_affinity->ns[pods[i]] &&
-              o_spread_sel(c, k, pods[j]))
-            return 1;
+  if (o_spread_dyn_fallback(s, c, pods, np)) return 1;
   /* two pods of the candidate listing one scalar resource (the later one sees
    * the earlier one's AddPod): outside the encoded set */
   if (c->pod_scalar_off) {

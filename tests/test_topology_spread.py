@@ -75,8 +75,29 @@ def cases():
            [[spread(web("p"), zc())]], [OK], [[0]])
     yield ("terminating_not_counted", N(), [[web("e", deletion_age_s=5.0)], [], [], []],
            [[spread(web("p"), zc())]], [OK], [[0]])
-    yield ("earlier_pod_counted_falls_back", N(), [[], [], [], []],
-           [[web("q"), spread(web("p"), zc())]], [FB], [[-1, -1]])
+    # the pods of one candidate counted by each other: planned on the domain path
+    yield ("earlier_pod_counted", N(), [[], [], [], []],
+           [[web("q"), spread(web("p"), zc())]], [OK], [[0, 2]])
+    yield ("three_replicas_zone", N(), [[], [], [], []],
+           [[spread(web("p%d" % i), zc()) for i in range(3)]], [OK], [[0, 2, 0]])
+    yield ("replicas_zone_min_moves", N(), [[web("e")], [], [], []],
+           [[spread(web("p%d" % i), zc()) for i in range(3)]], [OK], [[2, 0, 2]])
+    yield ("replicas_zone_skew_two", N(), [[web("e")], [], [], []],
+           [[spread(web("p%d" % i), zc(skew=2)) for i in range(4)]], [OK], [[0, 2, 0, 2]])
+    yield ("replicas_hostname", N(), [[], [], [], []],
+           [[spread(web("p%d" % i), zc(key=H)) for i in range(3)]], [OK], [[0, 1, 2]])
+    yield ("replicas_hostname_with_base", N(), [[web("e")], [], [], []],
+           [[spread(web("p%d" % i), zc(key=H)) for i in range(3)]], [OK], [[1, 2, 3]])
+    yield ("replicas_hostname_skew_two", N(), [[], [], [], []],
+           [[spread(web("p%d" % i), zc(key=H, skew=2)) for i in range(3)]], [OK], [[0, 0, 1]])
+    # the 5th replica counts 4 earlier ones and only 4 nodes hold the minimum:
+    # the minimum could move, the planner leaves it to the reference path
+    yield ("replicas_hostname_min_could_move_falls_back", N(), [[], [], [], []],
+           [[spread(web("p%d" % i), zc(key=H)) for i in range(5)]], [FB], [[-1] * 5])
+    yield ("replicas_zone_and_hostname", N(), [[], [], [], []],
+           [[spread(web("p%d" % i), zc(), zc(key=H)) for i in range(3)]], [OK], [[0, 2, 1]])
+    yield ("interacting_constraint_sharing_a_key_falls_back", N(), [[], [], [], []],
+           [[web("q"), spread(web("p"), zc(), zc(sel=LabelSelector(match_labels={"tier": "fe"})))]], [FB], [[-1, -1]])
     yield ("earlier_pod_other_namespace_planned", N(), [[web("e")], [], [], []],
            [[web("q", ns="other"), spread(web("p"), zc())]], [OK], [[0, 2]])
     yield ("earlier_pod_not_selected_planned", N(), [[web("e")], [], [], []],
@@ -122,6 +143,12 @@ def cases():
                   Node("d", cpu_milli=4000)]
     yield ("keyless_node_counts_into_empty_value", empty_zone, [[web("x")], [], [web("y"), web("z")]],
            [[spread(web("p"), zc())]], [OK], [[0]])
+    # the same on the domain path: q (too big for a and e) lands on the keyless
+    # d and counts into (zone, ""), so the minimum is 1 and p fits a
+    small_e = [Node("a", cpu_milli=4000, labels={Z: "z1"}), Node("e", cpu_milli=1000, labels={Z: ""}),
+               Node("d", cpu_milli=4000)]
+    yield ("earlier_pod_on_keyless_node_counts_into_empty_value", small_e, [[web("x")], [], []],
+           [[web("q", cpu=3950), spread(web("p"), zc())]], [OK], [[2, 0]])
 
 
 def run_oracle(nodes, spot_pods, cands):
