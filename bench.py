@@ -441,26 +441,33 @@ def main():
     # The whole housekeeping tick from the cluster arrays: NewNodeMap (A1-A5),
     # the candidate lists (GetPodsForDeletionOnNodeDrain + owner filter),
     # GetClusterSnapshot (A6), then the reference-faithful planning.
-    full_tick = []
+    full_tick, stages = [], {"new_node_map": [], "pods_for_deletion": [], "snapshot_create": [], "plan_first": []}
     for _ in range(args.e2e_reps):
         t1 = time.perf_counter()
         nm2 = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+        t2 = time.perf_counter()
         co2, cp2, _, _, st = pods_for_deletion(lib.sr_pods_for_deletion, sc.ptr, ctypes.byref(sc.drain),
                                                nm2.on_demand, nm2.node_pod_off, nm2.node_pod_idx)
         assert st == capi.SR_OK, st
         lo2, lp2, gi2 = shard(co2, cp2, rank, world)
+        t3 = time.perf_counter()
         snap2 = ctypes.c_void_p()
         st = lib.sr_snapshot_create(sc.ptr, capi.ptr(nm2.spot, capi.P32), len(nm2.spot),
                                     capi.ptr(nm2.node_pod_off, capi.P32), capi.ptr(nm2.node_pod_idx, capi.P32),
                                     ctypes.byref(snap2))
         assert st == capi.SR_OK
+        t4 = time.perf_counter()
         c2 = capi.sr_candidates(len(lo2) - 1, capi.ptr(lo2, capi.P32), capi.ptr(lp2, capi.P32),
                                 capi.ptr(gi2, capi.P32))
         fo = capi.sr_plan_out()
         fo.winner_map = capi.ptr(wmap2, capi.P32)
         st = lib.sr_plan_first(checker.handle, snap2, sc.ptr, ctypes.byref(c2), ctypes.byref(fo))
         assert st == capi.SR_OK, checker.last_error()
-        full_tick.append(1e3 * (time.perf_counter() - t1))
+        t5 = time.perf_counter()
+        full_tick.append(1e3 * (t5 - t1))
+        for k, a, b in (("new_node_map", t1, t2), ("pods_for_deletion", t2, t3), ("snapshot_create", t3, t4),
+                        ("plan_first", t4, t5)):
+            stages[k].append(1e3 * (b - a))
         assert fo.first_ok == first_ok_ref
         lib.sr_snapshot_destroy(snap2)
     end_to_end = None
@@ -478,6 +485,8 @@ def main():
                 "span": "sr_plan_prepare + sr_plan_run over every candidate, same fresh one-node-changed snapshots"}),
             "pods_for_deletion_ms": round(pfd_ms, 3), "reps": len(ref_t), "host_threads": host_threads(),
             "full_tick_median_ms": round(float(np.median(full_tick)), 3) if full_tick else None,
+            "full_tick_stages_median_ms": {k: round(float(np.median(v)), 3) for k, v in stages.items()} if full_tick
+            else None,
             "full_tick_span": "cluster arrays -> sr_new_node_map -> sr_pods_for_deletion -> sr_snapshot_create -> "
                               "sr_plan_first"})
 
