@@ -227,6 +227,31 @@ def rand_spread_scenario(seed):
     return nodes, spot_pods, cands
 
 
+def rand_spread_replicas(seed):
+    """Large candidates of Deployment replicas spread over zones (65-230 pods
+    per candidate: 2-4 pod groups of the domain path), with a hostname
+    constraint on some, over pools whose nodes already run replicas."""
+    r = random.Random(8080 + seed)
+    zones = ["z%d" % i for i in range(2 + seed % 4)]
+    n_spot = 30 + seed % 40
+    nodes = [Node("s%d" % i, cpu_milli=64000, memory=256 * 2 ** 30, pods=110,
+                  labels={Z: r.choice(zones), H: "s%d" % i}) for i in range(n_spot)]
+    apps = ["web", "api"]
+    spot_pods = [[Pod("b%d_%d" % (i, j), namespace="default", containers=[Container(cpu_milli=r.choice([100, 250]))],
+                      labels={"app": r.choice(apps)}) for j in range(r.randrange(4))] for i in range(n_spot)]
+    cands = []
+    for ci in range(3):
+        n = 65 + r.randrange(166)
+        app = r.choice(apps)
+        cs = [zc(skew=r.choice([1, 2, 3]), sel=LabelSelector(match_labels={"app": app}))]
+        if r.random() < 0.3:
+            cs.append(zc(skew=r.choice([2, 4]), sel=LabelSelector(match_labels={"app": app}), key=H))
+        cands.append([spread(Pod("c%d_%d" % (ci, j), namespace="default",
+                                 containers=[Container(cpu_milli=r.choice([50, 100, 250, 500]))],
+                                 labels={"app": app}), *cs) for j in range(n)])
+    return nodes, spot_pods, cands
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_oracle_random_spread_runs(seed):
     """The random generator exercises planned, failing and fallback candidates."""
@@ -262,5 +287,16 @@ def test_gpu_random_spread_clusters(checker, seed):
     candidates are the oracle's."""
     from test_gpu_parity import run_scenario
     nodes, spot_pods, cands = rand_spread_scenario(seed)
+    _, o, p = run_scenario(checker, nodes, spot_pods, cands)
+    assert sum(int(s) != FB for s in p.status) >= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_spread_replica_candidates(checker, seed):
+    """65-230 replicas per candidate spread over zones (and hostnames): the
+    domain path's pod groups against the oracle."""
+    from test_gpu_parity import run_scenario
+    nodes, spot_pods, cands = rand_spread_replicas(seed)
     _, o, p = run_scenario(checker, nodes, spot_pods, cands)
     assert sum(int(s) != FB for s in p.status) >= 1

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Randomised parity stress (tools only): product vs oracle on many seeded
 scenarios, mixing every encoded feature, inter-pod (anti-)affinity on hostname
-and shared keys, large candidates and wide pools.  Runs until --seconds elapse
+and shared keys, topology spread, large candidates and wide pools.  Runs until --seconds elapse
 and prints the first mismatch.  GPU required.
 
   python tools/parity_stress.py [--seconds 180] [--seed0 100000]
@@ -18,6 +18,7 @@ sys.path[:0] = [os.path.join(REPO, "tests"), os.path.join(REPO, "k8s-spot-resche
 from randcluster import rand_scenario  # noqa: E402
 from spotplanner.planner import PredicateChecker  # noqa: E402
 import test_gpu_parity as P  # noqa: E402
+import test_topology_spread as S  # noqa: E402
 
 
 def main():
@@ -30,7 +31,7 @@ def main():
     kinds = {}
     try:
         while time.time() - t0 < a.seconds:
-            k = seed % 9
+            k = seed % 11
             if k == 0:
                 args = dict(n_spot=5 + seed % 60, n_cand=12, max_pods=4 + seed % 30)
             elif k == 1:
@@ -50,9 +51,14 @@ def main():
             elif k == 7:  # the domain path with 2-4 pod groups (65-230 interacting pods)
                 args = dict(n_spot=20 + seed % 30, n_cand=3, max_pods=65 + seed % 165, features=False, anti=0.2,
                             aff=0.15 if seed % 2 else 0.0, shared_keys=True, valid_selectors=True)
-            else:  # scalar resources on most nodes and candidates
+            elif k == 8:  # scalar resources on most nodes and candidates
                 args = dict(n_spot=6 + seed % 20, n_cand=12, max_pods=4 + seed % 8)
-            nodes, spot_pods, cands = rand_scenario(seed, **args)
+            if k == 9:  # topology spread, static and between the pods of a candidate
+                nodes, spot_pods, cands = S.rand_spread_scenario(seed)
+            elif k == 10:  # replica candidates of 65-230 pods spread over zones / hostnames
+                nodes, spot_pods, cands = S.rand_spread_replicas(seed)
+            else:
+                nodes, spot_pods, cands = rand_scenario(seed, **args)
             if k == 7:
                 for c in cands:  # no init containers / scalars: nothing sends them to the fallback path
                     for p in c:
@@ -77,7 +83,7 @@ def main():
             if n % 25 == 0:
                 print("  %d scenarios, %.0f s" % (n, time.time() - t0), flush=True)
     except Exception:
-        print("MISMATCH at seed %d kind %d" % (seed, seed % 9))
+        print("MISMATCH at seed %d kind %d" % (seed, seed % 11))
         traceback.print_exc()
         return 1
     finally:
