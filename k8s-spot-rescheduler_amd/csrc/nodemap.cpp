@@ -38,15 +38,64 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   const sr_pods& P = c->pods;
   const int32_t nn = N.n, np = P.n;
   // Per-node LIST results: counting sort by node index keeps list order.
+  // Large clusters: K pod ranges counted and scattered in parallel, range k's
+  // pods of a node placed after those of ranges < k (still list order).
   std::vector<int32_t> start(static_cast<size_t>(nn) + 1, 0);
-  for (int32_t i = 0; i < np; ++i) {
-    if (P.node[i] < -1 || P.node[i] >= nn) return SR_ERR_INVALID_ARG;
-    if (P.node[i] >= 0) ++start[P.node[i] + 1];
+  std::vector<int32_t> listed(np > 0 ? np : 1);
+  const size_t K = std::min<size_t>(pool_threads(), np >= (1 << 17) ? static_cast<size_t>(np) >> 16 : 1);
+  if (K <= 1) {
+    for (int32_t i = 0; i < np; ++i) {
+      if (P.node[i] < -1 || P.node[i] >= nn) return SR_ERR_INVALID_ARG;
+      if (P.node[i] >= 0) ++start[P.node[i] + 1];
+    }
+    for (int32_t i = 0; i < nn; ++i) start[i + 1] += start[i];
+    std::vector<int32_t> cursor(start.begin(), start.end() - 1);
+    for (int32_t i = 0; i < np; ++i)
+      if (P.node[i] >= 0) listed[cursor[P.node[i]]++] = i;
+  } else {
+    std::vector<int32_t> cnt(K * static_cast<size_t>(nn), 0);  // [range][node], then the range's cursor
+    std::atomic<bool> bad{false};
+    auto range = [&](size_t k, int32_t* lo, int32_t* hi) {
+      *lo = static_cast<int32_t>(static_cast<size_t>(np) * k / K);
+      *hi = static_cast<int32_t>(static_cast<size_t>(np) * (k + 1) / K);
+    };
+    parallel_for(K, 1, [&](size_t a, size_t b) {
+      for (size_t k = a; k < b; ++k) {
+        int32_t lo, hi;
+        range(k, &lo, &hi);
+        int32_t* c = &cnt[k * static_cast<size_t>(nn)];
+        for (int32_t i = lo; i < hi; ++i) {
+          const int32_t nd = P.node[i];
+          if (nd < -1 || nd >= nn) bad.store(true, std::memory_order_relaxed);
+          else if (nd >= 0) ++c[nd];
+        }
+      }
+    });
+    if (bad.load()) return SR_ERR_INVALID_ARG;
+    parallel_for(static_cast<size_t>(nn), 4096, [&](size_t a, size_t b) {  // per node: total, then per-range offsets
+      for (size_t nd = a; nd < b; ++nd) {
+        int32_t acc = 0;
+        for (size_t k = 0; k < K; ++k) {
+          const int32_t x = cnt[k * static_cast<size_t>(nn) + nd];
+          cnt[k * static_cast<size_t>(nn) + nd] = acc;
+          acc += x;
+        }
+        start[nd + 1] = acc;
+      }
+    });
+    for (int32_t i = 0; i < nn; ++i) start[i + 1] += start[i];
+    parallel_for(K, 1, [&](size_t a, size_t b) {
+      for (size_t k = a; k < b; ++k) {
+        int32_t lo, hi;
+        range(k, &lo, &hi);
+        int32_t* c = &cnt[k * static_cast<size_t>(nn)];
+        for (int32_t i = lo; i < hi; ++i) {
+          const int32_t nd = P.node[i];
+          if (nd >= 0) listed[start[nd] + c[nd]++] = i;
+        }
+      }
+    });
   }
-  for (int32_t i = 0; i < nn; ++i) start[i + 1] += start[i];
-  std::vector<int32_t> listed(np > 0 ? np : 1), cursor(start.begin(), start.end() - 1);
-  for (int32_t i = 0; i < np; ++i)
-    if (P.node[i] >= 0) listed[cursor[P.node[i]]++] = i;
 
   const int64_t* cpu = P.cpu_sort_milli;
   auto by_cpu_desc = [cpu](int32_t x, int32_t y) { return cpu[x] > cpu[y]; };

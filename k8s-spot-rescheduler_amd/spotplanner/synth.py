@@ -126,7 +126,7 @@ def new_node_map(fn, cluster_ptr, n_nodes: int, n_pods: int, od_label, spot_labe
     st = fn(cluster_ptr, ctypes.byref(params), ctypes.byref(m))
     if st != capi.SR_OK:
         raise RuntimeError("new_node_map status %d" % st)
-    return NodeMapArrays(spot[: ns[0]].copy(), od[: nod[0]].copy(), off, idx[: int(off[-1])].copy(), req, free)
+    return NodeMapArrays(spot[: ns[0]].copy(), od[: nod[0]].copy(), off, idx[: int(off[-1])], req, free)
 
 
 def pods_for_deletion(fn, cluster_ptr, drain_ptr, nodes: np.ndarray, node_pod_off: np.ndarray,
@@ -176,12 +176,14 @@ class Tick:
 
 def shard(cand_off: np.ndarray, cand_pods: np.ndarray, rank: int, world: int):
     """Candidates c with c % world == rank (interleaved, so every rank holds early candidates)."""
-    idx = np.arange(rank, len(cand_off) - 1, world, dtype=np.int32)
-    off = [0]
-    pods = []
-    for c in idx:
-        seg = cand_pods[cand_off[c]:cand_off[c + 1]]
-        pods.append(seg)
-        off.append(off[-1] + len(seg))
-    return (np.asarray(off, np.int32), np.ascontiguousarray(np.concatenate(pods).astype(np.int32))
-            if pods else np.zeros(0, np.int32), idx)
+    n = len(cand_off) - 1
+    idx = np.arange(rank, max(n, 0), world, dtype=np.int32)
+    cand_off = np.asarray(cand_off)
+    if world == 1:
+        return np.ascontiguousarray(cand_off, np.int32), np.ascontiguousarray(cand_pods, np.int32), idx
+    lens = (cand_off[idx + 1] - cand_off[idx]).astype(np.int64)
+    off = np.zeros(len(idx) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    # positions of the kept candidates' pods: each range shifted to its new start
+    pos = np.repeat(cand_off[idx].astype(np.int64) - off[:-1], lens) + np.arange(off[-1], dtype=np.int64)
+    return off.astype(np.int32), np.ascontiguousarray(np.asarray(cand_pods)[pos], np.int32), idx
