@@ -9,6 +9,8 @@
 
 #include <climits>
 #include <deque>
+#include <memory>
+#include <utility>
 #include <cstdint>
 #include <string>
 #include <unordered_map>
@@ -48,15 +50,39 @@ struct SpotNode {
 // terms (resolved words, anti_term_words).  Copied when the pod enters the
 // snapshot, so later calls may pass any cluster encoded with the same string
 // interner: pod indices of the creating cluster are never kept.
+// Trivial (no member initializers): the snapshot's pod arena grows without a
+// zero fill and snap_pod_from writes every field.
 struct SnapPod {
-  int32_t ns = -1;
-  uint8_t meta = 0;    // ns / labels / terms known (the cluster passed sr_pod_affinity)
-  uint8_t anti = 0;    // carries required anti-affinity
-  uint8_t opaque = 0;  // ... that the encoder cannot read (anti_opaque)
-  uint8_t term = 0;    // DeletionTimestamp set (countPodsMatchSelector skips it); 2: unknown (no sr_spread)
-  uint32_t lab = 0, nlab = 0;       // labels: sr_snapshot::lkey / lval [lab, lab + nlab)
-  uint32_t terms = 0, nterms = 0;   // anti-affinity terms: sr_snapshot::term_words [terms, terms + nterms),
-                                    // {n words, words...} per term (rare)
+  int32_t ns;
+  uint8_t meta;    // ns / labels / terms known (the cluster passed sr_pod_affinity)
+  uint8_t anti;    // carries required anti-affinity
+  uint8_t opaque;  // ... that the encoder cannot read (anti_opaque)
+  uint8_t term;    // DeletionTimestamp set (countPodsMatchSelector skips it); 2: unknown (no sr_spread)
+  uint32_t lab, nlab;       // labels: sr_snapshot::lkey / lval [lab, lab + nlab)
+  uint32_t terms, nterms;   // anti-affinity terms: sr_snapshot::term_words [terms, terms + nterms),
+                            // {n words, words...} per term (rare)
+};
+
+// std::allocator that default-initializes on resize() / emplace_back(): the
+// snapshot's pod and label arenas (a million entries at C4) are filled in
+// parallel right after they grow, so the serial zero fill is skipped.
+template <class T>
+struct UninitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = UninitAlloc<U>;
+  };
+  UninitAlloc() = default;
+  template <class U>
+  UninitAlloc(const UninitAlloc<U>&) {}
+  template <class U>
+  void construct(U* p) {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
 };
 
 // Mutable part: scheduler NodeInfo.Requested, len(Pods), UsedPorts, the pods
@@ -89,8 +115,8 @@ struct sr_snapshot {
   // fingerprint (node_state_fp, kept current by AddPod / Revert)
   std::vector<int32_t> node_names;
   std::vector<uint64_t> node_sfp, node_dfp, saved_dfp;
-  std::vector<sr::SnapPod> pods;  // every pod ever added (NodeState::pods index it)
-  std::vector<int32_t> lkey, lval;  // the pods' labels (one arena: no allocation per pod)
+  std::vector<sr::SnapPod, sr::UninitAlloc<sr::SnapPod>> pods;  // every pod ever added (NodeState::pods index it)
+  std::vector<int32_t, sr::UninitAlloc<int32_t>> lkey, lval;     // the pods' labels (one arena: no allocation per pod)
   std::vector<int32_t> term_words;  // the pods' anti-affinity terms (one arena)
   size_t fork_pods = 0;           // pods.size() at Fork: Revert drops the rest
   size_t fork_labels = 0;         // lkey.size() at Fork

@@ -158,6 +158,7 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
 void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out, int32_t* k, int32_t* v, uint32_t lab,
                    std::vector<int32_t>* terms) {
   *out = SnapPod{};
+  out->ns = -1;
   out->anti = has_anti_terms(c, pod) ? 1 : 0;
   out->opaque = anti_opaque(c, pod) ? 1 : 0;
   out->term = c->spread ? (c->spread->terminating[pod] ? 1 : 0) : 2;
