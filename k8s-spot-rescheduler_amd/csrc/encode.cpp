@@ -564,7 +564,12 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
     return !S->terminating[q] && A->ns[q] == A->ns[pod] && spread_selects(c, k, q);
   };
   std::vector<uint64_t> aff, words;
-  std::vector<int32_t> cnt;
+  // replicas share their NodeAffinity and their constraints' counts: both are
+  // computed once per distinct content (the nodeSelector / affinity words; the
+  // namespace and selector)
+  std::map<std::vector<int32_t>, std::vector<uint64_t>> aff_rows;
+  std::map<std::vector<int32_t>, std::vector<int32_t>> counts;
+  std::vector<int32_t> key_words;
   for (int32_t i = 0; i < nc; ++i) {
     if (status[i] != STATUS_PENDING) continue;
     const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
@@ -597,7 +602,14 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
           }
         if (n_counted == 0) continue;
         if (!affd) {
-          pod_affinity_row(C, snap, c, pod, aff);
+          key_words.clear();
+          for_each_spec_word(c, c->pods, pod, [&](int32_t x) { key_words.push_back(x); });
+          auto it = aff_rows.find(key_words);
+          if (it == aff_rows.end()) {
+            pod_affinity_row(C, snap, c, pod, aff);
+            it = aff_rows.emplace(key_words, aff).first;
+          }
+          aff = it->second;
           for (int32_t k2 = S->off[pod]; k2 < S->off[pod + 1]; ++k2) {
             const std::vector<int32_t>& col = label_column(C, snap, S->topology_key[k2]);
             for (int32_t n = 0; n < n_spot; ++n)
@@ -621,7 +633,20 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
           break;
         }
         const int32_t self = spread_selects(c, k, pod) ? 1 : 0, skew = S->max_skew[k];
-        spread_node_counts(snap, c, k, A->ns[pod], cnt);
+        key_words.assign({A->ns[pod], S->selector_nil[k]});
+        for (int32_t x = S->ml_off[k]; x < S->ml_off[k + 1]; ++x) key_words.insert(key_words.end(), {S->ml_key[x], S->ml_val[x]});
+        key_words.push_back(-1);
+        for (int32_t x = S->me_off[k]; x < S->me_off[k + 1]; ++x) {
+          key_words.insert(key_words.end(), {S->me_key[x], S->me_op[x], S->me_val_off[x + 1] - S->me_val_off[x]});
+          key_words.insert(key_words.end(), S->me_vals + S->me_val_off[x], S->me_vals + S->me_val_off[x + 1]);
+        }
+        auto ci = counts.find(key_words);
+        if (ci == counts.end()) {
+          std::vector<int32_t> v;
+          spread_node_counts(snap, c, k, A->ns[pod], v);
+          ci = counts.emplace(key_words, std::move(v)).first;
+        }
+        const std::vector<int32_t>& cnt = ci->second;
         const std::vector<int32_t>& dom = dk->dom[slot];
         uint64_t* sw = rec + slots * (kDynG + 3);
         for (int g = 0; g < kDynG; ++g) sw[g] = mk[g];

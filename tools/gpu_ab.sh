@@ -10,7 +10,7 @@ for rep in 1 2; do
   i=0
   for arm in "$@"; do
     i=$((i+1))
-    env $arm timeout -k 10 200 python bench.py --config 3 --steps 300 --warmup 20 --no-cpu-baseline $BENCH_ARGS > "$out/arm${i}_rep${rep}.log" 2>&1 || exit $?
+    env $arm timeout -k 10 200 python bench.py --config ${AB_CONFIG:-3} --steps 300 --warmup 20 --no-cpu-baseline $BENCH_ARGS > "$out/arm${i}_rep${rep}.log" 2>&1 || exit $?
     python - "$out/arm${i}_rep${rep}.log" "$arm" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
