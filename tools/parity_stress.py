@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=180.0)
     ap.add_argument("--seed0", type=int, default=100000)
     a = ap.parse_args()
-    c = PredicateChecker(0)
+    chk = PredicateChecker(0)
     t0, n, seed = time.time(), 0, a.seed0
     kinds = {}
     try:
@@ -76,7 +76,7 @@ def main():
                         p = c[r.randrange(len(c))]
                         p.containers[0].scalar = {"nvidia.com/gpu": r.choice([0, 1, 2])}
                         p.containers[0].cpu_milli = max(p.containers[0].cpu_milli, 10)
-            P.run_scenario(c, nodes, spot_pods, cands)
+            P.run_scenario(chk, nodes, spot_pods, cands)
             kinds[k] = kinds.get(k, 0) + 1
             n += 1
             seed += 1
@@ -87,7 +87,7 @@ def main():
         traceback.print_exc()
         return 1
     finally:
-        c.close()
+        chk.close()
     print("parity stress: %d scenarios in %.0f s, all equal to the oracle (by kind: %s)" % (n, time.time() - t0, kinds))
     return 0
 
