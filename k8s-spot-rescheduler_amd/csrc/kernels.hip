@@ -711,6 +711,11 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
 // The chain is one step per visited node instead of one per pod, and a step
 // touches no global memory unless the window moves or a pointer moves beyond
 // the head.
+// Node order visits one window of 64 spot nodes at a time (lanes = nodes,
+// pods in pod order); SR_K2_WINDOW=0 builds the single-node visits instead.
+#ifndef SR_K2_WINDOW
+#define SR_K2_WINDOW 1
+#endif
 constexpr int kNH = 8;             // F head words per pod kept in LDS (nodes [0, 512))
 constexpr int kNHS = kNH + 1;      // LDS stride per pod (odd number of words: conflict-free b64 reads)
 constexpr int kFar = 64 * kNH;     // pointer sentinel: next feasible node lies at or beyond the head, unresolved
@@ -817,6 +822,48 @@ __device__ __forceinline__ uint64_t place_runs(uint64_t P, int lane, int64_t rc,
     alone = zm | alone;
     if (O) alone &= ballot((pm & ports) == 0);
     P &= alone;
+  }
+  return placed;
+}
+
+// Window visit (node order, SR_K2_WINDOW): the pods of `todo` (lanes of one
+// pod group, in pod order; pods k >= kmax are irrelevant) placed one by one,
+// each on its first node of window W (its F word `cur` there) that fits the
+// running state of the window's nodes (lanes = nodes: NodeResourcesFit's
+// compares, the pod-count limit, the NodePorts / anti-affinity state bits),
+// which the placement then updates as ClusterSnapshot.AddPod would.  E: some
+// pod of the candidate asks for ephemeral storage (otherwise the ephemeral
+// check is the fixed `emask`); O: some pod sets or meets state bits.
+template <bool E, bool O>
+__device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W, int lane, int64_t rc, int64_t rm,
+                                                 int64_t re, uint64_t pm, uint64_t cur, uint64_t zm,
+                                                 uint64_t swap_mask, uint64_t emask, int64_t& ncpu, int64_t& nmem,
+                                                 int64_t& neph, uint64_t& nport, int& nleft, int& node) {
+  uint64_t placed = 0;
+  while (todo != 0) {
+    const int k = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    if (k >= kmax) break;
+    const int64_t c = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), k));
+    const int64_t m = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), k));
+    const int64_t e = E ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), k)) : 0;
+    const uint64_t q = O ? readlane64(pm, k) : 0ull;
+    uint64_t fit = readlane64(cur, k) & ballot(nleft >= 1);
+    const uint64_t res = ballot(ncpu >= c) & ballot(nmem >= m) & (E ? ballot(neph >= e) : emask);
+    fit &= ((zm >> k) & 1) ? ~0ull : res;  // fitsRequest skips the resource checks
+    if (O) fit &= ballot((nport & q) == 0);
+    if (fit != 0) {
+      const int j = __builtin_ctzll(fit);
+      if (lane == j) {  // ClusterSnapshot.AddPod on the candidate's copy of node 64 W + j
+        ncpu -= c;
+        nmem -= m;
+        if (E) neph -= e;
+        nleft -= 1;
+        if (O) nport |= swap_pairs(q, swap_mask);  // the bits it sets
+      }
+      if (lane == k) node = 64 * W + j;
+      placed |= 1ull << k;
+    }
   }
   return placed;
 }
@@ -968,6 +1015,21 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     }
     narrow = w.k2_narrow && ballot(!ok) == 0;
   }
+#if SR_K2_WINDOW
+  // some pod asks for ephemeral storage (E) / sets or meets state bits (O):
+  // without them those checks are uniform over the visit and never change
+  bool E, O;
+  {
+    uint64_t e = 0, o = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      e |= ballot(64 * g + lane < np && re[g] != 0);
+      o |= ballot(64 * g + lane < np && pm[g] != 0);
+    }
+    E = e != 0;
+    O = o != 0;
+  }
+#endif
   // node records of window 0 (spot nodes [0, 64)), where first fit usually
   // lands: in flight together with the F heads below
   int wcur = -1;  // register window: lane i holds the base record of node 64 * wcur + i
@@ -1229,18 +1291,46 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       ++windows;
       nbytes += 64u * 40u;
     }
+#if !SR_K2_WINDOW
     // node n's running state (ClusterSnapshot.AddPod on the candidate's copy)
     int64_t cpu = static_cast<int64_t>(readlane64(static_cast<uint64_t>(ncpu), b));
     int64_t mem = static_cast<int64_t>(readlane64(static_cast<uint64_t>(nmem), b));
     int64_t eph = static_cast<int64_t>(readlane64(static_cast<uint64_t>(neph), b));
     uint64_t ports = readlane64(nport, b);
     int left = __builtin_amdgcn_readlane(nleft, b);
+#endif
     if (PROF) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       st.cyc_b += t - cyc_t;
       cyc_t = t;
     }
     uint64_t failed[G];
+#if SR_K2_WINDOW
+    // Window visit: every pod whose pointer lies in window W, in pod order,
+    // goes to its first node of the window that fits the window's running
+    // state (lanes = nodes; ncpu .. nleft are updated in place: the window
+    // is never visited again).  The pod's F word of the window is `cur`.
+    {
+      const uint64_t emask = E ? 0ull : ballot(neph >= 0);  // no pod asks for ephemeral storage: fixed
+#pragma unroll
+      for (int g = 0; g < G; ++g) {  // groups in pod order: the state flows from one to the next
+        const uint64_t cand = ballot(((act[g] >> lane) & 1) && (ptr[g] >> 6) == W);
+        const uint64_t todo = 64 * g < dead ? cand : 0ull;  // wave-uniform
+        uint64_t placed = 0;
+        if (todo != 0) {
+          const int kmax = dead - 64 * g;  // pods above the first dead one are irrelevant
+#define SR_PW(e_, o_)                                                                                             \
+  place_window<e_, o_>(todo, kmax, W, lane, rc[g], rm[g], re[g], pm[g], cur[g], zm[g], w.swap_mask, emask, ncpu, \
+                       nmem, neph, nport, nleft, node[g])
+          placed = E ? (O ? SR_PW(true, true) : SR_PW(true, false)) : (O ? SR_PW(false, true) : SR_PW(false, false));
+#undef SR_PW
+        }
+        placements += __builtin_popcountll(placed);
+        act[g] &= ~placed;
+        failed[g] = cand & ~placed;
+      }
+    }
+#else
 #pragma unroll
     for (int g = 0; g < G; ++g) {  // groups in pod order: the state flows from one to the next
       const uint64_t cand = ballot(((act[g] >> lane) & 1) && ptr[g] == n);
@@ -1257,6 +1347,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       act[g] &= ~placed;
       failed[g] = cand & ~placed;
     }
+#endif
     if (PROF) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       st.cyc_c += t - cyc_t;
@@ -1269,7 +1360,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       const int k = 64 * g + lane;
       bool far_word = false;
       if ((failed[g] >> lane) & 1) {
-        const uint64_t f = b == 63 ? 0ull : cur[g] & (~0ull << (b + 1));
+            // window visits: a pod that failed left window W (no node of it fits)
+        const uint64_t f = (SR_K2_WINDOW || b == 63) ? 0ull : cur[g] & (~0ull << (b + 1));
         int nx = INT_MAX;
         if (f != 0) {  // the common case: the next feasible node is in the same word
           nx = W * 64 + __builtin_ctzll(f);
