@@ -840,10 +840,12 @@ __device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W,
                                                  uint64_t swap_mask, uint64_t emask, int64_t& ncpu, int64_t& nmem,
                                                  int64_t& neph, uint64_t& nport, int& nleft, int& node) {
   uint64_t placed = 0;
+  if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
+  // without state bits one branch per pod: a pod that fits nowhere selects
+  // lane 64 (no lane)
   while (todo != 0) {
     const int k = __builtin_ctzll(todo);
     todo &= todo - 1;
-    if (k >= kmax) break;
     const int64_t c = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), k));
     const int64_t m = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), k));
     const int64_t e = E ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), k)) : 0;
@@ -852,18 +854,88 @@ __device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W,
     const uint64_t res = ballot(ncpu >= c) & ballot(nmem >= m) & (E ? ballot(neph >= e) : emask);
     fit &= ((zm >> k) & 1) ? ~0ull : res;  // fitsRequest skips the resource checks
     if (O) fit &= ballot((nport & q) == 0);
-    if (fit != 0) {
-      const int j = __builtin_ctzll(fit);
-      if (lane == j) {  // ClusterSnapshot.AddPod on the candidate's copy of node 64 W + j
-        ncpu -= c;
-        nmem -= m;
-        if (E) neph -= e;
-        nleft -= 1;
-        if (O) nport |= swap_pairs(q, swap_mask);  // the bits it sets
+    if (O) {  // measured: with state bits the update is cheaper behind a branch (C5)
+      if (fit != 0) {
+        const int j = __builtin_ctzll(fit);
+        if (lane == j) {  // ClusterSnapshot.AddPod on the candidate's copy of node 64 W + j
+          ncpu -= c;
+          nmem -= m;
+          if (E) neph -= e;
+          nleft -= 1;
+          nport |= swap_pairs(q, swap_mask);  // the bits it sets
+        }
+        if (lane == k) node = 64 * W + j;
+        placed |= 1ull << k;
       }
-      if (lane == k) node = 64 * W + j;
-      placed |= 1ull << k;
+      continue;
     }
+    const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
+    const bool hit = lane == j;  // ClusterSnapshot.AddPod on the candidate's copy of node 64 W + j
+    ncpu -= hit ? c : 0;
+    nmem -= hit ? m : 0;
+    if (E) neph -= hit ? e : 0;
+    nleft -= hit ? 1 : 0;
+    node = (lane == k && j < 64) ? 64 * W + j : node;
+    placed |= fit != 0 ? 1ull << k : 0ull;
+  }
+  return placed;
+}
+
+// The free value f of a node scaled to the candidate's request granularity
+// 2^k (narrow candidates): f >> k, or -1 when f < 0 (no request fits, zero
+// included, as with the 64-bit compare).  Values at or above 2^31 are
+// clamped: every sum of the candidate's scaled requests stays below 2^31
+// (Narrow), so a clamped node never refuses a pod it would have taken.
+__device__ __forceinline__ int32_t scale32(int64_t f, int k) {
+  const int64_t q = f >> k;
+  return f < 0 ? -1 : (q > 0x7fffffffll ? 0x7fffffff : static_cast<int32_t>(q));
+}
+
+// place_window with the window's state and the pods' requests scaled to 32
+// bits (narrow candidates: S <= f equals S >> k <= f >> k for the multiples
+// S of 2^k the candidate's requests sum to): one compare and one select per
+// field instead of 64-bit pairs.
+template <bool E, bool O>
+__device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int W, int lane, uint32_t nc, uint32_t nm,
+                                                   uint32_t ne, uint64_t pm, uint64_t cur, uint64_t zm,
+                                                   uint64_t swap_mask, uint64_t emask, int32_t& c32, int32_t& m32,
+                                                   int32_t& e32, uint64_t& nport, int& nleft, int& node) {
+  uint64_t placed = 0;
+  if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
+  while (todo != 0) {
+    const int k = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const int32_t c = __builtin_amdgcn_readlane(static_cast<int>(nc), k);
+    const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
+    const int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
+    const uint64_t q = O ? readlane64(pm, k) : 0ull;
+    uint64_t fit = readlane64(cur, k) & ballot(nleft >= 1);
+    const uint64_t res = ballot(c32 >= c) & ballot(m32 >= m) & (E ? ballot(e32 >= e) : emask);
+    fit &= ((zm >> k) & 1) ? ~0ull : res;  // fitsRequest skips the resource checks
+    if (O) fit &= ballot((nport & q) == 0);
+    if (O) {  // as in place_window
+      if (fit != 0) {
+        const int j = __builtin_ctzll(fit);
+        if (lane == j) {
+          c32 -= c;
+          m32 -= m;
+          if (E) e32 -= e;
+          nleft -= 1;
+          nport |= swap_pairs(q, swap_mask);
+        }
+        if (lane == k) node = 64 * W + j;
+        placed |= 1ull << k;
+      }
+      continue;
+    }
+    const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
+    const bool hit = lane == j;  // ClusterSnapshot.AddPod on the candidate's copy of node 64 W + j
+    c32 -= hit ? c : 0;
+    m32 -= hit ? m : 0;
+    if (E) e32 -= hit ? e : 0;
+    nleft -= hit ? 1 : 0;
+    node = (lane == k && j < 64) ? 64 * W + j : node;
+    placed |= fit != 0 ? 1ull << k : 0ull;
   }
   return placed;
 }
@@ -985,9 +1057,11 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     const uint64_t e = ballot(64 * g + lane < np && static_cast<uint32_t>(r01[g]) == w.s_empty_off);
     if (e != 0) dead = min(dead, 64 * g + __builtin_ctzll(e));
   }
-  // Narrow (32-bit scaled) run passes when every request of the candidate
-  // allows them (place_runs_narrow): the smallest trailing-zero count per
-  // dimension, then every scaled request below 2^26.
+  // Narrow (32-bit scaled) placement when every request of the candidate
+  // allows it: the smallest trailing-zero count per dimension, then every
+  // scaled request below 2^26 (run passes, place_runs_narrow: 64 of them sum
+  // below 2^32) or 2^23 (window visits, place_window32: the <= 256 pods of
+  // the candidate sum below 2^31).
   Narrow nk;
   bool narrow;
   uint32_t nc[G], nm[G], ne[G];
@@ -1008,7 +1082,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     for (int g = 0; g < G; ++g) {
       const uint64_t a = static_cast<uint64_t>(rc[g]) >> nk.kc, b = static_cast<uint64_t>(rm[g]) >> nk.km,
                      c = static_cast<uint64_t>(re[g]) >> nk.ke;
-      ok = ok && (a | b | c) < (1ull << 26);
+      ok = ok && (a | b | c) < (1ull << (SR_K2_WINDOW ? 23 : 26));
       nc[g] = static_cast<uint32_t>(a);
       nm[g] = static_cast<uint32_t>(b);
       ne[g] = static_cast<uint32_t>(c);
@@ -1312,6 +1386,15 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     // is never visited again).  The pod's F word of the window is `cur`.
     {
       const uint64_t emask = E ? 0ull : ballot(neph >= 0);  // no pod asks for ephemeral storage: fixed
+      // narrow candidates: the window's free values scaled to 32 bits once
+      // per visit (the 64-bit copies are not read again: the window is not)
+      int32_t c32 = 0, m32 = 0, e32 = 0;
+      st.narrow = narrow;
+      if (narrow) {
+        c32 = scale32(ncpu, nk.kc);
+        m32 = scale32(nmem, nk.km);
+        e32 = scale32(neph, nk.ke);
+      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {  // groups in pod order: the state flows from one to the next
         const uint64_t cand = ballot(((act[g] >> lane) & 1) && (ptr[g] >> 6) == W);
@@ -1322,8 +1405,16 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
 #define SR_PW(e_, o_)                                                                                             \
   place_window<e_, o_>(todo, kmax, W, lane, rc[g], rm[g], re[g], pm[g], cur[g], zm[g], w.swap_mask, emask, ncpu, \
                        nmem, neph, nport, nleft, node[g])
-          placed = E ? (O ? SR_PW(true, true) : SR_PW(true, false)) : (O ? SR_PW(false, true) : SR_PW(false, false));
+#define SR_PW32(e_, o_)                                                                                           \
+  place_window32<e_, o_>(todo, kmax, W, lane, nc[g], nm[g], ne[g], pm[g], cur[g], zm[g], w.swap_mask, emask, c32, \
+                         m32, e32, nport, nleft, node[g])
+          if (narrow)
+            placed = E ? (O ? SR_PW32(true, true) : SR_PW32(true, false))
+                       : (O ? SR_PW32(false, true) : SR_PW32(false, false));
+          else
+            placed = E ? (O ? SR_PW(true, true) : SR_PW(true, false)) : (O ? SR_PW(false, true) : SR_PW(false, false));
 #undef SR_PW
+#undef SR_PW32
         }
         placements += __builtin_popcountll(placed);
         act[g] &= ~placed;

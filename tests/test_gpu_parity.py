@@ -541,19 +541,23 @@ def test_many_deployments_with_hostname_anti_affinity(checker):
 def _granular_scenario(seed: int):
     """Many small pods onto few nodes (run passes of several pods), with request
     granularities that do and do not allow the scaled 32-bit sums: MiB multiples,
-    odd byte counts, scaled values at the 2^26 limit, sums landing exactly on a
-    node's free value (not itself a multiple of the granularity), and
-    overcommitted nodes (negative free values)."""
+    odd byte counts, scaled values at the 2^26 limit (run passes) and the 2^23
+    limit (window visits), nodes whose scaled free memory is clamped at 2^31 - 1
+    (window visits), sums landing exactly on a node's free value (not itself a
+    multiple of the granularity), and overcommitted nodes (negative free
+    values)."""
     import random
     r = random.Random(seed)
-    mode = seed % 4
-    unit = {0: 1 << 20, 1: 1, 2: 1 << 20, 3: 3}[mode]
+    mode = seed % 6
+    unit = {0: 1 << 20, 1: 1, 2: 1 << 20, 3: 3, 4: 1 << 20, 5: 1 << 20}[mode]
     n_spot = 3 + seed % 5
     nodes = []
     for i in range(n_spot):
         mem = r.choice([1, 2, 4]) * GiB + r.choice([0, 1, 12345])
         if mode == 2:
             mem = (1 << 46) + r.choice([0, 1, 1 << 20])  # scaled by 2^20: just around 2^26
+        elif mode >= 4:
+            mem = r.choice([1 << 52, (1 << 51) - 1, (1 << 30) + 5])  # scaled by 2^20: around and above 2^31
         nodes.append(Node(name="n%d" % i, cpu_milli=r.choice([1000, 2000, 4001]), memory=mem, pods=110,
                           ephemeral=r.choice([0, 10 * GiB + 7]), labels={"kubernetes.io/hostname": "n%d" % i}))
     spot_pods = []
@@ -569,6 +573,10 @@ def _granular_scenario(seed: int):
         for k in range(r.randint(2, 24)):
             if mode == 2:
                 mem = r.choice([(1 << 45), (1 << 44) + (1 << 20), ((1 << 26) - 1) << 20, 1 << 20])
+            elif mode == 4:  # scaled requests at the window visits' 2^23 limit, some beyond it
+                mem = r.choice([((1 << 23) - 1) << 20, (1 << 23) << 20, (1 << 22) << 20, 1 << 20, 3 << 20])
+            elif mode == 5:  # every scaled request below 2^23: 32-bit window state on clamped nodes
+                mem = r.choice([((1 << 23) - 1) << 20, (1 << 21) << 20, 5 << 20, 1 << 20])
             else:
                 mem = r.randint(1, 600) * unit * (1 if mode != 0 else r.choice([1, 1, 64]))
             cpu = r.choice([0, 50, 100, 250, 333, 1000])
@@ -585,8 +593,9 @@ def _granular_scenario(seed: int):
 
 @pytest.mark.parametrize("narrow", [0, 1])
 def test_scaled_run_pass_matches_oracle(narrow):
-    # SR_K2_NARROW=0 keeps every run pass on 64-bit sums; 1 (the default) scales
-    # a candidate's requests to 32 bits where that is exact
+    # SR_K2_NARROW=0 keeps every placement on 64-bit values; 1 (the default)
+    # scales a candidate's requests (and, in window visits, the window's free
+    # values) to 32 bits where that is exact
     import os
     from spotplanner.planner import PredicateChecker
     os.environ["SR_K2_NARROW"] = str(narrow)
@@ -595,7 +604,7 @@ def test_scaled_run_pass_matches_oracle(narrow):
     finally:
         del os.environ["SR_K2_NARROW"]
     try:
-        for seed in range(24):
+        for seed in range(36):
             nodes, spot_pods, cands = _granular_scenario(7000 + seed)
             run_scenario(c, nodes, spot_pods, cands)
         for seed in range(10):

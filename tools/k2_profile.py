@@ -89,9 +89,10 @@ def main():
         sv = max(1, vis.sum())
         print("node order: cycles/visit min+window+state %.0f, placement %.0f, pointer moves %.0f"
               % (q[:, 9].sum() / sv, q[:, 10].sum() / sv, q[:, 11].sum() / sv))
+        print("node order: placement cycles per placed pod %.0f" % (q[:, 10].sum() / max(1, q[:, 6].sum())))
         print("node order: wave dur us p50/p90/max %s" % pct(dur[nodeo]))
         runv = (q[:, 13] & 0xffffffff).astype(np.int64)
-        print("node order: 32-bit scaled run passes in %d of %d waves; cycles per run-pass visit %.0f"
+        print("node order: 32-bit scaled placement in %d of %d waves; cycles per run-pass visit %.0f"
               % (int((q[:, 15] & 1).sum()), len(q), (q[:, 15] >> 1).sum() / max(1, runv.sum())))
     if (~nodeo).any():
         print("pod order:  wave dur us p50/p90/max %s" % pct(dur[~nodeo]))
