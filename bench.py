@@ -82,8 +82,10 @@ def k2_chain_summary(path):
         if line.startswith("node order: cycles/visit"):
             nums = [float(x.strip(",")) for x in line.split() if x.strip(",").replace(".", "").isdigit()]
             if len(nums) >= 3:
-                out.update({"cycles_per_visit_min_state": nums[0], "cycles_per_visit_placement": nums[1],
+                out.update({"cycles_per_visit_min_window": nums[0], "cycles_per_visit_placement": nums[1],
                             "cycles_per_visit_pointer_moves": nums[2]})
+        elif line.startswith("node order: placement cycles per placed pod"):
+            out["cycles_per_placed_pod"] = float(line.split()[-1])
         elif line.startswith("node order: visits"):
             out["visits_line"] = line.strip()
         elif line.startswith("wave dur us"):

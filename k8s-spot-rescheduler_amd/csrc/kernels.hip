@@ -7,9 +7,10 @@
 //  K2 placement   canDrainNode for every candidate at once (rescheduler.go:357-370),
 //                 one wave per candidate, with feasibility F = S & T & T & T:
 //                  - node order (k2_node_order; the k2_node kernel when every
-//                    candidate takes it): spot nodes visited in NodeInfoArray
-//                    order, each at most once, the candidate's pods placed on
-//                    it in pod order -- the same first fit as pod by pod;
+//                    candidate takes it): windows of 64 spot nodes visited in
+//                    NodeInfoArray order, each at most once, the candidate's
+//                    pods placed in it in pod order (lanes = nodes) -- the
+//                    same first fit as pod by pod;
 //                  - pod order (k2_run): candidates of more than 256 pods;
 //                  - the domain path (k2_domain): pods interacting through
 //                    shared topology domains (inter-pod (anti-)affinity).
@@ -53,8 +54,8 @@ __device__ __forceinline__ int wave_min(int v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
-// Inclusive prefix sum / OR over the 64 lanes: DPP row shifts within each row
-// of 16, then the row totals broadcast into the rows above (no LDS).
+// A 64-bit lane value shifted by a DPP row shift / row broadcast (zero where
+// nothing is shifted in): the steps of wave-wide scans without LDS.
 template <int CTRL, int ROW_MASK = 0xf>
 __device__ __forceinline__ uint64_t dpp_shifted(uint64_t v) {
   const uint32_t lo = static_cast<uint32_t>(
@@ -63,39 +64,6 @@ __device__ __forceinline__ uint64_t dpp_shifted(uint64_t v) {
       __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(v >> 32)), CTRL, ROW_MASK, 0xf, true));
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
-__device__ __forceinline__ int64_t scan_add(int64_t x) {
-  uint64_t v = static_cast<uint64_t>(x);
-  v += dpp_shifted<0x111>(v);       // row_shr:1
-  v += dpp_shifted<0x112>(v);       // row_shr:2
-  v += dpp_shifted<0x114>(v);       // row_shr:4
-  v += dpp_shifted<0x118>(v);       // row_shr:8
-  v += dpp_shifted<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
-  v += dpp_shifted<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
-  return static_cast<int64_t>(v);
-}
-// The same inclusive prefix sum on 32-bit lanes: one DPP add per step.
-__device__ __forceinline__ uint32_t scan_add32(uint32_t v) {
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, true));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, true));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, true));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, true));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, true));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, true));
-  return v;
-}
-
-// OR of the lanes below (exclusive): shift up one lane (wave_shr:1), then scan
-__device__ __forceinline__ uint64_t scan_or_excl(uint64_t v) {
-  v = dpp_shifted<0x138>(v);
-  v |= dpp_shifted<0x111>(v);
-  v |= dpp_shifted<0x112>(v);
-  v |= dpp_shifted<0x114>(v);
-  v |= dpp_shifted<0x118>(v);
-  v |= dpp_shifted<0x142, 0xa>(v);
-  v |= dpp_shifted<0x143, 0xc>(v);
-  return v;
-}
-
 // One word of an S row from its class's 8-slot program and the program's atom
 // words v[u] (AND, AND NOT, terms ORed with their atoms ANDed).
 __device__ __forceinline__ uint64_t eval_prog8(const int (&op)[8], const uint64_t (&v)[8]) {
@@ -386,11 +354,8 @@ struct K2Lds {
 struct K2Stats {
   uint32_t n_spec_miss = 0, n_min = 0, n_far = 0;
   uint64_t cyc_a = 0, cyc_b = 0, cyc_c = 0, cyc_d = 0;
-  // node order (profile builds): run-pass iterations / pod-by-pod rounds, and the visits taking each
-  uint32_t run_it = 0, seq_it = 0, run_visits = 0, seq_visits = 0;
-  uint64_t cyc_rec = 0;  // node order: wave entry -> pod records in registers
-  uint64_t cyc_run = 0;  // node order: cycles in run-pass visits
-  uint32_t narrow = 0;   // node order: the candidate's run passes are 32-bit scaled
+  uint64_t cyc_rec = 0;  // node order (profile builds): wave entry -> pod records in registers
+  uint32_t narrow = 0;   // node order: the candidate's window visits use 32-bit scaled state
 };
 
 // One candidate's canDrainNode with 64 * SPL touched-node slots.  Returns the
@@ -679,14 +644,15 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
 }
 
 // ------------------------------------------------------------ K2, node order
-// First fit in pod order (canDrainNode) equals first fit in NODE order: visit
-// the spot nodes in NodeInfoArray order and, at node n, consider the
-// candidate's unplaced pods in pod order, placing each one that fits n's
-// running state.  Every encoded predicate is node-local (a node's answer for
-// pod k depends only on the candidate's pods already placed on that node), so
-// by induction over k both orders place pod k on the same node: pods below k
-// have the same placements, hence every node presents the same state to k.
-// Each node is therefore visited at most once, at its base state, and only
+// First fit in pod order (canDrainNode) equals first fit in WINDOW order: visit
+// the spot nodes 64 at a time (windows of NodeInfoArray order) and, in window
+// W, place the candidate's pods not yet placed, in pod order, each on its first
+// node of W that fits W's running state.  Every encoded predicate is
+// node-local (a node's answer for pod k depends only on the candidate's pods
+// already placed on that node), so by induction over k both orders place pod
+// k on the same node: a pod placed in an earlier window never touched W, and
+// inside W the pods meet W's nodes in pod order, as canDrainNode presents
+// them.  Each window is therefore visited at most once, and only windows with
 // base-feasible nodes (F = S & T & T & T) are worth visiting; a pod whose F
 // row has no bit left can never be placed: it is the failing pod once every
 // lower pod is placed, and pods above it are irrelevant (canDrainNode stops).
@@ -698,24 +664,24 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
 //             (kNH words = 512 nodes) of each of those, 8 pods per load
 //             instruction (lanes = pod x word), goes to LDS, the pod's lane
 //             keeps its 8-bit mask of non-zero head words;
-//   visits    n = min pointer over unplaced pods (DPP wave-min); node n's base
-//             record from a 64-node register window; greedy placement in pod
-//             order (group by group) with the running state in SGPRs; pods
-//             that did not fit move their pointer to the next set bit of their
-//             F row.  A pod whose head holds no further bit points at kFar,
-//             the first chunk boundary: an unresolved pointer.  When the
-//             minimum reaches an unresolved pointer, its pods scan their rows
-//             from there, 64 words per round (lanes = words), which leaves a
-//             mask of the chunk's non-zero words for later moves; a mask that
-//             runs out makes the pointer the next chunk boundary, unresolved.
-// The chain is one step per visited node instead of one per pod, and a step
-// touches no global memory unless the window moves or a pointer moves beyond
-// the head.
-// Node order visits one window of 64 spot nodes at a time (lanes = nodes,
-// pods in pod order); SR_K2_WINDOW=0 builds the single-node visits instead.
-#ifndef SR_K2_WINDOW
-#define SR_K2_WINDOW 1
-#endif
+//   visits    n = min pointer over unplaced pods (DPP wave-min), W = n / 64;
+//             the base records of W's 64 nodes in one register per field
+//             (lanes = nodes), updated in place; the pods pointing into W one
+//             by one (place_window: its F word of W & ballots of the compares
+//             against the running state, the first set lane, the update of
+//             that lane); pods that did not fit move their pointer to the
+//             first set bit of their F row beyond W.  A pod whose head holds
+//             no further bit points at kFar, the first chunk boundary: an
+//             unresolved pointer.  When the minimum reaches an unresolved
+//             pointer, its pods scan their rows from there, 64 words per round
+//             (lanes = words), which leaves a mask of the chunk's non-zero
+//             words for later moves; a mask that runs out makes the pointer
+//             the next chunk boundary, unresolved.
+// The chain is one step per pod plus one window load per visited window
+// (C3: 1.06 windows per candidate); no step touches global memory unless the
+// window moves or a pointer moves beyond the head.  Measured against visiting
+// one node at a time (prefix-sum run passes over the pods pointing at it):
+// C3 K2 17.7 -> 13.1 us, C5 61 -> 42 us.
 constexpr int kNH = 8;             // F head words per pod kept in LDS (nodes [0, 512))
 constexpr int kNHS = kNH + 1;      // LDS stride per pod (odd number of words: conflict-free b64 reads)
 constexpr int kFar = 64 * kNH;     // pointer sentinel: next feasible node lies at or beyond the head, unresolved
@@ -745,88 +711,7 @@ __device__ __forceinline__ uint32_t from_lane(uint32_t v, int src) {
   return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(v)));
 }
 
-// Pods `P` (lanes, in pod order) whose pointer is node n, placed on n one by
-// one as ClusterSnapshot.AddPod would see them: NodeResourcesFit's compare per
-// resource, the pod-count limit, and the NodePorts / anti-affinity state bits.
-// E: some pod of P asks for ephemeral storage; O: some pod of P sets or
-// conflicts with state bits.  Without them those compares are uniform (a zero
-// request against the node's free value) and their state never changes.
-template <bool E, bool O>
-__device__ __forceinline__ uint64_t place_seq(uint64_t P, int lane, int64_t rc, int64_t rm, int64_t re, uint64_t pm,
-                                              uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
-                                              uint64_t& ports, int& left, uint64_t swap_mask, uint32_t& it) {
-  uint64_t placed = 0;
-  uint64_t rest = left >= 1 ? P : 0ull;
-  // One exit branch per placement: the checks are unconditional (lane masks
-  // straight from the compares); pods below the one placed that did not fit
-  // failed at n.
-  for (;;) {
-    ++it;
-    uint64_t res = ballot(rc <= cpu) & ballot(rm <= mem);
-    res &= E ? ballot(re <= eph) : (eph >= 0 ? ~0ull : 0ull);
-    uint64_t fm = rest & (zm | res);
-    if (O) fm &= ballot((pm & ports) == 0);
-    if (fm == 0) break;
-    const int j = __builtin_ctzll(fm);
-    placed |= 1ull << j;
-    rest &= j == 63 ? 0ull : ~0ull << (j + 1);
-    cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), j));
-    mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), j));
-    if (E) eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), j));
-    if (O) ports |= swap_pairs(readlane64(pm, j), swap_mask);  // the bits it sets
-    left -= 1;
-    rest = left >= 1 ? rest : 0ull;
-  }
-  return placed;
-}
-
-// The same placement by runs: with inclusive prefix sums of the requests of P,
-// every pod below the first one that fails fits (each against the node with
-// all pods before it placed), so that run is placed at once.  The first
-// failing pod then fails on its own, and so does every pod of P that does not
-// fit the node after the run: all of them are dropped before the next pass.
-// One pass per run of placements instead of one round per placement.
-template <bool E, bool O>
-__device__ __forceinline__ uint64_t place_runs(uint64_t P, int lane, int64_t rc, int64_t rm, int64_t re, uint64_t pm,
-                                               uint64_t sb, uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
-                                               uint64_t& ports, int& left, uint32_t& it) {
-  uint64_t placed = 0;
-  while (P != 0 && left >= 1) {
-    ++it;
-    const bool in = (P >> lane) & 1;
-    const int64_t ic = scan_add(in ? rc : 0), im = scan_add(in ? rm : 0);
-    const int64_t ie = E ? scan_add(in ? re : 0) : 0;
-    const uint64_t xo = O ? scan_or_excl(in ? sb : 0ull) : 0ull;
-    const int below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(P >> 32),
-                                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(P), 0));
-    uint64_t res = ballot(ic <= cpu) & ballot(im <= mem);
-    res &= E ? ballot(ie <= eph) : (eph >= 0 ? ~0ull : 0ull);
-    uint64_t ok = ballot(below < left) & (zm | res);
-    if (O) ok &= ballot((pm & (ports | xo)) == 0);
-    const uint64_t bad = P & ~ok;
-    const uint64_t run = bad == 0 ? P : P & ((1ull << __builtin_ctzll(bad)) - 1);
-    if (run != 0) {
-      const int last = 63 - __builtin_clzll(run);
-      cpu -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(ic), last));
-      mem -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(im), last));
-      if (E) eph -= static_cast<int64_t>(readlane64(static_cast<uint64_t>(ie), last));
-      if (O) ports |= readlane64(xo, last) | readlane64(sb, last);
-      left -= __builtin_popcountll(run);
-      placed |= run;
-    }
-    if (bad == 0) break;
-    P &= ~run;
-    // pods that do not fit the node as it is now fail whatever comes after
-    uint64_t alone = ballot(rc <= cpu) & ballot(rm <= mem);
-    alone &= E ? ballot(re <= eph) : (eph >= 0 ? ~0ull : 0ull);
-    alone = zm | alone;
-    if (O) alone &= ballot((pm & ports) == 0);
-    P &= alone;
-  }
-  return placed;
-}
-
-// Window visit (node order, SR_K2_WINDOW): the pods of `todo` (lanes of one
+// Window visit (node order): the pods of `todo` (lanes of one
 // pod group, in pod order; pods k >= kmax are irrelevant) placed one by one,
 // each on its first node of window W (its F word `cur` there) that fits the
 // running state of the window's nodes (lanes = nodes: NodeResourcesFit's
@@ -940,86 +825,11 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
   return placed;
 }
 
-// Narrow requests of a candidate: in each dimension every request is a
-// multiple of 2^k (k = the smallest trailing-zero count among them) and
-// request >> k < 2^26, so 64 of them sum below 2^32.  A sum S of such requests
-// fits a free value f exactly when S >> k <= f >> k (f >= 0; S is a multiple
-// of 2^k), so the run pass can scan 32-bit scaled requests.
+// A narrow candidate's request granularity per dimension: every request is a
+// multiple of 2^k (k = the smallest trailing-zero count among them).
 struct Narrow {
   int kc, km, ke;
 };
-__device__ __forceinline__ uint32_t cap32(int64_t f, int k) {  // f >> k clamped to [0, 2^32); f < 0: nothing fits
-  const int64_t q = f >> k;
-  return q < 0 ? 0u : (q > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(q));
-}
-
-template <bool E>
-__device__ __forceinline__ uint64_t place_runs_narrow(uint64_t P, int lane, int64_t rc, int64_t rm, int64_t re,
-                                                      uint32_t nc, uint32_t nm, uint32_t ne, const Narrow& k,
-                                                      uint64_t zm, int64_t& cpu, int64_t& mem, int64_t& eph,
-                                                      int& left, uint32_t& it) {
-  uint64_t placed = 0;
-  while (P != 0 && left >= 1) {
-    ++it;
-    const bool in = (P >> lane) & 1;
-    const uint32_t ic = scan_add32(in ? nc : 0u), im = scan_add32(in ? nm : 0u);
-    const uint32_t ie = E ? scan_add32(in ? ne : 0u) : 0u;
-    const int below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(P >> 32),
-                                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(P), 0));
-    // a negative free value: no sum fits (zero sums included), as with the 64-bit compare
-    uint64_t res = (cpu >= 0 ? ballot(ic <= cap32(cpu, k.kc)) : 0ull) & (mem >= 0 ? ballot(im <= cap32(mem, k.km)) : 0ull);
-    res &= eph >= 0 ? (E ? ballot(ie <= cap32(eph, k.ke)) : ~0ull) : 0ull;
-    const uint64_t ok = ballot(below < left) & (zm | res);
-    const uint64_t bad = P & ~ok;
-    const uint64_t run = bad == 0 ? P : P & ((1ull << __builtin_ctzll(bad)) - 1);
-    if (run != 0) {
-      const int last = 63 - __builtin_clzll(run);
-      cpu -= static_cast<int64_t>(static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ic), last))) << k.kc);
-      mem -= static_cast<int64_t>(static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(im), last))) << k.km);
-      if (E)
-        eph -= static_cast<int64_t>(static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ie), last))) << k.ke);
-      left -= __builtin_popcountll(run);
-      placed |= run;
-    }
-    if (bad == 0) break;
-    P &= ~run;
-    // pods that do not fit the node as it is now fail whatever comes after
-    uint64_t alone = ballot(rc <= cpu) & ballot(rm <= mem);
-    alone &= E ? ballot(re <= eph) : (eph >= 0 ? ~0ull : 0ull);
-    P &= zm | alone;
-  }
-  return placed;
-}
-
-// Placement at one node visit.  Visits whose pods set or meet state bits
-// (host ports, anti-affinity pairs) run pod by pod: the run pass would add an
-// OR scan and a rescan per failing pod, and measured slower there (C5).  The
-// others take the run pass from k2_scan_min pods on.  Few variants on purpose:
-// every extra copy of this code is instruction-cache footprint a wave jumps
-// between (measured on C5: specialising all four E / O combinations cost 5 %).
-__device__ __forceinline__ uint64_t place_at(const DevWorkload& w, uint64_t P, int lane, int64_t rc, int64_t rm,
-                                             int64_t re, uint64_t pm, uint64_t zm, uint32_t nc, uint32_t nm,
-                                             uint32_t ne, const Narrow& k, bool narrow, int64_t& cpu, int64_t& mem,
-                                             int64_t& eph, uint64_t& ports, int& left, K2Stats& st) {
-  const bool E = (ballot(re != 0) & P) != 0;  // some pod asks for ephemeral storage
-  const bool O = (ballot(pm != 0) & P) != 0;  // some pod sets / meets state bits
-  if (O) {
-    ++st.seq_visits;
-    return place_seq<true, true>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask, st.seq_it);
-  }
-  if (__builtin_popcountll(P) >= w.k2_scan_min) {
-    ++st.run_visits;
-    st.narrow = narrow;
-    if (narrow) {
-      if (E) return place_runs_narrow<true>(P, lane, rc, rm, re, nc, nm, ne, k, zm, cpu, mem, eph, left, st.run_it);
-      return place_runs_narrow<false>(P, lane, rc, rm, re, nc, nm, ne, k, zm, cpu, mem, eph, left, st.run_it);
-    }
-    if (E) return place_runs<true, false>(P, lane, rc, rm, re, pm, 0ull, zm, cpu, mem, eph, ports, left, st.run_it);
-    return place_runs<false, false>(P, lane, rc, rm, re, pm, 0ull, zm, cpu, mem, eph, ports, left, st.run_it);
-  }
-  ++st.seq_visits;
-  return place_seq<true, false>(P, lane, rc, rm, re, pm, zm, cpu, mem, eph, ports, left, w.swap_mask, st.seq_it);
-}
 
 template <int G, bool PROF>
 __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __restrict__ F, const int p0,
@@ -1059,9 +869,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   }
   // Narrow (32-bit scaled) placement when every request of the candidate
   // allows it: the smallest trailing-zero count per dimension, then every
-  // scaled request below 2^26 (run passes, place_runs_narrow: 64 of them sum
-  // below 2^32) or 2^23 (window visits, place_window32: the <= 256 pods of
-  // the candidate sum below 2^31).
+  // scaled request below 2^23 (place_window32: the <= 256 pods of the
+  // candidate sum below 2^31).
   Narrow nk;
   bool narrow;
   uint32_t nc[G], nm[G], ne[G];
@@ -1082,14 +891,13 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     for (int g = 0; g < G; ++g) {
       const uint64_t a = static_cast<uint64_t>(rc[g]) >> nk.kc, b = static_cast<uint64_t>(rm[g]) >> nk.km,
                      c = static_cast<uint64_t>(re[g]) >> nk.ke;
-      ok = ok && (a | b | c) < (1ull << (SR_K2_WINDOW ? 23 : 26));
+      ok = ok && (a | b | c) < (1ull << 23);
       nc[g] = static_cast<uint32_t>(a);
       nm[g] = static_cast<uint32_t>(b);
       ne[g] = static_cast<uint32_t>(c);
     }
     narrow = w.k2_narrow && ballot(!ok) == 0;
   }
-#if SR_K2_WINDOW
   // some pod asks for ephemeral storage (E) / sets or meets state bits (O):
   // without them those checks are uniform over the visit and never change
   bool E, O;
@@ -1103,7 +911,6 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     E = e != 0;
     O = o != 0;
   }
-#endif
   // node records of window 0 (spot nodes [0, 64)), where first fit usually
   // lands: in flight together with the F heads below
   int wcur = -1;  // register window: lane i holds the base record of node 64 * wcur + i
@@ -1353,7 +1160,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       continue;
     }
     ++visits;
-    const int W = n >> 6, b = n & 63;
+    const int W = n >> 6;
     if (W != wcur) {  // wave-uniform
       const uint64_t* nr = w.node_rec + static_cast<size_t>(W * 64 + lane) * 8;
       ncpu = static_cast<int64_t>(nr[0]);
@@ -1365,21 +1172,12 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       ++windows;
       nbytes += 64u * 40u;
     }
-#if !SR_K2_WINDOW
-    // node n's running state (ClusterSnapshot.AddPod on the candidate's copy)
-    int64_t cpu = static_cast<int64_t>(readlane64(static_cast<uint64_t>(ncpu), b));
-    int64_t mem = static_cast<int64_t>(readlane64(static_cast<uint64_t>(nmem), b));
-    int64_t eph = static_cast<int64_t>(readlane64(static_cast<uint64_t>(neph), b));
-    uint64_t ports = readlane64(nport, b);
-    int left = __builtin_amdgcn_readlane(nleft, b);
-#endif
     if (PROF) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       st.cyc_b += t - cyc_t;
       cyc_t = t;
     }
     uint64_t failed[G];
-#if SR_K2_WINDOW
     // Window visit: every pod whose pointer lies in window W, in pod order,
     // goes to its first node of the window that fits the window's running
     // state (lanes = nodes; ncpu .. nleft are updated in place: the window
@@ -1421,24 +1219,6 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         failed[g] = cand & ~placed;
       }
     }
-#else
-#pragma unroll
-    for (int g = 0; g < G; ++g) {  // groups in pod order: the state flows from one to the next
-      const uint64_t cand = ballot(((act[g] >> lane) & 1) && ptr[g] == n);
-      uint64_t placed = 0;
-      if (cand != 0) {  // wave-uniform
-        const uint32_t rv = st.run_visits;
-        const uint64_t t0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
-        placed = place_at(w, cand, lane, rc[g], rm[g], re[g], pm[g], zm[g], nc[g], nm[g], ne[g], nk, narrow, cpu,
-                          mem, eph, ports, left, st);
-        if (PROF && st.run_visits != rv) st.cyc_run += __builtin_amdgcn_s_memtime() - t0 + (placed & 0);
-        placements += __builtin_popcountll(placed);
-      }
-      if ((placed >> lane) & 1) node[g] = n;
-      act[g] &= ~placed;
-      failed[g] = cand & ~placed;
-    }
-#endif
     if (PROF) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       st.cyc_c += t - cyc_t;
@@ -1451,12 +1231,9 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       const int k = 64 * g + lane;
       bool far_word = false;
       if ((failed[g] >> lane) & 1) {
-            // window visits: a pod that failed left window W (no node of it fits)
-        const uint64_t f = (SR_K2_WINDOW || b == 63) ? 0ull : cur[g] & (~0ull << (b + 1));
+            // it left window W: no node of it fits
         int nx = INT_MAX;
-        if (f != 0) {  // the common case: the next feasible node is in the same word
-          nx = W * 64 + __builtin_ctzll(f);
-        } else if (W < kNH) {
+        if (W < kNH) {
           const uint32_t rem = hmask[g] & (0xffu << (W + 1)) & 0xffu;
           if (rem != 0) {
             const int w2 = __builtin_ctz(rem);
@@ -1920,11 +1697,11 @@ __device__ __forceinline__ void k2_finish(const DevWorkload& w, const K2Entry& x
       pr[9] = st.cyc_b;
       pr[10] = st.cyc_c;
       pr[11] = st.cyc_d;
-      if (wide == 2) {  // node order: placement passes
-        pr[12] = static_cast<uint64_t>(st.run_it) | static_cast<uint64_t>(st.seq_it) << 32;
-        pr[13] = static_cast<uint64_t>(st.run_visits) | static_cast<uint64_t>(st.seq_visits) << 32;
+      if (wide == 2) {  // node order
+        pr[12] = 0;
+        pr[13] = 0;
         pr[14] = st.cyc_rec - x.c_start;
-        pr[15] = st.cyc_run << 1 | st.narrow;
+        pr[15] = st.narrow;
       }
     }
   }

@@ -105,10 +105,9 @@ struct sr_ctx {
   FILE* prof_file = nullptr;  // SR_K2_PROFILE: per-wave K2 records appended per run
   int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
   size_t patch_min_bytes = 512u << 10;  // SR_PATCH_MIN_BYTES: node sections below go up whole
-  int32_t k2_narrow = 1;      // SR_K2_NARROW: 32-bit scaled run passes in node order (0: 64-bit only)
+  int32_t k2_narrow = 1;      // SR_K2_NARROW: 32-bit scaled window visits in node order (0: 64-bit only)
   int32_t k2_node_kernel = 1; // SR_K2_NODE_KERNEL: node-order-only K2 kernel when every candidate takes that path
   int32_t s_head_only = 1;    // SR_S_HEAD_ONLY: K0 writes S-row heads only on rows wider than 64 words (0: never)
-  int32_t k2_scan_min = 2;    // SR_K2_SCAN_MIN: smallest node visit placed by prefix sums (65: never)
 };
 
 namespace {
@@ -369,7 +368,6 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.out_bytes = static_cast<uint32_t*>(ctx->out_bytes.p);
   d.d_min = static_cast<int32_t*>(ctx->dmin.p);
   d.k2_mode = ctx->k2_mode;
-  d.k2_scan_min = ctx->k2_scan_min;
   d.k2_narrow = ctx->k2_narrow;
   d.k2_node_kernel = ctx->k2_node_kernel;
   // Wide rows, every candidate on the node-order kernel (launch_k2's condition)
@@ -692,7 +690,6 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* path = std::getenv("SR_K2_PROFILE")) ctx->prof_file = std::fopen(path, "ab");
   if (const char* m = std::getenv("SR_K2_MODE")) ctx->k2_mode = std::atoi(m) == 1 ? 1 : 0;
   if (const char* m = std::getenv("SR_PATCH_MIN_BYTES")) ctx->patch_min_bytes = std::strtoull(m, nullptr, 10);
-  if (const char* m = std::getenv("SR_K2_SCAN_MIN")) ctx->k2_scan_min = std::max(1, std::atoi(m));
   if (const char* m = std::getenv("SR_K2_NARROW")) ctx->k2_narrow = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K2_NODE_KERNEL")) ctx->k2_node_kernel = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_S_HEAD_ONLY")) ctx->s_head_only = std::atoi(m) != 0;

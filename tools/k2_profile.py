@@ -12,10 +12,10 @@ Each sr_plan_run appends {int64 n_cand, int64 n_k0} + n_cand x 16 u64 (K2)
           update, c = wait for the next rows, d = next pod's first clean node
           + DMA issue;  [12] cycles waiting for speculative records
 Node-order waves ([5] == 2) reuse the fields: [6] placements, [7] visits |
-windows << 32, [8] prologue (F heads) cycles, [9] min + window + node
-state, [10] placement, [11] pointer moves (+ far resolution), [14] cycles
-from wave start to the pod records and window 0 in registers, [15] cycles
-in run-pass visits << 1 | 1 if the candidate's run passes are 32-bit scaled.
+windows << 32, [8] prologue (F heads) cycles, [9] min + window load,
+[10] placement (window visits), [11] pointer moves (+ far resolution), [14]
+cycles from wave start to the pod records and window 0 in registers, [15] 1
+if the candidate's window visits use 32-bit scaled state.
 The last of the widest runs in the file is summarised (earlier ones are
 warmup; narrower ones are prefix batches of sr_plan_first)."""
 import sys
@@ -87,13 +87,11 @@ def main():
             " ".join("%.0f" % x for x in np.percentile(q[:, 14], [50, 90, 100])),
             " ".join("%.0f" % x for x in np.percentile(q[:, 8], [50, 90, 100]))))
         sv = max(1, vis.sum())
-        print("node order: cycles/visit min+window+state %.0f, placement %.0f, pointer moves %.0f"
+        print("node order: cycles/visit min+window %.0f, placement %.0f, pointer moves %.0f"
               % (q[:, 9].sum() / sv, q[:, 10].sum() / sv, q[:, 11].sum() / sv))
         print("node order: placement cycles per placed pod %.0f" % (q[:, 10].sum() / max(1, q[:, 6].sum())))
         print("node order: wave dur us p50/p90/max %s" % pct(dur[nodeo]))
-        runv = (q[:, 13] & 0xffffffff).astype(np.int64)
-        print("node order: 32-bit scaled placement in %d of %d waves; cycles per run-pass visit %.0f"
-              % (int((q[:, 15] & 1).sum()), len(q), (q[:, 15] >> 1).sum() / max(1, runv.sum())))
+        print("node order: 32-bit scaled window visits in %d of %d waves" % (int((q[:, 15] & 1).sum()), len(q)))
     if (~nodeo).any():
         print("pod order:  wave dur us p50/p90/max %s" % pct(dur[~nodeo]))
     r = r[~nodeo] if (~nodeo).any() else r
@@ -106,19 +104,13 @@ def main():
     print("cycles/step by section a,b,c,d,spec-wait:", " ".join("%.0f" % (x / st) for x in tot))
     last = np.argsort(-end)[:8]
     full = runs[last_run].astype(np.int64)
-    nodeo_rows = full[full[:, 5] == 2] if len(full) else full
-    if len(nodeo_rows):
-        ri, si = nodeo_rows[:, 12] & 0xffffffff, nodeo_rows[:, 12] >> 32
-        rv, sv = nodeo_rows[:, 13] & 0xffffffff, nodeo_rows[:, 13] >> 32
-        print("node order placement: run-pass visits %d (%.2f passes each), pod-by-pod visits %d (%.2f rounds each)"
-              % (rv.sum(), ri.sum() / max(1, rv.sum()), sv.sum(), si.sum() / max(1, sv.sum())))
     print("latest-ending waves: wave start_us dur_us steps mode | visits placements windows | "
-          "cycles: entry->records prologue min+state placement moves | run visits/passes seq visits/rounds")
+          "cycles: entry->records prologue min+window placement moves | 32-bit")
     for c in last:
         f = full[c]
-        print("  %5d %6.2f %6.2f %4d %2d | %3d %3d %3d | %6d %6d %6d %6d %6d | %3d/%3d %3d/%3d"
+        print("  %5d %6.2f %6.2f %4d %2d | %3d %3d %3d | %6d %6d %6d %6d %6d | %d"
               % (c, start[c], dur[c], steps[c], mode[c], f[7] & 0xffffffff, f[6], f[7] >> 32, f[14],
-                 f[8], f[9], f[10], f[11], f[13] & 0xffffffff, f[12] & 0xffffffff, f[13] >> 32, f[12] >> 32))
+                 f[8], f[9], f[10], f[11], f[15] & 1))
 
 
 if __name__ == "__main__":
