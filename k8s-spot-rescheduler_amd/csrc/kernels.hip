@@ -153,6 +153,17 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
       if (p && lane == 0) p[1] = __builtin_amdgcn_s_memrealtime();
     }
   } stamp{prof, lane};
+  // node patches (the few spot nodes changed since the generation the node
+  // section holds): written here for K2; the T rows below read them directly
+  if (blockIdx.x == 0 && wave == 0 && w.n_node_patch > 0 && lane < 11) {
+    for (int p = 0; p < w.n_node_patch; ++p) {
+      const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
+      const size_t node = static_cast<size_t>(pr[0]);
+      if (lane < 8) const_cast<uint64_t*>(w.node_rec)[node * 8 + lane] = pr[1 + lane];
+      else const_cast<int64_t*>(w.node_free)[static_cast<size_t>(lane - 8) * w.n_pad + node] =
+          static_cast<int64_t>(pr[1 + lane]);
+    }
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     unsigned long long* dm = reinterpret_cast<unsigned long long*>(w.d_min);
     dm[0] = ~0ull;
@@ -245,7 +256,11 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
       const int nvalid = max(0, min(64, w.n_spot - 64 * W));
       word = nvalid >= 64 ? ~0ull : (1ull << nvalid) - 1;
     } else {
-      const uint64_t fv = static_cast<uint64_t>(w.node_free[static_cast<size_t>(d - 1) * w.n_pad + 64 * W + lane]);
+      uint64_t fv = static_cast<uint64_t>(w.node_free[static_cast<size_t>(d - 1) * w.n_pad + 64 * W + lane]);
+      for (int p = 0; p < w.n_node_patch; ++p) {  // wave-uniform; block 0 may not have written them yet
+        const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
+        if (static_cast<uint64_t>(64 * W + lane) == pr[0]) fv = pr[8 + d];
+      }
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int i = 0; i < 32; ++i) lo |= static_cast<uint32_t>(static_cast<int64_t>(readlane64(fv, i)) >= thr) << i;

@@ -18,6 +18,7 @@ constexpr int kDevDynU64 = 5 * kDevDynG + 1 + kDevSpreadSlots * (kDevDynG + 3);
                                         // kDevDynG mask words, kDevDynG affinity mask words, the set word,
                                         // per spread slot kDevDynG mask words and 3 info words (SpreadDyn)
 constexpr int kDevDomKeys = 4;          // key slots (host.hpp kDomKeys)
+constexpr int kNodePatchU64 = 12;       // node patch: {node, node_rec[8], node_free[3]}
 constexpr int kDevDynTerms = 4;         // terms per domain-path affinity set (host.hpp kDynTerms)
 
 // Pointers into the device arena (layout: DESIGN.md §HBM layout).
@@ -25,6 +26,8 @@ struct DevWorkload {
   int32_t n_spot, n_pad, Wp;
   const int64_t* node_free;    // [3][n_pad] free cpu / memory / ephemeral per spot node (pads: INT64_MIN)
   const uint64_t* node_rec;    // [n_pad][8] AoS {free cpu, mem, eph, state bits, pods_left, 0, 0, 0} for K2
+  const uint64_t* node_patch;  // [n_node_patch][kNodePatchU64]: records of nodes changed since the generation the
+  int32_t n_node_patch;        //   node section holds; K0 writes them there (T rows use them directly)
   int32_t n_atoms;
   const uint64_t* atoms;       // [n_atoms][Wp] node bitsets (encode.cpp)
   const int32_t* cls_prog_off; // class atom programs (CSR): ops atom << 2 | {AND, AND NOT,

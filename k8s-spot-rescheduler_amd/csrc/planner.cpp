@@ -79,6 +79,7 @@ struct sr_ctx {
   uint64_t issued_checks = 0;  // checks of the prepared workload's plan (known after a full run)
   bool issued_known = false;
   sr::Workload wl;
+  std::vector<uint64_t> node_patch_words;  // this call's node patches (prepare)
   sr::EncoderCache enc;      // what the encoder keeps across calls (encode.cpp)
   uint64_t dev_state_gen = ~0ull;  // encoder state whose node records the device arena holds
   uint64_t host_state_gen = ~0ull; // ... and the pinned staging arena (kept between calls)
@@ -104,7 +105,8 @@ struct sr_ctx {
   int64_t last_rank_next = -1;  // reduced smallest unplanned global index of the last collective run (-1: none)
   FILE* prof_file = nullptr;  // SR_K2_PROFILE: per-wave K2 records appended per run
   int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
-  size_t patch_min_bytes = 512u << 10;  // SR_PATCH_MIN_BYTES: node sections below go up whole
+  int32_t node_patch = 1;     // SR_NODE_PATCH=0: a changed node section always goes up whole
+  bool patch_pending = false;  // a prepare left node patches for K0 that no run has applied yet
   int32_t k2_narrow = 1;      // SR_K2_NARROW: 32-bit scaled window visits in node order (0: 64-bit only)
   int32_t k2_node_kernel = 1; // SR_K2_NODE_KERNEL: node-order-only K2 kernel when every candidate takes that path
   int32_t s_head_only = 1;    // SR_S_HEAD_ONLY: K0 writes S-row heads only on rows wider than 64 words (0: never)
@@ -248,6 +250,23 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t o_dc = dyn ? pk.add(w.dyn_cand) : 0, o_dp = dyn ? pk.add(w.dyn_pod) : 0;
   const size_t o_dd = dyn ? pk.add(w.dk_dom) : 0, o_di = dyn ? pk.add(w.ds_info) : 0;
   const size_t o_st = dyn ? pk.add(w.sp_tab) : 0;
+  // Records of the few spot nodes the encoder patched since the last
+  // generation, {node, node_rec[8], node_free[3]} each: when the device holds
+  // that generation they ride in this call's copy and K0 writes them into
+  // the node section (no copy of the whole section, no copy per node).
+  constexpr size_t kPatchNodes = 8;
+  std::vector<uint64_t>& patch = ctx->node_patch_words;
+  patch.clear();
+  if (E.patched_from != ~0ull && E.state_gen == w.state_gen && !E.patched_nodes.empty() &&
+      E.patched_nodes.size() <= kPatchNodes) {
+    const size_t NP = static_cast<size_t>(w.n_pad);
+    for (int32_t i : E.patched_nodes) {
+      patch.push_back(static_cast<uint64_t>(i));
+      for (size_t j = 0; j < 8; ++j) patch.push_back(E.node_rec[static_cast<size_t>(i) * 8 + j]);
+      for (size_t dm = 0; dm < 3; ++dm) patch.push_back(static_cast<uint64_t>(E.node_free[dm * NP + i]));
+    }
+  }
+  const size_t o_np = patch.empty() ? 0 : pk.add(patch);
   const size_t bytes = pk.size();
 
   HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -260,13 +279,12 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t arena_cap = ctx->arena.cap;
   HIP_TRY(ctx, dev_reserve(ctx->arena, bytes));  // a new allocation holds no node records
   const bool same_arena = ctx->arena.cap == arena_cap;
+  if (ctx->patch_pending) ctx->dev_state_gen = ~0ull;  // the last prepare's patches never reached the device
   const bool nodes_resident = same_arena && ctx->dev_state_gen == w.state_gen;
-  // a few nodes changed since the generation on the device: upload just their
-  // records (4 small copies each) instead of the whole node section
-  constexpr size_t kPatchNodes = 8;
-  const bool nodes_patch = !nodes_resident && same_arena && ctx->dev_state_gen == E.patched_from &&
-                           E.state_gen == w.state_gen && !E.patched_nodes.empty() &&
-                           E.patched_nodes.size() <= kPatchNodes && node_bytes > ctx->patch_min_bytes;
+  // a few nodes changed since the generation on the device: K0 applies their
+  // records from this call's copy
+  const bool nodes_patch = ctx->node_patch && !nodes_resident && same_arena && ctx->dev_state_gen == E.patched_from &&
+                           !patch.empty();
   const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
   HIP_TRY(ctx, dev_reserve(ctx->tables, n_rows * row_bytes));
@@ -301,27 +319,12 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
     ctx->host_state_gen = w.state_gen;
   }
   pk.copy_to(static_cast<char*>(ctx->h_arena.p), node_bytes);
-  size_t patch_bytes = 0;
-  if (nodes_patch) {
-    char* hs = static_cast<char*>(ctx->h_arena.p);
-    char* ds = static_cast<char*>(ctx->arena.p);
-    const size_t NP = static_cast<size_t>(w.n_pad);
-    auto put = [&](size_t off, const void* src, size_t n) -> hipError_t {  // the staging copy is current
-      (void)src;
-      patch_bytes += n;
-      return hipMemcpyAsync(ds + off, hs + off, n, hipMemcpyHostToDevice, ctx->stream);
-    };
-    for (int32_t i : E.patched_nodes) {
-      HIP_TRY(ctx, put(o_nr + static_cast<size_t>(i) * 64, &E.node_rec[static_cast<size_t>(i) * 8], 64));
-      for (size_t dm = 0; dm < 3; ++dm)
-        HIP_TRY(ctx, put(o_nf + (dm * NP + static_cast<size_t>(i)) * 8, &E.node_free[dm * NP + i], 8));
-    }
-  }
   HIP_TRY(ctx, hipMemcpyAsync(static_cast<char*>(ctx->arena.p) + from, static_cast<char*>(ctx->h_arena.p) + from,
                               bytes - from, hipMemcpyHostToDevice, ctx->stream));
   if (!ctx->ev_upload) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_upload, hipEventDisableTiming));
   HIP_TRY(ctx, hipEventRecord(ctx->ev_upload, ctx->stream));  // kernels queue behind the copy
   ctx->dev_state_gen = w.state_gen;
+  ctx->patch_pending = nodes_patch;
   auto t2 = std::chrono::steady_clock::now();
 
   char* base = static_cast<char*>(ctx->arena.p);
@@ -396,7 +399,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, hipHostGetDevicePointer(&dres, ctx->h_early.p, 0));
   ctx->d_early = static_cast<uint64_t*>(dres);
   d.res_stat = d.res_map = nullptr;  // set per run
-  ctx->t.bytes_uploaded = static_cast<uint64_t>(bytes - from + patch_bytes);
+  ctx->t.bytes_uploaded = static_cast<uint64_t>(bytes - from);
+  d.node_patch = nodes_patch ? static_cast<const uint64_t*>(at(o_np)) : nullptr;
+  d.n_node_patch = nodes_patch ? static_cast<int32_t>(patch.size() / sr::kNodePatchU64) : 0;
 
   const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
   // K0 algorithmic bytes: every table row written once; every atom row a class
@@ -548,6 +553,7 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   } while (0)
   PAIR(0, e0a, e0b);
   HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
+  ctx->patch_pending = false;  // K0 writes the node patches (idempotent on later runs)
   PAIR(1, e1a, e1b);
   if (early) {
     d.res_stat = ctx->d_early;
@@ -689,7 +695,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   }
   if (const char* path = std::getenv("SR_K2_PROFILE")) ctx->prof_file = std::fopen(path, "ab");
   if (const char* m = std::getenv("SR_K2_MODE")) ctx->k2_mode = std::atoi(m) == 1 ? 1 : 0;
-  if (const char* m = std::getenv("SR_PATCH_MIN_BYTES")) ctx->patch_min_bytes = std::strtoull(m, nullptr, 10);
+  if (const char* m = std::getenv("SR_NODE_PATCH")) ctx->node_patch = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K2_NARROW")) ctx->k2_narrow = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K2_NODE_KERNEL")) ctx->k2_node_kernel = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_S_HEAD_ONLY")) ctx->s_head_only = std::atoi(m) != 0;

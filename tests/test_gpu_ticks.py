@@ -118,30 +118,32 @@ def _snapshot(lib, sc, nm):
 
 
 @pytest.fixture(scope="module")
-def patch_checker():
-    """A planner that uploads changed node records one by one at any pool size
-    (SR_PATCH_MIN_BYTES=0; by default only node sections above 512 KiB are patched)."""
+def whole_checker():
+    """A planner that uploads a changed node section whole (SR_NODE_PATCH=0; by
+    default the records of up to 8 changed nodes ride in the call's copy and K0
+    writes them into the resident section)."""
     from spotplanner.planner import PredicateChecker
-    os.environ["SR_PATCH_MIN_BYTES"] = "0"
+    os.environ["SR_NODE_PATCH"] = "0"
     try:
         c = PredicateChecker(0)
     finally:
-        del os.environ["SR_PATCH_MIN_BYTES"]
+        del os.environ["SR_NODE_PATCH"]
     yield c
     c.close()
 
 
 @pytest.mark.parametrize("config", [3, 5])
-@pytest.mark.parametrize("which", ["default", "patch"])
-def test_consecutive_ticks_one_node_changed(checker, patch_checker, which, config):
+@pytest.mark.parametrize("which", ["default", "whole"])
+def test_consecutive_ticks_one_node_changed(checker, whole_checker, which, config):
     """Tick after tick on fresh snapshots of one cluster, each with one more
     pod placed on some spot node (its state changes, the static view not):
-    every full plan equals the oracle on the same mutated snapshot.  `patch`:
-    the changed nodes' records go to the device one by one.  Config 5: the
+    every full plan equals the oracle on the same mutated snapshot.  `default`:
+    the changed nodes' records go to the device with the call's copy and K0
+    applies them; `whole`: the changed node section goes up whole.  Config 5: the
     added pods carry host ports, so the cached base port-conflict rows are
     patched node by node."""
-    other = checker
-    checker = patch_checker if which == "patch" else checker
+    other = whole_checker
+    checker = whole_checker if which == "whole" else checker
     sc = SynthCluster(config, seed=21, n_on_demand=200, n_spot=450)
     lib = capi.load_planner()
     nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
@@ -158,9 +160,9 @@ def test_consecutive_ticks_one_node_changed(checker, patch_checker, which, confi
             osnap.lib.oracle_snapshot_add_pod(osnap.h, sc.ptr, pod, pos)
         p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
         t = checker.timing()
-        if which == "patch":  # the same tick through the default planner: its upload for comparison
+        if which == "default":  # the same tick through the whole-section planner: its upload for comparison
             plan_arrays(other, h, sc.ptr, cand_off, cand_pods)
-            up_default = other.timing().bytes_uploaded
+            up_whole = other.timing().bytes_uploaded
         o = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
         assert np.array_equal(p.status, o["status"]), tick
         assert np.array_equal(p.node_of_pod, o["node_of_pod"]), tick
@@ -168,9 +170,9 @@ def test_consecutive_ticks_one_node_changed(checker, patch_checker, which, confi
         if tick >= 2:  # steady state: one node's state re-encoded, no spec is new
             assert t.enc_static_rebuilt == 0 and t.enc_state_nodes <= 2 and t.enc_new_specs == 0, \
                 (t.enc_static_rebuilt, t.enc_state_nodes, t.enc_new_specs)
-            if which == "patch":  # <= 2 node records (64 B + 3 free values each) instead of the section
+            if which == "default":  # <= 2 node patches in the call's copy instead of the section
                 n_pad = (len(nm.spot) + 127) // 128 * 128
-                assert up_default - t.bytes_uploaded >= n_pad * 88 - 256 - 2 * 88, (up_default, t.bytes_uploaded)
+                assert up_whole - t.bytes_uploaded >= n_pad * 88 - 256, (up_whole, t.bytes_uploaded)
         lib.sr_snapshot_destroy(h)
 
 

@@ -32,9 +32,9 @@ def main():
     ap.add_argument("--wide", action="store_true", help="C4-shaped clusters (5,000-node pools: rows over 64 words)")
     a = ap.parse_args()
     lib = capi.load_planner()
-    os.environ["SR_PATCH_MIN_BYTES"] = "0"  # the second planner uploads changed records one by one
+    os.environ["SR_NODE_PATCH"] = "0"  # the second planner uploads a changed node section whole
     patcher = PredicateChecker(0)
-    del os.environ["SR_PATCH_MIN_BYTES"]
+    del os.environ["SR_NODE_PATCH"]
     default = PredicateChecker(0)
     t0, ticks = time.time(), 0
     rng = np.random.default_rng(11)
