@@ -431,11 +431,29 @@ sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* e
       for (int d = 0; d < 3; ++d) {  // the sorted values with multiplicity, and the distinct ones
         std::vector<int64_t>& s = C.sorted_free[d];
         std::vector<int64_t>& v = C.node_vals[d];
-        const int64_t old = C.node_free[static_cast<size_t>(d) * NP + i];
-        s.erase(std::lower_bound(s.begin(), s.end(), old));
-        if (!std::binary_search(s.begin(), s.end(), old)) v.erase(std::lower_bound(v.begin(), v.end(), old));
-        if (!std::binary_search(s.begin(), s.end(), f[d])) v.insert(std::lower_bound(v.begin(), v.end(), f[d]), f[d]);
-        s.insert(std::upper_bound(s.begin(), s.end(), f[d]), f[d]);
+        const int64_t old = C.node_free[static_cast<size_t>(d) * NP + i], nv = f[d];
+        if (old == nv) continue;
+        // old leaves the distinct values when it was its only copy; nv enters them when absent
+        const bool old_goes = std::upper_bound(s.begin(), s.end(), old) - std::lower_bound(s.begin(), s.end(), old) == 1;
+        const bool nv_comes = !std::binary_search(s.begin(), s.end(), nv);
+        // one value replaced by another in a sorted array: only the span between
+        // their places moves (a node's free value usually moves a little)
+        auto replace_sorted = [](std::vector<int64_t>& a, int64_t from, int64_t to) {
+          const auto at = std::lower_bound(a.begin(), a.end(), from);
+          if (to > from) {
+            const auto ub = std::upper_bound(at + 1, a.end(), to);
+            std::move(at + 1, ub, at);
+            *(ub - 1) = to;
+          } else {
+            const auto ub = std::upper_bound(a.begin(), at, to);
+            std::move_backward(ub, at, at + 1);
+            *ub = to;
+          }
+        };
+        replace_sorted(s, old, nv);
+        if (old_goes && nv_comes) replace_sorted(v, old, nv);
+        else if (old_goes) v.erase(std::lower_bound(v.begin(), v.end(), old));
+        else if (nv_comes) v.insert(std::lower_bound(v.begin(), v.end(), nv), nv);
       }
       write_node(i, f, left);
     }

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../k8s-spot-rescheduler_amd/csrc/host.hpp"
@@ -96,6 +97,41 @@ int main(int argc, char** argv) {
   printf("one-node-changed encode (fresh snapshot) best %.3f ms (state nodes %d, static rebuilt %d)\n", best,
          last_state, last_static);
   phases("1node");
+  if (argc > 3 && std::string(argv[3]) == "check") {
+    // the state view patched node by node equals the one rebuilt from scratch:
+    // consecutive fresh snapshots, each with a few more pods on random spot nodes
+    std::vector<std::pair<int32_t, int32_t>> extra;
+    uint64_t x = 88172645463325252ull;
+    auto rnd = [&](uint64_t n) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x % n; };
+    int ticks = 0, patched = 0;
+    for (int r = 0; r < 300 && !cp.empty(); ++r) {
+      sr_snapshot* s2 = nullptr;
+      sr_snapshot_create(&c, spot.data(), ns, off.data(), idx.data(), &s2);
+      if (r % 7 == 6) extra.clear();  // sometimes the extra pods leave again
+      const int add = 1 + static_cast<int>(rnd(3));
+      for (int a = 0; a < add; ++a)
+        extra.emplace_back(cp[rnd(cp.size())], static_cast<int32_t>(rnd(static_cast<uint64_t>(ns))));
+      for (auto& e : extra) sr_snapshot_add_pod(s2, &c, e.first, e.second);
+      sr::encode_workload(&cache, s2, &c, &cands, &w, &err);
+      patched += cache.patched_from != ~0ull;
+      sr::EncoderCache fresh;
+      sr::Workload w2;
+      sr::encode_workload(&fresh, s2, &c, &cands, &w2, &err);
+      for (int d = 0; d < 3; ++d)
+        if (cache.sorted_free[d] != fresh.sorted_free[d] || cache.node_vals[d] != fresh.node_vals[d]) {
+          printf("views differ at tick %d, dimension %d\n", r, d);
+          return 2;
+        }
+      if (cache.node_rec != fresh.node_rec || cache.node_free != fresh.node_free ||
+          cache.podcount_row != fresh.podcount_row) {
+        printf("node records differ at tick %d\n", r);
+        return 2;
+      }
+      sr_snapshot_destroy(s2);
+      ++ticks;
+    }
+    printf("state views consistent: %d ticks (%d patched node by node)\n", ticks, patched);
+  }
   printf("Wp %d atoms %d classes %d program ops %zu t_rows %zu\n", w.Wp, w.n_atoms, w.n_classes, w.cls_prog.size(),
          w.t_dim.size());
   int tc[4] = {0, 0, 0, 0};
