@@ -1342,9 +1342,10 @@ static_assert(64 * 32 * 8 <= sizeof(K2Lds), "domain path: touched bitmap of 2048
 // state.  A pod record holds, per key slot, G mask words over the earlier
 // pods, G affinity mask words and the set word (kDevDynU64 words, layout of
 // encode.cpp).
-template <int CH, int G>
+template <int CH, int G, bool PROF>
 __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __restrict__ tl, const int p0,
-                                          const int np, const int dbase, int& status, uint32_t& nbytes) {
+                                          const int np, const int dbase, int& status, uint32_t& nbytes,
+                                          K2Stats& st) {
   static_assert(kDevDomKeys == 4 && kDevDynTerms == 4, "the selects below unroll 4 key slots / terms");
   static_assert(G >= 1 && G <= kDevDynG, "pod groups of the domain-path record");
   const int lane = threadIdx.x & 63;
@@ -1372,13 +1373,34 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
   nbytes += (48u + 8u * kDevDynU64 + 4u) * static_cast<uint32_t>(np) + 4u;
   status = -1;
   int k = 0;
+  // A pod's records in one register, lanes [0, kDevDynU64) its domain-path
+  // record, lanes [40, 46) its pod record, loaded one pod ahead (every pod
+  // step otherwise starts with a memory round trip for them)
+  static_assert(kDevDynU64 <= 40 && kRecU64 <= 24, "record lanes of the domain path");
+  auto records = [&](int q) -> uint64_t {
+    if (q >= np) return 0ull;
+    if (lane < kDevDynU64) return w.dyn_pod[static_cast<size_t>(dbase + q) * kDevDynU64 + lane];
+    if (lane >= 40 && lane < 40 + kRecU64) return w.pod_rec[static_cast<size_t>(p0 + q) * kRecU64 + (lane - 40)];
+    return 0ull;
+  };
+  uint64_t rv = records(0);
+  uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
+  auto stamp = [&](uint64_t& acc) {
+    if (PROF) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      acc += t - cyc_t;
+      cyc_t = t;
+    }
+  };
   for (; k < np; ++k) {
-    const uint64_t* pr = w.pod_rec + static_cast<size_t>(p0 + k) * kRecU64;
-    const int64_t rc = static_cast<int64_t>(pr[0]), rm = static_cast<int64_t>(pr[1]), re = static_cast<int64_t>(pr[2]);
-    const uint64_t pm = pr[3], r01 = pr[4], r23 = pr[5];
+    const uint64_t cur = rv;
+    rv = records(k + 1);
+    auto D = [&](int i) { return readlane64(cur, i); };        // domain-path record word i
+    auto PR = [&](int i) { return readlane64(cur, 40 + i); };  // pod record word i
+    const int64_t rc = static_cast<int64_t>(PR(0)), rm = static_cast<int64_t>(PR(1)), re = static_cast<int64_t>(PR(2));
+    const uint64_t pm = PR(3), r01 = PR(4), r23 = PR(5);
     const uint64_t pin = swap_pairs(pm, w.swap_mask);
     const bool zero = (rc | rm | re) == 0;
-    const uint64_t* dr = w.dyn_pod + static_cast<size_t>(dbase + k) * kDevDynU64;
     // anti-affinity: domains refused per key slot (earlier pods it interacts with)
     uint64_t fdom[kDevDomKeys];
 #pragma unroll
@@ -1386,13 +1408,14 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
       uint64_t any = 0, bits = 0;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const uint64_t m = kk < w.n_dk ? dr[kk * kDevDynG + g] : 0ull;
+        const uint64_t m = kk < w.n_dk ? D(kk * kDevDynG + g) : 0ull;
         any |= m;
         const bool in = 64 * g + lane < k && ((m >> lane) & 1) && pdom[g][kk] >= 0;
         bits |= in ? 1ull << pdom[g][kk] : 0ull;
       }
       fdom[kk] = any != 0 ? wave_or(bits) : 0ull;
     }
+    stamp(st.cyc_a);
     // topology spread planned here (SpreadDyn, encode.cpp): the pair counts
     // with the earlier pods the constraint counts.  Table key: base count per
     // domain in lane d, plus those pods domain by domain, the minimum over the
@@ -1403,19 +1426,19 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
     for (int g = 0; g < G; ++g) nlref[g] = 0;
 #pragma unroll
     for (int s2 = 0; s2 < kDevSpreadSlots; ++s2) {
-      const uint64_t* sw = dr + 5 * kDevDynG + 1 + s2 * (kDevDynG + 3);
-      const uint64_t i0 = sw[kDevDynG];
+      const int sw = 5 * kDevDynG + 1 + s2 * (kDevDynG + 3);  // the slot's words in the record
+      const uint64_t i0 = D(sw + kDevDynG);
       if (i0 == ~0ull) continue;  // wave-uniform
       const int kk = static_cast<int>(i0 & 3);
       const bool nl = ((i0 >> 2) & 1) != 0;
       const int self = static_cast<int>((i0 >> 3) & 1);
       const int64_t skew = static_cast<int32_t>(static_cast<uint32_t>(i0 >> 32));
-      const uint32_t off = static_cast<uint32_t>(sw[kDevDynG + 1]);
+      const uint32_t off = static_cast<uint32_t>(D(sw + kDevDynG + 1));
       uint64_t rem[G];
       int pd[G];  // the pod's domain of key slot kk
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        rem[g] = sw[g] & ballot(64 * g + lane < k);  // every earlier pod is placed
+        rem[g] = D(sw + g) & ballot(64 * g + lane < k);  // every earlier pod is placed
         int d = -1;
 #pragma unroll
         for (int k2 = 0; k2 < kDevDomKeys; ++k2) d = k2 == kk ? pdom[g][k2] : d;
@@ -1423,8 +1446,8 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
       }
       nbytes += 8u * (kDevDynG + 3) + 256u;
       if (!nl) {
-        const int edom = static_cast<int32_t>(static_cast<uint32_t>(sw[kDevDynG + 1] >> 32));
-        const uint64_t pm = sw[kDevDynG + 2];
+        const int edom = static_cast<int32_t>(static_cast<uint32_t>(D(sw + kDevDynG + 1) >> 32));
+        const uint64_t pm = D(sw + kDevDynG + 2);
 #pragma unroll
         for (int g = 0; g < G; ++g) pd[g] = pd[g] >= 0 ? pd[g] : edom;  // a keyless node: the pair of ""
         int cv = w.sp_tab[off + lane];
@@ -1483,7 +1506,7 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
     }
     // affinity: per term its key slot, base row and the earlier matching pods'
     // domains (table key) or pods (node-local key: adom holds their lanes per group)
-    const uint64_t meta = dr[5 * kDevDynG];
+    const uint64_t meta = D(5 * kDevDynG);
     int nt = 0;
     int tslot[kDevDynTerms] = {0, 0, 0, 0}, tbase[kDevDynTerms] = {0, 0, 0, 0};
     uint64_t adom[kDevDynTerms][G];
@@ -1506,7 +1529,7 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
         uint64_t bits = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-          const uint64_t mm = dr[4 * kDevDynG + g];
+          const uint64_t mm = D(4 * kDevDynG + g);
           int d = -1;
 #pragma unroll
           for (int kk = 0; kk < kDevDomKeys; ++kk) d = kk == tslot[i] ? pdom[g][kk] : d;
@@ -1520,6 +1543,7 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
       }
       if (!map_has && self) nt = 0;  // first pod of a self-affine group: KEYS(S) (in its class) only
     }
+    stamp(st.cyc_b);
     int ans = INT_MAX;
     for (int ch = 0; ch < CH && ans == INT_MAX && ch * 64 < Wp; ++ch) {
       const int wd = ch * 64 + lane;
@@ -1602,6 +1626,7 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
       }
       ans = min(cn, wave_min(best));
     }
+    stamp(st.cyc_c);
     if (ans == INT_MAX) {  // "pod %s can't be rescheduled on any existing spot node"
       status = k;
       break;
@@ -1652,6 +1677,7 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
 #pragma unroll
         for (int kk = 0; kk < kDevDomKeys; ++kk) pdom[g][kk] = dn[kk];
       }
+    stamp(st.cyc_d);
   }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -1760,8 +1786,8 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   const int dbase = w.dyn_cand ? __builtin_amdgcn_readfirstlane(w.dyn_cand[ci]) : -1;
   if (dbase >= 0) {  // writes out_node itself
     wide = 3;
-    if (np <= 64) k2_domain<CH, 1>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes);
-    else k2_domain<CH, kDevDynG>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes);
+    if (np <= 64) k2_domain<CH, 1, PROF>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes, st);
+    else k2_domain<CH, kDevDynG, PROF>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes, st);
   } else if (node_order) {  // writes out_node itself
     uint64_t* F = reinterpret_cast<uint64_t*>(&L);
     wide = 2;
