@@ -697,7 +697,11 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
 // window moves or a pointer moves beyond the head.  Measured against visiting
 // one node at a time (prefix-sum run passes over the pods pointing at it):
 // C3 K2 17.7 -> 13.1 us, C5 61 -> 42 us.
-constexpr int kNH = 8;             // F head words per pod kept in LDS (nodes [0, 512))
+#ifndef SR_K2_NH
+#define SR_K2_NH 8
+#endif
+constexpr int kNH = SR_K2_NH;      // F head words per pod kept in LDS (8: nodes [0, 512))
+static_assert(kNH == 2 || kNH == 4 || kNH == 8, "head words per pod: a power of two up to 8 (8-bit head masks)");
 constexpr int kNHS = kNH + 1;      // LDS stride per pod (odd number of words: conflict-free b64 reads)
 constexpr int kFar = 64 * kNH;     // pointer sentinel: next feasible node lies at or beyond the head, unresolved
 
@@ -970,28 +974,26 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   // each), full-row scans and far words, the mapping and status writes
   nbytes += (48u + 4u) * static_cast<uint32_t>(np) + 4u + 32u * static_cast<uint32_t>(min(Wp, kNH)) * dead;
 
-  // F heads of pods [0, dead): lanes = 8 pods x 8 words, kPB such batches per
-  // step with all their loads in flight together (one memory round trip per
-  // 8 * kPB pods)
+  // F heads of pods [0, dead): lanes = kPW pods x kNH words, kPB such batches
+  // per step with all their loads in flight together (one memory round trip
+  // per kPW * kPB pods)
   {
-#ifndef SR_K2_PROLOGUE_BATCHES
-#define SR_K2_PROLOGUE_BATCHES 0
-#endif
+    constexpr int kPW = 64 / kNH;  // pods per load instruction
     // up to 64 pods in one round trip (G = 1), 32 per round beyond
-    constexpr int kPB = SR_K2_PROLOGUE_BATCHES > 0 ? SR_K2_PROLOGUE_BATCHES : (G == 1 ? 8 : 4);
-    const int sub = lane >> 3, wd = lane & 7;
+    constexpr int kPB = (G == 1 ? 64 : 32) / kPW;
+    const int sub = lane / kNH, wd = lane % kNH;
     const bool wv = wd < Wp;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int lim = min(dead, 64 * g + 64);
-      for (int b0 = 64 * g; b0 < lim; b0 += 8 * kPB) {
+      for (int b0 = 64 * g; b0 < lim; b0 += kPW * kPB) {
         uint64_t x[kPB][4];
         int kk[kPB];
 #pragma unroll
         for (int h = 0; h < kPB; ++h) {
-          kk[h] = b0 + 8 * h + sub;
+          kk[h] = b0 + kPW * h + sub;
           x[h][0] = x[h][1] = x[h][2] = x[h][3] = 0;
-          if (b0 + 8 * h >= lim) continue;  // wave-uniform
+          if (b0 + kPW * h >= lim) continue;  // wave-uniform
           const int src = min(kk[h], np - 1) - 64 * g;  // lane of that pod in group g
           const uint32_t o0 = from_lane(static_cast<uint32_t>(r01[g]), src);
           const uint32_t o1 = from_lane(static_cast<uint32_t>(r01[g] >> 32), src);
@@ -1005,12 +1007,12 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         }
 #pragma unroll
         for (int h = 0; h < kPB; ++h) {
-          if (b0 + 8 * h >= lim) continue;  // wave-uniform
+          if (b0 + kPW * h >= lim) continue;  // wave-uniform
           const uint64_t f = (wv && kk[h] < np) ? (x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
           if (kk[h] < np) F[kk[h] * kNHS + wd] = f;
-          const uint64_t m = ballot(f != 0);  // 8 bits per pod: bit 8 * i + word
-          const int rel = 64 * g + lane - (b0 + 8 * h);
-          if (rel >= 0 && rel < 8) hmask[g] = static_cast<uint32_t>(m >> (8 * rel)) & 0xffu;
+          const uint64_t m = ballot(f != 0);  // kNH bits per pod: bit kNH * i + word
+          const int rel = 64 * g + lane - (b0 + kPW * h);
+          if (rel >= 0 && rel < kPW) hmask[g] = static_cast<uint32_t>(m >> (kNH * rel)) & ((1u << kNH) - 1u);
         }
       }
     }
