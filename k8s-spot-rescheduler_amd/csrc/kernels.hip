@@ -743,7 +743,9 @@ __device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W,
                                                  int64_t re, uint64_t pm, uint64_t cur, uint64_t zm,
                                                  uint64_t swap_mask, uint64_t emask, int64_t& ncpu, int64_t& nmem,
                                                  int64_t& neph, uint64_t& nport, int& nleft, int& node) {
-  uint64_t placed = 0;
+  // jv: the lane each pod took (64: none), turned into node / placed once per
+  // visit (measured: the bookkeeping in the step costs ~14% of a step)
+  int jv = 64;
   if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
   // without state bits one branch per pod: a pod that fits nowhere selects
   // lane 64 (no lane)
@@ -768,8 +770,7 @@ __device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W,
           nleft -= 1;
           nport |= swap_pairs(q, swap_mask);  // the bits it sets
         }
-        if (lane == k) node = 64 * W + j;
-        placed |= 1ull << k;
+        jv = lane == k ? j : jv;
       }
       continue;
     }
@@ -779,10 +780,10 @@ __device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W,
     nmem -= hit ? m : 0;
     if (E) neph -= hit ? e : 0;
     nleft -= hit ? 1 : 0;
-    node = (lane == k && j < 64) ? 64 * W + j : node;
-    placed |= fit != 0 ? 1ull << k : 0ull;
+    jv = lane == k ? j : jv;
   }
-  return placed;
+  node = jv < 64 ? 64 * W + jv : node;
+  return ballot(jv < 64);
 }
 
 // The free value f of a node scaled to the candidate's request granularity
@@ -801,10 +802,16 @@ __device__ __forceinline__ int32_t scale32(int64_t f, int k) {
 // field instead of 64-bit pairs.
 template <bool E, bool O>
 __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int W, int lane, uint32_t nc, uint32_t nm,
-                                                   uint32_t ne, uint64_t pm, uint64_t cur, uint64_t zm,
-                                                   uint64_t swap_mask, uint64_t emask, int32_t& c32, int32_t& m32,
-                                                   int32_t& e32, uint64_t& nport, int& nleft, int& node) {
-  uint64_t placed = 0;
+                                                   uint32_t ne, uint64_t pm, uint64_t cur, uint64_t swap_mask,
+                                                   int32_t& c32, int32_t& m32, int32_t& e32, uint64_t& nport,
+                                                   int& nleft, int& node) {
+  // The zero-request exemption and the fixed ephemeral gate are in the
+  // values, not in the step: an all-zero request is INT_MIN in nc / nm / ne
+  // (it meets every state value), and without E a lane whose ephemeral free
+  // value is negative holds INT_MIN as its cpu state (it refuses every other
+  // request); the update subtracts max(request, 0).  Measured: the scalar
+  // selects cost ~10% of a step.
+  int jv = 64;  // as in place_window
   if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
   while (todo != 0) {
     const int k = __builtin_ctzll(todo);
@@ -813,35 +820,34 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
     const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
     const int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
     const uint64_t q = O ? readlane64(pm, k) : 0ull;
-    uint64_t fit = readlane64(cur, k) & ballot(nleft >= 1);
-    const uint64_t res = ballot(c32 >= c) & ballot(m32 >= m) & (E ? ballot(e32 >= e) : emask);
-    fit &= ((zm >> k) & 1) ? ~0ull : res;  // fitsRequest skips the resource checks
+    uint64_t fit = readlane64(cur, k) & ballot(nleft >= 1) & ballot(c32 >= c) & ballot(m32 >= m);
+    if (E) fit &= ballot(e32 >= e);
     if (O) fit &= ballot((nport & q) == 0);
+    const int32_t cu = max(c, 0), mu = max(m, 0), eu = max(e, 0);
     if (O) {  // as in place_window
       if (fit != 0) {
         const int j = __builtin_ctzll(fit);
         if (lane == j) {
-          c32 -= c;
-          m32 -= m;
-          if (E) e32 -= e;
+          c32 -= cu;
+          m32 -= mu;
+          if (E) e32 -= eu;
           nleft -= 1;
           nport |= swap_pairs(q, swap_mask);
         }
-        if (lane == k) node = 64 * W + j;
-        placed |= 1ull << k;
+        jv = lane == k ? j : jv;
       }
       continue;
     }
     const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
     const bool hit = lane == j;  // ClusterSnapshot.AddPod on the candidate's copy of node 64 W + j
-    c32 -= hit ? c : 0;
-    m32 -= hit ? m : 0;
-    if (E) e32 -= hit ? e : 0;
+    c32 -= hit ? cu : 0;
+    m32 -= hit ? mu : 0;
+    if (E) e32 -= hit ? eu : 0;
     nleft -= hit ? 1 : 0;
-    node = (lane == k && j < 64) ? 64 * W + j : node;
-    placed |= fit != 0 ? 1ull << k : 0ull;
+    jv = lane == k ? j : jv;
   }
-  return placed;
+  node = jv < 64 ? 64 * W + jv : node;
+  return ballot(jv < 64);
 }
 
 // A narrow candidate's request granularity per dimension: every request is a
@@ -911,9 +917,11 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       const uint64_t a = static_cast<uint64_t>(rc[g]) >> nk.kc, b = static_cast<uint64_t>(rm[g]) >> nk.km,
                      c = static_cast<uint64_t>(re[g]) >> nk.ke;
       ok = ok && (a | b | c) < (1ull << 23);
-      nc[g] = static_cast<uint32_t>(a);
-      nm[g] = static_cast<uint32_t>(b);
-      ne[g] = static_cast<uint32_t>(c);
+      // an all-zero request (fitsRequest skips the resource checks) compares
+      // as INT_MIN: every state value meets it (place_window32)
+      nc[g] = zero[g] ? 0x80000000u : static_cast<uint32_t>(a);
+      nm[g] = zero[g] ? 0x80000000u : static_cast<uint32_t>(b);
+      ne[g] = zero[g] ? 0x80000000u : static_cast<uint32_t>(c);
     }
     narrow = w.k2_narrow && ballot(!ok) == 0;
   }
@@ -1206,7 +1214,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       int32_t c32 = 0, m32 = 0, e32 = 0;
       st.narrow = narrow;
       if (narrow) {
-        c32 = scale32(ncpu, nk.kc);
+        c32 = E || neph >= 0 ? scale32(ncpu, nk.kc) : INT_MIN;  // place_window32: the ephemeral gate
         m32 = scale32(nmem, nk.km);
         e32 = scale32(neph, nk.ke);
       }
@@ -1221,8 +1229,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   place_window<e_, o_>(todo, kmax, W, lane, rc[g], rm[g], re[g], pm[g], cur[g], zm[g], w.swap_mask, emask, ncpu, \
                        nmem, neph, nport, nleft, node[g])
 #define SR_PW32(e_, o_)                                                                                           \
-  place_window32<e_, o_>(todo, kmax, W, lane, nc[g], nm[g], ne[g], pm[g], cur[g], zm[g], w.swap_mask, emask, c32, \
-                         m32, e32, nport, nleft, node[g])
+  place_window32<e_, o_>(todo, kmax, W, lane, nc[g], nm[g], ne[g], pm[g], cur[g], w.swap_mask, c32, m32, e32, nport, \
+                         nleft, node[g])
           if (narrow)
             placed = E ? (O ? SR_PW32(true, true) : SR_PW32(true, false))
                        : (O ? SR_PW32(false, true) : SR_PW32(false, false));

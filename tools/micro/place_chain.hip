@@ -20,6 +20,15 @@
 //   V10 V7 pipelined: pod k's fit mask is taken against the state without
 //       pod k-1's update, and the bit of the node pod k-1 took is redone on the
 //       scalar unit (that update reaches the vector state one step later)
+//   V12 V7 with the per-lane checks folded into one compare: d = min3(cpu -
+//       c', memory - m', pods left - 1) >= 0 (c', m' = -2^30 for an all-zero
+//       request; the ephemeral gate folded into the cpu state), so the fit mask
+//       is one ballot and the F word (no scalar select chain)
+//   V13 V7 with the node and placed bookkeeping moved out of the step: the
+//       first lane j is selected into pod k's lane of a VGPR, the
+//       visit derives node / placed from it once
+//   V11 V7 two pods per step (place_window32_pairs): pod b's mask against the
+//       state before pod a and against it minus a, side by side (reported per pod)
 // Build: hipcc -O3 --offload-arch=gfx950 -o place_chain place_chain.hip
 #include <hip/hip_runtime.h>
 
@@ -56,7 +65,13 @@ __global__ __launch_bounds__(64) void k_chain(const int64_t* reqs, const int64_t
   uint64_t pk = (static_cast<uint64_t>(c32 & 0x3fffffffu) << 32) | 0x80000000ull | (m32 & 0x3fffffffu);
   const uint64_t rq = (static_cast<uint64_t>(rc32 & 0xffffu) << 32) | (rm32 >> 20);
   int32_t sc32 = static_cast<int32_t>(c32 & 0x3fffffff), sm32 = static_cast<int32_t>(m32 & 0x3fffffff), sleft = nleft;
-  int pj = 64, qj = 64;
+  int pj = 64, qj = 64, jv = 64;
+  const bool zr = (zm >> lane) & 1;
+  const int32_t cq = zr ? -(1 << 30) : static_cast<int32_t>(rc32), mq = zr ? -(1 << 30) : static_cast<int32_t>(rm32);
+  if constexpr (V == 12) {
+    sc32 = ((emask >> lane) & 1) ? sc32 : -1;
+    sleft -= 1;
+  }
   int32_t pc = 0, pm_ = 0, qc = 0, qm = 0;
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   for (int s = 0; s < kSteps; ++s) {
@@ -166,6 +181,59 @@ __global__ __launch_bounds__(64) void k_chain(const int64_t* reqs, const int64_t
       // pending: pod k-1's update moves to the "before last" slot, pod k's becomes pending
       pj = qj; pc = qc; pm_ = qm;
       qj = j; qc = c; qm = m;
+    } else if constexpr (V == 11) {
+      const int a = __builtin_amdgcn_readfirstlane((2 * s) & 63), b = a + 1;
+      const int32_t ca = __builtin_amdgcn_readlane(static_cast<int>(rc32), a);
+      const int32_t ma = __builtin_amdgcn_readlane(static_cast<int>(rm32), a);
+      const int32_t cb = __builtin_amdgcn_readlane(static_cast<int>(rc32), b);
+      const int32_t mb = __builtin_amdgcn_readlane(static_cast<int>(rm32), b);
+      const uint64_t za = 0ull - ((zm >> a) & 1), zb = 0ull - ((zm >> b) & 1);
+      const int32_t i32 = static_cast<int32_t>(c32), j32 = static_cast<int32_t>(m32);
+      const uint64_t l1 = ballot(nleft >= 1);
+      const uint64_t fa = readlane64(curw, a) & l1 & ((ballot(i32 >= ca) & ballot(j32 >= ma) & emask) | za);
+      const uint64_t fwb = readlane64(curw, b);
+      const uint64_t fold = fwb & l1 & ((ballot(i32 >= cb) & ballot(j32 >= mb) & emask) | zb);
+      const uint64_t fnew =
+          fwb & ballot(nleft >= 2) & ((ballot(i32 >= ca + cb) & ballot(j32 >= ma + mb) & emask) | zb);
+      const int ja = fa != 0 ? __builtin_ctzll(fa) : 64;
+      const uint64_t bit = ja < 64 ? 1ull << ja : 0ull;
+      const uint64_t fb = (fold & ~bit) | (fnew & bit);
+      const int jb = fb != 0 ? __builtin_ctzll(fb) : 64;
+      const bool ha = lane == ja, hb = lane == jb;
+      c32 -= (ha ? ca : 0) + (hb ? cb : 0);
+      m32 -= (ha ? ma : 0) + (hb ? mb : 0);
+      nleft -= (ha ? 1 : 0) + (hb ? 1 : 0);
+      node = (lane == a && ja < 64) ? 64 * 3 + ja : node;
+      node = (lane == b && jb < 64) ? 64 * 3 + jb : node;
+      placed |= (fa != 0 ? 1ull << a : 0ull) | (fb != 0 ? 1ull << b : 0ull);
+      fit = fa ^ fb;
+    } else if constexpr (V == 12) {
+      const int32_t c = __builtin_amdgcn_readlane(static_cast<int>(cq), k);
+      const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(mq), k);
+      const int32_t cu = __builtin_amdgcn_readlane(static_cast<int>(rc32), k);
+      const int32_t mu = __builtin_amdgcn_readlane(static_cast<int>(rm32), k);
+      const int32_t d = min(min(sc32 - c, sm32 - m), sleft);
+      fit = readlane64(curw, k) & ballot(d >= 0);
+      const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
+      const bool hit = lane == j;
+      sc32 -= hit ? cu : 0;
+      sm32 -= hit ? mu : 0;
+      sleft -= hit ? 1 : 0;
+      node = (lane == k && j < 64) ? 64 * 3 + j : node;
+      placed |= fit != 0 ? 1ull << k : 0ull;
+    } else if constexpr (V == 13) {
+      const int32_t c = __builtin_amdgcn_readlane(static_cast<int>(rc32), k);
+      const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(rm32), k);
+      const int32_t i32 = static_cast<int32_t>(c32), j32 = static_cast<int32_t>(m32);
+      fit = readlane64(curw, k) & ballot(nleft >= 1);
+      const uint64_t res = ballot(i32 >= c) & ballot(j32 >= m) & emask;
+      fit &= ((zm >> k) & 1) ? ~0ull : res;
+      const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
+      const bool hit = lane == j;
+      c32 -= hit ? c : 0u;
+      m32 -= hit ? m : 0u;
+      nleft -= hit ? 1 : 0;
+      jv = lane == k ? j : jv;
     } else {
       const uint32_t c = static_cast<uint32_t>(lreq[0][k]), m = static_cast<uint32_t>(lreq[1][k]);
       fit = ballot(c32 >= c) & ballot(m32 >= m);
@@ -176,6 +244,10 @@ __global__ __launch_bounds__(64) void k_chain(const int64_t* reqs, const int64_t
     }
     acc += fit;
   }
+  if constexpr (V == 13) {
+    placed = ballot(jv < 64);
+    node = jv < 64 ? 64 * 3 + jv : node;
+  }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   if (lane == 0) {
     out[0] = t1 - t0;
@@ -185,17 +257,17 @@ __global__ __launch_bounds__(64) void k_chain(const int64_t* reqs, const int64_t
 }
 
 template <int V>
-int run(const int64_t* dreq, const int64_t* dfree, uint64_t* dout, const char* name) {
+int run(const int64_t* dreq, const int64_t* dfree, uint64_t* dout, const char* name, int pods_per_step = 1) {
   std::vector<double> cyc;
   for (int r = 0; r < 21; ++r) {
     hipLaunchKernelGGL(k_chain<V>, dim3(1), dim3(64), 0, 0, dreq, dfree, dout);
     CK(hipDeviceSynchronize());
     uint64_t h[2];
     CK(hipMemcpy(h, dout, sizeof(h), hipMemcpyDeviceToHost));
-    cyc.push_back(static_cast<double>(h[0]) / kSteps);
+    cyc.push_back(static_cast<double>(h[0]) / kSteps / pods_per_step);
   }
   std::sort(cyc.begin(), cyc.end());
-  printf("%-58s %7.1f cycles/step (median of 21)\n", name, cyc[10]);
+  printf("%-58s %7.1f cycles/pod (median of 21)\n", name, cyc[10]);
   return 0;
 }
 
@@ -225,5 +297,8 @@ int main() {
   run<8>(dreq, dfree, dout, "V8 V6 with cpu/memory packed in one word");
   run<9>(dreq, dfree, dout, "V9 V7, selects after the first lane, node unconditional");
   run<10>(dreq, dfree, dout, "V10 V7 pipelined (last pod's node redone on SALU)");
+  run<11>(dreq, dfree, dout, "V11 V7 two pods per step", 2);
+  run<12>(dreq, dfree, dout, "V12 V7 with the checks folded into one min3 compare");
+  run<13>(dreq, dfree, dout, "V13 V7, node / placed once per visit");
   return 0;
 }
