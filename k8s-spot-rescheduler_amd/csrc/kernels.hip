@@ -751,7 +751,7 @@ __device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W,
   // lane 64 (no lane)
   while (todo != 0) {
     const int k = __builtin_ctzll(todo);
-    todo &= todo - 1;
+    todo &= ~(1ull << k);  // one scalar op fewer than todo &= todo - 1
     const int64_t c = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), k));
     const int64_t m = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), k));
     const int64_t e = E ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), k)) : 0;
@@ -815,7 +815,7 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
   if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
   while (todo != 0) {
     const int k = __builtin_ctzll(todo);
-    todo &= todo - 1;
+    todo &= ~(1ull << k);
     const int32_t c = __builtin_amdgcn_readlane(static_cast<int>(nc), k);
     const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
     const int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
