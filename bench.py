@@ -46,11 +46,33 @@ from spotplanner.synth import SynthCluster, new_node_map, pods_for_deletion, sha
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 DEFAULT_OD = {1: 10, 2: 300, 3: 1500, 4: 15000, 5: 300}
-WORKLOAD = {1: "C1 rescheduler_test-style 20 nodes / 200 pods",
-            2: "C2 1k nodes (300 od / 700 spot) / 30k pods, resource fit + PreferNoSchedule",
-            3: "C3 5k nodes (1500 od / 3500 spot) / 150k pods, nodeSelector + node affinity + tolerations",
-            4: "C4 50k nodes (15000 od / 35000 spot) / 1.5M pods, all candidates per tick",
-            5: "C5 1k nodes host-port + DaemonSet heavy"}
+WORKLOAD_KIND = {1: "rescheduler_test-style, cpu/mem requests only",
+                 2: "resource fit + PreferNoSchedule taints",
+                 3: "nodeSelector + node affinity + tolerations",
+                 4: "nodeSelector + node affinity + tolerations, all candidates per tick",
+                 5: "host-port + DaemonSet heavy"}
+
+
+def workload_name(config, n_nodes, n_od, n_spot, n_pods, world, scaling):
+    """config.workload: the cluster this run actually planned (node, on-demand,
+    spot and pod counts), and how its candidates were split over the ranks."""
+    s = "C%d %d nodes (%d od / %d spot) / %d pods, %s" % (config, n_nodes, n_od, n_spot, n_pods,
+                                                          WORKLOAD_KIND[config])
+    if world > 1:
+        s += "; %s scaling: %d candidates sharded c %% %d" % (scaling, n_od, world)
+    return s
+
+
+def cluster_on_demand(config, world, scaling):
+    """On-demand node count of the synthetic cluster: the config's own (strong
+    scaling: a fixed cluster split over the ranks) or world x it (weak: each
+    rank holds one config-sized candidate set over the same spot pool)."""
+    return DEFAULT_OD[config] * (world if scaling == "weak" else 1)
+
+
+def shard_sizes(n_cand, world):
+    """Candidates per rank under the c % world split (shard())."""
+    return [len(range(r, n_cand, world)) for r in range(world)]
 
 
 E2E_IDLE = os.environ.get("SR_BENCH_E2E_IDLE", "1") != "0"
@@ -184,11 +206,33 @@ def _free_port():
     return port
 
 
-def visible_devices():
-    """HIP devices this process would see, without initialising the GPU
-    (torch.cuda.device_count() does not initialise HIP on this image)."""
-    import torch
-    return torch.cuda.device_count()
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def visible_devices(kfd_nodes=KFD_NODES, environ=None):
+    """GPUs this process would see, counted without any HIP call (the launcher
+    must not initialise the runtime in a parent that starts the ranks): the KFD
+    topology nodes with SIMDs (GPU agents; CPU agents report simd_count 0),
+    restricted by ROCR/HIP/CUDA_VISIBLE_DEVICES when one is set."""
+    environ = os.environ if environ is None else environ
+    n = 0
+    try:
+        entries = os.listdir(kfd_nodes)
+    except OSError:
+        entries = []
+    for e in entries:
+        try:
+            with open(os.path.join(kfd_nodes, e, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if len(line.split(None, 1)) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
 
 
 def launch_ranks(n, argv, script=None, devices=None):
@@ -231,6 +275,8 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the config's cluster, candidates split over the ranks; weak: N x its candidates")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e-reps", type=int, default=20, help="steady-state end-to-end ticks timed after the steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -255,7 +301,7 @@ def main():
     torch.cuda.set_device(local)
 
     lib = capi.load_planner()
-    sc = SynthCluster(args.config, n_on_demand=DEFAULT_OD[args.config] * world)
+    sc = SynthCluster(args.config, n_on_demand=cluster_on_demand(args.config, world, args.scaling))
     nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
     # run()'s candidate lists (rescheduler.go:228-264): GetPodsForDeletionOnNodeDrain + the
     # DaemonSet-owner filter, on the host (sr_pods_for_deletion)
@@ -519,11 +565,14 @@ def main():
             "latency_span": "median of 50 single sr_plan_run calls on an idle device: launch to the winner and "
                             "its mapping in host memory (ms_per_step: back-to-back ticks, every candidate planned)",
             "plans_per_s": (len(cand_off) - 1) / (elapsed / args.steps),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "int64",
             "data": "synthetic",
-            "config": {"workload": WORKLOAD[args.config], "nodes": sc.n_nodes, "pods": sc.n_pods,
+            "config": {"workload": workload_name(args.config, sc.n_nodes, len(nm.on_demand), len(nm.spot),
+                                                 sc.n_pods, world, args.scaling),
+                       "nodes": sc.n_nodes, "pods": sc.n_pods, "on_demand_nodes": int(len(nm.on_demand)),
                        "spot_nodes": int(len(nm.spot)), "candidates": int(len(cand_off) - 1),
-                       "candidate_pods": int(len(cand_pods)), "parallelism": "candidates c%%%d" % world},
+                       "candidate_pods": int(len(cand_pods)), "parallelism": "candidates c%%%d" % world,
+                       "candidates_per_rank": shard_sizes(len(cand_off) - 1, world)},
             "collective": {"backend": "rccl" if rccl_ranks else "none", "ranks": rccl_ranks,
                            "per_tick": "one allreduce(min) of 3 x u64" if rccl_ranks else "none (one GPU)"},
             "first_ok": int(out.first_ok), "winner": int(out.winner),
@@ -537,6 +586,14 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "kernel_ms": round(dom_ms, 5),
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms_source": "HIP events of the timed region (every %d-th step, recorded by the "
+                                             "kernel's own dispatch); they open at the dispatch, so they include "
+                                             "the gap after the previous kernel" % max(1, args.event_every),
+                         "kernel_ms_calibration": round(breakdown[dom], 5),
+                         "frac_calibration": round(alg / (breakdown[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                         if breakdown[dom] > 0 else None,
+                         "calibration_source": "kernels_ms: the untimed calibration pass before the timed region, "
+                                               "every kernel bracketed on every run",
                          "traffic_source": traffic_src,
                          "algorithmic_bytes": int(alg),
                          "bytes_definition": "bytes the kernel moves, counted by K2 per candidate (pod records, "

@@ -405,6 +405,12 @@ sr_status   sr_create(int32_t device, sr_ctx **out);
 void        sr_destroy(sr_ctx *ctx);
 const char *sr_last_error(const sr_ctx *ctx);
 const char *sr_build_info(void);
+/* SR_ABI_VERSION the library was built with.  The sr_cluster layout grows at
+ * its end between versions (ABI 4 added str_label, the scalar tables, acc_*
+ * and spread): a binding compares this with the SR_ABI_VERSION it was built
+ * against before its first call and refuses to run on a mismatch, since the
+ * library would otherwise read fields past the end of a shorter struct. */
+int32_t     sr_abi_version(void);
 
 /* Batched findSpotNodeForPod (rescheduler.go:338-353): for each pod, the first
  * spot node (NodeInfoArray order) whose predicates pass against the snapshot

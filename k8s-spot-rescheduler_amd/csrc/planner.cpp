@@ -677,9 +677,13 @@ static sr_status plan_first(sr_ctx* ctx, const sr_snapshot* snap, const sr_clust
 
 extern "C" {
 
+#define SR_STR2(x) #x
+#define SR_STR(x) SR_STR2(x)
 const char* sr_build_info(void) {
-  return "srplanner abi=2 target=gfx950 kernels=K0-tables,K2-placement(fused feasibility),K3-winner";
+  return "srplanner abi=" SR_STR(SR_ABI_VERSION) " target=gfx950 kernels=K0-tables,K2-placement(fused feasibility),K3-winner";
 }
+
+int32_t sr_abi_version(void) { return SR_ABI_VERSION; }
 
 sr_status sr_create(int32_t device, sr_ctx** out) {
   if (!out) return SR_ERR_INVALID_ARG;

@@ -107,6 +107,10 @@ inline uint64_t pair_key(int32_t key, int32_t val) {
 
 bool spread_invalid(const sr_cluster* c, int32_t k) {
   const sr_spread* S = c->spread;
+  // maxSkew < 1 never reaches the scheduler (API validation rejects it); the
+  // encoded forms (domain path, node-local caps) assume maxSkew >= 1, so the
+  // C ABI routes such a constraint to the reference path instead of guessing
+  if (S->max_skew[k] < 1) return true;
   if (S->selector_nil[k]) return false;
   for (int32_t i = S->ml_off[k]; i < S->ml_off[k + 1]; ++i)
     if (!label_req_strings_ok(c, S->ml_key[i], S->ml_val, i, i + 1)) return true;

@@ -239,8 +239,24 @@ def load_planner():
             "(the planner has no CPU fallback)" % path)
     lib = ctypes.CDLL(path)
     _declare_planner(lib)
+    check_abi(lib, path)
     _planner = lib
     return lib
+
+
+class PlannerAbiMismatch(RuntimeError):
+    pass
+
+
+def check_abi(lib, path="libsrplanner.so"):
+    """The shim contract: before the first planner call, the
+    library's SR_ABI_VERSION must equal the header's this binding was built
+    from -- sr_cluster grows at its end between versions, and a library fed a
+    shorter struct would read past it."""
+    have = int(lib.sr_abi_version())
+    if have != SR_ABI_VERSION:  # noqa: F821 (parsed from the header)
+        raise PlannerAbiMismatch("%s has SR_ABI_VERSION %d, this binding was built against %d"
+                                 % (path, have, SR_ABI_VERSION))  # noqa: F821
 
 
 def _declare_planner(lib):
@@ -276,6 +292,8 @@ def _declare_planner(lib):
     lib.sr_last_error.restype = ctypes.c_char_p
     lib.sr_build_info.argtypes = []
     lib.sr_build_info.restype = ctypes.c_char_p
+    lib.sr_abi_version.argtypes = []
+    lib.sr_abi_version.restype = ctypes.c_int32
     lib.sr_find_spot_nodes.argtypes = [VP, VP, PC, P32, ctypes.c_int32, P32, PU8]
     lib.sr_find_spot_nodes.restype = S
     lib.sr_can_drain_node.argtypes = [VP, VP, PC, P32, ctypes.c_int32, P32, P32, PU8]
@@ -304,5 +322,5 @@ def _declare_planner(lib):
 EXPORTED = ["sr_new_node_map", "sr_node_has_label", "sr_pods_for_deletion", "sr_snapshot_create", "sr_snapshot_destroy",
             "sr_snapshot_add_pod", "sr_snapshot_fork", "sr_snapshot_revert", "sr_snapshot_node_state",
             "sr_snapshot_num_nodes", "sr_create", "sr_destroy", "sr_last_error", "sr_build_info",
-            "sr_find_spot_nodes", "sr_can_drain_node", "sr_plan", "sr_plan_first", "sr_plan_prepare", "sr_plan_run",
+            "sr_abi_version", "sr_find_spot_nodes", "sr_can_drain_node", "sr_plan", "sr_plan_first", "sr_plan_prepare", "sr_plan_run",
             "sr_set_timing", "sr_get_timing", "sr_comm_unique_id", "sr_comm_init", "sr_comm_init_host"]

@@ -1033,6 +1033,9 @@ static int o_spread_sel(const sr_cluster *c, int32_t k, int32_t pod) {
  * constraint selector that fails to build (NewRequirement's rules). */
 static int o_spread_invalid(const sr_cluster *c, int32_t k) {
   const sr_spread *S = c->spread;
+  /* maxSkew < 1 fails API validation and never reaches the scheduler: the
+   * planner's C ABI accepts it but routes it to the reference path */
+  if (S->max_skew[k] < 1) return 1;
   if (S->selector_nil[k]) return 0;
   for (int32_t i = S->ml_off[k]; i < S->ml_off[k + 1]; i++)
     if (!o_req_strings_ok(c, S->ml_key[i], S->ml_val, i, i + 1)) return 1;

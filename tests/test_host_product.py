@@ -30,6 +30,21 @@ def test_build_info_names_gfx950():
     assert b"gfx950" in capi.load_planner().sr_build_info()
 
 
+def test_abi_version_matches_header_and_build_info():
+    """the library reports the SR_ABI_VERSION it was built with (sr_abi_version and sr_build_info),
+    and the binding refuses a library whose version differs from the header's."""
+    lib = capi.load_planner()
+    assert lib.sr_abi_version() == capi.SR_ABI_VERSION
+    assert ("abi=%d " % capi.SR_ABI_VERSION).encode() in lib.sr_build_info()
+
+    class Old:
+        def sr_abi_version(self):
+            return capi.SR_ABI_VERSION - 1
+    import pytest
+    with pytest.raises(capi.PlannerAbiMismatch):
+        capi.check_abi(Old())
+
+
 def test_sr_create_without_device_fails_loudly():
     import torch
     if torch.cuda.device_count() > 0:

@@ -134,6 +134,10 @@ def cases():
                LabelSelectorRequirement("app", "NotIn", ["web"])])))]], [OK], [[2]])
     yield ("invalid_selector_falls_back", N(), [[], [], [], []],
            [[spread(web("p"), zc(sel=LabelSelector(match_labels={"bad key!": "x"})))]], [FB], [[-1]])
+    # maxSkew <= 0 fails API validation; the C ABI accepts it and sends the pod to the reference path
+    yield ("max_skew_zero_falls_back", N(), [[web("e")], [], [], []], [[spread(web("p"), zc(skew=0))]], [FB], [[-1]])
+    yield ("max_skew_negative_falls_back", N(), [[], [], [], []],
+           [[web("q"), spread(web("p"), zc(skew=-1, key=H))]], [FB], [[-1, -1]])
     yield ("in_without_values_falls_back", N(), [[], [], [], []],
            [[spread(web("p"), zc(sel=LabelSelector(match_expressions=[LabelSelectorRequirement("app", "In", [])])))]],
            [FB], [[-1]])
