@@ -836,11 +836,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     rq[1] = P.req_memory[pod];
     rq[2] = P.req_ephemeral[pod];
     if (!in_range(rq[0]) || !in_range(rq[1]) || !in_range(rq[2])) return true;
-    // NodeInfo.AddPod adds another amount than the fit request (init
-    // containers) and later pods of the candidate see it: the device's
-    // running state subtracts the request
+    // NodeInfo.AddPod's accounting (init containers: it can differ from the
+    // fit request; the candidate's extension records carry it, see below)
     for (int r = 0; r < 3 && !last; ++r)
-      if (pod_acc(c, pod, r) != rq[r]) return true;
+      if (!in_range(pod_acc(c, pod, r))) return true;
     if (has_scalars(c, pod)) {
       // a listed scalar keeps an all-zero cpu / memory / ephemeral request
       // from skipping the resource checks: not encoded
@@ -871,6 +870,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     }
   std::vector<uint8_t>& cand_ports = C.scratch.cand_ports;  // the candidate's pods ask for host ports
   cand_ports.assign(static_cast<size_t>(nc), 0);
+  std::vector<uint8_t>& cand_ext = C.scratch.cand_ext;       // bit 0: accounting differs, bit 1: shared scalars
+  cand_ext.assign(static_cast<size_t>(nc), 0);
+  std::vector<int32_t>& cand_sname = C.scratch.cand_sname;   // [2 * candidate] its shared scalar names (-1: none)
+  cand_sname.resize(static_cast<size_t>(2 * nc));
   std::atomic<bool> bad_index{false};
   auto pass1 = [&](size_t lo, size_t hi) {
     bool bad = false;
@@ -890,21 +893,46 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       // an existing pod's opaque anti-affinity may select any incoming pod
       bool fb = (c->pod_affinity ? snap->opaque_total : snap->anti_total) > 0 || (e - b) > MAX_CAND_PODS;
       for (int32_t j = b; j < e && !fb; ++j) fb = pod_fallback(cands->cand_pods[j], j, j + 1 == e);
+      // Extension records (K2's pod-order and domain paths): a pod followed by
+      // others whose AddPod accounting differs from its fit request (the
+      // running state subtracts the accounting), and scalar resources listed
+      // by two or more pods of the candidate (the later ones see the earlier
+      // ones' AddPod: a running scalar state per touched node, at most
+      // kExtScalars names per candidate)
+      uint8_t ext = 0;
+      cand_sname[2 * i] = cand_sname[2 * i + 1] = -1;
+      for (int32_t j = b; j + 1 < e && !fb && !(ext & 1); ++j) {
+        const int32_t pod = cands->cand_pods[j];
+        ext |= (pod_acc(c, pod, 0) != P.req_milli_cpu[pod] || pod_acc(c, pod, 1) != P.req_memory[pod] ||
+                pod_acc(c, pod, 2) != P.req_ephemeral[pod]) ? 1 : 0;
+      }
       if (!fb && c->pod_scalar_off) {
-        // two pods of the candidate listing one scalar resource: the later
-        // one sees the earlier one's AddPod on the node -- a running state
-        // the device does not keep for scalars (the check is a static atom)
-        int32_t names[64], nn = 0;
+        int32_t names[64], cnt[64], nn = 0;
         for (int32_t j = b; j < e && !fb; ++j) {
           const int32_t pod = cands->cand_pods[j];
           for (int32_t k = c->pod_scalar_off[pod]; k < c->pod_scalar_off[pod + 1] && !fb; ++k) {
             const int32_t name = c->pod_scalar_name[k];
-            for (int32_t u = 0; u < nn && !fb; ++u) fb = names[u] == name;
-            if (nn == 64) fb = true;
-            else names[nn++] = name;
+            int32_t u = 0;
+            while (u < nn && names[u] != name) ++u;
+            if (u < nn) {
+              ++cnt[u];
+            } else if (nn == 64) {
+              fb = true;  // more scalar entries than the candidate's table holds
+            } else {
+              names[nn] = name;
+              cnt[nn++] = 1;
+            }
           }
         }
+        int32_t shared = 0;
+        for (int32_t u = 0; u < nn && !fb; ++u)
+          if (cnt[u] >= 2) {
+            if (shared == kExtScalars) fb = true;
+            else cand_sname[2 * i + shared++] = names[u];
+          }
+        if (shared > 0) ext |= 2;
       }
+      cand_ext[i] = fb ? 0 : ext;
       if (fb) w->status_host[i] = SR_CAND_FALLBACK;
       for (int32_t j = b; j < e && !fb && !cand_ports[i]; ++j)
         cand_ports[i] = P.port_off[cands->cand_pods[j]] != P.port_off[cands->cand_pods[j] + 1];
@@ -1043,6 +1071,27 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     }
     return m;
   };
+
+  // ---- shared scalar names of this call (extension records): a table row of
+  // base free values per name, at most kExtScalarNames per call, the
+  // candidates needing another one go to the reference path
+  std::vector<int32_t> scal_names;
+  for (int32_t i = 0; i < nc; ++i) {
+    if (w->status_host[i] != STATUS_PENDING || !(cand_ext[i] & 2)) continue;
+    int32_t need = 0;
+    for (int j = 0; j < 2; ++j) {
+      const int32_t nm = cand_sname[2 * i + j];
+      need += nm >= 0 && std::find(scal_names.begin(), scal_names.end(), nm) == scal_names.end();
+    }
+    if (static_cast<int32_t>(scal_names.size()) + need > kExtScalarNames) {
+      w->status_host[i] = SR_CAND_FALLBACK;
+      continue;
+    }
+    for (int j = 0; j < 2; ++j) {
+      const int32_t nm = cand_sname[2 * i + j];
+      if (nm >= 0 && std::find(scal_names.begin(), scal_names.end(), nm) == scal_names.end()) scal_names.push_back(nm);
+    }
+  }
 
   // ---- outcome bookkeeping for non-active candidates
   for (int32_t i = 0; i < nc; ++i) {
@@ -1736,6 +1785,58 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
           }
         }
       }
+    }
+  }
+  // extension records: per pod of such a candidate {AddPod accounting of
+  // cpu / memory / ephemeral, per scalar slot the fit request (INT64_MIN: the
+  // pod does not list it) and the accounting, the slots' name rows}; per
+  // shared scalar name of the call, the base free value of every spot node
+  {
+    const int32_t n_act = static_cast<int32_t>(w->cand_src.size());
+    bool any_ext = false;
+    for (int32_t k = 0; k < n_act && !any_ext; ++k) any_ext = cand_ext[w->cand_src[k]] != 0;
+    if (any_ext) {
+      w->ext_cand.assign(static_cast<size_t>(n_act), -1);
+      for (int32_t k = 0; k < n_act; ++k) {
+        const int32_t i = w->cand_src[k];
+        if (!cand_ext[i]) continue;
+        w->ext_cand[k] = static_cast<int32_t>(w->pod_ext.size() / kExtU64);
+        int32_t row[2] = {-1, -1};
+        for (int j = 0; j < 2; ++j)
+          if (cand_sname[2 * i + j] >= 0)
+            row[j] = static_cast<int32_t>(std::find(scal_names.begin(), scal_names.end(), cand_sname[2 * i + j]) -
+                                          scal_names.begin());
+        for (int32_t q = w->cand_off[k]; q < w->cand_off[k + 1]; ++q) {
+          const int32_t pod = active_pod[q];
+          uint64_t x[kExtU64];
+          for (int r = 0; r < 3; ++r) x[r] = static_cast<uint64_t>(pod_acc(c, pod, r));
+          for (int j = 0; j < 2; ++j) {
+            int64_t rq = INT64_MIN, ac = 0;
+            if (row[j] >= 0)
+              for (int32_t a = c->pod_scalar_off[pod]; a < c->pod_scalar_off[pod + 1]; ++a)
+                if (c->pod_scalar_name[a] == cand_sname[2 * i + j]) {
+                  rq = c->pod_scalar_req[a];
+                  ac = c->pod_scalar_acc[a];
+                }
+            x[3 + j] = static_cast<uint64_t>(rq);
+            x[5 + j] = static_cast<uint64_t>(ac);
+          }
+          x[7] = static_cast<uint64_t>(static_cast<uint32_t>(row[0])) |
+                 static_cast<uint64_t>(static_cast<uint32_t>(row[1])) << 32;
+          w->pod_ext.insert(w->pod_ext.end(), x, x + kExtU64);
+        }
+      }
+      w->n_scal_names = static_cast<int32_t>(scal_names.size());
+      w->node_scal.assign(std::max<size_t>(1, scal_names.size()) * static_cast<size_t>(w->n_pad), 0);
+      auto value_of = [](const std::vector<std::pair<int32_t, int64_t>>& v, int32_t name) -> int64_t {
+        auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(name, INT64_MIN));
+        return it != v.end() && it->first == name ? it->second : 0;
+      };
+      for (size_t u = 0; u < scal_names.size(); ++u)
+        for (int32_t n = 0; n < n_spot; ++n)  // Go int64 arithmetic: alloc - requested wraps like the reference's
+          w->node_scal[u * static_cast<size_t>(w->n_pad) + static_cast<size_t>(n)] = static_cast<int64_t>(
+              static_cast<uint64_t>(value_of(snap->nodes[n].scalar_alloc, scal_names[u])) -
+              static_cast<uint64_t>(value_of(snap->state[n].scalar_req, scal_names[u])));
     }
   }
   phase(4);

@@ -224,6 +224,11 @@ constexpr int kDynPods = 64 * kDynG;  // pods of a candidate planned on the doma
 constexpr int kSpreadSlots = 2;  // topology spread constraints per pod planned on the domain path
 constexpr int kSpreadU64 = kSpreadSlots * (kDynG + 3);  // their words in the pod record
 constexpr int kDynU64 = 5 * kDynG + 1 + kSpreadU64;  // words per pod record (kernels.hpp)
+// K2 extension records (pod-order and domain paths): AddPod accounting that
+// differs from the fit request, scalar resources shared inside a candidate
+constexpr int kExtScalars = 2;      // shared scalar names per candidate
+constexpr int kExtScalarNames = 8;  // shared scalar names per call (node_scal rows)
+constexpr int kExtU64 = 8;          // {acc cpu, mem, eph, req s0, req s1, acc s0, acc s1, row s0 | row s1 << 32}
 
 // The encoded workload of one planning call (host copy; uploaded as one
 // arena).  The spot nodes' state (capacity records, free values) lives in the
@@ -281,6 +286,11 @@ struct Workload {
   std::vector<int32_t> dk_dom;    // [n_dk][n_spot] domain of each spot node (node-local key: the node), -1 absent
   int32_t dk_row[kDomKeys] = {-1, -1, -1, -1};  // atom of domain 0 of each table key (-1: node-local key)
   std::vector<int32_t> ds_info;   // [set][2 + 2 * kDynTerms] {terms, map_empty, (key slot, base atom) per term}
+  // ---- extension records (kExtU64 per pod of the candidates that need them)
+  std::vector<int32_t> ext_cand;  // [n_active] first record in pod_ext, -1: none (empty: no such candidate)
+  std::vector<uint64_t> pod_ext;
+  int32_t n_scal_names = 0;
+  std::vector<int64_t> node_scal; // [n_scal_names][n_pad] alloc - requested of each shared scalar name
   // ---- host-decided outcomes for every input candidate
   std::vector<int32_t> status_host;  // SR_CAND_EMPTY / SR_CAND_FALLBACK / PENDING
   int32_t first_fallback = -1;       // global index
@@ -294,9 +304,12 @@ struct Workload {
   void reset() {
     t_thr.clear();
     for (auto* v : {&cls_prog_off, &cls_prog, &cls_prog8, &t_dim, &pod_src, &cand_off, &cand_global, &cand_src, &list,
-                    &status_host, &dyn_cand, &dk_dom, &ds_info, &sp_tab})
+                    &status_host, &dyn_cand, &dk_dom, &ds_info, &sp_tab, &ext_cand})
       v->clear();
     dyn_pod.clear();
+    pod_ext.clear();
+    node_scal.clear();
+    n_scal_names = 0;
     n_dk = 0;
     for (int32_t& r : dk_row) r = -1;
     atoms.clear();
@@ -383,7 +396,8 @@ struct EncoderCache {
   uint64_t psig_gen = ~0ull;
   // ---- per-call scratch (kept: fresh multi-MB buffers page-fault on every call)
   struct Scratch {
-    std::vector<uint8_t> cand_ports, spec_shard, key_seen;
+    std::vector<uint8_t> cand_ports, spec_shard, key_seen, cand_ext;
+    std::vector<int32_t> cand_sname;
     std::vector<int32_t> active_pod, active_src, act_of, pod_spec, pod_key, key_slot, psig_class;
     std::vector<uint64_t> spec_hash;
     std::vector<int64_t> req_flat;  // [input candidate pod][3] requests (cpu, memory, ephemeral)

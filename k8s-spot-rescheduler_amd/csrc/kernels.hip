@@ -377,9 +377,12 @@ struct K2Stats {
 // number of pods placed (np = all; status = failing pod or -1), or -1 when the
 // candidate touches more distinct nodes than it has slots (the caller reruns
 // it with more).
-template <int SPL, int CH, bool PROF>
+// EXT: the candidate has extension records at pod_ext[ebase ..] (the running
+// state subtracts NodeInfo.AddPod's accounting instead of the fit request, and
+// keeps up to two shared scalar resources per touched node).
+template <int SPL, int CH, bool PROF, bool EXT = false>
 __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int p0, const int np, int& status,
-                                      K2Stats& st, uint32_t& nbytes) {
+                                      K2Stats& st, uint32_t& nbytes, const int ebase = -1) {
   const int lane = threadIdx.x & 63;
   const int Wp = w.Wp;
   const uint64_t* __restrict__ tab = w.S;  // S rows then T rows: pod records hold word offsets
@@ -430,13 +433,18 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
   int64_t scpu[SPL], smem[SPL], seph[SPL];
   int sleft[SPL];
   uint64_t sport[SPL];
+  int64_t ss0[SPL], ss1[SPL];  // EXT: shared scalar resources' running free values
 #pragma unroll
   for (int s = 0; s < SPL; ++s) {
     snode[s] = INT_MAX;
     scpu[s] = smem[s] = seph[s] = 0;
     sleft[s] = 0;
     sport[s] = 0;
+    ss0[s] = ss1[s] = 0;
   }
+  // EXT: the scalar slots' node_scal rows (uniform over the candidate's records)
+  const uint64_t erow = EXT ? w.pod_ext[static_cast<size_t>(ebase) * kDevExtU64 + 7] : ~0ull;
+  const int erow0 = static_cast<int32_t>(static_cast<uint32_t>(erow)), erow1 = static_cast<int32_t>(erow >> 32);
   int nslots = 0;
   uint64_t cyc_t = 0;
   auto cyc = [&]() -> uint64_t { return PROF ? __builtin_amdgcn_s_memtime() : 0ull; };
@@ -449,8 +457,19 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
   int cnode0 = INT_MAX;
   int64_t nrc = 0, nrm = 0, nre = 0;
   uint64_t npm = 0;
+  int64_t nac = 0, nam = 0, nae = 0, nsr0 = INT64_MIN, nsr1 = INT64_MIN, nsa0 = 0, nsa1 = 0;  // EXT record
   bool sbit[SPL];
   auto gather_next = [&](int kn) {
+    if (EXT) {  // uniform: scalar loads, consumed by the next step
+      const uint64_t* er = w.pod_ext + static_cast<size_t>(ebase + kn) * kDevExtU64;
+      nac = static_cast<int64_t>(er[0]);
+      nam = static_cast<int64_t>(er[1]);
+      nae = static_cast<int64_t>(er[2]);
+      nsr0 = static_cast<int64_t>(er[3]);
+      nsr1 = static_cast<int64_t>(er[4]);
+      nsa0 = static_cast<int64_t>(er[5]);
+      nsa1 = static_cast<int64_t>(er[6]);
+    }
     const uint64_t* img = L.ring[kn & (kRing - 1)];
     const uint64_t* pr = L.pods[kn & (kPodWin - 1)];
     uint64_t sw[SPL];
@@ -496,8 +515,12 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
   int k = 0;
   for (; k < np; ++k) {
     if (PROF) cyc_t = cyc();
-    nbytes += 4u * kHead * 8u + 64u;  // this pod's head and speculative record
+    nbytes += 4u * kHead * 8u + 64u + (EXT ? 64u : 0u);  // this pod's head, speculative record (and extension)
     const int64_t rc = nrc, rm = nrm, re = nre;
+    // what AddPod subtracts (EXT: calculateResource, else the fit request) and
+    // the shared scalars' fit requests / accounting
+    const int64_t ac = EXT ? nac : rc, am = EXT ? nam : rm, ae = EXT ? nae : re;
+    const int64_t sr0 = nsr0, sr1 = nsr1, sa0 = nsa0, sa1 = nsa1;
     const uint64_t pm = npm;                          // state bits the pod sets
     const uint64_t pin = swap_pairs(pm, w.swap_mask);  // ... and those it conflicts with
     const bool zero = (rc | rm | re) == 0;  // fitsRequest skips the resource checks
@@ -512,7 +535,8 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
 #pragma unroll
       for (int s = 0; s < SPL; ++s) {
         const int nd = snode[s];
-        const bool fit = zero | ((rc <= scpu[s]) & (rm <= smem[s]) & (re <= seph[s]));  // NodeResourcesFit
+        const bool fit = (zero | ((rc <= scpu[s]) & (rm <= smem[s]) & (re <= seph[s]))) &  // NodeResourcesFit
+                         (!EXT | ((sr0 <= ss0[s]) & (sr1 <= ss1[s])));
         const bool ok = (nd < hi) & sbit[s] & (sleft[s] >= 1) & ((sport[s] & pin) == 0) & fit;
         best = ok ? min(best, nd) : best;
       }
@@ -552,7 +576,8 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
           const int nd = snode[s];
           const bool in = (nd >= lo) & (nd < hi);
           const uint64_t sw = img[in ? (nd >> 6) - base : 0];
-          const bool fit = zero | ((rc <= scpu[s]) & (rm <= smem[s]) & (re <= seph[s]));
+          const bool fit = (zero | ((rc <= scpu[s]) & (rm <= smem[s]) & (re <= seph[s]))) &
+                           (!EXT | ((sr0 <= ss0[s]) & (sr1 <= ss1[s])));
           const bool ok =
               in & (((sw >> (nd & 63)) & 1ull) != 0) & (sleft[s] >= 1) & ((sport[s] & pin) == 0) & fit;
           best = ok ? min(best, nd) : best;
@@ -576,11 +601,15 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
 #pragma unroll
     for (int s = 0; s < SPL; ++s) {
       if (snode[s] == ans) {
-        scpu[s] -= rc;
-        smem[s] -= rm;
-        seph[s] -= re;
+        scpu[s] -= ac;
+        smem[s] -= am;
+        seph[s] -= ae;
         sleft[s] -= 1;
         sport[s] |= pm;
+        if (EXT) {
+          ss0[s] -= sa0;
+          ss1[s] -= sa1;
+        }
         hit = true;
       }
     }
@@ -590,6 +619,9 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
         SR_WAIT_VM(0);
         return -1;
       }
+      // EXT: the node's base free value of each shared scalar (0: no slot)
+      const int64_t b0 = EXT && erow0 >= 0 ? w.node_scal[static_cast<size_t>(erow0) * w.n_pad + ans] : 0;
+      const int64_t b1 = EXT && erow1 >= 0 ? w.node_scal[static_cast<size_t>(erow1) * w.n_pad + ans] : 0;
       const uint64_t* rec;
       if (ans < kNodeCache) {
         rec = L.cache[ans];
@@ -611,11 +643,15 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
       for (int s = 0; s < SPL; ++s) {
         if ((s == (ns >> 6)) & (lane == (ns & 63))) {
           snode[s] = ans;
-          scpu[s] = fc - rc;
-          smem[s] = fm - rm;
-          seph[s] = fe - re;
+          scpu[s] = fc - ac;
+          smem[s] = fm - am;
+          seph[s] = fe - ae;
           sleft[s] = pl - 1;
           sport[s] = pb | pm;
+          if (EXT) {
+            ss0[s] = b0 - sa0;
+            ss1[s] = b1 - sa1;
+          }
         }
       }
       const int tw = ans >> 6;
@@ -1355,7 +1391,7 @@ static_assert(64 * 32 * 8 <= sizeof(K2Lds), "domain path: touched bitmap of 2048
 template <int CH, int G, bool PROF>
 __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __restrict__ tl, const int p0,
                                           const int np, const int dbase, int& status, uint32_t& nbytes,
-                                          K2Stats& st) {
+                                          K2Stats& st, const int ebase = -1) {
   static_assert(kDevDomKeys == 4 && kDevDynTerms == 4, "the selects below unroll 4 key slots / terms");
   static_assert(G >= 1 && G <= kDevDynG, "pod groups of the domain-path record");
   const int lane = threadIdx.x & 63;
@@ -1366,6 +1402,10 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
   int snode[G], sleft[G], nslots = 0;
   int64_t scpu[G], smem[G], seph[G];
   uint64_t sport[G];
+  int64_t ss0[G], ss1[G];  // extension records: shared scalar resources' running free values
+  const bool ext = ebase >= 0;
+  const uint64_t erow = ext ? w.pod_ext[static_cast<size_t>(ebase) * kDevExtU64 + 7] : ~0ull;
+  const int erow0 = static_cast<int32_t>(static_cast<uint32_t>(erow)), erow1 = static_cast<int32_t>(erow >> 32);
   // pod 64 g + lane: its node and its domain in every key slot
   int pnode[G];
   int pdom[G][kDevDomKeys];
@@ -1375,6 +1415,7 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
     sleft[g] = 0;
     scpu[g] = smem[g] = seph[g] = 0;
     sport[g] = 0;
+    ss0[g] = ss1[g] = 0;
     pnode[g] = -1;
 #pragma unroll
     for (int kk = 0; kk < kDevDomKeys; ++kk) pdom[g][kk] = -1;
@@ -1384,15 +1425,19 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
   status = -1;
   int k = 0;
   // A pod's records in one register, lanes [0, kDevDynU64) its domain-path
-  // record, lanes [40, 46) its pod record, loaded one pod ahead (every pod
-  // step otherwise starts with a memory round trip for them)
-  static_assert(kDevDynU64 <= 40 && kRecU64 <= 24, "record lanes of the domain path");
+  // record, lanes [40, 46) its pod record, lanes [48, 56) its extension record,
+  // loaded one pod ahead (every pod step otherwise starts with a memory round
+  // trip for them)
+  static_assert(kDevDynU64 <= 40 && kRecU64 <= 8 && kDevExtU64 <= 8, "record lanes of the domain path");
   auto records = [&](int q) -> uint64_t {
     if (q >= np) return 0ull;
     if (lane < kDevDynU64) return w.dyn_pod[static_cast<size_t>(dbase + q) * kDevDynU64 + lane];
     if (lane >= 40 && lane < 40 + kRecU64) return w.pod_rec[static_cast<size_t>(p0 + q) * kRecU64 + (lane - 40)];
+    if (ext && lane >= 48 && lane < 48 + kDevExtU64)
+      return w.pod_ext[static_cast<size_t>(ebase + q) * kDevExtU64 + (lane - 48)];
     return 0ull;
   };
+  if (ext) nbytes += 8u * kDevExtU64 * static_cast<uint32_t>(np);
   uint64_t rv = records(0);
   uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
   auto stamp = [&](uint64_t& acc) {
@@ -1411,6 +1456,11 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
     const uint64_t pm = PR(3), r01 = PR(4), r23 = PR(5);
     const uint64_t pin = swap_pairs(pm, w.swap_mask);
     const bool zero = (rc | rm | re) == 0;
+    // what AddPod subtracts and the shared scalars (extension record)
+    auto EX = [&](int i) { return static_cast<int64_t>(readlane64(cur, 48 + i)); };
+    const int64_t ac = ext ? EX(0) : rc, am = ext ? EX(1) : rm, ae = ext ? EX(2) : re;
+    const int64_t sr0 = ext ? EX(3) : INT64_MIN, sr1 = ext ? EX(4) : INT64_MIN;
+    const int64_t sa0 = ext ? EX(5) : 0, sa1 = ext ? EX(6) : 0;
     // anti-affinity: domains refused per key slot (earlier pods it interacts with)
     uint64_t fdom[kDevDomKeys];
 #pragma unroll
@@ -1630,7 +1680,8 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
         const int src = in ? (snode[g] >> 6) - ch * 64 : 0;
         const uint64_t ws = (static_cast<uint64_t>(from_lane(static_cast<uint32_t>(sd >> 32), src)) << 32) |
                             from_lane(static_cast<uint32_t>(sd), src);
-        const bool fit = zero | ((rc <= scpu[g]) & (rm <= smem[g]) & (re <= seph[g]));
+        const bool fit = (zero | ((rc <= scpu[g]) & (rm <= smem[g]) & (re <= seph[g]))) & (sr0 <= ss0[g]) &
+                         (sr1 <= ss1[g]);
         const bool ok = in & (((ws >> (snode[g] & 63)) & 1ull) != 0) & (sleft[g] >= 1) & ((sport[g] & pin) == 0) & fit;
         best = ok ? min(best, snode[g]) : best;
       }
@@ -1648,11 +1699,13 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
       if (ballot(snode[g] == ans) != 0) {
         hit = true;
         if (snode[g] == ans) {
-          scpu[g] -= rc;
-          smem[g] -= rm;
-          seph[g] -= re;
+          scpu[g] -= ac;
+          smem[g] -= am;
+          seph[g] -= ae;
           sleft[g] -= 1;
           sport[g] |= pm;
+          ss0[g] -= sa0;
+          ss1[g] -= sa1;
         }
       }
     }
@@ -1662,16 +1715,20 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
                     fe = static_cast<int64_t>(rec[2]);
       const uint64_t pb = rec[3];
       const int pl = static_cast<int>(static_cast<int64_t>(rec[4]));
+      const int64_t b0 = ext && erow0 >= 0 ? w.node_scal[static_cast<size_t>(erow0) * w.n_pad + ans] : 0;
+      const int64_t b1 = ext && erow1 >= 0 ? w.node_scal[static_cast<size_t>(erow1) * w.n_pad + ans] : 0;
       nbytes += 40u;
 #pragma unroll
       for (int g = 0; g < G; ++g)
         if (lane + 64 * g == nslots) {
           snode[g] = ans;
-          scpu[g] = fc - rc;
-          smem[g] = fm - rm;
-          seph[g] = fe - re;
+          scpu[g] = fc - ac;
+          smem[g] = fm - am;
+          seph[g] = fe - ae;
           sleft[g] = pl - 1;
           sport[g] = pb | pm;
+          ss0[g] = b0 - sa0;
+          ss1[g] = b1 - sa1;
         }
       ++nslots;
       if (lane == 0) tl[ans >> 6] |= 1ull << (ans & 63);
@@ -1792,12 +1849,18 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   int status = -1;
   int wide = 0;
   uint32_t nbytes = 0;
-  const bool node_order = np <= 4 * 64 && w.k2_mode == 0;
   const int dbase = w.dyn_cand ? __builtin_amdgcn_readfirstlane(w.dyn_cand[ci]) : -1;
+  const int ebase = w.ext_cand ? __builtin_amdgcn_readfirstlane(w.ext_cand[ci]) : -1;
+  const bool node_order = np <= 4 * 64 && w.k2_mode == 0 && ebase < 0;
   if (dbase >= 0) {  // writes out_node itself
     wide = 3;
-    if (np <= 64) k2_domain<CH, 1, PROF>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes, st);
-    else k2_domain<CH, kDevDynG, PROF>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes, st);
+    if (np <= 64) k2_domain<CH, 1, PROF>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes, st, ebase);
+    else k2_domain<CH, kDevDynG, PROF>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes, st, ebase);
+  } else if (ebase >= 0) {  // extension records: pod order with the extended running state
+    int placed = k2_run<1, CH, PROF, true>(w, L, p0, np, status, st, nbytes, ebase);
+    wide = placed < 0 ? 1 : 0;
+    if (placed < 0) placed = k2_run<8, CH, PROF, true>(w, L, p0, np, status, st, nbytes, ebase);
+    for (int i = lane; i < np; i += 64) w.out_node[p0 + i] = i < placed ? L.omap[i] : -1;
   } else if (node_order) {  // writes out_node itself
     uint64_t* F = reinterpret_cast<uint64_t*>(&L);
     wide = 2;
@@ -1847,7 +1910,7 @@ hipError_t launch_k2(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEve
   const int n = w.n_list;
   if (n <= 0) return hipSuccess;
   const dim3 grid((n + 3) / 4), block(256);
-  if (!w.dyn_cand && w.k2_mode == 0 && w.max_np >= 1 && w.max_np <= 4 * 64 && w.k2_node_kernel) {
+  if (!w.dyn_cand && !w.ext_cand && w.k2_mode == 0 && w.max_np >= 1 && w.max_np <= 4 * 64 && w.k2_node_kernel) {
     const int G = w.max_np <= 64 ? 1 : (w.max_np <= 128 ? 2 : 4);
     const size_t lds = 4 * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
     if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);

@@ -20,6 +20,7 @@ constexpr int kDevDynU64 = 5 * kDevDynG + 1 + kDevSpreadSlots * (kDevDynG + 3);
 constexpr int kDevDomKeys = 4;          // key slots (host.hpp kDomKeys)
 constexpr int kNodePatchU64 = 12;       // node patch: {node, node_rec[8], node_free[3]}
 constexpr int kDevDynTerms = 4;         // terms per domain-path affinity set (host.hpp kDynTerms)
+constexpr int kDevExtU64 = 8;           // extension record words (host.hpp kExtU64)
 
 // Pointers into the device arena (layout: DESIGN.md §HBM layout).
 struct DevWorkload {
@@ -64,6 +65,13 @@ struct DevWorkload {
   int32_t dk_row[4];        // atom of domain 0 per table key slot, -1: node-local key
   const int32_t* sp_tab;    // spread base counts per domain / caps per node (host.hpp SpreadDyn)
   const int32_t* ds_info;   // [set][2 + 2 * 4] {terms, map_empty, (key slot, base-row atom) per term}
+  // extension records (pod-order and domain paths; null when the call has none):
+  // candidates whose AddPod accounting differs from the fit request or whose
+  // pods share a scalar resource
+  const int32_t* ext_cand;   // [n_cand] first record in pod_ext, -1: none
+  const uint64_t* pod_ext;   // [..][kDevExtU64] {acc cpu, acc mem, acc eph, req s0, req s1 (INT64_MIN: not
+                             //  listed), acc s0, acc s1, node_scal row of s0 | of s1 << 32 (-1: no slot)}
+  const int64_t* node_scal;  // [rows][n_pad] base free value (allocatable - requested) of a shared scalar
   // outputs / scratch
   uint64_t* S;         // [n_classes][Wp] static-class rows, followed by
   uint64_t* T;         // [n_t][Wp] capacity threshold rows (one table)

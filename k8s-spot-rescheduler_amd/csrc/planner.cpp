@@ -250,6 +250,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t o_dc = dyn ? pk.add(w.dyn_cand) : 0, o_dp = dyn ? pk.add(w.dyn_pod) : 0;
   const size_t o_dd = dyn ? pk.add(w.dk_dom) : 0, o_di = dyn ? pk.add(w.ds_info) : 0;
   const size_t o_st = dyn ? pk.add(w.sp_tab) : 0;
+  const bool ext = !w.ext_cand.empty();
+  const size_t o_ec = ext ? pk.add(w.ext_cand) : 0, o_ep = ext ? pk.add(w.pod_ext) : 0;
+  const size_t o_ns = ext ? pk.add(w.node_scal) : 0;
   // Records of the few spot nodes the encoder patched since the last
   // generation, {node, node_rec[8], node_free[3]} each: when the device holds
   // that generation they ride in this call's copy and K0 writes them into
@@ -360,6 +363,10 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.ds_info = dyn ? static_cast<const int32_t*>(at(o_di)) : nullptr;
   d.sp_tab = dyn ? static_cast<const int32_t*>(at(o_st)) : nullptr;
   d.n_dk = w.n_dk;
+  d.ext_cand = ext ? static_cast<const int32_t*>(at(o_ec)) : nullptr;
+  d.pod_ext = ext ? static_cast<const uint64_t*>(at(o_ep)) : nullptr;
+  d.node_scal = ext ? static_cast<const int64_t*>(at(o_ns)) : nullptr;
+  static_assert(sr::kDevExtU64 == sr::kExtU64, "extension record layout shared by encode.cpp and kernels.hip");
   static_assert(sr::kDevDynU64 == sr::kDynU64 && sr::kDevDomKeys == sr::kDomKeys && sr::kDevDynTerms == sr::kDynTerms &&
                     sr::kDevSpreadSlots == sr::kSpreadSlots,
                 "domain-path layout shared by encode.cpp and kernels.hip");
@@ -377,7 +384,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   // and every class program in its 8-slot record: K0 writes only the S-row
   // heads, K2 evaluates S words beyond them from the programs.
   d.s_head_only = 0;
-  if (ctx->s_head_only && w.Wp > 64 && w.dyn_cand.empty() && ctx->k2_mode == 0 && ctx->k2_node_kernel &&
+  if (ctx->s_head_only && w.Wp > 64 && w.dyn_cand.empty() && w.ext_cand.empty() && ctx->k2_mode == 0 && ctx->k2_node_kernel &&
       w.max_cand_pods >= 1 && w.max_cand_pods <= 256) {
     bool short_programs = true;
     for (int32_t k = 0; k < w.n_classes && short_programs; ++k)

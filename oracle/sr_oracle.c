@@ -1346,29 +1346,29 @@ static int o_spread_dyn_fallback(const oracle_snapshot *s, const sr_cluster *c, 
 }
 
 static int o_cand_fallback(const oracle_snapshot *s, const sr_cluster *c, const int32_t *pods, int32_t np) {
-  const sr_pods *P = &c->pods;
   for (int32_t i = 0; i < np; i++)
     if (oracle_pod_needs_fallback(s, c, pods[i])) return 1;
-  /* a pod followed by more pods of the candidate whose AddPod accounting
-   * differs from its fit request (init containers): outside the encoded set */
-  for (int32_t i = 0; i + 1 < np; i++)
-    if (o_acc(c, pods[i], 0) != P->req_milli_cpu[pods[i]] || o_acc(c, pods[i], 1) != P->req_memory[pods[i]] ||
-        o_acc(c, pods[i], 2) != P->req_ephemeral[pods[i]])
-      return 1;
   if (o_spread_dyn_fallback(s, c, pods, np)) return 1;
-  /* two pods of the candidate listing one scalar resource (the later one sees
-   * the earlier one's AddPod): outside the encoded set */
+  /* scalar resources: the planner's per-candidate table holds 64 distinct
+   * names, and it keeps a running state for at most 2 names listed by more
+   * than one pod of the candidate (the later pods see the earlier ones'
+   * AddPod); beyond that, the reference path */
   if (c->pod_scalar_off) {
-    int32_t entries = 0; /* the planner tracks up to 64 scalar entries per candidate */
-    for (int32_t i = 0; i < np; i++) entries += c->pod_scalar_off[pods[i] + 1] - c->pod_scalar_off[pods[i]];
-    if (entries > 64) return 1;
-  }
-  if (c->pod_scalar_off)
+    int32_t names[64], cnt[64], nn = 0, shared = 0;
     for (int32_t i = 0; i < np; i++)
-      for (int32_t a = c->pod_scalar_off[pods[i]]; a < c->pod_scalar_off[pods[i] + 1]; a++)
-        for (int32_t j = i + 1; j < np; j++)
-          for (int32_t b = c->pod_scalar_off[pods[j]]; b < c->pod_scalar_off[pods[j] + 1]; b++)
-            if (c->pod_scalar_name[a] == c->pod_scalar_name[b]) return 1;
+      for (int32_t a = c->pod_scalar_off[pods[i]]; a < c->pod_scalar_off[pods[i] + 1]; a++) {
+        int32_t u = 0;
+        while (u < nn && names[u] != c->pod_scalar_name[a]) u++;
+        if (u < nn) {
+          if (++cnt[u] == 2) shared++;
+        } else {
+          if (nn == 64) return 1;
+          names[nn] = c->pod_scalar_name[a];
+          cnt[nn++] = 1;
+        }
+      }
+    if (shared > 2) return 1;
+  }
   return 0;
 }
 

@@ -87,27 +87,18 @@ def test_gpu_domain_path_limit_falls_back(checker):
     assert int(p.status[0]) == capi.SR_CAND_FALLBACK
 
 
-def _strip_init(cands):
-    # init containers make AddPod's accounting differ from the fit request:
-    # such a pod followed by others sends its candidate to the fallback path
-    for c in cands:
-        for p in c:
-            p.init_containers = []
-            for ct in p.containers:
-                ct.scalar = {}
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(8))
 def test_gpu_large_shared_key_candidates(checker, seed):
     """65-200 pods per candidate interacting through zone / team anti-affinity
     (and affinity on half the seeds): the domain path with 2-4 pod groups,
-    bit-exact with the oracle and without fallback."""
+    bit-exact with the oracle and without fallback -- init containers and
+    scalar resources included (extension records)."""
     from test_gpu_parity import run_scenario
     nodes_, spot_pods, cands = rand_scenario(7400 + seed, n_spot=24 + 4 * seed, n_cand=3, max_pods=200,
                                              features=False, anti=0.2, aff=0.15 if seed % 2 else 0.0,
                                              shared_keys=True, valid_selectors=True)
-    _strip_init(cands)
+
     for i, c in enumerate(cands):  # 65 .. 200 pods each
         while len(c) < 65 + 45 * i:
             c.extend(cands[(i + 1) % 3][:65 + 45 * i - len(c)] or [c[0]])

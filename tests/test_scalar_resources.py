@@ -4,12 +4,18 @@ accounting: the NodeResourcesFit ScalarResources loop behind CheckPredicates
 not vendored: parity unpinned beyond the hand-derived answers here and in
 tests/known_answer.py).
 
-The planner encodes a pod's scalar checks as base-snapshot atoms.  That is
-exact while no earlier pod of the same candidate can change the node's
-Requested for the same name, so a candidate where two pods list one scalar
-resource goes to the reference path, as does a pod whose AddPod accounting
-differs from its fit request (init containers) when later pods of its
-candidate follow it.  Checked on the oracle (CPU) and the GPU (C-ABI)."""
+The planner encodes a pod's scalar checks as base-snapshot atoms, exact while
+no earlier pod of the same candidate changes the node's Requested for the
+same name.  A candidate where two pods list one scalar resource (up to two
+such names), or where a pod whose AddPod accounting differs from its fit
+request (init containers) is followed by others, is planned with extension
+records: K2's running state per touched node subtracts the accounting
+(calculateResource: regular containers + Overhead) and keeps the shared
+scalars' free values.  Rules assumed (k8s v1.19.2, parity unpinned):
+fitsRequest checks alloc[s] >= request[s] + requested[s] for every listed
+name, the request being max(sum of containers, each init container) +
+Overhead; NodeInfo.AddPod adds the containers' sum + Overhead only.
+Checked on the oracle (CPU) and the GPU (C-ABI)."""
 import ctypes
 
 import numpy as np
@@ -42,14 +48,42 @@ def nodes3():
 def cases():
     """(name, spot pods, candidates, expected oracle statuses, expected mappings)"""
     yield ("one_gpu_pod", [[], [], []], [[gpod("p")]], [OK], [[0]])
-    yield ("two_pods_share_a_name_fall_back", [[], [], []], [[gpod("p"), gpod("q")]], [FB], [[-1, -1]])
+    # a has one GPU: p takes it, q sees p's AddPod there and goes to c
+    yield ("two_pods_share_a_name", [[], [], []], [[gpod("p"), gpod("q")]], [OK], [[0, 2]])
+    # c's four GPUs hold four more; the sixth pod finds none left
+    yield ("shared_name_runs_out", [[], [], []], [[gpod("p%d" % i) for i in range(5)]], [OK], [[0, 2, 2, 2, 2]])
+    yield ("shared_name_exhausted_fails", [[], [], []], [[gpod("p%d" % i) for i in range(6)]], [5],
+           [[0, 2, 2, 2, 2, -1]])
+    # two GPUs per pod: a (1, used by u) never fits, c takes two pods, the third fits nowhere
+    yield ("shared_name_two_each", [[gpod("u", gpu=1)], [], []],
+           [[gpod("p", gpu=2), gpod("q", gpu=2)], [gpod("p", gpu=2), gpod("q", gpu=2), gpod("r", gpu=2)]],
+           [OK, 2], [[2, 2], [2, 2, -1]])
+    # an init container's GPU is in the fit request, not in AddPod's accounting: a fits both
+    yield ("shared_name_init_container_not_accounted", [[], [], []],
+           [[gpod("i", gpu=0, init_gpu=1), gpod("j", gpu=0, init_gpu=1)]], [OK], [[0, 0]])
+    # two names in the running slots: hugepages listed with 0 on nodes allocating none still passes
+    yield ("two_shared_names", [[], [], []],
+           [[Pod("p", containers=[Container(cpu_milli=100, scalar={G: 1, "hugepages-2Mi": 0})]),
+             Pod("q", containers=[Container(cpu_milli=100, scalar={G: 1, "hugepages-2Mi": 0})])]],
+           [OK], [[0, 2]])
+    # three names listed by two pods each: beyond the two running scalar slots
+    yield ("three_shared_names_fall_back", [[], [], []],
+           [[Pod("p", containers=[Container(cpu_milli=100, scalar={G: 1, "x.io/a": 1, "x.io/b": 1})]),
+             Pod("q", containers=[Container(cpu_milli=100, scalar={G: 1, "x.io/a": 1, "x.io/b": 1})])]],
+           [FB], [[-1, -1]])
     yield ("different_names_are_independent", [[], [], []],
            [[gpod("p"), Pod("q", containers=[Container(cpu_milli=10, scalar={"hugepages-2Mi": 0})])]], [OK], [[0, 0]])
     yield ("base_usage_counts", [[gpod("u")], [], []], [[gpod("p")]], [OK], [[2]])
     yield ("listed_zero_with_zero_cpu_falls_back", [[], [], []], [[gpod("p", gpu=0, cpu=0)]], [FB], [[-1]])
-    yield ("init_container_pod_before_others_falls_back", [[], [], []],
-           [[Pod("i", containers=[Container(cpu_milli=100)], init_containers=[Container(cpu_milli=900)]),
-             Pod("q", containers=[Container(cpu_milli=100)])]], [FB], [[-1, -1]])
+    # i fits a with its init container's 3950m but AddPod adds only 100m: q (3800m) still fits a
+    # (subtracting the fit request instead would send q to b)
+    yield ("init_container_pod_before_others", [[], [], []],
+           [[Pod("i", containers=[Container(cpu_milli=100)], init_containers=[Container(cpu_milli=3950)]),
+             Pod("q", containers=[Container(cpu_milli=3800)])]], [OK], [[0, 0]])
+    # fit 3000m, accounting 1000m: two per 4000m node (a after one: 3000 free, after two: 2000 < 3000)
+    yield ("init_container_pods_fill_a_node", [[], [], []],
+           [[Pod("i%d" % k, containers=[Container(cpu_milli=1000)], init_containers=[Container(cpu_milli=3000)])
+             for k in range(5)]], [OK], [[0, 0, 1, 1, 2]])
     yield ("init_container_pod_last_is_planned", [[], [], []],
            [[Pod("q", containers=[Container(cpu_milli=100)]),
              Pod("i", containers=[Container(cpu_milli=100)], init_containers=[Container(cpu_milli=3950)])]],
@@ -150,3 +184,76 @@ def test_gpu_random_scalar_clusters(checker, seed):
                 p.containers[0].cpu_milli = 10
     _, o, p = run_scenario(checker, nodes, spot_pods, cands)
     assert sum(int(s) != FB for s in p.status) >= 1
+
+
+def init_and_gpu_scenario(seed):
+    """Random clusters where most pods carry init containers (fit request !=
+    AddPod accounting) and most candidates list one GPU name in several pods
+    (a running scalar state per touched node), some hugepages too."""
+    import random
+    nodes, spot_pods, cands = rand_scenario(9100 + seed, n_spot=6 + seed % 20, n_cand=12, max_pods=4 + seed % 12,
+                                            features=seed % 2 == 0)
+    r = random.Random(seed)
+    for n in nodes:
+        if r.random() < 0.8:
+            n.scalar = {G: r.choice([0, 1, 2, 4, 8]), "hugepages-2Mi": r.choice([0, 8 << 20])}
+    for c in cands:
+        gpu_cand = r.random() < 0.7
+        for p in c:
+            if r.random() < 0.5:
+                p.init_containers = [Container(cpu_milli=r.choice([200, 1500, 3000]),
+                                               memory=r.choice([0, 1 * GiB, 6 * GiB]),
+                                               scalar={G: r.choice([1, 2])} if gpu_cand and r.random() < 0.3 else {})]
+            if gpu_cand and r.random() < 0.6:
+                p.containers[0].scalar = {G: r.choice([0, 1, 1, 2])}
+                if r.random() < 0.2:
+                    p.containers[0].scalar["hugepages-2Mi"] = r.choice([2 << 20, 4 << 20])
+                if p.containers[0].cpu_milli == 0:
+                    p.containers[0].cpu_milli = 10
+    return nodes, spot_pods, cands
+
+
+def test_oracle_plans_init_and_shared_scalar_candidates():
+    """The extension cases are planned (not fallback) by the oracle for most candidates of the random clusters
+    below, and some of them fail late (the running state matters)."""
+    planned = shared = 0
+    for seed in range(20):
+        nodes, spot_pods, cands = init_and_gpu_scenario(seed)
+        flat = [p for c in cands for p in c]
+        sc = Scenario(nodes, spot_pods, flat)
+        off = np.cumsum([0] + [len(c) for c in cands]).astype(np.int32)
+        o = oracle_plan(sc.oracle_snapshot(), sc.ptr, off, np.arange(sc.q0, sc.q0 + len(flat), dtype=np.int32),
+                        mode=1)
+        for k, c in enumerate(cands):
+            if int(o["status"][k]) == FB:
+                continue
+            planned += 1
+            shared += sum(1 for p in c if any(G in ct.scalar for ct in p.containers + p.init_containers)) >= 2
+    assert planned >= 120 and shared >= 40, (planned, shared)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(20))
+def test_gpu_random_init_and_shared_scalar_candidates(checker, seed):
+    """Init-container-heavy and GPU-sharing candidates on the device's extension records, bit-exact with the
+    oracle (every status and every pod's node)."""
+    from test_gpu_parity import run_scenario
+    nodes, spot_pods, cands = init_and_gpu_scenario(seed)
+    run_scenario(checker, nodes, spot_pods, cands)
+
+
+@pytest.mark.gpu
+def test_gpu_large_extension_candidates(checker):
+    """Extension records on candidates of 65-300 pods (pod order with 64 and 512 touched-node slots)."""
+    from test_gpu_parity import run_scenario
+    nodes = [Node("n%d" % i, cpu_milli=4000 + 1000 * (i % 5), memory=64 * GiB, scalar={G: 2 * (i % 4)})
+             for i in range(160)]
+    cands = []
+    for npods in (65, 130, 300):
+        c = []
+        for k in range(npods):
+            c.append(Pod("p%d_%d" % (npods, k), containers=[Container(cpu_milli=100 + 50 * (k % 7), scalar={G: 1})],
+                         init_containers=[Container(cpu_milli=1500)] if k % 3 == 0 else []))
+        cands.append(c)
+    _, o, p = run_scenario(checker, nodes, [[] for _ in nodes], cands)
+    assert all(int(s) != FB for s in o["status"])
