@@ -42,7 +42,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 from spotplanner import capi  # noqa: E402
 from spotplanner.planner import PredicateChecker  # noqa: E402
-from spotplanner.synth import SynthCluster, new_node_map, pods_for_deletion, shard  # noqa: E402
+from spotplanner.synth import REALISTIC, SynthCluster, new_node_map, pods_for_deletion, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 DEFAULT_OD = {1: 10, 2: 300, 3: 1500, 4: 15000, 5: 300}
@@ -53,11 +53,15 @@ WORKLOAD_KIND = {1: "rescheduler_test-style, cpu/mem requests only",
                  5: "host-port + DaemonSet heavy"}
 
 
-def workload_name(config, n_nodes, n_od, n_spot, n_pods, world, scaling):
+def workload_name(config, n_nodes, n_od, n_spot, n_pods, world, scaling, variant="baseline"):
     """config.workload: the cluster this run actually planned (node, on-demand,
     spot and pod counts), and how its candidates were split over the ranks."""
     s = "C%d %d nodes (%d od / %d spot) / %d pods, %s" % (config, n_nodes, n_od, n_spot, n_pods,
                                                           WORKLOAD_KIND[config])
+    if variant == "realistic":
+        s += ("; realistic variant: %d%% StatefulSet pods with a zonal EBS CSI claim (CSINode limit 25), "
+              "%d%% with an init container, %d%% of GPU-node pods asking for a GPU"
+              % tuple(round(100 * REALISTIC[k]) for k in ("stateful_fraction", "init_fraction", "gpu_fraction")))
     if world > 1:
         s += "; %s scaling: %d candidates sharded c %% %d" % (scaling, n_od, world)
     return s
@@ -275,6 +279,9 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--variant", default="baseline", choices=["baseline", "realistic"],
+                    help="realistic: the config with StatefulSet volumes, init containers and GPU pods "
+                         "(reports the fallback ratio on them); baseline: BASELINE.json's config as specified")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: the config's cluster, candidates split over the ranks; weak: N x its candidates")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -301,7 +308,8 @@ def main():
     torch.cuda.set_device(local)
 
     lib = capi.load_planner()
-    sc = SynthCluster(args.config, n_on_demand=cluster_on_demand(args.config, world, args.scaling))
+    sc = SynthCluster(args.config, n_on_demand=cluster_on_demand(args.config, world, args.scaling),
+                      **(REALISTIC if args.variant == "realistic" else {}))
     nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
     # run()'s candidate lists (rescheduler.go:228-264): GetPodsForDeletionOnNodeDrain + the
     # DaemonSet-owner filter, on the host (sr_pods_for_deletion)
@@ -568,7 +576,8 @@ def main():
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "int64",
             "data": "synthetic",
             "config": {"workload": workload_name(args.config, sc.n_nodes, len(nm.on_demand), len(nm.spot),
-                                                 sc.n_pods, world, args.scaling),
+                                                 sc.n_pods, world, args.scaling, args.variant),
+                       "variant": args.variant,
                        "nodes": sc.n_nodes, "pods": sc.n_pods, "on_demand_nodes": int(len(nm.on_demand)),
                        "spot_nodes": int(len(nm.spot)), "candidates": int(len(cand_off) - 1),
                        "candidate_pods": int(len(cand_pods)), "parallelism": "candidates c%%%d" % world,

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SR_ABI_VERSION 4
+#define SR_ABI_VERSION 5
 
 /* ------------------------------------------------------------------ status */
 typedef int32_t sr_status;
@@ -197,6 +197,59 @@ typedef struct {
   const uint8_t *terminating;    /* [pods.n] DeletionTimestamp != nil: never counted */
 } sr_spread;
 
+/* The volume filters of CheckPredicates (rescheduler.go:344) [upstream k8s
+ * v1.19.2 plugins volumebinding, volumezone, volumerestrictions and
+ * nodevolumelimits: EBSLimits, GCEPDLimits, AzureDiskLimits (non-CSI) and
+ * NodeVolumeLimits (CSI)], with every PersistentVolumeClaim already resolved by
+ * the shim through the scheduler's own listers (PVC -> PV, StorageClass,
+ * CSINode).  A pod whose volumes the shim cannot describe here (an unbound
+ * claim with WaitForFirstConsumer binding, an RBD volume, a lister error) keeps
+ * SR_POD_FB_VOLUMES; without this table every pod with such volumes does. */
+#define SR_DISK_GCE_PD   0  /* GCEPersistentDisk.PDName: two mounts conflict unless both are read-only */
+#define SR_DISK_AWS_EBS  1  /* AWSElasticBlockStore.VolumeID: two mounts always conflict */
+#define SR_DISK_ISCSI    2  /* ISCSI.IQN: two mounts conflict unless both are read-only */
+typedef struct {
+  /* VolumeBinding PreFilter fails (an unbound claim with Immediate binding, a
+   * claim or volume the listers do not find): the pod fits no node. [pods.n] */
+  const uint8_t *prefilter_fail;
+  /* VolumeRestrictions: the pod's inline GCE PD / AWS EBS / ISCSI volumes */
+  const int32_t *disk_off;         /* [pods.n+1] */
+  const int32_t *disk_kind;        /* SR_DISK_* */
+  const int32_t *disk_id;          /* interned PDName / VolumeID / IQN */
+  const uint8_t *disk_ro;          /* ReadOnly */
+  /* volume limits: the pod's attachable volumes, each (limit key, unique volume
+   * name) once per pod -- the filters' unique names of inline and PV-backed
+   * volumes (a claim without a volume counts as one unique name of its own) */
+  const int32_t *att_off;          /* [pods.n+1] */
+  const int32_t *att_key;          /* interned limit key: attachable-volumes-aws-ebs, -gce-pd, -azure-disk, -csi-<driver> */
+  const int32_t *att_id;           /* interned unique volume name */
+  const uint8_t *att_noncsi;       /* non-CSI filter key: checked whenever the pod has such a volume, even one already attached */
+  /* the limit of each key per node (non-CSI: Allocatable or the filter's
+   * default; CSI: the CSINode driver's allocatable count).  A key without an
+   * entry on a node never refuses there. */
+  const int32_t *limit_off;        /* [nodes.n+1] */
+  const int32_t *limit_key;
+  const int64_t *limit;
+  /* VolumeZone: per bound PV, each zone / region label (one of zone_keys) with
+   * the values volumehelpers.LabelZonesToSet parses ("a__b" -> {a, b}; a label
+   * that fails to parse is skipped by the filter and not passed) */
+  const int32_t *zone_off;         /* [pods.n+1] */
+  const int32_t *zone_key;
+  const int32_t *zone_val_off;     /* [zones+1] */
+  const int32_t *zone_vals;
+  int32_t zone_keys[4];            /* interned failure-domain.beta.kubernetes.io/zone, .../region,
+                                      topology.kubernetes.io/zone, .../region (-1: never interned) */
+  /* VolumeBinding: Spec.NodeAffinity.Required of each bound PV
+   * (volumeutil.CheckNodeAffinity: MatchNodeSelectorTerms on the node's labels
+   * with no fields, so a matchFields requirement reads "") */
+  const int32_t *pv_off;           /* [pods.n+1] pods -> PVs with a Required node affinity */
+  const int32_t *pv_term_off;      /* [pvs+1] PVs -> NodeSelectorTerms */
+  const int32_t *term_expr_off;    /* [terms+1] */
+  const int32_t *term_field_off;   /* [terms+1] */
+  const int32_t *expr_key, *expr_op, *expr_val_off, *expr_vals;
+  const int32_t *field_key, *field_op, *field_val_off, *field_vals;
+} sr_volumes;
+
 typedef struct {
   sr_nodes nodes;
   sr_pods  pods;
@@ -256,6 +309,8 @@ typedef struct {
    * carries SR_POD_FB_TOPOLOGY_SPREAD).  Pod labels and namespaces come from
    * pod_affinity, which must be given with it. */
   const sr_spread *spread;
+  /* Volume filters (ABI 5).  NULL: pods with volumes carry SR_POD_FB_VOLUMES. */
+  const sr_volumes *volumes;
 } sr_cluster;
 #define SR_STR_LABEL_VALUE 1u
 #define SR_STR_LABEL_KEY   2u
@@ -409,7 +464,8 @@ const char *sr_build_info(void);
  * its end between versions (ABI 4 added str_label, the scalar tables, acc_*
  * and spread): a binding compares this with the SR_ABI_VERSION it was built
  * against before its first call and refuses to run on a mismatch, since the
- * library would otherwise read fields past the end of a shorter struct. */
+ * library would otherwise read fields past the end of a shorter struct (ABI 5
+ * added sr_cluster.volumes). */
 int32_t     sr_abi_version(void);
 
 /* Batched findSpotNodeForPod (rescheduler.go:338-353): for each pod, the first

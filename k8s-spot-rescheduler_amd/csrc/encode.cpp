@@ -29,6 +29,7 @@
 // place).  Pod specs and requirements are interned by content across calls,
 // so a call canonicalises only specs it has never seen.
 #include <algorithm>
+#include <array>
 #include <map>
 #include <atomic>
 #include <chrono>
@@ -38,6 +39,7 @@
 #include <functional>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "host.hpp"
@@ -75,7 +77,28 @@ int32_t serial_pods() {
 
 bool in_range(int64_t v) { return v >= 0 && v < kQuantityLimit; }
 
-enum : int32_t { REQ_LABEL_EQ = 0, REQ_LABEL_EXPR = 1, REQ_FIELD = 2 };
+// HostPortInfo.CheckConflict of one (protocol, port) entry pair by their IPs
+// (0.0.0.0 = -1 meets every IP, an IP meets 0.0.0.0 and itself), and
+// VolumeRestrictions' isVolumeConflict for disks (-1: read-write, meets every
+// mount; kReadOnlyMount: meets read-write mounts only).
+bool port_conflict(int32_t a, int32_t b) { return a == -1 || b == -1 || (a == b && a != kReadOnlyMount); }
+
+// (limit key, unique volume name) as one word.
+inline uint64_t att_word(int32_t key, int32_t id) {
+  return static_cast<uint64_t>(static_cast<uint32_t>(key)) << 32 | static_cast<uint32_t>(id);
+}
+// The pod's attachable volumes of limit key `key`.
+int32_t pod_att_of(const sr_cluster* c, int32_t pod, int32_t key) {
+  int32_t n = 0;
+  for (int32_t a = c->volumes->att_off[pod]; a < c->volumes->att_off[pod + 1]; ++a) n += c->volumes->att_key[a] == key;
+  return n;
+}
+constexpr int32_t kNoName = INT32_MIN;  // no shared scalar name (volume keys are negative names)
+
+// REQ_ZONE: VolumeZone's check of one PV zone / region label {key, zone keys
+// [4], values}: a node passes when it carries none of the four zone keys, or
+// its value of `key` ("" when absent) is one of the values.
+enum : int32_t { REQ_LABEL_EQ = 0, REQ_LABEL_EXPR = 1, REQ_FIELD = 2, REQ_ZONE = 3 };
 
 inline uint64_t mix(uint64_t h, uint64_t x) {
   h = (h ^ x) * 0xff51afd7ed558ccdull;
@@ -180,10 +203,62 @@ void for_each_spec_word(const sr_cluster* c, const sr_pods& P, int32_t pod, F&& 
     f(P.tol_val[i]);
     f(P.tol_effect[i]);
   }
-  for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i) {
-    f(P.port_proto[i]);
-    f(P.port_num[i]);
-    f(P.port_ip[i]);
+  for_each_port(c, pod, [&](int32_t proto, int32_t port, int32_t ip) {  // host ports and inline disks
+    f(proto);
+    f(port);
+    f(ip);
+  });
+  if (has_volume_spec(c, pod)) {  // the volume filters' static part (attachable volumes: counts per key)
+    const sr_volumes* V = c->volumes;
+    f(-9);
+    f(V->prefilter_fail[pod]);
+    f(V->zone_off[pod + 1] - V->zone_off[pod]);
+    for (int32_t z = V->zone_off[pod]; z < V->zone_off[pod + 1]; ++z) {
+      f(V->zone_key[z]);
+      f(V->zone_val_off[z + 1] - V->zone_val_off[z]);
+      for (int32_t v = V->zone_val_off[z]; v < V->zone_val_off[z + 1]; ++v) f(V->zone_vals[v]);
+    }
+    for (int i = 0; i < 4; ++i) f(V->zone_keys[i]);
+    f(V->pv_off[pod + 1] - V->pv_off[pod]);
+    for (int32_t pv = V->pv_off[pod]; pv < V->pv_off[pod + 1]; ++pv) {
+      f(V->pv_term_off[pv + 1] - V->pv_term_off[pv]);
+      for (int32_t t = V->pv_term_off[pv]; t < V->pv_term_off[pv + 1]; ++t) {
+        f(V->term_expr_off[t + 1] - V->term_expr_off[t]);
+        for (int32_t e = V->term_expr_off[t]; e < V->term_expr_off[t + 1]; ++e) {
+          f(V->expr_key[e]);
+          f(V->expr_op[e]);
+          f(V->expr_val_off[e + 1] - V->expr_val_off[e]);
+          for (int32_t v = V->expr_val_off[e]; v < V->expr_val_off[e + 1]; ++v) f(V->expr_vals[v]);
+          f(label_req_strings_ok(c, V->expr_key[e], V->expr_vals, V->expr_val_off[e], V->expr_val_off[e + 1]) ? 1 : 0);
+          if (V->expr_op[e] == SR_OP_GT || V->expr_op[e] == SR_OP_LT)
+            for (int32_t v = V->expr_val_off[e]; v < V->expr_val_off[e + 1]; ++v) {
+              int64_t x = 0;
+              f(str_int(c, V->expr_vals[v], &x) ? 1 : 0);
+              f(static_cast<int32_t>(static_cast<uint64_t>(x)));
+              f(static_cast<int32_t>(static_cast<uint64_t>(x) >> 32));
+            }
+        }
+        f(V->term_field_off[t + 1] - V->term_field_off[t]);
+        for (int32_t g = V->term_field_off[t]; g < V->term_field_off[t + 1]; ++g) {
+          f(V->field_key[g]);
+          f(V->field_op[g]);
+          f(V->field_val_off[g + 1] - V->field_val_off[g]);
+          for (int32_t v = V->field_val_off[g]; v < V->field_val_off[g + 1]; ++v) f(V->field_vals[v]);
+        }
+      }
+    }
+    std::vector<std::pair<int32_t, int32_t>> per_key;  // (key, count), the ids themselves are not static
+    for (int32_t a = V->att_off[pod]; a < V->att_off[pod + 1]; ++a) {
+      auto it = std::find_if(per_key.begin(), per_key.end(), [&](const auto& x) { return x.first == V->att_key[a]; });
+      if (it == per_key.end()) per_key.emplace_back(V->att_key[a], 1);
+      else ++it->second;
+    }
+    std::sort(per_key.begin(), per_key.end());
+    f(static_cast<int32_t>(per_key.size()));
+    for (const auto& kc : per_key) {
+      f(kc.first);
+      f(kc.second);
+    }
   }
   if (has_spread(c, pod)) {  // topology spread constraints (with the pod's namespace and self-match)
     f(-8);
@@ -204,7 +279,7 @@ void for_each_spec_word(const sr_cluster* c, const sr_pods& P, int32_t pod, F&& 
 bool has_static_spec(const sr_cluster* c, const sr_pods& P, int32_t pod) {
   return P.sel_off[pod] != P.sel_off[pod + 1] || P.tol_off[pod] != P.tol_off[pod + 1] ||
          P.port_off[pod] != P.port_off[pod + 1] || P.aff_required[pod] != 0 || has_scalars(c, pod) ||
-         has_spread(c, pod);
+         has_spread(c, pod) || has_ports(c, pod) || has_volume_spec(c, pod);
 }
 
 // Requirement word group {len, type, key, op, sorted unique values}.
@@ -230,7 +305,67 @@ struct SpecDraft {
   std::vector<int32_t> tol, ports;
   std::vector<int64_t> scalars;  // {name, fit request}*, sorted by name
   std::vector<int32_t> spread;   // spread_words
+  // volume filters: requirement groups ANDed (VolumeZone, single-term PV node
+  // affinity) and the PV selectors with several terms ({n terms, per term
+  // {n groups, groups...}} each)
+  std::vector<int32_t> vsel;
+  std::vector<std::vector<int32_t>> vpv;
 };
+
+// Drafts one NodeSelectorTerm (MatchNodeSelectorTerms [upstream core/v1/helper]:
+// NodeSelectorRequirementsAsSelector over the expressions, As-FieldSelector
+// over the fields) into requirement groups; false when it fails to build
+// (it matches nothing).  `no_fields`: the PV form (volumeutil.CheckNodeAffinity
+// passes no fields, so a field requirement reads "" and is decided here).
+bool draft_term(const sr_cluster* c, const int32_t* expr_key, const int32_t* expr_op, const int32_t* expr_val_off,
+                const int32_t* expr_vals, int32_t e0, int32_t e1, const int32_t* field_key, const int32_t* field_op,
+                const int32_t* field_val_off, const int32_t* field_vals, int32_t f0, int32_t f1, bool no_fields,
+                std::vector<int32_t>& term, int32_t* n_groups) {
+  bool valid = true;
+  term.clear();
+  int32_t n = 0;
+  for (int32_t e = e0; e < e1 && valid; ++e) {
+    const int32_t nv = expr_val_off[e + 1] - expr_val_off[e];
+    const int32_t op = expr_op[e];
+    if (expr_key[e] == c->id_empty) valid = false;  // validateLabelKey("") fails
+    // validateLabelKey / validateLabelValue on every value (every operator)
+    else if (!label_req_strings_ok(c, expr_key[e], expr_vals, expr_val_off[e], expr_val_off[e + 1]))
+      valid = false;
+    else if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) valid = false;
+    else if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) valid = false;
+    else if (op == SR_OP_GT || op == SR_OP_LT) {  // exactly one value, an integer (labels.NewRequirement)
+      int64_t x;
+      valid = nv == 1 && str_int(c, expr_vals[expr_val_off[e]], &x);
+    } else if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST) {
+      valid = false;
+    }
+    if (valid && (op == SR_OP_GT || op == SR_OP_LT)) {  // {value id, its integer (lo, hi)}
+      int64_t x = 0;
+      str_int(c, expr_vals[expr_val_off[e]], &x);
+      const int32_t w[3] = {expr_vals[expr_val_off[e]], static_cast<int32_t>(static_cast<uint64_t>(x)),
+                            static_cast<int32_t>(static_cast<uint64_t>(x) >> 32)};
+      term.insert(term.end(), {6, REQ_LABEL_EXPR, expr_key[e], op, w[0], w[1], w[2]});
+      ++n;
+    } else if (valid) {
+      put_req(term, REQ_LABEL_EXPR, expr_key[e], op, expr_vals + expr_val_off[e], nv);
+      ++n;
+    }
+  }
+  for (int32_t f = f0; f < f1 && valid; ++f) {  // NodeSelectorRequirementsAsFieldSelector
+    const int32_t nv = field_val_off[f + 1] - field_val_off[f];
+    const int32_t op = field_op[f];
+    valid = (op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 1;
+    if (valid && no_fields) {  // fields.Set(nil): every key reads ""
+      const bool eq = field_vals[field_val_off[f]] == c->id_empty && c->id_empty != -1;
+      valid = op == SR_OP_IN ? eq : !eq;
+    } else if (valid) {
+      put_req(term, REQ_FIELD, field_key[f], op, &field_vals[field_val_off[f]], 1);
+      ++n;
+    }
+  }
+  *n_groups = n;
+  return valid;
+}
 
 void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
   const sr_pods& P = c->pods;
@@ -245,46 +380,10 @@ void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
       const int32_t e0 = P.term_expr_off[t], e1 = P.term_expr_off[t + 1];
       const int32_t f0 = P.term_field_off[t], f1 = P.term_field_off[t + 1];
       if (e0 == e1 && f0 == f1) continue;  // an empty term selects nothing
-      bool valid = true;
-      term.clear();
       int32_t n = 0;
-      for (int32_t e = e0; e < e1 && valid; ++e) {
-        const int32_t nv = P.expr_val_off[e + 1] - P.expr_val_off[e];
-        const int32_t op = P.expr_op[e];
-        if (P.expr_key[e] == c->id_empty) valid = false;  // validateLabelKey("") fails
-        // validateLabelKey / validateLabelValue on every value (every operator)
-        else if (!label_req_strings_ok(c, P.expr_key[e], P.expr_vals, P.expr_val_off[e], P.expr_val_off[e + 1]))
-          valid = false;
-        else if ((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 0) valid = false;
-        else if ((op == SR_OP_EXISTS || op == SR_OP_DOES_NOT_EXIST) && nv != 0) valid = false;
-        else if (op == SR_OP_GT || op == SR_OP_LT) {  // exactly one value, an integer (labels.NewRequirement)
-          int64_t x;
-          valid = nv == 1 && str_int(c, P.expr_vals[P.expr_val_off[e]], &x);
-        } else if (op != SR_OP_IN && op != SR_OP_NOT_IN && op != SR_OP_EXISTS && op != SR_OP_DOES_NOT_EXIST) {
-          valid = false;
-        }
-        if (valid && (op == SR_OP_GT || op == SR_OP_LT)) {  // {value id, its integer (lo, hi)}
-          int64_t x = 0;
-          str_int(c, P.expr_vals[P.expr_val_off[e]], &x);
-          const int32_t w[3] = {P.expr_vals[P.expr_val_off[e]], static_cast<int32_t>(static_cast<uint64_t>(x)),
-                                static_cast<int32_t>(static_cast<uint64_t>(x) >> 32)};
-          term.insert(term.end(), {6, REQ_LABEL_EXPR, P.expr_key[e], op, w[0], w[1], w[2]});
-          ++n;
-        } else if (valid) {
-          put_req(term, REQ_LABEL_EXPR, P.expr_key[e], op, P.expr_vals + P.expr_val_off[e], nv);
-          ++n;
-        }
-      }
-      for (int32_t f = f0; f < f1 && valid; ++f) {  // NodeSelectorRequirementsAsFieldSelector
-        const int32_t nv = P.field_val_off[f + 1] - P.field_val_off[f];
-        const int32_t op = P.field_op[f];
-        valid = (op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 1;
-        if (valid) {
-          put_req(term, REQ_FIELD, P.field_key[f], op, &P.field_vals[P.field_val_off[f]], 1);
-          ++n;
-        }
-      }
-      if (!valid) continue;  // a term that fails to build matches nothing
+      if (!draft_term(c, P.expr_key, P.expr_op, P.expr_val_off, P.expr_vals, e0, e1, P.field_key, P.field_op,
+                      P.field_val_off, P.field_vals, f0, f1, false, term, &n))
+        continue;  // a term that fails to build matches nothing
       d->terms.push_back(n);
       d->terms.insert(d->terms.end(), term.begin(), term.end());
       ++d->n_terms;
@@ -297,17 +396,70 @@ void draft_spec(const sr_cluster* c, int32_t pod, SpecDraft* d) {
     d->tol.push_back(P.tol_val[i]);
     d->tol.push_back(P.tol_effect[i]);
   }
-  for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i) {
-    if (P.port_num[i] <= 0) continue;  // HostPortInfo ignores port <= 0
-    d->ports.push_back(P.port_proto[i]);
-    d->ports.push_back(P.port_num[i]);
-    d->ports.push_back(P.port_ip[i]);
-  }
+  // HostPortInfo ignores port <= 0; inline disks as pseudo ports (VolumeRestrictions)
+  for_each_port(c, pod, [&](int32_t proto, int32_t port, int32_t ip) {
+    d->ports.push_back(proto);
+    d->ports.push_back(port);
+    d->ports.push_back(ip);
+  });
   if (has_spread(c, pod)) spread_words(c, pod, d->spread);
-  if (has_scalars(c, pod)) {  // fitsRequest's ScalarResources loop: one (name, request) check each
-    std::vector<std::pair<int64_t, int64_t>> sc;
-    for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; ++i)
-      sc.emplace_back(c->pod_scalar_name[i], c->pod_scalar_req[i]);
+  std::vector<std::pair<int64_t, int64_t>> sc;
+  if (has_volume_spec(c, pod)) {
+    const sr_volumes* V = c->volumes;
+    // VolumeBinding PreFilter failing: the pod fits no node
+    if (V->prefilter_fail[pod]) d->flags |= CLS_IMPOSSIBLE;
+    // VolumeZone: each PV zone / region label a REQ_ZONE requirement
+    for (int32_t z = V->zone_off[pod]; z < V->zone_off[pod + 1]; ++z) {
+      std::vector<int32_t> vals(V->zone_vals + V->zone_val_off[z], V->zone_vals + V->zone_val_off[z + 1]);
+      std::sort(vals.begin(), vals.end());
+      vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+      d->vsel.push_back(static_cast<int32_t>(7 + vals.size()));
+      d->vsel.insert(d->vsel.end(), {REQ_ZONE, V->zone_key[z], SR_OP_IN, V->zone_keys[0], V->zone_keys[1],
+                                     V->zone_keys[2], V->zone_keys[3]});
+      d->vsel.insert(d->vsel.end(), vals.begin(), vals.end());
+    }
+    // VolumeBinding Filter: every bound PV's Required node affinity (terms ORed)
+    std::vector<int32_t> term, sel;
+    for (int32_t pv = V->pv_off[pod]; pv < V->pv_off[pod + 1]; ++pv) {
+      sel.assign(1, 0);
+      int32_t n_terms = 0, one = -1;
+      for (int32_t t = V->pv_term_off[pv]; t < V->pv_term_off[pv + 1]; ++t) {
+        const int32_t e0 = V->term_expr_off[t], e1 = V->term_expr_off[t + 1];
+        const int32_t f0 = V->term_field_off[t], f1 = V->term_field_off[t + 1];
+        if (e0 == e1 && f0 == f1) continue;  // an empty term selects nothing
+        int32_t n = 0;
+        if (!draft_term(c, V->expr_key, V->expr_op, V->expr_val_off, V->expr_vals, e0, e1, V->field_key,
+                        V->field_op, V->field_val_off, V->field_vals, f0, f1, true, term, &n))
+          continue;
+        if (n_terms == 0) one = static_cast<int32_t>(sel.size());
+        sel.push_back(n);
+        sel.insert(sel.end(), term.begin(), term.end());
+        ++n_terms;
+      }
+      sel[0] = n_terms;
+      if (n_terms == 0) {
+        d->flags |= CLS_IMPOSSIBLE;  // no term can match
+      } else if (n_terms == 1) {  // its requirements ANDed with the others
+        d->vsel.insert(d->vsel.end(), sel.begin() + one + 1, sel.end());
+        if (sel[one] == 0) continue;  // a term of decided fields only: every node
+      } else {
+        d->vpv.push_back(sel);
+      }
+    }
+    // volume limits: attachable volumes per limit key ride the scalar
+    // machinery (alloc = the node's limit, requested = its unique attachable
+    // volumes of the key), one (key, count) check each
+    for (int32_t a = V->att_off[pod]; a < V->att_off[pod + 1]; ++a) {
+      const int64_t name = vol_name(V->att_key[a]);
+      auto it = std::find_if(sc.begin(), sc.end(), [&](const auto& x) { return x.first == name; });
+      if (it == sc.end()) sc.emplace_back(name, 1);
+      else ++it->second;
+    }
+  }
+  if (has_scalars(c, pod) || !sc.empty()) {  // fitsRequest's ScalarResources loop: one (name, request) check each
+    if (has_scalars(c, pod))
+      for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; ++i)
+        sc.emplace_back(c->pod_scalar_name[i], c->pod_scalar_req[i]);
     std::sort(sc.begin(), sc.end());
     for (const auto& x : sc) {
       d->scalars.push_back(x.first);
@@ -486,12 +638,28 @@ const std::vector<int32_t>& label_column(EncoderCache& C, const sr_snapshot* sna
 // Node row of requirement `rw` = {type, key, op, vals...} over the static view:
 // Requirement.Matches on the node's labels, or the metadata.name field.
 void build_req_row(const EncoderCache& C, const sr_snapshot* snap, const sr_cluster* c, const int32_t* rw,
-                   size_t len, const std::vector<int32_t>* col, std::vector<uint64_t>& row) {
+                   size_t len, const std::vector<int32_t>* col, std::vector<uint64_t>& row,
+                   const std::vector<int32_t>* const* zcols = nullptr) {
   const int32_t type = rw[0], key = rw[1], op = rw[2];
   const int32_t* vals = rw + 3;
   const size_t nv = len - 3;
   row.assign(static_cast<size_t>(C.Wp), 0);
   auto set = [&](int32_t n) { row[static_cast<size_t>(n >> 6)] |= 1ull << (n & 63); };
+  if (type == REQ_ZONE) {
+    // VolumeZone.Filter [upstream k8s v1.19.2 plugins/volumezone]: a node
+    // without any of the four zone / region labels passes; otherwise its value
+    // of the PV label's key ("" when absent: never in a LabelZonesToSet set)
+    // must be one of the PV's values
+    const int32_t* zv = rw + 7;
+    const size_t nz = len - 7;
+    for (int32_t n = 0; n < C.n_spot; ++n) {
+      bool any = false;
+      for (int z = 0; z < 4; ++z) any = any || (zcols && zcols[z] && (*zcols[z])[n] != INT32_MIN);
+      const int32_t v = (*col)[n];
+      if (!any || (v != INT32_MIN && std::binary_search(zv, zv + nz, v))) set(n);
+    }
+    return;
+  }
   if (type == REQ_FIELD) {
     // fields.Set{"metadata.name": node.Name}; any other key reads as "".
     const bool is_name = key == C.id_metadata_name && C.id_metadata_name != -1;
@@ -763,6 +931,10 @@ uint64_t node_state_fp(const SpotNode& sn, const NodeState& st) {
     h = mix(mix(mix(h, 0x5CA1ull), static_cast<uint32_t>(a.first)), static_cast<uint64_t>(a.second));
   for (const auto& r : st.scalar_req)
     h = mix(mix(mix(h, 0x5CA2ull), static_cast<uint32_t>(r.first)), static_cast<uint64_t>(r.second));
+  for (const auto& l : sn.vol_limit)
+    h = mix(mix(mix(h, 0x5CA3ull), static_cast<uint32_t>(l.first)), static_cast<uint64_t>(l.second));
+  for (const auto& a : st.att)  // sorted
+    h = mix(mix(mix(h, 0x5CA4ull), static_cast<uint32_t>(a.first)), static_cast<uint32_t>(a.second));
   uint64_t ports = 0;  // order-independent
   for (const Port& u : st.ports)
     ports += mix(mix(mix(0x9E37ull, static_cast<uint32_t>(u.ip)), static_cast<uint32_t>(u.proto)),
@@ -842,7 +1014,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       if (!in_range(pod_acc(c, pod, r))) return true;
     if (has_scalars(c, pod)) {
       // a listed scalar keeps an all-zero cpu / memory / ephemeral request
-      // from skipping the resource checks: not encoded
+      // from skipping the resource checks: not encoded (the volume limit keys
+      // are other filters: they do not)
       if (rq[0] == 0 && rq[1] == 0 && rq[2] == 0) return true;
       if (snap->scalar_unknown_total > 0) return true;  // some node's scalar usage is unknown
       for (int32_t i = c->pod_scalar_off[pod]; i < c->pod_scalar_off[pod + 1]; ++i)
@@ -868,6 +1041,21 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       *err = "cand_pod_off not monotone";
       return SR_ERR_INVALID_ARG;
     }
+  // attachable volumes the spot nodes already hold (limit key, unique name),
+  // when some candidate pod has attachable volumes
+  std::unordered_set<uint64_t> vol_base_set;
+  const std::unordered_set<uint64_t>* vol_base = nullptr;
+  if (c->volumes) {
+    bool any = false;
+    for (int32_t i = 0; i < nc && !any; ++i)
+      for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1] && !any; ++j)
+        any = cands->cand_pods[j] >= 0 && cands->cand_pods[j] < P.n && att_count(c, cands->cand_pods[j]) > 0;
+    if (any) {
+      for (const NodeState& st : snap->state)
+        for (const auto& a : st.att) vol_base_set.insert(att_word(a.first, a.second));
+      vol_base = &vol_base_set;
+    }
+  }
   std::vector<uint8_t>& cand_ports = C.scratch.cand_ports;  // the candidate's pods ask for host ports
   cand_ports.assign(static_cast<size_t>(nc), 0);
   std::vector<uint8_t>& cand_ext = C.scratch.cand_ext;       // bit 0: accounting differs, bit 1: shared scalars
@@ -900,29 +1088,58 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       // ones' AddPod: a running scalar state per touched node, at most
       // kExtScalars names per candidate)
       uint8_t ext = 0;
-      cand_sname[2 * i] = cand_sname[2 * i + 1] = -1;
+      cand_sname[2 * i] = cand_sname[2 * i + 1] = kNoName;
       for (int32_t j = b; j + 1 < e && !fb && !(ext & 1); ++j) {
         const int32_t pod = cands->cand_pods[j];
         ext |= (pod_acc(c, pod, 0) != P.req_milli_cpu[pod] || pod_acc(c, pod, 1) != P.req_memory[pod] ||
                 pod_acc(c, pod, 2) != P.req_ephemeral[pod]) ? 1 : 0;
       }
-      if (!fb && c->pod_scalar_off) {
-        int32_t names[64], cnt[64], nn = 0;
+      if (!fb && c->volumes && vol_base && !vol_base->empty()) {
+        // an attachable volume some spot node already holds, or two pods of
+        // the candidate sharing one: the volume counts stop being additive
         for (int32_t j = b; j < e && !fb; ++j) {
           const int32_t pod = cands->cand_pods[j];
-          for (int32_t k = c->pod_scalar_off[pod]; k < c->pod_scalar_off[pod + 1] && !fb; ++k) {
-            const int32_t name = c->pod_scalar_name[k];
-            int32_t u = 0;
-            while (u < nn && names[u] != name) ++u;
-            if (u < nn) {
-              ++cnt[u];
-            } else if (nn == 64) {
-              fb = true;  // more scalar entries than the candidate's table holds
-            } else {
-              names[nn] = name;
-              cnt[nn++] = 1;
-            }
+          for (int32_t a = c->volumes->att_off[pod]; a < c->volumes->att_off[pod + 1] && !fb; ++a)
+            fb = vol_base->count(att_word(c->volumes->att_key[a], c->volumes->att_id[a])) != 0;
+        }
+      }
+      if (!fb && c->volumes) {
+        std::vector<uint64_t> ids;
+        for (int32_t j = b; j < e; ++j) {
+          const int32_t pod = cands->cand_pods[j];
+          for (int32_t a = c->volumes->att_off[pod]; a < c->volumes->att_off[pod + 1]; ++a)
+            ids.push_back(att_word(c->volumes->att_key[a], c->volumes->att_id[a]));
+        }
+        std::sort(ids.begin(), ids.end());
+        fb = std::adjacent_find(ids.begin(), ids.end()) != ids.end();
+      }
+      if (!fb && (c->pod_scalar_off || c->volumes)) {
+        // names listed by the candidate's pods: scalar resources, then the
+        // volume limit keys (negative names, one per pod with such volumes)
+        int32_t names[64], cnt[64], nn = 0;
+        auto count_name = [&](int32_t name) {
+          int32_t u = 0;
+          while (u < nn && names[u] != name) ++u;
+          if (u < nn) {
+            ++cnt[u];
+          } else if (nn == 64) {
+            fb = true;  // more scalar entries than the candidate's table holds
+          } else {
+            names[nn] = name;
+            cnt[nn++] = 1;
           }
+        };
+        for (int32_t j = b; j < e && !fb; ++j) {
+          const int32_t pod = cands->cand_pods[j];
+          if (c->pod_scalar_off)
+            for (int32_t k = c->pod_scalar_off[pod]; k < c->pod_scalar_off[pod + 1] && !fb; ++k)
+              count_name(c->pod_scalar_name[k]);
+          if (c->volumes)
+            for (int32_t a = c->volumes->att_off[pod]; a < c->volumes->att_off[pod + 1] && !fb; ++a) {
+              bool first = true;  // each key once per pod
+              for (int32_t a2 = c->volumes->att_off[pod]; a2 < a; ++a2) first = first && c->volumes->att_key[a2] != c->volumes->att_key[a];
+              if (first) count_name(vol_name(c->volumes->att_key[a]));
+            }
         }
         int32_t shared = 0;
         for (int32_t u = 0; u < nn && !fb; ++u)
@@ -934,8 +1151,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
       cand_ext[i] = fb ? 0 : ext;
       if (fb) w->status_host[i] = SR_CAND_FALLBACK;
-      for (int32_t j = b; j < e && !fb && !cand_ports[i]; ++j)
-        cand_ports[i] = P.port_off[cands->cand_pods[j]] != P.port_off[cands->cand_pods[j] + 1];
+      for (int32_t j = b; j < e && !fb && !cand_ports[i]; ++j) cand_ports[i] = has_ports(c, cands->cand_pods[j]);
     }
   };
   if (w->n_input_pods > serial_pods()) parallel_for(static_cast<size_t>(nc), 64, pass1);
@@ -984,11 +1200,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   std::unordered_map<int64_t, uint8_t> group_specific;  // (proto, port) -> has a specific IP
   for (int32_t i = 0; i < nc; ++i) {
     if (w->status_host[i] != STATUS_PENDING || !cand_ports[i]) continue;
-    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
-      const int32_t pod = cands->cand_pods[j];
-      for (int32_t k = P.port_off[pod]; k < P.port_off[pod + 1]; ++k)
-        if (P.port_num[k] > 0) group_specific[port_key(P.port_proto[k], P.port_num[k])] |= P.port_ip[k] != -1;
-    }
+    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j)
+      for_each_port(c, cands->cand_pods[j], [&](int32_t proto, int32_t port, int32_t ip) {
+        group_specific[port_key(proto, port)] |= ip != -1;
+      });
   }
   struct PortGroup {
     int32_t pair = -1;                            // pair index (specific IPs), else
@@ -1003,11 +1218,9 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       const int32_t pairs0 = n_port_pairs, single0 = n_port_single;
       std::vector<std::pair<int64_t, int32_t>> added_ips;  // undone if the candidate overflows
       std::vector<int64_t> added_groups;
-      for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
-        const int32_t pod = cands->cand_pods[j];
-        for (int32_t k = P.port_off[pod]; k < P.port_off[pod + 1]; ++k) {
-          if (P.port_num[k] <= 0) continue;
-          const int64_t key = port_key(P.port_proto[k], P.port_num[k]);
+      for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j)
+        for_each_port(c, cands->cand_pods[j], [&](int32_t proto, int32_t port, int32_t ip) {
+          const int64_t key = port_key(proto, port);
           auto ins = groups.emplace(key, PortGroup{});
           PortGroup& g = ins.first->second;
           if (ins.second) {
@@ -1015,12 +1228,13 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
             if (group_specific[key]) g.pair = n_port_pairs++;
             else g.single = n_port_single++;
           }
-          if (P.port_ip[k] != -1 && g.ip_bit.emplace(P.port_ip[k], n_port_single).second) {
+          // a read-only disk mount sets S only: it meets read-write mounts (W)
+          // and never another read-only one
+          if (ip != -1 && ip != kReadOnlyMount && g.ip_bit.emplace(ip, n_port_single).second) {
             ++n_port_single;
-            added_ips.emplace_back(key, P.port_ip[k]);
+            added_ips.emplace_back(key, ip);
           }
-        }
-      }
+        });
       if (bit_shift + 2 * n_port_pairs + n_port_single > 64) {  // overflow: undo, fall back
         for (const auto& ki : added_ips) groups[ki.first].ip_bit.erase(ki.second);
         for (int64_t key : added_groups) groups.erase(key);
@@ -1047,6 +1261,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     const int32_t wbit = g.pair >= 0 ? bit_shift + 2 * g.pair : single_base + g.single;
     bit_query[wbit] = static_cast<int32_t>(port_query.size());
     port_query.push_back(PortQuery{proto, port, -1});
+    if (g.pair >= 0 && proto >= kDiskProto) {  // a disk's S bit: the read-only mount's base conflicts
+      bit_query[wbit + 1] = static_cast<int32_t>(port_query.size());
+      port_query.push_back(PortQuery{proto, port, kReadOnlyMount});
+    }
     for (const auto& ib : g.ip_bit) {
       bit_query[single_base + ib.second] = static_cast<int32_t>(port_query.size());
       port_query.push_back(PortQuery{proto, port, ib.first});
@@ -1063,6 +1281,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         m |= 1ull << (single_base + g.single);
       } else if (ports[k + 2] == -1) {
         m |= 3ull << (bit_shift + 2 * g.pair);  // W and S
+      } else if (ports[k + 2] == kReadOnlyMount) {
+        m |= 2ull << (bit_shift + 2 * g.pair);  // S: a read-only disk mount
       } else {
         auto ib = g.ip_bit.find(ports[k + 2]);
         if (ib == g.ip_bit.end()) continue;
@@ -1081,7 +1301,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     int32_t need = 0;
     for (int j = 0; j < 2; ++j) {
       const int32_t nm = cand_sname[2 * i + j];
-      need += nm >= 0 && std::find(scal_names.begin(), scal_names.end(), nm) == scal_names.end();
+      need += nm != kNoName && std::find(scal_names.begin(), scal_names.end(), nm) == scal_names.end();
     }
     if (static_cast<int32_t>(scal_names.size()) + need > kExtScalarNames) {
       w->status_host[i] = SR_CAND_FALLBACK;
@@ -1089,7 +1309,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     }
     for (int j = 0; j < 2; ++j) {
       const int32_t nm = cand_sname[2 * i + j];
-      if (nm >= 0 && std::find(scal_names.begin(), scal_names.end(), nm) == scal_names.end()) scal_names.push_back(nm);
+      if (nm != kNoName && std::find(scal_names.begin(), scal_names.end(), nm) == scal_names.end())
+        scal_names.push_back(nm);
     }
   }
 
@@ -1273,6 +1494,22 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       sp.ports.swap(d.ports);
       sp.scalars.swap(d.scalars);
       sp.spread.swap(d.spread);
+      int32_t n_vsel = 0;
+      for (size_t i = 0; i < d.vsel.size(); i += 1 + static_cast<size_t>(d.vsel[i])) ++n_vsel;
+      intern_groups(C.req_dict, d.vsel.data(), n_vsel, sp.vsel, nullptr);
+      for (const std::vector<int32_t>& pv : d.vpv) {  // canonical {n terms, per term {n, requirement ids}}
+        std::vector<int32_t> words(1, pv[0]);
+        for (size_t i = 1, t = 0; t < static_cast<size_t>(pv[0]); ++t) {
+          size_t used = 0;
+          intern_groups(C.req_dict, pv.data() + i + 1, pv[i], ids, &used);
+          words.push_back(static_cast<int32_t>(ids.size()));
+          words.insert(words.end(), ids.begin(), ids.end());
+          i += 1 + used;
+        }
+        sp.vpv.push_back(C.pvsel_dict.intern(words));
+      }
+      std::sort(sp.vpv.begin(), sp.vpv.end());
+      sp.vpv.erase(std::unique(sp.vpv.begin(), sp.vpv.end()), sp.vpv.end());
     }
   }
   for (size_t id = C.spec_req_off.size() - 1; id < C.spec.size(); ++id) {
@@ -1280,6 +1517,14 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     C.spec_req.insert(C.spec_req.end(), sp.sel.begin(), sp.sel.end());
     for (size_t i = 0; i < sp.terms.size(); i += 1 + static_cast<size_t>(sp.terms[i]))
       C.spec_req.insert(C.spec_req.end(), sp.terms.begin() + i + 1, sp.terms.begin() + i + 1 + sp.terms[i]);
+    C.spec_req.insert(C.spec_req.end(), sp.vsel.begin(), sp.vsel.end());
+    for (int32_t pv : sp.vpv) {  // the PV selectors' requirements
+      const int32_t* w = C.pvsel_dict.data(pv);
+      for (size_t i = 1, t = 0; t < static_cast<size_t>(w[0]); ++t) {
+        C.spec_req.insert(C.spec_req.end(), w + i + 1, w + i + 1 + w[i]);
+        i += 1 + static_cast<size_t>(w[i]);
+      }
+    }
     C.spec_req_off.push_back(static_cast<uint32_t>(C.spec_req.size()));
   }
   phase(7);
@@ -1387,9 +1632,16 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     return ins.first->second;
   };
   auto key_dm = [&](int32_t k) { return k < n_spec_ids ? 0 : key_sdm[k - n_spec_ids]; };
+  // PV selectors with several terms (VolumeBinding): one atom each
+  std::vector<int32_t> pvsel_atom(C.pvsel_dict.size(), -1), used_pvsel;
   for (int32_t k : keys) {
     const int32_t id = k < n_spec_ids ? k : key_spec[k - n_spec_ids];
     for (uint32_t i = C.spec_req_off[id]; i < C.spec_req_off[id + 1]; ++i) use_req(C.spec_req[i]);
+    for (int32_t pv : C.spec[id].vpv)
+      if (pvsel_atom[pv] < 0) {
+        pvsel_atom[pv] = static_cast<int32_t>(used_pvsel.size());
+        used_pvsel.push_back(pv);
+      }
     const std::vector<int64_t>& sc = C.spec[id].scalars;
     for (size_t i = 0; i + 2 <= sc.size(); i += 2) scalar_atom_index(sc[i], sc[i + 1]);
     if (!C.spec[id].spread.empty()) spread_atom_index(id, key_dm(k));
@@ -1403,7 +1655,8 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   const int32_t A_SPREAD = A_SCALAR + n_scalars;  // scalar and spread atoms: the class's `sc_` list
   const int32_t A_ANTI = A_SPREAD + n_spreads;  // DA(t) at A_ANTI + 2t, DB(t) at A_ANTI + 2t + 1
   const int32_t A_AFF = A_ANTI + 2 * anti.n_terms;  // SAT(S) at A_AFF + 2s, KEYS(S) at A_AFF + 2s + 1
-  const int32_t A_COMP = A_AFF + 2 * aff.n_sets;
+  const int32_t A_VOL = A_AFF + 2 * aff.n_sets;  // PV selector atoms
+  const int32_t A_COMP = A_VOL + static_cast<int32_t>(used_pvsel.size());
   // Composite atoms, one per distinct untolerated-taint set U of the pods:
   // atom 0 AND NOT (OR of U's taint atoms) -- the pod-count check and
   // TaintToleration / NodeUnschedulable in one row, so a class program opens
@@ -1438,6 +1691,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     out.insert(out.end(), sp.sel.begin(), sp.sel.end());
     out.push_back(sp.n_terms);
     out.insert(out.end(), sp.terms.begin(), sp.terms.end());
+    out.push_back(static_cast<int32_t>(sp.vsel.size()));
+    out.insert(out.end(), sp.vsel.begin(), sp.vsel.end());
+    out.push_back(static_cast<int32_t>(sp.vpv.size()));
+    out.insert(out.end(), sp.vpv.begin(), sp.vpv.end());
     out.push_back(untol);
   };
   w->cls_prog_off.push_back(0);
@@ -1453,9 +1710,17 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     const int32_t n_terms = *tp++;
     const int32_t* term_words = tp;
     for (int32_t k = 0; k < n_terms; ++k) tp += 1 + *tp;
+    const int32_t n_vsel = *tp++;
+    const int32_t* vsel = tp;
+    tp += n_vsel;
+    const int32_t n_vpv = *tp++;
+    const int32_t* vpv = tp;
+    tp += n_vpv;
     const int32_t untol = *tp;
     emit(comp_atom(untol), PROG_AND);  // len(pods)+1 <= allowed pods, untolerated taints
     for (int32_t k = 0; k < n_sel; ++k) emit(A_REQ + req_atom[sel[k]], PROG_AND);
+    for (int32_t k = 0; k < n_vsel; ++k) emit(A_REQ + req_atom[vsel[k]], PROG_AND);  // VolumeZone, PV affinity
+    for (int32_t k = 0; k < n_vpv; ++k) emit(A_VOL + pvsel_atom[vpv[k]], PROG_AND);
     for (uint64_t m = ports; m; m &= m - 1) {  // the base UsedPorts conflicting with each host port it asks for
       const int32_t b = __builtin_ctzll(m);
       if (bit_query[b] >= 0) emit(A_PORT + bit_query[b], PROG_ANDNOT);
@@ -1579,14 +1844,17 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     for (int32_t r : used_reqs)
       if (C.req_row_gen[r] != C.static_gen) stale.push_back(r);
     std::vector<const std::vector<int32_t>*> cols(stale.size(), nullptr);
+    std::vector<std::array<const std::vector<int32_t>*, 4>> zcols(stale.size());
     for (size_t i = 0; i < stale.size(); ++i) {  // label columns: serial (the cache is not thread-safe)
       const int32_t* rw = C.req_dict.data(stale[i]);
       if (rw[0] != REQ_FIELD) cols[i] = &label_column(C, snap, rw[1]);
+      for (int z = 0; z < 4; ++z)
+        zcols[i][z] = rw[0] == REQ_ZONE && rw[3 + z] >= 0 ? &label_column(C, snap, rw[3 + z]) : nullptr;
     }
     auto build = [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         const int32_t r = stale[i];
-        build_req_row(C, snap, c, C.req_dict.data(r), C.req_dict.len(r), cols[i], C.req_rows[r]);
+        build_req_row(C, snap, c, C.req_dict.data(r), C.req_dict.len(r), cols[i], C.req_rows[r], zcols[i].data());
         C.req_row_gen[r] = C.static_gen;
       }
     };
@@ -1595,6 +1863,22 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     for (int32_t i = 0; i < n_reqs; ++i)
       std::copy(C.req_rows[used_reqs[i]].begin(), C.req_rows[used_reqs[i]].end(),
                 A + static_cast<size_t>(A_REQ + i) * Wp);
+    // PV selectors: OR over the terms of the AND of their requirement rows
+    for (size_t i = 0; i < used_pvsel.size(); ++i) {
+      const int32_t* pw = C.pvsel_dict.data(used_pvsel[i]);
+      uint64_t* row = A + static_cast<size_t>(A_VOL + static_cast<int32_t>(i)) * Wp;
+      std::vector<uint64_t> t(static_cast<size_t>(Wp));
+      for (size_t j = 1, term = 0; term < static_cast<size_t>(pw[0]); ++term) {
+        for (int32_t n = 0; n < n_spot; ++n) t[n >> 6] |= 1ull << (n & 63);
+        for (int32_t g = 0; g < pw[j]; ++g) {
+          const std::vector<uint64_t>& rr = C.req_rows[pw[j + 1 + g]];
+          for (int32_t x = 0; x < Wp; ++x) t[x] &= rr[x];
+        }
+        for (int32_t x = 0; x < Wp; ++x) row[x] |= t[x];
+        std::fill(t.begin(), t.end(), 0);
+        j += 1 + static_cast<size_t>(pw[j]);
+      }
+    }
   }
   std::copy(C.taint_rows.begin(), C.taint_rows.end(), A + static_cast<size_t>(A_TAINT) * Wp);
   if (n_ports > 0) {
@@ -1603,7 +1887,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     // patched a few nodes patches their bits, any other refresh drops them.
     auto conflicts = [&](int32_t n, const PortQuery& pq) {
       for (const Port& u : snap->state[n].ports)
-        if (pq.proto == u.proto && pq.port == u.port && (pq.ip == -1 || u.ip == -1 || u.ip == pq.ip)) return true;
+        if (pq.proto == u.proto && pq.port == u.port && port_conflict(pq.ip, u.ip)) return true;
       return false;
     };
     auto qkey = [](const PortQuery& pq) {
@@ -1648,7 +1932,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         for (const Port& u : snap->state[n].ports)
           for (size_t m = 0; m < missing.size(); ++m) {
             const PortQuery& pq = port_query[missing[m]];
-            if (pq.proto == u.proto && pq.port == u.port && (pq.ip == -1 || u.ip == -1 || u.ip == pq.ip))
+            if (pq.proto == u.proto && pq.port == u.port && port_conflict(pq.ip, u.ip))
               fresh[m][static_cast<size_t>(n >> 6)] |= 1ull << (n & 63);
           }
       for (size_t m = 0; m < missing.size(); ++m) {
@@ -1670,17 +1954,16 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   }
   // NodeResourcesFit's ScalarResources loop against the base snapshot:
   // alloc[s] < request + requested[s] fails (a node without s allocates 0)
+  // (volume limit keys under negative names: the node's limit, or unlimited,
+  // against its unique attachable volumes of the key plus the pod's count)
   if (n_scalars > 0) {
-    auto value_of = [](const std::vector<std::pair<int32_t, int64_t>>& v, int64_t name) -> int64_t {
-      auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(static_cast<int32_t>(name), INT64_MIN));
-      return it != v.end() && it->first == name ? it->second : 0;
-    };
     for (int32_t q = 0; q < n_scalars; ++q) {
       uint64_t* row = A + static_cast<size_t>(A_SCALAR + q) * Wp;
-      const int64_t name = scalar_query[q].first, req = scalar_query[q].second;
+      const int32_t name = static_cast<int32_t>(scalar_query[q].first);
+      const int64_t req = scalar_query[q].second;
       for (int32_t n = 0; n < n_spot; ++n) {
-        const int64_t alloc = value_of(snap->nodes[n].scalar_alloc, name);
-        const int64_t used = value_of(snap->state[n].scalar_req, name);
+        const int64_t alloc = scalar_alloc_of(snap->nodes[n], name);
+        const int64_t used = scalar_used_of(snap->state[n], name);
         // Go int64 arithmetic: request + requested wraps like the reference's
         const int64_t need = static_cast<int64_t>(static_cast<uint64_t>(req) + static_cast<uint64_t>(used));
         if (!(alloc < need)) row[n >> 6] |= 1ull << (n & 63);
@@ -1803,7 +2086,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         w->ext_cand[k] = static_cast<int32_t>(w->pod_ext.size() / kExtU64);
         int32_t row[2] = {-1, -1};
         for (int j = 0; j < 2; ++j)
-          if (cand_sname[2 * i + j] >= 0)
+          if (cand_sname[2 * i + j] != kNoName)
             row[j] = static_cast<int32_t>(std::find(scal_names.begin(), scal_names.end(), cand_sname[2 * i + j]) -
                                           scal_names.begin());
         for (int32_t q = w->cand_off[k]; q < w->cand_off[k + 1]; ++q) {
@@ -1812,12 +2095,17 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
           for (int r = 0; r < 3; ++r) x[r] = static_cast<uint64_t>(pod_acc(c, pod, r));
           for (int j = 0; j < 2; ++j) {
             int64_t rq = INT64_MIN, ac = 0;
-            if (row[j] >= 0)
+            const int32_t nm = cand_sname[2 * i + j];
+            if (row[j] >= 0 && nm >= 0) {
               for (int32_t a = c->pod_scalar_off[pod]; a < c->pod_scalar_off[pod + 1]; ++a)
-                if (c->pod_scalar_name[a] == cand_sname[2 * i + j]) {
+                if (c->pod_scalar_name[a] == nm) {
                   rq = c->pod_scalar_req[a];
                   ac = c->pod_scalar_acc[a];
                 }
+            } else if (row[j] >= 0) {  // a volume limit key: the pod's attachable volumes of it (distinct)
+              const int32_t n_att = pod_att_of(c, pod, vol_key_of(nm));
+              if (n_att > 0) rq = ac = n_att;
+            }
             x[3 + j] = static_cast<uint64_t>(rq);
             x[5 + j] = static_cast<uint64_t>(ac);
           }
@@ -1828,15 +2116,11 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
       w->n_scal_names = static_cast<int32_t>(scal_names.size());
       w->node_scal.assign(std::max<size_t>(1, scal_names.size()) * static_cast<size_t>(w->n_pad), 0);
-      auto value_of = [](const std::vector<std::pair<int32_t, int64_t>>& v, int32_t name) -> int64_t {
-        auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(name, INT64_MIN));
-        return it != v.end() && it->first == name ? it->second : 0;
-      };
       for (size_t u = 0; u < scal_names.size(); ++u)
         for (int32_t n = 0; n < n_spot; ++n)  // Go int64 arithmetic: alloc - requested wraps like the reference's
           w->node_scal[u * static_cast<size_t>(w->n_pad) + static_cast<size_t>(n)] = static_cast<int64_t>(
-              static_cast<uint64_t>(value_of(snap->nodes[n].scalar_alloc, scal_names[u])) -
-              static_cast<uint64_t>(value_of(snap->state[n].scalar_req, scal_names[u])));
+              static_cast<uint64_t>(scalar_alloc_of(snap->nodes[n], scal_names[u])) -
+              static_cast<uint64_t>(scalar_used_of(snap->state[n], scal_names[u])));
     }
   }
   phase(4);

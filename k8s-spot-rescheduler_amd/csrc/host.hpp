@@ -7,6 +7,7 @@
 // the gfx950 kernels consume (layout: DESIGN.md §HBM layout).
 #pragma once
 
+#include <algorithm>
 #include <climits>
 #include <deque>
 #include <memory>
@@ -43,6 +44,7 @@ struct SpotNode {
   std::vector<std::pair<int32_t, int32_t>> labels;  // (key, value)
   std::vector<TaintRec> taints;
   std::vector<std::pair<int32_t, int64_t>> scalar_alloc;  // Allocatable scalar resources (name, value), by name
+  std::vector<std::pair<int32_t, int64_t>> vol_limit;     // volume limits (limit key, count), by key
 };
 
 // The snapshot's own copy of what InterPodAffinity reads from a pod it holds
@@ -100,7 +102,72 @@ struct NodeState {
   std::vector<std::pair<int32_t, int64_t>> scalar_req;  // Requested scalar resources (name, value), by name
   int32_t scalar_unknown = 0;  // pods added without scalar tables that carry scalar requests
   int32_t term_unknown = 0;    // pods added without sr_spread (deletion state unknown)
+  std::vector<std::pair<int32_t, int32_t>> att;  // attachable volumes (limit key, unique name) of its pods, sorted
 };
+
+// ---- volume filters (sr_volumes)
+// VolumeRestrictions' inline disks ride the host-port machinery as pseudo
+// ports: protocol kDiskProto + SR_DISK_*, port = disk id + 1, ip = -1 for a
+// read-write mount (it conflicts with every mount of the disk) or
+// kReadOnlyMount (it conflicts with read-write mounts only; an EBS mount is
+// always read-write: any two conflict).
+constexpr int32_t kDiskProto = 16;
+constexpr int32_t kReadOnlyMount = -2;
+// A limit key without an entry on a node never refuses there.
+constexpr int64_t kVolUnlimited = int64_t(1) << 61;
+// The volume limit keys ride the scalar-resource machinery under negative
+// names: key k -> -(k + 1) (real scalar names are interned ids >= 0).
+inline int32_t vol_name(int32_t key) { return -(key + 1); }
+inline int32_t vol_key_of(int32_t name) { return -name - 1; }
+// Host ports (port > 0) then inline disks of a pod as (protocol, port, ip).
+template <class F>
+inline void for_each_port(const sr_cluster* c, int32_t pod, F&& f) {
+  const sr_pods& P = c->pods;
+  for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i)
+    if (P.port_num[i] > 0) f(P.port_proto[i], P.port_num[i], P.port_ip[i]);
+  if (const sr_volumes* V = c->volumes)
+    for (int32_t i = V->disk_off[pod]; i < V->disk_off[pod + 1]; ++i)
+      f(kDiskProto + V->disk_kind[i], V->disk_id[i] + 1,
+        V->disk_ro[i] && V->disk_kind[i] != SR_DISK_AWS_EBS ? kReadOnlyMount : -1);
+}
+inline bool has_ports(const sr_cluster* c, int32_t pod) {
+  bool any = false;
+  for_each_port(c, pod, [&](int32_t, int32_t, int32_t) { any = true; });
+  return any;
+}
+// The pod's attachable volumes (sr_volumes.att_*), count of entries.
+inline int32_t att_count(const sr_cluster* c, int32_t pod) {
+  return c->volumes ? c->volumes->att_off[pod + 1] - c->volumes->att_off[pod] : 0;
+}
+// The pod carries anything the volume filters read beyond its inline disks.
+inline bool has_volume_spec(const sr_cluster* c, int32_t pod) {
+  const sr_volumes* V = c->volumes;
+  return V && (V->prefilter_fail[pod] || V->att_off[pod + 1] > V->att_off[pod] ||
+               V->zone_off[pod + 1] > V->zone_off[pod] || V->pv_off[pod + 1] > V->pv_off[pod]);
+}
+// Unique attachable volumes of limit key `key` on a node.
+inline int64_t vol_used(const NodeState& st, int32_t key) {
+  auto lo = std::lower_bound(st.att.begin(), st.att.end(), std::make_pair(key, INT32_MIN));
+  auto hi = std::lower_bound(lo, st.att.end(), std::make_pair(key + 1, INT32_MIN));
+  return hi - lo;
+}
+inline int64_t vol_limit_of(const SpotNode& sn, int32_t key) {
+  auto it = std::lower_bound(sn.vol_limit.begin(), sn.vol_limit.end(), std::make_pair(key, INT64_MIN));
+  return it != sn.vol_limit.end() && it->first == key ? it->second : kVolUnlimited;
+}
+// Allocatable and Requested of a scalar-machinery name on a node: a scalar
+// resource (0 when absent), or a volume limit key (limit or kVolUnlimited, and
+// the node's unique attachable volumes of the key).
+inline int64_t scalar_alloc_of(const SpotNode& sn, int32_t name) {
+  if (name < 0) return vol_limit_of(sn, vol_key_of(name));
+  auto it = std::lower_bound(sn.scalar_alloc.begin(), sn.scalar_alloc.end(), std::make_pair(name, INT64_MIN));
+  return it != sn.scalar_alloc.end() && it->first == name ? it->second : 0;
+}
+inline int64_t scalar_used_of(const NodeState& st, int32_t name) {
+  if (name < 0) return vol_used(st, vol_key_of(name));
+  auto it = std::lower_bound(st.scalar_req.begin(), st.scalar_req.end(), std::make_pair(name, INT64_MIN));
+  return it != st.scalar_req.end() && it->first == name ? it->second : 0;
+}
 
 }  // namespace sr
 
@@ -338,6 +405,8 @@ struct SpecInfo {
   std::vector<int32_t> ports;  // host ports {protocol, port, ip}* with port > 0
   std::vector<int64_t> scalars;  // scalar resources {name, fit request}*, sorted by name
   std::vector<int32_t> spread;   // DoNotSchedule topology spread constraints (spread_words), empty: none
+  std::vector<int32_t> vsel;     // volume filters: requirement ids ANDed (VolumeZone REQ_ZONE, one-term PV affinity)
+  std::vector<int32_t> vpv;      // PV selectors with several terms (EncoderCache::pvsel_dict ids), sorted
   uint64_t untol_gen = ~0ull;  // static generation `untol` was computed for
   int32_t untol = -1;          // set of spot-pool taints it does not tolerate (EncoderCache::untol_dict)
   uint64_t psig_gen = ~0ull;   // static generation `psig` was interned for
@@ -390,6 +459,7 @@ struct EncoderCache {
   std::vector<uint32_t> spec_req_off{0};  // [spec id + 1] the specs' requirement ids (selector, then
   std::vector<int32_t> spec_req;          //   terms), flat: the per-call key pass reads them in key order
   WordDict req_dict;                   // requirement words {type, key, op, vals...} -> requirement id
+  WordDict pvsel_dict;                 // PV selectors {n terms, per term {n, requirement ids}} -> id
   WordDict untol_dict;                 // untolerated-taint sets (valid for untol_gen)
   uint64_t untol_gen = ~0ull;
   WordDict psig_dict;                  // class signatures of port-free specs (valid for psig_gen)
@@ -417,6 +487,7 @@ struct EncoderCache {
     spec_req_off.assign(1, 0);
     spec_req.clear();
     req_dict.clear();
+    pvsel_dict.clear();
     req_rows.clear();
     req_row_gen.clear();
     untol_dict.clear();

@@ -207,8 +207,15 @@ static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod, const
   st.unknown += sp.meta ? 0 : 1;
   st.term_unknown += sp.term == 2 ? 1 : 0;
   st.pods.push_back(store);
-  for (int32_t i = P.port_off[pod]; i < P.port_off[pod + 1]; ++i)
-    if (P.port_num[i] > 0) st.ports.push_back(Port{P.port_ip[i], P.port_proto[i], P.port_num[i]});
+  // UsedPorts += container host ports; the inline disks VolumeRestrictions
+  // compares as pseudo ports (host.hpp for_each_port)
+  for_each_port(c, pod, [&](int32_t proto, int32_t port, int32_t ip) { st.ports.push_back(Port{ip, proto, port}); });
+  if (const sr_volumes* V = c->volumes)  // the node's unique attachable volumes per limit key
+    for (int32_t i = V->att_off[pod]; i < V->att_off[pod + 1]; ++i) {
+      const std::pair<int32_t, int32_t> a(V->att_key[i], V->att_id[i]);
+      auto it = std::lower_bound(st.att.begin(), st.att.end(), a);
+      if (it == st.att.end() || *it != a) st.att.insert(it, a);
+    }
 }
 
 // A term whose label selector metav1.LabelSelectorAsSelector rejects: a key
@@ -343,6 +350,11 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
         for (int32_t j = c->node_scalar_off[node]; j < c->node_scalar_off[node + 1]; ++j)
           sn.scalar_alloc.emplace_back(c->node_scalar_name[j], c->node_scalar_alloc[j]);
         std::sort(sn.scalar_alloc.begin(), sn.scalar_alloc.end());
+      }
+      if (const sr_volumes* V = c->volumes) {
+        for (int32_t j = V->limit_off[node]; j < V->limit_off[node + 1]; ++j)
+          sn.vol_limit.emplace_back(V->limit_key[j], V->limit[j]);
+        std::sort(sn.vol_limit.begin(), sn.vol_limit.end());
       }
       sn.static_fp = node_static_fp(sn, c);
       s->state[i].pods.reserve(static_cast<size_t>(off[node + 1] - off[node]));

@@ -21,6 +21,11 @@ typedef struct {
   int32_t n_on_demand;     /* 0 = config default */
   int32_t n_spot;          /* 0 = config default */
   double pinned_fraction;  /* < 0 = default; share of on-demand pods pinned to on-demand nodes */
+  /* "realistic" variant (all 0 = the BASELINE config as specified): */
+  double stateful_fraction; /* share of ReplicaSet-slot pods that are StatefulSet pods with one EBS CSI claim,
+                               its PV in the pod's zone (zone label + node affinity), CSINode count 25 per node */
+  double init_fraction;     /* share of pods with an init container (fit request != AddPod accounting) */
+  double gpu_fraction;      /* share of pods on GPU nodes (1 in 8 nodes, 4 nvidia.com/gpu) asking for one GPU */
 } sr_synth_params;
 
 typedef struct sr_synth sr_synth;

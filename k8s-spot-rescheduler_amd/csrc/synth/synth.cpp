@@ -11,6 +11,7 @@
 // (C3/C4), host ports + specific host IPs (C5).
 #include "sr_synth.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <string>
@@ -45,6 +46,24 @@ struct sr_synth {
   std::vector<int64_t> deletion_age, grace;
   sr_node_label od{}, spot{};
   std::vector<uint8_t> str_label;  // sr_cluster.str_label over `strings`
+  // realistic variant (sr_synth_params.*_fraction)
+  bool has_volumes = false, has_scalars = false, has_acc = false;
+  std::vector<int64_t> acc_cpu, acc_mem, acc_eph;  // NodeInfo.AddPod accounting (containers only)
+  std::vector<int32_t> pod_sc_off{0}, pod_sc_name;
+  std::vector<int64_t> pod_sc_req, pod_sc_acc;
+  std::vector<int32_t> node_sc_off{0}, node_sc_name;
+  std::vector<int64_t> node_sc_alloc;
+  std::vector<uint8_t> v_prefilter, v_disk_ro, v_att_noncsi;
+  std::vector<int32_t> v_disk_off{0}, v_disk_kind, v_disk_id;
+  std::vector<int32_t> v_att_off{0}, v_att_key, v_att_id;
+  std::vector<int32_t> v_limit_off{0}, v_limit_key;
+  std::vector<int64_t> v_limit;
+  std::vector<int32_t> v_zone_off{0}, v_zone_key, v_zone_val_off{0}, v_zone_vals;
+  std::vector<int32_t> v_pv_off{0}, v_pv_term_off{0}, v_term_expr_off{0}, v_term_field_off{0};
+  std::vector<int32_t> v_expr_key, v_expr_op, v_expr_val_off{0}, v_expr_vals;
+  std::vector<int32_t> v_field_key, v_field_op, v_field_val_off{0}, v_field_vals;
+  int32_t zone_keys[4] = {-1, -1, -1, -1};
+  mutable sr_volumes vview{};  // the sr_volumes of sr_synth_view
 
   int32_t id(const std::string& s) {
     auto it = ids.find(s);
@@ -131,6 +150,10 @@ Cfg config_defaults(int c) {
 
 struct PodSpec {
   int64_t cpu = 0, mem = 0, eph = 0;
+  int64_t init_cpu = 0, init_mem = 0;  // an init container (realistic variant)
+  int32_t gpu = 0;                     // nvidia.com/gpu request
+  int32_t volume = -1;                 // a bound EBS CSI claim: its volume id string
+  int32_t zone = -1;                   // ... its PV's zone value
   int32_t prio = 0;
   uint32_t flags = 0;
   std::vector<std::pair<int32_t, int32_t>> sel;
@@ -153,9 +176,38 @@ struct PodSpec {
 void push_pod(sr_synth* s, int32_t node, const PodSpec& p) {
   s->pod_node.push_back(node);
   s->cpu_sort.push_back(p.cpu);
-  s->req_cpu.push_back(p.cpu);
-  s->req_mem.push_back(p.mem);
+  s->req_cpu.push_back(std::max(p.cpu, p.init_cpu));  // computePodResourceRequest: max with the init container
+  s->req_mem.push_back(std::max(p.mem, p.init_mem));
   s->req_eph.push_back(p.eph);
+  s->acc_cpu.push_back(p.cpu);  // calculateResource: the containers only
+  s->acc_mem.push_back(p.mem);
+  s->acc_eph.push_back(p.eph);
+  if (p.gpu > 0) {
+    s->pod_sc_name.push_back(s->id("nvidia.com/gpu"));
+    s->pod_sc_req.push_back(p.gpu);
+    s->pod_sc_acc.push_back(p.gpu);
+  }
+  s->pod_sc_off.push_back(static_cast<int32_t>(s->pod_sc_name.size()));
+  s->v_prefilter.push_back(0);
+  s->v_disk_off.push_back(0);
+  if (p.volume >= 0) {  // one bound EBS CSI claim: attachable, zone label, node affinity
+    s->v_att_key.push_back(s->id("attachable-volumes-csi-ebs.csi.aws.com"));
+    s->v_att_id.push_back(p.volume);
+    s->v_att_noncsi.push_back(0);
+    s->v_zone_key.push_back(s->id("topology.kubernetes.io/zone"));
+    s->v_zone_vals.push_back(p.zone);
+    s->v_zone_val_off.push_back(static_cast<int32_t>(s->v_zone_vals.size()));
+    s->v_expr_key.push_back(s->id("topology.kubernetes.io/zone"));
+    s->v_expr_op.push_back(SR_OP_IN);
+    s->v_expr_vals.push_back(p.zone);
+    s->v_expr_val_off.push_back(static_cast<int32_t>(s->v_expr_vals.size()));
+    s->v_term_expr_off.push_back(static_cast<int32_t>(s->v_expr_key.size()));
+    s->v_term_field_off.push_back(static_cast<int32_t>(s->v_field_key.size()));
+    s->v_pv_term_off.push_back(static_cast<int32_t>(s->v_term_expr_off.size() - 1));
+  }
+  s->v_att_off.push_back(static_cast<int32_t>(s->v_att_key.size()));
+  s->v_zone_off.push_back(static_cast<int32_t>(s->v_zone_key.size()));
+  s->v_pv_off.push_back(static_cast<int32_t>(s->v_pv_term_off.size() - 1));
   s->priority.push_back(p.prio);
   s->has_priority.push_back(1);
   s->flags.push_back(p.flags);
@@ -206,6 +258,8 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
   if (prm && prm->n_on_demand > 0) cfg.n_od = prm->n_on_demand;
   if (prm && prm->n_spot > 0) cfg.n_spot = prm->n_spot;
   if (prm && prm->pinned_fraction >= 0) cfg.pinned = prm->pinned_fraction;
+  const double f_stateful = prm ? prm->stateful_fraction : 0, f_init = prm ? prm->init_fraction : 0,
+               f_gpu = prm ? prm->gpu_fraction : 0;
   Rng rng{prm && prm->seed ? prm->seed : 0x5EED0000ull + static_cast<uint64_t>(config)};
   auto* s = new sr_synth();
   // fixed ids first
@@ -228,6 +282,16 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
   const int n_types = cfg.topology && cfg.constraints ? 8 : 5;
   s->od = sr_node_label{ROLE, WORKER, 1};
   s->spot = sr_node_label{ROLE, SPOTW, 1};
+  s->has_volumes = f_stateful > 0;
+  s->has_scalars = f_gpu > 0;
+  s->has_acc = f_init > 0;
+  if (s->has_volumes) {
+    s->zone_keys[0] = s->id("failure-domain.beta.kubernetes.io/zone");
+    s->zone_keys[1] = s->id("failure-domain.beta.kubernetes.io/region");
+    s->zone_keys[2] = ZONE;
+    s->zone_keys[3] = s->id("topology.kubernetes.io/region");
+  }
+  int32_t n_volumes = 0;
 
   const int n_nodes = cfg.n_od + cfg.n_spot;
   std::vector<uint8_t> is_spot(n_nodes, 0);
@@ -253,10 +317,11 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
     s->label_val.push_back(spot ? SPOTW : WORKER);
     s->label_key.push_back(HOST);
     s->label_val.push_back(nm);
-    int32_t team = -1;
+    int32_t team = -1, node_zone = -1;
     if (cfg.topology) {
+      node_zone = zones[rng.below(3)];
       s->label_key.push_back(ZONE);
-      s->label_val.push_back(zones[rng.below(3)]);
+      s->label_val.push_back(node_zone);
       s->label_key.push_back(ITYPE);
       s->label_val.push_back(types[t]);
     }
@@ -283,6 +348,18 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
       s->taint_eff.push_back(SR_EFFECT_NO_SCHEDULE);
     }
     s->taint_off.push_back(static_cast<int32_t>(s->taint_key.size()));
+    // realistic variant: GPUs on 1 in 8 nodes, the EBS CSI driver's attach limit on every node
+    const bool gpu_node = f_gpu > 0 && rng.chance(0.125);
+    if (gpu_node) {
+      s->node_sc_name.push_back(s->id("nvidia.com/gpu"));
+      s->node_sc_alloc.push_back(4);
+    }
+    s->node_sc_off.push_back(static_cast<int32_t>(s->node_sc_name.size()));
+    if (f_stateful > 0) {
+      s->v_limit_key.push_back(s->id("attachable-volumes-csi-ebs.csi.aws.com"));
+      s->v_limit.push_back(25);
+    }
+    s->v_limit_off.push_back(static_cast<int32_t>(s->v_limit_key.size()));
 
     // DaemonSet pod first in the node's list
     PodSpec ds;
@@ -346,6 +423,16 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
           else
             p.tols.push_back({DEDICATED, SR_TOL_EXISTS, E, SR_EFFECT_EMPTY});
         }
+      }
+      if (f_init > 0 && rng.chance(f_init)) {  // e.g. a migration / warm-up step heavier than the app
+        p.init_cpu = 2 * p.cpu;
+        p.init_mem = p.mem + 256 * kMi;
+      }
+      if (gpu_node && rng.chance(f_gpu)) p.gpu = 1;
+      if (f_stateful > 0 && node_zone >= 0 && p.prio >= 0 && rng.chance(f_stateful)) {
+        std::snprintf(buf, sizeof(buf), "vol-%08d", n_volumes++);
+        p.volume = s->id(buf);
+        p.zone = node_zone;
       }
       if (cfg.ports && rng.chance(0.30)) {
         static const int32_t kPorts[3] = {80, 443, 8080};
@@ -429,6 +516,55 @@ void sr_synth_view(const sr_synth* s, sr_cluster* c) {
   c->pod_scalar_req = c->pod_scalar_acc = c->node_scalar_alloc = nullptr;
   c->acc_milli_cpu = c->acc_memory = c->acc_ephemeral = nullptr;  // AddPod adds the fit request
   c->spread = nullptr;  // no topology spread constraints in the BASELINE configs
+  c->volumes = nullptr;  // realistic variant only (sr_synth_params.stateful_fraction)
+  if (s->has_acc) {
+    c->acc_milli_cpu = s->acc_cpu.data();
+    c->acc_memory = s->acc_mem.data();
+    c->acc_ephemeral = s->acc_eph.data();
+  }
+  if (s->has_scalars) {
+    c->pod_scalar_off = s->pod_sc_off.data();
+    c->pod_scalar_name = s->pod_sc_name.data();
+    c->pod_scalar_req = s->pod_sc_req.data();
+    c->pod_scalar_acc = s->pod_sc_acc.data();
+    c->node_scalar_off = s->node_sc_off.data();
+    c->node_scalar_name = s->node_sc_name.data();
+    c->node_scalar_alloc = s->node_sc_alloc.data();
+  }
+  if (s->has_volumes) {
+    sr_volumes& v = s->vview;
+    v = sr_volumes{};
+    v.prefilter_fail = s->v_prefilter.data();
+    v.disk_off = s->v_disk_off.data();
+    v.disk_kind = s->v_disk_kind.data();
+    v.disk_id = s->v_disk_id.data();
+    v.disk_ro = s->v_disk_ro.data();
+    v.att_off = s->v_att_off.data();
+    v.att_key = s->v_att_key.data();
+    v.att_id = s->v_att_id.data();
+    v.att_noncsi = s->v_att_noncsi.data();
+    v.limit_off = s->v_limit_off.data();
+    v.limit_key = s->v_limit_key.data();
+    v.limit = s->v_limit.data();
+    v.zone_off = s->v_zone_off.data();
+    v.zone_key = s->v_zone_key.data();
+    v.zone_val_off = s->v_zone_val_off.data();
+    v.zone_vals = s->v_zone_vals.data();
+    for (int i = 0; i < 4; ++i) v.zone_keys[i] = s->zone_keys[i];
+    v.pv_off = s->v_pv_off.data();
+    v.pv_term_off = s->v_pv_term_off.data();
+    v.term_expr_off = s->v_term_expr_off.data();
+    v.term_field_off = s->v_term_field_off.data();
+    v.expr_key = s->v_expr_key.data();
+    v.expr_op = s->v_expr_op.data();
+    v.expr_val_off = s->v_expr_val_off.data();
+    v.expr_vals = s->v_expr_vals.data();
+    v.field_key = s->v_field_key.data();
+    v.field_op = s->v_field_op.data();
+    v.field_val_off = s->v_field_val_off.data();
+    v.field_vals = s->v_field_vals.data();
+    c->volumes = &v;
+  }
 }
 
 void sr_synth_drain(const sr_synth* s, sr_pod_drain* d) {

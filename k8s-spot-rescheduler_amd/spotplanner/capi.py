@@ -74,6 +74,17 @@ class sr_spread(ctypes.Structure):
                 ("me_op", P32), ("me_val_off", P32), ("me_vals", P32), ("terminating", PU8)]
 
 
+class sr_volumes(ctypes.Structure):
+    _fields_ = [("prefilter_fail", PU8), ("disk_off", P32), ("disk_kind", P32), ("disk_id", P32), ("disk_ro", PU8),
+                ("att_off", P32), ("att_key", P32), ("att_id", P32), ("att_noncsi", PU8),
+                ("limit_off", P32), ("limit_key", P32), ("limit", P64),
+                ("zone_off", P32), ("zone_key", P32), ("zone_val_off", P32), ("zone_vals", P32),
+                ("zone_keys", ctypes.c_int32 * 4),
+                ("pv_off", P32), ("pv_term_off", P32), ("term_expr_off", P32), ("term_field_off", P32),
+                ("expr_key", P32), ("expr_op", P32), ("expr_val_off", P32), ("expr_vals", P32),
+                ("field_key", P32), ("field_op", P32), ("field_val_off", P32), ("field_vals", P32)]
+
+
 class sr_cluster(ctypes.Structure):
     _fields_ = [("nodes", sr_nodes), ("pods", sr_pods), ("id_empty", ctypes.c_int32),
                 ("id_metadata_name", ctypes.c_int32), ("id_unschedulable_key", ctypes.c_int32),
@@ -83,7 +94,7 @@ class sr_cluster(ctypes.Structure):
                 ("pod_scalar_off", P32), ("pod_scalar_name", P32), ("pod_scalar_req", P64), ("pod_scalar_acc", P64),
                 ("node_scalar_off", P32), ("node_scalar_name", P32), ("node_scalar_alloc", P64),
                 ("acc_milli_cpu", P64), ("acc_memory", P64), ("acc_ephemeral", P64),
-                ("spread", ctypes.POINTER(sr_spread))]
+                ("spread", ctypes.POINTER(sr_spread)), ("volumes", ctypes.POINTER(sr_volumes))]
 
 
 class sr_node_label(ctypes.Structure):
@@ -206,6 +217,21 @@ def make_cluster_struct(A) -> sr_cluster:
         ts.terminating = ptr(A["ts_terminating"], PU8)
         c._spread = ts  # keeps the struct alive as long as the cluster struct
         c.spread = ctypes.pointer(ts)
+    if A.get("vol_prefilter_fail") is not None:
+        v = sr_volumes()
+        v.prefilter_fail = ptr(A["vol_prefilter_fail"], PU8)
+        for f in ("disk_off", "disk_kind", "disk_id", "att_off", "att_key", "att_id", "limit_off", "limit_key",
+                  "zone_off", "zone_key", "zone_val_off", "zone_vals", "pv_off", "pv_term_off", "term_expr_off",
+                  "term_field_off", "expr_key", "expr_op", "expr_val_off", "expr_vals", "field_key", "field_op",
+                  "field_val_off", "field_vals"):
+            setattr(v, f, ptr(A["vol_" + f], P32))
+        v.disk_ro = ptr(A["vol_disk_ro"], PU8)
+        v.att_noncsi = ptr(A["vol_att_noncsi"], PU8)
+        v.limit = ptr(A["vol_limit"], P64)
+        for i in range(4):
+            v.zone_keys[i] = int(A["vol_zone_keys"][i])
+        c._volumes = v  # keeps the struct alive as long as the cluster struct
+        c.volumes = ctypes.pointer(v)
     if A.get("pa_ns") is not None:
         pa = sr_pod_affinity()
         for f in ("ns", "label_off", "label_key", "label_val", "anti_off", "topology_key", "ns_off", "ns_ids",

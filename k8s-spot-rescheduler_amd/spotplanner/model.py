@@ -106,6 +106,120 @@ class TopologySpreadConstraint:
 
 
 @dataclass
+class Volume:
+    """A Spec.Volumes entry the volume filters read (the rest: local_storage)."""
+    name: str = "data"
+    claim: Optional[str] = None        # PersistentVolumeClaim.ClaimName
+    gce_pd: Optional[str] = None       # GCEPersistentDisk.PDName
+    aws_ebs: Optional[str] = None      # AWSElasticBlockStore.VolumeID
+    iscsi_iqn: Optional[str] = None    # ISCSI.IQN
+    azure_disk: Optional[str] = None   # AzureDisk.DiskName
+    rbd_image: Optional[str] = None    # RBD (not encoded: the shim flags the pod)
+    read_only: bool = False
+
+
+@dataclass
+class PersistentVolume:
+    name: str
+    kind: str = "csi"                  # csi | aws-ebs | gce-pd | azure-disk | nfs (not attachable)
+    volume_id: str = ""                # CSI VolumeHandle / EBS VolumeID / PD name / DiskName
+    driver: str = "ebs.csi.aws.com"    # CSI driver
+    labels: Dict[str, str] = field(default_factory=dict)        # zone / region labels (VolumeZone)
+    node_affinity: Optional[List[NodeSelectorTerm]] = None      # Spec.NodeAffinity.Required.NodeSelectorTerms
+
+
+@dataclass
+class PersistentVolumeClaim:
+    name: str
+    namespace: str = "kube-system"
+    volume_name: str = ""              # Spec.VolumeName of a bound claim ("" unbound)
+    binding_mode: str = "Immediate"    # its StorageClass's VolumeBindingMode
+
+
+ZONE_KEYS = ("failure-domain.beta.kubernetes.io/zone", "failure-domain.beta.kubernetes.io/region",
+             "topology.kubernetes.io/zone", "topology.kubernetes.io/region")
+NONCSI_KEYS = {"aws-ebs": "attachable-volumes-aws-ebs", "gce-pd": "attachable-volumes-gce-pd",
+               "azure-disk": "attachable-volumes-azure-disk"}
+NONCSI_DEFAULT = {"attachable-volumes-aws-ebs": 39, "attachable-volumes-gce-pd": 16,
+                  "attachable-volumes-azure-disk": 16}  # nodevolumelimits defaults (KUBE_MAX_PD_VOLS unset)
+
+
+@dataclass
+class VolumeWorld:
+    """The listers the volume filters read: claims, volumes, and per node the
+    CSINode drivers' allocatable counts (CSI limits; the non-CSI limits come
+    from Node.scalar attachable-volumes-* or the filter default)."""
+    pvcs: List[PersistentVolumeClaim] = field(default_factory=list)
+    pvs: List[PersistentVolume] = field(default_factory=list)
+    csi_limits: Dict[str, Dict[str, int]] = field(default_factory=dict)  # node name -> {driver: count}
+
+
+def _att_key(pv_kind: str, driver: str) -> Optional[str]:
+    if pv_kind == "csi":
+        return "attachable-volumes-csi-" + driver
+    return NONCSI_KEYS.get(pv_kind)
+
+
+def resolve_volumes(pod: "Pod", world: VolumeWorld):
+    """What the Go shim derives from a pod's volumes through the scheduler's
+    listers [upstream k8s v1.19.2]: (prefilter_fail, fallback, disks, attachable,
+    zones, pv_terms).  VolumeBinding's GetPodVolumes: a missing claim or
+    volume, or an unbound claim with Immediate binding, fails PreFilter; an
+    unbound claim with WaitForFirstConsumer needs the binder (not encoded).  RBD
+    volumes are not encoded."""
+    pvcs = {(c.namespace, c.name): c for c in world.pvcs}
+    pvs = {v.name: v for v in world.pvs}
+    pf, fb = False, False
+    disks, att, zones, pv_terms = [], [], [], []
+    for v in pod.volumes:
+        if v.rbd_image is not None:
+            fb = True
+        if v.gce_pd is not None:
+            disks.append((capi.SR_DISK_GCE_PD, v.gce_pd, v.read_only))
+            att.append(("attachable-volumes-gce-pd", "gce-pd/" + v.gce_pd, True))
+        if v.aws_ebs is not None:
+            disks.append((capi.SR_DISK_AWS_EBS, v.aws_ebs, v.read_only))
+            att.append(("attachable-volumes-aws-ebs", "aws-ebs/" + v.aws_ebs, True))
+        if v.iscsi_iqn is not None:
+            disks.append((capi.SR_DISK_ISCSI, v.iscsi_iqn, v.read_only))
+        if v.azure_disk is not None:
+            att.append(("attachable-volumes-azure-disk", "azure-disk/" + v.azure_disk, True))
+        if v.claim is None:
+            continue
+        pvc = pvcs.get((pod.namespace, v.claim))
+        if pvc is None:
+            pf = True
+            continue
+        if not pvc.volume_name:
+            if pvc.binding_mode == "WaitForFirstConsumer":
+                fb = True
+            else:
+                pf = True
+            continue
+        pv = pvs.get(pvc.volume_name)
+        if pv is None:
+            pf = True
+            continue
+        for k in ZONE_KEYS:
+            if k in pv.labels:
+                zs = [z.strip() for z in pv.labels[k].split("__")]
+                if all(zs):  # LabelZonesToSet fails on an empty zone: the filter skips the label
+                    zones.append((k, zs))
+        if pv.node_affinity is not None:
+            pv_terms.append(pv.node_affinity)
+        key = _att_key(pv.kind, pv.driver)
+        if key is not None:
+            uid = ("csi/%s/%s" % (pv.driver, pv.volume_id)) if pv.kind == "csi" else "%s/%s" % (pv.kind, pv.volume_id)
+            att.append((key, uid, pv.kind != "csi"))
+    seen, uatt = set(), []
+    for a in att:  # each (key, unique name) once per pod
+        if (a[0], a[1]) not in seen:
+            seen.add((a[0], a[1]))
+            uatt.append(a)
+    return pf, fb, disks, uatt, zones, pv_terms
+
+
+@dataclass
 class OwnerReference:
     kind: str
     name: str = ""
@@ -146,6 +260,7 @@ class Pod:
     deletion_age_s: Optional[float] = None    # now - DeletionTimestamp; None = not being deleted
     grace_seconds: Optional[int] = None       # Spec.TerminationGracePeriodSeconds (None = nil)
     local_storage: bool = False               # an EmptyDir or HostPath volume
+    volumes: List[Volume] = field(default_factory=list)  # resolved through encode_cluster's VolumeWorld
 
     def cpu_sort_milli(self) -> int:
         """getPodCPURequests (nodes/nodes.go:159-165): Σ regular containers' CPU."""
@@ -273,7 +388,7 @@ def _daemonset_owner_walk(pod: Pod):
     return False, False
 
 
-def pod_flags(pod: Pod, scalar_tables: bool = True, spread_tables: bool = True) -> int:
+def pod_flags(pod: Pod, scalar_tables: bool = True, spread_tables: bool = True, volume_tables: bool = True) -> int:
     f = 0
     if _daemonset_owner_walk(pod)[0]:
         f |= capi.SR_POD_DAEMONSET_CONTROLLER
@@ -284,7 +399,7 @@ def pod_flags(pod: Pod, scalar_tables: bool = True, spread_tables: bool = True) 
     conts = list(pod.containers) + list(pod.init_containers) + ([pod.overhead] if pod.overhead else [])
     if not scalar_tables and any(c.scalar for c in conts):  # the shim passes no scalar tables
         f |= capi.SR_POD_FB_SCALAR_RESOURCES
-    if pod.has_pvc:
+    if pod.has_pvc or (pod.volumes and not volume_tables):
         f |= capi.SR_POD_FB_VOLUMES
     if pod.hard_topology_spread or (not spread_tables and any(c.when_unsatisfiable == "DoNotSchedule"
                                                               for c in pod.topology_spread)):
@@ -438,9 +553,74 @@ def _encode_spread(pods: List[Pod], it: Interner) -> dict:
                 ts_terminating=_u8(term))
 
 
+def _encode_volumes(nodes: List[Node], pods: List[Pod], world: VolumeWorld, it: Interner, flags: List[int]) -> dict:
+    """sr_volumes arrays (the shim's resolution of every pod's volumes)."""
+    pf, do, dk, di, dr = [], [0], [], [], []
+    ao, ak, ai, an = [0], [], [], []
+    zo, zk, zvo, zv = [0], [], [0], []
+    pvo, pto, teo, tfo = [0], [0], [0], [0]
+    ek, eo, evo, ev, fk, fo, fvo, fv = [], [], [0], [], [], [], [0], []
+    for i, p in enumerate(pods):
+        fail, fb, disks, att, zones, pv_terms = resolve_volumes(p, world)
+        if fb:
+            flags[i] |= capi.SR_POD_FB_VOLUMES
+        pf.append(1 if fail else 0)
+        for kind, vid, ro in disks:
+            dk.append(kind)
+            di.append(it.id(vid))
+            dr.append(1 if ro else 0)
+        do.append(len(dk))
+        for key, uid, noncsi in att:
+            ak.append(it.id(key))
+            ai.append(it.id(uid))
+            an.append(1 if noncsi else 0)
+        ao.append(len(ak))
+        for key, vals in zones:
+            zk.append(it.id(key))
+            zv.extend(it.id(v) for v in vals)
+            zvo.append(len(zv))
+        zo.append(len(zk))
+        for terms in pv_terms:
+            for term in terms:
+                for r in term.match_expressions:
+                    ek.append(it.id(r.key))
+                    eo.append(SEL_OPS.get(r.operator, capi.SR_OP_OTHER))
+                    ev.extend(it.id(v) for v in r.values)
+                    evo.append(len(ev))
+                teo.append(len(ek))
+                for r in term.match_fields:
+                    fk.append(it.id(r.key))
+                    fo.append(SEL_OPS.get(r.operator, capi.SR_OP_OTHER))
+                    fv.extend(it.id(v) for v in r.values)
+                    fvo.append(len(fv))
+                tfo.append(len(fk))
+            pto.append(len(teo) - 1)
+        pvo.append(len(pto) - 1)
+    lo, lk, lv = [0], [], []
+    for n in nodes:
+        lim = {}
+        for key, default in NONCSI_DEFAULT.items():  # non-CSI: Allocatable, else the filter's default
+            lim[key] = n.scalar.get(key, default)
+        for driver, count in world.csi_limits.get(n.name, {}).items():
+            lim["attachable-volumes-csi-" + driver] = count
+        for key in sorted(lim):
+            lk.append(it.id(key))
+            lv.append(lim[key])
+        lo.append(len(lk))
+    return dict(vol_prefilter_fail=_u8(pf), vol_disk_off=_i32(do), vol_disk_kind=_i32(dk), vol_disk_id=_i32(di),
+                vol_disk_ro=_u8(dr), vol_att_off=_i32(ao), vol_att_key=_i32(ak), vol_att_id=_i32(ai),
+                vol_att_noncsi=_u8(an), vol_limit_off=_i32(lo), vol_limit_key=_i32(lk), vol_limit=_i64(lv),
+                vol_zone_off=_i32(zo), vol_zone_key=_i32(zk), vol_zone_val_off=_i32(zvo), vol_zone_vals=_i32(zv),
+                vol_zone_keys=[it.peek(k) for k in ZONE_KEYS], vol_pv_off=_i32(pvo), vol_pv_term_off=_i32(pto),
+                vol_term_expr_off=_i32(teo), vol_term_field_off=_i32(tfo), vol_expr_key=_i32(ek),
+                vol_expr_op=_i32(eo), vol_expr_val_off=_i32(evo), vol_expr_vals=_i32(ev), vol_field_key=_i32(fk),
+                vol_field_op=_i32(fo), vol_field_val_off=_i32(fvo), vol_field_vals=_i32(fv))
+
+
 def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Interner] = None,
                    pod_node: Optional[List[int]] = None, scalar_tables: bool = True,
-                   accounting: bool = True, spread_tables: bool = True) -> EncodedCluster:
+                   accounting: bool = True, spread_tables: bool = True,
+                   volumes: Optional[VolumeWorld] = None, volume_tables: bool = True) -> EncodedCluster:
     """Encode nodes and pods.  pod_node[i] is the node index of pods[i] (default:
     looked up by pod.node_name; -1 when unbound).  Pods of one node keep their
     relative order (= the per-node LIST order).  scalar_tables=False: no scalar
@@ -493,7 +673,7 @@ def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Intern
         re.append(eph)
         hp.append(0 if p.priority is None else 1)
         pr.append(0 if p.priority is None else p.priority)
-        fl.append(pod_flags(p, scalar_tables, spread_tables))
+        fl.append(pod_flags(p, scalar_tables, spread_tables, volume_tables))
         for k, v in p.node_selector.items():
             sk.append(it.id(k))
             sv.append(it.id(v))
@@ -533,6 +713,11 @@ def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Intern
              tol_off=_i32(tolo), tol_key=_i32(tolk), tol_op=_i32(tolop), tol_val=_i32(tolv),
              tol_eff=_i32(tole), port_off=_i32(po), port_proto=_i32(pp), port_num=_i32(pnum),
              port_ip=_i32(pip))
+    if volume_tables:
+        for k in ZONE_KEYS:  # interned up front: nodes carrying them match the keys' ids
+            it.id(k)
+        A.update(_encode_volumes(nodes, pods, volumes or VolumeWorld(), it, fl))
+        A["flags"] = _u32(fl)
     A.update(_encode_pod_affinity(pods, it))
     if spread_tables:
         A.update(_encode_spread(pods, it))

@@ -15,7 +15,14 @@ from . import capi
 
 class sr_synth_params(ctypes.Structure):
     _fields_ = [("config", ctypes.c_int32), ("seed", ctypes.c_uint64), ("n_on_demand", ctypes.c_int32),
-                ("n_spot", ctypes.c_int32), ("pinned_fraction", ctypes.c_double)]
+                ("n_spot", ctypes.c_int32), ("pinned_fraction", ctypes.c_double),
+                ("stateful_fraction", ctypes.c_double), ("init_fraction", ctypes.c_double),
+                ("gpu_fraction", ctypes.c_double)]
+
+
+# The "realistic" variant of a config (bench --variant realistic): StatefulSet
+# pods with zonal EBS CSI claims, init containers, GPU pods on GPU nodes.
+REALISTIC = dict(stateful_fraction=0.15, init_fraction=0.2, gpu_fraction=0.3)
 
 
 _synth = None
@@ -51,9 +58,11 @@ def synth_label_flags(s: str) -> int:
 
 class SynthCluster:
     def __init__(self, config: int, seed: int = 0, n_on_demand: int = 0, n_spot: int = 0,
-                 pinned_fraction: float = -1.0):
+                 pinned_fraction: float = -1.0, stateful_fraction: float = 0.0, init_fraction: float = 0.0,
+                 gpu_fraction: float = 0.0):
         self.lib = load_synth()
-        p = sr_synth_params(config, seed, n_on_demand, n_spot, pinned_fraction)
+        p = sr_synth_params(config, seed, n_on_demand, n_spot, pinned_fraction, stateful_fraction, init_fraction,
+                            gpu_fraction)
         self.handle = self.lib.sr_synth_generate(ctypes.byref(p))
         self.cluster = capi.sr_cluster()
         self.lib.sr_synth_view(self.handle, ctypes.byref(self.cluster))

@@ -424,6 +424,11 @@ struct oracle_snapshot {
   /* Allocatable scalar resources per position, copied at AddNodeWithPods */
   int32_t *alloc_off, *alloc_name;
   int64_t *alloc_val;
+  /* the attachable volumes (limit key << 32 | unique name) of every pod the
+   * snapshot holds, sorted; rebuilt on demand after a change (planner limit:
+   * a candidate pod whose attachable volume is already on a spot node) */
+  uint64_t *vb;
+  int32_t vb_n, vb_valid;
 };
 
 /* labels.NewRequirement's validateLabelKey (validation.IsQualifiedName) /
@@ -622,11 +627,13 @@ void oracle_snapshot_destroy(oracle_snapshot *s) {
   free(s->alloc_off);
   free(s->alloc_name);
   free(s->alloc_val);
+  free(s->vb);
   free(s);
 }
 
 void oracle_snapshot_add_pod(oracle_snapshot *s, const sr_cluster *c, int32_t pod, int32_t pos) {
   int32_t before = s->st[pos].anti, obefore = s->st[pos].opaque, ubefore = s->st[pos].sc_unknown;
+  s->vb_valid = 0;
   o_state_add_pod(&s->st[pos], c, pod);
   s->anti_total += s->st[pos].anti - before;
   s->opaque_total += s->st[pos].opaque - obefore;
@@ -646,6 +653,7 @@ int32_t oracle_snapshot_revert(oracle_snapshot *s) {
   s->st = s->saved;
   s->saved = NULL;
   s->forked = 0;
+  s->vb_valid = 0;
   s->anti_total = s->opaque_total = s->sc_unknown_total = 0;
   for (int32_t i = 0; i < s->n; i++) {
     s->anti_total += s->st[i].anti;
@@ -1131,9 +1139,213 @@ static int o_spread_ok(const o_state *st, const int32_t *node, int32_t n, const 
   return ok;
 }
 
+/* ===================================================================== */
+/* Volume filters [upstream k8s v1.19.2 plugins volumebinding, volumezone,
+ * volumerestrictions, nodevolumelimits], over the shim's resolved
+ * sr_volumes.  Not pinned by any reference test. */
+
+static uint64_t o_att_word(int32_t key, int32_t id) { return (uint64_t)(uint32_t)key << 32 | (uint32_t)id; }
+
+static int o_cmp_u64(const void *a, const void *b) {
+  uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+  return x < y ? -1 : x > y;
+}
+
+/* the snapshot's attachable volumes, sorted (s->vb) */
+static void o_vol_base_build(oracle_snapshot *s, const sr_cluster *c) {
+  const sr_volumes *V = c->volumes;
+  int32_t n = 0, cap = 0;
+  free(s->vb);
+  s->vb = NULL;
+  for (int32_t i = 0; i < s->n && V; i++)
+    for (int32_t q = 0; q < s->st[i].nlist; q++) {
+      int32_t pod = s->st[i].list[q];
+      for (int32_t a = V->att_off[pod]; a < V->att_off[pod + 1]; a++) {
+        if (n == cap) {
+          cap = cap ? 2 * cap : 64;
+          s->vb = (uint64_t *)realloc(s->vb, sizeof(uint64_t) * (size_t)cap);
+        }
+        s->vb[n++] = o_att_word(V->att_key[a], V->att_id[a]);
+      }
+    }
+  if (n) qsort(s->vb, (size_t)n, sizeof(uint64_t), o_cmp_u64);
+  s->vb_n = n;
+  s->vb_valid = 1;
+}
+
+/* labels.NewRequirement validation + Requirement.Matches over a PV term's expressions */
+static int o_vexpr_valid(const sr_cluster *c, const sr_volumes *V, int32_t e) {
+  int32_t nv = V->expr_val_off[e + 1] - V->expr_val_off[e];
+  if (V->expr_key[e] == c->id_empty && c->id_empty != -1) return 0;
+  if (!o_req_strings_ok(c, V->expr_key[e], V->expr_vals, V->expr_val_off[e], V->expr_val_off[e + 1])) return 0;
+  switch (V->expr_op[e]) {
+    case SR_OP_IN:
+    case SR_OP_NOT_IN:
+      return nv > 0;
+    case SR_OP_EXISTS:
+    case SR_OP_DOES_NOT_EXIST:
+      return nv == 0;
+    case SR_OP_GT:
+    case SR_OP_LT: {
+      int64_t x;
+      return nv == 1 && o_str_int(c, V->expr_vals[V->expr_val_off[e]], &x);
+    }
+    default:
+      return 0;
+  }
+}
+
+static int o_vexpr_match(const sr_cluster *c, const sr_volumes *V, int32_t e, int32_t node) {
+  int32_t v;
+  int has = o_node_label(c, node, V->expr_key[e], &v);
+  int32_t lo = V->expr_val_off[e], hi = V->expr_val_off[e + 1];
+  int64_t lv, rv;
+  switch (V->expr_op[e]) {
+    case SR_OP_GT:
+      return has && o_str_int(c, v, &lv) && o_str_int(c, V->expr_vals[lo], &rv) && lv > rv;
+    case SR_OP_LT:
+      return has && o_str_int(c, v, &lv) && o_str_int(c, V->expr_vals[lo], &rv) && lv < rv;
+    case SR_OP_IN:
+      return has && o_in_values(V->expr_vals, lo, hi, v);
+    case SR_OP_NOT_IN:
+      return !has || !o_in_values(V->expr_vals, lo, hi, v);
+    case SR_OP_EXISTS:
+      return has;
+    case SR_OP_DOES_NOT_EXIST:
+      return !has;
+    default:
+      return 0;
+  }
+}
+
+/* VolumeBinding.Filter on the bound claims: volumeutil.CheckNodeAffinity =
+ * v1helper.MatchNodeSelectorTerms(terms, node labels, nil fields) per PV with
+ * a Required node affinity: terms ORed, an empty term matches nothing, a term
+ * failing to build matches nothing, a field requirement reads "" */
+static int o_pv_affinity_ok(const sr_cluster *c, int32_t pod, int32_t node) {
+  const sr_volumes *V = c->volumes;
+  for (int32_t pv = V->pv_off[pod]; pv < V->pv_off[pod + 1]; pv++) {
+    int matched = 0;
+    for (int32_t t = V->pv_term_off[pv]; t < V->pv_term_off[pv + 1] && !matched; t++) {
+      int32_t e0 = V->term_expr_off[t], e1 = V->term_expr_off[t + 1];
+      int32_t f0 = V->term_field_off[t], f1 = V->term_field_off[t + 1];
+      if (e0 == e1 && f0 == f1) continue;
+      int ok = 1;
+      for (int32_t e = e0; e < e1 && ok; e++)
+        if (!o_vexpr_valid(c, V, e)) ok = 0;
+      for (int32_t e = e0; e < e1 && ok; e++)
+        if (!o_vexpr_match(c, V, e, node)) ok = 0;
+      for (int32_t f = f0; f < f1 && ok; f++) {
+        int32_t nv = V->field_val_off[f + 1] - V->field_val_off[f], op = V->field_op[f];
+        if (!((op == SR_OP_IN || op == SR_OP_NOT_IN) && nv == 1)) ok = 0;
+      }
+      for (int32_t f = f0; f < f1 && ok; f++) {
+        int eq = V->field_vals[V->field_val_off[f]] == c->id_empty && c->id_empty != -1; /* fields.Set(nil) */
+        if (!(V->field_op[f] == SR_OP_IN ? eq : !eq)) ok = 0;
+      }
+      if (ok) matched = 1;
+    }
+    if (!matched) return 0;
+  }
+  return 1;
+}
+
+/* VolumeZone.Filter: a node without any of the four zone / region labels
+ * passes; otherwise, per PV zone label, the node's value of its key ("" when
+ * absent) must be in the label's LabelZonesToSet values */
+static int o_volume_zone_ok(const sr_cluster *c, int32_t pod, int32_t node) {
+  const sr_volumes *V = c->volumes;
+  if (V->zone_off[pod] == V->zone_off[pod + 1]) return 1;
+  int any = 0;
+  for (int z = 0; z < 4; z++) {
+    int32_t v;
+    if (V->zone_keys[z] >= 0 && o_node_label(c, node, V->zone_keys[z], &v)) any = 1;
+  }
+  if (!any) return 1;
+  for (int32_t z = V->zone_off[pod]; z < V->zone_off[pod + 1]; z++) {
+    int32_t v;
+    if (!o_node_label(c, node, V->zone_key[z], &v)) return 0; /* "" is never in the set */
+    if (!o_in_values(V->zone_vals, V->zone_val_off[z], V->zone_val_off[z + 1], v)) return 0;
+  }
+  return 1;
+}
+
+/* VolumeRestrictions.Filter: isVolumeConflict of each inline disk against the
+ * disks of every pod on the node (same GCE PD / ISCSI IQN unless both mounts
+ * are read-only; the same EBS VolumeID always) */
+static int o_disks_ok(const o_state *st, const sr_cluster *c, int32_t pod) {
+  const sr_volumes *V = c->volumes;
+  for (int32_t d = V->disk_off[pod]; d < V->disk_off[pod + 1]; d++)
+    for (int32_t q = 0; q < st->nlist; q++) {
+      int32_t e = st->list[q];
+      for (int32_t f = V->disk_off[e]; f < V->disk_off[e + 1]; f++) {
+        if (V->disk_kind[f] != V->disk_kind[d] || V->disk_id[f] != V->disk_id[d]) continue;
+        if (V->disk_kind[d] == SR_DISK_AWS_EBS || !(V->disk_ro[d] && V->disk_ro[f])) return 0;
+      }
+    }
+  return 1;
+}
+
+/* nodevolumelimits: per limit key the node's unique attachable volumes plus
+ * the pod's volumes not already among them, against the node's limit (none:
+ * no check).  Non-CSI filters check whenever the pod has such a volume; the
+ * CSI filter only when some volume is new. */
+static int o_volume_limits_ok(const o_state *st, const sr_cluster *c, int32_t pod, int32_t node) {
+  const sr_volumes *V = c->volumes;
+  for (int32_t a = V->att_off[pod]; a < V->att_off[pod + 1]; a++) {
+    int32_t key = V->att_key[a], first = 1;
+    for (int32_t b = V->att_off[pod]; b < a; b++)
+      if (V->att_key[b] == key) first = 0;
+    if (!first) continue;
+    int64_t limit = -1;
+    for (int32_t l = V->limit_off[node]; l < V->limit_off[node + 1]; l++)
+      if (V->limit_key[l] == key) limit = V->limit[l];
+    if (limit < 0) continue; /* no limit for the key on this node */
+    /* existing unique volumes of the key: count each id once */
+    int64_t existing = 0;
+    for (int32_t q = 0; q < st->nlist; q++) {
+      int32_t e = st->list[q];
+      for (int32_t f = V->att_off[e]; f < V->att_off[e + 1]; f++) {
+        if (V->att_key[f] != key) continue;
+        int seen = 0;
+        for (int32_t q2 = 0; q2 <= q && !seen; q2++) {
+          int32_t e2 = st->list[q2];
+          int32_t end = q2 == q ? f : V->att_off[e2 + 1];
+          for (int32_t g = V->att_off[e2]; g < end && !seen; g++)
+            seen = V->att_key[g] == key && V->att_id[g] == V->att_id[f];
+        }
+        if (!seen) existing++;
+      }
+    }
+    int64_t fresh = 0;
+    for (int32_t b = V->att_off[pod]; b < V->att_off[pod + 1]; b++) {
+      if (V->att_key[b] != key) continue;
+      int on = 0;
+      for (int32_t q = 0; q < st->nlist && !on; q++) {
+        int32_t e = st->list[q];
+        for (int32_t f = V->att_off[e]; f < V->att_off[e + 1] && !on; f++)
+          on = V->att_key[f] == key && V->att_id[f] == V->att_id[b];
+      }
+      if (!on) fresh++;
+    }
+    if (!V->att_noncsi[a] && fresh == 0) continue;
+    if (existing + fresh > limit) return 0;
+  }
+  return 1;
+}
+
 int32_t oracle_pod_needs_fallback(const oracle_snapshot *s, const sr_cluster *c, int32_t pod) {
   const sr_pods *P = &c->pods;
   if (P->flags[pod] & SR_POD_FB_MASK) return 1;
+  /* planner limit: an attachable volume some spot node already holds (the
+   * device counts a pod's volumes as all new) */
+  if (c->volumes && c->volumes->att_off[pod + 1] > c->volumes->att_off[pod]) {
+    if (!s->vb_valid) o_vol_base_build((oracle_snapshot *)s, c);
+    for (int32_t a = c->volumes->att_off[pod]; a < c->volumes->att_off[pod + 1]; a++) {
+      uint64_t w = o_att_word(c->volumes->att_key[a], c->volumes->att_id[a]);
+      if (s->vb_n && bsearch(&w, s->vb, (size_t)s->vb_n, sizeof(uint64_t), o_cmp_u64)) return 1;
+    }
+  }
   /* outside the encoded set: scalar resources on an all-zero
    * cpu / memory / ephemeral request, or while some snapshot pod's scalar
    * usage is unknown */
@@ -1171,6 +1383,13 @@ static int o_check(const oracle_snapshot *s, const o_state *st, const int32_t *n
   if (!o_spread_ok(st, node, n, c, pod, pos)) return 0;
   if (!o_interpod_ok(st, node, n, c, pod, nd)) return 0;
   if (!o_pod_affinity_ok(st, node, n, c, pod, nd)) return 0;
+  if (c->volumes) {
+    if (c->volumes->prefilter_fail[pod]) return 0; /* VolumeBinding PreFilter */
+    if (!o_disks_ok(sp, c, pod)) return 0;
+    if (!o_volume_limits_ok(sp, c, pod, nd)) return 0;
+    if (!o_pv_affinity_ok(c, pod, nd)) return 0;
+    if (!o_volume_zone_ok(c, pod, nd)) return 0;
+  }
   return 1;
 }
 
@@ -1349,24 +1568,43 @@ static int o_cand_fallback(const oracle_snapshot *s, const sr_cluster *c, const 
   for (int32_t i = 0; i < np; i++)
     if (oracle_pod_needs_fallback(s, c, pods[i])) return 1;
   if (o_spread_dyn_fallback(s, c, pods, np)) return 1;
-  /* scalar resources: the planner's per-candidate table holds 64 distinct
-   * names, and it keeps a running state for at most 2 names listed by more
-   * than one pod of the candidate (the later pods see the earlier ones'
-   * AddPod); beyond that, the reference path */
-  if (c->pod_scalar_off) {
-    int32_t names[64], cnt[64], nn = 0, shared = 0;
+  /* planner limit: two pods of the candidate sharing an attachable volume */
+  if (c->volumes)
     for (int32_t i = 0; i < np; i++)
-      for (int32_t a = c->pod_scalar_off[pods[i]]; a < c->pod_scalar_off[pods[i] + 1]; a++) {
+      for (int32_t a = c->volumes->att_off[pods[i]]; a < c->volumes->att_off[pods[i] + 1]; a++)
+        for (int32_t j = i + 1; j < np; j++)
+          for (int32_t b = c->volumes->att_off[pods[j]]; b < c->volumes->att_off[pods[j] + 1]; b++)
+            if (c->volumes->att_key[a] == c->volumes->att_key[b] && c->volumes->att_id[a] == c->volumes->att_id[b])
+              return 1;
+  /* scalar resources and volume limit keys: the planner's per-candidate table
+   * holds 64 distinct names, and it keeps a running state for at most 2 names
+   * listed by more than one pod of the candidate (the later pods see the
+   * earlier ones' AddPod); beyond that, the reference path */
+  if (c->pod_scalar_off || c->volumes) {
+    int32_t names[64], cnt[64], nn = 0, shared = 0;
+    for (int32_t i = 0; i < np; i++) {
+      int32_t n_here = 0, here[64];
+      if (c->pod_scalar_off)
+        for (int32_t a = c->pod_scalar_off[pods[i]]; a < c->pod_scalar_off[pods[i] + 1] && n_here < 64; a++)
+          here[n_here++] = c->pod_scalar_name[a];
+      if (c->volumes)
+        for (int32_t a = c->volumes->att_off[pods[i]]; a < c->volumes->att_off[pods[i] + 1] && n_here < 64; a++) {
+          int32_t name = -(c->volumes->att_key[a] + 1), dup = 0; /* each limit key once per pod */
+          for (int32_t h = 0; h < n_here; h++) dup |= here[h] == name;
+          if (!dup) here[n_here++] = name;
+        }
+      for (int32_t h = 0; h < n_here; h++) {
         int32_t u = 0;
-        while (u < nn && names[u] != c->pod_scalar_name[a]) u++;
+        while (u < nn && names[u] != here[h]) u++;
         if (u < nn) {
           if (++cnt[u] == 2) shared++;
         } else {
           if (nn == 64) return 1;
-          names[nn] = c->pod_scalar_name[a];
+          names[nn] = here[h];
           cnt[nn++] = 1;
         }
       }
+    }
     if (shared > 2) return 1;
   }
   return 0;
@@ -1385,6 +1623,7 @@ int32_t oracle_plan(const oracle_snapshot *s, const sr_cluster *c, const sr_cand
   for (int32_t i = 0; i < nc; i++) status[i] = ORACLE_NOT_EVALUATED;
   for (int32_t i = 0; i < total; i++) map[i] = -1;
   uint64_t checks = 0, fb_pods = 0;
+  if (c->volumes && !s->vb_valid) o_vol_base_build((oracle_snapshot *)s, c); /* before any worker reads it */
 
   if (mode == 0 || threads <= 1) {
     o_state *st = o_copy_states(s->st, s->n);
