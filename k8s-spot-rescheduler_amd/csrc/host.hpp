@@ -286,7 +286,7 @@ enum : int32_t { CLS_AFF_REQUIRED = 1, CLS_IMPOSSIBLE = 2 };
 constexpr int kDomKeys = 4;   // key slots per encode
 constexpr int kDomMax = 64;   // domains of a table key (one bit each in a 64-bit mask)
 constexpr int kDynTerms = 4;  // terms of an affinity set planned on the domain path
-constexpr int kDynG = 4;      // domain path: mask words per pod set (64 pods each)
+constexpr int kDynG = 8;      // domain path: mask words per pod set (64 pods each)
 constexpr int kDynPods = 64 * kDynG;  // pods of a candidate planned on the domain path
 constexpr int kSpreadSlots = 2;  // topology spread constraints per pod planned on the domain path
 constexpr int kSpreadU64 = kSpreadSlots * (kDynG + 3);  // their words in the pod record

@@ -1424,21 +1424,25 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
   nbytes += (48u + 8u * kDevDynU64 + 4u) * static_cast<uint32_t>(np) + 4u;
   status = -1;
   int k = 0;
-  // A pod's records in one register, lanes [0, kDevDynU64) its domain-path
-  // record, lanes [40, 46) its pod record, lanes [48, 56) its extension record,
-  // loaded one pod ahead (every pod step otherwise starts with a memory round
-  // trip for them)
-  static_assert(kDevDynU64 <= 40 && kRecU64 <= 8 && kDevExtU64 <= 8, "record lanes of the domain path");
+  // A pod's records in two registers, loaded one pod ahead (every pod step
+  // otherwise starts with a memory round trip for them): lanes [0,
+  // kDevDynU64) of one its domain-path record; lanes [0, 6) of the other its
+  // pod record, lanes [8, 16) its extension record
+  static_assert(kDevDynU64 <= 64 && kRecU64 <= 8 && kDevExtU64 <= 8, "record lanes of the domain path");
   auto records = [&](int q) -> uint64_t {
     if (q >= np) return 0ull;
     if (lane < kDevDynU64) return w.dyn_pod[static_cast<size_t>(dbase + q) * kDevDynU64 + lane];
-    if (lane >= 40 && lane < 40 + kRecU64) return w.pod_rec[static_cast<size_t>(p0 + q) * kRecU64 + (lane - 40)];
-    if (ext && lane >= 48 && lane < 48 + kDevExtU64)
-      return w.pod_ext[static_cast<size_t>(ebase + q) * kDevExtU64 + (lane - 48)];
+    return 0ull;
+  };
+  auto records_pod = [&](int q) -> uint64_t {
+    if (q >= np) return 0ull;
+    if (lane < kRecU64) return w.pod_rec[static_cast<size_t>(p0 + q) * kRecU64 + lane];
+    if (ext && lane >= 8 && lane < 8 + kDevExtU64)
+      return w.pod_ext[static_cast<size_t>(ebase + q) * kDevExtU64 + (lane - 8)];
     return 0ull;
   };
   if (ext) nbytes += 8u * kDevExtU64 * static_cast<uint32_t>(np);
-  uint64_t rv = records(0);
+  uint64_t rv = records(0), rvp = records_pod(0);
   uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
   auto stamp = [&](uint64_t& acc) {
     if (PROF) {
@@ -1448,16 +1452,17 @@ __device__ __forceinline__ void k2_domain(const DevWorkload& w, uint64_t* __rest
     }
   };
   for (; k < np; ++k) {
-    const uint64_t cur = rv;
+    const uint64_t cur = rv, curp = rvp;
     rv = records(k + 1);
-    auto D = [&](int i) { return readlane64(cur, i); };        // domain-path record word i
-    auto PR = [&](int i) { return readlane64(cur, 40 + i); };  // pod record word i
+    rvp = records_pod(k + 1);
+    auto D = [&](int i) { return readlane64(cur, i); };    // domain-path record word i
+    auto PR = [&](int i) { return readlane64(curp, i); };  // pod record word i
     const int64_t rc = static_cast<int64_t>(PR(0)), rm = static_cast<int64_t>(PR(1)), re = static_cast<int64_t>(PR(2));
     const uint64_t pm = PR(3), r01 = PR(4), r23 = PR(5);
     const uint64_t pin = swap_pairs(pm, w.swap_mask);
     const bool zero = (rc | rm | re) == 0;
     // what AddPod subtracts and the shared scalars (extension record)
-    auto EX = [&](int i) { return static_cast<int64_t>(readlane64(cur, 48 + i)); };
+    auto EX = [&](int i) { return static_cast<int64_t>(readlane64(curp, 8 + i)); };
     const int64_t ac = ext ? EX(0) : rc, am = ext ? EX(1) : rm, ae = ext ? EX(2) : re;
     const int64_t sr0 = ext ? EX(3) : INT64_MIN, sr1 = ext ? EX(4) : INT64_MIN;
     const int64_t sa0 = ext ? EX(5) : 0, sa1 = ext ? EX(6) : 0;
@@ -1854,8 +1859,10 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   const bool node_order = np <= 4 * 64 && w.k2_mode == 0 && ebase < 0;
   if (dbase >= 0) {  // writes out_node itself
     wide = 3;
-    if (np <= 64) k2_domain<CH, 1, PROF>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes, st, ebase);
-    else k2_domain<CH, kDevDynG, PROF>(w, reinterpret_cast<uint64_t*>(&L), p0, np, dbase, status, nbytes, st, ebase);
+    uint64_t* tl = reinterpret_cast<uint64_t*>(&L);
+    if (np <= 64) k2_domain<CH, 1, PROF>(w, tl, p0, np, dbase, status, nbytes, st, ebase);
+    else if (np <= 256) k2_domain<CH, 4, PROF>(w, tl, p0, np, dbase, status, nbytes, st, ebase);
+    else k2_domain<CH, kDevDynG, PROF>(w, tl, p0, np, dbase, status, nbytes, st, ebase);
   } else if (ebase >= 0) {  // extension records: pod order with the extended running state
     int placed = k2_run<1, CH, PROF, true>(w, L, p0, np, status, st, nbytes, ebase);
     wide = placed < 0 ? 1 : 0;

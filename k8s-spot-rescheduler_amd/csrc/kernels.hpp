@@ -11,7 +11,7 @@ namespace sr {
 
 constexpr int kResultHeader = 8;           // words before the winner's mapping in `result`
 constexpr size_t kK0ProfWaves = 32768;  // K0 waves profiled after K2's [n_cand][16] records
-constexpr int kDevDynG = 4;             // domain path: groups of 64 pods (<= 256 pods per candidate)
+constexpr int kDevDynG = 8;             // domain path: groups of 64 pods (<= 512 pods per candidate)
 constexpr int kDevSpreadSlots = 2;     // spread constraints per pod on the domain path (host.hpp kSpreadSlots)
 constexpr int kDevDynU64 = 5 * kDevDynG + 1 + kDevSpreadSlots * (kDevDynG + 3);
                                         // domain-path pod record words (host.hpp kDynU64): per key slot

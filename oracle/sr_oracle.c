@@ -1479,7 +1479,7 @@ static int32_t o_eval_candidate(const oracle_snapshot *s, o_state *st, const int
  * plans on its domain path: a pod whose constraint counts an
  * earlier pod of the candidate (its namespace, not terminating, selected),
  * when the pod has pairs at all, makes the candidate a fallback if it has
- * more than 256 pods, if the pod has another constraint on that key or more
+ * more than 512 pods, if the pod has another constraint on that key or more
  * than 2 such constraints, if the key is shared (not on every spot node with
  * distinct values) and has more than 64 values, or if the key is node-local
  * and no more of the pairs' nodes hold the minimum count than the constraint
@@ -1496,7 +1496,7 @@ static int o_spread_dyn_fallback(const oracle_snapshot *s, const sr_cluster *c, 
     for (int32_t k = S->off[pods[i]]; k < S->off[pods[i] + 1] && !any; k++)
       for (int32_t j = 0; j < i && !any; j++) any = o_spread_counted(c, k, pods[i], pods[j]);
   if (!any) return 0;
-  if (np > 256) return 1;
+  if (np > 512) return 1;
   const int32_t n = s->n;
   uint8_t *pair = (uint8_t *)malloc((size_t)n + 1);
   int fb = 0;

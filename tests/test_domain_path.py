@@ -72,19 +72,38 @@ def test_gpu_random_shared_key_plans(checker, seed):
 
 
 @pytest.mark.gpu
-def test_gpu_domain_path_limit_falls_back(checker):
-    """Up to 256 pods interacting across nodes are planned on the device
-    (4 groups of 64 lanes); a 257-pod candidate takes the fallback path
-    (kDynPods).  The oracle plans every one of them."""
+def test_gpu_domain_path_up_to_512_pods(checker):
+    """Up to 512 pods interacting across nodes are planned on the device
+    (8 groups of 64 lanes: candidates of 300 and 512 pods, and 257 / 256 / 65 /
+    64 around the group boundaries), bit-exact with the oracle; a 513-pod
+    candidate exceeds the planner's per-candidate limit (MAX_CAND_PODS) and
+    takes the fallback path.  The oracle plans every one of them."""
     from domain_cases import pod, term
     from test_gpu_parity import run_scenario
-    big = [[pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(256)] + [pod("d", "db")],
-           [pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(255)] + [pod("d", "db")],
-           [pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(64)] + [pod("d", "db")],
-           [pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(63)] + [pod("d", "db")]]
-    _, o, p = run_scenario(checker, nodes(), [[] for _ in range(4)], big, extra_fallback=lambda c: c == 0)
-    assert [int(x) for x in p.status[1:]] == [int(x) for x in o["status"][1:]]
-    assert int(p.status[0]) == capi.SR_CAND_FALLBACK
+    sizes = [512, 300, 257, 256, 64, 63]
+    big = [[pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(n)] + [pod("d", "db")] for n in sizes]
+    big.append([pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(512)] + [pod("d", "db")])
+    _, o, p = run_scenario(checker, nodes(), [[] for _ in range(4)], big, extra_fallback=lambda c: c == len(sizes))
+    assert [int(x) for x in p.status[:len(sizes)]] == [int(x) for x in o["status"][:len(sizes)]]
+    assert all(int(x) != capi.SR_CAND_FALLBACK for x in p.status[:len(sizes)])
+    assert int(p.status[len(sizes)]) == capi.SR_CAND_FALLBACK
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_large_domain_candidates_300_512(checker, seed):
+    """Zone anti-affinity / affinity candidates of 300-512 pods with init containers and scalars on the
+    8-group domain path, against the oracle."""
+    from test_gpu_parity import run_scenario
+    nodes_, spot_pods, cands = rand_scenario(7600 + seed, n_spot=48 + 8 * seed, n_cand=2, max_pods=200,
+                                             features=False, anti=0.2, aff=0.15 if seed % 2 else 0.0,
+                                             shared_keys=True, valid_selectors=True)
+    for i, c in enumerate(cands):  # 300 .. 512 pods each
+        want = 300 + 212 * i
+        while len(c) < want:
+            c.extend(cands[(i + 1) % 2][:want - len(c)] or [c[0]])
+    _, o, p = run_scenario(checker, nodes_, spot_pods, cands)
+    assert all(int(s) != capi.SR_CAND_FALLBACK for s in o["status"])
 
 
 @pytest.mark.gpu
