@@ -1912,31 +1912,81 @@ void launch(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, hipEvent
   else hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
 }
 
+}  // namespace
+
+// The K2 launchers are compiled in parts (SR_KPART, Makefile: one object per
+// part, built in parallel; -1 = everything in one translation unit): 0 = the
+// dispatch, K0 and K3; 1 = the node-order kernels; 2..7 = the general kernel
+// for rows of 1, 2, 4, 8, 16, 32 chunks of 64 words.
+#ifndef SR_KPART
+#define SR_KPART -1
+#endif
+template <bool PROF>
+hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+template <int CH, bool PROF>
+hipError_t launch_k2_place_ch(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+
+#if SR_KPART == -1 || SR_KPART == 1
+template <bool PROF>
+hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  const int n = w.n_list;
+  const dim3 grid((n + 3) / 4), block(256);
+  const size_t lds = 4 * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
+  if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (G == 2) launch(k2_node<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else launch(k2_node<4, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  return hipGetLastError();
+}
+template hipError_t launch_k2_node_g<false>(const DevWorkload&, int, hipStream_t, hipEvent_t, hipEvent_t);
+template hipError_t launch_k2_node_g<true>(const DevWorkload&, int, hipStream_t, hipEvent_t, hipEvent_t);
+#endif
+
+#if SR_KPART == -1 || SR_KPART >= 2
+template <int CH, bool PROF>
+hipError_t launch_k2_place_ch(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  const int n = w.n_list;
+  const dim3 grid((n + 3) / 4), block(256);
+  launch(k2_place<CH, PROF>, grid, block, 4 * sizeof(K2Lds), s, ev0, ev1, w, w.list, n);
+  return hipGetLastError();
+}
+#define SR_PLACE_INST(CH)                                                                                      \
+  template hipError_t launch_k2_place_ch<CH, false>(const DevWorkload&, hipStream_t, hipEvent_t, hipEvent_t); \
+  template hipError_t launch_k2_place_ch<CH, true>(const DevWorkload&, hipStream_t, hipEvent_t, hipEvent_t);
+#endif
+#if SR_KPART == -1 || SR_KPART == 2
+SR_PLACE_INST(1)
+#endif
+#if SR_KPART == -1 || SR_KPART == 3
+SR_PLACE_INST(2)
+#endif
+#if SR_KPART == -1 || SR_KPART == 4
+SR_PLACE_INST(4)
+#endif
+#if SR_KPART == -1 || SR_KPART == 5
+SR_PLACE_INST(8)
+#endif
+#if SR_KPART == -1 || SR_KPART == 6
+SR_PLACE_INST(16)
+#endif
+#if SR_KPART == -1 || SR_KPART == 7
+SR_PLACE_INST(32)
+#endif
+
+#if SR_KPART == -1 || SR_KPART == 0
 template <bool PROF>
 hipError_t launch_k2(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
   if (n <= 0) return hipSuccess;
-  const dim3 grid((n + 3) / 4), block(256);
-  if (!w.dyn_cand && !w.ext_cand && w.k2_mode == 0 && w.max_np >= 1 && w.max_np <= 4 * 64 && w.k2_node_kernel) {
-    const int G = w.max_np <= 64 ? 1 : (w.max_np <= 128 ? 2 : 4);
-    const size_t lds = 4 * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
-    if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-    else if (G == 2) launch(k2_node<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-    else launch(k2_node<4, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-    return hipGetLastError();
-  }
-  const size_t lds = 4 * sizeof(K2Lds);
+  if (!w.dyn_cand && !w.ext_cand && w.k2_mode == 0 && w.max_np >= 1 && w.max_np <= 4 * 64 && w.k2_node_kernel)
+    return launch_k2_node_g<PROF>(w, w.max_np <= 64 ? 1 : (w.max_np <= 128 ? 2 : 4), s, ev0, ev1);
   const int chunks = (w.Wp + 63) / 64;
-  if (chunks <= 1) launch(k2_place<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-  else if (chunks <= 2) launch(k2_place<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-  else if (chunks <= 4) launch(k2_place<4, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-  else if (chunks <= 8) launch(k2_place<8, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-  else if (chunks <= 16) launch(k2_place<16, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-  else launch(k2_place<32, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-  return hipGetLastError();
+  if (chunks <= 1) return launch_k2_place_ch<1, PROF>(w, s, ev0, ev1);
+  if (chunks <= 2) return launch_k2_place_ch<2, PROF>(w, s, ev0, ev1);
+  if (chunks <= 4) return launch_k2_place_ch<4, PROF>(w, s, ev0, ev1);
+  if (chunks <= 8) return launch_k2_place_ch<8, PROF>(w, s, ev0, ev1);
+  if (chunks <= 16) return launch_k2_place_ch<16, PROF>(w, s, ev0, ev1);
+  return launch_k2_place_ch<32, PROF>(w, s, ev0, ev1);
 }
-
-}  // namespace
 
 hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hipStream_t s, hipEvent_t ev0,
                          hipEvent_t ev1) {
@@ -1957,5 +2007,6 @@ hipError_t launch_winner(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hi
   launch(k3_winner, dim3(1), dim3(64), 0, s, ev0, ev1, w);
   return hipGetLastError();
 }
+#endif  // SR_KPART 0
 
 }  // namespace sr
