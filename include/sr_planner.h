@@ -311,6 +311,13 @@ typedef struct {
   const sr_spread *spread;
   /* Volume filters (ABI 5).  NULL: pods with volumes carry SR_POD_FB_VOLUMES. */
   const sr_volumes *volumes;
+  /* [pods.n] A value the shim changes whenever the pod object changes (e.g. a
+   * hash of UID and ResourceVersion; 0 = unknown).  The planner's encoder keeps
+   * what it derived from a pod's spec keyed by (pod index, stamp) across calls
+   * and re-derives it only for pods whose stamp changed, so the string ids a
+   * stamped pod's spec uses must stay the same across calls (one interner per
+   * process).  NULL: no stamps (every call re-reads every pod's spec).  ABI 5. */
+  const uint64_t *pod_stamp;
 } sr_cluster;
 #define SR_STR_LABEL_VALUE 1u
 #define SR_STR_LABEL_KEY   2u
@@ -564,6 +571,7 @@ typedef struct {
   int32_t  enc_static_rebuilt; /* 1: the last prepare rebuilt the spot pool's static view (order, labels, taints) */
   int32_t  enc_state_nodes;    /* spot nodes whose capacity state the last prepare re-encoded */
   int32_t  prefix_batches;     /* batches the last sr_plan_first ran */
+  int32_t  enc_memo_pods;      /* candidate pods the last prepare found in its per-pod memo (sr_cluster.pod_stamp) */
 } sr_timing;
 /* mask: which kernels sr_plan_run brackets with HIP events (resets the sums):
  * 1 = K0, 2 = K2, 4 = collective (multi-GPU) + K3; 0 = no events.  Events are read back lazily, by

@@ -94,6 +94,8 @@ int32_t pod_att_of(const sr_cluster* c, int32_t pod, int32_t key) {
   return n;
 }
 constexpr int32_t kNoName = INT32_MIN;  // no shared scalar name (volume keys are negative names)
+// EncoderCache::PodMemo::bits
+enum : uint32_t { MEMO_PLAIN = 1, MEMO_FB = 2, MEMO_ACC_BAD = 4, MEMO_ACC_DIFF = 8, MEMO_PORTS = 16 };
 
 // REQ_ZONE: VolumeZone's check of one PV zone / region label {key, zone keys
 // [4], values}: a node passes when it carries none of the four zone keys, or
@@ -995,6 +997,21 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   w->state_gen = C.state_gen;
   phase(0);
 
+  // ---- per-pod memo (sr_cluster.pod_stamp): valid for the cluster's table
+  // shape it was derived under
+  const uint64_t* stamps = c->pod_stamp;
+  if (stamps) {
+    const uint64_t shape = 1 | (c->str_int ? 2u : 0u) | (c->str_label ? 4u : 0u) | (c->pod_affinity ? 8u : 0u) |
+                           (c->spread ? 16u : 0u) | (c->pod_scalar_off ? 32u : 0u) | (c->volumes ? 64u : 0u) |
+                           (c->acc_milli_cpu ? 128u : 0u);
+    if (C.memo_shape != shape) {
+      C.pod_memo.clear();
+      C.memo_shape = shape;
+    }
+    if (C.pod_memo.size() < static_cast<size_t>(P.n)) C.pod_memo.resize(static_cast<size_t>(P.n));
+  }
+  std::atomic<int32_t> memo_hits{0};
+
   // ---- pass 1: candidate-level fallback (host-decided)
   w->status_host.assign(static_cast<size_t>(nc), STATUS_PENDING);
   // the candidate pods' requests, gathered once in input order (the per-pod
@@ -1035,6 +1052,40 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         if (spread_invalid(c, k)) return true;
     }
     return anti_opaque(c, pod) || aff_opaque(c, pod);  // required (anti-)affinity the encoded set cannot read
+  };
+  // The same checks through the memo: for a "plain" pod (no scalar resources,
+  // spread constraints or attachable volumes: nothing snapshot-dependent) the
+  // answer is a function of the pod alone; MEMO_ACC_DIFF and MEMO_PORTS feed
+  // the extension and host-port passes.
+  auto pod_bits = [&](int32_t pod) -> uint32_t {
+    uint32_t b = 0;
+    const bool plain = !has_scalars(c, pod) && !has_spread(c, pod) && att_count(c, pod) == 0;
+    if (plain) {
+      b |= MEMO_PLAIN;
+      const int64_t rq[3] = {P.req_milli_cpu[pod], P.req_memory[pod], P.req_ephemeral[pod]};
+      bool fb = (P.flags[pod] & SR_POD_FB_MASK) || !in_range(rq[0]) || !in_range(rq[1]) || !in_range(rq[2]);
+      if (!fb && P.aff_required[pod])
+        for (int32_t t = P.term_off[pod]; t < P.term_off[pod + 1] && !fb; ++t)
+          for (int32_t e = P.term_expr_off[t]; e < P.term_expr_off[t + 1] && !fb; ++e)
+            fb = ((P.expr_op[e] == SR_OP_GT || P.expr_op[e] == SR_OP_LT) && !c->str_int) || !c->str_label;
+      fb = fb || anti_opaque(c, pod) || aff_opaque(c, pod);
+      if (fb) b |= MEMO_FB;
+      for (int r = 0; r < 3; ++r)
+        if (!in_range(pod_acc(c, pod, r))) b |= MEMO_ACC_BAD;
+    }
+    if (pod_acc(c, pod, 0) != P.req_milli_cpu[pod] || pod_acc(c, pod, 1) != P.req_memory[pod] ||
+        pod_acc(c, pod, 2) != P.req_ephemeral[pod])
+      b |= MEMO_ACC_DIFF;
+    if (has_ports(c, pod)) b |= MEMO_PORTS;
+    return b;
+  };
+  auto memo_bits = [&](int32_t pod) -> uint32_t {
+    if (!stamps || stamps[pod] == 0) return pod_bits(pod);
+    EncoderCache::PodMemo& m = C.pod_memo[static_cast<size_t>(pod)];
+    if (m.stamp_bits == stamps[pod]) return m.bits;
+    m.bits = pod_bits(pod);
+    m.stamp_bits = stamps[pod];
+    return m.bits;
   };
   for (int32_t i = 0; i < nc; ++i)
     if (cands->cand_pod_off[i + 1] < cands->cand_pod_off[i]) {
@@ -1080,7 +1131,6 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
       // an existing pod's opaque anti-affinity may select any incoming pod
       bool fb = (c->pod_affinity ? snap->opaque_total : snap->anti_total) > 0 || (e - b) > MAX_CAND_PODS;
-      for (int32_t j = b; j < e && !fb; ++j) fb = pod_fallback(cands->cand_pods[j], j, j + 1 == e);
       // Extension records (K2's pod-order and domain paths): a pod followed by
       // others whose AddPod accounting differs from its fit request (the
       // running state subtracts the accounting), and scalar resources listed
@@ -1088,12 +1138,27 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       // ones' AddPod: a running scalar state per touched node, at most
       // kExtScalars names per candidate)
       uint8_t ext = 0;
-      cand_sname[2 * i] = cand_sname[2 * i + 1] = kNoName;
-      for (int32_t j = b; j + 1 < e && !fb && !(ext & 1); ++j) {
+      bool ports = false;
+      int32_t hits = 0;
+      for (int32_t j = b; j < e && !fb; ++j) {
         const int32_t pod = cands->cand_pods[j];
-        ext |= (pod_acc(c, pod, 0) != P.req_milli_cpu[pod] || pod_acc(c, pod, 1) != P.req_memory[pod] ||
-                pod_acc(c, pod, 2) != P.req_ephemeral[pod]) ? 1 : 0;
+        const bool last = j + 1 == e;
+        const uint32_t mb = memo_bits(pod);
+        hits += stamps && stamps[pod] != 0 ? 1 : 0;
+        if (mb & MEMO_PLAIN) {
+          fb = (mb & MEMO_FB) || (!last && (mb & MEMO_ACC_BAD));
+          int64_t* rq = &req_flat[static_cast<size_t>(j - w->pod_base) * 3];
+          rq[0] = P.req_milli_cpu[pod];
+          rq[1] = P.req_memory[pod];
+          rq[2] = P.req_ephemeral[pod];
+        } else {
+          fb = pod_fallback(pod, j, last);
+        }
+        if (!last && (mb & MEMO_ACC_DIFF)) ext |= 1;
+        ports = ports || (mb & MEMO_PORTS);
       }
+      if (stamps) memo_hits.fetch_add(hits, std::memory_order_relaxed);
+      cand_sname[2 * i] = cand_sname[2 * i + 1] = kNoName;
       if (!fb && c->volumes && vol_base && !vol_base->empty()) {
         // an attachable volume some spot node already holds, or two pods of
         // the candidate sharing one: the volume counts stop being additive
@@ -1103,7 +1168,9 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
             fb = vol_base->count(att_word(c->volumes->att_key[a], c->volumes->att_id[a])) != 0;
         }
       }
-      if (!fb && c->volumes) {
+      bool any_att = false;
+      for (int32_t j = b; j < e && !fb && c->volumes && !any_att; ++j) any_att = att_count(c, cands->cand_pods[j]) > 0;
+      if (!fb && any_att) {
         std::vector<uint64_t> ids;
         for (int32_t j = b; j < e; ++j) {
           const int32_t pod = cands->cand_pods[j];
@@ -1151,7 +1218,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       }
       cand_ext[i] = fb ? 0 : ext;
       if (fb) w->status_host[i] = SR_CAND_FALLBACK;
-      for (int32_t j = b; j < e && !fb && !cand_ports[i]; ++j) cand_ports[i] = has_ports(c, cands->cand_pods[j]);
+      cand_ports[i] = !fb && ports;
     }
   };
   if (w->n_input_pods > serial_pods()) parallel_for(static_cast<size_t>(nc), 64, pass1);
@@ -1400,6 +1467,11 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
         const size_t b0 = buf.size();
         spec_woff[q] = static_cast<uint32_t>(b0);
         const int32_t pod = active_pod[q];
+        if (stamps && stamps[pod] != 0 && C.pod_memo[static_cast<size_t>(pod)].stamp_spec == stamps[pod]) {
+          pod_spec[q] = C.pod_memo[static_cast<size_t>(pod)].spec;  // a global id already
+          spec_shard[q] = 0xfe;
+          continue;
+        }
         if (!has_static_spec(c, P, pod)) continue;  // spec 0
         for_each_spec_word(c, P, pod, [&](int32_t x) { buf.push_back(x); });
         const uint64_t h = hash_words(buf.data() + b0, buf.size() - b0);
@@ -1452,6 +1524,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       new_spec_pod.push_back(active_pod[q]);
     }
   C.last_new_specs = static_cast<int32_t>(new_spec_pod.size());
+  C.last_memo_hits = memo_hits.load(std::memory_order_relaxed);
   const int32_t n_spec_ids = spec0 + static_cast<int32_t>(new_spec_pod.size());
   const bool combos = anti.active || aff.active || sdyn.active;
   // keys present in this call (pods without inter-pod terms: the spec id),
@@ -1461,8 +1534,16 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   key_seen.assign(static_cast<size_t>(n_spec_ids), 0);
   pfor(static_cast<size_t>(na), 4096, [&](size_t lo, size_t hi) {
     for (size_t q = lo; q < hi; ++q) {
-      const int32_t g = spec_shard[q] == 0xff ? 0 : C.spec_shards[spec_shard[q]].global[pod_spec[q]];
+      const uint8_t sh = spec_shard[q];
+      const int32_t g = sh == 0xff ? 0 : sh == 0xfe ? pod_spec[q] : C.spec_shards[sh].global[pod_spec[q]];
       pod_spec[q] = g;
+      if (stamps && sh != 0xfe) {
+        const int32_t pod = active_pod[q];
+        if (stamps[pod] != 0) {
+          C.pod_memo[static_cast<size_t>(pod)].spec = g;
+          C.pod_memo[static_cast<size_t>(pod)].stamp_spec = stamps[pod];
+        }
+      }
       if (!combos && !__atomic_load_n(&key_seen[g], __ATOMIC_RELAXED)) __atomic_store_n(&key_seen[g], uint8_t(1), __ATOMIC_RELAXED);
     }
   });

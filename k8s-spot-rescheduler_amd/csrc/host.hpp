@@ -474,6 +474,19 @@ struct EncoderCache {
     std::vector<uint32_t> spec_woff;
     std::vector<std::vector<int32_t>> spec_words, chunk_shard;
   } scratch;
+  // ---- per-pod memo by (pod index, sr_cluster.pod_stamp): the spec id and
+  // the snapshot-independent part of the candidate checks of pods the shim
+  // stamped, valid while the stamp, the content dictionaries (spec ids) and
+  // the cluster's table shape are unchanged
+  struct PodMemo {
+    uint64_t stamp_spec = 0;  // stamp `spec` was derived for (0: none)
+    uint64_t stamp_bits = 0;  // stamp `bits` were derived for (0: none)
+    int32_t spec = 0;
+    uint32_t bits = 0;        // MEMO_* (encode.cpp)
+  };
+  std::vector<PodMemo> pod_memo;
+  uint64_t memo_shape = 0;
+  int32_t last_memo_hits = 0;
   // ---- per-call counters (bench: what the last call had to rebuild)
   int32_t last_new_specs = 0, last_static_changed = 0, last_state_changed = 0;
   // the last state refresh patched these nodes' records on top of generation
@@ -482,6 +495,7 @@ struct EncoderCache {
   uint64_t patched_from = ~0ull;
 
   void clear_content() {  // drops every content-interned dictionary
+    pod_memo.clear();     // its spec ids index them
     spec_shards.clear();
     spec.clear();
     spec_req_off.assign(1, 0);

@@ -434,6 +434,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   ctx->t.enc_new_specs = ctx->enc.last_new_specs;
   ctx->t.enc_static_rebuilt = ctx->enc.last_static_changed;
   ctx->t.enc_state_nodes = ctx->enc.last_state_changed;
+  ctx->t.enc_memo_pods = ctx->enc.last_memo_hits;
   ctx->prepared = true;
   return SR_OK;
 }

@@ -64,6 +64,7 @@ struct sr_synth {
   std::vector<int32_t> v_field_key, v_field_op, v_field_val_off{0}, v_field_vals;
   int32_t zone_keys[4] = {-1, -1, -1, -1};
   mutable sr_volumes vview{};  // the sr_volumes of sr_synth_view
+  std::vector<uint64_t> stamp;  // sr_cluster.pod_stamp: pods never change after generation
 
   int32_t id(const std::string& s) {
     auto it = ids.find(s);
@@ -448,6 +449,8 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
     }
   }
   for (const std::string& str : s->strings) s->str_label.push_back(label_flags(str));
+  s->stamp.resize(s->pod_node.size());
+  for (size_t i = 0; i < s->stamp.size(); ++i) s->stamp[i] = 0x5EED000000000000ull + i + 1;
   return s;
 }
 
@@ -517,6 +520,7 @@ void sr_synth_view(const sr_synth* s, sr_cluster* c) {
   c->acc_milli_cpu = c->acc_memory = c->acc_ephemeral = nullptr;  // AddPod adds the fit request
   c->spread = nullptr;  // no topology spread constraints in the BASELINE configs
   c->volumes = nullptr;  // realistic variant only (sr_synth_params.stateful_fraction)
+  c->pod_stamp = s->stamp.data();
   if (s->has_acc) {
     c->acc_milli_cpu = s->acc_cpu.data();
     c->acc_memory = s->acc_mem.data();

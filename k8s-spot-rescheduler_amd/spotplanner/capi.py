@@ -94,7 +94,8 @@ class sr_cluster(ctypes.Structure):
                 ("pod_scalar_off", P32), ("pod_scalar_name", P32), ("pod_scalar_req", P64), ("pod_scalar_acc", P64),
                 ("node_scalar_off", P32), ("node_scalar_name", P32), ("node_scalar_alloc", P64),
                 ("acc_milli_cpu", P64), ("acc_memory", P64), ("acc_ephemeral", P64),
-                ("spread", ctypes.POINTER(sr_spread)), ("volumes", ctypes.POINTER(sr_volumes))]
+                ("spread", ctypes.POINTER(sr_spread)), ("volumes", ctypes.POINTER(sr_volumes)),
+                ("pod_stamp", ctypes.POINTER(ctypes.c_uint64))]
 
 
 class sr_node_label(ctypes.Structure):
@@ -143,7 +144,7 @@ class sr_timing(ctypes.Structure):
                 ("n_words", ctypes.c_int32), ("n_rows_static", ctypes.c_int32), ("n_rows_threshold", ctypes.c_int32),
                 ("n_classes", ctypes.c_int32), ("bytes_uploaded", ctypes.c_uint64), ("enc_new_specs", ctypes.c_int32),
                 ("enc_static_rebuilt", ctypes.c_int32), ("enc_state_nodes", ctypes.c_int32),
-                ("prefix_batches", ctypes.c_int32)]
+                ("prefix_batches", ctypes.c_int32), ("enc_memo_pods", ctypes.c_int32)]
 
 
 def ptr(arr, typ):
@@ -232,6 +233,8 @@ def make_cluster_struct(A) -> sr_cluster:
             v.zone_keys[i] = int(A["vol_zone_keys"][i])
         c._volumes = v  # keeps the struct alive as long as the cluster struct
         c.volumes = ctypes.pointer(v)
+    if A.get("pod_stamp") is not None:
+        c.pod_stamp = ptr(A["pod_stamp"], ctypes.POINTER(ctypes.c_uint64))
     if A.get("pa_ns") is not None:
         pa = sr_pod_affinity()
         for f in ("ns", "label_off", "label_key", "label_val", "anti_off", "topology_key", "ns_off", "ns_ids",

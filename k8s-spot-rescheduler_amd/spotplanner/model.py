@@ -620,7 +620,8 @@ def _encode_volumes(nodes: List[Node], pods: List[Pod], world: VolumeWorld, it: 
 def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Interner] = None,
                    pod_node: Optional[List[int]] = None, scalar_tables: bool = True,
                    accounting: bool = True, spread_tables: bool = True,
-                   volumes: Optional[VolumeWorld] = None, volume_tables: bool = True) -> EncodedCluster:
+                   volumes: Optional[VolumeWorld] = None, volume_tables: bool = True,
+                   stamps: Optional[List[int]] = None) -> EncodedCluster:
     """Encode nodes and pods.  pod_node[i] is the node index of pods[i] (default:
     looked up by pod.node_name; -1 when unbound).  Pods of one node keep their
     relative order (= the per-node LIST order).  scalar_tables=False: no scalar
@@ -744,6 +745,8 @@ def encode_cluster(nodes: List[Node], pods: List[Pod], interner: Optional[Intern
         accs = [p.node_accounting() for p in pods]
         A.update(acc_cpu=_i64([a[0] for a in accs]), acc_mem=_i64([a[1] for a in accs]),
                  acc_eph=_i64([a[2] for a in accs]))
+    if stamps is not None:  # sr_cluster.pod_stamp (the shim: a hash of UID and ResourceVersion)
+        A["pod_stamp"] = np.ascontiguousarray(np.asarray(stamps, dtype=np.uint64).reshape(-1))
     A["n_nodes"] = len(nodes)
     A["n_pods"] = len(pods)
     A["id_empty"] = e

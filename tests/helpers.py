@@ -32,7 +32,7 @@ class Scenario:
     """Spot nodes (in NodeInfoArray order) with their pods, plus extra
     "query" pods (unbound), encoded as ONE cluster."""
 
-    def __init__(self, spot_nodes, spot_pods, query_pods, interner=None, volumes=None):
+    def __init__(self, spot_nodes, spot_pods, query_pods, interner=None, volumes=None, stamps=None):
         self.interner = interner or Interner()
         self.nodes = list(spot_nodes)
         self.spot_pods = [list(ps) for ps in spot_pods]
@@ -44,7 +44,7 @@ class Scenario:
         self.q0 = len(pods)
         pods.extend(self.query)
         pod_node.extend([-1] * len(self.query))
-        self.enc = encode_cluster(self.nodes, pods, self.interner, pod_node=pod_node, volumes=volumes)
+        self.enc = encode_cluster(self.nodes, pods, self.interner, pod_node=pod_node, volumes=volumes, stamps=stamps)
         self.spot = np.arange(len(self.nodes), dtype=np.int32)
         off = np.zeros(len(self.nodes) + 1, np.int32)
         for i, ps in enumerate(self.spot_pods):

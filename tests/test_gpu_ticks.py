@@ -241,3 +241,48 @@ def test_ticks_node_labels_and_taints_change(checker):
         lib.sr_snapshot_destroy(h)
         o = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=1)
         assert np.array_equal(p.status, o["status"]) and np.array_equal(p.node_of_pod, o["node_of_pod"])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_ticks_with_pod_stamps(checker, seed):
+    """sr_cluster.pod_stamp: the encoder keeps each stamped pod's spec id and candidate checks across calls.
+    Ticks alternate between two versions of the candidate pods (specs, requests and accounting of some pods
+    changed, with new stamps), then repeat a version with its old stamps; every tick equals the oracle, and a
+    stamped tick equals the same tick without stamps."""
+    import copy
+    import random
+    from spotplanner.model import Container
+    nodes, spot_pods, cands = rand_scenario(9900 + seed, n_spot=12 + seed, n_cand=8, max_pods=6)
+    r = random.Random(seed)
+    alt = copy.deepcopy(cands)
+    changed = []
+    for ci, c in enumerate(alt):
+        for pi, p in enumerate(c):
+            if r.random() < 0.3:
+                p.node_selector = {} if p.node_selector else {"zone": "z1"}
+                p.containers = [Container(cpu_milli=p.containers[0].cpu_milli + 150 if p.containers else 150)]
+                p.init_containers = [Container(cpu_milli=900)] if r.random() < 0.5 else []
+                changed.append((ci, pi))
+    n_spot_pods = sum(len(ps) for ps in spot_pods)
+
+    def stamps_of(version, flat_len):
+        base = [1000 + i for i in range(n_spot_pods)]
+        flat = [(ci, pi) for ci, c in enumerate(cands) for pi in range(len(c))]
+        return base + [(5000 if version and k in changed else 3000) + i for i, k in enumerate(flat)][:flat_len]
+
+    interner = Interner()  # one string dictionary per process (INTEGRATION.md): the stamps' contract
+    for version in (0, 1, 0, 1, 1, 0):
+        cs = alt if version else cands
+        flat = [p for c in cs for p in c]
+        for st in (stamps_of(version, len(flat)), None):
+            sc = Scenario(nodes, spot_pods, flat, interner=interner, stamps=st)
+            off = np.cumsum([0] + [len(c) for c in cs]).astype(np.int32)
+            cand_pods = np.arange(sc.q0, sc.q0 + len(flat), dtype=np.int32)
+            o = oracle_plan(sc.oracle_snapshot(), sc.ptr, off, cand_pods, mode=1)
+            h = sc.product_snapshot()
+            try:
+                p = plan_arrays(checker, h, sc.ptr, off, cand_pods)
+            finally:
+                capi.load_planner().sr_snapshot_destroy(h)
+            from test_gpu_parity import compare_plans
+            compare_plans(o, p, off, None)

@@ -69,7 +69,7 @@ int main(int argc, char** argv) {
     printf("encode failed: %s\n", err.c_str());
     return 1;
   }
-  printf("cold encode %.3f ms (new specs %d)\n", ms_since(t0), cache.last_new_specs);
+  printf("cold encode %.3f ms (new specs %d, memo hits %d)\n", ms_since(t0), cache.last_new_specs, cache.last_memo_hits);
   phases("cold");
   double best = 1e30;
   for (int r = 0; r < 20; ++r) {
@@ -94,8 +94,8 @@ int main(int argc, char** argv) {
     last_static = cache.last_static_changed;
     sr_snapshot_destroy(s2);
   }
-  printf("one-node-changed encode (fresh snapshot) best %.3f ms (state nodes %d, static rebuilt %d)\n", best,
-         last_state, last_static);
+  printf("one-node-changed encode (fresh snapshot) best %.3f ms (state nodes %d, static rebuilt %d, memo hits %d)\n",
+         best, last_state, last_static, cache.last_memo_hits);
   phases("1node");
   if (argc > 3 && std::string(argv[3]) == "check") {
     // the state view patched node by node equals the one rebuilt from scratch:
