@@ -836,11 +836,21 @@ __device__ __forceinline__ int32_t scale32(int64_t f, int k) {
 // bits (narrow candidates: S <= f equals S >> k <= f >> k for the multiples
 // S of 2^k the candidate's requests sum to): one compare and one select per
 // field instead of 64-bit pairs.
+// SR_K2_OSET: the bits each pod sets come from its lane (`ps`) instead of
+// being recomputed from the conflict bits on the scalar unit every step;
+// SR_K2_OPRED: with state bits the update is predicated like the branch-free
+// step instead of sitting behind a branch.
+#ifndef SR_K2_OSET
+#define SR_K2_OSET 0
+#endif
+#ifndef SR_K2_OPRED
+#define SR_K2_OPRED 0
+#endif
 template <bool E, bool O>
 __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int W, int lane, uint32_t nc, uint32_t nm,
-                                                   uint32_t ne, uint64_t pm, uint64_t cur, uint64_t swap_mask,
-                                                   int32_t& c32, int32_t& m32, int32_t& e32, uint64_t& nport,
-                                                   int& nleft, int& node) {
+                                                   uint32_t ne, uint64_t pm, uint64_t ps, uint64_t cur,
+                                                   uint64_t swap_mask, int32_t& c32, int32_t& m32, int32_t& e32,
+                                                   uint64_t& nport, int& nleft, int& node) {
   // The zero-request exemption and the fixed ephemeral gate are in the
   // values, not in the step: an all-zero request is INT_MIN in nc / nm / ne
   // (it meets every state value), and without E a lane whose ephemeral free
@@ -860,6 +870,18 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
     if (E) fit &= ballot(e32 >= e);
     if (O) fit &= ballot((nport & q) == 0);
     const int32_t cu = max(c, 0), mu = max(m, 0), eu = max(e, 0);
+    if (O && SR_K2_OPRED) {
+      const uint64_t set = SR_K2_OSET ? readlane64(ps, k) : swap_pairs(q, swap_mask);
+      const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
+      const bool hit = lane == j;
+      c32 -= hit ? cu : 0;
+      m32 -= hit ? mu : 0;
+      if (E) e32 -= hit ? eu : 0;
+      nleft -= hit ? 1 : 0;
+      nport |= hit ? set : 0ull;
+      jv = lane == k ? j : jv;
+      continue;
+    }
     if (O) {  // as in place_window
       if (fit != 0) {
         const int j = __builtin_ctzll(fit);
@@ -868,7 +890,7 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
           m32 -= mu;
           if (E) e32 -= eu;
           nleft -= 1;
-          nport |= swap_pairs(q, swap_mask);
+          nport |= SR_K2_OSET ? readlane64(ps, k) : swap_pairs(q, swap_mask);
         }
         jv = lane == k ? j : jv;
       }
@@ -900,7 +922,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   const int Wp = w.Wp;
   const uint64_t* __restrict__ tab = w.S;
   int64_t rc[G], rm[G], re[G];
-  uint64_t pm[G], r01[G], r23[G], fmask[G], act[G];
+  uint64_t pm[G], ps[G], r01[G], r23[G], fmask[G], act[G];
   int fbase[G];  // first word of the 64-word chunk fmask describes (rows wider than 64 words)
   bool unres[G]; // the pointer is a chunk boundary not yet scanned (kFar: the end of the head)
   uint64_t cur[G];  // F word holding the pod's pointer: moves inside a word need no LDS read
@@ -915,6 +937,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     rm[g] = static_cast<int64_t>(pr[1]);
     re[g] = static_cast<int64_t>(pr[2]);
     pm[g] = swap_pairs(pr[3], w.swap_mask);  // the state bits the pod conflicts with
+    ps[g] = SR_K2_OSET ? pr[3] : 0ull;        // ... and those it sets
     r01[g] = pr[4];
     r23[g] = pr[5];
     zero[g] = (rc[g] | rm[g] | re[g]) == 0;  // fitsRequest skips the resource checks
@@ -1265,8 +1288,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   place_window<e_, o_>(todo, kmax, W, lane, rc[g], rm[g], re[g], pm[g], cur[g], zm[g], w.swap_mask, emask, ncpu, \
                        nmem, neph, nport, nleft, node[g])
 #define SR_PW32(e_, o_)                                                                                           \
-  place_window32<e_, o_>(todo, kmax, W, lane, nc[g], nm[g], ne[g], pm[g], cur[g], w.swap_mask, c32, m32, e32, nport, \
-                         nleft, node[g])
+  place_window32<e_, o_>(todo, kmax, W, lane, nc[g], nm[g], ne[g], pm[g], ps[g], cur[g], w.swap_mask, c32, m32, e32, \
+                         nport, nleft, node[g])
           if (narrow)
             placed = E ? (O ? SR_PW32(true, true) : SR_PW32(true, false))
                        : (O ? SR_PW32(false, true) : SR_PW32(false, false));
@@ -1844,7 +1867,7 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wave);
+  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * (blockDim.x >> 6)) + wave);
   if (li >= n_list) return;
   const K2Entry x = k2_entry<PROF>(list, li);
   const int ci = x.ci, p0 = x.p0, np = x.np;
@@ -1891,7 +1914,7 @@ template <int GMAX, bool PROF>
 __global__ __launch_bounds__(256) void k2_node(DevWorkload w, const int4* __restrict__ list, int n_list) {
   extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
   const int wave = threadIdx.x >> 6;
-  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wave);
+  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * (blockDim.x >> 6)) + wave);
   if (li >= n_list) return;
   const K2Entry x = k2_entry<PROF>(list, li);
   uint64_t* F = k2_lds + static_cast<size_t>(wave) * (64 * GMAX * kNHS + (w.s_head_only ? 64 * GMAX * 4 : 0));
@@ -1930,8 +1953,9 @@ hipError_t launch_k2_place_ch(const DevWorkload& w, hipStream_t s, hipEvent_t ev
 template <bool PROF>
 hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
-  const dim3 grid((n + 3) / 4), block(256);
-  const size_t lds = 4 * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
+  const int wpb = w.k2_wpb == 1 || w.k2_wpb == 2 ? w.k2_wpb : 4;  // waves per block
+  const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
+  const size_t lds = wpb * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
   if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   else if (G == 2) launch(k2_node<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   else launch(k2_node<4, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
@@ -1945,8 +1969,9 @@ template hipError_t launch_k2_node_g<true>(const DevWorkload&, int, hipStream_t,
 template <int CH, bool PROF>
 hipError_t launch_k2_place_ch(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
-  const dim3 grid((n + 3) / 4), block(256);
-  launch(k2_place<CH, PROF>, grid, block, 4 * sizeof(K2Lds), s, ev0, ev1, w, w.list, n);
+  const int wpb = w.k2_wpb == 1 || w.k2_wpb == 2 ? w.k2_wpb : 4;  // waves per block
+  const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
+  launch(k2_place<CH, PROF>, grid, block, wpb * sizeof(K2Lds), s, ev0, ev1, w, w.list, n);
   return hipGetLastError();
 }
 #define SR_PLACE_INST(CH)                                                                                      \
