@@ -836,20 +836,14 @@ __device__ __forceinline__ int32_t scale32(int64_t f, int k) {
 // bits (narrow candidates: S <= f equals S >> k <= f >> k for the multiples
 // S of 2^k the candidate's requests sum to): one compare and one select per
 // field instead of 64-bit pairs.
-// SR_K2_OSET: the bits each pod sets come from its lane (`ps`) instead of
-// being recomputed from the conflict bits on the scalar unit every step;
-// SR_K2_OPRED: with state bits the update is predicated like the branch-free
-// step instead of sitting behind a branch.
-#ifndef SR_K2_OSET
-#define SR_K2_OSET 0
-#endif
-#ifndef SR_K2_OPRED
-#define SR_K2_OPRED 0
-#endif
+// The bits a placed pod sets come from its lane (`ps`, read with the pod's
+// request) rather than being recomputed from its conflict bits on the scalar
+// unit every step (A/B on MI355X, r04: K2 -1.5% on C5, equal on C3; the
+// predicated, branch-free form of the update measured 3% slower).
 template <bool E, bool O>
 __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int W, int lane, uint32_t nc, uint32_t nm,
                                                    uint32_t ne, uint64_t pm, uint64_t ps, uint64_t cur,
-                                                   uint64_t swap_mask, int32_t& c32, int32_t& m32, int32_t& e32,
+                                                   int32_t& c32, int32_t& m32, int32_t& e32,
                                                    uint64_t& nport, int& nleft, int& node) {
   // The zero-request exemption and the fixed ephemeral gate are in the
   // values, not in the step: an all-zero request is INT_MIN in nc / nm / ne
@@ -870,18 +864,6 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
     if (E) fit &= ballot(e32 >= e);
     if (O) fit &= ballot((nport & q) == 0);
     const int32_t cu = max(c, 0), mu = max(m, 0), eu = max(e, 0);
-    if (O && SR_K2_OPRED) {
-      const uint64_t set = SR_K2_OSET ? readlane64(ps, k) : swap_pairs(q, swap_mask);
-      const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
-      const bool hit = lane == j;
-      c32 -= hit ? cu : 0;
-      m32 -= hit ? mu : 0;
-      if (E) e32 -= hit ? eu : 0;
-      nleft -= hit ? 1 : 0;
-      nport |= hit ? set : 0ull;
-      jv = lane == k ? j : jv;
-      continue;
-    }
     if (O) {  // as in place_window
       if (fit != 0) {
         const int j = __builtin_ctzll(fit);
@@ -890,7 +872,7 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
           m32 -= mu;
           if (E) e32 -= eu;
           nleft -= 1;
-          nport |= SR_K2_OSET ? readlane64(ps, k) : swap_pairs(q, swap_mask);
+          nport |= readlane64(ps, k);
         }
         jv = lane == k ? j : jv;
       }
@@ -937,7 +919,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     rm[g] = static_cast<int64_t>(pr[1]);
     re[g] = static_cast<int64_t>(pr[2]);
     pm[g] = swap_pairs(pr[3], w.swap_mask);  // the state bits the pod conflicts with
-    ps[g] = SR_K2_OSET ? pr[3] : 0ull;        // ... and those it sets
+    ps[g] = pr[3];                            // ... and those it sets
     r01[g] = pr[4];
     r23[g] = pr[5];
     zero[g] = (rc[g] | rm[g] | re[g]) == 0;  // fitsRequest skips the resource checks
@@ -1288,7 +1270,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   place_window<e_, o_>(todo, kmax, W, lane, rc[g], rm[g], re[g], pm[g], cur[g], zm[g], w.swap_mask, emask, ncpu, \
                        nmem, neph, nport, nleft, node[g])
 #define SR_PW32(e_, o_)                                                                                           \
-  place_window32<e_, o_>(todo, kmax, W, lane, nc[g], nm[g], ne[g], pm[g], ps[g], cur[g], w.swap_mask, c32, m32, e32, \
+  place_window32<e_, o_>(todo, kmax, W, lane, nc[g], nm[g], ne[g], pm[g], ps[g], cur[g], c32, m32, e32, \
                          nport, nleft, node[g])
           if (narrow)
             placed = E ? (O ? SR_PW32(true, true) : SR_PW32(true, false))

@@ -80,9 +80,9 @@ def test_gpu_domain_path_up_to_512_pods(checker):
     takes the fallback path.  The oracle plans every one of them."""
     from domain_cases import pod, term
     from test_gpu_parity import run_scenario
-    sizes = [512, 300, 257, 256, 64, 63]
+    sizes = [511, 299, 256, 255, 64, 63]  # web pods; each candidate adds one db pod
     big = [[pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(n)] + [pod("d", "db")] for n in sizes]
-    big.append([pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(512)] + [pod("d", "db")])
+    big.append([pod("w%d" % i, "web", anti=[term("zone", "db")]) for i in range(512)] + [pod("d", "db")])  # 513
     _, o, p = run_scenario(checker, nodes(), [[] for _ in range(4)], big, extra_fallback=lambda c: c == len(sizes))
     assert [int(x) for x in p.status[:len(sizes)]] == [int(x) for x in o["status"][:len(sizes)]]
     assert all(int(x) != capi.SR_CAND_FALLBACK for x in p.status[:len(sizes)])
