@@ -454,7 +454,7 @@ def main():
         return {"median_ms": round(float(np.median(xs)), 4), "min_ms": round(float(np.min(xs)), 4)}
 
     ref_t, ref_batches, ref_enc, ref_state, ref_up, ref_upl = [], [], [], [], [], []
-    all_t, all_enc, all_upl, all_state = [], [], [], []
+    all_t, all_enc, all_upl, all_state, all_reused, all_patches, all_bytes = [], [], [], [], [], [], []
     wmap2 = np.zeros_like(wmap)
     for r in range(args.e2e_reps + 2):  # two untimed ticks first: the planner's view of the pool settles
         h = fresh_snapshot(r)
@@ -492,6 +492,9 @@ def main():
             all_enc.append(tq.ms_pack_host)
             all_upl.append(tq.ms_upload)
             all_state.append(tq.enc_state_nodes)
+            all_reused.append(tq.enc_reused)
+            all_patches.append(tq.enc_pod_patches)
+            all_bytes.append(tq.bytes_uploaded)
         assert fo.first_ok == out.first_ok or world > 1
         lib.sr_snapshot_destroy(h)
     # The whole housekeeping tick from the cluster arrays: NewNodeMap (A1-A5),
@@ -538,6 +541,8 @@ def main():
             "all_candidates": dict(summary(all_t), **{
                 "encode_ms": round(float(np.median(all_enc)), 3), "upload_ms": round(float(np.median(all_upl)), 3),
                 "state_nodes_reencoded": int(np.median(all_state)),
+                "candidate_side_reused": "%d of %d ticks" % (int(np.sum(all_reused)), len(all_reused)),
+                "pod_patches_median": int(np.median(all_patches)), "upload_bytes": int(np.median(all_bytes)),
                 "span": "sr_plan_prepare + sr_plan_run over every candidate, same fresh one-node-changed snapshots"}),
             "pods_for_deletion_ms": round(pfd_ms, 3), "reps": len(ref_t), "host_threads": host_threads(),
             "full_tick_median_ms": round(float(np.median(full_tick)), 3) if full_tick else None,

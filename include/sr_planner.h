@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SR_ABI_VERSION 5
+#define SR_ABI_VERSION 6
 
 /* ------------------------------------------------------------------ status */
 typedef int32_t sr_status;
@@ -316,7 +316,11 @@ typedef struct {
    * what it derived from a pod's spec keyed by (pod index, stamp) across calls
    * and re-derives it only for pods whose stamp changed, so the string ids a
    * stamped pod's spec uses must stay the same across calls (one interner per
-   * process).  NULL: no stamps (every call re-reads every pod's spec).  ABI 5. */
+   * process).  A stamp also covers what the pod's spec resolves through (its
+   * PVCs' bound PVs).  With every candidate pod stamped, a call whose
+   * candidate input (cand_pod_off, cand_pods, cand_global, stamps) equals the
+   * previous call's keeps that call's candidate side (sr_timing.enc_reused).
+   * NULL: no stamps (every call re-reads every pod's spec).  ABI 5. */
   const uint64_t *pod_stamp;
 } sr_cluster;
 #define SR_STR_LABEL_VALUE 1u
@@ -472,7 +476,8 @@ const char *sr_build_info(void);
  * and spread): a binding compares this with the SR_ABI_VERSION it was built
  * against before its first call and refuses to run on a mismatch, since the
  * library would otherwise read fields past the end of a shorter struct (ABI 5
- * added sr_cluster.volumes). */
+ * added sr_cluster.volumes and pod_stamp; ABI 6 the sr_timing enc_reused /
+ * enc_pod_patches counters, which sr_get_timing writes). */
 int32_t     sr_abi_version(void);
 
 /* Batched findSpotNodeForPod (rescheduler.go:338-353): for each pod, the first
@@ -572,6 +577,9 @@ typedef struct {
   int32_t  enc_state_nodes;    /* spot nodes whose capacity state the last prepare re-encoded */
   int32_t  prefix_batches;     /* batches the last sr_plan_first ran */
   int32_t  enc_memo_pods;      /* candidate pods the last prepare found in its per-pod memo (sr_cluster.pod_stamp) */
+  int32_t  enc_reused;         /* 1: the last prepare kept the candidate side of the call before (same stamped
+                                * candidate input; ABI 6), updating only capacity-dependent rows and records */
+  int32_t  enc_pod_patches;    /* ... and re-pointed this many pod records (uploaded as patches) */
 } sr_timing;
 /* mask: which kernels sr_plan_run brackets with HIP events (resets the sums):
  * 1 = K0, 2 = K2, 4 = collective (multi-GPU) + K3; 0 = no events.  Events are read back lazily, by

@@ -944,9 +944,264 @@ uint64_t node_state_fp(const SpotNode& sn, const NodeState& st) {
   return mix(h, ports);
 }
 
+namespace {
+
+// A class whose S row is certainly empty: it ANDs an empty atom, ANDs the
+// complement of a full one, or each of its ORed terms holds an empty atom.
+bool class_empty(const Workload& w, int32_t k, const uint8_t* atom_empty, const uint8_t* atom_full) {
+  bool empty = false, has_terms = false, all_terms_empty = true, term_empty = false;
+  for (int32_t o = w.cls_prog_off[k]; o < w.cls_prog_off[k + 1]; ++o) {
+    const int32_t atom = w.cls_prog[o] >> 2, kind = w.cls_prog[o] & 3;
+    if (kind == PROG_AND) {
+      empty = empty || atom_empty[atom];
+    } else if (kind == PROG_ANDNOT) {
+      empty = empty || atom_full[atom];
+    } else {
+      if (kind == PROG_TERM_START) {
+        if (has_terms) all_terms_empty = all_terms_empty && term_empty;
+        has_terms = true;
+        term_empty = false;
+      }
+      term_empty = term_empty || atom_empty[atom];
+    }
+  }
+  if (has_terms) all_terms_empty = all_terms_empty && term_empty;
+  return empty || (has_terms && all_terms_empty);
+}
+
+// Composite atom rows: the pod-count atom AND NOT (any taint of the set).
+void composite_rows(const EncoderCache& C, const std::vector<int32_t>& comp_sets, int32_t a_comp, int32_t Wp,
+                    uint64_t* A) {
+  for (size_t k = 0; k < comp_sets.size(); ++k) {
+    uint64_t* row = A + static_cast<size_t>(a_comp + static_cast<int32_t>(k)) * Wp;
+    const int32_t* u = C.untol_dict.data(comp_sets[k]);
+    const size_t nu = C.untol_dict.len(comp_sets[k]);
+    for (int32_t i = 0; i < Wp; ++i) {
+      uint64_t any = 0;
+      for (size_t j = 0; j < nu; ++j) any |= C.taint_rows[static_cast<size_t>(u[j]) * Wp + i];
+      row[i] = A[i] & ~any;
+    }
+  }
+}
+
+void atom_flags(const uint64_t* row, int32_t Wp, int32_t n_spot, uint8_t* empty, uint8_t* full) {
+  int64_t pop = 0;
+  for (int32_t i = 0; i < Wp; ++i) pop += __builtin_popcountll(row[i]);
+  *empty = pop == 0;
+  *full = pop == n_spot;
+}
+
+// The call's candidate input equals the one CandReuse saved, every pod stamped.
+bool same_cand_input(const CandReuse& R, const sr_candidates* cands, const uint64_t* stamps) {
+  const int32_t nc = cands->n_cand;
+  if (!R.have_input || !stamps || static_cast<size_t>(nc) + 1 != R.pod_off.size() ||
+      (cands->cand_global != nullptr) != !R.glob.empty())
+    return false;
+  if (std::memcmp(cands->cand_pod_off, R.pod_off.data(), sizeof(int32_t) * (static_cast<size_t>(nc) + 1)) != 0)
+    return false;
+  if (cands->cand_global && std::memcmp(cands->cand_global, R.glob.data(), sizeof(int32_t) * nc) != 0) return false;
+  const int32_t b = cands->cand_pod_off[0];
+  const size_t n = R.pods.size();
+  std::atomic<bool> same{true};
+  auto cmp = [&](size_t lo, size_t hi) {
+    bool ok = std::memcmp(cands->cand_pods + b + lo, R.pods.data() + lo, sizeof(int32_t) * (hi - lo)) == 0;
+    for (size_t j = lo; j < hi && ok; ++j) {
+      if (j + 32 < hi) __builtin_prefetch(stamps + R.pods[j + 32]);  // scattered reads: keep many in flight
+      ok = stamps[R.pods[j]] != 0 && stamps[R.pods[j]] == R.stamps[j];
+    }
+    if (!ok) same.store(false, std::memory_order_relaxed);
+  };
+  if (n > (size_t(1) << 18)) parallel_for(n, 65536, cmp);  // a sequential pass is ~0.1 ns per byte compared
+  else cmp(0, n);
+  return same.load(std::memory_order_relaxed);
+}
+
+void save_cand_input(CandReuse& R, const sr_candidates* cands, const uint64_t* stamps, int32_t n_pods) {
+  R.drop();
+  const int32_t nc = cands->n_cand;
+  const int32_t b = nc > 0 ? cands->cand_pod_off[0] : 0, e = nc > 0 ? cands->cand_pod_off[nc] : 0;
+  for (int32_t j = b; j < e; ++j)
+    if (cands->cand_pods[j] < 0 || cands->cand_pods[j] >= n_pods || stamps[cands->cand_pods[j]] == 0) return;
+  R.pod_off.assign(cands->cand_pod_off, cands->cand_pod_off + nc + 1);
+  if (nc == 0) R.pod_off.assign(1, 0);
+  R.glob.assign(cands->cand_global ? cands->cand_global : nullptr, cands->cand_global ? cands->cand_global + nc : nullptr);
+  R.pods.assign(cands->cand_pods + b, cands->cand_pods + e);
+  R.stamps.resize(R.pods.size());
+  for (size_t j = 0; j < R.pods.size(); ++j) R.stamps[j] = stamps[R.pods[j]];
+  R.have_input = true;
+}
+
+// The candidate-side reuse encode (CandReuse): the Workload of
+// the last call, its state-dependent parts brought up to the current state
+// view.  False when a dimension ran out of spare T rows (the caller encodes in
+// full; the index is rebuilt).
+bool reuse_encode(EncoderCache& C, Workload* w) {
+  CandReuse& R = w->reuse;
+  const int32_t Wp = w->Wp, n_spot = w->n_spot;
+  uint64_t* A = w->atoms.data();
+  // pod count and the composites built on it, in the words where it changed
+  std::vector<int32_t> words;
+  for (int32_t i = 0; i < Wp; ++i)
+    if (A[i] != C.podcount_row[i]) words.push_back(i);
+  for (int32_t i : words) {
+    A[i] = C.podcount_row[i];
+    for (size_t k = 0; k < R.comp_sets.size(); ++k) {
+      const int32_t* u = C.untol_dict.data(R.comp_sets[k]);
+      const size_t nu = C.untol_dict.len(R.comp_sets[k]);
+      uint64_t any = 0;
+      for (size_t j = 0; j < nu; ++j) any |= C.taint_rows[static_cast<size_t>(u[j]) * Wp + i];
+      A[static_cast<size_t>(R.a_comp + static_cast<int32_t>(k)) * Wp + i] = A[i] & ~any;
+    }
+  }
+  bool flags_moved = false;
+  auto refresh_flags = [&](int32_t a) {
+    uint8_t e = 0, f = 0;
+    atom_flags(A + static_cast<size_t>(a) * Wp, Wp, n_spot, &e, &f);
+    flags_moved = flags_moved || e != R.atom_empty[a] || f != R.atom_full[a];
+    R.atom_empty[a] = e;
+    R.atom_full[a] = f;
+  };
+  if (!words.empty()) {
+    refresh_flags(0);
+    for (size_t k = 0; k < R.comp_sets.size(); ++k) refresh_flags(R.a_comp + static_cast<int32_t>(k));
+  }
+  std::vector<int32_t> flipped;  // classes whose certain emptiness changed
+  if (flags_moved)
+    for (int32_t k = 0; k < static_cast<int32_t>(R.cls_empty.size()); ++k) {
+      const uint8_t e = class_empty(*w, k, R.atom_empty.data(), R.atom_full.data()) ? 1 : 0;
+      if (e != R.cls_empty[k]) {
+        R.cls_empty[k] = e;
+        flipped.push_back(k);
+      }
+    }
+  // thresholds: a distinct request whose smallest node value >= it moved
+  constexpr int64_t kNever = INT64_MAX;
+  // Only requests in the interval (previous value, value] of a node value
+  // that appeared or disappeared since the last update can move: the two
+  // sorted value lists are merged, and each such interval's requests found
+  // by binary search.
+  std::vector<std::pair<int32_t, int64_t>> moved[3];  // (distinct request, new threshold)
+  std::vector<int32_t> cand_u;
+  for (int d = 0; d < 3; ++d) {
+    const std::vector<int64_t>& v = C.node_vals[d];
+    const std::vector<int64_t>& old = R.vals[d];
+    const std::vector<int64_t>& dr = R.dreq[d];
+    cand_u.clear();
+    auto interval = [&](int64_t lo, int64_t hi) {  // requests in (lo, hi]
+      const size_t a = static_cast<size_t>(std::upper_bound(dr.begin(), dr.end(), lo) - dr.begin());
+      const size_t b = static_cast<size_t>(std::upper_bound(dr.begin(), dr.end(), hi) - dr.begin());
+      for (size_t u = a; u < b; ++u) cand_u.push_back(static_cast<int32_t>(u));
+    };
+    size_t i = 0, j = 0;
+    while (i < old.size() || j < v.size()) {
+      if (j == v.size() || (i < old.size() && old[i] < v[j])) {  // gone
+        interval(i == 0 ? INT64_MIN : old[i - 1], old[i]);
+        ++i;
+      } else if (i == old.size() || v[j] < old[i]) {  // new
+        interval(j == 0 ? INT64_MIN : v[j - 1], v[j]);
+        ++j;
+      } else {
+        ++i;
+        ++j;
+      }
+    }
+    std::sort(cand_u.begin(), cand_u.end());
+    cand_u.erase(std::unique(cand_u.begin(), cand_u.end()), cand_u.end());
+    for (int32_t u : cand_u) {
+      const size_t pos = static_cast<size_t>(std::lower_bound(v.begin(), v.end(), dr[u]) - v.begin());
+      const int64_t thr = pos == v.size() ? kNever : v[pos];
+      if (thr != R.dthr[d][u]) moved[d].emplace_back(u, thr);
+    }
+    R.vals[d] = v;
+  }
+  for (int d = 0; d < 3; ++d)  // rows left without requests become spare ...
+    for (const auto& m : moved[d]) {
+      const int32_t row = R.drow[d][m.first];
+      if (--R.row_refs[row] == 0) {
+        R.row_of[d].erase(R.dthr[d][m.first]);
+        w->t_thr[row] = kTSpare;
+        R.spare[d].push_back(row);
+      }
+    }
+  for (int d = 0; d < 3; ++d)  // ... before the new thresholds take rows
+    for (const auto& m : moved[d]) {
+      int32_t row;
+      auto it = R.row_of[d].find(m.second);
+      if (it != R.row_of[d].end()) {
+        row = it->second;
+      } else {
+        if (R.spare[d].empty()) {
+          R.indexed = false;
+          return false;
+        }
+        row = R.spare[d].back();
+        R.spare[d].pop_back();
+        R.row_of[d].emplace(m.second, row);
+        w->t_thr[row] = m.second;
+        R.row_refs[row] = 0;
+      }
+      ++R.row_refs[row];
+      R.drow[d][m.first] = row;
+      R.dthr[d][m.first] = m.second;
+    }
+  // the records of the pods asking within a moved interval or of a flipped class
+  if (++R.epoch == 0) {
+    std::fill(R.mark.begin(), R.mark.end(), 0u);
+    R.epoch = 1;
+  }
+  w->pod_patch.clear();
+  const uint64_t Wp64 = static_cast<uint64_t>(Wp);
+  auto off = [&](int32_t table_row) { return static_cast<uint64_t>(table_row) * Wp64; };
+  auto repoint = [&](int32_t q) {
+    if (R.mark[q] == R.epoch) return;
+    R.mark[q] = R.epoch;
+    const int32_t* ri = &R.pod_ri[static_cast<size_t>(q) * 3];
+    const bool zero = ri[0] < 0;
+    int32_t cls = R.pod_cls[q], row[3] = {0, 0, 0};
+    bool dead = R.cls_empty[cls] != 0;
+    if (!zero)
+      for (int d = 0; d < 3; ++d) {
+        row[d] = R.drow[d][ri[d]];
+        dead = dead || R.dthr[d][ri[d]] == kNever;
+      }
+    if (dead) cls = w->empty_class;
+    int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
+    r[0] = cls;
+    for (int d = 0; d < 3; ++d) r[1 + d] = row[d];
+    uint64_t* rec = &w->pod_rec[static_cast<size_t>(q) * 6];
+    const uint64_t r4 = off(cls) | off(w->n_classes + row[0]) << 32;
+    const uint64_t r5 = off(w->n_classes + row[1]) | off(w->n_classes + row[2]) << 32;
+    if (rec[4] == r4 && rec[5] == r5) return;
+    rec[4] = r4;
+    rec[5] = r5;
+    w->pod_patch.insert(w->pod_patch.end(), {static_cast<uint64_t>(q), r4, r5});
+  };
+  for (int d = 0; d < 3; ++d)
+    for (const auto& m : moved[d])
+      for (int32_t i = R.dpod_off[d][m.first]; i < R.dpod_off[d][m.first + 1]; ++i) repoint(R.dpod[d][i]);
+  for (int32_t k : flipped)
+    for (int32_t i = R.cls_pod_off[k]; i < R.cls_pod_off[k + 1]; ++i) repoint(R.cls_pod[i]);
+  w->reused = true;
+  return true;
+}
+
+}  // namespace
+
+namespace {
+sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
+                      Workload* w, std::string* err);
+}  // namespace
+
 sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr_cluster* c,
                           const sr_candidates* cands, Workload* w, std::string* err) {
-  EncoderCache& C = *cache;
+  const sr_status st = encode_impl(*cache, snap, c, cands, w, err);
+  if (st != SR_OK) w->reuse.drop();  // the Workload no longer holds the input it saved
+  return st;
+}
+
+namespace {
+sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
+                      Workload* w, std::string* err) {
   const sr_pods& P = c->pods;
   const int32_t nc = cands->n_cand;
   auto t_last = std::chrono::steady_clock::now();
@@ -956,10 +1211,6 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     t_last = now;
   };
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
-  w->reset();
-  w->n_input_cand = nc;
-  w->pod_base = nc > 0 ? cands->cand_pod_off[0] : 0;
-  w->n_input_pods = nc > 0 ? cands->cand_pod_off[nc] - w->pod_base : 0;
   if (!snap->nodes.empty() &&
       (c->id_empty != snap->id_empty || c->id_metadata_name != snap->id_metadata_name ||
        c->id_unschedulable_key != snap->id_unschedulable_key)) {
@@ -988,13 +1239,9 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     *err = "too many spot nodes for one device plan";
     return SR_ERR_CAPACITY;
   }
-  w->n_spot = n_spot;
-  w->Wp = Wp;
-  w->n_pad = Wp * 64;
   refresh_static(C, snap, Wp);
   sr_status st = refresh_state(C, snap, err);
   if (st != SR_OK) return st;
-  w->state_gen = C.state_gen;
   phase(0);
 
   // ---- per-pod memo (sr_cluster.pod_stamp): valid for the cluster's table
@@ -1011,6 +1258,47 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     if (C.pod_memo.size() < static_cast<size_t>(P.n)) C.pod_memo.resize(static_cast<size_t>(P.n));
   }
   std::atomic<int32_t> memo_hits{0};
+
+  // ---- candidate-side reuse (CandReuse): the same stamped
+  // candidate input as the last call
+  CandReuse& R = w->reuse;
+  const bool same_input = stamps && R.shape == C.memo_shape && same_cand_input(R, cands, stamps);
+  if (same_input && R.indexed && R.content_gen == C.content_gen && R.static_gen == C.static_gen && R.n_spot == n_spot && R.Wp == Wp &&
+      snap->anti_total == 0 && snap->opaque_total == 0) {
+    w->state_gen = C.state_gen;
+    if (reuse_encode(C, w)) {
+      C.last_new_specs = 0;
+      C.last_memo_hits = w->n_input_pods;
+      C.last_reused = 1;
+      C.last_pod_patches = static_cast<int32_t>(w->pod_patch.size() / kPodPatchWords);
+      for (int i = 1; i < 16; ++i) encode_phase_ms[i] = 0;
+      phase(11);
+      return SR_OK;
+    }
+  }
+  C.last_reused = 0;
+  C.last_pod_patches = 0;
+  R.indexed = false;
+  if (!same_input) {
+    if (stamps) {
+      save_cand_input(R, cands, stamps, P.n);
+      R.shape = C.memo_shape;
+    } else {
+      R.drop();
+    }
+  }
+  // the second consecutive encode of one input builds the index (below,
+  // when the candidate side turns out to read no other snapshot state)
+  const bool want_index = same_input;
+  w->reset();
+  w->cand_gen = C.cand_gen_next++;
+  w->n_input_cand = nc;
+  w->pod_base = nc > 0 ? cands->cand_pod_off[0] : 0;
+  w->n_input_pods = nc > 0 ? cands->cand_pod_off[nc] - w->pod_base : 0;
+  w->n_spot = n_spot;
+  w->Wp = Wp;
+  w->n_pad = Wp * 64;
+  w->state_gen = C.state_gen;
 
   // ---- pass 1: candidate-level fallback (host-decided)
   w->status_host.assign(static_cast<size_t>(nc), STATUS_PENDING);
@@ -2081,16 +2369,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     std::copy_n(&aff.sat[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_AFF + 2 * t) * Wp);
     std::copy_n(&aff.keys[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_AFF + 2 * t + 1) * Wp);
   }
-  for (size_t k = 0; k < comp_sets.size(); ++k) {  // atom 0 AND NOT (any taint of the set)
-    uint64_t* row = A + static_cast<size_t>(A_COMP + static_cast<int32_t>(k)) * Wp;
-    const int32_t* u = C.untol_dict.data(comp_sets[k]);
-    const size_t nu = C.untol_dict.len(comp_sets[k]);
-    for (int32_t i = 0; i < Wp; ++i) {
-      uint64_t any = 0;
-      for (size_t j = 0; j < nu; ++j) any |= C.taint_rows[static_cast<size_t>(u[j]) * Wp + i];
-      row[i] = A[i] & ~any;
-    }
-  }
+  composite_rows(C, comp_sets, A_COMP, Wp, A);  // atom 0 AND NOT (any taint of the set)
   for (size_t k = 0; k < dk.key.size(); ++k)
     if (!dk.node_local[k])
       for (int32_t n = 0; n < n_spot; ++n)
@@ -2235,36 +2514,10 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
   // value in some dimension (the never-row).  Sound, not complete: the rest
   // is found exactly on the device.
   std::vector<uint8_t> cls_empty(static_cast<size_t>(w->n_classes), 0);
-  {
-    std::vector<uint8_t> atom_empty(static_cast<size_t>(w->n_atoms)), atom_full(static_cast<size_t>(w->n_atoms));
-    for (int32_t a = 0; a < w->n_atoms; ++a) {
-      const uint64_t* row = A + static_cast<size_t>(a) * Wp;
-      int64_t pop = 0;
-      for (int32_t i = 0; i < Wp; ++i) pop += __builtin_popcountll(row[i]);
-      atom_empty[a] = pop == 0;
-      atom_full[a] = pop == n_spot;
-    }
-    for (int32_t k = 0; k < w->n_classes; ++k) {
-      bool empty = false, has_terms = false, all_terms_empty = true, term_empty = false;
-      for (int32_t o = w->cls_prog_off[k]; o < w->cls_prog_off[k + 1]; ++o) {
-        const int32_t atom = w->cls_prog[o] >> 2, kind = w->cls_prog[o] & 3;
-        if (kind == PROG_AND) {
-          empty = empty || atom_empty[atom];
-        } else if (kind == PROG_ANDNOT) {
-          empty = empty || atom_full[atom];
-        } else {
-          if (kind == PROG_TERM_START) {
-            if (has_terms) all_terms_empty = all_terms_empty && term_empty;
-            has_terms = true;
-            term_empty = false;
-          }
-          term_empty = term_empty || atom_empty[atom];
-        }
-      }
-      if (has_terms) all_terms_empty = all_terms_empty && term_empty;
-      cls_empty[k] = empty || (has_terms && all_terms_empty);
-    }
-  }
+  std::vector<uint8_t> atom_empty(static_cast<size_t>(w->n_atoms)), atom_full(static_cast<size_t>(w->n_atoms));
+  for (int32_t a = 0; a < w->n_atoms; ++a)
+    atom_flags(A + static_cast<size_t>(a) * Wp, Wp, n_spot, &atom_empty[a], &atom_full[a]);
+  for (int32_t k = 0; k < w->n_classes; ++k) cls_empty[k] = class_empty(*w, k, atom_empty.data(), atom_full.data());
   phase(8);
   std::vector<uint8_t> used[3];  // lower-bound positions some pod asks for, per dimension
   for (int d = 0; d < 3; ++d) used[d].assign(C.node_vals[d].size() + 1, 0);
@@ -2307,7 +2560,7 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     if (chunk_dead) any_dead.store(true, std::memory_order_relaxed);
   });
   phase(10);
-  if (any_dead.load(std::memory_order_relaxed)) {
+  if (any_dead.load(std::memory_order_relaxed) || want_index) {  // (a reuse encode may need it later)
     emit(0, PROG_AND);
     emit(0, PROG_ANDNOT);
     w->cls_prog_off.push_back(static_cast<int32_t>(w->cls_prog.size()));
@@ -2333,6 +2586,16 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
       } else {
         std::sort(used_list[d].begin(), used_list[d].end());
         for (int32_t pos : used_list[d]) add_row(static_cast<size_t>(pos));
+      }
+      if (want_index) {  // spare rows for thresholds a reuse encode adds: up to the next 64 (K0's row groups;
+                         // SR_T_SPARE=n: exactly n, tests of the spare-exhausted path)
+        static const int spare_env = std::getenv("SR_T_SPARE") ? std::atoi(std::getenv("SR_T_SPARE")) : -1;
+        const size_t n_used = w->t_dim.size() - static_cast<size_t>(w->t_off[d + 1]);
+        const size_t n_rows = spare_env >= 0 ? n_used + static_cast<size_t>(spare_env) : (n_used + 4 + 63) / 64 * 64;
+        for (size_t i = n_used; i < n_rows; ++i) {
+          w->t_dim.push_back(d);
+          w->t_thr.push_back(kTSpare);
+        }
       }
       w->t_off[d + 2] = static_cast<int32_t>(w->t_dim.size());
     }
@@ -2400,7 +2663,100 @@ sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr
     }
   }
   phase(6);
+
+  // ---- the reuse index (CandReuse), when this input was also
+  // the last call's and its candidate side reads nothing from the snapshot but
+  // node capacities and pod counts
+  if (want_index) {
+    bool state_free = snap->anti_total == 0 && snap->opaque_total == 0 && !anti.active && !aff.active &&
+                      !sdyn.active && n_ports == 0 && n_scalars == 0 && n_spreads == 0 && w->dyn_cand.empty() &&
+                      scal_names.empty() && w->swap_mask == 0 && w->empty_class >= 0;
+    const sr_pod_affinity* PA = c->pod_affinity;
+    for (int32_t j = w->pod_base; j < w->pod_base + w->n_input_pods && state_free; ++j) {
+      const int32_t pod = cands->cand_pods[j];
+      const uint32_t mb = memo_bits(pod);
+      state_free = (mb & MEMO_PLAIN) && !(mb & MEMO_PORTS);
+      if (PA)
+        state_free = state_free && PA->anti_off[pod] == PA->anti_off[pod + 1] &&
+                     (!PA->aff_off || PA->aff_off[pod] == PA->aff_off[pod + 1]);
+    }
+    if (state_free) {
+      const size_t NA = static_cast<size_t>(na);
+      const int32_t n_base_cls = static_cast<int32_t>(cls_empty.size());
+      R.content_gen = C.content_gen;
+      R.static_gen = C.static_gen;
+      R.n_spot = n_spot;
+      R.Wp = Wp;
+      R.a_comp = A_COMP;
+      R.comp_sets = comp_sets;
+      R.atom_empty = atom_empty;
+      R.atom_full = atom_full;
+      R.cls_empty = cls_empty;
+      R.pod_cls.resize(NA);
+      R.pod_ri.assign(NA * 3, -1);
+      auto req_of = [&](size_t q) { return &req_flat[static_cast<size_t>(active_src[q] - w->pod_base) * 3]; };
+      auto is_zero = [&](size_t q) {
+        const int64_t* rq = req_of(q);
+        return rq[0] == 0 && rq[1] == 0 && rq[2] == 0;
+      };
+      for (size_t q = 0; q < NA; ++q) R.pod_cls[q] = key_class[key_slot[pod_key[q]]];
+      pfor(3, 1, [&](size_t lo, size_t hi) {
+        for (size_t d = lo; d < hi; ++d) {
+          std::vector<int64_t>& dr = R.dreq[d];
+          dr.clear();
+          for (size_t q = 0; q < NA; ++q)
+            if (!is_zero(q)) dr.push_back(req_of(q)[d]);
+          std::sort(dr.begin(), dr.end());
+          dr.erase(std::unique(dr.begin(), dr.end()), dr.end());
+          const std::vector<int64_t>& v = C.node_vals[d];
+          R.vals[d] = v;
+          R.dthr[d].resize(dr.size());
+          R.drow[d].resize(dr.size());
+          for (size_t u = 0; u < dr.size(); ++u) {
+            const size_t pos = static_cast<size_t>(std::lower_bound(v.begin(), v.end(), dr[u]) - v.begin());
+            R.dthr[d][u] = pos == v.size() ? INT64_MAX : v[pos];
+            R.drow[d][u] = t_index[d][pos];
+          }
+          std::vector<int32_t>& po = R.dpod_off[d];
+          po.assign(dr.size() + 1, 0);
+          for (size_t q = 0; q < NA; ++q) {
+            if (is_zero(q)) continue;
+            const int32_t u = static_cast<int32_t>(std::lower_bound(dr.begin(), dr.end(), req_of(q)[d]) - dr.begin());
+            R.pod_ri[q * 3 + d] = u;
+            ++po[u + 1];
+          }
+          for (size_t u = 0; u < dr.size(); ++u) po[u + 1] += po[u];
+          R.dpod[d].resize(static_cast<size_t>(po.back()));
+          std::vector<int32_t> fill(po.begin(), po.end() - 1);
+          for (size_t q = 0; q < NA; ++q)
+            if (R.pod_ri[q * 3 + d] >= 0) R.dpod[d][fill[R.pod_ri[q * 3 + d]]++] = static_cast<int32_t>(q);
+        }
+      });
+      R.row_refs.assign(w->t_dim.size(), 0);
+      for (int d = 0; d < 3; ++d) {
+        R.row_of[d].clear();
+        R.spare[d].clear();
+        for (size_t u = 0; u < R.dreq[d].size(); ++u) {
+          ++R.row_refs[R.drow[d][u]];
+          R.row_of[d][R.dthr[d][u]] = R.drow[d][u];
+        }
+        for (int32_t row = w->t_off[d + 1]; row < w->t_off[d + 2]; ++row)
+          if (w->t_thr[row] == kTSpare) R.spare[d].push_back(row);
+      }
+      R.cls_pod_off.assign(static_cast<size_t>(n_base_cls) + 1, 0);
+      for (size_t q = 0; q < NA; ++q) ++R.cls_pod_off[R.pod_cls[q] + 1];
+      for (int32_t k = 0; k < n_base_cls; ++k) R.cls_pod_off[k + 1] += R.cls_pod_off[k];
+      R.cls_pod.resize(NA);
+      std::vector<int32_t> fill(R.cls_pod_off.begin(), R.cls_pod_off.end() - 1);
+      for (size_t q = 0; q < NA; ++q) R.cls_pod[fill[R.pod_cls[q]]++] = static_cast<int32_t>(q);
+      R.mark.assign(NA, 0);
+      R.epoch = 0;
+      R.indexed = true;
+    }
+  }
   return SR_OK;
 }
+
+}  // namespace
 
 }  // namespace sr

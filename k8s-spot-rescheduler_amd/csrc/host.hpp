@@ -296,6 +296,48 @@ constexpr int kDynU64 = 5 * kDynG + 1 + kSpreadU64;  // words per pod record (ke
 constexpr int kExtScalars = 2;      // shared scalar names per candidate
 constexpr int kExtScalarNames = 8;  // shared scalar names per call (node_scal rows)
 constexpr int kExtU64 = 8;          // {acc cpu, mem, eph, req s0, req s1, acc s0, acc s1, row s0 | row s1 << 32}
+constexpr int kPodPatchWords = 3;   // {active pod, rec[4], rec[5]} (kernels.hpp kPodPatchU64)
+constexpr int64_t kTSpare = INT64_MAX - 1;  // threshold of a spare T row (kernels.hpp kTPad)
+
+// Candidate-side reuse (encode.cpp reuse_encode), one per Workload.  When a
+// call's candidate input (lists, global indices, every pod stamped and
+// unchanged) equals the one the Workload was last encoded for, and that side
+// reads nothing from the snapshot but
+// node capacities and pod counts (no host ports, scalar resources, topology
+// spread, attachable volumes or inter-pod terms, no existing pod with
+// anti-affinity), the Workload is kept: only the pod-count and composite
+// atom rows, the T-row thresholds and the records of the pods whose T rows
+// or dead flag moved are updated.  T rows are slots keyed by threshold value
+// (a dimension's group has spare rows, kTPad), so a threshold that moves
+// re-points only the pods asking within the moved interval.  The index is
+// built by the second consecutive full encode of one input.
+struct CandReuse {
+  bool have_input = false;  // the last call's candidate input
+  std::vector<int32_t> pod_off, pods, glob;
+  std::vector<uint64_t> stamps;
+  uint64_t shape = 0;
+  bool indexed = false;  // the index below describes the Workload holding it
+  uint64_t content_gen = 0;  // EncoderCache::content_gen it was built under (the classes name its ids)
+  uint64_t static_gen = 0;
+  int32_t n_spot = -1, Wp = 0;
+  int32_t a_comp = 0;                          // first composite atom
+  std::vector<int32_t> comp_sets;              // untolerated-taint set of each composite atom
+  std::vector<uint8_t> atom_empty, atom_full;  // [n_atoms]
+  std::vector<uint8_t> cls_empty;              // [classes before the empty class]
+  std::vector<int32_t> pod_cls;                // [active pod] class before the dead check
+  std::vector<int32_t> pod_ri;                 // [active pod][3] distinct request (-1: zero-request pod)
+  std::vector<int64_t> vals[3];                // the node values the thresholds below were taken from
+  std::vector<int64_t> dreq[3], dthr[3];       // distinct requests, their threshold (node value >= it)
+  std::vector<int32_t> drow[3];                // ... and T row
+  std::vector<int32_t> dpod_off[3], dpod[3];   // CSR distinct request -> active pods
+  std::vector<int32_t> cls_pod_off, cls_pod;   // CSR class -> active pods
+  std::unordered_map<int64_t, int32_t> row_of[3];  // threshold -> T row
+  std::vector<int32_t> row_refs;               // [T row] distinct requests on it
+  std::vector<int32_t> spare[3];               // free T rows of each dimension's group
+  std::vector<uint32_t> mark;                  // [active pod] epoch of the last patch
+  uint32_t epoch = 0;
+  void drop() { have_input = indexed = false; }
+};
 
 // The encoded workload of one planning call (host copy; uploaded as one
 // arena).  The spot nodes' state (capacity records, free values) lives in the
@@ -365,6 +407,13 @@ struct Workload {
   int32_t n_input_cand = 0;
   int32_t n_input_pods = 0;
   int32_t pod_base = 0;  // cand_pod_off[0] of the call: pod_src - pod_base indexes its pods
+  // ---- candidate-side reuse (EncoderCache::CandReuse): every array above
+  // except atoms, t_thr and the node state belongs to candidate generation
+  // cand_gen; a reuse encode keeps them and lists the pod records it changed
+  uint64_t cand_gen = 0;
+  bool reused = false;
+  std::vector<uint64_t> pod_patch;  // [n][kPodPatchWords] {active pod, rec[4], rec[5]} (reuse encodes)
+  CandReuse reuse;                  // kept by reset(): the encoder rebuilds or drops it
 
   // Back to the default state, keeping every buffer's capacity: a planner
   // encodes one tick after another, and fresh multi-MB buffers page-fault.
@@ -391,6 +440,8 @@ struct Workload {
     first_fallback = -1;
     fallback_pods = 0;
     n_input_cand = n_input_pods = pod_base = 0;
+    reused = false;
+    pod_patch.clear();
   }
 };
 
@@ -493,8 +544,13 @@ struct EncoderCache {
   // patched_from (~0: it rebuilt them all); the planner uploads only those
   std::vector<int32_t> patched_nodes;
   uint64_t patched_from = ~0ull;
+  uint64_t cand_gen_next = 1;
+  int32_t last_reused = 0, last_pod_patches = 0;
+
+  uint64_t content_gen = 0;  // bumped by clear_content (a Workload's CandReuse is valid for one value)
 
   void clear_content() {  // drops every content-interned dictionary
+    ++content_gen;        // reuse indices: their classes and atoms name them
     pod_memo.clear();     // its spec ids index them
     spec_shards.clear();
     spec.clear();

@@ -164,6 +164,15 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
           static_cast<int64_t>(pr[1 + lane]);
     }
   }
+  // pod patches (a candidate-side reuse encode re-pointed these records' rows):
+  // K2 reads pod_rec after this kernel, every thread of the grid takes a share
+  for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < w.n_pod_patch;
+       i += static_cast<int>(gridDim.x * blockDim.x)) {
+    const uint64_t* pp = w.pod_patch + static_cast<size_t>(i) * kPodPatchU64;
+    uint64_t* rec = const_cast<uint64_t*>(w.pod_rec) + static_cast<size_t>(pp[0]) * 6;
+    rec[4] = pp[1];
+    rec[5] = pp[2];
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     unsigned long long* dm = reinterpret_cast<unsigned long long*>(w.d_min);
     dm[0] = ~0ull;
@@ -269,7 +278,7 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
         hi |= static_cast<uint32_t>(static_cast<int64_t>(readlane64(fv, 32 + i)) >= thr) << i;
       word = static_cast<uint64_t>(hi) << 32 | lo;
     }
-    if (lane < nr) w.T[static_cast<size_t>(r0 + lane) * Wp + W] = word;
+    if (lane < nr && thr != kTPad) w.T[static_cast<size_t>(r0 + lane) * Wp + W] = word;  // spare rows: unread
   }
 }
 

@@ -19,6 +19,8 @@ constexpr int kDevDynU64 = 5 * kDevDynG + 1 + kDevSpreadSlots * (kDevDynG + 3);
                                         // per spread slot kDevDynG mask words and 3 info words (SpreadDyn)
 constexpr int kDevDomKeys = 4;          // key slots (host.hpp kDomKeys)
 constexpr int kNodePatchU64 = 12;       // node patch: {node, node_rec[8], node_free[3]}
+constexpr int kPodPatchU64 = 3;         // pod patch: {active pod, pod_rec[4], pod_rec[5]}
+constexpr int64_t kTPad = INT64_MAX - 1;  // threshold of a spare T row (no pod points at it; K0 skips it)
 constexpr int kDevDynTerms = 4;         // terms per domain-path affinity set (host.hpp kDynTerms)
 constexpr int kDevExtU64 = 8;           // extension record words (host.hpp kExtU64)
 
@@ -29,6 +31,8 @@ struct DevWorkload {
   const uint64_t* node_rec;    // [n_pad][8] AoS {free cpu, mem, eph, state bits, pods_left, 0, 0, 0} for K2
   const uint64_t* node_patch;  // [n_node_patch][kNodePatchU64]: records of nodes changed since the generation the
   int32_t n_node_patch;        //   node section holds; K0 writes them there (T rows use them directly)
+  const uint64_t* pod_patch;   // [n_pod_patch][kPodPatchU64]: row words of the pod records a candidate-side
+  int32_t n_pod_patch;         //   reuse encode re-pointed (K0 writes them into pod_rec for K2)
   int32_t n_atoms;
   const uint64_t* atoms;       // [n_atoms][Wp] node bitsets (encode.cpp)
   const int32_t* cls_prog_off; // class atom programs (CSR): ops atom << 2 | {AND, AND NOT,
@@ -38,7 +42,7 @@ struct DevWorkload {
   uint32_t s_empty_off;     // word offset of the all-zero S row pods with a certainly empty F row point
                             // at (encode.cpp), 0xffffffff if there is none
   int32_t n_t;              // threshold rows: row 0 = every node, then cpu, memory,
-  int32_t t_off[5];         //   ephemeral rows [t_off[d + 1], t_off[d + 2]) in threshold order
+  int32_t t_off[5];         //   ephemeral rows [t_off[d + 1], t_off[d + 2]) (any order; kTPad: spare)
   const int64_t* t_thr;
   int32_t n_pods;
   uint64_t swap_mask;       // state bits [0, 2 * pairs): anti-affinity pairs; a pod conflicts with the

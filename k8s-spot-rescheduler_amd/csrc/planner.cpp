@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -64,26 +65,46 @@ struct HostBuf {
   size_t cap = 0;
 };
 
+// One workload slot: an encoded candidate input with its device arena and
+// pinned staging copy.  sr_plan_first's prefix batches and an every-candidate
+// plan are different inputs; with a slot each, a tick whose inputs equal the
+// previous tick's reuses each one's candidate side (CandReuse) and its
+// device-resident records instead of re-encoding and re-uploading them.
+struct Slot {
+  sr::Workload wl;
+  DevBuf arena;
+  HostBuf h_arena;
+  uint64_t dev_state_gen = ~0ull;   // encoder state whose node records the device arena holds
+  uint64_t host_state_gen = ~0ull;  // ... and the pinned staging arena
+  uint64_t dev_cand_gen = ~0ull;    // candidate generation (Workload::cand_gen) the device arena holds
+  uint64_t host_cand_gen = ~0ull;   // ... and the staging arena
+  bool patch_pending = false;       // a prepare left node patches for K0 that no run has applied yet
+  bool pod_patch_pending = false;   // ... pod patches
+  uint64_t key = 0;                 // fingerprint of the input it was last prepared for
+  uint64_t used = 0;                // clock of its last prepare (least recently used is replaced)
+};
+
 }  // namespace
 
 struct sr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  DevBuf arena, tables, out_node, out_status, out_bytes, dmin, prof, scratch;
-  HostBuf h_arena, h_result, h_status, h_node, h_bytes;
+  DevBuf tables, out_node, out_status, out_bytes, dmin, prof, scratch;
+  HostBuf h_result, h_status, h_node, h_bytes;
   HostBuf h_early;           // mapped: K2's per-candidate result words (single-rank runs)
   HostBuf h_comm;            // pinned: the reduced words of a caller-provided collective
   bool in_flight = false;    // a run returned with K2 still planning candidates past the winner
   uint64_t* d_early = nullptr;  // device address of h_early
   uint64_t issued_checks = 0;  // checks of the prepared workload's plan (known after a full run)
   bool issued_known = false;
-  sr::Workload wl;
+  std::vector<std::unique_ptr<Slot>> slots;  // SR_PLAN_SLOTS (default 4), made on first use
+  int32_t n_slots = 4;
+  Slot* cur = nullptr;       // the slot of the last prepare
+  uint64_t slot_clock = 0;
   std::vector<uint64_t> node_patch_words;  // this call's node patches (prepare)
   sr::EncoderCache enc;      // what the encoder keeps across calls (encode.cpp)
-  uint64_t dev_state_gen = ~0ull;  // encoder state whose node records the device arena holds
-  uint64_t host_state_gen = ~0ull; // ... and the pinned staging arena (kept between calls)
-  hipEvent_t ev_upload = nullptr;  // the last upload (the staging buffer is reused after it)
+  hipEvent_t ev_upload = nullptr;  // the last upload (a staging buffer is reused after it)
   int32_t prefix_batch = 16;       // first batch of sr_plan_first (SR_PREFIX_BATCH; tools/gpu_prefix.sh)
   sr::DevWorkload dw{};
   bool prepared = false;
@@ -106,7 +127,6 @@ struct sr_ctx {
   FILE* prof_file = nullptr;  // SR_K2_PROFILE: per-wave K2 records appended per run
   int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
   int32_t node_patch = 1;     // SR_NODE_PATCH=0: a changed node section always goes up whole
-  bool patch_pending = false;  // a prepare left node patches for K0 that no run has applied yet
   int32_t k2_narrow = 1;      // SR_K2_NARROW: 32-bit scaled window visits in node order (0: 64-bit only)
   int32_t k2_wpb = 4;         // SR_K2_WPB: K2 waves per block (1, 2, 4)
   int32_t k2_node_kernel = 1; // SR_K2_NODE_KERNEL: node-order-only K2 kernel when every candidate takes that path
@@ -221,15 +241,55 @@ sr_status allreduce_min_dev(sr_ctx* ctx, void* words, int32_t n) {
   return SR_OK;
 }
 
+// The slot for this input: the one last prepared for an input with the same
+// fingerprint (the encoder then compares the input in full), else a new one
+// while fewer than n_slots exist, else the least recently used.
+Slot& pick_slot(sr_ctx* ctx, const sr_candidates* cands) {
+  const int32_t n = cands->n_cand;
+  uint64_t key = 0x5107ull + static_cast<uint64_t>(n);
+  if (n > 0) {
+    const int32_t b = cands->cand_pod_off[0], e = cands->cand_pod_off[n];
+    auto mixin = [&](uint64_t x) { key = (key ^ x) * 0x100000001B3ull; };
+    mixin(static_cast<uint32_t>(b));
+    mixin(static_cast<uint32_t>(e));
+    if (e > b) {
+      mixin(static_cast<uint32_t>(cands->cand_pods[b]));
+      mixin(static_cast<uint32_t>(cands->cand_pods[b + (e - b) / 2]));
+      mixin(static_cast<uint32_t>(cands->cand_pods[e - 1]));
+    }
+    if (cands->cand_global) {
+      mixin(static_cast<uint32_t>(cands->cand_global[0]));
+      mixin(static_cast<uint32_t>(cands->cand_global[n - 1]));
+    }
+  }
+  Slot* pick = nullptr;
+  for (auto& sl : ctx->slots)
+    if (sl->key == key) pick = sl.get();
+  if (!pick && static_cast<int32_t>(ctx->slots.size()) < ctx->n_slots) {
+    ctx->slots.push_back(std::make_unique<Slot>());
+    pick = ctx->slots.back().get();
+  }
+  if (!pick) {
+    pick = ctx->slots.front().get();
+    for (auto& sl : ctx->slots)
+      if (sl->used < pick->used) pick = sl.get();
+  }
+  pick->key = key;
+  pick->used = ++ctx->slot_clock;
+  return *pick;
+}
+
 sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands) {
   auto t0 = std::chrono::steady_clock::now();
   ctx->prepared = false;
-  sr::Workload& w = ctx->wl;
+  Slot& sl = pick_slot(ctx, cands);
+  ctx->cur = &sl;
+  sr::Workload& w = sl.wl;
   std::string err;
   sr_status st = sr::encode_workload(&ctx->enc, snap, c, cands, &w, &err);
   if (st != SR_OK) {
     ctx->err = err;
-    ctx->dev_state_gen = ~0ull;  // the encoder may have moved on: upload the node records again
+    sl.dev_state_gen = ~0ull;  // the encoder may have moved on: upload the node records again
     return st;
   }
   const int32_t na = static_cast<int32_t>(w.pod_src.size());
@@ -237,13 +297,16 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   // Arena: the spot nodes' records and free values first (uploaded only when
   // the encoder's state view changed), then this call's sections.
   const sr::EncoderCache& E = ctx->enc;
+  // Arena: the node section (spot nodes' records and free values), the
+  // candidate section (class programs, pod records, candidate lists, domain
+  // path and extension records: one candidate generation, w.cand_gen), then
+  // this call's tick section (atoms, thresholds, patches).  Sections the
+  // device already holds are not copied again.
   Packer pk;
   const size_t o_nr = pk.add(E.node_rec);
   const size_t o_nf = pk.add(E.node_free);
   const size_t node_bytes = pk.size();
-  const size_t o_at = pk.add(w.atoms);
   const size_t o_cpo = pk.add(w.cls_prog_off), o_cp = pk.add(w.cls_prog), o_cp8 = pk.add(w.cls_prog8);
-  const size_t o_tt = pk.add(w.t_thr);
   const size_t o_prec = pk.add(w.pod_rec);
   const size_t o_co = pk.add(w.cand_off), o_cg = pk.add(w.cand_global);
   const size_t o_ls = pk.add(w.list);
@@ -254,6 +317,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const bool ext = !w.ext_cand.empty();
   const size_t o_ec = ext ? pk.add(w.ext_cand) : 0, o_ep = ext ? pk.add(w.pod_ext) : 0;
   const size_t o_ns = ext ? pk.add(w.node_scal) : 0;
+  const size_t tick_from = pk.size();
+  const size_t o_at = pk.add(w.atoms);
+  const size_t o_tt = pk.add(w.t_thr);
   // Records of the few spot nodes the encoder patched since the last
   // generation, {node, node_rec[8], node_free[3]} each: when the device holds
   // that generation they ride in this call's copy and K0 writes them into
@@ -271,23 +337,28 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
     }
   }
   const size_t o_np = patch.empty() ? 0 : pk.add(patch);
+  const size_t o_pp = w.pod_patch.empty() ? 0 : pk.add(w.pod_patch);
   const size_t bytes = pk.size();
 
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   st = settle(ctx);
   if (st != SR_OK) return st;
   if (ctx->ev_upload) HIP_TRY(ctx, hipEventSynchronize(ctx->ev_upload));  // staging buffer free again
-  const size_t h_cap = ctx->h_arena.cap;
-  HIP_TRY(ctx, host_reserve(ctx->h_arena, bytes));
-  if (ctx->h_arena.cap != h_cap) ctx->host_state_gen = ~0ull;  // a new staging buffer holds no node records
-  const size_t arena_cap = ctx->arena.cap;
-  HIP_TRY(ctx, dev_reserve(ctx->arena, bytes));  // a new allocation holds no node records
-  const bool same_arena = ctx->arena.cap == arena_cap;
-  if (ctx->patch_pending) ctx->dev_state_gen = ~0ull;  // the last prepare's patches never reached the device
-  const bool nodes_resident = same_arena && ctx->dev_state_gen == w.state_gen;
+  const size_t h_cap = sl.h_arena.cap;
+  HIP_TRY(ctx, host_reserve(sl.h_arena, bytes));
+  if (sl.h_arena.cap != h_cap) sl.host_state_gen = sl.host_cand_gen = ~0ull;  // a new staging buffer holds neither
+  const size_t arena_cap = sl.arena.cap;
+  HIP_TRY(ctx, dev_reserve(sl.arena, bytes));  // a new allocation holds no node records
+  const bool same_arena = sl.arena.cap == arena_cap;
+  if (sl.patch_pending) sl.dev_state_gen = ~0ull;  // the slot's last prepare's patches never reached the device
+  if (sl.pod_patch_pending) sl.dev_cand_gen = ~0ull;
+  const bool nodes_resident = same_arena && sl.dev_state_gen == w.state_gen;
+  // a reuse encode's candidate section is on the device: K0 re-points the
+  // records it lists (or none changed)
+  const bool cand_resident = w.reused && same_arena && sl.dev_cand_gen == w.cand_gen;
   // a few nodes changed since the generation on the device: K0 applies their
   // records from this call's copy
-  const bool nodes_patch = ctx->node_patch && !nodes_resident && same_arena && ctx->dev_state_gen == E.patched_from &&
+  const bool nodes_patch = ctx->node_patch && !nodes_resident && same_arena && sl.dev_state_gen == E.patched_from &&
                            !patch.empty();
   const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
@@ -305,11 +376,11 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   // when that is the current one, or the one the encoder patched a few nodes
   // on, only those nodes' records are rewritten (no copy of the whole section).
   {
-    char* hs = static_cast<char*>(ctx->h_arena.p);
+    char* hs = static_cast<char*>(sl.h_arena.p);
     const size_t NP = static_cast<size_t>(w.n_pad);
-    if (ctx->host_state_gen == w.state_gen) {
+    if (sl.host_state_gen == w.state_gen) {
       // current
-    } else if (E.patched_from != ~0ull && ctx->host_state_gen == E.patched_from && E.state_gen == w.state_gen &&
+    } else if (E.patched_from != ~0ull && sl.host_state_gen == E.patched_from && E.state_gen == w.state_gen &&
                !E.patched_nodes.empty()) {
       for (int32_t i : E.patched_nodes) {
         std::memcpy(hs + o_nr + static_cast<size_t>(i) * 64, &E.node_rec[static_cast<size_t>(i) * 8], 64);
@@ -320,18 +391,36 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
       std::memcpy(hs + o_nr, E.node_rec.data(), E.node_rec.size() * sizeof(uint64_t));
       std::memcpy(hs + o_nf, E.node_free.data(), E.node_free.size() * sizeof(int64_t));
     }
-    ctx->host_state_gen = w.state_gen;
+    sl.host_state_gen = w.state_gen;
   }
-  pk.copy_to(static_cast<char*>(ctx->h_arena.p), node_bytes);
-  HIP_TRY(ctx, hipMemcpyAsync(static_cast<char*>(ctx->arena.p) + from, static_cast<char*>(ctx->h_arena.p) + from,
-                              bytes - from, hipMemcpyHostToDevice, ctx->stream));
+  // the candidate section: kept in staging across a reuse encode (its pod
+  // patches applied there too), packed again otherwise
+  char* hs = static_cast<char*>(sl.h_arena.p);
+  if (w.reused && sl.host_cand_gen == w.cand_gen) {
+    for (size_t i = 0; i < w.pod_patch.size(); i += sr::kPodPatchWords)
+      std::memcpy(hs + o_prec + (static_cast<size_t>(w.pod_patch[i]) * 6 + 4) * 8, &w.pod_patch[i + 1], 16);
+    pk.copy_to(hs, tick_from);
+  } else {
+    pk.copy_to(hs, node_bytes);
+  }
+  sl.host_cand_gen = w.cand_gen;
+  char* dv = static_cast<char*>(sl.arena.p);
+  if (!cand_resident) {
+    HIP_TRY(ctx, hipMemcpyAsync(dv + from, hs + from, bytes - from, hipMemcpyHostToDevice, ctx->stream));
+  } else {
+    if (from < node_bytes)
+      HIP_TRY(ctx, hipMemcpyAsync(dv, hs, node_bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dv + tick_from, hs + tick_from, bytes - tick_from, hipMemcpyHostToDevice, ctx->stream));
+  }
   if (!ctx->ev_upload) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_upload, hipEventDisableTiming));
   HIP_TRY(ctx, hipEventRecord(ctx->ev_upload, ctx->stream));  // kernels queue behind the copy
-  ctx->dev_state_gen = w.state_gen;
-  ctx->patch_pending = nodes_patch;
+  sl.dev_state_gen = w.state_gen;
+  sl.patch_pending = nodes_patch;
+  sl.dev_cand_gen = w.cand_gen;
+  sl.pod_patch_pending = cand_resident && !w.pod_patch.empty();
   auto t2 = std::chrono::steady_clock::now();
 
-  char* base = static_cast<char*>(ctx->arena.p);
+  char* base = static_cast<char*>(sl.arena.p);
   auto at = [base](size_t off) { return static_cast<void*>(base + off); };
   sr::DevWorkload& d = ctx->dw;
   d = sr::DevWorkload{};
@@ -408,9 +497,14 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, hipHostGetDevicePointer(&dres, ctx->h_early.p, 0));
   ctx->d_early = static_cast<uint64_t*>(dres);
   d.res_stat = d.res_map = nullptr;  // set per run
-  ctx->t.bytes_uploaded = static_cast<uint64_t>(bytes - from);
+  ctx->t.bytes_uploaded = static_cast<uint64_t>(cand_resident ? (from < node_bytes ? node_bytes : 0) + bytes - tick_from
+                                                               : bytes - from);
   d.node_patch = nodes_patch ? static_cast<const uint64_t*>(at(o_np)) : nullptr;
   d.n_node_patch = nodes_patch ? static_cast<int32_t>(patch.size() / sr::kNodePatchU64) : 0;
+  const bool pods_patch = cand_resident && !w.pod_patch.empty();
+  d.pod_patch = pods_patch ? static_cast<const uint64_t*>(at(o_pp)) : nullptr;
+  d.n_pod_patch = pods_patch ? static_cast<int32_t>(w.pod_patch.size() / sr::kPodPatchU64) : 0;
+  static_assert(sr::kPodPatchU64 == sr::kPodPatchWords && sr::kTPad == sr::kTSpare, "patch layout shared with encode.cpp");
 
   const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
   // K0 algorithmic bytes: every table row written once; every atom row a class
@@ -437,6 +531,8 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   ctx->t.enc_static_rebuilt = ctx->enc.last_static_changed;
   ctx->t.enc_state_nodes = ctx->enc.last_state_changed;
   ctx->t.enc_memo_pods = ctx->enc.last_memo_hits;
+  ctx->t.enc_reused = ctx->enc.last_reused;
+  ctx->t.enc_pod_patches = ctx->enc.last_pod_patches;
   ctx->prepared = true;
   return SR_OK;
 }
@@ -460,7 +556,7 @@ sr_status flush_timing(sr_ctx* ctx) {
 // arrived after 100 ms falls back to the stream, which also surfaces a kernel
 // fault as an error.
 sr_status finish_early(sr_ctx* ctx, sr_plan_out* out) {
-  const sr::Workload& w = ctx->wl;
+  const sr::Workload& w = ctx->cur->wl;
   const sr::DevWorkload& d = ctx->dw;
   if (ctx->timing_cur) ctx->t.n_runs += 1;
   volatile uint64_t* stat = static_cast<volatile uint64_t*>(ctx->h_early.p);
@@ -516,7 +612,7 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     ctx->err = "sr_plan_run before sr_plan_prepare";
     return SR_ERR_STATE;
   }
-  const sr::Workload& w = ctx->wl;
+  const sr::Workload& w = ctx->cur->wl;
   sr::DevWorkload& d = ctx->dw;
   hipStream_t s = ctx->stream;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -563,7 +659,8 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   } while (0)
   PAIR(0, e0a, e0b);
   HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
-  ctx->patch_pending = false;  // K0 writes the node patches (idempotent on later runs)
+  ctx->cur->patch_pending = false;  // K0 writes the node and pod patches (idempotent on later runs)
+  ctx->cur->pod_patch_pending = false;
   PAIR(1, e1a, e1b);
   if (early) {
     d.res_stat = ctx->d_early;
@@ -715,6 +812,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_S_HEAD_ONLY")) ctx->s_head_only = std::atoi(m) != 0;
   if (const char* b = std::getenv("SR_PREFIX_BATCH")) ctx->prefix_batch = std::max(1, std::atoi(b));
   if (const char* m = std::getenv("SR_K2_WPB")) ctx->k2_wpb = std::atoi(m);
+  if (const char* m = std::getenv("SR_PLAN_SLOTS")) ctx->n_slots = std::max(1, std::min(16, std::atoi(m)));
   *out = ctx;
   return SR_OK;
 }
@@ -724,13 +822,16 @@ void sr_destroy(sr_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) (void)rccl().comm_destroy(ctx->comm);
-  for (DevBuf* b : {&ctx->arena, &ctx->tables, &ctx->out_node, &ctx->out_status, &ctx->out_bytes, &ctx->dmin,
-                    &ctx->prof, &ctx->scratch})
+  for (DevBuf* b : {&ctx->tables, &ctx->out_node, &ctx->out_status, &ctx->out_bytes, &ctx->dmin, &ctx->prof,
+                    &ctx->scratch})
     if (b->p) (void)hipFree(b->p);
   if (ctx->ev_upload) (void)hipEventDestroy(ctx->ev_upload);
-  for (HostBuf* b : {&ctx->h_arena, &ctx->h_result, &ctx->h_status, &ctx->h_node, &ctx->h_bytes, &ctx->h_early,
-                     &ctx->h_comm})
+  for (HostBuf* b : {&ctx->h_result, &ctx->h_status, &ctx->h_node, &ctx->h_bytes, &ctx->h_early, &ctx->h_comm})
     if (b->p) (void)hipHostFree(b->p);
+  for (auto& sl : ctx->slots) {
+    if (sl->arena.p) (void)hipFree(sl->arena.p);
+    if (sl->h_arena.p) (void)hipHostFree(sl->h_arena.p);
+  }
   for (auto* v : {&ctx->ev_start, &ctx->ev_end})
     for (hipEvent_t e : *v) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

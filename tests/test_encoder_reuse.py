@@ -1,0 +1,68 @@
+"""Candidate-side reuse of the persistent encoder (host only, no GPU).
+
+A housekeeping tick whose candidate input (lists, global indices, stamped
+pods) equals the previous tick's keeps the previous encoding and brings only
+its capacity-dependent parts up to date: pod-count / composite atom rows, the
+T-row thresholds and the records of the pods asking within a moved threshold
+interval (host.hpp CandReuse).  tools/encode_stats' `reuse`
+mode drives tick after tick of fresh snapshots with pods added on random spot
+nodes (bursts included, and the extra pods leaving again) and compares every
+reused workload with one encoded from scratch on the same snapshot: atoms,
+class programs and request words equal, per pod the same dead flag, class and
+threshold per dimension.  Reference: nodes/nodes.go:63-145 (the tick's model,
+rebuilt by run() every tick, rescheduler.go:195,215)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "k8s-spot-rescheduler_amd")
+TOOL = os.path.join(PKG, "bin", "encode_stats")
+
+
+@pytest.fixture(scope="module")
+def tool():
+    subprocess.run(["make", "-C", PKG, "-j8", "tools"], check=True, stdout=subprocess.DEVNULL)
+    return TOOL
+
+
+def run_check(tool, config, ticks, burst=24, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    out = subprocess.run([tool, str(config), "100000", "reuse", str(ticks), str(burst)], env=e, check=True,
+                         capture_output=True, text=True, timeout=600).stdout
+    m = re.search(r"reuse check: (\d+) ticks \((\d+) reused, (\d+) full\), (\d+) pod patches.*mismatches (\d+)", out)
+    assert m, out
+    ticks_, reused, full, patches, bad = map(int, m.groups())
+    one = re.search(r"one-node-changed encode .*reused (\d), pod patches (\d+)", out)
+    return dict(ticks=ticks_, reused=reused, full=full, patches=patches, bad=bad,
+                one_node_reused=int(one.group(1)), out=out)
+
+
+@pytest.mark.parametrize("config", [1, 2, 3])
+def test_reuse_matches_fresh_encode(tool, config):
+    """Every tick after the index is built reuses the candidate side, and the
+    reused workload plans like a fresh encode (zero mismatches)."""
+    r = run_check(tool, config, 120 if config < 3 else 60)
+    assert r["bad"] == 0, r["out"]
+    assert r["reused"] == r["ticks"] and r["full"] == 0, r["out"]
+    assert r["one_node_reused"] == 1
+    assert r["patches"] > 0, r["out"]  # thresholds moved under some pods and their records were re-pointed
+
+
+def test_spare_rows_exhausted_falls_back_to_full_encode(tool):
+    """No spare T row (SR_T_SPARE=0): a threshold that needs a new row ends
+    the reuse, the tick is encoded in full and the next one reuses again."""
+    r = run_check(tool, 2, 80, burst=60, env={"SR_T_SPARE": "0"})
+    assert r["bad"] == 0, r["out"]
+    assert r["full"] >= 1 and r["reused"] >= 1, r["out"]
+
+
+def test_host_port_cluster_is_not_reused(tool):
+    """C5's candidates ask for host ports: the candidate side reads the spot
+    pods' ports, so every tick is encoded in full (and stays exact)."""
+    r = run_check(tool, 5, 20)
+    assert r["bad"] == 0, r["out"]
+    assert r["reused"] == 0 and r["full"] == r["ticks"], r["out"]

@@ -176,6 +176,63 @@ def test_consecutive_ticks_one_node_changed(checker, whole_checker, which, confi
         lib.sr_snapshot_destroy(h)
 
 
+def test_ticks_candidate_side_reuse():
+    """Candidate-side reuse (host.hpp CandReuse) through the planner: tick
+    after tick the same stamped candidate input on fresh snapshots whose spot
+    nodes gain pods (one at a time, bursts of 20, then all leave again).  From
+    the third tick on the encoder keeps the candidate side, the device keeps
+    its pod records and K0 re-points the ones whose thresholds moved (pod
+    patches); every plan equals the oracle.  In between: a prepare whose
+    patches no run applies (the next tick uploads the records whole), and
+    sr_plan_first's prefix batches on the same planner (other inputs, other
+    workload slots: the every-candidate input stays reused)."""
+    from spotplanner.planner import PredicateChecker
+    ck = PredicateChecker(0)
+    try:
+        sc = SynthCluster(3, seed=22, n_on_demand=200, n_spot=450)
+        lib = capi.load_planner()
+        nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+        cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+        n_rec_bytes = int(cand_off[-1]) * 48
+        rng = np.random.default_rng(9)
+        extra, patched, reused = [], 0, 0
+        for tick in range(16):
+            h = _snapshot(lib, sc, nm)
+            osnap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
+            if tick == 11:
+                extra.clear()
+            elif tick:
+                for _ in range(20 if tick % 4 == 3 else 1):
+                    extra.append((int(cand_pods[rng.integers(len(cand_pods))]), int(rng.integers(len(nm.spot)))))
+            for pod, pos in extra:
+                assert lib.sr_snapshot_add_pod(h, sc.ptr, pod, pos) == capi.SR_OK
+                osnap.lib.oracle_snapshot_add_pod(osnap.h, sc.ptr, pod, pos)
+            o = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
+            if tick == 6:  # prepared, never run: its pod patches never reach the device
+                c = capi.sr_candidates(len(cand_off) - 1, capi.ptr(cand_off, capi.P32), capi.ptr(cand_pods, capi.P32),
+                                       None)
+                assert lib.sr_plan_prepare(ck.handle, h, sc.ptr, ctypes.byref(c)) == capi.SR_OK
+            if tick in (9, 10):  # the reference-faithful tick first: its batches take other slots
+                ref_early = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=0)
+                fo, status, nodes, wmap = plan_first(ck, h, sc.ptr, cand_off, cand_pods)
+                check_first(fo, status, nodes, wmap, o, ref_early, cand_off)
+            p = plan_arrays(ck, h, sc.ptr, cand_off, cand_pods)
+            t = ck.timing()
+            assert np.array_equal(p.status, o["status"]), tick
+            assert np.array_equal(p.node_of_pod, o["node_of_pod"]), tick
+            assert p.winner == o["winner"], tick
+            if tick >= 2:
+                assert t.enc_reused == 1, (tick, t.enc_reused)
+                reused += 1
+                patched += t.enc_pod_patches
+                if tick != 6:  # the records stay on the device: the copy holds atoms, thresholds and patches
+                    assert t.bytes_uploaded < n_rec_bytes // 4, (tick, t.bytes_uploaded, n_rec_bytes)
+            lib.sr_snapshot_destroy(h)
+        assert reused == 14 and patched > 0, (reused, patched)
+    finally:
+        ck.close()
+
+
 def test_ticks_alternating_clusters_and_interners(checker):
     """Static-view changes between ticks: two clusters in turn (different
     spot pools and specs), and the same random scenario encoded through two

@@ -1,6 +1,6 @@
 // Host-only harness: NewNodeMap + snapshot + encode_workload on a synthetic
 // config, printing the workload's dimensions and host-side timings (no GPU).
-//   make -C k8s-spot-rescheduler_amd tools && k8s-spot-rescheduler_amd/bin/encode_stats 3 [max candidates]
+//   make -C k8s-spot-rescheduler_amd tools && k8s-spot-rescheduler_amd/bin/encode_stats 3 [max candidates] [check | reuse [ticks [burst]]]
 // Encodes are timed cold (empty encoder cache), warm (the same snapshot
 // again) and after one spot node changed (a fresh snapshot with one more pod
 // on one node), the steady state of a planner between two ticks.
@@ -23,8 +23,8 @@ static double ms_since(std::chrono::steady_clock::time_point a) {
 static void phases(const char* tag) {
   const double* p = sr::encode_phase_ms;
   printf("  %-6s phases(ms): views %.3f pass1 %.3f ports %.3f gather %.3f shards %.3f specs-new %.3f keys %.3f "
-         "classes %.3f atoms %.3f lb+empty %.3f pods %.3f trows %.3f recs %.3f lists %.3f\n",
-         tag, p[0], p[5], p[1], p[9], p[14], p[7], p[2], p[3], p[4], p[8], p[10], p[12], p[13], p[6]);
+         "classes %.3f atoms %.3f lb+empty %.3f pods %.3f trows %.3f recs %.3f lists %.3f reuse %.3f\n",
+         tag, p[0], p[5], p[1], p[9], p[14], p[7], p[2], p[3], p[4], p[8], p[10], p[12], p[13], p[6], p[11]);
 }
 
 int main(int argc, char** argv) {
@@ -94,8 +94,9 @@ int main(int argc, char** argv) {
     last_static = cache.last_static_changed;
     sr_snapshot_destroy(s2);
   }
-  printf("one-node-changed encode (fresh snapshot) best %.3f ms (state nodes %d, static rebuilt %d, memo hits %d)\n",
-         best, last_state, last_static, cache.last_memo_hits);
+  printf("one-node-changed encode (fresh snapshot) best %.3f ms (state nodes %d, static rebuilt %d, memo hits %d, "
+         "reused %d, pod patches %d)\n", best, last_state, last_static, cache.last_memo_hits, cache.last_reused,
+         cache.last_pod_patches);
   phases("1node");
   if (argc > 3 && std::string(argv[3]) == "check") {
     // the state view patched node by node equals the one rebuilt from scratch:
@@ -131,6 +132,76 @@ int main(int argc, char** argv) {
       ++ticks;
     }
     printf("state views consistent: %d ticks (%d patched node by node)\n", ticks, patched);
+  }
+  if (argc > 3 && std::string(argv[3]) == "reuse") {
+    // candidate-side reuse: every tick a fresh snapshot with a few more (or
+    // fewer) pods on random spot nodes and the same candidate input; the
+    // reused workload must plan like one encoded from scratch: same atoms,
+    // programs and requests, per pod the same dead flag, class and threshold
+    // per dimension
+    std::vector<std::pair<int32_t, int32_t>> extra;
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&](uint64_t n) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x % n; };
+    const int ticks = argc > 4 ? atoi(argv[4]) : 200;
+    const int burst = argc > 5 ? atoi(argv[5]) : 24;  // pods added every fifth tick (many new free values)
+    int reused = 0, full = 0, bad = 0;
+    long patches = 0;
+    double ms_reuse = 0, ms_views = 0;
+    for (int r = 0; r < ticks && !cp.empty(); ++r) {
+      sr_snapshot* s2 = nullptr;
+      sr_snapshot_create(&c, spot.data(), ns, off.data(), idx.data(), &s2);
+      if (r % 9 == 8) extra.clear();
+      const int add = r % 5 == 4 ? burst : 1 + static_cast<int>(rnd(3));  // sometimes a burst: many new free values
+      for (int a = 0; a < add; ++a)
+        extra.emplace_back(cp[rnd(cp.size())], static_cast<int32_t>(rnd(static_cast<uint64_t>(ns))));
+      for (auto& e : extra) sr_snapshot_add_pod(s2, &c, e.first, e.second);
+      t0 = std::chrono::steady_clock::now();
+      if (sr::encode_workload(&cache, s2, &c, &cands, &w, &err) != SR_OK) return 1;
+      const double ms = ms_since(t0);
+      if (cache.last_reused) {
+        ++reused;
+        patches += cache.last_pod_patches;
+        ms_reuse += ms;
+        ms_views += sr::encode_phase_ms[0];
+      } else {
+        ++full;
+      }
+      sr::EncoderCache fresh;
+      sr::Workload f;
+      if (sr::encode_workload(&fresh, s2, &c, &cands, &f, &err) != SR_OK) return 1;
+      auto fail = [&](const char* what, long i) {
+        if (bad++ < 5) printf("tick %d (reused %d): %s differs at %ld\n", r, cache.last_reused, what, i);
+      };
+      if (w.atoms != f.atoms) fail("atoms", 0);
+      if (w.pod_src != f.pod_src || w.cand_off != f.cand_off || w.list != f.list || w.status_host != f.status_host)
+        fail("candidate lists", 0);
+      const int32_t nb = f.empty_class >= 0 ? f.empty_class : f.n_classes;  // classes before the empty one
+      if (w.cls_prog_off.size() < static_cast<size_t>(nb) + 1 ||
+          !std::equal(f.cls_prog_off.begin(), f.cls_prog_off.begin() + nb + 1, w.cls_prog_off.begin()) ||
+          !std::equal(f.cls_prog.begin(), f.cls_prog.begin() + f.cls_prog_off[nb], w.cls_prog.begin()))
+        fail("class programs", 0);
+      auto thr = [](const sr::Workload& v, int32_t row) { return row == 0 ? INT64_MIN : v.t_thr[row]; };
+      for (size_t q = 0; q < f.pod_src.size(); ++q) {
+        const int32_t* a = &w.pod_rows[q * 4];
+        const int32_t* b = &f.pod_rows[q * 4];
+        const bool da = a[0] == w.empty_class, db = b[0] == f.empty_class;
+        if (da != db || (!da && a[0] != b[0])) fail("class", static_cast<long>(q));
+        for (int d = 0; d < 3 && !da; ++d)
+          if (thr(w, a[1 + d]) != thr(f, b[1 + d]) || w.t_dim[a[1 + d]] != f.t_dim[b[1 + d]]) fail("threshold", static_cast<long>(q));
+        for (int k = 0; k < 4; ++k)
+          if (w.pod_rec[q * 6 + k] != f.pod_rec[q * 6 + k]) fail("request words", static_cast<long>(q));
+        const uint64_t Wp64 = static_cast<uint64_t>(w.Wp);
+        if (w.pod_rec[q * 6 + 4] != (static_cast<uint64_t>(a[0]) * Wp64 | static_cast<uint64_t>(w.n_classes + a[1]) * Wp64 << 32) ||
+            w.pod_rec[q * 6 + 5] != (static_cast<uint64_t>(w.n_classes + a[2]) * Wp64 |
+                                     static_cast<uint64_t>(w.n_classes + a[3]) * Wp64 << 32))
+          fail("row words", static_cast<long>(q));
+      }
+      sr_snapshot_destroy(s2);
+    }
+    printf("reuse check: %d ticks (%d reused, %d full), %ld pod patches, reuse encode avg %.3f ms (views %.3f), "
+           "mismatches %d\n", reused + full, reused, full, patches, reused ? ms_reuse / reused : 0.0,
+           reused ? ms_views / reused : 0.0, bad);
+    if (bad) return 2;
   }
   printf("Wp %d atoms %d classes %d program ops %zu t_rows %zu\n", w.Wp, w.n_atoms, w.n_classes, w.cls_prog.size(),
          w.t_dim.size());

@@ -6,7 +6,7 @@ every-candidate plan, each against the oracle on the same mutated snapshot.
 Exercises the persistent encoder's caches (state patches, port-conflict rows,
 staging arena, node-record patch uploads).  GPU required.
 
-  python tools/tick_stress.py [--seconds 150]
+  python tools/tick_stress.py [--seconds 150] [--wide] [--reuse]
 """
 import argparse
 import os
@@ -30,6 +30,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=150.0)
     ap.add_argument("--wide", action="store_true", help="C4-shaped clusters (5,000-node pools: rows over 64 words)")
+    ap.add_argument("--reuse", action="store_true",
+                    help="every tick plans all candidates on one planner per cluster: the same stamped input tick "
+                         "after tick, so the candidate side is reused (CandReuse) and its records patched on the device")
     a = ap.parse_args()
     lib = capi.load_planner()
     os.environ["SR_NODE_PATCH"] = "0"  # the second planner uploads a changed node section whole
@@ -47,10 +50,12 @@ def main():
         nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
         maps.append((nm, *build_candidates(nm, sc.pod_flags())))
     extra = [[], []]
+    per_cluster = [PredicateChecker(0), PredicateChecker(0)] if a.reuse else []
+    reused = patches = 0
     while time.time() - t0 < a.seconds:
         ci = (ticks // 10) % 2  # ten ticks of one cluster, then ten of the other
         sc, (nm, cand_off, cand_pods) = clusters[ci], maps[ci]
-        ck = patcher if ticks % 3 == 0 else default
+        ck = per_cluster[ci] if a.reuse else patcher if ticks % 3 == 0 else default
         if rng.random() < 0.3 and extra[ci]:
             extra[ci].pop(int(rng.integers(len(extra[ci]))))  # a pod leaves again
         for _ in range(int(rng.integers(1, 4))):
@@ -62,7 +67,15 @@ def main():
             assert lib.sr_snapshot_add_pod(h, sc.ptr, pod, pos) == capi.SR_OK
             osnap.lib.oracle_snapshot_add_pod(osnap.h, sc.ptr, pod, pos)
         ref_all = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
-        if ticks % 2 == 0:
+        if a.reuse:
+            p = plan_arrays(ck, h, sc.ptr, cand_off, cand_pods)
+            t = ck.timing()
+            reused += t.enc_reused
+            patches += t.enc_pod_patches
+            assert np.array_equal(p.status, ref_all["status"]), ticks
+            assert np.array_equal(p.node_of_pod, ref_all["node_of_pod"]), ticks
+            assert p.winner == ref_all["winner"], ticks
+        elif ticks % 2 == 0:
             ref_early = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=0)
             o, status, nodes, wmap = T.plan_first(ck, h, sc.ptr, cand_off, cand_pods)
             T.check_first(o, status, nodes, wmap, ref_all, ref_early, cand_off)
@@ -77,7 +90,10 @@ def main():
             print("  %d ticks, %.0f s" % (ticks, time.time() - t0), flush=True)
     patcher.close()
     default.close()
-    print("tick stress: %d ticks in %.0f s, every plan equal to the oracle" % (ticks, time.time() - t0))
+    for ck in per_cluster:
+        ck.close()
+    print("tick stress: %d ticks in %.0f s, every plan equal to the oracle%s" % (
+        ticks, time.time() - t0, " (%d reused, %d pod patches)" % (reused, patches) if a.reuse else ""))
     return 0
 
 
