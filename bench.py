@@ -152,7 +152,7 @@ def plan_parity(o, gpu_status, gpu_nodes, cand_off):
     return ok, int(fb.sum()), n_fb_pods
 
 
-def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, gpu_checks, seconds):
+def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, gpu_checks, seconds, mutation=None):
     """The oracle (C restatement of the reference planner) on this host, rank 0
     only; BASELINE.md's three modes, each a median after 2 untimed warm-ups:
     all candidates on 1 thread (bounded by `seconds`, >= 3 runs), the
@@ -160,6 +160,8 @@ def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, gpu
     the host's CPU share (>= 10 runs)."""
     from oracle_lib import OracleSnapshot, oracle_plan
     snap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
+    if mutation is not None:  # the steady-state tick's snapshot: one more pod on one spot node
+        snap.lib.oracle_snapshot_add_pod(snap.h, sc.ptr, mutation[0], mutation[1])
 
     def timed(mode, threads, min_runs, budget_s, max_runs=500):
         for _ in range(2):  # warm-ups
@@ -284,6 +286,9 @@ def main():
                          "(reports the fallback ratio on them); baseline: BASELINE.json's config as specified")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: the config's cluster, candidates split over the ranks; weak: N x its candidates")
+    ap.add_argument("--tick", default="steady", choices=["steady", "cold"],
+                    help="steady: the timed step replays a steady-state tick (the previous tick's candidate input, "
+                         "one spot node changed: incremental K0 + K2); cold: a first tick (every table row)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e-reps", type=int, default=20, help="steady-state end-to-end ticks timed after the steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -349,6 +354,33 @@ def main():
     wmap = np.zeros(max(1, maxp), np.int32)
     out = capi.sr_plan_out()
     out.winner_map = capi.ptr(wmap, capi.P32)
+    mut_pod = int(cand_pods[0]) if len(cand_pods) else 0  # the same pod on every rank: one cluster state
+    mut_pos = min(7, len(nm.spot) - 1)
+    mutation = None
+    steady = {"tick": "cold", "k0": "every row"}
+    if args.tick == "steady" and mut_pos >= 0 and len(cand_pods):
+        # The steady state of a planner between two housekeeping ticks: the
+        # previous tick's candidate input on its snapshot (twice: the second
+        # encode indexes the candidate side), then this tick, a fresh snapshot
+        # with one more pod on one spot node.  The timed steps replay this
+        # tick's device work: K0 on the changed word columns and moved
+        # threshold rows (the rest of the tables is the previous tick's), K2, K3.
+        for _ in range(2):
+            assert lib.sr_plan_prepare(checker.handle, snap, sc.ptr, ctypes.byref(cands)) == capi.SR_OK
+            assert lib.sr_plan_run(checker.handle, ctypes.byref(out)) == capi.SR_OK, checker.last_error()
+        tick_snap = ctypes.c_void_p()
+        assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot),
+                                      capi.ptr(nm.node_pod_off, capi.P32), capi.ptr(nm.node_pod_idx, capi.P32),
+                                      ctypes.byref(tick_snap)) == capi.SR_OK
+        assert lib.sr_snapshot_add_pod(tick_snap, sc.ptr, mut_pod, mut_pos) == capi.SR_OK
+        lib.sr_snapshot_destroy(snap)
+        snap = tick_snap
+        assert lib.sr_plan_prepare(checker.handle, snap, sc.ptr, ctypes.byref(cands)) == capi.SR_OK
+        tq = checker.timing()
+        mutation = (mut_pod, mut_pos)
+        steady = {"tick": "steady: the previous tick's candidate input, one more pod on spot node %d" % mut_pos,
+                  "candidate_side_reused": bool(tq.enc_reused), "pod_patches": int(tq.enc_pod_patches),
+                  "k0": "incremental (changed word columns, moved threshold rows)" if tq.enc_reused else "every row"}
     # one run with per-candidate outputs first: K2's byte counts and the
     # reference-equivalent check count of this workload's plan
     status = np.zeros(max(1, len(loff) - 1), np.int32)
@@ -437,8 +469,6 @@ def main():
     # a planner that keeps what it derived from the previous tick.  Snapshot
     # creation is host work of NewNodeMap / GetClusterSnapshot (in full_tick).
     first_ok_ref = out.first_ok
-    mut_pod = int(lpods[0]) if len(lpods) else 0
-    mut_pos = min(7, len(nm.spot) - 1)
 
     def fresh_snapshot(r):
         h = ctypes.c_void_p()
@@ -582,7 +612,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": workload_name(args.config, sc.n_nodes, len(nm.on_demand), len(nm.spot),
                                                  sc.n_pods, world, args.scaling, args.variant),
-                       "variant": args.variant,
+                       "variant": args.variant, **steady,
                        "nodes": sc.n_nodes, "pods": sc.n_pods, "on_demand_nodes": int(len(nm.on_demand)),
                        "spot_nodes": int(len(nm.spot)), "candidates": int(len(cand_off) - 1),
                        "candidate_pods": int(len(cand_pods)), "parallelism": "candidates c%%%d" % world,
@@ -619,7 +649,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(sc, nm, cand_off, cand_pods, int(len(nm.spot)), status[:len(loff) - 1],
-                                                nodes_out[:len(lpods)], issued_local, args.cpu_seconds)
+                                                nodes_out[:len(lpods)], issued_local, args.cpu_seconds, mutation)
         print(json.dumps(line), flush=True)
     lib.sr_snapshot_destroy(snap)
     checker.close()

@@ -138,6 +138,48 @@ __device__ void s_row_general(const DevWorkload& w, int cls, int lane) {
   }
 }
 
+// What every K0 launch does besides its rows: the node patches (the few spot
+// nodes changed since the generation the node section holds: written for K2;
+// T rows read them directly), the pod patches (records a candidate-side reuse
+// encode re-pointed; K2 reads pod_rec after this kernel, every thread of the
+// grid takes a share) and the reset of d_min.
+__device__ __forceinline__ void k0_common(const DevWorkload& w, int local_first_fallback, int wave, int lane) {
+  if (blockIdx.x == 0 && wave == 0 && w.n_node_patch > 0 && lane < 11) {
+    for (int p = 0; p < w.n_node_patch; ++p) {
+      const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
+      const size_t node = static_cast<size_t>(pr[0]);
+      if (lane < 8) const_cast<uint64_t*>(w.node_rec)[node * 8 + lane] = pr[1 + lane];
+      else const_cast<int64_t*>(w.node_free)[static_cast<size_t>(lane - 8) * w.n_pad + node] =
+          static_cast<int64_t>(pr[1 + lane]);
+    }
+  }
+  for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < w.n_pod_patch;
+       i += static_cast<int>(gridDim.x * blockDim.x)) {
+    const uint64_t* pp = w.pod_patch + static_cast<size_t>(i) * kPodPatchU64;
+    uint64_t* rec = const_cast<uint64_t*>(w.pod_rec) + static_cast<size_t>(pp[0]) * 6;
+    rec[4] = pp[1];
+    rec[5] = pp[2];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    unsigned long long* dm = reinterpret_cast<unsigned long long*>(w.d_min);
+    dm[0] = ~0ull;
+    dm[1] = local_first_fallback < 0 ? ~0ull : static_cast<unsigned long long>(local_first_fallback) << 32;
+    dm[2] = w.rank_next;
+  }
+}
+
+// Free value of spot position n in dimension d (1..3) with this launch's node
+// patches applied (block 0 writes them into node_free; other waves may run
+// first, so they read the patch itself).
+__device__ __forceinline__ int64_t free_of(const DevWorkload& w, int d, int n) {
+  int64_t v = w.node_free[static_cast<size_t>(d - 1) * w.n_pad + n];
+  for (int p = 0; p < w.n_node_patch; ++p) {
+    const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
+    if (static_cast<uint64_t>(n) == pr[0]) v = static_cast<int64_t>(pr[8 + d]);
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, int local_first_fallback) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -153,32 +195,7 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
       if (p && lane == 0) p[1] = __builtin_amdgcn_s_memrealtime();
     }
   } stamp{prof, lane};
-  // node patches (the few spot nodes changed since the generation the node
-  // section holds): written here for K2; the T rows below read them directly
-  if (blockIdx.x == 0 && wave == 0 && w.n_node_patch > 0 && lane < 11) {
-    for (int p = 0; p < w.n_node_patch; ++p) {
-      const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
-      const size_t node = static_cast<size_t>(pr[0]);
-      if (lane < 8) const_cast<uint64_t*>(w.node_rec)[node * 8 + lane] = pr[1 + lane];
-      else const_cast<int64_t*>(w.node_free)[static_cast<size_t>(lane - 8) * w.n_pad + node] =
-          static_cast<int64_t>(pr[1 + lane]);
-    }
-  }
-  // pod patches (a candidate-side reuse encode re-pointed these records' rows):
-  // K2 reads pod_rec after this kernel, every thread of the grid takes a share
-  for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < w.n_pod_patch;
-       i += static_cast<int>(gridDim.x * blockDim.x)) {
-    const uint64_t* pp = w.pod_patch + static_cast<size_t>(i) * kPodPatchU64;
-    uint64_t* rec = const_cast<uint64_t*>(w.pod_rec) + static_cast<size_t>(pp[0]) * 6;
-    rec[4] = pp[1];
-    rec[5] = pp[2];
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    unsigned long long* dm = reinterpret_cast<unsigned long long*>(w.d_min);
-    dm[0] = ~0ull;
-    dm[1] = local_first_fallback < 0 ? ~0ull : static_cast<unsigned long long>(local_first_fallback) << 32;
-    dm[2] = w.rank_next;
-  }
+  k0_common(w, local_first_fallback, wave, lane);
   const size_t Wp = static_cast<size_t>(w.Wp);
   if (static_cast<int>(blockIdx.x) < s_blocks) {
     // S rows (NodeAffinity: nodeSelector pairs, required terms ORed with
@@ -265,11 +282,7 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
       const int nvalid = max(0, min(64, w.n_spot - 64 * W));
       word = nvalid >= 64 ? ~0ull : (1ull << nvalid) - 1;
     } else {
-      uint64_t fv = static_cast<uint64_t>(w.node_free[static_cast<size_t>(d - 1) * w.n_pad + 64 * W + lane]);
-      for (int p = 0; p < w.n_node_patch; ++p) {  // wave-uniform; block 0 may not have written them yet
-        const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
-        if (static_cast<uint64_t>(64 * W + lane) == pr[0]) fv = pr[8 + d];
-      }
+      const uint64_t fv = static_cast<uint64_t>(free_of(w, d, 64 * W + lane));
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int i = 0; i < 32; ++i) lo |= static_cast<uint32_t>(static_cast<int64_t>(readlane64(fv, i)) >= thr) << i;
@@ -279,6 +292,99 @@ __global__ __launch_bounds__(256) void k0_tables(DevWorkload w, int s_blocks, in
       word = static_cast<uint64_t>(hi) << 32 | lo;
     }
     if (lane < nr && thr != kTPad) w.T[static_cast<size_t>(r0 + lane) * Wp + W] = word;  // spare rows: unread
+  }
+}
+
+
+// K0, incremental (a candidate-side reuse tick whose tables this slot's last
+// run wrote): the class programs, atoms outside the changed word columns and
+// every unmoved threshold are those the tables were built from, so only the
+// word columns holding changed spot nodes (k0_cols) are recomputed, in every
+// S row (lanes = classes) and T row (lanes = rows), and the T rows whose
+// threshold moved (k0_rows) whole (lanes = words).  Waves [0, s_waves): S
+// columns; then t_waves (dimension, 64-row group) waves; then one wave per
+// moved row.
+__global__ __launch_bounds__(256) void k0_incremental(DevWorkload w, int s_waves, int t_waves,
+                                                      int local_first_fallback) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  k0_common(w, local_first_fallback, wave, lane);
+  const int wv = static_cast<int>(blockIdx.x) * 4 + wave;
+  const size_t Wp = static_cast<size_t>(w.Wp);
+  if (wv < s_waves) {
+    const int cls = wv * 64 + lane;
+    if (cls >= w.n_classes) return;
+    const int s_words = w.s_head_only ? min(w.Wp, kSHead) : w.Wp;
+    const int4* p8 = reinterpret_cast<const int4*>(w.cls_prog8 + static_cast<size_t>(cls) * 8);
+    const int4 a = p8[0], b = p8[1];
+    const int op[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    for (int c = 0; c < w.n_k0_cols; ++c) {
+      const int W = w.k0_cols[c];
+      if (W >= s_words) continue;
+      uint64_t acc;
+      if (op[0] == -2) {  // a long program, read through cls_prog_off
+        acc = ~0ull;
+        uint64_t any = 0, cur = 0;
+        bool has = false;
+        for (int o = w.cls_prog_off[cls]; o < w.cls_prog_off[cls + 1]; ++o) {
+          const int x = w.cls_prog[o];
+          const uint64_t v = w.atoms[static_cast<size_t>(x >> 2) * Wp + W];
+          switch (x & 3) {
+            case PROG_AND: acc &= v; break;
+            case PROG_ANDNOT: acc &= ~v; break;
+            case PROG_TERM_START:
+              any |= has ? cur : 0;
+              cur = v;
+              has = true;
+              break;
+            default: cur &= v; break;
+          }
+        }
+        if (has) acc &= any | cur;
+      } else {
+        uint64_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = op[u] >= 0 ? w.atoms[static_cast<size_t>(op[u] >> 2) * Wp + W] : 0;
+        acc = eval_prog8(op, v);
+      }
+      w.S[static_cast<size_t>(cls) * Wp + W] = acc;
+    }
+    return;
+  }
+  int tw = wv - s_waves;
+  if (tw < t_waves) {
+    int d = 1;  // row 0 (every node) never changes
+    for (; d < 4; ++d) {
+      const int waves_d = (w.t_off[d + 1] - w.t_off[d] + 63) / 64;
+      if (tw < waves_d) break;
+      tw -= waves_d;
+    }
+    if (d == 4) return;  // wave-uniform
+    const int r0 = w.t_off[d] + 64 * tw;
+    const int nr = min(64, w.t_off[d + 1] - r0);
+    const int64_t thr = lane < nr ? w.t_thr[r0 + lane] : INT64_MAX;
+    for (int c = 0; c < w.n_k0_cols; ++c) {
+      const int W = w.k0_cols[c];
+      const uint64_t fv = static_cast<uint64_t>(free_of(w, d, 64 * W + lane));
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) lo |= static_cast<uint32_t>(static_cast<int64_t>(readlane64(fv, i)) >= thr) << i;
+#pragma unroll
+      for (int i = 0; i < 32; ++i)
+        hi |= static_cast<uint32_t>(static_cast<int64_t>(readlane64(fv, 32 + i)) >= thr) << i;
+      if (lane < nr && thr != kTPad) w.T[static_cast<size_t>(r0 + lane) * Wp + W] = static_cast<uint64_t>(hi) << 32 | lo;
+    }
+    return;
+  }
+  const int mr = tw - t_waves;
+  if (mr >= w.n_k0_rows) return;
+  const int row = w.k0_rows[mr];
+  const int d = row < w.t_off[2] ? 1 : row < w.t_off[3] ? 2 : 3;
+  const int64_t thr = w.t_thr[row];
+  for (int W = lane; W < w.Wp; W += 64) {
+    uint64_t word = 0;
+    for (int i = 0; i < 64; ++i) word |= static_cast<uint64_t>(free_of(w, d, 64 * W + i) >= thr) << i;
+    w.T[static_cast<size_t>(row) * Wp + W] = word;
   }
 }
 
@@ -2011,6 +2117,15 @@ hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hip
   int t_waves = 0;
   for (int d = 0; d < 4; ++d) t_waves += (w.t_off[d + 1] - w.t_off[d] + 63) / 64 * wgroups;
   const unsigned blocks = static_cast<unsigned>(std::max(1, s_blocks + (t_waves + 3) / 4));
+  if (w.k0_inc) {
+    const int s_waves = w.n_k0_cols > 0 ? (w.n_classes + 63) / 64 : 0;
+    int tw = 0;
+    for (int d = 1; d < 4 && w.n_k0_cols > 0; ++d) tw += (w.t_off[d + 1] - w.t_off[d] + 63) / 64;
+    const int waves = s_waves + tw + w.n_k0_rows;
+    launch(k0_incremental, dim3(static_cast<unsigned>(std::max(1, (waves + 3) / 4))), dim3(256), 0, s, ev0, ev1, w,
+           s_waves, tw, local_first_fallback);
+    return hipGetLastError();
+  }
   launch(k0_tables, dim3(blocks), dim3(256), 0, s, ev0, ev1, w, s_blocks, local_first_fallback);
   return hipGetLastError();
 }

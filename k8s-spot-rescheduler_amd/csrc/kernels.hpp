@@ -33,6 +33,10 @@ struct DevWorkload {
   int32_t n_node_patch;        //   node section holds; K0 writes them there (T rows use them directly)
   const uint64_t* pod_patch;   // [n_pod_patch][kPodPatchU64]: row words of the pod records a candidate-side
   int32_t n_pod_patch;         //   reuse encode re-pointed (K0 writes them into pod_rec for K2)
+  int32_t k0_inc;              // K0 rewrites only the word columns k0_cols of every row and the rows k0_rows
+  int32_t n_k0_cols, n_k0_rows;  //   whole (the tables hold this candidate generation's rows otherwise current)
+  const int32_t* k0_cols;
+  const int32_t* k0_rows;
   int32_t n_atoms;
   const uint64_t* atoms;       // [n_atoms][Wp] node bitsets (encode.cpp)
   const int32_t* cls_prog_off; // class atom programs (CSR): ops atom << 2 | {AND, AND NOT,

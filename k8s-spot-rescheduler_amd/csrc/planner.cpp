@@ -80,6 +80,10 @@ struct Slot {
   uint64_t host_cand_gen = ~0ull;   // ... and the staging arena
   bool patch_pending = false;       // a prepare left node patches for K0 that no run has applied yet
   bool pod_patch_pending = false;   // ... pod patches
+  DevBuf tables;                    // S and T rows (K0 writes, K2 reads)
+  uint64_t tables_cand_gen = ~0ull; // candidate generation, encoder state and thresholds of the last K0 run
+  uint64_t tables_state_gen = ~0ull;  //   on `tables` (incremental K0: the rows only need the changes since)
+  std::vector<int64_t> tables_thr;
   uint64_t key = 0;                 // fingerprint of the input it was last prepared for
   uint64_t used = 0;                // clock of its last prepare (least recently used is replaced)
 };
@@ -90,7 +94,7 @@ struct sr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  DevBuf tables, out_node, out_status, out_bytes, dmin, prof, scratch;
+  DevBuf out_node, out_status, out_bytes, dmin, prof, scratch;
   HostBuf h_result, h_status, h_node, h_bytes;
   HostBuf h_early;           // mapped: K2's per-candidate result words (single-rank runs)
   HostBuf h_comm;            // pinned: the reduced words of a caller-provided collective
@@ -103,6 +107,8 @@ struct sr_ctx {
   Slot* cur = nullptr;       // the slot of the last prepare
   uint64_t slot_clock = 0;
   std::vector<uint64_t> node_patch_words;  // this call's node patches (prepare)
+  std::vector<int32_t> k0_cols, k0_rows;   // this call's incremental K0 (prepare)
+  int32_t k0_incremental = 1;  // SR_K0_INCREMENTAL=0: K0 always rewrites every row
   sr::EncoderCache enc;      // what the encoder keeps across calls (encode.cpp)
   hipEvent_t ev_upload = nullptr;  // the last upload (a staging buffer is reused after it)
   int32_t prefix_batch = 16;       // first batch of sr_plan_first (SR_PREFIX_BATCH; tools/gpu_prefix.sh)
@@ -338,6 +344,29 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   }
   const size_t o_np = patch.empty() ? 0 : pk.add(patch);
   const size_t o_pp = w.pod_patch.empty() ? 0 : pk.add(w.pod_patch);
+  // Incremental K0: a reuse tick whose slot tables hold this candidate
+  // generation at the state the encoder patched from (or the current one)
+  // rewrites the word columns of the changed nodes and the T rows whose
+  // threshold moved; anything else rewrites every row.
+  std::vector<int32_t>& kcols = ctx->k0_cols;
+  std::vector<int32_t>& krows = ctx->k0_rows;
+  kcols.clear();
+  krows.clear();
+  bool k0_inc = ctx->k0_incremental && w.reused && sl.tables_cand_gen == w.cand_gen &&
+                sl.tables_thr.size() == w.t_thr.size() &&
+                (sl.tables_state_gen == w.state_gen ||
+                 (E.patched_from != ~0ull && sl.tables_state_gen == E.patched_from && E.state_gen == w.state_gen));
+  if (k0_inc && sl.tables_state_gen != w.state_gen) {
+    for (int32_t i : E.patched_nodes) kcols.push_back(i >> 6);
+    std::sort(kcols.begin(), kcols.end());
+    kcols.erase(std::unique(kcols.begin(), kcols.end()), kcols.end());
+  }
+  if (k0_inc)
+    for (size_t r = 0; r < w.t_thr.size(); ++r)
+      if (w.t_thr[r] != sl.tables_thr[r] && w.t_thr[r] != sr::kTSpare) krows.push_back(static_cast<int32_t>(r));
+  if (kcols.size() > 32 || krows.size() > 256) k0_inc = false;
+  if (!k0_inc) kcols.clear(), krows.clear();
+  const size_t o_kc = kcols.empty() ? 0 : pk.add(kcols), o_kr = krows.empty() ? 0 : pk.add(krows);
   const size_t bytes = pk.size();
 
   HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -362,7 +391,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
                            !patch.empty();
   const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
-  HIP_TRY(ctx, dev_reserve(ctx->tables, n_rows * row_bytes));
+  const size_t t_cap = sl.tables.cap;
+  HIP_TRY(ctx, dev_reserve(sl.tables, n_rows * row_bytes));
+  if (sl.tables.cap != t_cap) sl.tables_cand_gen = ~0ull;  // a new allocation holds no rows
   HIP_TRY(ctx, dev_reserve(ctx->out_node, sizeof(int32_t) * std::max(1, na)));
   HIP_TRY(ctx, dev_reserve(ctx->out_status, sizeof(int32_t) * std::max(1, ncand)));
   HIP_TRY(ctx, dev_reserve(ctx->out_bytes, sizeof(uint32_t) * std::max(1, ncand)));
@@ -461,7 +492,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
                     sr::kDevSpreadSlots == sr::kSpreadSlots,
                 "domain-path layout shared by encode.cpp and kernels.hip");
   for (int k = 0; k < sr::kDomKeys; ++k) d.dk_row[k] = w.dk_row[k];
-  d.S = static_cast<uint64_t*>(ctx->tables.p);
+  d.S = static_cast<uint64_t*>(sl.tables.p);
   d.T = d.S + static_cast<size_t>(w.n_classes) * w.Wp;
   d.out_node = static_cast<int32_t*>(ctx->out_node.p);
   d.out_status = static_cast<int32_t*>(ctx->out_status.p);
@@ -501,6 +532,11 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
                                                                : bytes - from);
   d.node_patch = nodes_patch ? static_cast<const uint64_t*>(at(o_np)) : nullptr;
   d.n_node_patch = nodes_patch ? static_cast<int32_t>(patch.size() / sr::kNodePatchU64) : 0;
+  d.k0_inc = k0_inc ? 1 : 0;
+  d.n_k0_cols = static_cast<int32_t>(kcols.size());
+  d.n_k0_rows = static_cast<int32_t>(krows.size());
+  d.k0_cols = kcols.empty() ? nullptr : static_cast<const int32_t*>(at(o_kc));
+  d.k0_rows = krows.empty() ? nullptr : static_cast<const int32_t*>(at(o_kr));
   const bool pods_patch = cand_resident && !w.pod_patch.empty();
   d.pod_patch = pods_patch ? static_cast<const uint64_t*>(at(o_pp)) : nullptr;
   d.n_pod_patch = pods_patch ? static_cast<int32_t>(w.pod_patch.size() / sr::kPodPatchU64) : 0;
@@ -513,6 +549,14 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const uint64_t s_row = d.s_head_only ? static_cast<uint64_t>(std::min(w.Wp, 8)) * 8 : row;  // S words K0 writes
   ctx->t.bytes_tables = static_cast<uint64_t>(w.n_classes) * s_row + w.t_dim.size() * row + atom_reads * s_row +
                         3ull * 8 * w.n_pad + 32ull * w.n_classes;
+  if (k0_inc) {  // the changed columns of every row (S columns inside the written head), the moved rows whole
+    const int32_t s_words = d.s_head_only ? std::min(w.Wp, 8) : w.Wp;
+    uint64_t s_cols = 0;
+    for (int32_t col : kcols) s_cols += col < s_words ? 1 : 0;
+    ctx->t.bytes_tables = (static_cast<uint64_t>(w.n_classes) + atom_reads) * 8 * s_cols +
+                          (32ull * w.n_classes) * (s_cols > 0 ? 1 : 0) + w.t_dim.size() * 8 * kcols.size() +
+                          3ull * 64 * 8 * kcols.size() + krows.size() * (row + 8ull * w.n_pad);
+  }
   // K2: counted by the kernel itself per candidate (out_bytes), read back by
   // the next run with status or node_of_pod outputs
   ctx->t.bytes_placement = 0;
@@ -533,6 +577,8 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   ctx->t.enc_memo_pods = ctx->enc.last_memo_hits;
   ctx->t.enc_reused = ctx->enc.last_reused;
   ctx->t.enc_pod_patches = ctx->enc.last_pod_patches;
+  ctx->t.k0_columns = k0_inc ? static_cast<int32_t>(kcols.size()) : -1;
+  ctx->t.k0_rows_moved = static_cast<int32_t>(krows.size());
   ctx->prepared = true;
   return SR_OK;
 }
@@ -659,8 +705,12 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   } while (0)
   PAIR(0, e0a, e0b);
   HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
-  ctx->cur->patch_pending = false;  // K0 writes the node and pod patches (idempotent on later runs)
-  ctx->cur->pod_patch_pending = false;
+  Slot& sl = *ctx->cur;
+  sl.patch_pending = false;  // K0 writes the node and pod patches (idempotent on later runs)
+  sl.pod_patch_pending = false;
+  sl.tables_cand_gen = w.cand_gen;  // and brings the rows to this workload (a rerun: idempotent)
+  sl.tables_state_gen = w.state_gen;
+  if (sl.tables_thr != w.t_thr) sl.tables_thr = w.t_thr;
   PAIR(1, e1a, e1b);
   if (early) {
     d.res_stat = ctx->d_early;
@@ -813,6 +863,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* b = std::getenv("SR_PREFIX_BATCH")) ctx->prefix_batch = std::max(1, std::atoi(b));
   if (const char* m = std::getenv("SR_K2_WPB")) ctx->k2_wpb = std::atoi(m);
   if (const char* m = std::getenv("SR_PLAN_SLOTS")) ctx->n_slots = std::max(1, std::min(16, std::atoi(m)));
+  if (const char* m = std::getenv("SR_K0_INCREMENTAL")) ctx->k0_incremental = std::atoi(m) != 0;
   *out = ctx;
   return SR_OK;
 }
@@ -822,7 +873,7 @@ void sr_destroy(sr_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) (void)rccl().comm_destroy(ctx->comm);
-  for (DevBuf* b : {&ctx->tables, &ctx->out_node, &ctx->out_status, &ctx->out_bytes, &ctx->dmin, &ctx->prof,
+  for (DevBuf* b : {&ctx->out_node, &ctx->out_status, &ctx->out_bytes, &ctx->dmin, &ctx->prof,
                     &ctx->scratch})
     if (b->p) (void)hipFree(b->p);
   if (ctx->ev_upload) (void)hipEventDestroy(ctx->ev_upload);
@@ -830,6 +881,7 @@ void sr_destroy(sr_ctx* ctx) {
     if (b->p) (void)hipHostFree(b->p);
   for (auto& sl : ctx->slots) {
     if (sl->arena.p) (void)hipFree(sl->arena.p);
+    if (sl->tables.p) (void)hipFree(sl->tables.p);
     if (sl->h_arena.p) (void)hipHostFree(sl->h_arena.p);
   }
   for (auto* v : {&ctx->ev_start, &ctx->ev_end})

@@ -145,7 +145,8 @@ class sr_timing(ctypes.Structure):
                 ("n_classes", ctypes.c_int32), ("bytes_uploaded", ctypes.c_uint64), ("enc_new_specs", ctypes.c_int32),
                 ("enc_static_rebuilt", ctypes.c_int32), ("enc_state_nodes", ctypes.c_int32),
                 ("prefix_batches", ctypes.c_int32), ("enc_memo_pods", ctypes.c_int32),
-                ("enc_reused", ctypes.c_int32), ("enc_pod_patches", ctypes.c_int32)]
+                ("enc_reused", ctypes.c_int32), ("enc_pod_patches", ctypes.c_int32),
+                ("k0_columns", ctypes.c_int32), ("k0_rows_moved", ctypes.c_int32)]
 
 
 def ptr(arr, typ):

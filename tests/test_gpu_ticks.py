@@ -195,7 +195,7 @@ def test_ticks_candidate_side_reuse():
         cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
         n_rec_bytes = int(cand_off[-1]) * 48
         rng = np.random.default_rng(9)
-        extra, patched, reused = [], 0, 0
+        extra, patched, reused, k0_cols = [], 0, 0, 0
         for tick in range(16):
             h = _snapshot(lib, sc, nm)
             osnap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
@@ -223,12 +223,15 @@ def test_ticks_candidate_side_reuse():
             assert p.winner == o["winner"], tick
             if tick >= 2:
                 assert t.enc_reused == 1, (tick, t.enc_reused)
+                if tick not in (6, 9, 10):  # K0 on the changed word columns only (the slot's tables are current)
+                    assert t.k0_columns >= 0, (tick, t.k0_columns)
+                    k0_cols += t.k0_columns
                 reused += 1
                 patched += t.enc_pod_patches
                 if tick != 6:  # the records stay on the device: the copy holds atoms, thresholds and patches
                     assert t.bytes_uploaded < n_rec_bytes // 4, (tick, t.bytes_uploaded, n_rec_bytes)
             lib.sr_snapshot_destroy(h)
-        assert reused == 14 and patched > 0, (reused, patched)
+        assert reused == 14 and patched > 0 and k0_cols > 0, (reused, patched, k0_cols)
     finally:
         ck.close()
 
