@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -449,8 +450,31 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
     }
   }
   for (const std::string& str : s->strings) s->str_label.push_back(label_flags(str));
+  // Stamps (sr_cluster.pod_stamp): the generation is a function of the
+  // parameters, so (parameters, pod index) names the pod's content; two
+  // clusters of different parameters never share a stamp.
+  uint64_t h = 0xCBF29CE484222325ull;
+  auto fold = [&](uint64_t x) { h = (h ^ x) * 0x100000001B3ull; };
+  if (prm) {  // field by field (the struct has padding)
+    auto bits = [](double d) {
+      uint64_t u;
+      std::memcpy(&u, &d, sizeof(u));
+      return u;
+    };
+    fold(static_cast<uint64_t>(prm->config));
+    fold(prm->seed);
+    fold(static_cast<uint64_t>(prm->n_on_demand));
+    fold(static_cast<uint64_t>(prm->n_spot));
+    for (double d : {prm->pinned_fraction, prm->stateful_fraction, prm->init_fraction, prm->gpu_fraction}) fold(bits(d));
+  }
   s->stamp.resize(s->pod_node.size());
-  for (size_t i = 0; i < s->stamp.size(); ++i) s->stamp[i] = 0x5EED000000000000ull + i + 1;
+  for (size_t i = 0; i < s->stamp.size(); ++i) {
+    uint64_t x = h ^ (0x9E3779B97F4A7C15ull * (i + 1));
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    s->stamp[i] = x | 1;  // never 0 (unknown)
+  }
   return s;
 }
 

@@ -325,10 +325,11 @@ def test_ticks_with_pod_stamps(checker, seed):
                 changed.append((ci, pi))
     n_spot_pods = sum(len(ps) for ps in spot_pods)
 
-    def stamps_of(version, flat_len):
-        base = [1000 + i for i in range(n_spot_pods)]
+    def stamps_of(version, flat_len):  # distinct per seed: the planner is shared by the session's tests
+        tag = (seed + 1) << 40
+        base = [tag + 1000 + i for i in range(n_spot_pods)]
         flat = [(ci, pi) for ci, c in enumerate(cands) for pi in range(len(c))]
-        return base + [(5000 if version and k in changed else 3000) + i for i, k in enumerate(flat)][:flat_len]
+        return base + [tag + (5000 if version and k in changed else 3000) + i for i, k in enumerate(flat)][:flat_len]
 
     interner = Interner()  # one string dictionary per process: the stamps' contract
     for version in (0, 1, 0, 1, 1, 0):
