@@ -13,6 +13,7 @@
 
 #include <cstdint>
 #include <utility>
+#include <vector>
 
 namespace sr {
 
@@ -23,6 +24,25 @@ class GoSlice {
   GoSlice(T* data, Less less) : d_(data), less_(less) {}
 
   void sort(int n) { quick(0, n, max_depth(n)); }
+
+  // A span of quickSort_func's recursion: quick(a, b, depth) sorts it exactly
+  // as the serial sort would, independently of every other span.
+  struct Span {
+    int a, b, depth;
+  };
+  // One partition step of quick() on a span longer than `grain` (the same
+  // pivot, the same swaps): its two sub-spans, or the span itself when the
+  // serial sort would finish it here (short, or at depth 0: heapsort).
+  void split(const Span& s, int grain, Span* lo, Span* hi, bool* leaf) {
+    *leaf = s.b - s.a <= grain || s.depth == 0;
+    if (*leaf) return;
+    const int depth = s.depth - 1;
+    auto [mlo, mhi] = pivot(s.a, s.b);
+    *lo = Span{s.a, mlo, depth};
+    *hi = Span{mhi, s.b, depth};
+  }
+  void finish(const Span& s) { quick(s.a, s.b, s.depth); }
+  static int depth_of(int n) { return max_depth(n); }
 
  private:
   T* d_;
@@ -154,6 +174,44 @@ class GoSlice {
 template <class T, class Less>
 inline void go_sort_slice(T* data, int n, Less less) {
   GoSlice<T, Less>(data, less).sort(n);
+}
+
+// The same sort with the recursion's independent spans on a thread pool:
+// partition steps level by level (each span's pivot and swaps are the serial
+// sort's), then the remaining spans sorted in parallel.  Identical output:
+// quickSort_func sorts the two sides of a pivot independently, and the side it
+// recurses into first only changes its stack depth.
+// par(n, fn): runs fn(i) for i in [0, n), in any order or concurrently.
+template <class T, class Less, class Par>
+inline void go_sort_slice_parallel(T* data, int n, Less less, Par par, int grain = 4096) {
+  using S = GoSlice<T, Less>;
+  using Span = typename S::Span;
+  if (n <= 2 * grain) {
+    S(data, less).sort(n);
+    return;
+  }
+  std::vector<Span> level{Span{0, n, S::depth_of(n)}}, leaves;
+  while (!level.empty() && leaves.size() < 256) {
+    std::vector<Span> lo(level.size()), hi(level.size());
+    std::vector<char> leaf(level.size());
+    par(static_cast<int>(level.size()), [&](int i) {
+      bool lf = false;
+      S(data, less).split(level[static_cast<size_t>(i)], grain, &lo[static_cast<size_t>(i)], &hi[static_cast<size_t>(i)], &lf);
+      leaf[static_cast<size_t>(i)] = lf;
+    });
+    std::vector<Span> next;
+    for (size_t i = 0; i < level.size(); ++i) {
+      if (leaf[i]) {
+        leaves.push_back(level[i]);
+      } else {
+        next.push_back(lo[i]);
+        next.push_back(hi[i]);
+      }
+    }
+    level.swap(next);
+  }
+  leaves.insert(leaves.end(), level.begin(), level.end());
+  par(static_cast<int>(leaves.size()), [&](int i) { S(data, less).finish(leaves[static_cast<size_t>(i)]); });
 }
 
 }  // namespace sr

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "gosort.hpp"
@@ -98,7 +99,11 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   }
 
   const int64_t* cpu = P.cpu_sort_milli;
-  auto by_cpu_desc = [cpu](int32_t x, int32_t y) { return cpu[x] > cpu[y]; };
+  // the reference's less functions (nodes/nodes.go:76-80, 95-101) on (key, id) pairs: the same
+  // comparisons, so Go's sort makes the same swaps
+  using KV = std::pair<int64_t, int32_t>;
+  auto by_key_desc = [](const KV& x, const KV& y) { return x.first > y.first; };
+  auto by_key_asc = [](const KV& x, const KV& y) { return x.first < y.first; };
   // Per node (independent, on the pool): the spot / on-demand test, the
   // priority filter of getPodsOnNode, RequestedCPU and the pod sort.  Pass 1
   // counts the kept pods, pass 2 writes them at their prefix offsets.
@@ -123,20 +128,22 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   if (nil_priority.load()) return SR_ERR_NIL_PRIORITY;
   for (int32_t node = 0; node < nn; ++node) nkept[node + 1] += nkept[node];
   parallel_for(static_cast<size_t>(nn), 64, [&](size_t lo, size_t hi) {
+    std::vector<std::pair<int64_t, int32_t>> kv;  // (cpu, pod): the sort compares keys held in place
     for (size_t node = lo; node < hi; ++node) {
       const bool spot = kind[node] == 1;
-      int32_t kept = nkept[node];
-      out->node_pod_off[node] = kept;
+      out->node_pod_off[node] = nkept[node];
       int64_t requested = 0;
+      kv.clear();
       for (int32_t j = start[node]; j < start[node + 1]; ++j) {
         const int32_t pod = listed[j];
         if (P.priority[pod] < p->priority_threshold && spot) continue;
-        out->node_pod_idx[kept++] = pod;
+        kv.emplace_back(cpu[pod], pod);
         requested += cpu[pod];
       }
       out->requested_cpu[node] = requested;
       out->free_cpu[node] = N.alloc_milli_cpu[node] - requested;
-      go_sort_slice(out->node_pod_idx + nkept[node], kept - nkept[node], by_cpu_desc);
+      go_sort_slice(kv.data(), static_cast<int>(kv.size()), by_key_desc);
+      for (size_t k = 0; k < kv.size(); ++k) out->node_pod_idx[nkept[node] + static_cast<int32_t>(k)] = kv[k].second;
     }
   });
   int32_t ns = 0, nod = 0;
@@ -148,8 +155,18 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   }
   out->node_pod_off[nn] = nkept[nn];
   const int64_t* req = out->requested_cpu;
-  go_sort_slice(out->spot, ns, [req](int32_t x, int32_t y) { return req[x] > req[y]; });
-  go_sort_slice(out->on_demand, nod, [req](int32_t x, int32_t y) { return req[x] < req[y]; });
+  auto par = [](int n, const std::function<void(int)>& fn) {
+    parallel_for(static_cast<size_t>(n), 1, [&](size_t a, size_t b) {
+      for (size_t i = a; i < b; ++i) fn(static_cast<int>(i));
+    });
+  };
+  std::vector<KV> kv_spot(static_cast<size_t>(ns)), kv_od(static_cast<size_t>(nod));
+  for (int32_t i = 0; i < ns; ++i) kv_spot[i] = KV(req[out->spot[i]], out->spot[i]);
+  for (int32_t i = 0; i < nod; ++i) kv_od[i] = KV(req[out->on_demand[i]], out->on_demand[i]);
+  go_sort_slice_parallel(kv_spot.data(), ns, by_key_desc, par);
+  go_sort_slice_parallel(kv_od.data(), nod, by_key_asc, par);
+  for (int32_t i = 0; i < ns; ++i) out->spot[i] = kv_spot[i].second;
+  for (int32_t i = 0; i < nod; ++i) out->on_demand[i] = kv_od[i].second;
   *out->n_spot = ns;
   *out->n_on_demand = nod;
   return SR_OK;
@@ -296,17 +313,23 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
   s->node_sfp.resize(n_spot);
   s->node_dfp.resize(n_spot);
   const sr_nodes& N = c->nodes;
-  for (int32_t i = 0; i < n_spot; ++i) {  // validate first: the build below cannot fail
-    const int32_t node = spot[i];
-    if (node < 0 || node >= N.n) {
-      delete s;
-      return SR_ERR_INVALID_ARG;
-    }
-    for (int32_t j = off[node]; j < off[node + 1]; ++j)
-      if (idx[j] < 0 || idx[j] >= c->pods.n) {
-        delete s;
-        return SR_ERR_INVALID_ARG;
+  std::atomic<bool> bad{false};  // validate first: the build below cannot fail
+  parallel_for(static_cast<size_t>(n_spot), 512, [&](size_t lo, size_t hi) {
+    const int32_t np = c->pods.n, nn = N.n;
+    bool b = false;
+    for (size_t i = lo; i < hi && !b; ++i) {
+      const int32_t node = spot[i];
+      if (node < 0 || node >= nn) {
+        b = true;
+        break;
       }
+      for (int32_t j = off[node]; j < off[node + 1]; ++j) b |= static_cast<uint32_t>(idx[j]) >= static_cast<uint32_t>(np);
+    }
+    if (b) bad.store(true, std::memory_order_relaxed);
+  });
+  if (bad.load()) {
+    delete s;
+    return SR_ERR_INVALID_ARG;
   }
   // the snapshot's pod store: the pods of spot node i at [base[i], base[i + 1])
   std::vector<int32_t> base(static_cast<size_t>(n_spot) + 1, 0);

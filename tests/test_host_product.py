@@ -218,6 +218,21 @@ def test_product_new_node_map_matches_oracle(config):
     assert np.all(np.diff(off) >= 0)
 
 
+def test_product_new_node_map_parallel_sort_matches_oracle():
+    """Pools above 8,192 nodes: the product sorts the spot and on-demand
+    lists (nodes/nodes.go:95-101) with Go's quickSort_func split over a thread
+    pool (gosort.hpp go_sort_slice_parallel); tie-heavy RequestedCPU sums must
+    still come out in the serial sort's exact order."""
+    sc = SynthCluster(3, seed=41, n_on_demand=9000, n_spot=12000)
+    lib = capi.load_planner()
+    prod = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    orc = oracle_new_node_map(sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    assert len(prod.spot) > 8192 and len(prod.on_demand) > 8192
+    assert len(np.unique(prod.requested_cpu[prod.spot])) < len(prod.spot) // 2  # ties everywhere
+    for f in ("spot", "on_demand", "node_pod_off", "node_pod_idx", "requested_cpu"):
+        assert np.array_equal(getattr(prod, f), getattr(orc, f)), f
+
+
 def test_product_new_node_map_priority_threshold_matches_oracle():
     sc = SynthCluster(3, n_on_demand=200, n_spot=400)
     lib = capi.load_planner()
