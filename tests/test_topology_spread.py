@@ -111,6 +111,15 @@ def cases():
            [[spread(Pod("p", namespace="default", containers=[Container(cpu_milli=100)], labels={"app": "web"},
                         required_node_affinity=[NodeSelectorTerm([NodeSelectorRequirement(Z, "In", ["z1"])])]),
                     zc())]], [OK], [[0]])
+    # v1.19.2 calPreFilterState: the pairs come from the nodes passing the pod's
+    # node affinity, but processNode then counts the matching pods of EVERY node
+    # whose value names an existing pair.  p refuses node a by affinity, yet e on
+    # a counts into (zone, z1): z1 = 1, z2 = 0, so b (1 + 1 - 0 > 1) fails and c
+    # is the first fit.  (Counting only passing nodes would give z1 = 0 and b.)
+    yield ("pods_on_node_failing_affinity_still_counted", N(), [[web("e")], [], [], []],
+           [[spread(Pod("p", namespace="default", containers=[Container(cpu_milli=100)], labels={"app": "web"},
+                        required_node_affinity=[NodeSelectorTerm([NodeSelectorRequirement(H, "NotIn", ["a"])])]),
+                    zc())]], [OK], [[2]])
     yield ("no_pairs_pass_every_node", N(), [[web("e"), web("f")], [], [], []],
            [[spread(web("p"), zc(key="example.com/rack"))]], [OK], [[0]])
     yield ("nil_selector_counts_nothing", N(), [[web("e"), web("f")], [], [], []],
