@@ -378,9 +378,11 @@ def main():
         assert lib.sr_plan_prepare(checker.handle, snap, sc.ptr, ctypes.byref(cands)) == capi.SR_OK
         tq = checker.timing()
         mutation = (mut_pod, mut_pos)
+        k0 = ("none: the tables stand, K2 recomputes the changed node's bits (K0 runs once 16 nodes changed)"
+              if tq.k0_columns == -2 else "every row" if tq.k0_columns == -1 else
+              "incremental: %d word columns, %d moved threshold rows" % (tq.k0_columns, tq.k0_rows_moved))
         steady = {"tick": "steady: the previous tick's candidate input, one more pod on spot node %d" % mut_pos,
-                  "candidate_side_reused": bool(tq.enc_reused), "pod_patches": int(tq.enc_pod_patches),
-                  "k0": "incremental (changed word columns, moved threshold rows)" if tq.enc_reused else "every row"}
+                  "candidate_side_reused": bool(tq.enc_reused), "pod_patches": int(tq.enc_pod_patches), "k0": k0}
     # one run with per-candidate outputs first: K2's byte counts and the
     # reference-equivalent check count of this workload's plan
     status = np.zeros(max(1, len(loff) - 1), np.int32)

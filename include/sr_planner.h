@@ -580,8 +580,10 @@ typedef struct {
   int32_t  enc_reused;         /* 1: the last prepare kept the candidate side of the call before (same stamped
                                 * candidate input; ABI 6), updating only capacity-dependent rows and records */
   int32_t  enc_pod_patches;    /* ... and re-pointed this many pod records (uploaded as patches) */
-  int32_t  k0_columns;         /* word columns K0 rewrites for the last prepare (-1: every row; ABI 6) */
+  int32_t  k0_columns;         /* word columns K0 rewrites for the last prepare (-1: every row; -2: no K0, the
+                                * tables stand and K2 recomputes the changed nodes' bits; ABI 6) */
   int32_t  k0_rows_moved;      /* ... and threshold rows it rewrites whole */
+  int32_t  k0_dirty_nodes;     /* no K0: spot nodes changed since the tables were written */
 } sr_timing;
 /* mask: which kernels sr_plan_run brackets with HIP events (resets the sums):
  * 1 = K0, 2 = K2, 4 = collective (multi-GPU) + K3; 0 = no events.  Events are read back lazily, by

@@ -1150,6 +1150,7 @@ bool reuse_encode(EncoderCache& C, Workload* w) {
     R.epoch = 1;
   }
   w->pod_patch.clear();
+  w->class_flip = false;
   const uint64_t Wp64 = static_cast<uint64_t>(Wp);
   auto off = [&](int32_t table_row) { return static_cast<uint64_t>(table_row) * Wp64; };
   auto repoint = [&](int32_t q) {
@@ -1166,6 +1167,7 @@ bool reuse_encode(EncoderCache& C, Workload* w) {
       }
     if (dead) cls = w->empty_class;
     int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
+    if (r[0] != cls) w->class_flip = true;
     r[0] = cls;
     for (int d = 0; d < 3; ++d) r[1 + d] = row[d];
     uint64_t* rec = &w->pod_rec[static_cast<size_t>(q) * 6];

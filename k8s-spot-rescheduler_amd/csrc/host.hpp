@@ -412,6 +412,7 @@ struct Workload {
   // cand_gen; a reuse encode keeps them and lists the pod records it changed
   uint64_t cand_gen = 0;
   bool reused = false;
+  bool class_flip = false;          // a reuse encode moved some pod to or from the empty class
   std::vector<uint64_t> pod_patch;  // [n][kPodPatchWords] {active pod, rec[4], rec[5]} (reuse encodes)
   CandReuse reuse;                  // kept by reset(): the encoder rebuilds or drops it
 
@@ -441,6 +442,7 @@ struct Workload {
     fallback_pods = 0;
     n_input_cand = n_input_pods = pod_base = 0;
     reused = false;
+    class_flip = false;
     pod_patch.clear();
   }
 };

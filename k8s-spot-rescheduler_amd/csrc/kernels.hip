@@ -862,6 +862,17 @@ __device__ __forceinline__ uint64_t f_word_far(const uint64_t* __restrict__ tab,
          tab[static_cast<uint32_t>(r23) + wd] & tab[static_cast<uint32_t>(r23 >> 32) + wd];
 }
 
+// The S part alone, from the lane's class program (s_head_only).
+__device__ __forceinline__ uint64_t f_word_prog_s(const DevWorkload& w, const int32_t* pg, int wd) {
+  int op[8];
+  uint64_t v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) op[u] = pg[u];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = op[u] >= 0 ? w.atoms[static_cast<size_t>(op[u] >> 2) * w.Wp + wd] : 0ull;
+  return eval_prog8(op, v);
+}
+
 // The same word with the S part evaluated from the lane's class program (in
 // LDS) when K0 wrote only the heads of the S rows (s_head_only).
 __device__ __forceinline__ uint64_t f_word_prog(const DevWorkload& w, const uint64_t* __restrict__ tab,
@@ -874,6 +885,41 @@ __device__ __forceinline__ uint64_t f_word_prog(const DevWorkload& w, const uint
   for (int u = 0; u < 8; ++u) v[u] = op[u] >= 0 ? w.atoms[static_cast<size_t>(op[u] >> 2) * w.Wp + wd] : 0ull;
   return eval_prog8(op, v) & tab[static_cast<uint32_t>(r01 >> 32) + wd] & tab[static_cast<uint32_t>(r23) + wd] &
          tab[static_cast<uint32_t>(r23 >> 32) + wd];
+}
+
+// A K0-less run (k0_skip): the T rows predate the changes of the spot nodes
+// in node_patch, so their bits of an F word (S & T rows) are recomputed from
+// the S word and the nodes' current free values (fitsRequest per dimension;
+// an all-zero request skips it).  Every other node's T bits stand: its free
+// value is the one the rows were built from, and no node value then lay
+// between a request and its row's threshold.
+__device__ __forceinline__ uint64_t fix_dirty(const DevWorkload& w, uint64_t f, uint64_t s, int wd, int64_t rc,
+                                              int64_t rm, int64_t re, bool zero) {
+  for (int p = 0; p < w.n_node_patch; ++p) {
+    const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
+    const int n = static_cast<int>(pr[0]);
+    if ((n >> 6) != wd) continue;
+    const uint64_t bit = 1ull << (n & 63);
+    const bool fits = zero || (static_cast<int64_t>(pr[9]) >= rc && static_cast<int64_t>(pr[10]) >= rm &&
+                               static_cast<int64_t>(pr[11]) >= re);
+    f = fits ? (f | (s & bit)) : (f & ~bit);
+  }
+  return f;
+}
+
+// A K0-less run: lane i's base record of window W from node_patch when node
+// 64 W + i changed since the node section was written.
+__device__ __forceinline__ void window_patch(const DevWorkload& w, int W, int lane, int64_t& ncpu, int64_t& nmem,
+                                             int64_t& neph, uint64_t& nport, int& nleft) {
+  for (int p = 0; p < w.n_node_patch; ++p) {
+    const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
+    if (static_cast<int>(pr[0]) != 64 * W + lane) continue;
+    ncpu = static_cast<int64_t>(pr[1]);
+    nmem = static_cast<int64_t>(pr[2]);
+    neph = static_cast<int64_t>(pr[3]);
+    nport = pr[4];
+    nleft = static_cast<int>(static_cast<int64_t>(pr[5]));
+  }
 }
 
 // 32-bit value of lane `src` (per-lane source index), through the LDS crossbar.
@@ -1110,6 +1156,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     neph = static_cast<int64_t>(nr[2]);
     nport = nr[3];
     nleft = static_cast<int>(static_cast<int64_t>(nr[4]));
+    if (w.k0_skip) window_patch(w, 0, lane, ncpu, nmem, neph, nport, nleft);
     wcur = 0;
     nbytes += 64u * 40u;
   }
@@ -1172,7 +1219,16 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
 #pragma unroll
         for (int h = 0; h < kPB; ++h) {
           if (b0 + kPW * h >= lim) continue;  // wave-uniform
-          const uint64_t f = (wv && kk[h] < np) ? (x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
+          uint64_t f = (wv && kk[h] < np) ? (x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
+          if (w.k0_skip) {  // the pod's requests from its lane
+            const int src = min(kk[h], np - 1) - 64 * g;
+            auto lane64 = [&](int64_t v) {
+              return static_cast<int64_t>(static_cast<uint64_t>(from_lane(static_cast<uint32_t>(v >> 32), src)) << 32 |
+                                          from_lane(static_cast<uint32_t>(v), src));
+            };
+            const int64_t qc = lane64(rc[g]), qm = lane64(rm[g]), qe = lane64(re[g]);
+            if (wv && kk[h] < np) f = fix_dirty(w, f, x[h][0], wd, qc, qm, qe, (qc | qm | qe) == 0);
+          }
           if (kk[h] < np) F[kk[h] * kNHS + wd] = f;
           const uint64_t m = ballot(f != 0);  // kNH bits per pod: bit kNH * i + word
           const int rel = 64 * g + lane - (b0 + kPW * h);
@@ -1245,6 +1301,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
           while (pend != 0) {
             int js[Q];
             uint64_t a01[Q], a23[Q];
+            int64_t qr[Q][3];
             int op[Q][8];
             uint32_t nops[Q];
 #pragma unroll
@@ -1254,6 +1311,9 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
               const int j = js[q] < 0 ? 0 : js[q];
               a01[q] = readlane64(r01[g], j);
               a23[q] = readlane64(r23[g], j);
+              qr[q][0] = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc[g]), j));
+              qr[q][1] = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm[g]), j));
+              qr[q][2] = static_cast<int64_t>(readlane64(static_cast<uint64_t>(re[g]), j));
               nops[q] = 0;
               if constexpr (HO) {  // the pod's class program (LDS, broadcast)
 #pragma unroll
@@ -1292,15 +1352,19 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
 #pragma unroll
               for (int q = 0; q < Q; ++q) {
                 if (!((todo >> q) & 1)) continue;  // wave-uniform
-                uint64_t f;
+                uint64_t f, sw0;
                 if constexpr (HO) {
                   uint64_t v8[8];
 #pragma unroll
                   for (int u = 0; u < 8; ++u) v8[u] = x[q][u];
-                  f = eval_prog8(op[q], v8) & x[q][8] & x[q][9] & x[q][10];
+                  sw0 = eval_prog8(op[q], v8);
+                  f = sw0 & x[q][8] & x[q][9] & x[q][10];
                 } else {
+                  sw0 = x[q][0];
                   f = x[q][0] & x[q][1] & x[q][2] & x[q][3];
                 }
+                if (w.k0_skip)
+                  f = fix_dirty(w, f, sw0, word, qr[q][0], qr[q][1], qr[q][2], (qr[q][0] | qr[q][1] | qr[q][2]) == 0);
                 f = wv ? f : 0ull;
                 const uint64_t m = ballot(f != 0);
                 // algorithmic bytes: the words a sequential scan reads, up to the
@@ -1349,6 +1413,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       neph = static_cast<int64_t>(nr[2]);
       nport = nr[3];
       nleft = static_cast<int>(static_cast<int64_t>(nr[4]));
+      if (w.k0_skip) window_patch(w, W, lane, ncpu, nmem, neph, nport, nleft);
       wcur = W;
       ++windows;
       nbytes += 64u * 40u;
@@ -1431,6 +1496,11 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
             const int w2 = fbase[g] + __builtin_ctzll(rem);
             cur[g] = w.s_head_only ? f_word_prog(w, tab, PG + (64 * g + lane) * 8, r01[g], r23[g], w2)
                                    : f_word_far(tab, r01[g], r23[g], w2);
+            if (w.k0_skip) {  // the S word again for the changed nodes' bits
+              const uint64_t sw0 = w.s_head_only ? f_word_prog_s(w, PG + (64 * g + lane) * 8, w2)
+                                                 : tab[static_cast<uint32_t>(r01[g]) + w2];
+              cur[g] = fix_dirty(w, cur[g], sw0, w2, rc[g], rm[g], re[g], zero[g]);
+            }
             nx = w2 * 64 + __builtin_ctzll(cur[g]);
             far_word = true;
           } else if (fbase[g] + 64 < Wp) {
@@ -1908,6 +1978,13 @@ __device__ __forceinline__ void k2_finish(const DevWorkload& w, const K2Entry& x
   const int lane = threadIdx.x & 63;
   const int ci = x.ci, p0 = x.p0, np = x.np;
   int best = 0;  // lane 0: this candidate is the first drainable one so far
+  if (lane == 0 && ci == 0) {  // once per run: the next run's first word (K0 may not run then), this run's others
+    unsigned long long* dn = reinterpret_cast<unsigned long long*>(w.d_min_next);
+    unsigned long long* dm = reinterpret_cast<unsigned long long*>(w.d_min);
+    dn[0] = ~0ull;
+    dm[1] = w.first_fallback_local < 0 ? ~0ull : static_cast<unsigned long long>(w.first_fallback_local) << 32;
+    dm[2] = w.rank_next;
+  }
   if (lane == 0) {
     w.out_status[ci] = status;
     w.out_bytes[ci] = nbytes;

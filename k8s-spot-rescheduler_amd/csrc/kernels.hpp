@@ -33,6 +33,11 @@ struct DevWorkload {
   int32_t n_node_patch;        //   node section holds; K0 writes them there (T rows use them directly)
   const uint64_t* pod_patch;   // [n_pod_patch][kPodPatchU64]: row words of the pod records a candidate-side
   int32_t n_pod_patch;         //   reuse encode re-pointed (K0 writes them into pod_rec for K2)
+  int32_t k0_skip;             // no K0 this run: the tables and the node section are those of the slot's device
+                               //   generation; node_patch lists every spot node changed since (K2 takes their
+                               //   records from it and recomputes their bits of T rows, skip_mode: DESIGN §4)
+  int32_t* d_min_next;         // the next run's d_min buffer (runs alternate): K2 resets its first word
+  int32_t first_fallback_local;  // d_min[1] of the run (K2 sets it too: K0 may not run)
   int32_t k0_inc;              // K0 rewrites only the word columns k0_cols of every row and the rows k0_rows
   int32_t n_k0_cols, n_k0_rows;  //   whole (the tables hold this candidate generation's rows otherwise current)
   const int32_t* k0_cols;

@@ -76,14 +76,24 @@ struct Slot {
   HostBuf h_arena;
   uint64_t dev_state_gen = ~0ull;   // encoder state whose node records the device arena holds
   uint64_t host_state_gen = ~0ull;  // ... and the pinned staging arena
-  uint64_t dev_cand_gen = ~0ull;    // candidate generation (Workload::cand_gen) the device arena holds
-  uint64_t host_cand_gen = ~0ull;   // ... and the staging arena
-  bool patch_pending = false;       // a prepare left node patches for K0 that no run has applied yet
-  bool pod_patch_pending = false;   // ... pod patches
+  uint64_t dev_cand_gen = ~0ull;    // candidate generation (Workload::cand_gen) the device arena holds (its
+                                    //   pod records as of the last K0 run plus none of the pending patches)
+  uint64_t host_cand_gen = ~0ull;   // ... and the staging arena (every patch applied)
   DevBuf tables;                    // S and T rows (K0 writes, K2 reads)
-  uint64_t tables_cand_gen = ~0ull; // candidate generation, encoder state and thresholds of the last K0 run
-  uint64_t tables_state_gen = ~0ull;  //   on `tables` (incremental K0: the rows only need the changes since)
+  uint64_t tables_cand_gen = ~0ull; // candidate generation, encoder state, thresholds and atoms of the last K0
+  uint64_t tables_state_gen = ~0ull;  //   run on `tables` (incremental K0 / K0-less runs: what changed since)
   std::vector<int64_t> tables_thr;
+  std::vector<uint64_t> tables_atoms;
+  // spot nodes changed since tables_state_gen (valid: every state step since was one the encoder patched)
+  std::vector<int32_t> dirty;
+  bool dirty_valid = false;
+  uint64_t seen_gen = ~0ull;        // encoder state at the slot's last prepare
+  std::vector<int32_t> pending;     // pods re-pointed since the last K0 run (their device records are older)
+  std::vector<uint8_t> pending_mark;
+  bool class_flip = false;          // ... some of them to or from the empty class
+  // what the next K0 launch of this slot brings the tables and the node section to (run() commits it)
+  bool commit_k0 = false;
+  bool need_k0 = true;              // the device records name rows no K0 run has written yet
   uint64_t key = 0;                 // fingerprint of the input it was last prepared for
   uint64_t used = 0;                // clock of its last prepare (least recently used is replaced)
 };
@@ -108,7 +118,11 @@ struct sr_ctx {
   uint64_t slot_clock = 0;
   std::vector<uint64_t> node_patch_words;  // this call's node patches (prepare)
   std::vector<int32_t> k0_cols, k0_rows;   // this call's incremental K0 (prepare)
+  std::vector<uint64_t> pod_patch_words;   // this call's pod patches (prepare)
   int32_t k0_incremental = 1;  // SR_K0_INCREMENTAL=0: K0 always rewrites every row
+  int32_t k0_skip = 1;         // SR_K0_SKIP=0: every run launches K0
+  uint64_t run_count = 0;      // runs of this context: d_min alternates between two buffers
+  bool dmin_ready[2] = {false, false};  // buffer reset by the previous run's K2 (a K0-less run needs it)
   sr::EncoderCache enc;      // what the encoder keeps across calls (encode.cpp)
   hipEvent_t ev_upload = nullptr;  // the last upload (a staging buffer is reused after it)
   int32_t prefix_batch = 16;       // first batch of sr_plan_first (SR_PREFIX_BATCH; tools/gpu_prefix.sh)
@@ -326,45 +340,85 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t tick_from = pk.size();
   const size_t o_at = pk.add(w.atoms);
   const size_t o_tt = pk.add(w.t_thr);
-  // Records of the few spot nodes the encoder patched since the last
-  // generation, {node, node_rec[8], node_free[3]} each: when the device holds
-  // that generation they ride in this call's copy and K0 writes them into
-  // the node section (no copy of the whole section, no copy per node).
-  constexpr size_t kPatchNodes = 8;
+  // ---- the slot's device state against this call.  Spot nodes changed since
+  // the slot's tables were written, accumulated over K0-less runs:
+  if (w.state_gen != sl.seen_gen) {
+    if (sl.dirty_valid && E.patched_from != ~0ull && E.patched_from == sl.seen_gen && E.state_gen == w.state_gen) {
+      for (int32_t i : E.patched_nodes)
+        if (std::find(sl.dirty.begin(), sl.dirty.end(), i) == sl.dirty.end()) sl.dirty.push_back(i);
+    } else {
+      sl.dirty_valid = false;
+    }
+    sl.seen_gen = w.state_gen;
+  }
+  constexpr size_t kDirtyMax = 64;
+  if (sl.dirty.size() > kDirtyMax) sl.dirty_valid = false;
+  // pods the encoder re-pointed since the last K0 run of this candidate generation
+  if (!w.reused || sl.dev_cand_gen != w.cand_gen) {
+    sl.pending.clear();
+    sl.pending_mark.assign(static_cast<size_t>(na), 0);
+    sl.class_flip = false;
+  } else {
+    if (sl.pending_mark.size() != static_cast<size_t>(na)) sl.pending_mark.assign(static_cast<size_t>(na), 0);
+    for (size_t i = 0; i < w.pod_patch.size(); i += sr::kPodPatchWords) {
+      const int32_t q = static_cast<int32_t>(w.pod_patch[i]);
+      if (!sl.pending_mark[q]) {
+        sl.pending_mark[q] = 1;
+        sl.pending.push_back(q);
+      }
+    }
+    sl.class_flip = sl.class_flip || w.class_flip;
+  }
+  const bool tables_cur = w.reused && sl.tables_cand_gen == w.cand_gen && sl.dev_cand_gen == w.cand_gen &&
+                          sl.tables_thr.size() == w.t_thr.size() && sl.dirty_valid;
+  // A K0-less run: the tables stand for every node but the changed ones, whose
+  // records and T bits K2 takes from the node patches; the atoms (S rows) must
+  // be the tables' and no pod may have left the empty class (K2's dead-pod
+  // shortcut reads the device records).  Node-order candidates only.
+  constexpr size_t kSkipDirty = 16;
+  const bool k0_skip = ctx->k0_skip && tables_cur && sl.dirty.size() <= kSkipDirty && !sl.class_flip &&
+                       w.ext_cand.empty() && w.dyn_cand.empty() && w.max_cand_pods <= 256 && ctx->k2_mode == 0 &&
+                       sl.tables_atoms == w.atoms;
+  // node patches {node, node_rec[8], node_free[3]}: the changed nodes' records
+  // ride in the call's copy; K0 writes them into the node section (or K2 reads
+  // them, K0-less)
+  constexpr size_t kPatchNodes = 16;
   std::vector<uint64_t>& patch = ctx->node_patch_words;
   patch.clear();
-  if (E.patched_from != ~0ull && E.state_gen == w.state_gen && !E.patched_nodes.empty() &&
-      E.patched_nodes.size() <= kPatchNodes) {
+  if (sl.dirty_valid && !sl.dirty.empty() && sl.dirty.size() <= kPatchNodes) {  // a superset of the nodes the
+                                                                                 // device section lacks
     const size_t NP = static_cast<size_t>(w.n_pad);
-    for (int32_t i : E.patched_nodes) {
+    for (int32_t i : sl.dirty) {
       patch.push_back(static_cast<uint64_t>(i));
       for (size_t j = 0; j < 8; ++j) patch.push_back(E.node_rec[static_cast<size_t>(i) * 8 + j]);
       for (size_t dm = 0; dm < 3; ++dm) patch.push_back(static_cast<uint64_t>(E.node_free[dm * NP + i]));
     }
   }
   const size_t o_np = patch.empty() ? 0 : pk.add(patch);
-  const size_t o_pp = w.pod_patch.empty() ? 0 : pk.add(w.pod_patch);
-  // Incremental K0: a reuse tick whose slot tables hold this candidate
-  // generation at the state the encoder patched from (or the current one)
-  // rewrites the word columns of the changed nodes and the T rows whose
-  // threshold moved; anything else rewrites every row.
+  // pod patches of a K0 run: every pod re-pointed since the last one
+  std::vector<uint64_t>& ppatch = ctx->pod_patch_words;
+  ppatch.clear();
+  if (w.reused && sl.dev_cand_gen == w.cand_gen)  // (unused if the run turns out K0-less)
+    for (int32_t q : sl.pending)
+      ppatch.insert(ppatch.end(), {static_cast<uint64_t>(q), w.pod_rec[static_cast<size_t>(q) * 6 + 4],
+                                   w.pod_rec[static_cast<size_t>(q) * 6 + 5]});
+  const size_t o_pp = ppatch.empty() ? 0 : pk.add(ppatch);
+  // Incremental K0: the tables hold this candidate generation: the word
+  // columns of the changed nodes and the T rows whose threshold moved are
+  // rewritten; anything else rewrites every row.
   std::vector<int32_t>& kcols = ctx->k0_cols;
   std::vector<int32_t>& krows = ctx->k0_rows;
   kcols.clear();
   krows.clear();
-  bool k0_inc = ctx->k0_incremental && w.reused && sl.tables_cand_gen == w.cand_gen &&
-                sl.tables_thr.size() == w.t_thr.size() &&
-                (sl.tables_state_gen == w.state_gen ||
-                 (E.patched_from != ~0ull && sl.tables_state_gen == E.patched_from && E.state_gen == w.state_gen));
-  if (k0_inc && sl.tables_state_gen != w.state_gen) {
-    for (int32_t i : E.patched_nodes) kcols.push_back(i >> 6);
+  bool k0_inc = ctx->k0_incremental && tables_cur;  // (unused if the run turns out K0-less)
+  if (k0_inc) {
+    for (int32_t i : sl.dirty) kcols.push_back(i >> 6);
     std::sort(kcols.begin(), kcols.end());
     kcols.erase(std::unique(kcols.begin(), kcols.end()), kcols.end());
-  }
-  if (k0_inc)
     for (size_t r = 0; r < w.t_thr.size(); ++r)
       if (w.t_thr[r] != sl.tables_thr[r] && w.t_thr[r] != sr::kTSpare) krows.push_back(static_cast<int32_t>(r));
-  if (kcols.size() > 32 || krows.size() > 256) k0_inc = false;
+    if (kcols.size() > 32 || krows.size() > 256) k0_inc = false;
+  }
   if (!k0_inc) kcols.clear(), krows.clear();
   const size_t o_kc = kcols.empty() ? 0 : pk.add(kcols), o_kr = krows.empty() ? 0 : pk.add(krows);
   const size_t bytes = pk.size();
@@ -379,21 +433,25 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t arena_cap = sl.arena.cap;
   HIP_TRY(ctx, dev_reserve(sl.arena, bytes));  // a new allocation holds no node records
   const bool same_arena = sl.arena.cap == arena_cap;
-  if (sl.patch_pending) sl.dev_state_gen = ~0ull;  // the slot's last prepare's patches never reached the device
-  if (sl.pod_patch_pending) sl.dev_cand_gen = ~0ull;
   const bool nodes_resident = same_arena && sl.dev_state_gen == w.state_gen;
   // a reuse encode's candidate section is on the device: K0 re-points the
-  // records it lists (or none changed)
+  // records that moved (a K0-less run reads them as they are)
   const bool cand_resident = w.reused && same_arena && sl.dev_cand_gen == w.cand_gen;
+  bool skip = k0_skip && cand_resident && same_arena && !sl.need_k0;
   // a few nodes changed since the generation on the device: K0 applies their
-  // records from this call's copy
-  const bool nodes_patch = ctx->node_patch && !nodes_resident && same_arena && sl.dev_state_gen == E.patched_from &&
-                           !patch.empty();
+  // records from this call's copy (K0-less: K2 reads them there)
+  const bool nodes_patch = !nodes_resident && same_arena && !patch.empty() && (skip || ctx->node_patch);
   const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
   const size_t t_cap = sl.tables.cap;
   HIP_TRY(ctx, dev_reserve(sl.tables, n_rows * row_bytes));
-  if (sl.tables.cap != t_cap) sl.tables_cand_gen = ~0ull;  // a new allocation holds no rows
+  if (sl.tables.cap != t_cap) {  // a new allocation holds no rows: every row below
+    sl.tables_cand_gen = ~0ull;
+    skip = false;
+    k0_inc = false;
+    kcols.clear();
+    krows.clear();
+  }
   HIP_TRY(ctx, dev_reserve(ctx->out_node, sizeof(int32_t) * std::max(1, na)));
   HIP_TRY(ctx, dev_reserve(ctx->out_status, sizeof(int32_t) * std::max(1, ncand)));
   HIP_TRY(ctx, dev_reserve(ctx->out_bytes, sizeof(uint32_t) * std::max(1, ncand)));
@@ -435,6 +493,12 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
     pk.copy_to(hs, node_bytes);
   }
   sl.host_cand_gen = w.cand_gen;
+  if (!cand_resident) {  // the records go up whole, current: nothing pending, but rows to write
+    sl.pending.clear();
+    std::fill(sl.pending_mark.begin(), sl.pending_mark.end(), 0);
+    sl.class_flip = false;
+    sl.need_k0 = true;
+  }
   char* dv = static_cast<char*>(sl.arena.p);
   if (!cand_resident) {
     HIP_TRY(ctx, hipMemcpyAsync(dv + from, hs + from, bytes - from, hipMemcpyHostToDevice, ctx->stream));
@@ -445,10 +509,10 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   }
   if (!ctx->ev_upload) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_upload, hipEventDisableTiming));
   HIP_TRY(ctx, hipEventRecord(ctx->ev_upload, ctx->stream));  // kernels queue behind the copy
-  sl.dev_state_gen = w.state_gen;
-  sl.patch_pending = nodes_patch;
+  if (!nodes_patch) sl.dev_state_gen = w.state_gen;  // the section went up whole (or was current)
   sl.dev_cand_gen = w.cand_gen;
-  sl.pod_patch_pending = cand_resident && !w.pod_patch.empty();
+  // run() commits what a K0 launch brings the slot to
+  sl.commit_k0 = !skip;
   auto t2 = std::chrono::steady_clock::now();
 
   char* base = static_cast<char*>(sl.arena.p);
@@ -530,16 +594,22 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.res_stat = d.res_map = nullptr;  // set per run
   ctx->t.bytes_uploaded = static_cast<uint64_t>(cand_resident ? (from < node_bytes ? node_bytes : 0) + bytes - tick_from
                                                                : bytes - from);
-  d.node_patch = nodes_patch ? static_cast<const uint64_t*>(at(o_np)) : nullptr;
-  d.n_node_patch = nodes_patch ? static_cast<int32_t>(patch.size() / sr::kNodePatchU64) : 0;
+  // K0 writes the patches into the node section; a K0-less run's K2 reads them
+  // (every changed node, whether or not the section went up whole)
+  const bool use_patch = skip ? !patch.empty() : nodes_patch;
+  d.node_patch = use_patch ? static_cast<const uint64_t*>(at(o_np)) : nullptr;
+  d.n_node_patch = use_patch ? static_cast<int32_t>(patch.size() / sr::kNodePatchU64) : 0;
+  if (skip) k0_inc = false;
   d.k0_inc = k0_inc ? 1 : 0;
   d.n_k0_cols = static_cast<int32_t>(kcols.size());
   d.n_k0_rows = static_cast<int32_t>(krows.size());
   d.k0_cols = kcols.empty() ? nullptr : static_cast<const int32_t*>(at(o_kc));
   d.k0_rows = krows.empty() ? nullptr : static_cast<const int32_t*>(at(o_kr));
-  const bool pods_patch = cand_resident && !w.pod_patch.empty();
+  const bool pods_patch = !skip && cand_resident && !ppatch.empty();
   d.pod_patch = pods_patch ? static_cast<const uint64_t*>(at(o_pp)) : nullptr;
-  d.n_pod_patch = pods_patch ? static_cast<int32_t>(w.pod_patch.size() / sr::kPodPatchU64) : 0;
+  d.n_pod_patch = pods_patch ? static_cast<int32_t>(ppatch.size() / sr::kPodPatchU64) : 0;
+  d.k0_skip = skip ? 1 : 0;
+  d.first_fallback_local = w.first_fallback;
   static_assert(sr::kPodPatchU64 == sr::kPodPatchWords && sr::kTPad == sr::kTSpare, "patch layout shared with encode.cpp");
 
   const uint64_t row = static_cast<uint64_t>(w.Wp) * 8;
@@ -577,8 +647,10 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   ctx->t.enc_memo_pods = ctx->enc.last_memo_hits;
   ctx->t.enc_reused = ctx->enc.last_reused;
   ctx->t.enc_pod_patches = ctx->enc.last_pod_patches;
-  ctx->t.k0_columns = k0_inc ? static_cast<int32_t>(kcols.size()) : -1;
-  ctx->t.k0_rows_moved = static_cast<int32_t>(krows.size());
+  ctx->t.k0_columns = skip ? -2 : k0_inc ? static_cast<int32_t>(kcols.size()) : -1;
+  ctx->t.k0_rows_moved = k0_inc ? static_cast<int32_t>(krows.size()) : 0;
+  ctx->t.k0_dirty_nodes = skip ? static_cast<int32_t>(patch.size() / sr::kNodePatchU64) : 0;
+  if (skip) ctx->t.bytes_tables = 0;
   ctx->prepared = true;
   return SR_OK;
 }
@@ -704,13 +776,33 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     if (_st != SR_OK) return _st;             \
   } while (0)
   PAIR(0, e0a, e0b);
-  HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
+  // d_min alternates between two buffers: K0 resets this run's, K2 the next's
+  const int par = static_cast<int>(ctx->run_count++ & 1);
+  d.d_min = static_cast<int32_t*>(ctx->dmin.p) + 8 * par;
+  d.d_min_next = static_cast<int32_t*>(ctx->dmin.p) + 8 * (1 - par);
   Slot& sl = *ctx->cur;
-  sl.patch_pending = false;  // K0 writes the node and pod patches (idempotent on later runs)
-  sl.pod_patch_pending = false;
-  sl.tables_cand_gen = w.cand_gen;  // and brings the rows to this workload (a rerun: idempotent)
-  sl.tables_state_gen = w.state_gen;
-  if (sl.tables_thr != w.t_thr) sl.tables_thr = w.t_thr;
+  if (d.k0_skip) {
+    if (!ctx->dmin_ready[par])  // no K2 of a previous run reset it: reset here
+      HIP_TRY(ctx, hipMemsetAsync(d.d_min, 0xff, sizeof(uint64_t), s));
+  } else {
+    HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
+    if (sl.commit_k0) {  // K0 wrote the node and pod patches and brought the rows to this workload (a rerun:
+      sl.commit_k0 = false;  // idempotent)
+      sl.tables_cand_gen = w.cand_gen;
+      sl.tables_state_gen = sl.dev_state_gen = w.state_gen;
+      if (sl.tables_thr != w.t_thr) sl.tables_thr = w.t_thr;
+      if (sl.tables_atoms != w.atoms) sl.tables_atoms = w.atoms;
+      sl.dirty.clear();
+      sl.dirty_valid = true;
+      sl.seen_gen = w.state_gen;
+      for (int32_t q : sl.pending) sl.pending_mark[q] = 0;
+      sl.pending.clear();
+      sl.class_flip = false;
+      sl.need_k0 = false;
+    }
+  }
+  ctx->dmin_ready[par] = false;
+  ctx->dmin_ready[1 - par] = d.n_list > 0;  // K2's first candidate resets it
   PAIR(1, e1a, e1b);
   if (early) {
     d.res_stat = ctx->d_early;
