@@ -376,7 +376,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   // be the tables' and no pod may have left the empty class (K2's dead-pod
   // shortcut reads the device records).  Node-order candidates only.
   constexpr size_t kSkipDirty = 16;
-  const bool k0_skip = ctx->k0_skip && tables_cur && sl.dirty.size() <= kSkipDirty && !sl.class_flip &&
+  const bool k0_skip = ctx->k0_skip && ncand > 0 && tables_cur && sl.dirty.size() <= kSkipDirty && !sl.class_flip &&
                        w.ext_cand.empty() && w.dyn_cand.empty() && w.max_cand_pods <= 256 && ctx->k2_mode == 0 &&
                        sl.tables_atoms == w.atoms;
   // node patches {node, node_rec[8], node_free[3]}: the changed nodes' records
