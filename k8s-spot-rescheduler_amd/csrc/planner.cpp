@@ -440,7 +440,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   bool skip = k0_skip && cand_resident && same_arena && !sl.need_k0;
   // a few nodes changed since the generation on the device: K0 applies their
   // records from this call's copy (K0-less: K2 reads them there)
-  const bool nodes_patch = !nodes_resident && same_arena && !patch.empty() && (skip || ctx->node_patch);
+  const bool nodes_patch = !nodes_resident && same_arena && !patch.empty() && ctx->node_patch;
   const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
   const size_t t_cap = sl.tables.cap;
