@@ -775,7 +775,11 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     sr_status _st = pair_for((k), &a, &b);    \
     if (_st != SR_OK) return _st;             \
   } while (0)
-  PAIR(0, e0a, e0b);
+  hipEvent_t e0a = nullptr, e0b = nullptr;  // K0's pair only when it is launched (an unrecorded event fails)
+  if (!d.k0_skip) {
+    sr_status pst = pair_for(0, &e0a, &e0b);
+    if (pst != SR_OK) return pst;
+  }
   // d_min alternates between two buffers: K0 resets this run's, K2 the next's
   const int par = static_cast<int>(ctx->run_count++ & 1);
   d.d_min = static_cast<int32_t*>(ctx->dmin.p) + 8 * par;
