@@ -960,6 +960,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_K2_WPB")) ctx->k2_wpb = std::atoi(m);
   if (const char* m = std::getenv("SR_PLAN_SLOTS")) ctx->n_slots = std::max(1, std::min(16, std::atoi(m)));
   if (const char* m = std::getenv("SR_K0_INCREMENTAL")) ctx->k0_incremental = std::atoi(m) != 0;
+  if (const char* m = std::getenv("SR_K0_SKIP")) ctx->k0_skip = std::atoi(m) != 0;
   *out = ctx;
   return SR_OK;
 }
