@@ -1185,6 +1185,13 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   // each), full-row scans and far words, the mapping and status writes
   nbytes += (48u + 4u) * static_cast<uint32_t>(np) + 4u + 32u * static_cast<uint32_t>(min(Wp, kNH)) * dead;
 
+  // head words holding a node changed since the tables were written (K0-less runs)
+  uint32_t dirty_head = 0;
+  if (w.k0_skip)
+    for (int p = 0; p < w.n_node_patch; ++p) {
+      const int wd0 = static_cast<int>(w.node_patch[static_cast<size_t>(p) * kNodePatchU64] >> 6);
+      dirty_head |= wd0 < kNH ? 1u << wd0 : 0u;
+    }
   // F heads of pods [0, dead): lanes = kPW pods x kNH words, kPB such batches
   // per step with all their loads in flight together (one memory round trip
   // per kPW * kPB pods)
@@ -1220,7 +1227,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         for (int h = 0; h < kPB; ++h) {
           if (b0 + kPW * h >= lim) continue;  // wave-uniform
           uint64_t f = (wv && kk[h] < np) ? (x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
-          if (w.k0_skip) {  // the pod's requests from its lane
+          if (dirty_head != 0) {  // the pod's requests from its lane
             const int src = min(kk[h], np - 1) - 64 * g;
             auto lane64 = [&](int64_t v) {
               return static_cast<int64_t>(static_cast<uint64_t>(from_lane(static_cast<uint32_t>(v >> 32), src)) << 32 |
