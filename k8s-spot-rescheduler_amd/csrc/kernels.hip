@@ -1185,13 +1185,27 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   // each), full-row scans and far words, the mapping and status writes
   nbytes += (48u + 4u) * static_cast<uint32_t>(np) + 4u + 32u * static_cast<uint32_t>(min(Wp, kNH)) * dead;
 
-  // head words holding a node changed since the tables were written (K0-less runs)
+  // head words holding a node changed since the tables were written (K0-less
+  // runs), and per pod (its lane) whether it fits each changed node: bit p for
+  // node patch p (at most 16)
   uint32_t dirty_head = 0;
+  uint32_t dfit[G];
   if (w.k0_skip)
     for (int p = 0; p < w.n_node_patch; ++p) {
       const int wd0 = static_cast<int>(w.node_patch[static_cast<size_t>(p) * kNodePatchU64] >> 6);
       dirty_head |= wd0 < kNH ? 1u << wd0 : 0u;
     }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    dfit[g] = 0;
+    if (dirty_head != 0)
+      for (int p = 0; p < w.n_node_patch; ++p) {
+        const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
+        const bool fits = zero[g] || (static_cast<int64_t>(pr[9]) >= rc[g] && static_cast<int64_t>(pr[10]) >= rm[g] &&
+                                      static_cast<int64_t>(pr[11]) >= re[g]);
+        dfit[g] |= fits ? 1u << p : 0u;
+      }
+  }
   // F heads of pods [0, dead): lanes = kPW pods x kNH words, kPB such batches
   // per step with all their loads in flight together (one memory round trip
   // per kPW * kPB pods)
@@ -1227,14 +1241,15 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         for (int h = 0; h < kPB; ++h) {
           if (b0 + kPW * h >= lim) continue;  // wave-uniform
           uint64_t f = (wv && kk[h] < np) ? (x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
-          if (dirty_head != 0) {  // the pod's requests from its lane
-            const int src = min(kk[h], np - 1) - 64 * g;
-            auto lane64 = [&](int64_t v) {
-              return static_cast<int64_t>(static_cast<uint64_t>(from_lane(static_cast<uint32_t>(v >> 32), src)) << 32 |
-                                          from_lane(static_cast<uint32_t>(v), src));
-            };
-            const int64_t qc = lane64(rc[g]), qm = lane64(rm[g]), qe = lane64(re[g]);
-            if (wv && kk[h] < np) f = fix_dirty(w, f, x[h][0], wd, qc, qm, qe, (qc | qm | qe) == 0);
+          if (dirty_head != 0) {  // the changed nodes' bits, from the pod's fit mask (its lane)
+            const uint32_t fm = from_lane(dfit[g], min(kk[h], np - 1) - 64 * g);
+            for (int p = 0; p < w.n_node_patch; ++p) {
+              const int n = static_cast<int>(w.node_patch[static_cast<size_t>(p) * kNodePatchU64]);
+              if ((n >> 6) != wd) continue;
+              const uint64_t bit = 1ull << (n & 63);
+              f = (fm >> p) & 1 ? (f | (x[h][0] & bit)) : (f & ~bit);
+            }
+            f = (wv && kk[h] < np) ? f : 0ull;
           }
           if (kk[h] < np) F[kk[h] * kNHS + wd] = f;
           const uint64_t m = ballot(f != 0);  // kNH bits per pod: bit kNH * i + word
