@@ -23,7 +23,8 @@ import os
 import sys
 from collections import defaultdict
 
-KEYS = {"k2_place": "k2_placement", "k2_node": "k2_placement", "k0_tables": "k0_tables", "k3_winner": "k3_winner"}
+KEYS = {"k2_place": "k2_placement", "k2_node": "k2_placement", "k0_tables": "k0_tables", "k0_incremental": "k0_tables",
+        "k3_winner": "k3_winner"}
 
 
 def kernel_key(name):
