@@ -895,13 +895,11 @@ __device__ __forceinline__ uint64_t f_word_prog(const DevWorkload& w, const uint
 // between a request and its row's threshold.
 __device__ __forceinline__ uint64_t fix_dirty(const DevWorkload& w, uint64_t f, uint64_t s, int wd, int64_t rc,
                                               int64_t rm, int64_t re, bool zero) {
-  for (int p = 0; p < w.n_node_patch; ++p) {
-    const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
-    const int n = static_cast<int>(pr[0]);
+  for (int p = 0; p < w.n_dirty; ++p) {
+    const int n = w.dirty_node[p];
     if ((n >> 6) != wd) continue;
     const uint64_t bit = 1ull << (n & 63);
-    const bool fits = zero || (static_cast<int64_t>(pr[9]) >= rc && static_cast<int64_t>(pr[10]) >= rm &&
-                               static_cast<int64_t>(pr[11]) >= re);
+    const bool fits = zero || (w.dirty_free[p][0] >= rc && w.dirty_free[p][1] >= rm && w.dirty_free[p][2] >= re);
     f = fits ? (f | (s & bit)) : (f & ~bit);
   }
   return f;
@@ -1190,19 +1188,17 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   // node patch p (at most 16)
   uint32_t dirty_head = 0;
   uint32_t dfit[G];
-  if (w.k0_skip)
-    for (int p = 0; p < w.n_node_patch; ++p) {
-      const int wd0 = static_cast<int>(w.node_patch[static_cast<size_t>(p) * kNodePatchU64] >> 6);
-      dirty_head |= wd0 < kNH ? 1u << wd0 : 0u;
-    }
+  for (int p = 0; p < w.n_dirty; ++p) {  // kernel arguments
+    const int wd0 = w.dirty_node[p] >> 6;
+    dirty_head |= wd0 < kNH ? 1u << wd0 : 0u;
+  }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     dfit[g] = 0;
     if (dirty_head != 0)
-      for (int p = 0; p < w.n_node_patch; ++p) {
-        const uint64_t* pr = w.node_patch + static_cast<size_t>(p) * kNodePatchU64;
-        const bool fits = zero[g] || (static_cast<int64_t>(pr[9]) >= rc[g] && static_cast<int64_t>(pr[10]) >= rm[g] &&
-                                      static_cast<int64_t>(pr[11]) >= re[g]);
+      for (int p = 0; p < w.n_dirty; ++p) {
+        const bool fits = zero[g] || (w.dirty_free[p][0] >= rc[g] && w.dirty_free[p][1] >= rm[g] &&
+                                      w.dirty_free[p][2] >= re[g]);
         dfit[g] |= fits ? 1u << p : 0u;
       }
   }
@@ -1243,8 +1239,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
           uint64_t f = (wv && kk[h] < np) ? (x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
           if (dirty_head != 0) {  // the changed nodes' bits, from the pod's fit mask (its lane)
             const uint32_t fm = from_lane(dfit[g], min(kk[h], np - 1) - 64 * g);
-            for (int p = 0; p < w.n_node_patch; ++p) {
-              const int n = static_cast<int>(w.node_patch[static_cast<size_t>(p) * kNodePatchU64]);
+            for (int p = 0; p < w.n_dirty; ++p) {
+              const int n = w.dirty_node[p];
               if ((n >> 6) != wd) continue;
               const uint64_t bit = 1ull << (n & 63);
               f = (fm >> p) & 1 ? (f | (x[h][0] & bit)) : (f & ~bit);

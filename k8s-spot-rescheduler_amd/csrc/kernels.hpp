@@ -36,6 +36,9 @@ struct DevWorkload {
   int32_t k0_skip;             // no K0 this run: the tables and the node section are those of the slot's device
                                //   generation; node_patch lists every spot node changed since (K2 takes their
                                //   records from it and recomputes their bits of T rows, skip_mode: DESIGN §4)
+  int32_t n_dirty;             // K0-less runs: the changed nodes and their free cpu / memory / ephemeral, in the
+  int32_t dirty_node[16];      //   kernel arguments (K2's first loads need them: no memory round trip)
+  int64_t dirty_free[16][3];
   int32_t* d_min_next;         // the next run's d_min buffer (runs alternate): K2 resets its first word
   int32_t first_fallback_local;  // d_min[1] of the run (K2 sets it too: K0 may not run)
   int32_t k0_inc;              // K0 rewrites only the word columns k0_cols of every row and the rows k0_rows

@@ -609,6 +609,16 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.pod_patch = pods_patch ? static_cast<const uint64_t*>(at(o_pp)) : nullptr;
   d.n_pod_patch = pods_patch ? static_cast<int32_t>(ppatch.size() / sr::kPodPatchU64) : 0;
   d.k0_skip = skip ? 1 : 0;
+  d.n_dirty = 0;
+  if (skip) {  // the changed nodes in the kernel arguments (<= 16: kSkipDirty)
+    const size_t NP = static_cast<size_t>(w.n_pad);
+    for (int32_t i : sl.dirty) {
+      d.dirty_node[d.n_dirty] = i;
+      for (size_t dm = 0; dm < 3; ++dm) d.dirty_free[d.n_dirty][dm] = E.node_free[dm * NP + static_cast<size_t>(i)];
+      ++d.n_dirty;
+    }
+  }
+  static_assert(sizeof(d.dirty_node) / sizeof(d.dirty_node[0]) == 16, "kSkipDirty nodes in the kernel arguments");
   d.first_fallback_local = w.first_fallback;
   static_assert(sr::kPodPatchU64 == sr::kPodPatchWords && sr::kTPad == sr::kTSpare, "patch layout shared with encode.cpp");
 
