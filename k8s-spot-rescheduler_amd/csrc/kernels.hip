@@ -1217,12 +1217,15 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       for (int b0 = 64 * g; b0 < lim; b0 += kPW * kPB) {
         uint64_t x[kPB][4];
         int kk[kPB];
+        uint32_t fm[kPB];  // the pod's fit mask of the changed nodes (K0-less runs), with its row offsets
 #pragma unroll
         for (int h = 0; h < kPB; ++h) {
           kk[h] = b0 + kPW * h + sub;
           x[h][0] = x[h][1] = x[h][2] = x[h][3] = 0;
+          fm[h] = 0;
           if (b0 + kPW * h >= lim) continue;  // wave-uniform
           const int src = min(kk[h], np - 1) - 64 * g;  // lane of that pod in group g
+          if (dirty_head != 0) fm[h] = from_lane(dfit[g], src);
           const uint32_t o0 = from_lane(static_cast<uint32_t>(r01[g]), src);
           const uint32_t o1 = from_lane(static_cast<uint32_t>(r01[g] >> 32), src);
           const uint32_t o2 = from_lane(static_cast<uint32_t>(r23[g]), src);
@@ -1237,13 +1240,12 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         for (int h = 0; h < kPB; ++h) {
           if (b0 + kPW * h >= lim) continue;  // wave-uniform
           uint64_t f = (wv && kk[h] < np) ? (x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
-          if (dirty_head != 0) {  // the changed nodes' bits, from the pod's fit mask (its lane)
-            const uint32_t fm = from_lane(dfit[g], min(kk[h], np - 1) - 64 * g);
+          if (dirty_head != 0) {  // the changed nodes' bits, from the pod's fit mask
             for (int p = 0; p < w.n_dirty; ++p) {
               const int n = w.dirty_node[p];
               if ((n >> 6) != wd) continue;
               const uint64_t bit = 1ull << (n & 63);
-              f = (fm >> p) & 1 ? (f | (x[h][0] & bit)) : (f & ~bit);
+              f = (fm[h] >> p) & 1 ? (f | (x[h][0] & bit)) : (f & ~bit);
             }
             f = (wv && kk[h] < np) ? f : 0ull;
           }
