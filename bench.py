@@ -289,6 +289,8 @@ def main():
     ap.add_argument("--tick", default="steady", choices=["steady", "cold"],
                     help="steady: the timed step replays a steady-state tick (the previous tick's candidate input, "
                          "one spot node changed: incremental K0 + K2); cold: a first tick (every table row)")
+    ap.add_argument("--mut-pos", type=int, default=7,
+                    help="spot position of the steady tick's changed node (7: inside the 512-node F heads)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e-reps", type=int, default=20, help="steady-state end-to-end ticks timed after the steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -355,7 +357,7 @@ def main():
     out = capi.sr_plan_out()
     out.winner_map = capi.ptr(wmap, capi.P32)
     mut_pod = int(cand_pods[0]) if len(cand_pods) else 0  # the same pod on every rank: one cluster state
-    mut_pos = min(7, len(nm.spot) - 1)
+    mut_pos = min(args.mut_pos, len(nm.spot) - 1)
     mutation = None
     steady = {"tick": "cold", "k0": "every row"}
     if args.tick == "steady" and mut_pos >= 0 and len(cand_pods):

@@ -9,7 +9,7 @@ for arm in "$@"; do
   i=$((i + 1))
   rm -f /tmp/k2prof_ab.bin
   env $arm SR_K2_PROFILE=/tmp/k2prof_ab.bin timeout -k 10 300 python bench.py --config $cfg --steps 3 --warmup 3 \
-    --e2e-reps 0 --no-cpu-baseline > gpurun_out/$T/bench_$i.log 2>&1 || exit $?
+    --e2e-reps 0 --no-cpu-baseline ${K2AB_ARGS:-} > gpurun_out/$T/bench_$i.log 2>&1 || exit $?
   python tools/k2_profile.py /tmp/k2prof_ab.bin > gpurun_out/$T/k2prof_$i.txt 2>&1
   echo "== $arm"; head -22 gpurun_out/$T/k2prof_$i.txt; rm -f /tmp/k2prof_ab.bin
 done
