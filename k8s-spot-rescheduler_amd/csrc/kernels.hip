@@ -1192,11 +1192,6 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     const int wd0 = w.dirty_node[p] >> 6;
     dirty_head |= wd0 < kNH ? 1u << wd0 : 0u;
   }
-  // one changed head word (the usual case): its changed bits, and per pod the
-  // ones it fits, as 64-bit masks (no loop over the changes per F word)
-  const bool one_word = dirty_head != 0 && (dirty_head & (dirty_head - 1)) == 0;
-  const int dw_word = one_word ? __builtin_ctz(dirty_head) : -1;
-  uint64_t dw_bits = 0;
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     dfit[g] = 0;
@@ -1204,27 +1199,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       for (int p = 0; p < w.n_dirty; ++p) {
         const bool fits = zero[g] || (w.dirty_free[p][0] >= rc[g] && w.dirty_free[p][1] >= rm[g] &&
                                       w.dirty_free[p][2] >= re[g]);
-        const int n = w.dirty_node[p];
-        if (one_word) {  // dfit as the fitted bits of the word (low / high halves below)
-          if ((n >> 6) == dw_word) {
-            dw_bits |= 1ull << (n & 63);
-            dfit[g] |= fits && (n & 63) < 32 ? 1u << (n & 31) : 0u;
-          }
-        } else {
-          dfit[g] |= fits ? 1u << p : 0u;
-        }
-      }
-  }
-  uint32_t dfit_hi[G];  // one changed head word: the fitted bits 32-63
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    dfit_hi[g] = 0;
-    if (one_word)
-      for (int p = 0; p < w.n_dirty; ++p) {
-        const int n = w.dirty_node[p];
-        const bool fits = zero[g] || (w.dirty_free[p][0] >= rc[g] && w.dirty_free[p][1] >= rm[g] &&
-                                      w.dirty_free[p][2] >= re[g]);
-        dfit_hi[g] |= fits && (n >> 6) == dw_word && (n & 63) >= 32 ? 1u << (n & 31) : 0u;
+        dfit[g] |= fits ? 1u << p : 0u;
       }
   }
   // F heads of pods [0, dead): lanes = kPW pods x kNH words, kPB such batches
@@ -1242,16 +1217,15 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       for (int b0 = 64 * g; b0 < lim; b0 += kPW * kPB) {
         uint64_t x[kPB][4];
         int kk[kPB];
-        uint32_t fm[kPB], fm_hi[kPB];  // the pod's fit mask of the changed nodes (K0-less runs), with its row offsets
+        uint32_t fm[kPB];  // the pod's fit mask of the changed nodes (K0-less runs), with its row offsets
 #pragma unroll
         for (int h = 0; h < kPB; ++h) {
           kk[h] = b0 + kPW * h + sub;
           x[h][0] = x[h][1] = x[h][2] = x[h][3] = 0;
-          fm[h] = fm_hi[h] = 0;
+          fm[h] = 0;
           if (b0 + kPW * h >= lim) continue;  // wave-uniform
           const int src = min(kk[h], np - 1) - 64 * g;  // lane of that pod in group g
           if (dirty_head != 0) fm[h] = from_lane(dfit[g], src);
-          if (one_word) fm_hi[h] = from_lane(dfit_hi[g], src);
           const uint32_t o0 = from_lane(static_cast<uint32_t>(r01[g]), src);
           const uint32_t o1 = from_lane(static_cast<uint32_t>(r01[g] >> 32), src);
           const uint32_t o2 = from_lane(static_cast<uint32_t>(r23[g]), src);
@@ -1266,11 +1240,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
         for (int h = 0; h < kPB; ++h) {
           if (b0 + kPW * h >= lim) continue;  // wave-uniform
           uint64_t f = (wv && kk[h] < np) ? (x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
-          if (one_word) {  // the changed nodes' bits of the one changed word, from the pod's fitted bits
-            const uint64_t fitted = static_cast<uint64_t>(fm_hi[h]) << 32 | fm[h];
-            if (wd == dw_word) f = (f & ~dw_bits) | (x[h][0] & fitted);
-            f = (wv && kk[h] < np) ? f : 0ull;
-          } else if (dirty_head != 0) {  // several changed head words: per change, the pod's fit bit
+          if (dirty_head != 0) {  // the changed nodes' bits, from the pod's fit mask
             for (int p = 0; p < w.n_dirty; ++p) {
               const int n = w.dirty_node[p];
               if ((n >> 6) != wd) continue;
