@@ -999,11 +999,57 @@ __device__ __forceinline__ int32_t scale32(int64_t f, int k) {
 // request) rather than being recomputed from its conflict bits on the scalar
 // unit every step (A/B on MI355X, r04: K2 -1.5% on C5, equal on C3; the
 // predicated, branch-free form of the update measured 3% slower).
-template <bool E, bool O>
+// X (exclusive candidate: every pod sets and conflicts with one state bit,
+// e.g. one host port): a node takes at most one of its pods, and a node no
+// pod took in this window still holds the window's entry state, so every
+// pod's first fit is computed against that state with the nodes taken so far
+// masked out (no update between steps: the chain is the scalar mask), and the
+// nodes' updates follow in one permute of the placed pods' requests.
+template <bool E, bool O, bool X = false>
 __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int W, int lane, uint32_t nc, uint32_t nm,
                                                    uint32_t ne, uint64_t pm, uint64_t ps, uint64_t cur,
                                                    int32_t& c32, int32_t& m32, int32_t& e32,
                                                    uint64_t& nport, int& nleft, int& node) {
+  if constexpr (X) {
+    int jv = 64;
+    if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
+    const uint64_t base = ballot(nleft >= 1);
+    uint64_t taken = 0;
+    while (todo != 0) {
+      const int k = __builtin_ctzll(todo);
+      todo &= ~(1ull << k);
+      const int32_t c = __builtin_amdgcn_readlane(static_cast<int>(nc), k);
+      const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
+      const int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
+      const uint64_t q = readlane64(pm, k);
+      uint64_t fit = readlane64(cur, k) & base & ~taken & ballot(c32 >= c) & ballot(m32 >= m) &
+                     ballot((nport & q) == 0);
+      if (E) fit &= ballot(e32 >= e);
+      const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
+      taken |= fit & (0ull - fit);  // the lowest set bit: node j
+      jv = lane == k ? j : jv;
+    }
+    // node lane j receives the request and the set bits of the pod that took
+    // it; the other pods send zeros to a node nobody took (one exists unless
+    // all 64 did, and then every pod of the window placed)
+    const int dst = jv < 64 ? jv : (taken == ~0ull ? lane : __builtin_ctzll(~taken));
+    const bool snd = jv < 64;
+    auto send = [&](uint32_t v) {
+      return static_cast<uint32_t>(__builtin_amdgcn_ds_permute(dst << 2, static_cast<int>(snd ? v : 0u)));
+    };
+    const uint32_t rc = send(static_cast<uint32_t>(max(static_cast<int32_t>(nc), 0)));
+    const uint32_t rm = send(static_cast<uint32_t>(max(static_cast<int32_t>(nm), 0)));
+    const uint32_t re = E ? send(static_cast<uint32_t>(max(static_cast<int32_t>(ne), 0))) : 0u;
+    const uint32_t rs_lo = send(static_cast<uint32_t>(ps)), rs_hi = send(static_cast<uint32_t>(ps >> 32));
+    const bool got = (taken >> lane) & 1;
+    c32 -= got ? static_cast<int32_t>(rc) : 0;
+    m32 -= got ? static_cast<int32_t>(rm) : 0;
+    if (E) e32 -= got ? static_cast<int32_t>(re) : 0;
+    nleft -= got ? 1 : 0;
+    nport |= got ? (static_cast<uint64_t>(rs_hi) << 32 | rs_lo) : 0ull;
+    node = jv < 64 ? 64 * W + jv : node;
+    return ballot(jv < 64);
+  }
   // The zero-request exemption and the fixed ephemeral gate are in the
   // values, not in the step: an all-zero request is INT_MIN in nc / nm / ne
   // (it meets every state value), and without E a lane whose ephemeral free
@@ -1137,6 +1183,19 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     }
     E = e != 0;
     O = o != 0;
+  }
+  // exclusive candidate (place_window32 X): a state bit every pod sets and
+  // conflicts with -- pod 0's candidates checked against every pod
+  bool X = false;
+  if (O) {
+    const uint64_t m0 = readlane64(ps[0] & pm[0], 0);
+    for (uint64_t bits = m0; bits != 0 && !X; bits &= bits - 1) {
+      const int b = __builtin_ctzll(bits);
+      bool all = true;
+#pragma unroll
+      for (int g = 0; g < G; ++g) all = all && ballot(64 * g + lane < np && !(((ps[g] & pm[g]) >> b) & 1)) == 0;
+      X = all && w.k2_excl;
+    }
   }
   // node records of window 0 (spot nodes [0, 64)), where first fit usually
   // lands: in flight together with the F heads below
@@ -1472,13 +1531,19 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
 #define SR_PW32(e_, o_)                                                                                           \
   place_window32<e_, o_>(todo, kmax, W, lane, nc[g], nm[g], ne[g], pm[g], ps[g], cur[g], c32, m32, e32, \
                          nport, nleft, node[g])
-          if (narrow)
+#define SR_PW32X(e_)                                                                                            \
+  place_window32<e_, true, true>(todo, kmax, W, lane, nc[g], nm[g], ne[g], pm[g], ps[g], cur[g], c32, m32, e32, \
+                                 nport, nleft, node[g])
+          if (narrow && X)
+            placed = E ? SR_PW32X(true) : SR_PW32X(false);
+          else if (narrow)
             placed = E ? (O ? SR_PW32(true, true) : SR_PW32(true, false))
                        : (O ? SR_PW32(false, true) : SR_PW32(false, false));
           else
             placed = E ? (O ? SR_PW(true, true) : SR_PW(true, false)) : (O ? SR_PW(false, true) : SR_PW(false, false));
 #undef SR_PW
 #undef SR_PW32
+#undef SR_PW32X
         }
         placements += __builtin_popcountll(placed);
         act[g] &= ~placed;

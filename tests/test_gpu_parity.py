@@ -320,6 +320,38 @@ def test_intra_candidate_host_port_conflict(checker):
     assert list(p.node_of_pod) == [0, 1, -1]
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_exclusive_port_candidates(checker, seed):
+    """Candidates whose pods all ask for one host port (no two can share a
+    node: K2's taken-mask step, place_window32 X) next to ones with mixed ports
+    and host IPs (the regular step), 5-160 pods over several windows, spot
+    nodes already using the port or full, uneven requests: against the oracle."""
+    import random
+    r = random.Random(4400 + seed)
+    n = r.randint(60, 220)
+    nodes = [Node("n%d" % i, r.choice([500, 1000, 2000, 4000]), memory=r.choice([1, 2, 4]) * GiB,
+                  pods=r.choice([2, 5, 110])) for i in range(n)]
+    port = lambda p_, ip="": ContainerPort(p_, host_ip=ip)  # noqa: E731
+    spot = [[Pod("s%d_%d" % (i, k), containers=[Container(r.choice([50, 400, 900]),
+                                                          ports=[port(80)] if r.random() < 0.15 else [])])
+             for k in range(r.randint(0, 2))] for i in range(n)]
+    cands = []
+    for c in range(6):
+        m = r.randint(5, 160)
+        excl = c % 2 == 0
+        pods = []
+        for k in range(m):
+            ports = [port(80)] if excl else ([port(r.choice([80, 443]), r.choice(["", "10.0.0.1"]))]
+                                             if r.random() < 0.6 else [])
+            if excl and r.random() < 0.3:
+                ports.append(port(9100))  # a second port, still exclusive through port 80
+            pods.append(Pod("c%d_%d" % (c, k), containers=[Container(r.choice([0, 10, 100, 700]),
+                                                                     memory=r.choice([0, 64, 512]) * 2 ** 20,
+                                                                     ports=ports)]))
+        cands.append(pods)
+    run_scenario(checker, nodes, spot, cands)
+
+
 def test_host_ip_conflicts_inside_a_candidate(checker):
     # HostPortInfo.CheckConflict between the candidate's own pods and the base
     # UsedPorts: 0.0.0.0 conflicts with every IP of (protocol, port), a
