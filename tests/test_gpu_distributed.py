@@ -114,6 +114,31 @@ def _worker(rank, world, port, out):
                       for k, (g, s) in enumerate(zip(gidx, p.status))})
             results[("first_synth", cfg)] = _run_first(lib, checkers[2], h, sc.ptr, loff, lpods, gidx)
             lib.sr_snapshot_destroy(h)
+            if config == 3:  # steady ticks through the collective: reuse, K0-less and incremental K0 runs
+                ck = PredicateChecker(0)
+                ck.attach_collective(world, rank, allreduce_min)
+                rng = np.random.default_rng(77)  # the same changes on both ranks
+                extra = []
+                for t in range(8):
+                    if t:
+                        for _ in range(1 if t % 3 else 12):
+                            extra.append((int(cand_pods[rng.integers(len(cand_pods))]), int(rng.integers(len(nm.spot)))))
+                    h = ctypes.c_void_p()
+                    assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot),
+                                                  capi.ptr(nm.node_pod_off, capi.P32),
+                                                  capi.ptr(nm.node_pod_idx, capi.P32), ctypes.byref(h)) == capi.SR_OK
+                    for pod, pos in extra:
+                        assert lib.sr_snapshot_add_pod(h, sc.ptr, pod, pos) == capi.SR_OK
+                    p = plan_arrays(ck, h, sc.ptr, loff, lpods, cand_global=gidx)
+                    tm = ck.timing()
+                    results[("steady", t)] = dict(
+                        first_ok=p.first_ok, first_fallback=p.first_fallback, winner=p.winner,
+                        wmap=[int(x) for x in p.winner_map] if len(p.winner_map) else None,
+                        k0=int(tm.k0_columns), reused=int(tm.enc_reused), extra=list(extra),
+                        mine={int(g): (int(s_), [int(x) for x in p.node_of_pod[loff[k]:loff[k + 1]]])
+                              for k, (g, s_) in enumerate(zip(gidx, p.status))})
+                    lib.sr_snapshot_destroy(h)
+                ck.close()
         # sr_plan_first: fallback patterns, both shardings, both batch sizes
         for seed in SEEDS:
             nodes, spot_pods, cands, _, _, _ = plan_first_scenario(seed)
@@ -245,3 +270,38 @@ def test_two_ranks_plan_first_fallback_patterns(two_rank_results, seed, split, b
     ref_all = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=1)
     ref_early = oracle_plan(sc.oracle_snapshot(), sc.ptr, cand_off, cand_pods, mode=0)
     _check_first(two_rank_results, ("first", seed, split, batch), ref_all, ref_early, cand_off)
+
+
+def test_two_ranks_steady_ticks_through_the_collective(two_rank_results):
+    """Consecutive ticks of one cluster through the collective, the same
+    stamped candidate shards every tick and a few more pods on spot nodes each
+    time: the candidate side is reused, K0 is skipped while few nodes changed
+    (K2 sets the run's d_min words for the allreduce) or runs on the changed
+    columns; every tick's merged plan equals the oracle on the mutated snapshot."""
+    from oracle_lib import OracleSnapshot, oracle_plan
+    from spotplanner import capi
+    from spotplanner.synth import new_node_map
+    sc, _, cand_off, cand_pods, _ = _synth((3, 240, 600, 0.3))
+    lib = capi.load_planner()
+    nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    n = len(cand_off) - 1
+    kinds = set()
+    for t in range(8):
+        r0 = two_rank_results[0][("steady", t)]
+        osn = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
+        for pod, pos in r0["extra"]:
+            osn.lib.oracle_snapshot_add_pod(osn.h, sc.ptr, pod, pos)
+        o = oracle_plan(osn, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
+        merged = _merged(two_rank_results, ("steady", t))
+        assert sorted(merged) == list(range(n))
+        for c in range(n):
+            s_, m = merged[c]
+            assert s_ == int(o["status"][c]), (t, c)
+            assert m == list(o["node_of_pod"][int(cand_off[c]):int(cand_off[c + 1])]), (t, c)
+        for res in two_rank_results:
+            r = res[("steady", t)]
+            assert (r["first_ok"], r["winner"]) == (int(o["first_ok"]), int(o["winner"])), t
+            if t >= 2:
+                assert r["reused"] == 1, t
+                kinds.add(r["k0"])
+    assert -2 in kinds  # at least one K0-less tick on some rank
