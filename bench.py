@@ -533,36 +533,89 @@ def main():
         lib.sr_snapshot_destroy(h)
     # The whole housekeeping tick from the cluster arrays: NewNodeMap (A1-A5),
     # the candidate lists (GetPodsForDeletionOnNodeDrain + owner filter),
-    # GetClusterSnapshot (A6), then the reference-faithful planning.
-    full_tick, stages = [], {"new_node_map": [], "pods_for_deletion": [], "snapshot_create": [], "plan_first": []}
-    for _ in range(args.e2e_reps):
-        t1 = time.perf_counter()
-        nm2 = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
-        t2 = time.perf_counter()
-        co2, cp2, _, _, st = pods_for_deletion(lib.sr_pods_for_deletion, sc.ptr, ctypes.byref(sc.drain),
-                                               nm2.on_demand, nm2.node_pod_off, nm2.node_pod_idx)
-        assert st == capi.SR_OK, st
-        lo2, lp2, gi2 = shard(co2, cp2, rank, world)
-        t3 = time.perf_counter()
-        snap2 = ctypes.c_void_p()
-        st = lib.sr_snapshot_create(sc.ptr, capi.ptr(nm2.spot, capi.P32), len(nm2.spot),
-                                    capi.ptr(nm2.node_pod_off, capi.P32), capi.ptr(nm2.node_pod_idx, capi.P32),
-                                    ctypes.byref(snap2))
-        assert st == capi.SR_OK
-        t4 = time.perf_counter()
-        c2 = capi.sr_candidates(len(lo2) - 1, capi.ptr(lo2, capi.P32), capi.ptr(lp2, capi.P32),
-                                capi.ptr(gi2, capi.P32))
-        fo = capi.sr_plan_out()
-        fo.winner_map = capi.ptr(wmap2, capi.P32)
-        st = lib.sr_plan_first(checker.handle, snap2, sc.ptr, ctypes.byref(c2), ctypes.byref(fo))
-        assert st == capi.SR_OK, checker.last_error()
-        t5 = time.perf_counter()
-        full_tick.append(1e3 * (t5 - t1))
-        for k, a, b in (("new_node_map", t1, t2), ("pods_for_deletion", t2, t3), ("snapshot_create", t3, t4),
-                        ("plan_first", t4, t5)):
-            stages[k].append(1e3 * (b - a))
-        assert fo.first_ok == first_ok_ref
-        lib.sr_snapshot_destroy(snap2)
+    # GetClusterSnapshot (A6), then the reference-faithful planning.  Between
+    # two ticks one pod on a spot node changes its cpu request (and stamp), so
+    # that node's pod sort, RequestedCPU, place in the spot order and snapshot
+    # state change.  "kept": a long-running planner that keeps the previous
+    # tick's node map cache and snapshot (sr_new_node_map_cached,
+    # sr_snapshot_refresh); "fresh": everything rebuilt every tick.
+    cl = sc.cluster
+    tick_pod = int(nm.node_pod_idx[nm.node_pod_off[nm.spot[mut_pos]]]) if mut_pos >= 0 and len(nm.spot) else -1
+    if tick_pod >= 0 and nm.node_pod_off[nm.spot[mut_pos] + 1] == nm.node_pod_off[nm.spot[mut_pos]]:
+        tick_pod = -1
+    tick_arrays = [np.ctypeslib.as_array(a, shape=(sc.n_pods,)) for a in
+                   (cl.pods.cpu_sort_milli, cl.pods.req_milli_cpu, cl.acc_milli_cpu) if a] if tick_pod >= 0 else []
+    tick_base = [int(a[tick_pod]) for a in tick_arrays]
+    stamps_v = np.ctypeslib.as_array(cl.pod_stamp, shape=(sc.n_pods,)) if cl.pod_stamp and tick_pod >= 0 else None
+    stamp_base = int(stamps_v[tick_pod]) if stamps_v is not None else 0
+
+    def set_tick_state(k):  # state k of the changing pod (0: as generated)
+        for a, b in zip(tick_arrays, tick_base):
+            a[tick_pod] = b + k
+        if stamps_v is not None:
+            stamps_v[tick_pod] = stamp_base ^ (0x5A5A5A5A00000000 * k)
+
+    nm_cache = ctypes.c_void_p()
+    assert lib.sr_node_map_cache_create(ctypes.byref(nm_cache)) == capi.SR_OK
+    kept_snap = None
+    stage_names = ("new_node_map", "pods_for_deletion", "snapshot", "plan_first")
+    full_ticks = {"kept": ([], {k: [] for k in stage_names}), "fresh": ([], {k: [] for k in stage_names})}
+    tick_first_ok = {}
+    tick_rebuilt, tick_sorted = [], []
+    for mode in ("kept", "fresh"):
+        for r in range(args.e2e_reps + 1):  # the first tick untimed (the kept path fills its caches)
+            set_tick_state(r % 2)
+            sorted_n = ctypes.c_int32(0)
+            rebuilt = ctypes.c_int32(0)
+            t1 = time.perf_counter()
+            if mode == "kept":
+                nm2 = new_node_map(lambda cp, pp, mp: lib.sr_new_node_map_cached(nm_cache, cp, pp, mp,
+                                                                                 ctypes.byref(sorted_n)),
+                                   sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+            else:
+                nm2 = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+            t2 = time.perf_counter()
+            co2, cp2, _, _, st = pods_for_deletion(lib.sr_pods_for_deletion, sc.ptr, ctypes.byref(sc.drain),
+                                                   nm2.on_demand, nm2.node_pod_off, nm2.node_pod_idx)
+            assert st == capi.SR_OK, st
+            lo2, lp2, gi2 = shard(co2, cp2, rank, world)
+            t3 = time.perf_counter()
+            args_snap = (sc.ptr, capi.ptr(nm2.spot, capi.P32), len(nm2.spot), capi.ptr(nm2.node_pod_off, capi.P32),
+                         capi.ptr(nm2.node_pod_idx, capi.P32))
+            if mode == "kept" and kept_snap is not None:
+                st = lib.sr_snapshot_refresh(kept_snap, *args_snap, ctypes.byref(rebuilt))
+                snap2 = kept_snap
+            else:
+                snap2 = ctypes.c_void_p()
+                st = lib.sr_snapshot_create(*args_snap, ctypes.byref(snap2))
+                if mode == "kept":
+                    kept_snap = snap2
+            assert st == capi.SR_OK
+            t4 = time.perf_counter()
+            c2 = capi.sr_candidates(len(lo2) - 1, capi.ptr(lo2, capi.P32), capi.ptr(lp2, capi.P32),
+                                    capi.ptr(gi2, capi.P32))
+            fo = capi.sr_plan_out()
+            fo.winner_map = capi.ptr(wmap2, capi.P32)
+            st = lib.sr_plan_first(checker.handle, snap2, sc.ptr, ctypes.byref(c2), ctypes.byref(fo))
+            assert st == capi.SR_OK, checker.last_error()
+            t5 = time.perf_counter()
+            # both paths plan the same cluster state alike
+            assert tick_first_ok.setdefault(r % 2, fo.first_ok) == fo.first_ok
+            if mode == "fresh":
+                lib.sr_snapshot_destroy(snap2)
+            if r == 0:
+                continue
+            if mode == "kept":
+                tick_rebuilt.append(rebuilt.value)
+                tick_sorted.append(sorted_n.value)
+            ft, stg = full_ticks[mode]
+            ft.append(1e3 * (t5 - t1))
+            for k, a, b in zip(stage_names, (t1, t2, t3, t4), (t2, t3, t4, t5)):
+                stg[k].append(1e3 * (b - a))
+    set_tick_state(0)
+    if kept_snap is not None:
+        lib.sr_snapshot_destroy(kept_snap)
+    lib.sr_node_map_cache_destroy(nm_cache)
     end_to_end = None
     if ref_t:
         end_to_end = dict(summary(ref_t), **{
@@ -579,11 +632,22 @@ def main():
                 "pod_patches_median": int(np.median(all_patches)), "upload_bytes": int(np.median(all_bytes)),
                 "span": "sr_plan_prepare + sr_plan_run over every candidate, same fresh one-node-changed snapshots"}),
             "pods_for_deletion_ms": round(pfd_ms, 3), "reps": len(ref_t), "host_threads": host_threads(),
-            "full_tick_median_ms": round(float(np.median(full_tick)), 3) if full_tick else None,
-            "full_tick_stages_median_ms": {k: round(float(np.median(v)), 3) for k, v in stages.items()} if full_tick
-            else None,
-            "full_tick_span": "cluster arrays -> sr_new_node_map -> sr_pods_for_deletion -> sr_snapshot_create -> "
-                              "sr_plan_first"})
+            "full_tick_median_ms": (round(float(np.median(full_ticks["kept"][0])), 3)
+                                    if full_ticks["kept"][0] else None),
+            "full_tick_stages_median_ms": {k: round(float(np.median(v)), 3) for k, v in full_ticks["kept"][1].items()}
+            if full_ticks["kept"][0] else None,
+            "full_tick_kept_state": {"nodes_sorted_median": int(np.median(tick_sorted)) if tick_sorted else None,
+                                     "snapshot_nodes_rebuilt_median": int(np.median(tick_rebuilt))
+                                     if tick_rebuilt else None},
+            "full_tick_fresh_median_ms": (round(float(np.median(full_ticks["fresh"][0])), 3)
+                                          if full_ticks["fresh"][0] else None),
+            "full_tick_fresh_stages_median_ms": {k: round(float(np.median(v)), 3)
+                                                 for k, v in full_ticks["fresh"][1].items()}
+            if full_ticks["fresh"][0] else None,
+            "full_tick_span": "cluster arrays (one spot pod's cpu request changed since the previous tick) -> "
+                              "sr_new_node_map_cached -> sr_pods_for_deletion -> sr_snapshot_refresh of the "
+                              "previous tick's snapshot -> sr_plan_first; fresh: sr_new_node_map and "
+                              "sr_snapshot_create every tick"})
 
     if rank == 0:
         alg = {"k2_placement": tm.bytes_placement, "k0_tables": tm.bytes_tables}[dom]

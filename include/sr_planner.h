@@ -358,6 +358,18 @@ typedef struct {
 sr_status sr_new_node_map(const sr_cluster *cluster, const sr_node_map_params *params,
                           sr_node_map *out);
 
+/* NewNodeMap of consecutive housekeeping ticks (rescheduler.go:195): the cache
+ * keeps each node's pod sort (by node name) and reuses it for a node whose
+ * LISTed pods carry the same non-zero pod_stamp values in the same order under
+ * the same params and node kind.  Output identical to sr_new_node_map;
+ * cache NULL = sr_new_node_map.  out_sorted (optional): nodes whose pods were
+ * sorted anew.  Not thread-safe per cache. */
+typedef struct sr_node_map_cache sr_node_map_cache;
+sr_status sr_node_map_cache_create(sr_node_map_cache **out);
+void      sr_node_map_cache_destroy(sr_node_map_cache *cache);
+sr_status sr_new_node_map_cached(sr_node_map_cache *cache, const sr_cluster *cluster,
+                                 const sr_node_map_params *params, sr_node_map *out, int32_t *out_sorted);
+
 /* Replaces isSpotNode / isOnDemandNode (nodes/nodes.go:168-209).  Host-only. */
 int32_t sr_node_has_label(const sr_cluster *cluster, int32_t node, const sr_node_label *label);
 
@@ -451,6 +463,18 @@ typedef struct sr_snapshot sr_snapshot;
 sr_status sr_snapshot_create(const sr_cluster *cluster, const int32_t *spot_nodes, int32_t n_spot,
                              const int32_t *node_pod_off, const int32_t *node_pod_idx,
                              sr_snapshot **out);
+/* GetClusterSnapshot of the next housekeeping tick (nodes/nodes.go:226-232,
+ * rescheduler.go:215) into a snapshot built by an earlier tick: afterwards
+ * `snap` holds what sr_snapshot_create on these arguments would build.  A spot
+ * node (matched by name) whose pod list carries the same non-zero pod_stamp
+ * values in the same order as the snapshot's keeps its state and pod copies;
+ * the other nodes are rebuilt.  Without stamps, or after the cluster's optional
+ * tables changed, the whole snapshot is rebuilt.  SR_ERR_STATE while forked;
+ * SR_ERR_INVALID_ARG leaves `snap` unchanged.  out_rebuilt (optional): spot
+ * nodes whose state was rebuilt. */
+sr_status sr_snapshot_refresh(sr_snapshot *snap, const sr_cluster *cluster, const int32_t *spot_nodes,
+                              int32_t n_spot, const int32_t *node_pod_off, const int32_t *node_pod_idx,
+                              int32_t *out_rebuilt);
 void      sr_snapshot_destroy(sr_snapshot *snap);
 /* ClusterSnapshot.AddPod(pod, nodeName) (rescheduler.go:366); spot_pos = position in the NodeInfoArray. */
 sr_status sr_snapshot_add_pod(sr_snapshot *snap, const sr_cluster *cluster, int32_t pod, int32_t spot_pos);

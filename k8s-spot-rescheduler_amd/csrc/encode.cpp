@@ -1250,9 +1250,7 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   // shape it was derived under
   const uint64_t* stamps = c->pod_stamp;
   if (stamps) {
-    const uint64_t shape = 1 | (c->str_int ? 2u : 0u) | (c->str_label ? 4u : 0u) | (c->pod_affinity ? 8u : 0u) |
-                           (c->spread ? 16u : 0u) | (c->pod_scalar_off ? 32u : 0u) | (c->volumes ? 64u : 0u) |
-                           (c->acc_milli_cpu ? 128u : 0u);
+    const uint64_t shape = cluster_shape(c);
     if (C.memo_shape != shape) {
       C.pod_memo.clear();
       C.memo_shape = shape;

@@ -63,6 +63,7 @@ struct SnapPod {
   uint32_t lab, nlab;       // labels: sr_snapshot::lkey / lval [lab, lab + nlab)
   uint32_t terms, nterms;   // anti-affinity terms: sr_snapshot::term_words [terms, terms + nterms),
                             // {n words, words...} per term (rare)
+  uint64_t stamp;           // the pod's sr_cluster.pod_stamp when it entered (0: unknown; sr_snapshot_refresh)
 };
 
 // std::allocator that default-initializes on resize() / emplace_back(): the
@@ -195,6 +196,10 @@ struct sr_snapshot {
   int64_t scalar_unknown_total = 0;  // pods whose scalar requests are unknown: candidates asking for any fall back
   int64_t term_unknown_total = 0;    // pods whose deletion state is unknown: pods with spread constraints fall back
   uint64_t version = 0;  // bumped on every mutation
+  // sr_snapshot_refresh: the cluster shape the store was built under
+  // (cluster_shape) and a scratch map node name -> previous spot position
+  uint64_t shape = 0;
+  std::vector<int32_t> pos_of_name;
 };
 
 namespace sr {
@@ -231,6 +236,14 @@ inline bool has_scalars(const sr_cluster* c, int32_t pod) {
   return c->pod_scalar_off && c->pod_scalar_off[pod + 1] > c->pod_scalar_off[pod];
 }
 // NodeInfo.AddPod's accounting of resource r (0 cpu, 1 memory, 2 ephemeral) for the pod.
+// Which optional tables the cluster passes: what a stamped pod derives depends
+// on them too, so memos keyed by pod_stamp are valid under one shape only.
+inline uint64_t cluster_shape(const sr_cluster* c) {
+  return 1 | (c->str_int ? 2u : 0u) | (c->str_label ? 4u : 0u) | (c->pod_affinity ? 8u : 0u) |
+         (c->spread ? 16u : 0u) | (c->pod_scalar_off ? 32u : 0u) | (c->volumes ? 64u : 0u) |
+         (c->acc_milli_cpu ? 128u : 0u);
+}
+
 inline int64_t pod_acc(const sr_cluster* c, int32_t pod, int r) {
   const sr_pods& P = c->pods;
   switch (r) {

@@ -16,6 +16,31 @@
 #include "host.hpp"
 #include "pool.hpp"
 
+// Per-node pod sorts of earlier NewNodeMap calls (sr_new_node_map_cached),
+// by node name: the stamps of the node's LISTed pods in list order, its kind,
+// and the sorted kept pods as positions in that list.
+struct sr_node_map_cache {
+  struct Entry {
+    int8_t kind = -1;
+    uint32_t epoch = 0;             // the call that last claimed it (a repeated name is not cached)
+    int64_t requested = 0;
+    std::vector<uint64_t> stamps;   // every LISTed pod, list order
+    std::vector<int32_t> perm;      // kept pods, sorted: positions in the list
+  };
+  uint64_t shape = 0;
+  sr_node_map_params params{};
+  uint32_t epoch = 0;
+  std::vector<int32_t> slot_of_name;  // [n_strings] -> entries, -1
+  std::vector<Entry> entries;
+  std::vector<int32_t> names, slot;   // the last call's node names and their entries (-1: none)
+  void clear() {
+    std::fill(slot_of_name.begin(), slot_of_name.end(), -1);
+    entries.clear();
+    names.clear();
+    slot.clear();
+  }
+};
+
 namespace sr {
 
 // isSpotNode / isOnDemandNode (nodes/nodes.go:168-209).
@@ -34,7 +59,12 @@ static bool node_has_label(const sr_cluster* c, int32_t node, const sr_node_labe
   return val == l->value;            // labels[k] == v, missing key reads as ""
 }
 
-static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, sr_node_map* out) {
+static bool same_label(const sr_node_label& a, const sr_node_label& b) {
+  return a.key == b.key && a.value == b.value && a.has_value == b.has_value;
+}
+
+static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, sr_node_map* out,
+                              sr_node_map_cache* cache, int32_t* out_sorted) {
   const sr_nodes& N = c->nodes;
   const sr_pods& P = c->pods;
   const int32_t nn = N.n, np = P.n;
@@ -104,16 +134,86 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   using KV = std::pair<int64_t, int32_t>;
   auto by_key_desc = [](const KV& x, const KV& y) { return x.first > y.first; };
   auto by_key_asc = [](const KV& x, const KV& y) { return x.first < y.first; };
-  // Per node (independent, on the pool): the spot / on-demand test, the
-  // priority filter of getPodsOnNode, RequestedCPU and the pod sort.  Pass 1
-  // counts the kept pods, pass 2 writes them at their prefix offsets.
   std::vector<int8_t> kind(static_cast<size_t>(nn), 0);  // 1 spot, 2 on-demand
-  std::vector<int32_t> nkept(static_cast<size_t>(nn) + 1, 0);
-  std::atomic<bool> nil_priority{false};
-  parallel_for(static_cast<size_t>(nn), 64, [&](size_t lo, size_t hi) {
+  parallel_for(static_cast<size_t>(nn), 256, [&](size_t lo, size_t hi) {
     for (size_t node = lo; node < hi; ++node) {
       const bool spot = node_has_label(c, static_cast<int32_t>(node), &p->spot);
       kind[node] = spot ? 1 : node_has_label(c, static_cast<int32_t>(node), &p->on_demand) ? 2 : 0;
+    }
+  });
+  // The cache's entry per node (-1: none): valid for one cluster shape and
+  // one set of params, stamped pods only.
+  const uint64_t* stamps = c->pod_stamp;
+  std::vector<int32_t> no_slot;
+  const std::vector<int32_t>* slot_v = &no_slot;
+  if (cache && stamps) {
+    const uint64_t shape = cluster_shape(c);
+    bool fresh = false;
+    if (cache->shape != shape || !same_label(cache->params.spot, p->spot) ||
+        !same_label(cache->params.on_demand, p->on_demand) ||
+        cache->params.priority_threshold != p->priority_threshold ||
+        cache->entries.size() > 2 * static_cast<size_t>(nn) + 1024) {
+      cache->clear();
+      cache->shape = shape;
+      cache->params = *p;
+      fresh = true;
+    }
+    const int32_t ns_str = c->n_strings;
+    // the same node names in the same order as the last call: the same slots
+    if (fresh || cache->names.size() != static_cast<size_t>(nn) ||
+        !std::equal(N.name, N.name + nn, cache->names.begin())) {
+      if (cache->slot_of_name.size() < static_cast<size_t>(ns_str))
+        cache->slot_of_name.resize(static_cast<size_t>(ns_str), -1);
+      const uint32_t ep = ++cache->epoch;
+      std::vector<int32_t>& slot = cache->slot;
+      slot.assign(static_cast<size_t>(nn), -1);
+      for (int32_t node = 0; node < nn; ++node) {
+        const int32_t nm = N.name[node];
+        if (nm < 0 || nm >= ns_str) continue;
+        int32_t& e = cache->slot_of_name[nm];
+        if (e < 0) {
+          e = static_cast<int32_t>(cache->entries.size());
+          cache->entries.emplace_back();
+        }
+        auto& en = cache->entries[static_cast<size_t>(e)];
+        if (en.epoch == ep) {  // a second node of this name: neither is cached
+          en.kind = -1;
+          for (int32_t m = 0; m < node; ++m)
+            if (slot[m] == e) slot[m] = -1;
+          continue;
+        }
+        en.epoch = ep;
+        slot[node] = e;
+      }
+      cache->names.assign(N.name, N.name + nn);
+    }
+    slot_v = &cache->slot;
+  }
+  const std::vector<int32_t>& slot = *slot_v;
+  // Per node (independent, on the pool): the priority filter of
+  // getPodsOnNode, RequestedCPU and the pod sort, or the cached sort of the
+  // same stamped pods.  Pass 1 counts the kept pods, pass 2 writes them at
+  // their prefix offsets.
+  std::vector<int32_t> nkept(static_cast<size_t>(nn) + 1, 0);
+  std::vector<uint8_t> hit(static_cast<size_t>(nn), 0);
+  std::atomic<bool> nil_priority{false};
+  parallel_for(static_cast<size_t>(nn), 64, [&](size_t lo, size_t hi) {
+    for (size_t node = lo; node < hi; ++node) {
+      const bool spot = kind[node] == 1;
+      if (!slot.empty() && slot[node] >= 0) {
+        const auto& en = cache->entries[static_cast<size_t>(slot[node])];
+        const int32_t n = start[node + 1] - start[node];
+        bool same = en.kind == kind[node] && static_cast<int32_t>(en.stamps.size()) == n;
+        for (int32_t k = 0; k < n && same; ++k) {
+          const uint64_t st = stamps[listed[start[node] + k]];
+          same = st != 0 && st == en.stamps[static_cast<size_t>(k)];
+        }
+        if (same) {
+          hit[node] = 1;
+          nkept[node + 1] = static_cast<int32_t>(en.perm.size());
+          continue;
+        }
+      }
       int32_t k = 0;
       for (int32_t j = start[node]; j < start[node + 1]; ++j) {
         const int32_t pod = listed[j];
@@ -127,25 +227,52 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   });
   if (nil_priority.load()) return SR_ERR_NIL_PRIORITY;
   for (int32_t node = 0; node < nn; ++node) nkept[node + 1] += nkept[node];
+  std::atomic<int32_t> sorted{0};
   parallel_for(static_cast<size_t>(nn), 64, [&](size_t lo, size_t hi) {
-    std::vector<std::pair<int64_t, int32_t>> kv;  // (cpu, pod): the sort compares keys held in place
+    std::vector<std::pair<int64_t, int32_t>> kv;  // (cpu, position in the node's list): the sort compares keys held in place
+    int32_t my_sorted = 0;
     for (size_t node = lo; node < hi; ++node) {
       const bool spot = kind[node] == 1;
+      const int32_t s0 = start[node];
       out->node_pod_off[node] = nkept[node];
+      int32_t* dst = out->node_pod_idx + nkept[node];
+      if (hit[node]) {
+        const auto& en = cache->entries[static_cast<size_t>(slot[node])];
+        for (size_t k = 0; k < en.perm.size(); ++k) dst[k] = listed[s0 + en.perm[k]];
+        out->requested_cpu[node] = en.requested;
+        out->free_cpu[node] = N.alloc_milli_cpu[node] - en.requested;
+        continue;
+      }
+      ++my_sorted;
       int64_t requested = 0;
       kv.clear();
-      for (int32_t j = start[node]; j < start[node + 1]; ++j) {
+      for (int32_t j = s0; j < start[node + 1]; ++j) {
         const int32_t pod = listed[j];
         if (P.priority[pod] < p->priority_threshold && spot) continue;
-        kv.emplace_back(cpu[pod], pod);
+        kv.emplace_back(cpu[pod], j - s0);
         requested += cpu[pod];
       }
       out->requested_cpu[node] = requested;
       out->free_cpu[node] = N.alloc_milli_cpu[node] - requested;
       go_sort_slice(kv.data(), static_cast<int>(kv.size()), by_key_desc);
-      for (size_t k = 0; k < kv.size(); ++k) out->node_pod_idx[nkept[node] + static_cast<int32_t>(k)] = kv[k].second;
+      for (size_t k = 0; k < kv.size(); ++k) dst[k] = listed[s0 + kv[k].second];
+      if (!slot.empty() && slot[node] >= 0) {  // remember this sort
+        auto& en = cache->entries[static_cast<size_t>(slot[node])];
+        const int32_t n = start[node + 1] - s0;
+        en.kind = kind[node];
+        en.stamps.resize(static_cast<size_t>(n));
+        for (int32_t k = 0; k < n; ++k) {
+          en.stamps[static_cast<size_t>(k)] = stamps[listed[s0 + k]];
+          if (!en.stamps[static_cast<size_t>(k)]) en.kind = -1;  // an unstamped pod: never a hit
+        }
+        en.perm.resize(kv.size());
+        for (size_t k = 0; k < kv.size(); ++k) en.perm[k] = kv[k].second;
+        en.requested = requested;
+      }
     }
+    sorted.fetch_add(my_sorted, std::memory_order_relaxed);
   });
+  if (out_sorted) *out_sorted = sorted.load();
   int32_t ns = 0, nod = 0;
   for (int32_t node = 0; node < nn; ++node) {
     if (kind[node] == 1)
@@ -176,6 +303,7 @@ void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out, int32_t* k, i
                    std::vector<int32_t>* terms) {
   *out = SnapPod{};
   out->ns = -1;
+  out->stamp = c->pod_stamp ? c->pod_stamp[pod] : 0;
   out->anti = has_anti_terms(c, pod) ? 1 : 0;
   out->opaque = anti_opaque(c, pod) ? 1 : 0;
   out->term = c->spread ? (c->spread->terminating[pod] ? 1 : 0) : 2;
@@ -300,22 +428,14 @@ void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t 
   s->version++;
 }
 
-static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32_t n_spot,
-                                 const int32_t* off, const int32_t* idx, sr_snapshot** out) {
-  if (n_spot < 0 || (n_spot > 0 && (!spot || !off || !idx))) return SR_ERR_INVALID_ARG;
-  auto* s = new sr_snapshot();
-  s->id_empty = c->id_empty;
-  s->id_metadata_name = c->id_metadata_name;
-  s->id_unschedulable_key = c->id_unschedulable_key;
-  s->nodes.resize(n_spot);
-  s->state.resize(n_spot);
-  s->node_names.resize(n_spot);
-  s->node_sfp.resize(n_spot);
-  s->node_dfp.resize(n_spot);
-  const sr_nodes& N = c->nodes;
-  std::atomic<bool> bad{false};  // validate first: the build below cannot fail
+// The input of GetClusterSnapshot: spot node indices and each node's pod list
+// in range (checked before anything is built, so a build cannot fail).
+static bool snapshot_input_ok(const sr_cluster* c, const int32_t* spot, int32_t n_spot, const int32_t* off,
+                              const int32_t* idx) {
+  if (n_spot < 0 || (n_spot > 0 && (!spot || !off || !idx))) return false;
+  std::atomic<bool> bad{false};
   parallel_for(static_cast<size_t>(n_spot), 512, [&](size_t lo, size_t hi) {
-    const int32_t np = c->pods.n, nn = N.n;
+    const int32_t np = c->pods.n, nn = c->nodes.n;
     bool b = false;
     for (size_t i = lo; i < hi && !b; ++i) {
       const int32_t node = spot[i];
@@ -327,88 +447,306 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
     }
     if (b) bad.store(true, std::memory_order_relaxed);
   });
-  if (bad.load()) {
-    delete s;
-    return SR_ERR_INVALID_ARG;
+  return !bad.load();
+}
+
+// The node AddNodeWithPods copies (nodes/nodes.go:229): allocatable,
+// labels, taints, scalar and volume limits.
+static void spot_node_from(const sr_cluster* c, int32_t node, SpotNode& sn) {
+  const sr_nodes& N = c->nodes;
+  sn = SpotNode{};
+  sn.name = N.name[node];
+  sn.alloc[0] = N.alloc_milli_cpu[node];
+  sn.alloc[1] = N.alloc_memory[node];
+  sn.alloc[2] = N.alloc_ephemeral[node];
+  sn.alloc_pods = N.alloc_pods[node];
+  sn.unschedulable = N.unschedulable[node];
+  sn.labels.reserve(static_cast<size_t>(N.label_off[node + 1] - N.label_off[node]));
+  for (int32_t j = N.label_off[node]; j < N.label_off[node + 1]; ++j) sn.labels.emplace_back(N.label_key[j], N.label_val[j]);
+  for (int32_t j = N.taint_off[node]; j < N.taint_off[node + 1]; ++j)
+    sn.taints.push_back(TaintRec{N.taint_key[j], N.taint_val[j], N.taint_effect[j]});
+  if (c->node_scalar_off) {
+    for (int32_t j = c->node_scalar_off[node]; j < c->node_scalar_off[node + 1]; ++j)
+      sn.scalar_alloc.emplace_back(c->node_scalar_name[j], c->node_scalar_alloc[j]);
+    std::sort(sn.scalar_alloc.begin(), sn.scalar_alloc.end());
   }
-  // the snapshot's pod store: the pods of spot node i at [base[i], base[i + 1])
-  std::vector<int32_t> base(static_cast<size_t>(n_spot) + 1, 0);
-  for (int32_t i = 0; i < n_spot; ++i) base[i + 1] = base[i] + (off[spot[i] + 1] - off[spot[i]]);
-  s->pods.resize(static_cast<size_t>(base[n_spot]));
-  // their labels: node i's at [lbase[i], lbase[i + 1])
-  std::vector<uint32_t> lbase(static_cast<size_t>(n_spot) + 1, 0);
+  if (const sr_volumes* V = c->volumes) {
+    for (int32_t j = V->limit_off[node]; j < V->limit_off[node + 1]; ++j) sn.vol_limit.emplace_back(V->limit_key[j], V->limit[j]);
+    std::sort(sn.vol_limit.begin(), sn.vol_limit.end());
+  }
+  sn.static_fp = node_static_fp(sn, c);
+}
+
+// AddNodeWithPods' pods for the spot positions `pos` (empty states): each
+// position's pods are appended to the snapshot's store, their labels to the
+// label arena, on the pool; the rare anti-affinity terms go to per-chunk
+// arenas, concatenated afterwards.
+static void build_states(sr_snapshot* s, const sr_cluster* c, const int32_t* spot, const int32_t* off,
+                         const int32_t* idx, const std::vector<int32_t>& pos) {
+  const size_t n = pos.size();
+  if (n == 0) return;
+  // position pos[q]'s pods at [base[q], base[q + 1]) of the store, labels at [lbase[q], lbase[q + 1])
+  std::vector<int32_t> base(n + 1, static_cast<int32_t>(s->pods.size()));
+  for (size_t q = 0; q < n; ++q) base[q + 1] = base[q] + (off[spot[pos[q]] + 1] - off[spot[pos[q]]]);
+  std::vector<uint32_t> lbase(n + 1, static_cast<uint32_t>(s->lkey.size()));
   if (c->pod_affinity) {
-    parallel_for(static_cast<size_t>(n_spot), 256, [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) {
-        uint32_t n = 0;
-        for (int32_t j = off[spot[i]]; j < off[spot[i] + 1]; ++j) n += pod_label_count(c, idx[j]);
-        lbase[i + 1] = n;
+    std::vector<uint32_t> cnt(n, 0);
+    parallel_for(n, 256, [&](size_t lo, size_t hi) {
+      for (size_t q = lo; q < hi; ++q) {
+        const int32_t node = spot[pos[q]];
+        uint32_t k = 0;
+        for (int32_t j = off[node]; j < off[node + 1]; ++j) k += pod_label_count(c, idx[j]);
+        cnt[q] = k;
       }
     });
-    for (int32_t i = 0; i < n_spot; ++i) lbase[i + 1] += lbase[i];
+    for (size_t q = 0; q < n; ++q) lbase[q + 1] = lbase[q] + cnt[q];
   }
-  s->lkey.resize(lbase[n_spot]);
-  s->lval.resize(lbase[n_spot]);
-  // AddNodeWithPods per spot node: independent nodes, on the pool; the rare
-  // anti-affinity terms go to per-chunk arenas, concatenated afterwards
+  s->pods.resize(static_cast<size_t>(base[n]));
+  s->lkey.resize(lbase[n]);
+  s->lval.resize(lbase[n]);
   constexpr size_t kNodeChunk = 32;
-  std::vector<std::vector<int32_t>> chunk_terms((static_cast<size_t>(n_spot) + kNodeChunk - 1) / kNodeChunk);
-  parallel_for(static_cast<size_t>(n_spot), kNodeChunk, [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) {
-      std::vector<int32_t>* terms = &chunk_terms[i / kNodeChunk];
-      const int32_t node = spot[i];
-      SpotNode& sn = s->nodes[i];
-      sn.name = N.name[node];
-      sn.alloc[0] = N.alloc_milli_cpu[node];
-      sn.alloc[1] = N.alloc_memory[node];
-      sn.alloc[2] = N.alloc_ephemeral[node];
-      sn.alloc_pods = N.alloc_pods[node];
-      sn.unschedulable = N.unschedulable[node];
-      sn.labels.reserve(static_cast<size_t>(N.label_off[node + 1] - N.label_off[node]));
-      for (int32_t j = N.label_off[node]; j < N.label_off[node + 1]; ++j)
-        sn.labels.emplace_back(N.label_key[j], N.label_val[j]);
-      for (int32_t j = N.taint_off[node]; j < N.taint_off[node + 1]; ++j)
-        sn.taints.push_back(TaintRec{N.taint_key[j], N.taint_val[j], N.taint_effect[j]});
-      if (c->node_scalar_off) {
-        for (int32_t j = c->node_scalar_off[node]; j < c->node_scalar_off[node + 1]; ++j)
-          sn.scalar_alloc.emplace_back(c->node_scalar_name[j], c->node_scalar_alloc[j]);
-        std::sort(sn.scalar_alloc.begin(), sn.scalar_alloc.end());
-      }
-      if (const sr_volumes* V = c->volumes) {
-        for (int32_t j = V->limit_off[node]; j < V->limit_off[node + 1]; ++j)
-          sn.vol_limit.emplace_back(V->limit_key[j], V->limit[j]);
-        std::sort(sn.vol_limit.begin(), sn.vol_limit.end());
-      }
-      sn.static_fp = node_static_fp(sn, c);
-      s->state[i].pods.reserve(static_cast<size_t>(off[node + 1] - off[node]));
-      uint32_t lab = lbase[i];
+  std::vector<std::vector<int32_t>> chunk_terms((n + kNodeChunk - 1) / kNodeChunk);
+  parallel_for(n, kNodeChunk, [&](size_t lo, size_t hi) {
+    for (size_t q = lo; q < hi; ++q) {
+      std::vector<int32_t>* terms = &chunk_terms[q / kNodeChunk];
+      const int32_t node = spot[pos[q]];
+      NodeState& st = s->state[pos[q]];
+      st.pods.reserve(static_cast<size_t>(off[node + 1] - off[node]));
+      uint32_t lab = lbase[q];
       for (int32_t j = off[node]; j < off[node + 1]; ++j) {
-        const int32_t store = base[i] + (j - off[node]);
+        const int32_t store = base[q] + (j - off[node]);
         snap_pod_from(c, idx[j], &s->pods[store], s->lkey.data(), s->lval.data(), lab, terms);
         lab += s->pods[store].nlab;
-        state_add_pod(s->state[i], c, idx[j], s->pods[store], store);
+        state_add_pod(st, c, idx[j], s->pods[store], store);
       }
-      s->node_names[i] = sn.name;
-      s->node_sfp[i] = sn.static_fp;
-      s->node_dfp[i] = node_state_fp(sn, s->state[i]);
     }
   });
   for (size_t ch = 0; ch < chunk_terms.size(); ++ch) {
     if (chunk_terms[ch].empty()) continue;
     const uint32_t shift = static_cast<uint32_t>(s->term_words.size());
     s->term_words.insert(s->term_words.end(), chunk_terms[ch].begin(), chunk_terms[ch].end());
-    const size_t i1 = std::min(static_cast<size_t>(n_spot), (ch + 1) * kNodeChunk);
-    for (int32_t q = base[ch * kNodeChunk]; q < base[i1]; ++q)
-      if (s->pods[q].nterms) s->pods[q].terms += shift;
+    const size_t q1 = std::min(n, (ch + 1) * kNodeChunk);
+    for (int32_t e = base[ch * kNodeChunk]; e < base[q1]; ++e)
+      if (s->pods[e].nterms) s->pods[e].terms += shift;
   }
-  for (int32_t i = 0; i < n_spot; ++i) {
-    s->anti_total += s->state[i].anti;
-    s->opaque_total += s->state[i].opaque;
-    s->unknown_total += s->state[i].unknown;
-    s->scalar_unknown_total += s->state[i].scalar_unknown;
-    s->term_unknown_total += s->state[i].term_unknown;
+}
+
+// Per-position views the encoder compares (names, fingerprints) and the totals.
+static void finish_snapshot(sr_snapshot* s) {
+  const size_t n = s->nodes.size();
+  s->node_names.resize(n);
+  s->node_sfp.resize(n);
+  s->node_dfp.resize(n);
+  parallel_for(n, 256, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      s->node_names[i] = s->nodes[i].name;
+      s->node_sfp[i] = s->nodes[i].static_fp;
+      s->node_dfp[i] = node_state_fp(s->nodes[i], s->state[i]);
+    }
+  });
+  s->anti_total = s->opaque_total = s->unknown_total = s->scalar_unknown_total = s->term_unknown_total = 0;
+  for (const NodeState& st : s->state) {
+    s->anti_total += st.anti;
+    s->opaque_total += st.opaque;
+    s->unknown_total += st.unknown;
+    s->scalar_unknown_total += st.scalar_unknown;
+    s->term_unknown_total += st.term_unknown;
   }
+}
+
+static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32_t n_spot,
+                                 const int32_t* off, const int32_t* idx, sr_snapshot** out) {
+  if (!snapshot_input_ok(c, spot, n_spot, off, idx)) return SR_ERR_INVALID_ARG;
+  auto* s = new sr_snapshot();
+  s->id_empty = c->id_empty;
+  s->id_metadata_name = c->id_metadata_name;
+  s->id_unschedulable_key = c->id_unschedulable_key;
+  s->shape = cluster_shape(c);
+  s->nodes.resize(n_spot);
+  s->state.resize(n_spot);
+  parallel_for(static_cast<size_t>(n_spot), 64, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) spot_node_from(c, spot[i], s->nodes[i]);
+  });
+  std::vector<int32_t> pos(static_cast<size_t>(n_spot));
+  for (int32_t i = 0; i < n_spot; ++i) pos[i] = i;
+  build_states(s, c, spot, off, idx, pos);
+  finish_snapshot(s);
   *out = s;
+  return SR_OK;
+}
+
+// The snapshot's copy of `node` still equals the cluster's (nodes with scalar
+// resources or volume limits are copied anew).
+static bool spot_node_same(const sr_cluster* c, int32_t node, const SpotNode& sn) {
+  const sr_nodes& N = c->nodes;
+  if (sn.name != N.name[node] || sn.alloc[0] != N.alloc_milli_cpu[node] || sn.alloc[1] != N.alloc_memory[node] ||
+      sn.alloc[2] != N.alloc_ephemeral[node] || sn.alloc_pods != N.alloc_pods[node] ||
+      sn.unschedulable != N.unschedulable[node] || !sn.scalar_alloc.empty() || !sn.vol_limit.empty())
+    return false;
+  if (c->node_scalar_off && c->node_scalar_off[node + 1] != c->node_scalar_off[node]) return false;
+  if (c->volumes && c->volumes->limit_off[node + 1] != c->volumes->limit_off[node]) return false;
+  const int32_t l0 = N.label_off[node], nl = N.label_off[node + 1] - l0;
+  if (static_cast<int32_t>(sn.labels.size()) != nl) return false;
+  for (int32_t j = 0; j < nl; ++j)
+    if (sn.labels[j].first != N.label_key[l0 + j] || sn.labels[j].second != N.label_val[l0 + j]) return false;
+  const int32_t t0 = N.taint_off[node], nt = N.taint_off[node + 1] - t0;
+  if (static_cast<int32_t>(sn.taints.size()) != nt) return false;
+  for (int32_t j = 0; j < nt; ++j) {
+    const TaintRec& t = sn.taints[j];
+    if (t.key != N.taint_key[t0 + j] || t.val != N.taint_val[t0 + j] || t.effect != N.taint_effect[t0 + j]) return false;
+  }
+  return true;
+}
+
+// GetClusterSnapshot again on a snapshot built from an earlier call's cluster:
+// afterwards it holds what snapshot_create on these arguments would build.
+// A spot node (by name) whose pod list carries the same non-zero stamps in the
+// same order as its state in the snapshot keeps that state and its pods in the
+// store (a stamp covers everything a pod contributes, sr_cluster.pod_stamp);
+// the others are rebuilt, their pods appended to the store.  A node whose
+// static part equals the cluster's keeps its copy too.  The store is rebuilt
+// whole once dead entries outnumber live ones, or when the cluster's shape
+// changed.
+static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int32_t* spot, int32_t n_spot,
+                                  const int32_t* off, const int32_t* idx, int32_t* out_rebuilt) {
+  if (s->forked) return SR_ERR_STATE;  // a forked snapshot is mid-simulation
+  if (n_spot < 0 || (n_spot > 0 && (!spot || !off || !idx))) return SR_ERR_INVALID_ARG;
+  const uint64_t* stamps = c->pod_stamp;
+  auto rebuild = [&]() {
+    sr_snapshot* t = nullptr;
+    const sr_status st = snapshot_create(c, spot, n_spot, off, idx, &t);
+    if (st != SR_OK) return st;
+    const uint64_t v = s->version;
+    std::vector<int32_t> scratch;
+    scratch.swap(s->pos_of_name);
+    *s = std::move(*t);
+    delete t;
+    s->pos_of_name.swap(scratch);
+    s->version = v + 1;
+    if (out_rebuilt) *out_rebuilt = n_spot;
+    return SR_OK;
+  };
+  if (!stamps || s->shape != cluster_shape(c) || s->id_empty != c->id_empty ||
+      s->id_metadata_name != c->id_metadata_name || s->id_unschedulable_key != c->id_unschedulable_key)
+    return rebuild();
+  // previous position of each node, by name (unique per cluster; a repeated
+  // name claims the previous state once)
+  const int32_t ns_str = c->n_strings, nn = c->nodes.n, np = c->pods.n;
+  if (s->pos_of_name.size() < static_cast<size_t>(ns_str)) s->pos_of_name.resize(static_cast<size_t>(ns_str), -1);
+  const int32_t n_old = static_cast<int32_t>(s->nodes.size());
+  for (int32_t o = 0; o < n_old; ++o) {
+    const int32_t nm = s->node_names[o];
+    if (nm >= 0 && nm < ns_str) s->pos_of_name[nm] = o;
+  }
+  std::vector<int32_t> from(static_cast<size_t>(n_spot), -1);
+  bool bad = false;
+  for (int32_t i = 0; i < n_spot && !bad; ++i) {
+    if (spot[i] < 0 || spot[i] >= nn) {
+      bad = true;
+      break;
+    }
+    const int32_t nm = c->nodes.name[spot[i]];
+    if (nm < 0 || nm >= ns_str) continue;
+    const int32_t o = s->pos_of_name[nm];
+    if (o >= 0) {
+      from[i] = o;
+      s->pos_of_name[nm] = -1;  // claimed
+    }
+  }
+  for (int32_t o = 0; o < n_old; ++o) {
+    const int32_t nm = s->node_names[o];
+    if (nm >= 0 && nm < ns_str) s->pos_of_name[nm] = -1;
+  }
+  if (bad) return SR_ERR_INVALID_ARG;
+  // Pass 1 (reads only): the input validated, per position whether the pods
+  // and the static part stand
+  std::vector<uint8_t> keep(static_cast<size_t>(n_spot), 0);  // bit 0: state, bit 1: static part
+  std::atomic<bool> bad_pod{false};
+  std::atomic<size_t> live{0};
+  parallel_for(static_cast<size_t>(n_spot), 64, [&](size_t lo, size_t hi) {
+    bool b = false;
+    size_t my_live = 0;
+    for (size_t i = lo; i < hi; ++i) {
+      const int32_t node = spot[i], j0 = off[node], n = off[node + 1] - j0;
+      my_live += static_cast<size_t>(n);
+      for (int32_t j = j0; j < j0 + n; ++j) b |= static_cast<uint32_t>(idx[j]) >= static_cast<uint32_t>(np);
+      const int32_t o = from[i];
+      if (o < 0 || b) continue;
+      const NodeState& prev = s->state[static_cast<size_t>(o)];
+      bool same = static_cast<int64_t>(prev.pods.size()) == n && prev.npods == n;
+      for (int32_t k = 0; k < n && same; ++k) {
+        if (k + 8 < n) __builtin_prefetch(&stamps[idx[j0 + k + 8]]);  // a gather: a node's pods lie anywhere
+        const uint64_t st = stamps[idx[j0 + k]];
+        same = st != 0 && s->pods[static_cast<size_t>(prev.pods[k])].stamp == st;
+      }
+      keep[i] = static_cast<uint8_t>((same ? 1 : 0) | (spot_node_same(c, node, s->nodes[static_cast<size_t>(o)]) ? 2 : 0));
+    }
+    if (b) bad_pod.store(true, std::memory_order_relaxed);
+    live.fetch_add(my_live, std::memory_order_relaxed);
+  });
+  if (bad_pod.load()) return SR_ERR_INVALID_ARG;
+  if (s->pods.size() > 2 * live.load() + 4096) return rebuild();  // mostly dead entries: compact
+  // Pass 2: kept states and copies move to their new positions (most stay
+  // where they are: only the moved ones go through a side buffer), the rest
+  // is built
+  std::vector<int32_t> moved;
+  for (int32_t i = 0; i < n_spot; ++i)
+    if (keep[i] && from[i] != i) moved.push_back(i);
+  std::vector<NodeState> side_state(moved.size());
+  std::vector<SpotNode> side_node(moved.size());
+  std::vector<uint64_t> side_dfp(moved.size());
+  for (size_t q = 0; q < moved.size(); ++q) {
+    const int32_t i = moved[q], o = from[i];
+    if (keep[i] & 1) side_state[q] = std::move(s->state[o]);
+    if (keep[i] & 2) side_node[q] = std::move(s->nodes[o]);
+    side_dfp[q] = s->node_dfp[o];
+  }
+  s->state.resize(static_cast<size_t>(n_spot));
+  s->nodes.resize(static_cast<size_t>(n_spot));
+  s->node_names.resize(static_cast<size_t>(n_spot));
+  s->node_sfp.resize(static_cast<size_t>(n_spot));
+  s->node_dfp.resize(static_cast<size_t>(n_spot));
+  for (size_t q = 0; q < moved.size(); ++q) {
+    const int32_t i = moved[q];
+    if (keep[i] & 1) s->state[i] = std::move(side_state[q]);
+    if (keep[i] & 2) s->nodes[i] = std::move(side_node[q]);
+    s->node_dfp[i] = side_dfp[q];
+  }
+  parallel_for(static_cast<size_t>(n_spot), 256, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      if (!(keep[i] & 1)) {  // rebuilt below: empty, its vectors' storage kept
+        NodeState& st = s->state[i];
+        std::vector<Port> ports(std::move(st.ports));
+        std::vector<int32_t> pods(std::move(st.pods));
+        ports.clear();
+        pods.clear();
+        st = NodeState{};
+        st.ports = std::move(ports);
+        st.pods = std::move(pods);
+      }
+      if (!(keep[i] & 2)) spot_node_from(c, spot[i], s->nodes[i]);
+      s->node_names[i] = s->nodes[i].name;
+      s->node_sfp[i] = s->nodes[i].static_fp;
+    }
+  });
+  std::vector<int32_t> pos;
+  for (int32_t i = 0; i < n_spot; ++i)
+    if (!(keep[i] & 1)) pos.push_back(i);
+  build_states(s, c, spot, off, idx, pos);
+  for (int32_t i = 0; i < n_spot; ++i)  // the state fingerprint of every node not kept whole
+    if (keep[i] != 3) s->node_dfp[i] = node_state_fp(s->nodes[i], s->state[i]);
+  s->saved.clear();
+  s->saved_dfp.clear();
+  s->anti_total = s->opaque_total = s->unknown_total = s->scalar_unknown_total = s->term_unknown_total = 0;
+  for (const NodeState& st : s->state) {
+    s->anti_total += st.anti;
+    s->opaque_total += st.opaque;
+    s->unknown_total += st.unknown;
+    s->scalar_unknown_total += st.scalar_unknown;
+    s->term_unknown_total += st.term_unknown;
+  }
+  s->version++;
+  if (out_rebuilt) *out_rebuilt = static_cast<int32_t>(pos.size());
   return SR_OK;
 }
 
@@ -418,7 +756,21 @@ extern "C" {
 
 sr_status sr_new_node_map(const sr_cluster* cluster, const sr_node_map_params* params, sr_node_map* out) {
   if (!cluster || !params || !out) return SR_ERR_INVALID_ARG;
-  return sr::new_node_map(cluster, params, out);
+  return sr::new_node_map(cluster, params, out, nullptr, nullptr);
+}
+
+sr_status sr_node_map_cache_create(sr_node_map_cache** out) {
+  if (!out) return SR_ERR_INVALID_ARG;
+  *out = new sr_node_map_cache();
+  return SR_OK;
+}
+
+void sr_node_map_cache_destroy(sr_node_map_cache* cache) { delete cache; }
+
+sr_status sr_new_node_map_cached(sr_node_map_cache* cache, const sr_cluster* cluster, const sr_node_map_params* params,
+                                 sr_node_map* out, int32_t* out_sorted) {
+  if (!cluster || !params || !out) return SR_ERR_INVALID_ARG;
+  return sr::new_node_map(cluster, params, out, cache, out_sorted);
 }
 
 int32_t sr_node_has_label(const sr_cluster* cluster, int32_t node, const sr_node_label* label) {
@@ -430,6 +782,13 @@ sr_status sr_snapshot_create(const sr_cluster* cluster, const int32_t* spot_node
                              const int32_t* node_pod_off, const int32_t* node_pod_idx, sr_snapshot** out) {
   if (!cluster || !out) return SR_ERR_INVALID_ARG;
   return sr::snapshot_create(cluster, spot_nodes, n_spot, node_pod_off, node_pod_idx, out);
+}
+
+sr_status sr_snapshot_refresh(sr_snapshot* snap, const sr_cluster* cluster, const int32_t* spot_nodes,
+                              int32_t n_spot, const int32_t* node_pod_off, const int32_t* node_pod_idx,
+                              int32_t* out_rebuilt) {
+  if (!snap || !cluster) return SR_ERR_INVALID_ARG;
+  return sr::snapshot_refresh(snap, cluster, spot_nodes, n_spot, node_pod_off, node_pod_idx, out_rebuilt);
 }
 
 void sr_snapshot_destroy(sr_snapshot* snap) { delete snap; }

@@ -352,3 +352,63 @@ def test_ticks_with_pod_stamps(checker, seed):
                 capi.load_planner().sr_snapshot_destroy(h)
             from test_gpu_parity import compare_plans
             compare_plans(o, p, off, None)
+
+
+@pytest.mark.parametrize("config", [3, 5])
+def test_ticks_kept_node_map_and_snapshot(checker, config):
+    """A long-running planner's housekeeping ticks: the cluster changes between
+    ticks (pods change requests, move, leave; stamps with them), the node map
+    comes from the node map cache and the snapshot is the previous tick's,
+    refreshed (sr_snapshot_refresh).  Every tick's node map equals the oracle's
+    and every plan equals the oracle's on a snapshot built from scratch."""
+    from oracle_lib import oracle_new_node_map
+    sc = SynthCluster(config, seed=23, n_on_demand=200, n_spot=450)
+    lib = capi.load_planner()
+    cl = sc.cluster
+    cpu = [np.ctypeslib.as_array(a, shape=(sc.n_pods,)) for a in
+           (cl.pods.cpu_sort_milli, cl.pods.req_milli_cpu, cl.acc_milli_cpu) if a]
+    node = np.ctypeslib.as_array(cl.pods.node, shape=(sc.n_pods,))
+    stamps = np.ctypeslib.as_array(cl.pod_stamp, shape=(sc.n_pods,))
+    saved = [a.copy() for a in cpu] + [node.copy(), stamps.copy()]
+    cache = ctypes.c_void_p()
+    assert lib.sr_node_map_cache_create(ctypes.byref(cache)) == capi.SR_OK
+    rng = np.random.default_rng(config)
+    h, rebuilt_total = None, 0
+    try:
+        for tick in range(10):
+            if tick:
+                for p in rng.integers(0, sc.n_pods, 6):
+                    for a in cpu:
+                        a[p] = max(0, int(a[p]) + int(rng.integers(-50, 200)))
+                    stamps[p] += 2
+                for p in rng.integers(0, sc.n_pods, 2):
+                    node[p] = rng.integers(-1, sc.n_nodes)
+                    stamps[p] += 2
+            nm = new_node_map(lambda cp, pp, mp: lib.sr_new_node_map_cached(cache, cp, pp, mp, None), sc.ptr,
+                              sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+            orc = oracle_new_node_map(sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+            for f in ("spot", "on_demand", "node_pod_off", "node_pod_idx", "requested_cpu"):
+                assert np.array_equal(getattr(nm, f), getattr(orc, f)), (tick, f)
+            args = (sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot), capi.ptr(nm.node_pod_off, capi.P32),
+                    capi.ptr(nm.node_pod_idx, capi.P32))
+            if h is None:
+                h = ctypes.c_void_p()
+                assert lib.sr_snapshot_create(*args, ctypes.byref(h)) == capi.SR_OK
+            else:
+                rebuilt = ctypes.c_int32()
+                assert lib.sr_snapshot_refresh(h, *args, ctypes.byref(rebuilt)) == capi.SR_OK
+                rebuilt_total += rebuilt.value
+            cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+            osnap = OracleSnapshot(sc.ptr, orc.spot, orc.node_pod_off, orc.node_pod_idx)
+            p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+            o = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
+            assert np.array_equal(p.status, o["status"]), tick
+            assert np.array_equal(p.node_of_pod, o["node_of_pod"]), tick
+            assert p.winner == o["winner"], tick
+        assert 0 < rebuilt_total < 9 * len(nm.spot) // 4, rebuilt_total  # only the changed nodes
+    finally:
+        for a, b in zip(cpu + [node, stamps], saved):
+            a[:] = b
+        if h is not None:
+            lib.sr_snapshot_destroy(h)
+        lib.sr_node_map_cache_destroy(cache)
