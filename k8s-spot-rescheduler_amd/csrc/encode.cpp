@@ -483,6 +483,65 @@ void intern_groups(WordDict& dict, const int32_t* g, int32_t n_groups, std::vect
   if (used) *used = i;
 }
 
+// Moves the bits at the positions perm_k of a [Wp] row to where their nodes went.
+void permute_row(const EncoderCache& C, uint64_t* row, std::vector<uint8_t>& tmp) {
+  const std::vector<int32_t>& k = C.perm_k;
+  tmp.resize(k.size());
+  for (size_t q = 0; q < k.size(); ++q) {
+    const int32_t o = C.perm_src[k[q]];
+    tmp[q] = static_cast<uint8_t>(row[o >> 6] >> (o & 63) & 1);
+  }
+  for (size_t q = 0; q < k.size(); ++q) {
+    const int32_t i = k[q];
+    const uint64_t bit = 1ull << (i & 63);
+    row[i >> 6] = tmp[q] ? (row[i >> 6] | bit) : (row[i >> 6] & ~bit);
+  }
+}
+
+// The spot pool holds the same nodes as the cached view (names and static
+// fingerprints), some at other positions: permute the position-indexed static
+// data (label columns, taint and requirement rows) instead of rebuilding it.
+// The moved positions count as changed nodes for the state view.
+bool permute_static(EncoderCache& C, const sr_snapshot* snap) {
+  const int32_t n = C.n_spot;
+  int32_t max_name = -1;
+  for (int32_t i = 0; i < n; ++i) {
+    if (C.names[i] < 0 || snap->node_names[i] < 0) return false;
+    max_name = std::max(max_name, std::max(C.names[i], snap->node_names[i]));
+  }
+  std::vector<int32_t>& pos = C.pos_scratch;
+  if (pos.size() < static_cast<size_t>(max_name) + 1) pos.resize(static_cast<size_t>(max_name) + 1, -1);
+  for (int32_t i = 0; i < n; ++i) pos[C.names[i]] = i;
+  C.perm_src.assign(static_cast<size_t>(n), -1);
+  bool ok = true;
+  for (int32_t i = 0; i < n && ok; ++i) {
+    const int32_t nm = snap->node_names[i], o = pos[nm];
+    ok = o >= 0 && C.static_fp[o] == snap->node_sfp[i];
+    C.perm_src[i] = o;
+    pos[nm] = -1;  // claimed: a repeated name fails
+  }
+  for (int32_t i = 0; i < n; ++i) pos[C.names[i]] = -1;
+  if (!ok) return false;
+  C.perm_k.clear();
+  for (int32_t i = 0; i < n; ++i)
+    if (C.perm_src[i] != i) C.perm_k.push_back(i);
+  std::vector<int32_t> vals(C.perm_k.size());
+  for (auto& kc : C.label_col) {
+    std::vector<int32_t>& col = kc.second;
+    for (size_t q = 0; q < C.perm_k.size(); ++q) vals[q] = col[C.perm_src[C.perm_k[q]]];
+    for (size_t q = 0; q < C.perm_k.size(); ++q) col[C.perm_k[q]] = vals[q];
+  }
+  std::vector<uint8_t> tmp;
+  for (size_t t = 0; t < C.taints.size(); ++t) permute_row(C, &C.taint_rows[t * static_cast<size_t>(C.Wp)], tmp);
+  for (size_t r = 0; r < C.req_rows.size(); ++r)
+    if (C.req_row_gen[r] == C.static_gen) permute_row(C, C.req_rows[r].data(), tmp);
+  C.names = snap->node_names;
+  C.static_fp = snap->node_sfp;
+  C.perm_dirty.insert(C.perm_dirty.end(), C.perm_k.begin(), C.perm_k.end());
+  ++C.layout_gen;
+  return true;
+}
+
 // ---- static view: names, labels, taints of the spot pool in NodeInfoArray order
 void refresh_static(EncoderCache& C, const sr_snapshot* snap, int32_t Wp) {
   const int32_t n = static_cast<int32_t>(snap->nodes.size());
@@ -491,6 +550,12 @@ void refresh_static(EncoderCache& C, const sr_snapshot* snap, int32_t Wp) {
          std::equal(C.static_fp.begin(), C.static_fp.end(), snap->node_sfp.begin());
   C.last_static_changed = same ? 0 : 1;
   if (same) return;
+  if (C.n_spot == n && C.Wp == Wp && n > 0 && permute_static(C, snap)) {
+    C.last_static_changed = 2;
+    return;
+  }
+  C.perm_dirty.clear();
+  ++C.layout_gen;
   ++C.static_gen;
   C.n_spot = n;
   C.Wp = Wp;
@@ -528,9 +593,16 @@ sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* e
   const std::vector<uint64_t>& fp = snap->node_dfp;  // kept current by the snapshot
   std::vector<int32_t> changed;
   const bool full = !C.state_valid || C.state_fp.size() != static_cast<size_t>(n);
-  if (!full)
+  if (!full) {
     for (int32_t i = 0; i < n; ++i)
       if (fp[i] != C.state_fp[i]) changed.push_back(i);
+    if (!C.perm_dirty.empty()) {  // permuted positions: another node's records, whatever its fingerprint
+      changed.insert(changed.end(), C.perm_dirty.begin(), C.perm_dirty.end());
+      std::sort(changed.begin(), changed.end());
+      changed.erase(std::unique(changed.begin(), changed.end()), changed.end());
+    }
+  }
+  C.perm_dirty.clear();
   C.last_state_changed = full ? n : static_cast<int32_t>(changed.size());
   if (!full && changed.empty()) return SR_OK;
   C.patched_from = ~0ull;
@@ -1039,6 +1111,11 @@ bool reuse_encode(EncoderCache& C, Workload* w) {
   CandReuse& R = w->reuse;
   const int32_t Wp = w->Wp, n_spot = w->n_spot;
   uint64_t* A = w->atoms.data();
+  if (w->layout_gen != C.layout_gen) {  // the spot order moved (permute_static): every atom row follows
+    std::vector<uint8_t> tmp;
+    for (int32_t a = 0; a < w->n_atoms; ++a) permute_row(C, A + static_cast<size_t>(a) * Wp, tmp);
+    w->layout_gen = C.layout_gen;
+  }
   // pod count and the composites built on it, in the words where it changed
   std::vector<int32_t> words;
   for (int32_t i = 0; i < Wp; ++i)
@@ -1264,7 +1341,8 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   CandReuse& R = w->reuse;
   const bool same_input = stamps && R.shape == C.memo_shape && same_cand_input(R, cands, stamps);
   if (same_input && R.indexed && R.content_gen == C.content_gen && R.static_gen == C.static_gen && R.n_spot == n_spot && R.Wp == Wp &&
-      snap->anti_total == 0 && snap->opaque_total == 0) {
+      (w->layout_gen == C.layout_gen || w->layout_gen + 1 == C.layout_gen) && snap->anti_total == 0 &&
+      snap->opaque_total == 0) {
     w->state_gen = C.state_gen;
     if (reuse_encode(C, w)) {
       C.last_new_specs = 0;
@@ -1299,6 +1377,7 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   w->Wp = Wp;
   w->n_pad = Wp * 64;
   w->state_gen = C.state_gen;
+  w->layout_gen = C.layout_gen;
 
   // ---- pass 1: candidate-level fallback (host-decided)
   w->status_host.assign(static_cast<size_t>(nc), STATUS_PENDING);

@@ -361,6 +361,7 @@ struct Workload {
   int32_t n_pad = 0;    // node arrays padded to Wp*64 entries
   int32_t Wp = 0;       // 64-bit words per bitmask row (even)
   uint64_t state_gen = 0;  // EncoderCache state the workload refers to (node_rec / node_free)
+  uint64_t layout_gen = 0; // EncoderCache node order its atom rows follow
   // ---- atom rows [n_atoms][Wp]: node bitsets every static predicate is built from
   //   atom 0                 len(pods)+1 <= allowed pods
   //   atoms 1 .. R           node matches requirement r (nodeSelector pair, matchExpression, matchField)
@@ -502,6 +503,13 @@ struct EncoderCache {
   std::vector<uint64_t> taint_rows; // [taint][Wp]
   std::vector<uint64_t> req_row_gen;             // [req] static generation of its row (~0: none)
   std::vector<std::vector<uint64_t>> req_rows;   // [req][Wp]
+  // The same nodes (names, static fingerprints) in another order: the view is
+  // permuted, not rebuilt (the spot order follows RequestedCPU, which moves
+  // whenever pods come or go).  layout_gen counts permutations; perm_src[i] is
+  // the previous position of the node now at i, perm_k the positions that
+  // moved; perm_dirty hands them to the state view as changed nodes.
+  uint64_t layout_gen = 0;
+  std::vector<int32_t> perm_src, perm_k, perm_dirty, pos_scratch;
   // ---- state view
   std::vector<uint64_t> state_fp;
   bool state_valid = false;  // the arrays below describe the current static view

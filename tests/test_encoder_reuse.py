@@ -28,17 +28,18 @@ def tool():
     return TOOL
 
 
-def run_check(tool, config, ticks, burst=24, env=None):
+def run_check(tool, config, ticks, burst=24, env=None, mode="reuse"):
     e = dict(os.environ)
     e.update(env or {})
-    out = subprocess.run([tool, str(config), "100000", "reuse", str(ticks), str(burst)], env=e, check=True,
+    out = subprocess.run([tool, str(config), "100000", mode, str(ticks), str(burst)], env=e, check=True,
                          capture_output=True, text=True, timeout=600).stdout
     m = re.search(r"reuse check: (\d+) ticks \((\d+) reused, (\d+) full\), (\d+) pod patches.*mismatches (\d+)", out)
     assert m, out
     ticks_, reused, full, patches, bad = map(int, m.groups())
     one = re.search(r"one-node-changed encode .*reused (\d), pod patches (\d+)", out)
+    moved = re.search(r"spot order moved (\d+)", out)
     return dict(ticks=ticks_, reused=reused, full=full, patches=patches, bad=bad,
-                one_node_reused=int(one.group(1)), out=out)
+                one_node_reused=int(one.group(1)), moved=int(moved.group(1)), out=out)
 
 
 @pytest.mark.parametrize("config", [1, 2, 3])
@@ -66,3 +67,16 @@ def test_host_port_cluster_is_not_reused(tool):
     r = run_check(tool, 5, 20)
     assert r["bad"] == 0, r["out"]
     assert r["reused"] == 0 and r["full"] == r["ticks"], r["out"]
+
+
+@pytest.mark.parametrize("config", [2, 3])
+def test_reuse_survives_spot_order_moves(tool, config):
+    """Pods on spot nodes change their cpu requests between ticks, so
+    NewNodeMap re-sorts the spot list and the snapshot holds the same nodes in
+    another order (nodes/nodes.go:95-97).  The encoder permutes its static view
+    and the kept atom rows (encode.cpp permute_static) instead of rebuilding:
+    every tick stays reused and equals a fresh encode."""
+    r = run_check(tool, config, 60, mode="reuse-perm")
+    assert r["bad"] == 0, r["out"]
+    assert r["moved"] >= 30, r["out"]
+    assert r["reused"] == r["ticks"] and r["full"] == 0, r["out"]

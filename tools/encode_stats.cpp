@@ -1,6 +1,7 @@
 // Host-only harness: NewNodeMap + snapshot + encode_workload on a synthetic
 // config, printing the workload's dimensions and host-side timings (no GPU).
 //   make -C k8s-spot-rescheduler_amd tools && k8s-spot-rescheduler_amd/bin/encode_stats 3 [max candidates] [check | reuse [ticks [burst]]]
+//   (reuse-perm: pods on spot nodes change requests between ticks, the spot order moves)
 // Encodes are timed cold (empty encoder cache), warm (the same snapshot
 // again) and after one spot node changed (a fresh snapshot with one more pod
 // on one node), the steady state of a planner between two ticks.
@@ -133,7 +134,8 @@ int main(int argc, char** argv) {
     }
     printf("state views consistent: %d ticks (%d patched node by node)\n", ticks, patched);
   }
-  if (argc > 3 && std::string(argv[3]) == "reuse") {
+  const bool perm = argc > 3 && std::string(argv[3]) == "reuse-perm";
+  if (argc > 3 && (std::string(argv[3]) == "reuse" || perm)) {
     // candidate-side reuse: every tick a fresh snapshot with a few more (or
     // fewer) pods on random spot nodes and the same candidate input; the
     // reused workload must plan like one encoded from scratch: same atoms,
@@ -147,7 +149,26 @@ int main(int argc, char** argv) {
     int reused = 0, full = 0, bad = 0;
     long patches = 0;
     double ms_reuse = 0, ms_views = 0;
+    int permuted = 0;
     for (int r = 0; r < ticks && !cp.empty(); ++r) {
+      if (perm && r > 0) {
+        // reuse-perm: pods on spot nodes change their cpu request (and stamp):
+        // NewNodeMap re-sorts the spot list, the snapshot follows its order
+        for (int k = 0, nk = 1 + static_cast<int>(rnd(3)); k < nk; ++k) {
+          const int32_t node = spot[rnd(static_cast<uint64_t>(ns))];
+          if (off[node + 1] == off[node]) continue;
+          const int32_t pod = idx[off[node] + static_cast<int32_t>(rnd(static_cast<uint64_t>(off[node + 1] - off[node])))];
+          const int64_t d = static_cast<int64_t>(rnd(400)) - 150;
+          auto bump = [&](const int64_t* a) { const_cast<int64_t*>(a)[pod] = std::max<int64_t>(0, a[pod] + d); };
+          bump(c.pods.cpu_sort_milli);
+          bump(c.pods.req_milli_cpu);
+          if (c.acc_milli_cpu) bump(c.acc_milli_cpu);
+          const_cast<uint64_t*>(c.pod_stamp)[pod] = (x | 1);
+        }
+        std::vector<int32_t> before(spot.begin(), spot.begin() + ns);
+        if (sr_new_node_map(&c, &prm, &m) != SR_OK) return 1;
+        permuted += !std::equal(before.begin(), before.end(), spot.begin());
+      }
       sr_snapshot* s2 = nullptr;
       sr_snapshot_create(&c, spot.data(), ns, off.data(), idx.data(), &s2);
       if (r % 9 == 8) extra.clear();
@@ -199,8 +220,8 @@ int main(int argc, char** argv) {
       sr_snapshot_destroy(s2);
     }
     printf("reuse check: %d ticks (%d reused, %d full), %ld pod patches, reuse encode avg %.3f ms (views %.3f), "
-           "mismatches %d\n", reused + full, reused, full, patches, reused ? ms_reuse / reused : 0.0,
-           reused ? ms_views / reused : 0.0, bad);
+           "spot order moved %d, mismatches %d\n", reused + full, reused, full, patches, reused ? ms_reuse / reused : 0.0,
+           reused ? ms_views / reused : 0.0, permuted, bad);
     if (bad) return 2;
   }
   printf("Wp %d atoms %d classes %d program ops %zu t_rows %zu\n", w.Wp, w.n_atoms, w.n_classes, w.cls_prog.size(),
