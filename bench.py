@@ -555,28 +555,30 @@ def main():
         if stamps_v is not None:
             stamps_v[tick_pod] = stamp_base ^ (0x5A5A5A5A00000000 * k)
 
+    nm_bufs, pfd_bufs = {}, {}
     nm_cache = ctypes.c_void_p()
     assert lib.sr_node_map_cache_create(ctypes.byref(nm_cache)) == capi.SR_OK
     kept_snap = None
     stage_names = ("new_node_map", "pods_for_deletion", "snapshot", "plan_first")
     full_ticks = {"kept": ([], {k: [] for k in stage_names}), "fresh": ([], {k: [] for k in stage_names})}
     tick_first_ok = {}
-    tick_rebuilt, tick_sorted = [], []
+    tick_rebuilt, tick_sorted, tick_plan = [], [], []
     for mode in ("kept", "fresh"):
         for r in range(args.e2e_reps + 1):  # the first tick untimed (the kept path fills its caches)
             set_tick_state(r % 2)
             sorted_n = ctypes.c_int32(0)
             rebuilt = ctypes.c_int32(0)
             t1 = time.perf_counter()
-            if mode == "kept":
+            if mode == "kept":  # the planner's buffers and caches from the previous tick
                 nm2 = new_node_map(lambda cp, pp, mp: lib.sr_new_node_map_cached(nm_cache, cp, pp, mp,
                                                                                  ctypes.byref(sorted_n)),
-                                   sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+                                   sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label, bufs=nm_bufs)
             else:
                 nm2 = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
             t2 = time.perf_counter()
             co2, cp2, _, _, st = pods_for_deletion(lib.sr_pods_for_deletion, sc.ptr, ctypes.byref(sc.drain),
-                                                   nm2.on_demand, nm2.node_pod_off, nm2.node_pod_idx)
+                                                   nm2.on_demand, nm2.node_pod_off, nm2.node_pod_idx,
+                                                   bufs=pfd_bufs if mode == "kept" else None)
             assert st == capi.SR_OK, st
             lo2, lp2, gi2 = shard(co2, cp2, rank, world)
             t3 = time.perf_counter()
@@ -599,6 +601,10 @@ def main():
             st = lib.sr_plan_first(checker.handle, snap2, sc.ptr, ctypes.byref(c2), ctypes.byref(fo))
             assert st == capi.SR_OK, checker.last_error()
             t5 = time.perf_counter()
+            tq = checker.timing()
+            if r and mode == "kept":
+                tick_plan.append((tq.prefix_batches, tq.enc_reused, tq.enc_static_rebuilt, tq.enc_state_nodes,
+                                  tq.ms_pack_host, tq.k0_columns))
             # both paths plan the same cluster state alike
             assert tick_first_ok.setdefault(r % 2, fo.first_ok) == fo.first_ok
             if mode == "fresh":
@@ -638,7 +644,10 @@ def main():
             if full_ticks["kept"][0] else None,
             "full_tick_kept_state": {"nodes_sorted_median": int(np.median(tick_sorted)) if tick_sorted else None,
                                      "snapshot_nodes_rebuilt_median": int(np.median(tick_rebuilt))
-                                     if tick_rebuilt else None},
+                                     if tick_rebuilt else None,
+                                     "plan_first_last": dict(zip(("prefix_batches", "enc_reused", "static_view",
+                                                                  "state_nodes", "encode_ms_last_batch", "k0_columns"),
+                                                                 tick_plan[-1])) if tick_plan else None},
             "full_tick_fresh_median_ms": (round(float(np.median(full_ticks["fresh"][0])), 3)
                                           if full_ticks["fresh"][0] else None),
             "full_tick_fresh_stages_median_ms": {k: round(float(np.median(v)), 3)

@@ -7,6 +7,7 @@
 // skipNodesWithLocalStorage = false, checkReferences = false, no listers,
 // minReplica 0, now), then the DaemonSet-owner filter (:240-256).  Host code:
 // two parallel passes over the on-demand pods, no device work.
+#include <algorithm>
 #include <atomic>
 #include <climits>
 #include <vector>
@@ -111,8 +112,9 @@ int32_t node_list(const sr_cluster* c, const sr_pod_drain* D, const sr_drain_par
 
 }  // namespace
 
-// Two passes over the nodes on the pool: list lengths (and blocking pods),
-// then the lists at their offsets.
+// One pass over the nodes on the pool writes each node's list into a scratch
+// copy of the LIST layout (a list never outgrows its node's pods), then the
+// lists move to their prefix offsets.
 extern "C" sr_status sr_pods_for_deletion(const sr_cluster* c, const sr_pod_drain* D, const sr_drain_params* prm,
                                           const int32_t* nodes, int32_t n_nodes, const int32_t* node_pod_off,
                                           const int32_t* node_pod_idx, int32_t* out_cand_off, int32_t* out_cand_pods,
@@ -120,32 +122,46 @@ extern "C" sr_status sr_pods_for_deletion(const sr_cluster* c, const sr_pod_drai
   if (!c || !D || !prm || n_nodes < 0 || (n_nodes > 0 && (!nodes || !node_pod_off || !node_pod_idx)) ||
       !out_cand_off || !out_cand_pods || !out_block_pod || !out_block_reason || D->n != c->pods.n)
     return SR_ERR_INVALID_ARG;
+  // the scratch is indexed by the nodes' LIST offsets (a malformed node is
+  // reported by node_list, in input order, and writes nothing)
+  auto well_formed = [&](int32_t node) {
+    return node >= 0 && node < c->nodes.n && node_pod_off[node] >= 0 && node_pod_off[node] <= node_pod_off[node + 1];
+  };
+  int32_t span = 0;
+  for (int32_t i = 0; i < n_nodes; ++i)
+    if (well_formed(nodes[i])) span = std::max(span, node_pod_off[nodes[i] + 1]);
+  thread_local std::vector<int32_t> scratch;  // kept per calling thread: a fresh buffer page-faults every call
+  if (scratch.size() < static_cast<size_t>(span)) scratch.resize(static_cast<size_t>(span));
+  int32_t* const lists = scratch.data();  // (the pool's threads name their own thread_local)
   // the error of the first failing node in input order (what the serial loop returned)
   std::atomic<int64_t> first_err{INT64_MAX};
-  auto pass = [&](bool write) {
-    auto body = [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) {
-        sr_status st = SR_OK;
-        int32_t* out = write ? out_cand_pods + out_cand_off[i] : nullptr;
-        const int32_t k = node_list(c, D, prm, nodes[i], node_pod_off, node_pod_idx, out, &out_block_pod[i],
-                                    &out_block_reason[i], &st);
-        if (st != SR_OK) {
-          const int64_t v = static_cast<int64_t>(i) << 8 | st;
-          int64_t cur = first_err.load();
-          while (v < cur && !first_err.compare_exchange_weak(cur, v)) {
-          }
-          return;
+  auto body = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      sr_status st = SR_OK;
+      int32_t* out = well_formed(nodes[i]) ? lists + node_pod_off[nodes[i]] : nullptr;
+      const int32_t k = node_list(c, D, prm, nodes[i], node_pod_off, node_pod_idx, out, &out_block_pod[i],
+                                  &out_block_reason[i], &st);
+      if (st != SR_OK) {
+        const int64_t v = static_cast<int64_t>(i) << 8 | st;
+        int64_t cur = first_err.load();
+        while (v < cur && !first_err.compare_exchange_weak(cur, v)) {
         }
-        if (!write) out_cand_off[i + 1] = k < 0 ? 0 : k;  // lengths, summed below
+        return;
       }
-    };
-    if (n_nodes > 256) sr::parallel_for(static_cast<size_t>(n_nodes), 64, body);
-    else body(0, static_cast<size_t>(n_nodes));
+      out_cand_off[i + 1] = k < 0 ? 0 : k;  // lengths, summed below
+    }
   };
-  out_cand_off[0] = 0;
-  pass(false);
+  if (n_nodes > 256) sr::parallel_for(static_cast<size_t>(n_nodes), 64, body);
+  else body(0, static_cast<size_t>(n_nodes));
   if (first_err.load() != INT64_MAX) return static_cast<sr_status>(first_err.load() & 0xff);
+  out_cand_off[0] = 0;
   for (int32_t i = 0; i < n_nodes; ++i) out_cand_off[i + 1] += out_cand_off[i];
-  pass(true);
+  auto move = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i)
+      std::copy(lists + node_pod_off[nodes[i]], lists + node_pod_off[nodes[i]] + (out_cand_off[i + 1] - out_cand_off[i]),
+                out_cand_pods + out_cand_off[i]);
+  };
+  if (n_nodes > 256) sr::parallel_for(static_cast<size_t>(n_nodes), 256, move);
+  else move(0, static_cast<size_t>(n_nodes));
   return SR_OK;
 }

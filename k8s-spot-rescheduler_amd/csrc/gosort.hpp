@@ -214,4 +214,45 @@ inline void go_sort_slice_parallel(T* data, int n, Less less, Par par, int grain
   par(static_cast<int>(leaves.size()), [&](int i) { S(data, less).finish(leaves[static_cast<size_t>(i)]); });
 }
 
+// Several independent slices, each sorted exactly as go_sort_slice would sort
+// it, their spans sharing each level's pool dispatch.
+template <class T, class Less, class Par>
+inline void go_sort_slices_parallel(const std::vector<std::pair<T*, int>>& slices, Less less, Par par,
+                                    int grain = 4096) {
+  using S = GoSlice<T, Less>;
+  using Span = typename S::Span;
+  struct Item {
+    T* data;
+    Span sp;
+  };
+  std::vector<Item> level, leaves;
+  for (const auto& sl : slices)
+    if (sl.second > 1) (sl.second <= 2 * grain ? leaves : level).push_back(Item{sl.first, Span{0, sl.second, S::depth_of(sl.second)}});
+  while (!level.empty() && leaves.size() < 256) {
+    std::vector<Span> lo(level.size()), hi(level.size());
+    std::vector<char> leaf(level.size());
+    par(static_cast<int>(level.size()), [&](int i) {
+      bool lf = false;
+      const Item& it = level[static_cast<size_t>(i)];
+      S(it.data, less).split(it.sp, grain, &lo[static_cast<size_t>(i)], &hi[static_cast<size_t>(i)], &lf);
+      leaf[static_cast<size_t>(i)] = lf;
+    });
+    std::vector<Item> next;
+    for (size_t i = 0; i < level.size(); ++i) {
+      if (leaf[i]) {
+        leaves.push_back(level[i]);
+      } else {
+        next.push_back(Item{level[i].data, lo[i]});
+        next.push_back(Item{level[i].data, hi[i]});
+      }
+    }
+    level.swap(next);
+  }
+  leaves.insert(leaves.end(), level.begin(), level.end());
+  par(static_cast<int>(leaves.size()), [&](int i) {
+    const Item& it = leaves[static_cast<size_t>(i)];
+    S(it.data, less).finish(it.sp);
+  });
+}
+
 }  // namespace sr

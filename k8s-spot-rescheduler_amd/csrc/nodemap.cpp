@@ -8,6 +8,7 @@
 // rescheduler.go:269,273,366) live here too.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <functional>
 #include <vector>
@@ -27,6 +28,15 @@ struct sr_node_map_cache {
     std::vector<uint64_t> stamps;   // every LISTed pod, list order
     std::vector<int32_t> perm;      // kept pods, sorted: positions in the list
   };
+  // per-call buffers kept across calls (fresh multi-MB buffers page-fault)
+  // and the last call's spot / on-demand sort: its input (key, node) pairs in
+  // node order and its output
+  struct Scratch {
+    std::vector<int32_t> start, listed, cnt, nkept;
+    std::vector<int8_t> kind;
+    std::vector<uint8_t> hit;
+  } scratch;
+  std::vector<std::pair<int64_t, int32_t>> list_in[2], list_out[2];
   uint64_t shape = 0;
   sr_node_map_params params{};
   uint32_t epoch = 0;
@@ -38,10 +48,31 @@ struct sr_node_map_cache {
     entries.clear();
     names.clear();
     slot.clear();
+    for (int k = 0; k < 2; ++k) list_in[k].clear(), list_out[k].clear();
   }
 };
 
 namespace sr {
+
+// Phase timestamps of NewNodeMap / the snapshot refresh for tools/refresh_check's
+// profiling build (-DSR_NM_PROFILE); compiled out otherwise.
+#ifdef SR_NM_PROFILE
+double nm_phase_ms[8];
+#define NM_MARK(i)                                                                                     \
+  do {                                                                                                 \
+    const auto now_ = std::chrono::steady_clock::now();                                               \
+    nm_phase_ms[i] = std::chrono::duration<double, std::milli>(now_ - nm_t_).count();                 \
+    nm_t_ = now_;                                                                                      \
+  } while (0)
+#define NM_START() auto nm_t_ = std::chrono::steady_clock::now()
+#else
+#define NM_MARK(i) \
+  do {             \
+  } while (0)
+#define NM_START() \
+  do {             \
+  } while (0)
+#endif
 
 // isSpotNode / isOnDemandNode (nodes/nodes.go:168-209).
 static bool node_has_label(const sr_cluster* c, int32_t node, const sr_node_label* l) {
@@ -68,11 +99,16 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   const sr_nodes& N = c->nodes;
   const sr_pods& P = c->pods;
   const int32_t nn = N.n, np = P.n;
+  NM_START();
   // Per-node LIST results: counting sort by node index keeps list order.
   // Large clusters: K pod ranges counted and scattered in parallel, range k's
   // pods of a node placed after those of ranges < k (still list order).
-  std::vector<int32_t> start(static_cast<size_t>(nn) + 1, 0);
-  std::vector<int32_t> listed(np > 0 ? np : 1);
+  sr_node_map_cache::Scratch local;
+  sr_node_map_cache::Scratch& W = cache ? cache->scratch : local;
+  std::vector<int32_t>& start = W.start;
+  std::vector<int32_t>& listed = W.listed;
+  start.assign(static_cast<size_t>(nn) + 1, 0);
+  if (listed.size() < static_cast<size_t>(np > 0 ? np : 1)) listed.resize(static_cast<size_t>(np > 0 ? np : 1));
   const size_t K = std::min<size_t>(pool_threads(), np >= (1 << 17) ? static_cast<size_t>(np) >> 16 : 1);
   if (K <= 1) {
     for (int32_t i = 0; i < np; ++i) {
@@ -84,7 +120,8 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
     for (int32_t i = 0; i < np; ++i)
       if (P.node[i] >= 0) listed[cursor[P.node[i]]++] = i;
   } else {
-    std::vector<int32_t> cnt(K * static_cast<size_t>(nn), 0);  // [range][node], then the range's cursor
+    std::vector<int32_t>& cnt = W.cnt;  // [range][node], then the range's cursor
+    cnt.assign(K * static_cast<size_t>(nn), 0);
     std::atomic<bool> bad{false};
     auto range = [&](size_t k, int32_t* lo, int32_t* hi) {
       *lo = static_cast<int32_t>(static_cast<size_t>(np) * k / K);
@@ -129,12 +166,14 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   }
 
   const int64_t* cpu = P.cpu_sort_milli;
+  NM_MARK(0);
   // the reference's less functions (nodes/nodes.go:76-80, 95-101) on (key, id) pairs: the same
   // comparisons, so Go's sort makes the same swaps
   using KV = std::pair<int64_t, int32_t>;
   auto by_key_desc = [](const KV& x, const KV& y) { return x.first > y.first; };
   auto by_key_asc = [](const KV& x, const KV& y) { return x.first < y.first; };
-  std::vector<int8_t> kind(static_cast<size_t>(nn), 0);  // 1 spot, 2 on-demand
+  std::vector<int8_t>& kind = W.kind;  // 1 spot, 2 on-demand
+  kind.assign(static_cast<size_t>(nn), 0);
   parallel_for(static_cast<size_t>(nn), 256, [&](size_t lo, size_t hi) {
     for (size_t node = lo; node < hi; ++node) {
       const bool spot = node_has_label(c, static_cast<int32_t>(node), &p->spot);
@@ -190,12 +229,15 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
     slot_v = &cache->slot;
   }
   const std::vector<int32_t>& slot = *slot_v;
+  NM_MARK(1);
   // Per node (independent, on the pool): the priority filter of
   // getPodsOnNode, RequestedCPU and the pod sort, or the cached sort of the
   // same stamped pods.  Pass 1 counts the kept pods, pass 2 writes them at
   // their prefix offsets.
-  std::vector<int32_t> nkept(static_cast<size_t>(nn) + 1, 0);
-  std::vector<uint8_t> hit(static_cast<size_t>(nn), 0);
+  std::vector<int32_t>& nkept = W.nkept;
+  std::vector<uint8_t>& hit = W.hit;
+  nkept.assign(static_cast<size_t>(nn) + 1, 0);
+  hit.assign(static_cast<size_t>(nn), 0);
   std::atomic<bool> nil_priority{false};
   parallel_for(static_cast<size_t>(nn), 64, [&](size_t lo, size_t hi) {
     for (size_t node = lo; node < hi; ++node) {
@@ -227,6 +269,7 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   });
   if (nil_priority.load()) return SR_ERR_NIL_PRIORITY;
   for (int32_t node = 0; node < nn; ++node) nkept[node + 1] += nkept[node];
+  NM_MARK(2);
   std::atomic<int32_t> sorted{0};
   parallel_for(static_cast<size_t>(nn), 64, [&](size_t lo, size_t hi) {
     std::vector<std::pair<int64_t, int32_t>> kv;  // (cpu, position in the node's list): the sort compares keys held in place
@@ -273,6 +316,7 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
     sorted.fetch_add(my_sorted, std::memory_order_relaxed);
   });
   if (out_sorted) *out_sorted = sorted.load();
+  NM_MARK(3);
   int32_t ns = 0, nod = 0;
   for (int32_t node = 0; node < nn; ++node) {
     if (kind[node] == 1)
@@ -287,15 +331,41 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
       for (size_t i = a; i < b; ++i) fn(static_cast<int>(i));
     });
   };
-  std::vector<KV> kv_spot(static_cast<size_t>(ns)), kv_od(static_cast<size_t>(nod));
-  for (int32_t i = 0; i < ns; ++i) kv_spot[i] = KV(req[out->spot[i]], out->spot[i]);
-  for (int32_t i = 0; i < nod; ++i) kv_od[i] = KV(req[out->on_demand[i]], out->on_demand[i]);
-  go_sort_slice_parallel(kv_spot.data(), ns, by_key_desc, par);
-  go_sort_slice_parallel(kv_od.data(), nod, by_key_asc, par);
-  for (int32_t i = 0; i < ns; ++i) out->spot[i] = kv_spot[i].second;
-  for (int32_t i = 0; i < nod; ++i) out->on_demand[i] = kv_od[i].second;
+  // The on-demand list sorts on ~RequestedCPU with the spot list's less
+  // function (x < y exactly when ~x > ~y: every comparison, so every swap, is
+  // by_key_asc's), so both split over the pool together.  A list whose input
+  // pairs equal the cache's last ones takes its last output.
+  (void)by_key_asc;
+  std::vector<KV> in[2], sorted_v[2];
+  const int32_t len[2] = {ns, nod};
+  const int32_t* ids[2] = {out->spot, out->on_demand};
+  std::vector<std::pair<KV*, int>> todo;
+  bool reuse[2] = {false, false};
+  for (int k = 0; k < 2; ++k) {
+    in[k].resize(static_cast<size_t>(len[k]));
+    for (int32_t i = 0; i < len[k]; ++i) {
+      const int64_t r = req[ids[k][i]];
+      in[k][static_cast<size_t>(i)] = KV(k == 0 ? r : ~r, ids[k][i]);
+    }
+    reuse[k] = cache && cache->list_in[k] == in[k];
+    if (!reuse[k]) {
+      sorted_v[k] = in[k];
+      todo.emplace_back(sorted_v[k].data(), len[k]);
+    }
+  }
+  if (!todo.empty()) go_sort_slices_parallel(todo, by_key_desc, par);
+  int32_t* dst[2] = {out->spot, out->on_demand};
+  for (int k = 0; k < 2; ++k) {
+    const std::vector<KV>& res = reuse[k] ? cache->list_out[k] : sorted_v[k];
+    for (int32_t i = 0; i < len[k]; ++i) dst[k][i] = res[static_cast<size_t>(i)].second;
+    if (cache && !reuse[k]) {
+      cache->list_in[k].swap(in[k]);
+      cache->list_out[k].swap(sorted_v[k]);
+    }
+  }
   *out->n_spot = ns;
   *out->n_on_demand = nod;
+  NM_MARK(4);
   return SR_OK;
 }
 

@@ -119,15 +119,25 @@ class NodeMapArrays:
                                 capi.ptr(self.requested_cpu, capi.P64), capi.ptr(self.free_cpu, capi.P64))
 
 
-def new_node_map(fn, cluster_ptr, n_nodes: int, n_pods: int, od_label, spot_label, priority_threshold=0):
-    """Calls sr_new_node_map-shaped `fn` (the product's, or the oracle's in tests)."""
-    spot = np.zeros(max(n_nodes, 1), np.int32)
-    od = np.zeros(max(n_nodes, 1), np.int32)
-    ns, nod = np.zeros(1, np.int32), np.zeros(1, np.int32)
-    off = np.zeros(n_nodes + 1, np.int32)
-    idx = np.zeros(max(n_pods, 1), np.int32)
-    req = np.zeros(max(n_nodes, 1), np.int64)
-    free = np.zeros(max(n_nodes, 1), np.int64)
+def new_node_map(fn, cluster_ptr, n_nodes: int, n_pods: int, od_label, spot_label, priority_threshold=0,
+                 bufs: Optional[dict] = None):
+    """Calls sr_new_node_map-shaped `fn` (the product's, or the oracle's in tests).
+    `bufs`: output arrays kept across calls (a long-running planner's), filled
+    on first use; the result's arrays are views of them."""
+    def buf(name, n, dt):
+        if bufs is None:
+            return np.zeros(n, dt)
+        a = bufs.get(name)
+        if a is None or len(a) != n:
+            a = bufs[name] = np.zeros(n, dt)
+        return a
+    spot = buf("spot", max(n_nodes, 1), np.int32)
+    od = buf("od", max(n_nodes, 1), np.int32)
+    ns, nod = buf("ns", 1, np.int32), buf("nod", 1, np.int32)
+    off = buf("off", n_nodes + 1, np.int32)
+    idx = buf("idx", max(n_pods, 1), np.int32)
+    req = buf("req", max(n_nodes, 1), np.int64)
+    free = buf("free", max(n_nodes, 1), np.int64)
     m = capi.sr_node_map(capi.ptr(spot, capi.P32), capi.ptr(ns, capi.P32), capi.ptr(od, capi.P32),
                          capi.ptr(nod, capi.P32), capi.ptr(off, capi.P32), capi.ptr(idx, capi.P32),
                          capi.ptr(req, capi.P64), capi.ptr(free, capi.P64))
@@ -135,27 +145,44 @@ def new_node_map(fn, cluster_ptr, n_nodes: int, n_pods: int, od_label, spot_labe
     st = fn(cluster_ptr, ctypes.byref(params), ctypes.byref(m))
     if st != capi.SR_OK:
         raise RuntimeError("new_node_map status %d" % st)
+    if bufs is not None:
+        return NodeMapArrays(spot[: ns[0]], od[: nod[0]], off, idx[: int(off[-1])], req, free)
     return NodeMapArrays(spot[: ns[0]].copy(), od[: nod[0]].copy(), off, idx[: int(off[-1])], req, free)
 
 
 def pods_for_deletion(fn, cluster_ptr, drain_ptr, nodes: np.ndarray, node_pod_off: np.ndarray,
-                      node_pod_idx: np.ndarray, delete_non_replicated: bool = False, owner_filter: bool = True):
+                      node_pod_idx: np.ndarray, delete_non_replicated: bool = False, owner_filter: bool = True,
+                      bufs: Optional[dict] = None):
     """sr_pods_for_deletion-shaped `fn` (the product's, or the oracle's in tests)
-    over `nodes`: (cand_off, cand_pods, block_pod, block_reason, status)."""
+    over `nodes`: (cand_off, cand_pods, block_pod, block_reason, status).
+    `bufs`: output arrays kept across calls (sized for every listed pod)."""
     nodes = np.ascontiguousarray(nodes, np.int32)
     n = len(nodes)
-    off = np.zeros(n + 1, np.int32)
     npo = np.asarray(node_pod_off)
-    total = int(np.sum(npo[nodes + 1] - npo[nodes])) if n else 0
-    pods = np.zeros(max(1, total), np.int32)
-    bp = np.full(max(1, n), -1, np.int32)
-    br = np.zeros(max(1, n), np.int32)
+    if bufs is None:
+        off = np.zeros(n + 1, np.int32)
+        total = int(np.sum(npo[nodes + 1] - npo[nodes])) if n else 0
+        pods = np.zeros(max(1, total), np.int32)
+        bp = np.full(max(1, n), -1, np.int32)
+        br = np.zeros(max(1, n), np.int32)
+    else:  # the kept arrays: room for every pod of the node map (a list never holds more)
+        def buf(name, k):
+            a = bufs.get(name)
+            if a is None or len(a) < k:
+                a = bufs[name] = np.zeros(k, np.int32)
+            return a
+        off = buf("off", n + 1)[: n + 1]
+        pods = buf("pods", max(1, int(npo[-1])))
+        bp = buf("bp", max(1, n))[: max(1, n)]
+        br = buf("br", max(1, n))[: max(1, n)]
     prm = capi.sr_drain_params(1 if delete_non_replicated else 0, 0,  # rescheduler.go:231 arguments 3, 4
                                1 if owner_filter else 0)
     st = fn(cluster_ptr, drain_ptr, ctypes.byref(prm), capi.ptr(nodes, capi.P32), n,
             capi.ptr(np.ascontiguousarray(node_pod_off, np.int32), capi.P32),
             capi.ptr(np.ascontiguousarray(node_pod_idx, np.int32), capi.P32), capi.ptr(off, capi.P32),
             capi.ptr(pods, capi.P32), capi.ptr(bp, capi.P32), capi.ptr(br, capi.P32))
+    if bufs is not None:
+        return off, pods[: int(off[-1])], bp[:n], br[:n], st
     return off, pods[: int(off[-1])].copy(), bp[:n], br[:n], st
 
 

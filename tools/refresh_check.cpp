@@ -18,6 +18,10 @@
 #include "../k8s-spot-rescheduler_amd/csrc/host.hpp"
 #include "../k8s-spot-rescheduler_amd/csrc/synth/sr_synth.h"
 
+#ifdef SR_NM_PROFILE
+namespace sr { extern double nm_phase_ms[8]; }
+#endif
+
 namespace {
 
 double ms_since(std::chrono::steady_clock::time_point a) {
@@ -258,6 +262,7 @@ int main(int argc, char** argv) {
 
   // timing: ticks with one pod's requests changed
   std::vector<double> t_map, t_map_c, t_create, t_refresh;
+  std::vector<double> ph[5];
   for (int r = 0; r < 15; ++r) {
     mutate(0);
     sr_node_map m1 = ref.view(nn, np), m2 = got.view(nn, np);
@@ -267,6 +272,9 @@ int main(int argc, char** argv) {
     t0 = std::chrono::steady_clock::now();
     sr_new_node_map_cached(cache, &c, &prm, &m2, nullptr);
     t_map_c.push_back(ms_since(t0));
+#ifdef SR_NM_PROFILE
+    for (int k = 0; k < 5; ++k) ph[k].push_back(sr::nm_phase_ms[k]);
+#endif
     sr_snapshot* fresh = nullptr;
     t0 = std::chrono::steady_clock::now();
     sr_snapshot_create(&c, ref.spot.data(), ref.ns, ref.off.data(), ref.idx.data(), &fresh);
@@ -282,6 +290,10 @@ int main(int argc, char** argv) {
   };
   printf("one-pod ticks (median ms): new_node_map %.3f cached %.3f | snapshot_create %.3f refresh %.3f\n", med(t_map),
          med(t_map_c), med(t_create), med(t_refresh));
+#ifdef SR_NM_PROFILE
+  printf("cached node map phases (median ms): LIST grouping %.3f kinds+slots %.3f pass1 %.3f pass2 %.3f lists %.3f\n",
+         med(ph[0]), med(ph[1]), med(ph[2]), med(ph[3]), med(ph[4]));
+#endif
   sr_snapshot_destroy(kept);
   sr_node_map_cache_destroy(cache);
   sr_synth_destroy(syn);

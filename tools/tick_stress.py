@@ -6,8 +6,14 @@ every-candidate plan, each against the oracle on the same mutated snapshot.
 Exercises the persistent encoder's caches (state patches, port-conflict rows,
 staging arena, node-record patch uploads).  GPU required.
 
-  python tools/tick_stress.py [--seconds 150] [--wide] [--reuse]
+  python tools/tick_stress.py [--seconds 150] [--wide] [--reuse] [--moves]
+
+--moves: pods on spot nodes also change their cpu requests (and stamps)
+between ticks, so NewNodeMap re-sorts the spot list; the node map comes from a
+node map cache and the snapshot is the previous tick's, refreshed
+(sr_snapshot_refresh), while the oracle rebuilds both from scratch.
 """
+import ctypes
 import argparse
 import os
 import sys
@@ -33,6 +39,9 @@ def main():
     ap.add_argument("--reuse", action="store_true",
                     help="every tick plans all candidates on one planner per cluster: the same stamped input tick "
                          "after tick, so the candidate side is reused (CandReuse) and its records patched on the device")
+    ap.add_argument("--moves", action="store_true",
+                    help="spot pods change cpu requests between ticks (the spot order moves); kept node map cache and "
+                         "refreshed snapshot")
     a = ap.parse_args()
     lib = capi.load_planner()
     os.environ["SR_NODE_PATCH"] = "0"  # the second planner uploads a changed node section whole
@@ -50,6 +59,18 @@ def main():
         nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
         maps.append((nm, *build_candidates(nm, sc.pod_flags())))
     extra = [[], []]
+    caches, kept = [], [None, None]
+    if a.moves:
+        from oracle_lib import oracle_new_node_map
+        for _ in clusters:
+            caches.append(ctypes.c_void_p())
+            assert lib.sr_node_map_cache_create(ctypes.byref(caches[-1])) == capi.SR_OK
+        views = []
+        for sc in clusters:
+            cl = sc.cluster
+            views.append(([np.ctypeslib.as_array(x, shape=(sc.n_pods,)) for x in
+                           (cl.pods.cpu_sort_milli, cl.pods.req_milli_cpu, cl.acc_milli_cpu) if x],
+                          np.ctypeslib.as_array(cl.pod_stamp, shape=(sc.n_pods,))))
     per_cluster = [PredicateChecker(0), PredicateChecker(0)] if a.reuse else []
     reused = patches = 0
     while time.time() - t0 < a.seconds:
@@ -61,7 +82,32 @@ def main():
         for _ in range(int(rng.integers(1, 4))):
             extra[ci].append((int(cand_pods[rng.integers(len(cand_pods))]), int(rng.integers(len(nm.spot)))))
         extra[ci] = extra[ci][-6:]
-        h = T._snapshot(lib, sc, nm)
+        if a.moves:
+            cpu, stamps = views[ci]
+            for _ in range(int(rng.integers(1, 4))):  # pods on spot nodes change requests: the spot order moves
+                node = nm.spot[rng.integers(len(nm.spot))]
+                lo, hi = nm.node_pod_off[node], nm.node_pod_off[node + 1]
+                if hi > lo:
+                    pod = nm.node_pod_idx[rng.integers(lo, hi)]
+                    d = int(rng.integers(-150, 250))
+                    for x in cpu:
+                        x[pod] = max(0, int(x[pod]) + d)
+                    stamps[pod] += 2
+            nm = new_node_map(lambda cp, pp, mp: lib.sr_new_node_map_cached(caches[ci], cp, pp, mp, None), sc.ptr,
+                              sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+            orc = oracle_new_node_map(sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+            assert np.array_equal(nm.spot, orc.spot) and np.array_equal(nm.node_pod_idx, orc.node_pod_idx), ticks
+            maps[ci] = (nm, cand_off, cand_pods)
+            args = (sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot), capi.ptr(nm.node_pod_off, capi.P32),
+                    capi.ptr(nm.node_pod_idx, capi.P32))
+            if kept[ci] is None:
+                kept[ci] = ctypes.c_void_p()
+                assert lib.sr_snapshot_create(*args, ctypes.byref(kept[ci])) == capi.SR_OK
+            else:
+                assert lib.sr_snapshot_refresh(kept[ci], *args, None) == capi.SR_OK
+            h = kept[ci]
+        else:
+            h = T._snapshot(lib, sc, nm)
         osnap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
         for pod, pos in extra[ci]:
             assert lib.sr_snapshot_add_pod(h, sc.ptr, pod, pos) == capi.SR_OK
@@ -84,7 +130,8 @@ def main():
             assert np.array_equal(p.status, ref_all["status"]), ticks
             assert np.array_equal(p.node_of_pod, ref_all["node_of_pod"]), ticks
             assert p.winner == ref_all["winner"], ticks
-        lib.sr_snapshot_destroy(h)
+        if not a.moves:
+            lib.sr_snapshot_destroy(h)
         ticks += 1
         if ticks % 20 == 0:
             print("  %d ticks, %.0f s" % (ticks, time.time() - t0), flush=True)
@@ -92,6 +139,11 @@ def main():
     default.close()
     for ck in per_cluster:
         ck.close()
+    for h in kept:
+        if h is not None:
+            lib.sr_snapshot_destroy(h)
+    for cache in caches:
+        lib.sr_node_map_cache_destroy(cache)
     print("tick stress: %d ticks in %.0f s, every plan equal to the oracle%s" % (
         ticks, time.time() - t0, " (%d reused, %d pod patches)" % (reused, patches) if a.reuse else ""))
     return 0
