@@ -63,7 +63,6 @@ struct SnapPod {
   uint32_t lab, nlab;       // labels: sr_snapshot::lkey / lval [lab, lab + nlab)
   uint32_t terms, nterms;   // anti-affinity terms: sr_snapshot::term_words [terms, terms + nterms),
                             // {n words, words...} per term (rare)
-  uint64_t stamp;           // the pod's sr_cluster.pod_stamp when it entered (0: unknown; sr_snapshot_refresh)
 };
 
 // std::allocator that default-initializes on resize() / emplace_back(): the
@@ -184,6 +183,8 @@ struct sr_snapshot {
   std::vector<int32_t> node_names;
   std::vector<uint64_t> node_sfp, node_dfp, saved_dfp;
   std::vector<sr::SnapPod, sr::UninitAlloc<sr::SnapPod>> pods;  // every pod ever added (NodeState::pods index it)
+  std::vector<uint64_t, sr::UninitAlloc<uint64_t>> stamps;       // ... their sr_cluster.pod_stamp (0: unknown),
+                                                                 // read by sr_snapshot_refresh
   std::vector<int32_t, sr::UninitAlloc<int32_t>> lkey, lval;     // the pods' labels (one arena: no allocation per pod)
   std::vector<int32_t> term_words;  // the pods' anti-affinity terms (one arena)
   size_t fork_pods = 0;           // pods.size() at Fork: Revert drops the rest

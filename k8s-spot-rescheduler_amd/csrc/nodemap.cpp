@@ -57,7 +57,7 @@ namespace sr {
 // Phase timestamps of NewNodeMap / the snapshot refresh for tools/refresh_check's
 // profiling build (-DSR_NM_PROFILE); compiled out otherwise.
 #ifdef SR_NM_PROFILE
-double nm_phase_ms[8];
+double nm_phase_ms[10];
 #define NM_MARK(i)                                                                                     \
   do {                                                                                                 \
     const auto now_ = std::chrono::steady_clock::now();                                               \
@@ -121,7 +121,7 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
       if (P.node[i] >= 0) listed[cursor[P.node[i]]++] = i;
   } else {
     std::vector<int32_t>& cnt = W.cnt;  // [range][node], then the range's cursor
-    cnt.assign(K * static_cast<size_t>(nn), 0);
+    if (cnt.size() < K * static_cast<size_t>(nn)) cnt.resize(K * static_cast<size_t>(nn));
     std::atomic<bool> bad{false};
     auto range = [&](size_t k, int32_t* lo, int32_t* hi) {
       *lo = static_cast<int32_t>(static_cast<size_t>(np) * k / K);
@@ -132,6 +132,7 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
         int32_t lo, hi;
         range(k, &lo, &hi);
         int32_t* c = &cnt[k * static_cast<size_t>(nn)];
+        std::fill(c, c + nn, 0);  // each range zeroes its own row
         for (int32_t i = lo; i < hi; ++i) {
           const int32_t nd = P.node[i];
           if (nd < -1 || nd >= nn) bad.store(true, std::memory_order_relaxed);
@@ -140,16 +141,20 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
       }
     });
     if (bad.load()) return SR_ERR_INVALID_ARG;
-    parallel_for(static_cast<size_t>(nn), 4096, [&](size_t a, size_t b) {  // per node: total, then per-range offsets
-      for (size_t nd = a; nd < b; ++nd) {
-        int32_t acc = 0;
-        for (size_t k = 0; k < K; ++k) {
-          const int32_t x = cnt[k * static_cast<size_t>(nn) + nd];
-          cnt[k * static_cast<size_t>(nn) + nd] = acc;
-          acc += x;
+    // per node: the per-range offsets and the total, a block of nodes at a
+    // time with each range's row read in sequence (the rows lie nn apart)
+    parallel_for(static_cast<size_t>(nn), 2048, [&](size_t a, size_t b) {
+      int32_t acc[2048];
+      std::fill(acc, acc + (b - a), 0);
+      for (size_t k = 0; k < K; ++k) {
+        int32_t* c = &cnt[k * static_cast<size_t>(nn)];
+        for (size_t nd = a; nd < b; ++nd) {
+          const int32_t x = c[nd];
+          c[nd] = acc[nd - a];
+          acc[nd - a] += x;
         }
-        start[nd + 1] = acc;
       }
+      for (size_t nd = a; nd < b; ++nd) start[nd + 1] = acc[nd - a];
     });
     for (int32_t i = 0; i < nn; ++i) start[i + 1] += start[i];
     parallel_for(K, 1, [&](size_t a, size_t b) {
@@ -373,7 +378,6 @@ void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out, int32_t* k, i
                    std::vector<int32_t>* terms) {
   *out = SnapPod{};
   out->ns = -1;
-  out->stamp = c->pod_stamp ? c->pod_stamp[pod] : 0;
   out->anti = has_anti_terms(c, pod) ? 1 : 0;
   out->opaque = anti_opaque(c, pod) ? 1 : 0;
   out->term = c->spread ? (c->spread->terminating[pod] ? 1 : 0) : 2;
@@ -483,6 +487,7 @@ bool aff_opaque(const sr_cluster* c, int32_t pod) {
 void snapshot_add_pod(sr_snapshot* s, const sr_cluster* c, int32_t pod, int32_t pos) {
   const int32_t store = static_cast<int32_t>(s->pods.size());
   s->pods.emplace_back();
+  s->stamps.push_back(c->pod_stamp ? c->pod_stamp[pod] : 0);
   const uint32_t lab = static_cast<uint32_t>(s->lkey.size());
   s->lkey.resize(lab + pod_label_count(c, pod));
   s->lval.resize(s->lkey.size());
@@ -572,6 +577,7 @@ static void build_states(sr_snapshot* s, const sr_cluster* c, const int32_t* spo
     for (size_t q = 0; q < n; ++q) lbase[q + 1] = lbase[q] + cnt[q];
   }
   s->pods.resize(static_cast<size_t>(base[n]));
+  s->stamps.resize(static_cast<size_t>(base[n]));
   s->lkey.resize(lbase[n]);
   s->lval.resize(lbase[n]);
   constexpr size_t kNodeChunk = 32;
@@ -586,6 +592,7 @@ static void build_states(sr_snapshot* s, const sr_cluster* c, const int32_t* spo
       for (int32_t j = off[node]; j < off[node + 1]; ++j) {
         const int32_t store = base[q] + (j - off[node]);
         snap_pod_from(c, idx[j], &s->pods[store], s->lkey.data(), s->lval.data(), lab, terms);
+        s->stamps[store] = c->pod_stamp ? c->pod_stamp[idx[j]] : 0;
         lab += s->pods[store].nlab;
         state_add_pod(st, c, idx[j], s->pods[store], store);
       }
@@ -702,6 +709,7 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
   // previous position of each node, by name (unique per cluster; a repeated
   // name claims the previous state once)
   const int32_t ns_str = c->n_strings, nn = c->nodes.n, np = c->pods.n;
+  NM_START();
   if (s->pos_of_name.size() < static_cast<size_t>(ns_str)) s->pos_of_name.resize(static_cast<size_t>(ns_str), -1);
   const int32_t n_old = static_cast<int32_t>(s->nodes.size());
   for (int32_t o = 0; o < n_old; ++o) {
@@ -728,6 +736,7 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
     if (nm >= 0 && nm < ns_str) s->pos_of_name[nm] = -1;
   }
   if (bad) return SR_ERR_INVALID_ARG;
+  NM_MARK(5);
   // Pass 1 (reads only): the input validated, per position whether the pods
   // and the static part stand
   std::vector<uint8_t> keep(static_cast<size_t>(n_spot), 0);  // bit 0: state, bit 1: static part
@@ -736,19 +745,33 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
   parallel_for(static_cast<size_t>(n_spot), 64, [&](size_t lo, size_t hi) {
     bool b = false;
     size_t my_live = 0;
-    for (size_t i = lo; i < hi; ++i) {
+    // the stamps are a gather (a node's pods lie anywhere in the cluster's
+    // arrays): the next node's are requested while this one is compared
+    auto prefetch_node = [&](size_t i) {
+      const int32_t nd = spot[i];
+      for (int32_t j = off[nd]; j < off[nd + 1]; ++j)
+        if (static_cast<uint32_t>(idx[j]) < static_cast<uint32_t>(np)) __builtin_prefetch(&stamps[idx[j]]);
+    };
+    if (lo < hi) prefetch_node(lo);
+    for (size_t i = lo; i < hi && !b; ++i) {
+      if (i + 1 < hi) prefetch_node(i + 1);
       const int32_t node = spot[i], j0 = off[node], n = off[node + 1] - j0;
       my_live += static_cast<size_t>(n);
-      for (int32_t j = j0; j < j0 + n; ++j) b |= static_cast<uint32_t>(idx[j]) >= static_cast<uint32_t>(np);
       const int32_t o = from[i];
-      if (o < 0 || b) continue;
-      const NodeState& prev = s->state[static_cast<size_t>(o)];
-      bool same = static_cast<int64_t>(prev.pods.size()) == n && prev.npods == n;
-      for (int32_t k = 0; k < n && same; ++k) {
-        if (k + 8 < n) __builtin_prefetch(&stamps[idx[j0 + k + 8]]);  // a gather: a node's pods lie anywhere
-        const uint64_t st = stamps[idx[j0 + k]];
-        same = st != 0 && s->pods[static_cast<size_t>(prev.pods[k])].stamp == st;
+      const NodeState* prev = o >= 0 ? &s->state[static_cast<size_t>(o)] : nullptr;
+      bool same = prev && static_cast<int64_t>(prev->pods.size()) == n && prev->npods == n;
+      for (int32_t k = 0; k < n; ++k) {  // the pods validated and, while equal, their stamps compared
+        const int32_t pod = idx[j0 + k];
+        if (static_cast<uint32_t>(pod) >= static_cast<uint32_t>(np)) {
+          b = true;
+          break;
+        }
+        if (same) {
+          const uint64_t st = stamps[pod];
+          same = st != 0 && s->stamps[static_cast<size_t>(prev->pods[k])] == st;
+        }
       }
+      if (b || !prev) continue;
       keep[i] = static_cast<uint8_t>((same ? 1 : 0) | (spot_node_same(c, node, s->nodes[static_cast<size_t>(o)]) ? 2 : 0));
     }
     if (b) bad_pod.store(true, std::memory_order_relaxed);
@@ -756,6 +779,7 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
   });
   if (bad_pod.load()) return SR_ERR_INVALID_ARG;
   if (s->pods.size() > 2 * live.load() + 4096) return rebuild();  // mostly dead entries: compact
+  NM_MARK(6);
   // Pass 2: kept states and copies move to their new positions (most stay
   // where they are: only the moved ones go through a side buffer), the rest
   // is built
@@ -799,6 +823,7 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
       s->node_sfp[i] = s->nodes[i].static_fp;
     }
   });
+  NM_MARK(7);
   std::vector<int32_t> pos;
   for (int32_t i = 0; i < n_spot; ++i)
     if (!(keep[i] & 1)) pos.push_back(i);
@@ -816,6 +841,7 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
     s->term_unknown_total += st.term_unknown;
   }
   s->version++;
+  NM_MARK(8);
   if (out_rebuilt) *out_rebuilt = static_cast<int32_t>(pos.size());
   return SR_OK;
 }
@@ -890,6 +916,7 @@ sr_status sr_snapshot_revert(sr_snapshot* snap) {
   snap->saved.clear();
   snap->node_dfp.swap(snap->saved_dfp);
   snap->pods.resize(snap->fork_pods);  // pods added since Fork are referenced by no state any more
+  snap->stamps.resize(snap->fork_pods);
   snap->lkey.resize(snap->fork_labels);
   snap->lval.resize(snap->fork_labels);
   snap->term_words.resize(snap->fork_terms);

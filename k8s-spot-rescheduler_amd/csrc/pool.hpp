@@ -36,21 +36,22 @@ class Pool {
     n_ = n;
     grain_ = grain;
     next_.store(0);
-    pending_ = workers_.size();
-    ++gen_;
+    gen_.fetch_add(1, std::memory_order_release);
     cv_.notify_all();
     lk.unlock();
     run_chunks();
+    // every chunk is claimed; the workers that claimed one are counted in
+    // in_flight_ (they joined under the lock before claiming)
     lk.lock();
-    done_cv_.wait(lk, [&] { return pending_ == 0; });
-    job_ = nullptr;
+    done_cv_.wait(lk, [&] { return in_flight_ == 0; });
+    job_ = nullptr;  // a worker waking for this generation now skips it
   }
 
   ~Pool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
-      ++gen_;
+      gen_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
     for (auto& t : workers_) t.join();
@@ -72,28 +73,39 @@ class Pool {
     }
   }
 
+  // A worker spins a little (~tens of microseconds) for the next generation
+  // before it sleeps: a host phase issues parallel loops back to back, and a
+  // condition-variable wake-up per loop and worker costs more than the loop.
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      for (int i = 0; i < kSpin && gen_.load(std::memory_order_acquire) == seen; ++i) {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return gen_ != seen; });
-      seen = gen_;
+      cv_.wait(lk, [&] { return gen_.load(std::memory_order_relaxed) != seen; });
+      seen = gen_.load(std::memory_order_relaxed);
       if (stop_) return;
+      if (!job_) continue;  // that generation's loop is over
+      ++in_flight_;
       lk.unlock();
       run_chunks();
       lk.lock();
-      if (--pending_ == 0) done_cv_.notify_one();
+      if (--in_flight_ == 0) done_cv_.notify_one();
     }
   }
 
+  static constexpr int kSpin = 4000;
   std::vector<std::thread> workers_;
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(size_t, size_t)>* job_ = nullptr;
   size_t n_ = 0, grain_ = 1;
   std::atomic<size_t> next_{0};
-  size_t pending_ = 0;
-  uint64_t gen_ = 0;
+  size_t in_flight_ = 0;
+  std::atomic<uint64_t> gen_{0};
   bool stop_ = false;
 };
 

@@ -19,7 +19,7 @@
 #include "../k8s-spot-rescheduler_amd/csrc/synth/sr_synth.h"
 
 #ifdef SR_NM_PROFILE
-namespace sr { extern double nm_phase_ms[8]; }
+namespace sr { extern double nm_phase_ms[10]; }
 #endif
 
 namespace {
@@ -88,7 +88,7 @@ const char* snapshot_diff(const sr_snapshot* a, const sr_snapshot* b, size_t* at
     for (size_t k = 0; k < s.pods.size(); ++k) {
       const sr::SnapPod &p = a->pods[s.pods[k]], &q = b->pods[t.pods[k]];
       if (p.ns != q.ns || p.meta != q.meta || p.anti != q.anti || p.opaque != q.opaque || p.term != q.term ||
-          p.stamp != q.stamp || p.nlab != q.nlab || p.nterms != q.nterms)
+          a->stamps[s.pods[k]] != b->stamps[t.pods[k]] || p.nlab != q.nlab || p.nterms != q.nterms)
         return "pod copy";
       if (!std::equal(a->lkey.begin() + p.lab, a->lkey.begin() + p.lab + p.nlab, b->lkey.begin() + q.lab) ||
           !std::equal(a->lval.begin() + p.lab, a->lval.begin() + p.lab + p.nlab, b->lval.begin() + q.lab))
@@ -262,7 +262,10 @@ int main(int argc, char** argv) {
 
   // timing: ticks with one pod's requests changed
   std::vector<double> t_map, t_map_c, t_create, t_refresh;
-  std::vector<double> ph[5];
+  std::vector<double> ph[9], t_pfd;
+  sr_pod_drain drain;
+  sr_synth_drain(syn, &drain);
+  const sr_drain_params dprm{0, 0, 1};
   for (int r = 0; r < 15; ++r) {
     mutate(0);
     sr_node_map m1 = ref.view(nn, np), m2 = got.view(nn, np);
@@ -282,17 +285,30 @@ int main(int argc, char** argv) {
     t0 = std::chrono::steady_clock::now();
     sr_snapshot_refresh(kept, &c, ref.spot.data(), ref.ns, ref.off.data(), ref.idx.data(), nullptr);
     t_refresh.push_back(ms_since(t0));
+#ifdef SR_NM_PROFILE
+    for (int k = 5; k < 9; ++k) ph[k].push_back(sr::nm_phase_ms[k]);
+#endif
+    {  // the candidate lists of the tick (podsForDeletion over the on-demand nodes)
+      std::vector<int32_t> coff(ref.nod + 1), cpods(std::max(1, ref.off.back())), bp(std::max(1, ref.nod)),
+          br(std::max(1, ref.nod));
+      t0 = std::chrono::steady_clock::now();
+      sr_pods_for_deletion(&c, &drain, &dprm, ref.od.data(), ref.nod, ref.off.data(), ref.idx.data(), coff.data(),
+                           cpods.data(), bp.data(), br.data());
+      t_pfd.push_back(ms_since(t0));
+    }
     sr_snapshot_destroy(fresh);
   }
   auto med = [](std::vector<double> v) {
     std::sort(v.begin(), v.end());
     return v[v.size() / 2];
   };
-  printf("one-pod ticks (median ms): new_node_map %.3f cached %.3f | snapshot_create %.3f refresh %.3f\n", med(t_map),
-         med(t_map_c), med(t_create), med(t_refresh));
+  printf("one-pod ticks (median ms): new_node_map %.3f cached %.3f | snapshot_create %.3f refresh %.3f | "
+         "pods_for_deletion %.3f\n", med(t_map), med(t_map_c), med(t_create), med(t_refresh), med(t_pfd));
 #ifdef SR_NM_PROFILE
   printf("cached node map phases (median ms): LIST grouping %.3f kinds+slots %.3f pass1 %.3f pass2 %.3f lists %.3f\n",
          med(ph[0]), med(ph[1]), med(ph[2]), med(ph[3]), med(ph[4]));
+  printf("refresh phases (median ms): by name %.3f pass1 %.3f pass2 %.3f rebuild+totals %.3f\n", med(ph[5]),
+         med(ph[6]), med(ph[7]), med(ph[8]));
 #endif
   sr_snapshot_destroy(kept);
   sr_node_map_cache_destroy(cache);
