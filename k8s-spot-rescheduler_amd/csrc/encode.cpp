@@ -83,6 +83,13 @@ bool in_range(int64_t v) { return v >= 0 && v < kQuantityLimit; }
 // mount; kReadOnlyMount: meets read-write mounts only).
 bool port_conflict(int32_t a, int32_t b) { return a == -1 || b == -1 || (a == b && a != kReadOnlyMount); }
 
+// A host-port query (protocol, port, IP) whose base conflicts make an atom row.
+struct PortQuery {
+  int32_t proto, port, ip;
+};
+static_assert(sizeof(PortQuery) == 3 * sizeof(int32_t), "CandReuse::port_q holds queries as int32 triples");
+
+
 // (limit key, unique volume name) as one word.
 inline uint64_t att_word(int32_t key, int32_t id) {
   return static_cast<uint64_t>(static_cast<uint32_t>(key)) << 32 | static_cast<uint32_t>(id);
@@ -105,6 +112,81 @@ enum : int32_t { REQ_LABEL_EQ = 0, REQ_LABEL_EXPR = 1, REQ_FIELD = 2, REQ_ZONE =
 inline uint64_t mix(uint64_t h, uint64_t x) {
   h = (h ^ x) * 0xff51afd7ed558ccdull;
   return h ^ (h >> 32);
+}
+
+// HostPortInfo.CheckConflict of each query against every spot node's base
+// UsedPorts, row q written to dst + q * Wp.  Rows are kept in C.port_rows by
+// query across calls: a state refresh that patched a few nodes patches their
+// bits, any other refresh drops them.
+void port_conflict_rows(EncoderCache& C, const sr_snapshot* snap, const PortQuery* queries, int32_t n_ports,
+                        int32_t Wp, uint64_t* dst) {
+  const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
+  auto conflicts = [&](int32_t n, const PortQuery& pq) {
+    for (const Port& u : snap->state[n].ports)
+      if (pq.proto == u.proto && pq.port == u.port && port_conflict(pq.ip, u.ip)) return true;
+    return false;
+  };
+  auto qkey = [](const PortQuery& pq) {
+    return mix(mix(mix(0x51ull, static_cast<uint32_t>(pq.proto)), static_cast<uint32_t>(pq.port)),
+               static_cast<uint32_t>(pq.ip));
+  };
+  if (C.port_rows_gen != C.state_gen) {
+    const bool patch = C.patched_from != ~0ull && C.port_rows_gen == C.patched_from && !C.patched_nodes.empty() &&
+                       C.port_rows.size() < 4096;
+    if (patch) {
+      for (auto& kv : C.port_rows) {
+        // the key does not carry the query: rebuild it from the row's stored tail
+        const std::vector<uint64_t>& row = kv.second;
+        const PortQuery pq{static_cast<int32_t>(row[Wp]), static_cast<int32_t>(row[Wp + 1]),
+                           static_cast<int32_t>(row[Wp + 2])};
+        for (int32_t n : C.patched_nodes) {
+          uint64_t& wd = kv.second[static_cast<size_t>(n >> 6)];
+          const uint64_t bit = 1ull << (n & 63);
+          wd = conflicts(n, pq) ? (wd | bit) : (wd & ~bit);
+        }
+      }
+    } else {
+      C.port_rows.clear();
+    }
+    C.port_rows_gen = C.state_gen;
+  }
+  std::vector<int32_t> missing;
+  std::vector<std::vector<uint64_t>*> rows(static_cast<size_t>(n_ports), nullptr);
+  for (int32_t q = 0; q < n_ports; ++q) {
+    const PortQuery& pq = queries[q];
+    auto it = C.port_rows.find(qkey(pq));
+    if (it != C.port_rows.end() && static_cast<int32_t>(it->second[Wp]) == pq.proto &&
+        static_cast<int32_t>(it->second[Wp + 1]) == pq.port && static_cast<int32_t>(it->second[Wp + 2]) == pq.ip) {
+      rows[q] = &it->second;
+    } else {
+      missing.push_back(q);
+    }
+  }
+  if (!missing.empty()) {  // one pass over the nodes for every query not cached
+    std::vector<std::vector<uint64_t>> fresh(missing.size(), std::vector<uint64_t>(static_cast<size_t>(Wp) + 3, 0));
+    for (int32_t n = 0; n < n_spot; ++n)
+      for (const Port& u : snap->state[n].ports)
+        for (size_t m = 0; m < missing.size(); ++m) {
+          const PortQuery& pq = queries[missing[m]];
+          if (pq.proto == u.proto && pq.port == u.port && port_conflict(pq.ip, u.ip))
+            fresh[m][static_cast<size_t>(n >> 6)] |= 1ull << (n & 63);
+        }
+    for (size_t m = 0; m < missing.size(); ++m) {
+      const PortQuery& pq = queries[missing[m]];
+      fresh[m][Wp] = static_cast<uint64_t>(static_cast<uint32_t>(pq.proto));
+      fresh[m][Wp + 1] = static_cast<uint64_t>(static_cast<uint32_t>(pq.port));
+      fresh[m][Wp + 2] = static_cast<uint64_t>(static_cast<uint32_t>(pq.ip));
+      if (C.port_rows.size() < 4096 && C.port_rows.find(qkey(pq)) == C.port_rows.end()) {
+        auto& slot = C.port_rows[qkey(pq)];
+        slot = std::move(fresh[m]);
+        rows[missing[m]] = &slot;
+      } else {  // full, or another query under the same key: not cached
+        std::copy_n(fresh[m].begin(), Wp, dst + static_cast<size_t>(missing[m]) * Wp);
+      }
+    }
+  }
+  for (int32_t q = 0; q < n_ports; ++q)
+    if (rows[q]) std::copy_n(rows[q]->begin(), Wp, dst + static_cast<size_t>(q) * Wp);
 }
 
 // v1.Toleration.ToleratesTaint [upstream k8s.io/api/core/v1/toleration.go]
@@ -1107,7 +1189,7 @@ void save_cand_input(CandReuse& R, const sr_candidates* cands, const uint64_t* s
 // the last call, its state-dependent parts brought up to the current state
 // view.  False when a dimension ran out of spare T rows (the caller encodes in
 // full; the index is rebuilt).
-bool reuse_encode(EncoderCache& C, Workload* w) {
+bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w) {
   CandReuse& R = w->reuse;
   const int32_t Wp = w->Wp, n_spot = w->n_spot;
   uint64_t* A = w->atoms.data();
@@ -1141,6 +1223,21 @@ bool reuse_encode(EncoderCache& C, Workload* w) {
   if (!words.empty()) {
     refresh_flags(0);
     for (size_t k = 0; k < R.comp_sets.size(); ++k) refresh_flags(R.a_comp + static_cast<int32_t>(k));
+  }
+  // host-port queries: their base conflict rows follow the spot pods' ports
+  const int32_t n_ports = static_cast<int32_t>(R.port_q.size() / 3);
+  if (n_ports > 0) {
+    std::vector<uint64_t>& rows = R.port_scratch;
+    rows.resize(static_cast<size_t>(n_ports) * Wp);
+    port_conflict_rows(C, snap, reinterpret_cast<const PortQuery*>(R.port_q.data()), n_ports, Wp, rows.data());
+    for (int32_t q = 0; q < n_ports; ++q) {
+      uint64_t* a = A + static_cast<size_t>(R.a_port + q) * Wp;
+      const uint64_t* r = rows.data() + static_cast<size_t>(q) * Wp;
+      if (!std::equal(r, r + Wp, a)) {
+        std::copy_n(r, Wp, a);
+        refresh_flags(R.a_port + q);
+      }
+    }
   }
   std::vector<int32_t> flipped;  // classes whose certain emptiness changed
   if (flags_moved)
@@ -1344,7 +1441,7 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
       (w->layout_gen == C.layout_gen || w->layout_gen + 1 == C.layout_gen) && snap->anti_total == 0 &&
       snap->opaque_total == 0) {
     w->state_gen = C.state_gen;
-    if (reuse_encode(C, w)) {
+    if (reuse_encode(C, snap, w)) {
       C.last_new_specs = 0;
       C.last_memo_hits = w->n_input_pods;
       C.last_reused = 1;
@@ -1683,9 +1780,6 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   // (protocol, port, ip) a pod can ask for, addressed by the bit that stands
   // for the query (single bits: 0.0.0.0 of a single group or I(ip); the W bit
   // of a pair: 0.0.0.0 of that group).
-  struct PortQuery {
-    int32_t proto, port, ip;
-  };
   std::vector<PortQuery> port_query;
   int32_t bit_query[64];
   for (int32_t& b : bit_query) b = -1;
@@ -2329,77 +2423,7 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
     }
   }
   std::copy(C.taint_rows.begin(), C.taint_rows.end(), A + static_cast<size_t>(A_TAINT) * Wp);
-  if (n_ports > 0) {
-    // HostPortInfo.CheckConflict of each query against every node's base
-    // UsedPorts.  Rows are kept across calls by query: a state refresh that
-    // patched a few nodes patches their bits, any other refresh drops them.
-    auto conflicts = [&](int32_t n, const PortQuery& pq) {
-      for (const Port& u : snap->state[n].ports)
-        if (pq.proto == u.proto && pq.port == u.port && port_conflict(pq.ip, u.ip)) return true;
-      return false;
-    };
-    auto qkey = [](const PortQuery& pq) {
-      return mix(mix(mix(0x51ull, static_cast<uint32_t>(pq.proto)), static_cast<uint32_t>(pq.port)),
-                 static_cast<uint32_t>(pq.ip));
-    };
-    if (C.port_rows_gen != C.state_gen) {
-      const bool patch = C.patched_from != ~0ull && C.port_rows_gen == C.patched_from && !C.patched_nodes.empty() &&
-                         C.port_rows.size() < 4096;
-      if (patch) {
-        for (auto& kv : C.port_rows) {
-          // the key does not carry the query: rebuild it from the row's stored tail
-          const std::vector<uint64_t>& row = kv.second;
-          const PortQuery pq{static_cast<int32_t>(row[Wp]), static_cast<int32_t>(row[Wp + 1]),
-                             static_cast<int32_t>(row[Wp + 2])};
-          for (int32_t n : C.patched_nodes) {
-            uint64_t& wd = kv.second[static_cast<size_t>(n >> 6)];
-            const uint64_t bit = 1ull << (n & 63);
-            wd = conflicts(n, pq) ? (wd | bit) : (wd & ~bit);
-          }
-        }
-      } else {
-        C.port_rows.clear();
-      }
-      C.port_rows_gen = C.state_gen;
-    }
-    std::vector<int32_t> missing;
-    std::vector<std::vector<uint64_t>*> rows(static_cast<size_t>(n_ports), nullptr);
-    for (int32_t q = 0; q < n_ports; ++q) {
-      const PortQuery& pq = port_query[q];
-      auto it = C.port_rows.find(qkey(pq));
-      if (it != C.port_rows.end() && static_cast<int32_t>(it->second[Wp]) == pq.proto &&
-          static_cast<int32_t>(it->second[Wp + 1]) == pq.port && static_cast<int32_t>(it->second[Wp + 2]) == pq.ip) {
-        rows[q] = &it->second;
-      } else {
-        missing.push_back(q);
-      }
-    }
-    if (!missing.empty()) {  // one pass over the nodes for every query not cached
-      std::vector<std::vector<uint64_t>> fresh(missing.size(), std::vector<uint64_t>(static_cast<size_t>(Wp) + 3, 0));
-      for (int32_t n = 0; n < n_spot; ++n)
-        for (const Port& u : snap->state[n].ports)
-          for (size_t m = 0; m < missing.size(); ++m) {
-            const PortQuery& pq = port_query[missing[m]];
-            if (pq.proto == u.proto && pq.port == u.port && port_conflict(pq.ip, u.ip))
-              fresh[m][static_cast<size_t>(n >> 6)] |= 1ull << (n & 63);
-          }
-      for (size_t m = 0; m < missing.size(); ++m) {
-        const PortQuery& pq = port_query[missing[m]];
-        fresh[m][Wp] = static_cast<uint64_t>(static_cast<uint32_t>(pq.proto));
-        fresh[m][Wp + 1] = static_cast<uint64_t>(static_cast<uint32_t>(pq.port));
-        fresh[m][Wp + 2] = static_cast<uint64_t>(static_cast<uint32_t>(pq.ip));
-        if (C.port_rows.size() < 4096 && C.port_rows.find(qkey(pq)) == C.port_rows.end()) {
-          auto& slot = C.port_rows[qkey(pq)];
-          slot = std::move(fresh[m]);
-          rows[missing[m]] = &slot;
-        } else {  // full, or another query under the same key: not cached
-          std::copy_n(fresh[m].begin(), Wp, A + static_cast<size_t>(A_PORT + missing[m]) * Wp);
-        }
-      }
-    }
-    for (int32_t q = 0; q < n_ports; ++q)
-      if (rows[q]) std::copy_n(rows[q]->begin(), Wp, A + static_cast<size_t>(A_PORT + q) * Wp);
-  }
+  if (n_ports > 0) port_conflict_rows(C, snap, port_query.data(), n_ports, Wp, A + static_cast<size_t>(A_PORT) * Wp);
   // NodeResourcesFit's ScalarResources loop against the base snapshot:
   // alloc[s] < request + requested[s] fails (a node without s allocates 0)
   // (volume limit keys under negative names: the node's limit, or unlimited,
@@ -2747,14 +2771,16 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   // the last call's and its candidate side reads nothing from the snapshot but
   // node capacities and pod counts
   if (want_index) {
+    // host ports read the snapshot through their base conflict rows only
+    // (atoms A_PORT..): a reuse encode recomputes those rows (CandReuse::port_q)
     bool state_free = snap->anti_total == 0 && snap->opaque_total == 0 && !anti.active && !aff.active &&
-                      !sdyn.active && n_ports == 0 && n_scalars == 0 && n_spreads == 0 && w->dyn_cand.empty() &&
-                      scal_names.empty() && w->swap_mask == 0 && w->empty_class >= 0;
+                      !sdyn.active && n_scalars == 0 && n_spreads == 0 && w->dyn_cand.empty() &&
+                      scal_names.empty() && w->empty_class >= 0 && bit_shift == 0;
     const sr_pod_affinity* PA = c->pod_affinity;
     for (int32_t j = w->pod_base; j < w->pod_base + w->n_input_pods && state_free; ++j) {
       const int32_t pod = cands->cand_pods[j];
       const uint32_t mb = memo_bits(pod);
-      state_free = (mb & MEMO_PLAIN) && !(mb & MEMO_PORTS);
+      state_free = (mb & MEMO_PLAIN) != 0;
       if (PA)
         state_free = state_free && PA->anti_off[pod] == PA->anti_off[pod + 1] &&
                      (!PA->aff_off || PA->aff_off[pod] == PA->aff_off[pod + 1]);
@@ -2768,6 +2794,9 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
       R.Wp = Wp;
       R.a_comp = A_COMP;
       R.comp_sets = comp_sets;
+      R.a_port = A_PORT;
+      R.port_q.clear();
+      for (const PortQuery& pq : port_query) R.port_q.insert(R.port_q.end(), {pq.proto, pq.port, pq.ip});
       R.atom_empty = atom_empty;
       R.atom_full = atom_full;
       R.cls_empty = cls_empty;

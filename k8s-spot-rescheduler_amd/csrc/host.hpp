@@ -317,11 +317,11 @@ constexpr int64_t kTSpare = INT64_MAX - 1;  // threshold of a spare T row (kerne
 // call's candidate input (lists, global indices, every pod stamped and
 // unchanged) equals the one the Workload was last encoded for, and that side
 // reads nothing from the snapshot but
-// node capacities and pod counts (no host ports, scalar resources, topology
-// spread, attachable volumes or inter-pod terms, no existing pod with
-// anti-affinity), the Workload is kept: only the pod-count and composite
-// atom rows, the T-row thresholds and the records of the pods whose T rows
-// or dead flag moved are updated.  T rows are slots keyed by threshold value
+// node capacities, pod counts and the spot pods' host ports (no scalar
+// resources, topology spread, attachable volumes or inter-pod terms, no
+// existing pod with anti-affinity), the Workload is kept: only the pod-count,
+// composite and host-port conflict atom rows, the T-row thresholds and the
+// records of the pods whose T rows or dead flag moved are updated.  T rows are slots keyed by threshold value
 // (a dimension's group has spare rows, kTPad), so a threshold that moves
 // re-points only the pods asking within the moved interval.  The index is
 // built by the second consecutive full encode of one input.
@@ -336,6 +336,9 @@ struct CandReuse {
   int32_t n_spot = -1, Wp = 0;
   int32_t a_comp = 0;                          // first composite atom
   std::vector<int32_t> comp_sets;              // untolerated-taint set of each composite atom
+  int32_t a_port = 0;                          // first host-port query atom
+  std::vector<int32_t> port_q;                 // the queries {proto, port, ip}* of those atoms
+  std::vector<uint64_t> port_scratch;          // their rows, recomputed by each reuse encode
   std::vector<uint8_t> atom_empty, atom_full;  // [n_atoms]
   std::vector<uint8_t> cls_empty;              // [classes before the empty class]
   std::vector<int32_t> pod_cls;                // [active pod] class before the dead check

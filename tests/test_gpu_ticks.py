@@ -176,8 +176,9 @@ def test_consecutive_ticks_one_node_changed(checker, whole_checker, which, confi
         lib.sr_snapshot_destroy(h)
 
 
-def test_ticks_candidate_side_reuse():
-    """Candidate-side reuse (host.hpp CandReuse) through the planner: tick
+@pytest.mark.parametrize("config", [3, 5])
+def test_ticks_candidate_side_reuse(config):
+    """Candidate-side reuse (host.hpp CandReuse) through the planner (C5: host-port candidates): tick
     after tick the same stamped candidate input on fresh snapshots whose spot
     nodes gain pods (one at a time, bursts of 20, then all leave again).  From
     the third tick on the encoder keeps the candidate side, the device keeps
@@ -191,7 +192,7 @@ def test_ticks_candidate_side_reuse():
     from spotplanner.planner import PredicateChecker
     ck = PredicateChecker(0)
     try:
-        sc = SynthCluster(3, seed=22, n_on_demand=200, n_spot=450)
+        sc = SynthCluster(config, seed=22, n_on_demand=200, n_spot=450)
         lib = capi.load_planner()
         nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
         cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
@@ -236,7 +237,9 @@ def test_ticks_candidate_side_reuse():
                     # the node section (whole when many nodes changed), not the 48-B pod records
                     assert t.bytes_uploaded < n_rec_bytes // 2, (tick, t.bytes_uploaded, n_rec_bytes)
             lib.sr_snapshot_destroy(h)
-        assert reused == 14 and patched > 0 and k0_cols > 0 and k0_less > 0, (reused, patched, k0_cols, k0_less)
+        # C5: the added pods carry host ports, so the port conflict atoms change and K0 rewrites their columns
+        assert reused == 14 and patched > 0 and k0_cols > 0 and (k0_less > 0 or config == 5), \
+            (reused, patched, k0_cols, k0_less)
     finally:
         ck.close()
 
