@@ -114,6 +114,34 @@ inline uint64_t mix(uint64_t h, uint64_t x) {
   return h ^ (h >> 32);
 }
 
+// NodeResourcesFit's ScalarResources check of one (name, request) against the
+// base snapshot: bit n set when alloc[s] >= request + requested[s] on spot node
+// n (a node without s allocates 0; volume limit keys under negative names: the
+// node's limit, or unlimited, against its unique attachable volumes of the key
+// plus the pod's count).  row: [Wp] words, zeroed by the caller.
+void scalar_query_row(const sr_snapshot* snap, int64_t name64, int64_t req, uint64_t* row) {
+  const int32_t name = static_cast<int32_t>(name64);
+  const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
+  for (int32_t n = 0; n < n_spot; ++n) {
+    const int64_t alloc = scalar_alloc_of(snap->nodes[n], name);
+    const int64_t used = scalar_used_of(snap->state[n], name);
+    // Go int64 arithmetic: request + requested wraps like the reference's
+    const int64_t need = static_cast<int64_t>(static_cast<uint64_t>(req) + static_cast<uint64_t>(used));
+    if (!(alloc < need)) row[n >> 6] |= 1ull << (n & 63);
+  }
+}
+
+// The base free value (alloc - requested) of each shared scalar name on every
+// spot node: the extension records' node_scal rows, [names][n_pad].
+void node_scal_rows(const sr_snapshot* snap, const std::vector<int32_t>& names, int32_t n_pad, int64_t* out) {
+  const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
+  for (size_t u = 0; u < names.size(); ++u)
+    for (int32_t n = 0; n < n_spot; ++n)  // Go int64 arithmetic: alloc - requested wraps like the reference's
+      out[u * static_cast<size_t>(n_pad) + static_cast<size_t>(n)] = static_cast<int64_t>(
+          static_cast<uint64_t>(scalar_alloc_of(snap->nodes[n], names[u])) -
+          static_cast<uint64_t>(scalar_used_of(snap->state[n], names[u])));
+}
+
 // HostPortInfo.CheckConflict of each query against every spot node's base
 // UsedPorts, row q written to dst + q * Wp.  Rows are kept in C.port_rows by
 // query across calls: a state refresh that patched a few nodes patches their
@@ -1189,10 +1217,20 @@ void save_cand_input(CandReuse& R, const sr_candidates* cands, const uint64_t* s
 // the last call, its state-dependent parts brought up to the current state
 // view.  False when a dimension ran out of spare T rows (the caller encodes in
 // full; the index is rebuilt).
-bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w) {
+bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_t prev_state_gen) {
   CandReuse& R = w->reuse;
   const int32_t Wp = w->Wp, n_spot = w->n_spot;
   uint64_t* A = w->atoms.data();
+  // the host-decided outcomes that read the snapshot must still hold: scalar
+  // usage known on every node, no planned candidate's attachable volume on a
+  // spot node (only the nodes changed since the last encode can have one now)
+  if (R.scalars && snap->scalar_unknown_total > 0) return false;
+  if (!R.att_words.empty() && prev_state_gen != C.state_gen) {
+    if (C.patched_from != prev_state_gen) return false;  // changes not known node by node
+    for (int32_t n : C.patched_nodes)
+      for (const auto& a : snap->state[n].att)
+        if (std::binary_search(R.att_words.begin(), R.att_words.end(), att_word(a.first, a.second))) return false;
+  }
   if (w->layout_gen != C.layout_gen) {  // the spot order moved (permute_static): every atom row follows
     std::vector<uint8_t> tmp;
     for (int32_t a = 0; a < w->n_atoms; ++a) permute_row(C, A + static_cast<size_t>(a) * Wp, tmp);
@@ -1248,6 +1286,19 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w) {
         flipped.push_back(k);
       }
     }
+  // scalar-resource / volume-limit queries and the shared scalar rows follow
+  // the spot nodes' usage
+  for (size_t q = 0; q < R.scalar_q.size(); ++q) {
+    uint64_t* a = A + static_cast<size_t>(R.a_scalar + static_cast<int32_t>(q)) * Wp;
+    std::vector<uint64_t>& row = R.port_scratch;
+    row.assign(static_cast<size_t>(Wp), 0);
+    scalar_query_row(snap, R.scalar_q[q].first, R.scalar_q[q].second, row.data());
+    if (!std::equal(row.begin(), row.end(), a)) {
+      std::copy(row.begin(), row.end(), a);
+      refresh_flags(R.a_scalar + static_cast<int32_t>(q));
+    }
+  }
+  if (!R.scal_names.empty()) node_scal_rows(snap, R.scal_names, w->n_pad, w->node_scal.data());
   // thresholds: a distinct request whose smallest node value >= it moved
   constexpr int64_t kNever = INT64_MAX;
   // Only requests in the interval (previous value, value] of a node value
@@ -1440,8 +1491,9 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   if (same_input && R.indexed && R.content_gen == C.content_gen && R.static_gen == C.static_gen && R.n_spot == n_spot && R.Wp == Wp &&
       (w->layout_gen == C.layout_gen || w->layout_gen + 1 == C.layout_gen) && snap->anti_total == 0 &&
       snap->opaque_total == 0) {
+    const uint64_t prev_state_gen = w->state_gen;
     w->state_gen = C.state_gen;
-    if (reuse_encode(C, snap, w)) {
+    if (reuse_encode(C, snap, w, prev_state_gen)) {
       C.last_new_specs = 0;
       C.last_memo_hits = w->n_input_pods;
       C.last_reused = 1;
@@ -2428,20 +2480,8 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   // alloc[s] < request + requested[s] fails (a node without s allocates 0)
   // (volume limit keys under negative names: the node's limit, or unlimited,
   // against its unique attachable volumes of the key plus the pod's count)
-  if (n_scalars > 0) {
-    for (int32_t q = 0; q < n_scalars; ++q) {
-      uint64_t* row = A + static_cast<size_t>(A_SCALAR + q) * Wp;
-      const int32_t name = static_cast<int32_t>(scalar_query[q].first);
-      const int64_t req = scalar_query[q].second;
-      for (int32_t n = 0; n < n_spot; ++n) {
-        const int64_t alloc = scalar_alloc_of(snap->nodes[n], name);
-        const int64_t used = scalar_used_of(snap->state[n], name);
-        // Go int64 arithmetic: request + requested wraps like the reference's
-        const int64_t need = static_cast<int64_t>(static_cast<uint64_t>(req) + static_cast<uint64_t>(used));
-        if (!(alloc < need)) row[n >> 6] |= 1ull << (n & 63);
-      }
-    }
-  }
+  for (int32_t q = 0; q < n_scalars; ++q)
+    scalar_query_row(snap, scalar_query[q].first, scalar_query[q].second, A + static_cast<size_t>(A_SCALAR + q) * Wp);
   // PodTopologySpread against the base snapshot, over the spec's NodeAffinity
   // row (nodeSelector AND, OR of the required terms) built from its requirement rows
   for (int32_t q = 0; q < n_spreads; ++q) {
@@ -2579,11 +2619,7 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
       }
       w->n_scal_names = static_cast<int32_t>(scal_names.size());
       w->node_scal.assign(std::max<size_t>(1, scal_names.size()) * static_cast<size_t>(w->n_pad), 0);
-      for (size_t u = 0; u < scal_names.size(); ++u)
-        for (int32_t n = 0; n < n_spot; ++n)  // Go int64 arithmetic: alloc - requested wraps like the reference's
-          w->node_scal[u * static_cast<size_t>(w->n_pad) + static_cast<size_t>(n)] = static_cast<int64_t>(
-              static_cast<uint64_t>(scalar_alloc_of(snap->nodes[n], scal_names[u])) -
-              static_cast<uint64_t>(scalar_used_of(snap->state[n], scal_names[u])));
+      node_scal_rows(snap, scal_names, w->n_pad, w->node_scal.data());
     }
   }
   phase(4);
@@ -2771,20 +2807,31 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   // the last call's and its candidate side reads nothing from the snapshot but
   // node capacities and pod counts
   if (want_index) {
-    // host ports read the snapshot through their base conflict rows only
-    // (atoms A_PORT..): a reuse encode recomputes those rows (CandReuse::port_q)
+    // host ports, scalar resources and volume limits read the snapshot through
+    // atom rows a reuse encode recomputes (CandReuse::port_q, scalar_q) and the
+    // shared scalar rows (scal_names)
     bool state_free = snap->anti_total == 0 && snap->opaque_total == 0 && !anti.active && !aff.active &&
-                      !sdyn.active && n_scalars == 0 && n_spreads == 0 && w->dyn_cand.empty() &&
-                      scal_names.empty() && w->empty_class >= 0 && bit_shift == 0;
+                      !sdyn.active && n_spreads == 0 && w->dyn_cand.empty() && w->empty_class >= 0 && bit_shift == 0;
     const sr_pod_affinity* PA = c->pod_affinity;
     for (int32_t j = w->pod_base; j < w->pod_base + w->n_input_pods && state_free; ++j) {
       const int32_t pod = cands->cand_pods[j];
       const uint32_t mb = memo_bits(pod);
-      state_free = (mb & MEMO_PLAIN) != 0;
+      // scalar resources and attachable volumes read the snapshot through
+      // their atom rows and the shared scalar rows (recomputed by a reuse) and
+      // through the fallback checks (rechecked by a reuse); spread does not
+      state_free = (mb & MEMO_PLAIN) != 0 || !has_spread(c, pod);
       if (PA)
         state_free = state_free && PA->anti_off[pod] == PA->anti_off[pod + 1] &&
                      (!PA->aff_off || PA->aff_off[pod] == PA->aff_off[pod + 1]);
+      // a fallback decided by the snapshot must not be able to turn back:
+      // scalar usage unknown on some node, or an attachable volume of a
+      // fallback candidate (a spot node may hold it)
+      if (has_scalars(c, pod) && snap->scalar_unknown_total > 0) state_free = false;
     }
+    for (int32_t i = 0; i < nc && state_free && c->volumes; ++i)
+      if (w->status_host[i] == SR_CAND_FALLBACK)
+        for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1] && state_free; ++j)
+          state_free = att_count(c, cands->cand_pods[j]) == 0;
     if (state_free) {
       const size_t NA = static_cast<size_t>(na);
       const int32_t n_base_cls = static_cast<int32_t>(cls_empty.size());
@@ -2794,6 +2841,22 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
       R.Wp = Wp;
       R.a_comp = A_COMP;
       R.comp_sets = comp_sets;
+      R.a_scalar = A_SCALAR;
+      R.scalar_q = scalar_query;
+      R.scal_names = w->ext_cand.empty() ? std::vector<int32_t>() : scal_names;
+      R.scalars = false;
+      R.att_words.clear();
+      for (int32_t i = 0; i < nc; ++i) {
+        const bool planned = w->status_host[i] == STATUS_PENDING;
+        for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+          const int32_t pod = cands->cand_pods[j];
+          R.scalars = R.scalars || has_scalars(c, pod);
+          if (planned && c->volumes)
+            for (int32_t a = c->volumes->att_off[pod]; a < c->volumes->att_off[pod + 1]; ++a)
+              R.att_words.push_back(att_word(c->volumes->att_key[a], c->volumes->att_id[a]));
+        }
+      }
+      std::sort(R.att_words.begin(), R.att_words.end());
       R.a_port = A_PORT;
       R.port_q.clear();
       for (const PortQuery& pq : port_query) R.port_q.insert(R.port_q.end(), {pq.proto, pq.port, pq.ip});

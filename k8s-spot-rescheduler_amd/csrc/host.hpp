@@ -317,11 +317,12 @@ constexpr int64_t kTSpare = INT64_MAX - 1;  // threshold of a spare T row (kerne
 // call's candidate input (lists, global indices, every pod stamped and
 // unchanged) equals the one the Workload was last encoded for, and that side
 // reads nothing from the snapshot but
-// node capacities, pod counts and the spot pods' host ports (no scalar
-// resources, topology spread, attachable volumes or inter-pod terms, no
-// existing pod with anti-affinity), the Workload is kept: only the pod-count,
-// composite and host-port conflict atom rows, the T-row thresholds and the
-// records of the pods whose T rows or dead flag moved are updated.  T rows are slots keyed by threshold value
+// node capacities, pod counts, the spot pods' host ports, scalar usage and
+// attachable volumes (no topology spread or inter-pod terms, no existing pod
+// with anti-affinity), the Workload is kept: only the pod-count, composite,
+// host-port conflict and scalar atom rows, the shared scalar rows, the T-row
+// thresholds and the records of the pods whose T rows or dead flag moved are
+// updated.  T rows are slots keyed by threshold value
 // (a dimension's group has spare rows, kTPad), so a threshold that moves
 // re-points only the pods asking within the moved interval.  The index is
 // built by the second consecutive full encode of one input.
@@ -339,6 +340,12 @@ struct CandReuse {
   int32_t a_port = 0;                          // first host-port query atom
   std::vector<int32_t> port_q;                 // the queries {proto, port, ip}* of those atoms
   std::vector<uint64_t> port_scratch;          // their rows, recomputed by each reuse encode
+  int32_t a_scalar = 0;                        // first scalar-resource / volume-limit query atom
+  std::vector<std::pair<int64_t, int64_t>> scalar_q;  // their (name, request): rows recomputed by each reuse
+  std::vector<int32_t> scal_names;             // shared scalar names of the extension records (node_scal rows)
+  bool scalars = false;                        // some candidate pod lists scalar resources
+  std::vector<uint64_t> att_words;             // attachable volumes of the planned candidates' pods: a spot node
+                                               // that comes to hold one sends its candidate to the fallback path
   std::vector<uint8_t> atom_empty, atom_full;  // [n_atoms]
   std::vector<uint8_t> cls_empty;              // [classes before the empty class]
   std::vector<int32_t> pod_cls;                // [active pod] class before the dead check

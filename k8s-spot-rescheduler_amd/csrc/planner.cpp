@@ -337,8 +337,8 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t o_st = dyn ? pk.add(w.sp_tab) : 0;
   const bool ext = !w.ext_cand.empty();
   const size_t o_ec = ext ? pk.add(w.ext_cand) : 0, o_ep = ext ? pk.add(w.pod_ext) : 0;
-  const size_t o_ns = ext ? pk.add(w.node_scal) : 0;
   const size_t tick_from = pk.size();
+  const size_t o_ns = ext ? pk.add(w.node_scal) : 0;  // the spot nodes' scalar usage: state, so every tick
   const size_t o_at = pk.add(w.atoms);
   const size_t o_tt = pk.add(w.t_thr);
   // ---- the slot's device state against this call.  Spot nodes changed since

@@ -82,3 +82,16 @@ def test_reuse_survives_spot_order_moves(tool, config):
     assert r["bad"] == 0, r["out"]
     assert r["moved"] >= 30, r["out"]
     assert r["reused"] == r["ticks"] and r["full"] == 0, r["out"]
+
+
+@pytest.mark.parametrize("mode", ["reuse", "reuse-perm"])
+def test_realistic_variant_reuse(tool, mode):
+    """The realistic variant (scalar resources, attachable volumes, init
+    containers): a reuse recomputes the scalar / volume-limit atom rows and the
+    shared scalar rows, and rechecks the fallback decisions that read the
+    snapshot (a planned candidate's attachable volume now on a changed spot node
+    ends the reuse).  Compared with a full encode by a copy of the encoder taken
+    before the call (class and atom numbering follow its dictionaries' history)."""
+    r = run_check(tool, 3, 40, env={"SR_SYNTH_REALISTIC": "1"}, mode=mode)
+    assert r["bad"] == 0, r["out"]
+    assert r["reused"] >= 3, r["out"]

@@ -415,3 +415,56 @@ def test_ticks_kept_node_map_and_snapshot(checker, config):
         if h is not None:
             lib.sr_snapshot_destroy(h)
         lib.sr_node_map_cache_destroy(cache)
+
+
+@pytest.mark.parametrize("config", [3, 5])
+def test_ticks_realistic_variant_reuse(checker, config):
+    """The realistic variant (StatefulSet pods with EBS claims, init
+    containers, GPU pods): the candidates read the spot nodes' scalar usage and
+    attachable volumes.  Tick after tick pods on spot nodes change requests
+    (stamps with them, the spot order moves), the snapshot is refreshed; the
+    candidate side is reused (its scalar and volume-limit rows and shared
+    scalar rows recomputed) and every plan equals the oracle's."""
+    from spotplanner.synth import REALISTIC
+    sc = SynthCluster(config, seed=24, n_on_demand=150, n_spot=400, **REALISTIC)
+    lib = capi.load_planner()
+    cl = sc.cluster
+    cpu = [np.ctypeslib.as_array(a, shape=(sc.n_pods,)) for a in
+           (cl.pods.cpu_sort_milli, cl.pods.req_milli_cpu, cl.acc_milli_cpu) if a]
+    stamps = np.ctypeslib.as_array(cl.pod_stamp, shape=(sc.n_pods,))
+    saved = [a.copy() for a in cpu] + [stamps.copy()]
+    nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+    spot_pods = np.concatenate([nm.node_pod_idx[nm.node_pod_off[n]:nm.node_pod_off[n + 1]] for n in nm.spot])
+    rng = np.random.default_rng(config)
+    h, reused = None, 0
+    try:
+        for tick in range(10):
+            if tick:
+                for p in rng.choice(spot_pods, 3):
+                    for a in cpu:
+                        a[p] = max(0, int(a[p]) + int(rng.integers(-100, 300)))
+                    stamps[p] += 2
+            nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+            args = (sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot), capi.ptr(nm.node_pod_off, capi.P32),
+                    capi.ptr(nm.node_pod_idx, capi.P32))
+            if h is None:
+                h = ctypes.c_void_p()
+                assert lib.sr_snapshot_create(*args, ctypes.byref(h)) == capi.SR_OK
+            else:
+                assert lib.sr_snapshot_refresh(h, *args, None) == capi.SR_OK
+            co, cp = build_candidates(nm, sc.pod_flags())
+            assert np.array_equal(co, cand_off) and np.array_equal(cp, cand_pods)  # the on-demand side is untouched
+            osnap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
+            p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+            reused += checker.timing().enc_reused
+            o = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
+            assert np.array_equal(p.status, o["status"]), tick
+            assert np.array_equal(p.node_of_pod, o["node_of_pod"]), tick
+            assert p.winner == o["winner"], tick
+        assert reused >= 5, reused
+    finally:
+        for a, b in zip(cpu + [stamps], saved):
+            a[:] = b
+        if h is not None:
+            lib.sr_snapshot_destroy(h)

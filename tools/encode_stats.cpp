@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstdlib>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -32,6 +33,12 @@ int main(int argc, char** argv) {
   sr_synth_params p{};
   p.config = argc > 1 ? atoi(argv[1]) : 3;
   p.pinned_fraction = -1;
+  const bool realistic = std::getenv("SR_SYNTH_REALISTIC") != nullptr;
+  if (realistic) {  // bench --variant realistic (spotplanner/synth.py REALISTIC)
+    p.stateful_fraction = 0.15;
+    p.init_fraction = 0.2;
+    p.gpu_fraction = 0.3;
+  }
   sr_synth* s = sr_synth_generate(&p);
   sr_cluster c;
   sr_synth_view(s, &c);
@@ -176,6 +183,11 @@ int main(int argc, char** argv) {
       for (int a = 0; a < add; ++a)
         extra.emplace_back(cp[rnd(cp.size())], static_cast<int32_t>(rnd(static_cast<uint64_t>(ns))));
       for (auto& e : extra) sr_snapshot_add_pod(s2, &c, e.first, e.second);
+      // the realistic variant compares with a full encode by a copy of the
+      // encoder as it was before this call: its class and atom numbering
+      // depends on the dictionaries' history (scalar and volume queries)
+      std::unique_ptr<sr::EncoderCache> twin;
+      if (realistic) twin.reset(new sr::EncoderCache(cache));
       t0 = std::chrono::steady_clock::now();
       if (sr::encode_workload(&cache, s2, &c, &cands, &w, &err) != SR_OK) return 1;
       const double ms = ms_since(t0);
@@ -189,7 +201,7 @@ int main(int argc, char** argv) {
       }
       sr::EncoderCache fresh;
       sr::Workload f;
-      if (sr::encode_workload(&fresh, s2, &c, &cands, &f, &err) != SR_OK) return 1;
+      if (sr::encode_workload(twin ? twin.get() : &fresh, s2, &c, &cands, &f, &err) != SR_OK) return 1;
       auto fail = [&](const char* what, long i) {
         if (bad++ < 5) printf("tick %d (reused %d): %s differs at %ld\n", r, cache.last_reused, what, i);
       };
