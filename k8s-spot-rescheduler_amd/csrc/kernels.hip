@@ -991,6 +991,35 @@ __device__ __forceinline__ int32_t scale32(int64_t f, int k) {
   return f < 0 ? -1 : (q > 0x7fffffffll ? 0x7fffffff : static_cast<int32_t>(q));
 }
 
+// The checks of one pod against the window's 32-bit state as one lane test:
+// x - r saturated to 32 bits is >= 0 exactly when x >= r (the clamped
+// difference keeps its sign), s | -s is negative exactly when s != 0 (the
+// state bits the pod conflicts with), and the OR of such values is >= 0
+// exactly when every test passes, so the pod-count, cpu, memory (ephemeral,
+// state-bit) checks cost one ballot instead of three to five chained through
+// VCC.
+#ifndef SR_K2_LEAN_STEP
+#define SR_K2_LEAN_STEP 1
+#endif
+template <bool E, bool O>
+__device__ __forceinline__ uint64_t fits32(int32_t c32, int32_t m32, int32_t e32, int nleft, uint64_t conflict,
+                                           int32_t c, int32_t m, int32_t e) {
+  if constexpr (SR_K2_LEAN_STEP) {
+    int32_t t = __builtin_elementwise_sub_sat(c32, c) | __builtin_elementwise_sub_sat(m32, m) | (nleft - 1);
+    if (E) t |= __builtin_elementwise_sub_sat(e32, e);
+    if (O) {
+      const uint32_t x = static_cast<uint32_t>(conflict) | static_cast<uint32_t>(conflict >> 32);
+      t |= static_cast<int32_t>(x | (0u - x));
+    }
+    return ballot(t >= 0);
+  } else {
+    uint64_t f = ballot(nleft >= 1) & ballot(c32 >= c) & ballot(m32 >= m);
+    if (E) f &= ballot(e32 >= e);
+    if (O) f &= ballot(conflict == 0);
+    return f;
+  }
+}
+
 // place_window with the window's state and the pods' requests scaled to 32
 // bits (narrow candidates: S <= f equals S >> k <= f >> k for the multiples
 // S of 2^k the candidate's requests sum to): one compare and one select per
@@ -1022,9 +1051,7 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
       const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
       const int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
       const uint64_t q = readlane64(pm, k);
-      uint64_t fit = readlane64(cur, k) & base & ~taken & ballot(c32 >= c) & ballot(m32 >= m) &
-                     ballot((nport & q) == 0);
-      if (E) fit &= ballot(e32 >= e);
+      uint64_t fit = readlane64(cur, k) & base & ~taken & fits32<E, true>(c32, m32, e32, 1, nport & q, c, m, e);
       const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
       taken |= fit & (0ull - fit);  // the lowest set bit: node j
       jv = lane == k ? j : jv;
@@ -1065,9 +1092,7 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
     const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
     const int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
     const uint64_t q = O ? readlane64(pm, k) : 0ull;
-    uint64_t fit = readlane64(cur, k) & ballot(nleft >= 1) & ballot(c32 >= c) & ballot(m32 >= m);
-    if (E) fit &= ballot(e32 >= e);
-    if (O) fit &= ballot((nport & q) == 0);
+    uint64_t fit = readlane64(cur, k) & fits32<E, O>(c32, m32, e32, nleft, nport & q, c, m, e);
     const int32_t cu = max(c, 0), mu = max(m, 0), eu = max(e, 0);
     if (O) {  // as in place_window
       if (fit != 0) {
