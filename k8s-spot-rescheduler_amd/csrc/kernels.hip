@@ -1085,45 +1085,6 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
   // selects cost ~10% of a step.
   int jv = 64;  // as in place_window
   if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
-#ifndef SR_K2_PIPE
-#define SR_K2_PIPE 0
-#endif
-  if (SR_K2_PIPE && O && todo != 0) {  // A/B: the next pod's lanes read while this pod's step runs
-    int k = __builtin_ctzll(todo);
-    int32_t c = __builtin_amdgcn_readlane(static_cast<int>(nc), k);
-    int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
-    int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
-    uint64_t q = readlane64(pm, k), cw = readlane64(cur, k), pset = readlane64(ps, k);
-    for (;;) {
-      todo &= ~(1ull << k);
-      const uint64_t fit = cw & fits32<E, O>(c32, m32, e32, nleft, nport & q, c, m, e);
-      const int kn = todo != 0 ? __builtin_ctzll(todo) : k;
-      const int32_t cn = __builtin_amdgcn_readlane(static_cast<int>(nc), kn);
-      const int32_t mn = __builtin_amdgcn_readlane(static_cast<int>(nm), kn);
-      const int32_t en = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), kn) : 0;
-      const uint64_t qn = readlane64(pm, kn), cwn = readlane64(cur, kn), psn = readlane64(ps, kn);
-      if (fit != 0) {
-        const int j = __builtin_ctzll(fit);
-        if (lane == j) {
-          c32 -= max(c, 0);
-          m32 -= max(m, 0);
-          if (E) e32 -= max(e, 0);
-          nleft -= 1;
-          nport |= pset;
-        }
-        jv = lane == k ? j : jv;
-      }
-      if (todo == 0) break;
-      k = kn;
-      c = cn;
-      m = mn;
-      e = en;
-      q = qn;
-      cw = cwn;
-      pset = psn;
-    }
-    todo = 0;
-  }
   while (todo != 0) {
     const int k = __builtin_ctzll(todo);
     todo &= ~(1ull << k);
@@ -1133,21 +1094,6 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
     const uint64_t q = O ? readlane64(pm, k) : 0ull;
     uint64_t fit = readlane64(cur, k) & fits32<E, O>(c32, m32, e32, nleft, nport & q, c, m, e);
     const int32_t cu = max(c, 0), mu = max(m, 0), eu = max(e, 0);
-#ifndef SR_K2_O_PRED
-#define SR_K2_O_PRED 0
-#endif
-    if (O && SR_K2_O_PRED) {  // A/B: the state-bit update predicated like the step below
-      const uint64_t pset = readlane64(ps, k);
-      const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
-      const bool hit = lane == j;
-      c32 -= hit ? cu : 0;
-      m32 -= hit ? mu : 0;
-      if (E) e32 -= hit ? eu : 0;
-      nleft -= hit ? 1 : 0;
-      nport |= hit ? pset : 0ull;
-      jv = lane == k ? j : jv;
-      continue;
-    }
     if (O) {  // as in place_window
       if (fit != 0) {
         const int j = __builtin_ctzll(fit);
