@@ -83,14 +83,14 @@ E2E_IDLE = os.environ.get("SR_BENCH_E2E_IDLE", "1") != "0"
 
 
 def latest_profile(name):
-    """profiles/rNN/<name> of the newest round that has it, or None."""
+    """profiles/rNN/final/<name> or profiles/rNN/<name> of the newest round that has it, or None."""
     base = os.path.join(REPO, "profiles")
     rounds = sorted((d for d in os.listdir(base) if d.startswith("r") and d[1:].isdigit()), reverse=True) \
         if os.path.isdir(base) else []
     for d in rounds:
-        p = os.path.join(base, d, name)
-        if os.path.exists(p):
-            return p
+        for p in (os.path.join(base, d, "final", name), os.path.join(base, d, name)):
+            if os.path.exists(p):
+                return p
     return None
 
 
