@@ -1126,7 +1126,9 @@ struct Narrow {
   int kc, km, ke;
 };
 
-template <int G, bool PROF>
+// WIDE: the F heads of 64 pods per memory round trip also for G > 1 (more
+// registers: for launches whose waves fit the SIMDs at the lower occupancy)
+template <int G, bool PROF, bool WIDE = false>
 __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __restrict__ F, const int p0,
                                               const int np, int& status, K2Stats& st, uint32_t& nbytes) {
   static_assert(64 * G * kNHS * 8 <= sizeof(K2Lds), "node-order LDS exceeds the wave's K2 region");
@@ -1291,8 +1293,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   // per kPW * kPB pods)
   {
     constexpr int kPW = 64 / kNH;  // pods per load instruction
-    // up to 64 pods in one round trip (G = 1), 32 per round beyond
-    constexpr int kPB = (G == 1 ? 64 : 32) / kPW;
+    // up to 64 pods in one round trip (G = 1 or WIDE), 32 per round beyond
+    constexpr int kPB = (G == 1 || WIDE ? 64 : 32) / kPW;
     const int sub = lane / kNH, wd = lane % kNH;
     const bool wv = wd < Wp;
 #pragma unroll
@@ -2194,7 +2196,7 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
 // candidate, <= 64 * GMAX pods, default mode): only that path is compiled, so
 // the kernel holds far fewer registers than k2_place (more waves per SIMD on
 // the large configs), and a wave's LDS is just its F heads.
-template <int GMAX, bool PROF>
+template <int GMAX, bool PROF, bool WIDE = false>
 __global__ __launch_bounds__(256) void k2_node(DevWorkload w, const int4* __restrict__ list, int n_list) {
   extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
   const int wave = threadIdx.x >> 6;
@@ -2206,8 +2208,9 @@ __global__ __launch_bounds__(256) void k2_node(DevWorkload w, const int4* __rest
   int status = -1;
   uint32_t nbytes = 0;
   if (GMAX == 1 || x.np <= 64) k2_node_order<1, PROF>(w, F, x.p0, x.np, status, st, nbytes);
-  else if (GMAX == 2 || x.np <= 128) k2_node_order<(GMAX >= 2 ? 2 : 1), PROF>(w, F, x.p0, x.np, status, st, nbytes);
-  else k2_node_order<GMAX, PROF>(w, F, x.p0, x.np, status, st, nbytes);
+  else if (GMAX == 2 || x.np <= 128)
+    k2_node_order<(GMAX >= 2 ? 2 : 1), PROF, WIDE>(w, F, x.p0, x.np, status, st, nbytes);
+  else k2_node_order<GMAX, PROF, WIDE>(w, F, x.p0, x.np, status, st, nbytes);
   k2_finish<PROF>(w, x, status, 2, nbytes, st);
 }
 
@@ -2240,8 +2243,17 @@ hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent
   const int wpb = w.k2_wpb == 1 || w.k2_wpb == 2 ? w.k2_wpb : 4;  // waves per block
   const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
   const size_t lds = wpb * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
+  // wide F-head rounds where the extra registers cost nothing: launches of at
+  // most two waves per SIMD (256 CUs x 4 SIMDs), and G = 4 (one wave per SIMD
+  // either way)
+#ifndef SR_K2_WIDE_HEADS
+#define SR_K2_WIDE_HEADS 0
+#endif
+  const bool wide = SR_K2_WIDE_HEADS && n <= 2048;
   if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (G == 2 && wide) launch(k2_node<2, PROF, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   else if (G == 2) launch(k2_node<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (SR_K2_WIDE_HEADS) launch(k2_node<4, PROF, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   else launch(k2_node<4, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   return hipGetLastError();
 }
