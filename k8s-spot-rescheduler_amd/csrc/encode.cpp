@@ -701,20 +701,41 @@ void refresh_static(EncoderCache& C, const sr_snapshot* snap, int32_t Wp) {
 sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* err) {
   const int32_t n = C.n_spot, NP = C.n_pad, Wp = C.Wp;
   const std::vector<uint64_t>& fp = snap->node_dfp;  // kept current by the snapshot
-  std::vector<int32_t> changed;
+  std::vector<int32_t> changed, moved;
   const bool full = !C.state_valid || C.state_fp.size() != static_cast<size_t>(n);
-  if (!full) {
-    for (int32_t i = 0; i < n; ++i)
-      if (fp[i] != C.state_fp[i]) changed.push_back(i);
-    if (!C.perm_dirty.empty()) {  // permuted positions: another node's records, whatever its fingerprint
-      changed.insert(changed.end(), C.perm_dirty.begin(), C.perm_dirty.end());
-      std::sort(changed.begin(), changed.end());
-      changed.erase(std::unique(changed.begin(), changed.end()), changed.end());
+  if (!full && !C.perm_dirty.empty()) {
+    // the spot order moved (permute_static): each moved node's records and
+    // fingerprint follow it to its new position (the multiset of free values
+    // is unchanged); only nodes whose own state changed are patched below,
+    // but every moved position is a changed record for the device
+    moved = C.perm_dirty;
+    const std::vector<int32_t>& K = C.perm_k;
+    std::vector<uint64_t> rec(K.size() * 8), sfp(K.size());
+    std::vector<int64_t> fr(K.size() * 3);
+    std::vector<uint8_t> pc(K.size());
+    for (size_t q = 0; q < K.size(); ++q) {
+      const int32_t o = C.perm_src[K[q]];
+      std::copy_n(&C.node_rec[static_cast<size_t>(o) * 8], 8, &rec[q * 8]);
+      for (int d = 0; d < 3; ++d) fr[q * 3 + d] = C.node_free[static_cast<size_t>(d) * NP + o];
+      pc[q] = static_cast<uint8_t>(C.podcount_row[static_cast<size_t>(o >> 6)] >> (o & 63) & 1);
+      sfp[q] = C.state_fp[o];
+    }
+    for (size_t q = 0; q < K.size(); ++q) {
+      const int32_t i = K[q];
+      std::copy_n(&rec[q * 8], 8, &C.node_rec[static_cast<size_t>(i) * 8]);
+      for (int d = 0; d < 3; ++d) C.node_free[static_cast<size_t>(d) * NP + i] = fr[q * 3 + d];
+      uint64_t& word = C.podcount_row[static_cast<size_t>(i >> 6)];
+      const uint64_t bit = 1ull << (i & 63);
+      word = pc[q] ? (word | bit) : (word & ~bit);
+      C.state_fp[i] = sfp[q];
     }
   }
   C.perm_dirty.clear();
-  C.last_state_changed = full ? n : static_cast<int32_t>(changed.size());
-  if (!full && changed.empty()) return SR_OK;
+  if (!full)
+    for (int32_t i = 0; i < n; ++i)
+      if (fp[i] != C.state_fp[i]) changed.push_back(i);
+  C.last_state_changed = full ? n : static_cast<int32_t>(changed.size() + moved.size());
+  if (!full && changed.empty() && moved.empty()) return SR_OK;
   C.patched_from = ~0ull;
   C.patched_nodes.clear();
   ++C.state_gen;
@@ -761,6 +782,11 @@ sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* e
   } else {  // a few nodes changed: patch their records and the sorted values
     C.patched_from = C.state_gen - 1;
     C.patched_nodes = changed;
+    if (!moved.empty()) {  // and the moved records
+      C.patched_nodes.insert(C.patched_nodes.end(), moved.begin(), moved.end());
+      std::sort(C.patched_nodes.begin(), C.patched_nodes.end());
+      C.patched_nodes.erase(std::unique(C.patched_nodes.begin(), C.patched_nodes.end()), C.patched_nodes.end());
+    }
     for (int32_t i : changed) {
       int64_t f[3], left;
       if (!node_values(i, f, &left)) return fail();

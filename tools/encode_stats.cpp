@@ -106,14 +106,32 @@ int main(int argc, char** argv) {
          "reused %d, pod patches %d)\n", best, last_state, last_static, cache.last_memo_hits, cache.last_reused,
          cache.last_pod_patches);
   phases("1node");
-  if (argc > 3 && std::string(argv[3]) == "check") {
+  const bool check_perm = argc > 3 && std::string(argv[3]) == "check-perm";
+  if (argc > 3 && (std::string(argv[3]) == "check" || check_perm)) {
     // the state view patched node by node equals the one rebuilt from scratch:
     // consecutive fresh snapshots, each with a few more pods on random spot nodes
     std::vector<std::pair<int32_t, int32_t>> extra;
     uint64_t x = 88172645463325252ull;
     auto rnd = [&](uint64_t n) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x % n; };
     int ticks = 0, patched = 0;
+    int moved_ticks = 0;
     for (int r = 0; r < 300 && !cp.empty(); ++r) {
+      if (check_perm && r > 0) {  // pods on spot nodes change cpu requests: the spot order moves
+        for (int k = 0, nk = 1 + static_cast<int>(rnd(3)); k < nk; ++k) {
+          const int32_t node = spot[rnd(static_cast<uint64_t>(ns))];
+          if (off[node + 1] == off[node]) continue;
+          const int32_t pod = idx[off[node] + static_cast<int32_t>(rnd(static_cast<uint64_t>(off[node + 1] - off[node])))];
+          const int64_t d = static_cast<int64_t>(rnd(400)) - 150;
+          auto bump = [&](const int64_t* a) { const_cast<int64_t*>(a)[pod] = std::max<int64_t>(0, a[pod] + d); };
+          bump(c.pods.cpu_sort_milli);
+          bump(c.pods.req_milli_cpu);
+          if (c.acc_milli_cpu) bump(c.acc_milli_cpu);
+          const_cast<uint64_t*>(c.pod_stamp)[pod] = (x | 1);
+        }
+        std::vector<int32_t> before(spot.begin(), spot.begin() + ns);
+        if (sr_new_node_map(&c, &prm, &m) != SR_OK) return 1;
+        moved_ticks += !std::equal(before.begin(), before.end(), spot.begin());
+      }
       sr_snapshot* s2 = nullptr;
       sr_snapshot_create(&c, spot.data(), ns, off.data(), idx.data(), &s2);
       if (r % 7 == 6) extra.clear();  // sometimes the extra pods leave again
@@ -139,7 +157,8 @@ int main(int argc, char** argv) {
       sr_snapshot_destroy(s2);
       ++ticks;
     }
-    printf("state views consistent: %d ticks (%d patched node by node)\n", ticks, patched);
+    printf("state views consistent: %d ticks (%d patched node by node, spot order moved %d)\n", ticks, patched,
+           moved_ticks);
   }
   const bool perm = argc > 3 && std::string(argv[3]) == "reuse-perm";
   if (argc > 3 && (std::string(argv[3]) == "reuse" || perm)) {
