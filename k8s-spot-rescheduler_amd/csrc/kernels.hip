@@ -2247,7 +2247,7 @@ hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent
   // most two waves per SIMD (256 CUs x 4 SIMDs), and G = 4 (one wave per SIMD
   // either way)
 #ifndef SR_K2_WIDE_HEADS
-#define SR_K2_WIDE_HEADS 0
+#define SR_K2_WIDE_HEADS 1
 #endif
   const bool wide = SR_K2_WIDE_HEADS && n <= 2048;
   if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
