@@ -151,7 +151,24 @@ extern "C" sr_status sr_pods_for_deletion(const sr_cluster* c, const sr_pod_drai
       out_cand_off[i + 1] = k < 0 ? 0 : k;  // lengths, summed below
     }
   };
-  if (n_nodes > 256) sr::parallel_for(static_cast<size_t>(n_nodes), 64, body);
+  // a node named twice would have two pool threads write its scratch range:
+  // such an input runs the pass serially (same lists, no concurrent writes)
+  bool repeats = false;
+  if (n_nodes > 256) {
+    thread_local std::vector<uint32_t> seen;
+    thread_local uint32_t epoch = 0;
+    if (seen.size() < static_cast<size_t>(c->nodes.n)) seen.assign(static_cast<size_t>(c->nodes.n), 0);
+    if (++epoch == 0) {
+      std::fill(seen.begin(), seen.end(), 0u);
+      epoch = 1;
+    }
+    for (int32_t i = 0; i < n_nodes && !repeats; ++i)
+      if (well_formed(nodes[i])) {
+        repeats = seen[nodes[i]] == epoch;
+        seen[nodes[i]] = epoch;
+      }
+  }
+  if (n_nodes > 256 && !repeats) sr::parallel_for(static_cast<size_t>(n_nodes), 64, body);
   else body(0, static_cast<size_t>(n_nodes));
   if (first_err.load() != INT64_MAX) return static_cast<sr_status>(first_err.load() & 0xff);
   out_cand_off[0] = 0;

@@ -1249,13 +1249,22 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
   uint64_t* A = w->atoms.data();
   // the host-decided outcomes that read the snapshot must still hold: scalar
   // usage known on every node, no planned candidate's attachable volume on a
-  // spot node (only the nodes changed since the last encode can have one now)
+  // spot node (only the nodes changed since the last encode can have one now;
+  // every node when the state view was rebuilt rather than patched)
   if (R.scalars && snap->scalar_unknown_total > 0) return false;
   if (!R.att_words.empty() && prev_state_gen != C.state_gen) {
-    if (C.patched_from != prev_state_gen) return false;  // changes not known node by node
-    for (int32_t n : C.patched_nodes)
+    auto holds = [&](int32_t n) {
       for (const auto& a : snap->state[n].att)
-        if (std::binary_search(R.att_words.begin(), R.att_words.end(), att_word(a.first, a.second))) return false;
+        if (std::binary_search(R.att_words.begin(), R.att_words.end(), att_word(a.first, a.second))) return true;
+      return false;
+    };
+    if (C.patched_from == prev_state_gen) {
+      for (int32_t n : C.patched_nodes)
+        if (holds(n)) return false;
+    } else {
+      for (int32_t n = 0; n < n_spot; ++n)
+        if (holds(n)) return false;
+    }
   }
   if (w->layout_gen != C.layout_gen) {  // the spot order moved (permute_static): every atom row follows
     std::vector<uint8_t> tmp;
@@ -1303,15 +1312,6 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
       }
     }
   }
-  std::vector<int32_t> flipped;  // classes whose certain emptiness changed
-  if (flags_moved)
-    for (int32_t k = 0; k < static_cast<int32_t>(R.cls_empty.size()); ++k) {
-      const uint8_t e = class_empty(*w, k, R.atom_empty.data(), R.atom_full.data()) ? 1 : 0;
-      if (e != R.cls_empty[k]) {
-        R.cls_empty[k] = e;
-        flipped.push_back(k);
-      }
-    }
   // scalar-resource / volume-limit queries and the shared scalar rows follow
   // the spot nodes' usage
   for (size_t q = 0; q < R.scalar_q.size(); ++q) {
@@ -1325,6 +1325,17 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
     }
   }
   if (!R.scal_names.empty()) node_scal_rows(snap, R.scal_names, w->n_pad, w->node_scal.data());
+  // classes whose certain emptiness changed: after every atom row above was
+  // refreshed (pod count, composites, ports, scalar / volume-limit queries)
+  std::vector<int32_t> flipped;
+  if (flags_moved)
+    for (int32_t k = 0; k < static_cast<int32_t>(R.cls_empty.size()); ++k) {
+      const uint8_t e = class_empty(*w, k, R.atom_empty.data(), R.atom_full.data()) ? 1 : 0;
+      if (e != R.cls_empty[k]) {
+        R.cls_empty[k] = e;
+        flipped.push_back(k);
+      }
+    }
   // thresholds: a distinct request whose smallest node value >= it moved
   constexpr int64_t kNever = INT64_MAX;
   // Only requests in the interval (previous value, value] of a node value

@@ -62,6 +62,7 @@ class Pool {
     unsigned hw = std::thread::hardware_concurrency();
     unsigned want = std::min(16u, hw ? hw : 1u);
     if (const char* e = std::getenv("SR_HOST_THREADS")) want = static_cast<unsigned>(std::max(1, std::atoi(e)));
+    if (const char* e = std::getenv("SR_HOST_SPIN")) spin_ = std::max(0, std::atoi(e));
     for (unsigned i = 1; i < want; ++i) workers_.emplace_back([this] { loop(); });
   }
 
@@ -76,12 +77,18 @@ class Pool {
   // A worker spins a little (~tens of microseconds) for the next generation
   // before it sleeps: a host phase issues parallel loops back to back, and a
   // condition-variable wake-up per loop and worker costs more than the loop.
+  // SR_HOST_SPIN sets the spin count (0: sleep at once, for a planner sharing
+  // its cores with other work).
   void loop() {
     uint64_t seen = 0;
     for (;;) {
-      for (int i = 0; i < kSpin && gen_.load(std::memory_order_acquire) == seen; ++i) {
+      for (int i = 0; i < spin_ && gen_.load(std::memory_order_acquire) == seen; ++i) {
 #if defined(__x86_64__)
         __builtin_ia32_pause();
+#elif defined(__aarch64__)
+        asm volatile("yield");
+#else
+        if ((i & 63) == 63) std::this_thread::yield();
 #endif
       }
       std::unique_lock<std::mutex> lk(mu_);
@@ -97,7 +104,7 @@ class Pool {
     }
   }
 
-  static constexpr int kSpin = 4000;
+  int spin_ = 4000;
   std::vector<std::thread> workers_;
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;

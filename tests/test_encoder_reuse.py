@@ -95,3 +95,18 @@ def test_realistic_variant_reuse(tool, mode):
     r = run_check(tool, 3, 40, env={"SR_SYNTH_REALISTIC": "1"}, mode=mode)
     assert r["bad"] == 0, r["out"]
     assert r["reused"] >= 3, r["out"]
+
+
+def test_scalar_rows_turning_non_empty_flip_classes(tool):
+    """a scalar-resource query row that goes from empty to
+    non-empty (a spot node's extended-resource usage drops) must flip the
+    classes built on it out of the certainly-empty class in the same reuse
+    encode.  `reuse-scalar` fills every spot node allocating a GPU past its
+    allocatable for two ticks in six, then frees it; every tick stays reused
+    (the attachable-volume recheck scans every node when the state view was
+    rebuilt) and equals a fresh encode, with class flips recorded."""
+    r = run_check(tool, 3, 24, env={"SR_SYNTH_REALISTIC": "1"}, mode="reuse-scalar")
+    assert r["bad"] == 0, r["out"]
+    assert r["reused"] == r["ticks"], r["out"]
+    flips = int(re.search(r"class flips (\d+)", r["out"]).group(1))
+    assert flips >= 4, r["out"]

@@ -233,3 +233,21 @@ def test_update_spot_node_metrics_counts():
     n2 = NodeInfo(Node("s2", 4000), [mk("b"), mk("lonely", owner_references=[])], 0, 0)
     n3 = NodeInfo(Node("s3", 4000), [], 0, 0)
     assert updateSpotNodeMetrics([n1, n2, n3], []) == {"s1": 2, "s3": 0}
+
+
+def test_repeated_nodes_match_oracle():
+    # a node named twice in the input (the ABI does not forbid it)
+    # gets its list twice, computed without two threads sharing its scratch
+    # range (the repeated input runs serially): more than 256 nodes so the
+    # parallel pass would otherwise be taken
+    sc = SynthCluster(2)
+    lib = capi.load_planner()
+    nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    order = np.concatenate([nm.on_demand, nm.on_demand[:40], nm.on_demand[::-1][:7]]).astype(np.int32)
+    got = pods_for_deletion(lib.sr_pods_for_deletion, sc.ptr, ctypes.byref(sc.drain), order, nm.node_pod_off,
+                            nm.node_pod_idx)
+    want = pods_for_deletion(load_oracle().oracle_pods_for_deletion, sc.ptr, ctypes.byref(sc.drain), order,
+                             nm.node_pod_off, nm.node_pod_idx)
+    assert got[4] == want[4] == capi.SR_OK
+    for a, b in zip(got[:4], want[:4]):
+        assert np.array_equal(a, b)

@@ -1,7 +1,9 @@
 // Host-only harness: NewNodeMap + snapshot + encode_workload on a synthetic
 // config, printing the workload's dimensions and host-side timings (no GPU).
 //   make -C k8s-spot-rescheduler_amd tools && k8s-spot-rescheduler_amd/bin/encode_stats 3 [max candidates] [check | reuse [ticks [burst]]]
-//   (reuse-perm: pods on spot nodes change requests between ticks, the spot order moves)
+//   (reuse-perm: pods on spot nodes change requests between ticks, the spot order moves;
+//    reuse-scalar: every spot node allocating an extended resource is filled past its allocatable
+//    for two ticks in six and freed again, so scalar query rows go empty <-> non-empty while reused)
 // Encodes are timed cold (empty encoder cache), warm (the same snapshot
 // again) and after one spot node changed (a fresh snapshot with one more pod
 // on one node), the steady state of a planner between two ticks.
@@ -161,7 +163,8 @@ int main(int argc, char** argv) {
            moved_ticks);
   }
   const bool perm = argc > 3 && std::string(argv[3]) == "reuse-perm";
-  if (argc > 3 && (std::string(argv[3]) == "reuse" || perm)) {
+  const bool scal = argc > 3 && std::string(argv[3]) == "reuse-scalar";
+  if (argc > 3 && (std::string(argv[3]) == "reuse" || perm || scal)) {
     // candidate-side reuse: every tick a fresh snapshot with a few more (or
     // fewer) pods on random spot nodes and the same candidate input; the
     // reused workload must plan like one encoded from scratch: same atoms,
@@ -175,8 +178,40 @@ int main(int argc, char** argv) {
     int reused = 0, full = 0, bad = 0;
     long patches = 0;
     double ms_reuse = 0, ms_views = 0;
-    int permuted = 0;
-    for (int r = 0; r < ticks && !cp.empty(); ++r) {
+    int permuted = 0, flips = 0;
+    // reuse-scalar: a candidate pod listing one extended resource (no volume
+    // limit key) and, per spot node allocating that name, enough copies of it
+    // to exceed the allocatable
+    std::vector<std::pair<int32_t, int32_t>> fill;
+    if (scal && c.pod_scalar_off && c.node_scalar_off) {
+      int32_t gp = -1, name = 0;
+      int64_t rq = 0;
+      for (int32_t q : cp) {
+        const int32_t b = c.pod_scalar_off[q], e = c.pod_scalar_off[q + 1];
+        bool ok = e > b;
+        for (int32_t i = b; i < e && ok; ++i) ok = c.pod_scalar_name[i] >= 0 && c.pod_scalar_acc[i] > 0;
+        if (c.volumes) ok = ok && c.volumes->att_off[q] == c.volumes->att_off[q + 1];
+        if (ok) { gp = q; name = c.pod_scalar_name[b]; rq = c.pod_scalar_acc[b]; break; }
+      }
+      for (int32_t k = 0; gp >= 0 && k < ns; ++k)
+        for (int32_t i = c.node_scalar_off[spot[k]]; i < c.node_scalar_off[spot[k] + 1]; ++i)
+          if (c.node_scalar_name[i] == name)
+            for (int64_t u = 0; u <= c.node_scalar_alloc[i] / rq; ++u) fill.emplace_back(gp, k);
+      printf("reuse-scalar: pod %d fills %zu slots\n", gp, fill.size());
+      if (fill.empty()) return 3;
+    }
+    // the pods added at random: in reuse-scalar mode only pods without
+    // attachable volumes (a candidate's attachable volume on a spot node sends
+    // it to the reference path, and such a fallback ends the reuse)
+    std::vector<int32_t> pool;
+    for (int32_t q : cp) {
+      bool ok = true;
+      if (scal && c.pod_scalar_off)
+        for (int32_t i = c.pod_scalar_off[q]; i < c.pod_scalar_off[q + 1] && ok; ++i) ok = c.pod_scalar_name[i] >= 0;
+      if (scal && c.volumes) ok = ok && c.volumes->att_off[q] == c.volumes->att_off[q + 1];
+      if (ok) pool.push_back(q);
+    }
+    for (int r = 0; r < ticks && !pool.empty(); ++r) {
       if (perm && r > 0) {
         // reuse-perm: pods on spot nodes change their cpu request (and stamp):
         // NewNodeMap re-sorts the spot list, the snapshot follows its order
@@ -200,8 +235,10 @@ int main(int argc, char** argv) {
       if (r % 9 == 8) extra.clear();
       const int add = r % 5 == 4 ? burst : 1 + static_cast<int>(rnd(3));  // sometimes a burst: many new free values
       for (int a = 0; a < add; ++a)
-        extra.emplace_back(cp[rnd(cp.size())], static_cast<int32_t>(rnd(static_cast<uint64_t>(ns))));
+        extra.emplace_back(pool[rnd(pool.size())], static_cast<int32_t>(rnd(static_cast<uint64_t>(ns))));
       for (auto& e : extra) sr_snapshot_add_pod(s2, &c, e.first, e.second);
+      if (scal && r % 6 >= 2 && r % 6 < 4)
+        for (auto& e : fill) sr_snapshot_add_pod(s2, &c, e.first, e.second);
       // the realistic variant compares with a full encode by a copy of the
       // encoder as it was before this call: its class and atom numbering
       // depends on the dictionaries' history (scalar and volume queries)
@@ -212,6 +249,7 @@ int main(int argc, char** argv) {
       const double ms = ms_since(t0);
       if (cache.last_reused) {
         ++reused;
+        flips += w.class_flip;
         patches += cache.last_pod_patches;
         ms_reuse += ms;
         ms_views += sr::encode_phase_ms[0];
@@ -251,8 +289,8 @@ int main(int argc, char** argv) {
       sr_snapshot_destroy(s2);
     }
     printf("reuse check: %d ticks (%d reused, %d full), %ld pod patches, reuse encode avg %.3f ms (views %.3f), "
-           "spot order moved %d, mismatches %d\n", reused + full, reused, full, patches, reused ? ms_reuse / reused : 0.0,
-           reused ? ms_views / reused : 0.0, permuted, bad);
+           "spot order moved %d, class flips %d, mismatches %d\n", reused + full, reused, full, patches,
+           reused ? ms_reuse / reused : 0.0, reused ? ms_views / reused : 0.0, permuted, flips, bad);
     if (bad) return 2;
   }
   printf("Wp %d atoms %d classes %d program ops %zu t_rows %zu\n", w.Wp, w.n_atoms, w.n_classes, w.cls_prog.size(),
