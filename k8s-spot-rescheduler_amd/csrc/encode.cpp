@@ -119,27 +119,32 @@ inline uint64_t mix(uint64_t h, uint64_t x) {
 // n (a node without s allocates 0; volume limit keys under negative names: the
 // node's limit, or unlimited, against its unique attachable volumes of the key
 // plus the pod's count).  row: [Wp] words, zeroed by the caller.
-void scalar_query_row(const sr_snapshot* snap, int64_t name64, int64_t req, uint64_t* row) {
+inline bool scalar_query_node(const sr_snapshot* snap, int32_t n, int64_t name64, int64_t req) {
   const int32_t name = static_cast<int32_t>(name64);
+  const int64_t alloc = scalar_alloc_of(snap->nodes[n], name);
+  const int64_t used = scalar_used_of(snap->state[n], name);
+  // Go int64 arithmetic: request + requested wraps like the reference's
+  const int64_t need = static_cast<int64_t>(static_cast<uint64_t>(req) + static_cast<uint64_t>(used));
+  return !(alloc < need);
+}
+void scalar_query_row(const sr_snapshot* snap, int64_t name64, int64_t req, uint64_t* row) {
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
-  for (int32_t n = 0; n < n_spot; ++n) {
-    const int64_t alloc = scalar_alloc_of(snap->nodes[n], name);
-    const int64_t used = scalar_used_of(snap->state[n], name);
-    // Go int64 arithmetic: request + requested wraps like the reference's
-    const int64_t need = static_cast<int64_t>(static_cast<uint64_t>(req) + static_cast<uint64_t>(used));
-    if (!(alloc < need)) row[n >> 6] |= 1ull << (n & 63);
-  }
+  for (int32_t n = 0; n < n_spot; ++n)
+    if (scalar_query_node(snap, n, name64, req)) row[n >> 6] |= 1ull << (n & 63);
 }
 
 // The base free value (alloc - requested) of each shared scalar name on every
 // spot node: the extension records' node_scal rows, [names][n_pad].
+inline int64_t node_scal_value(const sr_snapshot* snap, int32_t n, int32_t name) {
+  // Go int64 arithmetic: alloc - requested wraps like the reference's
+  return static_cast<int64_t>(static_cast<uint64_t>(scalar_alloc_of(snap->nodes[n], name)) -
+                              static_cast<uint64_t>(scalar_used_of(snap->state[n], name)));
+}
 void node_scal_rows(const sr_snapshot* snap, const std::vector<int32_t>& names, int32_t n_pad, int64_t* out) {
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
   for (size_t u = 0; u < names.size(); ++u)
-    for (int32_t n = 0; n < n_spot; ++n)  // Go int64 arithmetic: alloc - requested wraps like the reference's
-      out[u * static_cast<size_t>(n_pad) + static_cast<size_t>(n)] = static_cast<int64_t>(
-          static_cast<uint64_t>(scalar_alloc_of(snap->nodes[n], names[u])) -
-          static_cast<uint64_t>(scalar_used_of(snap->state[n], names[u])));
+    for (int32_t n = 0; n < n_spot; ++n)
+      out[u * static_cast<size_t>(n_pad) + static_cast<size_t>(n)] = node_scal_value(snap, n, names[u]);
 }
 
 // HostPortInfo.CheckConflict of each query against every spot node's base
@@ -1313,18 +1318,40 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
     }
   }
   // scalar-resource / volume-limit queries and the shared scalar rows follow
-  // the spot nodes' usage
-  for (size_t q = 0; q < R.scalar_q.size(); ++q) {
-    uint64_t* a = A + static_cast<size_t>(R.a_scalar + static_cast<int32_t>(q)) * Wp;
-    std::vector<uint64_t>& row = R.port_scratch;
-    row.assign(static_cast<size_t>(Wp), 0);
-    scalar_query_row(snap, R.scalar_q[q].first, R.scalar_q[q].second, row.data());
-    if (!std::equal(row.begin(), row.end(), a)) {
-      std::copy(row.begin(), row.end(), a);
-      refresh_flags(R.a_scalar + static_cast<int32_t>(q));
+  // the spot nodes' usage: only the changed nodes' bits and values when the
+  // state view was patched node by node since this workload's last encode
+  // (its moved positions included: the rows were permuted above), every node
+  // otherwise
+  if (prev_state_gen != C.state_gen && C.patched_from == prev_state_gen) {
+    for (size_t q = 0; q < R.scalar_q.size(); ++q) {
+      uint64_t* a = A + static_cast<size_t>(R.a_scalar + static_cast<int32_t>(q)) * Wp;
+      bool moved_bit = false;
+      for (int32_t n : C.patched_nodes) {
+        uint64_t& wd = a[n >> 6];
+        const uint64_t bit = 1ull << (n & 63), old = wd;
+        wd = scalar_query_node(snap, n, R.scalar_q[q].first, R.scalar_q[q].second) ? (wd | bit) : (wd & ~bit);
+        moved_bit = moved_bit || wd != old;
+      }
+      if (moved_bit) refresh_flags(R.a_scalar + static_cast<int32_t>(q));
     }
+    if (!R.scal_names.empty())
+      for (size_t u = 0; u < R.scal_names.size(); ++u)
+        for (int32_t n : C.patched_nodes)
+          w->node_scal[u * static_cast<size_t>(w->n_pad) + static_cast<size_t>(n)] =
+              node_scal_value(snap, n, R.scal_names[u]);
+  } else if (prev_state_gen != C.state_gen) {
+    for (size_t q = 0; q < R.scalar_q.size(); ++q) {
+      uint64_t* a = A + static_cast<size_t>(R.a_scalar + static_cast<int32_t>(q)) * Wp;
+      std::vector<uint64_t>& row = R.port_scratch;
+      row.assign(static_cast<size_t>(Wp), 0);
+      scalar_query_row(snap, R.scalar_q[q].first, R.scalar_q[q].second, row.data());
+      if (!std::equal(row.begin(), row.end(), a)) {
+        std::copy(row.begin(), row.end(), a);
+        refresh_flags(R.a_scalar + static_cast<int32_t>(q));
+      }
+    }
+    if (!R.scal_names.empty()) node_scal_rows(snap, R.scal_names, w->n_pad, w->node_scal.data());
   }
-  if (!R.scal_names.empty()) node_scal_rows(snap, R.scal_names, w->n_pad, w->node_scal.data());
   // classes whose certain emptiness changed: after every atom row above was
   // refreshed (pod count, composites, ports, scalar / volume-limit queries)
   std::vector<int32_t> flipped;

@@ -981,6 +981,69 @@ __device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W,
   return ballot(jv < 64);
 }
 
+// Extension-record values of a pod (XT candidates, lanes = pods): what
+// NodeInfo.AddPod adds to Requested (calculateResource: no init containers),
+// and per shared scalar slot the fit request (INT64_MIN / INT_MIN: the pod does
+// not list the name) and the accounting.  64-bit, or scaled to 32 bits for
+// narrow candidates (cpu / memory / ephemeral by the candidate's granularity,
+// scalars unscaled).
+template <typename T>
+struct XVals {
+  T ac, am, ae, r0, r1, a0, a1;
+};
+
+// place_window for an XT candidate.  The interaction stays node-local (AddPod
+// changes only the chosen node: rescheduler.go:366), so window order still
+// equals pod order; the running state of a window's node subtracts the
+// accounting instead of the request and keeps the node's two shared scalar
+// slots (ns0 / ns1: allocatable - requested, from node_scal), checked against
+// the pod's scalar requests whatever its cpu / memory / ephemeral request
+// (volume limits have no zero-request exemption; a zero-request pod listing
+// an extended resource never reaches the device).
+template <bool E, bool O>
+__device__ __forceinline__ uint64_t place_window_x(uint64_t todo, int kmax, int W, int lane, int64_t rc, int64_t rm,
+                                                   int64_t re, const XVals<int64_t>& x, uint64_t pm, uint64_t cur,
+                                                   uint64_t zm, uint64_t swap_mask, uint64_t emask, int64_t& ncpu,
+                                                   int64_t& nmem, int64_t& neph, uint64_t& nport, int& nleft,
+                                                   int64_t& ns0, int64_t& ns1, int& node) {
+  int jv = 64;
+  if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
+  while (todo != 0) {
+    const int k = __builtin_ctzll(todo);
+    todo &= ~(1ull << k);
+    const int64_t c = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), k));
+    const int64_t m = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), k));
+    const int64_t e = E ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), k)) : 0;
+    const int64_t r0 = static_cast<int64_t>(readlane64(static_cast<uint64_t>(x.r0), k));
+    const int64_t r1 = static_cast<int64_t>(readlane64(static_cast<uint64_t>(x.r1), k));
+    const uint64_t q = O ? readlane64(pm, k) : 0ull;
+    uint64_t fit = readlane64(cur, k) & ballot(nleft >= 1) & ballot(ns0 >= r0) & ballot(ns1 >= r1);
+    const uint64_t res = ballot(ncpu >= c) & ballot(nmem >= m) & (E ? ballot(neph >= e) : emask);
+    fit &= ((zm >> k) & 1) ? ~0ull : res;  // fitsRequest skips the cpu / memory / ephemeral checks
+    if (O) fit &= ballot((nport & q) == 0);
+    if (fit != 0) {
+      const int j = __builtin_ctzll(fit);
+      const int64_t ac = static_cast<int64_t>(readlane64(static_cast<uint64_t>(x.ac), k));
+      const int64_t am = static_cast<int64_t>(readlane64(static_cast<uint64_t>(x.am), k));
+      const int64_t ae = static_cast<int64_t>(readlane64(static_cast<uint64_t>(x.ae), k));
+      const int64_t a0 = static_cast<int64_t>(readlane64(static_cast<uint64_t>(x.a0), k));
+      const int64_t a1 = static_cast<int64_t>(readlane64(static_cast<uint64_t>(x.a1), k));
+      if (lane == j) {  // ClusterSnapshot.AddPod: Requested grows by calculateResource
+        ncpu -= ac;
+        nmem -= am;
+        neph -= ae;
+        nleft -= 1;
+        ns0 -= a0;
+        ns1 -= a1;
+        if (O) nport |= swap_pairs(q, swap_mask);
+      }
+      jv = lane == k ? j : jv;
+    }
+  }
+  node = jv < 64 ? 64 * W + jv : node;
+  return ballot(jv < 64);
+}
+
 // The free value f of a node scaled to the candidate's request granularity
 // 2^k (narrow candidates): f >> k, or -1 when f < 0 (no request fits, zero
 // included, as with the 64-bit compare).  Values at or above 2^31 are
@@ -1120,6 +1183,59 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
   return ballot(jv < 64);
 }
 
+// place_window_x in 32-bit scaled form (narrow XT candidates): one lane test
+// per pod as in fits32, the two scalar slots included (an unlisted name is
+// INT_MIN: it meets every slot value); the update subtracts the scaled
+// accounting.
+template <bool E, bool O>
+__device__ __forceinline__ uint64_t place_window32_x(uint64_t todo, int kmax, int W, int lane, uint32_t nc, uint32_t nm,
+                                                     uint32_t ne, const XVals<uint32_t>& x, uint64_t pm, uint64_t ps,
+                                                     uint64_t cur, int32_t& c32, int32_t& m32, int32_t& e32,
+                                                     int32_t& s0, int32_t& s1, uint64_t& nport, int& nleft,
+                                                     int& node) {
+  int jv = 64;
+  if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
+  while (todo != 0) {
+    const int k = __builtin_ctzll(todo);
+    todo &= ~(1ull << k);
+    const int32_t c = __builtin_amdgcn_readlane(static_cast<int>(nc), k);
+    const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
+    const int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
+    const int32_t r0 = __builtin_amdgcn_readlane(static_cast<int>(x.r0), k);
+    const int32_t r1 = __builtin_amdgcn_readlane(static_cast<int>(x.r1), k);
+    const uint64_t q = O ? readlane64(pm, k) : 0ull;
+    int32_t t = __builtin_elementwise_sub_sat(c32, c) | __builtin_elementwise_sub_sat(m32, m) | (nleft - 1) |
+                __builtin_elementwise_sub_sat(s0, r0) | __builtin_elementwise_sub_sat(s1, r1);
+    if (E) t |= __builtin_elementwise_sub_sat(e32, e);
+    if (O) {
+      const uint64_t cf = nport & q;
+      const uint32_t u = static_cast<uint32_t>(cf) | static_cast<uint32_t>(cf >> 32);
+      t |= static_cast<int32_t>(u | (0u - u));
+    }
+    const uint64_t fit = readlane64(cur, k) & ballot(t >= 0);
+    if (fit != 0) {
+      const int j = __builtin_ctzll(fit);
+      const int32_t ac = __builtin_amdgcn_readlane(static_cast<int>(x.ac), k);
+      const int32_t am = __builtin_amdgcn_readlane(static_cast<int>(x.am), k);
+      const int32_t ae = __builtin_amdgcn_readlane(static_cast<int>(x.ae), k);
+      const int32_t a0 = __builtin_amdgcn_readlane(static_cast<int>(x.a0), k);
+      const int32_t a1 = __builtin_amdgcn_readlane(static_cast<int>(x.a1), k);
+      if (lane == j) {
+        c32 -= ac;
+        m32 -= am;
+        e32 -= ae;
+        s0 -= a0;
+        s1 -= a1;
+        nleft -= 1;
+        if (O) nport |= readlane64(ps, k);
+      }
+      jv = lane == k ? j : jv;
+    }
+  }
+  node = jv < 64 ? 64 * W + jv : node;
+  return ballot(jv < 64);
+}
+
 // A narrow candidate's request granularity per dimension: every request is a
 // multiple of 2^k (k = the smallest trailing-zero count among them).
 struct Narrow {
@@ -1128,9 +1244,12 @@ struct Narrow {
 
 // WIDE: the F heads of 64 pods per memory round trip also for G > 1 (more
 // registers: for launches whose waves fit the SIMDs at the lower occupancy)
-template <int G, bool PROF, bool WIDE = false>
+// XT: the candidate has extension records at pod_ext[ebase ..] (init-container
+// accounting, shared scalar / volume-limit slots: place_window_x).
+template <int G, bool PROF, bool WIDE = false, bool XT = false>
 __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __restrict__ F, const int p0,
-                                              const int np, int& status, K2Stats& st, uint32_t& nbytes) {
+                                              const int np, int& status, K2Stats& st, uint32_t& nbytes,
+                                              const int ebase = -1) {
   static_assert(64 * G * kNHS * 8 <= sizeof(K2Lds), "node-order LDS exceeds the wave's K2 region");
   const int lane = threadIdx.x & 63;
   const int Wp = w.Wp;
@@ -1165,6 +1284,22 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     const uint64_t e = ballot(64 * g + lane < np && static_cast<uint32_t>(r01[g]) == w.s_empty_off);
     if (e != 0) dead = min(dead, 64 * g + __builtin_ctzll(e));
   }
+  // XT: the pods' extension records and the slots' node_scal rows
+  XVals<int64_t> xv[G];
+  int erow0 = -1, erow1 = -1;
+  if constexpr (XT) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint64_t* er = w.pod_ext + static_cast<size_t>(ebase + min(64 * g + lane, np - 1)) * kDevExtU64;
+      xv[g] = {static_cast<int64_t>(er[0]), static_cast<int64_t>(er[1]), static_cast<int64_t>(er[2]),
+               static_cast<int64_t>(er[3]), static_cast<int64_t>(er[4]), static_cast<int64_t>(er[5]),
+               static_cast<int64_t>(er[6])};
+    }
+    const uint64_t erow = w.pod_ext[static_cast<size_t>(ebase) * kDevExtU64 + 7];
+    erow0 = __builtin_amdgcn_readfirstlane(static_cast<int32_t>(static_cast<uint32_t>(erow)));
+    erow1 = __builtin_amdgcn_readfirstlane(static_cast<int32_t>(erow >> 32));
+    nbytes += 64u * static_cast<uint32_t>(np);
+  }
   // Narrow (32-bit scaled) placement when every request of the candidate
   // allows it: the smallest trailing-zero count per dimension, then every
   // scaled request below 2^23 (place_window32: the <= 256 pods of the
@@ -1172,6 +1307,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   Narrow nk;
   bool narrow;
   uint32_t nc[G], nm[G], ne[G];
+  XVals<uint32_t> nx[G];  // XT, narrow
   {
     auto tz = [](int64_t v) { return v == 0 ? 64 : __builtin_ctzll(static_cast<uint64_t>(v)); };
     int mc = 64, mm = 64, me = 64;
@@ -1180,6 +1316,11 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       mc = min(mc, tz(rc[g]));
       mm = min(mm, tz(rm[g]));
       me = min(me, tz(re[g]));
+      if (XT && 64 * g + lane < np) {  // the accounting is subtracted at the same scale
+        mc = min(mc, tz(xv[g].ac));
+        mm = min(mm, tz(xv[g].am));
+        me = min(me, tz(xv[g].ae));
+      }
     }
     nk.kc = min(wave_min(mc), 62);
     nk.km = min(wave_min(mm), 62);
@@ -1195,6 +1336,27 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       nc[g] = zero[g] ? 0x80000000u : static_cast<uint32_t>(a);
       nm[g] = zero[g] ? 0x80000000u : static_cast<uint32_t>(b);
       ne[g] = zero[g] ? 0x80000000u : static_cast<uint32_t>(c);
+      if constexpr (XT) {
+        // accounting and scalar values below 2^23 (non-negative; a zero-request
+        // pod accounts nothing, as it meets even the INT_MIN ephemeral gate),
+        // scalars unscaled, an unlisted name INT_MIN
+        const XVals<int64_t>& v = xv[g];
+        const uint64_t lim = 1ull << 23;
+        const bool in = 64 * g + lane < np;
+        ok = ok && (!in || ((v.ac | v.am | v.ae | v.a0 | v.a1) >= 0 &&
+                            ((static_cast<uint64_t>(v.ac) >> nk.kc) | (static_cast<uint64_t>(v.am) >> nk.km) |
+                             (static_cast<uint64_t>(v.ae) >> nk.ke) | static_cast<uint64_t>(v.a0) |
+                             static_cast<uint64_t>(v.a1)) < lim &&
+                            (v.r0 == INT64_MIN || (v.r0 >= 0 && v.r0 < static_cast<int64_t>(lim))) &&
+                            (v.r1 == INT64_MIN || (v.r1 >= 0 && v.r1 < static_cast<int64_t>(lim))) &&
+                            (!zero[g] || (v.ac | v.am | v.ae) == 0)));
+        nx[g] = {static_cast<uint32_t>(static_cast<uint64_t>(v.ac) >> nk.kc),
+                 static_cast<uint32_t>(static_cast<uint64_t>(v.am) >> nk.km),
+                 static_cast<uint32_t>(static_cast<uint64_t>(v.ae) >> nk.ke),
+                 v.r0 == INT64_MIN ? 0x80000000u : static_cast<uint32_t>(v.r0),
+                 v.r1 == INT64_MIN ? 0x80000000u : static_cast<uint32_t>(v.r1), static_cast<uint32_t>(v.a0),
+                 static_cast<uint32_t>(v.a1)};
+      }
     }
     narrow = w.k2_narrow && ballot(!ok) == 0;
   }
@@ -1205,7 +1367,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     uint64_t e = 0, o = 0;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      e |= ballot(64 * g + lane < np && re[g] != 0);
+      e |= ballot(64 * g + lane < np && (re[g] != 0 || (XT && xv[g].ae != 0)));
       o |= ballot(64 * g + lane < np && pm[g] != 0);
     }
     E = e != 0;
@@ -1214,7 +1376,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   // exclusive candidate (place_window32 X): a state bit every pod sets and
   // conflicts with -- pod 0's candidates checked against every pod
   bool X = false;
-  if (O) {
+  if (O && !XT) {
     const uint64_t m0 = readlane64(ps[0] & pm[0], 0);
     for (uint64_t bits = m0; bits != 0 && !X; bits &= bits - 1) {
       const int b = __builtin_ctzll(bits);
@@ -1230,6 +1392,15 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   int64_t ncpu = 0, nmem = 0, neph = 0;
   uint64_t nport = 0;
   int nleft = 0;
+  int64_t ns0 = 0, ns1 = 0;  // XT: the node's shared scalar slots (allocatable - requested)
+  auto load_scal = [&](int W) {
+    if constexpr (XT) {
+      const size_t n = static_cast<size_t>(64 * W + lane);
+      ns0 = erow0 >= 0 ? w.node_scal[static_cast<size_t>(erow0) * w.n_pad + n] : 0;
+      ns1 = erow1 >= 0 ? w.node_scal[static_cast<size_t>(erow1) * w.n_pad + n] : 0;
+      nbytes += 64u * 16u;
+    }
+  };
 #ifndef SR_K2_PREFETCH_W0
 #define SR_K2_PREFETCH_W0 1
 #endif
@@ -1241,6 +1412,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     nport = nr[3];
     nleft = static_cast<int>(static_cast<int64_t>(nr[4]));
     if (w.k0_skip) window_patch(w, 0, lane, ncpu, nmem, neph, nport, nleft);
+    load_scal(0);
     wcur = 0;
     nbytes += 64u * 40u;
   }
@@ -1520,6 +1692,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       nport = nr[3];
       nleft = static_cast<int>(static_cast<int64_t>(nr[4]));
       if (w.k0_skip) window_patch(w, W, lane, ncpu, nmem, neph, nport, nleft);
+      load_scal(W);
       wcur = W;
       ++windows;
       nbytes += 64u * 40u;
@@ -1538,12 +1711,16 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       const uint64_t emask = E ? 0ull : ballot(neph >= 0);  // no pod asks for ephemeral storage: fixed
       // narrow candidates: the window's free values scaled to 32 bits once
       // per visit (the 64-bit copies are not read again: the window is not)
-      int32_t c32 = 0, m32 = 0, e32 = 0;
+      int32_t c32 = 0, m32 = 0, e32 = 0, s032 = 0, s132 = 0;
       st.narrow = narrow;
       if (narrow) {
         c32 = E || neph >= 0 ? scale32(ncpu, nk.kc) : INT_MIN;  // place_window32: the ephemeral gate
         m32 = scale32(nmem, nk.km);
         e32 = scale32(neph, nk.ke);
+        if (XT) {
+          s032 = scale32(ns0, 0);
+          s132 = scale32(ns1, 0);
+        }
       }
 #pragma unroll
       for (int g = 0; g < G; ++g) {  // groups in pod order: the state flows from one to the next
@@ -1561,7 +1738,18 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
 #define SR_PW32X(e_)                                                                                            \
   place_window32<e_, true, true>(todo, kmax, W, lane, nc[g], nm[g], ne[g], pm[g], ps[g], cur[g], c32, m32, e32, \
                                  nport, nleft, node[g])
-          if (narrow && X)
+#define SR_PWX(e_, o_)                                                                                          \
+  place_window_x<e_, o_>(todo, kmax, W, lane, rc[g], rm[g], re[g], xv[g], pm[g], cur[g], zm[g], w.swap_mask, emask, \
+                         ncpu, nmem, neph, nport, nleft, ns0, ns1, node[g])
+#define SR_PW32XT(e_, o_)                                                                                       \
+  place_window32_x<e_, o_>(todo, kmax, W, lane, nc[g], nm[g], ne[g], nx[g], pm[g], ps[g], cur[g], c32, m32, e32, \
+                           s032, s132, nport, nleft, node[g])
+          if (XT && narrow)
+            placed = E ? (O ? SR_PW32XT(true, true) : SR_PW32XT(true, false))
+                       : (O ? SR_PW32XT(false, true) : SR_PW32XT(false, false));
+          else if (XT)
+            placed = E ? (O ? SR_PWX(true, true) : SR_PWX(true, false)) : (O ? SR_PWX(false, true) : SR_PWX(false, false));
+          else if (narrow && X)
             placed = E ? SR_PW32X(true) : SR_PW32X(false);
           else if (narrow)
             placed = E ? (O ? SR_PW32(true, true) : SR_PW32(true, false))
@@ -1571,6 +1759,8 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
 #undef SR_PW
 #undef SR_PW32
 #undef SR_PW32X
+#undef SR_PWX
+#undef SR_PW32XT
         }
         placements += __builtin_popcountll(placed);
         act[g] &= ~placed;
@@ -2165,14 +2355,20 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
   uint32_t nbytes = 0;
   const int dbase = w.dyn_cand ? __builtin_amdgcn_readfirstlane(w.dyn_cand[ci]) : -1;
   const int ebase = w.ext_cand ? __builtin_amdgcn_readfirstlane(w.ext_cand[ci]) : -1;
-  const bool node_order = np <= 4 * 64 && w.k2_mode == 0 && ebase < 0;
+  const bool node_order = np <= 4 * 64 && w.k2_mode == 0;
   if (dbase >= 0) {  // writes out_node itself
     wide = 3;
     uint64_t* tl = reinterpret_cast<uint64_t*>(&L);
     if (np <= 64) k2_domain<CH, 1, PROF>(w, tl, p0, np, dbase, status, nbytes, st, ebase);
     else if (np <= 256) k2_domain<CH, 4, PROF>(w, tl, p0, np, dbase, status, nbytes, st, ebase);
     else k2_domain<CH, kDevDynG, PROF>(w, tl, p0, np, dbase, status, nbytes, st, ebase);
-  } else if (ebase >= 0) {  // extension records: pod order with the extended running state
+  } else if (node_order && ebase >= 0) {  // extension records, node order (place_window_x); writes out_node
+    uint64_t* F = reinterpret_cast<uint64_t*>(&L);
+    wide = 2;
+    if (np <= 64) k2_node_order<1, PROF, false, true>(w, F, p0, np, status, st, nbytes, ebase);
+    else if (np <= 128) k2_node_order<2, PROF, false, true>(w, F, p0, np, status, st, nbytes, ebase);
+    else k2_node_order<4, PROF, false, true>(w, F, p0, np, status, st, nbytes, ebase);
+  } else if (ebase >= 0) {  // extension records, pod order (SR_K2_MODE=1) with the extended running state
     int placed = k2_run<1, CH, PROF, true>(w, L, p0, np, status, st, nbytes, ebase);
     wide = placed < 0 ? 1 : 0;
     if (placed < 0) placed = k2_run<8, CH, PROF, true>(w, L, p0, np, status, st, nbytes, ebase);
@@ -2196,7 +2392,10 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
 // candidate, <= 64 * GMAX pods, default mode): only that path is compiled, so
 // the kernel holds far fewer registers than k2_place (more waves per SIMD on
 // the large configs), and a wave's LDS is just its F heads.
-template <int GMAX, bool PROF, bool WIDE = false>
+// XT: the launch holds candidates with extension records (ext_cand), which
+// take place_window_x; the others the plain steps (a separate instance, so a
+// launch without them keeps the lean kernel).
+template <int GMAX, bool PROF, bool WIDE = false, bool XT = false>
 __global__ __launch_bounds__(256) void k2_node(DevWorkload w, const int4* __restrict__ list, int n_list) {
   extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
   const int wave = threadIdx.x >> 6;
@@ -2207,6 +2406,17 @@ __global__ __launch_bounds__(256) void k2_node(DevWorkload w, const int4* __rest
   K2Stats st;
   int status = -1;
   uint32_t nbytes = 0;
+  if constexpr (XT) {
+    const int ebase = __builtin_amdgcn_readfirstlane(w.ext_cand[x.ci]);
+    if (ebase >= 0) {
+      if (GMAX == 1 || x.np <= 64) k2_node_order<1, PROF, false, true>(w, F, x.p0, x.np, status, st, nbytes, ebase);
+      else if (GMAX == 2 || x.np <= 128)
+        k2_node_order<(GMAX >= 2 ? 2 : 1), PROF, WIDE, true>(w, F, x.p0, x.np, status, st, nbytes, ebase);
+      else k2_node_order<GMAX, PROF, WIDE, true>(w, F, x.p0, x.np, status, st, nbytes, ebase);
+      k2_finish<PROF>(w, x, status, 2, nbytes, st);
+      return;
+    }
+  }
   if (GMAX == 1 || x.np <= 64) k2_node_order<1, PROF>(w, F, x.p0, x.np, status, st, nbytes);
   else if (GMAX == 2 || x.np <= 128)
     k2_node_order<(GMAX >= 2 ? 2 : 1), PROF, WIDE>(w, F, x.p0, x.np, status, st, nbytes);
@@ -2227,12 +2437,21 @@ void launch(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, hipEvent
 // The K2 launchers are compiled in parts (SR_KPART, Makefile: one object per
 // part, built in parallel; -1 = everything in one translation unit): 0 = the
 // dispatch, K0 and K3; 1 = the node-order kernels; 2..7 = the general kernel
-// for rows of 1, 2, 4, 8, 16, 32 chunks of 64 words.
+// for rows of 1, 2, 4, 8, 16, 32 chunks of 64 words; 8 = the node-order
+// kernels with extension records.
 #ifndef SR_KPART
 #define SR_KPART -1
 #endif
+// wide F-head rounds where the extra registers cost nothing: launches of at
+// most two waves per SIMD (256 CUs x 4 SIMDs), and G = 4 (one wave per SIMD
+// either way)
+#ifndef SR_K2_WIDE_HEADS
+#define SR_K2_WIDE_HEADS 1
+#endif
 template <bool PROF>
 hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+template <bool PROF>
+hipError_t launch_k2_node_xt_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 template <int CH, bool PROF>
 hipError_t launch_k2_place_ch(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 
@@ -2243,13 +2462,8 @@ hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent
   const int wpb = w.k2_wpb == 1 || w.k2_wpb == 2 ? w.k2_wpb : 4;  // waves per block
   const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
   const size_t lds = wpb * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
-  // wide F-head rounds where the extra registers cost nothing: launches of at
-  // most two waves per SIMD (256 CUs x 4 SIMDs), and G = 4 (one wave per SIMD
-  // either way)
-#ifndef SR_K2_WIDE_HEADS
-#define SR_K2_WIDE_HEADS 1
-#endif
   const bool wide = SR_K2_WIDE_HEADS && n <= 2048;
+  if (w.ext_cand) return launch_k2_node_xt_g<PROF>(w, G, s, ev0, ev1);  // some candidate has extension records
   if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   else if (G == 2 && wide) launch(k2_node<2, PROF, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   else if (G == 2) launch(k2_node<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
@@ -2259,6 +2473,26 @@ hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent
 }
 template hipError_t launch_k2_node_g<false>(const DevWorkload&, int, hipStream_t, hipEvent_t, hipEvent_t);
 template hipError_t launch_k2_node_g<true>(const DevWorkload&, int, hipStream_t, hipEvent_t, hipEvent_t);
+#endif
+
+#if SR_KPART == -1 || SR_KPART == 8
+// the node-order kernels of launches with extension-record candidates
+template <bool PROF>
+hipError_t launch_k2_node_xt_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  const int n = w.n_list;
+  const int wpb = w.k2_wpb == 1 || w.k2_wpb == 2 ? w.k2_wpb : 4;
+  const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
+  const size_t lds = wpb * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
+  const bool wide = SR_K2_WIDE_HEADS && n <= 2048;  // as launch_k2_node_g
+  if (G == 1) launch(k2_node<1, PROF, false, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (G == 2 && wide) launch(k2_node<2, PROF, true, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (G == 2) launch(k2_node<2, PROF, false, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (SR_K2_WIDE_HEADS) launch(k2_node<4, PROF, true, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else launch(k2_node<4, PROF, false, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  return hipGetLastError();
+}
+template hipError_t launch_k2_node_xt_g<false>(const DevWorkload&, int, hipStream_t, hipEvent_t, hipEvent_t);
+template hipError_t launch_k2_node_xt_g<true>(const DevWorkload&, int, hipStream_t, hipEvent_t, hipEvent_t);
 #endif
 
 #if SR_KPART == -1 || SR_KPART >= 2
@@ -2298,7 +2532,7 @@ template <bool PROF>
 hipError_t launch_k2(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
   if (n <= 0) return hipSuccess;
-  if (!w.dyn_cand && !w.ext_cand && w.k2_mode == 0 && w.max_np >= 1 && w.max_np <= 4 * 64 && w.k2_node_kernel)
+  if (!w.dyn_cand && w.k2_mode == 0 && w.max_np >= 1 && w.max_np <= 4 * 64 && w.k2_node_kernel)
     return launch_k2_node_g<PROF>(w, w.max_np <= 64 ? 1 : (w.max_np <= 128 ? 2 : 4), s, ev0, ev1);
   const int chunks = (w.Wp + 63) / 64;
   if (chunks <= 1) return launch_k2_place_ch<1, PROF>(w, s, ev0, ev1);

@@ -378,7 +378,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   // shortcut reads the device records).  Node-order candidates only.
   constexpr size_t kSkipDirty = 16;
   const bool k0_skip = ctx->k0_skip && ncand > 0 && tables_cur && sl.dirty.size() <= kSkipDirty && !sl.class_flip &&
-                       w.ext_cand.empty() && w.dyn_cand.empty() && w.max_cand_pods <= 256 && ctx->k2_mode == 0 &&
+                       w.dyn_cand.empty() && w.max_cand_pods <= 256 && ctx->k2_mode == 0 &&
                        sl.tables_atoms == w.atoms;
   // node patches {node, node_rec[8], node_free[3]}: the changed nodes' records
   // ride in the call's copy; K0 writes them into the node section (or K2 reads
@@ -572,7 +572,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   // and every class program in its 8-slot record: K0 writes only the S-row
   // heads, K2 evaluates S words beyond them from the programs.
   d.s_head_only = 0;
-  if (ctx->s_head_only && w.Wp > 64 && w.dyn_cand.empty() && w.ext_cand.empty() && ctx->k2_mode == 0 && ctx->k2_node_kernel &&
+  if (ctx->s_head_only && w.Wp > 64 && w.dyn_cand.empty() && ctx->k2_mode == 0 && ctx->k2_node_kernel &&
       w.max_cand_pods >= 1 && w.max_cand_pods <= 256) {
     bool short_programs = true;
     for (int32_t k = 0; k < w.n_classes && short_programs; ++k)

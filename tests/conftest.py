@@ -27,3 +27,17 @@ def checker():
     c = PredicateChecker(0)
     yield c
     c.close()
+
+
+@pytest.fixture(scope="session")
+def podorder_checker():
+    """A planner with SR_K2_MODE=1: K2's pod-order path for every candidate
+    (the A/B arm of the node-order window kernel)."""
+    from spotplanner.planner import PredicateChecker
+    os.environ["SR_K2_MODE"] = "1"
+    try:
+        c = PredicateChecker(0)
+    finally:
+        del os.environ["SR_K2_MODE"]
+    yield c
+    c.close()

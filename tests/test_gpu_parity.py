@@ -650,3 +650,14 @@ def test_scaled_run_pass_matches_oracle(narrow):
         tick_parity(c, SynthCluster(5, seed=21))
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("mode", ["node_order", "pod_order"])
+def test_synthetic_config3_realistic_plans_match_oracle(checker, podorder_checker, mode):
+    # bench --variant realistic at full C3 size: StatefulSet EBS claims under a
+    # CSINode limit, init containers, GPU pods -- extension-record candidates on
+    # the node-order window kernel (default) and on the pod-order path
+    from spotplanner.synth import REALISTIC
+    c = checker if mode == "node_order" else podorder_checker
+    o, p = tick_parity(c, SynthCluster(3, **REALISTIC), oracle_threads=16)
+    assert p.checks > 0

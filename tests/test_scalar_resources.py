@@ -31,6 +31,14 @@ G = "nvidia.com/gpu"
 OK, FB = capi.SR_CAND_OK, capi.SR_CAND_FALLBACK
 
 
+
+@pytest.fixture(params=["node_order", "pod_order"])
+def checker(request, checker):
+    """Every GPU case of this module under both K2 settings: the default
+    (extension-record candidates on the node-order window kernel) and
+    SR_K2_MODE=1 (pod order)."""
+    return checker if request.param == "node_order" else request.getfixturevalue("podorder_checker")
+
 def gpod(name, gpu=1, cpu=100, init_gpu=None, init_cpu=None):
     init = []
     if init_gpu is not None or init_cpu is not None:

@@ -43,6 +43,14 @@ BZ = "failure-domain.beta.kubernetes.io/zone"
 EBS_CSI = "ebs.csi.aws.com"
 
 
+
+@pytest.fixture(params=["node_order", "pod_order"])
+def checker(request, checker):
+    """Every GPU case of this module under both K2 settings: the default
+    (extension-record candidates on the node-order window kernel) and
+    SR_K2_MODE=1 (pod order)."""
+    return checker if request.param == "node_order" else request.getfixturevalue("podorder_checker")
+
 def nodes4():
     return [Node("a", cpu_milli=4000, labels={TZ: "z1", TR: "r1", "disk": "ssd"},
                  scalar={"attachable-volumes-aws-ebs": 1}),
