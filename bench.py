@@ -20,10 +20,11 @@ N > 1 runs one process per GPU: under torch.distributed.run (RANK /
 WORLD_SIZE / LOCAL_RANK / MASTER_* from the environment), or, when
 WORLD_SIZE is not set, as N child processes this one starts and waits for
 (it touches no GPU itself and exits non-zero if fewer than N devices are
-visible or any rank fails).  Candidates are the on-demand nodes of a cluster
-with N x 1,500 on-demand nodes and the same 3,500-node spot pool, sharded
-c % N == rank (weak scaling: every GPU holds one C3-sized candidate set);
-the ranks reduce each tick's outcome with one RCCL allreduce(min).
+visible or any rank fails).  Candidates are sharded c % N == rank: with
+--scaling strong the config's own cluster is split over the ranks, with
+--scaling weak the cluster has N x the config's on-demand nodes over the same
+spot pool (every GPU holds one config-sized candidate set); the ranks reduce
+each tick's outcome with one RCCL allreduce(min).
 """
 import argparse
 import ctypes
@@ -661,18 +662,29 @@ def main():
     if rank == 0:
         alg = {"k2_placement": tm.bytes_placement, "k0_tables": tm.bytes_tables}[dom]
         achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-        traffic, traffic_src = None, None
-        pmc = os.path.join(REPO, "profiles", "pmc_traffic_c%d.json" % args.config)
-        if os.path.exists(pmc) and world == 1:
+        # PMC traffic of the same kernel on this config and variant, from the
+        # committed rocprofv3 passes (not measured in this run), else null
+        traffic, traffic_src, traffic_null = None, None, None
+        pmc_name = "pmc_traffic_c%d%s.json" % (args.config, "" if args.variant == "baseline" else "_" + args.variant)
+        pmc = os.path.join(REPO, "profiles", pmc_name)
+        if world > 1:
+            traffic_null = "no PMC pass of the multi-rank command"
+        elif not os.path.exists(pmc):
+            traffic_null = "no committed PMC pass for config %d, variant %s (profiles/%s)" % (args.config,
+                                                                                          args.variant, pmc_name)
+        else:
             with open(pmc) as f:
                 pj = json.load(f)
             traffic = pj.get(dom)
+            if traffic is None:
+                traffic_null = "profiles/%s holds no %s entry" % (pmc_name, dom)
             traffic_src = {"file": os.path.relpath(pmc, REPO), "measured_at_head": pj.get("measured_at_head", "unknown"),
                            "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench command "
                                   "(tools/gpu_round.sh); not measured in this run"}
         chain = k2_chain_summary(latest_profile("c%d_k2_wave_profile.txt" % args.config))
         line = {
-            "metric": "reference-equivalent pod x spot-node feasibility checks/s (drain-plan latency = ms_per_step)",
+            "metric": "reference-equivalent pod x spot-node feasibility checks/s (drain-plan latency: "
+                      "drain_plan_latency_ms)",
             "value": total_issued / elapsed * args.steps if elapsed > 0 else 0.0,
             "unit": "checks/s",
             "checks_per_tick": {"reference_equivalent": int(total_issued), "dense_equivalent": int(total_dense),
@@ -682,6 +694,11 @@ def main():
                                         "pods x spot nodes (notional, not work done)"},
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_step, "latency_ms": round(float(np.median(lat)), 5),
+            "drain_plan_latency_ms": end_to_end["median_ms"] if end_to_end else None,
+            "drain_plan_latency_span": "host to host, SURVEY 8(d): sr_plan_first on a fresh snapshot with one spot "
+                                       "node changed (encode + H2D + kernels + winner and mapping on the host); "
+                                       "end_to_end_tick has the every-candidate plan and the whole housekeeping "
+                                       "tick; ms_per_step is the device tick (inputs resident, back to back)",
             "latency_span": "median of 50 single sr_plan_run calls on an idle device: launch to the winner and "
                             "its mapping in host memory (ms_per_step: back-to-back ticks, every candidate planned)",
             "plans_per_s": (len(cand_off) - 1) / (elapsed / args.steps),
@@ -715,7 +732,7 @@ def main():
                          if breakdown[dom] > 0 else None,
                          "calibration_source": "kernels_ms: the untimed calibration pass before the timed region, "
                                                "every kernel bracketed on every run",
-                         "traffic_source": traffic_src,
+                         "traffic_source": traffic_src, "traffic_null_reason": traffic_null,
                          "algorithmic_bytes": int(alg),
                          "bytes_definition": "bytes the kernel moves, counted by K2 per candidate (pod records, "
                                              "F-row heads and full-row scans, 64-node record windows, outputs; "

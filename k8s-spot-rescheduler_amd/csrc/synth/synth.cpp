@@ -138,15 +138,17 @@ struct Cfg {
   double od_fill_lo, od_fill_hi, spot_fill_lo, spot_fill_hi;
   bool prefer_taints, topology, constraints, ports;
   double pinned;
+  int64_t pods_per_node_x100;  // BASELINE.json's pod count per node x 100 (0: whatever the fill gives);
+                               // the fill lands a little below it and small pods top it up exactly
 };
 
 Cfg config_defaults(int c) {
   switch (c) {
-    case 1: return {10, 10, 9, 9, 0.3, 0.6, 0.4, 0.9, false, false, false, false, 0.0};
-    case 2: return {300, 700, 0, 0, 0.55, 0.98, 0.55, 0.98, true, true, false, false, 0.0};
-    case 3: return {1500, 3500, 0, 0, 0.5, 0.98, 0.5, 0.98, false, true, true, false, 0.15};
-    case 4: return {15000, 35000, 0, 0, 0.5, 0.98, 0.5, 0.98, false, true, true, false, 0.15};
-    default: return {300, 700, 0, 0, 0.55, 0.98, 0.55, 0.98, false, true, false, true, 0.0};
+    case 1: return {10, 10, 9, 9, 0.3, 0.6, 0.4, 0.9, false, false, false, false, 0.0, 0};
+    case 2: return {300, 700, 0, 0, 0.45, 0.85, 0.45, 0.85, true, true, false, false, 0.0, 3000};
+    case 3: return {1500, 3500, 0, 0, 0.5, 0.98, 0.5, 0.98, false, true, true, false, 0.15, 3000};
+    case 4: return {15000, 35000, 0, 0, 0.5, 0.98, 0.5, 0.98, false, true, true, false, 0.15, 3000};
+    default: return {300, 700, 0, 0, 0.55, 0.98, 0.55, 0.98, false, true, false, true, 0.0, 0};
   }
 }
 
@@ -302,6 +304,8 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
 
   const int64_t cpu_choices[7] = {50, 100, 100, 250, 500, 1000, 2000};
   char buf[64];
+  std::vector<int64_t> node_used(static_cast<size_t>(n_nodes), 0);
+  std::vector<int32_t> node_pods(static_cast<size_t>(n_nodes), 0);
   for (int node = 0; node < n_nodes; ++node) {
     const bool spot = is_spot[node];
     std::snprintf(buf, sizeof(buf), "node-%06d", node);
@@ -447,6 +451,31 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
         p.ports.push_back({SR_PROTO_TCP, port, ip});
       }
       push_pod(s, node, p);
+    }
+    node_used[node] = used;
+  }
+  // Top-up to BASELINE.json's pod count (C2 30k, C3 150k, C4 1.5M for the
+  // default node counts): 50m / 64Mi ReplicaSet pods appended round robin to
+  // nodes with a free pod slot and 50m of CPU headroom (LIST order: last on
+  // their node).
+  if (cfg.pods_per_node_x100 > 0) {
+    std::fill(node_pods.begin(), node_pods.end(), 0);
+    for (int32_t nd : s->pod_node) ++node_pods[nd];
+    const int64_t target = cfg.pods_per_node_x100 * n_nodes / 100;
+    int64_t total = static_cast<int64_t>(s->pod_node.size());
+    for (bool room = true; total < target && room;) {
+      room = false;
+      for (int node = 0; node < n_nodes && total < target; ++node) {
+        if (node_pods[node] >= 110 || node_used[node] + 50 > s->alloc_cpu[node]) continue;
+        PodSpec p;
+        p.cpu = 50;
+        p.mem = 64 * kMi;
+        push_pod(s, node, p);
+        node_used[node] += 50;
+        ++node_pods[node];
+        ++total;
+        room = true;
+      }
     }
   }
   for (const std::string& str : s->strings) s->str_label.push_back(label_flags(str));
