@@ -43,6 +43,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 from spotplanner import capi  # noqa: E402
 from spotplanner.planner import PredicateChecker  # noqa: E402
+from spotplanner.scaling import choose_scaling, predict  # noqa: E402
 from spotplanner.synth import REALISTIC, SynthCluster, new_node_map, pods_for_deletion, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -205,6 +206,25 @@ def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, gpu
             "fallback_ratio": round(n_fb / max(1, len(cand_off) - 1), 4)}
 
 
+def rank_record(rank, n_cand, n_pods, local_elapsed_s, steps, breakdown_ms):
+    """One rank's own tick parts for the line's per_rank: its shard, its timed
+    region's time per step before the max over ranks, and the calibration
+    pass's K0 / K2 / collective / K3 per tick."""
+    return {"rank": int(rank), "candidates": int(n_cand), "candidate_pods": int(n_pods),
+            "ms_per_step_local": round(1e3 * local_elapsed_s / max(1, steps), 5),
+            **{k + "_ms": round(float(v), 5) for k, v in breakdown_ms.items()}}
+
+
+def gather_per_rank(rec, world):
+    """Every rank's record on every rank, in rank order (gloo all_gather_object)."""
+    if world <= 1:
+        return [rec]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, rec)
+    return out
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -285,8 +305,10 @@ def main():
     ap.add_argument("--variant", default="baseline", choices=["baseline", "realistic"],
                     help="realistic: the config with StatefulSet volumes, init containers and GPU pods "
                          "(reports the fallback ratio on them); baseline: BASELINE.json's config as specified")
-    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
-                    help="strong: the config's cluster, candidates split over the ranks; weak: N x its candidates")
+    ap.add_argument("--scaling", default="auto", choices=["auto", "strong", "weak"],
+                    help="strong: the config's cluster, candidates split over the ranks; weak: N x its candidates; "
+                         "auto: strong where the predicted sharded tick beats one GPU's, else weak "
+                         "(spotplanner/scaling.py, DESIGN.md 7)")
     ap.add_argument("--tick", default="steady", choices=["steady", "cold"],
                     help="steady: the timed step replays a steady-state tick (the previous tick's candidate input, "
                          "one spot node changed: incremental K0 + K2); cold: a first tick (every table row)")
@@ -309,6 +331,12 @@ def main():
     if world != args.gpus:
         print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
         sys.exit(2)
+    scaling_choice = None
+    if args.scaling == "auto":
+        args.scaling, why = choose_scaling(args.config, world)
+        scaling_choice = {"requested": "auto", "chosen": args.scaling, "reason": why,
+                          "prediction_us": predict(args.config, world) if world > 1 else None,
+                          "model": "spotplanner/scaling.py (measured 1-GPU parts, assumed allreduce latency)"}
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -402,14 +430,14 @@ def main():
 
     # Calibration (untimed): every kernel bracketed with events -> per-kernel
     # breakdown and the dominant kernel.
-    names = ["k0_tables", "k2_placement", "k3_winner_and_collective"]
+    names = ["k0_tables", "k2_placement", "k3_winner", "collective"]
     checker.set_timing(7)
     for _ in range(max(5, min(args.steps, 20))):
         st = lib.sr_plan_run(checker.handle, ctypes.byref(out))
         assert st == capi.SR_OK, (st, checker.last_error())
     tm = checker.timing()
     breakdown = dict(zip(names, [x / max(1, tm.n_runs) for x in
-                                 (tm.ms_tables, tm.ms_placement, tm.ms_winner)]))
+                                 (tm.ms_tables, tm.ms_placement, tm.ms_winner, tm.ms_collective)]))
     dom = max(names[:2], key=lambda x: breakdown[x])
     dom_bit = 1 << names.index(dom)
 
@@ -426,6 +454,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    local_elapsed = elapsed
     assert bad == capi.SR_OK, (bad, checker.last_error())  # a failing run must not be timed as a fast step
     tm = checker.timing()
     dom_ms = ([tm.ms_tables, tm.ms_placement][names.index(dom)] / max(1, tm.n_runs) if not args.no_events
@@ -441,6 +470,8 @@ def main():
     else:
         total_issued, total_dense = issued_local, dense_local
     ms_step = 1e3 * elapsed / args.steps
+    per_rank = gather_per_rank(rank_record(rank, len(loff) - 1, len(lpods), local_elapsed, args.steps, breakdown),
+                               world)
 
     # per-candidate outputs once more (outside the timed region): the parity
     # check and K2's byte counts of the same plan
@@ -713,6 +744,8 @@ def main():
                        "candidates_per_rank": shard_sizes(len(cand_off) - 1, world)},
             "collective": {"backend": "rccl" if rccl_ranks else "none", "ranks": rccl_ranks,
                            "per_tick": "one allreduce(min) of 3 x u64" if rccl_ranks else "none (one GPU)"},
+            "per_rank": per_rank,
+            "scaling_choice": scaling_choice,
             "first_ok": int(out.first_ok), "winner": int(out.winner),
             "fallback_candidates": int(np.sum(status[:len(loff) - 1] == capi.SR_CAND_FALLBACK)),
             "kernels_ms": {kk: round(v, 5) for kk, v in breakdown.items()},

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SR_ABI_VERSION 6
+#define SR_ABI_VERSION 7
 
 /* ------------------------------------------------------------------ status */
 typedef int32_t sr_status;
@@ -501,7 +501,7 @@ const char *sr_build_info(void);
  * against before its first call and refuses to run on a mismatch, since the
  * library would otherwise read fields past the end of a shorter struct (ABI 5
  * added sr_cluster.volumes and pod_stamp; ABI 6 the sr_timing enc_reused /
- * enc_pod_patches counters, which sr_get_timing writes). */
+ * enc_pod_patches counters, which sr_get_timing writes; ABI 7 sr_timing.ms_collective). */
 int32_t     sr_abi_version(void);
 
 /* Batched findSpotNodeForPod (rescheduler.go:338-353): for each pod, the first
@@ -586,7 +586,8 @@ typedef struct {
   int32_t  n_runs;          /* timed runs accumulated */
   double   ms_tables;       /* K0: class / threshold row tables */
   double   ms_placement;    /* K2: feasibility rows + per-candidate first-fit placement */
-  double   ms_winner;       /* collective (multi-GPU) + K3, which writes the result to mapped host memory */
+  double   ms_winner;       /* K3, which writes the result to mapped host memory (ABI 7: without the
+                               collective, which is ms_collective) */
   double   ms_pack_host;    /* last sr_plan_prepare host encoding */
   double   ms_upload;       /* last sr_plan_prepare upload */
   uint64_t bytes_tables;    /* algorithmic bytes per K0 launch */
@@ -608,9 +609,10 @@ typedef struct {
                                 * tables stand and K2 recomputes the changed nodes' bits; ABI 6) */
   int32_t  k0_rows_moved;      /* ... and threshold rows it rewrites whole */
   int32_t  k0_dirty_nodes;     /* no K0: spot nodes changed since the tables were written */
+  double   ms_collective;      /* multi-GPU: the allreduce(min) between K2 and K3 (ABI 7) */
 } sr_timing;
 /* mask: which kernels sr_plan_run brackets with HIP events (resets the sums):
- * 1 = K0, 2 = K2, 4 = collective (multi-GPU) + K3; 0 = no events.  Events are read back lazily, by
+ * 1 = K0, 2 = K2, 4 = collective (multi-GPU) and K3, timed apart; 0 = no events.  Events are read back lazily, by
  * sr_get_timing / sr_set_timing, so timed runs do not synchronise.  Timestamped dispatches
  * lengthen a tick, so SR_TIME_EVERY(n) samples every n-th run only (n_runs counts sampled runs). */
 #define SR_TIME_TABLES      1

@@ -2864,6 +2864,20 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
       l[2] = e;
       l[3] = w->cand_global[i];
     }
+    if (!w->ext_cand.empty()) {  // the entries' extension-record heads, in list order
+      w->list_ext.assign(n_act * 4, -1);
+      for (size_t j = 0; j < n_act; ++j) {
+        const int32_t e = w->ext_cand[static_cast<size_t>(w->list[j * 4])];
+        int32_t* x = &w->list_ext[j * 4];
+        x[0] = e;
+        x[3] = 0;
+        if (e >= 0) {
+          const uint64_t erow = w->pod_ext[static_cast<size_t>(e) * kExtU64 + 7];
+          x[1] = static_cast<int32_t>(static_cast<uint32_t>(erow));
+          x[2] = static_cast<int32_t>(erow >> 32);
+        }
+      }
+    }
   }
   phase(6);
 

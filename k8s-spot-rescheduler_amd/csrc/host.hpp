@@ -423,6 +423,8 @@ struct Workload {
   // ---- extension records (kExtU64 per pod of the candidates that need them)
   std::vector<int32_t> ext_cand;  // [n_active] first record in pod_ext, -1: none (empty: no such candidate)
   std::vector<uint64_t> pod_ext;
+  std::vector<int32_t> list_ext;  // [n][4] per work-list entry {first record (-1: none), node_scal row of slot 0,
+                                  // of slot 1 (-1: no slot), 0}: K2 reads it with the entry (no dependent loads)
   int32_t n_scal_names = 0;
   std::vector<int64_t> node_scal; // [n_scal_names][n_pad] alloc - requested of each shared scalar name
   // ---- host-decided outcomes for every input candidate
@@ -446,7 +448,7 @@ struct Workload {
   void reset() {
     t_thr.clear();
     for (auto* v : {&cls_prog_off, &cls_prog, &cls_prog8, &t_dim, &pod_src, &cand_off, &cand_global, &cand_src, &list,
-                    &status_host, &dyn_cand, &dk_dom, &ds_info, &sp_tab, &ext_cand})
+                    &status_host, &dyn_cand, &dk_dom, &ds_info, &sp_tab, &ext_cand, &list_ext})
       v->clear();
     dyn_pod.clear();
     pod_ext.clear();

@@ -1246,10 +1246,13 @@ struct Narrow {
 // registers: for launches whose waves fit the SIMDs at the lower occupancy)
 // XT: the candidate has extension records at pod_ext[ebase ..] (init-container
 // accounting, shared scalar / volume-limit slots: place_window_x).
+// erow0_in / erow1_in: the slots' node_scal rows from the work-list entry's
+// list_ext (k2_node), or -2: read them from the candidate's first record.
 template <int G, bool PROF, bool WIDE = false, bool XT = false>
 __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __restrict__ F, const int p0,
                                               const int np, int& status, K2Stats& st, uint32_t& nbytes,
-                                              const int ebase = -1) {
+                                              const int ebase = -1, const int erow0_in = -2,
+                                              const int erow1_in = -2) {
   static_assert(64 * G * kNHS * 8 <= sizeof(K2Lds), "node-order LDS exceeds the wave's K2 region");
   const int lane = threadIdx.x & 63;
   const int Wp = w.Wp;
@@ -1295,9 +1298,14 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
                static_cast<int64_t>(er[3]), static_cast<int64_t>(er[4]), static_cast<int64_t>(er[5]),
                static_cast<int64_t>(er[6])};
     }
-    const uint64_t erow = w.pod_ext[static_cast<size_t>(ebase) * kDevExtU64 + 7];
-    erow0 = __builtin_amdgcn_readfirstlane(static_cast<int32_t>(static_cast<uint32_t>(erow)));
-    erow1 = __builtin_amdgcn_readfirstlane(static_cast<int32_t>(erow >> 32));
+    if (erow0_in == -2) {
+      const uint64_t erow = w.pod_ext[static_cast<size_t>(ebase) * kDevExtU64 + 7];
+      erow0 = __builtin_amdgcn_readfirstlane(static_cast<int32_t>(static_cast<uint32_t>(erow)));
+      erow1 = __builtin_amdgcn_readfirstlane(static_cast<int32_t>(erow >> 32));
+    } else {
+      erow0 = erow0_in;
+      erow1 = erow1_in;
+    }
     nbytes += 64u * static_cast<uint32_t>(np);
   }
   // Narrow (32-bit scaled) placement when every request of the candidate
@@ -2338,8 +2346,14 @@ __device__ __forceinline__ void k2_finish(const DevWorkload& w, const K2Entry& x
   }
 }
 
+// SR_K2_KARG=0 (A/B): the K2 kernels read the by-value argument instead
+#ifndef SR_K2_KARG
+#define SR_K2_KARG 1
+#endif
 template <int CH, bool PROF>
-__global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __restrict__ list, int n_list) {
+__global__ __launch_bounds__(256) void k2_place(DevWorkload w_arg, const int4* __restrict__ list, int n_list) {
+  const DevWorkload& w = SR_K2_KARG ? *(const DevWorkload*)__builtin_amdgcn_kernarg_segment_ptr() : w_arg;
+  (void)w_arg;  // as in k2_node
   extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -2396,23 +2410,32 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w, const int4* __res
 // take place_window_x; the others the plain steps (a separate instance, so a
 // launch without them keeps the lean kernel).
 template <int GMAX, bool PROF, bool WIDE = false, bool XT = false>
-__global__ __launch_bounds__(256) void k2_node(DevWorkload w, const int4* __restrict__ list, int n_list) {
+__global__ __launch_bounds__(256) void k2_node(DevWorkload w_arg, const int4* __restrict__ list, int n_list) {
+  // the workload read in place from the kernel-argument segment (w_arg is its
+  // first argument): each field is a scalar load where it is used, instead of
+  // values held (or spilled to scratch) across the kernel
+  const DevWorkload& w = SR_K2_KARG ? *(const DevWorkload*)__builtin_amdgcn_kernarg_segment_ptr() : w_arg;
+  (void)w_arg;
   extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
   const int wave = threadIdx.x >> 6;
   const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * (blockDim.x >> 6)) + wave);
   if (li >= n_list) return;
+  int4 xe = {-1, -1, -1, 0};
+  if (XT) xe = w.list_ext[li];  // issued with the entry: one round trip for both
   const K2Entry x = k2_entry<PROF>(list, li);
   uint64_t* F = k2_lds + static_cast<size_t>(wave) * (64 * GMAX * kNHS + (w.s_head_only ? 64 * GMAX * 4 : 0));
   K2Stats st;
   int status = -1;
   uint32_t nbytes = 0;
   if constexpr (XT) {
-    const int ebase = __builtin_amdgcn_readfirstlane(w.ext_cand[x.ci]);
+    const int ebase = __builtin_amdgcn_readfirstlane(xe.x);
+    const int er0 = __builtin_amdgcn_readfirstlane(xe.y), er1 = __builtin_amdgcn_readfirstlane(xe.z);
     if (ebase >= 0) {
-      if (GMAX == 1 || x.np <= 64) k2_node_order<1, PROF, false, true>(w, F, x.p0, x.np, status, st, nbytes, ebase);
+      if (GMAX == 1 || x.np <= 64)
+        k2_node_order<1, PROF, false, true>(w, F, x.p0, x.np, status, st, nbytes, ebase, er0, er1);
       else if (GMAX == 2 || x.np <= 128)
-        k2_node_order<(GMAX >= 2 ? 2 : 1), PROF, WIDE, true>(w, F, x.p0, x.np, status, st, nbytes, ebase);
-      else k2_node_order<GMAX, PROF, WIDE, true>(w, F, x.p0, x.np, status, st, nbytes, ebase);
+        k2_node_order<(GMAX >= 2 ? 2 : 1), PROF, WIDE, true>(w, F, x.p0, x.np, status, st, nbytes, ebase, er0, er1);
+      else k2_node_order<GMAX, PROF, WIDE, true>(w, F, x.p0, x.np, status, st, nbytes, ebase, er0, er1);
       k2_finish<PROF>(w, x, status, 2, nbytes, st);
       return;
     }

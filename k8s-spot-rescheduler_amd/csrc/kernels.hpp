@@ -88,6 +88,8 @@ struct DevWorkload {
   const uint64_t* pod_ext;   // [..][kDevExtU64] {acc cpu, acc mem, acc eph, req s0, req s1 (INT64_MIN: not
                              //  listed), acc s0, acc s1, node_scal row of s0 | of s1 << 32 (-1: no slot)}
   const int64_t* node_scal;  // [rows][n_pad] base free value (allocatable - requested) of a shared scalar
+  const int4* list_ext;      // [n_list] per work-list entry {first record in pod_ext (-1: none), node_scal row of
+                             //  slot 0, of slot 1 (-1: no slot), 0}
   // outputs / scratch
   uint64_t* S;         // [n_classes][Wp] static-class rows, followed by
   uint64_t* T;         // [n_t][Wp] capacity threshold rows (one table)

@@ -337,6 +337,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t o_st = dyn ? pk.add(w.sp_tab) : 0;
   const bool ext = !w.ext_cand.empty();
   const size_t o_ec = ext ? pk.add(w.ext_cand) : 0, o_ep = ext ? pk.add(w.pod_ext) : 0;
+  const size_t o_le = ext ? pk.add(w.list_ext) : 0;
   const size_t tick_from = pk.size();
   const size_t o_ns = ext ? pk.add(w.node_scal) : 0;  // the spot nodes' scalar usage: state, so every tick
   const size_t o_at = pk.add(w.atoms);
@@ -551,6 +552,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.n_dk = w.n_dk;
   d.ext_cand = ext ? static_cast<const int32_t*>(at(o_ec)) : nullptr;
   d.pod_ext = ext ? static_cast<const uint64_t*>(at(o_ep)) : nullptr;
+  d.list_ext = ext ? static_cast<const int4*>(at(o_le)) : nullptr;
   d.node_scal = ext ? static_cast<const int64_t*>(at(o_ns)) : nullptr;
   static_assert(sr::kDevExtU64 == sr::kExtU64, "extension record layout shared by encode.cpp and kernels.hip");
   static_assert(sr::kDevDynU64 == sr::kDynU64 && sr::kDevDomKeys == sr::kDomKeys && sr::kDevDynTerms == sr::kDynTerms &&
@@ -670,7 +672,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
 sr_status flush_timing(sr_ctx* ctx) {
   if (ctx->ev_used == 0) return SR_OK;
   HIP_TRY(ctx, hipEventSynchronize(ctx->ev_end[ctx->ev_used - 1]));
-  double* sums[3] = {&ctx->t.ms_tables, &ctx->t.ms_placement, &ctx->t.ms_winner};
+  double* sums[4] = {&ctx->t.ms_tables, &ctx->t.ms_placement, &ctx->t.ms_winner, &ctx->t.ms_collective};
   for (size_t i = 0; i < ctx->ev_used; ++i) {
     float ms = 0;
     HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev_start[i], ctx->ev_end[i]));
@@ -759,9 +761,10 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   // Timed kernels get an event pair from the pool, recorded by their own
   // dispatch (hipExtLaunchKernelGGL); the collective is bracketed with
   // plain records.  Events are read back lazily (flush_timing).
+  // k: 0 = K0, 1 = K2, 2 = K3, 3 = the collective (mask bit 2, with K3)
   auto pair_for = [&](int k, hipEvent_t* a, hipEvent_t* b) -> sr_status {
     *a = *b = nullptr;
-    if (!(timing >> k & 1)) return SR_OK;
+    if (!(timing >> (k == 3 ? 2 : k) & 1)) return SR_OK;
     if (ctx->ev_used == ctx->ev_start.size()) {
       if (ctx->ev_used >= 3072) {  // bounded pool: read back what is pending
         sr_status st = flush_timing(ctx);
@@ -830,11 +833,12 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   if (early) return finish_early(ctx, out);
   PAIR(2, e2a, e2b);
   if (collective) {
-    if (e2a) HIP_TRY(ctx, hipEventRecord(e2a, s));
+    PAIR(3, eca, ecb);
+    if (eca) HIP_TRY(ctx, hipEventRecord(eca, s));
     sr_status cst = allreduce_min_dev(ctx, d.d_min, 3);  // first ok, first fallback, rank_next
     if (cst != SR_OK) return cst;
-    HIP_TRY(ctx, sr::launch_winner(d, s));
-    if (e2b) HIP_TRY(ctx, hipEventRecord(e2b, s));
+    if (ecb) HIP_TRY(ctx, hipEventRecord(ecb, s));
+    HIP_TRY(ctx, sr::launch_winner(d, s, e2a, e2b));
   } else {
     HIP_TRY(ctx, sr::launch_winner(d, s, e2a, e2b));
   }
@@ -1177,7 +1181,7 @@ sr_status sr_set_timing(sr_ctx* ctx, int32_t mask) {
   ctx->timing_every = std::max(1, (mask >> 8) & 0xffff);
   ctx->timing_runs = 0;
   ctx->t.n_runs = 0;
-  ctx->t.ms_tables = ctx->t.ms_placement = ctx->t.ms_winner = 0;
+  ctx->t.ms_tables = ctx->t.ms_placement = ctx->t.ms_winner = ctx->t.ms_collective = 0;
   return SR_OK;
 }
 

@@ -146,7 +146,8 @@ class sr_timing(ctypes.Structure):
                 ("enc_static_rebuilt", ctypes.c_int32), ("enc_state_nodes", ctypes.c_int32),
                 ("prefix_batches", ctypes.c_int32), ("enc_memo_pods", ctypes.c_int32),
                 ("enc_reused", ctypes.c_int32), ("enc_pod_patches", ctypes.c_int32),
-                ("k0_columns", ctypes.c_int32), ("k0_rows_moved", ctypes.c_int32), ("k0_dirty_nodes", ctypes.c_int32)]
+                ("k0_columns", ctypes.c_int32), ("k0_rows_moved", ctypes.c_int32), ("k0_dirty_nodes", ctypes.c_int32),
+                ("ms_collective", ctypes.c_double)]
 
 
 def ptr(arr, typ):

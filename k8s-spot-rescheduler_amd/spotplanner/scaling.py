@@ -1,0 +1,86 @@
+"""Multi-GPU tick prediction and the sharding choice.
+
+The reference plans a tick's candidates one after another (rescheduler.go:
+228-287); the planner shards them c % N over N GPUs, each holding the whole
+spot snapshot, and reduces the tick's outcome with one allreduce(min) of
+three u64 words followed by K3 (the reduced header and the winner's mapping to
+host memory).  A rank's device tick is K2 over its shard plus, for N > 1, the
+collective and K3:
+
+    tick(N) = max(chain, K2_1 * share(N)) + gap + [N > 1] (allreduce(N) + K3)
+
+  chain   the longest candidate's dependent placement chain (one wave: no
+          number of GPUs shortens it);
+  K2_1    K2 over the whole candidate set on one GPU (throughput part);
+  share   1/N under strong scaling (the config's candidates split), 1 under
+          weak scaling (every rank holds a config-sized candidate set);
+  gap     launch and kernel-boundary time of a back-to-back tick beyond K2;
+  K3      the winner kernel after the collective (one GPU: K2 writes the
+          result itself, no K3).
+
+Sharding a fixed tick pays only when tick_strong(N) < tick(1): K2 must be
+throughput-bound well above its chain.  C4 (15,000 candidates, K2 68 us
+against a 41 us longest wave) is, up to the point where that wave and the
+collective dominate; C3 (1,500 candidates, a 12.2 us chain in a 13.8 us K2)
+is not, so a strong-scaled C3 tick on 8 GPUs is slower than on one.  `choose_scaling` makes that call per config for bench.py --scaling auto.
+"""
+
+# Measured on one MI355X at round 4's final head (profiles/r04/final/
+# c*_bench.json: kernels_ms.k2_placement = K2, ms_per_step - K2 = gap (>= 0);
+# c*_k2_wave_profile.txt: the longest wave = chain; C1 has no wave profile, its
+# 10 candidates are one chain).  K3 4.5 us.  Microseconds.
+PARTS = {
+    1: dict(k2=7.1, chain=7.1, gap=6.4, k3=4.5),
+    2: dict(k2=18.6, chain=16.9, gap=0.7, k3=4.5),
+    3: dict(k2=13.8, chain=12.2, gap=2.6, k3=4.5),
+    4: dict(k2=67.8, chain=41.3, gap=0.0, k3=4.5),
+    5: dict(k2=36.9, chain=36.9, gap=0.5, k3=4.5),
+}
+
+# RCCL allreduce of 24 B over xGMI, per rank count.  ASSUMED, not measured:
+# no multi-GPU box was available to this build; RCCL's
+# small-message latency on one node, of the order of its LL protocol's few
+# hops per ring step.  bench.py reports the measured value per rank when it
+# runs on N GPUs (per_rank[].collective_ms).
+ALLREDUCE_US = {1: 0.0, 2: 8.0, 4: 12.0, 8: 20.0}
+
+
+def allreduce_us(n):
+    if n in ALLREDUCE_US:
+        return ALLREDUCE_US[n]
+    lo = max(k for k in ALLREDUCE_US if k <= n)
+    return ALLREDUCE_US[lo] * (n / lo) ** 0.5
+
+
+def predict_tick_us(parts, n, scaling):
+    """Predicted back-to-back device tick of one rank, us."""
+    share = 1.0 / n if scaling == "strong" else 1.0
+    k2 = max(parts["chain"], parts["k2"] * share)
+    return k2 + parts["gap"] + ((allreduce_us(n) + parts["k3"]) if n > 1 else 0.0)
+
+
+def predict(config, n):
+    """Per-N prediction for a config: both scalings, the strong tick's speed-up
+    over one GPU, and the predicted scaling efficiencies the driver would
+    compute from the bench values (weak: N x the work in tick(N); strong: the
+    same work in tick(N))."""
+    p = PARTS[config]
+    t1 = predict_tick_us(p, 1, "strong")
+    ts = predict_tick_us(p, n, "strong")
+    tw = predict_tick_us(p, n, "weak")
+    return {"n": n, "tick1_us": round(t1, 2), "strong_tick_us": round(ts, 2), "weak_tick_us": round(tw, 2),
+            "strong_efficiency": round(t1 / (n * ts), 3), "weak_efficiency": round(t1 / tw, 3),
+            "strong_pays": ts < t1}
+
+
+def choose_scaling(config, n):
+    """bench.py --scaling auto: shard the config's own tick (strong) where that
+    shortens it, else give every rank a config-sized candidate set (weak)."""
+    if n <= 1:
+        return "strong", "one GPU"
+    r = predict(config, n)
+    if r["strong_pays"]:
+        return "strong", "predicted strong tick %.1f us < 1-GPU tick %.1f us" % (r["strong_tick_us"], r["tick1_us"])
+    return "weak", ("predicted strong tick %.1f us >= 1-GPU tick %.1f us (K2 chain-bound: the longest candidate's "
+                    "chain %.1f us of %.1f us): sharding the config's tick does not pay"
+                    % (r["strong_tick_us"], r["tick1_us"], PARTS[config]["chain"], PARTS[config]["k2"]))

@@ -99,7 +99,7 @@ def c3_lists():
 
 @pytest.mark.parametrize("n", [2, 4, 8])
 def test_strong_scaling_shards_the_c3_cluster(c3_lists, n):
-    """--scaling strong (default) keeps BASELINE's C3 cluster (5,000 nodes: 1,500 on-demand / 3,500 spot) at
+    """--scaling strong keeps BASELINE's C3 cluster (5,000 nodes: 1,500 on-demand / 3,500 spot) at
     every N and splits its 1,500 candidates c % N; the workload string names the counts actually planned."""
     from spotplanner.synth import shard
     sc, nm, off, pods = c3_lists
@@ -130,6 +130,10 @@ def test_weak_scaling_multiplies_candidates_and_says_so(n):
     assert "weak scaling" in w
 
 
-def test_bench_defaults_to_strong_scaling():
+def test_bench_defaults_to_auto_scaling():
+    # --scaling auto: the model (spotplanner/scaling.py) picks strong where the
+    # sharded tick beats one GPU's (C4), weak where K2 is chain-bound (C3)
     src = open(os.path.join(REPO, "bench.py")).read()
-    assert 'default="strong"' in src and '"scaling": args.scaling' in src
+    assert 'default="auto"' in src and '"scaling": args.scaling' in src
+    from spotplanner.scaling import choose_scaling
+    assert choose_scaling(3, 8)[0] == "weak" and choose_scaling(4, 2)[0] == "strong"

@@ -183,6 +183,9 @@ def cases():
            "b takes 3 (count 3), c has no CSINode limit")
     yield ("csi_limit_without_volume_on_full_node", w_lim, [[pod("e", csi("e1"))], [], [], []],
            [[pod("p")]], [OK], [[0]], "no new volume: no check")
+    yield ("csi_limit_over_limit_node_no_new_volume", w_lim, [[pod("e", csi("e1")), pod("f", csi("q5"))], [], [], []],
+           [[pod("p")]], [OK], [[0]],
+           "a holds 2 > CSINode count 1, but p brings no new volume: csi.go returns before counting (DESIGN 2.11)")
     w_ebs = world(("q1", pv("ve", kind="aws-ebs", vid="vol-9")))
     yield ("ebs_allocatable_limit", w_ebs, [[pod("e", Volume(aws_ebs="vol-1"))], [], [], []],
            [[pod("p", Volume(aws_ebs="vol-2"))]], [OK], [[1]],

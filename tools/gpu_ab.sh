@@ -15,9 +15,11 @@ for rep in 1 2; do
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 e = d.get("end_to_end_tick") or {}
+k = d["kernels_ms"]
 print("%-40s ms/step %.4f  latency %.4f  K0 %.4f  K2 %.4f  K3 %.4f  e2e %.4f  all %.3f" % (sys.argv[2],
-      d["ms_per_step"], d.get("latency_ms", 0), d["kernels_ms"]["k0_tables"], d["kernels_ms"]["k2_placement"],
-      d["kernels_ms"]["k3_winner_and_collective"], e.get("median_ms", 0), (e.get("all_candidates") or {}).get("median_ms", 0)))
+      d["ms_per_step"], d.get("latency_ms", 0), k["k0_tables"], k["k2_placement"],
+      k.get("k3_winner", k.get("k3_winner_and_collective", 0)), e.get("median_ms", 0),
+      (e.get("all_candidates") or {}).get("median_ms", 0)))
 PY
   done
 done
