@@ -44,7 +44,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 from spotplanner import capi  # noqa: E402
 from spotplanner.planner import PredicateChecker  # noqa: E402
 from spotplanner.scaling import choose_scaling, predict  # noqa: E402
-from spotplanner.synth import REALISTIC, SynthCluster, new_node_map, pods_for_deletion, shard  # noqa: E402
+from spotplanner.synth import AFFINITY, REALISTIC, SynthCluster, new_node_map, pods_for_deletion, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 DEFAULT_OD = {1: 10, 2: 300, 3: 1500, 4: 15000, 5: 300}
@@ -64,6 +64,11 @@ def workload_name(config, n_nodes, n_od, n_spot, n_pods, world, scaling, variant
         s += ("; realistic variant: %d%% StatefulSet pods with a zonal EBS CSI claim (CSINode limit 25), "
               "%d%% with an init container, %d%% of GPU-node pods asking for a GPU"
               % tuple(round(100 * REALISTIC[k]) for k in ("stateful_fraction", "init_fraction", "gpu_fraction")))
+    elif variant == "affinity":
+        s += ("; affinity variant: every pod in a Deployment (~5 replicas, 16 namespaces), %d%% of the Deployments "
+              "with required hostname pod anti-affinity, %d%% with a zone DoNotSchedule topology spread constraint "
+              "(maxSkew 1), their spot replicas included"
+              % tuple(round(100 * AFFINITY[k]) for k in ("anti_fraction", "spread_fraction")))
     if world > 1:
         s += "; %s scaling: %d candidates sharded c %% %d" % (scaling, n_od, world)
     return s
@@ -302,9 +307,10 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
-    ap.add_argument("--variant", default="baseline", choices=["baseline", "realistic"],
-                    help="realistic: the config with StatefulSet volumes, init containers and GPU pods "
-                         "(reports the fallback ratio on them); baseline: BASELINE.json's config as specified")
+    ap.add_argument("--variant", default="baseline", choices=["baseline", "realistic", "affinity"],
+                    help="realistic: the config with StatefulSet volumes, init containers and GPU pods; affinity: "
+                         "Deployments with hostname anti-affinity and zone topology spread (both report the "
+                         "fallback ratio on them); baseline: BASELINE.json's config as specified")
     ap.add_argument("--scaling", default="auto", choices=["auto", "strong", "weak"],
                     help="strong: the config's cluster, candidates split over the ranks; weak: N x its candidates; "
                          "auto: strong where the predicted sharded tick beats one GPU's, else weak "
@@ -345,7 +351,7 @@ def main():
 
     lib = capi.load_planner()
     sc = SynthCluster(args.config, n_on_demand=cluster_on_demand(args.config, world, args.scaling),
-                      **(REALISTIC if args.variant == "realistic" else {}))
+                      **({"realistic": REALISTIC, "affinity": AFFINITY}.get(args.variant, {})))
     nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
     # run()'s candidate lists (rescheduler.go:228-264): GetPodsForDeletionOnNodeDrain + the
     # DaemonSet-owner filter, on the host (sr_pods_for_deletion)

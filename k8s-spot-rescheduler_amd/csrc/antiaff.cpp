@@ -251,12 +251,57 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
     // are unknown (added from a cluster without sr_pod_affinity)
     if (own_terms && snap->unknown_total > 0) status[i] = SR_CAND_FALLBACK;
   }
-  const int32_t T = static_cast<int32_t>(dict.size());
+  // ---- the terms that matter to this call: InterPodAffinity for a pod P
+  // reads only the existing pods' terms that select P and P's own terms, so a
+  // term no pending candidate pod has or is selected by constrains nothing
+  // here (a prefix batch of 16 candidates keeps a handful of the snapshot's
+  // thousands of Deployment terms).  Kept terms are renumbered densely.
+  std::vector<Term> terms;
+  {
+    const int32_t T_all = static_cast<int32_t>(dict.size());
+    std::vector<Term> all(static_cast<size_t>(T_all));
+    for (int32_t t = 0; t < T_all; ++t) all[t] = parse_term(dict.data(t));
+    std::vector<uint8_t> keep(static_cast<size_t>(T_all), 0);
+    std::unordered_map<uint64_t, std::vector<int32_t>> idx;
+    std::vector<int32_t> unidx;
+    for (int32_t t = 0; t < T_all; ++t) {
+      if (all[t].nil) continue;
+      if (all[t].ml.empty()) unidx.push_back(t);
+      else idx[static_cast<uint64_t>(static_cast<uint32_t>(all[t].ml[0].first)) << 32 |
+               static_cast<uint32_t>(all[t].ml[0].second)].push_back(t);
+    }
+    for (int32_t i = 0; i < nc; ++i) {
+      if (status[i] != STATUS_PENDING) continue;
+      for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+        for (int32_t t : has[j - base]) keep[t] = 1;
+        const PodMeta m = meta_of(A, cands->cand_pods[j]);
+        for (int32_t t : unidx)
+          if (!keep[t] && term_selects(all[t], m)) keep[t] = 1;
+        for (int32_t l = 0; l < m.n; ++l) {
+          auto it = idx.find(static_cast<uint64_t>(static_cast<uint32_t>(m.key[l])) << 32 | static_cast<uint32_t>(m.val[l]));
+          if (it == idx.end()) continue;
+          for (int32_t t : it->second)
+            if (!keep[t] && term_selects(all[t], m)) keep[t] = 1;
+        }
+      }
+    }
+    std::vector<int32_t> nid(static_cast<size_t>(T_all), -1);
+    for (int32_t t = 0; t < T_all; ++t)
+      if (keep[t]) {
+        nid[t] = static_cast<int32_t>(terms.size());
+        terms.push_back(std::move(all[t]));
+      }
+    size_t w2 = 0;
+    for (const auto& nt : base_has)
+      if (nid[nt.second] >= 0) base_has[w2++] = {nt.first, nid[nt.second]};
+    base_has.resize(w2);
+    for (auto& h : has)
+      for (int32_t& t : h) t = nid[t];  // every term a pending pod has is kept
+  }
+  const int32_t T = static_cast<int32_t>(terms.size());
   if (T == 0) return;
   at.active = true;
   at.n_terms = T;
-  std::vector<Term> terms(static_cast<size_t>(T));
-  for (int32_t t = 0; t < T; ++t) terms[t] = parse_term(dict.data(t));
 
   // ---- topology keys (few distinct: hostname, zone, ...): each spot node's
   // value, the nodes of every value, node-local keys (every node carries the

@@ -951,7 +951,7 @@ void pod_affinity_row(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
 // node-local key whose minimum could move (no more nodes at the minimum than
 // the constraint counts pods of the candidate).
 void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
-                    std::vector<int32_t>& status, DomKeys* dk, SpreadDyn* out) {
+                    std::vector<int32_t>& status, DomKeys* dk, SpreadDyn* out, SpreadIndex& six) {
   SpreadDyn& sd = *out;
   sd = SpreadDyn{};
   const sr_spread* S = c->spread;
@@ -1044,7 +1044,7 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
         auto ci = counts.find(key_words);
         if (ci == counts.end()) {
           std::vector<int32_t> v;
-          spread_node_counts(snap, c, k, A->ns[pod], v);
+          spread_node_counts(six, c, k, A->ns[pod], v);
           ci = counts.emplace(key_words, std::move(v)).first;
         }
         const std::vector<int32_t>& cnt = ci->second;
@@ -1821,7 +1821,8 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   analyse_affinity(snap, c, cands, Wp, w->status_host, &dk, &aff);
   // ---- topology spread between the pods of one candidate (domain path)
   SpreadDyn sdyn;
-  analyse_spread(C, snap, c, cands, w->status_host, &dk, &sdyn);
+  SpreadIndex six(snap);  // spread rows: node values per key, snapshot pods per label (built lazily)
+  analyse_spread(C, snap, c, cands, w->status_host, &dk, &sdyn, six);
   auto spread_dm = [&](int32_t flat) -> int32_t { return sdyn.dmask.empty() ? 0 : sdyn.dmask[flat - sdyn.base]; };
   // affinity planned on the domain path: the pod's class carries KEYS(S), the
   // device the rest (an earlier pod of its candidate matches all its terms)
@@ -2565,7 +2566,7 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
       }
       for (int32_t x = 0; x < Wp; ++x) aff_row[x] &= any[x];
     }
-    spread_row(snap, sp.spread.data(), aff_row.data(), static_cast<uint32_t>(spread_query[q].second),
+    spread_row(six, sp.spread.data(), aff_row.data(), static_cast<uint32_t>(spread_query[q].second),
                A + static_cast<size_t>(A_SPREAD + q) * Wp);
   }
   for (int32_t t = 0; t < anti.n_terms; ++t) {

@@ -266,10 +266,41 @@ inline bool has_spread(const sr_cluster* c, int32_t pod) {
 bool spread_invalid(const sr_cluster* c, int32_t k);
 bool spread_selects(const sr_cluster* c, int32_t k, int32_t pod);
 void spread_words(const sr_cluster* c, int32_t pod, std::vector<int32_t>& out);
+// One encode's view of the snapshot for the spread rows (spread.cpp), built
+// lazily: per topology key the spot nodes' values and a node bitset per value,
+// and the snapshot pods per (label key, value), so a constraint with a
+// matchLabels pair counts only the pods carrying it (a Deployment's replicas)
+// instead of every snapshot pod.
+struct SpreadIndex {
+  struct KeyView {
+    std::vector<int32_t> val;     // [n_spot] the node's value (INT32_MIN: no such label)
+    std::vector<int32_t> values;  // distinct values
+    std::vector<uint64_t> bits;   // [values][Wp] nodes carrying each value
+    std::vector<uint64_t> has;    // [Wp] nodes carrying the key
+  };
+  explicit SpreadIndex(const sr_snapshot* s);
+  const KeyView& key(int32_t k);
+  // snapshot pods carrying label (k, v): (spot position, SnapPod index); null: none
+  const std::vector<std::pair<int32_t, int32_t>>* pods_with(int32_t k, int32_t v);
+  const sr_snapshot* snap;
+  int32_t n_spot, Wp;
+  std::unordered_map<int32_t, KeyView> keys;
+  // per label key (built on its first query: one pass over the snapshot pods'
+  // labels, then a counting sort by value id): CSR over the value ids
+  struct LabelCol {
+    std::vector<int32_t> off;                        // [max value id + 2]
+    std::vector<std::pair<int32_t, int32_t>> pods;   // (spot position, SnapPod index)
+  };
+  std::unordered_map<int32_t, LabelCol> by_key;
+  std::vector<std::pair<int32_t, int32_t>> scratch;  // pods_with's return view
+};
 // Constraints in `dmask` (bit k: the k-th) keep only their key check (SpreadDyn).
-void spread_row(const sr_snapshot* snap, const int32_t* words, const uint64_t* aff_row, uint32_t dmask, uint64_t* row);
+void spread_row(SpreadIndex& ix, const int32_t* words, const uint64_t* aff_row, uint32_t dmask, uint64_t* row);
+// The same by a scan of every snapshot pod (SR_SPREAD_CHECK=1 compares both).
+void spread_row_scan(const sr_snapshot* snap, const int32_t* words, const uint64_t* aff_row, uint32_t dmask,
+                     uint64_t* row);
 // Per spot node, the snapshot pods constraint k counts (namespace `ns`, not terminating, selected).
-void spread_node_counts(const sr_snapshot* snap, const sr_cluster* c, int32_t k, int32_t ns, std::vector<int32_t>& out);
+void spread_node_counts(SpreadIndex& ix, const sr_cluster* c, int32_t k, int32_t ns, std::vector<int32_t>& out);
 inline bool has_anti_terms(const sr_cluster* c, int32_t pod) {
   return (c->pods.flags[pod] & SR_POD_HAS_REQ_ANTI_AFFINITY) ||
          (c->pod_affinity && c->pod_affinity->anti_off[pod + 1] > c->pod_affinity->anti_off[pod]);

@@ -25,6 +25,8 @@
 // reference path.
 #include <algorithm>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <unordered_map>
 
 #include "host.hpp"
@@ -152,13 +154,83 @@ bool spread_selects(const sr_cluster* c, int32_t k, int32_t pod) {
   return true;
 }
 
-void spread_node_counts(const sr_snapshot* snap, const sr_cluster* c, int32_t k, int32_t ns, std::vector<int32_t>& out) {
+SpreadIndex::SpreadIndex(const sr_snapshot* s)
+    : snap(s), n_spot(static_cast<int32_t>(s->nodes.size())), Wp(std::max(2, ((n_spot + 63) / 64 + 1) & ~1)) {}
+
+const SpreadIndex::KeyView& SpreadIndex::key(int32_t k) {
+  auto it = keys.find(k);
+  if (it != keys.end()) return it->second;
+  KeyView& v = keys[k];
+  v.val.assign(static_cast<size_t>(n_spot), INT32_MIN);
+  v.has.assign(static_cast<size_t>(Wp), 0);
+  std::unordered_map<int32_t, int32_t> slot;
+  for (int32_t n = 0; n < n_spot; ++n)
+    for (const auto& kv : snap->nodes[n].labels)
+      if (kv.first == k) {
+        v.val[n] = kv.second;
+        v.has[n >> 6] |= 1ull << (n & 63);
+        auto ins = slot.emplace(kv.second, static_cast<int32_t>(v.values.size()));
+        if (ins.second) {
+          v.values.push_back(kv.second);
+          v.bits.resize(v.values.size() * static_cast<size_t>(Wp), 0);
+        }
+        v.bits[static_cast<size_t>(ins.first->second) * Wp + (n >> 6)] |= 1ull << (n & 63);
+      }
+  return v;
+}
+
+const std::vector<std::pair<int32_t, int32_t>>* SpreadIndex::pods_with(int32_t k, int32_t v) {
+  auto it = by_key.find(k);
+  if (it == by_key.end()) {  // the label column of key k: (value, node, pod), counting-sorted by value
+    LabelCol& col = by_key[k];
+    std::vector<int32_t> vals;
+    std::vector<std::pair<int32_t, int32_t>> at;
+    int32_t vmax = -1;
+    for (int32_t n = 0; n < n_spot; ++n)
+      for (int32_t e : snap->state[n].pods) {
+        const SnapPod& sp = snap->pods[e];
+        for (uint32_t i = 0; i < sp.nlab; ++i)
+          if (snap->lkey[sp.lab + i] == k && snap->lval[sp.lab + i] >= 0) {
+            vals.push_back(snap->lval[sp.lab + i]);
+            at.emplace_back(n, e);
+            vmax = std::max(vmax, snap->lval[sp.lab + i]);
+            break;  // keys are unique per pod
+          }
+      }
+    col.off.assign(static_cast<size_t>(vmax) + 2, 0);
+    for (int32_t x : vals) ++col.off[static_cast<size_t>(x) + 1];
+    for (size_t i = 1; i < col.off.size(); ++i) col.off[i] += col.off[i - 1];
+    col.pods.resize(at.size());
+    std::vector<int32_t> fill(col.off.begin(), col.off.end() - 1);
+    for (size_t i = 0; i < at.size(); ++i) col.pods[static_cast<size_t>(fill[vals[i]]++)] = at[i];
+    it = by_key.find(k);
+  }
+  const LabelCol& col = it->second;
+  if (v < 0 || static_cast<size_t>(v) + 1 >= col.off.size() || col.off[v] == col.off[v + 1]) return nullptr;
+  scratch.assign(col.pods.begin() + col.off[v], col.pods.begin() + col.off[v + 1]);
+  return &scratch;
+}
+
+void spread_node_counts(SpreadIndex& ix, const sr_cluster* c, int32_t k, int32_t ns, std::vector<int32_t>& out) {
+  const sr_snapshot* snap = ix.snap;
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
   const sr_spread* S = c->spread;
   out.assign(static_cast<size_t>(n_spot), 0);
   if (S->selector_nil[k]) return;
-  for (int32_t n = 0; n < n_spot; ++n)
-    for (int32_t e : snap->state[n].pods) {
+  // a matchLabels pair bounds the pods to test: those carrying it
+  std::vector<std::pair<int32_t, int32_t>> all;
+  const std::vector<std::pair<int32_t, int32_t>>* list = nullptr;
+  if (S->ml_off[k + 1] > S->ml_off[k]) {
+    list = ix.pods_with(S->ml_key[S->ml_off[k]], S->ml_val[S->ml_off[k]]);
+    if (!list) return;
+  } else {
+    for (int32_t n = 0; n < n_spot; ++n)
+      for (int32_t e : snap->state[n].pods) all.emplace_back(n, e);
+    list = &all;
+  }
+  for (const auto& ne : *list) {
+    const int32_t n = ne.first, e = ne.second;
+    {
       const SnapPod& sp = snap->pods[e];
       if (sp.term || sp.ns != ns) continue;
       const int32_t *lk = snap->lkey.data() + sp.lab, *lv = snap->lval.data() + sp.lab;
@@ -188,6 +260,7 @@ void spread_node_counts(const sr_snapshot* snap, const sr_cluster* c, int32_t k,
       }
       if (ok) ++out[n];
     }
+  }
 }
 
 void spread_words(const sr_cluster* c, int32_t pod, std::vector<int32_t>& out) {
@@ -225,7 +298,108 @@ void spread_words(const sr_cluster* c, int32_t pod, std::vector<int32_t>& out) {
   }
 }
 
-void spread_row(const sr_snapshot* snap, const int32_t* w, const uint64_t* aff_row, uint32_t dmask, uint64_t* row) {
+void spread_row(SpreadIndex& ix, const int32_t* w, const uint64_t* aff_row, uint32_t dmask, uint64_t* row) {
+  const sr_snapshot* snap = ix.snap;
+  const int32_t n_spot = ix.n_spot, Wp = ix.Wp;  // the encoder's row width (KeyView strides)
+  const int32_t ns = w[0], nk = w[1];
+  std::vector<Constraint> cs(static_cast<size_t>(nk));
+  const int32_t* p = w + 2;
+  for (int32_t k = 0; k < nk; ++k) p = parse(p, &cs[k]);
+  std::vector<const SpreadIndex::KeyView*> kv(static_cast<size_t>(nk));
+  for (int32_t k = 0; k < nk; ++k) kv[k] = &ix.key(cs[k].key);
+  // PreFilter: the nodes passing NodeAffinity and carrying every key define
+  // the pairs; none at all -> Filter passes every node
+  std::vector<uint64_t> elig(aff_row, aff_row + Wp);
+  for (int32_t k = 0; k < nk; ++k)
+    for (int32_t i = 0; i < Wp; ++i) elig[i] &= kv[k]->has[i];
+  bool any = false;
+  for (int32_t i = 0; i < Wp && !any; ++i) any = elig[i] != 0;
+  if (!any) {
+    for (int32_t n = 0; n < n_spot; ++n) row[n >> 6] |= 1ull << (n & 63);
+    return;
+  }
+  // per constraint, per value of its key: the pair exists, its count (two
+  // constraints on one key add into the same pairs: counted by key below)
+  std::unordered_map<int32_t, std::vector<int64_t>> count;  // key -> per value (-1: no such pair)
+  for (int32_t k = 0; k < nk; ++k) {
+    auto ins = count.emplace(cs[k].key, std::vector<int64_t>());
+    if (!ins.second) continue;
+    const SpreadIndex::KeyView& v = *kv[k];
+    ins.first->second.assign(v.values.size(), -1);
+    for (size_t j = 0; j < v.values.size(); ++j)
+      for (int32_t i = 0; i < Wp; ++i)
+        if (v.bits[j * Wp + i] & elig[i]) {
+          ins.first->second[j] = 0;
+          break;
+        }
+  }
+  // processNode: every selected pod, every constraint, the pair of its node's
+  // value ("" when the node lacks the key)
+  auto value_slot = [&](const SpreadIndex::KeyView& v, int32_t n) -> int32_t {
+    const int32_t x = v.val[n] == INT32_MIN ? snap->id_empty : v.val[n];
+    for (size_t j = 0; j < v.values.size(); ++j)
+      if (v.values[j] == x) return static_cast<int32_t>(j);
+    return -1;
+  };
+  std::vector<std::pair<int32_t, int32_t>> all;
+  for (int32_t k = 0; k < nk; ++k) {
+    const Constraint& ck = cs[k];
+    if (ck.nil) continue;
+    const std::vector<std::pair<int32_t, int32_t>>* list;
+    if (ck.n_ml > 0) {
+      list = ix.pods_with(ck.ml[0], ck.ml[1]);
+      if (!list) continue;
+    } else {
+      if (all.empty())
+        for (int32_t n = 0; n < n_spot; ++n)
+          for (int32_t e : snap->state[n].pods) all.emplace_back(n, e);
+      list = &all;
+    }
+    std::vector<int64_t>& cnt = count[ck.key];
+    for (const auto& ne : *list) {
+      const SnapPod& sp = snap->pods[ne.second];
+      if (sp.term || sp.ns != ns) continue;  // terminating (unknown: planned on the reference path)
+      if (!selects(ck, snap->lkey.data() + sp.lab, snap->lval.data() + sp.lab, static_cast<int32_t>(sp.nlab))) continue;
+      const int32_t j = value_slot(*kv[k], ne.first);
+      if (j >= 0 && cnt[j] >= 0) ++cnt[j];
+    }
+  }
+  // Filter per node: row = AND over the constraints of the nodes carrying a
+  // value whose pair count (0 without a pair) + self - the key's minimum is
+  // within maxSkew (a device-planned constraint: the key check only)
+  std::vector<uint64_t> acc(static_cast<size_t>(Wp), ~0ull), part(static_cast<size_t>(Wp));
+  for (int32_t k = 0; k < nk; ++k) {
+    const SpreadIndex::KeyView& v = *kv[k];
+    if ((dmask >> k) & 1) {
+      for (int32_t i = 0; i < Wp; ++i) acc[i] &= v.has[i];
+      continue;
+    }
+    const std::vector<int64_t>& cnt = count[cs[k].key];
+    int64_t mn = INT64_MAX;  // TpKeyToCriticalPaths[key][0].MatchNum: the minimum over the key's pairs
+    for (int64_t x : cnt)
+      if (x >= 0) mn = std::min(mn, x);
+    std::fill(part.begin(), part.end(), 0ull);
+    for (size_t j = 0; j < v.values.size(); ++j) {
+      const int64_t match = cnt[j] < 0 ? 0 : cnt[j];
+      if (match + cs[k].self - mn <= cs[k].max_skew)
+        for (int32_t i = 0; i < Wp; ++i) part[i] |= v.bits[j * Wp + i];
+    }
+    for (int32_t i = 0; i < Wp; ++i) acc[i] &= part[i];
+  }
+  for (int32_t i = 0; i < Wp; ++i) row[i] |= acc[i];
+  if (std::getenv("SR_SPREAD_CHECK")) {  // debug: the scan must agree
+    std::vector<uint64_t> r2(static_cast<size_t>(Wp), 0);
+    spread_row_scan(snap, w, aff_row, dmask, r2.data());
+    for (int32_t i = 0; i < Wp; ++i)
+      if (r2[i] != acc[i]) {
+        std::fprintf(stderr, "spread_row: indexed row differs from the scan at word %d\n", i);
+        std::abort();
+      }
+  }
+}
+
+void spread_row_scan(const sr_snapshot* snap, const int32_t* w, const uint64_t* aff_row, uint32_t dmask,
+                     uint64_t* row) {
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
   const int32_t ns = w[0], nk = w[1];
   std::vector<Constraint> cs(static_cast<size_t>(nk));

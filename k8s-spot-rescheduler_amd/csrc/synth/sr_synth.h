@@ -26,6 +26,13 @@ typedef struct {
                                its PV in the pod's zone (zone label + node affinity), CSINode count 25 per node */
   double init_fraction;     /* share of pods with an init container (fit request != AddPod accounting) */
   double gpu_fraction;      /* share of pods on GPU nodes (1 in 8 nodes, 4 nvidia.com/gpu) asking for one GPU */
+  /* "affinity" variant (both 0 = none): every pod belongs to a Deployment (label app=<name>, one of 16
+   * namespaces; ~5 replicas per Deployment, spot and on-demand alike, never two replicas of an anti-affinity
+   * Deployment on one node); a share of the Deployments carries required pod anti-affinity on the hostname
+   * key, another share a zone DoNotSchedule topology spread constraint (maxSkew 1), both selecting their own
+   * replicas.  Drawn from a separate stream: the cluster is otherwise the config's. */
+  double anti_fraction;     /* share of Deployments with hostname anti-affinity */
+  double spread_fraction;   /* share of Deployments with a zone DoNotSchedule spread constraint */
 } sr_synth_params;
 
 typedef struct sr_synth sr_synth;

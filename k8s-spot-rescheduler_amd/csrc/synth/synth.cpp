@@ -65,6 +65,16 @@ struct sr_synth {
   std::vector<int32_t> v_field_key, v_field_op, v_field_val_off{0}, v_field_vals;
   int32_t zone_keys[4] = {-1, -1, -1, -1};
   mutable sr_volumes vview{};  // the sr_volumes of sr_synth_view
+  // affinity variant (sr_synth_params.anti_fraction / spread_fraction)
+  bool has_affinity = false;
+  std::vector<int32_t> a_ns, a_label_off{0}, a_label_key, a_label_val, a_anti_off{0};
+  std::vector<int32_t> a_topo, a_ns_off{0}, a_ml_off{0}, a_ml_key, a_ml_val, a_me_off{0};
+  std::vector<uint8_t> a_sel_nil;
+  std::vector<int32_t> s_off{0}, s_skew, s_topo, s_ml_off{0}, s_ml_key, s_ml_val, s_me_off{0};
+  std::vector<uint8_t> s_sel_nil, s_term;
+  std::vector<int32_t> a_none{0};  // the empty tables' non-null base
+  mutable sr_pod_affinity aview{};
+  mutable sr_spread sview{};
   std::vector<uint64_t> stamp;  // sr_cluster.pod_stamp: pods never change after generation
 
   int32_t id(const std::string& s) {
@@ -160,6 +170,8 @@ struct PodSpec {
   int32_t zone = -1;                   // ... its PV's zone value
   int32_t prio = 0;
   uint32_t flags = 0;
+  int32_t ns = -1, app = -1;  // affinity variant: namespace and app label
+  bool anti = false, spread = false;
   std::vector<std::pair<int32_t, int32_t>> sel;
   bool aff = false;
   struct Expr {
@@ -245,6 +257,33 @@ void push_pod(sr_synth* s, int32_t node, const PodSpec& p) {
     s->port_ip.push_back(q.ip);
   }
   s->port_off.push_back(static_cast<int32_t>(s->port_proto.size()));
+  if (s->has_affinity) {  // namespace, app label; the Deployment's anti-affinity term / spread constraint
+    s->a_ns.push_back(p.ns);
+    s->a_label_key.push_back(s->id("app"));
+    s->a_label_val.push_back(p.app);
+    s->a_label_off.push_back(static_cast<int32_t>(s->a_label_key.size()));
+    if (p.anti) {  // podAntiAffinity required: topologyKey hostname, matchLabels app=<name>
+      s->a_topo.push_back(s->id("kubernetes.io/hostname"));
+      s->a_ns_off.push_back(static_cast<int32_t>(s->a_ns_off.back()));
+      s->a_sel_nil.push_back(0);
+      s->a_ml_key.push_back(s->id("app"));
+      s->a_ml_val.push_back(p.app);
+      s->a_ml_off.push_back(static_cast<int32_t>(s->a_ml_key.size()));
+      s->a_me_off.push_back(s->a_me_off.back());
+    }
+    s->a_anti_off.push_back(static_cast<int32_t>(s->a_topo.size()));
+    if (p.spread) {  // topologySpreadConstraints: maxSkew 1, zone, DoNotSchedule, matchLabels app=<name>
+      s->s_skew.push_back(1);
+      s->s_topo.push_back(s->id("topology.kubernetes.io/zone"));
+      s->s_sel_nil.push_back(0);
+      s->s_ml_key.push_back(s->id("app"));
+      s->s_ml_val.push_back(p.app);
+      s->s_ml_off.push_back(static_cast<int32_t>(s->s_ml_key.size()));
+      s->s_me_off.push_back(s->s_me_off.back());
+    }
+    s->s_off.push_back(static_cast<int32_t>(s->s_skew.size()));
+    s->s_term.push_back(0);
+  }
   s->drain_flags.push_back((p.flags & SR_POD_DAEMONSET_CONTROLLER) ? SR_DRAIN_CTRL_DAEMONSET : SR_DRAIN_CTRL_REPLICASET);
   s->phase.push_back(SR_PHASE_RUNNING);
   s->restart.push_back(SR_RESTART_ALWAYS);
@@ -287,6 +326,36 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
   s->od = sr_node_label{ROLE, WORKER, 1};
   s->spot = sr_node_label{ROLE, SPOTW, 1};
   s->has_volumes = f_stateful > 0;
+  const double f_anti = prm ? prm->anti_fraction : 0, f_spread = prm ? prm->spread_fraction : 0;
+  s->has_affinity = f_anti > 0 || f_spread > 0;
+  // affinity variant: Deployments of ~5 replicas, their kinds and replicas
+  // drawn from their own stream (the rest of the cluster is unchanged)
+  Rng arng{(prm && prm->seed ? prm->seed : 0x5EED0000ull + static_cast<uint64_t>(config)) ^ 0xAFF1A17Eull};
+  const int64_t n_deploy = std::max<int64_t>(1, (static_cast<int64_t>(cfg.n_od + cfg.n_spot) * 30) / 5);
+  int32_t ns_ids[16];
+  if (s->has_affinity)
+    for (int i = 0; i < 16; ++i) ns_ids[i] = s->id("ns-" + std::to_string(i));
+  auto deploy_kind = [&](int64_t d) {  // 0 none, 1 anti-affinity, 2 spread (a hash of d: stable)
+    const double u = static_cast<double>((static_cast<uint64_t>(d) * 0x9E3779B97F4A7C15ull) >> 11) *
+                     (1.0 / 9007199254740992.0);
+    return u < f_anti ? 1 : u < f_anti + f_spread ? 2 : 0;
+  };
+  std::vector<int64_t> node_anti;  // the anti-affinity Deployments with a replica on the current node
+  auto assign_deploy = [&](PodSpec& p) {
+    if (!s->has_affinity) return;
+    int64_t d = static_cast<int64_t>(arng.next() % static_cast<uint64_t>(n_deploy));
+    for (int t = 0; t < 8 && deploy_kind(d) == 1 &&
+                    std::find(node_anti.begin(), node_anti.end(), d) != node_anti.end(); ++t)
+      d = static_cast<int64_t>(arng.next() % static_cast<uint64_t>(n_deploy));
+    int kind = deploy_kind(d);
+    if (kind == 1 && std::find(node_anti.begin(), node_anti.end(), d) != node_anti.end()) kind = -1;  // none
+    if (kind == 1) node_anti.push_back(d);
+    p.ns = ns_ids[d % 16];
+    p.app = s->id(kind < 0 ? "solo-" + std::to_string(s->pod_node.size()) : "app-" + std::to_string(d));
+    p.anti = kind == 1;
+    p.spread = kind == 2;
+    if (p.anti) p.flags |= SR_POD_HAS_REQ_ANTI_AFFINITY;
+  };
   s->has_scalars = f_gpu > 0;
   s->has_acc = f_init > 0;
   if (s->has_volumes) {
@@ -367,8 +436,13 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
     }
     s->v_limit_off.push_back(static_cast<int32_t>(s->v_limit_key.size()));
 
+    node_anti.clear();
     // DaemonSet pod first in the node's list
     PodSpec ds;
+    if (s->has_affinity) {
+      ds.ns = s->id("kube-system");
+      ds.app = s->id("node-exporter");
+    }
     ds.cpu = 100;
     ds.mem = 128 * kMi;
     ds.flags = SR_POD_DAEMONSET_CONTROLLER;
@@ -440,6 +514,7 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
         p.volume = s->id(buf);
         p.zone = node_zone;
       }
+      assign_deploy(p);
       if (cfg.ports && rng.chance(0.30)) {
         static const int32_t kPorts[3] = {80, 443, 8080};
         const int32_t port = kPorts[rng.below(3)];
@@ -470,6 +545,11 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
         PodSpec p;
         p.cpu = 50;
         p.mem = 64 * kMi;
+        if (s->has_affinity) {
+          node_anti.clear();  // (a filler pod never joins an anti-affinity Deployment)
+          p.ns = ns_ids[node % 16];
+          p.app = s->id("filler-" + std::to_string(node));
+        }
         push_pod(s, node, p);
         node_used[node] += 50;
         ++node_pods[node];
@@ -494,7 +574,9 @@ sr_synth* sr_synth_generate(const sr_synth_params* prm) {
     fold(prm->seed);
     fold(static_cast<uint64_t>(prm->n_on_demand));
     fold(static_cast<uint64_t>(prm->n_spot));
-    for (double d : {prm->pinned_fraction, prm->stateful_fraction, prm->init_fraction, prm->gpu_fraction}) fold(bits(d));
+    for (double d : {prm->pinned_fraction, prm->stateful_fraction, prm->init_fraction, prm->gpu_fraction,
+                     prm->anti_fraction, prm->spread_fraction})
+      fold(bits(d));
   }
   s->stamp.resize(s->pod_node.size());
   for (size_t i = 0; i < s->stamp.size(); ++i) {
@@ -574,6 +656,39 @@ void sr_synth_view(const sr_synth* s, sr_cluster* c) {
   c->spread = nullptr;  // no topology spread constraints in the BASELINE configs
   c->volumes = nullptr;  // realistic variant only (sr_synth_params.stateful_fraction)
   c->pod_stamp = s->stamp.data();
+  if (s->has_affinity) {
+    sr_pod_affinity& a = s->aview;
+    a = sr_pod_affinity{};
+    a.ns = s->a_ns.data();
+    a.label_off = s->a_label_off.data();
+    a.label_key = s->a_label_key.data();
+    a.label_val = s->a_label_val.data();
+    a.anti_off = s->a_anti_off.data();
+    a.topology_key = s->a_topo.data();
+    a.ns_off = s->a_ns_off.data();
+    a.ns_ids = s->a_none.data();
+    a.selector_nil = s->a_sel_nil.data();
+    a.ml_off = s->a_ml_off.data();
+    a.ml_key = s->a_ml_key.data();
+    a.ml_val = s->a_ml_val.data();
+    a.me_off = s->a_me_off.data();
+    a.me_key = a.me_op = a.me_val_off = a.me_vals = s->a_none.data();
+    a.aff_off = nullptr;
+    c->pod_affinity = &a;
+    sr_spread& sp = s->sview;
+    sp = sr_spread{};
+    sp.off = s->s_off.data();
+    sp.max_skew = s->s_skew.data();
+    sp.topology_key = s->s_topo.data();
+    sp.selector_nil = s->s_sel_nil.data();
+    sp.ml_off = s->s_ml_off.data();
+    sp.ml_key = s->s_ml_key.data();
+    sp.ml_val = s->s_ml_val.data();
+    sp.me_off = s->s_me_off.data();
+    sp.me_key = sp.me_op = sp.me_val_off = sp.me_vals = s->a_none.data();
+    sp.terminating = s->s_term.data();
+    c->spread = &sp;
+  }
   if (s->has_acc) {
     c->acc_milli_cpu = s->acc_cpu.data();
     c->acc_memory = s->acc_mem.data();

@@ -17,12 +17,17 @@ class sr_synth_params(ctypes.Structure):
     _fields_ = [("config", ctypes.c_int32), ("seed", ctypes.c_uint64), ("n_on_demand", ctypes.c_int32),
                 ("n_spot", ctypes.c_int32), ("pinned_fraction", ctypes.c_double),
                 ("stateful_fraction", ctypes.c_double), ("init_fraction", ctypes.c_double),
-                ("gpu_fraction", ctypes.c_double)]
+                ("gpu_fraction", ctypes.c_double), ("anti_fraction", ctypes.c_double),
+                ("spread_fraction", ctypes.c_double)]
 
 
 # The "realistic" variant of a config (bench --variant realistic): StatefulSet
 # pods with zonal EBS CSI claims, init containers, GPU pods on GPU nodes.
 REALISTIC = dict(stateful_fraction=0.15, init_fraction=0.2, gpu_fraction=0.3)
+# The "affinity" variant (bench --variant affinity): every pod in a Deployment,
+# 10 % of the Deployments with required hostname anti-affinity, 10 % with a
+# zone DoNotSchedule topology spread constraint (their spot replicas included).
+AFFINITY = dict(anti_fraction=0.10, spread_fraction=0.10)
 
 
 _synth = None
@@ -59,10 +64,10 @@ def synth_label_flags(s: str) -> int:
 class SynthCluster:
     def __init__(self, config: int, seed: int = 0, n_on_demand: int = 0, n_spot: int = 0,
                  pinned_fraction: float = -1.0, stateful_fraction: float = 0.0, init_fraction: float = 0.0,
-                 gpu_fraction: float = 0.0):
+                 gpu_fraction: float = 0.0, anti_fraction: float = 0.0, spread_fraction: float = 0.0):
         self.lib = load_synth()
         p = sr_synth_params(config, seed, n_on_demand, n_spot, pinned_fraction, stateful_fraction, init_fraction,
-                            gpu_fraction)
+                            gpu_fraction, anti_fraction, spread_fraction)
         self.handle = self.lib.sr_synth_generate(ctypes.byref(p))
         self.cluster = capi.sr_cluster()
         self.lib.sr_synth_view(self.handle, ctypes.byref(self.cluster))

@@ -661,3 +661,16 @@ def test_synthetic_config3_realistic_plans_match_oracle(checker, podorder_checke
     c = checker if mode == "node_order" else podorder_checker
     o, p = tick_parity(c, SynthCluster(3, **REALISTIC), oracle_threads=16)
     assert p.checks > 0
+
+
+@pytest.mark.parametrize("mode", ["node_order", "pod_order"])
+def test_synthetic_config3_affinity_plans_match_oracle(checker, podorder_checker, mode):
+    # bench --variant affinity at full C3 size: every pod in a Deployment, 10 %
+    # of them with required hostname anti-affinity (spot replicas included), 10 %
+    # with a zone DoNotSchedule spread constraint -- state-bit pairs, the domain
+    # path for replicas that count each other, and the pruned term set
+    from spotplanner.synth import AFFINITY
+    c = checker if mode == "node_order" else podorder_checker
+    o, p = tick_parity(c, SynthCluster(3, **AFFINITY), oracle_threads=16)
+    assert p.checks > 0
+

@@ -87,9 +87,14 @@ def test_plan_first_matches_reference_loop(checker, small_batch_checker, seed, w
         capi.load_planner().sr_snapshot_destroy(h)
 
 
-@pytest.mark.parametrize("config", [1, 2, 3, 5])
-def test_plan_first_synthetic_configs(checker, small_batch_checker, config):
-    sc = SynthCluster(config)
+@pytest.mark.parametrize("config,variant", [(1, None), (2, None), (3, None), (5, None), (3, "realistic"),
+                                            (3, "affinity")])
+def test_plan_first_synthetic_configs(checker, small_batch_checker, config, variant):
+    # the variants: extension records on the node-order kernel (realistic), and
+    # each prefix batch keeping only the anti-affinity terms its candidates have
+    # or are selected by, with zone-spread replicas on the domain path (affinity)
+    from spotplanner.synth import AFFINITY, REALISTIC
+    sc = SynthCluster(config, **{"realistic": REALISTIC, "affinity": AFFINITY}.get(variant, {}))
     lib = capi.load_planner()
     nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
     cand_off, cand_pods = build_candidates(nm, sc.pod_flags())

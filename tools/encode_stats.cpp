@@ -41,6 +41,11 @@ int main(int argc, char** argv) {
     p.init_fraction = 0.2;
     p.gpu_fraction = 0.3;
   }
+  const bool affinity = std::getenv("SR_SYNTH_AFFINITY") != nullptr;
+  if (affinity) {  // bench --variant affinity (spotplanner/synth.py AFFINITY)
+    p.anti_fraction = 0.10;
+    p.spread_fraction = 0.10;
+  }
   sr_synth* s = sr_synth_generate(&p);
   sr_cluster c;
   sr_synth_view(s, &c);
@@ -243,7 +248,7 @@ int main(int argc, char** argv) {
       // encoder as it was before this call: its class and atom numbering
       // depends on the dictionaries' history (scalar and volume queries)
       std::unique_ptr<sr::EncoderCache> twin;
-      if (realistic) twin.reset(new sr::EncoderCache(cache));
+      if (realistic || affinity) twin.reset(new sr::EncoderCache(cache));
       t0 = std::chrono::steady_clock::now();
       if (sr::encode_workload(&cache, s2, &c, &cands, &w, &err) != SR_OK) return 1;
       const double ms = ms_since(t0);
