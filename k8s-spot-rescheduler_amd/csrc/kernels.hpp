@@ -23,6 +23,10 @@ constexpr int kPodPatchU64 = 3;         // pod patch: {active pod, pod_rec[4], p
 constexpr int64_t kTPad = INT64_MAX - 1;  // threshold of a spare T row (no pod points at it; K0 skips it)
 constexpr int kDevDynTerms = 4;         // terms per domain-path affinity set (host.hpp kDynTerms)
 constexpr int kDevExtU64 = 8;           // extension record words (host.hpp kExtU64)
+#ifndef SR_LIST_INLINE
+#define SR_LIST_INLINE 128
+#endif
+constexpr int kListInline = SR_LIST_INLINE;  // work-list entries also carried in the kernel arguments
 
 // Pointers into the device arena (layout: DESIGN.md §HBM layout).
 struct DevWorkload {
@@ -92,7 +96,9 @@ struct DevWorkload {
                              //  slot 0, of slot 1 (-1: no slot), 0}
   // outputs / scratch
   uint64_t* S;         // [n_classes][Wp] static-class rows, followed by
-  uint64_t* T;         // [n_t][Wp] capacity threshold rows (one table)
+  uint64_t* T;         // [n_t][Wp] capacity threshold rows (one table), followed by
+  uint64_t* pod_head;  // [n_pods + 128][16] per pod its F row head (S & T & T & T, words [0, 8)) and S row
+                       // head, written by K0b after every K0 run (null: K2 ANDs the row heads itself)
   int32_t* out_node;   // [n_pods] spot position or -1
   int32_t* out_status; // [n_cand]
   uint32_t* out_bytes; // [n_cand] bytes K2 moved for the candidate (the roofline's algorithmic bytes)
@@ -116,6 +122,11 @@ struct DevWorkload {
                        // 1: pod order everywhere (SR_K2_MODE=1, A/B measurement)
   uint64_t* prof;      // optional [n_cand][16] K2 + [kK0ProfWaves][2] K0 per-wave profile
                        // (SR_K2_PROFILE), else null
+  // the first kListInline work-list entries (the longest candidates, whose
+  // chains set K2's time): a wave li < n_list_head reads its entry with the
+  // other kernel arguments instead of one memory round trip later
+  int32_t n_list_head;
+  int4 list_head[kListInline > 0 ? kListInline : 1];
 };
 
 // K0: S and T rows (also resets d_min: d_min[1] = local first fallback).
@@ -124,6 +135,8 @@ hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hip
                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // K2: per-candidate feasibility rows + first-fit placement; atomicMin of first_ok into d_min[0].
 hipError_t launch_placement(const DevWorkload& w, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// K0b: every pod's F and S row heads into pod_head (after K0; its events: ev1 only).
+hipError_t launch_heads(const DevWorkload& w, hipStream_t s, hipEvent_t ev1 = nullptr);
 // K3: winner mapping into `result` (after the collective when ranks > 1), then the run's seq.
 // Not launched when K2 writes res_stat / res_map itself (single rank).
 hipError_t launch_winner(const DevWorkload& w, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);

@@ -121,6 +121,7 @@ struct sr_ctx {
   std::vector<uint64_t> pod_patch_words;   // this call's pod patches (prepare)
   int32_t k0_incremental = 1;  // SR_K0_INCREMENTAL=0: K0 always rewrites every row
   int32_t k0_skip = 1;         // SR_K0_SKIP=0: every run launches K0
+  int32_t pod_heads = 1;       // SR_POD_HEADS=0: no K0b, K2 ANDs the row heads itself
   uint64_t run_count = 0;      // runs of this context: d_min alternates between two buffers
   bool dmin_ready[2] = {false, false};  // buffer reset by the previous run's K2 (a K0-less run needs it)
   sr::EncoderCache enc;      // what the encoder keeps across calls (encode.cpp)
@@ -446,7 +447,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
   const size_t t_cap = sl.tables.cap;
-  HIP_TRY(ctx, dev_reserve(sl.tables, n_rows * row_bytes));
+  // the pod heads (K0b) after the rows
+  const size_t head_bytes = ctx->pod_heads ? (static_cast<size_t>(na) + 128) * 16 * sizeof(uint64_t) : 0;
+  HIP_TRY(ctx, dev_reserve(sl.tables, n_rows * row_bytes + head_bytes));
   if (sl.tables.cap != t_cap) {  // a new allocation holds no rows: every row below
     sl.tables_cand_gen = ~0ull;
     skip = false;
@@ -543,6 +546,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.cand_global = static_cast<const int32_t*>(at(o_cg));
   d.list = static_cast<const int4*>(at(o_ls));
   d.n_list = static_cast<int32_t>(w.list.size() / 4);
+  d.n_list_head = std::min(d.n_list, sr::kListInline);
+  for (int32_t i = 0; i < d.n_list_head; ++i)
+    d.list_head[i] = int4{w.list[4 * i], w.list[4 * i + 1], w.list[4 * i + 2], w.list[4 * i + 3]};
   d.max_np = w.max_cand_pods;
   d.dyn_cand = dyn ? static_cast<const int32_t*>(at(o_dc)) : nullptr;
   d.dyn_pod = dyn ? static_cast<const uint64_t*>(at(o_dp)) : nullptr;
@@ -561,6 +567,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   for (int k = 0; k < sr::kDomKeys; ++k) d.dk_row[k] = w.dk_row[k];
   d.S = static_cast<uint64_t*>(sl.tables.p);
   d.T = d.S + static_cast<size_t>(w.n_classes) * w.Wp;
+  d.pod_head = ctx->pod_heads && ctx->k2_mode == 0 ? d.T + w.t_dim.size() * static_cast<size_t>(w.Wp) : nullptr;
   d.out_node = static_cast<int32_t*>(ctx->out_node.p);
   d.out_status = static_cast<int32_t*>(ctx->out_status.p);
   d.out_bytes = static_cast<uint32_t*>(ctx->out_bytes.p);
@@ -804,7 +811,8 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     if (!ctx->dmin_ready[par])  // no K2 of a previous run reset it: reset here
       HIP_TRY(ctx, hipMemsetAsync(d.d_min, 0xff, sizeof(uint64_t), s));
   } else {
-    HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
+    HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, d.pod_head ? nullptr : e0b));
+    if (d.pod_head) HIP_TRY(ctx, sr::launch_heads(d, s, e0b));  // K0b: the pod heads of the rows K0 wrote
     if (sl.commit_k0) {  // K0 wrote the node and pod patches and brought the rows to this workload (a rerun:
       sl.commit_k0 = false;  // idempotent)
       sl.tables_cand_gen = w.cand_gen;
@@ -978,6 +986,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_PLAN_SLOTS")) ctx->n_slots = std::max(1, std::min(16, std::atoi(m)));
   if (const char* m = std::getenv("SR_K0_INCREMENTAL")) ctx->k0_incremental = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K0_SKIP")) ctx->k0_skip = std::atoi(m) != 0;
+  if (const char* m = std::getenv("SR_POD_HEADS")) ctx->pod_heads = std::atoi(m) != 0;
   *out = ctx;
   return SR_OK;
 }
