@@ -34,6 +34,7 @@
 #include <climits>
 #include <cstring>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "host.hpp"
 #include "pool.hpp"
@@ -226,13 +227,45 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
   WordDict dict;
   std::vector<int32_t> words;
   std::vector<std::pair<int32_t, int32_t>> base_has;  // (node, term)
-  for (int32_t n = 0; n < n_spot; ++n)
-    for (int32_t e : snap->state[n].pods) {
-      const SnapPod& sp = snap->pods[e];
-      const int32_t* tw = snap->term_words.data() + sp.terms;
-      for (size_t i = 0; i < sp.nterms; i += 1 + static_cast<size_t>(tw[i]))
-        base_has.emplace_back(n, dict.intern(tw + i + 1, static_cast<size_t>(tw[i])));
+  // A base pod's term matters here only when it selects some pending
+  // candidate pod (its DA row), so a term whose first matchLabels pair no
+  // pending pod carries is not even interned; nil selectors select nothing.
+  // The snapshot's pods are scanned in parallel, the kept terms interned in
+  // node order.
+  std::unordered_set<uint64_t> cand_labels;
+  for (int32_t i = 0; i < nc; ++i) {
+    if (status[i] != STATUS_PENDING) continue;
+    for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
+      const int32_t pod = cands->cand_pods[j];
+      for (int32_t l = A.label_off[pod]; l < A.label_off[pod + 1]; ++l)
+        cand_labels.insert(static_cast<uint64_t>(static_cast<uint32_t>(A.label_key[l])) << 32 |
+                           static_cast<uint32_t>(A.label_val[l]));
     }
+  }
+  {
+    constexpr int32_t kNodes = 256;
+    const size_t n_parts = (static_cast<size_t>(n_spot) + kNodes - 1) / kNodes;
+    std::vector<std::vector<std::pair<int32_t, const int32_t*>>> part(n_parts);  // (node, term words)
+    parallel_for(n_parts, 1, [&](size_t lo, size_t hi) {
+      for (size_t ch = lo; ch < hi; ++ch)
+        for (int32_t n = static_cast<int32_t>(ch) * kNodes; n < std::min<int32_t>(n_spot, (ch + 1) * kNodes); ++n)
+          for (int32_t e : snap->state[n].pods) {
+            const SnapPod& sp = snap->pods[e];
+            const int32_t* tw = snap->term_words.data() + sp.terms;
+            for (size_t i = 0; i < sp.nterms; i += 1 + static_cast<size_t>(tw[i])) {
+              const int32_t* w = tw + i + 1;  // {tk, n ns, ns..., nil, n ml, (k, v)...}
+              const int32_t* p = w + 2 + w[1];
+              if (p[0] != 0) continue;  // nil: selects nothing
+              if (p[1] > 0 && !cand_labels.count(static_cast<uint64_t>(static_cast<uint32_t>(p[2])) << 32 |
+                                                 static_cast<uint32_t>(p[3])))
+                continue;
+              part[ch].emplace_back(n, tw + i);
+            }
+          }
+    });
+    for (const auto& pc : part)
+      for (const auto& nt : pc) base_has.emplace_back(nt.first, dict.intern(nt.second + 1, static_cast<size_t>(nt.second[0])));
+  }
   std::vector<std::vector<int32_t>> has(static_cast<size_t>(n_flat));  // term ids per flat candidate pod
   for (int32_t i = 0; i < nc; ++i) {
     if (status[i] != STATUS_PENDING) continue;

@@ -1822,6 +1822,20 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   // ---- topology spread between the pods of one candidate (domain path)
   SpreadDyn sdyn;
   SpreadIndex six(snap);  // spread rows: node values per key, snapshot pods per label (built lazily)
+  if (c->spread) {  // the label values the call's constraints select on (SpreadIndex::want)
+    const sr_spread* S = c->spread;
+    for (int32_t i = 0; i < nc; ++i) {
+      if (w->status_host[i] != STATUS_PENDING) continue;
+      for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j)
+        for (int32_t k = S->off[cands->cand_pods[j]]; k < S->off[cands->cand_pods[j] + 1]; ++k) {
+          if (S->selector_nil[k] || S->ml_off[k] == S->ml_off[k + 1]) continue;
+          int32_t f = S->ml_off[k];
+          for (int32_t x = S->ml_off[k] + 1; x < S->ml_off[k + 1]; ++x)
+            if (S->ml_key[x] < S->ml_key[f]) f = x;
+          six.want(S->ml_key[f], S->ml_val[f]);
+        }
+    }
+  }
   analyse_spread(C, snap, c, cands, w->status_host, &dk, &sdyn, six);
   auto spread_dm = [&](int32_t flat) -> int32_t { return sdyn.dmask.empty() ? 0 : sdyn.dmask[flat - sdyn.base]; };
   // affinity planned on the domain path: the pod's class carries KEYS(S), the

@@ -285,14 +285,16 @@ struct SpreadIndex {
   const sr_snapshot* snap;
   int32_t n_spot, Wp;
   std::unordered_map<int32_t, KeyView> keys;
-  // per label key (built on its first query: one pass over the snapshot pods'
-  // labels, then a counting sort by value id): CSR over the value ids
+  // the label values the call's constraints select on, registered before the
+  // first query (want); a query finds its pods in a per-key column built by
+  // one parallel pass over the snapshot's pods for every wanted value of the
+  // key (an unregistered value rebuilds the column with it)
+  void want(int32_t k, int32_t v) { wanted[k].push_back(v); }
+  std::unordered_map<int32_t, std::vector<int32_t>> wanted;
   struct LabelCol {
-    std::vector<int32_t> off;                        // [max value id + 2]
-    std::vector<std::pair<int32_t, int32_t>> pods;   // (spot position, SnapPod index)
+    std::unordered_map<int32_t, std::vector<std::pair<int32_t, int32_t>>> pods;  // value -> (spot position, pod)
   };
   std::unordered_map<int32_t, LabelCol> by_key;
-  std::vector<std::pair<int32_t, int32_t>> scratch;  // pods_with's return view
 };
 // Constraints in `dmask` (bit k: the k-th) keep only their key check (SpreadDyn).
 void spread_row(SpreadIndex& ix, const int32_t* words, const uint64_t* aff_row, uint32_t dmask, uint64_t* row);

@@ -2638,9 +2638,9 @@ hipError_t launch_placement(const DevWorkload& w, hipStream_t s, hipEvent_t ev0,
   return w.prof ? launch_k2<true>(w, s, ev0, ev1) : launch_k2<false>(w, s, ev0, ev1);
 }
 
-hipError_t launch_heads(const DevWorkload& w, hipStream_t s, hipEvent_t ev1) {
+hipError_t launch_heads(const DevWorkload& w, hipStream_t s) {
   const unsigned waves = static_cast<unsigned>((w.n_pods + 7) / 8);
-  launch(k0_heads, dim3(std::max(1u, (waves + 3) / 4)), dim3(256), 0, s, nullptr, ev1, w);
+  launch(k0_heads, dim3(std::max(1u, (waves + 3) / 4)), dim3(256), 0, s, nullptr, nullptr, w);
   return hipGetLastError();
 }
 

@@ -135,8 +135,8 @@ hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hip
                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // K2: per-candidate feasibility rows + first-fit placement; atomicMin of first_ok into d_min[0].
 hipError_t launch_placement(const DevWorkload& w, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-// K0b: every pod's F and S row heads into pod_head (after K0; its events: ev1 only).
-hipError_t launch_heads(const DevWorkload& w, hipStream_t s, hipEvent_t ev1 = nullptr);
+// K0b: every pod's F and S row heads into pod_head (after K0).
+hipError_t launch_heads(const DevWorkload& w, hipStream_t s);
 // K3: winner mapping into `result` (after the collective when ranks > 1), then the run's seq.
 // Not launched when K2 writes res_stat / res_map itself (single rank).
 hipError_t launch_winner(const DevWorkload& w, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);

@@ -121,7 +121,7 @@ struct sr_ctx {
   std::vector<uint64_t> pod_patch_words;   // this call's pod patches (prepare)
   int32_t k0_incremental = 1;  // SR_K0_INCREMENTAL=0: K0 always rewrites every row
   int32_t k0_skip = 1;         // SR_K0_SKIP=0: every run launches K0
-  int32_t pod_heads = 1;       // SR_POD_HEADS=0: no K0b, K2 ANDs the row heads itself
+  int32_t pod_heads = 0;       // SR_POD_HEADS=1: K0b writes pod heads K2 reads with the records (measured: no gain)
   uint64_t run_count = 0;      // runs of this context: d_min alternates between two buffers
   bool dmin_ready[2] = {false, false};  // buffer reset by the previous run's K2 (a K0-less run needs it)
   sr::EncoderCache enc;      // what the encoder keeps across calls (encode.cpp)
@@ -811,8 +811,14 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     if (!ctx->dmin_ready[par])  // no K2 of a previous run reset it: reset here
       HIP_TRY(ctx, hipMemsetAsync(d.d_min, 0xff, sizeof(uint64_t), s));
   } else {
-    HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, d.pod_head ? nullptr : e0b));
-    if (d.pod_head) HIP_TRY(ctx, sr::launch_heads(d, s, e0b));  // K0b: the pod heads of the rows K0 wrote
+    if (d.pod_head) {  // K0, then K0b (the pod heads of the rows K0 wrote), timed together
+      if (e0a) HIP_TRY(ctx, hipEventRecord(e0a, s));
+      HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s));
+      HIP_TRY(ctx, sr::launch_heads(d, s));
+      if (e0b) HIP_TRY(ctx, hipEventRecord(e0b, s));
+    } else {
+      HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
+    }
     if (sl.commit_k0) {  // K0 wrote the node and pod patches and brought the rows to this workload (a rerun:
       sl.commit_k0 = false;  // idempotent)
       sl.tables_cand_gen = w.cand_gen;

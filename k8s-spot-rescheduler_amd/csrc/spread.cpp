@@ -30,6 +30,7 @@
 #include <unordered_map>
 
 #include "host.hpp"
+#include "pool.hpp"
 
 namespace sr {
 
@@ -181,34 +182,41 @@ const SpreadIndex::KeyView& SpreadIndex::key(int32_t k) {
 
 const std::vector<std::pair<int32_t, int32_t>>* SpreadIndex::pods_with(int32_t k, int32_t v) {
   auto it = by_key.find(k);
-  if (it == by_key.end()) {  // the label column of key k: (value, node, pod), counting-sorted by value
-    LabelCol& col = by_key[k];
-    std::vector<int32_t> vals;
-    std::vector<std::pair<int32_t, int32_t>> at;
-    int32_t vmax = -1;
-    for (int32_t n = 0; n < n_spot; ++n)
-      for (int32_t e : snap->state[n].pods) {
-        const SnapPod& sp = snap->pods[e];
-        for (uint32_t i = 0; i < sp.nlab; ++i)
-          if (snap->lkey[sp.lab + i] == k && snap->lval[sp.lab + i] >= 0) {
-            vals.push_back(snap->lval[sp.lab + i]);
-            at.emplace_back(n, e);
-            vmax = std::max(vmax, snap->lval[sp.lab + i]);
-            break;  // keys are unique per pod
+  if (it == by_key.end() || !it->second.pods.count(v)) {  // (re)build the column of key k
+    std::vector<int32_t>& vals = wanted[k];
+    if (std::find(vals.begin(), vals.end(), v) == vals.end()) vals.push_back(v);
+    std::sort(vals.begin(), vals.end());
+    vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+    // snapshot pods in node chunks on the pool; each chunk keeps the (value,
+    // node, pod) of wanted values in node order
+    constexpr int32_t kNodes = 256;
+    const size_t n_parts = (static_cast<size_t>(n_spot) + kNodes - 1) / kNodes;
+    struct Hit {
+      int32_t v, n, e;
+    };
+    std::vector<std::vector<Hit>> part(n_parts);
+    parallel_for(n_parts, 1, [&](size_t lo, size_t hi) {
+      for (size_t ch = lo; ch < hi; ++ch)
+        for (int32_t n = static_cast<int32_t>(ch) * kNodes; n < std::min<int32_t>(n_spot, (ch + 1) * kNodes); ++n)
+          for (int32_t e : snap->state[n].pods) {
+            const SnapPod& sp = snap->pods[e];
+            for (uint32_t i = 0; i < sp.nlab; ++i)
+              if (snap->lkey[sp.lab + i] == k) {
+                const int32_t x = snap->lval[sp.lab + i];
+                if (std::binary_search(vals.begin(), vals.end(), x)) part[ch].push_back(Hit{x, n, e});
+                break;  // keys are unique per pod
+              }
           }
-      }
-    col.off.assign(static_cast<size_t>(vmax) + 2, 0);
-    for (int32_t x : vals) ++col.off[static_cast<size_t>(x) + 1];
-    for (size_t i = 1; i < col.off.size(); ++i) col.off[i] += col.off[i - 1];
-    col.pods.resize(at.size());
-    std::vector<int32_t> fill(col.off.begin(), col.off.end() - 1);
-    for (size_t i = 0; i < at.size(); ++i) col.pods[static_cast<size_t>(fill[vals[i]]++)] = at[i];
+    });
+    LabelCol& col = by_key[k];
+    col.pods.clear();
+    for (int32_t x : vals) col.pods[x];  // wanted values without pods: an empty list
+    for (const auto& pc : part)
+      for (const Hit& h : pc) col.pods[h.v].emplace_back(h.n, h.e);
     it = by_key.find(k);
   }
-  const LabelCol& col = it->second;
-  if (v < 0 || static_cast<size_t>(v) + 1 >= col.off.size() || col.off[v] == col.off[v + 1]) return nullptr;
-  scratch.assign(col.pods.begin() + col.off[v], col.pods.begin() + col.off[v + 1]);
-  return &scratch;
+  const auto& lst = it->second.pods.find(v)->second;
+  return lst.empty() ? nullptr : &lst;
 }
 
 void spread_node_counts(SpreadIndex& ix, const sr_cluster* c, int32_t k, int32_t ns, std::vector<int32_t>& out) {
@@ -221,7 +229,10 @@ void spread_node_counts(SpreadIndex& ix, const sr_cluster* c, int32_t k, int32_t
   std::vector<std::pair<int32_t, int32_t>> all;
   const std::vector<std::pair<int32_t, int32_t>>* list = nullptr;
   if (S->ml_off[k + 1] > S->ml_off[k]) {
-    list = ix.pods_with(S->ml_key[S->ml_off[k]], S->ml_val[S->ml_off[k]]);
+    int32_t f = S->ml_off[k];  // the pair with the smallest key (spread_words' first)
+    for (int32_t i = S->ml_off[k] + 1; i < S->ml_off[k + 1]; ++i)
+      if (S->ml_key[i] < S->ml_key[f]) f = i;
+    list = ix.pods_with(S->ml_key[f], S->ml_val[f]);
     if (!list) return;
   } else {
     for (int32_t n = 0; n < n_spot; ++n)
