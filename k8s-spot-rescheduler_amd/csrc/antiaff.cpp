@@ -202,10 +202,131 @@ bool term_selects(const Term& t, const PodMeta& m) {
   return true;
 }
 
+inline uint64_t label_key(int32_t k, int32_t v) {
+  return static_cast<uint64_t>(static_cast<uint32_t>(k)) << 32 | static_cast<uint32_t>(v);
+}
+
+using LabelIndex = std::unordered_map<uint64_t, std::vector<int32_t>>;
+
+// The terms selecting a pod: an index on each term's first MatchLabels pair
+// (a pod can only be selected through one of its own labels); terms without
+// MatchLabels are tried on every pod, nil selectors never.
+template <class F>
+void for_each_selecting(const std::vector<Term>& terms, const LabelIndex& by_label, const std::vector<int32_t>& unindexed,
+                        const PodMeta& m, F&& f) {
+  for (int32_t t : unindexed)
+    if (term_selects(terms[t], m)) f(t);
+  for (int32_t i = 0; i < m.n; ++i) {
+    auto it = by_label.find(label_key(m.key[i], m.val[i]));
+    if (it == by_label.end()) continue;
+    for (int32_t t : it->second)
+      if (term_selects(terms[t], m)) f(t);
+  }
+}
+
 }  // namespace
 
+// The snapshot-side state of one encode's DA / DB rows (analyse_anti with
+// `keep`): per spot node the (term, side) of each of its pods -- side 0: the
+// pod has the term, 1: the term selects it -- and per (term, side, value of
+// the term's key) the pods counted, so a reuse encode moves only the rows of
+// the values whose count went to or from zero.
+struct AntiReuse {
+  int32_t n_spot = 0, Wp = 0;
+  WordDict all;                           // every term the full encode interned
+  std::vector<int32_t> nid;               // [all id] kept term, -1: selects no pending candidate pod
+  std::unordered_set<uint64_t> cand_labels;
+  std::vector<Term> terms;                // kept
+  LabelIndex by_label;
+  std::vector<int32_t> unindexed;
+  struct KeyVals {
+    std::vector<int32_t> val;                                 // [n_spot] INT_MIN: absent
+    std::unordered_map<int32_t, std::vector<int32_t>> nodes;  // value -> spot nodes
+  };
+  std::vector<KeyVals> keys;
+  std::vector<int32_t> kidx;              // [term] key
+  std::vector<uint8_t> any_built;         // [2t + side] the class programs AND NOT the row
+  std::vector<int64_t> total;             // [2t + side] pods counted (on nodes carrying the key)
+  std::unordered_map<uint64_t, int32_t> cnt;   // (2t + side) << 32 | value -> pods
+  std::vector<std::vector<int32_t>> contrib;   // [node] 2t + side per pod and term, sorted
+};
+
+namespace {
+
+// Node n's codes 2t + side; false: a term the full encode never interned that
+// passes its filter (it may select a candidate pod).
+bool node_contrib(const AntiReuse& R, const sr_snapshot* snap, int32_t n, std::vector<int32_t>& out) {
+  out.clear();
+  for (int32_t e : snap->state[n].pods) {
+    const SnapPod& sp = snap->pods[e];
+    const int32_t* tw = snap->term_words.data() + sp.terms;
+    for (size_t i = 0; i < sp.nterms; i += 1 + static_cast<size_t>(tw[i])) {
+      const int32_t* w = tw + i + 1;  // {tk, n ns, ns..., nil, n ml, (k, v)...}
+      const int32_t* p = w + 2 + w[1];
+      if (p[0] != 0) continue;  // nil: selects nothing
+      if (p[1] > 0 && !R.cand_labels.count(label_key(p[2], p[3]))) continue;
+      const size_t len = static_cast<size_t>(tw[i]);
+      const int32_t id = R.all.find(w, len, hash_words(w, len));
+      if (id < 0) return false;
+      if (R.nid[id] >= 0) out.push_back(2 * R.nid[id]);
+    }
+    for_each_selecting(R.terms, R.by_label, R.unindexed, meta_of(snap, sp), [&](int32_t t) { out.push_back(2 * t + 1); });
+  }
+  std::sort(out.begin(), out.end());
+  return true;
+}
+
+}  // namespace
+
+bool anti_reuse_patch(AntiReuse& R, const sr_snapshot* snap, const std::vector<int32_t>& nodes, uint64_t* A,
+                      int32_t a_anti, std::vector<int32_t>& atoms, std::vector<int32_t>& words) {
+  if (static_cast<int32_t>(snap->nodes.size()) != R.n_spot) return false;
+  const int32_t Wp = R.Wp;
+  std::vector<int32_t> now;
+  std::vector<std::pair<int32_t, int32_t>> delta;  // (code, +1 / -1)
+  for (int32_t n : nodes) {
+    if (!node_contrib(R, snap, n, now)) return false;
+    std::vector<int32_t>& was = R.contrib[n];
+    if (now == was) continue;
+    delta.clear();
+    size_t i = 0, j = 0;  // sorted multisets: what left, what came
+    while (i < was.size() || j < now.size()) {
+      if (j == now.size() || (i < was.size() && was[i] < now[j])) delta.emplace_back(was[i++], -1);
+      else if (i == was.size() || now[j] < was[i]) delta.emplace_back(now[j++], +1);
+      else ++i, ++j;
+    }
+    was.swap(now);
+    for (const auto& d : delta) {
+      const int32_t code = d.first, t = code >> 1;
+      const AntiReuse::KeyVals& K = R.keys[R.kidx[t]];
+      const int32_t v = K.val[n];
+      if (v == INT_MIN) continue;
+      // the class programs AND NOT the row exactly when it is not empty
+      R.total[code] += d.second;
+      if ((R.total[code] > 0) != (R.any_built[code] != 0)) return false;
+      const uint64_t key = static_cast<uint64_t>(code) << 32 | static_cast<uint32_t>(v);
+      int32_t& c = R.cnt[key];
+      const int32_t before = c;
+      c += d.second;
+      if ((before == 0) == (c == 0)) continue;
+      // the value's domain joins or leaves the row
+      uint64_t* row = A + static_cast<size_t>(a_anti + code) * Wp;
+      auto it = K.nodes.find(v);
+      if (it != K.nodes.end())
+        for (int32_t m : it->second) {
+          if (c != 0) row[m >> 6] |= 1ull << (m & 63);
+          else row[m >> 6] &= ~(1ull << (m & 63));
+          words.push_back(m >> 6);
+        }
+      if (c == 0) R.cnt.erase(key);
+      atoms.push_back(a_anti + code);
+    }
+  }
+  return true;
+}
+
 void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
-                  std::vector<int32_t>& status, DomKeys* dk, AntiTerms* out) {
+                  std::vector<int32_t>& status, DomKeys* dk, AntiTerms* out, std::shared_ptr<AntiReuse>* keep_state) {
   AntiTerms& at = *out;
   at = AntiTerms{};
   const sr_pod_affinity* PA = c->pod_affinity;
@@ -221,6 +342,14 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
   if (PA->anti_off[c->pods.n] == 0 && snap->anti_total == 0) return;  // no term anywhere
   const sr_pod_affinity& A = *PA;
   const int32_t n_spot = static_cast<int32_t>(snap->nodes.size());
+  AntiReuse* R = nullptr;
+  if (keep_state) {
+    *keep_state = std::make_shared<AntiReuse>();
+    R = keep_state->get();
+    R->n_spot = n_spot;
+    R->Wp = Wp;
+    R->contrib.resize(static_cast<size_t>(n_spot));
+  }
 
   // ---- distinct terms: base pods (every snapshot node; the snapshot's own
   // copies) and pending candidates (the call's cluster)
@@ -318,18 +447,31 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
         }
       }
     }
-    std::vector<int32_t> nid(static_cast<size_t>(T_all), -1);
+    // numbered in the order of their words: the numbering (atoms, state-bit
+    // pairs) is a function of the kept set, not of the order the snapshot's
+    // pods were met in (a reuse encode's rows stay where a fresh encode puts them)
+    std::vector<int32_t> order;
     for (int32_t t = 0; t < T_all; ++t)
-      if (keep[t]) {
-        nid[t] = static_cast<int32_t>(terms.size());
-        terms.push_back(std::move(all[t]));
-      }
+      if (keep[t]) order.push_back(t);
+    std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+      return std::lexicographical_compare(dict.data(a), dict.data(a) + dict.len(a), dict.data(b), dict.data(b) + dict.len(b));
+    });
+    std::vector<int32_t> nid(static_cast<size_t>(T_all), -1);
+    for (int32_t t : order) {
+      nid[t] = static_cast<int32_t>(terms.size());
+      terms.push_back(std::move(all[t]));
+    }
     size_t w2 = 0;
     for (const auto& nt : base_has)
       if (nid[nt.second] >= 0) base_has[w2++] = {nt.first, nid[nt.second]};
     base_has.resize(w2);
     for (auto& h : has)
       for (int32_t& t : h) t = nid[t];  // every term a pending pod has is kept
+    if (R) {
+      R->cand_labels = cand_labels;
+      R->nid = std::move(nid);
+      R->all = std::move(dict);
+    }
   }
   const int32_t T = static_cast<int32_t>(terms.size());
   if (T == 0) return;
@@ -381,24 +523,14 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
   // ---- which terms select a pod: an index on each term's first MatchLabels
   // pair (a pod can only be selected through one of its own labels); terms
   // without MatchLabels are tried on every pod, nil selectors never
-  std::unordered_map<uint64_t, std::vector<int32_t>> by_label;
+  LabelIndex by_label;
   std::vector<int32_t> unindexed;
-  auto label_key = [](int32_t k, int32_t v) { return static_cast<uint64_t>(static_cast<uint32_t>(k)) << 32 | static_cast<uint32_t>(v); };
   for (int32_t t = 0; t < T; ++t) {
     if (terms[t].nil) continue;
     if (terms[t].ml.empty()) unindexed.push_back(t);
     else by_label[label_key(terms[t].ml[0].first, terms[t].ml[0].second)].push_back(t);
   }
-  auto for_each_selecting = [&](const PodMeta& m, auto&& f) {
-    for (int32_t t : unindexed)
-      if (term_selects(terms[t], m)) f(t);
-    for (int32_t i = 0; i < m.n; ++i) {
-      auto it = by_label.find(label_key(m.key[i], m.val[i]));
-      if (it == by_label.end()) continue;
-      for (int32_t t : it->second)
-        if (term_selects(terms[t], m)) f(t);
-    }
-  };
+  auto selecting = [&](const PodMeta& m, auto&& f) { for_each_selecting(terms, by_label, unindexed, m, f); };
 
   // ---- domains of the base pods: SA(t) values hosting a pod that has t,
   // SB(t) values hosting a pod t selects
@@ -414,13 +546,28 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       for (size_t ch = lo; ch < hi; ++ch)
         for (int32_t n = static_cast<int32_t>(ch * kNodes); n < std::min<int32_t>(n_spot, (ch + 1) * kNodes); ++n)
           for (int32_t e : snap->state[n].pods)
-            for_each_selecting(meta_of(snap, snap->pods[e]), [&](int32_t t) {
-              const int32_t v = keys[kidx[t]].val[n];
-              if (v != INT_MIN) part[ch].emplace_back(t, v);
-            });
+            selecting(meta_of(snap, snap->pods[e]), [&](int32_t t) { part[ch].emplace_back(t, n); });
     });
     for (const auto& pc : part)
-      for (const auto& tv : pc) sb[tv.first].push_back(tv.second);
+      for (const auto& tn : pc) {
+        const int32_t v = keys[kidx[tn.first]].val[tn.second];
+        if (v != INT_MIN) sb[tn.first].push_back(v);
+      }
+    if (R) {  // per node: the pods' (term, side) codes, and the counts per value
+      R->total.assign(static_cast<size_t>(2 * T), 0);
+      for (const auto& nt : base_has) R->contrib[nt.first].push_back(2 * nt.second);
+      for (const auto& pc : part)
+        for (const auto& tn : pc) R->contrib[tn.second].push_back(2 * tn.first + 1);
+      for (int32_t n = 0; n < n_spot; ++n) {
+        std::sort(R->contrib[n].begin(), R->contrib[n].end());
+        for (int32_t code : R->contrib[n]) {
+          const int32_t v = keys[kidx[code >> 1]].val[n];
+          if (v == INT_MIN) continue;
+          ++R->total[code];
+          ++R->cnt[static_cast<uint64_t>(code) << 32 | static_cast<uint32_t>(v)];
+        }
+      }
+    }
   }
   at.da.assign(static_cast<size_t>(T) * Wp, 0);
   at.db.assign(static_cast<size_t>(T) * Wp, 0);
@@ -443,6 +590,22 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       }
     }
   });
+  if (R) {
+    R->terms = terms;
+    R->by_label = by_label;
+    R->unindexed = unindexed;
+    R->kidx = kidx;
+    R->keys.resize(keys.size());
+    for (size_t k = 0; k < keys.size(); ++k) {
+      R->keys[k].val = keys[k].val;
+      R->keys[k].nodes = keys[k].nodes;
+    }
+    R->any_built.resize(static_cast<size_t>(2 * T));
+    for (int32_t t = 0; t < T; ++t) {
+      R->any_built[2 * t] = at.da_any[t];
+      R->any_built[2 * t + 1] = at.db_any[t];
+    }
+  }
 
   // ---- per pending candidate pod: ids t << 1 (t selects it) | t << 1 | 1 (it has t)
   std::vector<std::vector<int32_t>> ids(static_cast<size_t>(n_flat));
@@ -452,7 +615,7 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
       for (int32_t j = cands->cand_pod_off[i]; j < cands->cand_pod_off[i + 1]; ++j) {
         const int32_t pod = cands->cand_pods[j];
         std::vector<int32_t>& v = ids[j - base];
-        for_each_selecting(meta_of(A, pod), [&](int32_t t) { v.push_back(t << 1); });
+        selecting(meta_of(A, pod), [&](int32_t t) { v.push_back(t << 1); });
         for (int32_t t : has[j - base]) v.push_back(t << 1 | 1);
         std::sort(v.begin(), v.end());
       }

@@ -951,7 +951,7 @@ void pod_affinity_row(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
 // node-local key whose minimum could move (no more nodes at the minimum than
 // the constraint counts pods of the candidate).
 void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands,
-                    std::vector<int32_t>& status, DomKeys* dk, SpreadDyn* out, SpreadIndex& six) {
+                    std::vector<int32_t>& status, DomKeys* dk, SpreadDyn* out, SpreadIndex& six, SpreadReuse* keep) {
   SpreadDyn& sd = *out;
   sd = SpreadDyn{};
   const sr_spread* S = c->spread;
@@ -969,8 +969,18 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
   // computed once per distinct content (the nodeSelector / affinity words; the
   // namespace and selector)
   std::map<std::vector<int32_t>, std::vector<uint64_t>> aff_rows;
-  std::map<std::vector<int32_t>, std::vector<int32_t>> counts;
+  std::map<std::vector<int32_t>, std::vector<int32_t>> counts;  // spread_selector_words -> node counts
   std::vector<int32_t> key_words;
+  struct PendingSlot {  // a table entry for the reuse state (SpreadReuse), once the candidate is planned
+    std::vector<int32_t> sel;
+    uint32_t off;
+    bool local;
+    std::vector<uint64_t> pairs;
+    int32_t skew, self, n_counted, slot;
+    uint64_t pm;
+    int32_t edom;
+  };
+  std::vector<PendingSlot> pend;
   for (int32_t i = 0; i < nc; ++i) {
     if (status[i] != STATUS_PENDING) continue;
     const int32_t b = cands->cand_pod_off[i], e = cands->cand_pod_off[i + 1];
@@ -982,6 +992,7 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
     }
     if (!any) continue;
     bool fb = e - b > kDynPods;
+    pend.clear();
     words.assign(static_cast<size_t>(e - b) * kSpreadU64, 0);
     std::vector<uint8_t> dm(static_cast<size_t>(e - b), 0);
     const size_t tab0 = sd.tab.size();
@@ -1034,13 +1045,7 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
           break;
         }
         const int32_t self = spread_selects(c, k, pod) ? 1 : 0, skew = S->max_skew[k];
-        key_words.assign({A->ns[pod], S->selector_nil[k]});
-        for (int32_t x = S->ml_off[k]; x < S->ml_off[k + 1]; ++x) key_words.insert(key_words.end(), {S->ml_key[x], S->ml_val[x]});
-        key_words.push_back(-1);
-        for (int32_t x = S->me_off[k]; x < S->me_off[k + 1]; ++x) {
-          key_words.insert(key_words.end(), {S->me_key[x], S->me_op[x], S->me_val_off[x + 1] - S->me_val_off[x]});
-          key_words.insert(key_words.end(), S->me_vals + S->me_val_off[x], S->me_vals + S->me_val_off[x + 1]);
-        }
+        spread_selector_words(c, A->ns[pod], k, key_words);
         auto ci = counts.find(key_words);
         if (ci == counts.end()) {
           std::vector<int32_t> v;
@@ -1065,6 +1070,7 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
           }
           if (n0 <= n_counted) {
             fb = true;
+            sd.state_fb = true;  // decided by the base counts
             break;
           }
           for (int32_t n = 0; n < n_spot; ++n) {
@@ -1077,6 +1083,7 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
                       static_cast<uint64_t>(static_cast<uint32_t>(skew)) << 32;
           sw[kDynG + 1] = off;
           sw[kDynG + 2] = 0;
+          if (keep) pend.push_back(PendingSlot{key_words, off, true, aff, skew, self, n_counted, slot, 0, -1});
         } else {
           // pairs by domain; a node lacking the key counts into the pair of ""
           int32_t edom = -1;
@@ -1100,6 +1107,7 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
                       static_cast<uint64_t>(static_cast<uint32_t>(skew)) << 32;
           sw[kDynG + 1] = off | static_cast<uint64_t>(static_cast<uint32_t>(edom)) << 32;
           sw[kDynG + 2] = pm;
+          if (keep) pend.push_back(PendingSlot{key_words, off, false, {}, skew, self, n_counted, slot, pm, edom});
           dm[u - b] |= static_cast<uint8_t>(1u << (k - S->off[pod]));
         }
         ++slots;
@@ -1117,6 +1125,9 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
     }
     sd.cand_dyn[i] = 1;
     sd.active = true;
+    for (const PendingSlot& ps : pend)
+      spread_reuse_slot(*keep, ps.sel, counts.find(ps.sel)->second, ps.off, ps.local, ps.pairs, ps.skew, ps.self,
+                        ps.n_counted, dk->dom[ps.slot], ps.pm, ps.edom);
     std::copy(words.begin(), words.end(), sd.rec.begin() + static_cast<size_t>(b - base) * kSpreadU64);
     std::copy(dm.begin(), dm.end(), sd.dmask.begin() + (b - base));
   }
@@ -1150,6 +1161,7 @@ uint64_t node_state_fp(const SpotNode& sn, const NodeState& st) {
     h = mix(mix(mix(h, 0x5CA3ull), static_cast<uint32_t>(l.first)), static_cast<uint64_t>(l.second));
   for (const auto& a : st.att)  // sorted
     h = mix(mix(mix(h, 0x5CA4ull), static_cast<uint32_t>(a.first)), static_cast<uint32_t>(a.second));
+  h = mix(mix(h, 0x3E7Aull), st.meta_sum);
   uint64_t ports = 0;  // order-independent
   for (const Port& u : st.ports)
     ports += mix(mix(mix(0x9E37ull, static_cast<uint32_t>(u.ip)), static_cast<uint32_t>(u.proto)),
@@ -1252,6 +1264,14 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
   CandReuse& R = w->reuse;
   const int32_t Wp = w->Wp, n_spot = w->n_spot;
   uint64_t* A = w->atoms.data();
+  w->atom_cols.clear();
+  w->tab_changed = false;
+  w->atoms_prev_ver = w->atoms_ver;
+  w->atom_rows.clear();
+  w->atom_rows_all = false;
+  std::vector<int32_t>& rows_moved = w->atom_rows;
+  // the inter-pod and spread states are kept per spot position
+  if ((R.anti || R.spread) && w->layout_gen != C.layout_gen) return false;
   // the host-decided outcomes that read the snapshot must still hold: scalar
   // usage known on every node, no planned candidate's attachable volume on a
   // spot node (only the nodes changed since the last encode can have one now;
@@ -1275,6 +1295,7 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
     std::vector<uint8_t> tmp;
     for (int32_t a = 0; a < w->n_atoms; ++a) permute_row(C, A + static_cast<size_t>(a) * Wp, tmp);
     w->layout_gen = C.layout_gen;
+    w->atom_rows_all = true;
   }
   // pod count and the composites built on it, in the words where it changed
   std::vector<int32_t> words;
@@ -1289,6 +1310,10 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
       for (size_t j = 0; j < nu; ++j) any |= C.taint_rows[static_cast<size_t>(u[j]) * Wp + i];
       A[static_cast<size_t>(R.a_comp + static_cast<int32_t>(k)) * Wp + i] = A[i] & ~any;
     }
+  }
+  if (!words.empty()) {
+    rows_moved.push_back(0);
+    for (size_t k = 0; k < R.comp_sets.size(); ++k) rows_moved.push_back(R.a_comp + static_cast<int32_t>(k));
   }
   bool flags_moved = false;
   auto refresh_flags = [&](int32_t a) {
@@ -1314,6 +1339,7 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
       if (!std::equal(r, r + Wp, a)) {
         std::copy_n(r, Wp, a);
         refresh_flags(R.a_port + q);
+        rows_moved.push_back(R.a_port + q);
       }
     }
   }
@@ -1332,7 +1358,10 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
         wd = scalar_query_node(snap, n, R.scalar_q[q].first, R.scalar_q[q].second) ? (wd | bit) : (wd & ~bit);
         moved_bit = moved_bit || wd != old;
       }
-      if (moved_bit) refresh_flags(R.a_scalar + static_cast<int32_t>(q));
+      if (moved_bit) {
+        refresh_flags(R.a_scalar + static_cast<int32_t>(q));
+        rows_moved.push_back(R.a_scalar + static_cast<int32_t>(q));
+      }
     }
     if (!R.scal_names.empty())
       for (size_t u = 0; u < R.scal_names.size(); ++u)
@@ -1348,12 +1377,40 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
       if (!std::equal(row.begin(), row.end(), a)) {
         std::copy(row.begin(), row.end(), a);
         refresh_flags(R.a_scalar + static_cast<int32_t>(q));
+        rows_moved.push_back(R.a_scalar + static_cast<int32_t>(q));
       }
     }
     if (!R.scal_names.empty()) node_scal_rows(snap, R.scal_names, w->n_pad, w->node_scal.data());
   }
+  // required anti-affinity and topology spread: the DA / DB rows, the spread
+  // rows and the domain-path tables follow the nodes whose pods changed
+  // (every node when the state view was rebuilt since this workload's encode)
+  if ((R.anti || R.spread) && prev_state_gen != C.state_gen) {
+    std::vector<int32_t> every;
+    const std::vector<int32_t>* nodes = &C.patched_nodes;
+    if (C.patched_from != prev_state_gen) {
+      every.resize(static_cast<size_t>(n_spot));
+      for (int32_t n = 0; n < n_spot; ++n) every[n] = n;
+      nodes = &every;
+    }
+    std::vector<int32_t> moved_atoms;
+    if (R.anti && !anti_reuse_patch(*R.anti, snap, *nodes, A, R.a_anti, moved_atoms, w->atom_cols)) return false;
+    if (R.spread &&
+        !spread_reuse_patch(*R.spread, snap, *nodes, A, w->sp_tab, &w->tab_changed, moved_atoms, w->atom_cols))
+      return false;
+    std::sort(moved_atoms.begin(), moved_atoms.end());
+    moved_atoms.erase(std::unique(moved_atoms.begin(), moved_atoms.end()), moved_atoms.end());
+    for (int32_t a : moved_atoms) refresh_flags(a);
+    rows_moved.insert(rows_moved.end(), moved_atoms.begin(), moved_atoms.end());
+    std::sort(w->atom_cols.begin(), w->atom_cols.end());
+    w->atom_cols.erase(std::unique(w->atom_cols.begin(), w->atom_cols.end()), w->atom_cols.end());
+  }
+  std::sort(rows_moved.begin(), rows_moved.end());
+  rows_moved.erase(std::unique(rows_moved.begin(), rows_moved.end()), rows_moved.end());
+  if (w->atom_rows_all || !rows_moved.empty()) w->atoms_ver = C.atoms_ver_next++;
   // classes whose certain emptiness changed: after every atom row above was
-  // refreshed (pod count, composites, ports, scalar / volume-limit queries)
+  // refreshed (pod count, composites, ports, scalar / volume-limit queries,
+  // inter-pod and spread rows)
   std::vector<int32_t> flipped;
   if (flags_moved)
     for (int32_t k = 0; k < static_cast<int32_t>(R.cls_empty.size()); ++k) {
@@ -1553,8 +1610,9 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   CandReuse& R = w->reuse;
   const bool same_input = stamps && R.shape == C.memo_shape && same_cand_input(R, cands, stamps);
   if (same_input && R.indexed && R.content_gen == C.content_gen && R.static_gen == C.static_gen && R.n_spot == n_spot && R.Wp == Wp &&
-      (w->layout_gen == C.layout_gen || w->layout_gen + 1 == C.layout_gen) && snap->anti_total == 0 &&
-      snap->opaque_total == 0) {
+      (w->layout_gen == C.layout_gen || w->layout_gen + 1 == C.layout_gen) && snap->opaque_total == 0 &&
+      (snap->anti_total == 0 || R.anti) &&
+      (!(R.anti || R.spread) || (snap->unknown_total == 0 && snap->term_unknown_total == 0))) {
     const uint64_t prev_state_gen = w->state_gen;
     w->state_gen = C.state_gen;
     if (reuse_encode(C, snap, w, prev_state_gen)) {
@@ -1583,6 +1641,10 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   const bool want_index = same_input;
   w->reset();
   w->cand_gen = C.cand_gen_next++;
+  w->atoms_ver = C.atoms_ver_next++;
+  w->atoms_prev_ver = 0;
+  w->atom_rows.clear();
+  w->atom_rows_all = true;
   w->n_input_cand = nc;
   w->pod_base = nc > 0 ? cands->cand_pod_off[0] : 0;
   w->n_input_pods = nc > 0 ? cands->cand_pod_off[nc] - w->pod_base : 0;
@@ -1813,7 +1875,9 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   // the candidates it sends to the fallback path (antiaff.cpp)
   DomKeys dk;  // topology keys of the domain path (K2 k2_domain)
   AntiTerms anti;
-  analyse_anti(snap, c, cands, Wp, w->status_host, &dk, &anti);
+  // the index build (want_index) keeps the snapshot-side state a reuse encode patches
+  std::shared_ptr<AntiReuse> anti_keep;
+  analyse_anti(snap, c, cands, Wp, w->status_host, &dk, &anti, want_index ? &anti_keep : nullptr);
   const int32_t bit_shift = 2 * anti.n_pairs;  // host-port bits sit above the pairs
   // ---- required pod affinity: term sets, their node rows, and the
   // candidates whose pods interact through them (antiaff.cpp)
@@ -1836,7 +1900,8 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
         }
     }
   }
-  analyse_spread(C, snap, c, cands, w->status_host, &dk, &sdyn, six);
+  std::shared_ptr<SpreadReuse> spread_keep = want_index && c->spread ? spread_reuse_new(snap, Wp) : nullptr;
+  analyse_spread(C, snap, c, cands, w->status_host, &dk, &sdyn, six, spread_keep.get());
   auto spread_dm = [&](int32_t flat) -> int32_t { return sdyn.dmask.empty() ? 0 : sdyn.dmask[flat - sdyn.base]; };
   // affinity planned on the domain path: the pod's class carries KEYS(S), the
   // device the rest (an earlier pod of its candidate matches all its terms)
@@ -2581,7 +2646,7 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
       for (int32_t x = 0; x < Wp; ++x) aff_row[x] &= any[x];
     }
     spread_row(six, sp.spread.data(), aff_row.data(), static_cast<uint32_t>(spread_query[q].second),
-               A + static_cast<size_t>(A_SPREAD + q) * Wp);
+               A + static_cast<size_t>(A_SPREAD + q) * Wp, spread_keep.get(), A_SPREAD + q);
   }
   for (int32_t t = 0; t < anti.n_terms; ++t) {
     std::copy_n(&anti.da[static_cast<size_t>(t) * Wp], Wp, A + static_cast<size_t>(A_ANTI + 2 * t) * Wp);
@@ -2903,19 +2968,23 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
     // host ports, scalar resources and volume limits read the snapshot through
     // atom rows a reuse encode recomputes (CandReuse::port_q, scalar_q) and the
     // shared scalar rows (scal_names)
-    bool state_free = snap->anti_total == 0 && snap->opaque_total == 0 && !anti.active && !aff.active &&
-                      !sdyn.active && n_spreads == 0 && w->dyn_cand.empty() && w->empty_class >= 0 && bit_shift == 0;
+    // inter-pod anti-affinity and topology spread read the snapshot through
+    // the DA / DB rows, the spread rows and the domain-path tables, which a
+    // reuse patches node by node (AntiReuse, SpreadReuse), and through host
+    // decisions that must not be able to turn: no opaque or unknown pods
+    // (pass 1), no candidate sent to the reference path on the base counts
+    // (analyse_spread); required pod affinity is not followed
+    bool state_free = snap->opaque_total == 0 && (snap->anti_total == 0 || anti_keep) && !aff.active &&
+                      !sdyn.state_fb && w->empty_class >= 0;
+    if ((anti_keep || spread_keep) && (snap->unknown_total > 0 || snap->term_unknown_total > 0)) state_free = false;
+    if (!c->pod_affinity && snap->anti_total > 0) state_free = false;  // pass 1 sent everything back on it
     const sr_pod_affinity* PA = c->pod_affinity;
     for (int32_t j = w->pod_base; j < w->pod_base + w->n_input_pods && state_free; ++j) {
       const int32_t pod = cands->cand_pods[j];
-      const uint32_t mb = memo_bits(pod);
       // scalar resources and attachable volumes read the snapshot through
       // their atom rows and the shared scalar rows (recomputed by a reuse) and
-      // through the fallback checks (rechecked by a reuse); spread does not
-      state_free = (mb & MEMO_PLAIN) != 0 || !has_spread(c, pod);
-      if (PA)
-        state_free = state_free && PA->anti_off[pod] == PA->anti_off[pod + 1] &&
-                     (!PA->aff_off || PA->aff_off[pod] == PA->aff_off[pod + 1]);
+      // through the fallback checks (rechecked by a reuse)
+      if (PA) state_free = !PA->aff_off || PA->aff_off[pod] == PA->aff_off[pod + 1];
       // a fallback decided by the snapshot must not be able to turn back:
       // scalar usage unknown on some node, or an attachable volume of a
       // fallback candidate (a spot node may hold it)
@@ -2950,6 +3019,9 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
         }
       }
       std::sort(R.att_words.begin(), R.att_words.end());
+      R.anti = anti_keep;
+      R.a_anti = A_ANTI;
+      R.spread = spread_keep;
       R.a_port = A_PORT;
       R.port_q.clear();
       for (const PortQuery& pq : port_query) R.port_q.insert(R.port_q.end(), {pq.proto, pq.port, pq.ip});

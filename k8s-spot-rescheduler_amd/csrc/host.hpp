@@ -63,6 +63,8 @@ struct SnapPod {
   uint32_t lab, nlab;       // labels: sr_snapshot::lkey / lval [lab, lab + nlab)
   uint32_t terms, nterms;   // anti-affinity terms: sr_snapshot::term_words [terms, terms + nterms),
                             // {n words, words...} per term (rare)
+  uint64_t meta_fp;         // fingerprint of what the inter-pod and spread filters read of it: namespace,
+                            // deletion state, labels, terms (order-independent)
 };
 
 // std::allocator that default-initializes on resize() / emplace_back(): the
@@ -103,6 +105,8 @@ struct NodeState {
   int32_t scalar_unknown = 0;  // pods added without scalar tables that carry scalar requests
   int32_t term_unknown = 0;    // pods added without sr_spread (deletion state unknown)
   std::vector<std::pair<int32_t, int32_t>> att;  // attachable volumes (limit key, unique name) of its pods, sorted
+  uint64_t meta_sum = 0;       // sum of its pods' SnapPod::meta_fp (node_state_fp: a reuse encode's
+                               // inter-pod and spread rows follow the nodes whose pods changed)
 };
 
 // ---- volume filters (sr_volumes)
@@ -277,6 +281,8 @@ struct SpreadIndex {
     std::vector<int32_t> values;  // distinct values
     std::vector<uint64_t> bits;   // [values][Wp] nodes carrying each value
     std::vector<uint64_t> has;    // [Wp] nodes carrying the key
+    std::vector<int32_t> slot;    // [n_spot] the value slot of the node's pair (a node without the key: the
+                                  // slot of "" when some node carries ""), -1 none
   };
   explicit SpreadIndex(const sr_snapshot* s);
   const KeyView& key(int32_t k);
@@ -296,8 +302,34 @@ struct SpreadIndex {
   };
   std::unordered_map<int32_t, LabelCol> by_key;
 };
-// Constraints in `dmask` (bit k: the k-th) keep only their key check (SpreadDyn).
-void spread_row(SpreadIndex& ix, const int32_t* words, const uint64_t* aff_row, uint32_t dmask, uint64_t* row);
+// The snapshot-side state of one encode's spread rows and domain-path tables
+// that a reuse encode (CandReuse) brings up to date node by node (spread.cpp):
+// per distinct selector (namespace + selector words) the spot nodes' counts of
+// the snapshot pods it counts, and per row / table entry the selectors and
+// static inputs it was computed from.
+struct SpreadReuse;
+struct AntiReuse;  // antiaff.cpp
+std::shared_ptr<SpreadReuse> spread_reuse_new(const sr_snapshot* snap, int32_t Wp);
+// Constraints in `dmask` (bit k: the k-th) keep only their key check
+// (SpreadDyn).  `keep`: registers the row as atom `atom` of the workload.
+void spread_row(SpreadIndex& ix, const int32_t* words, const uint64_t* aff_row, uint32_t dmask, uint64_t* row,
+                SpreadReuse* keep = nullptr, int32_t atom = -1);
+// {namespace, nil, n matchLabels, (key, value)* sorted, n matchExpressions,
+// (key, op, n, values sorted)*}: constraint k's counting selector for a pod of
+// namespace `ns` (the counters' key).
+void spread_selector_words(const sr_cluster* c, int32_t ns, int32_t k, std::vector<int32_t>& out);
+// A domain-path table entry of analyse_spread (node-local key: tab[off + n]
+// for every spot node, `pairs` its pairs; table key: tab[off + d] per domain).
+void spread_reuse_slot(SpreadReuse& R, const std::vector<int32_t>& sel_words, const std::vector<int32_t>& node_cnt,
+                       uint32_t off, bool node_local, const std::vector<uint64_t>& pairs, int32_t skew, int32_t self,
+                       int32_t n_counted, const std::vector<int32_t>& dom, uint64_t pm, int32_t edom);
+// Brings the rows (atoms) and tables to the snapshot after the pods of `nodes`
+// changed; the atoms whose rows changed and the row words touched are
+// appended.  False: a table's minimum could now move under the candidate
+// (the full encode would send it to the reference path).
+bool spread_reuse_patch(SpreadReuse& R, const sr_snapshot* snap, const std::vector<int32_t>& nodes, uint64_t* A,
+                        std::vector<int32_t>& tab, bool* tab_changed, std::vector<int32_t>& atoms,
+                        std::vector<int32_t>& words);
 // The same by a scan of every snapshot pod (SR_SPREAD_CHECK=1 compares both).
 void spread_row_scan(const sr_snapshot* snap, const int32_t* words, const uint64_t* aff_row, uint32_t dmask,
                      uint64_t* row);
@@ -379,6 +411,9 @@ struct CandReuse {
   bool scalars = false;                        // some candidate pod lists scalar resources
   std::vector<uint64_t> att_words;             // attachable volumes of the planned candidates' pods: a spot node
                                                // that comes to hold one sends its candidate to the fallback path
+  std::shared_ptr<AntiReuse> anti;             // DA / DB rows at a_anti (null: no inter-pod term in the call)
+  int32_t a_anti = 0;
+  std::shared_ptr<SpreadReuse> spread;         // spread rows and domain-path tables (null: no constraint)
   std::vector<uint8_t> atom_empty, atom_full;  // [n_atoms]
   std::vector<uint8_t> cls_empty;              // [classes before the empty class]
   std::vector<int32_t> pod_cls;                // [active pod] class before the dead check
@@ -393,7 +428,11 @@ struct CandReuse {
   std::vector<int32_t> spare[3];               // free T rows of each dimension's group
   std::vector<uint32_t> mark;                  // [active pod] epoch of the last patch
   uint32_t epoch = 0;
-  void drop() { have_input = indexed = false; }
+  void drop() {
+    have_input = indexed = false;
+    anti.reset();
+    spread.reset();
+  }
 };
 
 // The encoded workload of one planning call (host copy; uploaded as one
@@ -474,6 +513,15 @@ struct Workload {
   bool reused = false;
   bool class_flip = false;          // a reuse encode moved some pod to or from the empty class
   std::vector<uint64_t> pod_patch;  // [n][kPodPatchWords] {active pod, rec[4], rec[5]} (reuse encodes)
+  std::vector<int32_t> atom_cols;   // row words a reuse encode changed in the inter-pod / spread atoms (beyond the
+                                    // changed nodes' own words: a zone's nodes, a moved minimum), sorted
+  bool tab_changed = false;         // a reuse encode rewrote sp_tab entries
+  // version of `atoms` (a new one per encode that changes any row); a reuse
+  // encode that moved rows lists them (atom_rows_all: too many to list, or a
+  // permutation) against the version it started from
+  uint64_t atoms_ver = 0, atoms_prev_ver = 0;
+  std::vector<int32_t> atom_rows;
+  bool atom_rows_all = false;
   CandReuse reuse;                  // kept by reset(): the encoder rebuilds or drops it
 
   // Back to the default state, keeping every buffer's capacity: a planner
@@ -504,6 +552,8 @@ struct Workload {
     reused = false;
     class_flip = false;
     pod_patch.clear();
+    atom_cols.clear();
+    tab_changed = false;
   }
 };
 
@@ -614,6 +664,7 @@ struct EncoderCache {
   std::vector<int32_t> patched_nodes;
   uint64_t patched_from = ~0ull;
   uint64_t cand_gen_next = 1;
+  uint64_t atoms_ver_next = 1;  // Workload::atoms_ver
   int32_t last_reused = 0, last_pod_patches = 0;
 
   uint64_t content_gen = 0;  // bumped by clear_content (a Workload's CandReuse is valid for one value)
@@ -676,8 +727,18 @@ struct AntiTerms {
 // Collects the terms of the snapshot's pods and of the pending candidates,
 // builds the static node sets and decides which candidates fall back
 // (status -> SR_CAND_FALLBACK) or need state bits.
+// `keep`: also builds the state a reuse encode patches (AntiReuse).
+struct AntiReuse;
 void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
-                  std::vector<int32_t>& status, DomKeys* dk, AntiTerms* out);
+                  std::vector<int32_t>& status, DomKeys* dk, AntiTerms* out,
+                  std::shared_ptr<AntiReuse>* keep = nullptr);
+// Brings the DA / DB atom rows (DA(t) at a_anti + 2t, DB(t) at a_anti + 2t + 1)
+// to the snapshot after the pods of `nodes` changed; the atoms whose rows
+// changed and the row words touched are appended.  False: a change the reuse
+// cannot follow -- a term it never saw that may select a candidate pod, or a
+// set that was empty when the class programs were emitted and no longer is.
+bool anti_reuse_patch(AntiReuse& R, const sr_snapshot* snap, const std::vector<int32_t>& nodes, uint64_t* A,
+                      int32_t a_anti, std::vector<int32_t>& atoms, std::vector<int32_t>& words);
 
 // Required pod affinity of one encode (antiaff.cpp).
 struct AffTerms {
@@ -725,6 +786,7 @@ struct SpreadDyn {
   std::vector<uint64_t> rec;       // [flat - base][kSpreadU64] (empty: no such candidate)
   std::vector<uint8_t> dmask;      // [flat - base] bit k: the pod's k-th constraint is a device-planned table key
   std::vector<int32_t> tab;
+  bool state_fb = false;           // a candidate went to the reference path on the base counts (n0 <= counted)
 };
 
 // Builds the workload; returns SR_OK or an error with *err filled.  `cache`

@@ -16,6 +16,7 @@
 #include "gosort.hpp"
 #include "host.hpp"
 #include "pool.hpp"
+#include "worddict.hpp"
 
 // Per-node pod sorts of earlier NewNodeMap calls (sr_new_node_map_cached),
 // by node name: the stamps of the node's LISTed pods in list order, its kind,
@@ -374,6 +375,11 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   return SR_OK;
 }
 
+static inline uint64_t pod_meta_mix(uint64_t h, uint64_t x) {
+  h = (h ^ x) * 0xff51afd7ed558ccdull;
+  return h ^ (h >> 32);
+}
+
 void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out, int32_t* k, int32_t* v, uint32_t lab,
                    std::vector<int32_t>* terms) {
   *out = SnapPod{};
@@ -381,6 +387,7 @@ void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out, int32_t* k, i
   out->anti = has_anti_terms(c, pod) ? 1 : 0;
   out->opaque = anti_opaque(c, pod) ? 1 : 0;
   out->term = c->spread ? (c->spread->terminating[pod] ? 1 : 0) : 2;
+  out->meta_fp = pod_meta_mix(0x5EEDull, out->term);
   const sr_pod_affinity* A = c->pod_affinity;
   if (!A) return;
   out->meta = 1;
@@ -389,6 +396,10 @@ void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out, int32_t* k, i
   out->nlab = pod_label_count(c, pod);
   std::copy(A->label_key + A->label_off[pod], A->label_key + A->label_off[pod + 1], k + lab);
   std::copy(A->label_val + A->label_off[pod], A->label_val + A->label_off[pod + 1], v + lab);
+  uint64_t fp = pod_meta_mix(pod_meta_mix(0x3E7Aull, static_cast<uint32_t>(out->ns)), out->term);
+  for (int32_t i = A->label_off[pod]; i < A->label_off[pod + 1]; ++i)  // labels: a map (order-independent)
+    fp += pod_meta_mix(pod_meta_mix(0x1AB7ull, static_cast<uint32_t>(A->label_key[i])), static_cast<uint32_t>(A->label_val[i]));
+  out->meta_fp = fp;
   if (out->opaque || !out->anti) return;  // opaque: never read, every candidate falls back while it is there
   std::vector<int32_t> words;
   out->terms = static_cast<uint32_t>(terms->size());
@@ -398,6 +409,8 @@ void snap_pod_from(const sr_cluster* c, int32_t pod, SnapPod* out, int32_t* k, i
     terms->insert(terms->end(), words.begin(), words.end());
   }
   out->nterms = static_cast<uint32_t>(terms->size()) - out->terms;
+  for (uint32_t i = out->terms; i < out->terms + out->nterms; i += 1 + static_cast<uint32_t>((*terms)[i]))
+    out->meta_fp += pod_meta_mix(0x7E4Dull, hash_words(terms->data() + i + 1, static_cast<size_t>((*terms)[i])));
 }
 
 // scheduler NodeInfo.AddPod [upstream k8s v1.19 framework/types.go]: Requested +=
@@ -421,6 +434,7 @@ static void state_add_pod(NodeState& st, const sr_cluster* c, int32_t pod, const
     st.scalar_unknown += 1;  // its scalar requests are not in the call: unknown to the planner
   }
   st.npods += 1;
+  st.meta_sum += sp.meta_fp;
   st.anti += sp.anti;
   st.opaque += sp.opaque;
   st.unknown += sp.meta ? 0 : 1;

@@ -83,7 +83,14 @@ struct Slot {
   uint64_t tables_cand_gen = ~0ull; // candidate generation, encoder state, thresholds and atoms of the last K0
   uint64_t tables_state_gen = ~0ull;  //   run on `tables` (incremental K0 / K0-less runs: what changed since)
   std::vector<int64_t> tables_thr;
-  std::vector<uint64_t> tables_atoms;
+  uint64_t tables_atoms_ver = ~0ull;   // Workload::atoms_ver of the last K0 run
+  std::vector<int32_t> atom_cols;      // inter-pod / spread atom words changed since (reuse encodes)
+  // atom rows changed since version atoms_log_ver (reuse encodes of one
+  // candidate generation): the staging and device copies of an older version
+  // that is atoms_log_ver take only those rows
+  uint64_t atoms_log_ver = ~0ull, last_atoms_ver = ~0ull;
+  std::vector<int32_t> atoms_log;
+  uint64_t host_atoms_ver = ~0ull, dev_atoms_ver = ~0ull;
   // spot nodes changed since tables_state_gen (valid: every state step since was one the encoder patched)
   std::vector<int32_t> dirty;
   bool dirty_valid = false;
@@ -335,14 +342,36 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const bool dyn = !w.dyn_cand.empty();
   const size_t o_dc = dyn ? pk.add(w.dyn_cand) : 0, o_dp = dyn ? pk.add(w.dyn_pod) : 0;
   const size_t o_dd = dyn ? pk.add(w.dk_dom) : 0, o_di = dyn ? pk.add(w.ds_info) : 0;
-  const size_t o_st = dyn ? pk.add(w.sp_tab) : 0;
   const bool ext = !w.ext_cand.empty();
   const size_t o_ec = ext ? pk.add(w.ext_cand) : 0, o_ep = ext ? pk.add(w.pod_ext) : 0;
   const size_t o_le = ext ? pk.add(w.list_ext) : 0;
-  const size_t tick_from = pk.size();
-  const size_t o_ns = ext ? pk.add(w.node_scal) : 0;  // the spot nodes' scalar usage: state, so every tick
+  // the tick section: the atoms (rows a reuse encode changed go up alone),
+  // then what follows the spot nodes' state every tick
   const size_t o_at = pk.add(w.atoms);
+  const size_t tick_rest = pk.size();
+  const size_t o_ns = ext ? pk.add(w.node_scal) : 0;  // the spot nodes' scalar usage
+  const size_t o_st = dyn ? pk.add(w.sp_tab) : 0;     // the domain path's base counts
   const size_t o_tt = pk.add(w.t_thr);
+  // the atom-row log (see Slot)
+  if (w.atoms_ver != sl.last_atoms_ver) {
+    const bool follows = w.reused && !w.atom_rows_all && w.atoms_prev_ver == sl.last_atoms_ver;
+    if (follows && sl.atoms_log_ver != ~0ull) {
+      sl.atoms_log.insert(sl.atoms_log.end(), w.atom_rows.begin(), w.atom_rows.end());
+    } else if (follows) {
+      sl.atoms_log_ver = sl.last_atoms_ver;
+      sl.atoms_log = w.atom_rows;
+    } else {
+      sl.atoms_log_ver = ~0ull;
+      sl.atoms_log.clear();
+    }
+    if (sl.atoms_log.size() > 256) {
+      sl.atoms_log_ver = ~0ull;
+      sl.atoms_log.clear();
+    }
+    sl.last_atoms_ver = w.atoms_ver;
+  }
+  if (!w.reused || sl.dev_cand_gen != w.cand_gen) sl.atom_cols.clear();
+  else sl.atom_cols.insert(sl.atom_cols.end(), w.atom_cols.begin(), w.atom_cols.end());
   // ---- the slot's device state against this call.  Spot nodes changed since
   // the slot's tables were written, accumulated over K0-less runs:
   if (w.state_gen != sl.seen_gen) {
@@ -381,7 +410,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   constexpr size_t kSkipDirty = 16;
   const bool k0_skip = ctx->k0_skip && ncand > 0 && tables_cur && sl.dirty.size() <= kSkipDirty && !sl.class_flip &&
                        w.dyn_cand.empty() && w.max_cand_pods <= 256 && ctx->k2_mode == 0 &&
-                       sl.tables_atoms == w.atoms;
+                       sl.tables_atoms_ver == w.atoms_ver;
   // node patches {node, node_rec[8], node_free[3]}: the changed nodes' records
   // ride in the call's copy; K0 writes them into the node section (or K2 reads
   // them, K0-less)
@@ -416,6 +445,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   bool k0_inc = ctx->k0_incremental && tables_cur;  // (unused if the run turns out K0-less)
   if (k0_inc) {
     for (int32_t i : sl.dirty) kcols.push_back(i >> 6);
+    kcols.insert(kcols.end(), sl.atom_cols.begin(), sl.atom_cols.end());
     std::sort(kcols.begin(), kcols.end());
     kcols.erase(std::unique(kcols.begin(), kcols.end()), kcols.end());
     for (size_t r = 0; r < w.t_thr.size(); ++r)
@@ -432,10 +462,11 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   if (ctx->ev_upload) HIP_TRY(ctx, hipEventSynchronize(ctx->ev_upload));  // staging buffer free again
   const size_t h_cap = sl.h_arena.cap;
   HIP_TRY(ctx, host_reserve(sl.h_arena, bytes));
-  if (sl.h_arena.cap != h_cap) sl.host_state_gen = sl.host_cand_gen = ~0ull;  // a new staging buffer holds neither
+  if (sl.h_arena.cap != h_cap) sl.host_state_gen = sl.host_cand_gen = sl.host_atoms_ver = ~0ull;  // holds none
   const size_t arena_cap = sl.arena.cap;
   HIP_TRY(ctx, dev_reserve(sl.arena, bytes));  // a new allocation holds no node records
   const bool same_arena = sl.arena.cap == arena_cap;
+  if (!same_arena) sl.dev_atoms_ver = ~0ull;
   const bool nodes_resident = same_arena && sl.dev_state_gen == w.state_gen;
   // a reuse encode's candidate section is on the device: K0 re-points the
   // records that moved (a K0-less run reads them as they are)
@@ -490,14 +521,29 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   // the candidate section: kept in staging across a reuse encode (its pod
   // patches applied there too), packed again otherwise
   char* hs = static_cast<char*>(sl.h_arena.p);
+  const size_t row_bytes8 = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
+  auto log_rows = [&](uint64_t have) {  // the rows a copy of version `have` lacks (null: every row)
+    return have == w.atoms_ver ? &sl.atoms_log  // (unused)
+           : sl.atoms_log_ver != ~0ull && have == sl.atoms_log_ver ? &sl.atoms_log : nullptr;
+  };
   if (w.reused && sl.host_cand_gen == w.cand_gen) {
     for (size_t i = 0; i < w.pod_patch.size(); i += sr::kPodPatchWords)
       std::memcpy(hs + o_prec + (static_cast<size_t>(w.pod_patch[i]) * 6 + 4) * 8, &w.pod_patch[i + 1], 16);
-    pk.copy_to(hs, tick_from);
+    if (sl.host_atoms_ver != w.atoms_ver) {
+      const std::vector<int32_t>* rows = log_rows(sl.host_atoms_ver);
+      if (rows) {
+        for (int32_t r : *rows)
+          std::memcpy(hs + o_at + static_cast<size_t>(r) * row_bytes8, w.atoms.data() + static_cast<size_t>(r) * w.Wp, row_bytes8);
+      } else {
+        std::memcpy(hs + o_at, w.atoms.data(), w.atoms.size() * sizeof(uint64_t));
+      }
+    }
+    pk.copy_to(hs, tick_rest);
   } else {
     pk.copy_to(hs, node_bytes);
   }
   sl.host_cand_gen = w.cand_gen;
+  sl.host_atoms_ver = w.atoms_ver;
   if (!cand_resident) {  // the records go up whole, current: nothing pending, but rows to write
     sl.pending.clear();
     std::fill(sl.pending_mark.begin(), sl.pending_mark.end(), 0);
@@ -505,12 +551,31 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
     sl.need_k0 = true;
   }
   char* dv = static_cast<char*>(sl.arena.p);
+  size_t atoms_up = tick_rest - o_at;  // atom bytes uploaded
   if (!cand_resident) {
     HIP_TRY(ctx, hipMemcpyAsync(dv + from, hs + from, bytes - from, hipMemcpyHostToDevice, ctx->stream));
   } else {
     if (from < node_bytes)
       HIP_TRY(ctx, hipMemcpyAsync(dv, hs, node_bytes, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(dv + tick_from, hs + tick_from, bytes - tick_from, hipMemcpyHostToDevice, ctx->stream));
+    // the atoms: current, a few rows behind (each row alone), or whole
+    const std::vector<int32_t>* rows = sl.dev_atoms_ver == w.atoms_ver ? nullptr : log_rows(sl.dev_atoms_ver);
+    if (sl.dev_atoms_ver == w.atoms_ver) {
+      atoms_up = 0;
+    } else if (rows && rows->size() <= 32) {
+      for (int32_t r : *rows) {
+        const size_t o = o_at + static_cast<size_t>(r) * row_bytes8;
+        HIP_TRY(ctx, hipMemcpyAsync(dv + o, hs + o, row_bytes8, hipMemcpyHostToDevice, ctx->stream));
+      }
+      atoms_up = rows->size() * row_bytes8;
+    } else {
+      HIP_TRY(ctx, hipMemcpyAsync(dv + o_at, hs + o_at, tick_rest - o_at, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(dv + tick_rest, hs + tick_rest, bytes - tick_rest, hipMemcpyHostToDevice, ctx->stream));
+  }
+  sl.dev_atoms_ver = w.atoms_ver;
+  if (sl.host_atoms_ver == w.atoms_ver) {  // both copies current: the log starts again here
+    sl.atoms_log_ver = w.atoms_ver;
+    sl.atoms_log.clear();
   }
   if (!ctx->ev_upload) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_upload, hipEventDisableTiming));
   HIP_TRY(ctx, hipEventRecord(ctx->ev_upload, ctx->stream));  // kernels queue behind the copy
@@ -603,7 +668,8 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, hipHostGetDevicePointer(&dres, ctx->h_early.p, 0));
   ctx->d_early = static_cast<uint64_t*>(dres);
   d.res_stat = d.res_map = nullptr;  // set per run
-  ctx->t.bytes_uploaded = static_cast<uint64_t>(cand_resident ? (from < node_bytes ? node_bytes : 0) + bytes - tick_from
+  ctx->t.bytes_uploaded = static_cast<uint64_t>(cand_resident ? (from < node_bytes ? node_bytes : 0) + atoms_up +
+                                                                   bytes - tick_rest
                                                                : bytes - from);
   // K0 writes the patches into the node section; a K0-less run's K2 reads them
   // (every changed node, whether or not the section went up whole)
@@ -824,7 +890,8 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
       sl.tables_cand_gen = w.cand_gen;
       sl.tables_state_gen = sl.dev_state_gen = w.state_gen;
       if (sl.tables_thr != w.t_thr) sl.tables_thr = w.t_thr;
-      if (sl.tables_atoms != w.atoms) sl.tables_atoms = w.atoms;
+      sl.tables_atoms_ver = w.atoms_ver;
+      sl.atom_cols.clear();
       sl.dirty.clear();
       sl.dirty_valid = true;
       sl.seen_gen = w.state_gen;

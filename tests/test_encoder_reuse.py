@@ -110,3 +110,17 @@ def test_scalar_rows_turning_non_empty_flip_classes(tool):
     assert r["reused"] == r["ticks"], r["out"]
     flips = int(re.search(r"class flips (\d+)", r["out"]).group(1))
     assert flips >= 4, r["out"]
+
+
+@pytest.mark.parametrize("config", [2, 3])
+def test_affinity_variant_reuse(tool, config):
+    """The affinity variant (hostname anti-affinity, zone DoNotSchedule
+    spread): a reuse patches the DA / DB rows (AntiReuse: per node the pods'
+    (term, side) codes, per value the counts), the spread rows and the domain
+    path's base-count tables (SpreadReuse: per selector the nodes' counts) for
+    the changed nodes only.  The added pods are the candidates' own replicas,
+    so rows and tables move; every tick stays reused and equals a fresh encode
+    (its kept terms numbered by their words, so the atom layout is the same)."""
+    r = run_check(tool, config, 30, env={"SR_SYNTH_AFFINITY": "1"})
+    assert r["bad"] == 0, r["out"]
+    assert r["reused"] >= r["ticks"] * 3 // 4, r["out"]  # a DA / DB row turning (non-)empty re-encodes

@@ -473,3 +473,56 @@ def test_ticks_realistic_variant_reuse(checker, config):
             a[:] = b
         if h is not None:
             lib.sr_snapshot_destroy(h)
+
+
+def _with_extra(nm, n_nodes, extra):
+    """node_pod_off / node_pod_idx with the (pod, spot position) pairs of
+    `extra` appended to their spot nodes' lists (a pod of the cluster placed
+    there as well, as sr_snapshot_add_pod does)."""
+    add = {}
+    for pod, pos in extra:
+        add.setdefault(int(nm.spot[pos]), []).append(pod)
+    off, idx = [0], []
+    for n in range(n_nodes):
+        idx.extend(nm.node_pod_idx[nm.node_pod_off[n]:nm.node_pod_off[n + 1]].tolist())
+        idx.extend(add.get(n, []))
+        off.append(len(idx))
+    return np.asarray(off, np.int32), np.asarray(idx, np.int32)
+
+
+@pytest.mark.parametrize("config", [2, 3])
+def test_ticks_affinity_variant_reuse(checker, config):
+    """The affinity variant (Deployments with hostname anti-affinity and zone
+    DoNotSchedule spread): the candidates read the spot nodes' pods through
+    the DA / DB rows, the spread rows and the domain path's base counts.  Tick
+    after tick a fresh snapshot holds a changing set of extra replicas on
+    random spot nodes (added a few at a time, dropped every fifth tick); the
+    candidate side is reused (AntiReuse / SpreadReuse patch the changed nodes)
+    and every plan equals the oracle's."""
+    from spotplanner.synth import AFFINITY
+    sc = SynthCluster(config, seed=31, n_on_demand=150, n_spot=400, **AFFINITY)
+    lib = capi.load_planner()
+    nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+    rng = np.random.default_rng(config)
+    extra, reused = [], 0
+    for tick in range(12):
+        if tick % 5 == 4:
+            extra.clear()
+        for _ in range(int(rng.integers(1, 4))):
+            extra.append((int(rng.choice(cand_pods)), int(rng.integers(len(nm.spot)))))
+        off, idx = _with_extra(nm, sc.n_nodes, extra)
+        h = ctypes.c_void_p()
+        assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot), capi.ptr(off, capi.P32),
+                                      capi.ptr(idx, capi.P32), ctypes.byref(h)) == capi.SR_OK
+        try:
+            osnap = OracleSnapshot(sc.ptr, nm.spot, off, idx)
+            p = plan_arrays(checker, h, sc.ptr, cand_off, cand_pods)
+            reused += checker.timing().enc_reused
+            o = oracle_plan(osnap, sc.ptr, cand_off, cand_pods, mode=1, threads=8)
+            assert np.array_equal(p.status, o["status"]), tick
+            assert np.array_equal(p.node_of_pod, o["node_of_pod"]), tick
+            assert p.winner == o["winner"], tick
+        finally:
+            lib.sr_snapshot_destroy(h)
+    assert reused >= 6, reused

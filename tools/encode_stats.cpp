@@ -267,7 +267,13 @@ int main(int argc, char** argv) {
       auto fail = [&](const char* what, long i) {
         if (bad++ < 5) printf("tick %d (reused %d): %s differs at %ld\n", r, cache.last_reused, what, i);
       };
-      if (w.atoms != f.atoms) fail("atoms", 0);
+      if (w.atoms != f.atoms) {
+        long a = 0;
+        while (a < f.n_atoms && std::equal(f.atoms.begin() + a * f.Wp, f.atoms.begin() + (a + 1) * f.Wp, w.atoms.begin() + a * f.Wp)) ++a;
+        fail("atoms", a);
+      }
+      if (w.sp_tab != f.sp_tab) fail("spread tables", 0);
+      if (w.dyn_cand != f.dyn_cand || w.dyn_pod != f.dyn_pod || w.dk_dom != f.dk_dom) fail("domain path", 0);
       if (w.pod_src != f.pod_src || w.cand_off != f.cand_off || w.list != f.list || w.status_host != f.status_host)
         fail("candidate lists", 0);
       const int32_t nb = f.empty_class >= 0 ? f.empty_class : f.n_classes;  // classes before the empty one
