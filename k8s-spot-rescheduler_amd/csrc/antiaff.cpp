@@ -325,6 +325,16 @@ bool anti_reuse_patch(AntiReuse& R, const sr_snapshot* snap, const std::vector<i
   return true;
 }
 
+void anti_reuse_permute(AntiReuse& R, const std::vector<int32_t>& src, const std::vector<int32_t>& moved) {
+  permute_positions(R.contrib.data(), src, moved);
+  const std::vector<int32_t> to = permute_targets(R.n_spot, src, moved);
+  for (AntiReuse::KeyVals& K : R.keys) {
+    permute_positions(K.val.data(), src, moved);
+    for (auto& vn : K.nodes)
+      for (int32_t& m : vn.second) m = to[m];
+  }
+}
+
 void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands, int32_t Wp,
                   std::vector<int32_t>& status, DomKeys* dk, AntiTerms* out, std::shared_ptr<AntiReuse>* keep_state) {
   AntiTerms& at = *out;

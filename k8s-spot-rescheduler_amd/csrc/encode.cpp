@@ -640,6 +640,7 @@ bool permute_static(EncoderCache& C, const sr_snapshot* snap) {
   C.perm_k.clear();
   for (int32_t i = 0; i < n; ++i)
     if (C.perm_src[i] != i) C.perm_k.push_back(i);
+  C.perm_to = permute_targets(n, C.perm_src, C.perm_k);
   std::vector<int32_t> vals(C.perm_k.size());
   for (auto& kc : C.label_col) {
     std::vector<int32_t>& col = kc.second;
@@ -744,6 +745,10 @@ sr_status refresh_state(EncoderCache& C, const sr_snapshot* snap, std::string* e
   C.patched_from = ~0ull;
   C.patched_nodes.clear();
   ++C.state_gen;
+  // the nodes whose own state changed (a moved node's follows it): the
+  // reuse's inter-pod and spread states are permuted, then patched only there
+  C.content_from = full ? ~0ull : C.state_gen - 1;
+  C.content_nodes = changed;
   auto node_values = [&](int32_t i, int64_t out[3], int64_t* left) -> bool {
     const SpotNode& sn = snap->nodes[i];
     const NodeState& st = snap->state[i];
@@ -1270,8 +1275,7 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
   w->atom_rows.clear();
   w->atom_rows_all = false;
   std::vector<int32_t>& rows_moved = w->atom_rows;
-  // the inter-pod and spread states are kept per spot position
-  if ((R.anti || R.spread) && w->layout_gen != C.layout_gen) return false;
+
   // the host-decided outcomes that read the snapshot must still hold: scalar
   // usage known on every node, no planned candidate's attachable volume on a
   // spot node (only the nodes changed since the last encode can have one now;
@@ -1292,10 +1296,18 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
     }
   }
   if (w->layout_gen != C.layout_gen) {  // the spot order moved (permute_static): every atom row follows
-    std::vector<uint8_t> tmp;
-    for (int32_t a = 0; a < w->n_atoms; ++a) permute_row(C, A + static_cast<size_t>(a) * Wp, tmp);
+    for (int32_t a = 0; a < w->n_atoms; ++a) permute_bits(A + static_cast<size_t>(a) * Wp, Wp, C.perm_src, C.perm_k, C.perm_to);
     w->layout_gen = C.layout_gen;
     w->atom_rows_all = true;
+    // the inter-pod and spread states, the domain path's node domains and
+    // node-local base tables are kept per spot position too
+    if (R.anti) anti_reuse_permute(*R.anti, C.perm_src, C.perm_k);
+    if (R.spread) {
+      spread_reuse_permute(*R.spread, C.perm_src, C.perm_k, w->sp_tab);
+      w->tab_changed = true;
+    }
+    for (int32_t k = 0; k < w->n_dk; ++k)  // (a node-local key's domain is the position itself)
+      if (w->dk_row[k] >= 0) permute_positions(w->dk_dom.data() + static_cast<size_t>(k) * n_spot, C.perm_src, C.perm_k);
   }
   // pod count and the composites built on it, in the words where it changed
   std::vector<int32_t> words;
@@ -1387,8 +1399,8 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
   // (every node when the state view was rebuilt since this workload's encode)
   if ((R.anti || R.spread) && prev_state_gen != C.state_gen) {
     std::vector<int32_t> every;
-    const std::vector<int32_t>* nodes = &C.patched_nodes;
-    if (C.patched_from != prev_state_gen) {
+    const std::vector<int32_t>* nodes = &C.content_nodes;
+    if (C.content_from != prev_state_gen) {
       every.resize(static_cast<size_t>(n_spot));
       for (int32_t n = 0; n < n_spot; ++n) every[n] = n;
       nodes = &every;

@@ -330,6 +330,70 @@ void spread_reuse_slot(SpreadReuse& R, const std::vector<int32_t>& sel_words, co
 bool spread_reuse_patch(SpreadReuse& R, const sr_snapshot* snap, const std::vector<int32_t>& nodes, uint64_t* A,
                         std::vector<int32_t>& tab, bool* tab_changed, std::vector<int32_t>& atoms,
                         std::vector<int32_t>& words);
+// The spot order moved: the per-position state and the node-local table
+// entries of `tab` follow their nodes.
+void spread_reuse_permute(SpreadReuse& R, const std::vector<int32_t>& src, const std::vector<int32_t>& moved,
+                          std::vector<int32_t>& tab);
+// Position-indexed helpers of the permutations (src[i]: the previous position
+// of the node now at i; moved: the positions with src[i] != i).
+template <class T>
+void permute_positions(T* v, const std::vector<int32_t>& src, const std::vector<int32_t>& moved) {
+  std::vector<T> tmp(moved.size());
+  for (size_t q = 0; q < moved.size(); ++q) tmp[q] = std::move(v[src[moved[q]]]);
+  for (size_t q = 0; q < moved.size(); ++q) v[moved[q]] = std::move(tmp[q]);
+}
+// A [Wp] row whose bits follow their nodes: through the moved positions, or,
+// for a row with fewer set bits than that, through its set bits (`to`: new
+// position of every previous one).
+inline void permute_bits(uint64_t* row, int32_t Wp, const std::vector<int32_t>& src, const std::vector<int32_t>& moved,
+                         const std::vector<int32_t>& to) {
+  if (moved.size() <= 256) {  // few moved positions: through them
+    uint8_t tmp[256];
+    for (size_t q = 0; q < moved.size(); ++q) tmp[q] = static_cast<uint8_t>(row[src[moved[q]] >> 6] >> (src[moved[q]] & 63) & 1);
+    for (size_t q = 0; q < moved.size(); ++q) {
+      const int32_t i = moved[q];
+      const uint64_t bit = 1ull << (i & 63);
+      row[i >> 6] = tmp[q] ? (row[i >> 6] | bit) : (row[i >> 6] & ~bit);
+    }
+    return;
+  }
+  size_t pop = 0;
+  for (int32_t i = 0; i < Wp; ++i) pop += static_cast<size_t>(__builtin_popcountll(row[i]));
+  if (pop == 0) return;
+  if (pop < moved.size()) {
+    int32_t set[64];
+    size_t k = 0;
+    bool small = pop <= 64;
+    if (small) {
+      for (int32_t i = 0; i < Wp; ++i)
+        for (uint64_t m = row[i]; m; m &= m - 1) set[k++] = i * 64 + __builtin_ctzll(m);
+      for (int32_t i = 0; i < Wp; ++i) row[i] = 0;
+      for (size_t q = 0; q < k; ++q) row[to[set[q]] >> 6] |= 1ull << (to[set[q]] & 63);
+      return;
+    }
+    std::vector<int32_t> bits;
+    bits.reserve(pop);
+    for (int32_t i = 0; i < Wp; ++i)
+      for (uint64_t m = row[i]; m; m &= m - 1) bits.push_back(i * 64 + __builtin_ctzll(m));
+    for (int32_t i = 0; i < Wp; ++i) row[i] = 0;
+    for (int32_t b : bits) row[to[b] >> 6] |= 1ull << (to[b] & 63);
+    return;
+  }
+  std::vector<uint8_t> tmp(moved.size());
+  for (size_t q = 0; q < moved.size(); ++q) tmp[q] = static_cast<uint8_t>(row[src[moved[q]] >> 6] >> (src[moved[q]] & 63) & 1);
+  for (size_t q = 0; q < moved.size(); ++q) {
+    const int32_t i = moved[q];
+    const uint64_t bit = 1ull << (i & 63);
+    row[i >> 6] = tmp[q] ? (row[i >> 6] | bit) : (row[i >> 6] & ~bit);
+  }
+}
+// new position of every previous position
+inline std::vector<int32_t> permute_targets(int32_t n, const std::vector<int32_t>& src, const std::vector<int32_t>& moved) {
+  std::vector<int32_t> to(static_cast<size_t>(n));
+  for (int32_t i = 0; i < n; ++i) to[i] = i;
+  for (int32_t i : moved) to[src[i]] = i;
+  return to;
+}
 // The same by a scan of every snapshot pod (SR_SPREAD_CHECK=1 compares both).
 void spread_row_scan(const sr_snapshot* snap, const int32_t* words, const uint64_t* aff_row, uint32_t dmask,
                      uint64_t* row);
@@ -606,6 +670,7 @@ struct EncoderCache {
   // moved; perm_dirty hands them to the state view as changed nodes.
   uint64_t layout_gen = 0;
   std::vector<int32_t> perm_src, perm_k, perm_dirty, pos_scratch;
+  std::vector<int32_t> perm_to;  // new position of every previous one
   // ---- state view
   std::vector<uint64_t> state_fp;
   bool state_valid = false;  // the arrays below describe the current static view
@@ -663,6 +728,8 @@ struct EncoderCache {
   // patched_from (~0: it rebuilt them all); the planner uploads only those
   std::vector<int32_t> patched_nodes;
   uint64_t patched_from = ~0ull;
+  std::vector<int32_t> content_nodes;  // ... of which these changed their own state (not only their position)
+  uint64_t content_from = ~0ull;
   uint64_t cand_gen_next = 1;
   uint64_t atoms_ver_next = 1;  // Workload::atoms_ver
   int32_t last_reused = 0, last_pod_patches = 0;
@@ -739,6 +806,9 @@ void analyse_anti(const sr_snapshot* snap, const sr_cluster* c, const sr_candida
 // set that was empty when the class programs were emitted and no longer is.
 bool anti_reuse_patch(AntiReuse& R, const sr_snapshot* snap, const std::vector<int32_t>& nodes, uint64_t* A,
                       int32_t a_anti, std::vector<int32_t>& atoms, std::vector<int32_t>& words);
+// The spot order moved (EncoderCache::perm_src / perm_k): the per-position
+// state follows its nodes.
+void anti_reuse_permute(AntiReuse& R, const std::vector<int32_t>& src, const std::vector<int32_t>& moved);
 
 // Required pod affinity of one encode (antiaff.cpp).
 struct AffTerms {

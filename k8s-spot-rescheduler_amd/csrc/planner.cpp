@@ -341,7 +341,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t o_ls = pk.add(w.list);
   const bool dyn = !w.dyn_cand.empty();
   const size_t o_dc = dyn ? pk.add(w.dyn_cand) : 0, o_dp = dyn ? pk.add(w.dyn_pod) : 0;
-  const size_t o_dd = dyn ? pk.add(w.dk_dom) : 0, o_di = dyn ? pk.add(w.ds_info) : 0;
+  const size_t o_di = dyn ? pk.add(w.ds_info) : 0;
   const bool ext = !w.ext_cand.empty();
   const size_t o_ec = ext ? pk.add(w.ext_cand) : 0, o_ep = ext ? pk.add(w.pod_ext) : 0;
   const size_t o_le = ext ? pk.add(w.list_ext) : 0;
@@ -351,6 +351,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t tick_rest = pk.size();
   const size_t o_ns = ext ? pk.add(w.node_scal) : 0;  // the spot nodes' scalar usage
   const size_t o_st = dyn ? pk.add(w.sp_tab) : 0;     // the domain path's base counts
+  const size_t o_dd = dyn ? pk.add(w.dk_dom) : 0;     // ... and node domains (the spot order may move)
   const size_t o_tt = pk.add(w.t_thr);
   // the atom-row log (see Slot)
   if (w.atoms_ver != sl.last_atoms_ver) {

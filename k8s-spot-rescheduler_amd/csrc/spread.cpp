@@ -410,6 +410,28 @@ std::shared_ptr<SpreadReuse> spread_reuse_new(const sr_snapshot* snap, int32_t W
   return r;
 }
 
+void spread_reuse_permute(SpreadReuse& R, const std::vector<int32_t>& src, const std::vector<int32_t>& moved,
+                          std::vector<int32_t>& tab) {
+  permute_positions(R.node_nz.data(), src, moved);
+  const std::vector<int32_t> to = permute_targets(R.n_spot, src, moved);
+  for (SpreadReuse::Counter& C : R.ctr)
+    for (auto& e : C.nz) e.first = to[e.first];
+  for (auto& kv : R.keys) {
+    SpreadIndex::KeyView& v = kv.second;
+    permute_positions(v.val.data(), src, moved);
+    permute_positions(v.slot.data(), src, moved);
+    permute_bits(v.has.data(), R.Wp, src, moved, to);
+    for (size_t j = 0; j < v.values.size(); ++j) permute_bits(v.bits.data() + j * static_cast<size_t>(R.Wp), R.Wp, src, moved, to);
+  }
+  for (SpreadReuse::Query& q : R.queries) permute_bits(q.aff.data(), R.Wp, src, moved, to);
+  for (SpreadReuse::Slot& sl : R.slots)
+    if (sl.local) {
+      permute_bits(sl.pairs.data(), R.Wp, src, moved, to);
+      permute_positions(tab.data() + sl.off, src, moved);
+    }
+  for (auto& d : R.doms) permute_positions(d.data(), src, moved);
+}
+
 void spread_reuse_slot(SpreadReuse& R, const std::vector<int32_t>& sel_words, const std::vector<int32_t>& node_cnt,
                        uint32_t off, bool node_local, const std::vector<uint64_t>& pairs, int32_t skew, int32_t self,
                        int32_t n_counted, const std::vector<int32_t>& dom, uint64_t pm, int32_t edom) {

@@ -124,3 +124,14 @@ def test_affinity_variant_reuse(tool, config):
     r = run_check(tool, config, 30, env={"SR_SYNTH_AFFINITY": "1"})
     assert r["bad"] == 0, r["out"]
     assert r["reused"] >= r["ticks"] * 3 // 4, r["out"]  # a DA / DB row turning (non-)empty re-encodes
+
+
+def test_affinity_variant_reuse_survives_spot_order_moves(tool):
+    """The affinity variant with the spot order moving between ticks: the
+    AntiReuse / SpreadReuse states, the node-local base tables and the domain
+    path's node domains are permuted with the atom rows (anti_reuse_permute,
+    spread_reuse_permute), then patched for the nodes whose own pods changed."""
+    r = run_check(tool, 2, 40, env={"SR_SYNTH_AFFINITY": "1"}, mode="reuse-perm")
+    assert r["bad"] == 0, r["out"]
+    assert r["moved"] >= 20, r["out"]
+    assert r["reused"] >= r["ticks"] * 3 // 4, r["out"]
