@@ -622,8 +622,8 @@ def main():
             t3 = time.perf_counter()
             args_snap = (sc.ptr, capi.ptr(nm2.spot, capi.P32), len(nm2.spot), capi.ptr(nm2.node_pod_off, capi.P32),
                          capi.ptr(nm2.node_pod_idx, capi.P32))
-            if mode == "kept" and kept_snap is not None:
-                st = lib.sr_snapshot_refresh(kept_snap, *args_snap, ctypes.byref(rebuilt))
+            if mode == "kept" and kept_snap is not None:  # linked to this tick's cached node map
+                st = lib.sr_snapshot_refresh_cached(kept_snap, nm_cache, *args_snap, ctypes.byref(rebuilt))
                 snap2 = kept_snap
             else:
                 snap2 = ctypes.c_void_p()
@@ -692,7 +692,7 @@ def main():
                                                  for k, v in full_ticks["fresh"][1].items()}
             if full_ticks["fresh"][0] else None,
             "full_tick_span": "cluster arrays (one spot pod's cpu request changed since the previous tick) -> "
-                              "sr_new_node_map_cached -> sr_pods_for_deletion -> sr_snapshot_refresh of the "
+                              "sr_new_node_map_cached -> sr_pods_for_deletion -> sr_snapshot_refresh_cached of the "
                               "previous tick's snapshot -> sr_plan_first; fresh: sr_new_node_map and "
                               "sr_snapshot_create every tick"})
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SR_ABI_VERSION 7
+#define SR_ABI_VERSION 8
 
 /* ------------------------------------------------------------------ status */
 typedef int32_t sr_status;
@@ -475,6 +475,14 @@ sr_status sr_snapshot_create(const sr_cluster *cluster, const int32_t *spot_node
 sr_status sr_snapshot_refresh(sr_snapshot *snap, const sr_cluster *cluster, const int32_t *spot_nodes,
                               int32_t n_spot, const int32_t *node_pod_off, const int32_t *node_pod_idx,
                               int32_t *out_rebuilt);
+/* sr_snapshot_refresh when this tick's node map came from sr_new_node_map_cached(cache, ...) and `snap` was
+ * last refreshed (or rebuilt) by this call from the cache's previous node map and not changed since: a spot node
+ * whose LISTed pods that node map found unchanged (same non-zero stamps, same order) keeps its state without its
+ * pods' stamps being gathered again.  Otherwise (another cache, a skipped tick, an AddPod since) exactly
+ * sr_snapshot_refresh.  Either way `snap` ends up as sr_snapshot_create would build it. */
+sr_status sr_snapshot_refresh_cached(sr_snapshot *snap, const sr_node_map_cache *cache, const sr_cluster *cluster,
+                                     const int32_t *spot_nodes, int32_t n_spot, const int32_t *node_pod_off,
+                                     const int32_t *node_pod_idx, int32_t *out_rebuilt);
 void      sr_snapshot_destroy(sr_snapshot *snap);
 /* ClusterSnapshot.AddPod(pod, nodeName) (rescheduler.go:366); spot_pos = position in the NodeInfoArray. */
 sr_status sr_snapshot_add_pod(sr_snapshot *snap, const sr_cluster *cluster, int32_t pod, int32_t spot_pos);
@@ -501,7 +509,8 @@ const char *sr_build_info(void);
  * against before its first call and refuses to run on a mismatch, since the
  * library would otherwise read fields past the end of a shorter struct (ABI 5
  * added sr_cluster.volumes and pod_stamp; ABI 6 the sr_timing enc_reused /
- * enc_pod_patches counters, which sr_get_timing writes; ABI 7 sr_timing.ms_collective). */
+ * enc_pod_patches counters, which sr_get_timing writes; ABI 7 sr_timing.ms_collective; ABI 8
+ * sr_snapshot_refresh_cached). */
 int32_t     sr_abi_version(void);
 
 /* Batched findSpotNodeForPod (rescheduler.go:338-353): for each pod, the first

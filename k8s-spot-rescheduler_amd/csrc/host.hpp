@@ -37,6 +37,7 @@ struct TaintRec {
 // snapshot is created (AddNodeWithPods, nodes/nodes.go:229).
 struct SpotNode {
   uint64_t static_fp = 0;  // node_static_fp
+  uint64_t copy_fp = 0;    // fingerprint of the cluster fields it was copied from (0: copied anew every refresh)
   int32_t name = -1;
   int64_t alloc[3] = {0, 0, 0};  // milli-cpu, memory, ephemeral
   int64_t alloc_pods = 0;
@@ -205,6 +206,14 @@ struct sr_snapshot {
   // (cluster_shape) and a scratch map node name -> previous spot position
   uint64_t shape = 0;
   std::vector<int32_t> pos_of_name;
+  // sr_snapshot_refresh_cached: the node map cache call this snapshot was last
+  // refreshed from, and the version it had then (null: none)
+  const void* map_cache = nullptr;
+  uint64_t map_calls = 0, map_version = 0;
+  // the spot node indices of the last create / refresh, and a scratch map
+  // node index -> previous position (sr_snapshot_refresh: nodes keep their
+  // cluster index from tick to tick; the name is still checked)
+  std::vector<int32_t> spot_prev, pos_of_node;
 };
 
 namespace sr {

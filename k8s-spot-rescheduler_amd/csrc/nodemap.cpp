@@ -41,6 +41,11 @@ struct sr_node_map_cache {
   uint64_t shape = 0;
   sr_node_map_params params{};
   uint32_t epoch = 0;
+  // calls made (sr_snapshot_refresh_cached links a snapshot to one call), and
+  // whether the last one completed (scratch.hit: its nodes whose LISTed pods
+  // equal the previous call's)
+  uint64_t calls = 0;
+  bool hit_valid = false;
   std::vector<int32_t> slot_of_name;  // [n_strings] -> entries, -1
   std::vector<Entry> entries;
   std::vector<int32_t> names, slot;   // the last call's node names and their entries (-1: none)
@@ -101,6 +106,10 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   const sr_pods& P = c->pods;
   const int32_t nn = N.n, np = P.n;
   NM_START();
+  if (cache) {
+    ++cache->calls;
+    cache->hit_valid = false;
+  }
   // Per-node LIST results: counting sort by node index keeps list order.
   // Large clusters: K pod ranges counted and scattered in parallel, range k's
   // pods of a node placed after those of ranges < k (still list order).
@@ -371,6 +380,7 @@ static sr_status new_node_map(const sr_cluster* c, const sr_node_map_params* p, 
   }
   *out->n_spot = ns;
   *out->n_on_demand = nod;
+  if (cache) cache->hit_valid = stamps != nullptr && W.hit.size() == static_cast<size_t>(nn);
   NM_MARK(4);
   return SR_OK;
 }
@@ -541,6 +551,31 @@ static bool snapshot_input_ok(const sr_cluster* c, const int32_t* spot, int32_t 
 
 // The node AddNodeWithPods copies (nodes/nodes.go:229): allocatable,
 // labels, taints, scalar and volume limits.
+static inline uint64_t fp_mix(uint64_t h, uint64_t x) {
+  h = (h ^ x) * 0xff51afd7ed558ccdull;
+  return h ^ (h >> 32);
+}
+
+// Fingerprint of everything a snapshot's SpotNode copies from the cluster's
+// node (0: a node with scalar resources or volume limits, copied anew).
+static uint64_t cluster_node_fp(const sr_cluster* c, int32_t node) {
+  const sr_nodes& N = c->nodes;
+  if (c->node_scalar_off && c->node_scalar_off[node + 1] != c->node_scalar_off[node]) return 0;
+  if (c->volumes && c->volumes->limit_off[node + 1] != c->volumes->limit_off[node]) return 0;
+  uint64_t h = fp_mix(fp_mix(0xC0DEull, static_cast<uint32_t>(N.name[node])), N.unschedulable[node]);
+  h = fp_mix(fp_mix(fp_mix(h, static_cast<uint64_t>(N.alloc_milli_cpu[node])), static_cast<uint64_t>(N.alloc_memory[node])),
+             static_cast<uint64_t>(N.alloc_ephemeral[node]));
+  h = fp_mix(h, static_cast<uint64_t>(N.alloc_pods[node]));
+  h = fp_mix(h, static_cast<uint64_t>(N.label_off[node + 1] - N.label_off[node]));
+  for (int32_t j = N.label_off[node]; j < N.label_off[node + 1]; ++j)  // in order, as the copy holds them
+    h = fp_mix(h, static_cast<uint64_t>(static_cast<uint32_t>(N.label_key[j])) << 32 | static_cast<uint32_t>(N.label_val[j]));
+  h = fp_mix(h, static_cast<uint64_t>(N.taint_off[node + 1] - N.taint_off[node]));
+  for (int32_t j = N.taint_off[node]; j < N.taint_off[node + 1]; ++j)
+    h = fp_mix(fp_mix(h, static_cast<uint64_t>(static_cast<uint32_t>(N.taint_key[j])) << 32 | static_cast<uint32_t>(N.taint_val[j])),
+               static_cast<uint64_t>(N.taint_effect[j]));
+  return h | 1;  // never 0
+}
+
 static void spot_node_from(const sr_cluster* c, int32_t node, SpotNode& sn) {
   const sr_nodes& N = c->nodes;
   sn = SpotNode{};
@@ -564,6 +599,7 @@ static void spot_node_from(const sr_cluster* c, int32_t node, SpotNode& sn) {
     std::sort(sn.vol_limit.begin(), sn.vol_limit.end());
   }
   sn.static_fp = node_static_fp(sn, c);
+  sn.copy_fp = cluster_node_fp(c, node);
 }
 
 // AddNodeWithPods' pods for the spot positions `pos` (empty states): each
@@ -662,31 +698,15 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
   for (int32_t i = 0; i < n_spot; ++i) pos[i] = i;
   build_states(s, c, spot, off, idx, pos);
   finish_snapshot(s);
+  s->spot_prev.assign(spot, spot + n_spot);
   *out = s;
   return SR_OK;
 }
 
 // The snapshot's copy of `node` still equals the cluster's (nodes with scalar
 // resources or volume limits are copied anew).
-static bool spot_node_same(const sr_cluster* c, int32_t node, const SpotNode& sn) {
-  const sr_nodes& N = c->nodes;
-  if (sn.name != N.name[node] || sn.alloc[0] != N.alloc_milli_cpu[node] || sn.alloc[1] != N.alloc_memory[node] ||
-      sn.alloc[2] != N.alloc_ephemeral[node] || sn.alloc_pods != N.alloc_pods[node] ||
-      sn.unschedulable != N.unschedulable[node] || !sn.scalar_alloc.empty() || !sn.vol_limit.empty())
-    return false;
-  if (c->node_scalar_off && c->node_scalar_off[node + 1] != c->node_scalar_off[node]) return false;
-  if (c->volumes && c->volumes->limit_off[node + 1] != c->volumes->limit_off[node]) return false;
-  const int32_t l0 = N.label_off[node], nl = N.label_off[node + 1] - l0;
-  if (static_cast<int32_t>(sn.labels.size()) != nl) return false;
-  for (int32_t j = 0; j < nl; ++j)
-    if (sn.labels[j].first != N.label_key[l0 + j] || sn.labels[j].second != N.label_val[l0 + j]) return false;
-  const int32_t t0 = N.taint_off[node], nt = N.taint_off[node + 1] - t0;
-  if (static_cast<int32_t>(sn.taints.size()) != nt) return false;
-  for (int32_t j = 0; j < nt; ++j) {
-    const TaintRec& t = sn.taints[j];
-    if (t.key != N.taint_key[t0 + j] || t.val != N.taint_val[t0 + j] || t.effect != N.taint_effect[t0 + j]) return false;
-  }
-  return true;
+static inline bool spot_node_same(const sr_cluster* c, int32_t node, const SpotNode& sn) {
+  return sn.copy_fp != 0 && sn.copy_fp == cluster_node_fp(c, node);
 }
 
 // GetClusterSnapshot again on a snapshot built from an earlier call's cluster:
@@ -699,8 +719,18 @@ static bool spot_node_same(const sr_cluster* c, int32_t node, const SpotNode& sn
 // whole once dead entries outnumber live ones, or when the cluster's shape
 // changed.
 static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int32_t* spot, int32_t n_spot,
-                                  const int32_t* off, const int32_t* idx, int32_t* out_rebuilt) {
+                                  const int32_t* off, const int32_t* idx, int32_t* out_rebuilt,
+                                  const sr_node_map_cache* cache = nullptr) {
   if (s->forked) return SR_ERR_STATE;  // a forked snapshot is mid-simulation
+  // Linked to the node map cache (sr_snapshot_refresh_cached): the snapshot
+  // was last refreshed from the output of the cache's previous call and not
+  // changed since, so a node whose LISTed pods that call found unchanged
+  // (same non-zero stamps, same order: the same kept pods in the same sort)
+  // holds exactly those pods -- their stamps are not gathered again.
+  const bool linked = cache && cache->hit_valid && s->map_cache == cache && s->map_calls + 1 == cache->calls &&
+                      s->map_version == s->version && cache->scratch.hit.size() == static_cast<size_t>(c->nodes.n);
+  const uint8_t* hit = linked ? cache->scratch.hit.data() : nullptr;
+  s->map_cache = nullptr;
   if (n_spot < 0 || (n_spot > 0 && (!spot || !off || !idx))) return SR_ERR_INVALID_ARG;
   const uint64_t* stamps = c->pod_stamp;
   auto rebuild = [&]() {
@@ -708,12 +738,19 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
     const sr_status st = snapshot_create(c, spot, n_spot, off, idx, &t);
     if (st != SR_OK) return st;
     const uint64_t v = s->version;
-    std::vector<int32_t> scratch;
+    std::vector<int32_t> scratch, scratch2;
     scratch.swap(s->pos_of_name);
+    scratch2.swap(s->pos_of_node);
     *s = std::move(*t);
     delete t;
     s->pos_of_name.swap(scratch);
+    s->pos_of_node.swap(scratch2);
     s->version = v + 1;
+    if (cache && cache->hit_valid) {
+      s->map_cache = cache;
+      s->map_calls = cache->calls;
+      s->map_version = s->version;
+    }
     if (out_rebuilt) *out_rebuilt = n_spot;
     return SR_OK;
   };
@@ -724,32 +761,56 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
   // name claims the previous state once)
   const int32_t ns_str = c->n_strings, nn = c->nodes.n, np = c->pods.n;
   NM_START();
-  if (s->pos_of_name.size() < static_cast<size_t>(ns_str)) s->pos_of_name.resize(static_cast<size_t>(ns_str), -1);
   const int32_t n_old = static_cast<int32_t>(s->nodes.size());
-  for (int32_t o = 0; o < n_old; ++o) {
-    const int32_t nm = s->node_names[o];
-    if (nm >= 0 && nm < ns_str) s->pos_of_name[nm] = o;
-  }
   std::vector<int32_t> from(static_cast<size_t>(n_spot), -1);
-  bool bad = false;
-  for (int32_t i = 0; i < n_spot && !bad; ++i) {
-    if (spot[i] < 0 || spot[i] >= nn) {
-      bad = true;
-      break;
-    }
-    const int32_t nm = c->nodes.name[spot[i]];
-    if (nm < 0 || nm >= ns_str) continue;
-    const int32_t o = s->pos_of_name[nm];
-    if (o >= 0) {
-      from[i] = o;
-      s->pos_of_name[nm] = -1;  // claimed
-    }
-  }
-  for (int32_t o = 0; o < n_old; ++o) {
-    const int32_t nm = s->node_names[o];
-    if (nm >= 0 && nm < ns_str) s->pos_of_name[nm] = -1;
-  }
+  std::vector<uint8_t> claimed(static_cast<size_t>(n_old), 0);
+  bool bad = false, missed = false;
+  for (int32_t i = 0; i < n_spot && !bad; ++i) bad = spot[i] < 0 || spot[i] >= nn;
   if (bad) return SR_ERR_INVALID_ARG;
+  // by cluster node index first (a node keeps its index from tick to tick;
+  // an [nn] map instead of one over every string), the name checked
+  if (s->spot_prev.size() == static_cast<size_t>(n_old)) {
+    std::vector<int32_t>& pon = s->pos_of_node;
+    if (pon.size() < static_cast<size_t>(nn)) pon.resize(static_cast<size_t>(nn), -1);
+    for (int32_t o = 0; o < n_old; ++o)
+      if (s->spot_prev[o] >= 0 && s->spot_prev[o] < nn) pon[s->spot_prev[o]] = o;
+    for (int32_t i = 0; i < n_spot; ++i) {
+      const int32_t o = pon[spot[i]];
+      if (o >= 0 && s->node_names[o] == c->nodes.name[spot[i]] && c->nodes.name[spot[i]] >= 0) {
+        from[i] = o;
+        claimed[o] = 1;
+        pon[spot[i]] = -1;
+      } else {
+        missed = true;
+      }
+    }
+    for (int32_t o = 0; o < n_old; ++o)
+      if (s->spot_prev[o] >= 0 && s->spot_prev[o] < nn) pon[s->spot_prev[o]] = -1;
+  } else {
+    missed = n_spot > 0;
+  }
+  if (missed) {  // the rest by name (unique per cluster; a repeated name claims a previous state once)
+    if (s->pos_of_name.size() < static_cast<size_t>(ns_str)) s->pos_of_name.resize(static_cast<size_t>(ns_str), -1);
+    for (int32_t o = 0; o < n_old; ++o) {
+      const int32_t nm = s->node_names[o];
+      if (!claimed[o] && nm >= 0 && nm < ns_str) s->pos_of_name[nm] = o;
+    }
+    for (int32_t i = 0; i < n_spot; ++i) {
+      if (from[i] >= 0) continue;
+      const int32_t nm = c->nodes.name[spot[i]];
+      if (nm < 0 || nm >= ns_str) continue;
+      const int32_t o = s->pos_of_name[nm];
+      if (o >= 0) {
+        from[i] = o;
+        claimed[o] = 1;
+        s->pos_of_name[nm] = -1;  // claimed
+      }
+    }
+    for (int32_t o = 0; o < n_old; ++o) {
+      const int32_t nm = s->node_names[o];
+      if (nm >= 0 && nm < ns_str) s->pos_of_name[nm] = -1;
+    }
+  }
   NM_MARK(5);
   // Pass 1 (reads only): the input validated, per position whether the pods
   // and the static part stand
@@ -768,12 +829,16 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
     };
     if (lo < hi) prefetch_node(lo);
     for (size_t i = lo; i < hi && !b; ++i) {
-      if (i + 1 < hi) prefetch_node(i + 1);
+      if (i + 1 < hi && !(hit && hit[spot[i + 1]])) prefetch_node(i + 1);
       const int32_t node = spot[i], j0 = off[node], n = off[node + 1] - j0;
       my_live += static_cast<size_t>(n);
       const int32_t o = from[i];
       const NodeState* prev = o >= 0 ? &s->state[static_cast<size_t>(o)] : nullptr;
       bool same = prev && static_cast<int64_t>(prev->pods.size()) == n && prev->npods == n;
+      if (same && hit && hit[node]) {  // unchanged since the previous node map (linked): kept as it is
+        keep[i] = static_cast<uint8_t>(1 | (spot_node_same(c, node, s->nodes[static_cast<size_t>(o)]) ? 2 : 0));
+        continue;
+      }
       for (int32_t k = 0; k < n; ++k) {  // the pods validated and, while equal, their stamps compared
         const int32_t pod = idx[j0 + k];
         if (static_cast<uint32_t>(pod) >= static_cast<uint32_t>(np)) {
@@ -794,6 +859,22 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
   if (bad_pod.load()) return SR_ERR_INVALID_ARG;
   if (s->pods.size() > 2 * live.load() + 4096) return rebuild();  // mostly dead entries: compact
   NM_MARK(6);
+  // the totals follow the states: those not kept leave them (the rebuilt
+  // ones join below)
+  {
+    std::vector<uint8_t> state_kept(static_cast<size_t>(n_old), 0);
+    for (int32_t i = 0; i < n_spot; ++i)
+      if (keep[i] & 1) state_kept[from[i]] = 1;
+    for (int32_t o = 0; o < n_old; ++o) {
+      if (state_kept[o]) continue;
+      const NodeState& st = s->state[o];
+      s->anti_total -= st.anti;
+      s->opaque_total -= st.opaque;
+      s->unknown_total -= st.unknown;
+      s->scalar_unknown_total -= st.scalar_unknown;
+      s->term_unknown_total -= st.term_unknown;
+    }
+  }
   // Pass 2: kept states and copies move to their new positions (most stay
   // where they are: only the moved ones go through a side buffer), the rest
   // is built
@@ -846,15 +927,21 @@ static sr_status snapshot_refresh(sr_snapshot* s, const sr_cluster* c, const int
     if (keep[i] != 3) s->node_dfp[i] = node_state_fp(s->nodes[i], s->state[i]);
   s->saved.clear();
   s->saved_dfp.clear();
-  s->anti_total = s->opaque_total = s->unknown_total = s->scalar_unknown_total = s->term_unknown_total = 0;
-  for (const NodeState& st : s->state) {
+  for (int32_t i : pos) {
+    const NodeState& st = s->state[i];
     s->anti_total += st.anti;
     s->opaque_total += st.opaque;
     s->unknown_total += st.unknown;
     s->scalar_unknown_total += st.scalar_unknown;
     s->term_unknown_total += st.term_unknown;
   }
+  s->spot_prev.assign(spot, spot + n_spot);
   s->version++;
+  if (cache && cache->hit_valid) {  // the next cached refresh may skip this call's unchanged nodes
+    s->map_cache = cache;
+    s->map_calls = cache->calls;
+    s->map_version = s->version;
+  }
   NM_MARK(8);
   if (out_rebuilt) *out_rebuilt = static_cast<int32_t>(pos.size());
   return SR_OK;
@@ -892,6 +979,13 @@ sr_status sr_snapshot_create(const sr_cluster* cluster, const int32_t* spot_node
                              const int32_t* node_pod_off, const int32_t* node_pod_idx, sr_snapshot** out) {
   if (!cluster || !out) return SR_ERR_INVALID_ARG;
   return sr::snapshot_create(cluster, spot_nodes, n_spot, node_pod_off, node_pod_idx, out);
+}
+
+sr_status sr_snapshot_refresh_cached(sr_snapshot* snap, const sr_node_map_cache* cache, const sr_cluster* cluster,
+                                     const int32_t* spot_nodes, int32_t n_spot, const int32_t* node_pod_off,
+                                     const int32_t* node_pod_idx, int32_t* out_rebuilt) {
+  if (!snap || !cluster) return SR_ERR_INVALID_ARG;
+  return sr::snapshot_refresh(snap, cluster, spot_nodes, n_spot, node_pod_off, node_pod_idx, out_rebuilt, cache);
 }
 
 sr_status sr_snapshot_refresh(sr_snapshot* snap, const sr_cluster* cluster, const int32_t* spot_nodes,

@@ -313,6 +313,8 @@ def _declare_planner(lib):
     lib.sr_snapshot_create.restype = S
     lib.sr_snapshot_refresh.argtypes = [VP, PC, P32, ctypes.c_int32, P32, P32, P32]
     lib.sr_snapshot_refresh.restype = S
+    lib.sr_snapshot_refresh_cached.argtypes = [VP, VP, PC, P32, ctypes.c_int32, P32, P32, P32]
+    lib.sr_snapshot_refresh_cached.restype = S
     lib.sr_snapshot_destroy.argtypes = [VP]
     lib.sr_snapshot_destroy.restype = None
     lib.sr_snapshot_add_pod.argtypes = [VP, PC, ctypes.c_int32, ctypes.c_int32]
@@ -361,7 +363,8 @@ def _declare_planner(lib):
 
 # Every symbol include/sr_planner.h declares (checked by tests on CPU).
 EXPORTED = ["sr_new_node_map", "sr_node_map_cache_create", "sr_node_map_cache_destroy", "sr_new_node_map_cached",
-            "sr_node_has_label", "sr_pods_for_deletion", "sr_snapshot_create", "sr_snapshot_refresh", "sr_snapshot_destroy",
+            "sr_node_has_label", "sr_pods_for_deletion", "sr_snapshot_create", "sr_snapshot_refresh", "sr_snapshot_refresh_cached",
+            "sr_snapshot_destroy",
             "sr_snapshot_add_pod", "sr_snapshot_fork", "sr_snapshot_revert", "sr_snapshot_node_state",
             "sr_snapshot_num_nodes", "sr_create", "sr_destroy", "sr_last_error", "sr_build_info",
             "sr_abi_version", "sr_find_spot_nodes", "sr_can_drain_node", "sr_plan", "sr_plan_first", "sr_plan_prepare", "sr_plan_run",

@@ -367,8 +367,11 @@ def test_ticks_kept_node_map_and_snapshot(checker, config):
     """A long-running planner's housekeeping ticks: the cluster changes between
     ticks (pods change requests, move, leave; stamps with them), the node map
     comes from the node map cache and the snapshot is the previous tick's,
-    refreshed (sr_snapshot_refresh).  Every tick's node map equals the oracle's
-    and every plan equals the oracle's on a snapshot built from scratch."""
+    refreshed (sr_snapshot_refresh_cached, linked to the cache's node map:
+    the nodes it found unchanged are kept without gathering their stamps;
+    every third tick the plain sr_snapshot_refresh).  Every tick's node map
+    equals the oracle's and every plan equals the oracle's on a snapshot built
+    from scratch."""
     from oracle_lib import oracle_new_node_map
     sc = SynthCluster(config, seed=23, n_on_demand=200, n_spot=450)
     lib = capi.load_planner()
@@ -404,7 +407,10 @@ def test_ticks_kept_node_map_and_snapshot(checker, config):
                 assert lib.sr_snapshot_create(*args, ctypes.byref(h)) == capi.SR_OK
             else:
                 rebuilt = ctypes.c_int32()
-                assert lib.sr_snapshot_refresh(h, *args, ctypes.byref(rebuilt)) == capi.SR_OK
+                if tick % 3 == 2:
+                    assert lib.sr_snapshot_refresh(h, *args, ctypes.byref(rebuilt)) == capi.SR_OK
+                else:
+                    assert lib.sr_snapshot_refresh_cached(h, cache, *args, ctypes.byref(rebuilt)) == capi.SR_OK
                 rebuilt_total += rebuilt.value
             cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
             osnap = OracleSnapshot(sc.ptr, orc.spot, orc.node_pod_off, orc.node_pod_idx)

@@ -235,7 +235,12 @@ int main(int argc, char** argv) {
         sr_snapshot_add_pod(kept, &c, static_cast<int32_t>(rng.below(np)),
                             static_cast<int32_t>(rng.below(kept->nodes.size())));
       int32_t rebuilt = 0;
-      if (sr_snapshot_refresh(kept, &c, ref.spot.data(), ref.ns, ref.off.data(), ref.idx.data(), &rebuilt) != SR_OK) {
+      // mostly linked to the node map cache (sr_snapshot_refresh_cached), now and then the plain refresh
+      const sr_status rs = t % 7 == 2 ? sr_snapshot_refresh(kept, &c, ref.spot.data(), ref.ns, ref.off.data(),
+                                                             ref.idx.data(), &rebuilt)
+                                      : sr_snapshot_refresh_cached(kept, cache, &c, ref.spot.data(), ref.ns,
+                                                                    ref.off.data(), ref.idx.data(), &rebuilt);
+      if (rs != SR_OK) {
         printf("tick %d: refresh failed\n", t);
         return 2;
       }
@@ -261,12 +266,12 @@ int main(int argc, char** argv) {
          static_cast<double>(sorted_sum) / ticks, nn, bad, states_err);
 
   // timing: ticks with one pod's requests changed
-  std::vector<double> t_map, t_map_c, t_create, t_refresh;
+  std::vector<double> t_map, t_map_c, t_create, t_refresh, t_refresh_c;
   std::vector<double> ph[9], t_pfd;
   sr_pod_drain drain;
   sr_synth_drain(syn, &drain);
   const sr_drain_params dprm{0, 0, 1};
-  for (int r = 0; r < 15; ++r) {
+  for (int r = 0; r < 30; ++r) {
     mutate(0);
     sr_node_map m1 = ref.view(nn, np), m2 = got.view(nn, np);
     auto t0 = std::chrono::steady_clock::now();
@@ -283,11 +288,16 @@ int main(int argc, char** argv) {
     sr_snapshot_create(&c, ref.spot.data(), ref.ns, ref.off.data(), ref.idx.data(), &fresh);
     t_create.push_back(ms_since(t0));
     t0 = std::chrono::steady_clock::now();
-    sr_snapshot_refresh(kept, &c, ref.spot.data(), ref.ns, ref.off.data(), ref.idx.data(), nullptr);
-    t_refresh.push_back(ms_since(t0));
+    if (r < 15) {
+      sr_snapshot_refresh(kept, &c, ref.spot.data(), ref.ns, ref.off.data(), ref.idx.data(), nullptr);
+      t_refresh.push_back(ms_since(t0));
+    } else {  // linked to this tick's cached node map (the previous refresh was linked too, but the first)
+      sr_snapshot_refresh_cached(kept, cache, &c, ref.spot.data(), ref.ns, ref.off.data(), ref.idx.data(), nullptr);
+      t_refresh_c.push_back(ms_since(t0));
 #ifdef SR_NM_PROFILE
-    for (int k = 5; k < 9; ++k) ph[k].push_back(sr::nm_phase_ms[k]);
+      for (int k = 5; k < 9; ++k) ph[k].push_back(sr::nm_phase_ms[k]);
 #endif
+    }
     {  // the candidate lists of the tick (podsForDeletion over the on-demand nodes)
       std::vector<int32_t> coff(ref.nod + 1), cpods(std::max(1, ref.off.back())), bp(std::max(1, ref.nod)),
           br(std::max(1, ref.nod));
@@ -302,12 +312,13 @@ int main(int argc, char** argv) {
     std::sort(v.begin(), v.end());
     return v[v.size() / 2];
   };
-  printf("one-pod ticks (median ms): new_node_map %.3f cached %.3f | snapshot_create %.3f refresh %.3f | "
-         "pods_for_deletion %.3f\n", med(t_map), med(t_map_c), med(t_create), med(t_refresh), med(t_pfd));
+  printf("one-pod ticks (median ms): new_node_map %.3f cached %.3f | snapshot_create %.3f refresh %.3f cached %.3f | "
+         "pods_for_deletion %.3f\n", med(t_map), med(t_map_c), med(t_create), med(t_refresh), med(t_refresh_c),
+         med(t_pfd));
 #ifdef SR_NM_PROFILE
   printf("cached node map phases (median ms): LIST grouping %.3f kinds+slots %.3f pass1 %.3f pass2 %.3f lists %.3f\n",
          med(ph[0]), med(ph[1]), med(ph[2]), med(ph[3]), med(ph[4]));
-  printf("refresh phases (median ms): by name %.3f pass1 %.3f pass2 %.3f rebuild+totals %.3f\n", med(ph[5]),
+  printf("cached refresh phases (median ms): by name %.3f pass1 %.3f pass2 %.3f rebuild+totals %.3f\n", med(ph[5]),
          med(ph[6]), med(ph[7]), med(ph[8]));
 #endif
   sr_snapshot_destroy(kept);
