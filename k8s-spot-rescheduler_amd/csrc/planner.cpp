@@ -129,6 +129,16 @@ struct sr_ctx {
   int32_t k0_incremental = 1;  // SR_K0_INCREMENTAL=0: K0 always rewrites every row
   int32_t k0_skip = 1;         // SR_K0_SKIP=0: every run launches K0
   int32_t pod_heads = 0;       // SR_POD_HEADS=1: K0b writes pod heads K2 reads with the records (measured: no gain)
+  // SR_K2_SPLIT=0: one K2 launch.  Otherwise a workload with domain-path (or
+  // over-256-pod) candidates plans them on the general kernel on a second
+  // stream while the node-order kernel (fewer registers, several waves per
+  // SIMD) plans the rest, when the work list exceeds k2_split_min entries
+  // (below that the general kernel holds every wave at once: C3's affinity
+  // variant, 1,500 waves, K2 20 -> 39 us split; C4's, 15,000, 142 -> 89 us)
+  int32_t k2_split = 1;
+  int32_t k2_split_min = 4096;  // SR_K2_SPLIT_MIN
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint64_t run_count = 0;      // runs of this context: d_min alternates between two buffers
   bool dmin_ready[2] = {false, false};  // buffer reset by the previous run's K2 (a K0-less run needs it)
   sr::EncoderCache enc;      // what the encoder keeps across calls (encode.cpp)
@@ -911,7 +921,38 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   } else {
     d.res_stat = d.res_map = nullptr;
   }
-  HIP_TRY(ctx, sr::launch_placement(d, s, e1a, e1b));
+  // the split launch (see sr_ctx::k2_split): both kernels take their part
+  // of the work list (the node-order part first in it), the general one on
+  // stream2 between a fork and a join event
+  const int32_t n_node = w.n_list_node;
+  if (ctx->k2_split && d.dyn_cand && d.n_list > ctx->k2_split_min && n_node > 0 && n_node < d.n_list &&
+      d.k2_mode == 0 && d.k2_node_kernel &&
+      w.max_np_node >= 1 && w.max_np_node <= 256) {
+    if (!ctx->stream2) {
+      HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+      HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+      HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    }
+    sr::DevWorkload dp = d, dn = d;
+    dp.list = d.list + n_node;
+    dp.n_list = d.n_list - n_node;
+    dp.n_list_head = 0;
+    if (d.list_ext) dp.list_ext = d.list_ext + n_node;
+    dn.n_list = n_node;
+    dn.n_list_head = std::min(d.n_list_head, n_node);
+    dn.max_np = w.max_np_node;
+    dn.dyn_cand = nullptr;  // none of its candidates is on the domain path
+    if (e1a) HIP_TRY(ctx, hipEventRecord(e1a, s));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, s));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+    HIP_TRY(ctx, sr::launch_placement(dp, ctx->stream2, nullptr, nullptr));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
+    HIP_TRY(ctx, sr::launch_placement(dn, s, nullptr, nullptr));
+    HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0));
+    if (e1b) HIP_TRY(ctx, hipEventRecord(e1b, s));
+  } else {
+    HIP_TRY(ctx, sr::launch_placement(d, s, e1a, e1b));
+  }
   if (early) return finish_early(ctx, out);
   PAIR(2, e2a, e2b);
   if (collective) {
@@ -1061,6 +1102,8 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_K0_INCREMENTAL")) ctx->k0_incremental = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K0_SKIP")) ctx->k0_skip = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_POD_HEADS")) ctx->pod_heads = std::atoi(m) != 0;
+  if (const char* m = std::getenv("SR_K2_SPLIT")) ctx->k2_split = std::atoi(m) != 0;
+  if (const char* m = std::getenv("SR_K2_SPLIT_MIN")) ctx->k2_split_min = std::max(0, std::atoi(m));
   *out = ctx;
   return SR_OK;
 }
@@ -1074,6 +1117,10 @@ void sr_destroy(sr_ctx* ctx) {
                     &ctx->scratch})
     if (b->p) (void)hipFree(b->p);
   if (ctx->ev_upload) (void)hipEventDestroy(ctx->ev_upload);
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join})
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   for (HostBuf* b : {&ctx->h_result, &ctx->h_status, &ctx->h_node, &ctx->h_bytes, &ctx->h_early, &ctx->h_comm})
     if (b->p) (void)hipHostFree(b->p);
   for (auto& sl : ctx->slots) {
