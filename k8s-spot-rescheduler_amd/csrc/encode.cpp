@@ -2932,42 +2932,12 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   // makespan; the head goes first because a winner-only tick returns once the
   // candidates up to the winner are planned, and run() drains the first
   // drainable one (rescheduler.go:280-286) -- on a grid larger than the chip
-  // holds at once, low indices must not wait for a later dispatch round.
-  // Beyond the head, candidates likely to scan far go first: a pod that few
-  // spot nodes have room for (fewer than 1/16 of them in some dimension:
-  // the spot order runs from the busiest node, so its first fit -- or its
-  // failure -- lies far along its rows) makes its wave one of the longest.
+  // holds at once, low indices must not wait for a later dispatch round.  With
+  // domain-path candidates the node-order part comes first (n_list_node): a
+  // large list is planned by two kernels side by side (planner.cpp k2_split).
   {
     const size_t n_act = w->cand_off.size() - 1;
     const int32_t kListHead = list_head();
-    static const bool risk_first = [] {
-      const char* e = std::getenv("SR_LIST_RISK");
-      return !e || std::atoi(e) != 0;
-    }();
-    std::vector<uint8_t> risky;
-    if (risk_first && static_cast<int64_t>(n_act) > kListHead && n_spot >= 4096) {
-      std::vector<int32_t> room(w->t_thr.size(), n_spot);  // per T row: spot nodes with free >= its threshold
-      for (size_t r = 0; r < w->t_thr.size(); ++r) {
-        const int d = w->t_dim[r];
-        if (d > 2 || w->t_thr[r] == kTSpare) continue;
-        const std::vector<int64_t>& sf = C.sorted_free[d];
-        room[r] = static_cast<int32_t>(sf.end() - std::lower_bound(sf.begin(), sf.end(), w->t_thr[r]));
-      }
-      const int32_t few = n_spot / 16;
-      risky.assign(n_act, 0);
-      pfor(n_act, 256, [&](size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; ++i) {
-          if (static_cast<int32_t>(i) < kListHead) continue;
-          bool rk = false;
-          for (int32_t q = w->cand_off[i]; q < w->cand_off[i + 1] && !rk; ++q) {
-            const int32_t* r = &w->pod_rows[static_cast<size_t>(q) * 4];
-            if (r[0] == w->empty_class) continue;  // dead: found without a scan
-            rk = room[r[1]] < few || room[r[2]] < few || room[r[3]] < few;
-          }
-          risky[i] = rk ? 1 : 0;
-        }
-      });
-    }
     // candidates on the domain path or of more than 256 pods after the rest
     // (the general kernel plans them, beside the node-order kernel)
     auto node_kernel = [&](size_t i) {
@@ -2976,8 +2946,8 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
     const bool split = !w->dyn_cand.empty();
     auto bucket = [&](size_t i) {
       const int32_t len = w->cand_off[i + 1] - w->cand_off[i];
-      const int32_t part = static_cast<int32_t>(i) < kListHead ? 0 : !risky.empty() && risky[i] ? 1 : 2;
-      return (split && !node_kernel(i) ? 3 : 0) * (MAX_CAND_PODS + 1) + part * (MAX_CAND_PODS + 1) + MAX_CAND_PODS - len;
+      const int32_t part = (split && !node_kernel(i) ? 2 : 0) + (static_cast<int32_t>(i) < kListHead ? 0 : 1);
+      return part * (MAX_CAND_PODS + 1) + MAX_CAND_PODS - len;
     };
     w->n_list_node = 0;
     w->max_np_node = 0;
@@ -2987,7 +2957,7 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
           ++w->n_list_node;
           w->max_np_node = std::max(w->max_np_node, w->cand_off[i + 1] - w->cand_off[i]);
         }
-    std::vector<int32_t> cnt(6 * (MAX_CAND_PODS + 1) + 1, 0);
+    std::vector<int32_t> cnt(4 * (MAX_CAND_PODS + 1) + 1, 0);
     for (size_t i = 0; i < n_act; ++i) ++cnt[bucket(i)];
     for (size_t v = 0, acc = 0; v < cnt.size(); ++v) {
       const int32_t k = cnt[v];

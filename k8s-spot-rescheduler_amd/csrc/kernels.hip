@@ -87,10 +87,6 @@ __device__ __forceinline__ uint64_t eval_prog8(const int (&op)[8], const uint64_
   return acc;
 }
 
-// K2 far scans: a lone pod's next chunks loaded together (0: one chunk per round trip)
-#ifndef SR_K2_FAR_MULTI
-#define SR_K2_FAR_MULTI 1
-#endif
 constexpr int kSHead = 8;  // S-row words K0 writes when s_head_only (= K2's F head, kNH)
 
 // K0: bitmask rows.  Blocks [0, s_blocks): S rows, kSClasses classes per
@@ -1636,92 +1632,6 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
 #pragma unroll
         for (int g = 0; g < G; ++g) {
           uint64_t pend = ballot(((act[g] >> lane) & 1) && ptr[g] == n && unres[g]);
-#if SR_K2_FAR_MULTI
-          // One pod left to resolve: its next Q chunks in flight together
-          // instead of one chunk per round trip (a failing pod scans every
-          // chunk of a 548-word row; each round trip is ~3k cycles).
-          if (pend != 0 && (pend & (pend - 1)) == 0) {
-            const int j = __builtin_ctzll(pend);
-            pend = 0;
-            const uint64_t b01 = readlane64(r01[g], j), b23 = readlane64(r23[g], j);
-            const int64_t q0 = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc[g]), j));
-            const int64_t q1 = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm[g]), j));
-            const int64_t q2 = static_cast<int64_t>(readlane64(static_cast<uint64_t>(re[g]), j));
-            int op1[8];
-            uint32_t nop1 = 0;
-            if constexpr (HO) {
-#pragma unroll
-              for (int u = 0; u < 8; ++u) {
-                op1[u] = __builtin_amdgcn_readfirstlane(PG[(64 * g + j) * 8 + u]);
-                nop1 += op1[u] >= 0 ? 1u : 0u;
-              }
-            }
-            int nx = INT_MAX, rcb = -1;
-            uint64_t fw = 0, rm_ = 0;
-            for (int cb0 = (sw >> 6) << 6; rcb < 0 && cb0 < Wp; cb0 += 64 * Q) {  // wave-uniform
-              uint64_t x[Q][HO ? 11 : 4];
-#pragma unroll
-              for (int q = 0; q < Q; ++q) {
-                const int word = cb0 + 64 * q + lane;
-                const uint32_t wi = word >= sw && word < Wp ? static_cast<uint32_t>(word) : 0u;
-                if constexpr (HO) {
-#pragma unroll
-                  for (int u = 0; u < 8; ++u)
-                    x[q][u] = op1[u] >= 0 ? w.atoms[static_cast<size_t>(op1[u] >> 2) * Wp + wi] : 0ull;
-                  x[q][8] = tab[static_cast<uint32_t>(b01 >> 32) + wi];
-                  x[q][9] = tab[static_cast<uint32_t>(b23) + wi];
-                  x[q][10] = tab[static_cast<uint32_t>(b23 >> 32) + wi];
-                } else {
-                  x[q][0] = tab[static_cast<uint32_t>(b01) + wi];
-                  x[q][1] = tab[static_cast<uint32_t>(b01 >> 32) + wi];
-                  x[q][2] = tab[static_cast<uint32_t>(b23) + wi];
-                  x[q][3] = tab[static_cast<uint32_t>(b23 >> 32) + wi];
-                }
-              }
-#pragma unroll
-              for (int q = 0; q < Q; ++q) {
-                const int cb = cb0 + 64 * q;
-                if (rcb >= 0 || cb >= Wp) break;  // wave-uniform
-                const int word = cb + lane;
-                const bool wv = word >= sw && word < Wp;
-                uint64_t f, sw0;
-                if constexpr (HO) {
-                  uint64_t v8[8];
-#pragma unroll
-                  for (int u = 0; u < 8; ++u) v8[u] = x[q][u];
-                  sw0 = eval_prog8(op1, v8);
-                  f = sw0 & x[q][8] & x[q][9] & x[q][10];
-                } else {
-                  sw0 = x[q][0];
-                  f = x[q][0] & x[q][1] & x[q][2] & x[q][3];
-                }
-                if (w.k0_skip) f = fix_dirty(w, f, sw0, word, q0, q1, q2, (q0 | q1 | q2) == 0);
-                f = wv ? f : 0ull;
-                const uint64_t m = ballot(f != 0);
-                const uint64_t vw = ballot(wv);
-                const int upto = m != 0 ? __builtin_ctzll(m) : 63;
-                const uint64_t need = upto == 63 ? vw : vw & ((2ull << upto) - 1);
-                nbytes += (HO ? 8u * (nop1 + 3u) : 32u) * static_cast<uint32_t>(__builtin_popcountll(need));
-                if (m == 0 && cb + 64 < Wp) continue;  // nothing in this chunk: the next one
-                rcb = cb;
-                rm_ = m;
-                if (m != 0) {
-                  const int w2 = __builtin_ctzll(m);
-                  fw = readlane64(f, w2);
-                  nx = (cb + w2) * 64 + __builtin_ctzll(fw);
-                }
-              }
-            }
-            if (lane == j) {
-              fmask[g] = rm_;
-              fbase[g] = rcb;
-              ptr[g] = nx;
-              cur[g] = fw;
-              unres[g] = false;
-            }
-            if (nx == INT_MAX) dead = min(dead, 64 * g + j);
-          }
-#endif
           while (pend != 0) {
             int js[Q];
             uint64_t a01[Q], a23[Q];
