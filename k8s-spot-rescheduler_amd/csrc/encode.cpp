@@ -1296,7 +1296,11 @@ bool reuse_encode(EncoderCache& C, const sr_snapshot* snap, Workload* w, uint64_
     }
   }
   if (w->layout_gen != C.layout_gen) {  // the spot order moved (permute_static): every atom row follows
-    for (int32_t a = 0; a < w->n_atoms; ++a) permute_bits(A + static_cast<size_t>(a) * Wp, Wp, C.perm_src, C.perm_k, C.perm_to);
+    auto rows = [&](size_t lo, size_t hi) {
+      for (size_t a = lo; a < hi; ++a) permute_bits(A + a * Wp, Wp, C.perm_src, C.perm_k, C.perm_to);
+    };
+    if (w->n_atoms > 512) parallel_for(static_cast<size_t>(w->n_atoms), 256, rows);  // (inter-pod atoms: thousands)
+    else rows(0, static_cast<size_t>(w->n_atoms));
     w->layout_gen = C.layout_gen;
     w->atom_rows_all = true;
     // the inter-pod and spread states, the domain path's node domains and

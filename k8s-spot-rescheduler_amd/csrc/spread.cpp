@@ -421,9 +421,17 @@ void spread_reuse_permute(SpreadReuse& R, const std::vector<int32_t>& src, const
     permute_positions(v.val.data(), src, moved);
     permute_positions(v.slot.data(), src, moved);
     permute_bits(v.has.data(), R.Wp, src, moved, to);
-    for (size_t j = 0; j < v.values.size(); ++j) permute_bits(v.bits.data() + j * static_cast<size_t>(R.Wp), R.Wp, src, moved, to);
+    auto rows = [&](size_t lo, size_t hi) {
+      for (size_t j = lo; j < hi; ++j) permute_bits(v.bits.data() + j * static_cast<size_t>(R.Wp), R.Wp, src, moved, to);
+    };
+    if (v.values.size() > 512) parallel_for(v.values.size(), 256, rows);  // a node-local key: a row per node
+    else rows(0, v.values.size());
   }
-  for (SpreadReuse::Query& q : R.queries) permute_bits(q.aff.data(), R.Wp, src, moved, to);
+  auto aff_rows = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) permute_bits(R.queries[i].aff.data(), R.Wp, src, moved, to);
+  };
+  if (R.queries.size() > 512) parallel_for(R.queries.size(), 256, aff_rows);
+  else aff_rows(0, R.queries.size());
   for (SpreadReuse::Slot& sl : R.slots)
     if (sl.local) {
       permute_bits(sl.pairs.data(), R.Wp, src, moved, to);
