@@ -165,7 +165,6 @@ __device__ __forceinline__ void k0_common(const DevWorkload& w, int local_first_
     dm[0] = ~0ull;
     dm[1] = local_first_fallback < 0 ? ~0ull : static_cast<unsigned long long>(local_first_fallback) << 32;
     dm[2] = w.rank_next;
-    dm[3] = 0;  // the persistent K2's work-list counter
   }
 }
 
@@ -2341,7 +2340,6 @@ __device__ __forceinline__ void k2_finish(const DevWorkload& w, const K2Entry& x
     unsigned long long* dn = reinterpret_cast<unsigned long long*>(w.d_min_next);
     unsigned long long* dm = reinterpret_cast<unsigned long long*>(w.d_min);
     dn[0] = ~0ull;
-    dn[3] = 0;  // the next run's work-list counter (a K0-less run reads it as it is)
     dm[1] = w.first_fallback_local < 0 ? ~0ull : static_cast<unsigned long long>(w.first_fallback_local) << 32;
     dm[2] = w.rank_next;
   }
@@ -2468,45 +2466,33 @@ __global__ __launch_bounds__(256) void k2_node(DevWorkload w_arg, const int4* __
   (void)w_arg;
   extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
   const int wave = threadIdx.x >> 6;
-  int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * (blockDim.x >> 6)) + wave);
-  const int grid_waves = static_cast<int>(gridDim.x * (blockDim.x >> 6));
+  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * (blockDim.x >> 6)) + wave);
+  if (li >= n_list) return;
+  int4 xe = {-1, -1, -1, 0};
+  if (XT) xe = w.list_ext[li];  // issued with the entry: one round trip for both
+  const K2Entry x = k2_entry<PROF>(w, list, li);
   uint64_t* F = k2_lds + static_cast<size_t>(wave) * (64 * GMAX * kNHS + (w.s_head_only ? 64 * GMAX * 4 : 0));
-  // one entry per wave, or (k2_persist) entries until the list runs out:
-  // after its first, a wave takes the next untaken one from the counter (list
-  // order kept: the head's candidates are still planned first); every wave
-  // leaves once the counter passes the list's end
-  while (li < n_list) {
-    int4 xe = {-1, -1, -1, 0};
-    if (XT) xe = w.list_ext[li];  // issued with the entry: one round trip for both
-    const K2Entry x = k2_entry<PROF>(w, list, li);
-    K2Stats st;
-    int status = -1;
-    uint32_t nbytes = 0;
-    bool done = false;
-    if constexpr (XT) {
-      const int ebase = __builtin_amdgcn_readfirstlane(xe.x);
-      const int er0 = __builtin_amdgcn_readfirstlane(xe.y), er1 = __builtin_amdgcn_readfirstlane(xe.z);
-      if (ebase >= 0) {
-        if (GMAX == 1 || x.np <= 64)
-          k2_node_order<1, PROF, false, true>(w, F, x.p0, x.np, status, st, nbytes, ebase, er0, er1);
-        else if (GMAX == 2 || x.np <= 128)
-          k2_node_order<(GMAX >= 2 ? 2 : 1), PROF, WIDE, true>(w, F, x.p0, x.np, status, st, nbytes, ebase, er0, er1);
-        else k2_node_order<GMAX, PROF, WIDE, true>(w, F, x.p0, x.np, status, st, nbytes, ebase, er0, er1);
-        done = true;
-      }
-    }
-    if (!done) {
-      if (GMAX == 1 || x.np <= 64) k2_node_order<1, PROF>(w, F, x.p0, x.np, status, st, nbytes);
+  K2Stats st;
+  int status = -1;
+  uint32_t nbytes = 0;
+  if constexpr (XT) {
+    const int ebase = __builtin_amdgcn_readfirstlane(xe.x);
+    const int er0 = __builtin_amdgcn_readfirstlane(xe.y), er1 = __builtin_amdgcn_readfirstlane(xe.z);
+    if (ebase >= 0) {
+      if (GMAX == 1 || x.np <= 64)
+        k2_node_order<1, PROF, false, true>(w, F, x.p0, x.np, status, st, nbytes, ebase, er0, er1);
       else if (GMAX == 2 || x.np <= 128)
-        k2_node_order<(GMAX >= 2 ? 2 : 1), PROF, WIDE>(w, F, x.p0, x.np, status, st, nbytes);
-      else k2_node_order<GMAX, PROF, WIDE>(w, F, x.p0, x.np, status, st, nbytes);
+        k2_node_order<(GMAX >= 2 ? 2 : 1), PROF, WIDE, true>(w, F, x.p0, x.np, status, st, nbytes, ebase, er0, er1);
+      else k2_node_order<GMAX, PROF, WIDE, true>(w, F, x.p0, x.np, status, st, nbytes, ebase, er0, er1);
+      k2_finish<PROF>(w, x, status, 2, nbytes, st);
+      return;
     }
-    k2_finish<PROF>(w, x, status, 2, nbytes, st);
-    if (!w.k2_persist) break;
-    int nx = 0;
-    if ((threadIdx.x & 63) == 0) nx = static_cast<int>(atomicAdd(reinterpret_cast<unsigned int*>(w.d_min + 6), 1u));
-    li = __builtin_amdgcn_readlane(nx, 0) + grid_waves;
   }
+  if (GMAX == 1 || x.np <= 64) k2_node_order<1, PROF>(w, F, x.p0, x.np, status, st, nbytes);
+  else if (GMAX == 2 || x.np <= 128)
+    k2_node_order<(GMAX >= 2 ? 2 : 1), PROF, WIDE>(w, F, x.p0, x.np, status, st, nbytes);
+  else k2_node_order<GMAX, PROF, WIDE>(w, F, x.p0, x.np, status, st, nbytes);
+  k2_finish<PROF>(w, x, status, 2, nbytes, st);
 }
 
 // Launch with optional HIP events recorded by the dispatch itself
@@ -2533,26 +2519,6 @@ void launch(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, hipEvent
 #ifndef SR_K2_WIDE_HEADS
 #define SR_K2_WIDE_HEADS 1
 #endif
-// The grid of a node-order launch: a wave per entry, or (k2_persist) no more
-// blocks than the chip holds at once (the waves then loop over the list).
-template <typename K>
-dim3 k2_node_grid(K kernel, const DevWorkload& w, int wpb, size_t lds) {
-  const int n = w.n_list;
-  int blocks = (n + wpb - 1) / wpb;
-  if (w.k2_persist) {
-    static int cus = [] {
-      int dev = 0, c = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-      return c > 0 ? c : 256;
-    }();
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64 * wpb, lds) == hipSuccess && per_cu > 0)
-      blocks = std::min(blocks, per_cu * cus);
-  }
-  return dim3(static_cast<unsigned>(std::max(1, blocks)));
-}
-
 template <bool PROF>
 hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 template <bool PROF>
@@ -2565,17 +2531,15 @@ template <bool PROF>
 hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
   const int wpb = w.k2_wpb == 1 || w.k2_wpb == 2 ? w.k2_wpb : 4;  // waves per block
-  const dim3 block(64 * wpb);
+  const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
   const size_t lds = wpb * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
   const bool wide = SR_K2_WIDE_HEADS && n <= 2048;
   if (w.ext_cand) return launch_k2_node_xt_g<PROF>(w, G, s, ev0, ev1);  // some candidate has extension records
-#define SR_K2N(...) launch(__VA_ARGS__, k2_node_grid(__VA_ARGS__, w, wpb, lds), block, lds, s, ev0, ev1, w, w.list, n)
-  if (G == 1) SR_K2N(k2_node<1, PROF>);
-  else if (G == 2 && wide) SR_K2N(k2_node<2, PROF, true>);
-  else if (G == 2) SR_K2N(k2_node<2, PROF>);
-  else if (SR_K2_WIDE_HEADS) SR_K2N(k2_node<4, PROF, true>);
-  else SR_K2N(k2_node<4, PROF>);
-#undef SR_K2N
+  if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (G == 2 && wide) launch(k2_node<2, PROF, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (G == 2) launch(k2_node<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (SR_K2_WIDE_HEADS) launch(k2_node<4, PROF, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else launch(k2_node<4, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   return hipGetLastError();
 }
 template hipError_t launch_k2_node_g<false>(const DevWorkload&, int, hipStream_t, hipEvent_t, hipEvent_t);
@@ -2588,16 +2552,14 @@ template <bool PROF>
 hipError_t launch_k2_node_xt_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
   const int wpb = w.k2_wpb == 1 || w.k2_wpb == 2 ? w.k2_wpb : 4;
-  const dim3 block(64 * wpb);
+  const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
   const size_t lds = wpb * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
   const bool wide = SR_K2_WIDE_HEADS && n <= 2048;  // as launch_k2_node_g
-#define SR_K2N(...) launch(__VA_ARGS__, k2_node_grid(__VA_ARGS__, w, wpb, lds), block, lds, s, ev0, ev1, w, w.list, n)
-  if (G == 1) SR_K2N(k2_node<1, PROF, false, true>);
-  else if (G == 2 && wide) SR_K2N(k2_node<2, PROF, true, true>);
-  else if (G == 2) SR_K2N(k2_node<2, PROF, false, true>);
-  else if (SR_K2_WIDE_HEADS) SR_K2N(k2_node<4, PROF, true, true>);
-  else SR_K2N(k2_node<4, PROF, false, true>);
-#undef SR_K2N
+  if (G == 1) launch(k2_node<1, PROF, false, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (G == 2 && wide) launch(k2_node<2, PROF, true, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (G == 2) launch(k2_node<2, PROF, false, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else if (SR_K2_WIDE_HEADS) launch(k2_node<4, PROF, true, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else launch(k2_node<4, PROF, false, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   return hipGetLastError();
 }
 template hipError_t launch_k2_node_xt_g<false>(const DevWorkload&, int, hipStream_t, hipEvent_t, hipEvent_t);

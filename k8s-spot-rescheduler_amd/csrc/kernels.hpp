@@ -118,8 +118,6 @@ struct DevWorkload {
   int32_t k2_narrow;   // node order: 32-bit scaled window visits where every request allows (SR_K2_NARROW=0: never)
   int32_t k2_wpb;      // K2 waves per block (SR_K2_WPB: 1, 2 or 4 (default))
   int32_t k2_excl;     // node order: exclusive candidates placed with the taken-mask step (SR_K2_EXCL=0: never)
-  int32_t k2_persist;  // node-order kernel: as many waves as the chip holds, each taking work-list entries from
-                       // the d_min buffer's counter word (d_min[6..7]) until the list runs out (SR_K2_PERSIST)
   int32_t k2_mode;     // 0: node-order first fit where it applies (<= 64 pods, <= 64-word rows);
                        // 1: pod order everywhere (SR_K2_MODE=1, A/B measurement)
   uint64_t* prof;      // optional [n_cand][16] K2 + [kK0ProfWaves][2] K0 per-wave profile

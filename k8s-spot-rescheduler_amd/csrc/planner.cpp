@@ -168,7 +168,6 @@ struct sr_ctx {
   int32_t k2_narrow = 1;      // SR_K2_NARROW: 32-bit scaled window visits in node order (0: 64-bit only)
   int32_t k2_wpb = 4;         // SR_K2_WPB: K2 waves per block (1, 2, 4)
   int32_t k2_excl = 1;        // SR_K2_EXCL: exclusive candidates (one host port) with the taken-mask step
-  int32_t k2_persist = 0;     // SR_K2_PERSIST: node-order K2 as a work queue over as many waves as the chip holds
   int32_t k2_node_kernel = 1; // SR_K2_NODE_KERNEL: node-order-only K2 kernel when every candidate takes that path
   int32_t s_head_only = 1;    // SR_S_HEAD_ONLY: K0 writes S-row heads only on rows wider than 64 words (0: never)
 };
@@ -653,7 +652,6 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   d.k2_narrow = ctx->k2_narrow;
   d.k2_wpb = ctx->k2_wpb;
   d.k2_excl = ctx->k2_excl;
-  d.k2_persist = ctx->k2_persist;
   d.k2_node_kernel = ctx->k2_node_kernel;
   // Wide rows, every candidate on the node-order kernel (launch_k2's condition)
   // and every class program in its 8-slot record: K0 writes only the S-row
@@ -887,10 +885,8 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   d.d_min_next = static_cast<int32_t*>(ctx->dmin.p) + 8 * (1 - par);
   Slot& sl = *ctx->cur;
   if (d.k0_skip) {
-    if (!ctx->dmin_ready[par]) {  // no K2 of a previous run reset it: reset here
+    if (!ctx->dmin_ready[par])  // no K2 of a previous run reset it: reset here
       HIP_TRY(ctx, hipMemsetAsync(d.d_min, 0xff, sizeof(uint64_t), s));
-      HIP_TRY(ctx, hipMemsetAsync(d.d_min + 6, 0, sizeof(uint64_t), s));  // the work-list counter
-    }
   } else {
     if (d.pod_head) {  // K0, then K0b (the pod heads of the rows K0 wrote), timed together
       if (e0a) HIP_TRY(ctx, hipEventRecord(e0a, s));
@@ -1102,7 +1098,6 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* b = std::getenv("SR_PREFIX_BATCH")) ctx->prefix_batch = std::max(1, std::atoi(b));
   if (const char* m = std::getenv("SR_K2_WPB")) ctx->k2_wpb = std::atoi(m);
   if (const char* m = std::getenv("SR_K2_EXCL")) ctx->k2_excl = std::atoi(m) != 0;
-  if (const char* m = std::getenv("SR_K2_PERSIST")) ctx->k2_persist = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_PLAN_SLOTS")) ctx->n_slots = std::max(1, std::min(16, std::atoi(m)));
   if (const char* m = std::getenv("SR_K0_INCREMENTAL")) ctx->k0_incremental = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K0_SKIP")) ctx->k0_skip = std::atoi(m) != 0;
