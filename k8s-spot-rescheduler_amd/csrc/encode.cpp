@@ -2937,8 +2937,9 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   // candidates up to the winner are planned, and run() drains the first
   // drainable one (rescheduler.go:280-286) -- on a grid larger than the chip
   // holds at once, low indices must not wait for a later dispatch round.  A
-  // list longer than the chip holds at once goes in three parts, each in that
-  // order (Workload::n_list_g1): planned by kernels side by side.
+  // list longer than the chip holds at once, with domain-path candidates, goes
+  // in two parts, each in that order (Workload::n_list_node): planned by two
+  // kernels side by side.
   {
     const size_t n_act = w->cand_off.size() - 1;
     const int32_t kListHead = list_head();
@@ -2946,25 +2947,23 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
       const char* e = std::getenv("SR_K2_SPLIT_MIN");
       return e ? std::max(0, std::atoi(e)) : 4096;
     }();
-    auto part_of = [&](size_t i) {  // 0: node order, <= 64 pods; 1: node order, 65-256; 2: the rest
+    auto part_of = [&](size_t i) {  // 1: node order; 2: the rest (domain path, more than 256 pods)
       const int32_t len = w->cand_off[i + 1] - w->cand_off[i];
-      if ((!w->dyn_cand.empty() && w->dyn_cand[i] >= 0) || len > 256) return 2;
-      return len <= 64 ? 0 : 1;
+      return (!w->dyn_cand.empty() && w->dyn_cand[i] >= 0) || len > 256 ? 2 : 1;
     };
-    const bool split = static_cast<int64_t>(n_act) > split_min;
+    const bool split = static_cast<int64_t>(n_act) > split_min && !w->dyn_cand.empty();
     auto bucket = [&](size_t i) {
       const int32_t len = w->cand_off[i + 1] - w->cand_off[i];
       const int32_t part = (split ? 2 * part_of(i) : 0) + (static_cast<int32_t>(i) < kListHead ? 0 : 1);
       return part * (MAX_CAND_PODS + 1) + MAX_CAND_PODS - len;
     };
-    w->n_list_g1 = w->n_list_node = w->max_np_node = 0;
+    w->n_list_node = w->max_np_node = 0;
     if (split)
-      for (size_t i = 0; i < n_act; ++i) {
-        const int p = part_of(i);
-        w->n_list_g1 += p == 0 ? 1 : 0;
-        w->n_list_node += p <= 1 ? 1 : 0;
-        if (p == 1) w->max_np_node = std::max(w->max_np_node, w->cand_off[i + 1] - w->cand_off[i]);
-      }
+      for (size_t i = 0; i < n_act; ++i)
+        if (part_of(i) == 1) {
+          ++w->n_list_node;
+          w->max_np_node = std::max(w->max_np_node, w->cand_off[i + 1] - w->cand_off[i]);
+        }
     std::vector<int32_t> cnt(6 * (MAX_CAND_PODS + 1) + 1, 0);
     for (size_t i = 0; i < n_act; ++i) ++cnt[bucket(i)];
     for (size_t v = 0, acc = 0; v < cnt.size(); ++v) {

@@ -551,12 +551,11 @@ struct Workload {
   std::vector<int32_t> cand_src;     // index in the caller's candidate list
   std::vector<int32_t> list;  // [n][4] K2 work list {candidate, first pod, end pod, global}, longest first
   int32_t max_cand_pods = 0;
-  // A large work list in three parts (planner.cpp k2_split): the first
-  // n_list_g1 entries are node-order candidates of <= 64 pods (the leanest
-  // kernel, most waves per SIMD), up to n_list_node those of 65-256 pods
-  // (max_np_node the largest), then the rest (domain path, more pods: the
-  // general kernel).  0: one part, the list in plain order.
-  int32_t n_list_g1 = 0, n_list_node = 0, max_np_node = 0;
+  // A large work list with domain-path candidates in two parts (planner.cpp
+  // k2_split): the first n_list_node entries are node-order candidates
+  // (max_np_node their largest pod count), then the rest (domain path, more
+  // than 256 pods: the general kernel).  0: one part, the list in plain order.
+  int32_t n_list_node = 0, max_np_node = 0;
   // ---- domain path: candidates whose pods interact through a topology key
   // with shared domains (antiaff.cpp), planned by K2's k2_domain
   std::vector<int32_t> dyn_cand;  // [n_active] first record in dyn_pod, -1: other paths (empty: none)
@@ -625,7 +624,7 @@ struct Workload {
     swap_mask = 0;
     for (int32_t& t : t_off) t = 0;
     max_cand_pods = 0;
-    n_list_g1 = n_list_node = max_np_node = 0;
+    n_list_node = max_np_node = 0;
     first_fallback = -1;
     fallback_pods = 0;
     n_input_cand = n_input_pods = pod_base = 0;

@@ -131,10 +131,11 @@ struct sr_ctx {
   int32_t pod_heads = 0;       // SR_POD_HEADS=1: K0b writes pod heads K2 reads with the records (measured: no gain)
   // SR_K2_SPLIT=0: one K2 launch.  Otherwise a work list the encoder split
   // (more entries than SR_K2_SPLIT_MIN, 4096: more waves than the chip holds
-  // at once) is planned by kernels side by side: its <= 64-pod node-order
-  // candidates on the leanest kernel, the wider ones and the domain-path ones
-  // on a second stream (C3's affinity variant, 1,500 entries, split: K2 20 ->
-  // 39 us; C4's, 15,000: 142 -> 89 us)
+  // at once, with domain-path candidates) is planned by two kernels side by
+  // side: the node-order candidates on the node-order kernel (fewer
+  // registers, several waves per SIMD), the rest on the general kernel on a
+  // second stream (C4's affinity variant, 15,000 entries: K2 142 -> 89 us; C3's,
+  // 1,500, split too: 20 -> 39 us)
   int32_t k2_split = 1;
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -920,41 +921,31 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   } else {
     d.res_stat = d.res_map = nullptr;
   }
-  // the split launch (see sr_ctx::k2_split): the <= 64-pod node-order part
-  // on this stream (the leanest kernel), the wider node-order part and the
-  // general one after it on stream2, between a fork and a join event
-  const int32_t n1 = w.n_list_g1, n12 = w.n_list_node;
-  if (ctx->k2_split && n12 > 0 && d.k2_mode == 0 && d.k2_node_kernel && w.max_np_node <= 256) {
+  // the split launch (see sr_ctx::k2_split): the node-order part on this
+  // stream, the general one on stream2 between a fork and a join event
+  const int32_t n_node = w.n_list_node;
+  if (ctx->k2_split && n_node > 0 && n_node < d.n_list && d.k2_mode == 0 && d.k2_node_kernel &&
+      w.max_np_node >= 1 && w.max_np_node <= 256) {
     if (!ctx->stream2) {
       HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
       HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
       HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
     }
-    auto part = [&](int32_t from, int32_t to) {
-      sr::DevWorkload p = d;
-      p.list = d.list + from;
-      p.n_list = to - from;
-      p.n_list_head = from == 0 ? std::min(d.n_list_head, to) : 0;
-      if (d.list_ext) p.list_ext = d.list_ext + from;
-      return p;
-    };
+    sr::DevWorkload dp = d, dn = d;
+    dp.list = d.list + n_node;
+    dp.n_list = d.n_list - n_node;
+    dp.n_list_head = 0;
+    if (d.list_ext) dp.list_ext = d.list_ext + n_node;
+    dn.n_list = n_node;
+    dn.n_list_head = std::min(d.n_list_head, n_node);
+    dn.max_np = w.max_np_node;
+    dn.dyn_cand = nullptr;  // none of its candidates is on the domain path
     if (e1a) HIP_TRY(ctx, hipEventRecord(e1a, s));
     HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, s));
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
-    if (n12 > n1) {  // 65-256 pods, node order
-      sr::DevWorkload p = part(n1, n12);
-      p.max_np = w.max_np_node;
-      p.dyn_cand = nullptr;  // none of its candidates is on the domain path
-      HIP_TRY(ctx, sr::launch_placement(p, ctx->stream2, nullptr, nullptr));
-    }
-    if (d.n_list > n12) HIP_TRY(ctx, sr::launch_placement(part(n12, d.n_list), ctx->stream2, nullptr, nullptr));
+    HIP_TRY(ctx, sr::launch_placement(dp, ctx->stream2, nullptr, nullptr));
     HIP_TRY(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
-    if (n1 > 0) {
-      sr::DevWorkload p = part(0, n1);
-      p.max_np = std::min(d.max_np, 64);
-      p.dyn_cand = nullptr;
-      HIP_TRY(ctx, sr::launch_placement(p, s, nullptr, nullptr));
-    }
+    HIP_TRY(ctx, sr::launch_placement(dn, s, nullptr, nullptr));
     HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0));
     if (e1b) HIP_TRY(ctx, hipEventRecord(e1b, s));
   } else {
