@@ -1140,6 +1140,28 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
 
 }  // namespace
 
+void reorder_list_by_cost(Workload& w, const uint32_t* cycles) {
+  const size_t n = w.list.size() / 4;
+  const int32_t head = list_head();
+  auto part = [&](size_t j) {
+    return (w.n_list_node > 0 && static_cast<int32_t>(j) >= w.n_list_node ? 2 : 0) + (w.list[j * 4] < head ? 0 : 1);
+  };
+  std::vector<int32_t> order(n);
+  for (size_t j = 0; j < n; ++j) order[j] = static_cast<int32_t>(j);
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    const int pa = part(static_cast<size_t>(a)), pb = part(static_cast<size_t>(b));
+    if (pa != pb) return pa < pb;
+    return cycles[w.list[static_cast<size_t>(a) * 4]] > cycles[w.list[static_cast<size_t>(b) * 4]];
+  });
+  std::vector<int32_t> l(w.list.size()), x(w.list_ext.size());
+  for (size_t j = 0; j < n; ++j) {
+    std::copy_n(&w.list[static_cast<size_t>(order[j]) * 4], 4, &l[j * 4]);
+    if (!x.empty()) std::copy_n(&w.list_ext[static_cast<size_t>(order[j]) * 4], 4, &x[j * 4]);
+  }
+  w.list.swap(l);
+  if (!x.empty()) w.list_ext.swap(x);
+}
+
 uint64_t node_static_fp(const SpotNode& n, const sr_cluster* c) {
   uint64_t h = mix(mix(0xC0FFEEull, static_cast<uint32_t>(n.name)), n.unschedulable);
   uint64_t labels = 0, taints = 0;  // order-independent sums (Go map iteration order varies)

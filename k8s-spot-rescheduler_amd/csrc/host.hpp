@@ -874,6 +874,12 @@ struct SpreadDyn {
   bool state_fb = false;           // a candidate went to the reference path on the base counts (n0 <= counted)
 };
 
+// The work list of a reused workload in the order of each candidate's wave
+// duration in its last run (`cycles`, by active candidate), longest first,
+// within the parts the list was built in (the head, the rest; the split
+// launch's two kernels); list_ext follows.
+void reorder_list_by_cost(Workload& w, const uint32_t* cycles);
+
 // Builds the workload; returns SR_OK or an error with *err filled.  `cache`
 // carries what the previous calls derived (and is updated).
 sr_status encode_workload(EncoderCache* cache, const sr_snapshot* snap, const sr_cluster* c,

@@ -2317,7 +2317,7 @@ template <bool PROF>
 __device__ __forceinline__ K2Entry k2_entry(const DevWorkload& w, const int4* __restrict__ list, int li) {
   K2Entry x;
   x.t_start = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
-  x.c_start = PROF ? __builtin_amdgcn_s_memtime() : 0;
+  x.c_start = PROF || w.out_cycles ? __builtin_amdgcn_s_memtime() : 0;
   const int4 e = li < w.n_list_head ? w.list_head[li] : list[li];  // the head: with the kernel arguments
   x.ci = __builtin_amdgcn_readfirstlane(e.x);
   x.p0 = __builtin_amdgcn_readfirstlane(e.y);
@@ -2346,6 +2346,8 @@ __device__ __forceinline__ void k2_finish(const DevWorkload& w, const K2Entry& x
   if (lane == 0) {
     w.out_status[ci] = status;
     w.out_bytes[ci] = nbytes;
+    if (w.out_cycles)
+      w.out_cycles[ci] = static_cast<uint32_t>(min(__builtin_amdgcn_s_memtime() - x.c_start, 0xffffffffull));
     // packed (global candidate << 32 | local candidate): min = first drainable
     if (status < 0) {
       const unsigned long long key = (static_cast<unsigned long long>(x.g) << 32) | static_cast<unsigned>(ci);

@@ -102,6 +102,8 @@ struct DevWorkload {
   int32_t* out_node;   // [n_pods] spot position or -1
   int32_t* out_status; // [n_cand]
   uint32_t* out_bytes; // [n_cand] bytes K2 moved for the candidate (the roofline's algorithmic bytes)
+  uint32_t* out_cycles; // [n_cand] the candidate's wave duration in cycles (null: not recorded): the next
+                        // ticks' work list runs longest first by it (planner.cpp, list_cost)
   int32_t* d_min;      // 3 x u64, reduced (min) over the ranks: packed {global << 32 | local} first ok,
                        // first fallback (~0 = none), and the smallest global candidate index a rank has
                        // not planned yet (rank_next; ~0 = none)

@@ -91,6 +91,10 @@ struct Slot {
   uint64_t atoms_log_ver = ~0ull, last_atoms_ver = ~0ull;
   std::vector<int32_t> atoms_log;
   uint64_t host_atoms_ver = ~0ull, dev_atoms_ver = ~0ull;
+  // the work list by cost (sr_ctx::list_cost): the candidate generation whose
+  // K2 durations were copied back (ctx->h_cycles), and the one the list was
+  // reordered for
+  uint64_t cost_gen = ~0ull, list_sorted_gen = ~0ull;
   // spot nodes changed since tables_state_gen (valid: every state step since was one the encoder patched)
   std::vector<int32_t> dirty;
   bool dirty_valid = false;
@@ -137,6 +141,16 @@ struct sr_ctx {
   // second stream (C4's affinity variant, 15,000 entries: K2 142 -> 89 us; C3's,
   // 1,500, split too: 20 -> 39 us)
   int32_t k2_split = 1;
+  // SR_LIST_COST=0: the work list stays longest-first by pod count.  Otherwise
+  // the first run of a candidate generation records each candidate's K2 wave
+  // duration, and the reused workloads of the next ticks dispatch the longest
+  // waves first (a candidate whose pods scan far along their rows is short by
+  // pod count but one of the longest waves: C4's last-starting waves)
+  int32_t list_cost = 1;
+  DevBuf out_cycles;
+  HostBuf h_cycles;
+  hipEvent_t ev_cost = nullptr;
+  const void* cost_slot = nullptr;  // the slot whose durations h_cycles holds
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint64_t run_count = 0;      // runs of this context: d_min alternates between two buffers
@@ -470,6 +484,15 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   st = settle(ctx);
   if (st != SR_OK) return st;
+  // a reused workload's list in the order of its last run's K2 durations
+  bool list_moved = false;
+  if (ctx->list_cost && w.reused && ctx->cost_slot == &sl && sl.cost_gen == w.cand_gen &&
+      sl.list_sorted_gen != w.cand_gen) {
+    HIP_TRY(ctx, hipEventSynchronize(ctx->ev_cost));
+    sr::reorder_list_by_cost(w, static_cast<const uint32_t*>(ctx->h_cycles.p));
+    sl.list_sorted_gen = w.cand_gen;
+    list_moved = true;
+  }
   if (ctx->ev_upload) HIP_TRY(ctx, hipEventSynchronize(ctx->ev_upload));  // staging buffer free again
   const size_t h_cap = sl.h_arena.cap;
   HIP_TRY(ctx, host_reserve(sl.h_arena, bytes));
@@ -549,6 +572,10 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
         std::memcpy(hs + o_at, w.atoms.data(), w.atoms.size() * sizeof(uint64_t));
       }
     }
+    if (list_moved) {
+      std::memcpy(hs + o_ls, w.list.data(), w.list.size() * sizeof(int32_t));
+      if (ext) std::memcpy(hs + o_le, w.list_ext.data(), w.list_ext.size() * sizeof(int32_t));
+    }
     pk.copy_to(hs, tick_rest);
   } else {
     pk.copy_to(hs, node_bytes);
@@ -582,6 +609,13 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
       HIP_TRY(ctx, hipMemcpyAsync(dv + o_at, hs + o_at, tick_rest - o_at, hipMemcpyHostToDevice, ctx->stream));
     }
     HIP_TRY(ctx, hipMemcpyAsync(dv + tick_rest, hs + tick_rest, bytes - tick_rest, hipMemcpyHostToDevice, ctx->stream));
+    if (list_moved) {  // the reordered work list into the resident candidate section
+      HIP_TRY(ctx, hipMemcpyAsync(dv + o_ls, hs + o_ls, w.list.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                                  ctx->stream));
+      if (ext)
+        HIP_TRY(ctx, hipMemcpyAsync(dv + o_le, hs + o_le, w.list_ext.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                                    ctx->stream));
+    }
   }
   sl.dev_atoms_ver = w.atoms_ver;
   if (sl.host_atoms_ver == w.atoms_ver) {  // both copies current: the log starts again here
@@ -879,6 +913,17 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     sr_status pst = pair_for(0, &e0a, &e0b);
     if (pst != SR_OK) return pst;
   }
+  // the first run of a candidate generation records its K2 durations (list_cost)
+  Slot& slc = *ctx->cur;
+  const bool want_cost = ctx->list_cost && d.n_cand > 0 && slc.list_sorted_gen != w.cand_gen &&
+                         !(slc.cost_gen == w.cand_gen && ctx->cost_slot == &slc);
+  d.out_cycles = nullptr;
+  if (want_cost) {
+    HIP_TRY(ctx, dev_reserve(ctx->out_cycles, sizeof(uint32_t) * static_cast<size_t>(d.n_cand)));
+    HIP_TRY(ctx, host_reserve(ctx->h_cycles, sizeof(uint32_t) * static_cast<size_t>(d.n_cand)));
+    if (!ctx->ev_cost) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_cost, hipEventDisableTiming));
+    d.out_cycles = static_cast<uint32_t*>(ctx->out_cycles.p);
+  }
   // d_min alternates between two buffers: K0 resets this run's, K2 the next's
   const int par = static_cast<int>(ctx->run_count++ & 1);
   d.d_min = static_cast<int32_t*>(ctx->dmin.p) + 8 * par;
@@ -950,6 +995,13 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     if (e1b) HIP_TRY(ctx, hipEventRecord(e1b, s));
   } else {
     HIP_TRY(ctx, sr::launch_placement(d, s, e1a, e1b));
+  }
+  if (want_cost) {  // after K2 in stream order: the next prepare waits for it (ev_cost)
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_cycles.p, d.out_cycles, sizeof(uint32_t) * static_cast<size_t>(d.n_cand),
+                                hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_cost, s));
+    slc.cost_gen = w.cand_gen;
+    ctx->cost_slot = &slc;
   }
   if (early) return finish_early(ctx, out);
   PAIR(2, e2a, e2b);
@@ -1101,6 +1153,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_K0_SKIP")) ctx->k0_skip = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_POD_HEADS")) ctx->pod_heads = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K2_SPLIT")) ctx->k2_split = std::atoi(m) != 0;
+  if (const char* m = std::getenv("SR_LIST_COST")) ctx->list_cost = std::atoi(m) != 0;
   *out = ctx;
   return SR_OK;
 }
@@ -1118,6 +1171,9 @@ void sr_destroy(sr_ctx* ctx) {
   for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join})
     if (e) (void)hipEventDestroy(e);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  if (ctx->ev_cost) (void)hipEventDestroy(ctx->ev_cost);
+  if (ctx->out_cycles.p) (void)hipFree(ctx->out_cycles.p);
+  if (ctx->h_cycles.p) (void)hipHostFree(ctx->h_cycles.p);
   for (HostBuf* b : {&ctx->h_result, &ctx->h_status, &ctx->h_node, &ctx->h_bytes, &ctx->h_early, &ctx->h_comm})
     if (b->p) (void)hipHostFree(b->p);
   for (auto& sl : ctx->slots) {
