@@ -92,9 +92,11 @@ struct Slot {
   std::vector<int32_t> atoms_log;
   uint64_t host_atoms_ver = ~0ull, dev_atoms_ver = ~0ull;
   // the work list by cost (sr_ctx::list_cost): the candidate generation whose
-  // K2 durations were copied back (ctx->h_cycles), and the one the list was
-  // reordered for
+  // K2 durations were copied back (h_cycles, complete at ev_cost), and the one
+  // the list was reordered for
   uint64_t cost_gen = ~0ull, list_sorted_gen = ~0ull;
+  HostBuf h_cycles;
+  hipEvent_t ev_cost = nullptr;
   // spot nodes changed since tables_state_gen (valid: every state step since was one the encoder patched)
   std::vector<int32_t> dirty;
   bool dirty_valid = false;
@@ -148,9 +150,6 @@ struct sr_ctx {
   // pod count but one of the longest waves: C4's last-starting waves)
   int32_t list_cost = 1;
   DevBuf out_cycles;
-  HostBuf h_cycles;
-  hipEvent_t ev_cost = nullptr;
-  const void* cost_slot = nullptr;  // the slot whose durations h_cycles holds
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint64_t run_count = 0;      // runs of this context: d_min alternates between two buffers
@@ -486,10 +485,9 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   if (st != SR_OK) return st;
   // a reused workload's list in the order of its last run's K2 durations
   bool list_moved = false;
-  if (ctx->list_cost && w.reused && ctx->cost_slot == &sl && sl.cost_gen == w.cand_gen &&
-      sl.list_sorted_gen != w.cand_gen) {
-    HIP_TRY(ctx, hipEventSynchronize(ctx->ev_cost));
-    sr::reorder_list_by_cost(w, static_cast<const uint32_t*>(ctx->h_cycles.p));
+  if (ctx->list_cost && w.reused && sl.cost_gen == w.cand_gen && sl.list_sorted_gen != w.cand_gen) {
+    HIP_TRY(ctx, hipEventSynchronize(sl.ev_cost));
+    sr::reorder_list_by_cost(w, static_cast<const uint32_t*>(sl.h_cycles.p));
     sl.list_sorted_gen = w.cand_gen;
     list_moved = true;
   }
@@ -916,12 +914,12 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   // the first run of a candidate generation records its K2 durations (list_cost)
   Slot& slc = *ctx->cur;
   const bool want_cost = ctx->list_cost && d.n_cand > 0 && slc.list_sorted_gen != w.cand_gen &&
-                         !(slc.cost_gen == w.cand_gen && ctx->cost_slot == &slc);
+                         slc.cost_gen != w.cand_gen;
   d.out_cycles = nullptr;
   if (want_cost) {
     HIP_TRY(ctx, dev_reserve(ctx->out_cycles, sizeof(uint32_t) * static_cast<size_t>(d.n_cand)));
-    HIP_TRY(ctx, host_reserve(ctx->h_cycles, sizeof(uint32_t) * static_cast<size_t>(d.n_cand)));
-    if (!ctx->ev_cost) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_cost, hipEventDisableTiming));
+    HIP_TRY(ctx, host_reserve(slc.h_cycles, sizeof(uint32_t) * static_cast<size_t>(d.n_cand)));
+    if (!slc.ev_cost) HIP_TRY(ctx, hipEventCreateWithFlags(&slc.ev_cost, hipEventDisableTiming));
     d.out_cycles = static_cast<uint32_t*>(ctx->out_cycles.p);
   }
   // d_min alternates between two buffers: K0 resets this run's, K2 the next's
@@ -997,11 +995,10 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     HIP_TRY(ctx, sr::launch_placement(d, s, e1a, e1b));
   }
   if (want_cost) {  // after K2 in stream order: the next prepare waits for it (ev_cost)
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_cycles.p, d.out_cycles, sizeof(uint32_t) * static_cast<size_t>(d.n_cand),
+    HIP_TRY(ctx, hipMemcpyAsync(slc.h_cycles.p, d.out_cycles, sizeof(uint32_t) * static_cast<size_t>(d.n_cand),
                                 hipMemcpyDeviceToHost, s));
-    HIP_TRY(ctx, hipEventRecord(ctx->ev_cost, s));
+    HIP_TRY(ctx, hipEventRecord(slc.ev_cost, s));
     slc.cost_gen = w.cand_gen;
-    ctx->cost_slot = &slc;
   }
   if (early) return finish_early(ctx, out);
   PAIR(2, e2a, e2b);
@@ -1171,15 +1168,15 @@ void sr_destroy(sr_ctx* ctx) {
   for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join})
     if (e) (void)hipEventDestroy(e);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
-  if (ctx->ev_cost) (void)hipEventDestroy(ctx->ev_cost);
   if (ctx->out_cycles.p) (void)hipFree(ctx->out_cycles.p);
-  if (ctx->h_cycles.p) (void)hipHostFree(ctx->h_cycles.p);
   for (HostBuf* b : {&ctx->h_result, &ctx->h_status, &ctx->h_node, &ctx->h_bytes, &ctx->h_early, &ctx->h_comm})
     if (b->p) (void)hipHostFree(b->p);
   for (auto& sl : ctx->slots) {
     if (sl->arena.p) (void)hipFree(sl->arena.p);
     if (sl->tables.p) (void)hipFree(sl->tables.p);
     if (sl->h_arena.p) (void)hipHostFree(sl->h_arena.p);
+    if (sl->h_cycles.p) (void)hipHostFree(sl->h_cycles.p);
+    if (sl->ev_cost) (void)hipEventDestroy(sl->ev_cost);
   }
   for (auto* v : {&ctx->ev_start, &ctx->ev_end})
     for (hipEvent_t e : *v) (void)hipEventDestroy(e);
