@@ -149,6 +149,8 @@ struct sr_ctx {
   // waves first (a candidate whose pods scan far along their rows is short by
   // pod count but one of the longest waves: C4's last-starting waves)
   int32_t list_cost = 1;
+  int32_t list_cost_min = 2048;  // SR_LIST_COST_MIN: only lists longer than this (C4 15,000 entries: K2 69 -> 45 us;
+                                 // C3's 1,500 waves are all resident at once: within noise, or +0.5 us)
   DevBuf out_cycles;
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -913,7 +915,7 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   }
   // the first run of a candidate generation records its K2 durations (list_cost)
   Slot& slc = *ctx->cur;
-  const bool want_cost = ctx->list_cost && d.n_cand > 0 && slc.list_sorted_gen != w.cand_gen &&
+  const bool want_cost = ctx->list_cost && d.n_list > ctx->list_cost_min && slc.list_sorted_gen != w.cand_gen &&
                          slc.cost_gen != w.cand_gen;
   d.out_cycles = nullptr;
   if (want_cost) {
@@ -1151,6 +1153,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_POD_HEADS")) ctx->pod_heads = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K2_SPLIT")) ctx->k2_split = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_LIST_COST")) ctx->list_cost = std::atoi(m) != 0;
+  if (const char* m = std::getenv("SR_LIST_COST_MIN")) ctx->list_cost_min = std::max(0, std::atoi(m));
   *out = ctx;
   return SR_OK;
 }
