@@ -19,22 +19,23 @@ collective and K3:
           result itself, no K3).
 
 Sharding a fixed tick pays only when tick_strong(N) < tick(1): K2 must be
-throughput-bound well above its chain.  C4 (15,000 candidates, K2 68 us
-against a 41 us longest wave) is, up to the point where that wave and the
-collective dominate; C3 (1,500 candidates, a 12.2 us chain in a 13.8 us K2)
-is not, so a strong-scaled C3 tick on 8 GPUs is slower than on one.  `choose_scaling` makes that call per config for bench.py --scaling auto.
+throughput-bound well above its chain.  None of C1-C5 is any more: C4's
+K2 (15,000 candidates) is 46 us against a 43 us longest wave since its work
+list runs longest wave first, and C3 (1,500 candidates) is a 12.9 us chain in
+a 14.5 us K2, so a strong-scaled tick on 2-8 GPUs is slower than on one.  `choose_scaling` makes that call per config for bench.py --scaling auto.
 """
 
-# Measured on one MI355X at round 4's final head (profiles/r04/final/
-# c*_bench.json: kernels_ms.k2_placement = K2, ms_per_step - K2 = gap (>= 0);
-# c*_k2_wave_profile.txt: the longest wave = chain; C1 has no wave profile, its
-# 10 candidates are one chain).  K3 4.5 us (DESIGN §4).  Microseconds.
+# Measured on one MI355X in round 5 (profiles/r05/final/c*_bench.json:
+# kernels_ms.k2_placement = K2, ms_per_step - K2 = gap (>= 0);
+# c*_k2_wave_profile.txt: the longest wave = chain, at most K2).  K3 4.5 us
+# (DESIGN §4).  Microseconds.  C4's K2 is 45-46 us since its work list runs
+# longest wave first, against a 43 us longest wave: it no longer shards well.
 PARTS = {
-    1: dict(k2=7.1, chain=7.1, gap=6.4, k3=4.5),
-    2: dict(k2=18.6, chain=16.9, gap=0.7, k3=4.5),
-    3: dict(k2=13.8, chain=12.2, gap=2.6, k3=4.5),
-    4: dict(k2=67.8, chain=41.3, gap=0.0, k3=4.5),
-    5: dict(k2=36.9, chain=36.9, gap=0.5, k3=4.5),
+    1: dict(k2=8.2, chain=6.5, gap=6.5, k3=4.5),
+    2: dict(k2=19.2, chain=17.8, gap=0.3, k3=4.5),
+    3: dict(k2=14.5, chain=12.9, gap=3.1, k3=4.5),
+    4: dict(k2=46.4, chain=43.0, gap=0.0, k3=4.5),
+    5: dict(k2=38.0, chain=37.8, gap=0.5, k3=4.5),
 }
 
 # RCCL allreduce of 24 B over xGMI, per rank count.  ASSUMED, not measured:

@@ -132,8 +132,9 @@ def test_weak_scaling_multiplies_candidates_and_says_so(n):
 
 def test_bench_defaults_to_auto_scaling():
     # --scaling auto: the model (spotplanner/scaling.py) picks strong where the
-    # sharded tick beats one GPU's (C4), weak where K2 is chain-bound (C3)
+    # sharded tick beats one GPU's, weak where K2 is chain-bound (round 5: C3
+    # and C4 alike)
     src = open(os.path.join(REPO, "bench.py")).read()
     assert 'default="auto"' in src and '"scaling": args.scaling' in src
     from spotplanner.scaling import choose_scaling
-    assert choose_scaling(3, 8)[0] == "weak" and choose_scaling(4, 2)[0] == "strong"
+    assert choose_scaling(3, 8)[0] == "weak" and choose_scaling(4, 2)[0] == "weak"

@@ -38,10 +38,17 @@ def test_c3_does_not_shard_its_own_tick(n):
     assert scaling.choose_scaling(3, n)[0] == "weak"
 
 
-def test_c4_shards_its_own_tick_at_two_gpus():
-    r = scaling.predict(4, 2)
-    assert r["strong_pays"] and r["strong_tick_us"] < r["tick1_us"]
-    assert scaling.choose_scaling(4, 2)[0] == "strong"
+def test_throughput_bound_tick_shards():
+    # a K2 well above its chain (C4 before its work list ran longest wave first:
+    # 67.8 us against a 41.3 us wave) is shortened by splitting the candidates
+    p = dict(k2=67.8, chain=41.3, gap=0.0, k3=4.5)
+    assert scaling.predict_tick_us(p, 2, "strong") < scaling.predict_tick_us(p, 1, "strong")
+
+
+@pytest.mark.parametrize("c", [1, 2, 3, 4, 5])
+def test_round5_configs_keep_their_own_tick_whole(c):
+    # round 5: every config's K2 is within a few us of its longest wave
+    assert scaling.choose_scaling(c, 2)[0] == "weak"
 
 
 def test_efficiencies_follow_the_driver_rule():
