@@ -511,6 +511,8 @@ struct K2Stats {
   uint64_t cyc_a = 0, cyc_b = 0, cyc_c = 0, cyc_d = 0;
   uint64_t cyc_rec = 0;  // node order (profile builds): wave entry -> pod records in registers
   uint32_t narrow = 0;   // node order: the candidate's window visits use 32-bit scaled state
+  uint64_t cyc_res = 0;  // node order: far-pointer resolution (part of cyc_b) | rounds << 40
+  uint64_t cyc_win = 0;  // node order: window record loads waited for (part of cyc_b)
 };
 
 // One candidate's canDrainNode with 64 * SPL touched-node slots.  Returns the
@@ -1622,6 +1624,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       for (int g = 0; g < G; ++g) unres_n |= ballot(((act[g] >> lane) & 1) && ptr[g] == n && unres[g]);
     }
     if (unres_n != 0) {
+      const uint64_t cyc_r0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
       const int sw = n >> 6;  // first word to scan (every pending pod points at n)
       // Q pods per round, all their loads for one chunk in flight together:
       // 4 row words each, or (s_head_only) their programs' atom words and 3 T
@@ -1728,8 +1731,15 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
           }
         }
       };
+      // pods per round (A/B: 8 or 16 pods per round made the realistic
+      // variant's resolution slower, 21-28k cycles against 17.5k)
+#ifndef SR_K2_RES_Q
+#define SR_K2_RES_Q 4
+#endif
+      constexpr int kResQ = SR_K2_RES_Q;
       if (w.s_head_only) resolve(std::integral_constant<int, 2>{}, std::true_type{});
-      else resolve(std::integral_constant<int, 4>{}, std::false_type{});
+      else resolve(std::integral_constant<int, kResQ>{}, std::false_type{});
+      if (PROF) st.cyc_res += (__builtin_amdgcn_s_memtime() - cyc_r0) + (1ull << 40);
       any = 0;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
@@ -1741,6 +1751,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     ++visits;
     const int W = n >> 6;
     if (W != wcur) {  // wave-uniform
+      const uint64_t cyc_w0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
       const uint64_t* nr = w.node_rec + static_cast<size_t>(W * 64 + lane) * 8;
       ncpu = static_cast<int64_t>(nr[0]);
       nmem = static_cast<int64_t>(nr[1]);
@@ -1752,6 +1763,10 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       wcur = W;
       ++windows;
       nbytes += 64u * 40u;
+      if (PROF) {  // profile builds: the window's records (and node patches) waited for here
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st.cyc_win += __builtin_amdgcn_s_memtime() - cyc_w0;
+      }
     }
     if (PROF) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -2368,8 +2383,8 @@ __device__ __forceinline__ void k2_finish(const DevWorkload& w, const K2Entry& x
       pr[10] = st.cyc_c;
       pr[11] = st.cyc_d;
       if (wide == 2) {  // node order
-        pr[12] = 0;
-        pr[13] = 0;
+        pr[12] = st.cyc_res;
+        pr[13] = st.cyc_win;
         pr[14] = st.cyc_rec - x.c_start;
         pr[15] = st.narrow;
       }

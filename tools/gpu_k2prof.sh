@@ -1,12 +1,19 @@
 #!/bin/bash
-# K2 per-wave profile only (no test suite): tools/gpu_k2prof.sh [tag] [configs...]
-cd "$GRAFT_REPO_ROOT" || exit 2
-T=${1:-k2prof}; shift
-mkdir -p gpurun_out/$T
-for cfg in ${@:-3}; do
-  rm -f /tmp/k2prof_c$cfg.bin
-  SR_K2_PROFILE="/tmp/k2prof_c$cfg.bin" timeout -k 10 300 python bench.py --config $cfg --steps 3 --warmup 3 \
-    --e2e-reps 0 --no-cpu-baseline > gpurun_out/$T/bench_prof_c$cfg.log 2>&1 || exit $?
-  python tools/k2_profile.py /tmp/k2prof_c$cfg.bin > gpurun_out/$T/k2prof_c$cfg.txt 2>&1
-  echo "== C$cfg"; cat gpurun_out/$T/k2prof_c$cfg.txt; rm -f /tmp/k2prof_c$cfg.bin
+# K2 per-wave profiles only (SR_K2_PROFILE), per "cfg:variant":
+#   tools/gpu_k2prof.sh tag "3:realistic 3:baseline"
+tag=${1:-k2prof}; entries=${2:-3:baseline}
+R="$GRAFT_REPO_ROOT"
+cd "$R" || exit 2
+out="$R/gpurun_out/$tag"
+mkdir -p "$out"
+for e in $entries; do
+  cfg=${e%%:*}; var=${e#*:}
+  name="c${cfg}$([ "$var" = baseline ] || echo "_$var")"
+  rm -f "/tmp/k2prof_$name.bin"
+  SR_K2_PROFILE="/tmp/k2prof_$name.bin" timeout -k 10 300 python bench.py --config $cfg --variant $var --steps 3 \
+    --warmup 3 --e2e-reps 0 --no-cpu-baseline > "$out/${name}_bench_prof.log" 2>&1 || exit $?
+  python tools/k2_profile.py "/tmp/k2prof_$name.bin" > "$out/${name}_k2_wave_profile.txt" 2>&1
+  rm -f "/tmp/k2prof_$name.bin"
+  echo "== $name"; cat "$out/${name}_k2_wave_profile.txt"
 done
+exit 0
