@@ -511,7 +511,8 @@ struct K2Stats {
   uint64_t cyc_a = 0, cyc_b = 0, cyc_c = 0, cyc_d = 0;
   uint64_t cyc_rec = 0;  // node order (profile builds): wave entry -> pod records in registers
   uint32_t narrow = 0;   // node order: the candidate's window visits use 32-bit scaled state
-  uint64_t cyc_res = 0;  // node order: far-pointer resolution (part of cyc_b) | rounds << 40
+  uint64_t cyc_res = 0;  // node order: far-pointer resolution cycles (part of cyc_b) | chunk rounds << 40 | pods
+                         // found dead << 56
   uint64_t cyc_win = 0;  // node order: window record loads waited for (part of cyc_b)
 };
 
@@ -1667,6 +1668,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
               const int word = cb + lane;
               const bool wv = word >= sw && word < Wp;
               const uint32_t wi = wv ? static_cast<uint32_t>(word) : 0u;
+              if (PROF) st.cyc_res += 1ull << 40;  // chunk rounds
               uint64_t x[Q][HO ? 11 : 4];
 #pragma unroll
               for (int q = 0; q < Q; ++q) {
@@ -1726,6 +1728,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
                   unres[g] = false;
                 }
                 if (nx == INT_MAX) dead = min(dead, 64 * g + js[q]);
+                if (PROF && nx == INT_MAX) st.cyc_res += 1ull << 56;  // pods whose scan found no node
               }
             }
           }
@@ -1739,7 +1742,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       constexpr int kResQ = SR_K2_RES_Q;
       if (w.s_head_only) resolve(std::integral_constant<int, 2>{}, std::true_type{});
       else resolve(std::integral_constant<int, kResQ>{}, std::false_type{});
-      if (PROF) st.cyc_res += (__builtin_amdgcn_s_memtime() - cyc_r0) + (1ull << 40);
+      if (PROF) st.cyc_res += __builtin_amdgcn_s_memtime() - cyc_r0;
       any = 0;
 #pragma unroll
       for (int g = 0; g < G; ++g) {

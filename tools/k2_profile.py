@@ -91,8 +91,9 @@ def main():
               % (q[:, 9].sum() / sv, q[:, 10].sum() / sv, q[:, 11].sum() / sv))
         print("node order: placement cycles per placed pod %.0f" % (q[:, 10].sum() / max(1, q[:, 6].sum())))
         res = q[:, 12] & ((1 << 40) - 1)
-        print("node order: of min+window, far resolution %.0f cycles/visit (%d rounds), window loads %.0f cycles/visit"
-              % (res.sum() / sv, int((q[:, 12] >> 40).sum()), q[:, 13].sum() / sv))
+        print("node order: of min+window, far resolution %.0f cycles/visit (%d chunk rounds, %d pods found no node), "
+              "window loads %.0f cycles/visit" % (res.sum() / sv, int(((q[:, 12] >> 40) & 0xffff).sum()),
+                                                 int((q[:, 12] >> 56).sum()), q[:, 13].sum() / sv))
         print("node order: wave dur us p50/p90/max %s" % pct(dur[nodeo]))
         print("node order: 32-bit scaled window visits in %d of %d waves" % (int((q[:, 15] & 1).sum()), len(q)))
     if (~nodeo).any():
@@ -108,14 +109,14 @@ def main():
     last = np.argsort(-end)[:8]
     full = runs[last_run].astype(np.int64)
     print("latest-ending waves: wave start_us dur_us steps mode | visits placements windows | "
-          "cycles: entry->records prologue min+window placement moves | 32-bit | resolve (rounds) window-loads")
+          "cycles: entry->records prologue min+window placement moves | 32-bit | resolve (chunk rounds, dead) window-loads")
     for c in last:
         f = full[c]
         nod = mode[c] == 2
-        print("  %5d %6.2f %6.2f %4d %2d | %3d %3d %3d | %6d %6d %6d %6d %6d | %d | %6d (%d) %6d"
+        print("  %5d %6.2f %6.2f %4d %2d | %3d %3d %3d | %6d %6d %6d %6d %6d | %d | %6d (%d, %d) %6d"
               % (c, start[c], dur[c], steps[c], mode[c], f[7] & 0xffffffff, f[6], f[7] >> 32, f[14],
                  f[8], f[9], f[10], f[11], f[15] & 1, (f[12] & ((1 << 40) - 1)) if nod else 0,
-                 (f[12] >> 40) if nod else 0, f[13] if nod else 0))
+                 ((f[12] >> 40) & 0xffff) if nod else 0, (f[12] >> 56) if nod else 0, f[13] if nod else 0))
 
 
 if __name__ == "__main__":
