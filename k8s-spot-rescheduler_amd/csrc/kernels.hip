@@ -2515,6 +2515,15 @@ __global__ __launch_bounds__(256) void k2_node(DevWorkload w_arg, const int4* __
   k2_finish<PROF>(w, x, status, 2, nbytes, st);
 }
 
+// K2 waves per block: SR_K2_WPB (1, 2, 4), else one wave per block for lists of
+// at most 2,048 entries (the waves spread over every CU, so a long chain wave
+// shares its CU with fewer others: C5 K2 38.2 -> 36.1 us, realistic C3 31.5 ->
+// 30.5, C3 15.0 -> 14.4) and four above (C4: 15,000 waves)
+static inline int k2_waves_per_block(const DevWorkload& w) {
+  if (w.k2_wpb == 1 || w.k2_wpb == 2 || w.k2_wpb == 4) return w.k2_wpb;
+  return w.n_list <= 2048 ? 1 : 4;
+}
+
 // Launch with optional HIP events recorded by the dispatch itself
 // (hipExtLaunchKernelGGL: no event packets or host calls around the kernel).
 template <typename K, typename... A>
@@ -2550,7 +2559,7 @@ hipError_t launch_k2_place_ch(const DevWorkload& w, hipStream_t s, hipEvent_t ev
 template <bool PROF>
 hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
-  const int wpb = w.k2_wpb == 1 || w.k2_wpb == 2 ? w.k2_wpb : 4;  // waves per block
+  const int wpb = k2_waves_per_block(w);  // waves per block
   const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
   const size_t lds = wpb * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
   const bool wide = SR_K2_WIDE_HEADS && n <= 2048;
@@ -2571,7 +2580,7 @@ template hipError_t launch_k2_node_g<true>(const DevWorkload&, int, hipStream_t,
 template <bool PROF>
 hipError_t launch_k2_node_xt_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
-  const int wpb = w.k2_wpb == 1 || w.k2_wpb == 2 ? w.k2_wpb : 4;
+  const int wpb = k2_waves_per_block(w);
   const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
   const size_t lds = wpb * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
   const bool wide = SR_K2_WIDE_HEADS && n <= 2048;  // as launch_k2_node_g
@@ -2590,7 +2599,7 @@ template hipError_t launch_k2_node_xt_g<true>(const DevWorkload&, int, hipStream
 template <int CH, bool PROF>
 hipError_t launch_k2_place_ch(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
-  const int wpb = w.k2_wpb == 1 || w.k2_wpb == 2 ? w.k2_wpb : 4;  // waves per block
+  const int wpb = k2_waves_per_block(w);  // waves per block
   const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
   launch(k2_place<CH, PROF>, grid, block, wpb * sizeof(K2Lds), s, ev0, ev1, w, w.list, n);
   return hipGetLastError();

@@ -118,7 +118,7 @@ struct DevWorkload {
                        // both null on runs that end with K3
   uint32_t seq;        // run sequence number: the tag of every result word (wraps)
   int32_t k2_narrow;   // node order: 32-bit scaled window visits where every request allows (SR_K2_NARROW=0: never)
-  int32_t k2_wpb;      // K2 waves per block (SR_K2_WPB: 1, 2 or 4 (default))
+  int32_t k2_wpb;      // K2 waves per block (SR_K2_WPB: 1, 2 or 4; 0 = 1 up to 2,048 entries, else 4)
   int32_t k2_excl;     // node order: exclusive candidates placed with the taken-mask step (SR_K2_EXCL=0: never)
   int32_t k2_mode;     // 0: node-order first fit where it applies (<= 64 pods, <= 64-word rows);
                        // 1: pod order everywhere (SR_K2_MODE=1, A/B measurement)

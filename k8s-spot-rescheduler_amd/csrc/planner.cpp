@@ -181,7 +181,7 @@ struct sr_ctx {
   int32_t k2_mode = 0;        // SR_K2_MODE=1: pod-order K2 only (A/B measurement)
   int32_t node_patch = 1;     // SR_NODE_PATCH=0: a changed node section always goes up whole
   int32_t k2_narrow = 1;      // SR_K2_NARROW: 32-bit scaled window visits in node order (0: 64-bit only)
-  int32_t k2_wpb = 4;         // SR_K2_WPB: K2 waves per block (1, 2, 4)
+  int32_t k2_wpb = 0;         // SR_K2_WPB: K2 waves per block (1, 2, 4; 0 = by list length)
   int32_t k2_excl = 1;        // SR_K2_EXCL: exclusive candidates (one host port) with the taken-mask step
   int32_t k2_node_kernel = 1; // SR_K2_NODE_KERNEL: node-order-only K2 kernel when every candidate takes that path
   int32_t s_head_only = 1;    // SR_S_HEAD_ONLY: K0 writes S-row heads only on rows wider than 64 words (0: never)
