@@ -3,9 +3,11 @@
 pod x node feasibility checks/s at 5k nodes / 150k pods).
 
 One step = one housekeeping tick's planning segment on device-resident inputs:
-K0 tables -> K2 feasibility rows + first-fit placement of every candidate (one
-GPU: each candidate's outcome and the first drainable mapping go straight to
-mapped host memory) -> for N>1: RCCL allreduce(min) -> K3 winner mapping.
+K0 tables -> K2 feasibility rows + first-fit placement of every candidate
+(each candidate's outcome and the first drainable mapping go straight to
+mapped host memory; for N>1 into one shared-memory segment every rank's host
+walks in global candidate order, or, with --transport rccl, an RCCL
+allreduce(min) -> K3 winner mapping).
 ms_per_step is the back-to-back tick with inputs in HBM (latency_ms: one tick
 on an idle device, launch to the winner on the host); `value` is
 reference-equivalent (pod, spot node) predicate checks per second over all
@@ -21,10 +23,12 @@ WORLD_SIZE / LOCAL_RANK / MASTER_* from the environment), or, when
 WORLD_SIZE is not set, as N child processes this one starts and waits for
 (it touches no GPU itself and exits non-zero if fewer than N devices are
 visible or any rank fails).  Candidates are sharded c % N == rank: with
---scaling strong the config's own cluster is split over the ranks, with
---scaling weak the cluster has N x the config's on-demand nodes over the same
-spot pool (every GPU holds one config-sized candidate set); the ranks reduce
-each tick's outcome with one RCCL allreduce(min).
+--scaling strong (the default, BASELINE's line) the config's own cluster is
+split over the ranks, with --scaling weak the cluster has N x the config's
+on-demand nodes over the same spot pool (every GPU holds one config-sized
+candidate set); a strong line carries the weak-scaled measurement beside it
+(weak_scaling).  The ranks reduce each tick's outcome through shared memory
+(--transport shm, no collective) or one RCCL allreduce(min) (--transport rccl).
 """
 import argparse
 import ctypes
@@ -43,7 +47,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 from spotplanner import capi  # noqa: E402
 from spotplanner.planner import PredicateChecker  # noqa: E402
-from spotplanner.scaling import choose_scaling, predict  # noqa: E402
+from spotplanner.scaling import predict  # noqa: E402
 from spotplanner.synth import AFFINITY, REALISTIC, SynthCluster, new_node_map, pods_for_deletion, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -301,57 +305,15 @@ def launch_ranks(n, argv, script=None, devices=None):
     return rc
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
-    ap.add_argument("--variant", default="baseline", choices=["baseline", "realistic", "affinity"],
-                    help="realistic: the config with StatefulSet volumes, init containers and GPU pods; affinity: "
-                         "Deployments with hostname anti-affinity and zone topology spread (both report the "
-                         "fallback ratio on them); baseline: BASELINE.json's config as specified")
-    ap.add_argument("--scaling", default="auto", choices=["auto", "strong", "weak"],
-                    help="strong: the config's cluster, candidates split over the ranks; weak: N x its candidates; "
-                         "auto: strong where the predicted sharded tick beats one GPU's, else weak "
-                         "(spotplanner/scaling.py, DESIGN.md 7)")
-    ap.add_argument("--tick", default="steady", choices=["steady", "cold"],
-                    help="steady: the timed step replays a steady-state tick (the previous tick's candidate input, "
-                         "one spot node changed: incremental K0 + K2); cold: a first tick (every table row)")
-    ap.add_argument("--mut-pos", type=int, default=7,
-                    help="spot position of the steady tick's changed node (7: inside the 512-node F heads)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--e2e-reps", type=int, default=20, help="steady-state end-to-end ticks timed after the steps")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-events", action="store_true",
-                    help="A/B only: no HIP events in the timed region (roofline from the calibration pass)")
-    ap.add_argument("--event-every", type=int, default=16,
-                    help="HIP events on every n-th step of the timed region (timestamped dispatches lengthen a tick)")
-    args = ap.parse_args()
-
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
-        sys.exit(2)
-    scaling_choice = None
-    if args.scaling == "auto":
-        args.scaling, why = choose_scaling(args.config, world)
-        scaling_choice = {"requested": "auto", "chosen": args.scaling, "reason": why,
-                          "prediction_us": predict(args.config, world) if world > 1 else None,
-                          "model": "spotplanner/scaling.py (measured 1-GPU parts, assumed allreduce latency)"}
+def measure_ticks(lib, checker, sc, rank, world, args):
+    """The timed region on one synthetic cluster: its node map and candidate
+    lists (run()'s, rescheduler.go:228-264), this rank's shard (c % world), the
+    steady-state tick prepared, one full run (K2's bytes, the reference-
+    equivalent checks), the warm-up, the calibration pass, then EXACTLY
+    args.steps sr_plan_run calls bracketed by barrier + synchronize (max over
+    ranks), and the full run once more for the parity check."""
     import torch
     import torch.distributed as dist
-    if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
-
-    lib = capi.load_planner()
-    sc = SynthCluster(args.config, n_on_demand=cluster_on_demand(args.config, world, args.scaling),
-                      **({"realistic": REALISTIC, "affinity": AFFINITY}.get(args.variant, {})))
     nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
     # run()'s candidate lists (rescheduler.go:228-264): GetPodsForDeletionOnNodeDrain + the
     # DaemonSet-owner filter, on the host (sr_pods_for_deletion)
@@ -367,19 +329,6 @@ def main():
                                 capi.ptr(nm.node_pod_off, capi.P32), capi.ptr(nm.node_pod_idx, capi.P32),
                                 ctypes.byref(snap))
     assert st == capi.SR_OK
-    checker = PredicateChecker(local)
-    rccl_ranks = 0
-    if world > 1:
-        uid = (ctypes.c_uint8 * capi.SR_UNIQUE_ID_BYTES)()
-        if rank == 0:
-            assert lib.sr_comm_unique_id(uid) == capi.SR_OK
-        box = [bytes(uid)]
-        dist.broadcast_object_list(box, src=0)
-        uid = (ctypes.c_uint8 * capi.SR_UNIQUE_ID_BYTES).from_buffer_copy(box[0])
-        st = lib.sr_comm_init(checker.handle, uid, world, rank)
-        assert st == capi.SR_OK, checker.last_error()
-        rccl_ranks = world
-
     cands = capi.sr_candidates(len(loff) - 1, capi.ptr(loff, capi.P32), capi.ptr(lpods, capi.P32),
                                capi.ptr(gidx, capi.P32))
     t0 = time.perf_counter()
@@ -419,7 +368,8 @@ def main():
               if tq.k0_columns == -2 else "every row" if tq.k0_columns == -1 else
               "incremental: %d word columns, %d moved threshold rows" % (tq.k0_columns, tq.k0_rows_moved))
         steady = {"tick": "steady: the previous tick's candidate input, one more pod on spot node %d" % mut_pos,
-                  "candidate_side_reused": bool(tq.enc_reused), "pod_patches": int(tq.enc_pod_patches), "k0": k0}
+                  "candidate_side_reused": bool(tq.enc_reused), "pod_patches": int(tq.enc_pod_patches), "k0": k0,
+                  "work_list_by_cost": bool(tq.k2_list_by_cost)}
     # one run with per-candidate outputs first: K2's byte counts and the
     # reference-equivalent check count of this workload's plan
     status = np.zeros(max(1, len(loff) - 1), np.int32)
@@ -475,7 +425,6 @@ def main():
         total_issued, total_dense = float(c[0].item()), float(c[1].item())
     else:
         total_issued, total_dense = issued_local, dense_local
-    ms_step = 1e3 * elapsed / args.steps
     per_rank = gather_per_rank(rank_record(rank, len(loff) - 1, len(lpods), local_elapsed, args.steps, breakdown),
                                world)
 
@@ -484,6 +433,111 @@ def main():
     st = lib.sr_plan_run(checker.handle, ctypes.byref(full))
     assert st == capi.SR_OK, (st, checker.last_error())
     tm = checker.timing()
+    return dict(nm=nm, cand_off=cand_off, cand_pods=cand_pods, loff=loff, lpods=lpods, snap=snap, cands=cands,
+                out=out, wmap=wmap, full=full, status=status, nodes_out=nodes_out, mutation=mutation, steady=steady,
+                pfd_ms=pfd_ms, pack_ms=pack_ms, breakdown=breakdown, dom=dom, dom_ms=dom_ms, elapsed=elapsed,
+                total_issued=total_issued, total_dense=total_dense, tm=tm, issued_local=issued_local,
+                per_rank=per_rank, mut_pod=mut_pod, mut_pos=mut_pos)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--variant", default="baseline", choices=["baseline", "realistic", "affinity"],
+                    help="realistic: the config with StatefulSet volumes, init containers and GPU pods; affinity: "
+                         "Deployments with hostname anti-affinity and zone topology spread (both report the "
+                         "fallback ratio on them); baseline: BASELINE.json's config as specified")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (BASELINE's line): the config's own cluster, its candidates split over the ranks; "
+                         "weak: N x its candidates over the same spot pool")
+    ap.add_argument("--no-weak-beside", action="store_true",
+                    help="N > 1 with --scaling strong: skip the weak-scaled measurement reported beside the line "
+                         "(weak_scaling)")
+    ap.add_argument("--transport", default="shm", choices=["shm", "rccl"],
+                    help="N > 1: shm = the ranks reduce each tick through one shared-memory segment (no collective, "
+                         "no K3; sr_comm_init_shm); rccl = one RCCL allreduce(min) + K3 (sr_comm_init)")
+    ap.add_argument("--tick", default="steady", choices=["steady", "cold"],
+                    help="steady: the timed step replays a steady-state tick (the previous tick's candidate input, "
+                         "one spot node changed: incremental K0 + K2); cold: a first tick (every table row)")
+    ap.add_argument("--mut-pos", type=int, default=7,
+                    help="spot position of the steady tick's changed node (7: inside the 512-node F heads)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--e2e-reps", type=int, default=20, help="steady-state end-to-end ticks timed after the steps")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true",
+                    help="A/B only: no HIP events in the timed region (roofline from the calibration pass)")
+    ap.add_argument("--event-every", type=int, default=16,
+                    help="HIP events on every n-th step of the timed region (timestamped dispatches lengthen a tick)")
+    args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # SR_BENCH_DEVICE: every rank on that one GPU (rehearsing the N > 1 path on a one-GPU box, --transport shm)
+    local = int(os.environ.get("SR_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+
+    lib = capi.load_planner()
+    checker = PredicateChecker(local)
+    transport = "none"
+    if world > 1 and args.transport == "shm":
+        # one shared-memory segment per job: its name and session from rank 0
+        box = [int.from_bytes(os.urandom(4), "little")]
+        dist.broadcast_object_list(box, src=0)
+        session = box[0]
+        checker.attach_shared_memory("/srbench-%08x" % session, session, world, rank,
+                                     max_cand=DEFAULT_OD[args.config] * world)
+        dist.barrier()  # every rank attached before any plans (rank 0's planner removes the name when it closes)
+        transport = "shm"
+    elif world > 1:
+        uid = (ctypes.c_uint8 * capi.SR_UNIQUE_ID_BYTES)()
+        if rank == 0:
+            assert lib.sr_comm_unique_id(uid) == capi.SR_OK
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0)
+        uid = (ctypes.c_uint8 * capi.SR_UNIQUE_ID_BYTES).from_buffer_copy(box[0])
+        st = lib.sr_comm_init(checker.handle, uid, world, rank)
+        assert st == capi.SR_OK, checker.last_error()
+        transport = "rccl"
+
+    variant_kw = {"realistic": REALISTIC, "affinity": AFFINITY}.get(args.variant, {})
+    sc = SynthCluster(args.config, n_on_demand=cluster_on_demand(args.config, world, args.scaling), **variant_kw)
+    M = measure_ticks(lib, checker, sc, rank, world, args)
+    nm, cand_off, cand_pods, loff, lpods = M["nm"], M["cand_off"], M["cand_pods"], M["loff"], M["lpods"]
+    snap, cands, out, wmap, full = M["snap"], M["cands"], M["out"], M["wmap"], M["full"]
+    status, nodes_out, mutation, steady = M["status"], M["nodes_out"], M["mutation"], M["steady"]
+    pfd_ms, pack_ms, breakdown, dom, dom_ms = M["pfd_ms"], M["pack_ms"], M["breakdown"], M["dom"], M["dom_ms"]
+    elapsed, total_issued, total_dense, tm = M["elapsed"], M["total_issued"], M["total_dense"], M["tm"]
+    issued_local, per_rank, mut_pod, mut_pos = M["issued_local"], M["per_rank"], M["mut_pod"], M["mut_pos"]
+    ms_step = 1e3 * elapsed / args.steps
+    # N > 1, strong scaling (the line): the weak-scaled tick beside it, labelled
+    # -- every rank one config-sized candidate set over the same spot pool
+    weak_scaling = None
+    if world > 1 and args.scaling == "strong" and not args.no_weak_beside:
+        sw = SynthCluster(args.config, n_on_demand=cluster_on_demand(args.config, world, "weak"), **variant_kw)
+        W = measure_ticks(lib, checker, sw, rank, world, args)
+        weak_scaling = {
+            "scaling": "weak", "value": W["total_issued"] / W["elapsed"] * args.steps if W["elapsed"] > 0 else 0.0,
+            "unit": "checks/s", "ms_per_step": 1e3 * W["elapsed"] / args.steps,
+            "plans_per_s": (len(W["cand_off"]) - 1) / (W["elapsed"] / args.steps),
+            "workload": workload_name(args.config, sw.n_nodes, len(W["nm"].on_demand), len(W["nm"].spot), sw.n_pods,
+                                      world, "weak", args.variant),
+            "candidates_per_rank": shard_sizes(len(W["cand_off"]) - 1, world), "per_rank": W["per_rank"],
+            "first_ok": int(W["out"].first_ok), "winner": int(W["out"].winner),
+            "note": "not the line's value: N x the config's candidates over the same spot pool (weak scaling), "
+                    "measured after the line in the same job"}
+        lib.sr_snapshot_destroy(W["snap"])
 
     # Result latency of one tick on an idle device: sr_plan_run from the launch
     # to the winner and its mapping in host memory.  On one rank the run returns
@@ -748,10 +802,18 @@ def main():
                        "spot_nodes": int(len(nm.spot)), "candidates": int(len(cand_off) - 1),
                        "candidate_pods": int(len(cand_pods)), "parallelism": "candidates c%%%d" % world,
                        "candidates_per_rank": shard_sizes(len(cand_off) - 1, world)},
-            "collective": {"backend": "rccl" if rccl_ranks else "none", "ranks": rccl_ranks,
-                           "per_tick": "one allreduce(min) of 3 x u64" if rccl_ranks else "none (one GPU)"},
+            "collective": {"backend": transport, "ranks": world if world > 1 else 0,
+                           "per_tick": {"shm": "no collective: every rank's K2 writes its outcomes into one "
+                                               "shared-memory segment, each host walks them in global order "
+                                               "(sr_comm_init_shm)",
+                                        "rccl": "one allreduce(min) of 3 x u64 + K3",
+                                        "none": "none (one GPU)"}[transport]},
             "per_rank": per_rank,
-            "scaling_choice": scaling_choice,
+            "weak_scaling": weak_scaling,
+            "scaling_model": {"prediction_us": predict(args.config, world),
+                              "model": "spotplanner/scaling.py: measured 1-GPU parts, ASSUMED RCCL allreduce "
+                                       "latency (the shm transport has none); per_rank holds the measured parts"}
+            if world > 1 else None,
             "first_ok": int(out.first_ok), "winner": int(out.winner),
             "fallback_candidates": int(np.sum(status[:len(loff) - 1] == capi.SR_CAND_FALLBACK)),
             "kernels_ms": {kk: round(v, 5) for kk, v in breakdown.items()},

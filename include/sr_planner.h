@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SR_ABI_VERSION 8
+#define SR_ABI_VERSION 9
 
 /* ------------------------------------------------------------------ status */
 typedef int32_t sr_status;
@@ -510,7 +510,7 @@ const char *sr_build_info(void);
  * library would otherwise read fields past the end of a shorter struct (ABI 5
  * added sr_cluster.volumes and pod_stamp; ABI 6 the sr_timing enc_reused /
  * enc_pod_patches counters, which sr_get_timing writes; ABI 7 sr_timing.ms_collective; ABI 8
- * sr_snapshot_refresh_cached). */
+ * sr_snapshot_refresh_cached; ABI 9 the sr_timing K2 launch fields). */
 int32_t     sr_abi_version(void);
 
 /* Batched findSpotNodeForPod (rescheduler.go:338-353): for each pod, the first
@@ -619,6 +619,11 @@ typedef struct {
   int32_t  k0_rows_moved;      /* ... and threshold rows it rewrites whole */
   int32_t  k0_dirty_nodes;     /* no K0: spot nodes changed since the tables were written */
   double   ms_collective;      /* multi-GPU: the allreduce(min) between K2 and K3 (ABI 7) */
+  int32_t  k2_launches;        /* K2 kernels of the last run: 2 = the split launch (domain-path candidates on a
+                                * second stream beside the node-order kernel; ABI 9) */
+  int32_t  k2_list_by_cost;    /* 1: the last prepare's work list runs in the order of the previous run's K2
+                                * wave durations (reused candidate side of a long list; ABI 9) */
+  int32_t  k2_coop;            /* candidates of the last run planned by a block of cooperating waves (ABI 9) */
 } sr_timing;
 /* mask: which kernels sr_plan_run brackets with HIP events (resets the sums):
  * 1 = K0, 2 = K2, 4 = collective (multi-GPU) and K3, timed apart; 0 = no events.  Events are read back lazily, by
@@ -648,6 +653,20 @@ sr_status sr_comm_init(sr_ctx *ctx, const uint8_t id[SR_UNIQUE_ID_BYTES], int32_
  * with SR_ERR_RCCL).  It is called from the thread that called the planner. */
 typedef int32_t (*sr_allreduce_min_fn)(void *user, uint64_t *words, int32_t n);
 sr_status sr_comm_init_host(sr_ctx *ctx, int32_t nranks, int32_t rank, sr_allreduce_min_fn fn, void *user);
+/* The ranks of ONE node reduce through host memory instead (ABI 9): every
+ * rank's K2 writes its candidates' outcomes into one POSIX shared-memory
+ * segment (`name`, e.g. "/sr-<job>", identical on every rank), mapped into
+ * every rank's GPU, and each rank's host walks them in global candidate order
+ * up to the first drainable candidate -- no collective call and no K3
+ * (rescheduler.go:280-286 stops at the first drainable candidate, whichever
+ * rank planned it).  `session`: identical on every rank, fresh
+ * for the job (it tags the shared words).  Shards must be interleaved:
+ * cand_global[i] = (first + i) * nranks + rank (SR_ERR_INVALID_ARG
+ * otherwise); max_cand bounds the candidates of one rank's call
+ * (SR_ERR_CAPACITY).  Every rank calls it before any rank plans and plans the
+ * same sequence of calls; rank 0's sr_destroy removes the name. */
+sr_status sr_comm_init_shm(sr_ctx *ctx, const char *name, uint32_t session, int32_t nranks, int32_t rank,
+                           int32_t max_cand);
 
 #ifdef __cplusplus
 }

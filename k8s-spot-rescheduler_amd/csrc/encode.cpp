@@ -52,16 +52,6 @@ double encode_phase_ms[16];  // host-side profile of the last encode (tools/enco
 
 namespace {
 
-// Candidates dispatched ahead of the longest-first rest (SR_LIST_HEAD, default
-// 1024: about one wave per SIMD).
-int32_t list_head() {
-  static const int32_t v = [] {
-    const char* e = std::getenv("SR_LIST_HEAD");
-    return e ? std::max(0, std::atoi(e)) : 1024;
-  }();
-  return v;
-}
-
 constexpr int64_t kQuantityLimit = int64_t(1) << 62;
 constexpr size_t kSpecShards = 16;             // fixed: spec ids do not depend on the thread count
 constexpr size_t kMaxSpecs = size_t(1) << 21;  // content dictionaries are dropped beyond these
@@ -1140,9 +1130,8 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
 
 }  // namespace
 
-void reorder_list_by_cost(Workload& w, const uint32_t* cycles) {
+void reorder_list_by_cost(Workload& w, const uint32_t* cycles, int32_t head) {
   const size_t n = w.list.size() / 4;
-  const int32_t head = list_head();
   auto part = [&](size_t j) {
     return (w.n_list_node > 0 && static_cast<int32_t>(j) >= w.n_list_node ? 2 : 0) + (w.list[j * 4] < head ? 0 : 1);
   };
@@ -2964,11 +2953,8 @@ sr_status encode_impl(EncoderCache& C, const sr_snapshot* snap, const sr_cluster
   // kernels side by side.
   {
     const size_t n_act = w->cand_off.size() - 1;
-    const int32_t kListHead = list_head();
-    static const int32_t split_min = [] {
-      const char* e = std::getenv("SR_K2_SPLIT_MIN");
-      return e ? std::max(0, std::atoi(e)) : 4096;
-    }();
+    const int32_t kListHead = C.list_head;
+    const int32_t split_min = C.split_min;
     auto part_of = [&](size_t i) {  // 1: node order; 2: the rest (domain path, more than 256 pods)
       const int32_t len = w->cand_off[i + 1] - w->cand_off[i];
       return (!w->dyn_cand.empty() && w->dyn_cand[i] >= 0) || len > 256 ? 2 : 1;

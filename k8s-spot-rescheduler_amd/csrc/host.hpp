@@ -666,6 +666,11 @@ struct SpecInfo {
 // "metadata.name" or the unschedulable key change, or when the dictionaries
 // grow past their bounds.
 struct EncoderCache {
+  // ---- per-context settings (sr_create reads them from the environment)
+  int32_t list_head = 1024;   // SR_LIST_HEAD: candidates dispatched ahead of the longest-first rest (about one
+                              //   wave per SIMD)
+  int32_t split_min = 4096;   // SR_K2_SPLIT_MIN: a work list with domain-path candidates and more entries than
+                              //   this goes in two parts (planner.cpp k2_split)
   int32_t id_empty = INT32_MIN, id_metadata_name = INT32_MIN, id_unschedulable_key = INT32_MIN;
   // ---- static view
   int32_t n_spot = -1, Wp = 0, n_pad = 0;
@@ -878,7 +883,7 @@ struct SpreadDyn {
 // duration in its last run (`cycles`, by active candidate), longest first,
 // within the parts the list was built in (the head, the rest; the split
 // launch's two kernels); list_ext follows.
-void reorder_list_by_cost(Workload& w, const uint32_t* cycles);
+void reorder_list_by_cost(Workload& w, const uint32_t* cycles, int32_t list_head);
 
 // Builds the workload; returns SR_OK or an error with *err filled.  `cache`
 // carries what the previous calls derived (and is updated).

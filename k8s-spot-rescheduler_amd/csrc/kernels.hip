@@ -419,31 +419,6 @@ __global__ __launch_bounds__(256) void k0_incremental(DevWorkload w, int s_waves
 // which never weakens a later count.
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef __attribute__((address_space(1))) void* gbl_vp;
-// K0b: each pod's F row head (S & T cpu & T mem & T eph, words [0, 8): the
-// first 512 spot nodes) and S row head, from the rows K0 just wrote and the
-// pod records as K0 patched them.  K2's node-order prologue reads both with
-// the pod records, one memory round trip earlier than ANDing the row heads
-// itself (their offsets come from the records); a K0-less run keeps them, its
-// changed nodes' bits recomputed from the S head (fix_dirty).  One wave per 8
-// pods, lanes = pod x word.
-__global__ __launch_bounds__(256) void k0_heads(DevWorkload w) {
-  const int lane = threadIdx.x & 63;
-  const int pod = (static_cast<int>(blockIdx.x) * 4 + static_cast<int>(threadIdx.x >> 6)) * 8 + (lane >> 3);
-  const int wd = lane & 7;
-  if (pod >= w.n_pods) return;
-  const uint64_t* pr = w.pod_rec + static_cast<size_t>(pod) * 6;
-  const uint64_t r01 = pr[4], r23 = pr[5];
-  uint64_t f = 0, sw = 0;
-  if (wd < w.Wp) {
-    const uint64_t* tab = w.S;
-    sw = tab[static_cast<uint32_t>(r01) + wd];
-    f = sw & tab[static_cast<uint32_t>(r01 >> 32) + wd] & tab[static_cast<uint32_t>(r23) + wd] &
-        tab[static_cast<uint32_t>(r23 >> 32) + wd];
-  }
-  w.pod_head[static_cast<size_t>(pod) * 16 + wd] = f;
-  w.pod_head[static_cast<size_t>(pod) * 16 + 8 + wd] = sw;
-}
-
 #define SR_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
 // Winner: d_min[0] = packed first drainable candidate (possibly reduced over
@@ -1315,18 +1290,6 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
     const uint64_t e = ballot(64 * g + lane < np && static_cast<uint32_t>(r01[g]) == w.s_empty_off);
     if (e != 0) dead = min(dead, 64 * g + __builtin_ctzll(e));
   }
-  // K0b's F / S heads of pods [0, 64), issued with the records (one round trip
-  // for both): lanes = 8 pods x 8 words, batch h = pods [8 h, 8 h + 8)
-  constexpr bool kEarlyHeads = kNH == 8 && (G == 1 || WIDE);  // the F-head loop's batch layout below
-  uint64_t hf0[8], hs0[8];
-  if (kEarlyHeads && w.pod_head) {
-#pragma unroll
-    for (int h = 0; h < 8; ++h) {
-      const uint64_t* ph = w.pod_head + static_cast<size_t>(p0 + min(8 * h + lane / 8, np - 1)) * 16 + (lane & 7);
-      hf0[h] = ph[0];
-      hs0[h] = ph[8];
-    }
-  }
   // XT: the pods' extension records and the slots' node_scal rows
   XVals<int64_t> xv[G];
   int erow0 = -1, erow1 = -1;
@@ -1487,7 +1450,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   // bytes moved (algorithmic, wave-uniform): pod records, F heads of pods
   // [0, dead) (4 rows x min(Wp, kNH) words), 64-node record windows (5 words
   // each), full-row scans and far words, the mapping and status writes
-  nbytes += (48u + 4u) * static_cast<uint32_t>(np) + 4u + (w.pod_head ? 16u : 32u) * static_cast<uint32_t>(min(Wp, kNH)) * dead;
+  nbytes += (48u + 4u) * static_cast<uint32_t>(np) + 4u + 32u * static_cast<uint32_t>(min(Wp, kNH)) * dead;
 
   // head words holding a node changed since the tables were written (K0-less
   // runs), and per pod (its lane) whether it fits each changed node: bit p for
@@ -1532,17 +1495,6 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
           if (b0 + kPW * h >= lim) continue;  // wave-uniform
           const int src = min(kk[h], np - 1) - 64 * g;  // lane of that pod in group g
           if (dirty_head != 0) fm[h] = from_lane(dfit[g], src);
-          if (kEarlyHeads && g == 0 && w.pod_head) {  // loaded with the records (b0 == 0 here)
-            x[h][0] = hs0[h];
-            x[h][1] = hf0[h];
-            continue;
-          }
-          if (w.pod_head) {  // K0b's heads: F in x[h][1], S in x[h][0]
-            const uint64_t* ph = w.pod_head + static_cast<size_t>(p0 + min(kk[h], np - 1)) * 16 + wd;
-            x[h][0] = ph[8];
-            x[h][1] = ph[0];
-            continue;
-          }
           const uint32_t o0 = from_lane(static_cast<uint32_t>(r01[g]), src);
           const uint32_t o1 = from_lane(static_cast<uint32_t>(r01[g] >> 32), src);
           const uint32_t o2 = from_lane(static_cast<uint32_t>(r23[g]), src);
@@ -1556,7 +1508,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
 #pragma unroll
         for (int h = 0; h < kPB; ++h) {
           if (b0 + kPW * h >= lim) continue;  // wave-uniform
-          uint64_t f = (wv && kk[h] < np) ? (w.pod_head ? x[h][1] : x[h][0] & x[h][1] & x[h][2] & x[h][3]) : 0ull;
+          uint64_t f = (wv && kk[h] < np) ? x[h][0] & x[h][1] & x[h][2] & x[h][3] : 0ull;
           if (dirty_head != 0) {  // the changed nodes' bits, from the pod's fit mask
             for (int p = 0; p < w.n_dirty; ++p) {
               const int n = w.dirty_node[p];
@@ -2665,12 +2617,6 @@ hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hip
 
 hipError_t launch_placement(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   return w.prof ? launch_k2<true>(w, s, ev0, ev1) : launch_k2<false>(w, s, ev0, ev1);
-}
-
-hipError_t launch_heads(const DevWorkload& w, hipStream_t s) {
-  const unsigned waves = static_cast<unsigned>((w.n_pods + 7) / 8);
-  launch(k0_heads, dim3(std::max(1u, (waves + 3) / 4)), dim3(256), 0, s, nullptr, nullptr, w);
-  return hipGetLastError();
 }
 
 hipError_t launch_winner(const DevWorkload& w, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {

@@ -96,9 +96,7 @@ struct DevWorkload {
                              //  slot 0, of slot 1 (-1: no slot), 0}
   // outputs / scratch
   uint64_t* S;         // [n_classes][Wp] static-class rows, followed by
-  uint64_t* T;         // [n_t][Wp] capacity threshold rows (one table), followed by
-  uint64_t* pod_head;  // [n_pods + 128][16] per pod its F row head (S & T & T & T, words [0, 8)) and S row
-                       // head, written by K0b after every K0 run (null: K2 ANDs the row heads itself)
+  uint64_t* T;         // [n_t][Wp] capacity threshold rows (one table)
   int32_t* out_node;   // [n_pods] spot position or -1
   int32_t* out_status; // [n_cand]
   uint32_t* out_bytes; // [n_cand] bytes K2 moved for the candidate (the roofline's algorithmic bytes)
@@ -137,8 +135,6 @@ hipError_t launch_tables(const DevWorkload& w, int32_t local_first_fallback, hip
                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // K2: per-candidate feasibility rows + first-fit placement; atomicMin of first_ok into d_min[0].
 hipError_t launch_placement(const DevWorkload& w, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-// K0b: every pod's F and S row heads into pod_head (after K0).
-hipError_t launch_heads(const DevWorkload& w, hipStream_t s);
 // K3: winner mapping into `result` (after the collective when ranks > 1), then the run's seq.
 // Not launched when K2 writes res_stat / res_map itself (single rank).
 hipError_t launch_winner(const DevWorkload& w, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);

@@ -704,9 +704,26 @@ static sr_status snapshot_create(const sr_cluster* c, const int32_t* spot, int32
 }
 
 // The snapshot's copy of `node` still equals the cluster's (nodes with scalar
-// resources or volume limits are copied anew).
+// resources or volume limits are copied anew): the fingerprint rejects most
+// changed nodes, and a match is confirmed field by field, so a fingerprint
+// collision can never keep a stale copy.
 static inline bool spot_node_same(const sr_cluster* c, int32_t node, const SpotNode& sn) {
-  return sn.copy_fp != 0 && sn.copy_fp == cluster_node_fp(c, node);
+  if (sn.copy_fp == 0 || sn.copy_fp != cluster_node_fp(c, node)) return false;
+  const sr_nodes& N = c->nodes;
+  if (sn.name != N.name[node] || sn.unschedulable != N.unschedulable[node] || sn.alloc[0] != N.alloc_milli_cpu[node] ||
+      sn.alloc[1] != N.alloc_memory[node] || sn.alloc[2] != N.alloc_ephemeral[node] || sn.alloc_pods != N.alloc_pods[node])
+    return false;
+  const int32_t l0 = N.label_off[node], nl = N.label_off[node + 1] - l0;
+  if (static_cast<size_t>(nl) != sn.labels.size()) return false;
+  for (int32_t j = 0; j < nl; ++j)
+    if (sn.labels[j].first != N.label_key[l0 + j] || sn.labels[j].second != N.label_val[l0 + j]) return false;
+  const int32_t t0 = N.taint_off[node], nt = N.taint_off[node + 1] - t0;
+  if (static_cast<size_t>(nt) != sn.taints.size()) return false;
+  for (int32_t j = 0; j < nt; ++j) {
+    const TaintRec& t = sn.taints[j];
+    if (t.key != N.taint_key[t0 + j] || t.val != N.taint_val[t0 + j] || t.effect != N.taint_effect[t0 + j]) return false;
+  }
+  return true;
 }
 
 // GetClusterSnapshot again on a snapshot built from an earlier call's cluster:

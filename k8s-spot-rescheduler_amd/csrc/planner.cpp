@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <climits>
 #include <cstdio>
@@ -23,6 +24,10 @@
 #include "kernels.hpp"
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 namespace {
 
@@ -134,7 +139,6 @@ struct sr_ctx {
   std::vector<uint64_t> pod_patch_words;   // this call's pod patches (prepare)
   int32_t k0_incremental = 1;  // SR_K0_INCREMENTAL=0: K0 always rewrites every row
   int32_t k0_skip = 1;         // SR_K0_SKIP=0: every run launches K0
-  int32_t pod_heads = 0;       // SR_POD_HEADS=1: K0b writes pod heads K2 reads with the records (measured: no gain)
   // SR_K2_SPLIT=0: one K2 launch.  Otherwise a work list the encoder split
   // (more entries than SR_K2_SPLIT_MIN, 4096: more waves than the chip holds
   // at once, with domain-path candidates) is planned by two kernels side by
@@ -173,6 +177,22 @@ struct sr_ctx {
   uint32_t seq = 0;  // run sequence number (wraps: tags compare as uint32)
   sr_timing t{};
   ncclComm_t comm = nullptr;
+  // sr_comm_init_shm: the ranks of one node reduce through host memory.  One
+  // POSIX shared-memory segment holds, per rank and per tick parity, the
+  // rank's published input words and the outcome words its K2 writes (mapped
+  // into every rank's GPU); each rank's host walks them in global candidate
+  // order up to the first drainable one (no collective, no K3: DESIGN.md §7).
+  struct Shm {
+    uint64_t* host = nullptr;  // the segment (every rank's regions)
+    uint64_t* dev = nullptr;   // its device address in this process
+    size_t bytes = 0;
+    int32_t max_cand = 0;      // input candidates per rank and call
+    uint32_t session = 0;
+    uint64_t tick = 0;         // runs through the segment (identical on every rank)
+    int32_t base = -1;         // the prepared call's first local candidate (cand_global[0] / nranks), -1: none
+    std::string name;
+    std::vector<int32_t> act_of;  // scratch: active candidate of each input candidate
+  } shm;
   sr_allreduce_min_fn host_fn = nullptr;  // sr_comm_init_host: the caller's allreduce(min)
   void* host_user = nullptr;
   int nranks = 1, rank = 0;
@@ -269,7 +289,166 @@ sr_status settle(sr_ctx* ctx) {
   return SR_OK;
 }
 
-bool has_comm(const sr_ctx* ctx) { return ctx->comm != nullptr || ctx->host_fn != nullptr; }
+bool has_comm(const sr_ctx* ctx) { return ctx->comm != nullptr || ctx->host_fn != nullptr || ctx->shm.host != nullptr; }
+
+// ---- the shared-memory transport (sr_comm_init_shm).  Per rank r and tick
+// parity p a region of kShmHdr + 2 * max_cand words, each word tag << 32 |
+// value (tag: the run's, identical on every rank):
+//   hdr[0] input candidates of the call   hdr[1] its first local index + 1 (0: none)
+//   hdr[2] first fallback (global) + 1    hdr[3] 1: the rank has finished this tick's walk
+//   hdr[4] smallest global index the rank has not planned after this call + 1 (0: none)
+//   in[i]  input candidate i: active candidate << 2 | 0, or 1 (no pods), 2 (fallback)
+//   st[ci] written by K2: active candidate ci is drainable (1) or not (0)
+constexpr size_t kShmHdr = 8;
+size_t shm_region_words(const sr_ctx* ctx) { return kShmHdr + 2 * static_cast<size_t>(ctx->shm.max_cand); }
+uint64_t* shm_region(sr_ctx* ctx, int32_t r, int p) {
+  return ctx->shm.host + (static_cast<size_t>(r) * 2 + static_cast<size_t>(p)) * shm_region_words(ctx);
+}
+// tags of the shared words: the high bit set, so they never equal a
+// single-rank run's (g_run_seq) in the context's private result words
+uint32_t shm_tag(const sr_ctx* ctx, uint64_t tick) {
+  return (ctx->shm.session + static_cast<uint32_t>(tick)) | 0x80000000u;
+}
+
+// Spins until ready().  A word of this rank's own K2 that has not arrived
+// after 100 ms is waited for on the stream (which surfaces a kernel fault);
+// another rank's after 60 s fails the run (that rank stopped planning).
+template <class F>
+sr_status shm_wait(sr_ctx* ctx, F ready, bool own, int32_t r) {
+  if (ready()) return SR_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  uint32_t spins = 0;
+  bool synced = false;
+  while (!ready()) {
+    if ((++spins & 1023) != 0) continue;
+    const auto dt = std::chrono::steady_clock::now() - t0;
+    if (own && !synced && dt > std::chrono::milliseconds(100)) {
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+      synced = true;
+      if (!ready()) {
+        ctx->err = "K2 outcome word not written by this run";
+        return SR_ERR_HIP;
+      }
+    } else if (!own && dt > std::chrono::seconds(60)) {
+      ctx->err = "rank " + std::to_string(r) + " published no outcome for this tick within 60 s";
+      return SR_ERR_RCCL;
+    }
+  }
+  return SR_OK;
+}
+
+// Before K2: this rank's input words and header for the run's tick, into the
+// region of the tick's parity once every rank has finished walking the tick
+// that used it before; K2 then writes the outcome words there.
+sr_status shm_publish(sr_ctx* ctx, int* par) {
+  auto& S = ctx->shm;
+  sr::DevWorkload& d = ctx->dw;
+  const sr::Workload& w = ctx->cur->wl;
+  const uint64_t tick = ++S.tick;
+  const int p = static_cast<int>(tick & 1);
+  if (tick > 2) {
+    const uint64_t done = static_cast<uint64_t>(shm_tag(ctx, tick - 2)) << 32 | 1u;
+    for (int32_t r = 0; r < ctx->nranks; ++r) {
+      volatile uint64_t* hd = shm_region(ctx, r, p);
+      sr_status st = shm_wait(ctx, [&] { return hd[3] == done; }, false, r);
+      if (st != SR_OK) return st;
+    }
+  }
+  const uint32_t tag = shm_tag(ctx, tick);
+  ctx->seq = tag;
+  d.seq = tag;
+  const uint64_t T = static_cast<uint64_t>(tag) << 32;
+  volatile uint64_t* reg = shm_region(ctx, ctx->rank, p);
+  const int32_t n_in = w.n_input_cand;
+  S.act_of.assign(static_cast<size_t>(std::max(0, n_in)), -1);
+  for (int32_t ci = 0; ci < static_cast<int32_t>(w.cand_src.size()); ++ci) S.act_of[w.cand_src[ci]] = ci;
+  for (int32_t i = 0; i < n_in; ++i) {
+    const int32_t a = S.act_of[i];
+    reg[kShmHdr + i] = T | static_cast<uint32_t>(a >= 0 ? a << 2 : w.status_host[i] == SR_CAND_FALLBACK ? 2 : 1);
+  }
+  std::atomic_thread_fence(std::memory_order_release);
+  reg[0] = T | static_cast<uint32_t>(n_in);
+  reg[1] = T | static_cast<uint32_t>(n_in > 0 ? S.base + 1 : 0);
+  reg[2] = T | static_cast<uint32_t>(w.first_fallback + 1);
+  reg[4] = T | static_cast<uint32_t>(d.rank_next == ~0ull ? 0 : d.rank_next + 1);
+  d.res_stat = S.dev + (const_cast<uint64_t*>(reg) - S.host) + kShmHdr + S.max_cand;
+  d.res_map = ctx->d_early + d.n_cand;
+  *par = p;
+  return SR_OK;
+}
+
+// After K2: the walk in global candidate order over every rank's words (rank
+// g % N holds global index g), up to the first drainable candidate or the
+// first index no rank planned in this call; the result words are written as
+// K3 would (`result`, tagged), the owner's mapping from its K2 (rescheduler.go:
+// 280-286 stops at the first drainable candidate, whichever rank planned it).
+sr_status shm_reduce(sr_ctx* ctx, int p) {
+  auto& S = ctx->shm;
+  const sr::Workload& w = ctx->cur->wl;
+  const uint32_t tag = ctx->dw.seq;
+  const int32_t N = ctx->nranks;
+  auto ready = [tag](volatile uint64_t* x) { return static_cast<uint32_t>(*x >> 32) == tag; };
+  std::vector<int64_t> n_r(static_cast<size_t>(N)), b_r(static_cast<size_t>(N));
+  int64_t ff = -1, nx = -1, g0 = INT64_MAX;
+  for (int32_t r = 0; r < N; ++r) {
+    volatile uint64_t* hd = shm_region(ctx, r, p);
+    for (int i : {0, 1, 2, 4}) {
+      sr_status st = shm_wait(ctx, [&] { return ready(hd + i); }, false, r);
+      if (st != SR_OK) return st;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    n_r[r] = static_cast<uint32_t>(hd[0]);
+    b_r[r] = static_cast<int64_t>(static_cast<uint32_t>(hd[1])) - 1;
+    if (n_r[r] > 0) g0 = std::min(g0, b_r[r] * N + r);
+    const int64_t f = static_cast<int64_t>(static_cast<uint32_t>(hd[2])) - 1;
+    if (f >= 0) ff = ff < 0 ? f : std::min(ff, f);
+    const int64_t x = static_cast<int64_t>(static_cast<uint32_t>(hd[4])) - 1;
+    if (x >= 0) nx = nx < 0 ? x : std::min(nx, x);
+  }
+  int64_t first_ok = -1;
+  int32_t owner = -1, oci = -1;
+  for (int64_t g = g0; g0 != INT64_MAX; ++g) {
+    const int32_t r = static_cast<int32_t>(g % N);
+    const int64_t li = g / N;
+    if (n_r[r] == 0 || li < b_r[r] || li >= b_r[r] + n_r[r]) break;  // no rank planned g in this call
+    volatile uint64_t* reg = shm_region(ctx, r, p);
+    volatile uint64_t* in = reg + kShmHdr + (li - b_r[r]);
+    sr_status st = shm_wait(ctx, [&] { return ready(in); }, false, r);
+    if (st != SR_OK) return st;
+    const uint32_t v = static_cast<uint32_t>(*in);
+    if ((v & 3u) != 0) continue;  // no pods to move, or the reference path
+    const int32_t ci = static_cast<int32_t>(v >> 2);
+    volatile uint64_t* sw = reg + kShmHdr + S.max_cand + ci;
+    st = shm_wait(ctx, [&] { return ready(sw); }, r == ctx->rank, r);
+    if (st != SR_OK) return st;
+    if (static_cast<uint32_t>(*sw) & 1u) {
+      first_ok = g;
+      owner = r;
+      oci = ci;
+      break;
+    }
+  }
+  shm_region(ctx, ctx->rank, p)[3] = static_cast<uint64_t>(tag) << 32 | 1u;  // this tick's words may be reused
+  volatile uint64_t* res = static_cast<volatile uint64_t*>(ctx->h_result.p);
+  const uint64_t T = static_cast<uint64_t>(tag) << 32;
+  int32_t np = 0;
+  if (owner == ctx->rank) {
+    const int32_t off = w.cand_off[oci];
+    np = w.cand_off[oci + 1] - off;
+    volatile uint64_t* map = static_cast<volatile uint64_t*>(ctx->h_early.p) + ctx->dw.n_cand + off;
+    for (int32_t q = 0; q < np; ++q) {
+      sr_status st = shm_wait(ctx, [&] { return ready(map + q); }, true, ctx->rank);
+      if (st != SR_OK) return st;
+      res[sr::kResultHeader + q] = T | static_cast<uint32_t>(map[q]);
+    }
+  }
+  res[0] = T | static_cast<uint32_t>(first_ok);
+  res[1] = T | (owner == ctx->rank ? 1u : 0u);
+  res[2] = T | static_cast<uint32_t>(np);
+  res[3] = T | static_cast<uint32_t>(ff);
+  res[4] = T | static_cast<uint32_t>(nx);
+  return SR_OK;
+}
 
 // allreduce(min) of n <= 8 uint64 words in device memory, stream-ordered:
 // RCCL in place, or the caller's collective on a pinned host copy.
@@ -336,6 +515,25 @@ Slot& pick_slot(sr_ctx* ctx, const sr_candidates* cands) {
 sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, const sr_candidates* cands) {
   auto t0 = std::chrono::steady_clock::now();
   ctx->prepared = false;
+  if (ctx->shm.host) {  // the walk finds global index g on rank g % N: interleaved shards only
+    const int32_t n = cands->n_cand, N = ctx->nranks;
+    if (n > ctx->shm.max_cand) {
+      ctx->err = "more candidates than sr_comm_init_shm's max_cand";
+      return SR_ERR_CAPACITY;
+    }
+    const int32_t* G = cands->cand_global;
+    if (n > 0 && !G && N > 1) {
+      ctx->err = "the shared-memory transport needs cand_global (interleaved shards)";
+      return SR_ERR_INVALID_ARG;
+    }
+    const int64_t b = n > 0 && G ? G[0] / N : 0;
+    for (int32_t i = 0; i < n; ++i)
+      if ((G ? G[i] : i) != (b + i) * N + ctx->rank) {
+        ctx->err = "the shared-memory transport needs interleaved shards: cand_global[i] = (first + i) * nranks + rank";
+        return SR_ERR_INVALID_ARG;
+      }
+    ctx->shm.base = n > 0 ? static_cast<int32_t>(b) : -1;
+  }
   Slot& sl = pick_slot(ctx, cands);
   ctx->cur = &sl;
   sr::Workload& w = sl.wl;
@@ -486,11 +684,12 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   st = settle(ctx);
   if (st != SR_OK) return st;
   // a reused workload's list in the order of its last run's K2 durations
+  // (list_sorted_gen is set once the reordered list's copies are queued: a
+  // prepare failing in between reorders and uploads it again next time)
   bool list_moved = false;
   if (ctx->list_cost && w.reused && sl.cost_gen == w.cand_gen && sl.list_sorted_gen != w.cand_gen) {
     HIP_TRY(ctx, hipEventSynchronize(sl.ev_cost));
-    sr::reorder_list_by_cost(w, static_cast<const uint32_t*>(sl.h_cycles.p));
-    sl.list_sorted_gen = w.cand_gen;
+    sr::reorder_list_by_cost(w, static_cast<const uint32_t*>(sl.h_cycles.p), ctx->enc.list_head);
     list_moved = true;
   }
   if (ctx->ev_upload) HIP_TRY(ctx, hipEventSynchronize(ctx->ev_upload));  // staging buffer free again
@@ -512,9 +711,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   const size_t n_rows = static_cast<size_t>(w.n_classes) + w.t_dim.size();
   const size_t row_bytes = static_cast<size_t>(w.Wp) * sizeof(uint64_t);
   const size_t t_cap = sl.tables.cap;
-  // the pod heads (K0b) after the rows
-  const size_t head_bytes = ctx->pod_heads ? (static_cast<size_t>(na) + 128) * 16 * sizeof(uint64_t) : 0;
-  HIP_TRY(ctx, dev_reserve(sl.tables, n_rows * row_bytes + head_bytes));
+  HIP_TRY(ctx, dev_reserve(sl.tables, n_rows * row_bytes));
   if (sl.tables.cap != t_cap) {  // a new allocation holds no rows: every row below
     sl.tables_cand_gen = ~0ull;
     skip = false;
@@ -626,6 +823,8 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   HIP_TRY(ctx, hipEventRecord(ctx->ev_upload, ctx->stream));  // kernels queue behind the copy
   if (!nodes_patch) sl.dev_state_gen = w.state_gen;  // the section went up whole (or was current)
   sl.dev_cand_gen = w.cand_gen;
+  if (list_moved) sl.list_sorted_gen = w.cand_gen;
+  ctx->t.k2_list_by_cost = sl.list_sorted_gen == w.cand_gen ? 1 : 0;
   // run() commits what a K0 launch brings the slot to
   sl.commit_k0 = !skip;
   auto t2 = std::chrono::steady_clock::now();
@@ -677,7 +876,6 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   for (int k = 0; k < sr::kDomKeys; ++k) d.dk_row[k] = w.dk_row[k];
   d.S = static_cast<uint64_t*>(sl.tables.p);
   d.T = d.S + static_cast<size_t>(w.n_classes) * w.Wp;
-  d.pod_head = ctx->pod_heads && ctx->k2_mode == 0 ? d.T + w.t_dim.size() * static_cast<size_t>(w.Wp) : nullptr;
   d.out_node = static_cast<int32_t*>(ctx->out_node.p);
   d.out_status = static_cast<int32_t*>(ctx->out_status.p);
   d.out_bytes = static_cast<uint32_t*>(ctx->out_bytes.p);
@@ -933,14 +1131,7 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     if (!ctx->dmin_ready[par])  // no K2 of a previous run reset it: reset here
       HIP_TRY(ctx, hipMemsetAsync(d.d_min, 0xff, sizeof(uint64_t), s));
   } else {
-    if (d.pod_head) {  // K0, then K0b (the pod heads of the rows K0 wrote), timed together
-      if (e0a) HIP_TRY(ctx, hipEventRecord(e0a, s));
-      HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s));
-      HIP_TRY(ctx, sr::launch_heads(d, s));
-      if (e0b) HIP_TRY(ctx, hipEventRecord(e0b, s));
-    } else {
-      HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
-    }
+    HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
     if (sl.commit_k0) {  // K0 wrote the node and pod patches and brought the rows to this workload (a rerun:
       sl.commit_k0 = false;  // idempotent)
       sl.tables_cand_gen = w.cand_gen;
@@ -960,17 +1151,24 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   ctx->dmin_ready[par] = false;
   ctx->dmin_ready[1 - par] = d.n_list > 0;  // K2's first candidate resets it
   PAIR(1, e1a, e1b);
+  const bool shm = collective && ctx->shm.host;  // ranks reduce through host memory: no collective, no K3
+  int shm_par = 0;
   if (early) {
     d.res_stat = ctx->d_early;
     d.res_map = ctx->d_early + d.n_cand;
+  } else if (shm) {
+    sr_status pst = shm_publish(ctx, &shm_par);
+    if (pst != SR_OK) return pst;
   } else {
     d.res_stat = d.res_map = nullptr;
   }
   // the split launch (see sr_ctx::k2_split): the node-order part on this
   // stream, the general one on stream2 between a fork and a join event
   const int32_t n_node = w.n_list_node;
-  if (ctx->k2_split && n_node > 0 && n_node < d.n_list && d.k2_mode == 0 && d.k2_node_kernel &&
-      w.max_np_node >= 1 && w.max_np_node <= 256) {
+  const bool split = ctx->k2_split && n_node > 0 && n_node < d.n_list && d.k2_mode == 0 && d.k2_node_kernel &&
+                     w.max_np_node >= 1 && w.max_np_node <= 256;
+  ctx->t.k2_launches = d.n_list > 0 ? (split ? 2 : 1) : 0;
+  if (split) {
     if (!ctx->stream2) {
       HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
       HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
@@ -1003,15 +1201,15 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     slc.cost_gen = w.cand_gen;
   }
   if (early) return finish_early(ctx, out);
-  PAIR(2, e2a, e2b);
-  if (collective) {
-    PAIR(3, eca, ecb);
-    if (eca) HIP_TRY(ctx, hipEventRecord(eca, s));
-    sr_status cst = allreduce_min_dev(ctx, d.d_min, 3);  // first ok, first fallback, rank_next
-    if (cst != SR_OK) return cst;
-    if (ecb) HIP_TRY(ctx, hipEventRecord(ecb, s));
-    HIP_TRY(ctx, sr::launch_winner(d, s, e2a, e2b));
-  } else {
+  if (!shm) {  // the shared-memory transport has no collective and no K3 (shm_reduce below)
+    PAIR(2, e2a, e2b);
+    if (collective) {
+      PAIR(3, eca, ecb);
+      if (eca) HIP_TRY(ctx, hipEventRecord(eca, s));
+      sr_status cst = allreduce_min_dev(ctx, d.d_min, 3);  // first ok, first fallback, rank_next
+      if (cst != SR_OK) return cst;
+      if (ecb) HIP_TRY(ctx, hipEventRecord(ecb, s));
+    }
     HIP_TRY(ctx, sr::launch_winner(d, s, e2a, e2b));
   }
 #undef PAIR
@@ -1029,6 +1227,8 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
       if (na) HIP_TRY(ctx, hipMemcpyAsync(ctx->h_node.p, d.out_node, sizeof(int32_t) * na, hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(ctx, hipStreamSynchronize(s));
+  } else if (shm) {
+    // (the walk below waits for the outcome words it needs)
   } else {
     // Every result word carries this run's sequence number in its upper
     // half (K3 stores them without ordering): poll the header, then the
@@ -1054,6 +1254,13 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
       }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+  }
+  if (shm) {  // every rank's outcome words in global order (ms_collective: this host walk)
+    const auto t0 = std::chrono::steady_clock::now();
+    sr_status sst = shm_reduce(ctx, shm_par);
+    if (sst != SR_OK) return sst;
+    if (timing & 4) ctx->t.ms_collective += std::chrono::duration<double, std::milli>(
+                                               std::chrono::steady_clock::now() - t0).count();
   }
 
   if (ctx->prof_file && ncand > 0) {  // diagnostics only (tools/k2_profile.py)
@@ -1150,10 +1357,11 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_PLAN_SLOTS")) ctx->n_slots = std::max(1, std::min(16, std::atoi(m)));
   if (const char* m = std::getenv("SR_K0_INCREMENTAL")) ctx->k0_incremental = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K0_SKIP")) ctx->k0_skip = std::atoi(m) != 0;
-  if (const char* m = std::getenv("SR_POD_HEADS")) ctx->pod_heads = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_K2_SPLIT")) ctx->k2_split = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_LIST_COST")) ctx->list_cost = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_LIST_COST_MIN")) ctx->list_cost_min = std::max(0, std::atoi(m));
+  if (const char* m = std::getenv("SR_K2_SPLIT_MIN")) ctx->enc.split_min = std::max(0, std::atoi(m));
+  if (const char* m = std::getenv("SR_LIST_HEAD")) ctx->enc.list_head = std::max(0, std::atoi(m));
   *out = ctx;
   return SR_OK;
 }
@@ -1163,6 +1371,12 @@ void sr_destroy(sr_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) (void)rccl().comm_destroy(ctx->comm);
+  if (ctx->shm.host) {
+    if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+    (void)hipHostUnregister(ctx->shm.host);
+    munmap(ctx->shm.host, ctx->shm.bytes);
+    if (ctx->rank == 0) shm_unlink(ctx->shm.name.c_str());  // the ranks keep their mappings
+  }
   for (DevBuf* b : {&ctx->out_node, &ctx->out_status, &ctx->out_bytes, &ctx->dmin, &ctx->prof,
                     &ctx->scratch})
     if (b->p) (void)hipFree(b->p);
@@ -1382,6 +1596,53 @@ sr_status sr_comm_unique_id(uint8_t out[SR_UNIQUE_ID_BYTES]) {
   static_assert(sizeof(id) == SR_UNIQUE_ID_BYTES, "ncclUniqueId size");
   if (!rccl().ok || rccl().get_unique_id(&id) != ncclSuccess) return SR_ERR_RCCL;
   std::memcpy(out, &id, sizeof(id));
+  return SR_OK;
+}
+
+sr_status sr_comm_init_shm(sr_ctx* ctx, const char* name, uint32_t session, int32_t nranks, int32_t rank,
+                           int32_t max_cand) {
+  if (!ctx || !name || name[0] != '/' || nranks < 1 || rank < 0 || rank >= nranks || max_cand < 1 ||
+      max_cand > (1 << 28) || has_comm(ctx))
+    return SR_ERR_INVALID_ARG;
+  if (hipSetDevice(ctx->device) != hipSuccess) return SR_ERR_HIP;
+  const size_t words = static_cast<size_t>(nranks) * 2 * (kShmHdr + 2 * static_cast<size_t>(max_cand));
+  const size_t bytes = (words * sizeof(uint64_t) + 4095) & ~size_t(4095);
+  const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+  if (fd < 0) {
+    ctx->err = std::string("shm_open(") + name + "): " + std::strerror(errno);
+    return SR_ERR_RCCL;
+  }
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || (sb.st_size != 0 && static_cast<size_t>(sb.st_size) != bytes) ||
+      (sb.st_size == 0 && ftruncate(fd, static_cast<off_t>(bytes)) != 0)) {  // every rank sizes it alike
+    ctx->err = std::string("shared segment ") + name + ": size mismatch or " + std::strerror(errno) +
+               " (every rank passes the same nranks and max_cand)";
+    close(fd);
+    return SR_ERR_RCCL;
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) {
+    ctx->err = std::string("mmap: ") + std::strerror(errno);
+    return SR_ERR_RCCL;
+  }
+  void* dp = nullptr;
+  hipError_t e = hipHostRegister(p, bytes, hipHostRegisterMapped);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, p, 0);
+  if (e != hipSuccess) {
+    munmap(p, bytes);
+    return hip_fail(ctx, e, "hipHostRegister(shared segment)");
+  }
+  auto& S = ctx->shm;
+  S.host = static_cast<uint64_t*>(p);
+  S.dev = static_cast<uint64_t*>(dp);
+  S.bytes = bytes;
+  S.max_cand = max_cand;
+  S.session = session;
+  S.tick = 0;
+  S.name = name;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
   return SR_OK;
 }
 

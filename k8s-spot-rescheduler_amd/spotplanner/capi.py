@@ -147,7 +147,8 @@ class sr_timing(ctypes.Structure):
                 ("prefix_batches", ctypes.c_int32), ("enc_memo_pods", ctypes.c_int32),
                 ("enc_reused", ctypes.c_int32), ("enc_pod_patches", ctypes.c_int32),
                 ("k0_columns", ctypes.c_int32), ("k0_rows_moved", ctypes.c_int32), ("k0_dirty_nodes", ctypes.c_int32),
-                ("ms_collective", ctypes.c_double)]
+                ("ms_collective", ctypes.c_double), ("k2_launches", ctypes.c_int32),
+                ("k2_list_by_cost", ctypes.c_int32), ("k2_coop", ctypes.c_int32)]
 
 
 def ptr(arr, typ):
@@ -359,6 +360,9 @@ def _declare_planner(lib):
     lib.sr_comm_init.restype = S
     lib.sr_comm_init_host.argtypes = [VP, ctypes.c_int32, ctypes.c_int32, ALLREDUCE_MIN_FN, VP]
     lib.sr_comm_init_host.restype = S
+    lib.sr_comm_init_shm.argtypes = [VP, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.c_int32]
+    lib.sr_comm_init_shm.restype = S
 
 
 # Every symbol include/sr_planner.h declares (checked by tests on CPU).
@@ -368,4 +372,5 @@ EXPORTED = ["sr_new_node_map", "sr_node_map_cache_create", "sr_node_map_cache_de
             "sr_snapshot_add_pod", "sr_snapshot_fork", "sr_snapshot_revert", "sr_snapshot_node_state",
             "sr_snapshot_num_nodes", "sr_create", "sr_destroy", "sr_last_error", "sr_build_info",
             "sr_abi_version", "sr_find_spot_nodes", "sr_can_drain_node", "sr_plan", "sr_plan_first", "sr_plan_prepare", "sr_plan_run",
-            "sr_set_timing", "sr_get_timing", "sr_comm_unique_id", "sr_comm_init", "sr_comm_init_host"]
+            "sr_set_timing", "sr_get_timing", "sr_comm_unique_id", "sr_comm_init", "sr_comm_init_host",
+            "sr_comm_init_shm"]

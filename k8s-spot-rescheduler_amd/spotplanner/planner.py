@@ -84,6 +84,14 @@ class PredicateChecker:
         _check(self.lib, self.lib.sr_comm_init_host(self.handle, nranks, rank, self._collective, None), self.handle,
                "sr_comm_init_host")
 
+    def attach_shared_memory(self, name: str, session: int, nranks: int, rank: int, max_cand: int):
+        """sr_comm_init_shm: the ranks of one node reduce each tick through one
+        shared-memory segment (`name`, identical on every rank): each rank's K2
+        writes its outcomes there and each host walks them in global candidate
+        order; shards must be interleaved (cand_global = (first + i) * nranks + rank)."""
+        _check(self.lib, self.lib.sr_comm_init_shm(self.handle, name.encode(), session & 0xffffffff, nranks, rank,
+                                                   max_cand), self.handle, "sr_comm_init_shm")
+
 
 def NewTestPredicateChecker(device: int = 0):
     """simulator.NewTestPredicateChecker() -> (checker, err) (rescheduler_test.go:41)."""

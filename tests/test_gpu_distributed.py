@@ -1,17 +1,21 @@
 """The product's sharded path at world size 2 on one GPU, through its own
-collective: two processes each plan their shard of the candidates through
-libsrplanner with a communicator attached (sr_comm_init_host: RCCL does not
-run two ranks on one device, so the allreduce(min) of the planner's three
-result words goes over gloo instead).  Everything else is the multi-GPU code
-path of bench.py's ranks: K0 + K2 per shard, the collective on the packed
-{global << 32 | local} words, K3 on every rank (the owner writes the mapping),
+transports: two processes each plan their shard of the candidates through
+libsrplanner with a communicator attached, either
+- `host_fn` (sr_comm_init_host: RCCL does not run two ranks on one device, so
+  the allreduce(min) of the planner's three result words goes over gloo):
+  K0 + K2 per shard, the collective on the packed {global << 32 | local}
+  words, K3 on every rank (the owner writes the mapping); or
+- `shm` (sr_comm_init_shm, bench.py's default on one node): every rank's K2
+  writes its outcome words into one shared-memory segment and each rank's
+  host walks them in global order -- no collective, no K3;
 and sr_plan_first's prefix batches stopping on the reduced bound.
 
 Checked against the oracle (rescheduler.go:228-287 evaluates the same
 candidates serially): sr_plan with interleaved shards (statuses, mappings,
 winner, the owner's mapping); sr_plan_first with interleaved AND contiguous
 shards, prefix batches of 2 and 16, on scenarios whose fallback candidates
-sit before, after and instead of the first drainable one."""
+sit before, after and instead of the first drainable one (the shared-memory
+transport takes interleaved shards only and refuses contiguous ones)."""
 import os
 import socket
 
@@ -60,7 +64,7 @@ def _run_first(lib, ck, h, cptr, loff, lpods, gidx):
                 batches=int(ck.timing().prefix_batches))
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, transport):
     import ctypes
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -84,6 +88,12 @@ def _worker(rank, world, port, out):
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return [int(x) + bias for x in t]
 
+    def attach(ck, name):
+        if transport == "shm":  # one segment per planner, the same name and session on both ranks
+            ck.attach_shared_memory("/srtest-%d-%s" % (port, name), port * 7919, world, rank, 4096)
+        else:
+            ck.attach_collective(world, rank, allreduce_min)
+
     results = {}
     try:
         lib = capi.load_planner()
@@ -91,8 +101,9 @@ def _worker(rank, world, port, out):
         for b in (16, 2):
             os.environ["SR_PREFIX_BATCH"] = str(b)
             checkers[b] = PredicateChecker(0)
-            checkers[b].attach_collective(world, rank, allreduce_min)
+            attach(checkers[b], "b%d" % b)
         del os.environ["SR_PREFIX_BATCH"]
+        dist.barrier()  # every rank attached before any plans (or rank 0's planner could unlink the name)
         # sr_plan over synthetic clusters: every candidate, interleaved shards
         for cfg in [(3, 240, 600, 0.3), (5, 200, 500, -1.0)]:
             config, n_od, n_spot, pinned = cfg
@@ -116,7 +127,8 @@ def _worker(rank, world, port, out):
             lib.sr_snapshot_destroy(h)
             if config == 3:  # steady ticks through the collective: reuse, K0-less and incremental K0 runs
                 ck = PredicateChecker(0)
-                ck.attach_collective(world, rank, allreduce_min)
+                attach(ck, "steady")
+                dist.barrier()
                 rng = np.random.default_rng(77)  # the same changes on both ranks
                 extra = []
                 for t in range(8):
@@ -138,6 +150,7 @@ def _worker(rank, world, port, out):
                         mine={int(g): (int(s_), [int(x) for x in p.node_of_pod[loff[k]:loff[k + 1]]])
                               for k, (g, s_) in enumerate(zip(gidx, p.status))})
                     lib.sr_snapshot_destroy(h)
+                dist.barrier()
                 ck.close()
         # sr_plan_first: fallback patterns, both shardings, both batch sizes
         for seed in SEEDS:
@@ -150,8 +163,16 @@ def _worker(rank, world, port, out):
             for split, fn in (("interleaved", shard), ("contiguous", _contiguous)):
                 loff, lpods, gidx = fn(cand_off, cand_pods, rank, world)
                 for b, ck in checkers.items():
+                    if transport == "shm" and split == "contiguous":  # refused before anything is planned
+                        c = capi.sr_candidates(len(loff) - 1, capi.ptr(loff, capi.P32), capi.ptr(lpods, capi.P32),
+                                               capi.ptr(gidx, capi.P32))
+                        o = capi.sr_plan_out()
+                        results[("first", seed, split, b)] = {
+                            "refused": lib.sr_plan_first(ck.handle, h, sc.ptr, ctypes.byref(c), ctypes.byref(o))}
+                        continue
                     results[("first", seed, split, b)] = _run_first(lib, ck, h, sc.ptr, loff, lpods, gidx)
             lib.sr_snapshot_destroy(h)
+        dist.barrier()  # no rank closes (rank 0: unlinks) a segment another still plans through
         for ck in checkers.values():
             ck.close()
         gathered = [None] * world
@@ -162,13 +183,13 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-@pytest.fixture(scope="module")
-def two_rank_results():
+@pytest.fixture(scope="module", params=["host_fn", "shm"])
+def two_rank_results(request):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, request.param)) for r in range(WORLD)]
     for p in procs:
         p.start()
     gathered = q.get(timeout=240)
@@ -227,8 +248,12 @@ def test_two_ranks_plan_every_candidate_through_the_collective(two_rank_results,
 
 def _check_first(two_rank_results, key, ref_all, ref_early, cand_off):
     from plan_first_cases import check_plan_first
+    from spotplanner import capi
     n = len(cand_off) - 1
     results = [res[key] for res in two_rank_results]
+    if "refused" in results[0]:  # the shared-memory transport and contiguous shards
+        assert all(r["refused"] == capi.SR_ERR_INVALID_ARG for r in results), results
+        return
     for r in results:  # the reduced outcome is the same on every rank
         assert (r["first_ok"], r["first_fallback"], r["winner"], r["batches"]) == \
             (results[0]["first_ok"], results[0]["first_fallback"], results[0]["winner"], results[0]["batches"])

@@ -1,0 +1,200 @@
+"""K2's dispatch forms against the oracle at test size.
+
+Three paths are on by default only on large work lists, so the full-size
+configs reach them only in the bench (C4: 15,000 candidates):
+
+- the split launch (planner.cpp `k2_split`): a list with domain-path
+  candidates and more entries than SR_K2_SPLIT_MIN (4,096) runs in two kernels
+  side by side, the node-order candidates on the node-order kernel and the rest
+  on the general kernel on a second stream; both write d_min and the
+  single-rank result words;
+- the cost-ordered work list (`list_cost`, lists above SR_LIST_COST_MIN =
+  2,048 entries): the first run of a candidate generation records each
+  candidate's wave duration, and the reused workloads of the next ticks
+  dispatch the longest waves first;
+- four waves per block (lists above 2,048 entries).
+
+Each planner here lowers those thresholds per context (environment at
+sr_create) so a 300-candidate cluster takes them, and every tick's statuses,
+mappings, first_ok / first_fallback / winner and winner-only result are
+compared with the oracle.  The winner is the first drainable candidate
+whatever the dispatch order (rescheduler.go:269-287)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from oracle_lib import OracleSnapshot, oracle_plan
+from spotplanner import capi
+from spotplanner.rescheduler import plan_arrays
+from spotplanner.synth import AFFINITY, SynthCluster, build_candidates, new_node_map
+from test_gpu_parity import compare_plans
+from test_gpu_ticks import _with_extra
+
+pytestmark = pytest.mark.gpu
+
+
+def make_checker(**env):
+    from spotplanner.planner import PredicateChecker
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return PredicateChecker(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+DISPATCH = {
+    # split launch + cost order, a short list head (head and rest parts in each split part)
+    "split_cost_head32": dict(SR_K2_SPLIT_MIN=64, SR_LIST_COST_MIN=0, SR_LIST_HEAD=32),
+    # split launch + cost order, four waves per block, the default list head (one part)
+    "split_cost_wpb4": dict(SR_K2_SPLIT_MIN=64, SR_LIST_COST_MIN=0, SR_K2_WPB=4),
+    # cost order without the split (one kernel: the general one)
+    "cost_nosplit": dict(SR_K2_SPLIT=0, SR_LIST_COST_MIN=0, SR_LIST_HEAD=16),
+}
+
+
+def _ticks(ck, sc, n_ticks, rng, expect_split, per_tick_extra=(1, 4)):
+    """Fresh snapshots of `sc`, each with a changing set of extra pods on random
+    spot nodes (the candidate input stays the same, so the encoder reuses its
+    candidate side from the third tick); every tick planned in full and
+    winner-only, both against the oracle."""
+    lib = capi.load_planner()
+    nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+    cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+    extra, by_cost, reused, splits = [], 0, 0, 0
+    for tick in range(n_ticks):
+        if tick % 6 == 5:
+            extra.clear()
+        if tick:
+            for _ in range(int(rng.integers(*per_tick_extra))):
+                extra.append((int(rng.choice(cand_pods)), int(rng.integers(len(nm.spot)))))
+        off, idx = _with_extra(nm, sc.n_nodes, extra)
+        h = ctypes.c_void_p()
+        assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot), capi.ptr(off, capi.P32),
+                                      capi.ptr(idx, capi.P32), ctypes.byref(h)) == capi.SR_OK
+        try:
+            o = oracle_plan(OracleSnapshot(sc.ptr, nm.spot, off, idx), sc.ptr, cand_off, cand_pods, mode=1,
+                            threads=8)
+            q = plan_arrays(ck, h, sc.ptr, cand_off, cand_pods, full=False)  # winner only: returns at the winner
+            tq = ck.timing()
+            p = plan_arrays(ck, h, sc.ptr, cand_off, cand_pods)
+            t = ck.timing()
+        finally:
+            lib.sr_snapshot_destroy(h)
+        compare_plans(o, p, cand_off)
+        assert np.array_equal(p.status, o["status"]), tick
+        assert (q.first_ok, q.first_fallback, q.winner) == (p.first_ok, p.first_fallback, p.winner), tick
+        assert np.array_equal(q.winner_map, p.winner_map), tick
+        for tt in (tq, t):
+            assert tt.k2_launches == (2 if expect_split else 1), (tick, tt.k2_launches)
+            splits += tt.k2_launches == 2
+        if tick >= 2:
+            reused += t.enc_reused
+            by_cost += tq.k2_list_by_cost + t.k2_list_by_cost
+    return reused, by_cost, splits
+
+
+@pytest.mark.parametrize("which", sorted(DISPATCH))
+def test_affinity_ticks_split_launch_and_cost_order(which):
+    """The affinity variant (hostname anti-affinity state bits, zone-spread
+    replicas on the domain path) over ten ticks: from the third tick the
+    candidate side is reused and the work list runs in cost order."""
+    ck = make_checker(**DISPATCH[which])
+    try:
+        sc = SynthCluster(3, seed=41, n_on_demand=300, n_spot=600, **AFFINITY)
+        reused, by_cost, splits = _ticks(ck, sc, 10, np.random.default_rng(41), expect_split=which != "cost_nosplit")
+        assert reused >= 6, reused
+        assert by_cost >= 10, by_cost  # both runs of most reused ticks
+    finally:
+        ck.close()
+
+
+def test_affinity_domain_path_candidates_exist():
+    """The split needs domain-path candidates in the list: the affinity cluster
+    above has them (the domain path plans zone-spread replicas that count each
+    other)."""
+    ck = make_checker(SR_K2_SPLIT_MIN=64)
+    try:
+        sc = SynthCluster(3, seed=41, n_on_demand=300, n_spot=600, **AFFINITY)
+        lib = capi.load_planner()
+        nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+        cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+        h = ctypes.c_void_p()
+        assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot),
+                                      capi.ptr(nm.node_pod_off, capi.P32), capi.ptr(nm.node_pod_idx, capi.P32),
+                                      ctypes.byref(h)) == capi.SR_OK
+        try:
+            plan_arrays(ck, h, sc.ptr, cand_off, cand_pods)
+            assert ck.timing().k2_launches == 2
+        finally:
+            lib.sr_snapshot_destroy(h)
+    finally:
+        ck.close()
+
+
+@pytest.mark.parametrize("config", [3, 5])
+def test_cost_order_k0_less_ticks(config):
+    """The cost-ordered list on the node-order kernel with K0-less steady ticks
+    (one to three pods added on spot nodes between ticks: K2 recomputes the
+    changed nodes' bits) and host-port candidates (C5)."""
+    ck = make_checker(SR_LIST_COST_MIN=0, SR_LIST_HEAD=64)
+    try:
+        sc = SynthCluster(config, seed=43, n_on_demand=300, n_spot=600)
+        reused, by_cost, _ = _ticks(ck, sc, 10, np.random.default_rng(config), expect_split=False)
+        assert reused >= 6 and by_cost >= 10, (reused, by_cost)
+    finally:
+        ck.close()
+
+
+def test_timed_runs_across_k0_and_k0_less_ticks():
+    """Timing on (every kernel bracketed with events) while ticks alternate
+    between runs that launch K0 and K0-less ones: an event pair is taken only
+    for a kernel that is launched, so reading the times back never meets an
+    unrecorded event (an A/B arm once failed here with `invalid resource
+    handle`)."""
+    ck = make_checker()
+    try:
+        sc = SynthCluster(3, seed=44, n_on_demand=200, n_spot=450)
+        lib = capi.load_planner()
+        nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+        cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+        c = capi.sr_candidates(len(cand_off) - 1, capi.ptr(cand_off, capi.P32), capi.ptr(cand_pods, capi.P32), None)
+        wmap = np.full(int(np.max(np.diff(cand_off))), -1, np.int32)
+        out = capi.sr_plan_out()
+        out.winner_map = capi.ptr(wmap, capi.P32)
+        ck.set_timing(7)
+        k0_less, k0_runs, runs = 0, 0, 0
+        rng = np.random.default_rng(44)
+        extra = []
+        for tick in range(8):
+            if tick >= 2:
+                extra.append((int(rng.choice(cand_pods)), int(rng.integers(len(nm.spot)))))
+            off, idx = _with_extra(nm, sc.n_nodes, extra)
+            h = ctypes.c_void_p()
+            assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot), capi.ptr(off, capi.P32),
+                                          capi.ptr(idx, capi.P32), ctypes.byref(h)) == capi.SR_OK
+            try:
+                assert lib.sr_plan_prepare(ck.handle, h, sc.ptr, ctypes.byref(c)) == capi.SR_OK, ck.last_error()
+                cols = ck.timing().k0_columns
+                k0_less += cols == -2
+                k0_runs += cols != -2
+                for _ in range(3):
+                    assert lib.sr_plan_run(ck.handle, ctypes.byref(out)) == capi.SR_OK, ck.last_error()
+                    runs += 1
+                o = oracle_plan(OracleSnapshot(sc.ptr, nm.spot, off, idx), sc.ptr, cand_off, cand_pods, mode=1,
+                                threads=8)
+                assert out.winner == o["winner"], tick
+            finally:
+                lib.sr_snapshot_destroy(h)
+            t = capi.sr_timing()
+            assert lib.sr_get_timing(ck.handle, ctypes.byref(t)) == capi.SR_OK, ck.last_error()
+            assert t.n_runs == runs and t.ms_placement > 0
+        assert k0_less >= 2 and k0_runs >= 2, (k0_less, k0_runs)
+    finally:
+        ck.close()
