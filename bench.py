@@ -433,8 +433,8 @@ def measure_ticks(lib, checker, sc, rank, world, args):
     st = lib.sr_plan_run(checker.handle, ctypes.byref(full))
     assert st == capi.SR_OK, (st, checker.last_error())
     tm = checker.timing()
-    return dict(nm=nm, cand_off=cand_off, cand_pods=cand_pods, loff=loff, lpods=lpods, snap=snap, cands=cands,
-                out=out, wmap=wmap, full=full, status=status, nodes_out=nodes_out, mutation=mutation, steady=steady,
+    return dict(nm=nm, cand_off=cand_off, cand_pods=cand_pods, loff=loff, lpods=lpods, gidx=gidx, snap=snap,
+                cands=cands, out=out, wmap=wmap, full=full, status=status, nodes_out=nodes_out, mutation=mutation, steady=steady,
                 pfd_ms=pfd_ms, pack_ms=pack_ms, breakdown=breakdown, dom=dom, dom_ms=dom_ms, elapsed=elapsed,
                 total_issued=total_issued, total_dense=total_dense, tm=tm, issued_local=issued_local,
                 per_rank=per_rank, mut_pod=mut_pod, mut_pos=mut_pos)
@@ -514,30 +514,15 @@ def main():
     variant_kw = {"realistic": REALISTIC, "affinity": AFFINITY}.get(args.variant, {})
     sc = SynthCluster(args.config, n_on_demand=cluster_on_demand(args.config, world, args.scaling), **variant_kw)
     M = measure_ticks(lib, checker, sc, rank, world, args)
+    # (loff / lpods / gidx stay referenced: `cands` points into them)
     nm, cand_off, cand_pods, loff, lpods = M["nm"], M["cand_off"], M["cand_pods"], M["loff"], M["lpods"]
+    gidx = M["gidx"]  # noqa: F841
     snap, cands, out, wmap, full = M["snap"], M["cands"], M["out"], M["wmap"], M["full"]
     status, nodes_out, mutation, steady = M["status"], M["nodes_out"], M["mutation"], M["steady"]
     pfd_ms, pack_ms, breakdown, dom, dom_ms = M["pfd_ms"], M["pack_ms"], M["breakdown"], M["dom"], M["dom_ms"]
     elapsed, total_issued, total_dense, tm = M["elapsed"], M["total_issued"], M["total_dense"], M["tm"]
     issued_local, per_rank, mut_pod, mut_pos = M["issued_local"], M["per_rank"], M["mut_pod"], M["mut_pos"]
     ms_step = 1e3 * elapsed / args.steps
-    # N > 1, strong scaling (the line): the weak-scaled tick beside it, labelled
-    # -- every rank one config-sized candidate set over the same spot pool
-    weak_scaling = None
-    if world > 1 and args.scaling == "strong" and not args.no_weak_beside:
-        sw = SynthCluster(args.config, n_on_demand=cluster_on_demand(args.config, world, "weak"), **variant_kw)
-        W = measure_ticks(lib, checker, sw, rank, world, args)
-        weak_scaling = {
-            "scaling": "weak", "value": W["total_issued"] / W["elapsed"] * args.steps if W["elapsed"] > 0 else 0.0,
-            "unit": "checks/s", "ms_per_step": 1e3 * W["elapsed"] / args.steps,
-            "plans_per_s": (len(W["cand_off"]) - 1) / (W["elapsed"] / args.steps),
-            "workload": workload_name(args.config, sw.n_nodes, len(W["nm"].on_demand), len(W["nm"].spot), sw.n_pods,
-                                      world, "weak", args.variant),
-            "candidates_per_rank": shard_sizes(len(W["cand_off"]) - 1, world), "per_rank": W["per_rank"],
-            "first_ok": int(W["out"].first_ok), "winner": int(W["out"].winner),
-            "note": "not the line's value: N x the config's candidates over the same spot pool (weak scaling), "
-                    "measured after the line in the same job"}
-        lib.sr_snapshot_destroy(W["snap"])
 
     # Result latency of one tick on an idle device: sr_plan_run from the launch
     # to the winner and its mapping in host memory.  On one rank the run returns
@@ -749,6 +734,25 @@ def main():
                               "sr_new_node_map_cached -> sr_pods_for_deletion -> sr_snapshot_refresh_cached of the "
                               "previous tick's snapshot -> sr_plan_first; fresh: sr_new_node_map and "
                               "sr_snapshot_create every tick"})
+
+    # N > 1, strong scaling (the line): the weak-scaled tick beside it, labelled
+    # -- every rank one config-sized candidate set over the same spot pool (after
+    # the latency and end-to-end sections, which plan the line's workload)
+    weak_scaling = None
+    if world > 1 and args.scaling == "strong" and not args.no_weak_beside:
+        sw = SynthCluster(args.config, n_on_demand=cluster_on_demand(args.config, world, "weak"), **variant_kw)
+        W = measure_ticks(lib, checker, sw, rank, world, args)
+        weak_scaling = {
+            "scaling": "weak", "value": W["total_issued"] / W["elapsed"] * args.steps if W["elapsed"] > 0 else 0.0,
+            "unit": "checks/s", "ms_per_step": 1e3 * W["elapsed"] / args.steps,
+            "plans_per_s": (len(W["cand_off"]) - 1) / (W["elapsed"] / args.steps),
+            "workload": workload_name(args.config, sw.n_nodes, len(W["nm"].on_demand), len(W["nm"].spot), sw.n_pods,
+                                      world, "weak", args.variant),
+            "candidates_per_rank": shard_sizes(len(W["cand_off"]) - 1, world), "per_rank": W["per_rank"],
+            "first_ok": int(W["out"].first_ok), "winner": int(W["out"].winner),
+            "note": "not the line's value: N x the config's candidates over the same spot pool (weak scaling), "
+                    "measured after the line in the same job"}
+        lib.sr_snapshot_destroy(W["snap"])
 
     if rank == 0:
         alg = {"k2_placement": tm.bytes_placement, "k0_tables": tm.bytes_tables}[dom]
