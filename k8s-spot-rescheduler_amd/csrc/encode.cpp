@@ -1130,9 +1130,20 @@ void analyse_spread(EncoderCache& C, const sr_snapshot* snap, const sr_cluster* 
 
 }  // namespace
 
-void reorder_list_by_cost(Workload& w, const uint32_t* cycles, int32_t head) {
+void reorder_list_by_cost(Workload& w, const uint32_t* cycles, int32_t head, int32_t n_front) {
   const size_t n = w.list.size() / 4;
+  auto cost = [&](size_t j) { return cycles[w.list[j * 4]]; };
+  std::vector<int8_t> front(n, 0);
+  std::vector<int32_t> first;  // entries of the first part (the node-order kernel's when the list is split)
+  for (size_t j = 0; j < n; ++j)
+    if (w.n_list_node == 0 || static_cast<int32_t>(j) < w.n_list_node) first.push_back(static_cast<int32_t>(j));
+  const size_t nf = std::min(first.size(), static_cast<size_t>(std::max(0, n_front)));
+  std::nth_element(first.begin(), first.begin() + static_cast<std::ptrdiff_t>(nf), first.end(),
+                   [&](int32_t a, int32_t b) { return cost(static_cast<size_t>(a)) > cost(static_cast<size_t>(b)); });
+  for (size_t i = 0; i < nf; ++i) front[static_cast<size_t>(first[i])] = 1;
+  w.n_coop_front = static_cast<int32_t>(nf);
   auto part = [&](size_t j) {
+    if (front[j]) return -1;
     return (w.n_list_node > 0 && static_cast<int32_t>(j) >= w.n_list_node ? 2 : 0) + (w.list[j * 4] < head ? 0 : 1);
   };
   std::vector<int32_t> order(n);

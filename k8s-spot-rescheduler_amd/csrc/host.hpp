@@ -556,6 +556,9 @@ struct Workload {
   // (max_np_node their largest pod count), then the rest (domain path, more
   // than 256 pods: the general kernel).  0: one part, the list in plain order.
   int32_t n_list_node = 0, max_np_node = 0;
+  // reorder_list_by_cost moved the costliest entries of the first part to the
+  // front of the list (the node-order kernel's cooperative blocks take them)
+  int32_t n_coop_front = 0;
   // ---- domain path: candidates whose pods interact through a topology key
   // with shared domains (antiaff.cpp), planned by K2's k2_domain
   std::vector<int32_t> dyn_cand;  // [n_active] first record in dyn_pod, -1: other paths (empty: none)
@@ -625,6 +628,7 @@ struct Workload {
     for (int32_t& t : t_off) t = 0;
     max_cand_pods = 0;
     n_list_node = max_np_node = 0;
+    n_coop_front = 0;
     first_fallback = -1;
     fallback_pods = 0;
     n_input_cand = n_input_pods = pod_base = 0;
@@ -882,8 +886,10 @@ struct SpreadDyn {
 // The work list of a reused workload in the order of each candidate's wave
 // duration in its last run (`cycles`, by active candidate), longest first,
 // within the parts the list was built in (the head, the rest; the split
-// launch's two kernels); list_ext follows.
-void reorder_list_by_cost(Workload& w, const uint32_t* cycles, int32_t list_head);
+// launch's two kernels), after the n_front longest entries of the first part
+// (the node-order kernel's), which go to the front (Workload::n_coop_front);
+// list_ext follows.
+void reorder_list_by_cost(Workload& w, const uint32_t* cycles, int32_t list_head, int32_t n_front);
 
 // Builds the workload; returns SR_OK or an error with *err filled.  `cache`
 // carries what the previous calls derived (and is updated).

@@ -851,10 +851,8 @@ __device__ __forceinline__ int k2_run(const DevWorkload& w, K2Lds& L, const int 
 // window moves or a pointer moves beyond the head.  Measured against visiting
 // one node at a time (prefix-sum run passes over the pods pointing at it):
 // C3 K2 17.7 -> 13.1 us, C5 61 -> 42 us.
-#ifndef SR_K2_NH
-#define SR_K2_NH 8
-#endif
-constexpr int kNH = SR_K2_NH;      // F head words per pod kept in LDS (8: nodes [0, 512))
+// F head words per pod kept in LDS (8: nodes [0, 512); measured against 4 and 2: DESIGN §4)
+constexpr int kNH = 8;
 static_assert(kNH == 2 || kNH == 4 || kNH == 8, "head words per pod: a power of two up to 8 (8-bit head masks)");
 constexpr int kNHS = kNH + 1;      // LDS stride per pod (odd number of words: conflict-free b64 reads)
 constexpr int kFar = 64 * kNH;     // pointer sentinel: next feasible node lies at or beyond the head, unresolved
@@ -1064,26 +1062,16 @@ __device__ __forceinline__ int32_t scale32(int64_t f, int k) {
 // exactly when every test passes, so the pod-count, cpu, memory (ephemeral,
 // state-bit) checks cost one ballot instead of three to five chained through
 // VCC.
-#ifndef SR_K2_LEAN_STEP
-#define SR_K2_LEAN_STEP 1
-#endif
 template <bool E, bool O>
 __device__ __forceinline__ uint64_t fits32(int32_t c32, int32_t m32, int32_t e32, int nleft, uint64_t conflict,
                                            int32_t c, int32_t m, int32_t e) {
-  if constexpr (SR_K2_LEAN_STEP) {
-    int32_t t = __builtin_elementwise_sub_sat(c32, c) | __builtin_elementwise_sub_sat(m32, m) | (nleft - 1);
-    if (E) t |= __builtin_elementwise_sub_sat(e32, e);
-    if (O) {
-      const uint32_t x = static_cast<uint32_t>(conflict) | static_cast<uint32_t>(conflict >> 32);
-      t |= static_cast<int32_t>(x | (0u - x));
-    }
-    return ballot(t >= 0);
-  } else {
-    uint64_t f = ballot(nleft >= 1) & ballot(c32 >= c) & ballot(m32 >= m);
-    if (E) f &= ballot(e32 >= e);
-    if (O) f &= ballot(conflict == 0);
-    return f;
+  int32_t t = __builtin_elementwise_sub_sat(c32, c) | __builtin_elementwise_sub_sat(m32, m) | (nleft - 1);
+  if (E) t |= __builtin_elementwise_sub_sat(e32, e);
+  if (O) {
+    const uint32_t x = static_cast<uint32_t>(conflict) | static_cast<uint32_t>(conflict >> 32);
+    t |= static_cast<int32_t>(x | (0u - x));
   }
+  return ballot(t >= 0);
 }
 
 // place_window with the window's state and the pods' requests scaled to 32
@@ -1245,17 +1233,162 @@ struct Narrow {
   int kc, km, ke;
 };
 
+// ------------------------------------------------ K2, cooperative resolution
+// The costliest candidates of a long work list get a block of kCoopWaves
+// waves instead of one (C4: its longest wave spent ~60 % of its cycles in one
+// far resolution -- several pods leaving the 512-node head together and
+// scanning their 548-word rows 64 words per dependent round trip).  Wave 0
+// keeps the candidate's placement chain; when pods need a far resolution it
+// posts them in LDS and every wave of the block scans a share of the chunks
+// (chunk k of the request to wave k % kCoopWaves, in order), so a resolution
+// costs about chunks / kCoopWaves round trips instead of `chunks`.  Each wave
+// records, per pod, the first chunk of its share with a non-zero word; the
+// chain takes the lowest over the waves: the same first feasible node a
+// sequential scan finds (findSpotNodeForPod's first fit, rescheduler.go:
+// 339-352, the scan over spot nodes being a first-set-bit reduction).
+constexpr int kCoopWaves = 4;
+constexpr int kCoopPods = 64;
+struct CoopArea {
+  int32_t cmd, n, sw, pad;                 // cmd 0: a resolution request of n pods from word sw; 1: exit
+  uint64_t r01[kCoopPods], r23[kCoopPods];  // the pods' row offsets
+  int64_t rq[kCoopPods][3];                 // ... requests (K0-less corrections)
+  int32_t op[kCoopPods][8];                 // ... class programs (head-only S rows)
+  uint32_t best[kCoopPods];                 // lowest chunk found by any wave so far (skips higher ones)
+  uint32_t rk[kCoopWaves][kCoopPods];       // per wave: first chunk of its share with a non-zero word (~0: none)
+  uint64_t rm[kCoopWaves][kCoopPods];       //   its non-zero-word mask
+  uint64_t rf[kCoopWaves][kCoopPods];       //   its first non-zero word
+};
+
+// Wave h's share of a request: chunks k = h, h + kCoopWaves, ... from the
+// request's first chunk, each for every pod not resolved by a lower chunk
+// yet, Q pods' loads in flight per round trip (as the chain's own resolve).
+template <bool HO>
+__device__ __forceinline__ void coop_scan(const DevWorkload& w, CoopArea& A, int h) {
+  const int lane = threadIdx.x & 63;
+  const int n = __builtin_amdgcn_readfirstlane(A.n), sw = __builtin_amdgcn_readfirstlane(A.sw);
+  const int Wp = w.Wp;
+  const uint64_t* __restrict__ tab = w.S;
+  if (lane < n) A.rk[h][lane] = 0xffffffffu;
+  const int cb0 = (sw >> 6) << 6;
+  const int nch = (Wp - cb0 + 63) >> 6;
+  const uint64_t all = n >= 64 ? ~0ull : (1ull << n) - 1;
+  uint64_t found = 0;  // pods this wave resolved
+  constexpr int Q = HO ? 2 : 4;
+  for (int k = h; k < nch; k += kCoopWaves) {
+    const int cb = cb0 + 64 * k;
+    const int word = cb + lane;
+    const bool wv = word >= sw && word < Wp;
+    const uint32_t wi = wv ? static_cast<uint32_t>(word) : 0u;
+    const uint64_t vw = ballot(wv);
+    // pods open at chunk k: not resolved by this wave, no lower chunk found by another
+    uint64_t open = all & ~found & ballot(lane < n && __hip_atomic_load(&A.best[lane], __ATOMIC_RELAXED,
+                                                                           __HIP_MEMORY_SCOPE_WORKGROUP) >
+                                                        static_cast<uint32_t>(k));
+    while (open != 0) {
+      int js[Q];
+      uint64_t a01[Q], a23[Q];
+      int op[Q][8];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        js[q] = open != 0 ? __builtin_ctzll(open) : -1;
+        open &= open - 1;
+        const int j = js[q] < 0 ? 0 : js[q];
+        a01[q] = readlane64(A.r01[j], 0);
+        a23[q] = readlane64(A.r23[j], 0);
+        if constexpr (HO) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) op[q][u] = __builtin_amdgcn_readfirstlane(A.op[j][u]);
+        }
+      }
+      uint64_t x[Q][HO ? 11 : 4];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (js[q] < 0) continue;  // wave-uniform
+        if constexpr (HO) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            x[q][u] = op[q][u] >= 0 ? w.atoms[static_cast<size_t>(op[q][u] >> 2) * Wp + wi] : 0ull;
+          x[q][8] = tab[static_cast<uint32_t>(a01[q] >> 32) + wi];
+          x[q][9] = tab[static_cast<uint32_t>(a23[q]) + wi];
+          x[q][10] = tab[static_cast<uint32_t>(a23[q] >> 32) + wi];
+        } else {
+          x[q][0] = tab[static_cast<uint32_t>(a01[q]) + wi];
+          x[q][1] = tab[static_cast<uint32_t>(a01[q] >> 32) + wi];
+          x[q][2] = tab[static_cast<uint32_t>(a23[q]) + wi];
+          x[q][3] = tab[static_cast<uint32_t>(a23[q] >> 32) + wi];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (js[q] < 0) continue;  // wave-uniform
+        const int j = js[q];
+        uint64_t f, sw0;
+        if constexpr (HO) {
+          uint64_t v8[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v8[u] = x[q][u];
+          sw0 = eval_prog8(op[q], v8);
+          f = sw0 & x[q][8] & x[q][9] & x[q][10];
+        } else {
+          sw0 = x[q][0];
+          f = x[q][0] & x[q][1] & x[q][2] & x[q][3];
+        }
+        if (w.k0_skip) {
+          const int64_t rc = A.rq[j][0], rm = A.rq[j][1], re = A.rq[j][2];
+          f = fix_dirty(w, f, sw0, word, rc, rm, re, (rc | rm | re) == 0);
+        }
+        const uint64_t m = ballot(wv && f != 0) & vw;
+        if (m == 0) continue;
+        found |= 1ull << j;
+        if (lane == 0) {
+          A.rk[h][j] = static_cast<uint32_t>(k);
+          A.rm[h][j] = m;
+          atomicMin(&A.best[j], static_cast<uint32_t>(k));
+        }
+        const uint64_t fw = readlane64(f, __builtin_ctzll(m));
+        if (lane == 0) A.rf[h][j] = fw;
+      }
+    }
+  }
+}
+
+// A helper wave of a cooperative block: scans its share of every request the
+// chain wave posts until the chain posts the exit (the same number of block
+// barriers on every wave).
+__device__ __forceinline__ void coop_helper(const DevWorkload& w, CoopArea& A, int h) {
+  for (;;) {
+    __syncthreads();
+    if (__hip_atomic_load(&A.cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) break;
+    if (w.s_head_only) coop_scan<true>(w, A, h);
+    else coop_scan<false>(w, A, h);
+    __syncthreads();
+  }
+}
+
+// Sum over the 64 lanes (DPP, as wave_min).
+__device__ __forceinline__ int wave_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
 // WIDE: the F heads of 64 pods per memory round trip also for G > 1 (more
 // registers: for launches whose waves fit the SIMDs at the lower occupancy)
 // XT: the candidate has extension records at pod_ext[ebase ..] (init-container
 // accounting, shared scalar / volume-limit slots: place_window_x).
 // erow0_in / erow1_in: the slots' node_scal rows from the work-list entry's
 // list_ext (k2_node), or -2: read them from the candidate's first record.
-template <int G, bool PROF, bool WIDE = false, bool XT = false>
+// COOP: the candidate's block cooperates on far resolutions (CoopArea A:
+// this wave is the chain, the block's other waves scan with it).
+template <int G, bool PROF, bool WIDE = false, bool XT = false, bool COOP = false>
 __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __restrict__ F, const int p0,
                                               const int np, int& status, K2Stats& st, uint32_t& nbytes,
                                               const int ebase = -1, const int erow0_in = -2,
-                                              const int erow1_in = -2) {
+                                              const int erow1_in = -2, CoopArea* A = nullptr) {
   static_assert(64 * G * kNHS * 8 <= sizeof(K2Lds), "node-order LDS exceeds the wave's K2 region");
   const int lane = threadIdx.x & 63;
   const int Wp = w.Wp;
@@ -1412,10 +1545,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       nbytes += 64u * 16u;
     }
   };
-#ifndef SR_K2_PREFETCH_W0
-#define SR_K2_PREFETCH_W0 1
-#endif
-  if (SR_K2_PREFETCH_W0 && dead > 0) {
+  if (dead > 0) {
     const uint64_t* nr = w.node_rec + static_cast<size_t>(lane) * 8;
     ncpu = static_cast<int64_t>(nr[0]);
     nmem = static_cast<int64_t>(nr[1]);
@@ -1686,13 +1816,82 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
           }
         }
       };
+      // Cooperative block: per pod group one request, every wave of the
+      // block scans its share of the chunks (coop_scan), the chain takes per
+      // pod the lowest chunk found
+      auto coop_resolve = [&]() {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const uint64_t pend = ballot(((act[g] >> lane) & 1) && ptr[g] == n && unres[g]);
+          if (pend == 0) continue;  // wave-uniform
+          const bool mine = (pend >> lane) & 1;
+          const int slot = __builtin_popcountll(pend & ((1ull << lane) - 1));
+          int nops = 0;
+          if (mine) {
+            A->r01[slot] = r01[g];
+            A->r23[slot] = r23[g];
+            A->rq[slot][0] = rc[g];
+            A->rq[slot][1] = rm[g];
+            A->rq[slot][2] = re[g];
+            if (w.s_head_only)
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int o = PG[(64 * g + lane) * 8 + u];
+                A->op[slot][u] = o;
+                nops += o >= 0 ? 1 : 0;
+              }
+            A->best[slot] = 0xffffffffu;
+          }
+          if (lane == 0) {
+            A->cmd = 0;
+            A->n = __builtin_popcountll(pend);
+            A->sw = sw;
+          }
+          __syncthreads();  // the request is posted: every wave scans its share
+          if (w.s_head_only) coop_scan<true>(w, *A, 0);
+          else coop_scan<false>(w, *A, 0);
+          __syncthreads();  // every share scanned
+          if (PROF) st.cyc_res += static_cast<uint64_t>((Wp - ((sw >> 6) << 6) + 64 * kCoopWaves - 1) /
+                                                        (64 * kCoopWaves)) << 40;
+          uint32_t bytes = 0;
+          if (mine) {
+            uint32_t kb = 0xffffffffu;
+            int hb = 0;
+#pragma unroll
+            for (int h = 0; h < kCoopWaves; ++h) {
+              const uint32_t k = A->rk[h][slot];
+              hb = k < kb ? h : hb;
+              kb = k < kb ? k : kb;
+            }
+            int nx = INT_MAX, words = Wp - sw;
+            if (kb != 0xffffffffu) {
+              const uint64_t m = A->rm[hb][slot], fw = A->rf[hb][slot];
+              const int cb = ((sw >> 6) << 6) + 64 * static_cast<int>(kb);
+              const int w2 = __builtin_ctzll(m);
+              nx = (cb + w2) * 64 + __builtin_ctzll(fw);
+              fmask[g] = m;
+              fbase[g] = cb;
+              cur[g] = fw;
+              words = cb + w2 + 1 - sw;  // the words a sequential scan reads, up to the first non-zero one
+            } else {
+              fmask[g] = 0;
+              cur[g] = 0;
+            }
+            ptr[g] = nx;
+            unres[g] = false;
+            bytes = static_cast<uint32_t>(words) * (w.s_head_only ? 8u * (static_cast<uint32_t>(nops) + 3u) : 32u);
+          }
+          nbytes += static_cast<uint32_t>(wave_sum(static_cast<int>(bytes)));
+          const uint64_t gone = ballot(mine && ptr[g] == INT_MAX);
+          if (gone != 0) dead = min(dead, 64 * g + __builtin_ctzll(gone));
+          if (PROF) st.cyc_res += static_cast<uint64_t>(__builtin_popcountll(gone)) << 56;
+        }
+      };
       // pods per round (A/B: 8 or 16 pods per round made the realistic
       // variant's resolution slower, 21-28k cycles against 17.5k)
-#ifndef SR_K2_RES_Q
-#define SR_K2_RES_Q 4
-#endif
-      constexpr int kResQ = SR_K2_RES_Q;
-      if (w.s_head_only) resolve(std::integral_constant<int, 2>{}, std::true_type{});
+      constexpr int kResQ = 4;
+      if constexpr (COOP) coop_resolve();
+      else if (w.s_head_only) resolve(std::integral_constant<int, 2>{}, std::true_type{});
       else resolve(std::integral_constant<int, kResQ>{}, std::false_type{});
       if (PROF) st.cyc_res += __builtin_amdgcn_s_memtime() - cyc_r0;
       any = 0;
@@ -2366,13 +2565,9 @@ __device__ __forceinline__ void k2_finish(const DevWorkload& w, const K2Entry& x
   }
 }
 
-// SR_K2_KARG=0 (A/B): the K2 kernels read the by-value argument instead
-#ifndef SR_K2_KARG
-#define SR_K2_KARG 1
-#endif
 template <int CH, bool PROF>
 __global__ __launch_bounds__(256) void k2_place(DevWorkload w_arg, const int4* __restrict__ list, int n_list) {
-  const DevWorkload& w = SR_K2_KARG ? *(const DevWorkload*)__builtin_amdgcn_kernarg_segment_ptr() : w_arg;
+  const DevWorkload& w = *(const DevWorkload*)__builtin_amdgcn_kernarg_segment_ptr();
   (void)w_arg;  // as in k2_node
   extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
   const int lane = threadIdx.x & 63;
@@ -2434,16 +2629,46 @@ __global__ __launch_bounds__(256) void k2_node(DevWorkload w_arg, const int4* __
   // the workload read in place from the kernel-argument segment (w_arg is its
   // first argument): each field is a scalar load where it is used, instead of
   // values held (or spilled to scratch) across the kernel
-  const DevWorkload& w = SR_K2_KARG ? *(const DevWorkload*)__builtin_amdgcn_kernarg_segment_ptr() : w_arg;
+  const DevWorkload& w = *(const DevWorkload*)__builtin_amdgcn_kernarg_segment_ptr();
   (void)w_arg;
   extern __shared__ __attribute__((aligned(16))) uint64_t k2_lds[];
   const int wave = threadIdx.x >> 6;
-  const int li = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * (blockDim.x >> 6)) + wave);
+  const size_t region = 64 * GMAX * kNHS + (w.s_head_only ? 64 * GMAX * 4 : 0);  // LDS words per wave
+  // the first n_coop blocks: one candidate each (the list's costliest), wave 0
+  // its chain, the other waves scanning with it (launches of kCoopWaves waves
+  // per block without extension records)
+  const int nco = XT ? 0 : w.n_coop;
+  if constexpr (!XT) {
+    static_assert(sizeof(CoopArea) <= (kCoopWaves - 1) * 64 * kNHS * 8, "the cooperative area fits the helpers' LDS");
+    if (static_cast<int>(blockIdx.x) < nco) {
+      CoopArea* A = reinterpret_cast<CoopArea*>(k2_lds + region);
+      if (wave != 0) {
+        coop_helper(w, *A, wave);
+        return;
+      }
+      const K2Entry x = k2_entry<PROF>(w, list, static_cast<int>(blockIdx.x));
+      K2Stats st;
+      int status = -1;
+      uint32_t nbytes = 0;
+      if (GMAX == 1 || x.np <= 64)
+        k2_node_order<1, PROF, false, false, true>(w, k2_lds, x.p0, x.np, status, st, nbytes, -1, -2, -2, A);
+      else if (GMAX == 2 || x.np <= 128)
+        k2_node_order<(GMAX >= 2 ? 2 : 1), PROF, WIDE, false, true>(w, k2_lds, x.p0, x.np, status, st, nbytes, -1,
+                                                                    -2, -2, A);
+      else k2_node_order<GMAX, PROF, WIDE, false, true>(w, k2_lds, x.p0, x.np, status, st, nbytes, -1, -2, -2, A);
+      if (threadIdx.x == 0) A->cmd = 1;  // the helpers leave
+      __syncthreads();
+      st.narrow |= 2;  // (profile: a cooperative block)
+      k2_finish<PROF>(w, x, status, 2, nbytes, st);
+      return;
+    }
+  }
+  const int li = __builtin_amdgcn_readfirstlane(nco + static_cast<int>((blockIdx.x - nco) * (blockDim.x >> 6)) + wave);
   if (li >= n_list) return;
   int4 xe = {-1, -1, -1, 0};
   if (XT) xe = w.list_ext[li];  // issued with the entry: one round trip for both
   const K2Entry x = k2_entry<PROF>(w, list, li);
-  uint64_t* F = k2_lds + static_cast<size_t>(wave) * (64 * GMAX * kNHS + (w.s_head_only ? 64 * GMAX * 4 : 0));
+  uint64_t* F = k2_lds + static_cast<size_t>(wave) * region;
   K2Stats st;
   int status = -1;
   uint32_t nbytes = 0;
@@ -2497,9 +2722,6 @@ void launch(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, hipEvent
 // wide F-head rounds where the extra registers cost nothing: launches of at
 // most two waves per SIMD (256 CUs x 4 SIMDs), and G = 4 (one wave per SIMD
 // either way)
-#ifndef SR_K2_WIDE_HEADS
-#define SR_K2_WIDE_HEADS 1
-#endif
 template <bool PROF>
 hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 template <bool PROF>
@@ -2512,15 +2734,16 @@ template <bool PROF>
 hipError_t launch_k2_node_g(const DevWorkload& w, int G, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = w.n_list;
   const int wpb = k2_waves_per_block(w);  // waves per block
-  const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
+  // cooperative blocks first (one candidate each), then wpb candidates per block
+  if (w.n_coop < 0 || w.n_coop > n || (w.n_coop > 0 && (wpb != kCoopWaves || w.ext_cand))) return hipErrorInvalidValue;
+  const dim3 grid(w.n_coop + (n - w.n_coop + wpb - 1) / wpb), block(64 * wpb);
   const size_t lds = wpb * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
-  const bool wide = SR_K2_WIDE_HEADS && n <= 2048;
+  const bool wide = n <= 2048;
   if (w.ext_cand) return launch_k2_node_xt_g<PROF>(w, G, s, ev0, ev1);  // some candidate has extension records
   if (G == 1) launch(k2_node<1, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   else if (G == 2 && wide) launch(k2_node<2, PROF, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   else if (G == 2) launch(k2_node<2, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-  else if (SR_K2_WIDE_HEADS) launch(k2_node<4, PROF, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-  else launch(k2_node<4, PROF>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else launch(k2_node<4, PROF, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   return hipGetLastError();
 }
 template hipError_t launch_k2_node_g<false>(const DevWorkload&, int, hipStream_t, hipEvent_t, hipEvent_t);
@@ -2535,12 +2758,11 @@ hipError_t launch_k2_node_xt_g(const DevWorkload& w, int G, hipStream_t s, hipEv
   const int wpb = k2_waves_per_block(w);
   const dim3 grid((n + wpb - 1) / wpb), block(64 * wpb);
   const size_t lds = wpb * static_cast<size_t>(64 * G * kNHS + (w.s_head_only ? 64 * G * 4 : 0)) * 8;
-  const bool wide = SR_K2_WIDE_HEADS && n <= 2048;  // as launch_k2_node_g
+  const bool wide = n <= 2048;  // as launch_k2_node_g
   if (G == 1) launch(k2_node<1, PROF, false, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   else if (G == 2 && wide) launch(k2_node<2, PROF, true, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   else if (G == 2) launch(k2_node<2, PROF, false, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-  else if (SR_K2_WIDE_HEADS) launch(k2_node<4, PROF, true, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
-  else launch(k2_node<4, PROF, false, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
+  else launch(k2_node<4, PROF, true, true>, grid, block, lds, s, ev0, ev1, w, w.list, n);
   return hipGetLastError();
 }
 template hipError_t launch_k2_node_xt_g<false>(const DevWorkload&, int, hipStream_t, hipEvent_t, hipEvent_t);

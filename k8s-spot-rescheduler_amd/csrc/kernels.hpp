@@ -23,10 +23,7 @@ constexpr int kPodPatchU64 = 3;         // pod patch: {active pod, pod_rec[4], p
 constexpr int64_t kTPad = INT64_MAX - 1;  // threshold of a spare T row (no pod points at it; K0 skips it)
 constexpr int kDevDynTerms = 4;         // terms per domain-path affinity set (host.hpp kDynTerms)
 constexpr int kDevExtU64 = 8;           // extension record words (host.hpp kExtU64)
-#ifndef SR_LIST_INLINE
-#define SR_LIST_INLINE 128
-#endif
-constexpr int kListInline = SR_LIST_INLINE;  // work-list entries also carried in the kernel arguments
+constexpr int kListInline = 128;  // work-list entries also carried in the kernel arguments
 
 // Pointers into the device arena (layout: DESIGN.md §HBM layout).
 struct DevWorkload {
@@ -118,6 +115,8 @@ struct DevWorkload {
   int32_t k2_narrow;   // node order: 32-bit scaled window visits where every request allows (SR_K2_NARROW=0: never)
   int32_t k2_wpb;      // K2 waves per block (SR_K2_WPB: 1, 2 or 4; 0 = 1 up to 2,048 entries, else 4)
   int32_t k2_excl;     // node order: exclusive candidates placed with the taken-mask step (SR_K2_EXCL=0: never)
+  int32_t n_coop;      // node-order kernel, four waves per block: the first n_coop work-list entries (the costliest)
+                       // are planned by one block each, its other waves scanning far resolutions with the chain
   int32_t k2_mode;     // 0: node-order first fit where it applies (<= 64 pods, <= 64-word rows);
                        // 1: pod order everywhere (SR_K2_MODE=1, A/B measurement)
   uint64_t* prof;      // optional [n_cand][16] K2 + [kK0ProfWaves][2] K0 per-wave profile
@@ -126,7 +125,7 @@ struct DevWorkload {
   // chains set K2's time): a wave li < n_list_head reads its entry with the
   // other kernel arguments instead of one memory round trip later
   int32_t n_list_head;
-  int4 list_head[kListInline > 0 ? kListInline : 1];
+  int4 list_head[kListInline];
 };
 
 // K0: S and T rows (also resets d_min: d_min[1] = local first fallback).

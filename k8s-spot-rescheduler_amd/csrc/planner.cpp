@@ -155,6 +155,10 @@ struct sr_ctx {
   int32_t list_cost = 1;
   int32_t list_cost_min = 2048;  // SR_LIST_COST_MIN: only lists longer than this (C4 15,000 entries: K2 69 -> 45 us;
                                  // C3's 1,500 waves are all resident at once: within noise, or +0.5 us)
+  // SR_K2_COOP: a cost-ordered list's costliest entries planned by cooperative
+  // blocks on the node-order kernel (four waves per block: the chain and
+  // three waves scanning far resolutions with it); 0: none
+  int32_t k2_coop = 64;
   DevBuf out_cycles;
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -689,7 +693,7 @@ sr_status prepare(sr_ctx* ctx, const sr_snapshot* snap, const sr_cluster* c, con
   bool list_moved = false;
   if (ctx->list_cost && w.reused && sl.cost_gen == w.cand_gen && sl.list_sorted_gen != w.cand_gen) {
     HIP_TRY(ctx, hipEventSynchronize(sl.ev_cost));
-    sr::reorder_list_by_cost(w, static_cast<const uint32_t*>(sl.h_cycles.p), ctx->enc.list_head);
+    sr::reorder_list_by_cost(w, static_cast<const uint32_t*>(sl.h_cycles.p), ctx->enc.list_head, ctx->k2_coop);
     list_moved = true;
   }
   if (ctx->ev_upload) HIP_TRY(ctx, hipEventSynchronize(ctx->ev_upload));  // staging buffer free again
@@ -1168,6 +1172,18 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   const bool split = ctx->k2_split && n_node > 0 && n_node < d.n_list && d.k2_mode == 0 && d.k2_node_kernel &&
                      w.max_np_node >= 1 && w.max_np_node <= 256;
   ctx->t.k2_launches = d.n_list > 0 ? (split ? 2 : 1) : 0;
+  // cooperative blocks for the front of a cost-ordered list, on a node-order
+  // launch of four waves per block without extension records
+  d.n_coop = 0;
+  {
+    const bool node_launch = split || (!d.dyn_cand && d.k2_mode == 0 && d.max_np >= 1 && d.max_np <= 256 &&
+                                       d.k2_node_kernel);
+    const int32_t len = split ? n_node : d.n_list;
+    const int32_t wpb = d.k2_wpb == 1 || d.k2_wpb == 2 || d.k2_wpb == 4 ? d.k2_wpb : (len <= 2048 ? 1 : 4);
+    if (node_launch && wpb == 4 && !d.ext_cand && ctx->cur->list_sorted_gen == w.cand_gen)
+      d.n_coop = std::min(w.n_coop_front, len);
+  }
+  ctx->t.k2_coop = d.n_coop;
   if (split) {
     if (!ctx->stream2) {
       HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
@@ -1178,6 +1194,7 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     dp.list = d.list + n_node;
     dp.n_list = d.n_list - n_node;
     dp.n_list_head = 0;
+    dp.n_coop = 0;  // (the general kernel)
     if (d.list_ext) dp.list_ext = d.list_ext + n_node;
     dn.n_list = n_node;
     dn.n_list_head = std::min(d.n_list_head, n_node);
@@ -1362,6 +1379,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_LIST_COST_MIN")) ctx->list_cost_min = std::max(0, std::atoi(m));
   if (const char* m = std::getenv("SR_K2_SPLIT_MIN")) ctx->enc.split_min = std::max(0, std::atoi(m));
   if (const char* m = std::getenv("SR_LIST_HEAD")) ctx->enc.list_head = std::max(0, std::atoi(m));
+  if (const char* m = std::getenv("SR_K2_COOP")) ctx->k2_coop = std::max(0, std::atoi(m));
   *out = ctx;
   return SR_OK;
 }

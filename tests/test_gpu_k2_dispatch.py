@@ -68,6 +68,7 @@ def _ticks(ck, sc, n_ticks, rng, expect_split, per_tick_extra=(1, 4)):
     nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
     cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
     extra, by_cost, reused, splits = [], 0, 0, 0
+    _ticks.coop = 0  # runs with cooperative blocks
     for tick in range(n_ticks):
         if tick % 6 == 5:
             extra.clear()
@@ -94,6 +95,7 @@ def _ticks(ck, sc, n_ticks, rng, expect_split, per_tick_extra=(1, 4)):
         for tt in (tq, t):
             assert tt.k2_launches == (2 if expect_split else 1), (tick, tt.k2_launches)
             splits += tt.k2_launches == 2
+            _ticks.coop += tt.k2_coop > 0
         if tick >= 2:
             reused += t.enc_reused
             by_cost += tq.k2_list_by_cost + t.k2_list_by_cost
@@ -196,5 +198,63 @@ def test_timed_runs_across_k0_and_k0_less_ticks():
             assert lib.sr_get_timing(ck.handle, ctypes.byref(t)) == capi.SR_OK, ck.last_error()
             assert t.n_runs == runs and t.ms_placement > 0
         assert k0_less >= 2 and k0_runs >= 2, (k0_less, k0_runs)
+    finally:
+        ck.close()
+
+
+# Every planner switch that is not the default, against the oracle: consecutive
+# ticks of a host-port cluster (exclusive-port candidates, K0-less and
+# incremental-K0 ticks, candidate-side reuse) and random scenarios on a pool
+# wider than 64 words (rows over several chunks, head-only S rows).
+SWITCHES = {
+    "node_kernel_off": dict(SR_K2_NODE_KERNEL=0),   # every launch on the general kernel
+    "excl_off": dict(SR_K2_EXCL=0),                 # exclusive candidates on the regular window step
+    "one_slot": dict(SR_PLAN_SLOTS=1),              # one workload slot: every other input re-encodes
+    "k0_inc_off": dict(SR_K0_INCREMENTAL=0),        # K0 rewrites every row whenever it runs
+    "k0_skip_off": dict(SR_K0_SKIP=0),              # every run launches K0
+    "wpb1": dict(SR_K2_WPB=1), "wpb2": dict(SR_K2_WPB=2), "wpb4": dict(SR_K2_WPB=4),
+    "list_cost_off": dict(SR_LIST_COST=0, SR_LIST_COST_MIN=0),
+    "prefix_batch_3": dict(SR_PREFIX_BATCH=3),
+}
+
+
+@pytest.mark.parametrize("which", sorted(SWITCHES))
+def test_planner_switches_match_oracle(which):
+    from randcluster import rand_scenario
+    from test_gpu_parity import run_scenario, test_gpu_exclusive_port_candidates
+    ck = make_checker(**SWITCHES[which])
+    try:
+        sc = SynthCluster(5, seed=51, n_on_demand=150, n_spot=400)
+        _ticks(ck, sc, 6, np.random.default_rng(51), expect_split=False)
+        for seed in range(2):
+            nodes, spot_pods, cands = rand_scenario(7500 + seed, n_spot=4200 + 700 * seed, n_cand=8, max_pods=20,
+                                                    anti=0.2, hostname_only=True)
+            run_scenario(ck, nodes, spot_pods, cands)
+        for seed in range(2):
+            test_gpu_exclusive_port_candidates(ck, seed)
+    finally:
+        ck.close()
+
+
+@pytest.mark.parametrize("case", ["c3", "c4_wide_head_only", "affinity_split"])
+def test_cooperative_blocks(case):
+    """Cooperative blocks (SR_K2_COOP): the costliest entries of a cost-ordered
+    list, on a node-order launch of four waves per block, are planned by one
+    block each whose other waves scan far resolutions with the chain wave; the
+    plan is the oracle's.  C3-shaped rows (10 words: resolutions beyond the
+    512-node head), a 6,000-node pool (94-word rows, head-only S rows: the
+    scans evaluate the class programs), and the affinity variant's split launch
+    (its node-order part cooperative)."""
+    env = dict(SR_LIST_COST_MIN=0, SR_K2_WPB=4, SR_K2_COOP=32)
+    if case == "affinity_split":
+        env["SR_K2_SPLIT_MIN"] = 64
+    ck = make_checker(**env)
+    try:
+        sc = {"c3": lambda: SynthCluster(3, seed=45, n_on_demand=300, n_spot=600),
+              "c4_wide_head_only": lambda: SynthCluster(4, seed=5, n_on_demand=400, n_spot=6000),
+              "affinity_split": lambda: SynthCluster(3, seed=41, n_on_demand=300, n_spot=600, **AFFINITY)}[case]()
+        reused, by_cost, _ = _ticks(ck, sc, 8, np.random.default_rng(45), expect_split=case == "affinity_split")
+        assert reused >= 4 and by_cost >= 8, (reused, by_cost)
+        assert _ticks.coop >= 8, _ticks.coop
     finally:
         ck.close()
