@@ -112,8 +112,9 @@ def k2_chain_summary(path):
         return None
     out = {"source": os.path.relpath(path, REPO)}
     lines = open(path).read().splitlines()
-    for i, line in enumerate(lines):
-        if line.startswith("latest-ending waves") and i + 1 < len(lines):
+    for i, line in enumerate(lines):  # the longest wave (older profiles: the latest-ending one)
+        if (line.startswith("longest waves") or (line.startswith("latest-ending waves") and "longest_wave" not in out)) \
+                and i + 1 < len(lines):
             out["longest_wave"] = {"columns": line.split(":", 1)[1].strip(), "values": lines[i + 1].strip()}
     for line in lines:
         if line.startswith("node order: cycles/visit"):
@@ -128,6 +129,44 @@ def k2_chain_summary(path):
         elif line.startswith("wave dur us"):
             out["wave_us_p50_p90_p99_max"] = [float(x) for x in line.split(":")[1].split()]
     return out
+
+
+# The chain's latency floor (roofline.latency): one dependent global load
+# (tools/micro/dep_load.hip on one MI355X: 526 cycles for a first touch in a
+# new kernel, 226 for an L2 hit) and one window step alone on a SIMD
+# (tools/micro/place_chain.hip V13: 214 cycles per placed pod).
+DEP_LOAD_CYCLES = 526
+STEP_CYCLES = 214
+
+
+def chain_latency(chain):
+    """The longest wave of the committed K2 profile against its dependent-
+    latency floor: every dependent memory round trip it cannot avoid (the
+    work-list entry, its pod records with window 0, the F heads, each further
+    window, each far-resolution chunk round) at DEP_LOAD_CYCLES, plus one
+    STEP_CYCLES step per placed pod, over the cycles the wave took."""
+    if not chain or "longest_wave" not in chain:
+        return None
+    parts = [p.split() for p in chain["longest_wave"]["values"].replace("(", " ").replace(")", " ")
+             .replace(",", " ").split("|")]
+    try:
+        visits, placed, windows = (int(x) for x in parts[1][:3])
+        cyc = [int(x) for x in parts[2][:5]]
+        rounds = int(parts[4][1]) if len(parts) > 4 and len(parts[4]) > 1 else 0
+    except (IndexError, ValueError):
+        return None
+    trips = 3 + max(0, windows - 1) + rounds
+    floor = trips * DEP_LOAD_CYCLES + placed * STEP_CYCLES
+    measured = sum(cyc)
+    return {"bound": "latency", "floor_cycles": floor, "measured_cycles": measured,
+            "frac": round(floor / measured, 4) if measured else None,
+            "longest_wave": {"dependent_round_trips": trips, "placements": placed, "visits": visits,
+                             "windows": windows, "chunk_rounds": rounds,
+                             "cycles_entry_records_prologue_minwindow_placement_moves": cyc},
+            "model": "floor = dependent round trips x %d cycles (tools/micro/dep_load.hip: a dependent load's first "
+                     "touch in a new kernel) + placed pods x %d cycles (tools/micro/place_chain.hip V13: one window "
+                     "step alone on a SIMD); measured = the longest K2 wave's cycles in the committed profile "
+                     "(%s)" % (DEP_LOAD_CYCLES, STEP_CYCLES, chain.get("source"))}
 
 
 def cpu_share():
@@ -165,10 +204,13 @@ def plan_parity(o, gpu_status, gpu_nodes, cand_off):
 
 def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, gpu_checks, seconds, mutation=None):
     """The oracle (C restatement of the reference planner) on this host, rank 0
-    only; BASELINE.md's three modes, each a median after 2 untimed warm-ups:
-    all candidates on 1 thread (bounded by `seconds`, >= 3 runs), the
+    only; BASELINE.md's three modes: all candidates on 1 thread (`value`), the
     reference-faithful early exit on 1 thread (>= 10 runs), all candidates on
-    the host's CPU share (>= 10 runs)."""
+    the host's CPU share.  The whole tick on the CPU share runs first: its plan
+    is the one compared with the GPU's.  Where the 1-thread whole tick would
+    overrun `seconds` (C4, the affinity variant at C4), the 1-thread figure is
+    a bounded sample: the first k candidates of the same tick, k x4 from 64
+    until one run takes seconds / 5; `sample` says which."""
     from oracle_lib import OracleSnapshot, oracle_plan
     snap = OracleSnapshot(sc.ptr, nm.spot, nm.node_pod_off, nm.node_pod_idx)
     if mutation is not None:  # the steady-state tick's snapshot: one more pod on one spot node
@@ -185,29 +227,60 @@ def cpu_baseline(sc, nm, cand_off, cand_pods, n_spot, gpu_status, gpu_nodes, gpu
             ts.append(time.perf_counter() - t0)
         return 1e3 * float(np.median(ts)), len(ts), sum(ts), r
 
-    ms_all, n_all, s_all, res = timed(1, 1, 3, seconds)
-    ms_early, n_early, _, early = timed(0, 1, 10, min(2.0, seconds / 4))
     threads = cpu_share()
-    ms_mt, n_mt, _, _ = timed(1, threads, 10, min(3.0, seconds / 3))
-    dense = float(len(cand_pods)) * n_spot
+    n_cand = len(cand_off) - 1
+    t0 = time.perf_counter()
+    res = oracle_plan(snap, sc.ptr, cand_off, cand_pods, mode=1, threads=threads)  # the plan compared
+    t_mt = time.perf_counter() - t0
+    full_1core = t_mt * threads <= seconds
+    if full_1core:
+        ms_all, n_all, s_all, r1 = timed(1, 1, 3, seconds)
+        checks_1 = float(r1["checks"])
+        sample = ("full tick: all %d candidates / %d pods x %d spot nodes, median of %d runs (%.1f s) after 2 "
+                  "warm-ups" % (n_cand, len(cand_pods), n_spot, n_all, s_all))
+        dense_1 = float(len(cand_pods)) * n_spot
+    else:
+        k = 64
+        while True:
+            k = min(k, n_cand)
+            off_k = np.ascontiguousarray(cand_off[:k + 1])
+            pods_k = np.ascontiguousarray(cand_pods[:int(off_k[-1])])
+            t0 = time.perf_counter()
+            rk = oracle_plan(snap, sc.ptr, off_k, pods_k, mode=1, threads=1)
+            dt = time.perf_counter() - t0
+            if dt >= seconds / 5 or k == n_cand:
+                break
+            k *= 4
+        ms_all, n_all, checks_1 = 1e3 * dt, 1, float(rk["checks"])
+        sample = ("bounded sample: the first %d of the tick's %d candidates (%d pods x %d spot nodes), one 1-thread "
+                  "run of %.1f s; the whole tick on %d threads took %.1f s" % (k, n_cand, len(pods_k), n_spot, dt,
+                                                                                threads, t_mt))
+        dense_1 = float(len(pods_k)) * n_spot
+    ms_early, n_early, _, early = timed(0, 1, 10, min(2.0, seconds / 4))
+    if t_mt > 1.0:  # a long whole tick: its one run is the CPU-share figure
+        ms_mt, n_mt = 1e3 * t_mt, 1
+    else:
+        ms_mt, n_mt, _, _ = timed(1, threads, 10, min(3.0, seconds / 3))
     parity, n_fb, n_fb_pods = plan_parity(res, gpu_status, gpu_nodes, cand_off)
-    return {"value": float(res["checks"]) / (ms_all / 1e3), "unit": "checks/s", "cores": 1, "kind": "port",
+    return {"value": checks_1 / (ms_all / 1e3), "unit": "checks/s", "cores": 1, "kind": "port",
             "host_cpus": os.cpu_count(), "host_cpus_affinity": len(os.sched_getaffinity(0)),
             "host_cpu_share_threads": threads,
-            "value_definition": "reference-equivalent checks (issued CheckPredicates calls) / 1-core all-candidates tick",
-            "dense_equivalent_per_s": dense / (ms_all / 1e3),
-            "sample": "full tick: all %d candidates / %d pods x %d spot nodes, median of %d runs (%.1f s) after 2 "
-                      "warm-ups" % (len(cand_off) - 1, len(cand_pods), n_spot, n_all, s_all),
-            "ms_per_tick_all_candidates_1core": round(ms_all, 3),
+            "value_definition": "reference-equivalent checks (issued CheckPredicates calls) / 1-core all-candidates "
+                                "time (the whole tick, or the bounded sample named in `sample`)",
+            "dense_equivalent_per_s": dense_1 / (ms_all / 1e3),
+            "sample": sample,
+            "ms_per_tick_all_candidates_1core": round(ms_all, 3) if full_1core else None,
+            "ms_1core_sample": None if full_1core else round(ms_all, 3),
             "ms_per_tick_reference_faithful_1core": round(ms_early, 4),
             "reference_faithful_runs": n_early,
             "reference_faithful_first_ok": int(early["first_ok"]),
             "ms_per_tick_all_candidates_%dthreads" % threads: round(ms_mt, 3),
             "all_candidates_threads_runs": n_mt,
             "threads_note": "all-candidates mode on the job's CPU share: min(sched_getaffinity, OMP_NUM_THREADS or "
-                            "SR_BENCH_CPU_THREADS); each mode is a median after 2 warm-ups",
+                            "SR_BENCH_CPU_THREADS); a median after 2 warm-ups, or one run when it takes over 1 s",
             "issued_checks_per_tick": int(res["checks"]),
             "plans_identical_to_gpu": parity,
+            "plans_compared": "the whole tick (%d candidates), planned by the oracle on %d threads" % (n_cand, threads),
             "reference_equivalent_checks_match_gpu": int(res["checks"]) == int(gpu_checks),
             "parity_rule": "device-evaluated candidates: status + every pod's node equal to the oracle; "
                            "fallback candidates take the reference path",
@@ -814,7 +887,7 @@ def main():
                                         "none": "none (one GPU)"}[transport]},
             "per_rank": per_rank,
             "weak_scaling": weak_scaling,
-            "scaling_model": {"prediction_us": predict(args.config, world),
+            "scaling_model": {"prediction_us": predict(args.config, world, transport),
                               "model": "spotplanner/scaling.py: measured 1-GPU parts, ASSUMED RCCL allreduce "
                                        "latency (the shm transport has none); per_rank holds the measured parts"}
             if world > 1 else None,
@@ -844,7 +917,8 @@ def main():
                                              "SURVEY 8(d) K2 formula over what is actually read)",
                          "limiter": "latency: one dependent placement chain per candidate (one wave each); the "
                                     "longest chain sets the kernel time, not bytes (DESIGN.md 4)",
-                         "chain": chain},
+                         "chain": chain,
+                         "latency": chain_latency(chain)},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(sc, nm, cand_off, cand_pods, int(len(nm.spot)), status[:len(loff) - 1],

@@ -2,12 +2,13 @@
 
 The reference plans a tick's candidates one after another (rescheduler.go:
 228-287); the planner shards them c % N over N GPUs, each holding the whole
-spot snapshot, and reduces the tick's outcome with one allreduce(min) of
-three u64 words followed by K3 (the reduced header and the winner's mapping to
-host memory).  A rank's device tick is K2 over its shard plus, for N > 1, the
-collective and K3:
+spot snapshot, and reduces the tick's outcome either through one shared-memory
+segment every rank's K2 writes its outcomes to (transport "shm", bench.py's
+default on one node: no collective, no K3) or with one RCCL allreduce(min) of
+three u64 words followed by K3 (transport "rccl").  A rank's device tick is K2
+over its shard plus, for N > 1 over RCCL, the collective and K3:
 
-    tick(N) = max(chain, K2_1 * share(N)) + gap + [N > 1] (allreduce(N) + K3)
+    tick(N) = max(chain, K2_1 * share(N)) + gap + [N > 1, rccl] (allreduce(N) + K3)
 
   chain   the longest candidate's dependent placement chain (one wave: no
           number of GPUs shortens it);
@@ -22,7 +23,10 @@ Sharding a fixed tick pays only when tick_strong(N) < tick(1): K2 must be
 throughput-bound well above its chain.  None of C1-C5 is any more: C4's
 K2 (15,000 candidates) is 46 us against a 43 us longest wave since its work
 list runs longest wave first, and C3 (1,500 candidates) is a 12.9 us chain in
-a 14.5 us K2, so a strong-scaled tick on 2-8 GPUs is slower than on one.  `choose_scaling` makes that call per config for bench.py --scaling auto.
+a 14.5 us K2, so a strong-scaled tick on 2-8 GPUs is no faster than on one
+(over RCCL, slower).  bench.py reports the strong-scaled line (BASELINE's) with
+the weak-scaled tick beside it; `choose_scaling` says which of the two the
+model expects to pay.
 """
 
 # Measured on one MI355X in round 5 (profiles/r05/final/c*_bench.json:
@@ -53,23 +57,25 @@ def allreduce_us(n):
     return ALLREDUCE_US[lo] * (n / lo) ** 0.5
 
 
-def predict_tick_us(parts, n, scaling):
-    """Predicted back-to-back device tick of one rank, us."""
+def predict_tick_us(parts, n, scaling, transport="rccl"):
+    """Predicted back-to-back device tick of one rank, us (transport "shm": the
+    ranks' hosts walk the shared outcome words, no collective and no K3)."""
     share = 1.0 / n if scaling == "strong" else 1.0
     k2 = max(parts["chain"], parts["k2"] * share)
-    return k2 + parts["gap"] + ((allreduce_us(n) + parts["k3"]) if n > 1 else 0.0)
+    return k2 + parts["gap"] + ((allreduce_us(n) + parts["k3"]) if n > 1 and transport == "rccl" else 0.0)
 
 
-def predict(config, n):
+def predict(config, n, transport="rccl"):
     """Per-N prediction for a config: both scalings, the strong tick's speed-up
     over one GPU, and the predicted scaling efficiencies the driver would
     compute from the bench values (weak: N x the work in tick(N); strong: the
     same work in tick(N))."""
     p = PARTS[config]
     t1 = predict_tick_us(p, 1, "strong")
-    ts = predict_tick_us(p, n, "strong")
-    tw = predict_tick_us(p, n, "weak")
-    return {"n": n, "tick1_us": round(t1, 2), "strong_tick_us": round(ts, 2), "weak_tick_us": round(tw, 2),
+    ts = predict_tick_us(p, n, "strong", transport)
+    tw = predict_tick_us(p, n, "weak", transport)
+    return {"n": n, "transport": transport, "tick1_us": round(t1, 2), "strong_tick_us": round(ts, 2),
+            "weak_tick_us": round(tw, 2),
             "strong_efficiency": round(t1 / (n * ts), 3), "weak_efficiency": round(t1 / tw, 3),
             "strong_pays": ts < t1}
 

@@ -101,3 +101,13 @@ def test_per_rank_records_gathered_in_rank_order(world):
         assert [x["rank"] for x in recs] == list(range(world))
         assert [x["candidates"] for x in recs] == [10 + k for k in range(world)]
         assert recs[world - 1]["k2_placement_ms"] == pytest.approx(0.01 * world)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_shared_memory_transport_adds_no_device_exchange(n):
+    # transport "shm" (sr_comm_init_shm): the ranks' hosts walk the outcome words K2 wrote; no allreduce, no K3
+    for c, p in scaling.PARTS.items():
+        assert scaling.predict_tick_us(p, n, "weak", "shm") == pytest.approx(scaling.predict_tick_us(p, 1, "weak"))
+        r = scaling.predict(c, n, "shm")
+        assert r["weak_efficiency"] == pytest.approx(1.0) and r["transport"] == "shm"
+        assert r["strong_tick_us"] <= r["tick1_us"] + 1e-9

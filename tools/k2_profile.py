@@ -108,15 +108,23 @@ def main():
     print("cycles/step by section a,b,c,d,spec-wait:", " ".join("%.0f" % (x / st) for x in tot))
     last = np.argsort(-end)[:8]
     full = runs[last_run].astype(np.int64)
-    print("latest-ending waves: wave start_us dur_us steps mode | visits placements windows | "
-          "cycles: entry->records prologue min+window placement moves | 32-bit | resolve (chunk rounds, dead) window-loads")
-    for c in last:
+    cols = ("wave start_us dur_us steps mode | visits placements windows | "
+            "cycles: entry->records prologue min+window placement moves | 32-bit (+2: cooperative block) | "
+            "resolve (chunk rounds, dead) window-loads")
+
+    def row(c):
         f = full[c]
         nod = mode[c] == 2
         print("  %5d %6.2f %6.2f %4d %2d | %3d %3d %3d | %6d %6d %6d %6d %6d | %d | %6d (%d, %d) %6d"
               % (c, start[c], dur[c], steps[c], mode[c], f[7] & 0xffffffff, f[6], f[7] >> 32, f[14],
-                 f[8], f[9], f[10], f[11], f[15] & 1, (f[12] & ((1 << 40) - 1)) if nod else 0,
+                 f[8], f[9], f[10], f[11], f[15] & 3, (f[12] & ((1 << 40) - 1)) if nod else 0,
                  ((f[12] >> 40) & 0xffff) if nod else 0, (f[12] >> 56) if nod else 0, f[13] if nod else 0))
+    print("latest-ending waves: " + cols)
+    for c in last:
+        row(c)
+    print("longest waves: " + cols)
+    for c in np.argsort(-dur, kind="stable")[:8]:
+        row(int(c))
 
 
 if __name__ == "__main__":
