@@ -258,3 +258,68 @@ def test_cooperative_blocks(case):
         assert _ticks.coop >= 8, _ticks.coop
     finally:
         ck.close()
+
+
+@pytest.mark.parametrize("config", [3, 5])
+def test_consecutive_runs_match_oracle(config):
+    """Consecutive runs of one prepared workload, as the bench's timed region
+    issues them: forty runs per tick -- winner-only runs (each returns once the
+    candidates up to the winner are planned, the rest of the grid finishing
+    behind the next launch), full runs with every output and runs with K2
+    timed interleaved -- each with the oracle's winner and mapping, then the
+    next tick's prepare (one more pod on a spot node: K0-less runs)."""
+    ck = make_checker()
+    try:
+        sc = SynthCluster(config, seed=47, n_on_demand=300, n_spot=600)
+        lib = capi.load_planner()
+        nm = new_node_map(lib.sr_new_node_map, sc.ptr, sc.n_nodes, sc.n_pods, sc.od_label, sc.spot_label)
+        cand_off, cand_pods = build_candidates(nm, sc.pod_flags())
+        n = len(cand_off) - 1
+        c = capi.sr_candidates(n, capi.ptr(cand_off, capi.P32), capi.ptr(cand_pods, capi.P32), None)
+        wmap = np.full(int(np.max(np.diff(cand_off))), -1, np.int32)
+        status = np.zeros(n, np.int32)
+        nodes = np.zeros(int(cand_off[-1]), np.int32)
+        rng = np.random.default_rng(config)
+        extra, k0_less = [], 0
+        for tick in range(6):
+            if tick:
+                extra.append((int(rng.choice(cand_pods)), int(rng.integers(len(nm.spot)))))
+            off, idx = _with_extra(nm, sc.n_nodes, extra)
+            h = ctypes.c_void_p()
+            assert lib.sr_snapshot_create(sc.ptr, capi.ptr(nm.spot, capi.P32), len(nm.spot), capi.ptr(off, capi.P32),
+                                          capi.ptr(idx, capi.P32), ctypes.byref(h)) == capi.SR_OK
+            try:
+                o = oracle_plan(OracleSnapshot(sc.ptr, nm.spot, off, idx), sc.ptr, cand_off, cand_pods, mode=1,
+                                threads=8)
+                want_map = o["node_of_pod"][cand_off[o["first_ok"]]:cand_off[o["first_ok"] + 1]] \
+                    if o["first_ok"] >= 0 else None
+                for _ in range(2 if tick == 0 else 1):
+                    assert lib.sr_plan_prepare(ck.handle, h, sc.ptr, ctypes.byref(c)) == capi.SR_OK, ck.last_error()
+                k0_less += ck.timing().k0_columns == -2
+                for r in range(40):
+                    out = capi.sr_plan_out()
+                    out.winner_map = capi.ptr(wmap, capi.P32)
+                    if r % 13 == 5:  # every output: waits for the other stream first
+                        out.status = capi.ptr(status, capi.P32)
+                        out.node_of_pod = capi.ptr(nodes, capi.P32)
+                    timed = r % 11 == 7
+                    if timed:
+                        ck.set_timing(2)
+                    assert lib.sr_plan_run(ck.handle, ctypes.byref(out)) == capi.SR_OK, ck.last_error()
+                    if timed:
+                        assert ck.timing().n_runs == 1
+                        ck.set_timing(0)
+                    assert (out.first_ok, out.winner) == (o["first_ok"], o["winner"]), (tick, r)
+                    if want_map is not None:
+                        assert np.array_equal(wmap[:out.winner_npods], want_map), (tick, r)
+                    if r % 13 == 5:  # candidates outside the encoded set (C5: > 64 state bits) take the reference path
+                        fb = status == capi.SR_CAND_FALLBACK
+                        assert np.all(fb | (status == o["status"])), (tick, r)
+                        for k in np.flatnonzero(~fb):
+                            seg = slice(int(cand_off[k]), int(cand_off[k + 1]))
+                            assert np.array_equal(nodes[seg], o["node_of_pod"][seg]), (tick, r, k)
+            finally:
+                lib.sr_snapshot_destroy(h)
+        assert k0_less >= 3, k0_less
+    finally:
+        ck.close()
