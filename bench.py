@@ -112,10 +112,13 @@ def k2_chain_summary(path):
         return None
     out = {"source": os.path.relpath(path, REPO)}
     lines = open(path).read().splitlines()
-    for i, line in enumerate(lines):  # the longest wave (older profiles: the latest-ending one)
-        if (line.startswith("longest waves") or (line.startswith("latest-ending waves") and "longest_wave" not in out)) \
-                and i + 1 < len(lines):
-            out["longest_wave"] = {"columns": line.split(":", 1)[1].strip(), "values": lines[i + 1].strip()}
+    for i, line in enumerate(lines):  # the longest node-order wave (older profiles: the latest-ending one)
+        if line.startswith("longest waves") or (line.startswith("latest-ending waves") and "longest_wave" not in out):
+            for row in lines[i + 1:i + 9]:
+                f = row.split("|")[0].split()
+                if len(f) == 5 and f[4] == "2":  # mode 2: node order (the chain model's kernel path)
+                    out["longest_wave"] = {"columns": line.split(":", 1)[1].strip(), "values": row.strip()}
+                    break
     for line in lines:
         if line.startswith("node order: cycles/visit"):
             nums = [float(x.strip(",")) for x in line.split() if x.strip(",").replace(".", "").isdigit()]
@@ -128,6 +131,8 @@ def k2_chain_summary(path):
             out["visits_line"] = line.strip()
         elif line.startswith("wave dur us"):
             out["wave_us_p50_p90_p99_max"] = [float(x) for x in line.split(":")[1].split()]
+        elif line.startswith("clock MHz"):
+            out["clock_mhz"] = float(line.split(":")[1].split()[0])
     return out
 
 
@@ -150,6 +155,7 @@ def chain_latency(chain):
     parts = [p.split() for p in chain["longest_wave"]["values"].replace("(", " ").replace(")", " ")
              .replace(",", " ").split("|")]
     try:
+        dur_us = float(parts[0][2])
         visits, placed, windows = (int(x) for x in parts[1][:3])
         cyc = [int(x) for x in parts[2][:5]]
         rounds = int(parts[4][1]) if len(parts) > 4 and len(parts[4]) > 1 else 0
@@ -157,10 +163,13 @@ def chain_latency(chain):
         return None
     trips = 3 + max(0, windows - 1) + rounds
     floor = trips * DEP_LOAD_CYCLES + placed * STEP_CYCLES
-    measured = sum(cyc)
+    # the wave's whole duration in core cycles (a far resolution that ends the
+    # wave falls outside the profile's section columns)
+    measured = int(round(dur_us * chain["clock_mhz"])) if chain.get("clock_mhz") else sum(cyc)
     return {"bound": "latency", "floor_cycles": floor, "measured_cycles": measured,
             "frac": round(floor / measured, 4) if measured else None,
-            "longest_wave": {"dependent_round_trips": trips, "placements": placed, "visits": visits,
+            "longest_wave": {"duration_us": dur_us, "dependent_round_trips": trips, "placements": placed,
+                             "visits": visits,
                              "windows": windows, "chunk_rounds": rounds,
                              "cycles_entry_records_prologue_minwindow_placement_moves": cyc},
             "model": "floor = dependent round trips x %d cycles (tools/micro/dep_load.hip: a dependent load's first "
@@ -849,7 +858,8 @@ def main():
             traffic_src = {"file": os.path.relpath(pmc, REPO), "measured_at_head": pj.get("measured_at_head", "unknown"),
                            "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench command "
                                   "(tools/gpu_round.sh); not measured in this run"}
-        chain = k2_chain_summary(latest_profile("c%d_k2_wave_profile.txt" % args.config))
+        chain = k2_chain_summary(latest_profile("c%d%s_k2_wave_profile.txt"
+                                                % (args.config, "" if args.variant == "baseline" else "_" + args.variant)))
         line = {
             "metric": "reference-equivalent pod x spot-node feasibility checks/s (drain-plan latency: "
                       "drain_plan_latency_ms)",
