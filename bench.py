@@ -47,7 +47,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 from spotplanner import capi  # noqa: E402
 from spotplanner.planner import PredicateChecker  # noqa: E402
-from spotplanner.scaling import predict  # noqa: E402
+from spotplanner.scaling import choose_scaling, predict  # noqa: E402
 from spotplanner.synth import AFFINITY, REALISTIC, SynthCluster, new_node_map, pods_for_deletion, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -898,8 +898,10 @@ def main():
             "per_rank": per_rank,
             "weak_scaling": weak_scaling,
             "scaling_model": {"prediction_us": predict(args.config, world, transport),
-                              "model": "spotplanner/scaling.py: measured 1-GPU parts, ASSUMED RCCL allreduce "
-                                       "latency (the shm transport has none); per_rank holds the measured parts"}
+                              "model": "spotplanner/scaling.py: measured 1-GPU parts (round 6), ASSUMED RCCL "
+                                       "allreduce latency, the shm transport's host walk bounded by the N=2 "
+                                       "rehearsal on one GPU; per_rank holds the measured parts",
+                              "strong_pays": choose_scaling(args.config, world, transport)[0] == "strong"}
             if world > 1 else None,
             "first_ok": int(out.first_ok), "winner": int(out.winner),
             "fallback_candidates": int(np.sum(status[:len(loff) - 1] == capi.SR_CAND_FALLBACK)),

@@ -20,27 +20,34 @@ over its shard plus, for N > 1 over RCCL, the collective and K3:
           result itself, no K3).
 
 Sharding a fixed tick pays only when tick_strong(N) < tick(1): K2 must be
-throughput-bound well above its chain.  None of C1-C5 is any more: C4's
-K2 (15,000 candidates) is 46 us against a 43 us longest wave since its work
-list runs longest wave first, and C3 (1,500 candidates) is a 12.9 us chain in
-a 14.5 us K2, so a strong-scaled tick on 2-8 GPUs is no faster than on one
-(over RCCL, slower).  bench.py reports the strong-scaled line (BASELINE's) with
-the weak-scaled tick beside it; `choose_scaling` says which of the two the
-model expects to pay.
+throughput-bound well above its chain.  Since round 6's cooperative blocks
+C4 is again: its longest wave is 28.8 us in a 44.4 us K2 (15,000 candidates),
+so over the shared-memory transport a 2-GPU tick is predicted at ~33 us.  C3
+(1,500 candidates) is a 12.2 us chain in a 14.5 us K2, C5 a 36 us chain in a
+35 us K2: a strong-scaled tick on 2-8 GPUs is no faster than on one.
+bench.py reports the strong-scaled line (BASELINE's) with the weak-scaled tick
+beside it; `choose_scaling` says which of the two the model expects to pay.
 """
 
-# Measured on one MI355X in round 5 (profiles/r05/final/c*_bench.json:
+# Measured on one MI355X in round 6 (profiles/r06/final/c*_bench.json:
 # kernels_ms.k2_placement = K2, ms_per_step - K2 = gap (>= 0);
-# c*_k2_wave_profile.txt: the longest wave = chain, at most K2).  K3 4.5 us
-# (DESIGN §4).  Microseconds.  C4's K2 is 45-46 us since its work list runs
-# longest wave first, against a 43 us longest wave: it no longer shards well.
+# c*_k2_wave_profile.txt: the longest wave = chain).  K3 4.5 us (DESIGN §4).
+# Microseconds.  C4's longest wave is 28.8 us since the cooperative blocks
+# (48.6 us before), so its 44 us K2 is throughput-bound again.
 PARTS = {
-    1: dict(k2=8.2, chain=6.5, gap=6.5, k3=4.5),
-    2: dict(k2=19.2, chain=17.8, gap=0.3, k3=4.5),
-    3: dict(k2=14.5, chain=12.9, gap=3.1, k3=4.5),
-    4: dict(k2=46.4, chain=43.0, gap=0.0, k3=4.5),
-    5: dict(k2=38.0, chain=37.8, gap=0.5, k3=4.5),
+    1: dict(k2=8.5, chain=5.2, gap=5.4, k3=4.5),
+    2: dict(k2=18.5, chain=17.2, gap=0.5, k3=4.5),
+    3: dict(k2=14.5, chain=12.2, gap=1.5, k3=4.5),
+    4: dict(k2=44.4, chain=28.8, gap=0.1, k3=4.5),
+    5: dict(k2=35.2, chain=36.0, gap=0.6, k3=4.5),
 }
+
+# The shared-memory transport's cost per tick beyond one GPU's: each host
+# waits for every rank's outcome words and walks them in global order.
+# Measured only as an upper bound: two ranks sharing one GPU
+# (profiles/r06/n2_shm_rehearsal.log: ms_per_step_local - K2 = 4.1-6.8 us,
+# both ranks' kernels on one device).  Microseconds.
+SHM_US = 4.0
 
 # RCCL allreduce of 24 B over xGMI, per rank count.  ASSUMED, not measured:
 # no multi-GPU box was available to this build (DESIGN §7); RCCL's
@@ -62,7 +69,9 @@ def predict_tick_us(parts, n, scaling, transport="rccl"):
     ranks' hosts walk the shared outcome words, no collective and no K3)."""
     share = 1.0 / n if scaling == "strong" else 1.0
     k2 = max(parts["chain"], parts["k2"] * share)
-    return k2 + parts["gap"] + ((allreduce_us(n) + parts["k3"]) if n > 1 and transport == "rccl" else 0.0)
+    if n <= 1:
+        return k2 + parts["gap"]
+    return k2 + parts["gap"] + (allreduce_us(n) + parts["k3"] if transport == "rccl" else SHM_US)
 
 
 def predict(config, n, transport="rccl"):
@@ -80,12 +89,12 @@ def predict(config, n, transport="rccl"):
             "strong_pays": ts < t1}
 
 
-def choose_scaling(config, n):
-    """bench.py --scaling auto: shard the config's own tick (strong) where that
-    shortens it, else give every rank a config-sized candidate set (weak)."""
+def choose_scaling(config, n, transport="shm"):
+    """Shard the config's own tick (strong) where that shortens it, else give
+    every rank a config-sized candidate set (weak)."""
     if n <= 1:
         return "strong", "one GPU"
-    r = predict(config, n)
+    r = predict(config, n, transport)
     if r["strong_pays"]:
         return "strong", "predicted strong tick %.1f us < 1-GPU tick %.1f us" % (r["strong_tick_us"], r["tick1_us"])
     return "weak", ("predicted strong tick %.1f us >= 1-GPU tick %.1f us (K2 chain-bound: the longest candidate's "

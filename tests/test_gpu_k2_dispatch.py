@@ -236,7 +236,7 @@ def test_planner_switches_match_oracle(which):
         ck.close()
 
 
-@pytest.mark.parametrize("case", ["c3", "c4_wide_head_only", "affinity_split"])
+@pytest.mark.parametrize("case", ["c3", "c4_wide_head_only", "affinity_split", "c3_all", "c3_off"])
 def test_cooperative_blocks(case):
     """Cooperative blocks (SR_K2_COOP): the costliest entries of a cost-ordered
     list, on a node-order launch of four waves per block, are planned by one
@@ -244,18 +244,24 @@ def test_cooperative_blocks(case):
     plan is the oracle's.  C3-shaped rows (10 words: resolutions beyond the
     512-node head), a 6,000-node pool (94-word rows, head-only S rows: the
     scans evaluate the class programs), and the affinity variant's split launch
-    (its node-order part cooperative)."""
-    env = dict(SR_LIST_COST_MIN=0, SR_K2_WPB=4, SR_K2_COOP=32)
+    (its node-order part cooperative); every entry cooperative (c3_all) and
+    none (c3_off) on the same ticks."""
+    env = dict(SR_LIST_COST_MIN=0, SR_K2_WPB=4, SR_K2_COOP={"c3_all": 4096, "c3_off": 0}.get(case, 32))
     if case == "affinity_split":
         env["SR_K2_SPLIT_MIN"] = 64
     ck = make_checker(**env)
     try:
         sc = {"c3": lambda: SynthCluster(3, seed=45, n_on_demand=300, n_spot=600),
+              "c3_all": lambda: SynthCluster(3, seed=45, n_on_demand=300, n_spot=600),
+              "c3_off": lambda: SynthCluster(3, seed=45, n_on_demand=300, n_spot=600),
               "c4_wide_head_only": lambda: SynthCluster(4, seed=5, n_on_demand=400, n_spot=6000),
               "affinity_split": lambda: SynthCluster(3, seed=41, n_on_demand=300, n_spot=600, **AFFINITY)}[case]()
         reused, by_cost, _ = _ticks(ck, sc, 8, np.random.default_rng(45), expect_split=case == "affinity_split")
         assert reused >= 4 and by_cost >= 8, (reused, by_cost)
-        assert _ticks.coop >= 8, _ticks.coop
+        if case == "c3_off":
+            assert _ticks.coop == 0, _ticks.coop
+        else:
+            assert _ticks.coop >= 8, _ticks.coop
     finally:
         ck.close()
 

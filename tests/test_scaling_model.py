@@ -31,11 +31,12 @@ def test_chain_bounds_the_sharded_tick():
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
-def test_c3_does_not_shard_its_own_tick(n):
-    # C3's K2 is one chain (12.2 of 13.8 us): a strong-scaled tick is slower
-    r = scaling.predict(3, n)
+@pytest.mark.parametrize("transport", ["rccl", "shm"])
+def test_c3_does_not_shard_its_own_tick(n, transport):
+    # C3's K2 is one chain (12.2 of 14.5 us): a strong-scaled tick is slower
+    r = scaling.predict(3, n, transport)
     assert not r["strong_pays"] and r["strong_tick_us"] > r["tick1_us"]
-    assert scaling.choose_scaling(3, n)[0] == "weak"
+    assert scaling.choose_scaling(3, n, transport)[0] == "weak"
 
 
 def test_throughput_bound_tick_shards():
@@ -45,10 +46,21 @@ def test_throughput_bound_tick_shards():
     assert scaling.predict_tick_us(p, 2, "strong") < scaling.predict_tick_us(p, 1, "strong")
 
 
-@pytest.mark.parametrize("c", [1, 2, 3, 4, 5])
-def test_round5_configs_keep_their_own_tick_whole(c):
-    # round 5: every config's K2 is within a few us of its longest wave
-    assert scaling.choose_scaling(c, 2)[0] == "weak"
+@pytest.mark.parametrize("c", [1, 2, 3, 5])
+def test_chain_bound_configs_keep_their_own_tick_whole(c):
+    # round 6: C1-C3 and C5's K2 is within a few us of its longest wave
+    for transport in ("rccl", "shm"):
+        assert scaling.choose_scaling(c, 2, transport)[0] == "weak"
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_c4_shards_over_shared_memory(n):
+    # round 6: the cooperative blocks cut C4's longest wave to 28.8 us of a 44.4 us
+    # K2, so splitting its 15,000 candidates pays where the exchange is cheap
+    r = scaling.predict(4, n, "shm")
+    assert r["strong_pays"] and r["strong_tick_us"] == pytest.approx(
+        scaling.PARTS[4]["chain"] + scaling.PARTS[4]["gap"] + scaling.SHM_US)
+    assert scaling.choose_scaling(4, n, "shm")[0] == "strong"
 
 
 def test_efficiencies_follow_the_driver_rule():
@@ -105,9 +117,10 @@ def test_per_rank_records_gathered_in_rank_order(world):
 
 @pytest.mark.parametrize("n", [2, 4, 8])
 def test_shared_memory_transport_adds_no_device_exchange(n):
-    # transport "shm" (sr_comm_init_shm): the ranks' hosts walk the outcome words K2 wrote; no allreduce, no K3
+    # transport "shm" (sr_comm_init_shm): the ranks' hosts walk the outcome words K2 wrote; no allreduce, no K3,
+    # only the host walk (SHM_US) on top of the one-GPU tick
     for c, p in scaling.PARTS.items():
-        assert scaling.predict_tick_us(p, n, "weak", "shm") == pytest.approx(scaling.predict_tick_us(p, 1, "weak"))
-        r = scaling.predict(c, n, "shm")
-        assert r["weak_efficiency"] == pytest.approx(1.0) and r["transport"] == "shm"
-        assert r["strong_tick_us"] <= r["tick1_us"] + 1e-9
+        assert scaling.predict_tick_us(p, n, "weak", "shm") == pytest.approx(
+            scaling.predict_tick_us(p, 1, "weak") + scaling.SHM_US)
+        assert scaling.predict_tick_us(p, n, "weak", "shm") < scaling.predict_tick_us(p, n, "weak", "rccl")
+        assert scaling.predict(c, n, "shm")["transport"] == "shm"
