@@ -2705,7 +2705,7 @@ static inline int k2_waves_per_block(const DevWorkload& w) {
 // (hipExtLaunchKernelGGL: no event packets or host calls around the kernel).
 template <typename K, typename... A>
 void launch(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, A... args) {
-  if (ev0) hipExtLaunchKernelGGL(kernel, grid, block, static_cast<uint32_t>(lds), s, ev0, ev1, 0, args...);
+  if (ev0 || ev1) hipExtLaunchKernelGGL(kernel, grid, block, static_cast<uint32_t>(lds), s, ev0, ev1, 0, args...);
   else hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
 }
 

@@ -159,6 +159,10 @@ struct sr_ctx {
   // blocks on the node-order kernel (four waves per block: the chain and
   // three waves scanning far resolutions with it); 0: none
   int32_t k2_coop = 64;
+  // SR_K2_DISPATCH_EVENTS=0: the split launch's fork and join as marker
+  // packets (hipEventRecord) instead of the completion signals of K0 and of
+  // the general kernel's dispatch
+  int32_t k2_dispatch_events = 1;
   DevBuf out_cycles;
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -1131,11 +1135,25 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   d.d_min = static_cast<int32_t*>(ctx->dmin.p) + 8 * par;
   d.d_min_next = static_cast<int32_t*>(ctx->dmin.p) + 8 * (1 - par);
   Slot& sl = *ctx->cur;
+  // the split launch (see sr_ctx::k2_split): the node-order part on this
+  // stream, the general one on stream2 between a fork and a join event
+  const int32_t n_node = w.n_list_node;
+  const bool split = ctx->k2_split && n_node > 0 && n_node < d.n_list && d.k2_mode == 0 && d.k2_node_kernel &&
+                     w.max_np_node >= 1 && w.max_np_node <= 256;
+  if (split && !ctx->stream2) {
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+    HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+  }
+  // the fork is K0's own completion signal when K0 runs untimed (no marker
+  // packet between K0 and K2: ~5 us per marker on the split tick)
+  bool forked = false;
   if (d.k0_skip) {
     if (!ctx->dmin_ready[par])  // no K2 of a previous run reset it: reset here
       HIP_TRY(ctx, hipMemsetAsync(d.d_min, 0xff, sizeof(uint64_t), s));
   } else {
-    HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, e0b));
+    forked = split && !e0b && ctx->k2_dispatch_events;
+    HIP_TRY(ctx, sr::launch_tables(d, w.first_fallback, s, e0a, forked ? ctx->ev_fork : e0b));
     if (sl.commit_k0) {  // K0 wrote the node and pod patches and brought the rows to this workload (a rerun:
       sl.commit_k0 = false;  // idempotent)
       sl.tables_cand_gen = w.cand_gen;
@@ -1166,11 +1184,6 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   } else {
     d.res_stat = d.res_map = nullptr;
   }
-  // the split launch (see sr_ctx::k2_split): the node-order part on this
-  // stream, the general one on stream2 between a fork and a join event
-  const int32_t n_node = w.n_list_node;
-  const bool split = ctx->k2_split && n_node > 0 && n_node < d.n_list && d.k2_mode == 0 && d.k2_node_kernel &&
-                     w.max_np_node >= 1 && w.max_np_node <= 256;
   ctx->t.k2_launches = d.n_list > 0 ? (split ? 2 : 1) : 0;
   // cooperative blocks for the front of a cost-ordered list, on a node-order
   // launch of four waves per block without extension records
@@ -1185,11 +1198,6 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
   }
   ctx->t.k2_coop = d.n_coop;
   if (split) {
-    if (!ctx->stream2) {
-      HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
-      HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-      HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-    }
     sr::DevWorkload dp = d, dn = d;
     dp.list = d.list + n_node;
     dp.n_list = d.n_list - n_node;
@@ -1201,10 +1209,11 @@ sr_status run(sr_ctx* ctx, sr_plan_out* out, bool full, bool use_comm) {
     dn.max_np = w.max_np_node;
     dn.dyn_cand = nullptr;  // none of its candidates is on the domain path
     if (e1a) HIP_TRY(ctx, hipEventRecord(e1a, s));
-    HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, s));
+    if (!forked) HIP_TRY(ctx, hipEventRecord(ctx->ev_fork, s));
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
-    HIP_TRY(ctx, sr::launch_placement(dp, ctx->stream2, nullptr, nullptr));
-    HIP_TRY(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
+    // the join is the general kernel's own completion signal
+    HIP_TRY(ctx, sr::launch_placement(dp, ctx->stream2, nullptr, ctx->k2_dispatch_events ? ctx->ev_join : nullptr));
+    if (!ctx->k2_dispatch_events) HIP_TRY(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
     HIP_TRY(ctx, sr::launch_placement(dn, s, nullptr, nullptr));
     HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0));
     if (e1b) HIP_TRY(ctx, hipEventRecord(e1b, s));
@@ -1378,6 +1387,7 @@ sr_status sr_create(int32_t device, sr_ctx** out) {
   if (const char* m = std::getenv("SR_LIST_COST")) ctx->list_cost = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_LIST_COST_MIN")) ctx->list_cost_min = std::max(0, std::atoi(m));
   if (const char* m = std::getenv("SR_K2_SPLIT_MIN")) ctx->enc.split_min = std::max(0, std::atoi(m));
+  if (const char* m = std::getenv("SR_K2_DISPATCH_EVENTS")) ctx->k2_dispatch_events = std::atoi(m) != 0;
   if (const char* m = std::getenv("SR_LIST_HEAD")) ctx->enc.list_head = std::max(0, std::atoi(m));
   if (const char* m = std::getenv("SR_K2_COOP")) ctx->k2_coop = std::max(0, std::atoi(m));
   *out = ctx;
