@@ -54,6 +54,8 @@ DISPATCH = {
     "split_cost_head32": dict(SR_K2_SPLIT_MIN=64, SR_LIST_COST_MIN=0, SR_LIST_HEAD=32),
     # split launch + cost order, four waves per block, the default list head (one part)
     "split_cost_wpb4": dict(SR_K2_SPLIT_MIN=64, SR_LIST_COST_MIN=0, SR_K2_WPB=4),
+    # the split launch's fork / join as marker packets (the default: dispatch completion signals)
+    "split_marker_events": dict(SR_K2_SPLIT_MIN=64, SR_LIST_COST_MIN=0, SR_K2_DISPATCH_EVENTS=0),
     # cost order without the split (one kernel: the general one)
     "cost_nosplit": dict(SR_K2_SPLIT=0, SR_LIST_COST_MIN=0, SR_LIST_HEAD=16),
 }
