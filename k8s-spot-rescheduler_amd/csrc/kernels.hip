@@ -2589,6 +2589,7 @@ __global__ __launch_bounds__(256) void k2_place(DevWorkload w_arg, const int4* _
     wide = 3;
     uint64_t* tl = reinterpret_cast<uint64_t*>(&L);
     if (np <= 64) k2_domain<CH, 1, PROF>(w, tl, p0, np, dbase, status, nbytes, st, ebase);
+    else if (np <= 128) k2_domain<CH, 2, PROF>(w, tl, p0, np, dbase, status, nbytes, st, ebase);  // (4: +37 % per pod)
     else if (np <= 256) k2_domain<CH, 4, PROF>(w, tl, p0, np, dbase, status, nbytes, st, ebase);
     else k2_domain<CH, kDevDynG, PROF>(w, tl, p0, np, dbase, status, nbytes, st, ebase);
   } else if (node_order && ebase >= 0) {  // extension records, node order (place_window_x); writes out_node
