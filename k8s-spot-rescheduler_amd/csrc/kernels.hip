@@ -934,6 +934,32 @@ __device__ __forceinline__ uint32_t from_lane(uint32_t v, int src) {
 // which the placement then updates as ClusterSnapshot.AddPod would.  E: some
 // pod of the candidate asks for ephemeral storage (otherwise the ephemeral
 // check is the fixed `emask`); O: some pod sets or meets state bits.
+// v_writelane_b32: lane k of v becomes the scalar x (two instructions where a
+// compare-and-select per pod took three; the lane select goes through m0, as
+// two SGPR operands exceed the constant bus); x and k wave-uniform
+// (m0 is a reserved register: the clobber tells the compiler it changed but
+// nothing preserves a value it held; no other instruction of these kernels
+// reads m0 -- checked in the ISA of every part)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ int writelane(int v, int x, int k) {
+  asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "s"(k) : "m0");
+  return v;
+}
+#pragma clang diagnostic pop
+// s_ff1_i32_b64: the lowest set bit of a scalar mask, -1 when it is zero (the
+// compiler's ctz of a maybe-zero value adds a compare and a select)
+__device__ __forceinline__ int ff1(uint64_t x) {
+  int r;
+  asm("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(x));
+  return r;
+}
+// s_bitset0_b64: clear bit k of a scalar mask (one op for shift + andn2)
+__device__ __forceinline__ uint64_t bitclear(uint64_t x, int k) {
+  asm("s_bitset0_b64 %0, %1" : "+s"(x) : "s"(k));
+  return x;
+}
+
 template <bool E, bool O>
 __device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W, int lane, int64_t rc, int64_t rm,
                                                  int64_t re, uint64_t pm, uint64_t cur, uint64_t zm,
@@ -944,10 +970,10 @@ __device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W,
   int jv = 64;
   if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
   // without state bits one branch per pod: a pod that fits nowhere selects
-  // lane 64 (no lane)
+  // lane -1 (no lane; jv keeps 64 for a pod not stepped)
   while (todo != 0) {
     const int k = __builtin_ctzll(todo);
-    todo &= ~(1ull << k);  // one scalar op fewer than todo &= todo - 1
+    todo = bitclear(todo, k);  // s_bitset0: one scalar op (todo &= todo - 1 takes two)
     const int64_t c = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), k));
     const int64_t m = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), k));
     const int64_t e = E ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), k)) : 0;
@@ -966,20 +992,21 @@ __device__ __forceinline__ uint64_t place_window(uint64_t todo, int kmax, int W,
           nleft -= 1;
           nport |= swap_pairs(q, swap_mask);  // the bits it sets
         }
-        jv = lane == k ? j : jv;
+        jv = writelane(jv, j, k);  // pod k took lane j
       }
       continue;
     }
-    const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
+    const int j = ff1(fit);  // -1 when it fits nowhere (no lane)
     const bool hit = lane == j;  // ClusterSnapshot.AddPod on the candidate's copy of node 64 W + j
     ncpu -= hit ? c : 0;
     nmem -= hit ? m : 0;
     if (E) neph -= hit ? e : 0;
     nleft -= hit ? 1 : 0;
-    jv = lane == k ? j : jv;
+    jv = writelane(jv, j, k);  // pod k took lane j
   }
-  node = jv < 64 ? 64 * W + jv : node;
-  return ballot(jv < 64);
+  const bool took = static_cast<unsigned>(jv) < 64u;  // -1 / 64: no lane
+  node = took ? 64 * W + jv : node;
+  return ballot(took);
 }
 
 // Extension-record values of a pod (XT candidates, lanes = pods): what
@@ -1011,7 +1038,7 @@ __device__ __forceinline__ uint64_t place_window_x(uint64_t todo, int kmax, int 
   if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
   while (todo != 0) {
     const int k = __builtin_ctzll(todo);
-    todo &= ~(1ull << k);
+    todo = bitclear(todo, k);
     const int64_t c = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rc), k));
     const int64_t m = static_cast<int64_t>(readlane64(static_cast<uint64_t>(rm), k));
     const int64_t e = E ? static_cast<int64_t>(readlane64(static_cast<uint64_t>(re), k)) : 0;
@@ -1038,11 +1065,12 @@ __device__ __forceinline__ uint64_t place_window_x(uint64_t todo, int kmax, int 
         ns1 -= a1;
         if (O) nport |= swap_pairs(q, swap_mask);
       }
-      jv = lane == k ? j : jv;
+      jv = writelane(jv, j, k);  // pod k took lane j
     }
   }
-  node = jv < 64 ? 64 * W + jv : node;
-  return ballot(jv < 64);
+  const bool took = static_cast<unsigned>(jv) < 64u;  // -1 / 64: no lane
+  node = took ? 64 * W + jv : node;
+  return ballot(took);
 }
 
 // The free value f of a node scaled to the candidate's request granularity
@@ -1100,7 +1128,7 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
     uint64_t taken = 0;
     while (todo != 0) {
       const int k = __builtin_ctzll(todo);
-      todo &= ~(1ull << k);
+      todo = bitclear(todo, k);
       const int32_t c = __builtin_amdgcn_readlane(static_cast<int>(nc), k);
       const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
       const int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
@@ -1108,7 +1136,7 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
       uint64_t fit = readlane64(cur, k) & base & ~taken & fits32<E, true>(c32, m32, e32, 1, nport & q, c, m, e);
       const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
       taken |= fit & (0ull - fit);  // the lowest set bit: node j
-      jv = lane == k ? j : jv;
+      jv = writelane(jv, j, k);  // pod k took lane j
     }
     // node lane j receives the request and the set bits of the pod that took
     // it; the other pods send zeros to a node nobody took (one exists unless
@@ -1141,7 +1169,7 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
   if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
   while (todo != 0) {
     const int k = __builtin_ctzll(todo);
-    todo &= ~(1ull << k);
+    todo = bitclear(todo, k);
     const int32_t c = __builtin_amdgcn_readlane(static_cast<int>(nc), k);
     const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
     const int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
@@ -1158,20 +1186,21 @@ __device__ __forceinline__ uint64_t place_window32(uint64_t todo, int kmax, int 
           nleft -= 1;
           nport |= readlane64(ps, k);
         }
-        jv = lane == k ? j : jv;
+        jv = writelane(jv, j, k);  // pod k took lane j
       }
       continue;
     }
-    const int j = fit != 0 ? __builtin_ctzll(fit) : 64;
+    const int j = ff1(fit);  // -1 when it fits nowhere (no lane)
     const bool hit = lane == j;  // ClusterSnapshot.AddPod on the candidate's copy of node 64 W + j
     c32 -= hit ? cu : 0;
     m32 -= hit ? mu : 0;
     if (E) e32 -= hit ? eu : 0;
     nleft -= hit ? 1 : 0;
-    jv = lane == k ? j : jv;
+    jv = writelane(jv, j, k);  // pod k took lane j
   }
-  node = jv < 64 ? 64 * W + jv : node;
-  return ballot(jv < 64);
+  const bool took = static_cast<unsigned>(jv) < 64u;  // -1 / 64: no lane
+  node = took ? 64 * W + jv : node;
+  return ballot(took);
 }
 
 // place_window_x in 32-bit scaled form (narrow XT candidates): one lane test
@@ -1188,7 +1217,7 @@ __device__ __forceinline__ uint64_t place_window32_x(uint64_t todo, int kmax, in
   if (kmax < 64) todo &= kmax <= 0 ? 0ull : (1ull << kmax) - 1;
   while (todo != 0) {
     const int k = __builtin_ctzll(todo);
-    todo &= ~(1ull << k);
+    todo = bitclear(todo, k);
     const int32_t c = __builtin_amdgcn_readlane(static_cast<int>(nc), k);
     const int32_t m = __builtin_amdgcn_readlane(static_cast<int>(nm), k);
     const int32_t e = E ? __builtin_amdgcn_readlane(static_cast<int>(ne), k) : 0;
@@ -1220,11 +1249,12 @@ __device__ __forceinline__ uint64_t place_window32_x(uint64_t todo, int kmax, in
         nleft -= 1;
         if (O) nport |= readlane64(ps, k);
       }
-      jv = lane == k ? j : jv;
+      jv = writelane(jv, j, k);  // pod k took lane j
     }
   }
-  node = jv < 64 ? 64 * W + jv : node;
-  return ballot(jv < 64);
+  const bool took = static_cast<unsigned>(jv) < 64u;  // -1 / 64: no lane
+  node = took ? 64 * W + jv : node;
+  return ballot(took);
 }
 
 // A narrow candidate's request granularity per dimension: every request is a
