@@ -96,6 +96,11 @@ def main():
                                                  int((q[:, 12] >> 56).sum()), q[:, 13].sum() / sv))
         print("node order: wave dur us p50/p90/max %s" % pct(dur[nodeo]))
         print("node order: 32-bit scaled window visits in %d of %d waves" % (int((q[:, 15] & 1).sum()), len(q)))
+        idle = (q[:, 6] == 0) & (vis == 0)  # no placement, no window visit: a pod with no feasible node first
+        dq = dur[nodeo]
+        print("node order: waves with no visit and no placement %d (%.1f %% of wave-us, p50 %.2f us)"
+              % (int(idle.sum()), 100.0 * dq[idle].sum() / max(1e-9, dq.sum()),
+                 float(np.median(dq[idle])) if idle.any() else 0.0))
     if (~nodeo).any():
         print("pod order:  wave dur us p50/p90/max %s" % pct(dur[~nodeo]))
     r = r[~nodeo] if (~nodeo).any() else r
