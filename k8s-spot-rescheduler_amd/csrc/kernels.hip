@@ -1593,10 +1593,13 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
   }
   // s_head_only: each pod's class program (8 slots) in LDS after the F heads,
   // for the S words beyond the head (k2_node sizes its LDS for it)
+  // (pods from the first dead one on are never scanned: a candidate whose
+  // first pod fits no node -- C4: 2,254 of 15,000 -- loads none)
   int32_t* PG = reinterpret_cast<int32_t*>(F + 64 * G * kNHS);
-  if (w.s_head_only) {
+  if (w.s_head_only && dead > 0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
+      if (64 * g >= dead) break;  // wave-uniform
       const uint32_t cls = static_cast<uint32_t>(r01[g]) / static_cast<uint32_t>(Wp);
       const int4* p8 = reinterpret_cast<const int4*>(w.cls_prog8 + static_cast<size_t>(cls) * 8);
       const int4 a = p8[0], b = p8[1];
@@ -1604,7 +1607,7 @@ __device__ __forceinline__ void k2_node_order(const DevWorkload& w, uint64_t* __
       dst[0] = a;
       dst[1] = b;
     }
-    nbytes += 32u * static_cast<uint32_t>(np);
+    nbytes += 32u * static_cast<uint32_t>(min(np, 64 * ((dead + 63) / 64)));
   }
   uint64_t cyc_t = PROF ? __builtin_amdgcn_s_memtime() : 0;
   // bytes moved (algorithmic, wave-uniform): pod records, F heads of pods
