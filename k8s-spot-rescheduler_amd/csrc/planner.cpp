@@ -153,8 +153,9 @@ struct sr_ctx {
   // waves first (a candidate whose pods scan far along their rows is short by
   // pod count but one of the longest waves: C4's last-starting waves)
   int32_t list_cost = 1;
-  int32_t list_cost_min = 2048;  // SR_LIST_COST_MIN: only lists longer than this (C4 15,000 entries: K2 69 -> 45 us;
-                                 // C3's 1,500 waves are all resident at once: within noise, or +0.5 us)
+  int32_t list_cost_min = 1024;  // SR_LIST_COST_MIN: only lists longer than this (C4 15,000 entries: K2 69 -> 45 us;
+                                 // round 6, C3's 1,500: K2 -0.3 us, realistic C3 -0.7 us, affinity C3 16.3 -> 13.3 us;
+                                 // C1 / C2 / C5's 300 entries keep the pod-count order)
   // SR_K2_COOP: a cost-ordered list's costliest entries planned by cooperative
   // blocks on the node-order kernel (four waves per block: the chain and
   // three waves scanning far resolutions with it); 0: none

@@ -9,7 +9,7 @@ configs reach them only in the bench (C4: 15,000 candidates):
   on the general kernel on a second stream; both write d_min and the
   single-rank result words;
 - the cost-ordered work list (`list_cost`, lists above SR_LIST_COST_MIN =
-  2,048 entries): the first run of a candidate generation records each
+  1,024 entries): the first run of a candidate generation records each
   candidate's wave duration, and the reused workloads of the next ticks
   dispatch the longest waves first;
 - four waves per block (lists above 2,048 entries).
