@@ -21,9 +21,9 @@ over its shard plus, for N > 1 over RCCL, the collective and K3:
 
 Sharding a fixed tick pays only when tick_strong(N) < tick(1): K2 must be
 throughput-bound well above its chain.  Since round 6's cooperative blocks
-C4 is again: its longest wave is 28.8 us in a 44.4 us K2 (15,000 candidates),
-so over the shared-memory transport a 2-GPU tick is predicted at ~33 us.  C3
-(1,500 candidates) is a 12.2 us chain in a 14.5 us K2, C5 a 36 us chain in a
+C4 is again: its longest wave is 26.3 us in a 43.8 us K2 (15,000 candidates),
+so over the shared-memory transport a 2-GPU tick is predicted at ~30 us.  C3
+(1,500 candidates) is a 12.2 us chain in a 14.2 us K2, C5 a 36 us chain in a
 35 us K2: a strong-scaled tick on 2-8 GPUs is no faster than on one.
 bench.py reports the strong-scaled line (BASELINE's) with the weak-scaled tick
 beside it; `choose_scaling` says which of the two the model expects to pay.
@@ -37,8 +37,8 @@ beside it; `choose_scaling` says which of the two the model expects to pay.
 PARTS = {
     1: dict(k2=8.5, chain=5.2, gap=5.4, k3=4.5),
     2: dict(k2=18.5, chain=17.2, gap=0.5, k3=4.5),
-    3: dict(k2=14.5, chain=12.2, gap=1.5, k3=4.5),
-    4: dict(k2=44.4, chain=28.8, gap=0.1, k3=4.5),
+    3: dict(k2=14.2, chain=12.2, gap=1.7, k3=4.5),   # profiles/r06/default_bench_c3.json
+    4: dict(k2=43.8, chain=26.3, gap=0.0, k3=4.5),   # profiles/r06/final/c4_* (list head 512)
     5: dict(k2=35.2, chain=36.0, gap=0.6, k3=4.5),
 }
 
